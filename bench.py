@@ -1,0 +1,233 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident CouloyDB log-record scan (decode + CRC -> index tuples).
+
+Contract (see task spec): `python bench.py --gpus N --steps K --warmup W` prints ONE
+JSON line on rank 0.  A step = one full scan (k_scan + k_resolve + result
+read-back) of the configuration's data files, already resident in HBM.  For N>1
+each rank (one per GPU, launched by torch.distributed.run) scans its own fid
+range of the same per-GPU size (weak scaling, no collective on the data path;
+the barrier and the max-over-ranks timing use torch.distributed).
+
+Workloads (BASELINE.json configs):
+  c2 (default): 16 files x 256 MiB, key 0x00||%09d, 256-B random values -> 276-B records
+  c1: one 64 MiB file of 1 KiB values (CPU plumbing config; also runnable here)
+  c3: 32 GiB, Zipf(1.1) value lengths 64 B-64 KiB
+Data is synthetic (splitmix64 values), written on the GPU by libclygen.so, a
+restatement of EncodeLogRecord + appendLogRecord's file rotation.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s device-resident log-record decode+CRC; Mrecords/s; index-load wall time"
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+DATA_FILE_SIZE = 256 << 20   # options.go:32
+
+
+class Workload:
+    pass
+
+
+def _zipf_lengths(n, rng, s=1.1, nmax=65473):
+    ranks = np.arange(1, nmax + 1, dtype=np.float64)
+    w = ranks ** (-s)
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    r = np.searchsorted(cdf, rng.random(n)) + 1
+    return (63 + r).astype(np.uint32)
+
+
+def make_workload(name, torch, rank=0, device=0, seed=0x434C59):
+    """Build the config's data files in HBM on `device`.  Returns a Workload with
+    dev_files [(ptr, len, fid)], d_buf, d_out (uint8 tensor), out_cap, expect_records."""
+    from couloydb_amd import _abi
+    gen = _abi.load_gen_lib()
+    if name == "c2":
+        nrec_file = DATA_FILE_SIZE // 276
+        nfiles_target = 16
+        vl = np.full(nrec_file * nfiles_target, 256, np.uint32)
+    elif name == "c1":
+        nfiles_target = 1
+        vl = np.full(64280, 1024, np.uint32)
+    elif name == "c3":
+        rng = np.random.default_rng(seed + 3)
+        nfiles_target = 128
+        vl = _zipf_lengths(int(32 * 2**30 / 3500), rng)
+        # trim/extend to ~32 GiB
+        sizes = vl.astype(np.int64) + 20
+        cum = np.cumsum(sizes)
+        vl = vl[: int(np.searchsorted(cum, 32 * 2**30 - nfiles_target * 70000))]
+    else:
+        raise ValueError(name)
+    n = len(vl)
+    recs = np.zeros(n, dtype=_abi.GEN_DTYPE)
+    recs["value_len"] = vl
+    recs["key_index"] = (np.arange(n, dtype=np.int64) + rank * n) % 1_000_000_000
+    maxf = 4096
+    fo = (ctypes.c_uint64 * maxf)()
+    fl = (ctypes.c_uint64 * maxf)()
+    nf = ctypes.c_uint32()
+    limit = DATA_FILE_SIZE if name != "c1" else 64 << 20
+    total = gen.cly_gen_layout(recs.ctypes.data, n, limit, 4096, fo, fl, maxf, ctypes.byref(nf))
+    dev = torch.device("cuda", device)
+    d_buf = torch.empty(int(total) + 4096, dtype=torch.uint8, device=dev)
+    d_recs = torch.from_numpy(recs.view(np.uint8)).to(dev)
+    base_dst = 0
+    rc = gen.cly_gen_encode(ctypes.c_void_p(d_buf.data_ptr() + base_dst), ctypes.c_void_p(d_recs.data_ptr()), n,
+                            seed + rank)
+    if rc != 0:
+        raise RuntimeError("cly_gen_encode failed: %d" % rc)
+    del d_recs
+    wl = Workload()
+    wl.name = name
+    wl.d_buf = d_buf
+    wl.dev_files = [(d_buf.data_ptr() + fo[i], int(fl[i]), rank * maxf + i) for i in range(nf.value)]
+    wl.file_off = [int(fo[i]) for i in range(nf.value)]
+    wl.bytes = int(sum(fl[i] for i in range(nf.value)))
+    wl.expect_records = n
+    wl.out_cap = n + 1024
+    wl.d_out = torch.empty(wl.out_cap * 48, dtype=torch.uint8, device=dev)
+
+    def file_bytes(i):
+        o, ln = wl.file_off[i], wl.dev_files[i][1]
+        return wl.d_buf[o:o + ln].cpu().numpy()
+    wl.file_bytes = file_bytes
+    torch.cuda.synchronize(dev)
+    return wl
+
+
+def cpu_baseline(wl, budget_s=12.0):
+    """Oracle (C restatement) on the host cores over a bounded sample of the same
+    workload: 'ref-algorithm' single thread over whole files; 'ref-faithful' =
+    the reference's per-record fstat+mmap/munmap pattern over a bounded record
+    count of one file."""
+    from oracle import cly_oracle as co
+    files, t_alg, nbytes, nrec = [], 0.0, 0, 0
+    i = 0
+    while i < len(wl.dev_files) and t_alg < budget_s * 0.6:
+        arr = wl.file_bytes(i)
+        t0 = time.perf_counter()
+        r = co.scan_files_mt([arr], [wl.dev_files[i][2]], 1)
+        t_alg += time.perf_counter() - t0
+        nbytes += len(arr)
+        nrec += int(r)
+        files.append(i)
+        i += 1
+    alg_gibs = nbytes / t_alg / 2**30
+    # ref-faithful on a bounded number of records of file 0
+    arr = wl.file_bytes(0)
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "000000000.cly")
+        arr.tofile(p)
+        t0 = time.perf_counter()
+        nf, st, end = co.scan_path_faithful(p, 0, 20000)
+        tf = time.perf_counter() - t0
+    faithful_gibs = end / tf / 2**30
+    return {"value": round(alg_gibs, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": "%d of %d files (%.2f GiB, %d records) scanned by oracle/cly_oracle.c clyo_scan_files_mt, 1 thread"
+                      % (len(files), len(wl.dev_files), nbytes / 2**30, nrec),
+            "mrecords_per_s": round(nrec / t_alg / 1e6, 3),
+            "ref_faithful": {"value": round(faithful_gibs, 5), "unit": "GiB/s",
+                             "mrecords_per_s": round(nf / tf / 1e6, 4),
+                             "sample": "first %d records of one file; per record fstat + 2x (open, mmap whole file, copy, munmap)" % nf},
+            "host_nproc": os.cpu_count()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", action="store_true", help="check one file against the oracle after timing")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+
+    from couloydb_amd import Scanner, build_info
+    wl = make_workload(args.config, torch, rank=rank, device=local)
+    sc = Scanner(local)
+
+    def step():
+        return sc.scan_device(wl.dev_files, wl.d_out.data_ptr(), wl.out_cap)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    scan_ms, res_ms, passes, recs = 0.0, 0.0, 0, 0
+    for _ in range(args.steps):
+        first, res, st, need = step()
+        scan_ms += st.scan_ms
+        res_ms += st.resolve_ms
+        passes = max(passes, st.passes)
+        recs = sum(r.n_records for r in res)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt, scan_ms / args.steps], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt, kern_ms = float(t[0]), float(t[1])
+    ms = dt / args.steps * 1e3
+    total_bytes = wl.bytes * world
+    total_recs = recs * world
+    value = total_bytes / (ms / 1e3) / 2**30
+    achieved = wl.bytes / (kern_ms / 1e3) / 1e9
+    ok = all(r.status == 0 for r in res) and recs == wl.expect_records
+    out = {
+        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (splitmix64 values, written in HBM by libclygen)",
+        "config": {"workload": args.config, "files_per_gpu": len(wl.dev_files),
+                   "bytes_per_gpu": wl.bytes, "records_per_gpu": recs,
+                   "parallelism": "files sharded by fid range, %d GPU(s), no collective" % world},
+        "mrecords_per_s": round(total_recs / (ms / 1e3) / 1e6, 2),
+        "kernel": {"k_scan_ms": round(kern_ms, 4), "k_resolve_ms": round(res_ms / args.steps, 4),
+                   "passes": passes, "build": build_info()},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "note": "achieved = input bytes per k_scan launch / its HIP-event duration"},
+        "parity_ok": ok,
+    }
+    if args.verify and rank == 0:
+        from oracle import cly_oracle as co
+        from couloydb_amd import TUPLE_DTYPE
+        first, res, st, need = step()
+        o = wl.d_out[: need * 48].cpu().numpy().view(TUPLE_DTYPE)
+        tt, so, eo = co.scan_file(wl.file_bytes(0), wl.dev_files[0][2])
+        g = o[first[0]:first[0] + res[0].n_records]
+        out["verify_file0"] = bool(len(g) == len(tt) and (g.view(np.uint8) == tt.view(np.uint8)).all()
+                                   and so == res[0].status and eo == res[0].end_offset)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(wl)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    sc.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

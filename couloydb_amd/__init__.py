@@ -1,0 +1,192 @@
+"""couloydb_amd — MI355X-native log-record scan for CouloyDB data files.
+
+Host-side mirror of the reference interface for the scan path
+(data/dataFile.go, data/logRecord.go, db.go:582-637), over the C-ABI of
+include/clyscan.h.  The decode + CRC runs in HIP kernels on gfx950; this module
+only moves buffers and shapes results.
+
+    from couloydb_amd import Scanner, DataFile
+    with Scanner(device=0) as sc:
+        res = sc.scan([DataFile.from_path("000000000.cly", fid=0)])
+        for rec, size in res.records(0): ...
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _abi
+from ._abi import (END_EOF, END_TORN, END_ZERO, ERR_CRC, ERR_OFFSET, ERR_TRUNC5, ERR_VARINT,
+                   TUPLE_DTYPE)
+
+__all__ = ["Scanner", "DataFile", "LogRecord", "LogPos", "ScanResult", "ScanError",
+           "ErrInvalidCRC", "TUPLE_DTYPE", "STATUS_NAMES"]
+
+# data/logRecord.go:10-16 / :20-26
+LogRecordNormal, LogRecordDeleted, LogRecordTxnCommit, LogRecordTxnRollback, LogRecordTxnBegin = range(5)
+String, Hash, List, ListMeta, Set = range(5)
+
+STATUS_NAMES = {END_EOF: "EOF", END_ZERO: "EOF(zero header)", END_TORN: "EOF(torn record)",
+                ERR_CRC: "ErrInvalidCRC", ERR_TRUNC5: "panic(5-byte tail)",
+                ERR_VARINT: "panic(varint overflow)", ERR_OFFSET: "mmap: invalid ReadAt offset"}
+
+
+class ScanError(RuntimeError):
+    def __init__(self, code, msg=""):
+        self.code = code
+        super().__init__("clyscan error %d: %s %s" % (code, STATUS_NAMES.get(code, ""), msg))
+
+
+class ErrInvalidCRC(ScanError):
+    """public.ErrInvalidCRC (public/errors.go:13)."""
+
+
+class LogPos(tuple):
+    """data.LogPos{Fid, Offset} (data/logRecord.go:52-55)."""
+    __slots__ = ()
+
+    def __new__(cls, fid, offset):
+        return tuple.__new__(cls, (fid, offset))
+
+    fid = property(lambda s: s[0])
+    offset = property(lambda s: s[1])
+
+
+class LogRecord:
+    """data.LogRecord (data/logRecord.go:43-49); Key/Value are views of the file bytes."""
+    __slots__ = ("key", "value", "type", "data_type", "expiration")
+
+    def __init__(self, key, value, type, data_type, expiration):
+        self.key, self.value, self.type, self.data_type, self.expiration = key, value, type, data_type, expiration
+
+
+class DataFile:
+    """A data file's bytes (host memory) plus its file id (data/dataFile.go:12-17)."""
+
+    def __init__(self, data, fid=0):
+        self.data = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        self.fid = fid
+
+    @classmethod
+    def from_path(cls, path, fid=None):
+        if fid is None:
+            fid = int(os.path.basename(path).split(".")[0])    # "%09d.cly", db.go:452-458
+        arr = np.fromfile(path, dtype=np.uint8) if os.path.getsize(path) else np.zeros(0, np.uint8)
+        return cls(arr, fid)
+
+
+class ScanResult:
+    """Output of one scan call: tuples (numpy structured array, TUPLE_DTYPE) in
+    file order, per-file first index, n_records, end_offset and status."""
+
+    def __init__(self, files, tuples, file_first, res, stats):
+        self.files = files
+        self.tuples = tuples
+        self.file_first = file_first
+        self.n_records = [r.n_records for r in res]
+        self.end_offset = [r.end_offset for r in res]
+        self.status = [r.status for r in res]
+        self.stats = stats
+
+    def file_tuples(self, i):
+        a = self.file_first[i]
+        return self.tuples[a:a + self.n_records[i]]
+
+    def records(self, i):
+        """Yield (LogRecord, size) exactly as repeated ReadLogRecord calls do; raise
+        ErrInvalidCRC / ScanError where the reference returns an error."""
+        f = self.files[i]
+        buf = f.data
+        for t in self.file_tuples(i):
+            o, h, ks, vs = int(t["offset"]), int(t["header_size"]), int(t["key_size"]), int(t["value_size"])
+            key = buf[o + h:o + h + ks].tobytes()
+            val = buf[o + h + ks:o + h + ks + vs].tobytes()
+            yield LogRecord(key, val, int(t["type"]), int(t["data_type"]), int(t["expiration"])), int(t["size"])
+        st = self.status[i]
+        if st == ERR_CRC:
+            raise ErrInvalidCRC(st, "at offset %d" % self.end_offset[i])
+        if st < 0:
+            raise ScanError(st, "at offset %d" % self.end_offset[i])
+
+
+class Scanner:
+    """One GPU context (cly_ctx).  Not thread-safe; one per device."""
+
+    def __init__(self, device=0, lib="libclyscan.so"):
+        self.lib = _abi.load_scan_lib(lib)
+        self.ctx = ctypes.c_void_p()
+        rc = self.lib.cly_ctx_create(device, ctypes.byref(self.ctx))
+        if rc != 0:
+            raise ScanError(rc, "cly_ctx_create(device=%d)" % device)
+
+    def close(self):
+        if self.ctx:
+            self.lib.cly_ctx_destroy(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _file_array(files, device_ptrs=None):
+        arr = (_abi.ClyFile * max(1, len(files)))()
+        for i, f in enumerate(files):
+            if device_ptrs is None:
+                arr[i].base = f.data.ctypes.data if len(f.data) else None
+                arr[i].len = len(f.data)
+            else:
+                arr[i].base, arr[i].len = device_ptrs[i]
+            arr[i].fid = f.fid if hasattr(f, "fid") else f[2]
+        return arr
+
+    def scan(self, files):
+        """Host-memory path (cly_scan): H2D, scan, D2H."""
+        files = list(files)
+        arr = self._file_array(files)
+        cap = int(self.lib.cly_scan_capacity(arr, len(files)))
+        out = np.zeros(max(cap, 1), dtype=TUPLE_DTYPE)
+        first = (ctypes.c_uint64 * max(1, len(files)))()
+        res = (_abi.ClyFileResult * max(1, len(files)))()
+        need = ctypes.c_uint64()
+        st = _abi.ClyStats()
+        rc = self.lib.cly_scan(self.ctx, arr, len(files), out.ctypes.data, cap, first, res,
+                               ctypes.byref(need), ctypes.byref(st))
+        if rc == _abi.ERR_CAPACITY:
+            out = np.zeros(int(need.value), dtype=TUPLE_DTYPE)
+            rc = self.lib.cly_scan(self.ctx, arr, len(files), out.ctypes.data, int(need.value), first, res,
+                                   ctypes.byref(need), ctypes.byref(st))
+        if rc != 0:
+            raise ScanError(rc, self.lib.cly_strerror(rc).decode())
+        n = len(files)
+        return ScanResult(files, out[:int(need.value)], [int(first[i]) for i in range(n)],
+                          [res[i] for i in range(n)], st)
+
+    def scan_device(self, dev_files, d_out, out_cap, stream=None):
+        """Device-resident path: dev_files = [(device_ptr, len, fid)], d_out =
+        device pointer of out_cap tuples.  Returns (file_first, results, stats, needed)."""
+        n = len(dev_files)
+        arr = (_abi.ClyFile * max(1, n))()
+        for i, (ptr, ln, fid) in enumerate(dev_files):
+            arr[i].base, arr[i].len, arr[i].fid = ptr, ln, fid
+        first = (ctypes.c_uint64 * max(1, n))()
+        res = (_abi.ClyFileResult * max(1, n))()
+        need = ctypes.c_uint64()
+        st = _abi.ClyStats()
+        rc = self.lib.cly_scan_device(self.ctx, arr, n, d_out, out_cap, first, res, ctypes.byref(need),
+                                      ctypes.byref(st), stream)
+        if rc != 0:
+            raise ScanError(rc, self.lib.cly_strerror(rc).decode())
+        return [int(first[i]) for i in range(n)], [res[i] for i in range(n)], st, int(need.value)
+
+
+def build_info(lib="libclyscan.so"):
+    return _abi.load_scan_lib(lib).cly_build_info().decode()

@@ -1,0 +1,115 @@
+"""ctypes declarations of the C-ABI in include/clyscan.h and include/clygen.h.
+
+The shared libraries are built in-tree by ``__graft_entry__.build()`` (or
+``make -C couloydb_amd/csrc``).  Loading fails loudly when they are missing:
+there is no CPU fallback for the scan.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+
+# status codes (include/clyscan.h)
+END_EOF, END_ZERO, END_TORN = 0, 1, 2
+ERR_CRC, ERR_TRUNC5, ERR_VARINT, ERR_OFFSET = -1, -2, -3, -4
+OK, ERR_CAPACITY, ERR_DEVICE, ERR_ARG, ERR_NOREPAIR = 0, -10, -11, -12, -13
+
+
+class ClyFile(ctypes.Structure):
+    _fields_ = [("base", ctypes.c_void_p), ("len", ctypes.c_uint64),
+                ("fid", ctypes.c_uint32), ("_pad", ctypes.c_uint32)]
+
+
+class ClyFileResult(ctypes.Structure):
+    _fields_ = [("n_records", ctypes.c_uint64), ("end_offset", ctypes.c_int64),
+                ("status", ctypes.c_int32), ("_pad", ctypes.c_int32)]
+
+
+class ClyStats(ctypes.Structure):
+    _fields_ = [("scan_ms", ctypes.c_double), ("resolve_ms", ctypes.c_double),
+                ("total_ms", ctypes.c_double), ("passes", ctypes.c_uint32),
+                ("n_chunks", ctypes.c_uint32), ("bytes", ctypes.c_uint64),
+                ("records", ctypes.c_uint64)]
+
+
+class ClyGenRec(ctypes.Structure):
+    _fields_ = [("dst", ctypes.c_uint64), ("key_index", ctypes.c_uint32),
+                ("value_len", ctypes.c_uint32), ("tx_id", ctypes.c_int64),
+                ("type", ctypes.c_uint8), ("dtype", ctypes.c_uint8),
+                ("value_mode", ctypes.c_uint8), ("_pad", ctypes.c_uint8),
+                ("_pad2", ctypes.c_int32)]
+
+
+# numpy view of cly_tuple (48 bytes)
+TUPLE_DTYPE = np.dtype([
+    ("offset", "<i8"), ("expiration", "<i8"), ("tx_id", "<i8"),
+    ("fid", "<u4"), ("size", "<u4"), ("key_size", "<u4"), ("value_size", "<u4"),
+    ("type", "u1"), ("data_type", "u1"), ("header_size", "u1"), ("txid_len", "u1"),
+    ("crc", "<u4")])
+assert TUPLE_DTYPE.itemsize == 48
+
+GEN_DTYPE = np.dtype([("dst", "<u8"), ("key_index", "<u4"), ("value_len", "<u4"),
+                      ("tx_id", "<i8"), ("type", "u1"), ("dtype", "u1"),
+                      ("value_mode", "u1"), ("_pad", "u1"), ("_pad2", "<i4")])
+assert GEN_DTYPE.itemsize == 32
+
+SCAN_SYMBOLS = ["cly_ctx_create", "cly_ctx_destroy", "cly_scan_capacity", "cly_scan",
+                "cly_scan_device", "cly_strerror", "cly_build_info"]
+GEN_SYMBOLS = ["cly_gen_record_size", "cly_gen_layout", "cly_gen_encode"]
+
+_libs = {}
+
+
+def lib_path(name="libclyscan.so"):
+    return os.path.join(PKG_DIR, name)
+
+
+def load_scan_lib(name="libclyscan.so"):
+    """Load (once) and type the scan library; raises if it is not built."""
+    if name in _libs:
+        return _libs[name]
+    path = lib_path(name)
+    if not os.path.exists(path):
+        raise RuntimeError("%s is not built (run __graft_entry__.build()); the scan has no CPU fallback" % path)
+    lib = ctypes.CDLL(path)
+    P = ctypes.POINTER
+    lib.cly_ctx_create.argtypes = [ctypes.c_int, P(ctypes.c_void_p)]
+    lib.cly_ctx_create.restype = ctypes.c_int
+    lib.cly_ctx_destroy.argtypes = [ctypes.c_void_p]
+    lib.cly_ctx_destroy.restype = None
+    lib.cly_scan_capacity.argtypes = [P(ClyFile), ctypes.c_int]
+    lib.cly_scan_capacity.restype = ctypes.c_uint64
+    lib.cly_scan.argtypes = [ctypes.c_void_p, P(ClyFile), ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                             P(ctypes.c_uint64), P(ClyFileResult), P(ctypes.c_uint64), P(ClyStats)]
+    lib.cly_scan.restype = ctypes.c_int
+    lib.cly_scan_device.argtypes = [ctypes.c_void_p, P(ClyFile), ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                                    P(ctypes.c_uint64), P(ClyFileResult), P(ctypes.c_uint64), P(ClyStats),
+                                    ctypes.c_void_p]
+    lib.cly_scan_device.restype = ctypes.c_int
+    lib.cly_strerror.argtypes = [ctypes.c_int]
+    lib.cly_strerror.restype = ctypes.c_char_p
+    lib.cly_build_info.argtypes = []
+    lib.cly_build_info.restype = ctypes.c_char_p
+    _libs[name] = lib
+    return lib
+
+
+def load_gen_lib():
+    if "gen" in _libs:
+        return _libs["gen"]
+    path = lib_path("libclygen.so")
+    if not os.path.exists(path):
+        raise RuntimeError("%s is not built (run __graft_entry__.build())" % path)
+    lib = ctypes.CDLL(path)
+    P = ctypes.POINTER
+    lib.cly_gen_record_size.argtypes = [ctypes.c_int64, ctypes.c_uint32]
+    lib.cly_gen_record_size.restype = ctypes.c_uint64
+    lib.cly_gen_layout.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                   P(ctypes.c_uint64), P(ctypes.c_uint64), ctypes.c_uint32, P(ctypes.c_uint32)]
+    lib.cly_gen_layout.restype = ctypes.c_uint64
+    lib.cly_gen_encode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]
+    lib.cly_gen_encode.restype = ctypes.c_int
+    _libs["gen"] = lib
+    return lib

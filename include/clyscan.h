@@ -1,0 +1,133 @@
+/*
+ * clyscan.h — C-ABI drop-in boundary for CouloyDB's full-data-file log-record
+ * scan, executed on an AMD Instinct MI355X (gfx950).
+ *
+ * Reference interface replaced (paths relative to the CouloyDB tree):
+ *   func (df *DataFile) ReadLogRecord(offset int64) (*LogRecord, int64, error)
+ *       data/dataFile.go:64-111, called in a loop "offset += size until io.EOF"
+ *       by db.loadIndex          db.go:582-637   (index rebuild at open)
+ *          db.merge              merge.go:90-143 (compaction)
+ *          db.loadIndexFromHintFile merge.go:257-287 (hint file)
+ *   DecodeLogRecordHeader        data/logRecord.go:86-114
+ *   GetLogRecordCRC (+ compare)  data/logRecord.go:136-146, data/dataFile.go:105-109
+ *   parseLogRecordKey            db.go:706-710   (tx_id / txid_len in cly_tuple)
+ *
+ * One call scans whole files: for every file it returns exactly the sequence of
+ * records that repeated ReadLogRecord(offset) calls return from offset 0, and the
+ * way that loop stops (io.EOF variants, ErrInvalidCRC, or the reference's panics
+ * mapped to error codes).  Plain C types only; no HIP/torch types cross the ABI.
+ *
+ * Threading: a cly_ctx owns one GPU's scratch memory and one HIP stream; calls on
+ * one context must be serialised by the caller (the reference scans on a single
+ * goroutine during open, db.go:104-112).  Use one context per GPU.
+ * Ownership: every buffer is caller-owned; nothing is retained after return.
+ */
+#ifndef CLYSCAN_H
+#define CLYSCAN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- per-file terminal status (cly_file_result.status) --------------------
+ * >= 0 : the reference loop sees io.EOF and stops cleanly (db.go:594-595).
+ * <  0 : the reference returns an error (or panics) out of loadIndex/merge.   */
+#define CLY_END_EOF      0   /* <=4 bytes left: DecodeLogRecordHeader -> nil   (logRecord.go:87-89, dataFile.go:82-84) */
+#define CLY_END_ZERO     1   /* crc==0 && KeySize==0 && ValueSize==0            (dataFile.go:85-87)                   */
+#define CLY_END_TORN     2   /* key/value run past EOF: mmap ReadAt short read -> io.EOF (dataFile.go:94-98)          */
+#define CLY_ERR_CRC     -1   /* public.ErrInvalidCRC                            (dataFile.go:105-109)                 */
+#define CLY_ERR_TRUNC5  -2   /* exactly 5 bytes left: buf[5] index panic        (logRecord.go:94)                     */
+#define CLY_ERR_VARINT  -3   /* varint overflow drives a slice index negative, or headerSize<4 at the CRC slice (panics) */
+#define CLY_ERR_OFFSET  -4   /* key/value read at a negative offset: "mmap: invalid ReadAt offset" (non-EOF error)    */
+
+/* ---- API return codes ---------------------------------------------------- */
+#define CLY_OK              0
+#define CLY_ERR_CAPACITY  -10  /* out_cap too small for the records found            */
+#define CLY_ERR_DEVICE    -11  /* HIP runtime error                                  */
+#define CLY_ERR_ARG       -12  /* bad argument (null pointer, file >= 4 GiB, ...)    */
+#define CLY_ERR_NOREPAIR  -13  /* speculation repair did not converge (never seen)   */
+
+/* A data file (`%09d.cly`, hint-index or merge-finished file).  For cly_scan the
+ * base is host memory (typically an mmap of the file); for cly_scan_device it is
+ * device memory (HBM) that holds the file's bytes.  len must be < 2^32.        */
+typedef struct cly_file {
+    const uint8_t* base;
+    uint64_t       len;
+    uint32_t       fid;       /* data.LogPos.Fid of records in this file        */
+    uint32_t       _pad;
+} cly_file;
+
+/* One decoded record = one successful ReadLogRecord call (48 bytes, file order).
+ * Key bytes live at base[offset+header_size .. offset+header_size+key_size);
+ * the realKey of parseLogRecordKey starts txid_len bytes later.                */
+typedef struct cly_tuple {
+    int64_t  offset;          /* LogPos.Offset (db.go:601)                      */
+    int64_t  expiration;      /* LogRecord.Expiration                           */
+    int64_t  tx_id;           /* parseLogRecordKey txId (db.go:707); 0 if none  */
+    uint32_t fid;             /* LogPos.Fid                                     */
+    uint32_t size;            /* recordSize returned by ReadLogRecord           */
+    uint32_t key_size;        /* LogRecordHeader.KeySize                        */
+    uint32_t value_size;      /* LogRecordHeader.ValueSize                      */
+    uint8_t  type;            /* LogRecord.Type  (0 Normal .. 4 TxnBegin)        */
+    uint8_t  data_type;       /* LogRecord.DataType (0 String .. 4 Set)          */
+    uint8_t  header_size;     /* headerSize from DecodeLogRecordHeader          */
+    uint8_t  txid_len;        /* bytes of the txId varint; 0xFF = Varint overflow
+                                 (parseLogRecordKey would panic)                 */
+    uint32_t crc;             /* stored (and verified) CRC32-IEEE               */
+} cly_tuple;
+
+typedef struct cly_file_result {
+    uint64_t n_records;       /* tuples emitted for this file                   */
+    int64_t  end_offset;      /* EOF statuses: final offset (= activityFile.WriteOff,
+                                 db.go:634-636); errors: offset of the failing record */
+    int32_t  status;          /* CLY_END_* / CLY_ERR_*                           */
+    int32_t  _pad;
+} cly_file_result;
+
+/* Timing of the last call (device work only; filled when requested).          */
+typedef struct cly_stats {
+    double   scan_ms;         /* decode+CRC kernel(s), HIP events              */
+    double   resolve_ms;      /* chain resolution + per-file result kernel     */
+    double   total_ms;        /* whole device pipeline incl. repair passes     */
+    uint32_t passes;          /* 1 = speculation verified first time           */
+    uint32_t n_chunks;
+    uint64_t bytes;           /* input bytes scanned                           */
+    uint64_t records;         /* tuples emitted over all files                 */
+} cly_stats;
+
+typedef struct cly_ctx cly_ctx;
+
+int  cly_ctx_create(int device, cly_ctx** out);
+void cly_ctx_destroy(cly_ctx* ctx);
+
+/* Upper bound on tuples for files whose records are >= 9 bytes (every record
+ * the reference writer produces is).  Exotic records shorter than that make
+ * cly_scan* return CLY_ERR_CAPACITY with the exact need in *needed.            */
+uint64_t cly_scan_capacity(const cly_file* files, int nfiles);
+
+/* Host-memory entry (the cgo path): copies the files to HBM, scans them, and
+ * copies tuples back.  file_first[i] = index in `out` of file i's first tuple. */
+int cly_scan(cly_ctx* ctx, const cly_file* files, int nfiles,
+             cly_tuple* out, uint64_t out_cap,
+             uint64_t* file_first, cly_file_result* res,
+             uint64_t* needed, cly_stats* stats);
+
+/* Device-resident entry: files[i].base are device pointers, d_out is device
+ * memory; file_first/res/needed/stats are host memory.  `stream` is a
+ * hipStream_t passed as void* (NULL = the context's own stream).               */
+int cly_scan_device(cly_ctx* ctx, const cly_file* files, int nfiles,
+                    cly_tuple* d_out, uint64_t out_cap,
+                    uint64_t* file_first, cly_file_result* res,
+                    uint64_t* needed, cly_stats* stats, void* stream);
+
+const char* cly_strerror(int code);
+
+/* Library build identification (gfx target, kernel configuration).            */
+const char* cly_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CLYSCAN_H */

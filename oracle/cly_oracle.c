@@ -1,0 +1,309 @@
+/*
+ * cly_oracle.c — TEST INFRASTRUCTURE ONLY (see cly_oracle.h).
+ *
+ * Scalar CPU restatement of the CouloyDB log-record scan.  Every function cites
+ * the reference lines it follows (paths relative to the CouloyDB source tree).
+ * Parity status: pinned by known-answer vectors + an independent Python
+ * restatement (zlib.crc32) — not by running the Go reference, which cannot be
+ * built here (no Go toolchain).
+ */
+#define _GNU_SOURCE
+#include "cly_oracle.h"
+
+#include <fcntl.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+/* ------------------------------------------------------------------------ */
+/* Go encoding/binary Uvarint / Varint / PutVarint (Go >= 1.18 semantics).   */
+/* Uvarint: at most MaxVarintLen64 = 10 bytes; a 10th byte > 1 or an 11th
+ * byte read is overflow -> (0, -(i+1)); a buffer that ends inside the varint
+ * is (0, 0).  Varint = zigzag(Uvarint).                                      */
+uint64_t clyo_uvarint(const uint8_t* buf, int64_t len, int* n) {
+    uint64_t x = 0;
+    unsigned s = 0;
+    for (int64_t i = 0; i < len; i++) {
+        uint8_t b = buf[i];
+        if (i == 10) { *n = -(int)(i + 1); return 0; }
+        if (b < 0x80) {
+            if (i == 9 && b > 1) { *n = -(int)(i + 1); return 0; }
+            *n = (int)(i + 1);
+            return x | ((uint64_t)b << s);
+        }
+        x |= (uint64_t)(b & 0x7f) << s;
+        s += 7;
+    }
+    *n = 0;
+    return 0;
+}
+
+int64_t clyo_varint(const uint8_t* buf, int64_t len, int* n) {
+    uint64_t ux = clyo_uvarint(buf, len, n);
+    int64_t x = (int64_t)(ux >> 1);
+    if (ux & 1) x = ~x;
+    return x;
+}
+
+int clyo_put_varint(uint8_t* buf, int64_t x) {
+    uint64_t ux = (uint64_t)x << 1;
+    if (x < 0) ux = ~ux;
+    int i = 0;
+    while (ux >= 0x80) { buf[i++] = (uint8_t)(ux | 0x80); ux >>= 7; }
+    buf[i++] = (uint8_t)ux;
+    return i;
+}
+
+/* ------------------------------------------------------------------------ */
+/* CRC-32/IEEE (reflected poly 0xEDB88320, init/xorout 0xFFFFFFFF): Go's
+ * crc32.ChecksumIEEE / crc32.Update(crc, IEEETable, p).  Slicing-by-8 with
+ * tables generated from the polynomial at first use.                        */
+static uint32_t g_tab[8][256];
+static pthread_once_t g_tab_once = PTHREAD_ONCE_INIT;
+
+static void build_tables(void) {
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+        g_tab[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; i++)
+        for (int t = 1; t < 8; t++)
+            g_tab[t][i] = (g_tab[t - 1][i] >> 8) ^ g_tab[0][g_tab[t - 1][i] & 0xff];
+}
+
+uint32_t clyo_crc32_update(uint32_t crc, const uint8_t* p, size_t len) {
+    pthread_once(&g_tab_once, build_tables);
+    crc = ~crc;
+    while (len && ((uintptr_t)p & 7)) { crc = g_tab[0][(crc ^ *p++) & 0xff] ^ (crc >> 8); len--; }
+    while (len >= 8) {
+        uint32_t lo, hi;
+        memcpy(&lo, p, 4); memcpy(&hi, p + 4, 4);
+        lo ^= crc;
+        crc = g_tab[7][lo & 0xff] ^ g_tab[6][(lo >> 8) & 0xff] ^ g_tab[5][(lo >> 16) & 0xff] ^
+              g_tab[4][lo >> 24] ^ g_tab[3][hi & 0xff] ^ g_tab[2][(hi >> 8) & 0xff] ^
+              g_tab[1][(hi >> 16) & 0xff] ^ g_tab[0][hi >> 24];
+        p += 8; len -= 8;
+    }
+    while (len--) crc = g_tab[0][(crc ^ *p++) & 0xff] ^ (crc >> 8);
+    return ~crc;
+}
+
+static inline uint32_t le32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+/* ------------------------------------------------------------------------ */
+/* DataFile.ReadLogRecord (data/dataFile.go:64-111) with DecodeLogRecordHeader
+ * (data/logRecord.go:86-114) and GetLogRecordCRC (data/logRecord.go:136-146)
+ * inlined, reading through golang.org/x/exp/mmap ReaderAt.ReadAt semantics
+ * (off<0 || off>len -> error; short read -> io.EOF).                         */
+int clyo_read_log_record(const uint8_t* F, uint64_t n, uint64_t off, clyo_tuple* t) {
+    const int64_t fileSize = (int64_t)n;                 /* dataFile.go:65 Writer.Size() */
+    int64_t headerBytes = 26;                            /* maxLogRecordHeaderSize, logRecord.go:31 */
+    if ((int64_t)off + 26 > fileSize) headerBytes = fileSize - (int64_t)off;   /* :70-73 */
+    /* readNBytes(headerBytes, off) :76 — a full read (headerBytes <= n-off).  */
+    const uint8_t* buf = F + off;
+    if (headerBytes <= 4) return CLYO_END_EOF;           /* logRecord.go:87-89 -> dataFile.go:82-84 */
+    if (headerBytes == 5) return CLYO_ERR_TRUNC5;        /* logRecord.go:94: buf[5] out of range -> panic */
+    uint32_t crc = le32(buf);                            /* logRecord.go:92 */
+    uint8_t type = buf[4], dtype = buf[5];               /* :93-94 */
+    int64_t idx = 6;                                     /* :97 */
+    int a, b, c;
+    /* each binary.Varint(buf[index:]) slices first: a negative index panics */
+    int64_t ks = clyo_varint(buf + idx, headerBytes - idx, &a); idx += a;     /* :100-102 */
+    if (idx < 0) return CLYO_ERR_VARINT;
+    int64_t vs = clyo_varint(buf + idx, headerBytes - idx, &b); idx += b;     /* :105-107 */
+    if (idx < 0) return CLYO_ERR_VARINT;
+    int64_t exp = clyo_varint(buf + idx, headerBytes - idx, &c); idx += c;    /* :109-111 */
+    uint32_t KS = (uint32_t)ks, VS = (uint32_t)vs;       /* uint32() truncation, :101,:106 */
+    const int64_t headerSize = idx;                      /* :113 */
+    if (crc == 0 && KS == 0 && VS == 0) return CLYO_END_ZERO;   /* dataFile.go:85-87 */
+    const int64_t kv = (int64_t)KS + (int64_t)VS;        /* :89 */
+    if (kv > 0) {                                        /* :94 readNBytes(ks+vs, off+headerSize) */
+        int64_t koff = (int64_t)off + headerSize;
+        if (koff < 0 || koff > fileSize) return CLYO_ERR_OFFSET;  /* mmap: invalid ReadAt offset */
+        if (fileSize - koff < kv) return CLYO_END_TORN;           /* short read -> io.EOF */
+    }
+    if (headerSize < 4) return CLYO_ERR_VARINT;          /* headerBuf[4:headerSize] panics (:105) */
+    /* GetLogRecordCRC: ChecksumIEEE(header[4:hs]) then Update(key), Update(value):
+     * the bytes are contiguous, F[off+4 : off+headerSize+kv]. */
+    uint32_t got = clyo_crc32_update(0, buf + 4, (size_t)(headerSize - 4 + kv));
+    if (got != crc) return CLYO_ERR_CRC;                 /* dataFile.go:105-109 */
+    t->offset = (int64_t)off;
+    t->expiration = exp;
+    t->fid = 0;
+    t->size = (uint32_t)(headerSize + kv);
+    t->key_size = KS;
+    t->value_size = VS;
+    t->type = type;
+    t->data_type = dtype;
+    t->header_size = (uint8_t)headerSize;
+    t->crc = crc;
+    /* parseLogRecordKey (db.go:706-710): Varint over the key bytes */
+    int tn;
+    int64_t tx = clyo_varint(buf + headerSize, (int64_t)KS, &tn);
+    if (tn < 0) { t->tx_id = 0; t->txid_len = 0xFF; }   /* key[n:] with n<0 panics in the reference */
+    else { t->tx_id = tx; t->txid_len = (uint8_t)tn; }
+    return CLYO_REC;
+}
+
+/* db.loadIndex inner loop (db.go:590-631) for one file. */
+uint64_t clyo_scan_file(const uint8_t* F, uint64_t n, uint32_t fid,
+                        clyo_tuple* out, uint64_t cap,
+                        int64_t* end_offset, int32_t* status) {
+    uint64_t off = 0, cnt = 0;
+    for (;;) {
+        clyo_tuple t;
+        int r = clyo_read_log_record(F, n, off, &t);     /* db.go:592 */
+        if (r != CLYO_REC) { *status = r; *end_offset = (int64_t)off; return cnt; }
+        t.fid = fid;                                     /* db.go:601 LogPos{Fid, Offset} */
+        if (cnt < cap) out[cnt] = t;
+        cnt++;
+        off += t.size;                                   /* db.go:630 */
+    }
+}
+
+/* EncodeLogRecord (data/logRecord.go:57-84). */
+uint64_t clyo_encode_record(uint8_t* out, uint8_t type, uint8_t dtype,
+                            const uint8_t* key, uint64_t klen,
+                            const uint8_t* val, uint64_t vlen, int64_t expiration) {
+    out[4] = type;                                       /* :62 */
+    out[5] = dtype;                                      /* :63 */
+    int idx = 6;
+    idx += clyo_put_varint(out + idx, (int64_t)klen);    /* :66 */
+    idx += clyo_put_varint(out + idx, (int64_t)vlen);    /* :67 */
+    idx += clyo_put_varint(out + idx, expiration);       /* :68 */
+    if (klen) memmove(out + idx, key, klen);             /* :75 */
+    if (vlen) memmove(out + idx + klen, val, vlen);      /* :77 */
+    uint64_t size = (uint64_t)idx + klen + vlen;         /* :70 */
+    uint32_t crc = clyo_crc32_update(0, out + 4, size - 4);   /* :80 */
+    out[0] = (uint8_t)crc; out[1] = (uint8_t)(crc >> 8);      /* :81 LittleEndian */
+    out[2] = (uint8_t)(crc >> 16); out[3] = (uint8_t)(crc >> 24);
+    return size;
+}
+
+/* ------------------------------------------------------------------------ */
+/* "ref-faithful" CPU baseline: the reference's per-call I/O pattern.        */
+static int mmap_read(const char* path, uint8_t* dst, int64_t len, int64_t off, int* eof) {
+    /* driver/mmap.go:25-32 -> x/exp/mmap Open (open, fstat, mmap, close) +
+     * ReadAt + Close (munmap), once per readNBytes call. */
+    *eof = 0;
+    int fd = open(path, O_RDONLY);
+    if (fd < 0) return -1;
+    struct stat st;
+    if (fstat(fd, &st) != 0) { close(fd); return -1; }
+    int64_t size = st.st_size;
+    uint8_t* data = NULL;
+    if (size > 0) {
+        data = (uint8_t*)mmap(NULL, (size_t)size, PROT_READ, MAP_SHARED, fd, 0);
+        if (data == MAP_FAILED) { close(fd); return -1; }
+    }
+    close(fd);
+    int rc = 0;
+    if (off < 0 || off > size) rc = -1;
+    else {
+        int64_t avail = size - off, cp = len < avail ? len : avail;
+        if (cp > 0) memcpy(dst, data + off, (size_t)cp);
+        if (cp < len) *eof = 1;
+    }
+    if (data) munmap(data, (size_t)size);
+    return rc;
+}
+
+int64_t clyo_scan_path_faithful(const char* path, uint32_t fid, uint64_t max_records,
+                                int64_t* end_offset, int32_t* status) {
+    (void)fid;
+    int wfd = open(path, O_RDONLY);                      /* Writer: driver/fileIO.go */
+    if (wfd < 0) return -1;
+    int64_t off = 0, cnt = 0;
+    uint8_t hdr[26];
+    *status = CLYO_REC;                                  /* stopped by max_records */
+    for (;;) {
+        if (max_records && (uint64_t)cnt >= max_records) break;
+        struct stat st;
+        if (fstat(wfd, &st) != 0) { close(wfd); return -1; }   /* dataFile.go:65 */
+        int64_t fileSize = st.st_size;
+        int64_t hb = 26;
+        if (off + 26 > fileSize) hb = fileSize - off;
+        int eof;
+        if (mmap_read(path, hdr, hb, off, &eof) != 0) { close(wfd); return -1; }
+        int64_t kvLen = 0, hsz = 0;
+        {   /* decode with the same semantics as clyo_read_log_record */
+            if (hb <= 4) { *status = CLYO_END_EOF; break; }
+            if (hb == 5) { *status = CLYO_ERR_TRUNC5; break; }
+            int a, b, c;
+            int64_t idx = 6;
+            int64_t ks = clyo_varint(hdr + idx, hb - idx, &a); idx += a;
+            if (idx < 0) { *status = CLYO_ERR_VARINT; break; }
+            int64_t vs = clyo_varint(hdr + idx, hb - idx, &b); idx += b;
+            if (idx < 0) { *status = CLYO_ERR_VARINT; break; }
+            (void)clyo_varint(hdr + idx, hb - idx, &c); idx += c;
+            uint32_t crc = le32(hdr), KS = (uint32_t)ks, VS = (uint32_t)vs;
+            if (crc == 0 && KS == 0 && VS == 0) { *status = CLYO_END_ZERO; break; }
+            hsz = idx;
+            kvLen = (int64_t)KS + VS;
+            uint8_t* kvb = (uint8_t*)malloc(kvLen > 0 ? (size_t)kvLen : 1);   /* make([]byte, n) */
+            if (kvLen > 0) {
+                int e2;
+                if (mmap_read(path, kvb, kvLen, off + hsz, &e2) != 0) { free(kvb); *status = CLYO_ERR_OFFSET; break; }
+                if (e2) { free(kvb); *status = CLYO_END_TORN; break; }
+            }
+            if (hsz < 4) { free(kvb); *status = CLYO_ERR_VARINT; break; }
+            uint32_t got = clyo_crc32_update(0, hdr + 4, (size_t)(hsz - 4));
+            got = clyo_crc32_update(got, kvb, (size_t)kvLen);
+            free(kvb);
+            if (got != crc) { *status = CLYO_ERR_CRC; break; }
+        }
+        cnt++;
+        off += hsz + kvLen;
+    }
+    *end_offset = off;
+    close(wfd);
+    return cnt;
+}
+
+/* ------------------------------------------------------------------------ */
+/* "ref-algorithm" CPU baseline: clyo_scan_file over files on nthreads.      */
+typedef struct {
+    const uint8_t* const* bases; const uint64_t* lens; const uint32_t* fids;
+    int nfiles, tid, nthreads; uint64_t records;
+} mt_arg;
+
+static void* mt_worker(void* p) {
+    mt_arg* a = (mt_arg*)p;
+    enum { CAP = 4096 };
+    clyo_tuple* scratch = (clyo_tuple*)malloc(sizeof(clyo_tuple) * CAP);
+    for (int f = a->tid; f < a->nfiles; f += a->nthreads) {
+        const uint8_t* F = a->bases[f];
+        uint64_t n = a->lens[f], off = 0, k = 0;
+        for (;;) {
+            clyo_tuple t;
+            if (clyo_read_log_record(F, n, off, &t) != CLYO_REC) break;
+            t.fid = a->fids[f];
+            scratch[k++ & (CAP - 1)] = t;                /* the tuple stream the index consumes */
+            off += t.size;
+        }
+        a->records += k;
+    }
+    free(scratch);
+    return NULL;
+}
+
+uint64_t clyo_scan_files_mt(const uint8_t* const* bases, const uint64_t* lens,
+                            const uint32_t* fids, int nfiles, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    pthread_t th[256];
+    mt_arg args[256];
+    if (nthreads > 256) nthreads = 256;
+    for (int i = 0; i < nthreads; i++) {
+        args[i] = (mt_arg){bases, lens, fids, nfiles, i, nthreads, 0};
+        pthread_create(&th[i], NULL, mt_worker, &args[i]);
+    }
+    uint64_t total = 0;
+    for (int i = 0; i < nthreads; i++) { pthread_join(th[i], NULL); total += args[i].records; }
+    return total;
+}

@@ -1,0 +1,157 @@
+"""GPU parity tests: the HIP scan (through the C-ABI) against the golden fixtures
+and the CPU oracle, bit-exact, plus size-independent properties at the
+BASELINE.json config-2 size.  Run on an MI355X: pytest -m gpu."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from couloydb_amd import DataFile, Scanner, TUPLE_DTYPE, _abi
+from oracle import cly_oracle as co
+
+from .gpu_util import FIELDS, compare, fixed_records_file, mixed_corpus
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+with open(os.path.join(GOLD, "golden.json")) as _f:
+    GOLDEN = json.load(_f)
+FIXTURES = sorted(k for k in GOLDEN if not k.startswith("_"))
+LIBS = ["libclyscan.so", "libclyscan_small.so"]
+
+
+def fixture_file(name):
+    with open(os.path.join(GOLD, name + ".cly"), "rb") as f:
+        return DataFile(np.frombuffer(f.read(), np.uint8).copy(), GOLDEN[name]["fid"])
+
+
+@pytest.fixture(scope="module", params=LIBS)
+def scanner(request):
+    s = Scanner(0, lib=request.param)
+    yield s
+    s.close()
+
+
+def as_lists(t):
+    return [[int(r[f]) for f in FIELDS] for r in t]
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_fixture(scanner, name):
+    g = GOLDEN[name]
+    r = scanner.scan([fixture_file(name)])
+    assert (r.status[0], r.end_offset[0], r.n_records[0]) == (g["status"], g["end_offset"], g["n_records"])
+    assert as_lists(r.file_tuples(0)) == g["tuples"]
+
+
+def test_all_fixtures_one_call(scanner):
+    files = [fixture_file(n) for n in FIXTURES]
+    r = scanner.scan(files)
+    for i, n in enumerate(FIXTURES):
+        g = GOLDEN[n]
+        assert (r.status[i], r.end_offset[i]) == (g["status"], g["end_offset"]), n
+        assert as_lists(r.file_tuples(i)) == g["tuples"], n
+
+
+def test_records_iterator_matches_readlogrecord(scanner):
+    import make_golden as mg
+    f = fixture_file("txn_hash")
+    r = scanner.scan([f])
+    recs = list(r.records(0))
+    assert [s for _, s in recs] == [t[4] for t in GOLDEN["txn_hash"]["tuples"]]
+    raw = f.data.tobytes()
+    off = 0
+    for rec, size in recs:
+        st, t = mg.read_log_record(raw, off)
+        h = t["header_size"]
+        assert rec.key == raw[off + h: off + h + t["key_size"]]
+        assert rec.value == raw[off + h + t["key_size"]: off + t["size"]]
+        assert (rec.type, rec.data_type, rec.expiration) == (t["type"], t["data_type"], t["expiration"])
+        off += size
+    with pytest.raises(Exception):
+        list(scanner.scan([fixture_file("bitflip")]).records(0))
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_mixed_corpus_vs_oracle(scanner, seed):
+    files = []
+    for j in range(3):
+        data = mixed_corpus(seed * 7 + j, [40_000, 300_000, 1_500_000][j], corrupt=(seed % 4 == 3) * (j + 1))
+        files.append(DataFile(np.frombuffer(data, np.uint8).copy(), 1000 + j))
+    r = scanner.scan(files)
+    for i, f in enumerate(files):
+        t, st, end = co.scan_file(f.data, f.fid)
+        compare(r.file_tuples(i), r.status[i], r.end_offset[i], t, st, end, "seed %d file %d" % (seed, i))
+
+
+@pytest.mark.parametrize("shape", ["c1", "zero_values", "tiny"])
+def test_shapes_vs_oracle(scanner, shape):
+    if shape == "c1":       # BASELINE config 1: one 64 MiB file of 1 KiB values
+        data = fixed_records_file(64280, 1024, seed=11)
+    elif shape == "zero_values":   # TestDB_Reboot: value = key || 1024 zero bytes
+        data = fixed_records_file(8000, 1033, seed=12, zero_values=True)
+    else:
+        data = fixed_records_file(200000, 0, seed=13)
+    f = DataFile(data, 0)
+    r = scanner.scan([f])
+    t, st, end = co.scan_file(data, 0)
+    compare(r.file_tuples(0), r.status[0], r.end_offset[0], t, st, end, shape)
+
+
+@pytest.mark.parametrize("cut", [0, 1, 4, 5, 6, 13, 27, 31])
+def test_tails_at_chunk_boundaries(scanner, cut):
+    # lengths around chunk multiples for both builds (32 KiB and 2 KiB chunks)
+    base = fixed_records_file(400, 300, seed=cut)        # 400 x 320 B
+    for chunk in (2048, 32768):
+        k = (len(base) // chunk) * chunk - 7
+        for extra in (0, 3, 7, 8):
+            data = base[:k + extra] if k + extra <= len(base) else base
+            data = np.concatenate([data, np.zeros(cut, np.uint8)]) if cut % 2 else data[: len(data) - cut]
+            f = DataFile(np.ascontiguousarray(data), 5)
+            r = scanner.scan([f])
+            t, st, end = co.scan_file(f.data, 5)
+            compare(r.file_tuples(0), r.status[0], r.end_offset[0], t, st, end, "cut %d chunk %d +%d" % (cut, chunk, extra))
+
+
+def test_bitflips_everywhere_small(scanner):
+    base = fixed_records_file(60, 200, seed=5)
+    rng = np.random.default_rng(0)
+    files = []
+    for k in range(40):
+        d = base.copy()
+        pos = int(rng.integers(0, len(d)))
+        d[pos] ^= np.uint8(1 << int(rng.integers(0, 8)))
+        files.append(DataFile(d, k))
+    r = scanner.scan(files)
+    for i, f in enumerate(files):
+        t, st, end = co.scan_file(f.data, f.fid)
+        compare(r.file_tuples(i), r.status[i], r.end_offset[i], t, st, end, "flip %d" % i)
+
+
+@pytest.mark.slow
+def test_config2_device_generated_properties():
+    """BASELINE config 2 at full size (16 x 256 MiB, 256-B values), generated in
+    HBM: size-independent properties over all files + bit-exact oracle check of
+    one whole file."""
+    torch = pytest.importorskip("torch")
+    from bench import make_workload   # the bench's own input builder
+    wl = make_workload("c2", torch)
+    with Scanner(0) as sc:
+        first, res, st, need = sc.scan_device(wl.dev_files, wl.d_out.data_ptr(), wl.out_cap)
+        assert st.passes == 1
+        assert need == wl.expect_records
+        out = wl.d_out[: need * 48].cpu().numpy().view(TUPLE_DTYPE)
+    for i, (ptr, ln, fid) in enumerate(wl.dev_files):
+        assert res[i].status == 0 and res[i].end_offset == ln
+        t = out[first[i]:first[i] + res[i].n_records]
+        assert res[i].n_records == ln // 276
+        assert (t["size"] == 276).all() and (t["key_size"] == 10).all() and (t["value_size"] == 256).all()
+        assert (t["offset"] == np.arange(len(t), dtype=np.int64) * 276).all()
+        assert (t["fid"] == fid).all() and (t["txid_len"] == 1).all() and (t["tx_id"] == 0).all()
+    # bit-exact against the oracle on file 3 (D2H of the file bytes)
+    ptr, ln, fid = wl.dev_files[3]
+    host = wl.file_bytes(3)
+    t, st_o, end = co.scan_file(host, fid)
+    compare(out[first[3]:first[3] + res[3].n_records], res[3].status, res[3].end_offset, t, st_o, end, "c2 file 3")
