@@ -16,7 +16,7 @@
 //             every record's CRC-32 with LDS slicing tables and a segmented
 //             scan for records spanning lanes, counts records with a decoupled
 //             look-back, and writes cly_tuple entries plus a chunk summary.
-//   k_resolve one workgroup per file: checks the chunk-level speculation
+//   k_check / k_finish: check the chunk-level speculation
 //             (each chunk's guessed entry == its predecessor's exit), finishes
 //             the CRC of records that straddle chunks, and derives the per-file
 //             (n_records, end_offset, status).  A failed check (rare) asks the
@@ -66,7 +66,7 @@ struct DevFile {                 // 32 B
     uint32_t _pad;
 };
 
-struct ChunkSum {                // 64 B, written by k_scan, read by k_resolve
+struct ChunkSum {                // 80 B, written by k_scan, read by k_check / k_finish
     int64_t  entry;              // first chain position used (file offset), -1 none
     int64_t  exit;               // first chain position >= chunk end, or the TERM position
     int64_t  open_pos;           // chain's last record if it is still open at chunk end, else -1
@@ -86,7 +86,7 @@ struct ChunkSum {                // 64 B, written by k_scan, read by k_resolve
 };
 static_assert(sizeof(ChunkSum) == 80, "ChunkSum layout");
 
-struct FileOut {                 // per-file result from k_resolve
+struct FileOut {                 // per-file result from k_finish
     uint64_t n_records;
     int64_t  end_offset;
     int32_t  status;
@@ -100,7 +100,28 @@ struct Globals {                 // small control block, zeroed per pass
     uint32_t lb_timeout;         // look-back spin bound hit (never expected)
     uint32_t overflow;           // tuples beyond out_cap were dropped
     uint64_t total_records;      // inclusive count after the last chunk
+    uint32_t dbg_site;           // CLY_DEBUG builds: first out-of-range global index
+    uint32_t _pad;
+    int64_t  dbg_idx, dbg_lim;
 };
+
+#ifdef CLY_DEBUG
+__device__ int* g_trace;   // host-mapped progress trace (survives a device fault)
+#define TRACE(slot, v) do { if (g_trace) { g_trace[(slot)] = (v); __threadfence_system(); } } while (0)
+// Debug builds check every global index; a violation is recorded (site, index,
+// limit) and the access is redirected to element 0 instead of faulting.
+__device__ __forceinline__ int64_t cly_gidx(int64_t i, int64_t lim, unsigned site, Globals* g) {
+    if (i < 0 || i >= lim) {
+        if (atomicCAS(&g->dbg_site, 0u, site) == 0u) { g->dbg_idx = i; g->dbg_lim = lim; }
+        return 0;
+    }
+    return i;
+}
+#define GIDX(i, lim, site) cly_gidx((int64_t)(i), (int64_t)(lim), (site), g)
+#else
+#define GIDX(i, lim, site) (i)
+#define TRACE(slot, v) do { } while (0)
+#endif
 
 // ---------------------------------------------------------------------------
 // Go encoding/binary Varint (toolchain >= 1.18): zigzag over Uvarint; overflow
@@ -305,7 +326,7 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         int lo = 0, hi = nfiles - 1;
         while (lo < hi) {
             int mid = (lo + hi + 1) >> 1;
-            if ((int)file_chunk_prefix[mid] <= c) lo = mid; else hi = mid - 1;
+            if ((int)file_chunk_prefix[GIDX(mid, nfiles + 1, 1)] <= c) lo = mid; else hi = mid - 1;
         }
         S.fidx = lo;
         S.bad = ~0ULL;
@@ -314,13 +335,12 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     __syncthreads();
     const int chunk = S.chunk;
     if (chunk >= nchunks) return;                    // uniform
-    const DevFile F = files[S.fidx];
+    const DevFile F = files[GIDX(S.fidx, nfiles, 2)];
     const int cl = chunk - (int)F.first_chunk;       // chunk index within the file
     const int64_t cbase = (int64_t)cl * CLY_CHUNK;   // file offset of the chunk start
     const int64_t n = (int64_t)F.len - cbase;        // bytes from chunk start to file end
     const int end_rel = (int)(n < CLY_CHUNK ? n : CLY_CHUNK);
     const int win_len = (int)(n < CLY_WIN ? n : CLY_WIN);
-    const uint8_t* src = F.base + cbase;
 
     // ---- stage the chunk (+halo) in LDS: 16-B loads, bytewise tail, zero fill
     {
@@ -328,10 +348,10 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         const int nvec = win_len >> 4;
         for (int i = tid; i < CLY_WIN / 16; i += CLY_NT) {
             uint4 v = make_uint4(0, 0, 0, 0);
-            if (i < nvec) v = reinterpret_cast<const uint4*>(src)[i];
+            if (i < nvec) v = reinterpret_cast<const uint4*>(F.base)[GIDX((cbase >> 4) + i, (F.len + 15) >> 4, 3)];
             else if (i == nvec) {
                 uint32_t wv[4] = {0, 0, 0, 0};
-                for (int k = 0; k < (win_len & 15); k++) wv[k >> 2] |= (uint32_t)src[(i << 4) + k] << (8 * (k & 3));
+                for (int k = 0; k < (win_len & 15); k++) wv[k >> 2] |= (uint32_t)F.base[GIDX(cbase + (i << 4) + k, F.len, 4)] << (8 * (k & 3));
                 v = make_uint4(wv[0], wv[1], wv[2], wv[3]);
             }
             w4[i] = v;
@@ -355,7 +375,7 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     const uint8_t* w = reinterpret_cast<const uint8_t*>(S.win);
 
     // ---- forced entry (repair pass) / chunk 0 of a file always enters at 0
-    int64_t fe = forced ? forced[chunk] : FORCE_GUESS;
+    int64_t fe = forced ? forced[GIDX(chunk, nchunks, 5)] : FORCE_GUESS;
     if (cl == 0) fe = 0;
 
     // ---- per-lane speculative walks
@@ -382,19 +402,24 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         }
         const int entry = E;
         int last = -1, base = 0, term = 0, term_st = 0, term_pos = -1;
+        if (E >= 0 && E >= end_rel && (int64_t)E >= n - 5) {
+            // entry at (or within 5 bytes of) the end of the file: exact terminal
+            Hdr h = step_hdr(w, E, n, cbase + E);
+            term = 1; term_st = h.status; term_pos = E;
+        }
         if (E >= 0 && E < end_rel) {
             for (int k = 0; k < CLY_NT; k++) {
                 LaneInfo& L = S.lane[k];
                 const int la = k * CLY_SUB;
-                const int lb = min(la + CLY_SUB, end_rel);
+                const int lend = min(la + CLY_SUB, end_rel);
                 if (la >= end_rel) { L.conf = 0; L.prev = last; L.base = base; L.cnt = 0; continue; }
-                if (term || E >= lb) {      // stripe not on the chain (pass-through or after TERM)
+                if (term || E >= lend) {      // stripe not on the chain (pass-through or after TERM)
                     L.conf = 0; L.prev = term ? -2 : last; L.base = base; L.cnt = 0;
                     continue;
                 }
                 // E lies in this stripe
                 const bool spec_ok = (L.s == E) && (!L.lterm);
-                if (!spec_ok) exact_walk(w, E, lb, n, cbase, L);
+                if (!spec_ok) exact_walk(w, E, lend, n, cbase, L);
                 else { L.term_st = 0; }
                 L.conf = 1; L.prev = last; L.base = base;
                 base += L.cnt;
@@ -409,11 +434,12 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             }
         }
         const bool has_first = entry >= 0 && entry < end_rel;
-        ChunkSum& cs = sums[chunk];
+        ChunkSum& cs = sums[GIDX(chunk, nchunks, 6)];
         cs.entry = entry >= 0 ? cbase + entry : -1;
         cs.term = term;
         cs.term_status = term_st;
         cs.exit = term ? cbase + term_pos : (has_first ? cbase + E : -1);
+        if (term && !has_first) cs.head_len = (uint32_t)end_rel;
         cs.n_records = (uint32_t)base;
         cs.open_pos = (!term && has_first && last >= 0) ? cbase + last : -1;
         cs.chunk_len = (uint32_t)end_rel;
@@ -422,8 +448,8 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         cs.first4 = S.win[0];
         // decoupled look-back: publish this chunk's aggregate now
         unsigned long long v = (unsigned long long)base;
-        if (chunk == 0) __hip_atomic_store(&lb[chunk], v | LB_INC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else __hip_atomic_store(&lb[chunk], v | LB_AGG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (chunk == 0) __hip_atomic_store(&lb[GIDX(chunk, nchunks, 7)], v | LB_INC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else __hip_atomic_store(&lb[GIDX(chunk, nchunks, 7)], v | LB_AGG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
 
@@ -545,7 +571,7 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
 
     // ---- chunk summary: CRC fields
     if (tid == 0) {
-        ChunkSum& cs = sums[chunk];
+        ChunkSum& cs = sums[GIDX(chunk, nchunks, 8)];
         const int last_lane = (end_rel > 0) ? (end_rel - 1) / CLY_SUB : 0;
         const uint32_t end_state = S.sc_v[cur][last_lane];
         const bool has_first = cs.entry >= 0;      // a boundary (record or terminal) lies in the chunk
@@ -571,16 +597,16 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             int k = chunk - 1;
             uint32_t spins = 0;
             while (k >= 0) {
-                unsigned long long v = __hip_atomic_load(&lb[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                unsigned long long v = __hip_atomic_load(&lb[GIDX(k, nchunks, 9)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (v & LB_INC) { prefix += v & LB_MASK; break; }
                 if (v & LB_AGG) { prefix += v & LB_MASK; k--; continue; }
                 __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1u << 26)) { atomicOr(&g->lb_timeout, 1u); break; }
+                if (++spins > (1u << 22)) { atomicOr(&g->lb_timeout, 1u); break; }
             }
-            __hip_atomic_store(&lb[chunk], (unsigned long long)(prefix + cs.n_records) | LB_INC,
+            __hip_atomic_store(&lb[GIDX(chunk, nchunks, 10)], (unsigned long long)(prefix + cs.n_records) | LB_INC,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        out_base[chunk] = prefix;
+        out_base[GIDX(chunk, nchunks, 11)] = prefix;
         S.out_base = prefix;
         if (chunk == nchunks - 1) g->total_records = prefix + cs.n_records;
     }
@@ -609,7 +635,7 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                 int64_t tx = go_varint(w + p + h.hsz, klim, tn);
                 if (tn < 0) { t.tx_id = 0; t.txid_len = 0xFF; }
                 else { t.tx_id = tx; t.txid_len = (uint8_t)tn; }
-                out[idx] = t;
+                out[GIDX(idx, out_cap, 12)] = t;
             } else {
                 atomicOr(&g->overflow, 1u);
             }
@@ -619,8 +645,35 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// k_resolve: one workgroup per file.
-#define RES_NT 256
+// Chain verification + per-file results (two small kernels).
+//
+// k_check  (one thread per chunk): chunk i of a file "claims" an entry when its
+//          speculation started a chain (chunk 0 always claims offset 0).  With
+//          P(i) the nearest claiming chunk before i and X its exit, the claims are
+//          the true chain iff every chunk satisfies  claim ? X == entry : X >= end
+//          (induction from chunk 0).  The thread also derives the chunk's first
+//          end event: an in-chunk CRC failure, a terminal, or a CRC failure of the
+//          record that straddles into later chunks (finished here from the
+//          following chunks' head CRCs).
+// k_finish (one block per file): first failing chunk and first event by
+//          min-reduction; the event counts only if it and every chunk it relies
+//          on lie before the first failure.  Otherwise the host runs a repair
+//          pass with forced entries (k_scan forced mode).
+#define CHK_NT 256
+#define FIN_NT 256
+#define MAX_BACK 4096            // bound on the backward search for P(i)
+#define EVT_NONE 0
+#define EVT_BAD 1                // CRC failure of a record finished inside the chunk
+#define EVT_STRADDLE 2           // CRC failure of the record open at the chunk end
+#define EVT_TERM 3               // terminal position inside the chunk
+#define EVT_UNKNOWN 4            // straddle depends on chunks that failed the check
+
+struct ChunkChk {                // 16 B, written by k_check
+    int32_t ok;                  // 1 = consistent with the chain from chunk 0
+    int32_t evt;                 // EVT_*
+    int32_t dep_end;             // last chunk (local) the event relies on
+    int32_t _pad;
+};
 
 __device__ __forceinline__ uint32_t crc_bytes_bitwise(uint32_t s, uint32_t word, int lo, int hi) {
     for (int k = lo; k < hi; k++) s = cly_crc_byte_bitwise(s, (uint8_t)(word >> (8 * k)));
@@ -628,177 +681,179 @@ __device__ __forceinline__ uint32_t crc_bytes_bitwise(uint32_t s, uint32_t word,
 }
 
 // Advance register s (of a record whose CRC range starts at file offset cs)
-// over the head of chunk sum H at file offset hstart, head length hlen.
-__device__ uint32_t advance_head(uint32_t s, int64_t cs, const ChunkSum& H, int64_t hstart, int64_t hlen) {
-    // bytes [hstart, hstart+min(4,hlen)) from first4; only those >= cs count
-    int64_t l4 = hlen < 4 ? hlen : 4;
-    int lo = (int)(cs > hstart ? (cs - hstart < l4 ? cs - hstart : l4) : 0);
+// over the first hlen bytes of chunk H (which starts at file offset hstart).
+__device__ __forceinline__ uint32_t advance_head(uint32_t s, int64_t cs, const ChunkSum& H, int64_t hstart,
+                                                 int64_t hlen) {
+    const int64_t l4 = hlen < 4 ? hlen : 4;
+    const int lo = (int)(cs > hstart ? (cs - hstart < l4 ? cs - hstart : l4) : 0);
     s = crc_bytes_bitwise(s, H.first4, lo, (int)l4);
-    if (hlen > 4) {
-        // head_raw is raw over [hstart+4, hstart+hlen); if cs is beyond hstart+4
-        // the record started inside this head (cannot happen for a straddling
-        // record: it starts in an earlier chunk, so cs <= hstart + 3).
-        s = cly_multmodp(H.head_shift, s) ^ H.head_raw;
-    }
+    if (hlen > 4) s = cly_multmodp(H.head_shift, s) ^ H.head_raw;   // head_raw spans [hstart+4, hstart+hlen)
     return s;
 }
 
-__global__ void __launch_bounds__(RES_NT)
-k_resolve(const DevFile* __restrict__ files, const ChunkSum* __restrict__ sums,
-          const uint64_t* __restrict__ out_base, int64_t* __restrict__ forced_out,
-          FileOut* __restrict__ fout, Globals* __restrict__ g) {
-    const int f = blockIdx.x;
-    const int tid = threadIdx.x;
-    const DevFile F = files[f];
-    const int c0 = (int)F.first_chunk, nc = (int)F.nchunks;
-    const int64_t nlen = (int64_t)F.len;
+__device__ __forceinline__ bool claims(const ChunkSum& cs, int i) { return i == 0 || cs.entry >= 0; }
 
-    __shared__ int s_fail;            // first chunk (local) failing the speculation check
-    __shared__ unsigned long long s_evt;   // (chunk << 32) | kind: first end event
-    __shared__ int s_carry;
-    __shared__ int s_scan[RES_NT];
-    if (tid == 0) { s_fail = nc; s_evt = ~0ULL; s_carry = -1; }
-    __syncthreads();
-
-    // P(i) = nearest claiming chunk before i (chunk 0 always claims).
-    for (int t0 = 0; t0 < nc; t0 += RES_NT) {
-        const int i = t0 + tid;
-        int claim_idx = -1;
-        if (i < nc) {
-            const ChunkSum& cs = sums[c0 + i];
-            if (i == 0 || cs.entry >= 0) claim_idx = i;
-        }
-        // inclusive max-scan of claim_idx
-        s_scan[tid] = claim_idx;
-        __syncthreads();
-        for (int d = 1; d < RES_NT; d <<= 1) {
-            int v = s_scan[tid];
-            int o = tid >= d ? s_scan[tid - d] : -1;
-            __syncthreads();
-            s_scan[tid] = v > o ? v : o;
-            __syncthreads();
-        }
-        const int carry = s_carry;
-        int incl = s_scan[tid] > carry ? s_scan[tid] : carry;
-        int excl = tid > 0 ? (s_scan[tid - 1] > carry ? s_scan[tid - 1] : carry) : carry;
-        if (i < nc && i > 0) {
-            const ChunkSum& cs = sums[c0 + i];
-            const ChunkSum& ps = sums[c0 + excl];
-            const int64_t start = (int64_t)i * CLY_CHUNK;
-            const int64_t end = start + cs.chunk_len;
-            const int64_t X = ps.term ? INT64_MAX : ps.exit;
-            bool ok;
-            if (cs.entry >= 0) ok = (X == cs.entry);
-            else ok = (X >= end);
-            if (!ok) atomicMin(&s_fail, i);
-        }
-        __syncthreads();
-        if (tid == RES_NT - 1) s_carry = incl;
-        __syncthreads();
+__global__ void __launch_bounds__(CHK_NT)
+k_check(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ file_chunk_prefix,
+        int nchunks, const ChunkSum* __restrict__ sums, ChunkChk* __restrict__ chk, Globals* __restrict__ g) {
+    const int c = blockIdx.x * CHK_NT + threadIdx.x;
+    if (c >= nchunks) return;
+    int lo = 0, hi = nfiles - 1;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if ((int)file_chunk_prefix[GIDX(mid, nfiles + 1, 30)] <= c) lo = mid; else hi = mid - 1;
     }
-    const int fail = s_fail;
-
-    // End events among verified chunks (i < fail, claiming): kind 0 = CRC failure
-    // in chunk, 1 = straddling record CRC failure, 2 = terminal.
-    for (int i = tid; i < fail; i += RES_NT) {
-        const ChunkSum& cs = sums[c0 + i];
-        if (!(i == 0 || cs.entry >= 0)) continue;
-        unsigned long long evt = ~0ULL;
-        if (cs.bad_pos >= 0) evt = ((unsigned long long)i << 32) | 0u;
-        else if (cs.term) evt = ((unsigned long long)i << 32) | 2u;
+    const DevFile F = files[GIDX(lo, nfiles, 31)];
+    const int c0 = (int)F.first_chunk, nc = (int)F.nchunks, i = c - c0;
+    const ChunkSum cs = sums[GIDX(c, nchunks, 32)];
+    ChunkChk r;
+    r.ok = 1; r.evt = EVT_NONE; r.dep_end = i; r._pad = 0;
+    const bool cl = claims(cs, i);
+    if (i > 0) {
+        int p = i - 1, steps = 0;
+        while (p > 0 && sums[GIDX(c0 + p, nchunks, 33)].entry < 0 && steps < MAX_BACK) { p--; steps++; }
+        const ChunkSum ps = sums[GIDX(c0 + p, nchunks, 34)];
+        if (!claims(ps, p)) r.ok = 0;                          // search bound hit: let the host repair
+        else {
+            const int64_t X = ps.term ? INT64_MAX : ps.exit;
+            const int64_t end = (int64_t)i * CLY_CHUNK + cs.chunk_len;
+            r.ok = cl ? (X == cs.entry) : (X >= end);
+        }
+    }
+    if (cl) {
+        if (cs.bad_pos >= 0) r.evt = EVT_BAD;
+        else if (cs.term) r.evt = EVT_TERM;
         else if (cs.open_pos >= 0) {
-            // finish the straddling record: its bytes continue through the heads
-            // of following chunks up to the chain exit X.
+            // the open record's bytes continue through the heads of the following
+            // chunks up to the chain exit X (pass-through chunks carry all bytes)
             const int64_t X = cs.exit;
             uint32_t s = cs.open_state;
             const int64_t ocs = cs.open_pos + 4;
             int j = i + 1;
             bool known = true;
             while (j < nc && (int64_t)j * CLY_CHUNK < X) {
-                if (j >= fail) { known = false; break; }
-                const ChunkSum& h = sums[c0 + j];
+                const ChunkSum h = sums[GIDX(c0 + j, nchunks, 35)];
                 const int64_t hs = (int64_t)j * CLY_CHUNK;
                 const int64_t hl = (X - hs) < (int64_t)h.chunk_len ? (X - hs) : (int64_t)h.chunk_len;
-                // a chunk we pass through must carry the head over that length
-                if (hl != (int64_t)h.head_len) { known = false; break; }
+                if (hl != (int64_t)h.head_len) { known = false; break; }   // j's speculation disagrees
                 s = advance_head(s, ocs, h, hs, hl);
                 j++;
             }
-            if (known && ~s != cs.open_crc) evt = ((unsigned long long)i << 32) | 1u;
-            if (!known) evt = ((unsigned long long)(j < fail ? j : fail) << 32) | 3u;   // unresolved
+            r.dep_end = j - 1;
+            if (!known) { r.evt = EVT_UNKNOWN; r.dep_end = j; }
+            else if (~s != cs.open_crc) r.evt = EVT_STRADDLE;
         }
-        if (evt != ~0ULL) atomicMin(&s_evt, evt);
     }
-    __syncthreads();
+    chk[c] = r;
+}
 
-    if (tid == 0) {
-        const unsigned long long evt = s_evt;
-        FileOut fo;
-        const uint64_t first = out_base[c0];
-        fo.first_index = first;
-        fo.repair = 0;
-        int evt_chunk = evt == ~0ULL ? nc : (int)(evt >> 32);
-        const int kind = (int)(evt & 0xffffffffu);
-        if (evt != ~0ULL && kind != 3) {
-            const ChunkSum& cs = sums[c0 + evt_chunk];
-            const uint64_t ob = out_base[c0 + evt_chunk];
-            if (kind == 0) {
-                fo.status = CLY_ERR_CRC; fo.end_offset = cs.bad_pos; fo.n_records = ob + cs.bad_idx - first;
-            } else if (kind == 1) {
-                fo.status = CLY_ERR_CRC; fo.end_offset = cs.open_pos; fo.n_records = ob + cs.n_records - 1 - first;
-            } else {
-                fo.status = cs.term_status; fo.end_offset = cs.exit; fo.n_records = ob + cs.n_records - first;
-            }
-        } else if (fail < nc || kind == 3) {
-            // speculation failed before any end event: either the chain exits into
-            // [n-5, n) (terminal computable here) or a repair pass is needed.
-            int i = fail < evt_chunk ? fail : evt_chunk;
-            // entry into chunk i per the chain so far
-            int p = i - 1;
-            while (p > 0 && sums[c0 + p].entry < 0) p--;
-            const ChunkSum& ps = sums[c0 + p];
-            const int64_t E = ps.exit;
-            if (!ps.term && E >= nlen - 5 && E < nlen) {
-                fo.status = (nlen - E == 5) ? CLY_ERR_TRUNC5 : CLY_END_EOF;
-                fo.end_offset = E;
-                fo.n_records = out_base[c0 + p] + ps.n_records - first;
-            } else {
-                fo.repair = 1;
-                fo.status = 0; fo.end_offset = 0; fo.n_records = 0;
-                atomicOr(&g->repair, 1u);
-            }
+__global__ void __launch_bounds__(FIN_NT)
+k_finish(const DevFile* __restrict__ files, int nchunks, const ChunkSum* __restrict__ sums,
+         const ChunkChk* __restrict__ chk, const uint64_t* __restrict__ out_base,
+         int64_t* __restrict__ forced_out, FileOut* __restrict__ fout, Globals* __restrict__ g) {
+    const int f = blockIdx.x;
+    const int tid = threadIdx.x;
+    const DevFile F = files[f];
+    const int c0 = (int)F.first_chunk, nc = (int)F.nchunks;
+    const int64_t nlen = (int64_t)F.len;
+    __shared__ int red[FIN_NT];
+
+    // first chunk failing the chain check
+    int m = nc;
+    for (int i = tid; i < nc; i += FIN_NT)
+        if (!chk[GIDX(c0 + i, nchunks, 40)].ok) { m = i; break; }
+    red[tid] = m;
+    __syncthreads();
+    for (int d = FIN_NT / 2; d > 0; d >>= 1) {
+        if (tid < d && red[tid + d] < red[tid]) red[tid] = red[tid + d];
+        __syncthreads();
+    }
+    const int fail = red[0];
+    __syncthreads();
+    // first event among chunks before the failure
+    m = nc;
+    for (int i = tid; i < fail; i += FIN_NT)
+        if (chk[GIDX(c0 + i, nchunks, 41)].evt != EVT_NONE) { m = i; break; }
+    red[tid] = m;
+    __syncthreads();
+    for (int d = FIN_NT / 2; d > 0; d >>= 1) {
+        if (tid < d && red[tid + d] < red[tid]) red[tid] = red[tid + d];
+        __syncthreads();
+    }
+    const int ev = red[0];
+    if (tid != 0) return;
+    TRACE(0, 1); TRACE(1, fail); TRACE(2, ev);
+
+    FileOut fo;
+    const uint64_t first = out_base[GIDX(c0, nchunks, 42)];
+    fo.first_index = first;
+    fo.repair = 0;
+    bool need_repair = false;
+    if (ev < nc) {
+        const ChunkChk e = chk[GIDX(c0 + ev, nchunks, 43)];
+        const ChunkSum cs = sums[GIDX(c0 + ev, nchunks, 44)];
+        const uint64_t ob = out_base[GIDX(c0 + ev, nchunks, 45)];
+        if (e.evt == EVT_UNKNOWN || e.dep_end >= fail) need_repair = true;
+        else if (e.evt == EVT_BAD) {
+            fo.status = CLY_ERR_CRC; fo.end_offset = cs.bad_pos; fo.n_records = ob + cs.bad_idx - first;
+        } else if (e.evt == EVT_STRADDLE) {
+            fo.status = CLY_ERR_CRC; fo.end_offset = cs.open_pos; fo.n_records = ob + cs.n_records - 1 - first;
         } else {
-            // no event and no failure: the chain leaves the last claiming chunk at n
-            int p = nc - 1;
-            while (p > 0 && sums[c0 + p].entry < 0) p--;
-            const ChunkSum& ps = sums[c0 + p];
-            fo.status = CLY_END_EOF;
-            fo.end_offset = ps.exit;
-            fo.n_records = out_base[c0 + p] + ps.n_records - first;
+            fo.status = cs.term_status; fo.end_offset = cs.exit; fo.n_records = ob + cs.n_records - first;
         }
-        fout[f] = fo;
-        if (fo.repair) {
-            // forced entries for the repair pass: sequential over the file's chunks
-            // using verified exits; re-speculate after the first unknown.
-            int64_t E = 0;
-            bool known = true;
-            for (int i = 0; i < nc; i++) {
-                const ChunkSum& cs = sums[c0 + i];
-                const int64_t start = (int64_t)i * CLY_CHUNK, end = start + cs.chunk_len;
-                int64_t fv;
-                if (!known) fv = FORCE_GUESS;
-                else if (E >= end || E < 0) fv = FORCE_SKIP;
-                else {
-                    fv = E;
-                    if (cs.entry == E) E = cs.term ? -1 : cs.exit;
-                    else known = false;
-                }
-                forced_out[c0 + i] = fv;
-            }
+    } else if (fail < nc) {
+        need_repair = true;
+    } else {
+        // every chunk verified and no event: the chain leaves the last claiming chunk at n
+        int p = nc - 1;
+        while (p > 0 && sums[GIDX(c0 + p, nchunks, 46)].entry < 0) p--;
+        const ChunkSum ps = sums[GIDX(c0 + p, nchunks, 47)];
+        fo.status = CLY_END_EOF;
+        fo.end_offset = ps.exit;
+        fo.n_records = out_base[GIDX(c0 + p, nchunks, 48)] + ps.n_records - first;
+    }
+    if (need_repair) {
+        // The chain entered the first failing chunk at the exit of its predecessor.
+        // An entry within 5 bytes of the end of the file is a terminal (no data
+        // needed); otherwise the host re-runs k_scan with forced entries.
+        const int i = fail < ev ? fail : ev;
+        int p = i - 1;
+        while (p > 0 && sums[GIDX(c0 + p, nchunks, 49)].entry < 0) p--;
+        const ChunkSum ps = sums[GIDX(c0 + (p < 0 ? 0 : p), nchunks, 50)];
+        const int64_t E = ps.exit;
+        if (p >= 0 && !ps.term && E >= nlen - 5 && E < nlen && ps.bad_pos < 0) {
+            fo.status = (nlen - E == 5) ? CLY_ERR_TRUNC5 : CLY_END_EOF;
+            fo.end_offset = E;
+            fo.n_records = out_base[GIDX(c0 + p, nchunks, 51)] + ps.n_records - first;
+            need_repair = false;
         } else {
-            for (int i = 0; i < nc; i++) forced_out[c0 + i] = FORCE_GUESS;
+            fo.repair = 1; fo.status = 0; fo.end_offset = 0; fo.n_records = 0;
+            atomicOr(&g->repair, 1u);
         }
     }
+    TRACE(0, 2);
+    fout[f] = fo;
+    if (fo.repair) {
+        // forced entries: exact where the chain is known, re-speculate after it
+        int64_t E = 0;
+        bool known = true;
+        for (int i = 0; i < nc; i++) {
+            const ChunkSum cs = sums[GIDX(c0 + i, nchunks, 52)];
+            const int64_t start = (int64_t)i * CLY_CHUNK, end = start + cs.chunk_len;
+            int64_t fv;
+            if (!known) fv = FORCE_GUESS;
+            else if (E < 0 || E >= end) fv = (i == 0) ? 0 : FORCE_SKIP;
+            else {
+                fv = E;
+                if (cs.entry == E) E = cs.term ? -1 : cs.exit;
+                else known = false;
+            }
+            forced_out[GIDX(c0 + i, nchunks, 53)] = fv;
+        }
+    } else {
+        for (int i = 0; i < nc; i++) forced_out[GIDX(c0 + i, nchunks, 54)] = FORCE_GUESS;
+    }
+    TRACE(0, 3);
 }
 
 // ---------------------------------------------------------------------------
@@ -817,6 +872,7 @@ struct cly_ctx {
     unsigned long long* d_lb;
     uint64_t* d_outbase;
     int64_t* d_forced;
+    ChunkChk* d_chk;
     FileOut* d_fout;
     Globals* d_g;
     uint32_t* d_shift;
@@ -825,6 +881,7 @@ struct cly_ctx {
     uint32_t* h_prefix;
     FileOut* h_fout;
     Globals* h_g;
+    int* h_trace;               // CLY_DEBUG: host-mapped trace buffer
     // host-path staging
     uint8_t* d_bytes; uint64_t cap_bytes;
     cly_tuple* d_tuples; uint64_t cap_tuples;
@@ -858,6 +915,12 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     build_shift_tables(hs);
     HIPCK(hipMemcpy(c->d_shift, hs, shift_bytes, hipMemcpyHostToDevice));
     free(hs);
+#ifdef CLY_DEBUG
+    HIPCK(hipHostMalloc(&c->h_trace, 64 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+    memset(c->h_trace, 0, 64 * sizeof(int));
+    { int* dptr = nullptr; HIPCK(hipHostGetDevicePointer((void**)&dptr, c->h_trace, 0));
+      HIPCK(hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &dptr, sizeof(dptr))); }
+#endif
     HIPCK(hipFuncSetAttribute((const void*)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)sizeof(ScanShared)));
     *out = c;
@@ -869,7 +932,7 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     hipFree(c->d_files); hipFree(c->d_prefix); hipFree(c->d_sums); hipFree(c->d_lb);
-    hipFree(c->d_outbase); hipFree(c->d_forced); hipFree(c->d_fout); hipFree(c->d_g);
+    hipFree(c->d_outbase); hipFree(c->d_forced); hipFree(c->d_chk); hipFree(c->d_fout); hipFree(c->d_g);
     hipFree(c->d_shift); hipFree(c->d_bytes); hipFree(c->d_tuples);
     hipHostFree(c->h_files); hipHostFree(c->h_prefix); hipHostFree(c->h_fout); hipHostFree(c->h_g);
     for (int i = 0; i < 4; i++) hipEventDestroy(c->ev[i]);
@@ -900,8 +963,9 @@ static int ensure_files(cly_ctx* c, int nfiles) {
 
 static int ensure_chunks(cly_ctx* c, int nchunks) {
     if (nchunks <= c->cap_chunks) return CLY_OK;
-    hipFree(c->d_sums); hipFree(c->d_lb); hipFree(c->d_outbase); hipFree(c->d_forced);
+    hipFree(c->d_sums); hipFree(c->d_lb); hipFree(c->d_outbase); hipFree(c->d_forced); hipFree(c->d_chk);
     int cap = nchunks < 1024 ? 1024 : nchunks;
+    HIPCK(hipMalloc(&c->d_chk, sizeof(ChunkChk) * cap));
     HIPCK(hipMalloc(&c->d_sums, sizeof(ChunkSum) * cap));
     HIPCK(hipMalloc(&c->d_lb, sizeof(unsigned long long) * cap));
     HIPCK(hipMalloc(&c->d_outbase, sizeof(uint64_t) * cap));
@@ -943,6 +1007,14 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles,
     HIPCK(hipMemcpyAsync(c->d_files, c->h_files, sizeof(DevFile) * nfiles, hipMemcpyHostToDevice, st));
     HIPCK(hipMemcpyAsync(c->d_prefix, c->h_prefix, sizeof(uint32_t) * (nfiles + 1), hipMemcpyHostToDevice, st));
 
+#ifdef CLY_DEBUG
+    fprintf(stderr, "clyscan[debug] nfiles=%d nchunks=%d d_out=%p out_cap=%llu shared=%zu\n", nfiles, nchunks,
+            (void*)d_out, (unsigned long long)out_cap, sizeof(ScanShared));
+    for (int i = 0; i < nfiles && i < 8; i++)
+        fprintf(stderr, "clyscan[debug]   file %d base=%p len=%llu first_chunk=%u nchunks=%u\n", i,
+                (const void*)c->h_files[i].base, (unsigned long long)c->h_files[i].len, c->h_files[i].first_chunk,
+                c->h_files[i].nchunks);
+#endif
     double scan_ms = 0, res_ms = 0;
     uint32_t pass = 0;
     HIPCK(hipEventRecord(c->ev[0], st));
@@ -954,10 +1026,32 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles,
                            c->d_files, nfiles, c->d_prefix, nchunks, pass ? c->d_forced : nullptr,
                            c->d_shift, c->d_sums, c->d_lb, c->d_outbase, d_out, out_cap, c->d_g);
         HIPCK(hipGetLastError());
+#ifdef CLY_DEBUG
+        { hipError_t e = hipStreamSynchronize(st);
+          fprintf(stderr, "clyscan[debug] k_scan pass %u: %s\n", pass, hipGetErrorString(e));
+          if (e != hipSuccess) return CLY_ERR_DEVICE;
+          Globals hg; (void)hipMemcpy(&hg, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost);
+          if (hg.dbg_site) fprintf(stderr, "clyscan[debug] k_scan OOB site %u idx %lld lim %lld\n", hg.dbg_site,
+                                   (long long)hg.dbg_idx, (long long)hg.dbg_lim); }
+#endif
         HIPCK(hipEventRecord(c->ev[2], st));
-        hipLaunchKernelGGL(k_resolve, dim3(nfiles), dim3(RES_NT), 0, st,
-                           c->d_files, c->d_sums, c->d_outbase, c->d_forced, c->d_fout, c->d_g);
+        hipLaunchKernelGGL(k_check, dim3((nchunks + CHK_NT - 1) / CHK_NT), dim3(CHK_NT), 0, st,
+                           c->d_files, nfiles, c->d_prefix, nchunks, c->d_sums, c->d_chk, c->d_g);
         HIPCK(hipGetLastError());
+        hipLaunchKernelGGL(k_finish, dim3(nfiles), dim3(FIN_NT), 0, st,
+                           c->d_files, nchunks, c->d_sums, c->d_chk, c->d_outbase, c->d_forced, c->d_fout, c->d_g);
+        HIPCK(hipGetLastError());
+#ifdef CLY_DEBUG
+        { hipError_t e = hipStreamSynchronize(st);
+          fprintf(stderr, "clyscan[debug] k_check+k_finish pass %u: %s\n", pass, hipGetErrorString(e));
+          fprintf(stderr, "clyscan[debug] trace:");
+          for (int t = 0; t < 8; t++) fprintf(stderr, " %d", c->h_trace[t]);
+          fprintf(stderr, "\n");
+          if (e != hipSuccess) return CLY_ERR_DEVICE;
+          Globals hg; (void)hipMemcpy(&hg, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost);
+          if (hg.dbg_site) fprintf(stderr, "clyscan[debug] OOB site %u idx %lld lim %lld\n", hg.dbg_site,
+                                   (long long)hg.dbg_idx, (long long)hg.dbg_lim); }
+#endif
         HIPCK(hipEventRecord(c->ev[3], st));
         HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
         HIPCK(hipMemcpyAsync(c->h_fout, c->d_fout, sizeof(FileOut) * nfiles, hipMemcpyDeviceToHost, st));
