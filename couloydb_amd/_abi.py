@@ -63,7 +63,9 @@ _libs = {}
 
 
 def lib_path(name="libclyscan.so"):
-    return os.path.join(PKG_DIR, name)
+    """In-package library by name; an absolute path is taken as is (tests load
+    the CPU emulator tests/emu/libclyscan_emu*.so this way)."""
+    return name if os.path.isabs(name) else os.path.join(PKG_DIR, name)
 
 
 def load_scan_lib(name="libclyscan.so"):

@@ -19,15 +19,12 @@
 
 #define CLY_POLY 0xEDB88320u
 
-// a * b mod P, reflected representation.
+// a * b mod P, reflected representation (bit 31 = x^0).  Bounded loop: no
+// forward-progress assumptions for the optimizer to exploit when a == 0.
 CLY_HD uint32_t cly_multmodp(uint32_t a, uint32_t b) {
-    uint32_t m = 1u << 31, p = 0;
-    for (;;) {
-        if (a & m) {
-            p ^= b;
-            if ((a & (m - 1)) == 0) break;
-        }
-        m >>= 1;
+    uint32_t p = 0;
+    for (int k = 31; k >= 0; k--) {
+        if (a & (1u << k)) p ^= b;
         b = (b & 1) ? (b >> 1) ^ CLY_POLY : b >> 1;
     }
     return p;
