@@ -172,6 +172,55 @@ struct DevEnv {
         return true;
     }
     __device__ __forceinline__ bool spin_ok() const { return spins <= LB_SPIN_MAX; }
+    // look-back phase 1 by wave 0: 64 descriptors per round trip, back to the
+    // nearest FULL (scan_core.h lookback_compose does phase 2)
+    __device__ void lb_collect(ScanShared& S, int t) {
+        if (t >= 64) return;
+        const int64_t c = S.C.chunk;
+        int n = 0;
+        int64_t base = c - 1;
+        for (int win = 0;; win++) {
+            if (base < 0) { if (t == 0) { S.lb_jfull = -1; S.lb_n = n; } return; }
+            if (n >= CLY_LBWIN) { if (t == 0) { S.lb_jfull = -2; S.lb_n = n; } return; }
+            const int64_t j = base - t;
+            for (;;) {
+                uint64_t w0 = 0, x = 0, p = 0;
+                uint64_t st = DS_FULL;                 // j < 0: the virtual start
+                bool ready = true;
+                if (j >= 0) {
+                    w0 = ld(j, 0);
+                    st = ds_state(w0, epoch);
+                    if (st == DS_SPEC) { x = ld(j, 1); ready = ds_ok(x, epoch); }
+                    else if (st == DS_FULL) { x = ld(j, 2); p = ld(j, 3); ready = ds_ok(x, epoch) && ds_ok(p, epoch); }
+                    else ready = false;
+                }
+                const unsigned long long fullm = __ballot(ready && st == DS_FULL);
+                const unsigned long long nrm = __ballot(!ready);
+                const int ff = fullm ? __ffsll((long long)fullm) - 1 : 64;
+                const unsigned long long need = ff >= 63 ? ~0ull : ((2ull << ff) - 1);
+                if (nrm & need) {
+                    bool go = true;
+                    if (t == 0) go = spin();
+                    go = __shfl(go ? 1 : 0, 0, 64) != 0;
+                    if (!go) { if (t == 0) { S.lb_jfull = -1; S.lb_n = n; } return; }
+                    continue;
+                }
+                const int take = ff < 64 ? ff : 64;       // SPEC descriptors in this window
+                if (t < take && n + t < CLY_LBWIN) { S.lb_w0[n + t] = w0; S.lb_x[n + t] = x; }
+                if (ff < 64) {
+                    if (t == ff) {
+                        S.lb_jfull = j >= 0 ? j : -1;
+                        S.lb_fw0 = w0; S.lb_fx = x; S.lb_fp = p;
+                        S.lb_n = n + take;
+                    }
+                    return;
+                }
+                n += 64;
+                base -= 64;
+                break;
+            }
+        }
+    }
     template <class EX> __device__ __forceinline__ void crc(EX& ex, ScanShared& S) { crc_phase(ex, S, shift); }
     __device__ __forceinline__ void emit_lane(ScanShared& S, int t) {
         unsigned of = 0;
@@ -554,8 +603,8 @@ extern "C" const char* cly_strerror(int code) {
 }
 
 extern "C" const char* cly_build_info(void) {
-#define CLY_STR2(x) #x
-#define CLY_STR(x) CLY_STR2(x)
-    return "clyscan gfx950 NT=" CLY_STR(CLY_NT) " SUB=" CLY_STR(CLY_SUB) " CHUNK=" CLY_STR(CLY_CHUNK)
-           " REP=" CLY_STR(CLY_REP) " lookback=inline";
+    static char buf[160];
+    snprintf(buf, sizeof(buf), "clyscan gfx950 NT=%d SUB=%d CHUNK=%d REP=%d LBWIN=%d", CLY_NT, CLY_SUB, CLY_CHUNK,
+             CLY_REP, CLY_LBWIN);
+    return buf;
 }

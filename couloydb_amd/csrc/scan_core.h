@@ -48,7 +48,8 @@
 #define CLY_NT 256            // lanes per chunk (threads per workgroup)
 #endif
 #ifndef CLY_SUB
-#define CLY_SUB 128           // bytes per lane stripe
+#define CLY_SUB 124           // bytes per lane stripe: 31 dwords (odd), so lane k's
+                              // stripe starts at LDS bank 31k mod 32 (no conflicts)
 #endif
 #ifndef CLY_REP
 #define CLY_REP 2             // LDS replication of the CRC tables (bank spread)
@@ -57,9 +58,11 @@
 #define CLY_HALO 64           // >= 26 (max header) + 11 (txId varint) past the chunk end
 #define CLY_WIN (CLY_CHUNK + CLY_HALO)
 #define CLY_NWAVE (CLY_NT / 64)
+#define CLY_LBWIN 256         // look-back window (descriptors prefetched into LDS)
 static_assert(CLY_NT % 64 == 0 && CLY_NT <= 1024, "CLY_NT must be a multiple of 64");
-static_assert(CLY_SUB % 16 == 0 && CLY_SUB >= 32, "CLY_SUB must be a multiple of 16");
-static_assert(CLY_CHUNK <= 32768, "chunk-relative positions are int16");
+static_assert(CLY_SUB % 4 == 0 && CLY_SUB >= 28, "CLY_SUB must be a multiple of 4");
+static_assert(CLY_CHUNK % 16 == 0 && CLY_WIN % 16 == 0, "16-B staging");
+static_assert(CLY_CHUNK <= 32767, "chunk-relative positions are int16");
 
 #define REC_OK 100
 
@@ -235,6 +238,9 @@ struct ScanShared {
     uint8_t  sc_c0[CLY_NT];                   // phase-A constness (kept through the scan)
     // block reduction scratch
     int32_t  red[CLY_NWAVE * 2];
+    // look-back window: descriptors of chunks c-1, c-2, ... (SPEC words)
+    uint64_t lb_w0[CLY_LBWIN];
+    uint64_t lb_x[CLY_LBWIN];
     // scalars
     ChunkCtx C;
     ChainRes R;
@@ -248,6 +254,9 @@ struct ScanShared {
     int64_t  entry_g;                         // look-back: global entry position
     uint64_t p_excl;                          // records before the chunk (global slot)
     int32_t  in_dead;                         // look-back: chain ended before this chunk
+    int32_t  lb_n;                            // SPEC descriptors collected in lb_w0/lb_x
+    int64_t  lb_jfull;                        // nearest FULL chunk (-1: none before; -2: window exhausted)
+    uint64_t lb_fw0, lb_fx, lb_fp;            // its words
     int32_t  fail;                            // internal invariant violated (reported as a device error)
     int32_t  fail_k;
 };
@@ -336,40 +345,67 @@ CLY_DEV bool lb_compose_spec(LbState& s, int64_t j, uint64_t w0, uint64_t x) {
     return false;
 }
 
-// Single-lane decoupled look-back over descriptors of chunks < c.  Env
-// supplies ld(j, k) (word k of chunk j, agent-scope), pause() and a spin
-// bound (spin() returns false once exceeded).
+// Decoupled look-back, phase 1 (Env::lb_collect): the descriptors of chunks
+// c-1, c-2, ... back to the nearest one with FULL words are read (by a whole
+// wave on the GPU, 64 per round trip) into S.lb_w0/S.lb_x, S.lb_jfull and
+// S.lb_fw0/fx/fp.  Phase 2 (this function, one lane): compose forward from
+// that FULL through the speculative descriptors; a chunk whose guess does not
+// match the chain is waited for (its FULL words).  Env supplies ld(j, k)
+// (word k of chunk j, agent scope) and spin() (false once the bound is hit).
 template <class Env>
-CLY_DEV void lookback_seq(Env& env, int64_t c, int fof, uint32_t epoch, LbState& s) {
+CLY_DEV void lookback_compose(Env& env, ScanShared& S, uint32_t epoch, LbState& s) {
+    const int64_t c = S.C.chunk;
     s.E = 0; s.P = 0; s.dead = 0; s._pad = 0;
-    // nearest predecessor with FULL words
-    int64_t j = c - 1;
-    uint64_t w0 = 0;
-    while (j >= 0) {
-        w0 = env.ld(j, 0);
-        while (ds_state(w0, epoch) == 0) { if (!env.spin()) return; w0 = env.ld(j, 0); }
-        if (ds_state(w0, epoch) == DS_FULL) break;
-        j--;
+    int64_t j = S.lb_jfull;
+    if (j == -2) {
+        // window exhausted without a FULL: wait for the predecessor's FULL words
+        j = c - 1;
+        uint64_t w0 = env.ld(j, 0), x = env.ld(j, 2), p = env.ld(j, 3);
+        while (ds_state(w0, epoch) != DS_FULL || !ds_ok(x, epoch) || !ds_ok(p, epoch)) {
+            if (!env.spin()) return;
+            w0 = env.ld(j, 0); x = env.ld(j, 2); p = env.ld(j, 3);
+        }
+        s.dead = ds_term(w0); s.E = (int64_t)(x & DS_VAL_MASK); s.P = p & DS_VAL_MASK;
+    } else if (j >= 0) {
+        s.dead = ds_term(S.lb_fw0); s.E = (int64_t)(S.lb_fx & DS_VAL_MASK); s.P = S.lb_fp & DS_VAL_MASK;
     }
-    if (j >= 0) {
-        uint64_t x = env.ld(j, 2), p = env.ld(j, 3);
-        while (!ds_ok(x, epoch) || !ds_ok(p, epoch)) { if (!env.spin()) return; x = env.ld(j, 2); p = env.ld(j, 3); }
+    for (int64_t k = j + 1; k < c; k++) {
+        const int i = (int)(c - 1 - k);
+        if (lb_compose_spec(s, k, S.lb_w0[i], S.lb_x[i] & DS_VAL_MASK)) continue;
+        uint64_t w0 = env.ld(k, 0), x = env.ld(k, 2), p = env.ld(k, 3);
+        while (ds_state(w0, epoch) != DS_FULL || !ds_ok(x, epoch) || !ds_ok(p, epoch)) {
+            if (!env.spin()) return;
+            w0 = env.ld(k, 0); x = env.ld(k, 2); p = env.ld(k, 3);
+        }
         s.dead = ds_term(w0); s.E = (int64_t)(x & DS_VAL_MASK); s.P = p & DS_VAL_MASK;
     }
-    // compose forward through the speculative descriptors
-    for (int64_t k = j + 1; k < c; k++) {
-        uint64_t a0 = env.ld(k, 0);
-        if (ds_state(a0, epoch) == DS_SPEC) {
-            uint64_t x = env.ld(k, 1);
-            while (!ds_ok(x, epoch)) { if (!env.spin()) return; x = env.ld(k, 1); }
-            if (lb_compose_spec(s, k, a0, x & DS_VAL_MASK)) continue;
+    if (S.C.fof) { s.E = c * (int64_t)CLY_CHUNK; s.dead = 0; }
+}
+
+// Phase 1, sequential form (CPU emulator; same result as the wave form).
+template <class Env>
+CLY_DEV void lookback_collect_seq(Env& env, ScanShared& S, uint32_t epoch) {
+    const int64_t c = S.C.chunk;
+    int n = 0;
+    for (int64_t j = c - 1;; j--) {
+        if (j < 0) { S.lb_jfull = -1; break; }
+        if (n == CLY_LBWIN) { S.lb_jfull = -2; break; }
+        uint64_t w0 = env.ld(j, 0);
+        for (;;) {
+            const uint64_t st = ds_state(w0, epoch);
+            if (st == DS_SPEC) {
+                const uint64_t x = env.ld(j, 1);
+                if (ds_ok(x, epoch)) { S.lb_w0[n] = w0; S.lb_x[n] = x; n++; break; }
+            } else if (st == DS_FULL) {
+                const uint64_t x = env.ld(j, 2), p = env.ld(j, 3);
+                if (ds_ok(x, epoch) && ds_ok(p, epoch)) { S.lb_fw0 = w0; S.lb_fx = x; S.lb_fp = p; break; }
+            }
+            if (!env.spin()) { S.lb_jfull = -1; S.lb_n = n; return; }
+            w0 = env.ld(j, 0);
         }
-        while (ds_state(a0, epoch) != DS_FULL) { if (!env.spin()) return; a0 = env.ld(k, 0); }
-        uint64_t x = env.ld(k, 2), p = env.ld(k, 3);
-        while (!ds_ok(x, epoch) || !ds_ok(p, epoch)) { if (!env.spin()) return; x = env.ld(k, 2); p = env.ld(k, 3); }
-        s.dead = ds_term(a0); s.E = (int64_t)(x & DS_VAL_MASK); s.P = p & DS_VAL_MASK;
+        if (ds_state(w0, epoch) == DS_FULL) { S.lb_jfull = j; break; }
     }
-    if (fof) { s.E = c * (int64_t)CLY_CHUNK; s.dead = 0; }
+    S.lb_n = n;
 }
 
 // ---------------------------------------------------------------------------
@@ -378,6 +414,50 @@ CLY_DEV void lookback_seq(Env& env, int64_t c, int fof, uint32_t epoch, LbState&
 // Speculative walk of lane t: first candidate q in the stripe whose chain of
 // plain records leaves the stripe at an exit that decodes as a plain record
 // (checked when its header lies in the window) or is the end of the file.
+// SWAR byte masks (bit 7 of each byte): byte <= 4 (type/dtype), and byte
+// nonzero and even (first byte of the key-size varint of a record with ks >= 1).
+CLY_DEV uint32_t swar_le4(uint32_t W) { return ~(((W | 0x80808080u) - 0x05050505u) | W) & 0x80808080u; }
+CLY_DEV uint32_t swar_ks(uint32_t W) {
+    const uint32_t nz = ((W & 0x7f7f7f7fu) + 0x7f7f7f7fu) | W;
+    return nz & ~(W << 7) & 0x80808080u;
+}
+CLY_DEV uint32_t funnel(uint32_t hi, uint32_t lo, int sh) {
+#ifdef __HIPCC__
+    return __builtin_amdgcn_alignbit(hi, lo, sh);
+#else
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh);
+#endif
+}
+CLY_DEV int ctz32(uint32_t v) {
+#ifdef __HIPCC__
+    return __builtin_ctz(v);
+#else
+    return __builtin_ctz(v);
+#endif
+}
+
+// First q in [q0, b) whose bytes q+4, q+5 are <= 4 and q+6 is nonzero and even
+// (word-parallel filter over the LDS window); b if none.
+CLY_DEV int next_candidate(const uint32_t* w32, int q0, int b) {
+    int i = (q0 + 4) >> 2;                 // word holding byte q0+4
+    uint32_t Li = swar_le4(w32[i]), Ki = swar_ks(w32[i]);
+    for (;;) {
+        const int qbase = 4 * i - 4;       // candidates of word i: q in [qbase, qbase+4)
+        if (qbase >= b) return b;
+        const uint32_t Wn = w32[i + 1];
+        const uint32_t Ln = swar_le4(Wn), Kn = swar_ks(Wn);
+        uint32_t c = Li & funnel(Ln, Li, 8) & funnel(Kn, Ki, 16);
+        if (qbase < q0) c &= ~0u << (8 * (q0 - qbase));
+        if (c) {
+            const int q = qbase + (ctz32(c) >> 3);
+            return q < b ? q : b;
+        }
+        i++;
+        Li = Ln;
+        Ki = Kn;
+    }
+}
+
 CLY_NOINL void spec_lane(ScanShared& S, int t) {
     const ChunkCtx& C = S.C;
     const uint8_t* w = reinterpret_cast<const uint8_t*>(S.win);
@@ -385,9 +465,7 @@ CLY_NOINL void spec_lane(ScanShared& S, int t) {
     const int a = t * CLY_SUB;
     if (a >= C.dlen) return;
     const int b = a + CLY_SUB < C.dlen ? a + CLY_SUB : C.dlen;
-    for (int q = a; q < b; q++) {
-        const uint32_t k0 = w[q + 6];
-        if (w[q + 4] > 4 || w[q + 5] > 4 || k0 == 0 || (k0 & 1)) continue;
+    for (int q = next_candidate(S.win, a, b); q < b; q = next_candidate(S.win, q + 1, b)) {
         Hdr h = step_hdr(w, q, C.nrel, C.cbase + q);
         if (!h.good) continue;
         int64_t p = q;
@@ -831,27 +909,27 @@ CLY_DEV void chunk_body(EX& ex, ScanShared& S, Env& env) {
     ex.all([&](int t) { env.stage_lane(S, t); build_tab_lane(S.tab, t); });
     // ---- speculation
     ex.all([&](int t) { spec_lane(S, t); });
-    // ---- guess the entry and resolve the chain from it
-    ex.one([&]() {
-        int g = -1;
-        if (S.C.fof) g = 0;
-        else {
-            for (int k = 0; k < CLY_NT; k++)
-                if (S.sp_s[k] >= 0 && S.sp_vin[k]) { g = S.sp_s[k]; break; }
-            if (g < 0)
-                for (int k = 0; k < CLY_NT; k++)
-                    if (S.sp_s[k] >= 0) { g = S.sp_s[k]; break; }
-        }
-        S.guess = g;
-        S.mode = g >= 0 ? MODE_NORMAL : MODE_PASS;
-    });
-    ex.one([&]() { env.mark(S, 2); });
+    // ---- guess the entry: the first lane whose walk left through a checked
+    //      exit, else the first lane with any walk (first chunk of a file: 0)
+    {
+        const int key = ex.reduce_min([&](int t) -> int {
+            if (S.sp_s[t] < 0) return 2 * CLY_NT;
+            return S.sp_vin[t] ? t : CLY_NT + t;
+        });
+        ex.one([&]() {
+            int g = -1;
+            if (S.C.fof) g = 0;
+            else if (key < 2 * CLY_NT) g = S.sp_s[key % CLY_NT];
+            S.guess = g;
+            S.mode = g >= 0 ? MODE_NORMAL : MODE_PASS;
+            env.mark(S, 2);
+        });
+    }
     if (S.guess >= 0) resolve(ex, S, S.guess);
-    ex.one([&]() { env.mark(S, 3); });
     ex.all([&](int t) { env.dbg_lane(S, t); });
     // ---- publish the speculative descriptor
+    const int64_t cg = (int64_t)S.C.chunk * CLY_CHUNK;
     ex.one([&]() {
-        const int64_t cg = (int64_t)S.C.chunk * CLY_CHUNK;
         const ChainRes& R = S.R;
         const uint32_t ep = env.epoch;
         if (S.guess >= 0)
@@ -859,46 +937,32 @@ CLY_DEV void chunk_body(EX& ex, ScanShared& S, Env& env) {
                              ds_tag(ep, (uint64_t)(cg + R.xrel)));
         else
             env.publish_spec(S.C.chunk, ds_pack(ep, DS_SPEC, S.C.fof, 0, 0, 0, 0), ds_tag(ep, 0));
+        env.mark(S, 3);
     });
-    // ---- CRC for the guessed chain (hides the look-back latency)
-    env.crc(ex, S);
     // ---- look-back: true entry and output slot
+    ex.all([&](int t) { env.lb_collect(S, t); });
     ex.one([&]() {
         env.mark(S, 4);
         LbState ls;
-        lookback_seq(env, S.C.chunk, S.C.fof, env.epoch, ls);
+        lookback_compose(env, S, env.epoch, ls);
         if (!env.spin_ok()) { S.fail = 4; ls.dead = 1; }
         S.entry_g = ls.E;
         S.p_excl = ls.P;
         S.in_dead = ls.dead;
+        if (!S.in_dead && S.entry_g < cg) { S.fail = 2; S.in_dead = 1; }   // cannot happen
         env.mark(S, 5);
     });
-    // ---- decide the mode; redo the chain / CRC when the guess was wrong
-    const int64_t cg = (int64_t)S.C.chunk * CLY_CHUNK;
-    int redo = 0, newE = -1;
-    if (!S.in_dead && S.entry_g < cg) {
-        // a chain position before the chunk start cannot enter it: internal error
-        ex.one([&]() { S.fail = 2; S.in_dead = 1; });
-    }
-    {
-        if (S.in_dead) {
-            if (S.mode != MODE_DEAD) { redo = 1; }
-        } else if (S.entry_g >= cg + CLY_CHUNK) {
-            if (S.mode != MODE_PASS) redo = 2;
-        } else {
-            newE = (int)(S.entry_g - cg);
-            if (S.mode != MODE_NORMAL || S.guess != newE) redo = 3;
-        }
-    }
-    if (redo == 1) {
+    // ---- the true chain (re-resolved when the guess was wrong)
+    if (S.in_dead) {
         ex.one([&]() { S.mode = MODE_DEAD; S.R.cnt = 0; S.R.term = 1; });
-    } else if (redo == 2) {
+    } else if (S.entry_g >= cg + CLY_CHUNK) {
         ex.one([&]() { S.mode = MODE_PASS; S.R.cnt = 0; S.R.term = 0; });
-        env.crc(ex, S);
-    } else if (redo == 3) {
-        ex.one([&]() { S.mode = MODE_NORMAL; });
-        resolve(ex, S, newE);
-        env.crc(ex, S);
+    } else {
+        const int newE = (int)(S.entry_g - cg);
+        if (S.mode != MODE_NORMAL || S.guess != newE) {
+            ex.one([&]() { S.mode = MODE_NORMAL; });
+            resolve(ex, S, newE);
+        }
     }
     // ---- publish the resolved descriptor
     ex.one([&]() {
@@ -912,9 +976,10 @@ CLY_DEV void chunk_body(EX& ex, ScanShared& S, Env& env) {
         const uint32_t ep = env.epoch;
         env.publish_full(S.C.chunk, ds_pack(ep, DS_FULL, S.C.fof, dead, 0, 0, cnt), ds_tag(ep, X),
                          ds_tag(ep, S.p_excl + cnt), S.p_excl + cnt);
+        env.mark(S, 6);
     });
-    // ---- tuples and summary
-    ex.one([&]() { env.mark(S, 6); });
+    // ---- CRC, tuples, summary
+    if (S.mode != MODE_DEAD) env.crc(ex, S);
     ex.all([&](int t) { env.emit_lane(S, t); });
     ex.one([&]() {
         env.mark(S, 7);

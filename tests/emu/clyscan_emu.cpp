@@ -84,6 +84,7 @@ struct HostEnv {
     std::mt19937* rng;
 
     void mark(ScanShared&, int) {}
+    void lb_collect(ScanShared& S, int t) { if (t == 0) lookback_collect_seq(*this, S, epoch); }
     void dbg_lane(ScanShared& S, int t) {
         if (!run->lanes.empty() && S.C.chunk < 4) dbg_lane_fill(S, t, &run->lanes[(S.C.chunk * CLY_NT + t) * 8]);
     }
@@ -296,5 +297,7 @@ extern "C" int cly_scan_device(cly_ctx*, const cly_file*, int, cly_tuple*, uint6
 }
 extern "C" const char* cly_strerror(int code) { return code == 0 ? "ok" : "error"; }
 extern "C" const char* cly_build_info(void) {
-    return "clyscan CPU EMULATOR (test only) NT=" "" ;
+    static char buf[160];
+    snprintf(buf, sizeof(buf), "clyscan CPU EMULATOR (test only) NT=%d SUB=%d CHUNK=%d", CLY_NT, CLY_SUB, CLY_CHUNK);
+    return buf;
 }

@@ -103,7 +103,7 @@ def test_shapes(emu, shape):
 
 def test_chunk_boundary_tails(emu):
     base = fixed_records_file(400, 300, seed=3)
-    for chunk in (2048, 32768):
+    for chunk in (1792, 31744):
         k = (len(base) // chunk) * chunk - 7
         for extra in (0, 3, 7, 8):
             for cut in (0, 1, 5, 6, 13):
