@@ -172,54 +172,77 @@ struct DevEnv {
         return true;
     }
     __device__ __forceinline__ bool spin_ok() const { return spins <= LB_SPIN_MAX; }
-    // look-back phase 1 by wave 0: 64 descriptors per round trip, back to the
-    // nearest FULL (scan_core.h lookback_compose does phase 2)
-    __device__ void lb_collect(ScanShared& S, int t) {
+    // Decoupled look-back by wave 0: 64 descriptors per round trip into LDS,
+    // then every lane folds them in order (uniform; scan_core.h lb_walk_step).
+    __device__ void lookback(ScanShared& S, int t) {
         if (t >= 64) return;
         const int64_t c = S.C.chunk;
-        int n = 0;
-        int64_t base = c - 1;
-        for (int win = 0;; win++) {
-            if (base < 0) { if (t == 0) { S.lb_jfull = -1; S.lb_n = n; } return; }
-            if (n >= CLY_LBWIN) { if (t == 0) { S.lb_jfull = -2; S.lb_n = n; } return; }
-            const int64_t j = base - t;
-            for (;;) {
-                uint64_t w0 = 0, x = 0, p = 0;
-                uint64_t st = DS_FULL;                 // j < 0: the virtual start
-                bool ready = true;
-                if (j >= 0) {
-                    w0 = ld(j, 0);
-                    st = ds_state(w0, epoch);
-                    if (st == DS_SPEC) { x = ld(j, 1); ready = ds_ok(x, epoch); }
-                    else if (st == DS_FULL) { x = ld(j, 2); p = ld(j, 3); ready = ds_ok(x, epoch) && ds_ok(p, epoch); }
-                    else ready = false;
-                }
-                const unsigned long long fullm = __ballot(ready && st == DS_FULL);
-                const unsigned long long nrm = __ballot(!ready);
-                const int ff = fullm ? __ffsll((long long)fullm) - 1 : 64;
-                const unsigned long long need = ff >= 63 ? ~0ull : ((2ull << ff) - 1);
-                if (nrm & need) {
-                    bool go = true;
-                    if (t == 0) go = spin();
-                    go = __shfl(go ? 1 : 0, 0, 64) != 0;
-                    if (!go) { if (t == 0) { S.lb_jfull = -1; S.lb_n = n; } return; }
-                    continue;
-                }
-                const int take = ff < 64 ? ff : 64;       // SPEC descriptors in this window
-                if (t < take && n + t < CLY_LBWIN) { S.lb_w0[n + t] = w0; S.lb_x[n + t] = x; }
-                if (ff < 64) {
-                    if (t == ff) {
-                        S.lb_jfull = j >= 0 ? j : -1;
-                        S.lb_fw0 = w0; S.lb_fx = x; S.lb_fp = p;
-                        S.lb_n = n + take;
-                    }
-                    return;
-                }
-                n += 64;
-                base -= 64;
+        LbWalk w;
+        lb_walk_init(w, c, S.C.fof);
+        LbState out;
+        out.E = 0; out.P = 0; out.dead = 1; out._pad = 0;
+        int64_t jf = -1;
+        int r = 0;
+        bool ok = true;
+        for (int64_t base = c - 1; r == 0 && ok; base -= 64) {
+            if (base < 0) {
+                r = lb_apply_full_walk(w, 0, 0, 0, out) ? 1 : 2;
+                jf = -1;
                 break;
             }
+            const int64_t j = base - t;
+            uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+            int stop;
+            for (;;) {
+                bool ready = true, full = false;
+                if (j >= 0) {
+                    w0 = ld(j, 0);
+                    const uint64_t st = ds_state(w0, epoch);
+                    if (st == DS_SPEC) { w1 = ld(j, 1); ready = ds_ok(w1, epoch); }
+                    else if (st == DS_FULL) { w2 = ld(j, 2); w3 = ld(j, 3); ready = ds_ok(w2, epoch) && ds_ok(w3, epoch); full = ready; }
+                    else ready = false;
+                }
+                const unsigned long long endm = __ballot(full || j < 0);
+                stop = endm ? __ffsll((long long)endm) - 1 : 64;
+                const unsigned long long need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);
+                if (!(__ballot(!ready) & need)) break;
+                int go = 1;
+                if (t == 0) go = spin() ? 1 : 0;
+                if (!__shfl(go, 0, 64)) { ok = false; break; }
+            }
+            if (!ok) break;
+            S.lb_w[0][t] = w0; S.lb_w[1][t] = w1; S.lb_w[2][t] = w2; S.lb_w[3][t] = w3;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const int last = stop < 64 ? stop : 63;
+            for (int i = 0; i <= last && r == 0; i++) {
+                const int64_t ji = base - i;
+                if (ji < 0) {
+                    r = lb_apply_full_walk(w, 0, 0, 0, out) ? 1 : 2;
+                    jf = -1;
+                } else {
+                    r = lb_walk_step(w, ji, S.lb_w[0][i], S.lb_w[1][i], S.lb_w[2][i], S.lb_w[3][i], epoch, out, jf);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
         }
+        if (t != 0) return;
+        if (ok && r == 2) {
+            if (jf == -3) {
+                // nearest FULL before the chunk where the walk failed
+                jf = -1;
+                for (int64_t k = S.C.chunk - 1; k >= 0; k--) {
+                    uint64_t a0 = ld(k, 0);
+                    while (ds_state(a0, epoch) == 0 && spin()) a0 = ld(k, 0);
+                    if (ds_state(a0, epoch) == DS_FULL) { jf = k; break; }
+                }
+            }
+            lb_forward(*this, c, S.C.fof, jf, epoch, out);
+        }
+        S.entry_g = out.E;
+        S.p_excl = out.P;
+        S.in_dead = out.dead;
     }
     template <class EX> __device__ __forceinline__ void crc(EX& ex, ScanShared& S) { crc_phase(ex, S, shift); }
     __device__ __forceinline__ void emit_lane(ScanShared& S, int t) {

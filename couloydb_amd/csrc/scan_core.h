@@ -58,7 +58,7 @@
 #define CLY_HALO 64           // >= 26 (max header) + 11 (txId varint) past the chunk end
 #define CLY_WIN (CLY_CHUNK + CLY_HALO)
 #define CLY_NWAVE (CLY_NT / 64)
-#define CLY_LBWIN 256         // look-back window (descriptors prefetched into LDS)
+#define CLY_LBWIN 64          // look-back: descriptors read per round trip (one wave)
 static_assert(CLY_NT % 64 == 0 && CLY_NT <= 1024, "CLY_NT must be a multiple of 64");
 static_assert(CLY_SUB % 4 == 0 && CLY_SUB >= 28, "CLY_SUB must be a multiple of 4");
 static_assert(CLY_CHUNK % 16 == 0 && CLY_WIN % 16 == 0, "16-B staging");
@@ -238,9 +238,8 @@ struct ScanShared {
     uint8_t  sc_c0[CLY_NT];                   // phase-A constness (kept through the scan)
     // block reduction scratch
     int32_t  red[CLY_NWAVE * 2];
-    // look-back window: descriptors of chunks c-1, c-2, ... (SPEC words)
-    uint64_t lb_w0[CLY_LBWIN];
-    uint64_t lb_x[CLY_LBWIN];
+    // look-back window: words of 64 descriptors (GPU form of the walk)
+    uint64_t lb_w[4][64];
     // scalars
     ChunkCtx C;
     ChainRes R;
@@ -254,9 +253,7 @@ struct ScanShared {
     int64_t  entry_g;                         // look-back: global entry position
     uint64_t p_excl;                          // records before the chunk (global slot)
     int32_t  in_dead;                         // look-back: chain ended before this chunk
-    int32_t  lb_n;                            // SPEC descriptors collected in lb_w0/lb_x
-    int64_t  lb_jfull;                        // nearest FULL chunk (-1: none before; -2: window exhausted)
-    uint64_t lb_fw0, lb_fx, lb_fp;            // its words
+
     int32_t  fail;                            // internal invariant violated (reported as a device error)
     int32_t  fail_k;
 };
@@ -345,67 +342,176 @@ CLY_DEV bool lb_compose_spec(LbState& s, int64_t j, uint64_t w0, uint64_t x) {
     return false;
 }
 
-// Decoupled look-back, phase 1 (Env::lb_collect): the descriptors of chunks
-// c-1, c-2, ... back to the nearest one with FULL words are read (by a whole
-// wave on the GPU, 64 per round trip) into S.lb_w0/S.lb_x, S.lb_jfull and
-// S.lb_fw0/fx/fp.  Phase 2 (this function, one lane): compose forward from
-// that FULL through the speculative descriptors; a chunk whose guess does not
-// match the chain is waited for (its FULL words).  Env supplies ld(j, k)
-// (word k of chunk j, agent scope) and spin() (false once the bound is hit).
+// ---------------------------------------------------------------------------
+// Decoupled look-back (CUB-style, unbounded): walk back from chunk c-1 until a
+// chunk with FULL words, folding every speculative descriptor on the way into
+// an O(1) summary of the suffix (chunks j+1 .. c-1):
+//   requirement  on the chain position entering the suffix: none, == e0
+//                (EXACT: the first chunk's guess must be the true entry) or
+//                >= e0 (ATLEAST: the suffix starts with chunks covered by one
+//                record),
+//   result       E_c as a function of that position: the identity (only
+//                covered chunks so far), a constant exit, or dead,
+//   counts       records of the suffix (pending on the requirement) and of the
+//                part after a first-of-file chunk (fixed).
+// Folding chunk j in front: "tight" when its guessed chain exits where the
+// suffix requires (requirement becomes == g_j, counts += n_j), otherwise
+// "transparent" (j is covered by one record; requirement unchanged).  Both are
+// sufficient conditions; the FULL chunk's exit checks the final requirement.
+// A first-of-file chunk's guess (0) is exact: it fixes E_c, and the walk goes
+// on for the record count only.  On a failed check (a wrong guess or a wrong
+// tight/transparent choice) lb_forward() composes forward from the FULL chunk
+// with exact per-chunk checks (rare path).
+#define LB_REQ_NONE 0
+#define LB_REQ_EXACT 1
+#define LB_REQ_ATLEAST 2
+#define LB_RES_IDENT 0
+#define LB_RES_CONST 1
+#define LB_RES_DEAD 2
+struct LbWalk {
+    int64_t  e0, rx, cE;
+    uint64_t dp, dp_fixed;
+    int32_t  req, res, fixed, cdead;
+};
+
+CLY_DEV void lb_walk_init(LbWalk& w, int64_t c, int fof) {
+    w.e0 = 0; w.rx = 0; w.cE = 0; w.dp = 0; w.dp_fixed = 0;
+    w.req = LB_REQ_NONE; w.res = LB_RES_IDENT; w.fixed = 0; w.cdead = 0;
+    if (fof) { w.fixed = 1; w.cE = c * (int64_t)CLY_CHUNK; }
+}
+
+CLY_DEV bool lb_req_ok(const LbWalk& w, int64_t E) {
+    return w.req == LB_REQ_NONE || (w.req == LB_REQ_EXACT ? E == w.e0 : E >= w.e0);
+}
+
+// Fold SPEC descriptor (w0, exit x) of chunk j.  False = the walk cannot
+// continue consistently (only at a first-of-file chunk whose exact chain
+// misses the requirement).
+CLY_DEV bool lb_fold_spec(LbWalk& w, int64_t j, uint64_t w0, int64_t x) {
+    const int64_t cs = j * (int64_t)CLY_CHUNK;
+    const int term = ds_term(w0);
+    const uint32_t n = ds_cnt(w0);
+    if (ds_fof(w0)) {
+        if (!term && !lb_req_ok(w, x)) return false;
+        if (!w.fixed) {
+            w.fixed = 1;
+            if (term || w.res == LB_RES_DEAD) w.cdead = 1;
+            else w.cE = w.res == LB_RES_IDENT ? x : w.rx;
+        }
+        w.dp_fixed += (term ? 0 : w.dp) + n;
+        w.req = LB_REQ_NONE; w.res = LB_RES_IDENT; w.dp = 0;
+        return true;
+    }
+    if (ds_gvalid(w0) && (w.req == LB_REQ_NONE || (!term && lb_req_ok(w, x)))) {
+        if (term) { w.res = LB_RES_DEAD; w.dp = n; }
+        else { if (w.res == LB_RES_IDENT) { w.res = LB_RES_CONST; w.rx = x; } w.dp += n; }
+        w.req = LB_REQ_EXACT;
+        w.e0 = cs + ds_grel(w0);
+    } else if (w.req == LB_REQ_NONE) {
+        w.req = LB_REQ_ATLEAST;
+        w.e0 = cs + CLY_CHUNK;
+    }
+    return true;
+}
+
+// Apply FULL words of chunk j (exit X, dead, records P up to and including j).
+// False = the requirement fails (forward fallback needed).
+CLY_DEV bool lb_apply_full_walk(const LbWalk& w, int dead, int64_t X, uint64_t P, LbState& out) {
+    if (dead) {
+        out.dead = w.fixed ? w.cdead : 1;
+        out.E = w.fixed ? w.cE : 0;
+        out.P = P + w.dp_fixed;
+        return true;
+    }
+    if (!lb_req_ok(w, X)) return false;
+    if (w.fixed) { out.dead = w.cdead; out.E = w.cE; }
+    else { out.dead = w.res == LB_RES_DEAD; out.E = w.res == LB_RES_IDENT ? X : w.rx; }
+    out.P = P + w.dp + w.dp_fixed;
+    return true;
+}
+
+// Rare path: exact forward composition from the FULL chunk jf (or from the
+// start when jf < 0) to c, waiting for the FULL words of any chunk whose guess
+// does not match the chain.  Env supplies ld(j, k) and spin().
 template <class Env>
-CLY_DEV void lookback_compose(Env& env, ScanShared& S, uint32_t epoch, LbState& s) {
-    const int64_t c = S.C.chunk;
+CLY_DEV void lb_forward(Env& env, int64_t c, int fof, int64_t jf, uint32_t epoch, LbState& s) {
     s.E = 0; s.P = 0; s.dead = 0; s._pad = 0;
-    int64_t j = S.lb_jfull;
-    if (j == -2) {
-        // window exhausted without a FULL: wait for the predecessor's FULL words
-        j = c - 1;
-        uint64_t w0 = env.ld(j, 0), x = env.ld(j, 2), p = env.ld(j, 3);
+    if (jf >= 0) {
+        uint64_t w0 = env.ld(jf, 0), x = env.ld(jf, 2), p = env.ld(jf, 3);
         while (ds_state(w0, epoch) != DS_FULL || !ds_ok(x, epoch) || !ds_ok(p, epoch)) {
             if (!env.spin()) return;
-            w0 = env.ld(j, 0); x = env.ld(j, 2); p = env.ld(j, 3);
+            w0 = env.ld(jf, 0); x = env.ld(jf, 2); p = env.ld(jf, 3);
         }
         s.dead = ds_term(w0); s.E = (int64_t)(x & DS_VAL_MASK); s.P = p & DS_VAL_MASK;
-    } else if (j >= 0) {
-        s.dead = ds_term(S.lb_fw0); s.E = (int64_t)(S.lb_fx & DS_VAL_MASK); s.P = S.lb_fp & DS_VAL_MASK;
     }
-    for (int64_t k = j + 1; k < c; k++) {
-        const int i = (int)(c - 1 - k);
-        if (lb_compose_spec(s, k, S.lb_w0[i], S.lb_x[i] & DS_VAL_MASK)) continue;
-        uint64_t w0 = env.ld(k, 0), x = env.ld(k, 2), p = env.ld(k, 3);
+    for (int64_t k = jf + 1; k < c; k++) {
+        uint64_t w0 = env.ld(k, 0);
+        while (ds_state(w0, epoch) == 0) { if (!env.spin()) return; w0 = env.ld(k, 0); }
+        if (ds_state(w0, epoch) == DS_SPEC) {
+            uint64_t x = env.ld(k, 1);
+            while (!ds_ok(x, epoch)) { if (!env.spin()) return; x = env.ld(k, 1); }
+            if (lb_compose_spec(s, k, w0, x & DS_VAL_MASK)) continue;
+        }
+        uint64_t x = env.ld(k, 2), p = env.ld(k, 3);
         while (ds_state(w0, epoch) != DS_FULL || !ds_ok(x, epoch) || !ds_ok(p, epoch)) {
             if (!env.spin()) return;
             w0 = env.ld(k, 0); x = env.ld(k, 2); p = env.ld(k, 3);
         }
         s.dead = ds_term(w0); s.E = (int64_t)(x & DS_VAL_MASK); s.P = p & DS_VAL_MASK;
     }
-    if (S.C.fof) { s.E = c * (int64_t)CLY_CHUNK; s.dead = 0; }
+    if (fof) { s.E = c * (int64_t)CLY_CHUNK; s.dead = 0; }
 }
 
-// Phase 1, sequential form (CPU emulator; same result as the wave form).
-template <class Env>
-CLY_DEV void lookback_collect_seq(Env& env, ScanShared& S, uint32_t epoch) {
-    const int64_t c = S.C.chunk;
-    int n = 0;
-    for (int64_t j = c - 1;; j--) {
-        if (j < 0) { S.lb_jfull = -1; break; }
-        if (n == CLY_LBWIN) { S.lb_jfull = -2; break; }
-        uint64_t w0 = env.ld(j, 0);
-        for (;;) {
-            const uint64_t st = ds_state(w0, epoch);
-            if (st == DS_SPEC) {
-                const uint64_t x = env.ld(j, 1);
-                if (ds_ok(x, epoch)) { S.lb_w0[n] = w0; S.lb_x[n] = x; n++; break; }
-            } else if (st == DS_FULL) {
-                const uint64_t x = env.ld(j, 2), p = env.ld(j, 3);
-                if (ds_ok(x, epoch) && ds_ok(p, epoch)) { S.lb_fw0 = w0; S.lb_fx = x; S.lb_fp = p; break; }
-            }
-            if (!env.spin()) { S.lb_jfull = -1; S.lb_n = n; return; }
-            w0 = env.ld(j, 0);
-        }
-        if (ds_state(w0, epoch) == DS_FULL) { S.lb_jfull = j; break; }
+// One descriptor of the backward walk (words already loaded and ready).
+// Returns 0 = continue, 1 = done (out filled), 2 = forward fallback from jf.
+CLY_DEV int lb_walk_step(LbWalk& w, int64_t j, uint64_t w0, uint64_t w1, uint64_t w2, uint64_t w3,
+                         uint32_t epoch, LbState& out, int64_t& jf) {
+    if (ds_state(w0, epoch) == DS_FULL) {
+        if (lb_apply_full_walk(w, ds_term(w0), (int64_t)(w2 & DS_VAL_MASK), w3 & DS_VAL_MASK, out)) return 1;
+        jf = j;
+        return 2;
     }
-    S.lb_n = n;
+    if (!lb_fold_spec(w, j, w0, (int64_t)(w1 & DS_VAL_MASK))) {
+        jf = -3;              // find the nearest FULL before j, then compose forward
+        return 2;
+    }
+    return 0;
+}
+
+// Sequential form of the whole look-back (CPU emulator; the GPU form reads 64
+// descriptors per round trip and runs the same steps).
+template <class Env>
+CLY_DEV void lookback_seq(Env& env, int64_t c, int fof, uint32_t epoch, LbState& out) {
+    LbWalk w;
+    lb_walk_init(w, c, fof);
+    int64_t jf = -1;
+    int r = 0;
+    for (int64_t j = c - 1; j >= 0 && r == 0; j--) {
+        uint64_t w0, w1 = 0, w2 = 0, w3 = 0;
+        for (;;) {
+            w0 = env.ld(j, 0);
+            const uint64_t st = ds_state(w0, epoch);
+            if (st == DS_SPEC) { w1 = env.ld(j, 1); if (ds_ok(w1, epoch)) break; }
+            else if (st == DS_FULL) { w2 = env.ld(j, 2); w3 = env.ld(j, 3); if (ds_ok(w2, epoch) && ds_ok(w3, epoch)) break; }
+            if (!env.spin()) { out.E = 0; out.P = 0; out.dead = 1; return; }
+        }
+        r = lb_walk_step(w, j, w0, w1, w2, w3, epoch, out, jf);
+        if (r == 2 && jf == -3) {
+            // nearest FULL before j
+            jf = -1;
+            for (int64_t k = j - 1; k >= 0; k--) {
+                uint64_t a0 = env.ld(k, 0);
+                while (ds_state(a0, epoch) == 0) { if (!env.spin()) { out.dead = 1; return; } a0 = env.ld(k, 0); }
+                if (ds_state(a0, epoch) == DS_FULL) { jf = k; break; }
+            }
+        }
+    }
+    if (r == 0) {
+        // reached the start of everything: as a FULL with exit 0 and no records
+        if (!lb_apply_full_walk(w, 0, 0, 0, out)) { jf = -1; r = 2; }
+        else r = 1;
+    }
+    if (r == 2) lb_forward(env, c, fof, jf, epoch, out);
 }
 
 // ---------------------------------------------------------------------------
@@ -940,15 +1046,9 @@ CLY_DEV void chunk_body(EX& ex, ScanShared& S, Env& env) {
         env.mark(S, 3);
     });
     // ---- look-back: true entry and output slot
-    ex.all([&](int t) { env.lb_collect(S, t); });
+    ex.all([&](int t) { env.lookback(S, t); });
     ex.one([&]() {
-        env.mark(S, 4);
-        LbState ls;
-        lookback_compose(env, S, env.epoch, ls);
-        if (!env.spin_ok()) { S.fail = 4; ls.dead = 1; }
-        S.entry_g = ls.E;
-        S.p_excl = ls.P;
-        S.in_dead = ls.dead;
+        if (!env.spin_ok()) { S.fail = 4; S.in_dead = 1; }
         if (!S.in_dead && S.entry_g < cg) { S.fail = 2; S.in_dead = 1; }   // cannot happen
         env.mark(S, 5);
     });

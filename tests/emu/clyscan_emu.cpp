@@ -84,7 +84,12 @@ struct HostEnv {
     std::mt19937* rng;
 
     void mark(ScanShared&, int) {}
-    void lb_collect(ScanShared& S, int t) { if (t == 0) lookback_collect_seq(*this, S, epoch); }
+    void lookback(ScanShared& S, int t) {
+        if (t != 0) return;
+        LbState ls;
+        lookback_seq(*this, S.C.chunk, S.C.fof, epoch, ls);
+        S.entry_g = ls.E; S.p_excl = ls.P; S.in_dead = ls.dead;
+    }
     void dbg_lane(ScanShared& S, int t) {
         if (!run->lanes.empty() && S.C.chunk < 4) dbg_lane_fill(S, t, &run->lanes[(S.C.chunk * CLY_NT + t) * 8]);
     }
