@@ -42,6 +42,8 @@ struct Globals {                 // zeroed per call
     uint32_t lb_timeout;         // a look-back spin hit its bound (never expected)
     uint32_t fail;               // a chunk violated an internal invariant (never expected)
     uint64_t total;              // tuple slots used (records + any past an ErrInvalidCRC)
+    uint64_t phase[10];          // profiling build: summed clock cycles per chunk phase
+    uint64_t lbstat[8];          // profiling build: look-back windows, spins, slow steps, fallbacks, distance
 };
 
 struct FileOut {
@@ -126,6 +128,14 @@ struct DevEnv {
     uint32_t spins;
 
     __device__ __forceinline__ void mark(ScanShared& S, int v) {
+#ifdef CLY_PHASE_PROF
+        S.tstamp[v] = __builtin_amdgcn_s_memtime();
+        if (v == 8)
+            for (int k = 1; k <= 8; k++) {
+                const int pk = k == 5 ? 3 : k - 1;       // no stamp 4
+                if (k != 4) atomicAdd((unsigned long long*)&g->phase[k], (unsigned long long)(S.tstamp[k] - S.tstamp[pk]));
+            }
+#endif
         if (trace) { trace[2 * (S.C.chunk & 1023)] = v; trace[2 * (S.C.chunk & 1023) + 1] = S.C.chunk; __threadfence_system(); }
     }
     __device__ __forceinline__ void report_fail(ScanShared& S) { atomicMax(&g->fail, (uint32_t)S.fail); }
@@ -184,7 +194,14 @@ struct DevEnv {
         int64_t jf = -1;
         int r = 0;
         bool ok = true;
+#ifdef CLY_PHASE_PROF
+        uint32_t st_win = 0, st_spin = 0, st_slow = 0;
+#define LBSTAT(v) v
+#else
+#define LBSTAT(v)
+#endif
         for (int64_t base = c - 1; r == 0 && ok; base -= 64) {
+            LBSTAT(st_win++);
             if (base < 0) {
                 r = lb_apply_full_walk(w, 0, 0, 0, out) ? 1 : 2;
                 jf = -1;
@@ -207,16 +224,47 @@ struct DevEnv {
                 const unsigned long long need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);
                 if (!(__ballot(!ready) & need)) break;
                 int go = 1;
+                LBSTAT(st_spin++);
                 if (t == 0) go = spin() ? 1 : 0;
                 if (!__shfl(go, 0, 64)) { ok = false; break; }
             }
             if (!ok) break;
+            // fast path: a run of "tight" speculative descriptors from lane 0
+            // (guess valid, not first-of-file, not terminal, exit == the guessed
+            // entry of the chunk after it) folds at once: requirement == the
+            // last one's guess, counts summed by a wave reduction.
+            int i0 = 0;
+            {
+                const int64_t jn = j + 1;                          // chunk after lane t's chunk
+                const uint64_t w0n = __shfl_up(w0, 1, 64);          // its state word (lane t-1)
+                const bool spec = j >= 0 && ds_state(w0, epoch) == DS_SPEC && ds_gvalid(w0) && !ds_fof(w0) &&
+                                  !ds_term(w0);
+                const int64_t xj = (int64_t)(w1 & DS_VAL_MASK);
+                bool tight;
+                if (t == 0) tight = spec && lb_req_ok(w, xj);
+                else tight = spec && ds_gvalid(w0n) && !ds_fof(w0n) && xj == jn * (int64_t)CLY_CHUNK + ds_grel(w0n);
+                const unsigned long long tm = __ballot(tight && t < stop);
+                const int run = (~tm) ? __ffsll((long long)~tm) - 1 : 64;    // tight lanes 0..run-1
+                if (run > 0) {
+                    uint32_t cnt = (t < run) ? ds_cnt(w0) : 0u;
+                    #pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+                    const uint64_t w0l = __shfl(w0, run - 1, 64);
+                    const uint64_t x0 = __shfl(w1, 0, 64);
+                    if (w.res == LB_RES_IDENT) { w.res = LB_RES_CONST; w.rx = (int64_t)(x0 & DS_VAL_MASK); }
+                    w.dp += cnt;
+                    w.req = LB_REQ_EXACT;
+                    w.e0 = (base - (run - 1)) * (int64_t)CLY_CHUNK + ds_grel(w0l);
+                    i0 = run;
+                }
+            }
             S.lb_w[0][t] = w0; S.lb_w[1][t] = w1; S.lb_w[2][t] = w2; S.lb_w[3][t] = w3;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const int last = stop < 64 ? stop : 63;
-            for (int i = 0; i <= last && r == 0; i++) {
+            LBSTAT(st_slow += (last + 1 - i0));
+            for (int i = i0; i <= last && r == 0; i++) {
                 const int64_t ji = base - i;
                 if (ji < 0) {
                     r = lb_apply_full_walk(w, 0, 0, 0, out) ? 1 : 2;
@@ -228,6 +276,12 @@ struct DevEnv {
             __builtin_amdgcn_wave_barrier();
         }
         if (t != 0) return;
+#ifdef CLY_PHASE_PROF
+        atomicAdd((unsigned long long*)&g->lbstat[0], (unsigned long long)st_win);
+        atomicAdd((unsigned long long*)&g->lbstat[1], (unsigned long long)st_spin);
+        atomicAdd((unsigned long long*)&g->lbstat[2], (unsigned long long)st_slow);
+        if (ok && r == 2) atomicAdd((unsigned long long*)&g->lbstat[3], 1ull);
+#endif
         if (ok && r == 2) {
             if (jf == -3) {
                 // nearest FULL before the chunk where the walk failed
@@ -269,6 +323,9 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         S.C.chunk = c;
         S.C.fidx = lo;
     }
+#ifdef CLY_PHASE_PROF
+    if (threadIdx.x == 0) S.tstamp[0] = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();
     const int c = S.C.chunk;
     if (c >= nchunks) return;
@@ -288,6 +345,7 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         S.C.fof = cl == 0;
         S.C.lof = cl == (int)env.F.nchunks - 1;
         S.C.fid = env.F.fid;
+        S.C.gfile = env.F.base;
     }
     __syncthreads();
     DevExec ex{&S};
@@ -605,6 +663,12 @@ extern "C" int cly_dbg_chunks(cly_ctx* c, void* dbg_out, void* sums_out, int max
     if (dbg_out && c->d_dbg) HIPCK(hipMemcpy(dbg_out, c->d_dbg, sizeof(ChunkDbg) * n, hipMemcpyDeviceToHost));
     if (sums_out) HIPCK(hipMemcpy(sums_out, c->d_sums, sizeof(ChunkSum) * n, hipMemcpyDeviceToHost));
     return n;
+}
+// profiling build: summed cycles per phase of the last call (10 counters)
+extern "C" int cly_dbg_phases(cly_ctx* c, uint64_t* out) {
+    for (int k = 0; k < 10; k++) out[k] = c->h_g->phase[k];
+    for (int k = 0; k < 8; k++) out[10 + k] = c->h_g->lbstat[k];
+    return 18;
 }
 extern "C" int cly_dbg_sizes(int* out3) { out3[0] = sizeof(ChunkDbg); out3[1] = sizeof(ChunkSum); out3[2] = sizeof(ScanShared); return 0; }
 

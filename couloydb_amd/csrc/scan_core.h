@@ -188,6 +188,7 @@ CLY_DEV uint32_t shift_tab(const uint32_t* st, int lvl, uint32_t v) {
 // ---------------------------------------------------------------------------
 // Shared (LDS) state of one chunk.
 struct ChunkCtx {
+    const uint8_t* gfile; // the file's bytes in the executor's memory (device: HBM)
     int64_t  cbase;       // file offset of the chunk start
     int64_t  nrel;        // bytes from chunk start to end of file
     int32_t  dlen;        // data bytes in the chunk (<= CHUNK)
@@ -254,6 +255,9 @@ struct ScanShared {
     uint64_t p_excl;                          // records before the chunk (global slot)
     int32_t  in_dead;                         // look-back: chain ended before this chunk
 
+#ifdef CLY_PHASE_PROF
+    uint64_t tstamp[10];                      // profiling build: per-phase clock stamps
+#endif
     int32_t  fail;                            // internal invariant violated (reported as a device error)
     int32_t  fail_k;
 };
@@ -511,7 +515,7 @@ CLY_DEV void lookback_seq(Env& env, int64_t c, int fof, uint32_t epoch, LbState&
         if (!lb_apply_full_walk(w, 0, 0, 0, out)) { jf = -1; r = 2; }
         else r = 1;
     }
-    if (r == 2) lb_forward(env, c, fof, jf, epoch, out);
+    if (r == 2) { env.note_fallback(c, jf); lb_forward(env, c, fof, jf, epoch, out); }
 }
 
 // ---------------------------------------------------------------------------
@@ -593,12 +597,21 @@ CLY_NOINL void spec_lane(ScanShared& S, int t) {
                 const Hdr e = step_hdr(w, x, C.nrel, C.cbase + x);
                 if (!e.good) continue;
             } else {
-                vin = 0;
+                // exit beyond the window: check its header in global memory
+                uint8_t hb[28];
+                const uint8_t* gp = C.gfile + C.cbase + x;
+                for (int k = 0; k < need; k++) hb[k] = gp[k];
+                const Hdr e = step_hdr(hb, 0, C.nrel - x, C.cbase + x);
+                if (!e.good) continue;
             }
         }
-        S.sp_s[t] = (int16_t)q; S.sp_last[t] = (int16_t)p; S.sp_cnt[t] = (uint16_t)c; S.sp_vin[t] = vin;
-        S.sp_x[t] = (uint32_t)x;
-        return;
+        // keep the first candidate; a later one with a checked exit replaces
+        // one whose exit could not be checked (then the scan stops)
+        if (S.sp_s[t] < 0 || vin) {
+            S.sp_s[t] = (int16_t)q; S.sp_last[t] = (int16_t)p; S.sp_cnt[t] = (uint16_t)c; S.sp_vin[t] = vin;
+            S.sp_x[t] = (uint32_t)x;
+        }
+        if (vin) return;
     }
 }
 

@@ -65,6 +65,7 @@ struct EmuRun {
     uint64_t out_cap;
     std::atomic<unsigned> overflow{0};
     std::atomic<unsigned> fail{0};
+    std::atomic<unsigned> fallbacks{0};
     std::atomic<uint64_t> total{0};
     int nchunks;
     int jitter;
@@ -84,6 +85,10 @@ struct HostEnv {
     std::mt19937* rng;
 
     void mark(ScanShared&, int) {}
+    void note_fallback(int64_t c, int64_t jf) {
+        run->fallbacks.fetch_add(1);
+        if (getenv("CLY_EMU_VERBOSE")) fprintf(stderr, "fallback chunk %lld jf %lld\n", (long long)c, (long long)jf);
+    }
     void lookback(ScanShared& S, int t) {
         if (t != 0) return;
         LbState ls;
@@ -152,6 +157,7 @@ static void run_chunk(EmuRun& R, int c, ScanShared& S, std::mt19937& rng) {
     S.C.fof = cl == 0;
     S.C.lof = cl == (int)F.nchunks - 1;
     S.C.fid = F.fid;
+    S.C.gfile = F.base;
     HostExec ex;
     HostEnv env{&R, &F, &rng, R.epoch};
     chunk_body(ex, S, env);
@@ -254,6 +260,7 @@ extern "C" int cly_scan(cly_ctx* ctx, const cly_file* files, int nfiles, cly_tup
     ctx->sums = R.sums;
     ctx->dbg = R.dbg;
     ctx->lanes = R.lanes;
+    if (getenv("CLY_EMU_STATS")) fprintf(stderr, "emu: %d chunks, %u look-back fallbacks\n", R.nchunks, R.fallbacks.load());
     if (R.fail.load()) return CLY_ERR_DEVICE;
     if (R.overflow.load()) return CLY_ERR_CAPACITY;
     // k_fin
