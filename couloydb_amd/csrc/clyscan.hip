@@ -60,6 +60,8 @@ struct DevExec {
     ScanShared* S;
     template <class F> __device__ __forceinline__ void all(F f) { f((int)threadIdx.x); __syncthreads(); }
     template <class F> __device__ __forceinline__ void one(F f) { if (threadIdx.x == 0) f(); __syncthreads(); }
+    // phase whose lanes each return a predicate; true iff it holds for all lanes
+    template <class F> __device__ __forceinline__ bool all_and(F f) { return __syncthreads_and(f((int)threadIdx.x)) != 0; }
     template <class F> __device__ __forceinline__ int reduce_min(F f) {
         int v = f((int)threadIdx.x);
         #pragma unroll
@@ -145,23 +147,47 @@ struct DevEnv {
     }
 
     __device__ __forceinline__ ChunkDbg* dbg_slot(int c) { return dbg ? dbg + c : nullptr; }
+    // Chunk bytes (+halo) into LDS.  Whole windows go by LDS-DMA
+    // (global_load_lds_dwordx4: 1 KiB per wave instruction, all in flight at
+    // once, no register staging); the last chunk of a file (window cut by the
+    // file end) is staged through registers with a zero-filled tail.
     __device__ __forceinline__ void stage_lane(ScanShared& S, int t) {
-        uint4* w4 = reinterpret_cast<uint4*>(S.win);
         const int wl = S.C.win_len;
+        if (wl == CLY_WIN) {
+            const int lane = t & 63, wv = t >> 6;
+            const uint8_t* src = F.base + S.C.cbase;
+            #pragma unroll
+            for (int k = 0; k < (CLY_WIN / 16 + CLY_NT - 1) / CLY_NT; k++) {
+                const int slot0 = k * CLY_NT + wv * 64;
+                if (slot0 + lane < CLY_WIN / 16)
+                    __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)(slot0 + lane) * 16),
+                                                     (__attribute__((address_space(3))) void*)((char*)S.win + slot0 * 16),
+                                                     16, 0, 0);
+            }
+            return;
+        }
+        uint4* w4 = reinterpret_cast<uint4*>(S.win);
         const int nvec = wl >> 4;
         const uint4* src = reinterpret_cast<const uint4*>(F.base + S.C.cbase);
-        for (int i = t; i < CLY_WIN / 16; i += CLY_NT) {
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (i < nvec) v = src[i];
-            else if (i == nvec && (wl & 15)) {
-                uint32_t wv[4] = {0, 0, 0, 0};
-                const uint8_t* b = F.base + S.C.cbase + (i << 4);
-                for (int k = 0; k < (wl & 15); k++) wv[k >> 2] |= (uint32_t)b[k] << (8 * (k & 3));
-                v = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-            }
-            w4[i] = v;
+        uint4 v[(CLY_WIN / 16 + CLY_NT - 1) / CLY_NT];
+        #pragma unroll
+        for (int k = 0; k < (CLY_WIN / 16 + CLY_NT - 1) / CLY_NT; k++) {
+            const int i = t + k * CLY_NT;
+            v[k] = i < nvec ? src[i] : make_uint4(0, 0, 0, 0);
+        }
+        #pragma unroll
+        for (int k = 0; k < (CLY_WIN / 16 + CLY_NT - 1) / CLY_NT; k++) {
+            const int i = t + k * CLY_NT;
+            if (i < CLY_WIN / 16) w4[i] = v[k];
+        }
+        if (t == 0 && (wl & 15)) {
+            uint32_t wv4[4] = {0, 0, 0, 0};
+            const uint8_t* b = F.base + S.C.cbase + (nvec << 4);
+            for (int k = 0; k < (wl & 15); k++) wv4[k >> 2] |= (uint32_t)b[k] << (8 * (k & 3));
+            w4[nvec] = make_uint4(wv4[0], wv4[1], wv4[2], wv4[3]);
         }
     }
+    __device__ __forceinline__ void stage_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
     __device__ __forceinline__ void publish_spec(int c, uint64_t w0, uint64_t w1) {
         st_agent(&desc[c].w[1], w1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -847,10 +847,13 @@ template <class EX>
 CLY_DEV void crc_phase(EX& ex, ScanShared& S, const uint32_t* shift_tabs) {
     ex.one([&]() { S.bad = ~0ull; S.head_raw = 0; S.end_state = 0; });
     ex.all([&](int t) { crc_lane_a(S, t); });
+    // levels stop once every element is constant (records shorter than a few
+    // stripes: 1-2 levels instead of log2(NT))
     int cur = 0;
-    for (int lvl = 0, d = 1; d < CLY_NT; lvl++, d <<= 1) {
+    bool all_const = ex.all_and([&](int t) -> int { return S.sc_c[0][t]; });
+    for (int lvl = 0, d = 1; d < CLY_NT && !all_const; lvl++, d <<= 1) {
         const int src = cur;
-        ex.all([&](int t) {
+        all_const = ex.all_and([&](int t) -> int {
             uint32_t v = S.sc_v[src][t];
             uint8_t c = S.sc_c[src][t];
             if (t >= d && !c) {
@@ -859,6 +862,7 @@ CLY_DEV void crc_phase(EX& ex, ScanShared& S, const uint32_t* shift_tabs) {
             }
             S.sc_v[src ^ 1][t] = v;
             S.sc_c[src ^ 1][t] = c;
+            return c;
         });
         cur ^= 1;
     }
@@ -1025,7 +1029,7 @@ template <class EX, class Env>
 CLY_DEV void chunk_body(EX& ex, ScanShared& S, Env& env) {
     // ---- stage
     ex.one([&]() { S.fail = 0; env.mark(S, 1); });
-    ex.all([&](int t) { env.stage_lane(S, t); build_tab_lane(S.tab, t); });
+    ex.all([&](int t) { env.stage_lane(S, t); build_tab_lane(S.tab, t); env.stage_wait(); });
     // ---- speculation
     ex.all([&](int t) { spec_lane(S, t); });
     // ---- guess the entry: the first lane whose walk left through a checked

@@ -29,6 +29,11 @@
 struct HostExec {
     template <class F> void all(F f) { for (int t = 0; t < CLY_NT; t++) f(t); }
     template <class F> void one(F f) { f(); }
+    template <class F> bool all_and(F f) {
+        bool r = true;
+        for (int t = 0; t < CLY_NT; t++) r = (f(t) != 0) && r;
+        return r;
+    }
     template <class F> int reduce_min(F f) {
         int r = 0x7fffffff;
         for (int t = 0; t < CLY_NT; t++) { int v = f(t); if (v < r) r = v; }
@@ -85,6 +90,7 @@ struct HostEnv {
     std::mt19937* rng;
 
     void mark(ScanShared&, int) {}
+    void stage_wait() {}
     void note_fallback(int64_t c, int64_t jf) {
         run->fallbacks.fetch_add(1);
         if (getenv("CLY_EMU_VERBOSE")) fprintf(stderr, "fallback chunk %lld jf %lld\n", (long long)c, (long long)jf);
