@@ -55,51 +55,46 @@ struct FileOut {
 };
 
 // ---------------------------------------------------------------------------
-// Executor: one lane per thread; a phase ends with a workgroup barrier.
+// Executor: one chunk per wave, one stripe per lane.  A phase ends with a
+// wave-local LDS ordering point (no workgroup barrier: the waves of a
+// workgroup work on independent chunks); collectives are wave reductions.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 struct DevExec {
-    ScanShared* S;
-    template <class F> __device__ __forceinline__ void all(F f) { f((int)threadIdx.x); __syncthreads(); }
-    template <class F> __device__ __forceinline__ void one(F f) { if (threadIdx.x == 0) f(); __syncthreads(); }
+    int lane;
+    template <class F> __device__ __forceinline__ void all(F f) { f(lane); wave_sync(); }
+    template <class F> __device__ __forceinline__ void one(F f) { if (lane == 0) f(); wave_sync(); }
     // phase whose lanes each return a predicate; true iff it holds for all lanes
-    template <class F> __device__ __forceinline__ bool all_and(F f) { return __syncthreads_and(f((int)threadIdx.x)) != 0; }
+    template <class F> __device__ __forceinline__ bool all_and(F f) {
+        const int v = f(lane);
+        wave_sync();
+        return __ballot(v != 0) == ~0ull;
+    }
     template <class F> __device__ __forceinline__ int reduce_min(F f) {
-        int v = f((int)threadIdx.x);
+        int v = f(lane);
         #pragma unroll
         for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-        if ((threadIdx.x & 63) == 0) S->red[threadIdx.x >> 6] = v;
-        __syncthreads();
-        int r = S->red[0];
-        #pragma unroll
-        for (int k = 1; k < CLY_NWAVE; k++) r = min(r, S->red[k]);
-        __syncthreads();
-        return r;
+        return v;
     }
     template <class F> __device__ __forceinline__ void scan_max_incl(F f, int16_t* out) {
-        const int t = threadIdx.x, lane = t & 63;
-        int v = f(t);
+        int v = f(lane);
         #pragma unroll
         for (int o = 1; o < 64; o <<= 1) { const int u = __shfl_up(v, o, 64); if (lane >= o) v = max(v, u); }
-        if (lane == 63) S->red[t >> 6] = v;
-        __syncthreads();
-        int pre = -1;
-        for (int k = 0; k < (t >> 6); k++) pre = max(pre, S->red[k]);
-        out[t] = (int16_t)max(v, pre);
-        __syncthreads();
+        out[lane] = (int16_t)v;
+        wave_sync();
     }
     template <class F> __device__ __forceinline__ int scan_add_excl(F f, int16_t* out) {
-        const int t = threadIdx.x, lane = t & 63;
-        const int x = f(t);
+        const int x = f(lane);
         int v = x;
         #pragma unroll
         for (int o = 1; o < 64; o <<= 1) { const int u = __shfl_up(v, o, 64); if (lane >= o) v += u; }
-        if (lane == 63) S->red[t >> 6] = v;
-        __syncthreads();
-        int pre = 0, tot = 0;
-        #pragma unroll
-        for (int k = 0; k < CLY_NWAVE; k++) { if (k < (t >> 6)) pre += S->red[k]; tot += S->red[k]; }
-        out[t] = (int16_t)(pre + v - x);
-        __syncthreads();
-        return tot;
+        out[lane] = (int16_t)(v - x);
+        wave_sync();
+        return __shfl(v, 63, 64);
     }
 };
 
@@ -154,11 +149,11 @@ struct DevEnv {
     __device__ __forceinline__ void stage_lane(ScanShared& S, int t) {
         const int wl = S.C.win_len;
         if (wl == CLY_WIN) {
-            const int lane = t & 63, wv = t >> 6;
+            const int lane = t;
             const uint8_t* src = F.base + S.C.cbase;
             #pragma unroll
             for (int k = 0; k < (CLY_WIN / 16 + CLY_NT - 1) / CLY_NT; k++) {
-                const int slot0 = k * CLY_NT + wv * 64;
+                const int slot0 = k * CLY_NT;
                 if (slot0 + lane < CLY_WIN / 16)
                     __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)(slot0 + lane) * 16),
                                                      (__attribute__((address_space(3))) void*)((char*)S.win + slot0 * 16),
@@ -284,10 +279,6 @@ struct DevEnv {
                     i0 = run;
                 }
             }
-            S.lb_w[0][t] = w0; S.lb_w[1][t] = w1; S.lb_w[2][t] = w2; S.lb_w[3][t] = w3;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const int last = stop < 64 ? stop : 63;
             LBSTAT(st_slow += (last + 1 - i0));
             for (int i = i0; i <= last && r == 0; i++) {
@@ -296,10 +287,10 @@ struct DevEnv {
                     r = lb_apply_full_walk(w, 0, 0, 0, out) ? 1 : 2;
                     jf = -1;
                 } else {
-                    r = lb_walk_step(w, ji, S.lb_w[0][i], S.lb_w[1][i], S.lb_w[2][i], S.lb_w[3][i], epoch, out, jf);
+                    r = lb_walk_step(w, ji, __shfl(w0, i, 64), __shfl(w1, i, 64), __shfl(w2, i, 64),
+                                     __shfl(w3, i, 64), epoch, out, jf);
                 }
             }
-            __builtin_amdgcn_wave_barrier();
         }
         if (t != 0) return;
 #ifdef CLY_PHASE_PROF
@@ -333,49 +324,61 @@ struct DevEnv {
     __device__ __forceinline__ void summary(ScanShared& S) { write_summary(S, sums, x8n); }
 };
 
-__global__ void __launch_bounds__(CLY_NT)
+#ifndef CLY_WPB
+#define CLY_WPB 4                // waves (= chunks in flight) per workgroup
+#endif
+#define CLY_SCAN_LDS (CLY_TAB_WORDS * 4 + CLY_WPB * sizeof(ScanShared))
+
+// Persistent: every wave takes chunk tickets until none are left (tickets in
+// order, so a chunk only waits on chunks already taken by running waves).
+__global__ void __launch_bounds__(64 * CLY_WPB)
 k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ file_chunk_prefix, int nchunks,
        Desc* desc, ChunkSum* sums, const uint32_t* __restrict__ shift, const uint32_t* __restrict__ x8n,
        cly_tuple* out, uint64_t out_cap, Globals* g, ChunkDbg* dbg, int* trace, uint32_t epoch) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    ScanShared& S = *reinterpret_cast<ScanShared*>(smem_raw);
-    if (threadIdx.x == 0) {
-        const int c = (int)atomicAdd(&g->ticket, 1u);
+    uint32_t* tab = reinterpret_cast<uint32_t*>(smem_raw);
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) build_tab_lane(tab, i, 256);
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    ScanShared& S = reinterpret_cast<ScanShared*>(smem_raw + CLY_TAB_WORDS * 4)[wave];
+    DevExec ex{lane};
+    DevEnv env;
+    env.desc = desc; env.sums = sums; env.shift = shift; env.x8n = x8n;
+    env.out = out; env.out_cap = out_cap; env.g = g; env.nchunks = nchunks; env.dbg = dbg; env.trace = trace;
+    env.epoch = epoch;
+    env.lanes = trace ? trace + 2048 : nullptr;
+    for (;;) {
+        int c = 0;
+        if (lane == 0) c = (int)atomicAdd(&g->ticket, 1u);
+        c = __shfl(c, 0, 64);
+        if (c >= nchunks) break;
         int lo = 0, hi = nfiles - 1;
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
             if ((int)file_chunk_prefix[mid] <= c) lo = mid; else hi = mid - 1;
         }
-        S.C.chunk = c;
-        S.C.fidx = lo;
-    }
+        env.F = files[lo];
+        env.spins = 0;
+        if (lane == 0) {
 #ifdef CLY_PHASE_PROF
-    if (threadIdx.x == 0) S.tstamp[0] = __builtin_amdgcn_s_memtime();
+            S.tstamp[0] = __builtin_amdgcn_s_memtime();
 #endif
-    __syncthreads();
-    const int c = S.C.chunk;
-    if (c >= nchunks) return;
-    DevEnv env;
-    env.F = files[S.C.fidx];
-    env.desc = desc; env.sums = sums; env.shift = shift; env.x8n = x8n;
-    env.out = out; env.out_cap = out_cap; env.g = g; env.nchunks = nchunks; env.dbg = dbg; env.trace = trace;
-    env.epoch = epoch; env.spins = 0;
-    env.lanes = trace ? trace + 2048 : nullptr;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int cl = c - (int)env.F.first_chunk;
-        S.C.cbase = (int64_t)cl * CLY_CHUNK;
-        S.C.nrel = (int64_t)env.F.len - S.C.cbase;
-        S.C.dlen = (int)(S.C.nrel < CLY_CHUNK ? S.C.nrel : CLY_CHUNK);
-        S.C.win_len = (int)(S.C.nrel < CLY_WIN ? S.C.nrel : CLY_WIN);
-        S.C.fof = cl == 0;
-        S.C.lof = cl == (int)env.F.nchunks - 1;
-        S.C.fid = env.F.fid;
-        S.C.gfile = env.F.base;
+            const int cl = c - (int)env.F.first_chunk;
+            S.C.chunk = c;
+            S.C.fidx = lo;
+            S.C.cbase = (int64_t)cl * CLY_CHUNK;
+            S.C.nrel = (int64_t)env.F.len - S.C.cbase;
+            S.C.dlen = (int)(S.C.nrel < CLY_CHUNK ? S.C.nrel : CLY_CHUNK);
+            S.C.win_len = (int)(S.C.nrel < CLY_WIN ? S.C.nrel : CLY_WIN);
+            S.C.fof = cl == 0;
+            S.C.lof = cl == (int)env.F.nchunks - 1;
+            S.C.fid = env.F.fid;
+            S.C.gfile = env.F.base;
+            S.tab = tab;
+        }
+        wave_sync();
+        chunk_body(ex, S, env);
     }
-    __syncthreads();
-    DevExec ex{&S};
-    chunk_body(ex, S, env);
 }
 
 // One workgroup per file: first event of the file.
@@ -440,6 +443,7 @@ struct cly_ctx {
     ChunkDbg* d_dbg; int dbg_on; int last_nchunks;  // debug trace (cly_dbg_chunks)
     int* h_trace; int* d_trace;
     uint32_t epoch; int desc_fresh;
+    int scan_grid;
     uint8_t* d_bytes; uint64_t cap_bytes;          // host-path staging
     cly_tuple* d_tuples; uint64_t cap_tuples;
 };
@@ -478,8 +482,15 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     for (int n = 1; n <= CLY_CHUNK; n++) hx[n] = cly_multmodp(x8, hx[n - 1]);
     HIPCK(hipMemcpy(c->d_x8n, hx, x8_bytes, hipMemcpyHostToDevice));
     free(hx);
-    HIPCK(hipFuncSetAttribute((const void*)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sizeof(ScanShared)));
+    HIPCK(hipFuncSetAttribute((const void*)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CLY_SCAN_LDS));
+    // persistent grid: resident workgroups per CU x CUs
+    {
+        int per_cu = 0, ncu = 0;
+        HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_scan, 64 * CLY_WPB, CLY_SCAN_LDS));
+        HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+        if (per_cu < 1) per_cu = 1;
+        c->scan_grid = per_cu * ncu;
+    }
     *out = c;
     return CLY_OK;
 }
@@ -571,7 +582,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     }
     HIPCK(hipMemsetAsync(c->d_g, 0, sizeof(Globals), st));
     HIPCK(hipEventRecord(c->ev[0], st));
-    hipLaunchKernelGGL(k_scan, dim3(nchunks), dim3(CLY_NT), sizeof(ScanShared), st, c->d_files, nfiles, c->d_prefix,
+    hipLaunchKernelGGL(k_scan, dim3(c->scan_grid), dim3(64 * CLY_WPB), CLY_SCAN_LDS, st, c->d_files, nfiles, c->d_prefix,
                        nchunks, c->d_desc, c->d_sums, c->d_shift, c->d_x8n, d_out, out_cap, c->d_g,
                        c->dbg_on ? c->d_dbg : nullptr, c->dbg_on > 1 ? c->d_trace : nullptr, c->epoch);
     HIPCK(hipGetLastError());
@@ -697,6 +708,7 @@ extern "C" int cly_dbg_phases(cly_ctx* c, uint64_t* out) {
     return 18;
 }
 extern "C" int cly_dbg_sizes(int* out3) { out3[0] = sizeof(ChunkDbg); out3[1] = sizeof(ChunkSum); out3[2] = sizeof(ScanShared); return 0; }
+extern "C" int cly_dbg_grid(cly_ctx* c) { return c->scan_grid; }
 
 extern "C" const char* cly_strerror(int code) {
     switch (code) {
@@ -717,7 +729,7 @@ extern "C" const char* cly_strerror(int code) {
 
 extern "C" const char* cly_build_info(void) {
     static char buf[160];
-    snprintf(buf, sizeof(buf), "clyscan gfx950 NT=%d SUB=%d CHUNK=%d REP=%d LBWIN=%d", CLY_NT, CLY_SUB, CLY_CHUNK,
-             CLY_REP, CLY_LBWIN);
+    snprintf(buf, sizeof(buf), "clyscan gfx950 NT=%d SUB=%d CHUNK=%d REP=%d WPB=%d LDS=%d", CLY_NT, CLY_SUB, CLY_CHUNK,
+             CLY_REP, CLY_WPB, (int)CLY_SCAN_LDS);
     return buf;
 }

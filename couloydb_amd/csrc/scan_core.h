@@ -45,7 +45,7 @@
 // line (CLY_NOINL).
 
 #ifndef CLY_NT
-#define CLY_NT 256            // lanes per chunk (threads per workgroup)
+#define CLY_NT 64             // lanes per chunk: one wave processes one chunk
 #endif
 #ifndef CLY_SUB
 #define CLY_SUB 124           // bytes per lane stripe: 31 dwords (odd), so lane k's
@@ -59,7 +59,8 @@
 #define CLY_WIN (CLY_CHUNK + CLY_HALO)
 #define CLY_NWAVE (CLY_NT / 64)
 #define CLY_LBWIN 64          // look-back: descriptors read per round trip (one wave)
-static_assert(CLY_NT % 64 == 0 && CLY_NT <= 1024, "CLY_NT must be a multiple of 64");
+#define CLY_TAB_WORDS (4 * 256 * CLY_REP)
+static_assert(CLY_NT == 64, "one chunk per wave: CLY_NT is the wave width");
 static_assert(CLY_SUB % 4 == 0 && CLY_SUB >= 28, "CLY_SUB must be a multiple of 4");
 static_assert(CLY_CHUNK % 16 == 0 && CLY_WIN % 16 == 0, "16-B staging");
 static_assert(CLY_CHUNK <= 32767, "chunk-relative positions are int16");
@@ -165,9 +166,9 @@ CLY_DEV uint32_t crc_run(const CrcTab& T, uint32_t s, const uint8_t* w, int lo, 
     return s;
 }
 
-// Fill the slicing tables (lane t of NT builds entries t, t+NT, ...).
-CLY_DEV void build_tab_lane(uint32_t* tab, int t) {
-    for (int i = t; i < 256; i += CLY_NT) {
+// Fill the slicing tables (thread t of nthr builds entries t, t+nthr, ...).
+CLY_DEV void build_tab_lane(uint32_t* tab, int t, int nthr) {
+    for (int i = t; i < 256; i += nthr) {
         uint32_t c = i;
         for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ CLY_POLY : c >> 1;
         for (int tb = 0; tb < 4; tb++) {
@@ -217,7 +218,7 @@ struct ChainRes {
 
 struct ScanShared {
     uint32_t win[CLY_WIN / 4];                // chunk bytes (+ halo), zero past the file end
-    uint32_t tab[4 * 256 * CLY_REP];          // slicing-by-4 tables
+    const uint32_t* tab;                      // slicing-by-4 tables (shared by the workgroup)
     // speculation (entry independent)
     uint32_t sp_x[CLY_NT];                    // exit (rel) of the lane's speculative walk
     int16_t  sp_s[CLY_NT];                    // first record of the walk (rel), -1 none
@@ -237,10 +238,8 @@ struct ScanShared {
     uint32_t sc_v[2][CLY_NT];
     uint8_t  sc_c[2][CLY_NT];
     uint8_t  sc_c0[CLY_NT];                   // phase-A constness (kept through the scan)
-    // block reduction scratch
-    int32_t  red[CLY_NWAVE * 2];
-    // look-back window: words of 64 descriptors (GPU form of the walk)
-    uint64_t lb_w[4][64];
+
+
     // scalars
     ChunkCtx C;
     ChainRes R;
@@ -1029,7 +1028,7 @@ template <class EX, class Env>
 CLY_DEV void chunk_body(EX& ex, ScanShared& S, Env& env) {
     // ---- stage
     ex.one([&]() { S.fail = 0; env.mark(S, 1); });
-    ex.all([&](int t) { env.stage_lane(S, t); build_tab_lane(S.tab, t); env.stage_wait(); });
+    ex.all([&](int t) { env.stage_lane(S, t); env.stage_wait(); });
     // ---- speculation
     ex.all([&](int t) { spec_lane(S, t); });
     // ---- guess the entry: the first lane whose walk left through a checked

@@ -253,10 +253,13 @@ extern "C" int cly_scan(cly_ctx* ctx, const cly_file* files, int nfiles, cly_tup
         pool.emplace_back([&R, &ticket, k]() {
             std::mt19937 rng(1234u + (unsigned)k);
             ScanShared* S = (ScanShared*)aligned_alloc(64, (sizeof(ScanShared) + 63) & ~size_t(63));
+            std::vector<uint32_t> tab(CLY_TAB_WORDS);
+            for (int t = 0; t < 256; t++) build_tab_lane(tab.data(), t, 256);
             for (;;) {
                 const int c = ticket.fetch_add(1);
                 if (c >= R.nchunks) break;
                 memset(S, 0xA5, sizeof(ScanShared));     // stale LDS contents
+                S->tab = tab.data();
                 run_chunk(R, c, *S, rng);
             }
             free(S);
