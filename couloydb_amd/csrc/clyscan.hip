@@ -124,20 +124,20 @@ struct DevEnv {
     uint32_t epoch;              // call epoch tagging every descriptor word
     uint32_t spins;
 
-    __device__ __forceinline__ void mark(ScanShared& S, int v) {
+    __device__ __forceinline__ void mark(CLY_LDS ScanShared& S, int v) {
 #ifdef CLY_PHASE_PROF
         S.tstamp[v] = __builtin_amdgcn_s_memtime();
         if (v == 8)
             for (int k = 1; k <= 8; k++) {
                 const int pk = k == 5 ? 3 : k - 1;       // no stamp 4
-                if (k != 4) atomicAdd((unsigned long long*)&g->phase[k], (unsigned long long)(S.tstamp[k] - S.tstamp[pk]));
+                if (k != 4) S.pacc[k] += S.tstamp[k] - S.tstamp[pk];
             }
 #endif
         if (trace) { trace[2 * (S.C.chunk & 1023)] = v; trace[2 * (S.C.chunk & 1023) + 1] = S.C.chunk; __threadfence_system(); }
     }
-    __device__ __forceinline__ void report_fail(ScanShared& S) { atomicMax(&g->fail, (uint32_t)S.fail); }
+    __device__ __forceinline__ void report_fail(CLY_LDS ScanShared& S) { atomicMax(&g->fail, (uint32_t)S.fail); }
     int* lanes;                  // debug: per-lane trace of the first chunks
-    __device__ __forceinline__ void dbg_lane(ScanShared& S, int t) {
+    __device__ __forceinline__ void dbg_lane(CLY_LDS ScanShared& S, int t) {
         if (lanes && S.C.chunk < 4) dbg_lane_fill(S, t, lanes + (S.C.chunk * CLY_NT + t) * 8);
     }
 
@@ -146,7 +146,7 @@ struct DevEnv {
     // (global_load_lds_dwordx4: 1 KiB per wave instruction, all in flight at
     // once, no register staging); the last chunk of a file (window cut by the
     // file end) is staged through registers with a zero-filled tail.
-    __device__ __forceinline__ void stage_lane(ScanShared& S, int t) {
+    __device__ __forceinline__ void stage_lane(CLY_LDS ScanShared& S, int t) {
         const int wl = S.C.win_len;
         if (wl == CLY_WIN) {
             const int lane = t;
@@ -156,12 +156,12 @@ struct DevEnv {
                 const int slot0 = k * CLY_NT;
                 if (slot0 + lane < CLY_WIN / 16)
                     __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)(slot0 + lane) * 16),
-                                                     (__attribute__((address_space(3))) void*)((char*)S.win + slot0 * 16),
+                                                     (CLY_LDS void*)((CLY_LDS char*)S.win + slot0 * 16),
                                                      16, 0, 0);
             }
             return;
         }
-        uint4* w4 = reinterpret_cast<uint4*>(S.win);
+        CLY_LDS uint4* w4 = (CLY_LDS uint4*)(S.win);
         const int nvec = wl >> 4;
         const uint4* src = reinterpret_cast<const uint4*>(F.base + S.C.cbase);
         uint4 v[(CLY_WIN / 16 + CLY_NT - 1) / CLY_NT];
@@ -205,7 +205,7 @@ struct DevEnv {
     __device__ __forceinline__ bool spin_ok() const { return spins <= LB_SPIN_MAX; }
     // Decoupled look-back by wave 0: 64 descriptors per round trip into LDS,
     // then every lane folds them in order (uniform; scan_core.h lb_walk_step).
-    __device__ void lookback(ScanShared& S, int t) {
+    __device__ void lookback(CLY_LDS ScanShared& S, int t) {
         if (t >= 64) return;
         const int64_t c = S.C.chunk;
         LbWalk w;
@@ -294,10 +294,8 @@ struct DevEnv {
         }
         if (t != 0) return;
 #ifdef CLY_PHASE_PROF
-        atomicAdd((unsigned long long*)&g->lbstat[0], (unsigned long long)st_win);
-        atomicAdd((unsigned long long*)&g->lbstat[1], (unsigned long long)st_spin);
-        atomicAdd((unsigned long long*)&g->lbstat[2], (unsigned long long)st_slow);
-        if (ok && r == 2) atomicAdd((unsigned long long*)&g->lbstat[3], 1ull);
+        S.lacc[0] += st_win; S.lacc[1] += st_spin; S.lacc[2] += st_slow;
+        if (ok && r == 2) S.lacc[3] += 1;
 #endif
         if (ok && r == 2) {
             if (jf == -3) {
@@ -315,13 +313,13 @@ struct DevEnv {
         S.p_excl = out.P;
         S.in_dead = out.dead;
     }
-    template <class EX> __device__ __forceinline__ void crc(EX& ex, ScanShared& S) { crc_phase(ex, S, shift); }
-    __device__ __forceinline__ void emit_lane(ScanShared& S, int t) {
+    template <class EX> __device__ __forceinline__ void crc(EX& ex, CLY_LDS ScanShared& S) { crc_phase(ex, S, shift); }
+    __device__ __forceinline__ void emit_lane(CLY_LDS ScanShared& S, int t) {
         unsigned of = 0;
         ::emit_lane(S, t, out, out_cap, &of);
         if (of) atomicOr(&g->overflow, 1u);
     }
-    __device__ __forceinline__ void summary(ScanShared& S) { write_summary(S, sums, x8n); }
+    __device__ __forceinline__ void summary(CLY_LDS ScanShared& S) { write_summary(S, sums, x8n); }
 };
 
 #ifndef CLY_WPB
@@ -336,17 +334,20 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
        Desc* desc, ChunkSum* sums, const uint32_t* __restrict__ shift, const uint32_t* __restrict__ x8n,
        cly_tuple* out, uint64_t out_cap, Globals* g, ChunkDbg* dbg, int* trace, uint32_t epoch) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    uint32_t* tab = reinterpret_cast<uint32_t*>(smem_raw);
+    CLY_LDS uint32_t* tab = (CLY_LDS uint32_t*)(smem_raw);
     for (int i = threadIdx.x; i < 256; i += blockDim.x) build_tab_lane(tab, i, 256);
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    ScanShared& S = reinterpret_cast<ScanShared*>(smem_raw + CLY_TAB_WORDS * 4)[wave];
+    CLY_LDS ScanShared& S = ((CLY_LDS ScanShared*)(smem_raw + CLY_TAB_WORDS * 4))[wave];
     DevExec ex{lane};
     DevEnv env;
     env.desc = desc; env.sums = sums; env.shift = shift; env.x8n = x8n;
     env.out = out; env.out_cap = out_cap; env.g = g; env.nchunks = nchunks; env.dbg = dbg; env.trace = trace;
     env.epoch = epoch;
     env.lanes = trace ? trace + 2048 : nullptr;
+#ifdef CLY_PHASE_PROF
+    if (lane == 0) { for (int k = 0; k < 10; k++) S.pacc[k] = 0; for (int k = 0; k < 4; k++) S.lacc[k] = 0; }
+#endif
     for (;;) {
         int c = 0;
         if (lane == 0) c = (int)atomicAdd(&g->ticket, 1u);
@@ -379,6 +380,12 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         wave_sync();
         chunk_body(ex, S, env);
     }
+#ifdef CLY_PHASE_PROF
+    if (lane == 0) {
+        for (int k = 0; k < 10; k++) atomicAdd((unsigned long long*)&g->phase[k], (unsigned long long)S.pacc[k]);
+        for (int k = 0; k < 4; k++) atomicAdd((unsigned long long*)&g->lbstat[k], (unsigned long long)S.lacc[k]);
+    }
+#endif
 }
 
 // One workgroup per file: first event of the file.

@@ -38,6 +38,14 @@
 #define CLY_MEM inline
 #define CLY_NOINL static
 #endif
+// LDS address space on the device pass: keeps every access to the chunk's
+// shared state a ds_* instruction (a generic pointer would compile to flat_*
+// loads in the out-of-line lane routines).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define CLY_LDS __attribute__((address_space(3)))
+#else
+#define CLY_LDS
+#endif
 // Codegen note (ROCm 7.2, gfx950): values computed inside a lane-divergent
 // loop with several exits and used after it were observed clobbered by the
 // register allocator in this (large) kernel.  Lane routines therefore store
@@ -70,7 +78,8 @@ static_assert(CLY_CHUNK <= 32767, "chunk-relative positions are int16");
 // ---------------------------------------------------------------------------
 // Go encoding/binary Varint (toolchain >= 1.18, go.mod:3): zigzag over Uvarint;
 // overflow (10th byte > 1, or an 11th byte) -> (0, -(i+1)); short buffer -> (0, 0).
-CLY_DEV int64_t go_varint(const uint8_t* b, int64_t len, int& n) {
+template <class BP>
+CLY_DEV int64_t go_varint(BP b, int64_t len, int& n) {
     uint64_t x = 0;
     unsigned s = 0;
     const int lim = len < 11 ? (int)len : 11;
@@ -104,7 +113,8 @@ struct Hdr {
 // ReadLogRecord's header/bounds semantics at window position p, without the
 // CRC comparison.  nrel = bytes from the window start to the end of the file;
 // p_abs = file offset of p.  data/dataFile.go:64-103, data/logRecord.go:86-114.
-CLY_DEV Hdr step_hdr(const uint8_t* w, int64_t p, int64_t nrel, int64_t p_abs) {
+template <class BP>
+CLY_DEV Hdr step_hdr(BP w, int64_t p, int64_t nrel, int64_t p_abs) {
     Hdr h;
     h.status = 0; h.hsz = 0; h.size = 0; h.exp = 0; h.ks = 0; h.vs = 0; h.crc = 0; h.type = 0; h.dt = 0;
     h.good = false;
@@ -112,7 +122,7 @@ CLY_DEV Hdr step_hdr(const uint8_t* w, int64_t p, int64_t nrel, int64_t p_abs) {
     if (m > 26) m = 26;
     if (m <= 4) { h.status = CLY_END_EOF; return h; }       // logRecord.go:87-89
     if (m == 5) { h.status = CLY_ERR_TRUNC5; return h; }    // buf[5] index panic
-    const uint8_t* b = w + p;
+    const BP b = w + p;
     h.crc = (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
     h.type = b[4];
     h.dt = b[5];
@@ -139,7 +149,8 @@ CLY_DEV Hdr step_hdr(const uint8_t* w, int64_t p, int64_t nrel, int64_t p_abs) {
     return h;
 }
 
-CLY_DEV uint32_t le32(const uint8_t* b) {
+template <class BP>
+CLY_DEV uint32_t le32(BP b) {
     return (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
 }
 
@@ -147,7 +158,7 @@ CLY_DEV uint32_t le32(const uint8_t* b) {
 // CRC on LDS bytes: slicing-by-4 tables T0..T3, replicated CLY_REP times
 // (entry i of table t, replica r at dword (t*256 + i)*CLY_REP + r).
 struct CrcTab {
-    const uint32_t* t;
+    const CLY_LDS uint32_t* t;
     int r;
     CLY_MEM uint32_t at(int tab, uint32_t i) const { return t[((tab << 8) + (int)i) * CLY_REP + r]; }
     CLY_MEM uint32_t byte(uint32_t s, uint32_t b) const { return at(0, (s ^ b) & 0xff) ^ (s >> 8); }
@@ -158,16 +169,17 @@ struct CrcTab {
 };
 
 // Register s advanced over window bytes [lo, hi).
-CLY_DEV uint32_t crc_run(const CrcTab& T, uint32_t s, const uint8_t* w, int lo, int hi) {
+CLY_DEV uint32_t crc_run(const CrcTab& T, uint32_t s, const CLY_LDS uint8_t* w, int lo, int hi) {
     while (lo < hi && (lo & 3)) { s = T.byte(s, w[lo]); lo++; }
-    const uint32_t* w32 = (const uint32_t*)w;
+    const CLY_LDS uint32_t* w32 = (const CLY_LDS uint32_t*)w;
     while (hi - lo >= 4) { s = T.word(s, w32[lo >> 2]); lo += 4; }
     while (lo < hi) { s = T.byte(s, w[lo]); lo++; }
     return s;
 }
 
 // Fill the slicing tables (thread t of nthr builds entries t, t+nthr, ...).
-CLY_DEV void build_tab_lane(uint32_t* tab, int t, int nthr) {
+template <class TP>
+CLY_DEV void build_tab_lane(TP tab, int t, int nthr) {
     for (int i = t; i < 256; i += nthr) {
         uint32_t c = i;
         for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ CLY_POLY : c >> 1;
@@ -218,7 +230,7 @@ struct ChainRes {
 
 struct ScanShared {
     uint32_t win[CLY_WIN / 4];                // chunk bytes (+ halo), zero past the file end
-    const uint32_t* tab;                      // slicing-by-4 tables (shared by the workgroup)
+    const CLY_LDS uint32_t* tab;              // slicing-by-4 tables (shared by the workgroup)
     // speculation (entry independent)
     uint32_t sp_x[CLY_NT];                    // exit (rel) of the lane's speculative walk
     int16_t  sp_s[CLY_NT];                    // first record of the walk (rel), -1 none
@@ -256,6 +268,8 @@ struct ScanShared {
 
 #ifdef CLY_PHASE_PROF
     uint64_t tstamp[10];                      // profiling build: per-phase clock stamps
+    uint64_t pacc[10];                        //   summed per wave, flushed at kernel exit
+    uint64_t lacc[4];
 #endif
     int32_t  fail;                            // internal invariant violated (reported as a device error)
     int32_t  fail_k;
@@ -547,7 +561,7 @@ CLY_DEV int ctz32(uint32_t v) {
 
 // First q in [q0, b) whose bytes q+4, q+5 are <= 4 and q+6 is nonzero and even
 // (word-parallel filter over the LDS window); b if none.
-CLY_DEV int next_candidate(const uint32_t* w32, int q0, int b) {
+CLY_DEV int next_candidate(const CLY_LDS uint32_t* w32, int q0, int b) {
     int i = (q0 + 4) >> 2;                 // word holding byte q0+4
     uint32_t Li = swar_le4(w32[i]), Ki = swar_ks(w32[i]);
     for (;;) {
@@ -567,9 +581,9 @@ CLY_DEV int next_candidate(const uint32_t* w32, int q0, int b) {
     }
 }
 
-CLY_NOINL void spec_lane(ScanShared& S, int t) {
-    const ChunkCtx& C = S.C;
-    const uint8_t* w = reinterpret_cast<const uint8_t*>(S.win);
+CLY_NOINL void spec_lane(CLY_LDS ScanShared& S, int t) {
+    const CLY_LDS ChunkCtx& C = S.C;
+    const CLY_LDS uint8_t* w = (const CLY_LDS uint8_t*)(S.win);
     S.sp_s[t] = -1; S.sp_last[t] = -1; S.sp_cnt[t] = 0; S.sp_vin[t] = 0; S.sp_x[t] = 0;
     const int a = t * CLY_SUB;
     if (a >= C.dlen) return;
@@ -616,9 +630,9 @@ CLY_NOINL void spec_lane(ScanShared& S, int t) {
 
 // Exact walk (ReadLogRecord semantics, any record or terminal) of stripe k
 // from position e.
-CLY_NOINL void exact_walk(ScanShared& S, int k, int e) {
-    const ChunkCtx& C = S.C;
-    const uint8_t* w = reinterpret_cast<const uint8_t*>(S.win);
+CLY_NOINL void exact_walk(CLY_LDS ScanShared& S, int k, int e) {
+    const CLY_LDS ChunkCtx& C = S.C;
+    const CLY_LDS uint8_t* w = (const CLY_LDS uint8_t*)(S.win);
     const int a = k * CLY_SUB;
     const int b = a + CLY_SUB < C.dlen ? a + CLY_SUB : C.dlen;
     (void)a;
@@ -648,14 +662,14 @@ CLY_NOINL void exact_walk(ScanShared& S, int k, int e) {
 // resolve(E): the chunk's record chain from entry E (chunk-relative, < dlen or
 // >= dlen for "no lane").  Fills ws/wc/wl/wx/wterm/pk/base and S.R.
 template <class EX>
-CLY_DEV void resolve(EX& ex, ScanShared& S, int E) {
+CLY_DEV void resolve(EX& ex, CLY_LDS ScanShared& S, int E) {
     const int dlen = S.C.dlen;
     if (E >= dlen) {
         // only in the file's last chunk: E is the end of the file (ReadLogRecord there: io.EOF)
         ex.all([&](int t) { S.ws[t] = -1; S.wterm[t] = 0; S.pk[t] = -1; S.base[t] = 0; });
         ex.one([&]() {
-            const uint8_t* w = reinterpret_cast<const uint8_t*>(S.win);
-            ChainRes& R = S.R;
+            const CLY_LDS uint8_t* w = (const CLY_LDS uint8_t*)(S.win);
+            CLY_LDS ChainRes& R = S.R;
             R.E = E; R.k0 = CLY_NT; R.cnt = 0; R.last = -1; R.lterm = CLY_NT; R.xrel = E;
             R.tpos = E; R.eof_exit = 0;
             const Hdr h = step_hdr(w, E, S.C.nrel, S.C.cbase + E);
@@ -704,7 +718,7 @@ CLY_DEV void resolve(EX& ex, ScanShared& S, int E) {
     }
     const int total = ex.scan_add_excl([&](int t) -> int { return S.ws[t] >= 0 ? (int)S.wc[t] : 0; }, S.base);
     ex.one([&]() {
-        ChainRes& R = S.R;
+        CLY_LDS ChainRes& R = S.R;
         const int L = S.pk[CLY_NT - 1];
         R.E = E; R.k0 = k0; R.cnt = total;
         R.term = S.wterm[L]; R.tst = S.wtst[L];
@@ -727,7 +741,7 @@ CLY_DEV void resolve(EX& ex, ScanShared& S, int E) {
 //   (element (c, v): S -> c ? v : A^SUB S ^ v), phase B (heads that need the
 //   register entering the stripe).  Sets S.bad, S.head_raw, S.end_state.
 #define OPN_HEAD (-2)
-CLY_DEV void note_bad(ScanShared& S, unsigned long long key) {
+CLY_DEV void note_bad(CLY_LDS ScanShared& S, unsigned long long key) {
 #ifdef __HIPCC__
     atomicMin(&S.bad, key);
 #else
@@ -737,11 +751,11 @@ CLY_DEV void note_bad(ScanShared& S, unsigned long long key) {
 
 // Phase A of lane t: registers of the record pieces inside the stripe; writes
 // the scan element (sc_v[0][t], sc_c[0][t]).
-CLY_NOINL void crc_lane_a(ScanShared& S, int t) {
+CLY_NOINL void crc_lane_a(CLY_LDS ScanShared& S, int t) {
     const int dlen = S.C.dlen;
     const int mode = S.mode;
-    const ChainRes& R = S.R;
-    const uint8_t* w = reinterpret_cast<const uint8_t*>(S.win);
+    const CLY_LDS ChainRes& R = S.R;
+    const CLY_LDS uint8_t* w = (const CLY_LDS uint8_t*)(S.win);
     CrcTab T{S.tab, t % CLY_REP};
     const int a = t * CLY_SUB;
     const int b = a + CLY_SUB < dlen ? a + CLY_SUB : dlen;
@@ -807,11 +821,11 @@ CLY_NOINL void crc_lane_a(ScanShared& S, int t) {
 }
 
 // Phase B of lane t (after the scan; sc_v[fin] holds the inclusive scan).
-CLY_NOINL void crc_lane_b(ScanShared& S, int t, int fin) {
+CLY_NOINL void crc_lane_b(CLY_LDS ScanShared& S, int t, int fin) {
     const int dlen = S.C.dlen;
     const int mode = S.mode;
-    const ChainRes& R = S.R;
-    const uint8_t* w = reinterpret_cast<const uint8_t*>(S.win);
+    const CLY_LDS ChainRes& R = S.R;
+    const CLY_LDS uint8_t* w = (const CLY_LDS uint8_t*)(S.win);
     CrcTab T{S.tab, t % CLY_REP};
     const int a = t * CLY_SUB;
     const int b = a + CLY_SUB < dlen ? a + CLY_SUB : dlen;
@@ -843,7 +857,7 @@ CLY_NOINL void crc_lane_b(ScanShared& S, int t, int fin) {
 // segmented Kogge-Stone scan over lanes (element (c, v): S -> c ? v :
 // A^SUB S ^ v), phase B.  Sets S.bad, S.head_raw, S.end_state.
 template <class EX>
-CLY_DEV void crc_phase(EX& ex, ScanShared& S, const uint32_t* shift_tabs) {
+CLY_DEV void crc_phase(EX& ex, CLY_LDS ScanShared& S, const uint32_t* shift_tabs) {
     ex.one([&]() { S.bad = ~0ull; S.head_raw = 0; S.end_state = 0; });
     ex.all([&](int t) { crc_lane_a(S, t); });
     // levels stop once every element is constant (records shorter than a few
@@ -870,9 +884,9 @@ CLY_DEV void crc_phase(EX& ex, ScanShared& S, const uint32_t* shift_tabs) {
 }
 
 // Tuples for the records starting in lane t's stripe.
-CLY_NOINL void emit_lane(ScanShared& S, int t, cly_tuple* out, uint64_t out_cap, unsigned* overflow) {
+CLY_NOINL void emit_lane(CLY_LDS ScanShared& S, int t, cly_tuple* out, uint64_t out_cap, unsigned* overflow) {
     if (S.mode != MODE_NORMAL || S.ws[t] < 0) return;
-    const uint8_t* w = reinterpret_cast<const uint8_t*>(S.win);
+    const CLY_LDS uint8_t* w = (const CLY_LDS uint8_t*)(S.win);
     const int n = S.wc[t];
     uint64_t idx = S.p_excl + (uint64_t)S.base[t];
     int64_t p = S.ws[t];
@@ -905,9 +919,9 @@ CLY_NOINL void emit_lane(ScanShared& S, int t, cly_tuple* out, uint64_t out_cap,
 
 // Chunk summary for k_fin (one lane).
 // x8n[n] = x^(8n) mod P for n in [0, CLY_CHUNK] (host-built table).
-CLY_DEV void write_summary(ScanShared& S, ChunkSum* sums, const uint32_t* x8n) {
-    const ChunkCtx& C = S.C;
-    const uint8_t* w = reinterpret_cast<const uint8_t*>(S.win);
+CLY_DEV void write_summary(CLY_LDS ScanShared& S, ChunkSum* sums, const uint32_t* x8n) {
+    const CLY_LDS ChunkCtx& C = S.C;
+    const CLY_LDS uint8_t* w = (const CLY_LDS uint8_t*)(S.win);
     ChunkSum cs;
     cs.p_excl = S.p_excl;
     cs.evt_off = EVT_NONE;
@@ -934,7 +948,7 @@ CLY_DEV void write_summary(ScanShared& S, ChunkSum* sums, const uint32_t* x8n) {
             cs.evt_status = CLY_END_EOF;
         }
     } else {
-        const ChainRes& R = S.R;
+        const CLY_LDS ChainRes& R = S.R;
         cs.cnt = (uint32_t)R.cnt;
         cs.flags |= SUM_CLOSES;
         cs.head_len = (uint32_t)(R.E < C.dlen ? R.E : C.dlen);
@@ -1016,7 +1030,7 @@ struct ChunkDbg {
 };
 
 // Per-lane trace (debug builds of the trace only; 8 ints per lane).
-CLY_DEV void dbg_lane_fill(const ScanShared& S, int t, int* o) {
+CLY_DEV void dbg_lane_fill(const CLY_LDS ScanShared& S, int t, int* o) {
     o[0] = S.sp_s[t]; o[1] = (int)S.sp_x[t]; o[2] = S.sp_cnt[t]; o[3] = S.ws[t];
     o[4] = (int)S.wx[t]; o[5] = S.wc[t]; o[6] = S.pk[t]; o[7] = S.base[t] | (S.wterm[t] << 16) | (S.fail_k << 20);
 }
@@ -1025,7 +1039,7 @@ CLY_DEV void dbg_lane_fill(const ScanShared& S, int t, int* o) {
 // The chunk pipeline, common to kernel and emulator.  Env supplies the global
 // memory side: publish/lookback of descriptors, ticket, file table.
 template <class EX, class Env>
-CLY_DEV void chunk_body(EX& ex, ScanShared& S, Env& env) {
+CLY_DEV void chunk_body(EX& ex, CLY_LDS ScanShared& S, Env& env) {
     // ---- stage
     ex.one([&]() { S.fail = 0; env.mark(S, 1); });
     ex.all([&](int t) { env.stage_lane(S, t); env.stage_wait(); });
@@ -1052,7 +1066,7 @@ CLY_DEV void chunk_body(EX& ex, ScanShared& S, Env& env) {
     // ---- publish the speculative descriptor
     const int64_t cg = (int64_t)S.C.chunk * CLY_CHUNK;
     ex.one([&]() {
-        const ChainRes& R = S.R;
+        const CLY_LDS ChainRes& R = S.R;
         const uint32_t ep = env.epoch;
         if (S.guess >= 0)
             env.publish_spec(S.C.chunk, ds_pack(ep, DS_SPEC, S.C.fof, R.term, 1, S.guess, (uint32_t)R.cnt),
@@ -1082,7 +1096,7 @@ CLY_DEV void chunk_body(EX& ex, ScanShared& S, Env& env) {
     }
     // ---- publish the resolved descriptor
     ex.one([&]() {
-        const ChainRes& R = S.R;
+        const CLY_LDS ChainRes& R = S.R;
         uint64_t X;
         int dead;
         uint32_t cnt = 0;
