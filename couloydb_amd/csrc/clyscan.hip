@@ -128,10 +128,7 @@ struct DevEnv {
 #ifdef CLY_PHASE_PROF
         S.tstamp[v] = __builtin_amdgcn_s_memtime();
         if (v == 8)
-            for (int k = 1; k <= 8; k++) {
-                const int pk = k == 5 ? 3 : k - 1;       // no stamp 4
-                if (k != 4) S.pacc[k] += S.tstamp[k] - S.tstamp[pk];
-            }
+            for (int k = 1; k <= 8; k++) S.pacc[k] += S.tstamp[k] - S.tstamp[k - 1];
 #endif
         if (trace) { trace[2 * (S.C.chunk & 1023)] = v; trace[2 * (S.C.chunk & 1023) + 1] = S.C.chunk; __threadfence_system(); }
     }
@@ -234,10 +231,13 @@ struct DevEnv {
             for (;;) {
                 bool ready = true, full = false;
                 if (j >= 0) {
+                    // all four words in one round trip (w0 last: words written
+                    // before it are complete when it shows their state)
+                    w1 = ld(j, 1); w2 = ld(j, 2); w3 = ld(j, 3);
                     w0 = ld(j, 0);
                     const uint64_t st = ds_state(w0, epoch);
-                    if (st == DS_SPEC) { w1 = ld(j, 1); ready = ds_ok(w1, epoch); }
-                    else if (st == DS_FULL) { w2 = ld(j, 2); w3 = ld(j, 3); ready = ds_ok(w2, epoch) && ds_ok(w3, epoch); full = ready; }
+                    if (st == DS_SPEC) ready = ds_ok(w1, epoch);
+                    else if (st == DS_FULL) { ready = ds_ok(w2, epoch) && ds_ok(w3, epoch); full = ready; }
                     else ready = false;
                 }
                 const unsigned long long endm = __ballot(full || j < 0);

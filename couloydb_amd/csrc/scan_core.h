@@ -1075,6 +1075,9 @@ CLY_DEV void chunk_body(EX& ex, CLY_LDS ScanShared& S, Env& env) {
             env.publish_spec(S.C.chunk, ds_pack(ep, DS_SPEC, S.C.fof, 0, 0, 0, 0), ds_tag(ep, 0));
         env.mark(S, 3);
     });
+    // ---- CRC under the guessed chain (overlaps the wait for predecessors)
+    env.crc(ex, S);
+    ex.one([&]() { env.mark(S, 4); });
     // ---- look-back: true entry and output slot
     ex.all([&](int t) { env.lookback(S, t); });
     ex.one([&]() {
@@ -1082,16 +1085,20 @@ CLY_DEV void chunk_body(EX& ex, CLY_LDS ScanShared& S, Env& env) {
         if (!S.in_dead && S.entry_g < cg) { S.fail = 2; S.in_dead = 1; }   // cannot happen
         env.mark(S, 5);
     });
-    // ---- the true chain (re-resolved when the guess was wrong)
+    // ---- the true chain (re-resolved, and its CRC redone, when the guess was wrong)
     if (S.in_dead) {
         ex.one([&]() { S.mode = MODE_DEAD; S.R.cnt = 0; S.R.term = 1; });
     } else if (S.entry_g >= cg + CLY_CHUNK) {
-        ex.one([&]() { S.mode = MODE_PASS; S.R.cnt = 0; S.R.term = 0; });
+        if (S.mode != MODE_PASS) {
+            ex.one([&]() { S.mode = MODE_PASS; S.R.cnt = 0; S.R.term = 0; });
+            env.crc(ex, S);
+        }
     } else {
         const int newE = (int)(S.entry_g - cg);
         if (S.mode != MODE_NORMAL || S.guess != newE) {
             ex.one([&]() { S.mode = MODE_NORMAL; });
             resolve(ex, S, newE);
+            env.crc(ex, S);
         }
     }
     // ---- publish the resolved descriptor
@@ -1108,8 +1115,7 @@ CLY_DEV void chunk_body(EX& ex, CLY_LDS ScanShared& S, Env& env) {
                          ds_tag(ep, S.p_excl + cnt), S.p_excl + cnt);
         env.mark(S, 6);
     });
-    // ---- CRC, tuples, summary
-    if (S.mode != MODE_DEAD) env.crc(ex, S);
+    // ---- tuples, summary
     ex.all([&](int t) { env.emit_lane(S, t); });
     ex.one([&]() {
         env.mark(S, 7);

@@ -14,8 +14,8 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
 wl = make_workload(cfg, torch)
 sc = Scanner(0, lib="libclyscan_prof.so")
 sc.lib.cly_dbg_phases.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-names = {1: "ticket+setup", 2: "stage+tables+spec+guess", 3: "resolve+publish SPEC", 5: "look-back",
-         6: "re-resolve+publish FULL", 7: "CRC+emit", 8: "summary"}
+names = {1: "ticket+setup", 2: "stage+spec+guess", 3: "resolve+publish SPEC", 4: "CRC (guessed chain)",
+         5: "look-back", 6: "redo+publish FULL", 7: "emit", 8: "summary"}
 for it in range(3):
     first, res, st, need = sc.scan_device(wl.dev_files, wl.d_out.data_ptr(), wl.out_cap)
     ph = (ctypes.c_uint64 * 18)()
