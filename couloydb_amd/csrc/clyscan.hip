@@ -44,6 +44,8 @@ struct Globals {                 // zeroed per call
     uint64_t total;              // tuple slots used (records + any past an ErrInvalidCRC)
     uint64_t phase[10];          // profiling build: summed clock cycles per chunk phase
     uint64_t lbstat[8];          // profiling build: look-back windows, spins, slow steps, fallbacks, distance
+    uint32_t nfb, _pad2;
+    int64_t  fb[32][6];          // profiling build: first fallbacks (c, jf, req, e0, X, state)
 };
 
 struct FileOut {
@@ -272,6 +274,18 @@ struct DevEnv {
                     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
                     const uint64_t w0l = __shfl(w0, run - 1, 64);
                     const uint64_t x0 = __shfl(w1, 0, 64);
+                    // summary just before folding the run's last chunk (recovery)
+                    if (run >= 2) {
+                        const uint64_t w0p = __shfl(w0, run - 2, 64);
+                        w.prev = static_cast<const LbSum&>(w);
+                        if (w.prev.res == LB_RES_IDENT) { w.prev.res = LB_RES_CONST; w.prev.rx = (int64_t)(x0 & DS_VAL_MASK); }
+                        w.prev.dp += cnt - ds_cnt(w0l);
+                        w.prev.req = LB_REQ_EXACT;
+                        w.prev.e0 = (base - (run - 2)) * (int64_t)CLY_CHUNK + ds_grel(w0p);
+                    } else {
+                        w.prev = static_cast<const LbSum&>(w);
+                    }
+                    w.kreq = base - (run - 1);
                     if (w.res == LB_RES_IDENT) { w.res = LB_RES_CONST; w.rx = (int64_t)(x0 & DS_VAL_MASK); }
                     w.dp += cnt;
                     w.req = LB_REQ_EXACT;
@@ -297,6 +311,17 @@ struct DevEnv {
         S.lacc[0] += st_win; S.lacc[1] += st_spin; S.lacc[2] += st_slow;
         if (ok && r == 2) S.lacc[3] += 1;
 #endif
+#ifdef CLY_PHASE_PROF
+        if (ok && r == 2) {
+            const uint32_t k = atomicAdd(&g->nfb, 1u);
+            if (k < 32) {
+                g->fb[k][0] = c; g->fb[k][1] = jf; g->fb[k][2] = w.req; g->fb[k][3] = w.e0;
+                g->fb[k][4] = jf >= 0 ? (int64_t)(ld(jf, 2) & DS_VAL_MASK) : -1;
+                g->fb[k][5] = jf >= 0 ? (int64_t)ld(jf, 0) : -1;
+            }
+        }
+#endif
+        if (ok && r == 2 && lb_recover_kreq(*this, w, epoch, out)) r = 1;
         if (ok && r == 2) {
             if (jf == -3) {
                 // nearest FULL before the chunk where the walk failed
@@ -712,7 +737,9 @@ extern "C" int cly_dbg_chunks(cly_ctx* c, void* dbg_out, void* sums_out, int max
 extern "C" int cly_dbg_phases(cly_ctx* c, uint64_t* out) {
     for (int k = 0; k < 10; k++) out[k] = c->h_g->phase[k];
     for (int k = 0; k < 8; k++) out[10 + k] = c->h_g->lbstat[k];
-    return 18;
+    out[18] = c->h_g->nfb;
+    for (int k = 0; k < 32; k++) for (int m = 0; m < 6; m++) out[19 + k * 6 + m] = (uint64_t)c->h_g->fb[k][m];
+    return 19 + 32 * 6;
 }
 extern "C" int cly_dbg_sizes(int* out3) { out3[0] = sizeof(ChunkDbg); out3[1] = sizeof(ChunkSum); out3[2] = sizeof(ScanShared); return 0; }
 extern "C" int cly_dbg_grid(cly_ctx* c) { return c->scan_grid; }

@@ -273,6 +273,7 @@ struct ScanShared {
 #endif
     int32_t  fail;                            // internal invariant violated (reported as a device error)
     int32_t  fail_k;
+    int32_t  redo_crc;                        // the guessed chain was wrong: CRC again
 };
 
 #define MODE_NORMAL 0     // the chain enters (or ends) inside the chunk: R is valid
@@ -385,19 +386,29 @@ CLY_DEV bool lb_compose_spec(LbState& s, int64_t j, uint64_t w0, uint64_t x) {
 #define LB_RES_IDENT 0
 #define LB_RES_CONST 1
 #define LB_RES_DEAD 2
-struct LbWalk {
+struct LbSum {
     int64_t  e0, rx, cE;
     uint64_t dp, dp_fixed;
     int32_t  req, res, fixed, cdead;
+};
+// The walk keeps, next to its summary, the chunk kreq whose tight fold set the
+// current EXACT requirement and the summary just before that fold (prev): if
+// the final check fails (usually kreq's guess was wrong), waiting for kreq's
+// own FULL words and applying prev finishes the look-back.
+struct LbWalk : LbSum {
+    LbSum   prev;
+    int64_t kreq;             // -1: no tight fold since the last reset
 };
 
 CLY_DEV void lb_walk_init(LbWalk& w, int64_t c, int fof) {
     w.e0 = 0; w.rx = 0; w.cE = 0; w.dp = 0; w.dp_fixed = 0;
     w.req = LB_REQ_NONE; w.res = LB_RES_IDENT; w.fixed = 0; w.cdead = 0;
     if (fof) { w.fixed = 1; w.cE = c * (int64_t)CLY_CHUNK; }
+    w.prev = static_cast<const LbSum&>(w);
+    w.kreq = -1;
 }
 
-CLY_DEV bool lb_req_ok(const LbWalk& w, int64_t E) {
+CLY_DEV bool lb_req_ok(const LbSum& w, int64_t E) {
     return w.req == LB_REQ_NONE || (w.req == LB_REQ_EXACT ? E == w.e0 : E >= w.e0);
 }
 
@@ -417,9 +428,12 @@ CLY_DEV bool lb_fold_spec(LbWalk& w, int64_t j, uint64_t w0, int64_t x) {
         }
         w.dp_fixed += (term ? 0 : w.dp) + n;
         w.req = LB_REQ_NONE; w.res = LB_RES_IDENT; w.dp = 0;
+        w.kreq = -1;
         return true;
     }
     if (ds_gvalid(w0) && (w.req == LB_REQ_NONE || (!term && lb_req_ok(w, x)))) {
+        w.prev = static_cast<const LbSum&>(w);
+        w.kreq = j;
         if (term) { w.res = LB_RES_DEAD; w.dp = n; }
         else { if (w.res == LB_RES_IDENT) { w.res = LB_RES_CONST; w.rx = x; } w.dp += n; }
         w.req = LB_REQ_EXACT;
@@ -433,7 +447,7 @@ CLY_DEV bool lb_fold_spec(LbWalk& w, int64_t j, uint64_t w0, int64_t x) {
 
 // Apply FULL words of chunk j (exit X, dead, records P up to and including j).
 // False = the requirement fails (forward fallback needed).
-CLY_DEV bool lb_apply_full_walk(const LbWalk& w, int dead, int64_t X, uint64_t P, LbState& out) {
+CLY_DEV bool lb_apply_full_walk(const LbSum& w, int dead, int64_t X, uint64_t P, LbState& out) {
     if (dead) {
         out.dead = w.fixed ? w.cdead : 1;
         out.E = w.fixed ? w.cE : 0;
@@ -477,6 +491,20 @@ CLY_DEV void lb_forward(Env& env, int64_t c, int fof, int64_t jf, uint32_t epoch
         s.dead = ds_term(w0); s.E = (int64_t)(x & DS_VAL_MASK); s.P = p & DS_VAL_MASK;
     }
     if (fof) { s.E = c * (int64_t)CLY_CHUNK; s.dead = 0; }
+}
+
+// Recovery after a failed check: wait for the FULL words of w.kreq and apply
+// the summary from before its fold.  False = still inconsistent.
+template <class Env>
+CLY_DEV bool lb_recover_kreq(Env& env, const LbWalk& w, uint32_t epoch, LbState& out) {
+    if (w.kreq < 0) return false;
+    const int64_t k = w.kreq;
+    uint64_t w0 = env.ld(k, 0), x = env.ld(k, 2), p = env.ld(k, 3);
+    while (ds_state(w0, epoch) != DS_FULL || !ds_ok(x, epoch) || !ds_ok(p, epoch)) {
+        if (!env.spin()) return false;
+        x = env.ld(k, 2); p = env.ld(k, 3); w0 = env.ld(k, 0);
+    }
+    return lb_apply_full_walk(w.prev, ds_term(w0), (int64_t)(x & DS_VAL_MASK), p & DS_VAL_MASK, out);
 }
 
 // One descriptor of the backward walk (words already loaded and ready).
@@ -528,7 +556,7 @@ CLY_DEV void lookback_seq(Env& env, int64_t c, int fof, uint32_t epoch, LbState&
         if (!lb_apply_full_walk(w, 0, 0, 0, out)) { jf = -1; r = 2; }
         else r = 1;
     }
-    if (r == 2) { env.note_fallback(c, jf); lb_forward(env, c, fof, jf, epoch, out); }
+    if (r == 2 && !lb_recover_kreq(env, w, epoch, out)) { env.note_fallback(c, jf); lb_forward(env, c, fof, jf, epoch, out); }
 }
 
 // ---------------------------------------------------------------------------
@@ -1086,19 +1114,16 @@ CLY_DEV void chunk_body(EX& ex, CLY_LDS ScanShared& S, Env& env) {
         env.mark(S, 5);
     });
     // ---- the true chain (re-resolved, and its CRC redone, when the guess was wrong)
+    ex.one([&]() { S.redo_crc = 0; });
     if (S.in_dead) {
         ex.one([&]() { S.mode = MODE_DEAD; S.R.cnt = 0; S.R.term = 1; });
     } else if (S.entry_g >= cg + CLY_CHUNK) {
-        if (S.mode != MODE_PASS) {
-            ex.one([&]() { S.mode = MODE_PASS; S.R.cnt = 0; S.R.term = 0; });
-            env.crc(ex, S);
-        }
+        if (S.mode != MODE_PASS) ex.one([&]() { S.mode = MODE_PASS; S.R.cnt = 0; S.R.term = 0; S.redo_crc = 1; });
     } else {
         const int newE = (int)(S.entry_g - cg);
         if (S.mode != MODE_NORMAL || S.guess != newE) {
-            ex.one([&]() { S.mode = MODE_NORMAL; });
+            ex.one([&]() { S.mode = MODE_NORMAL; S.redo_crc = 1; });
             resolve(ex, S, newE);
-            env.crc(ex, S);
         }
     }
     // ---- publish the resolved descriptor
@@ -1115,6 +1140,8 @@ CLY_DEV void chunk_body(EX& ex, CLY_LDS ScanShared& S, Env& env) {
                          ds_tag(ep, S.p_excl + cnt), S.p_excl + cnt);
         env.mark(S, 6);
     });
+    // ---- CRC again when the chain changed (successors already have the FULL words)
+    if (S.redo_crc) env.crc(ex, S);
     // ---- tuples, summary
     ex.all([&](int t) { env.emit_lane(S, t); });
     ex.one([&]() {

@@ -71,9 +71,11 @@ struct EmuRun {
     std::atomic<unsigned> overflow{0};
     std::atomic<unsigned> fail{0};
     std::atomic<unsigned> fallbacks{0};
+    std::atomic<unsigned> recoveries{0};
     std::atomic<uint64_t> total{0};
     int nchunks;
     int jitter;
+    int delay_full;
     uint32_t epoch;
 };
 
@@ -95,11 +97,102 @@ struct HostEnv {
         run->fallbacks.fetch_add(1);
         if (getenv("CLY_EMU_VERBOSE")) fprintf(stderr, "fallback chunk %lld jf %lld\n", (long long)c, (long long)jf);
     }
+    // Same windowed walk as the GPU (DevEnv::lookback): 64 descriptors per
+    // round, tight-run fast path, then the exact steps; ballots are loops.
     void lookback(ScanShared& S, int t) {
         if (t != 0) return;
-        LbState ls;
-        lookback_seq(*this, S.C.chunk, S.C.fof, epoch, ls);
-        S.entry_g = ls.E; S.p_excl = ls.P; S.in_dead = ls.dead;
+        if (getenv("CLY_EMU_SEQ_LB")) {
+            LbState ls;
+            lookback_seq(*this, S.C.chunk, S.C.fof, epoch, ls);
+            S.entry_g = ls.E; S.p_excl = ls.P; S.in_dead = ls.dead;
+            return;
+        }
+        const int64_t c = S.C.chunk;
+        LbWalk w;
+        lb_walk_init(w, c, S.C.fof);
+        LbState out;
+        out.E = 0; out.P = 0; out.dead = 1; out._pad = 0;
+        int64_t jf = -1;
+        int r = 0;
+        for (int64_t base = c - 1; r == 0; base -= 64) {
+            if (base < 0) { r = lb_apply_full_walk(w, 0, 0, 0, out) ? 1 : 2; jf = -1; break; }
+            uint64_t W0[64], W1[64], W2[64], W3[64];
+            bool full[64], ready[64];
+            int stop;
+            for (;;) {
+                for (int l = 0; l < 64; l++) {
+                    const int64_t j = base - l;
+                    W0[l] = W1[l] = W2[l] = W3[l] = 0; ready[l] = true; full[l] = false;
+                    if (j >= 0) {
+                        W1[l] = ld(j, 1); W2[l] = ld(j, 2); W3[l] = ld(j, 3); W0[l] = ld(j, 0);
+                        const uint64_t st = ds_state(W0[l], epoch);
+                        if (st == DS_SPEC) ready[l] = ds_ok(W1[l], epoch);
+                        else if (st == DS_FULL) { ready[l] = ds_ok(W2[l], epoch) && ds_ok(W3[l], epoch); full[l] = ready[l]; }
+                        else ready[l] = false;
+                    }
+                }
+                stop = 64;
+                for (int l = 0; l < 64; l++) if (full[l] || base - l < 0) { stop = l; break; }
+                bool wait = false;
+                for (int l = 0; l <= (stop < 64 ? stop : 63); l++) if (!ready[l]) wait = true;
+                if (!wait) break;
+                spin();
+            }
+            int i0 = 0;
+            {
+                int run = 0;
+                for (int l = 0; l < stop; l++) {
+                    const int64_t j = base - l;
+                    const uint64_t w0 = W0[l];
+                    const bool spec = ds_state(w0, epoch) == DS_SPEC && ds_gvalid(w0) && !ds_fof(w0) && !ds_term(w0);
+                    const int64_t xj = (int64_t)(W1[l] & DS_VAL_MASK);
+                    bool tight;
+                    if (l == 0) tight = spec && lb_req_ok(w, xj);
+                    else tight = spec && ds_gvalid(W0[l - 1]) && !ds_fof(W0[l - 1]) &&
+                                 xj == (j + 1) * (int64_t)CLY_CHUNK + ds_grel(W0[l - 1]);
+                    if (!tight) break;
+                    run++;
+                }
+                if (run > 0) {
+                    uint32_t cnt = 0;
+                    for (int l = 0; l < run; l++) cnt += ds_cnt(W0[l]);
+                    const int64_t x0 = (int64_t)(W1[0] & DS_VAL_MASK);
+                    w.prev = static_cast<const LbSum&>(w);
+                    if (run >= 2) {
+                        if (w.prev.res == LB_RES_IDENT) { w.prev.res = LB_RES_CONST; w.prev.rx = x0; }
+                        w.prev.dp += cnt - ds_cnt(W0[run - 1]);
+                        w.prev.req = LB_REQ_EXACT;
+                        w.prev.e0 = (base - (run - 2)) * (int64_t)CLY_CHUNK + ds_grel(W0[run - 2]);
+                    }
+                    w.kreq = base - (run - 1);
+                    if (w.res == LB_RES_IDENT) { w.res = LB_RES_CONST; w.rx = (int64_t)(W1[0] & DS_VAL_MASK); }
+                    w.dp += cnt;
+                    w.req = LB_REQ_EXACT;
+                    w.e0 = (base - (run - 1)) * (int64_t)CLY_CHUNK + ds_grel(W0[run - 1]);
+                    i0 = run;
+                }
+            }
+            const int last = stop < 64 ? stop : 63;
+            for (int i = i0; i <= last && r == 0; i++) {
+                const int64_t ji = base - i;
+                if (ji < 0) { r = lb_apply_full_walk(w, 0, 0, 0, out) ? 1 : 2; jf = -1; }
+                else r = lb_walk_step(w, ji, W0[i], W1[i], W2[i], W3[i], epoch, out, jf);
+            }
+        }
+        if (r == 2 && lb_recover_kreq(*this, w, epoch, out)) { r = 1; run->recoveries.fetch_add(1); }
+        if (r == 2) {
+            if (jf == -3) {
+                jf = -1;
+                for (int64_t k = c - 1; k >= 0; k--) {
+                    uint64_t a0 = ld(k, 0);
+                    while (ds_state(a0, epoch) == 0) { spin(); a0 = ld(k, 0); }
+                    if (ds_state(a0, epoch) == DS_FULL) { jf = k; break; }
+                }
+            }
+            note_fallback(c, jf);
+            lb_forward(*this, c, S.C.fof, jf, epoch, out);
+        }
+        S.entry_g = out.E; S.p_excl = out.P; S.in_dead = out.dead;
     }
     void dbg_lane(ScanShared& S, int t) {
         if (!run->lanes.empty() && S.C.chunk < 4) dbg_lane_fill(S, t, &run->lanes[(S.C.chunk * CLY_NT + t) * 8]);
@@ -130,6 +223,8 @@ struct HostEnv {
     }
     void publish_full(int c, uint64_t w0, uint64_t w2, uint64_t w3, uint64_t total) {
         jitter_sleep(run->jitter, *rng);
+        if (run->delay_full >= 0 && c == run->delay_full)     // test knob: successors see only the SPEC
+            std::this_thread::sleep_for(std::chrono::milliseconds(30));
         st(&run->desc[c].w[2], w2);
         st(&run->desc[c].w[3], w3);
         if (run->jitter && ((*rng)() % 4 == 0)) std::this_thread::yield();
@@ -247,6 +342,8 @@ extern "C" int cly_scan(cly_ctx* ctx, const cly_file* files, int nfiles, cly_tup
     const int nthreads = th ? atoi(th) : 8;
     const char* jt = getenv("CLY_EMU_JITTER");
     R.jitter = jt ? atoi(jt) : 0;
+    const char* dfull = getenv("CLY_EMU_DELAY_FULL");
+    R.delay_full = dfull ? atoi(dfull) : -1;
     std::atomic<int> ticket{0};
     std::vector<std::thread> pool;
     for (int k = 0; k < (nthreads > 0 ? nthreads : 1); k++) {
@@ -269,7 +366,7 @@ extern "C" int cly_scan(cly_ctx* ctx, const cly_file* files, int nfiles, cly_tup
     ctx->sums = R.sums;
     ctx->dbg = R.dbg;
     ctx->lanes = R.lanes;
-    if (getenv("CLY_EMU_STATS")) fprintf(stderr, "emu: %d chunks, %u look-back fallbacks\n", R.nchunks, R.fallbacks.load());
+    if (getenv("CLY_EMU_STATS")) fprintf(stderr, "emu: %d chunks, %u look-back fallbacks, %u recoveries\n", R.nchunks, R.fallbacks.load(), R.recoveries.load());
     if (R.fail.load()) return CLY_ERR_DEVICE;
     if (R.overflow.load()) return CLY_ERR_CAPACITY;
     // k_fin

@@ -113,3 +113,37 @@ def test_chunk_boundary_tails(emu):
                 r = emu.scan([f])
                 t, st, end = co.scan_file(f.data, 5)
                 compare(r.file_tuples(0), r.status[0], r.end_offset[0], t, st, end, "chunk %d +%d cut %d" % (chunk, extra, cut))
+
+
+# Chunks captured on the GPU whose first lane holds a false candidate whose
+# chain merges into the true one: the speculative guess lands before the true
+# first record (tools/find_bad_guess.py + tools/replay_dump.py).
+FALSE_MERGE = ["false_merge_a", "false_merge_b"]
+
+
+def _golden_bytes(name):
+    return np.fromfile(os.path.join(GOLD, name + ".cly"), dtype=np.uint8)
+
+
+@pytest.mark.parametrize("name", FALSE_MERGE)
+def test_false_merge_fixtures(emu, name):
+    d = _golden_bytes(name)
+    r = emu.scan([DataFile(d, 3)])
+    t, st, end = co.scan_file(d, 3)
+    compare(r.file_tuples(0), r.status[0], r.end_offset[0], t, st, end, name)
+
+
+@pytest.mark.parametrize("seq", [False, True])
+def test_wrong_guess_recovery(monkeypatch, seq):
+    """The wrong-guess chunk publishes its resolved descriptor late: every
+    successor's look-back walks through its speculative descriptor, fails the
+    final check and recovers through that chunk's own resolved words."""
+    monkeypatch.setenv("CLY_EMU_THREADS", "32")
+    monkeypatch.setenv("CLY_EMU_DELAY_FULL", "2")
+    if seq:
+        monkeypatch.setenv("CLY_EMU_SEQ_LB", "1")
+    d = np.concatenate([_golden_bytes("false_merge_a"), fixed_records_file(4000, 256, seed=9)])
+    with Scanner(0, lib=_emu("libclyscan_emu.so")) as s:
+        r = s.scan([DataFile(d, 0)])
+    t, st, end = co.scan_file(d, 0)
+    compare(r.file_tuples(0), r.status[0], r.end_offset[0], t, st, end, "recovery")

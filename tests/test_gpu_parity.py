@@ -115,6 +115,19 @@ def test_tails_at_chunk_boundaries(scanner, cut):
             compare(r.file_tuples(0), r.status[0], r.end_offset[0], t, st, end, "cut %d chunk %d +%d" % (cut, chunk, extra))
 
 
+@pytest.mark.parametrize("name", ["false_merge_a", "false_merge_b"])
+def test_false_merge_fixtures(scanner, name):
+    """GPU-captured chunks whose speculative guess is a false candidate merging
+    into the true chain (the guess is wrong; the chunk re-resolves)."""
+    d = np.fromfile(os.path.join(GOLD, name + ".cly"), dtype=np.uint8)
+    long = np.concatenate([d, fixed_records_file(20000, 256, seed=9)])
+    for data in (d, long):
+        f = DataFile(np.ascontiguousarray(data), 3)
+        r = scanner.scan([f])
+        t, st, end = co.scan_file(f.data, 3)
+        compare(r.file_tuples(0), r.status[0], r.end_offset[0], t, st, end, name)
+
+
 def test_bitflips_everywhere_small(scanner):
     base = fixed_records_file(60, 200, seed=5)
     rng = np.random.default_rng(0)
