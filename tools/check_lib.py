@@ -1,6 +1,6 @@
 """Run the golden fixtures (and optional random corpora) through a scan library
-(default: the CPU emulator) and diff against the golden results / oracle.
-Usage: python tools/emu_check.py [lib] [--corpora N]"""
+(default: libclyscan.so) and diff against the golden results / oracle.
+Usage: python tools/check_lib.py [lib] [--corpora N]"""
 import json
 import os
 import sys
@@ -15,7 +15,7 @@ from oracle import cly_oracle as co  # noqa: E402
 from gpu_util import mixed_corpus  # noqa: E402
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
-lib = args[0] if args else os.path.join(ROOT, "tests", "emu", "libclyscan_emu_small.so")
+lib = args[0] if args else "libclyscan.so"
 ncorp = 0
 for a in sys.argv[1:]:
     if a.startswith("--corpora="):

@@ -5,8 +5,8 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 200 python tools/emu_check.py libclyscan_small.so --corpora=8 > gpurun_out/check_small.log 2>&1 || exit $?
-timeout -k 10 200 python tools/emu_check.py libclyscan.so --corpora=8 > gpurun_out/check.log 2>&1 || exit $?
+timeout -k 10 200 python tools/check_lib.py libclyscan_small.so --corpora=8 > gpurun_out/check_small.log 2>&1 || exit $?
+timeout -k 10 200 python tools/check_lib.py libclyscan.so --corpora=8 > gpurun_out/check.log 2>&1 || exit $?
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || exit $?
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
 timeout -k 10 600 python bench.py --steps 10 --warmup 2 ${BENCH_ARGS} > gpurun_out/bench.log 2>&1 || exit $?

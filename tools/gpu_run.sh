@@ -9,8 +9,8 @@ STAGES="${1:-check,pytest,smoke,bench}"
 run() { echo "== $1" >> gpurun_out/steps.log; }
 if [[ $STAGES == *check* ]]; then
   run check
-  timeout -k 10 300 python tools/emu_check.py libclyscan_small.so --corpora=12 > gpurun_out/check_small.log 2>&1 || exit $?
-  timeout -k 10 300 python tools/emu_check.py libclyscan.so --corpora=12 > gpurun_out/check.log 2>&1 || exit $?
+  timeout -k 10 300 python tools/check_lib.py libclyscan_small.so --corpora=12 > gpurun_out/check_small.log 2>&1 || exit $?
+  timeout -k 10 300 python tools/check_lib.py libclyscan.so --corpora=12 > gpurun_out/check.log 2>&1 || exit $?
 fi
 if [[ $STAGES == *pytest* ]]; then
   run pytest
