@@ -28,7 +28,6 @@
 #include "scan_core.h"
 
 #define CLY_KS_LEVELS 6                          // Kogge-Stone levels over 64 lanes
-#define CLY_WS_LEVELS 6                          // binary levels of a word shift (< 64 words)
 #define MODE_EMPTY 0                             // sub-tile beyond the end of its file
 #define MODE_NORMAL 1                            // the chain enters (or ends) inside the sub-tile
 #define MODE_PASS 2                              // one record covers the whole sub-tile
@@ -51,7 +50,18 @@ struct Globals {                 // zeroed per call
     uint64_t total;              // tuple slots used (records + any past an ErrInvalidCRC)
     uint32_t redo_units;         // units whose guessed entry was wrong (statistics)
     uint32_t redo_subs;          // sub-tiles re-resolved inside a unit (statistics)
+    uint64_t prof[24];           // profiling build (-DCLY_PROF): summed cycles per phase
 };
+
+#ifdef CLY_PROF
+#define PROF_INIT() uint64_t prof_t = __builtin_amdgcn_s_memtime(); uint64_t prof_acc[12] = {0,0,0,0,0,0,0,0,0,0,0,0}
+#define PROF(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); prof_acc[i] += t_ - prof_t; prof_t = t_; } while (0)
+#define PROF_FLUSH(base) do { if (lane == 0) for (int i_ = 0; i_ < 12; i_++) atomicAdd((unsigned long long*)&g->prof[(base) + i_], (unsigned long long)prof_acc[i_]); } while (0)
+#else
+#define PROF_INIT()
+#define PROF(i)
+#define PROF_FLUSH(base)
+#endif
 
 struct SubDbg {                  // debug trace of one sub-tile (cly_dbg_enable)
     int32_t mode, E, cnt, term, tst, last, lterm, eof_exit, k0, guess, bad, bpos;
@@ -97,20 +107,30 @@ struct Job {
     uint32_t uoff;               // the unit's offset in its file
     int32_t  _pad;
 };
+struct Cmp {                     // composer -> looker, per unit (slot = iteration & 1)
+    int32_t  unit, fidx;
+    uint32_t uoff;
+    int32_t  fof, gvalid, dead;
+    int64_t  G, X;               // unit-relative guessed entry and exit of the composed chain
+    uint32_t N;                  // records of the composed chain
+    int32_t  _pad;
+};
 struct Ctrl {
     Job      job[2];
     SubSum   sum[CLY_NDW];
-    SubEnt   ent[CLY_NDW];       // under the unit's guessed entry
-    SubEnt   fin[CLY_NDW];       // final (after the look-back)
-    uint64_t P;                  // records before the unit (global)
-    int32_t  changed;            // fin differs from ent
-    int32_t  job_seq, ent_seq, fin_seq;
+    SubEnt   ent[CLY_NDW];       // under the unit's composed entry
+    Cmp      cmp[2];
+    SubEnt   fin[2][CLY_NDW];    // final (after the look-back), slot = iteration & 1
+    uint64_t P[2];               // records before the unit (global)
+    int32_t  job_seq, ent_seq, spec_seq, fin_seq;
     int32_t  sum_seq[CLY_NDW];
-    int32_t  crc_seq[CLY_NDW];
 };
 #define LDS_WIN ((LDS_CTRL + (int)sizeof(Ctrl) + 15) & ~15)
 #define LDS_POOL (LDS_WIN + CLY_NDW * CLY_WIN)
-#define CLY_SCAN_LDS (LDS_POOL + CLY_NDW * 256 * 8)
+#define LDS_KSCOL (LDS_POOL + CLY_NDW * 192 * 8)              // 6 x 32 columns of A^(SUB*2^k)
+#define LDS_HSCOL (LDS_KSCOL + CLY_KS_LEVELS * 32 * 4)          // NWD x 32 columns of A^(4*w)
+#define CLY_SCAN_LDS (LDS_HSCOL + CLY_NWD * 32 * 4)
+#define CLY_COLS ((CLY_KS_LEVELS + CLY_NWD) * 32)                // words of the column table
 static_assert(CLY_SCAN_LDS <= 163840, "LDS budget");
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -124,11 +144,14 @@ __device__ __forceinline__ uint64_t ld_agent(const unsigned long long* p) {
 __device__ __forceinline__ void st_agent(unsigned long long* p, uint64_t v) {
     __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ int lds_ld_acq(const int32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+__device__ __forceinline__ int lds_ld_acq(const CLY_LDS int32_t* p) {
+    const int v = *(const volatile CLY_LDS int32_t*)p;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    return v;
 }
-__device__ __forceinline__ void lds_st_rel(int32_t* p, int v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+__device__ __forceinline__ void lds_st_rel(CLY_LDS int32_t* p, int v) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    *(volatile CLY_LDS int32_t*)p = v;
 }
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -162,11 +185,27 @@ __device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t s)
 __device__ __forceinline__ uint32_t lds_le32(const CLY_LDS uint32_t* w32, int p) {
     return alignb(w32[(p >> 2) + 1], w32[p >> 2], p & 3);
 }
+// struct copies to / from LDS (word by word: no generic-pointer flat access)
+template <class T> __device__ __forceinline__ T lds_get(const CLY_LDS T* p) {
+    static_assert(sizeof(T) % 4 == 0, "word-sized");
+    T v;
+    uint32_t* d = (uint32_t*)&v;
+    const CLY_LDS uint32_t* q = (const CLY_LDS uint32_t*)p;
+    #pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); i++) d[i] = q[i];
+    return v;
+}
+template <class T> __device__ __forceinline__ void lds_put(CLY_LDS T* p, const T& v) {
+    const uint32_t* d = (const uint32_t*)&v;
+    CLY_LDS uint32_t* q = (CLY_LDS uint32_t*)p;
+    #pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); i++) q[i] = d[i];
+}
 #define LDS_SPIN_MAX (1u << 26)
 #define LB_SPIN_MAX (1u << 24)
 
 // Wait until *p >= v (LDS mailbox), bounded.
-__device__ __forceinline__ bool lds_wait_ge(const int32_t* p, int v, Globals* g) {
+__device__ __forceinline__ bool lds_wait_ge(const CLY_LDS int32_t* p, int v, Globals* g) {
     uint32_t n = 0;
     while (lds_ld_acq(p) < v) {
         __builtin_amdgcn_s_sleep(1);
@@ -202,9 +241,19 @@ __device__ __forceinline__ uint32_t crc_unbyte(const CLY_LDS uint8_t* smem, uint
     const uint32_t t = *(const CLY_LDS uint32_t*)(smem + ((i << 8) | lane_off));
     return ((s ^ t) << 8) | i;
 }
-// A^(bytes) s through a 4x256 table of global memory (L2-resident)
-__device__ __forceinline__ uint32_t shift_tab(const uint32_t* __restrict__ t, uint32_t v) {
-    return t[v & 0xff] ^ t[256 + ((v >> 8) & 0xff)] ^ t[512 + ((v >> 16) & 0xff)] ^ t[768 + (v >> 24)];
+// M v for a linear map M given by its 32 columns M(1 << b) in LDS
+__device__ __forceinline__ uint32_t col_mul(const CLY_LDS uint8_t* smem, int col_byte_off, uint32_t v) {
+    const CLY_LDS u32x4* c4 = (const CLY_LDS u32x4*)(smem + col_byte_off);
+    uint32_t p = 0;
+    #pragma unroll
+    for (int q = 0; q < 8; q++) {
+        const u32x4 c = c4[q];
+        p ^= c.x & (uint32_t)__builtin_amdgcn_sbfe((int)v, 4 * q + 0, 1);
+        p ^= c.y & (uint32_t)__builtin_amdgcn_sbfe((int)v, 4 * q + 1, 1);
+        p ^= c.z & (uint32_t)__builtin_amdgcn_sbfe((int)v, 4 * q + 2, 1);
+        p ^= c.w & (uint32_t)__builtin_amdgcn_sbfe((int)v, 4 * q + 3, 1);
+    }
+    return p;
 }
 
 // ---------------------------------------------------------------------------
@@ -503,7 +552,7 @@ struct CrcOut {
 // Check points are collected (positions + the 4 bytes stored there) from the
 // pristine window into a per-wave pool before any patch is applied, in chain
 // order; patches, marks and the restore pass all read the pool.
-#define CP_POOL 256
+#define CP_POOL 192
 #define CP_REAL 0x10000u
 
 // Patch words of pool entry m (pos P, stored bytes c; cprev = previous entry's
@@ -557,8 +606,7 @@ __device__ __forceinline__ void crc_loop(const CLY_LDS uint8_t* smem, const uint
 __device__ __noinline__ void crc_slow(const Sub& T, const Chain& R, CLY_LDS uint8_t* smem, CrcOut& out);
 
 __device__ __noinline__ void crc_phase(const Sub& T, const Lane& L, const Chain& R, int lane, CLY_LDS uint8_t* smem,
-                                       CLY_LDS uint32_t* w32, CLY_LDS u32x2* pool, const uint32_t* __restrict__ ks_tab,
-                                       const uint32_t* __restrict__ ws_tab, CrcOut& out) {
+                                       CLY_LDS uint32_t* w32, CLY_LDS u32x2* pool, CrcOut& out) {
     const uint32_t lane_off = (uint32_t)(lane & 15) * 4;
     out.bad = 0; out.head_raw = 0; out.head_z = 0; out.end_state = 0;
     const bool normal = R.mode == MODE_NORMAL;
@@ -629,17 +677,13 @@ __device__ __noinline__ void crc_phase(const Sub& T, const Lane& L, const Chain&
         if (__ballot(!fin_lane) == 0ull) break;
         const int pc = __shfl_up(c, dd, 64);
         const uint32_t pv = __shfl_up(v, dd, 64);
-        if (!fin_lane) { v ^= shift_tab(ks_tab + lvl * 1024, pv); c = pc; }
+        if (!fin_lane) { v ^= col_mul(smem, LDS_KSCOL + lvl * 128, pv); c = pc; }
     }
     uint32_t s_in = __shfl_up(v, 1, 64);
     if (lane == 0) s_in = 0;
     out.end_state = __shfl(v, CLY_NT - 1, 64);
     // ---- reset checks: T = obs ^ A^(4 rs) S_in
-    uint32_t y = s_in;
-    #pragma unroll
-    for (int k = 0; k < CLY_WS_LEVELS; k++) {
-        if (rs > 0 && ((rs >> k) & 1)) y = shift_tab(ws_tab + k * 1024, y);
-    }
+    const uint32_t y = col_mul(smem, LDS_HSCOL + (rs > 0 ? rs : 0) * 128, s_in);
     const uint32_t Tv = obs ^ y;
     bool bad = err != 0;
     if (rs >= 0 && !rs_first) bad |= Tv != 0;
@@ -716,45 +760,12 @@ __device__ __noinline__ void crc_locate(const Sub& T, const Chain& R, CLY_LDS ui
 }
 
 // ---------------------------------------------------------------------------
-// Tuples for the records of lane `lane`.
-__device__ __noinline__ void emit_lane(const Sub& T, const Lane& L, uint64_t idx0, cly_tuple* out, uint64_t out_cap,
-                                       Globals* g) {
-    if (L.ws < 0) return;
-    const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)T.w32;
-    int64_t p = L.ws;
-    uint64_t idx = idx0;
-    bool of = false;
-    for (int i = 0; i < L.wc; i++, idx++) {
-        const Hdr h = hdr_at(T.w32, (int)p, T.nrel, T.cbase + p);
-        if (idx < out_cap) {
-            int tn;
-            const int64_t klim = h.ks < 11u ? (int64_t)h.ks : 11;
-            const int64_t tx = go_varint(w8 + p + h.hsz, klim, tn);      // parseLogRecordKey, db.go:706-710
-            uint4 q0, q1, q2;
-            const uint64_t off = (uint64_t)(T.cbase + p);
-            const uint64_t ex = (uint64_t)h.exp;
-            const uint64_t txv = tn < 0 ? 0ull : (uint64_t)tx;
-            q0.x = (uint32_t)off; q0.y = (uint32_t)(off >> 32); q0.z = (uint32_t)ex; q0.w = (uint32_t)(ex >> 32);
-            q1.x = (uint32_t)txv; q1.y = (uint32_t)(txv >> 32); q1.z = T.fid; q1.w = (uint32_t)h.size;
-            q2.x = h.ks; q2.y = h.vs;
-            q2.z = (h.type & 0xff) | ((h.dt & 0xff) << 8) | ((uint32_t)(h.hsz & 0xff) << 16) |
-                   ((uint32_t)(tn < 0 ? 0xFF : tn) << 24);
-            q2.w = h.crc;
-            uint4* dst = (uint4*)(out + idx);
-            dst[0] = q0; dst[1] = q1; dst[2] = q2;
-        } else {
-            of = true;
-        }
-        p += h.size;
-    }
-    if (of) atomicOr(&g->overflow, 1u);
-}
-
-// ---------------------------------------------------------------------------
 // Staging: the sub-tile bytes (+halo) into the window.  Whole windows go by
 // LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction); a window cut
 // by the file end is staged through registers with a zero-filled tail.
-__device__ __forceinline__ void stage(const Sub& T, int lane, CLY_LDS uint32_t* w32) {
+// Returns true when the window was issued by LDS-DMA and still has to be
+// waited for (stage_wait); the register path completes before returning.
+__device__ __forceinline__ bool stage(const Sub& T, int lane, CLY_LDS uint32_t* w32) {
     const int wl = T.win_len;
     const uint8_t* src = T.gfile + T.cbase;
     if (wl == CLY_WIN) {
@@ -765,8 +776,7 @@ __device__ __forceinline__ void stage(const Sub& T, int lane, CLY_LDS uint32_t* 
                 __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)(slot0 + lane) * 16),
                                                  (CLY_LDS void*)((CLY_LDS char*)w32 + slot0 * 16), 16, 0, 0);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        return;
+        return true;
     }
     CLY_LDS u32x4* w4 = (CLY_LDS u32x4*)w32;
     const int nvec = wl > 0 ? (wl >> 4) : 0;
@@ -779,6 +789,11 @@ __device__ __forceinline__ void stage(const Sub& T, int lane, CLY_LDS uint32_t* 
         for (int k = 0; k < (wl & 15); k++) v4[k >> 2] |= (uint32_t)b[k] << (8 * (k & 3));
         w4[nvec] = (u32x4){v4[0], v4[1], v4[2], v4[3]};
     }
+    wave_sync();
+    return false;
+}
+__device__ __forceinline__ void stage_wait() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
 }
 
@@ -903,15 +918,18 @@ __device__ __noinline__ void lookback(DevEnv& env, int64_t c, int fof, int lane,
     res.dead = __shfl(res.dead, 0, 64);
 }
 
-// Serial exact walk of sub-tile window w32 from rel (coordinator lane 0):
-// chain exit, records, terminated.  data/dataFile.go:64-111 per step.
-__device__ __noinline__ void coord_walk(const CLY_LDS uint32_t* w32, int64_t cbase, int64_t nrel, int lof, int64_t rel,
-                                        int64_t& exit, uint32_t& n, int& term) {
+// Serial exact walk of sub-tile k from rel (one lane): chain exit, records,
+// terminated.  data/dataFile.go:64-111 per step.  From the LDS window, or
+// (late recompose, the window is gone) from HBM.
+__device__ __noinline__ void coord_walk(const CLY_LDS uint32_t* w32, const uint8_t* gfile, int64_t cbase, int64_t nrel,
+                                        int lof, int64_t rel, int64_t& exit, uint32_t& n, int& term) {
     int64_t p = rel;
     n = 0;
     term = 0;
     while (p < CLY_TS) {
-        const Hdr h = hdr_at(w32, (int)p, nrel, cbase + p);
+        Hdr h;
+        if (w32) h = hdr_at(w32, (int)p, nrel, cbase + p);
+        else hdr_global(gfile, cbase, p, nrel, h);
         if (h.status != REC_OK) { term = 1; break; }
         n++;
         p += h.size;
@@ -920,58 +938,248 @@ __device__ __noinline__ void coord_walk(const CLY_LDS uint32_t* w32, int64_t cba
     exit = p;
 }
 
-// Compose the unit's sub-tile chains from unit-relative entry e (exact; the
-// coordinator walks a sub-tile itself where its data wave's guess differs).
-// Fills ent[], returns the unit exit / count / dead.
-__device__ __noinline__ void compose(Ctrl* C, const DevFile& F, uint32_t uoff, CLY_LDS uint8_t* smem, int64_t e,
-                                     SubEnt* ent, int64_t& X, uint32_t& N, int& dead, Globals* g) {
+// Compose the unit's sub-tile chains from unit-relative entry e (exact: a
+// sub-tile whose data wave guessed differently is walked here).  Writes the
+// per-sub-tile entries to `ent` (LDS) and returns the unit exit / count / dead.
+__device__ __noinline__ void compose(CLY_LDS Ctrl* C, CLY_LDS SubEnt* ent, const DevFile& F, uint32_t uoff,
+                                     CLY_LDS uint8_t* smem, bool from_global, int64_t e, int64_t& X, uint32_t& N,
+                                     int& dead, Globals* g) {
     uint32_t count = 0;
     dead = 0;
     for (int k = 0; k < CLY_NDW; k++) {
-        const SubSum s = C->sum[k];
+        const SubSum s = lds_get(&C->sum[k]);
         SubEnt o;
         o.base = count; o.entry = 0; o._pad = 0;
-        if (s.mode == MODE_EMPTY) { o.mode = MODE_EMPTY; ent[k] = o; continue; }
         const int64_t ks = (int64_t)k * CLY_TS;
-        if (dead) { o.mode = MODE_DEAD; ent[k] = o; continue; }
-        const int64_t rel = e - ks;
-        if (rel >= CLY_TS) { o.mode = MODE_PASS; ent[k] = o; continue; }
-        o.mode = MODE_NORMAL;
-        o.entry = (int)rel;
-        ent[k] = o;
-        if (s.mode == MODE_NORMAL && rel == s.guess) {
-            count += s.cnt;
-            if (s.term) dead = 1;
-            else e = ks + s.exit;
-        } else {
-            const int64_t cbase = (int64_t)uoff + ks;
-            const int64_t nrel = (int64_t)F.len - cbase;
-            const int lof = cbase + CLY_TS >= (int64_t)F.len;
-            const CLY_LDS uint32_t* w32 = (const CLY_LDS uint32_t*)(smem + LDS_WIN + k * CLY_WIN);
-            int64_t x;
-            uint32_t n;
-            int term;
-            coord_walk(w32, cbase, nrel, lof, rel, x, n, term);
-            atomicAdd(&g->redo_subs, 1u);
-            count += n;
-            if (term) dead = 1;
-            else e = ks + x;
+        if (s.mode == MODE_EMPTY) o.mode = MODE_EMPTY;
+        else if (dead) o.mode = MODE_DEAD;
+        else if (e - ks >= CLY_TS) o.mode = MODE_PASS;
+        else {
+            const int64_t rel = e - ks;
+            o.mode = MODE_NORMAL;
+            o.entry = (int)rel;
+            if (!from_global && s.mode == MODE_NORMAL && rel == s.guess) {
+                count += s.cnt;
+                if (s.term) dead = 1;
+                else e = ks + s.exit;
+            } else {
+                const int64_t cbase = (int64_t)uoff + ks;
+                const int64_t nrel = (int64_t)F.len - cbase;
+                const int lof = cbase + CLY_TS >= (int64_t)F.len;
+                const CLY_LDS uint32_t* w32 =
+                    from_global ? nullptr : (const CLY_LDS uint32_t*)(smem + LDS_WIN + k * CLY_WIN);
+                int64_t x;
+                uint32_t n;
+                int term;
+                coord_walk(w32, F.base, cbase, nrel, lof, rel, x, n, term);
+                atomicAdd(&g->redo_subs, 1u);
+                count += n;
+                if (term) dead = 1;
+                else e = ks + x;
+            }
         }
+        lds_put(&ent[k], o);
     }
     X = e;
     N = count;
 }
 
 // ---------------------------------------------------------------------------
-// The scan kernel: CLY_NDW data waves + 1 coordinator wave per workgroup.
-__global__ void __launch_bounds__(64 * (CLY_NDW + 1))
+// Data-wave pieces.
+// Sub-tile geometry of data wave k for job jb.
+__device__ __forceinline__ void sub_setup(Sub& T, const Job& jb, const DevFile& F, int k, CLY_LDS uint32_t* w32) {
+    T.gfile = F.base;
+    T.w32 = w32;
+    T.cbase = (int64_t)jb.uoff + (int64_t)k * CLY_TS;
+    T.nrel = (int64_t)F.len - T.cbase;
+    T.dlen = (int)(T.nrel < CLY_TS ? (T.nrel > 0 ? T.nrel : 0) : CLY_TS);
+    T.win_len = (int)(T.nrel < CLY_WIN ? (T.nrel > 0 ? T.nrel : 0) : CLY_WIN);
+    T.fof = T.cbase == 0;
+    T.lof = T.cbase + CLY_TS >= (int64_t)F.len;
+    T.chunk = (int64_t)jb.unit * CLY_NDW + k;
+    T.fid = F.fid;
+}
+
+// Speculation over the staged window: per lane the first candidate (register
+// SWAR filter over its stripe), then the candidate walks; the sub-tile guess.
+__device__ __noinline__ void sub_spec(const Sub& T, int lane, Spec& sp, int& guess) {
+    const CLY_LDS uint32_t* w32 = T.w32;
+    sp.s = -1; sp.last = -1; sp.c = 0; sp.x = 0;
+    int q0 = CLY_TS;
+    const int a = lane * CLY_SUB;
+    if (a < T.dlen) {
+        uint32_t dw[CLY_NWD + 2];
+        const CLY_LDS u32x4* s4 = (const CLY_LDS u32x4*)(w32 + lane * CLY_NWD);
+        #pragma unroll
+        for (int i = 0; i < CLY_NWD / 4; i++) {
+            const u32x4 v = s4[i];
+            dw[4 * i] = v.x; dw[4 * i + 1] = v.y; dw[4 * i + 2] = v.z; dw[4 * i + 3] = v.w;
+        }
+        dw[CLY_NWD] = w32[lane * CLY_NWD + CLY_NWD];
+        dw[CLY_NWD + 1] = w32[lane * CLY_NWD + CLY_NWD + 1];
+        int fm = CLY_NWD;
+        uint32_t Ln = swar_le4(dw[CLY_NWD + 1]), Kn = swar_ks(dw[CLY_NWD + 1]);
+        #pragma unroll
+        for (int m = CLY_NWD - 1; m >= 0; m--) {
+            const uint32_t Lm = swar_le4(dw[m + 1]), Km = swar_ks(dw[m + 1]);
+            const uint32_t cm = Lm & __builtin_amdgcn_alignbit(Ln, Lm, 8) & __builtin_amdgcn_alignbit(Kn, Km, 16);
+            fm = cm ? m : fm;
+            Ln = Lm; Kn = Km;
+        }
+        if (fm < CLY_NWD) q0 = next_candidate(w32, a + 4 * fm, a + CLY_SUB < T.dlen ? a + CLY_SUB : T.dlen);
+    }
+    spec_lane(T, lane, q0, sp);
+    if (T.fof) { guess = 0; return; }
+    const unsigned long long m = __ballot(sp.s >= 0);
+    guess = m ? __shfl(sp.s, __ffsll((long long)m) - 1, 64) : -1;
+}
+
+// Chain for the given final mode / entry.
+__device__ __forceinline__ void sub_chain(const Sub& T, const Spec& sp, int lane, int mode, int entry, Lane& L,
+                                          Chain& R) {
+    if (mode == MODE_NORMAL) resolve(T, sp, lane, entry, L, R);
+    else chain_none(L, R, mode);
+}
+
+// Per-sub-tile summary for k_fin (lane 0), with unit-relative record counts.
+__device__ __forceinline__ void sub_summary(const Sub& T, const Chain& R, const CrcOut& co, CLY_LDS uint8_t* smem,
+                                            uint32_t base, int bpos, uint32_t bidx, ChunkSum* sums, Globals* g) {
+    const CLY_LDS uint32_t* w32 = T.w32;
+    ChunkSum cs;
+    cs.p_excl = base;
+    cs.evt_off = EVT_NONE; cs.evt_gidx = 0; cs.evt_status = 0; cs.cnt = 0;
+    cs.open_pos = -1; cs.open_state = 0; cs.open_crc = 0;
+    cs.first4 = w32[0];
+    cs.head_raw = 0; cs.head_len = 0; cs.head_shift = 0; cs.head_z = 0; cs.flags = 0;
+    if (R.mode == MODE_DEAD) {
+        cs.flags = SUM_DEAD;
+    } else if (R.mode == MODE_PASS) {
+        cs.head_len = (uint32_t)T.dlen;
+        cs.head_raw = co.end_state;
+        cs.head_z = (uint32_t)(CLY_TS - T.dlen);
+        if (T.lof) {
+            cs.flags |= SUM_CLOSES;
+            cs.evt_off = T.cbase + T.dlen;
+            cs.evt_gidx = base;
+            cs.evt_status = CLY_END_EOF;
+        }
+    } else {
+        cs.cnt = R.cnt;
+        cs.flags |= SUM_CLOSES;
+        cs.head_len = (uint32_t)(R.E < T.dlen ? R.E : T.dlen);
+        cs.head_raw = co.head_raw;
+        cs.head_z = co.head_z;
+        if (bpos >= 0) {
+            cs.evt_off = T.cbase + bpos;
+            cs.evt_gidx = base + bidx;
+            cs.evt_status = CLY_ERR_CRC;
+        } else if (co.bad) {
+            atomicMax(&g->fail, 5u);
+        }
+        if (R.term && bpos < 0) {
+            cs.evt_off = T.cbase + R.tpos;
+            cs.evt_gidx = base + R.cnt;
+            cs.evt_status = R.tst;
+        }
+        // the last record is open at the end of the sub-tile unless a check
+        // point follows it inside the sub-tile
+        if (R.cnt > 0 && R.last >= 0 && (!R.term || (R.eof_exit && R.tpos >= CLY_TS))) {
+            cs.flags |= SUM_OPEN;
+            cs.open_pos = T.cbase + R.last;
+            cs.open_crc = lds_le32(w32, R.last);
+            const int ocs = R.last + 4;
+            if (ocs >= CLY_TS) {
+                cs.open_state = 0xFFFFFFFFu;
+            } else if (ocs + 4 > CLY_TS) {
+                uint32_t s = 0xFFFFFFFFu;
+                const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)w32;
+                for (int q = ocs; q < CLY_TS; q++) s = crc_byte(smem, s, w8[q], 0);
+                cs.open_state = s;
+            } else {
+                cs.open_state = co.end_state;
+            }
+        }
+    }
+    cs.head_shift = cs.head_len > 4 ? cs.head_len - 4 + cs.head_z : 0;   // exponent; k_fin maps it
+    sums[T.chunk] = cs;
+}
+
+// CRC + first failure + summary of a resolved sub-tile.
+__device__ __noinline__ void sub_crc(const Sub& T, const Lane& L, const Chain& R, int lane, CLY_LDS uint8_t* smem,
+                                        CLY_LDS u32x2* pool, uint32_t base, ChunkSum* sums, Globals* g) {
+    CrcOut co;
+    crc_phase(T, L, R, lane, smem, (CLY_LDS uint32_t*)T.w32, pool, co);
+    int bpos = -1;
+    uint32_t bidx = 0;
+    if (lane == 0) {
+        if (co.bad) crc_locate(T, R, smem, bpos, bidx);
+        sub_summary(T, R, co, smem, base, bpos, bidx, sums, g);
+    }
+}
+
+// Tuple words of one record at window position p (index independent).
+__device__ __forceinline__ void tuple_words(const Sub& T, int p, u32x4& q0, u32x4& q1, u32x4& q2, int64_t& size) {
+    const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)T.w32;
+    const Hdr h = hdr_at(T.w32, p, T.nrel, T.cbase + p);
+    int tn;
+    const int64_t klim = h.ks < 11u ? (int64_t)h.ks : 11;
+    const int64_t tx = go_varint(w8 + p + h.hsz, klim, tn);      // parseLogRecordKey, db.go:706-710
+    const uint64_t off = (uint64_t)(T.cbase + p);
+    const uint64_t ex = (uint64_t)h.exp;
+    const uint64_t txv = tn < 0 ? 0ull : (uint64_t)tx;
+    q0 = (u32x4){(uint32_t)off, (uint32_t)(off >> 32), (uint32_t)ex, (uint32_t)(ex >> 32)};
+    q1 = (u32x4){(uint32_t)txv, (uint32_t)(txv >> 32), T.fid, (uint32_t)h.size};
+    q2 = (u32x4){h.ks, h.vs,
+                 (h.type & 0xff) | ((h.dt & 0xff) << 8) | ((uint32_t)(h.hsz & 0xff) << 16) |
+                     ((uint32_t)(tn < 0 ? 0xFF : tn) << 24),
+                 h.crc};
+    size = h.size;
+}
+
+__device__ __forceinline__ void put_tuple(cly_tuple* out, uint64_t idx, uint64_t out_cap, const u32x4& q0,
+                                          const u32x4& q1, const u32x4& q2, bool& of) {
+    if (idx < out_cap) {
+        u32x4* dst = (u32x4*)(out + idx);
+        dst[0] = q0; dst[1] = q1; dst[2] = q2;
+    } else {
+        of = true;
+    }
+}
+
+// Tuples of this lane's records, written directly (output slot known).
+__device__ __noinline__ void emit_direct(const Sub& T, const Lane& L, uint64_t idx0, cly_tuple* out, uint64_t out_cap,
+                                            Globals* g) {
+    bool of = false;
+    if (L.ws >= 0) {
+        int p = L.ws;
+        for (int i = 0; i < L.wc; i++) {
+            u32x4 q0, q1, q2;
+            int64_t size;
+            tuple_words(T, p, q0, q1, q2, size);
+            put_tuple(out, idx0 + i, out_cap, q0, q1, q2, of);
+            p += (int)size;
+        }
+    }
+    if (of) atomicOr(&g->overflow, 1u);
+}
+
+// ---------------------------------------------------------------------------
+// The scan kernel: CLY_NDW data waves + a composer wave + a look-back wave per
+// workgroup (one workgroup per CU).  Pipeline of a data wave, iteration i on
+// unit u_i:  [window staged]  speculate + resolve -> summary  | composer:
+// compose u_i, SPEC |  CRC of u_i, tuples kept in registers  |  flush u_{i-1}
+// (output slot from the looker's look-back of u_{i-1})  |  issue the staging
+// of u_{i+1}.  The look-back of a unit thus overlaps the next unit's work.
+#define WAVES_PER_WG (CLY_NDW + 2)
+#define FLAG_FORCE_REDO 1
+
+__global__ void __launch_bounds__(64 * WAVES_PER_WG)
 k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ file_unit_prefix, int64_t nunits,
-       Desc* desc, ChunkSum* sums, const uint32_t* __restrict__ ks_tab, const uint32_t* __restrict__ ws_tab,
-       const uint32_t* __restrict__ x8n, cly_tuple* out, uint64_t out_cap, Globals* g, uint32_t epoch,
-       SubDbg* dbg) {
+       Desc* desc, ChunkSum* sums, uint64_t* unit_P, const uint32_t* __restrict__ cols, cly_tuple* out,
+       uint64_t out_cap, Globals* g, uint32_t epoch, SubDbg* dbg, int flags) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
-    Ctrl* C = (Ctrl*)(smem_raw + LDS_CTRL);
+    CLY_LDS Ctrl* C = (CLY_LDS Ctrl*)(smem + LDS_CTRL);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // tables: entry i of T_t replicated 16x, dword (i*64 + t*16 + r)
     for (int i = threadIdx.x; i < 256; i += blockDim.x) {
@@ -985,16 +1193,16 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             cv = (cv >> 8) ^ tl;
         }
     }
+    for (int i = threadIdx.x; i < CLY_COLS; i += blockDim.x) ((CLY_LDS uint32_t*)(smem + LDS_KSCOL))[i] = cols[i];
     if (threadIdx.x == 0) {
-        C->job_seq = 0; C->ent_seq = 0; C->fin_seq = 0;
-        for (int k = 0; k < CLY_NDW; k++) { C->sum_seq[k] = 0; C->crc_seq[k] = 0; }
+        C->job_seq = 0; C->ent_seq = 0; C->spec_seq = 0; C->fin_seq = 0;
+        for (int k = 0; k < CLY_NDW; k++) C->sum_seq[k] = 0;
     }
     __syncthreads();
 
     if (wave == CLY_NDW) {
-        // ================= coordinator =================
-        DevEnv env;
-        env.desc = desc; env.g = g; env.epoch = epoch; env.spins = 0; env.nunits = nunits;
+        // ================= composer: tickets, unit composition, SPEC =================
+        PROF_INIT();
         auto take = [&](int slot, int seq) {
             int u = 0;
             if (lane == 0) u = (int)atomicAdd(&g->ticket, 1u);
@@ -1009,95 +1217,141 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                 }
                 jb.unit = u; jb.fidx = lo; jb.uoff = (uint32_t)((int64_t)(u - (int)files[lo].first_unit) * CLY_UNIT);
             }
-            if (lane == 0) { C->job[slot] = jb; lds_st_rel(&C->job_seq, seq); }
+            if (lane == 0) { lds_put(&C->job[slot], jb); lds_st_rel(&C->job_seq, seq); }
             return jb;
         };
         Job jb = take(0, 1);
-        for (int it = 0; jb.unit >= 0; it++) {
-            const DevFile F = files[jb.fidx];
-            // all data waves posted their summaries for `it` (and so have read job[it&1])
-            for (int k = 0; k < CLY_NDW; k++) if (!lds_wait_ge(&C->sum_seq[k], it + 1, g)) return;
-            const Job next = take((it + 1) & 1, it + 2);
-            const int64_t u = jb.unit;
-            const int fof = jb.uoff == 0;
-            // unit guess
-            int gvalid = 0;
-            int64_t G = 0;
-            if (fof) { gvalid = 1; G = 0; }
-            else {
-                for (int k = 0; k < CLY_NDW; k++) {
-                    const SubSum s = C->sum[k];
-                    if (s.mode == MODE_NORMAL) { gvalid = 1; G = (int64_t)k * CLY_TS + s.guess; break; }
+        for (int it = 0;; it++) {
+            Cmp cm;
+            cm.unit = jb.unit; cm.fidx = jb.fidx; cm.uoff = jb.uoff; cm.fof = 0; cm.gvalid = 0; cm.dead = 0;
+            cm.G = 0; cm.X = 0; cm.N = 0; cm._pad = 0;
+            if (jb.unit >= 0) {
+                const DevFile F = files[jb.fidx];
+                const int64_t u = jb.unit;
+                const int fof = jb.uoff == 0;
+                // predecessor's published exit (a hint that corrects false-merge guesses)
+                uint64_t pw0 = 0, pw1 = 0, pw2 = 0;
+                if (!fof && lane == 0) { pw1 = ld_agent(&desc[u - 1].w[1]); pw2 = ld_agent(&desc[u - 1].w[2]); pw0 = ld_agent(&desc[u - 1].w[0]); }
+                for (int k = 0; k < CLY_NDW; k++) if (!lds_wait_ge(&C->sum_seq[k], it + 1, g)) return;
+                PROF(0);
+                const Job next = take((it + 1) & 1, it + 2);
+                PROF(1);
+                int gvalid = 0;
+                int64_t G = 0;
+                if (fof) { gvalid = 1; G = 0; }
+                else {
+                    for (int k = 0; k < CLY_NDW; k++) {
+                        const SubSum sk = lds_get(&C->sum[k]);
+                        if (sk.mode == MODE_NORMAL) { gvalid = 1; G = (int64_t)k * CLY_TS + sk.guess; break; }
+                    }
                 }
-            }
-            SubEnt ent[CLY_NDW];
-            int64_t X = 0;
-            uint32_t N = 0;
-            int dead = 0;
-            if (gvalid) {
-                if (lane == 0) compose(C, F, jb.uoff, smem, G, ent, X, N, dead, g);
+                int64_t X = 0;
+                uint32_t N = 0;
+                int dead = 0;
+                if (lane == 0) {
+                    int64_t e0 = gvalid ? G : -1;
+                    if (!fof) {
+                        const uint64_t st = ds_state(pw0, epoch);
+                        const int64_t ustart = u * CLY_UNIT;
+                        int64_t hx = -1;
+                        if (st == DS_FULL && ds_ok(pw2, epoch) && !ds_term(pw0)) hx = (int64_t)(pw2 & DS_VAL_MASK);
+                        else if (st == DS_SPEC && ds_ok(pw1, epoch) && ds_gvalid(pw0) && !ds_term(pw0)) hx = (int64_t)(pw1 & DS_VAL_MASK);
+                        if (hx >= ustart && hx < ustart + CLY_UNIT && hx - ustart != e0) {
+                            e0 = hx - ustart; gvalid = 1; G = e0;
+                        }
+                    }
+                    if (gvalid) compose(C, C->ent, F, jb.uoff, smem, false, G, X, N, dead, g);
+                    else {
+                        for (int k = 0; k < CLY_NDW; k++) {
+                            SubEnt o;
+                            o.mode = lds_get(&C->sum[k]).mode == MODE_EMPTY ? MODE_EMPTY : MODE_PASS;
+                            o.entry = 0; o.base = 0; o._pad = 0;
+                            lds_put(&C->ent[k], o);
+                        }
+                    }
+                    lds_st_rel(&C->ent_seq, it + 1);
+                }
+                gvalid = __shfl(gvalid, 0, 64); G = __shfl(G, 0, 64);
+                X = __shfl(X, 0, 64); N = __shfl(N, 0, 64); dead = __shfl(dead, 0, 64);
+                cm.fof = fof; cm.gvalid = gvalid; cm.dead = dead; cm.G = G; cm.X = X; cm.N = N;
+                PROF(2);
+                // the looker's slot it&1 is free once it finished unit it-2
+                if (it >= 2 && !lds_wait_ge(&C->fin_seq, it - 1, g)) return;
+                if (lane == 0) {
+                    lds_put(&C->cmp[it & 1], cm);
+                    st_agent(&desc[u].w[1], ds_tag(epoch, (uint64_t)(u * CLY_UNIT + X)));
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    st_agent(&desc[u].w[0], ds_pack(epoch, DS_SPEC, fof, dead, gvalid, G, N));
+                    lds_st_rel(&C->spec_seq, it + 1);
+                }
+                PROF(3);
+                jb = next;
             } else {
-                for (int k = 0; k < CLY_NDW; k++) {
-                    ent[k].mode = C->sum[k].mode == MODE_EMPTY ? MODE_EMPTY : MODE_PASS;
-                    ent[k].entry = 0; ent[k].base = 0; ent[k]._pad = 0;
-                }
+                if (it >= 2 && !lds_wait_ge(&C->fin_seq, it - 1, g)) return;
+                if (lane == 0) { lds_put(&C->cmp[it & 1], cm); lds_st_rel(&C->spec_seq, it + 1); }
+                break;
             }
-            X = __shfl(X, 0, 64); N = __shfl(N, 0, 64); dead = __shfl(dead, 0, 64);
-            if (lane == 0) {
-                for (int k = 0; k < CLY_NDW; k++) C->ent[k] = ent[k];
-                lds_st_rel(&C->ent_seq, it + 1);
-                // SPEC descriptor
-                st_agent(&desc[u].w[1], ds_tag(epoch, (uint64_t)(u * CLY_UNIT + X)));
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                st_agent(&desc[u].w[0], ds_pack(epoch, DS_SPEC, fof, dead, gvalid, G, N));
-            }
-            // look-back
+        }
+        PROF_FLUSH(12);
+        return;
+    }
+
+    if (wave == CLY_NDW + 1) {
+        // ================= looker: look-back, final entries, FULL =================
+        PROF_INIT();
+        DevEnv env;
+        env.desc = desc; env.g = g; env.epoch = epoch; env.spins = 0; env.nunits = nunits;
+        for (int it = 0;; it++) {
+            if (!lds_wait_ge(&C->spec_seq, it + 1, g)) return;
+            const Cmp cm = lds_get(&C->cmp[it & 1]);
+            if (cm.unit < 0) break;
+            PROF(6);
+            const int64_t u = cm.unit;
+            const DevFile F = files[cm.fidx];
             LbState lb;
-            lookback(env, u, fof, lane, lb);
-            if (env.spins > LB_SPIN_MAX) { lb.dead = 1; }
-            // final sub-tile entries
-            int changed = 0;
-            int64_t Xf = X;
-            uint32_t Nf = N;
-            int deadf = dead;
+            lookback(env, u, cm.fof, lane, lb);
+            PROF(7);
+            if (env.spins > LB_SPIN_MAX) lb.dead = 1;
             const int64_t ustart = u * CLY_UNIT;
-            if (lb.dead) {
-                changed = 1; Nf = 0; deadf = 1; Xf = 0;
-                for (int k = 0; k < CLY_NDW; k++) {
-                    ent[k].mode = C->sum[k].mode == MODE_EMPTY ? MODE_EMPTY : MODE_DEAD;
-                    ent[k].entry = 0; ent[k].base = 0;
-                }
-            } else if (gvalid && lb.E == ustart + G) {
-                changed = 0;
-            } else if (lb.E - ustart >= CLY_UNIT) {
-                changed = 1; Nf = 0; deadf = 0; Xf = lb.E - ustart;
-                for (int k = 0; k < CLY_NDW; k++) {
-                    ent[k].mode = C->sum[k].mode == MODE_EMPTY ? MODE_EMPTY : MODE_PASS;
-                    ent[k].entry = 0; ent[k].base = 0;
-                }
-            } else {
-                changed = 1;
-                if (lane == 0) atomicAdd(&g->redo_units, 1u);
-                // the windows must be restored (data waves done with their CRC patches)
-                for (int k = 0; k < CLY_NDW; k++) if (!lds_wait_ge(&C->crc_seq[k], it + 1, g)) return;
-                if (lane == 0) compose(C, F, jb.uoff, smem, lb.E - ustart, ent, Xf, Nf, deadf, g);
-                Xf = __shfl(Xf, 0, 64); Nf = __shfl(Nf, 0, 64); deadf = __shfl(deadf, 0, 64);
-            }
+            CLY_LDS SubEnt* fin = C->fin[it & 1];
+            int64_t Xf = cm.X;
+            uint32_t Nf = cm.N;
+            int deadf = cm.dead;
             if (lane == 0) {
-                // FULL descriptor (successors), then the final entries (own data waves)
+                if (lb.dead) {
+                    Nf = 0; deadf = 1; Xf = 0;
+                    for (int k = 0; k < CLY_NDW; k++) {
+                        SubEnt o; o.entry = 0; o.base = 0; o._pad = 0;
+                        o.mode = lds_get(&C->ent[k]).mode == MODE_EMPTY ? MODE_EMPTY : MODE_DEAD;
+                        lds_put(&fin[k], o);
+                    }
+                } else if (cm.gvalid && lb.E == ustart + cm.G) {
+                    for (int k = 0; k < CLY_NDW; k++) lds_put(&fin[k], lds_get(&C->ent[k]));
+                } else if (lb.E - ustart >= CLY_UNIT) {
+                    Nf = 0; deadf = 0; Xf = lb.E - ustart;
+                    for (int k = 0; k < CLY_NDW; k++) {
+                        SubEnt o; o.entry = 0; o.base = 0; o._pad = 0;
+                        o.mode = lds_get(&C->ent[k]).mode == MODE_EMPTY ? MODE_EMPTY : MODE_PASS;
+                        lds_put(&fin[k], o);
+                    }
+                } else {
+                    // wrong guess: recompose from the true entry, walking HBM (rare)
+                    atomicAdd(&g->redo_units, 1u);
+                    compose(C, fin, F, cm.uoff, smem, true, lb.E - ustart, Xf, Nf, deadf, g);
+                }
                 const uint64_t incl = lb.P + Nf;
                 st_agent(&desc[u].w[2], ds_tag(epoch, (uint64_t)(ustart + Xf)));
                 st_agent(&desc[u].w[3], ds_tag(epoch, incl));
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                st_agent(&desc[u].w[0], ds_pack(epoch, DS_FULL, fof, deadf, 0, 0, Nf));
+                st_agent(&desc[u].w[0], ds_pack(epoch, DS_FULL, cm.fof, deadf, 0, 0, Nf));
                 if (u == nunits - 1) g->total = incl;
-                for (int k = 0; k < CLY_NDW; k++) C->fin[k] = ent[k];
-                C->P = lb.P;
-                C->changed = changed;
+                unit_P[u] = lb.P;
+                C->P[it & 1] = lb.P;
                 lds_st_rel(&C->fin_seq, it + 1);
             }
-            jb = next;
+            PROF(8);
         }
+        PROF_FLUSH(12);
         return;
     }
 
@@ -1105,22 +1359,16 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     const int k = wave;
     CLY_LDS uint32_t* w32 = (CLY_LDS uint32_t*)(smem + LDS_WIN + k * CLY_WIN);
     CLY_LDS u32x2* pool = (CLY_LDS u32x2*)(smem + LDS_POOL + k * CP_POOL * 8);
+    PROF_INIT();
+    bool pending_dma = false;
     for (int it = 0;; it++) {
         if (!lds_wait_ge(&C->job_seq, it + 1, g)) return;
-        const Job jb = C->job[it & 1];
-        if (jb.unit < 0) return;
+        const Job jb = lds_get(&C->job[it & 1]);
+        if (jb.unit < 0) break;
+        PROF(0);
         const DevFile F = files[jb.fidx];
         Sub T;
-        T.gfile = F.base;
-        T.w32 = w32;
-        T.cbase = (int64_t)jb.uoff + (int64_t)k * CLY_TS;
-        T.nrel = (int64_t)F.len - T.cbase;
-        T.dlen = (int)(T.nrel < CLY_TS ? (T.nrel > 0 ? T.nrel : 0) : CLY_TS);
-        T.win_len = (int)(T.nrel < CLY_WIN ? (T.nrel > 0 ? T.nrel : 0) : CLY_WIN);
-        T.fof = T.cbase == 0;
-        T.lof = T.cbase + CLY_TS >= (int64_t)F.len;
-        T.chunk = (int64_t)jb.unit * CLY_NDW + k;
-        T.fid = F.fid;
+        sub_setup(T, jb, F, k, w32);
         const bool empty = T.nrel <= 0 && !T.fof;
         Spec sp;
         sp.s = -1; sp.last = -1; sp.c = 0; sp.x = 0;
@@ -1129,160 +1377,77 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         chain_none(L, R, MODE_PASS);
         int guess = -1;
         if (!empty) {
-            stage(T, lane, w32);
-            // ---- speculation: first candidate per lane (register SWAR filter), then walks
-            int q0 = CLY_TS;
-            const int a = lane * CLY_SUB;
-            if (a < T.dlen) {
-                uint32_t dw[CLY_NWD + 2];
-                const CLY_LDS u32x4* s4 = (const CLY_LDS u32x4*)(w32 + lane * CLY_NWD);
-                #pragma unroll
-                for (int i = 0; i < CLY_NWD / 4; i++) {
-                    const u32x4 v = s4[i];
-                    dw[4 * i] = v.x; dw[4 * i + 1] = v.y; dw[4 * i + 2] = v.z; dw[4 * i + 3] = v.w;
-                }
-                dw[CLY_NWD] = w32[lane * CLY_NWD + CLY_NWD];
-                dw[CLY_NWD + 1] = w32[lane * CLY_NWD + CLY_NWD + 1];
-                int fm = CLY_NWD;
-                uint32_t Ln = swar_le4(dw[CLY_NWD + 1]), Kn = swar_ks(dw[CLY_NWD + 1]);
-                #pragma unroll
-                for (int m = CLY_NWD - 1; m >= 0; m--) {
-                    const uint32_t Lm = swar_le4(dw[m + 1]), Km = swar_ks(dw[m + 1]);
-                    const uint32_t cm = Lm & __builtin_amdgcn_alignbit(Ln, Lm, 8) & __builtin_amdgcn_alignbit(Kn, Km, 16);
-                    fm = cm ? m : fm;
-                    Ln = Lm; Kn = Km;
-                }
-                if (fm < CLY_NWD) q0 = next_candidate(w32, a + 4 * fm, a + CLY_SUB < T.dlen ? a + CLY_SUB : T.dlen);
-                else q0 = CLY_TS;
-            }
-            spec_lane(T, lane, q0, sp);
-            if (T.fof) guess = 0;
-            else {
-                const unsigned long long m = __ballot(sp.s >= 0);
-                guess = m ? __shfl(sp.s, __ffsll((long long)m) - 1, 64) : -1;
-            }
+            if (!pending_dma) { if (stage(T, lane, w32)) stage_wait(); }
+            else stage_wait();
+            PROF(1);
+            sub_spec(T, lane, sp, guess);
+            PROF(2);
             if (guess >= 0) resolve(T, sp, lane, guess, L, R);
+            PROF(3);
         }
+        pending_dma = false;
         if (lane == 0) {
-            SubSum s;
-            s.mode = empty ? MODE_EMPTY : (guess >= 0 ? MODE_NORMAL : MODE_PASS);
-            s.guess = guess;
-            s.exit = R.xrel;
-            s.cnt = R.cnt;
-            s.term = R.term;
-            C->sum[k] = s;
+            SubSum ss;
+            ss.mode = empty ? MODE_EMPTY : (guess >= 0 ? MODE_NORMAL : MODE_PASS);
+            ss.guess = guess;
+            ss.exit = R.xrel;
+            ss.cnt = R.cnt;
+            ss.term = R.term;
+            lds_put(&C->sum[k], ss);
             lds_st_rel(&C->sum_seq[k], it + 1);
         }
         if (!lds_wait_ge(&C->ent_seq, it + 1, g)) return;
-        SubEnt e = C->ent[k];
-        int cur_mode = -1, cur_entry = -1;
-        CrcOut co;
-        co.bad = 0; co.head_raw = 0; co.head_z = 0; co.end_state = 0;
-        auto prepare = [&](const SubEnt& en) {
-            if (en.mode == MODE_NORMAL) {
-                if (!(guess >= 0 && en.entry == guess && R.mode == MODE_NORMAL && cur_mode < 0)) resolve(T, sp, lane, en.entry, L, R);
-            } else {
-                chain_none(L, R, en.mode);
-            }
-            cur_mode = en.mode; cur_entry = en.entry;
-        };
+        PROF(4);
+        const SubEnt e = lds_get(&C->ent[k]);
         if (!empty) {
-            prepare(e);
-            crc_phase(T, L, R, lane, smem, w32, pool, ks_tab, ws_tab, co);
+            if (e.mode == MODE_NORMAL ? !(guess >= 0 && e.entry == guess) : true) sub_chain(T, sp, lane, e.mode, e.entry, L, R);
+            sub_crc(T, L, R, lane, smem, pool, e.base, sums, g);
         }
-        if (lane == 0) lds_st_rel(&C->crc_seq[k], it + 1);
+        PROF(5);
         if (!lds_wait_ge(&C->fin_seq, it + 1, g)) return;
-        const SubEnt f = C->fin[k];
-        const uint64_t P = C->P;
-        if (empty) continue;
-        if (f.mode != cur_mode || (f.mode == MODE_NORMAL && f.entry != cur_entry)) {
-            cur_mode = -2;
-            if (f.mode == MODE_NORMAL) resolve(T, sp, lane, f.entry, L, R);
-            else chain_none(L, R, f.mode);
-            cur_mode = f.mode; cur_entry = f.entry;
-            crc_phase(T, L, R, lane, smem, w32, pool, ks_tab, ws_tab, co);
-        }
-        const uint64_t p_excl = P + f.base;
-        // ---- tuples
-        if (R.mode == MODE_NORMAL) emit_lane(T, L, p_excl + L.base, out, out_cap, g);
-        // ---- first failing record, summary
-        int bpos = -1;
-        uint32_t bidx = 0;
-        if (co.bad && lane == 0) crc_locate(T, R, smem, bpos, bidx);
-        if (lane == 0) {
-            ChunkSum cs;
-            cs.p_excl = p_excl;
-            cs.evt_off = EVT_NONE; cs.evt_gidx = 0; cs.evt_status = 0; cs.cnt = 0;
-            cs.open_pos = -1; cs.open_state = 0; cs.open_crc = 0;
-            cs.first4 = w32[0];
-            cs.head_raw = 0; cs.head_len = 0; cs.head_shift = 1u << 31; cs.head_z = 0; cs.flags = 0;
-            if (R.mode == MODE_DEAD) {
-                cs.flags = SUM_DEAD;
-            } else if (R.mode == MODE_PASS) {
-                cs.head_len = (uint32_t)T.dlen;
-                cs.head_raw = co.end_state;
-                cs.head_z = (uint32_t)(CLY_TS - T.dlen);
-                if (T.lof) {
-                    cs.flags |= SUM_CLOSES;
-                    cs.evt_off = T.cbase + T.dlen;
-                    cs.evt_gidx = p_excl;
-                    cs.evt_status = CLY_END_EOF;
-                }
-            } else {
-                cs.cnt = R.cnt;
-                cs.flags |= SUM_CLOSES;
-                cs.head_len = (uint32_t)(R.E < T.dlen ? R.E : T.dlen);
-                cs.head_raw = co.head_raw;
-                cs.head_z = co.head_z;
-                if (bpos >= 0) {
-                    cs.evt_off = T.cbase + bpos;
-                    cs.evt_gidx = p_excl + bidx;
-                    cs.evt_status = CLY_ERR_CRC;
-                } else if (co.bad) {
-                    atomicMax(&g->fail, 5u);
-                }
-                if (R.term && (bpos < 0)) {
-                    cs.evt_off = T.cbase + R.tpos;
-                    cs.evt_gidx = p_excl + R.cnt;
-                    cs.evt_status = R.tst;
-                }
-                // the last record is open at the end of the sub-tile unless a
-                // check point follows it inside the sub-tile
-                if (R.cnt > 0 && R.last >= 0 && (!R.term || (R.eof_exit && R.tpos >= CLY_TS))) {
-                    cs.flags |= SUM_OPEN;
-                    cs.open_pos = T.cbase + R.last;
-                    cs.open_crc = lds_le32(w32, R.last);
-                    const int ocs = R.last + 4;
-                    if (ocs >= CLY_TS) {
-                        cs.open_state = 0xFFFFFFFFu;
-                    } else if (ocs + 4 > CLY_TS) {
-                        uint32_t s = 0xFFFFFFFFu;
-                        const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)w32;
-                        for (int q = ocs; q < CLY_TS; q++) s = crc_byte(smem, s, w8[q], 0);
-                        cs.open_state = s;
-                    } else {
-                        cs.open_state = co.end_state;
-                    }
-                }
+        PROF(6);
+        const SubEnt f = lds_get(&C->fin[it & 1][k]);
+        const uint64_t P = C->P[it & 1];
+        if (!empty) {
+            if (f.mode != e.mode || (f.mode == MODE_NORMAL && f.entry != e.entry) || (flags & FLAG_FORCE_REDO)) {
+                sub_chain(T, sp, lane, f.mode, f.entry, L, R);
+                sub_crc(T, L, R, lane, smem, pool, f.base, sums, g);
+            } else if (f.base != e.base && lane == 0) {
+                // same chain, but the unit was recomposed: only its record base moved
+                ChunkSum* cs = &sums[T.chunk];
+                cs->p_excl = f.base;
+                if (cs->evt_off != EVT_NONE) cs->evt_gidx += (uint64_t)f.base - (uint64_t)e.base;
             }
-            const uint32_t hz = cs.head_len > 4 ? cs.head_len - 4 + cs.head_z : 0;
-            cs.head_shift = hz <= (uint32_t)(CLY_TS + 4) ? x8n[hz] : (1u << 31);
-            sums[T.chunk] = cs;
-            if (dbg) {
+            PROF(7);
+            if (R.mode == MODE_NORMAL) emit_direct(T, L, P + f.base + L.base, out, out_cap, g);
+            PROF(8);
+            if (dbg && lane == 0) {
                 SubDbg d;
                 d.mode = R.mode; d.E = R.E; d.cnt = (int)R.cnt; d.term = R.term; d.tst = R.tst; d.last = R.last;
-                d.lterm = R.lterm; d.eof_exit = R.eof_exit; d.k0 = R.k0; d.guess = guess; d.bad = co.bad; d.bpos = bpos;
+                d.lterm = R.lterm; d.eof_exit = R.eof_exit; d.k0 = R.k0; d.guess = guess; d.bad = 0; d.bpos = 0;
                 d.tpos = R.tpos; d.xrel = R.xrel;
                 dbg[T.chunk] = d;
             }
         }
+        // stage the next unit's sub-tile now (the window is free)
+        if (!lds_wait_ge(&C->job_seq, it + 2, g)) return;
+        const Job nj = lds_get(&C->job[(it + 1) & 1]);
+        if (nj.unit >= 0) {
+            const DevFile F2 = files[nj.fidx];
+            Sub T2;
+            sub_setup(T2, nj, F2, k, w32);
+            if (T2.nrel > 0 || T2.fof) pending_dma = stage(T2, lane, w32);
+        }
+        PROF(9);
     }
+    PROF_FLUSH(0);
 }
 
 // One workgroup per file: first event of the file.
 #define FIN_NT 256
 __global__ void __launch_bounds__(FIN_NT)
-k_fin(const DevFile* __restrict__ files, const ChunkSum* __restrict__ sums, FileOut* __restrict__ fout) {
+k_fin(const DevFile* __restrict__ files, const ChunkSum* __restrict__ sums, const uint64_t* __restrict__ unit_P,
+      const uint32_t* __restrict__ x8n, FileOut* __restrict__ fout) {
     const int f = blockIdx.x, tid = threadIdx.x;
     const DevFile F = files[f];
     const int64_t c0 = (int64_t)F.first_unit * CLY_NDW, nc = F.nsub;
@@ -1295,7 +1460,7 @@ k_fin(const DevFile* __restrict__ files, const ChunkSum* __restrict__ sums, File
     for (int64_t i = tid; i < nc; i += FIN_NT) {
         uint64_t gi = 0;
         int32_t st = 0;
-        const int64_t o = fin_chunk_event(sums, c0, nc, i, &gi, &st);
+        const int64_t o = fin_chunk_event(sums, unit_P, x8n, c0, nc, i, &gi, &st);
         if (o < best) { best = o; bg = gi; bs = st; }
     }
     r_off[tid] = best; r_g[tid] = bg; r_st[tid] = bs;
@@ -1308,7 +1473,7 @@ k_fin(const DevFile* __restrict__ files, const ChunkSum* __restrict__ sums, File
     }
     if (tid == 0) {
         FileOut fo;
-        const uint64_t first = sums[c0].p_excl;
+        const uint64_t first = unit_P[F.first_unit] + sums[c0].p_excl;
         fo.first_index = first;
         fo.ok = r_off[0] != EVT_NONE;
         fo.n_records = fo.ok ? r_g[0] - first : 0;
@@ -1333,8 +1498,7 @@ struct cly_ctx {
     Desc* d_desc; int64_t cap_units;
     ChunkSum* d_sums;
     Globals* d_g;
-    uint32_t* d_ks;              // Kogge-Stone shift tables: A^(SUB*2^k)
-    uint32_t* d_ws;              // word shift tables: A^(4*2^k)
+    uint32_t* d_cols;            // columns of A^(SUB*2^k) (Kogge-Stone) and A^(4w) (head shifts)
     uint32_t* d_x8n;
     DevFile* h_files;
     uint32_t* h_prefix;
@@ -1344,16 +1508,9 @@ struct cly_ctx {
     int scan_grid;
     uint8_t* d_bytes; uint64_t cap_bytes;          // host-path staging
     SubDbg* d_dbg; int dbg_on;
+    uint64_t* d_unitP;
     cly_tuple* d_tuples; uint64_t cap_tuples;
 };
-
-static void build_shift_tables(uint32_t* h, uint64_t step_bytes, int levels) {
-    for (int lvl = 0; lvl < levels; lvl++) {
-        const uint32_t xm = cly_x8n(step_bytes << lvl);
-        for (int bpos = 0; bpos < 4; bpos++)
-            for (uint32_t i = 0; i < 256; i++) h[lvl * 1024 + bpos * 256 + i] = cly_multmodp(xm, i << (8 * bpos));
-    }
-}
 
 extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     if (!out) return CLY_ERR_ARG;
@@ -1367,15 +1524,20 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     for (int i = 0; i < 4; i++) HIPCK(hipEventCreate(&c->ev[i]));
     HIPCK(hipMalloc(&c->d_g, sizeof(Globals)));
     HIPCK(hipHostMalloc(&c->h_g, sizeof(Globals), hipHostMallocDefault));
-    const size_t tab_bytes = sizeof(uint32_t) * 1024 * CLY_KS_LEVELS;
-    uint32_t* hs = (uint32_t*)calloc(1, tab_bytes);
-    HIPCK(hipMalloc(&c->d_ks, tab_bytes));
-    build_shift_tables(hs, CLY_SUB, CLY_KS_LEVELS);
-    HIPCK(hipMemcpy(c->d_ks, hs, tab_bytes, hipMemcpyHostToDevice));
-    HIPCK(hipMalloc(&c->d_ws, tab_bytes));
-    build_shift_tables(hs, 4, CLY_WS_LEVELS);
-    HIPCK(hipMemcpy(c->d_ws, hs, tab_bytes, hipMemcpyHostToDevice));
-    free(hs);
+    {
+        uint32_t* hc = (uint32_t*)calloc(CLY_COLS, sizeof(uint32_t));
+        for (int lvl = 0; lvl < CLY_KS_LEVELS; lvl++) {
+            const uint32_t xm = cly_x8n((uint64_t)CLY_SUB << lvl);
+            for (int b = 0; b < 32; b++) hc[lvl * 32 + b] = cly_multmodp(xm, 1u << b);
+        }
+        for (int w = 0; w < CLY_NWD; w++) {
+            const uint32_t xm = cly_x8n((uint64_t)4 * w);
+            for (int b = 0; b < 32; b++) hc[(CLY_KS_LEVELS + w) * 32 + b] = cly_multmodp(xm, 1u << b);
+        }
+        HIPCK(hipMalloc(&c->d_cols, sizeof(uint32_t) * CLY_COLS));
+        HIPCK(hipMemcpy(c->d_cols, hc, sizeof(uint32_t) * CLY_COLS, hipMemcpyHostToDevice));
+        free(hc);
+    }
     const size_t x8_bytes = sizeof(uint32_t) * (CLY_TS + 8);
     HIPCK(hipMalloc(&c->d_x8n, x8_bytes));
     uint32_t* hx = (uint32_t*)malloc(x8_bytes);
@@ -1387,7 +1549,7 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     HIPCK(hipFuncSetAttribute((const void*)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CLY_SCAN_LDS));
     {
         int per_cu = 0, ncu = 0;
-        HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_scan, 64 * (CLY_NDW + 1), CLY_SCAN_LDS));
+        HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_scan, 64 * WAVES_PER_WG, CLY_SCAN_LDS));
         HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
         if (per_cu < 1) per_cu = 1;
         c->scan_grid = per_cu * ncu;
@@ -1400,8 +1562,8 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
-    hipFree(c->d_files); hipFree(c->d_prefix); hipFree(c->d_fout); hipFree(c->d_desc); hipFree(c->d_sums); hipFree(c->d_dbg);
-    hipFree(c->d_g); hipFree(c->d_ks); hipFree(c->d_ws); hipFree(c->d_x8n); hipFree(c->d_bytes); hipFree(c->d_tuples);
+    hipFree(c->d_files); hipFree(c->d_prefix); hipFree(c->d_fout); hipFree(c->d_desc); hipFree(c->d_sums); hipFree(c->d_dbg); hipFree(c->d_unitP);
+    hipFree(c->d_g); hipFree(c->d_cols); hipFree(c->d_x8n); hipFree(c->d_bytes); hipFree(c->d_tuples);
     hipHostFree(c->h_files); hipHostFree(c->h_prefix); hipHostFree(c->h_fout); hipHostFree(c->h_g);
     for (int i = 0; i < 4; i++) hipEventDestroy(c->ev[i]);
     hipStreamDestroy(c->stream);
@@ -1438,6 +1600,8 @@ static int ensure_units(cly_ctx* c, int64_t nunits) {
     HIPCK(hipMalloc(&c->d_sums, sizeof(ChunkSum) * cap * CLY_NDW));
     hipFree(c->d_dbg);
     HIPCK(hipMalloc(&c->d_dbg, sizeof(SubDbg) * cap * CLY_NDW));
+    hipFree(c->d_unitP);
+    HIPCK(hipMalloc(&c->d_unitP, sizeof(uint64_t) * cap));
     c->cap_units = cap;
     return CLY_OK;
 }
@@ -1486,12 +1650,12 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     HIPCK(hipEventRecord(c->ev[0], st));
     int grid = c->scan_grid;
     if ((int64_t)grid > nunits) grid = (int)nunits;
-    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * (CLY_NDW + 1)), CLY_SCAN_LDS, st, c->d_files, nfiles, c->d_prefix,
-                       nunits, c->d_desc, c->d_sums, c->d_ks, c->d_ws, c->d_x8n, d_out, out_cap, c->d_g, c->epoch,
-                       c->dbg_on ? c->d_dbg : nullptr);
+    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * WAVES_PER_WG), CLY_SCAN_LDS, st, c->d_files, nfiles, c->d_prefix,
+                       nunits, c->d_desc, c->d_sums, c->d_unitP, c->d_cols, d_out, out_cap, c->d_g, c->epoch,
+                       c->dbg_on ? c->d_dbg : nullptr, c->dbg_on > 1 ? FLAG_FORCE_REDO : 0);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[1], st));
-    hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_sums, c->d_fout);
+    hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_sums, c->d_unitP, c->d_x8n, c->d_fout);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[2], st));
     HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
@@ -1584,10 +1748,19 @@ extern "C" int cly_dbg_sums(cly_ctx* c, void* out, int n) {
 }
 extern "C" int cly_dbg_sumsize(void) { return (int)sizeof(ChunkSum); }
 extern "C" int cly_dbg_enable(cly_ctx* c, int on) { c->dbg_on = on; return 0; }
+extern "C" int cly_dbg_unitp(cly_ctx* c, uint64_t* out, int n) {
+    HIPCK(hipDeviceSynchronize());
+    HIPCK(hipMemcpy(out, c->d_unitP, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
+    return n;
+}
 extern "C" int cly_dbg_subs(cly_ctx* c, void* out, int n) {
     HIPCK(hipDeviceSynchronize());
     HIPCK(hipMemcpy(out, c->d_dbg, sizeof(SubDbg) * n, hipMemcpyDeviceToHost));
     return n;
+}
+extern "C" int cly_dbg_prof(cly_ctx* c, uint64_t* out24) {
+    for (int i = 0; i < 24; i++) out24[i] = c->h_g->prof[i];
+    return 24;
 }
 extern "C" int cly_dbg_stats(cly_ctx* c, uint32_t* out4) {
     out4[0] = c->h_g->redo_units; out4[1] = c->h_g->redo_subs; out4[2] = c->scan_grid; out4[3] = CLY_SCAN_LDS;

@@ -340,15 +340,15 @@ CLY_DEV int lb_walk_step(LbWalk& w, int64_t j, uint64_t w0, uint64_t w1, uint64_
 // the launch).  CRC state convention: the register of crc_gf.h ("init form").
 struct ChunkSum {
     int64_t  evt_off;     // file offset of the sub-tile's first event, INT64_MAX none
-    uint64_t evt_gidx;    // global tuple index at the event
-    uint64_t p_excl;      // records before the sub-tile (global)
+    uint64_t evt_gidx;    // tuple index at the event, relative to the unit's first record
+    uint64_t p_excl;      // records of the unit before the sub-tile
     int64_t  open_pos;    // file offset of the record open at the sub-tile end (-1 none)
     int32_t  evt_status;
     uint32_t cnt;         // records starting in the sub-tile
     uint32_t open_state;  // its CRC register at the end of the sub-tile
     uint32_t open_crc;    // its stored CRC
     uint32_t head_raw;    // Z_z(raw register over [4, head_len)): z zero bytes appended
-    uint32_t head_shift;  // x^(8*(head_len - 4 + z)) mod P
+    uint32_t head_shift;  // head_len - 4 + z (k_fin multiplies by x^(8*head_shift))
     uint32_t first4;      // first 4 bytes of the sub-tile
     uint32_t head_len;    // bytes before the first boundary
     uint32_t flags;       // SUM_*
@@ -362,28 +362,30 @@ struct ChunkSum {
 // k_fin helpers: finish the CRC of the record open at the end of sub-tile i by
 // walking the heads of the following sub-tiles of the file.  Returns the
 // register after head H, times x^(8*zout) (zout zero bytes appended).
-CLY_DEV uint32_t fin_advance(uint32_t s, int64_t ocs, const ChunkSum& H, int64_t hstart, uint32_t* zout) {
+CLY_DEV uint32_t fin_advance(uint32_t s, int64_t ocs, const ChunkSum& H, const uint32_t* x8n, int64_t hstart,
+                             uint32_t* zout) {
     const int64_t hlen = H.head_len;
     const int64_t l4 = hlen < 4 ? hlen : 4;
     int lo = 0;
     if (ocs > hstart) lo = (int)(ocs - hstart < l4 ? ocs - hstart : l4);
     for (int k = lo; k < l4; k++) s = cly_crc_byte_bitwise(s, (uint8_t)(H.first4 >> (8 * k)));
     *zout = 0;
-    if (hlen > 4) { s = cly_multmodp(H.head_shift, s) ^ H.head_raw; *zout = H.head_z; }
+    if (hlen > 4) { s = cly_multmodp(x8n[H.head_shift], s) ^ H.head_raw; *zout = H.head_z; }
     return s;
 }
 
 // Event of sub-tile i of a file (sub-tiles c0 .. c0+nc-1): in-tile event, or
 // the CRC failure of its open record.  Returns the file offset (EVT_NONE if none).
-CLY_DEV int64_t fin_chunk_event(const ChunkSum* sums, int64_t c0, int64_t nc, int64_t i, uint64_t* gidx,
-                                int32_t* status) {
+CLY_DEV int64_t fin_chunk_event(const ChunkSum* sums, const uint64_t* unit_P, const uint32_t* x8n, int64_t c0,
+                                int64_t nc, int64_t i, uint64_t* gidx, int32_t* status) {
     const ChunkSum S = sums[c0 + i];
+    const uint64_t P = unit_P[(c0 + i) / CLY_NDW];     // records before the sub-tile's unit
     int64_t off = EVT_NONE;
     uint64_t g = 0;
     int32_t st = 0;
     if (!(S.flags & SUM_DEAD)) {
         off = S.evt_off;
-        g = S.evt_gidx;
+        g = P + S.evt_gidx;
         st = S.evt_status;
         if (S.flags & SUM_OPEN) {
             uint32_t s = S.open_state;
@@ -391,13 +393,13 @@ CLY_DEV int64_t fin_chunk_event(const ChunkSum* sums, int64_t c0, int64_t nc, in
             const int64_t ocs = S.open_pos + 4;
             for (int64_t j = i + 1; j < nc; j++) {
                 const ChunkSum H = sums[c0 + j];
-                s = fin_advance(s, ocs, H, j * (int64_t)CLY_TS, &z);
+                s = fin_advance(s, ocs, H, x8n, j * (int64_t)CLY_TS, &z);
                 if (H.flags & SUM_CLOSES) break;
                 z = 0;
             }
             if (s != cly_shift(~S.open_crc, z) && (off == EVT_NONE || S.open_pos < off)) {
                 off = S.open_pos;
-                g = S.p_excl + S.cnt - 1;
+                g = P + S.p_excl + S.cnt - 1;
                 st = CLY_ERR_CRC;
             }
         }

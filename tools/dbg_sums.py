@@ -47,6 +47,22 @@ ddt = np.dtype([(n, "<i4") for n in "mode E cnt term tst last lterm eof_exit k0 
 dbuf = np.zeros(rows, ddt)
 sc.lib.cly_dbg_subs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
 sc.lib.cly_dbg_subs(sc.ctx, dbuf.ctypes.data, rows)
+TS = int(sys.argv[5]) if len(sys.argv) > 5 else 1024
+import bisect
 for i, b in enumerate(dbuf):
     if i < lo: continue
-    print("sub", i, {k: int(b[k]) for k in ddt.names})
+    d = {k: int(b[k]) for k in ddt.names}
+    # oracle: first record start >= sub-tile start, records starting in the sub-tile
+    s0 = i * TS
+    j = bisect.bisect_left(offs, s0)
+    oe = (offs[j] - s0) if j < len(offs) else -1
+    on = bisect.bisect_left(offs, s0 + TS) - j
+    print("sub", i, "E", d["E"], "guess", d["guess"], "cnt", d["cnt"], "mode", d["mode"], "| oracle E", oe, "cnt", on,
+          "OK" if (d["mode"] != 1 or (d["E"] == oe and d["cnt"] == on)) else "DIFF")
+UNIT = int(sys.argv[6]) if len(sys.argv) > 6 else 2048
+nu = (len(data) + UNIT - 1) // UNIT
+up = (ctypes.c_uint64 * nu)()
+sc.lib.cly_dbg_unitp.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+sc.lib.cly_dbg_unitp(sc.ctx, up, nu)
+for u in range(nu):
+    print("unit", u, "P", up[u], "oracle", bisect.bisect_left(offs, u * UNIT))
