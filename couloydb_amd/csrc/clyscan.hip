@@ -37,7 +37,7 @@ struct DevFile {                 // 32 B
     const uint8_t* base;         // device pointer to the file's first byte (16-B aligned)
     uint64_t len;
     uint32_t fid;
-    uint32_t first_unit;         // global index of the file's first unit
+    uint32_t first_sub;          // global index of the file's first sub-tile
     uint32_t nsub;               // sub-tiles of the file (>= 1)
     uint32_t _pad;
 };
@@ -48,15 +48,17 @@ struct Globals {                 // zeroed per call
     uint32_t lb_timeout;         // a look-back / mailbox spin hit its bound (never expected)
     uint32_t fail;               // an internal invariant was violated (never expected)
     uint64_t total;              // tuple slots used (records + any past an ErrInvalidCRC)
-    uint32_t redo_units;         // units whose guessed entry was wrong (statistics)
-    uint32_t redo_subs;          // sub-tiles re-resolved inside a unit (statistics)
+    uint32_t nfix;               // fix list length (this round)
+    uint32_t fix_total;          // statistics: all fixes of the call
+    uint32_t ncand;              // sub-tiles whose chain disagrees with the link (this round)
+    uint32_t _pad0;
     uint64_t prof[24];           // profiling build (-DCLY_PROF): summed cycles per phase
 };
 
 #ifdef CLY_PROF
 #define PROF_INIT() uint64_t prof_t = __builtin_amdgcn_s_memtime(); uint64_t prof_acc[12] = {0,0,0,0,0,0,0,0,0,0,0,0}
 #define PROF(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); prof_acc[i] += t_ - prof_t; prof_t = t_; } while (0)
-#define PROF_FLUSH(base) do { if (lane == 0) for (int i_ = 0; i_ < 12; i_++) atomicAdd((unsigned long long*)&g->prof[(base) + i_], (unsigned long long)prof_acc[i_]); } while (0)
+#define PROF_FLUSH(base) do { if (lane == 0) for (int i_ = 0; i_ < 6; i_++) atomicAdd((unsigned long long*)&g->prof[(base) + i_], (unsigned long long)prof_acc[i_]); } while (0)
 #else
 #define PROF_INIT()
 #define PROF(i)
@@ -77,60 +79,53 @@ struct FileOut {
 };
 
 // ---------------------------------------------------------------------------
-// LDS layout (dynamic shared memory, byte offsets)
+// LDS layout of k_scan / k_fix (dynamic shared memory, byte offsets)
 //   [0, 65536)        CRC slicing-by-4 tables T0..T3, 16 replicas: dword
 //                     (i*64 + t*16 + r) = T_t[i] (replica r); lane l reads replica
 //                     l & 15, so one lookup instruction touches 16 banks x 2 lanes
 //   [65536, +256)     inverse of a zero-byte step (top byte of T0 -> index)
-//   [LDS_CTRL, ...)   coordinator <-> data-wave mailboxes
-//   [LDS_WIN + k*WIN) window of data wave k (sub-tile + halo, zero past the file end)
+//   [LDS_WIN + k*WIN) window of wave k (sub-tile + halo, zero past the file end)
+//   [LDS_POOL ...)    per-wave check-point pools
+//   [LDS_KSCOL ...)   columns of the Kogge-Stone and word shifts
 #define LDS_TAB 0
 #define LDS_INV 65536
-#define LDS_CTRL (LDS_INV + 256)
-
-struct SubSum {                  // data wave -> coordinator (under its own guess)
-    int32_t  mode;               // MODE_EMPTY / MODE_NORMAL (guess found) / MODE_PASS (none)
-    int32_t  guess;              // sub-tile-relative guessed entry
-    int64_t  exit;               // sub-tile-relative exit of the guessed chain
-    uint32_t cnt;
-    int32_t  term;               // the guessed chain ends inside the sub-tile
-};
-struct SubEnt {                  // coordinator -> data wave
-    int32_t  mode;
-    int32_t  entry;              // sub-tile-relative entry (MODE_NORMAL)
-    uint32_t base;               // records of the unit before this sub-tile
-    int32_t  _pad;
-};
-struct Job {
-    int32_t  unit;               // global unit index, -1: no more work
-    int32_t  fidx;
-    uint32_t uoff;               // the unit's offset in its file
-    int32_t  _pad;
-};
-struct Cmp {                     // composer -> looker, per unit (slot = iteration & 1)
-    int32_t  unit, fidx;
-    uint32_t uoff;
-    int32_t  fof, gvalid, dead;
-    int64_t  G, X;               // unit-relative guessed entry and exit of the composed chain
-    uint32_t N;                  // records of the composed chain
-    int32_t  _pad;
-};
-struct Ctrl {
-    Job      job[2];
-    SubSum   sum[CLY_NDW];
-    SubEnt   ent[CLY_NDW];       // under the unit's composed entry
-    Cmp      cmp[2];
-    SubEnt   fin[2][CLY_NDW];    // final (after the look-back), slot = iteration & 1
-    uint64_t P[2];               // records before the unit (global)
-    int32_t  job_seq, ent_seq, spec_seq, fin_seq;
-    int32_t  sum_seq[CLY_NDW];
-};
-#define LDS_WIN ((LDS_CTRL + (int)sizeof(Ctrl) + 15) & ~15)
+#define LDS_WIN (LDS_INV + 256)
 #define LDS_POOL (LDS_WIN + CLY_NDW * CLY_WIN)
 #define LDS_KSCOL (LDS_POOL + CLY_NDW * 192 * 8)              // 6 x 32 columns of A^(SUB*2^k)
 #define LDS_HSCOL (LDS_KSCOL + CLY_KS_LEVELS * 32 * 4)          // NWD x 32 columns of A^(4*w)
 #define CLY_SCAN_LDS (LDS_HSCOL + CLY_NWD * 32 * 4)
 #define CLY_COLS ((CLY_KS_LEVELS + CLY_NWD) * 32)                // words of the column table
+
+// Per-sub-tile result of k_scan / k_fix, read by the link scan (16 B).
+struct SubDesc {
+    int64_t  x;                  // global chain position after the sub-tile (MODE_NORMAL, not terminated)
+    uint32_t cnt;                // records of the sub-tile under its chain
+    int16_t  entry;              // sub-tile-relative entry of the chain (MODE_NORMAL)
+    uint8_t  mode;               // MODE_NORMAL / MODE_PASS / MODE_DEAD
+    uint8_t  flags;              // SD_*
+};
+#define SD_TERM 1                // the chain ends inside the sub-tile (incl. at the end of the file)
+#define SD_FOF 2                 // first sub-tile of its file
+#define SD_OVF 4                 // more tuples than the staging slot holds: k_place emits them from the data
+#define CLY_CAP 64               // tuples per sub-tile staging slot
+
+// Link-scan element: what a run of sub-tiles does to the chain state, for
+// each state it can be entered in (br[0]: chain live, br[1]: chain already
+// ended in this file).  A guessed chain counts only when entered live; the
+// first sub-tile of a file resets the state whatever it was.
+struct LinkBr {
+    int64_t  x;                  // chain position after the run (set)
+    uint64_t cnt;                // records the run adds
+    int32_t  set;                // the run fixes the state (else: passes it through)
+    int32_t  term;               // ... to ended
+};
+struct LinkAgg { LinkBr br[2]; };
+struct Fix {                     // a sub-tile whose chain disagrees with the state the link gives it
+    uint32_t s;
+    int32_t  mode, entry;        // the chain that state implies (mode < 0: not determined yet)
+    uint32_t file;
+    int64_t  x_in;               // chain position entering the sub-tile
+};
 static_assert(CLY_SCAN_LDS <= 163840, "LDS budget");
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -798,205 +793,18 @@ __device__ __forceinline__ void stage_wait() {
 }
 
 // ---------------------------------------------------------------------------
-// Coordinator pieces.
-struct DevEnv {
-    Desc* desc;
-    Globals* g;
-    uint32_t epoch;
-    uint32_t spins;
-    int64_t nunits;
-    __device__ __forceinline__ uint64_t ld(int64_t j, int k) { return ld_agent(&desc[j].w[k]); }
-    __device__ __forceinline__ bool spin() {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > LB_SPIN_MAX) { atomicOr(&g->lb_timeout, 1u); return false; }
-        return true;
-    }
-};
-
-// Decoupled look-back by the coordinator wave: 64 descriptors per round trip,
-// then every lane folds them in order (uniform; scan_core.h lb_walk_step).
-__device__ __noinline__ void lookback(DevEnv& env, int64_t c, int fof, int lane, LbState& res) {
-    const uint32_t epoch = env.epoch;
-    LbWalk w;
-    lb_walk_init(w, c, fof);
-    LbState out;
-    out.E = 0; out.P = 0; out.dead = 1; out._pad = 0;
-    int64_t jf = -1;
-    int r = 0;
-    bool ok = true;
-    for (int64_t base = c - 1; r == 0 && ok; base -= 64) {
-        if (base < 0) {
-            r = lb_apply_full_walk(w, 0, 0, 0, out) ? 1 : 2;
-            jf = -1;
-            break;
-        }
-        const int64_t j = base - lane;
-        uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-        int stop;
-        for (;;) {
-            bool ready = true, full = false;
-            if (j >= 0) {
-                w1 = env.ld(j, 1); w2 = env.ld(j, 2); w3 = env.ld(j, 3);
-                w0 = env.ld(j, 0);
-                const uint64_t st = ds_state(w0, epoch);
-                if (st == DS_SPEC) ready = ds_ok(w1, epoch);
-                else if (st == DS_FULL) { ready = ds_ok(w2, epoch) && ds_ok(w3, epoch); full = ready; }
-                else ready = false;
-            }
-            const unsigned long long endm = __ballot(full || j < 0);
-            stop = endm ? __ffsll((long long)endm) - 1 : 64;
-            const unsigned long long need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);
-            if (!(__ballot(!ready) & need)) break;
-            int go = 1;
-            if (lane == 0) go = env.spin() ? 1 : 0;
-            if (!__shfl(go, 0, 64)) { ok = false; break; }
-        }
-        if (!ok) break;
-        // fast path: a run of "tight" speculative descriptors from lane 0
-        int i0 = 0;
-        {
-            const int64_t jn = j + 1;
-            const uint64_t w0n = __shfl_up(w0, 1, 64);
-            const bool spec = j >= 0 && ds_state(w0, epoch) == DS_SPEC && ds_gvalid(w0) && !ds_fof(w0) && !ds_term(w0);
-            const int64_t xj = (int64_t)(w1 & DS_VAL_MASK);
-            bool tight;
-            if (lane == 0) tight = spec && lb_req_ok(w, xj);
-            else tight = spec && ds_gvalid(w0n) && !ds_fof(w0n) && xj == jn * CLY_UNIT + ds_grel(w0n);
-            const unsigned long long tm = __ballot(tight && lane < stop);
-            const int run = (~tm) ? __ffsll((long long)~tm) - 1 : 64;
-            if (run > 0) {
-                uint32_t cnt = (lane < run) ? ds_cnt(w0) : 0u;
-                #pragma unroll
-                for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-                const uint64_t w0l = __shfl(w0, run - 1, 64);
-                const uint64_t x0 = __shfl(w1, 0, 64);
-                if (run >= 2) {
-                    const uint64_t w0p = __shfl(w0, run - 2, 64);
-                    w.prev = static_cast<const LbSum&>(w);
-                    if (w.prev.res == LB_RES_IDENT) { w.prev.res = LB_RES_CONST; w.prev.rx = (int64_t)(x0 & DS_VAL_MASK); }
-                    w.prev.dp += cnt - ds_cnt(w0l);
-                    w.prev.req = LB_REQ_EXACT;
-                    w.prev.e0 = (base - (run - 2)) * CLY_UNIT + ds_grel(w0p);
-                } else {
-                    w.prev = static_cast<const LbSum&>(w);
-                }
-                w.kreq = base - (run - 1);
-                if (w.res == LB_RES_IDENT) { w.res = LB_RES_CONST; w.rx = (int64_t)(x0 & DS_VAL_MASK); }
-                w.dp += cnt;
-                w.req = LB_REQ_EXACT;
-                w.e0 = (base - (run - 1)) * CLY_UNIT + ds_grel(w0l);
-                i0 = run;
-            }
-        }
-        const int last = stop < 64 ? stop : 63;
-        for (int i = i0; i <= last && r == 0; i++) {
-            const int64_t ji = base - i;
-            if (ji < 0) {
-                r = lb_apply_full_walk(w, 0, 0, 0, out) ? 1 : 2;
-                jf = -1;
-            } else {
-                r = lb_walk_step(w, ji, __shfl(w0, i, 64), __shfl(w1, i, 64), __shfl(w2, i, 64),
-                                 __shfl(w3, i, 64), epoch, out, jf);
-            }
-        }
-    }
-    if (ok && r == 2 && lb_recover_kreq(env, w, epoch, out)) r = 1;
-    if (ok && r == 2) {
-        if (jf == -3) {
-            jf = -1;
-            for (int64_t k = c - 1; k >= 0; k--) {
-                uint64_t a0 = env.ld(k, 0);
-                while (ds_state(a0, epoch) == 0 && env.spin()) a0 = env.ld(k, 0);
-                if (ds_state(a0, epoch) == DS_FULL) { jf = k; break; }
-            }
-        }
-        lb_forward(env, c, fof, jf, epoch, out);
-    }
-    res = out;
-    res.E = __shfl(res.E, 0, 64);
-    res.P = __shfl(res.P, 0, 64);
-    res.dead = __shfl(res.dead, 0, 64);
-}
-
-// Serial exact walk of sub-tile k from rel (one lane): chain exit, records,
-// terminated.  data/dataFile.go:64-111 per step.  From the LDS window, or
-// (late recompose, the window is gone) from HBM.
-__device__ __noinline__ void coord_walk(const CLY_LDS uint32_t* w32, const uint8_t* gfile, int64_t cbase, int64_t nrel,
-                                        int lof, int64_t rel, int64_t& exit, uint32_t& n, int& term) {
-    int64_t p = rel;
-    n = 0;
-    term = 0;
-    while (p < CLY_TS) {
-        Hdr h;
-        if (w32) h = hdr_at(w32, (int)p, nrel, cbase + p);
-        else hdr_global(gfile, cbase, p, nrel, h);
-        if (h.status != REC_OK) { term = 1; break; }
-        n++;
-        p += h.size;
-    }
-    if (!term && lof && p == nrel) term = 1;
-    exit = p;
-}
-
-// Compose the unit's sub-tile chains from unit-relative entry e (exact: a
-// sub-tile whose data wave guessed differently is walked here).  Writes the
-// per-sub-tile entries to `ent` (LDS) and returns the unit exit / count / dead.
-__device__ __noinline__ void compose(CLY_LDS Ctrl* C, CLY_LDS SubEnt* ent, const DevFile& F, uint32_t uoff,
-                                     CLY_LDS uint8_t* smem, bool from_global, int64_t e, int64_t& X, uint32_t& N,
-                                     int& dead, Globals* g) {
-    uint32_t count = 0;
-    dead = 0;
-    for (int k = 0; k < CLY_NDW; k++) {
-        const SubSum s = lds_get(&C->sum[k]);
-        SubEnt o;
-        o.base = count; o.entry = 0; o._pad = 0;
-        const int64_t ks = (int64_t)k * CLY_TS;
-        if (s.mode == MODE_EMPTY) o.mode = MODE_EMPTY;
-        else if (dead) o.mode = MODE_DEAD;
-        else if (e - ks >= CLY_TS) o.mode = MODE_PASS;
-        else {
-            const int64_t rel = e - ks;
-            o.mode = MODE_NORMAL;
-            o.entry = (int)rel;
-            if (!from_global && s.mode == MODE_NORMAL && rel == s.guess) {
-                count += s.cnt;
-                if (s.term) dead = 1;
-                else e = ks + s.exit;
-            } else {
-                const int64_t cbase = (int64_t)uoff + ks;
-                const int64_t nrel = (int64_t)F.len - cbase;
-                const int lof = cbase + CLY_TS >= (int64_t)F.len;
-                const CLY_LDS uint32_t* w32 =
-                    from_global ? nullptr : (const CLY_LDS uint32_t*)(smem + LDS_WIN + k * CLY_WIN);
-                int64_t x;
-                uint32_t n;
-                int term;
-                coord_walk(w32, F.base, cbase, nrel, lof, rel, x, n, term);
-                atomicAdd(&g->redo_subs, 1u);
-                count += n;
-                if (term) dead = 1;
-                else e = ks + x;
-            }
-        }
-        lds_put(&ent[k], o);
-    }
-    X = e;
-    N = count;
-}
-
-// ---------------------------------------------------------------------------
 // Data-wave pieces.
-// Sub-tile geometry of data wave k for job jb.
-__device__ __forceinline__ void sub_setup(Sub& T, const Job& jb, const DevFile& F, int k, CLY_LDS uint32_t* w32) {
+// Geometry of global sub-tile sidx (file F).
+__device__ __forceinline__ void sub_setup(Sub& T, int64_t sidx, const DevFile& F, CLY_LDS uint32_t* w32) {
     T.gfile = F.base;
     T.w32 = w32;
-    T.cbase = (int64_t)jb.uoff + (int64_t)k * CLY_TS;
+    T.cbase = (sidx - (int64_t)F.first_sub) * CLY_TS;
     T.nrel = (int64_t)F.len - T.cbase;
     T.dlen = (int)(T.nrel < CLY_TS ? (T.nrel > 0 ? T.nrel : 0) : CLY_TS);
     T.win_len = (int)(T.nrel < CLY_WIN ? (T.nrel > 0 ? T.nrel : 0) : CLY_WIN);
     T.fof = T.cbase == 0;
     T.lof = T.cbase + CLY_TS >= (int64_t)F.len;
-    T.chunk = (int64_t)jb.unit * CLY_NDW + k;
+    T.chunk = sidx;
     T.fid = F.fid;
 }
 
@@ -1046,7 +854,6 @@ __device__ __forceinline__ void sub_summary(const Sub& T, const Chain& R, const 
                                             uint32_t base, int bpos, uint32_t bidx, ChunkSum* sums, Globals* g) {
     const CLY_LDS uint32_t* w32 = T.w32;
     ChunkSum cs;
-    cs.p_excl = base;
     cs.evt_off = EVT_NONE; cs.evt_gidx = 0; cs.evt_status = 0; cs.cnt = 0;
     cs.open_pos = -1; cs.open_state = 0; cs.open_crc = 0;
     cs.first4 = w32[0];
@@ -1160,27 +967,28 @@ __device__ __noinline__ void emit_direct(const Sub& T, const Lane& L, uint64_t i
             p += (int)size;
         }
     }
-    if (of) atomicOr(&g->overflow, 1u);
+    if (of && g) atomicOr(&g->overflow, 1u);
 }
 
 // ---------------------------------------------------------------------------
-// The scan kernel: CLY_NDW data waves + a composer wave + a look-back wave per
-// workgroup (one workgroup per CU).  Pipeline of a data wave, iteration i on
-// unit u_i:  [window staged]  speculate + resolve -> summary  | composer:
-// compose u_i, SPEC |  CRC of u_i, tuples kept in registers  |  flush u_{i-1}
-// (output slot from the looker's look-back of u_{i-1})  |  issue the staging
-// of u_{i+1}.  The look-back of a unit thus overlaps the next unit's work.
-#define WAVES_PER_WG (CLY_NDW + 2)
-#define FLAG_FORCE_REDO 1
+// Kernels.
+//   k_scan   every sub-tile independently: speculate, resolve the chain under
+//            its own guess, CRC, tuples into the sub-tile's staging slot
+//   k_link1/2/3   scan over sub-tile results: each guess is checked against the
+//            chain entering its sub-tile; output slot of every sub-tile
+//   k_fix    the (rare) sub-tiles whose guess was wrong, from their true entry
+//   k_place  staged tuples to their output slots
+//   k_fin    per file: straddling CRCs and the first event
+__device__ __forceinline__ int find_file(const uint32_t* __restrict__ sub_prefix, int nfiles, int64_t s) {
+    int lo = 0, hi = nfiles - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((int64_t)sub_prefix[mid] <= s) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
 
-__global__ void __launch_bounds__(64 * WAVES_PER_WG)
-k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ file_unit_prefix, int64_t nunits,
-       Desc* desc, ChunkSum* sums, uint64_t* unit_P, const uint32_t* __restrict__ cols, cly_tuple* out,
-       uint64_t out_cap, Globals* g, uint32_t epoch, SubDbg* dbg, int flags) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
-    CLY_LDS Ctrl* C = (CLY_LDS Ctrl*)(smem + LDS_CTRL);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+__device__ __forceinline__ void init_tables(CLY_LDS uint8_t* smem, const uint32_t* __restrict__ cols) {
     // tables: entry i of T_t replicated 16x, dword (i*64 + t*16 + r)
     for (int i = threadIdx.x; i < 256; i += blockDim.x) {
         uint32_t cv = i;
@@ -1194,263 +1002,305 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         }
     }
     for (int i = threadIdx.x; i < CLY_COLS; i += blockDim.x) ((CLY_LDS uint32_t*)(smem + LDS_KSCOL))[i] = cols[i];
-    if (threadIdx.x == 0) {
-        C->job_seq = 0; C->ent_seq = 0; C->spec_seq = 0; C->fin_seq = 0;
-        for (int k = 0; k < CLY_NDW; k++) C->sum_seq[k] = 0;
-    }
     __syncthreads();
+}
 
-    if (wave == CLY_NDW) {
-        // ================= composer: tickets, unit composition, SPEC =================
-        PROF_INIT();
-        auto take = [&](int slot, int seq) {
-            int u = 0;
-            if (lane == 0) u = (int)atomicAdd(&g->ticket, 1u);
-            u = __shfl(u, 0, 64);
-            Job jb;
-            jb.unit = -1; jb.fidx = 0; jb.uoff = 0; jb._pad = 0;
-            if (u < nunits) {
-                int lo = 0, hi = nfiles - 1;
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if ((int64_t)file_unit_prefix[mid] <= u) lo = mid; else hi = mid - 1;
-                }
-                jb.unit = u; jb.fidx = lo; jb.uoff = (uint32_t)((int64_t)(u - (int)files[lo].first_unit) * CLY_UNIT);
-            }
-            if (lane == 0) { lds_put(&C->job[slot], jb); lds_st_rel(&C->job_seq, seq); }
-            return jb;
-        };
-        Job jb = take(0, 1);
-        for (int it = 0;; it++) {
-            Cmp cm;
-            cm.unit = jb.unit; cm.fidx = jb.fidx; cm.uoff = jb.uoff; cm.fof = 0; cm.gvalid = 0; cm.dead = 0;
-            cm.G = 0; cm.X = 0; cm.N = 0; cm._pad = 0;
-            if (jb.unit >= 0) {
-                const DevFile F = files[jb.fidx];
-                const int64_t u = jb.unit;
-                const int fof = jb.uoff == 0;
-                // predecessor's published exit (a hint that corrects false-merge guesses)
-                uint64_t pw0 = 0, pw1 = 0, pw2 = 0;
-                if (!fof && lane == 0) { pw1 = ld_agent(&desc[u - 1].w[1]); pw2 = ld_agent(&desc[u - 1].w[2]); pw0 = ld_agent(&desc[u - 1].w[0]); }
-                for (int k = 0; k < CLY_NDW; k++) if (!lds_wait_ge(&C->sum_seq[k], it + 1, g)) return;
-                PROF(0);
-                const Job next = take((it + 1) & 1, it + 2);
-                PROF(1);
-                int gvalid = 0;
-                int64_t G = 0;
-                if (fof) { gvalid = 1; G = 0; }
-                else {
-                    for (int k = 0; k < CLY_NDW; k++) {
-                        const SubSum sk = lds_get(&C->sum[k]);
-                        if (sk.mode == MODE_NORMAL) { gvalid = 1; G = (int64_t)k * CLY_TS + sk.guess; break; }
-                    }
-                }
-                int64_t X = 0;
-                uint32_t N = 0;
-                int dead = 0;
-                if (lane == 0) {
-                    int64_t e0 = gvalid ? G : -1;
-                    if (!fof) {
-                        const uint64_t st = ds_state(pw0, epoch);
-                        const int64_t ustart = u * CLY_UNIT;
-                        int64_t hx = -1;
-                        if (st == DS_FULL && ds_ok(pw2, epoch) && !ds_term(pw0)) hx = (int64_t)(pw2 & DS_VAL_MASK);
-                        else if (st == DS_SPEC && ds_ok(pw1, epoch) && ds_gvalid(pw0) && !ds_term(pw0)) hx = (int64_t)(pw1 & DS_VAL_MASK);
-                        if (hx >= ustart && hx < ustart + CLY_UNIT && hx - ustart != e0) {
-                            e0 = hx - ustart; gvalid = 1; G = e0;
-                        }
-                    }
-                    if (gvalid) compose(C, C->ent, F, jb.uoff, smem, false, G, X, N, dead, g);
-                    else {
-                        for (int k = 0; k < CLY_NDW; k++) {
-                            SubEnt o;
-                            o.mode = lds_get(&C->sum[k]).mode == MODE_EMPTY ? MODE_EMPTY : MODE_PASS;
-                            o.entry = 0; o.base = 0; o._pad = 0;
-                            lds_put(&C->ent[k], o);
-                        }
-                    }
-                    lds_st_rel(&C->ent_seq, it + 1);
-                }
-                gvalid = __shfl(gvalid, 0, 64); G = __shfl(G, 0, 64);
-                X = __shfl(X, 0, 64); N = __shfl(N, 0, 64); dead = __shfl(dead, 0, 64);
-                cm.fof = fof; cm.gvalid = gvalid; cm.dead = dead; cm.G = G; cm.X = X; cm.N = N;
-                PROF(2);
-                // the looker's slot it&1 is free once it finished unit it-2
-                if (it >= 2 && !lds_wait_ge(&C->fin_seq, it - 1, g)) return;
-                if (lane == 0) {
-                    lds_put(&C->cmp[it & 1], cm);
-                    st_agent(&desc[u].w[1], ds_tag(epoch, (uint64_t)(u * CLY_UNIT + X)));
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    st_agent(&desc[u].w[0], ds_pack(epoch, DS_SPEC, fof, dead, gvalid, G, N));
-                    lds_st_rel(&C->spec_seq, it + 1);
-                }
-                PROF(3);
-                jb = next;
-            } else {
-                if (it >= 2 && !lds_wait_ge(&C->fin_seq, it - 1, g)) return;
-                if (lane == 0) { lds_put(&C->cmp[it & 1], cm); lds_st_rel(&C->spec_seq, it + 1); }
-                break;
-            }
-        }
-        PROF_FLUSH(12);
-        return;
-    }
+// Tuples of this lane's records into the sub-tile's staging slot (when they fit).
+__device__ __forceinline__ void stage_tuples(const Sub& T, const Lane& L, const Chain& R, cly_tuple* staging) {
+    if (R.mode != MODE_NORMAL || R.cnt > CLY_CAP) return;
+    emit_direct(T, L, (uint64_t)T.chunk * CLY_CAP + L.base, staging, ~0ull, nullptr);
+}
 
-    if (wave == CLY_NDW + 1) {
-        // ================= looker: look-back, final entries, FULL =================
-        PROF_INIT();
-        DevEnv env;
-        env.desc = desc; env.g = g; env.epoch = epoch; env.spins = 0; env.nunits = nunits;
-        for (int it = 0;; it++) {
-            if (!lds_wait_ge(&C->spec_seq, it + 1, g)) return;
-            const Cmp cm = lds_get(&C->cmp[it & 1]);
-            if (cm.unit < 0) break;
-            PROF(6);
-            const int64_t u = cm.unit;
-            const DevFile F = files[cm.fidx];
-            LbState lb;
-            lookback(env, u, cm.fof, lane, lb);
-            PROF(7);
-            if (env.spins > LB_SPIN_MAX) lb.dead = 1;
-            const int64_t ustart = u * CLY_UNIT;
-            CLY_LDS SubEnt* fin = C->fin[it & 1];
-            int64_t Xf = cm.X;
-            uint32_t Nf = cm.N;
-            int deadf = cm.dead;
-            if (lane == 0) {
-                if (lb.dead) {
-                    Nf = 0; deadf = 1; Xf = 0;
-                    for (int k = 0; k < CLY_NDW; k++) {
-                        SubEnt o; o.entry = 0; o.base = 0; o._pad = 0;
-                        o.mode = lds_get(&C->ent[k]).mode == MODE_EMPTY ? MODE_EMPTY : MODE_DEAD;
-                        lds_put(&fin[k], o);
-                    }
-                } else if (cm.gvalid && lb.E == ustart + cm.G) {
-                    for (int k = 0; k < CLY_NDW; k++) lds_put(&fin[k], lds_get(&C->ent[k]));
-                } else if (lb.E - ustart >= CLY_UNIT) {
-                    Nf = 0; deadf = 0; Xf = lb.E - ustart;
-                    for (int k = 0; k < CLY_NDW; k++) {
-                        SubEnt o; o.entry = 0; o.base = 0; o._pad = 0;
-                        o.mode = lds_get(&C->ent[k]).mode == MODE_EMPTY ? MODE_EMPTY : MODE_PASS;
-                        lds_put(&fin[k], o);
-                    }
-                } else {
-                    // wrong guess: recompose from the true entry, walking HBM (rare)
-                    atomicAdd(&g->redo_units, 1u);
-                    compose(C, fin, F, cm.uoff, smem, true, lb.E - ustart, Xf, Nf, deadf, g);
-                }
-                const uint64_t incl = lb.P + Nf;
-                st_agent(&desc[u].w[2], ds_tag(epoch, (uint64_t)(ustart + Xf)));
-                st_agent(&desc[u].w[3], ds_tag(epoch, incl));
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                st_agent(&desc[u].w[0], ds_pack(epoch, DS_FULL, cm.fof, deadf, 0, 0, Nf));
-                if (u == nunits - 1) g->total = incl;
-                unit_P[u] = lb.P;
-                C->P[it & 1] = lb.P;
-                lds_st_rel(&C->fin_seq, it + 1);
-            }
-            PROF(8);
-        }
-        PROF_FLUSH(12);
-        return;
-    }
+__device__ __forceinline__ SubDesc make_desc(const Sub& T, const Chain& R) {
+    SubDesc d;
+    d.mode = (uint8_t)R.mode;
+    d.cnt = R.mode == MODE_NORMAL ? R.cnt : 0;
+    d.entry = (int16_t)(R.mode == MODE_NORMAL ? R.E : -1);
+    d.x = (R.mode == MODE_NORMAL && !R.term) ? T.chunk * (int64_t)CLY_TS + R.xrel : 0;
+    d.flags = (uint8_t)(((R.mode == MODE_NORMAL && R.term) ? SD_TERM : 0) | (T.fof ? SD_FOF : 0) |
+                        (d.cnt > CLY_CAP ? SD_OVF : 0));
+    return d;
+}
 
-    // ================= data wave =================
-    const int k = wave;
-    CLY_LDS uint32_t* w32 = (CLY_LDS uint32_t*)(smem + LDS_WIN + k * CLY_WIN);
-    CLY_LDS u32x2* pool = (CLY_LDS u32x2*)(smem + LDS_POOL + k * CP_POOL * 8);
+// One sub-tile, start to end, for a chain given by (mode, entry) or, mode < 0,
+// by its own guess (mode -2: test mode, odd sub-tiles take a wrong guess).
+__device__ __forceinline__ void process_sub(int64_t sidx, int mode, int entry, const DevFile& F, int lane,
+                                            CLY_LDS uint8_t* smem, CLY_LDS uint32_t* w32, CLY_LDS u32x2* pool,
+                                            SubDesc* descs, ChunkSum* sums, cly_tuple* staging, Globals* g,
+                                            int prof_base, SubDesc& d) {
     PROF_INIT();
-    bool pending_dma = false;
-    for (int it = 0;; it++) {
-        if (!lds_wait_ge(&C->job_seq, it + 1, g)) return;
-        const Job jb = lds_get(&C->job[it & 1]);
-        if (jb.unit < 0) break;
-        PROF(0);
-        const DevFile F = files[jb.fidx];
-        Sub T;
-        sub_setup(T, jb, F, k, w32);
-        const bool empty = T.nrel <= 0 && !T.fof;
-        Spec sp;
-        sp.s = -1; sp.last = -1; sp.c = 0; sp.x = 0;
-        Lane L;
-        Chain R;
-        chain_none(L, R, MODE_PASS);
-        int guess = -1;
-        if (!empty) {
-            if (!pending_dma) { if (stage(T, lane, w32)) stage_wait(); }
-            else stage_wait();
-            PROF(1);
-            sub_spec(T, lane, sp, guess);
-            PROF(2);
-            if (guess >= 0) resolve(T, sp, lane, guess, L, R);
-            PROF(3);
-        }
-        pending_dma = false;
-        if (lane == 0) {
-            SubSum ss;
-            ss.mode = empty ? MODE_EMPTY : (guess >= 0 ? MODE_NORMAL : MODE_PASS);
-            ss.guess = guess;
-            ss.exit = R.xrel;
-            ss.cnt = R.cnt;
-            ss.term = R.term;
-            lds_put(&C->sum[k], ss);
-            lds_st_rel(&C->sum_seq[k], it + 1);
-        }
-        if (!lds_wait_ge(&C->ent_seq, it + 1, g)) return;
-        PROF(4);
-        const SubEnt e = lds_get(&C->ent[k]);
-        if (!empty) {
-            if (e.mode == MODE_NORMAL ? !(guess >= 0 && e.entry == guess) : true) sub_chain(T, sp, lane, e.mode, e.entry, L, R);
-            sub_crc(T, L, R, lane, smem, pool, e.base, sums, g);
-        }
-        PROF(5);
-        if (!lds_wait_ge(&C->fin_seq, it + 1, g)) return;
-        PROF(6);
-        const SubEnt f = lds_get(&C->fin[it & 1][k]);
-        const uint64_t P = C->P[it & 1];
-        if (!empty) {
-            if (f.mode != e.mode || (f.mode == MODE_NORMAL && f.entry != e.entry) || (flags & FLAG_FORCE_REDO)) {
-                sub_chain(T, sp, lane, f.mode, f.entry, L, R);
-                sub_crc(T, L, R, lane, smem, pool, f.base, sums, g);
-            } else if (f.base != e.base && lane == 0) {
-                // same chain, but the unit was recomposed: only its record base moved
-                ChunkSum* cs = &sums[T.chunk];
-                cs->p_excl = f.base;
-                if (cs->evt_off != EVT_NONE) cs->evt_gidx += (uint64_t)f.base - (uint64_t)e.base;
-            }
-            PROF(7);
-            if (R.mode == MODE_NORMAL) emit_direct(T, L, P + f.base + L.base, out, out_cap, g);
-            PROF(8);
-            if (dbg && lane == 0) {
-                SubDbg d;
-                d.mode = R.mode; d.E = R.E; d.cnt = (int)R.cnt; d.term = R.term; d.tst = R.tst; d.last = R.last;
-                d.lterm = R.lterm; d.eof_exit = R.eof_exit; d.k0 = R.k0; d.guess = guess; d.bad = 0; d.bpos = 0;
-                d.tpos = R.tpos; d.xrel = R.xrel;
-                dbg[T.chunk] = d;
-            }
-        }
-        // stage the next unit's sub-tile now (the window is free)
-        if (!lds_wait_ge(&C->job_seq, it + 2, g)) return;
-        const Job nj = lds_get(&C->job[(it + 1) & 1]);
-        if (nj.unit >= 0) {
-            const DevFile F2 = files[nj.fidx];
-            Sub T2;
-            sub_setup(T2, nj, F2, k, w32);
-            if (T2.nrel > 0 || T2.fof) pending_dma = stage(T2, lane, w32);
-        }
-        PROF(9);
+    Sub T;
+    sub_setup(T, sidx, F, w32);
+    if (stage(T, lane, w32)) stage_wait();
+    PROF(0);
+    Spec sp;
+    int guess = -1;
+    sub_spec(T, lane, sp, guess);
+    PROF(1);
+    Lane L;
+    Chain R;
+    if (mode < 0) {
+        const bool force = mode == -2 && !T.fof && (sidx & 1);     // test mode: wrong guesses
+        mode = guess >= 0 ? MODE_NORMAL : MODE_PASS;
+        entry = guess;
+        if (force) mode = (sidx & 2) ? MODE_DEAD : MODE_PASS;
     }
-    PROF_FLUSH(0);
+    sub_chain(T, sp, lane, mode, entry, L, R);
+    PROF(2);
+    sub_crc(T, L, R, lane, smem, pool, 0, sums, g);
+    PROF(3);
+    stage_tuples(T, L, R, staging);
+    PROF(4);
+    d = make_desc(T, R);
+    if (lane == 0) descs[T.chunk] = d;
+    PROF(5);
+    PROF_FLUSH(prof_base);
+}
+
+__global__ void __launch_bounds__(64 * CLY_NDW)
+k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ sub_prefix, int64_t nsub,
+       SubDesc* descs, ChunkSum* sums, const uint32_t* __restrict__ cols, cly_tuple* staging, Globals* g, int gmode) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
+    init_tables(smem, cols);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    CLY_LDS uint32_t* w32 = (CLY_LDS uint32_t*)(smem + LDS_WIN + wave * CLY_WIN);
+    CLY_LDS u32x2* pool = (CLY_LDS u32x2*)(smem + LDS_POOL + wave * CP_POOL * 8);
+    const int64_t stride = (int64_t)gridDim.x * CLY_NDW;
+    for (int64_t s = (int64_t)blockIdx.x * CLY_NDW + wave; s < nsub; s += stride) {
+        const DevFile F = files[find_file(sub_prefix, nfiles, s)];
+        SubDesc d;
+        process_sub(s, gmode, 0, F, lane, smem, w32, pool, descs, sums, staging, g, 0, d);
+    }
+}
+
+// Re-process the sub-tiles of the fix list from the chain the link gives them,
+// then walk on through the following sub-tiles of the file while the chain
+// stays live and disagrees with what they hold (stopping at a sub-tile of this
+// round's list: its own wave has it).
+__global__ void __launch_bounds__(64 * CLY_NDW)
+k_fix(const DevFile* __restrict__ files, const Fix* fixes, uint32_t nfix, const uint32_t* __restrict__ listed,
+      uint32_t stamp, SubDesc* descs, ChunkSum* sums, const uint32_t* __restrict__ cols, cly_tuple* staging,
+      Globals* g) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
+    init_tables(smem, cols);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    CLY_LDS uint32_t* w32 = (CLY_LDS uint32_t*)(smem + LDS_WIN + wave * CLY_WIN);
+    CLY_LDS u32x2* pool = (CLY_LDS u32x2*)(smem + LDS_POOL + wave * CP_POOL * 8);
+    for (uint32_t i = blockIdx.x * CLY_NDW + wave; i < nfix; i += gridDim.x * CLY_NDW) {
+        const Fix fx = fixes[i];
+        const DevFile F = files[fx.file];
+        const int64_t s_end = (int64_t)F.first_sub + F.nsub;
+        int64_t s = fx.s, x = fx.x_in;
+        int mode = fx.mode, entry = fx.entry;
+        for (;;) {
+            SubDesc d;
+            process_sub(s, mode, entry, F, lane, smem, w32, pool, descs, sums, staging, g, 8, d);
+            if (d.mode == MODE_DEAD || (d.mode == MODE_NORMAL && (d.flags & SD_TERM))) break;
+            if (d.mode == MODE_NORMAL) x = d.x;
+            if (++s >= s_end || listed[s] == stamp) break;
+            const int64_t rel = x - s * (int64_t)CLY_TS;
+            if (rel < 0) { if (lane == 0) atomicOr(&g->fail, 8u); break; }      // cannot happen
+            mode = rel >= CLY_TS ? MODE_PASS : MODE_NORMAL;
+            entry = rel >= CLY_TS ? 0 : (int)rel;
+            const SubDesc n = descs[s];
+            if (n.mode == mode && (mode != MODE_NORMAL || n.entry == entry)) break;
+        }
+    }
+}
+
+// ---- link scan over sub-tiles (three passes of LINK_NT threads x LINK_IT items)
+#define LINK_NT 256
+#define LINK_IT 8
+#define LINK_BLK (LINK_NT * LINK_IT)
+__device__ __forceinline__ LinkAgg link_op(const LinkAgg& a, const LinkAgg& b) {
+    LinkAgg r;
+    #pragma unroll
+    for (int t = 0; t < 2; t++) {
+        const LinkBr& ra = a.br[t];
+        const LinkBr& rb = b.br[ra.set ? ra.term : t];
+        r.br[t].set = ra.set | rb.set;
+        r.br[t].x = rb.set ? rb.x : ra.x;
+        r.br[t].term = rb.set ? rb.term : ra.term;
+        r.br[t].cnt = ra.cnt + rb.cnt;
+    }
+    return r;
+}
+__device__ __forceinline__ LinkAgg link_ident() {
+    LinkAgg e;
+    #pragma unroll
+    for (int t = 0; t < 2; t++) { e.br[t].x = 0; e.br[t].cnt = 0; e.br[t].set = 0; e.br[t].term = 0; }
+    return e;
+}
+__device__ __forceinline__ LinkAgg link_elem(const SubDesc& d) {
+    LinkAgg e = link_ident();
+    if (d.mode == MODE_NORMAL) {
+        const int32_t term = (d.flags & SD_TERM) != 0;
+        e.br[0].set = 1; e.br[0].x = d.x; e.br[0].term = term; e.br[0].cnt = d.cnt;
+        if (d.flags & SD_FOF) e.br[1] = e.br[0];
+    }
+    return e;
+}
+// Exclusive block scan of the threads' aggregates; returns the block total.
+__device__ __forceinline__ LinkAgg link_block_scan(LinkAgg v, LinkAgg& excl) {
+    __shared__ LinkAgg sh[LINK_NT];
+    const int t = threadIdx.x;
+    sh[t] = v;
+    __syncthreads();
+    for (int o = 1; o < LINK_NT; o <<= 1) {
+        LinkAgg u = link_ident();
+        if (t >= o) u = sh[t - o];
+        __syncthreads();
+        if (t >= o) sh[t] = link_op(u, sh[t]);
+        __syncthreads();
+    }
+    excl = t > 0 ? sh[t - 1] : link_ident();
+    const LinkAgg tot = sh[LINK_NT - 1];
+    __syncthreads();
+    return tot;
+}
+
+__global__ void __launch_bounds__(LINK_NT)
+k_link1(const SubDesc* __restrict__ descs, int64_t nsub, LinkAgg* blk) {
+    const int64_t b0 = (int64_t)blockIdx.x * LINK_BLK + (int64_t)threadIdx.x * LINK_IT;
+    LinkAgg v = link_ident();
+    for (int i = 0; i < LINK_IT; i++) if (b0 + i < nsub) v = link_op(v, link_elem(descs[b0 + i]));
+    LinkAgg ex;
+    const LinkAgg tot = link_block_scan(v, ex);
+    if (threadIdx.x == 0) blk[blockIdx.x] = tot;
+}
+
+// One block: exclusive scan of the block aggregates (in place).
+__global__ void __launch_bounds__(LINK_NT)
+k_link2(LinkAgg* blk, int64_t nblk) {
+    const int64_t per = (nblk + LINK_NT - 1) / LINK_NT;
+    const int64_t b0 = (int64_t)threadIdx.x * per;
+    LinkAgg v = link_ident();
+    for (int64_t i = 0; i < per; i++) if (b0 + i < nblk) v = link_op(v, blk[b0 + i]);
+    LinkAgg ex;
+    link_block_scan(v, ex);
+    LinkAgg run = ex;
+    for (int64_t i = 0; i < per; i++) {
+        if (b0 + i < nblk) { const LinkAgg a = blk[b0 + i]; blk[b0 + i] = run; run = link_op(run, a); }
+    }
+}
+
+// Per sub-tile: output slot, and whether its chain is the one the link state
+// implies; if not, a candidate (with the implied chain).  A wrong chain entered
+// live is "harmful" (it misleads the state of what follows): the first harmful
+// sub-tile of each file goes to fh[file].
+__global__ void __launch_bounds__(LINK_NT)
+k_link3(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ sub_prefix,
+        const SubDesc* __restrict__ descs, int64_t nsub, const LinkAgg* __restrict__ blk, uint64_t* sub_P, Fix* cand,
+        uint32_t cand_cap, int32_t* fh, Globals* g) {
+    const int64_t b0 = (int64_t)blockIdx.x * LINK_BLK + (int64_t)threadIdx.x * LINK_IT;
+    LinkAgg v = link_ident();
+    SubDesc d[LINK_IT];
+    for (int i = 0; i < LINK_IT; i++) {
+        if (b0 + i < nsub) { d[i] = descs[b0 + i]; v = link_op(v, link_elem(d[i])); }
+    }
+    LinkAgg ex;
+    link_block_scan(v, ex);
+    LinkAgg run = link_op(blk[blockIdx.x], ex);
+    for (int i = 0; i < LINK_IT; i++) {
+        const int64_t s = b0 + i;
+        if (s >= nsub) break;
+        const LinkBr& st = run.br[1];          // state entering s (sub-tile 0 resets it)
+        sub_P[s] = st.cnt;
+        int mode, entry = 0;
+        int64_t x_in = st.x;
+        bool live = true;
+        if (d[i].flags & SD_FOF) { mode = MODE_NORMAL; entry = 0; x_in = s * (int64_t)CLY_TS; }
+        else if (!st.set) { mode = -1; atomicOr(&g->fail, 6u); }            // cannot happen
+        else if (st.term) { mode = MODE_DEAD; live = false; }
+        else {
+            const int64_t rel = st.x - s * (int64_t)CLY_TS;
+            if (rel >= CLY_TS) mode = MODE_PASS;
+            else if (rel < 0) mode = -1;       // a sub-tile before s is wrong (and a candidate)
+            else { mode = MODE_NORMAL; entry = (int)rel; }
+        }
+        const bool ok = mode >= 0 && d[i].mode == mode && (mode != MODE_NORMAL || d[i].entry == entry);
+        if (!ok) {
+            const uint32_t f = (uint32_t)find_file(sub_prefix, nfiles, s);
+            // harmful: the wrong chain changes the state passed on (PASS and DEAD both pass it through)
+            if (live && mode >= 0 && (mode == MODE_NORMAL || d[i].mode == MODE_NORMAL)) atomicMin(&fh[f], (int32_t)s);
+            const uint32_t k = atomicAdd(&g->ncand, 1u);
+            if (k < cand_cap) {
+                Fix c;
+                c.s = (uint32_t)s; c.mode = mode; c.entry = entry; c.file = f; c.x_in = x_in;
+                cand[k] = c;
+            }
+        }
+        run = link_op(run, link_elem(d[i]));
+        if (s == nsub - 1) g->total = run.br[1].cnt;
+    }
+}
+
+// Fix list of the round: every candidate up to and including the first harmful
+// sub-tile of its file (its state is certain); later candidates only when they
+// hold a wrong record chain (never turned into PASS / DEAD on an uncertain
+// state, which would discard a good guess).
+__global__ void __launch_bounds__(LINK_NT)
+k_link4(const Fix* __restrict__ cand, const int32_t* __restrict__ fh, Fix* fixes, uint32_t* listed, uint32_t stamp,
+        Globals* g) {
+    const uint32_t n = g->ncand;
+    for (uint32_t i = blockIdx.x * LINK_NT + threadIdx.x; i < n; i += gridDim.x * LINK_NT) {
+        const Fix c = cand[i];
+        if (c.mode < 0) continue;
+        const bool certain = (int64_t)c.s <= (int64_t)fh[c.file];
+        if (!certain && c.mode != MODE_NORMAL) continue;
+        listed[c.s] = stamp;
+        fixes[atomicAdd(&g->nfix, 1u)] = c;
+    }
+}
+
+// Staged tuples of every sub-tile to their output slots (one wave per sub-tile);
+// sub-tiles whose tuples did not fit the staging slot are re-read and emitted.
+__global__ void __launch_bounds__(64 * CLY_NDW)
+k_place(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ sub_prefix, int64_t nsub,
+        const SubDesc* __restrict__ descs, const uint64_t* __restrict__ sub_P, const cly_tuple* __restrict__ staging,
+        cly_tuple* out, uint64_t out_cap, Globals* g) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    CLY_LDS uint32_t* w32 = (CLY_LDS uint32_t*)(smem + wave * CLY_WIN);
+    const int64_t stride = (int64_t)gridDim.x * CLY_NDW;
+    for (int64_t s = (int64_t)blockIdx.x * CLY_NDW + wave; s < nsub; s += stride) {
+        const SubDesc d = descs[s];
+        if (d.mode != MODE_NORMAL || d.cnt == 0) continue;
+        const uint64_t P = sub_P[s];
+        if (!(d.flags & SD_OVF)) {
+            const u32x4* src = (const u32x4*)(staging + (uint64_t)s * CLY_CAP);
+            u32x4* dst = (u32x4*)(out + P);
+            const uint32_t nq = d.cnt * 3;
+            const uint64_t lim = P + d.cnt <= out_cap ? nq : (out_cap > P ? (out_cap - P) * 3 : 0);
+            for (uint32_t q = lane; q < nq; q += 64) if (q < lim) dst[q] = src[q];
+            if (lim < nq && lane == 0) atomicOr(&g->overflow, 1u);
+        } else {
+            const DevFile F = files[find_file(sub_prefix, nfiles, s)];
+            Sub T;
+            sub_setup(T, s, F, w32);
+            if (stage(T, lane, w32)) stage_wait();
+            Spec sp;
+            int guess = -1;
+            sub_spec(T, lane, sp, guess);
+            Lane L;
+            Chain R;
+            sub_chain(T, sp, lane, MODE_NORMAL, d.entry, L, R);
+            emit_direct(T, L, P + L.base, out, out_cap, g);
+        }
+    }
 }
 
 // One workgroup per file: first event of the file.
 #define FIN_NT 256
 __global__ void __launch_bounds__(FIN_NT)
-k_fin(const DevFile* __restrict__ files, const ChunkSum* __restrict__ sums, const uint64_t* __restrict__ unit_P,
+k_fin(const DevFile* __restrict__ files, const ChunkSum* __restrict__ sums, const uint64_t* __restrict__ sub_P,
       const uint32_t* __restrict__ x8n, FileOut* __restrict__ fout) {
     const int f = blockIdx.x, tid = threadIdx.x;
     const DevFile F = files[f];
-    const int64_t c0 = (int64_t)F.first_unit * CLY_NDW, nc = F.nsub;
+    const int64_t c0 = (int64_t)F.first_sub, nc = F.nsub;
     __shared__ int64_t r_off[FIN_NT];
     __shared__ uint64_t r_g[FIN_NT];
     __shared__ int32_t r_st[FIN_NT];
@@ -1460,7 +1310,7 @@ k_fin(const DevFile* __restrict__ files, const ChunkSum* __restrict__ sums, cons
     for (int64_t i = tid; i < nc; i += FIN_NT) {
         uint64_t gi = 0;
         int32_t st = 0;
-        const int64_t o = fin_chunk_event(sums, unit_P, x8n, c0, nc, i, &gi, &st);
+        const int64_t o = fin_chunk_event(sums, sub_P, x8n, c0, nc, i, &gi, &st);
         if (o < best) { best = o; bg = gi; bs = st; }
     }
     r_off[tid] = best; r_g[tid] = bg; r_st[tid] = bs;
@@ -1473,7 +1323,7 @@ k_fin(const DevFile* __restrict__ files, const ChunkSum* __restrict__ sums, cons
     }
     if (tid == 0) {
         FileOut fo;
-        const uint64_t first = unit_P[F.first_unit] + sums[c0].p_excl;
+        const uint64_t first = sub_P[c0];
         fo.first_index = first;
         fo.ok = r_off[0] != EVT_NONE;
         fo.n_records = fo.ok ? r_g[0] - first : 0;
@@ -1495,8 +1345,17 @@ struct cly_ctx {
     DevFile* d_files; int cap_files;
     uint32_t* d_prefix;
     FileOut* d_fout;
-    Desc* d_desc; int64_t cap_units;
+    int64_t cap_subs;
+    SubDesc* d_desc;
     ChunkSum* d_sums;
+    uint64_t* d_subP;
+    cly_tuple* d_staging;
+    LinkAgg* d_blk;
+    Fix* d_fix;                  // fix list of a round
+    Fix* d_cand;                 // candidates of a round
+    uint32_t* d_listed;          // per sub-tile: stamp of the last round that listed it
+    int32_t* d_fh;               // per file: first harmful sub-tile of a round
+    uint32_t stamp;
     Globals* d_g;
     uint32_t* d_cols;            // columns of A^(SUB*2^k) (Kogge-Stone) and A^(4w) (head shifts)
     uint32_t* d_x8n;
@@ -1504,12 +1363,10 @@ struct cly_ctx {
     uint32_t* h_prefix;
     FileOut* h_fout;
     Globals* h_g;
-    uint32_t epoch; int desc_fresh;
     int scan_grid;
     uint8_t* d_bytes; uint64_t cap_bytes;          // host-path staging
-    SubDbg* d_dbg; int dbg_on;
-    uint64_t* d_unitP;
     cly_tuple* d_tuples; uint64_t cap_tuples;
+    int dbg_flags;
 };
 
 extern "C" int cly_ctx_create(int device, cly_ctx** out) {
@@ -1547,9 +1404,12 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     HIPCK(hipMemcpy(c->d_x8n, hx, x8_bytes, hipMemcpyHostToDevice));
     free(hx);
     HIPCK(hipFuncSetAttribute((const void*)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CLY_SCAN_LDS));
+    HIPCK(hipFuncSetAttribute((const void*)k_fix, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CLY_SCAN_LDS));
+    HIPCK(hipFuncSetAttribute((const void*)k_place, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(CLY_NDW * CLY_WIN)));
     {
         int per_cu = 0, ncu = 0;
-        HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_scan, 64 * WAVES_PER_WG, CLY_SCAN_LDS));
+        HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_scan, 64 * CLY_NDW, CLY_SCAN_LDS));
         HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
         if (per_cu < 1) per_cu = 1;
         c->scan_grid = per_cu * ncu;
@@ -1562,8 +1422,9 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
-    hipFree(c->d_files); hipFree(c->d_prefix); hipFree(c->d_fout); hipFree(c->d_desc); hipFree(c->d_sums); hipFree(c->d_dbg); hipFree(c->d_unitP);
-    hipFree(c->d_g); hipFree(c->d_cols); hipFree(c->d_x8n); hipFree(c->d_bytes); hipFree(c->d_tuples);
+    hipFree(c->d_files); hipFree(c->d_prefix); hipFree(c->d_fout); hipFree(c->d_desc); hipFree(c->d_sums);
+    hipFree(c->d_subP); hipFree(c->d_staging); hipFree(c->d_blk); hipFree(c->d_fix); hipFree(c->d_cand);
+    hipFree(c->d_listed); hipFree(c->d_fh); hipFree(c->d_g); hipFree(c->d_cols); hipFree(c->d_x8n); hipFree(c->d_bytes); hipFree(c->d_tuples);
     hipHostFree(c->h_files); hipHostFree(c->h_prefix); hipHostFree(c->h_fout); hipHostFree(c->h_g);
     for (int i = 0; i < 4; i++) hipEventDestroy(c->ev[i]);
     hipStreamDestroy(c->stream);
@@ -1578,9 +1439,10 @@ extern "C" uint64_t cly_scan_capacity(const cly_file* files, int nfiles) {
 
 static int ensure_files(cly_ctx* c, int nfiles) {
     if (nfiles <= c->cap_files) return CLY_OK;
-    hipFree(c->d_files); hipFree(c->d_prefix); hipFree(c->d_fout);
+    hipFree(c->d_files); hipFree(c->d_prefix); hipFree(c->d_fout); hipFree(c->d_fh);
     hipHostFree(c->h_files); hipHostFree(c->h_prefix); hipHostFree(c->h_fout);
     const int cap = nfiles < 64 ? 64 : nfiles;
+    HIPCK(hipMalloc(&c->d_fh, sizeof(int32_t) * cap));
     HIPCK(hipMalloc(&c->d_files, sizeof(DevFile) * cap));
     HIPCK(hipMalloc(&c->d_prefix, sizeof(uint32_t) * (cap + 1)));
     HIPCK(hipMalloc(&c->d_fout, sizeof(FileOut) * cap));
@@ -1591,20 +1453,26 @@ static int ensure_files(cly_ctx* c, int nfiles) {
     return CLY_OK;
 }
 
-static int ensure_units(cly_ctx* c, int64_t nunits) {
-    if (nunits <= c->cap_units) return CLY_OK;
-    hipFree(c->d_desc); hipFree(c->d_sums);
-    const int64_t cap = nunits < 1024 ? 1024 : nunits;
-    HIPCK(hipMalloc(&c->d_desc, sizeof(Desc) * cap));
-    c->desc_fresh = 1;
-    HIPCK(hipMalloc(&c->d_sums, sizeof(ChunkSum) * cap * CLY_NDW));
-    hipFree(c->d_dbg);
-    HIPCK(hipMalloc(&c->d_dbg, sizeof(SubDbg) * cap * CLY_NDW));
-    hipFree(c->d_unitP);
-    HIPCK(hipMalloc(&c->d_unitP, sizeof(uint64_t) * cap));
-    c->cap_units = cap;
+static int ensure_subs(cly_ctx* c, int64_t nsub) {
+    if (nsub <= c->cap_subs) return CLY_OK;
+    hipFree(c->d_desc); hipFree(c->d_sums); hipFree(c->d_subP); hipFree(c->d_staging); hipFree(c->d_blk);
+    hipFree(c->d_fix); hipFree(c->d_cand); hipFree(c->d_listed);
+    const int64_t cap = nsub < 1024 ? 1024 : nsub;
+    HIPCK(hipMalloc(&c->d_desc, sizeof(SubDesc) * cap));
+    HIPCK(hipMalloc(&c->d_sums, sizeof(ChunkSum) * cap));
+    HIPCK(hipMalloc(&c->d_subP, sizeof(uint64_t) * cap));
+    HIPCK(hipMalloc(&c->d_staging, sizeof(cly_tuple) * CLY_CAP * cap));
+    HIPCK(hipMalloc(&c->d_blk, sizeof(LinkAgg) * (cap / LINK_BLK + 2)));
+    HIPCK(hipMalloc(&c->d_fix, sizeof(Fix) * cap));
+    HIPCK(hipMalloc(&c->d_cand, sizeof(Fix) * cap));
+    HIPCK(hipMalloc(&c->d_listed, sizeof(uint32_t) * cap));
+    HIPCK(hipMemset(c->d_listed, 0, sizeof(uint32_t) * cap));
+    c->stamp = 0;
+    c->cap_subs = cap;
     return CLY_OK;
 }
+
+#define FIX_ROUNDS 64
 
 extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple* d_out, uint64_t out_cap,
                                uint64_t* file_first, cly_file_result* res, uint64_t* needed, cly_stats* stats,
@@ -1615,55 +1483,93 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     hipStream_t st = stream_v ? (hipStream_t)stream_v : c->stream;
     int rc = ensure_files(c, nfiles);
     if (rc) return rc;
-    int64_t nunits = 0;
-    uint64_t bytes = 0, nsub_total = 0;
+    int64_t nsub = 0;
+    uint64_t bytes = 0;
     for (int i = 0; i < nfiles; i++) {
         if (files[i].len >= (1ULL << 32)) return CLY_ERR_ARG;
         if (files[i].len && (((uintptr_t)files[i].base) & 15)) return CLY_ERR_ARG;
-        const uint64_t nu = files[i].len ? (files[i].len + CLY_UNIT - 1) / CLY_UNIT : 1;
         const uint64_t ns = files[i].len ? (files[i].len + CLY_TS - 1) / CLY_TS : 1;
         c->h_files[i].base = files[i].base;
         c->h_files[i].len = files[i].len;
         c->h_files[i].fid = files[i].fid;
-        c->h_files[i].first_unit = (uint32_t)nunits;
+        c->h_files[i].first_sub = (uint32_t)nsub;
         c->h_files[i].nsub = (uint32_t)ns;
         c->h_files[i]._pad = 0;
-        c->h_prefix[i] = (uint32_t)nunits;
-        nunits += (int64_t)nu;
-        nsub_total += ns;
+        c->h_prefix[i] = (uint32_t)nsub;
+        nsub += (int64_t)ns;
         bytes += files[i].len;
     }
-    if (nunits >= (1LL << 31) / CLY_NDW) return CLY_ERR_ARG;
-    c->h_prefix[nfiles] = (uint32_t)nunits;
-    rc = ensure_units(c, nunits);
+    if (nsub >= (1LL << 31)) return CLY_ERR_ARG;
+    c->h_prefix[nfiles] = (uint32_t)nsub;
+    rc = ensure_subs(c, nsub);
     if (rc) return rc;
     HIPCK(hipMemcpyAsync(c->d_files, c->h_files, sizeof(DevFile) * nfiles, hipMemcpyHostToDevice, st));
     HIPCK(hipMemcpyAsync(c->d_prefix, c->h_prefix, sizeof(uint32_t) * (nfiles + 1), hipMemcpyHostToDevice, st));
-    // descriptor words are tagged with the call epoch: zero them only when the
-    // 16-bit epoch wraps (or the buffer is new)
-    if (++c->epoch > 0xffff || c->desc_fresh) {
-        if (c->epoch > 0xffff) c->epoch = 1;
-        c->desc_fresh = 0;
-        HIPCK(hipMemsetAsync(c->d_desc, 0, sizeof(Desc) * c->cap_units, st));
-    }
     HIPCK(hipMemsetAsync(c->d_g, 0, sizeof(Globals), st));
+    const int64_t nblk = (nsub + LINK_BLK - 1) / LINK_BLK;
     HIPCK(hipEventRecord(c->ev[0], st));
     int grid = c->scan_grid;
-    if ((int64_t)grid > nunits) grid = (int)nunits;
-    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * WAVES_PER_WG), CLY_SCAN_LDS, st, c->d_files, nfiles, c->d_prefix,
-                       nunits, c->d_desc, c->d_sums, c->d_unitP, c->d_cols, d_out, out_cap, c->d_g, c->epoch,
-                       c->dbg_on ? c->d_dbg : nullptr, c->dbg_on > 1 ? FLAG_FORCE_REDO : 0);
+    if ((int64_t)grid * CLY_NDW > nsub) grid = (int)((nsub + CLY_NDW - 1) / CLY_NDW);
+    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * CLY_NDW), CLY_SCAN_LDS, st, c->d_files, nfiles, c->d_prefix, nsub,
+                       c->d_desc, c->d_sums, c->d_cols, c->d_staging, c->d_g, (c->dbg_flags & 2) ? -2 : -1);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[1], st));
-    hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_sums, c->d_unitP, c->d_x8n, c->d_fout);
-    HIPCK(hipGetLastError());
+    // link scan, then fix rounds until every sub-tile holds the chain its state implies
+    uint32_t rounds = 0, fixes = 0;
+    for (;;) {
+        const uint32_t stamp = ++c->stamp;
+        HIPCK(hipMemsetAsync(&c->d_g->nfix, 0, sizeof(uint32_t), st));
+        HIPCK(hipMemsetAsync(&c->d_g->ncand, 0, sizeof(uint32_t), st));
+        HIPCK(hipMemsetAsync(c->d_fh, 0x7f, sizeof(int32_t) * nfiles, st));
+        hipLaunchKernelGGL(k_link1, dim3(nblk), dim3(LINK_NT), 0, st, c->d_desc, nsub, c->d_blk);
+        hipLaunchKernelGGL(k_link2, dim3(1), dim3(LINK_NT), 0, st, c->d_blk, nblk);
+        hipLaunchKernelGGL(k_link3, dim3(nblk), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_prefix, c->d_desc, nsub,
+                           c->d_blk, c->d_subP, c->d_cand, (uint32_t)c->cap_subs, c->d_fh, c->d_g);
+        hipLaunchKernelGGL(k_link4, dim3(64), dim3(LINK_NT), 0, st, c->d_cand, c->d_fh, c->d_fix, c->d_listed, stamp,
+                           c->d_g);
+        HIPCK(hipGetLastError());
+        HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
+        HIPCK(hipStreamSynchronize(st));
+        const uint32_t ncand = c->h_g->ncand, nfix = c->h_g->nfix;
+        if (c->h_g->fail) break;
+        if (ncand == 0) break;
+        if (++rounds > FIX_ROUNDS || nfix == 0) {
+            fprintf(stderr, "clyscan: chain resolution did not converge (%u candidates, %u fixes)\n", ncand, nfix);
+            return CLY_ERR_NOREPAIR;
+        }
+        fixes += nfix;
+        if (c->dbg_flags & 4) {                          // debug trace of the fix rounds
+            Fix hf[8];
+            const uint32_t nshow = nfix < 8 ? nfix : 8;
+            HIPCK(hipMemcpy(hf, c->d_fix, sizeof(Fix) * nshow, hipMemcpyDeviceToHost));
+            fprintf(stderr, "round %u: %u candidates, %u fixes:", rounds, ncand, nfix);
+            for (uint32_t k = 0; k < nshow; k++) {
+                SubDesc d;
+                HIPCK(hipMemcpy(&d, c->d_desc + hf[k].s, sizeof(SubDesc), hipMemcpyDeviceToHost));
+                fprintf(stderr, " [s=%u want %d/%d have %d/%d cnt %u]", hf[k].s, hf[k].mode, hf[k].entry, d.mode,
+                        d.entry, d.cnt);
+            }
+            fprintf(stderr, "\n");
+        }
+        int fgrid = (int)((nfix + CLY_NDW - 1) / CLY_NDW);
+        if (fgrid > c->scan_grid) fgrid = c->scan_grid;
+        hipLaunchKernelGGL(k_fix, dim3(fgrid), dim3(64 * CLY_NDW), CLY_SCAN_LDS, st, c->d_files, c->d_fix, nfix,
+                           c->d_listed, stamp, c->d_desc, c->d_sums, c->d_cols, c->d_staging, c->d_g);
+        HIPCK(hipGetLastError());
+    }
     HIPCK(hipEventRecord(c->ev[2], st));
+    hipLaunchKernelGGL(k_place, dim3(c->scan_grid), dim3(64 * CLY_NDW), CLY_NDW * CLY_WIN, st, c->d_files, nfiles,
+                       c->d_prefix, nsub, c->d_desc, c->d_subP, c->d_staging, d_out, out_cap, c->d_g);
+    hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_sums, c->d_subP, c->d_x8n, c->d_fout);
+    HIPCK(hipGetLastError());
+    HIPCK(hipEventRecord(c->ev[3], st));
     HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(c->h_fout, c->d_fout, sizeof(FileOut) * nfiles, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
-    float ms_scan = 0, ms_fin = 0;
+    float ms_scan = 0, ms_link = 0, ms_tail = 0;
     HIPCK(hipEventElapsedTime(&ms_scan, c->ev[0], c->ev[1]));
-    HIPCK(hipEventElapsedTime(&ms_fin, c->ev[1], c->ev[2]));
+    HIPCK(hipEventElapsedTime(&ms_link, c->ev[1], c->ev[2]));
+    HIPCK(hipEventElapsedTime(&ms_tail, c->ev[2], c->ev[3]));
     if (c->h_g->lb_timeout || c->h_g->fail) {
         fprintf(stderr, "clyscan: internal error (timeout %u, invariant %u)\n", c->h_g->lb_timeout, c->h_g->fail);
         return CLY_ERR_DEVICE;
@@ -1679,10 +1585,11 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         total += c->h_fout[i].n_records;
     }
     if (needed) *needed = c->h_g->total;
+    c->h_g->fix_total = fixes;
     if (stats) {
-        stats->scan_ms = ms_scan; stats->resolve_ms = ms_fin; stats->total_ms = ms_scan + ms_fin;
-        stats->passes = 1 + (c->h_g->redo_units ? 1 : 0);
-        stats->n_chunks = (uint32_t)nsub_total; stats->bytes = bytes; stats->records = total;
+        stats->scan_ms = ms_scan; stats->resolve_ms = ms_link + ms_tail; stats->total_ms = ms_scan + ms_link + ms_tail;
+        stats->passes = 1 + rounds;
+        stats->n_chunks = (uint32_t)nsub; stats->bytes = bytes; stats->records = total;
     }
     if (c->h_g->overflow || c->h_g->total > out_cap) return CLY_ERR_CAPACITY;
     return CLY_OK;
@@ -1747,25 +1654,25 @@ extern "C" int cly_dbg_sums(cly_ctx* c, void* out, int n) {
     return n;
 }
 extern "C" int cly_dbg_sumsize(void) { return (int)sizeof(ChunkSum); }
-extern "C" int cly_dbg_enable(cly_ctx* c, int on) { c->dbg_on = on; return 0; }
-extern "C" int cly_dbg_unitp(cly_ctx* c, uint64_t* out, int n) {
+extern "C" int cly_dbg_descs(cly_ctx* c, void* out, int n) {
     HIPCK(hipDeviceSynchronize());
-    HIPCK(hipMemcpy(out, c->d_unitP, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
+    HIPCK(hipMemcpy(out, c->d_desc, sizeof(SubDesc) * n, hipMemcpyDeviceToHost));
     return n;
 }
-extern "C" int cly_dbg_subs(cly_ctx* c, void* out, int n) {
+extern "C" int cly_dbg_subp(cly_ctx* c, uint64_t* out, int n) {
     HIPCK(hipDeviceSynchronize());
-    HIPCK(hipMemcpy(out, c->d_dbg, sizeof(SubDbg) * n, hipMemcpyDeviceToHost));
+    HIPCK(hipMemcpy(out, c->d_subP, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
     return n;
+}
+extern "C" int cly_dbg_stats(cly_ctx* c, uint32_t* out4) {
+    out4[0] = c->h_g->fix_total; out4[1] = 0; out4[2] = c->scan_grid; out4[3] = CLY_SCAN_LDS;
+    return 4;
 }
 extern "C" int cly_dbg_prof(cly_ctx* c, uint64_t* out24) {
     for (int i = 0; i < 24; i++) out24[i] = c->h_g->prof[i];
     return 24;
 }
-extern "C" int cly_dbg_stats(cly_ctx* c, uint32_t* out4) {
-    out4[0] = c->h_g->redo_units; out4[1] = c->h_g->redo_subs; out4[2] = c->scan_grid; out4[3] = CLY_SCAN_LDS;
-    return 4;
-}
+extern "C" int cly_dbg_enable(cly_ctx* c, int on) { c->dbg_flags = on; return 0; }
 
 extern "C" const char* cly_strerror(int code) {
     switch (code) {
@@ -1786,7 +1693,7 @@ extern "C" const char* cly_strerror(int code) {
 
 extern "C" const char* cly_build_info(void) {
     static char buf[200];
-    snprintf(buf, sizeof(buf), "clyscan gfx950 SUB=%d NDW=%d TS=%d UNIT=%d LDS=%d tables=16x", CLY_SUB, CLY_NDW, CLY_TS,
-             (int)CLY_UNIT, (int)CLY_SCAN_LDS);
+    snprintf(buf, sizeof(buf), "clyscan gfx950 SUB=%d WAVES=%d TS=%d CAP=%d LDS=%d tables=16x", CLY_SUB, CLY_NDW, CLY_TS,
+             CLY_CAP, (int)CLY_SCAN_LDS);
     return buf;
 }

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Quick GPU parity check of both geometries (fixtures + random corpora, normal and
-# forced-redo paths), then an optional bench.
+# forced wrong-guess paths), then an optional bench.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out

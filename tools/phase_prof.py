@@ -1,5 +1,5 @@
-"""Per-phase cycle breakdown of k_scan (profiling build libclyscan_prof.so) on a
-bench workload: python tools/phase_prof.py [c1|c2|c3]"""
+"""Per-phase cycle breakdown of k_scan / k_fix (profiling build
+libclyscan_prof.so) on a bench workload: python tools/phase_prof.py [c1|c2|c3]"""
 import ctypes
 import os
 import sys
@@ -15,9 +15,7 @@ wl = make_workload(cfg, torch)
 sc = Scanner(0, lib="libclyscan_prof.so")
 sc.lib.cly_dbg_prof.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 sc.lib.cly_dbg_stats.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-dnames = ["wait job", "stage", "filter+spec", "resolve(guess)", "wait ent", "crc", "wait fin", "redo", "emit",
-          "locate+summary"]
-cnames = ["wait summaries", "take ticket", "compose+SPEC", "look-back", "final+FULL"]
+names = ["stage", "filter+spec", "resolve", "crc+summary", "stage tuples", "desc"]
 for it in range(3):
     first, res, st, need = sc.scan_device(wl.dev_files, wl.d_out.data_ptr(), wl.out_cap)
     pr = (ctypes.c_uint64 * 24)()
@@ -25,13 +23,10 @@ for it in range(3):
     s4 = (ctypes.c_uint32 * 4)()
     sc.lib.cly_dbg_stats(sc.ctx, s4)
     nsub = st.n_chunks
-    nunits = sum((ln + 73727) // 73728 for (_, ln, _) in wl.dev_files)
-    print("iter %d: k_scan %.3f ms, %d sub-tiles, %d units, redo_units %d redo_subs %d grid %d" % (
-        it, st.scan_ms, nsub, nunits, s4[0], s4[1], s4[2]), flush=True)
-    tot = sum(pr[i] for i in range(10))
-    for i, n in enumerate(dnames):
-        print("   data  %-16s %9.0f cyc/sub-tile  %5.1f%%" % (n, pr[i] / nsub, 100.0 * pr[i] / max(tot, 1)), flush=True)
-    tot = sum(pr[12 + i] for i in range(5))
-    for i, n in enumerate(cnames):
-        print("   coord %-16s %9.0f cyc/unit      %5.1f%%" % (n, pr[12 + i] / nunits, 100.0 * pr[12 + i] / max(tot, 1)),
-              flush=True)
+    print("iter %d: k_scan %.3f ms, link+place+fin %.3f ms, %d sub-tiles, %d fixes, passes %d, grid %d" % (
+        it, st.scan_ms, st.resolve_ms, nsub, s4[0], st.passes, s4[2]), flush=True)
+    for base, kname, n in ((0, "scan", nsub), (8, "fix", max(s4[0], 1))):
+        tot = sum(pr[base + i] for i in range(6))
+        for i, nm in enumerate(names):
+            print("   %-4s %-14s %9.0f cyc/sub-tile  %5.1f%%" % (kname, nm, pr[base + i] / n, 100.0 * pr[base + i] / max(tot, 1)),
+                  flush=True)
