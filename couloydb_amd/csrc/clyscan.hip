@@ -86,15 +86,16 @@ struct FileOut {
 //   [65536, +256)     inverse of a zero-byte step (top byte of T0 -> index)
 //   [LDS_WIN + k*WIN) window of wave k (sub-tile + halo, zero past the file end)
 //   [LDS_POOL ...)    per-wave check-point pools
-//   [LDS_KSCOL ...)   columns of the Kogge-Stone and word shifts
+//   [LDS_KSNIB ...)   nibble tables of the Kogge-Stone shifts A^(SUB*2^k): 8 x 16 words each
+//   [LDS_HSCOL ...)   columns of the word shifts A^(4w)
 #define LDS_TAB 0
 #define LDS_INV 65536
 #define LDS_WIN (LDS_INV + 256)
 #define LDS_POOL (LDS_WIN + CLY_NDW * CLY_WIN)
-#define LDS_KSCOL (LDS_POOL + CLY_NDW * 192 * 8)              // 6 x 32 columns of A^(SUB*2^k)
-#define LDS_HSCOL (LDS_KSCOL + CLY_KS_LEVELS * 32 * 4)          // NWD x 32 columns of A^(4*w)
+#define LDS_KSNIB (LDS_POOL + CLY_NDW * 192 * 8)
+#define LDS_HSCOL (LDS_KSNIB + CLY_KS_LEVELS * 128 * 4)
 #define CLY_SCAN_LDS (LDS_HSCOL + CLY_NWD * 32 * 4)
-#define CLY_COLS ((CLY_KS_LEVELS + CLY_NWD) * 32)                // words of the column table
+#define CLY_COLS (CLY_KS_LEVELS * 128 + CLY_NWD * 32)            // words of the shift tables
 
 // Per-sub-tile result of k_scan / k_fix, read by the link scan (16 B).
 struct SubDesc {
@@ -251,6 +252,15 @@ __device__ __forceinline__ uint32_t col_mul(const CLY_LDS uint8_t* smem, int col
     return p;
 }
 
+// A^(SUB*2^lvl) v by nibble tables: 8 lookups
+__device__ __forceinline__ uint32_t ks_mul(const CLY_LDS uint8_t* smem, int lvl, uint32_t v) {
+    const CLY_LDS uint32_t* t = (const CLY_LDS uint32_t*)(smem + LDS_KSNIB) + lvl * 128;
+    uint32_t p = 0;
+    #pragma unroll
+    for (int n = 0; n < 8; n++) p ^= t[n * 16 + ((v >> (4 * n)) & 15u)];
+    return p;
+}
+
 // ---------------------------------------------------------------------------
 // Header decode at window position p: fast path for headers whose three
 // varints are at most 4 bytes each and end within bytes 6..13 (every record
@@ -312,10 +322,21 @@ __device__ __forceinline__ Hdr hdr_at(const CLY_LDS uint32_t* w32, int p, int64_
 // Header at a position beyond the staged window (exit check of a long record):
 // read from global memory.
 __device__ __noinline__ void hdr_global(const uint8_t* gfile, int64_t cbase, int64_t x, int64_t nrel, Hdr& h) {
+    // bytes [x, x+26) from the dwords covering them (never past the file's last dword)
+    uint32_t wv[8];
+    const int64_t a = cbase + x, a0 = a & ~3ll;
+    const int64_t flen = cbase + nrel;
+    const uint32_t* gw = (const uint32_t*)(gfile + a0);
+    #pragma unroll
+    for (int k = 0; k < 8; k++) wv[k] = (a0 + 4 * k < flen) ? gw[k] : 0u;
     uint8_t hb[28];
+    const int sh = (int)(a - a0);
     const int64_t need = nrel - x < 26 ? nrel - x : 26;
-    const uint8_t* gp = gfile + cbase + x;
-    for (int k = 0; k < need; k++) hb[k] = gp[k];
+    #pragma unroll
+    for (int k = 0; k < 26; k++) {
+        const int q = k + sh;
+        hb[k] = k < need ? (uint8_t)(wv[q >> 2] >> (8 * (q & 3))) : 0;
+    }
     h = step_hdr(hb, 0, nrel - x, cbase + x);
 }
 
@@ -395,7 +416,7 @@ struct Spec {
 
 // Exact walk (ReadLogRecord semantics, any record or terminal) of the lane's
 // stripe [a, b) from position e.
-__device__ __noinline__ void exact_walk(const Sub& T, int a, int b, int e, Lane& L) {
+__device__ __forceinline__ void exact_walk(const Sub& T, int a, int b, int e, Lane& L) {
     (void)a;
     L.ws = e;
     int64_t p = e;
@@ -411,7 +432,7 @@ __device__ __noinline__ void exact_walk(const Sub& T, int a, int b, int e, Lane&
     }
 }
 
-__device__ __noinline__ void spec_lane(const Sub& T, int lane, int q0, Spec& r) {
+__device__ __forceinline__ void spec_lane(const Sub& T, int lane, int q0, Spec& r) {
     r.s = -1; r.last = -1; r.c = 0; r.x = 0;
     const int a = lane * CLY_SUB;
     if (a >= T.dlen) return;
@@ -430,7 +451,7 @@ __device__ __noinline__ void spec_lane(const Sub& T, int lane, int q0, Spec& r) 
             c++;
             x = p + h2.size;
         }
-        if (!ok) continue;
+        if (!ok || x > T.nrel) continue;               // a chain past the end of the file is not a guess
         if (x < T.nrel) {
             const int64_t need = T.nrel - x < 26 ? T.nrel - x : 26;
             Hdr e;
@@ -444,7 +465,7 @@ __device__ __noinline__ void spec_lane(const Sub& T, int lane, int q0, Spec& r) 
 }
 
 // resolve(E): the sub-tile's record chain from entry E (sub-tile-relative).
-__device__ __noinline__ void resolve(const Sub& T, const Spec& sp, int lane, int E, Lane& L, Chain& R) {
+__device__ __forceinline__ void resolve(const Sub& T, const Spec& sp, int lane, int E, Lane& L, Chain& R) {
     R.mode = MODE_NORMAL; R.E = E; R.eof_exit = 0;
     if (E >= T.dlen) {
         // only in the file's last sub-tile: E is the end of the file (ReadLogRecord there: io.EOF)
@@ -600,7 +621,7 @@ __device__ __forceinline__ void crc_loop(const CLY_LDS uint8_t* smem, const uint
 
 __device__ __noinline__ void crc_slow(const Sub& T, const Chain& R, CLY_LDS uint8_t* smem, CrcOut& out);
 
-__device__ __noinline__ void crc_phase(const Sub& T, const Lane& L, const Chain& R, int lane, CLY_LDS uint8_t* smem,
+__device__ __forceinline__ void crc_phase(const Sub& T, const Lane& L, const Chain& R, int lane, CLY_LDS uint8_t* smem,
                                        CLY_LDS uint32_t* w32, CLY_LDS u32x2* pool, CrcOut& out) {
     const uint32_t lane_off = (uint32_t)(lane & 15) * 4;
     out.bad = 0; out.head_raw = 0; out.head_z = 0; out.end_state = 0;
@@ -672,7 +693,7 @@ __device__ __noinline__ void crc_phase(const Sub& T, const Lane& L, const Chain&
         if (__ballot(!fin_lane) == 0ull) break;
         const int pc = __shfl_up(c, dd, 64);
         const uint32_t pv = __shfl_up(v, dd, 64);
-        if (!fin_lane) { v ^= col_mul(smem, LDS_KSCOL + lvl * 128, pv); c = pc; }
+        if (!fin_lane) { v ^= ks_mul(smem, lvl, pv); c = pc; }
     }
     uint32_t s_in = __shfl_up(v, 1, 64);
     if (lane == 0) s_in = 0;
@@ -808,9 +829,25 @@ __device__ __forceinline__ void sub_setup(Sub& T, int64_t sidx, const DevFile& F
     T.fid = F.fid;
 }
 
+// Second exit check of a speculative chain leaving its stripe at x (x itself
+// decoded as a plain record): the record after x must decode as one too.
+__device__ __forceinline__ int deep_check(const Sub& T, int64_t x) {
+    if (x >= T.nrel) return x == T.nrel;
+    Hdr e;
+    if (x + 26 <= T.win_len) e = hdr_at(T.w32, (int)x, T.nrel, T.cbase + x);
+    else hdr_global(T.gfile, T.cbase, x, T.nrel, e);
+    if (!e.good) return 0;
+    const int64_t x2 = x + e.size;
+    if (x2 >= T.nrel) return x2 == T.nrel;
+    Hdr f;
+    if (x2 + 26 <= T.win_len) f = hdr_at(T.w32, (int)x2, T.nrel, T.cbase + x2);
+    else hdr_global(T.gfile, T.cbase, x2, T.nrel, f);
+    return f.good ? 1 : 0;
+}
+
 // Speculation over the staged window: per lane the first candidate (register
 // SWAR filter over its stripe), then the candidate walks; the sub-tile guess.
-__device__ __noinline__ void sub_spec(const Sub& T, int lane, Spec& sp, int& guess) {
+__device__ __forceinline__ void sub_spec(const Sub& T, int lane, Spec& sp, int& guess) {
     const CLY_LDS uint32_t* w32 = T.w32;
     sp.s = -1; sp.last = -1; sp.c = 0; sp.x = 0;
     int q0 = CLY_TS;
@@ -838,8 +875,16 @@ __device__ __noinline__ void sub_spec(const Sub& T, int lane, Spec& sp, int& gue
     }
     spec_lane(T, lane, q0, sp);
     if (T.fof) { guess = 0; return; }
-    const unsigned long long m = __ballot(sp.s >= 0);
-    guess = m ? __shfl(sp.s, __ffsll((long long)m) - 1, 64) : -1;
+    // guess: the first lane whose chain also survives a second exit check
+    unsigned long long m = __ballot(sp.s >= 0);
+    guess = -1;
+    while (m) {
+        const int k = __ffsll((long long)m) - 1;
+        int ok = 0;
+        if (lane == k) ok = deep_check(T, sp.x);
+        if (__shfl(ok, k, 64)) { guess = __shfl(sp.s, k, 64); break; }
+        m &= m - 1;
+    }
 }
 
 // Chain for the given final mode / entry.
@@ -912,7 +957,7 @@ __device__ __forceinline__ void sub_summary(const Sub& T, const Chain& R, const 
 }
 
 // CRC + first failure + summary of a resolved sub-tile.
-__device__ __noinline__ void sub_crc(const Sub& T, const Lane& L, const Chain& R, int lane, CLY_LDS uint8_t* smem,
+__device__ __forceinline__ void sub_crc(const Sub& T, const Lane& L, const Chain& R, int lane, CLY_LDS uint8_t* smem,
                                         CLY_LDS u32x2* pool, uint32_t base, ChunkSum* sums, Globals* g) {
     CrcOut co;
     crc_phase(T, L, R, lane, smem, (CLY_LDS uint32_t*)T.w32, pool, co);
@@ -954,7 +999,7 @@ __device__ __forceinline__ void put_tuple(cly_tuple* out, uint64_t idx, uint64_t
 }
 
 // Tuples of this lane's records, written directly (output slot known).
-__device__ __noinline__ void emit_direct(const Sub& T, const Lane& L, uint64_t idx0, cly_tuple* out, uint64_t out_cap,
+__device__ __forceinline__ void emit_direct(const Sub& T, const Lane& L, uint64_t idx0, cly_tuple* out, uint64_t out_cap,
                                             Globals* g) {
     bool of = false;
     if (L.ws >= 0) {
@@ -1001,7 +1046,7 @@ __device__ __forceinline__ void init_tables(CLY_LDS uint8_t* smem, const uint32_
             cv = (cv >> 8) ^ tl;
         }
     }
-    for (int i = threadIdx.x; i < CLY_COLS; i += blockDim.x) ((CLY_LDS uint32_t*)(smem + LDS_KSCOL))[i] = cols[i];
+    for (int i = threadIdx.x; i < CLY_COLS; i += blockDim.x) ((CLY_LDS uint32_t*)(smem + LDS_KSNIB))[i] = cols[i];
     __syncthreads();
 }
 
@@ -1293,44 +1338,45 @@ k_place(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
     }
 }
 
-// One workgroup per file: first event of the file.
+// First event of every file: one thread per sub-tile (its in-tile event, or
+// the CRC failure of its open record), min-reduced per file on the key
+// (offset << 32 | sub-tile of the file); then one thread per file.
 #define FIN_NT 256
 __global__ void __launch_bounds__(FIN_NT)
-k_fin(const DevFile* __restrict__ files, const ChunkSum* __restrict__ sums, const uint64_t* __restrict__ sub_P,
-      const uint32_t* __restrict__ x8n, FileOut* __restrict__ fout) {
-    const int f = blockIdx.x, tid = threadIdx.x;
+k_fin1(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ sub_prefix, int64_t nsub,
+       const ChunkSum* __restrict__ sums, const uint64_t* __restrict__ sub_P, const uint32_t* __restrict__ x8n,
+       unsigned long long* fkey) {
+    const int64_t s = (int64_t)blockIdx.x * FIN_NT + threadIdx.x;
+    if (s >= nsub) return;
+    const int f = find_file(sub_prefix, nfiles, s);
     const DevFile F = files[f];
-    const int64_t c0 = (int64_t)F.first_sub, nc = F.nsub;
-    __shared__ int64_t r_off[FIN_NT];
-    __shared__ uint64_t r_g[FIN_NT];
-    __shared__ int32_t r_st[FIN_NT];
-    int64_t best = EVT_NONE;
-    uint64_t bg = 0;
-    int32_t bs = 0;
-    for (int64_t i = tid; i < nc; i += FIN_NT) {
+    uint64_t gi = 0;
+    int32_t st = 0;
+    const int64_t i = s - (int64_t)F.first_sub;
+    const int64_t o = fin_chunk_event(sums, sub_P, x8n, F.first_sub, F.nsub, i, &gi, &st);
+    if (o != EVT_NONE) atomicMin(&fkey[f], ((unsigned long long)o << 32) | (unsigned long long)i);
+}
+__global__ void __launch_bounds__(FIN_NT)
+k_fin2(const DevFile* __restrict__ files, int nfiles, const ChunkSum* __restrict__ sums,
+       const uint64_t* __restrict__ sub_P, const uint32_t* __restrict__ x8n, const unsigned long long* fkey,
+       FileOut* __restrict__ fout) {
+    const int f = blockIdx.x * FIN_NT + threadIdx.x;
+    if (f >= nfiles) return;
+    const DevFile F = files[f];
+    const unsigned long long key = fkey[f];
+    FileOut fo;
+    fo.first_index = sub_P[F.first_sub];
+    fo.ok = key != ~0ull;
+    fo.n_records = 0; fo.end_offset = EVT_NONE; fo.status = 0;
+    if (fo.ok) {
         uint64_t gi = 0;
         int32_t st = 0;
-        const int64_t o = fin_chunk_event(sums, sub_P, x8n, c0, nc, i, &gi, &st);
-        if (o < best) { best = o; bg = gi; bs = st; }
+        const int64_t i = (int64_t)(key & 0xffffffffull);
+        fo.end_offset = fin_chunk_event(sums, sub_P, x8n, F.first_sub, F.nsub, i, &gi, &st);
+        fo.n_records = gi - fo.first_index;
+        fo.status = st;
     }
-    r_off[tid] = best; r_g[tid] = bg; r_st[tid] = bs;
-    __syncthreads();
-    for (int d = FIN_NT / 2; d > 0; d >>= 1) {
-        if (tid < d && r_off[tid + d] < r_off[tid]) {
-            r_off[tid] = r_off[tid + d]; r_g[tid] = r_g[tid + d]; r_st[tid] = r_st[tid + d];
-        }
-        __syncthreads();
-    }
-    if (tid == 0) {
-        FileOut fo;
-        const uint64_t first = sub_P[c0];
-        fo.first_index = first;
-        fo.ok = r_off[0] != EVT_NONE;
-        fo.n_records = fo.ok ? r_g[0] - first : 0;
-        fo.end_offset = r_off[0];
-        fo.status = r_st[0];
-        fout[f] = fo;
-    }
+    fout[f] = fo;
 }
 
 // ---------------------------------------------------------------------------
@@ -1355,6 +1401,7 @@ struct cly_ctx {
     Fix* d_cand;                 // candidates of a round
     uint32_t* d_listed;          // per sub-tile: stamp of the last round that listed it
     int32_t* d_fh;               // per file: first harmful sub-tile of a round
+    unsigned long long* d_fkey;  // per file: first event key (k_fin1)
     uint32_t stamp;
     Globals* d_g;
     uint32_t* d_cols;            // columns of A^(SUB*2^k) (Kogge-Stone) and A^(4w) (head shifts)
@@ -1385,11 +1432,12 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
         uint32_t* hc = (uint32_t*)calloc(CLY_COLS, sizeof(uint32_t));
         for (int lvl = 0; lvl < CLY_KS_LEVELS; lvl++) {
             const uint32_t xm = cly_x8n((uint64_t)CLY_SUB << lvl);
-            for (int b = 0; b < 32; b++) hc[lvl * 32 + b] = cly_multmodp(xm, 1u << b);
+            for (int nb = 0; nb < 8; nb++)
+                for (uint32_t v = 0; v < 16; v++) hc[lvl * 128 + nb * 16 + v] = cly_multmodp(xm, v << (4 * nb));
         }
         for (int w = 0; w < CLY_NWD; w++) {
             const uint32_t xm = cly_x8n((uint64_t)4 * w);
-            for (int b = 0; b < 32; b++) hc[(CLY_KS_LEVELS + w) * 32 + b] = cly_multmodp(xm, 1u << b);
+            for (int b = 0; b < 32; b++) hc[CLY_KS_LEVELS * 128 + w * 32 + b] = cly_multmodp(xm, 1u << b);
         }
         HIPCK(hipMalloc(&c->d_cols, sizeof(uint32_t) * CLY_COLS));
         HIPCK(hipMemcpy(c->d_cols, hc, sizeof(uint32_t) * CLY_COLS, hipMemcpyHostToDevice));
@@ -1424,7 +1472,7 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     hipStreamSynchronize(c->stream);
     hipFree(c->d_files); hipFree(c->d_prefix); hipFree(c->d_fout); hipFree(c->d_desc); hipFree(c->d_sums);
     hipFree(c->d_subP); hipFree(c->d_staging); hipFree(c->d_blk); hipFree(c->d_fix); hipFree(c->d_cand);
-    hipFree(c->d_listed); hipFree(c->d_fh); hipFree(c->d_g); hipFree(c->d_cols); hipFree(c->d_x8n); hipFree(c->d_bytes); hipFree(c->d_tuples);
+    hipFree(c->d_listed); hipFree(c->d_fh); hipFree(c->d_fkey); hipFree(c->d_g); hipFree(c->d_cols); hipFree(c->d_x8n); hipFree(c->d_bytes); hipFree(c->d_tuples);
     hipHostFree(c->h_files); hipHostFree(c->h_prefix); hipHostFree(c->h_fout); hipHostFree(c->h_g);
     for (int i = 0; i < 4; i++) hipEventDestroy(c->ev[i]);
     hipStreamDestroy(c->stream);
@@ -1439,10 +1487,11 @@ extern "C" uint64_t cly_scan_capacity(const cly_file* files, int nfiles) {
 
 static int ensure_files(cly_ctx* c, int nfiles) {
     if (nfiles <= c->cap_files) return CLY_OK;
-    hipFree(c->d_files); hipFree(c->d_prefix); hipFree(c->d_fout); hipFree(c->d_fh);
+    hipFree(c->d_files); hipFree(c->d_prefix); hipFree(c->d_fout); hipFree(c->d_fh); hipFree(c->d_fkey);
     hipHostFree(c->h_files); hipHostFree(c->h_prefix); hipHostFree(c->h_fout);
     const int cap = nfiles < 64 ? 64 : nfiles;
     HIPCK(hipMalloc(&c->d_fh, sizeof(int32_t) * cap));
+    HIPCK(hipMalloc(&c->d_fkey, sizeof(unsigned long long) * cap));
     HIPCK(hipMalloc(&c->d_files, sizeof(DevFile) * cap));
     HIPCK(hipMalloc(&c->d_prefix, sizeof(uint32_t) * (cap + 1)));
     HIPCK(hipMalloc(&c->d_fout, sizeof(FileOut) * cap));
@@ -1560,7 +1609,11 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     HIPCK(hipEventRecord(c->ev[2], st));
     hipLaunchKernelGGL(k_place, dim3(c->scan_grid), dim3(64 * CLY_NDW), CLY_NDW * CLY_WIN, st, c->d_files, nfiles,
                        c->d_prefix, nsub, c->d_desc, c->d_subP, c->d_staging, d_out, out_cap, c->d_g);
-    hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_sums, c->d_subP, c->d_x8n, c->d_fout);
+    HIPCK(hipMemsetAsync(c->d_fkey, 0xff, sizeof(unsigned long long) * nfiles, st));
+    hipLaunchKernelGGL(k_fin1, dim3((unsigned)((nsub + FIN_NT - 1) / FIN_NT)), dim3(FIN_NT), 0, st, c->d_files, nfiles,
+                       c->d_prefix, nsub, c->d_sums, c->d_subP, c->d_x8n, c->d_fkey);
+    hipLaunchKernelGGL(k_fin2, dim3((nfiles + FIN_NT - 1) / FIN_NT), dim3(FIN_NT), 0, st, c->d_files, nfiles, c->d_sums,
+                       c->d_subP, c->d_x8n, c->d_fkey, c->d_fout);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[3], st));
     HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));

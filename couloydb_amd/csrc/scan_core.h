@@ -33,7 +33,8 @@
 #define CLY_NT 64
 #define CLY_NWD (CLY_SUB / 4)                 // words per stripe
 #define CLY_TS (CLY_NT * CLY_SUB)             // sub-tile bytes
-#define CLY_HALO 48                           // >= 26 (max header) + 11 (txId varint) + alignment
+#define CLY_HALO 320                          // >= 26 (max header) + 11 (txId varint); the larger halo lets
+                                              // exit checks of records up to ~290 B stay in LDS
 #define CLY_WIN (CLY_TS + CLY_HALO)
 static_assert(CLY_SUB % 16 == 0 && ((CLY_SUB / 16) & 1), "CLY_SUB = 16 * odd");
 static_assert(CLY_NWD <= 64, "check masks are 64-bit");
