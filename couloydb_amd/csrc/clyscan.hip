@@ -347,17 +347,17 @@ __device__ __forceinline__ uint32_t swar_ks(uint32_t W) {
     const uint32_t nz = ((W & 0x7f7f7f7fu) + 0x7f7f7f7fu) | W;
     return nz & ~(W << 7) & 0x80808080u;
 }
-// First q in [q0, b) whose bytes q+4, q+5 are <= 4 and q+6 is nonzero and
-// even (word-parallel filter over the LDS window); b if none.
+// First q in [q0, b) whose bytes q+4, q+5 (type, data type) are <= 4
+// (word-parallel filter over the LDS window); b if none.
 __device__ int next_candidate(const CLY_LDS uint32_t* w32, int q0, int b) {
     int i = (q0 + 4) >> 2;
-    uint32_t Li = swar_le4(w32[i]), Ki = swar_ks(w32[i]);
+    uint32_t Li = swar_le4(w32[i]);
     for (;;) {
         const int qbase = 4 * i - 4;
         if (qbase >= b) return b;
         const uint32_t Wn = w32[i + 1];
-        const uint32_t Ln = swar_le4(Wn), Kn = swar_ks(Wn);
-        uint32_t c = Li & __builtin_amdgcn_alignbit(Ln, Li, 8) & __builtin_amdgcn_alignbit(Kn, Ki, 16);
+        const uint32_t Ln = swar_le4(Wn);
+        uint32_t c = Li & __builtin_amdgcn_alignbit(Ln, Li, 8);
         if (qbase < q0) c &= ~0u << (8 * (q0 - qbase));
         if (c) {
             const int q = qbase + (__builtin_ctz(c) >> 3);
@@ -365,7 +365,6 @@ __device__ int next_candidate(const CLY_LDS uint32_t* w32, int q0, int b) {
         }
         i++;
         Li = Ln;
-        Ki = Kn;
     }
 }
 
@@ -437,7 +436,10 @@ __device__ __forceinline__ void spec_lane(const Sub& T, int lane, int q0, Spec& 
     const int a = lane * CLY_SUB;
     if (a >= T.dlen) return;
     const int b = a + CLY_SUB < T.dlen ? a + CLY_SUB : T.dlen;
+    const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)T.w32;
     for (int q = q0; q < b; q = next_candidate(T.w32, q + 1, b)) {
+        const uint32_t kb = w8[q + 6];                  // key-size varint: >= 1 needs an even nonzero first byte
+        if (kb == 0 || (kb & 1)) continue;
         const Hdr h = hdr_at(T.w32, q, T.nrel, T.cbase + q);
         if (!h.good) continue;
         int64_t p = q;
@@ -560,6 +562,7 @@ __device__ __forceinline__ void chain_none(Lane& L, Chain& R, int mode) {
 // reset check is obs ^ A^(4*rs) S_in.  All patches are XORs, so applying them
 // a second time restores the window.
 struct CrcOut {
+    uint32_t first4, open_crc, open_tail;   // pristine window values for the summary
     int      bad;                // some check failed (localised by crc_locate)
     uint32_t head_raw, head_z;   // Z_z(raw [4, E)) for k_fin
     uint32_t end_state;          // register at the end of the sub-tile (lane 63's inclusive scan)
@@ -626,6 +629,18 @@ __device__ __forceinline__ void crc_phase(const Sub& T, const Lane& L, const Cha
     const uint32_t lane_off = (uint32_t)(lane & 15) * 4;
     out.bad = 0; out.head_raw = 0; out.head_z = 0; out.end_state = 0;
     const bool normal = R.mode == MODE_NORMAL;
+    out.first4 = w32[0];
+    out.open_crc = 0; out.open_tail = 0xFFFFFFFFu;
+    if (normal && R.last >= 0) {
+        out.open_crc = lds_le32(w32, R.last);
+        const int ocs = R.last + 4;
+        if (ocs < CLY_TS && ocs + 4 > CLY_TS) {
+            const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)w32;
+            uint32_t st = 0xFFFFFFFFu;
+            for (int q = ocs; q < CLY_TS; q++) st = crc_byte(smem, st, w8[q], lane_off);
+            out.open_tail = st;
+        }
+    }
     // ---- check points of this lane: chain records, then its terminal
     const bool tcp = normal && L.wterm && L.wx < CLY_TS;
     const int n = normal ? ((L.ws >= 0 ? L.wc : 0) + (tcp ? 1 : 0)) : 0;
@@ -722,9 +737,12 @@ __device__ __forceinline__ void crc_phase(const Sub& T, const Lane& L, const Cha
         if ((Pl >> 2) + 1 == CLY_NT * CLY_NWD && Pl != R.E && out.end_state != 0) bad = true;
     }
     out.bad = __ballot(bad && normal) != 0ull;
-    // ---- restore the window (XOR patches are involutions)
-    crc_patch_all(smem, w32, pool, off, n, lane_off);
-    wave_sync();
+    // ---- restore the window for crc_locate (XOR patches are involutions);
+    // nothing else reads it after this phase
+    if (out.bad) {
+        crc_patch_all(smem, w32, pool, off, n, lane_off);
+        wave_sync();
+    }
 }
 
 // Slow path (more check points than the pool holds: sub-tiles of tiny
@@ -863,25 +881,31 @@ __device__ __forceinline__ void sub_spec(const Sub& T, int lane, Spec& sp, int& 
         dw[CLY_NWD] = w32[lane * CLY_NWD + CLY_NWD];
         dw[CLY_NWD + 1] = w32[lane * CLY_NWD + CLY_NWD + 1];
         int fm = CLY_NWD;
-        uint32_t Ln = swar_le4(dw[CLY_NWD + 1]), Kn = swar_ks(dw[CLY_NWD + 1]);
+        uint32_t Ln = swar_le4(dw[CLY_NWD + 1]);
         #pragma unroll
         for (int m = CLY_NWD - 1; m >= 0; m--) {
-            const uint32_t Lm = swar_le4(dw[m + 1]), Km = swar_ks(dw[m + 1]);
-            const uint32_t cm = Lm & __builtin_amdgcn_alignbit(Ln, Lm, 8) & __builtin_amdgcn_alignbit(Kn, Km, 16);
+            const uint32_t Lm = swar_le4(dw[m + 1]);
+            const uint32_t cm = Lm & __builtin_amdgcn_alignbit(Ln, Lm, 8);
             fm = cm ? m : fm;
-            Ln = Lm; Kn = Km;
+            Ln = Lm;
         }
         if (fm < CLY_NWD) q0 = next_candidate(w32, a + 4 * fm, a + CLY_SUB < T.dlen ? a + CLY_SUB : T.dlen);
     }
     spec_lane(T, lane, q0, sp);
     if (T.fof) { guess = 0; return; }
     // guess: the first lane whose chain also survives a second exit check
+    // (a lane whose exit is where the stripe holding it starts its own chain is
+    // confirmed without it)
+    const bool ext = sp.s >= 0 && sp.x < T.dlen;
+    const int tl = ext ? (int)(sp.x / CLY_SUB) : lane;
+    const int ts = __shfl(sp.s, tl, 64);
+    const int conf = ext && ts == (int)sp.x;
     unsigned long long m = __ballot(sp.s >= 0);
     guess = -1;
     while (m) {
         const int k = __ffsll((long long)m) - 1;
-        int ok = 0;
-        if (lane == k) ok = deep_check(T, sp.x);
+        int ok = conf;
+        if (lane == k && !ok) ok = deep_check(T, sp.x);
         if (__shfl(ok, k, 64)) { guess = __shfl(sp.s, k, 64); break; }
         m &= m - 1;
     }
@@ -897,11 +921,10 @@ __device__ __forceinline__ void sub_chain(const Sub& T, const Spec& sp, int lane
 // Per-sub-tile summary for k_fin (lane 0), with unit-relative record counts.
 __device__ __forceinline__ void sub_summary(const Sub& T, const Chain& R, const CrcOut& co, CLY_LDS uint8_t* smem,
                                             uint32_t base, int bpos, uint32_t bidx, ChunkSum* sums, Globals* g) {
-    const CLY_LDS uint32_t* w32 = T.w32;
     ChunkSum cs;
     cs.evt_off = EVT_NONE; cs.evt_gidx = 0; cs.evt_status = 0; cs.cnt = 0;
     cs.open_pos = -1; cs.open_state = 0; cs.open_crc = 0;
-    cs.first4 = w32[0];
+    cs.first4 = co.first4;
     cs.head_raw = 0; cs.head_len = 0; cs.head_shift = 0; cs.head_z = 0; cs.flags = 0;
     if (R.mode == MODE_DEAD) {
         cs.flags = SUM_DEAD;
@@ -938,15 +961,12 @@ __device__ __forceinline__ void sub_summary(const Sub& T, const Chain& R, const 
         if (R.cnt > 0 && R.last >= 0 && (!R.term || (R.eof_exit && R.tpos >= CLY_TS))) {
             cs.flags |= SUM_OPEN;
             cs.open_pos = T.cbase + R.last;
-            cs.open_crc = lds_le32(w32, R.last);
+            cs.open_crc = co.open_crc;
             const int ocs = R.last + 4;
             if (ocs >= CLY_TS) {
                 cs.open_state = 0xFFFFFFFFu;
             } else if (ocs + 4 > CLY_TS) {
-                uint32_t s = 0xFFFFFFFFu;
-                const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)w32;
-                for (int q = ocs; q < CLY_TS; q++) s = crc_byte(smem, s, w8[q], 0);
-                cs.open_state = s;
+                cs.open_state = co.open_tail;
             } else {
                 cs.open_state = co.end_state;
             }
@@ -1069,18 +1089,42 @@ __device__ __forceinline__ SubDesc make_desc(const Sub& T, const Chain& R) {
 
 // One sub-tile, start to end, for a chain given by (mode, entry) or, mode < 0,
 // by its own guess (mode -2: test mode, odd sub-tiles take a wrong guess).
+#define PF_N ((CLY_WIN / 16 + 63) / 64)       // 16-B pieces per lane of a prefetched window
+__device__ __forceinline__ void prefetch_issue(const uint8_t* src, int lane, u32x4 (&pf)[PF_N]) {
+    const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
+    #pragma unroll
+    for (int k = 0; k < PF_N; k++) {
+        const int slot = k * 64 + lane;
+        if (slot < CLY_WIN / 16) pf[k] = __builtin_nontemporal_load(s4 + slot);
+    }
+}
+__device__ __forceinline__ void prefetch_commit(CLY_LDS uint32_t* w32, int lane, const u32x4 (&pf)[PF_N]) {
+    CLY_LDS u32x4* w4 = (CLY_LDS u32x4*)w32;
+    #pragma unroll
+    for (int k = 0; k < PF_N; k++) {
+        const int slot = k * 64 + lane;
+        if (slot < CLY_WIN / 16) w4[slot] = pf[k];
+    }
+    wave_sync();
+}
+
+// One sub-tile: window (already in LDS when `ready`), speculation, chain,
+// tuples, CRC, descriptor.  When pf_src is set, the window of the wave's next
+// sub-tile is loaded into pf[] on the way (after the phases that read HBM).
 __device__ __forceinline__ void process_sub(int64_t sidx, int mode, int entry, const DevFile& F, int lane,
                                             CLY_LDS uint8_t* smem, CLY_LDS uint32_t* w32, CLY_LDS u32x2* pool,
                                             SubDesc* descs, ChunkSum* sums, cly_tuple* staging, Globals* g,
-                                            int prof_base, SubDesc& d) {
+                                            int prof_base, SubDesc& d, bool ready, const uint8_t* pf_src,
+                                            u32x4 (&pf)[PF_N]) {
     PROF_INIT();
     Sub T;
     sub_setup(T, sidx, F, w32);
-    if (stage(T, lane, w32)) stage_wait();
+    if (!ready && stage(T, lane, w32)) stage_wait();
     PROF(0);
     Spec sp;
     int guess = -1;
     sub_spec(T, lane, sp, guess);
+    if (pf_src) prefetch_issue(pf_src, lane, pf);
     PROF(1);
     Lane L;
     Chain R;
@@ -1092,9 +1136,9 @@ __device__ __forceinline__ void process_sub(int64_t sidx, int mode, int entry, c
     }
     sub_chain(T, sp, lane, mode, entry, L, R);
     PROF(2);
-    sub_crc(T, L, R, lane, smem, pool, 0, sums, g);
+    stage_tuples(T, L, R, staging);                 // before the CRC phase patches the window
     PROF(3);
-    stage_tuples(T, L, R, staging);
+    sub_crc(T, L, R, lane, smem, pool, 0, sums, g);
     PROF(4);
     d = make_desc(T, R);
     if (lane == 0) descs[T.chunk] = d;
@@ -1112,10 +1156,29 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     CLY_LDS uint32_t* w32 = (CLY_LDS uint32_t*)(smem + LDS_WIN + wave * CLY_WIN);
     CLY_LDS u32x2* pool = (CLY_LDS u32x2*)(smem + LDS_POOL + wave * CP_POOL * 8);
     const int64_t stride = (int64_t)gridDim.x * CLY_NDW;
-    for (int64_t s = (int64_t)blockIdx.x * CLY_NDW + wave; s < nsub; s += stride) {
-        const DevFile F = files[find_file(sub_prefix, nfiles, s)];
+    int64_t s = (int64_t)blockIdx.x * CLY_NDW + wave;
+    if (s >= nsub) return;
+    int f = find_file(sub_prefix, nfiles, s);
+    DevFile F = files[f];
+    u32x4 pf[PF_N];
+    bool ready = false;
+    for (;;) {
+        if (ready) prefetch_commit(w32, lane, pf);
+        // the wave's next sub-tile (files in order: walk forward from f)
+        const int64_t s2 = s + stride;
+        int f2 = f;
+        DevFile F2 = F;
+        const uint8_t* src2 = nullptr;
+        if (s2 < nsub) {
+            while (s2 >= (int64_t)F2.first_sub + F2.nsub) F2 = files[++f2];
+            const int64_t cb2 = (s2 - (int64_t)F2.first_sub) * CLY_TS;
+            if ((int64_t)F2.len - cb2 >= CLY_WIN) src2 = F2.base + cb2;
+        }
         SubDesc d;
-        process_sub(s, gmode, 0, F, lane, smem, w32, pool, descs, sums, staging, g, 0, d);
+        process_sub(s, gmode, 0, F, lane, smem, w32, pool, descs, sums, staging, g, 0, d, ready, src2, pf);
+        if (s2 >= nsub) break;
+        s = s2; f = f2; F = F2;
+        ready = src2 != nullptr;
     }
 }
 
@@ -1141,7 +1204,8 @@ k_fix(const DevFile* __restrict__ files, const Fix* fixes, uint32_t nfix, const 
         int mode = fx.mode, entry = fx.entry;
         for (;;) {
             SubDesc d;
-            process_sub(s, mode, entry, F, lane, smem, w32, pool, descs, sums, staging, g, 8, d);
+            u32x4 pf[PF_N];
+            process_sub(s, mode, entry, F, lane, smem, w32, pool, descs, sums, staging, g, 8, d, false, nullptr, pf);
             if (d.mode == MODE_DEAD || (d.mode == MODE_NORMAL && (d.flags & SD_TERM))) break;
             if (d.mode == MODE_NORMAL) x = d.x;
             if (++s >= s_end || listed[s] == stamp) break;
