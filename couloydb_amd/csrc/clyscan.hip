@@ -51,7 +51,7 @@ struct Globals {                 // zeroed per call
     uint32_t nfix;               // fix list length (this round)
     uint32_t fix_total;          // statistics: all fixes of the call
     uint32_t ncand;              // sub-tiles whose chain disagrees with the link (this round)
-    uint32_t _pad0;
+    uint32_t novf;               // sub-tiles with more tuples than their staging slot
     uint64_t prof[24];           // profiling build (-DCLY_PROF): summed cycles per phase
 };
 
@@ -1141,7 +1141,10 @@ __device__ __forceinline__ void process_sub(int64_t sidx, int mode, int entry, c
     sub_crc(T, L, R, lane, smem, pool, 0, sums, g);
     PROF(4);
     d = make_desc(T, R);
-    if (lane == 0) descs[T.chunk] = d;
+    if (lane == 0) {
+        descs[T.chunk] = d;
+        if (d.flags & SD_OVF) atomicAdd(&g->novf, 1u);
+    }
     PROF(5);
     PROF_FLUSH(prof_base);
 }
@@ -1364,8 +1367,54 @@ k_link4(const Fix* __restrict__ cand, const int32_t* __restrict__ fh, Fix* fixes
     }
 }
 
-// Staged tuples of every sub-tile to their output slots (one wave per sub-tile);
-// sub-tiles whose tuples did not fit the staging slot are re-read and emitted.
+// Staged tuples to their output slots: CP_SUBS sub-tiles per workgroup, one
+// 16-B piece per thread and step, all loads of a thread issued before its stores.
+#define CP_SUBS 16
+#define CP_NT 256
+#define CP_PER ((CP_SUBS * CLY_CAP * 3 + CP_NT - 1) / CP_NT)
+__global__ void __launch_bounds__(CP_NT)
+k_copy(const SubDesc* __restrict__ descs, const uint64_t* __restrict__ sub_P, const cly_tuple* __restrict__ staging,
+       cly_tuple* out, uint64_t out_cap, int64_t nsub, Globals* g) {
+    __shared__ uint32_t n_s[CP_SUBS];
+    __shared__ uint64_t p_s[CP_SUBS];
+    const int64_t s0 = (int64_t)blockIdx.x * CP_SUBS;
+    const int tid = threadIdx.x;
+    if (tid < CP_SUBS) {
+        const int64_t s = s0 + tid;
+        uint32_t n = 0;
+        uint64_t P = 0;
+        if (s < nsub) {
+            const SubDesc d = descs[s];
+            if (d.mode == MODE_NORMAL && !(d.flags & SD_OVF)) n = d.cnt * 3;
+            P = sub_P[s];
+        }
+        n_s[tid] = n;
+        p_s[tid] = P;
+    }
+    __syncthreads();
+    const u32x4* src = (const u32x4*)(staging + (uint64_t)s0 * CLY_CAP);
+    u32x4* dst = (u32x4*)out;
+    const uint64_t lim = out_cap * 3;
+    u32x4 v[CP_PER];
+    #pragma unroll
+    for (int k = 0; k < CP_PER; k++) {
+        const int e = k * CP_NT + tid, j = e / (CLY_CAP * 3), q = e - j * (CLY_CAP * 3);
+        if (j < CP_SUBS && (uint32_t)q < n_s[j]) v[k] = __builtin_nontemporal_load(src + e);
+    }
+    bool of = false;
+    #pragma unroll
+    for (int k = 0; k < CP_PER; k++) {
+        const int e = k * CP_NT + tid, j = e / (CLY_CAP * 3), q = e - j * (CLY_CAP * 3);
+        if (j < CP_SUBS && (uint32_t)q < n_s[j]) {
+            const uint64_t i = p_s[j] * 3 + (uint64_t)q;
+            if (i < lim) dst[i] = v[k]; else of = true;
+        }
+    }
+    if (of) atomicOr(&g->overflow, 1u);
+}
+
+// Sub-tiles whose tuples did not fit the staging slot: re-read and emitted
+// (one wave per sub-tile; launched only when there are any).
 __global__ void __launch_bounds__(64 * CLY_NDW)
 k_place(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ sub_prefix, int64_t nsub,
         const SubDesc* __restrict__ descs, const uint64_t* __restrict__ sub_P, const cly_tuple* __restrict__ staging,
@@ -1379,14 +1428,7 @@ k_place(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
         const SubDesc d = descs[s];
         if (d.mode != MODE_NORMAL || d.cnt == 0) continue;
         const uint64_t P = sub_P[s];
-        if (!(d.flags & SD_OVF)) {
-            const u32x4* src = (const u32x4*)(staging + (uint64_t)s * CLY_CAP);
-            u32x4* dst = (u32x4*)(out + P);
-            const uint32_t nq = d.cnt * 3;
-            const uint64_t lim = P + d.cnt <= out_cap ? nq : (out_cap > P ? (out_cap - P) * 3 : 0);
-            for (uint32_t q = lane; q < nq; q += 64) if (q < lim) dst[q] = src[q];
-            if (lim < nq && lane == 0) atomicOr(&g->overflow, 1u);
-        } else {
+        if (d.flags & SD_OVF) {
             const DevFile F = files[find_file(sub_prefix, nfiles, s)];
             Sub T;
             sub_setup(T, s, F, w32);
@@ -1671,8 +1713,12 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         HIPCK(hipGetLastError());
     }
     HIPCK(hipEventRecord(c->ev[2], st));
-    hipLaunchKernelGGL(k_place, dim3(c->scan_grid), dim3(64 * CLY_NDW), CLY_NDW * CLY_WIN, st, c->d_files, nfiles,
-                       c->d_prefix, nsub, c->d_desc, c->d_subP, c->d_staging, d_out, out_cap, c->d_g);
+    hipLaunchKernelGGL(k_copy, dim3((unsigned)((nsub + CP_SUBS - 1) / CP_SUBS)), dim3(CP_NT), 0, st, c->d_desc,
+                       c->d_subP, c->d_staging, d_out, out_cap, nsub, c->d_g);
+    if (c->h_g->novf) {
+        hipLaunchKernelGGL(k_place, dim3(c->scan_grid), dim3(64 * CLY_NDW), CLY_NDW * CLY_WIN, st, c->d_files,
+                           nfiles, c->d_prefix, nsub, c->d_desc, c->d_subP, c->d_staging, d_out, out_cap, c->d_g);
+    }
     HIPCK(hipMemsetAsync(c->d_fkey, 0xff, sizeof(unsigned long long) * nfiles, st));
     hipLaunchKernelGGL(k_fin1, dim3((unsigned)((nsub + FIN_NT - 1) / FIN_NT)), dim3(FIN_NT), 0, st, c->d_files, nfiles,
                        c->d_prefix, nsub, c->d_sums, c->d_subP, c->d_x8n, c->d_fkey);
