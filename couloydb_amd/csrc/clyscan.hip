@@ -126,7 +126,10 @@ struct Fix {                     // a sub-tile whose chain disagrees with the st
     int32_t  mode, entry;        // the chain that state implies (mode < 0: not determined yet)
     uint32_t file;
     int64_t  x_in;               // chain position entering the sub-tile
+    uint32_t certain;            // the state is certain (no wrong chain before it in the file)
+    uint32_t _pad;
 };
+#define LISTED_U 0x80000000u     // listed[s] = stamp: certain fix or walked; stamp | LISTED_U: uncertain fix
 static_assert(CLY_SCAN_LDS <= 163840, "LDS budget");
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -1187,12 +1190,12 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
 
 // Re-process the sub-tiles of the fix list from the chain the link gives them,
 // then walk on through the following sub-tiles of the file while the chain
-// stays live and disagrees with what they hold (stopping at a sub-tile of this
-// round's list: its own wave has it).
+// stays live and disagrees with what they hold (stopping at a sub-tile listed
+// or walked this round).  Pass 0 takes the certain fixes, pass 1 the uncertain
+// ones that no pass-0 walk went through.
 __global__ void __launch_bounds__(64 * CLY_NDW)
-k_fix(const DevFile* __restrict__ files, const Fix* fixes, uint32_t nfix, const uint32_t* __restrict__ listed,
-      uint32_t stamp, SubDesc* descs, ChunkSum* sums, const uint32_t* __restrict__ cols, cly_tuple* staging,
-      Globals* g) {
+k_fix(const DevFile* __restrict__ files, const Fix* fixes, uint32_t nfix, uint32_t* listed, uint32_t stamp, int pass,
+      SubDesc* descs, ChunkSum* sums, const uint32_t* __restrict__ cols, cly_tuple* staging, Globals* g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
     init_tables(smem, cols);
@@ -1201,6 +1204,9 @@ k_fix(const DevFile* __restrict__ files, const Fix* fixes, uint32_t nfix, const 
     CLY_LDS u32x2* pool = (CLY_LDS u32x2*)(smem + LDS_POOL + wave * CP_POOL * 8);
     for (uint32_t i = blockIdx.x * CLY_NDW + wave; i < nfix; i += gridDim.x * CLY_NDW) {
         const Fix fx = fixes[i];
+        if ((int)fx.certain != (pass == 0)) continue;
+        // an uncertain fix gives way to a walk of the first pass that went through it
+        if (pass == 1 && __builtin_nontemporal_load(&listed[fx.s]) != (stamp | LISTED_U)) continue;
         const DevFile F = files[fx.file];
         const int64_t s_end = (int64_t)F.first_sub + F.nsub;
         int64_t s = fx.s, x = fx.x_in;
@@ -1211,12 +1217,19 @@ k_fix(const DevFile* __restrict__ files, const Fix* fixes, uint32_t nfix, const 
             process_sub(s, mode, entry, F, lane, smem, w32, pool, descs, sums, staging, g, 8, d, false, nullptr, pf);
             if (d.mode == MODE_DEAD || (d.mode == MODE_NORMAL && (d.flags & SD_TERM))) break;
             if (d.mode == MODE_NORMAL) x = d.x;
-            if (++s >= s_end || listed[s] == stamp) break;
+            if (++s >= s_end) break;
+            const uint32_t ls = __builtin_nontemporal_load(&listed[s]);
+            // certain-listed or walked this round: its own wave has it (pass 0
+            // walks through uncertain fixes, which then give way)
+            if (ls == stamp || (pass == 1 && ls == (stamp | LISTED_U))) break;
             const int64_t rel = x - s * (int64_t)CLY_TS;
             if (rel < 0) { if (lane == 0) atomicOr(&g->fail, 8u); break; }      // cannot happen
             mode = rel >= CLY_TS ? MODE_PASS : MODE_NORMAL;
             entry = rel >= CLY_TS ? 0 : (int)rel;
             const SubDesc n = descs[s];
+            // walked (or already right for the walked chain): claimed for this round,
+            // so an uncertain fix listed there gives way
+            if (lane == 0) listed[s] = stamp;
             if (n.mode == mode && (mode != MODE_NORMAL || n.entry == entry)) break;
         }
     }
@@ -1305,7 +1318,7 @@ k_link2(LinkAgg* blk, int64_t nblk) {
 __global__ void __launch_bounds__(LINK_NT)
 k_link3(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ sub_prefix,
         const SubDesc* __restrict__ descs, int64_t nsub, const LinkAgg* __restrict__ blk, uint64_t* sub_P, Fix* cand,
-        uint32_t cand_cap, int32_t* fh, Globals* g) {
+        uint32_t cand_cap, int32_t* fh, unsigned long long* fck, Globals* g) {
     const int64_t b0 = (int64_t)blockIdx.x * LINK_BLK + (int64_t)threadIdx.x * LINK_IT;
     LinkAgg v = link_ident();
     SubDesc d[LINK_IT];
@@ -1341,11 +1354,63 @@ k_link3(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
             if (k < cand_cap) {
                 Fix c;
                 c.s = (uint32_t)s; c.mode = mode; c.entry = entry; c.file = f; c.x_in = x_in;
+                c.certain = 0; c._pad = 0;
                 cand[k] = c;
+                atomicMin(&fck[f], ((unsigned long long)s << 32) | k);      // first candidate of the file
             }
         }
         run = link_op(run, link_elem(d[i]));
         if (s == nsub - 1) g->total = run.br[1].cnt;
+    }
+}
+
+// Serial resolution (after parallel rounds that did not converge): one wave per
+// file walks from the file's first candidate to its end, keeping the exact
+// chain state, and re-processes every sub-tile that disagrees with it.  The
+// descriptors are read 64 ahead (one per lane).
+__global__ void __launch_bounds__(64)
+k_serial(const DevFile* __restrict__ files, const Fix* __restrict__ cand, const unsigned long long* __restrict__ fck,
+         SubDesc* descs, ChunkSum* sums, const uint32_t* __restrict__ cols, cly_tuple* staging, Globals* g) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const unsigned long long key = fck[blockIdx.x];
+    if (key == ~0ull) return;
+    CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
+    init_tables(smem, cols);
+    const int lane = threadIdx.x;
+    CLY_LDS uint32_t* w32 = (CLY_LDS uint32_t*)(smem + LDS_WIN);
+    CLY_LDS u32x2* pool = (CLY_LDS u32x2*)(smem + LDS_POOL);
+    const Fix c = cand[key & 0xffffffffull];
+    const DevFile F = files[blockIdx.x];
+    const int64_t s_end = (int64_t)F.first_sub + F.nsub;
+    if (c.mode < 0) { if (lane == 0) atomicOr(&g->fail, 9u); return; }      // cannot happen
+    int64_t s = c.s, x = c.x_in;
+    int mode = c.mode, entry = c.entry;
+    int64_t base = -1;
+    SubDesc ahead;
+    for (;;) {
+        if (s >= base + 64) {
+            base = s;
+            if (s + lane < s_end) ahead = descs[s + lane];
+        }
+        const int k = (int)(s - base);
+        SubDesc d;
+        d.x = (int64_t)__shfl((long long)ahead.x, k, 64);
+        d.cnt = (uint32_t)__shfl((int)ahead.cnt, k, 64);
+        d.entry = (int16_t)__shfl((int)ahead.entry, k, 64);
+        d.mode = (uint8_t)__shfl((int)ahead.mode, k, 64);
+        d.flags = (uint8_t)__shfl((int)ahead.flags, k, 64);
+        if (!(d.mode == mode && (mode != MODE_NORMAL || d.entry == entry))) {
+            u32x4 pf[PF_N];
+            process_sub(s, mode, entry, F, lane, smem, w32, pool, descs, sums, staging, g, 8, d, false, nullptr, pf);
+        }
+        bool dead = mode == MODE_DEAD || (d.mode == MODE_NORMAL && (d.flags & SD_TERM));
+        if (d.mode == MODE_NORMAL && !dead) x = d.x;
+        if (++s >= s_end) break;
+        if (dead) { mode = MODE_DEAD; entry = 0; continue; }
+        const int64_t rel = x - s * (int64_t)CLY_TS;
+        if (rel < 0) { if (lane == 0) atomicOr(&g->fail, 10u); break; }    // cannot happen
+        mode = rel >= CLY_TS ? MODE_PASS : MODE_NORMAL;
+        entry = rel >= CLY_TS ? 0 : (int)rel;
     }
 }
 
@@ -1362,8 +1427,10 @@ k_link4(const Fix* __restrict__ cand, const int32_t* __restrict__ fh, Fix* fixes
         if (c.mode < 0) continue;
         const bool certain = (int64_t)c.s <= (int64_t)fh[c.file];
         if (!certain && c.mode != MODE_NORMAL) continue;
-        listed[c.s] = stamp;
-        fixes[atomicAdd(&g->nfix, 1u)] = c;
+        listed[c.s] = certain ? stamp : (stamp | LISTED_U);
+        Fix e = c;
+        e.certain = certain;
+        fixes[atomicAdd(&g->nfix, 1u)] = e;
     }
 }
 
@@ -1508,6 +1575,7 @@ struct cly_ctx {
     uint32_t* d_listed;          // per sub-tile: stamp of the last round that listed it
     int32_t* d_fh;               // per file: first harmful sub-tile of a round
     unsigned long long* d_fkey;  // per file: first event key (k_fin1)
+    unsigned long long* d_fck;   // per file: first candidate key of a round
     uint32_t stamp;
     Globals* d_g;
     uint32_t* d_cols;            // columns of A^(SUB*2^k) (Kogge-Stone) and A^(4w) (head shifts)
@@ -1559,6 +1627,7 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     free(hx);
     HIPCK(hipFuncSetAttribute((const void*)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CLY_SCAN_LDS));
     HIPCK(hipFuncSetAttribute((const void*)k_fix, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CLY_SCAN_LDS));
+    HIPCK(hipFuncSetAttribute((const void*)k_serial, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CLY_SCAN_LDS));
     HIPCK(hipFuncSetAttribute((const void*)k_place, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)(CLY_NDW * CLY_WIN)));
     {
@@ -1578,7 +1647,7 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     hipStreamSynchronize(c->stream);
     hipFree(c->d_files); hipFree(c->d_prefix); hipFree(c->d_fout); hipFree(c->d_desc); hipFree(c->d_sums);
     hipFree(c->d_subP); hipFree(c->d_staging); hipFree(c->d_blk); hipFree(c->d_fix); hipFree(c->d_cand);
-    hipFree(c->d_listed); hipFree(c->d_fh); hipFree(c->d_fkey); hipFree(c->d_g); hipFree(c->d_cols); hipFree(c->d_x8n); hipFree(c->d_bytes); hipFree(c->d_tuples);
+    hipFree(c->d_listed); hipFree(c->d_fh); hipFree(c->d_fkey); hipFree(c->d_fck); hipFree(c->d_g); hipFree(c->d_cols); hipFree(c->d_x8n); hipFree(c->d_bytes); hipFree(c->d_tuples);
     hipHostFree(c->h_files); hipHostFree(c->h_prefix); hipHostFree(c->h_fout); hipHostFree(c->h_g);
     for (int i = 0; i < 4; i++) hipEventDestroy(c->ev[i]);
     hipStreamDestroy(c->stream);
@@ -1593,11 +1662,12 @@ extern "C" uint64_t cly_scan_capacity(const cly_file* files, int nfiles) {
 
 static int ensure_files(cly_ctx* c, int nfiles) {
     if (nfiles <= c->cap_files) return CLY_OK;
-    hipFree(c->d_files); hipFree(c->d_prefix); hipFree(c->d_fout); hipFree(c->d_fh); hipFree(c->d_fkey);
+    hipFree(c->d_files); hipFree(c->d_prefix); hipFree(c->d_fout); hipFree(c->d_fh); hipFree(c->d_fkey); hipFree(c->d_fck);
     hipHostFree(c->h_files); hipHostFree(c->h_prefix); hipHostFree(c->h_fout);
     const int cap = nfiles < 64 ? 64 : nfiles;
     HIPCK(hipMalloc(&c->d_fh, sizeof(int32_t) * cap));
     HIPCK(hipMalloc(&c->d_fkey, sizeof(unsigned long long) * cap));
+    HIPCK(hipMalloc(&c->d_fck, sizeof(unsigned long long) * cap));
     HIPCK(hipMalloc(&c->d_files, sizeof(DevFile) * cap));
     HIPCK(hipMalloc(&c->d_prefix, sizeof(uint32_t) * (cap + 1)));
     HIPCK(hipMalloc(&c->d_fout, sizeof(FileOut) * cap));
@@ -1627,7 +1697,8 @@ static int ensure_subs(cly_ctx* c, int64_t nsub) {
     return CLY_OK;
 }
 
-#define FIX_ROUNDS 64
+#define FIX_ROUNDS 8
+#define SERIAL_AFTER 2           // parallel fix rounds before the serial walk
 
 extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple* d_out, uint64_t out_cap,
                                uint64_t* file_first, cly_file_result* res, uint64_t* needed, cly_stats* stats,
@@ -1676,10 +1747,11 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         HIPCK(hipMemsetAsync(&c->d_g->nfix, 0, sizeof(uint32_t), st));
         HIPCK(hipMemsetAsync(&c->d_g->ncand, 0, sizeof(uint32_t), st));
         HIPCK(hipMemsetAsync(c->d_fh, 0x7f, sizeof(int32_t) * nfiles, st));
+        HIPCK(hipMemsetAsync(c->d_fck, 0xff, sizeof(unsigned long long) * nfiles, st));
         hipLaunchKernelGGL(k_link1, dim3(nblk), dim3(LINK_NT), 0, st, c->d_desc, nsub, c->d_blk);
         hipLaunchKernelGGL(k_link2, dim3(1), dim3(LINK_NT), 0, st, c->d_blk, nblk);
         hipLaunchKernelGGL(k_link3, dim3(nblk), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_prefix, c->d_desc, nsub,
-                           c->d_blk, c->d_subP, c->d_cand, (uint32_t)c->cap_subs, c->d_fh, c->d_g);
+                           c->d_blk, c->d_subP, c->d_cand, (uint32_t)c->cap_subs, c->d_fh, c->d_fck, c->d_g);
         hipLaunchKernelGGL(k_link4, dim3(64), dim3(LINK_NT), 0, st, c->d_cand, c->d_fh, c->d_fix, c->d_listed, stamp,
                            c->d_g);
         HIPCK(hipGetLastError());
@@ -1694,22 +1766,44 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         }
         fixes += nfix;
         if (c->dbg_flags & 4) {                          // debug trace of the fix rounds
-            Fix hf[8];
-            const uint32_t nshow = nfix < 8 ? nfix : 8;
+            const uint32_t nshow = nfix < 64 ? nfix : 64;
+            Fix* hf = (Fix*)malloc(sizeof(Fix) * nshow);
             HIPCK(hipMemcpy(hf, c->d_fix, sizeof(Fix) * nshow, hipMemcpyDeviceToHost));
             fprintf(stderr, "round %u: %u candidates, %u fixes:", rounds, ncand, nfix);
             for (uint32_t k = 0; k < nshow; k++) {
                 SubDesc d;
                 HIPCK(hipMemcpy(&d, c->d_desc + hf[k].s, sizeof(SubDesc), hipMemcpyDeviceToHost));
-                fprintf(stderr, " [s=%u want %d/%d have %d/%d cnt %u]", hf[k].s, hf[k].mode, hf[k].entry, d.mode,
-                        d.entry, d.cnt);
+                fprintf(stderr, " [s=%u%s want %d/%d have %d/%d cnt %u]", hf[k].s, hf[k].certain ? "C" : "", hf[k].mode,
+                        hf[k].entry, d.mode, d.entry, d.cnt);
             }
             fprintf(stderr, "\n");
+            free(hf);
+        }
+        if (rounds > SERIAL_AFTER) {
+            // the parallel rounds did not settle: one exact serial walk per file
+            hipLaunchKernelGGL(k_serial, dim3(nfiles), dim3(64), CLY_SCAN_LDS, st, c->d_files, c->d_cand, c->d_fck,
+                               c->d_desc, c->d_sums, c->d_cols, c->d_staging, c->d_g);
+            HIPCK(hipGetLastError());
+            continue;
         }
         int fgrid = (int)((nfix + CLY_NDW - 1) / CLY_NDW);
         if (fgrid > c->scan_grid) fgrid = c->scan_grid;
-        hipLaunchKernelGGL(k_fix, dim3(fgrid), dim3(64 * CLY_NDW), CLY_SCAN_LDS, st, c->d_files, c->d_fix, nfix,
-                           c->d_listed, stamp, c->d_desc, c->d_sums, c->d_cols, c->d_staging, c->d_g);
+        for (int pass = 0; pass < 2; pass++)
+            hipLaunchKernelGGL(k_fix, dim3(fgrid), dim3(64 * CLY_NDW), CLY_SCAN_LDS, st, c->d_files, c->d_fix, nfix,
+                               c->d_listed, stamp, pass, c->d_desc, c->d_sums, c->d_cols, c->d_staging, c->d_g);
+        if (c->dbg_flags & 8) {                          // debug: descriptors and stamps after the round
+            HIPCK(hipStreamSynchronize(st));
+            const int64_t nd = nsub < 64 ? nsub : 64;
+            SubDesc hd[64];
+            uint32_t hl[64];
+            HIPCK(hipMemcpy(hd, c->d_desc, sizeof(SubDesc) * nd, hipMemcpyDeviceToHost));
+            HIPCK(hipMemcpy(hl, c->d_listed, sizeof(uint32_t) * nd, hipMemcpyDeviceToHost));
+            fprintf(stderr, "  after (stamp %u):", stamp);
+            for (int64_t k = 0; k < nd; k++)
+                fprintf(stderr, " %lld:%d/%d/%u%s", (long long)k, hd[k].mode, hd[k].entry, hd[k].cnt,
+                        hl[k] == stamp ? "w" : (hl[k] == (stamp | LISTED_U) ? "u" : ""));
+            fprintf(stderr, "\n");
+        }
         HIPCK(hipGetLastError());
     }
     HIPCK(hipEventRecord(c->ev[2], st));

@@ -14,14 +14,22 @@ from couloydb_amd import DataFile, Scanner  # noqa: E402
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 lib = args[0] if args else "libclyscan_small.so"
 what = args[1] if len(args) > 1 else "corpus:0"
-if not what.startswith("corpus:"):
+if not what.startswith("corpus:") and what != "tiny":
     import torch
     from bench import make_workload
     wl = make_workload(what, torch)
 sc = Scanner(0, lib=lib)
 sc.lib.cly_dbg_enable.argtypes = [ctypes.c_void_p, ctypes.c_int]
-sc.lib.cly_dbg_enable(sc.ctx, 4 | (2 if "--force" in sys.argv else 0))
-if what.startswith("corpus:"):
+sc.lib.cly_dbg_enable(sc.ctx, 4 | (8 if "--descs" in sys.argv else 0) | (2 if "--force" in sys.argv else 0))
+if what == "tiny":
+    from gpu_util import fixed_records_file
+    data = fixed_records_file(200000, 0, seed=13)
+    try:
+        r = sc.scan([DataFile(data, 0)])
+        print("ok", r.n_records[0])
+    except Exception as e:
+        print("ERR", e)
+elif what.startswith("corpus:"):
     from gpu_util import mixed_corpus
     seed = int(what.split(":")[1])
     files = []
