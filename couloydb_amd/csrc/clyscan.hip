@@ -625,7 +625,8 @@ __device__ __forceinline__ void crc_loop(const CLY_LDS uint8_t* smem, const uint
     s_out = s; obs_out = obs; err_out = err;
 }
 
-__device__ __noinline__ void crc_slow(const Sub& T, const Chain& R, CLY_LDS uint8_t* smem, CrcOut& out);
+__device__ __noinline__ void crc_slow(const CLY_LDS uint32_t* w32, int64_t nrel, int64_t cbase, int E, uint32_t cnt,
+                                      CLY_LDS uint8_t* smem, CrcOut& out);
 
 __device__ __forceinline__ void crc_phase(const Sub& T, const Lane& L, const Chain& R, int lane, CLY_LDS uint8_t* smem,
                                        CLY_LDS uint32_t* w32, CLY_LDS u32x2* pool, CrcOut& out) {
@@ -651,7 +652,11 @@ __device__ __forceinline__ void crc_phase(const Sub& T, const Lane& L, const Cha
     const int off = (int)(incl - (uint32_t)n);
     const int total = (int)__shfl(incl, CLY_NT - 1, 64);
     if (total > CP_POOL) {
-        if (lane == 0) crc_slow(T, R, smem, out);
+        if (lane == 0) {
+            CrcOut t;                               // (own object: `out` stays in registers)
+            crc_slow(w32, T.nrel, T.cbase, R.E, R.cnt, smem, t);
+            out.bad = t.bad; out.head_raw = t.head_raw; out.head_z = t.head_z; out.end_state = t.end_state;
+        }
         out.bad = __shfl(out.bad, 0, 64); out.head_raw = __shfl(out.head_raw, 0, 64);
         out.head_z = __shfl(out.head_z, 0, 64); out.end_state = __shfl(out.end_state, 0, 64);
         return;
@@ -750,21 +755,24 @@ __device__ __forceinline__ void crc_phase(const Sub& T, const Lane& L, const Cha
 
 // Slow path (more check points than the pool holds: sub-tiles of tiny
 // records): one lane recomputes everything byte-serially from the window.
-__device__ __noinline__ void crc_slow(const Sub& T, const Chain& R, CLY_LDS uint8_t* smem, CrcOut& out) {
-    const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)T.w32;
+// (scalar arguments only: a struct passed by reference to a non-inlined
+// function is kept in scratch memory on every sub-tile)
+__device__ __noinline__ void crc_slow(const CLY_LDS uint32_t* w32, int64_t nrel, int64_t cbase, int E, uint32_t cnt,
+                                      CLY_LDS uint8_t* smem, CrcOut& out) {
+    const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)w32;
     out.bad = 0;
     // head: Z_z(raw [4, E))
     uint32_t s = 0;
-    for (int q = 4; q < R.E; q++) s = crc_byte(smem, s, w8[q], 0);
-    const uint32_t z = 4 - (R.E & 3);
+    for (int q = 4; q < E; q++) s = crc_byte(smem, s, w8[q], 0);
+    const uint32_t z = 4 - (E & 3);
     for (uint32_t k = 0; k < z; k++) s = crc_byte(smem, s, 0, 0);
     out.head_raw = s;
     out.head_z = z;
     // records
-    int64_t p = R.E;
+    int64_t p = E;
     uint32_t last_state = 0xFFFFFFFFu;
-    for (uint32_t i = 0; i < R.cnt; i++) {
-        const Hdr h = hdr_at(T.w32, (int)p, T.nrel, T.cbase + p);
+    for (uint32_t i = 0; i < cnt; i++) {
+        const Hdr h = hdr_at(w32, (int)p, nrel, cbase + p);
         const int64_t e = p + h.size;
         uint32_t r = 0xFFFFFFFFu;
         const int64_t hi = e < CLY_TS ? e : CLY_TS;
@@ -779,13 +787,14 @@ __device__ __noinline__ void crc_slow(const Sub& T, const Chain& R, CLY_LDS uint
 // Rare path: locate the first failing in-sub-tile record by a serial exact
 // walk (one lane) over the restored window.  Returns its position and local
 // index via (pos, idx); pos = -1 if none (cannot happen after a failed check).
-__device__ __noinline__ void crc_locate(const Sub& T, const Chain& R, CLY_LDS uint8_t* smem, int& pos, uint32_t& idx) {
+__device__ __noinline__ void crc_locate(const CLY_LDS uint32_t* w32, int64_t nrel, int64_t cbase, int E, uint32_t cnt,
+                                        CLY_LDS uint8_t* smem, int& pos, uint32_t& idx) {
     pos = -1; idx = 0;
-    const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)T.w32;
-    int64_t p = R.E;
+    const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)w32;
+    int64_t p = E;
     uint32_t i = 0;
-    while (p < CLY_TS && i < R.cnt) {
-        const Hdr h = hdr_at(T.w32, (int)p, T.nrel, T.cbase + p);
+    while (p < CLY_TS && i < cnt) {
+        const Hdr h = hdr_at(w32, (int)p, nrel, cbase + p);
         const int64_t e = p + h.size;
         if (e >= CLY_TS) break;                        // no in-tile check point: k_fin
         uint32_t s = 0xFFFFFFFFu;
@@ -987,7 +996,12 @@ __device__ __forceinline__ void sub_crc(const Sub& T, const Lane& L, const Chain
     int bpos = -1;
     uint32_t bidx = 0;
     if (lane == 0) {
-        if (co.bad) crc_locate(T, R, smem, bpos, bidx);
+        if (co.bad) {
+            int tp;
+            uint32_t ti;
+            crc_locate(T.w32, T.nrel, T.cbase, R.E, R.cnt, smem, tp, ti);
+            bpos = tp; bidx = ti;
+        }
         sub_summary(T, R, co, smem, base, bpos, bidx, sums, g);
     }
 }
@@ -1073,10 +1087,25 @@ __device__ __forceinline__ void init_tables(CLY_LDS uint8_t* smem, const uint32_
     __syncthreads();
 }
 
-// Tuples of this lane's records into the sub-tile's staging slot (when they fit).
+// Tuples of this lane's records into the sub-tile's staging slot (when they
+// fit).  The slot is three planes of CLY_CAP 16-B pieces (piece k of tuple i
+// at plane k, row i), so with one record per lane each store instruction
+// writes one contiguous run; k_copy interleaves the planes back.
 __device__ __forceinline__ void stage_tuples(const Sub& T, const Lane& L, const Chain& R, cly_tuple* staging) {
     if (R.mode != MODE_NORMAL || R.cnt > CLY_CAP) return;
-    emit_direct(T, L, (uint64_t)T.chunk * CLY_CAP + L.base, staging, ~0ull, nullptr);
+    if (L.ws < 0) return;
+    u32x4* slot = (u32x4*)staging + (uint64_t)T.chunk * (3 * CLY_CAP);
+    int p = L.ws;
+    for (int i = 0; i < L.wc; i++) {
+        u32x4 q0, q1, q2;
+        int64_t size;
+        tuple_words(T, p, q0, q1, q2, size);
+        const int r = (int)L.base + i;
+        slot[r] = q0;
+        slot[CLY_CAP + r] = q1;
+        slot[2 * CLY_CAP + r] = q2;
+        p += (int)size;
+    }
 }
 
 __device__ __forceinline__ SubDesc make_desc(const Sub& T, const Chain& R) {
@@ -1466,7 +1495,9 @@ k_copy(const SubDesc* __restrict__ descs, const uint64_t* __restrict__ sub_P, co
     #pragma unroll
     for (int k = 0; k < CP_PER; k++) {
         const int e = k * CP_NT + tid, j = e / (CLY_CAP * 3), q = e - j * (CLY_CAP * 3);
-        if (j < CP_SUBS && (uint32_t)q < n_s[j]) v[k] = __builtin_nontemporal_load(src + e);
+        const int r = q / 3, pl = q - 3 * r;                 // tuple r, piece pl (plane layout)
+        if (j < CP_SUBS && (uint32_t)q < n_s[j])
+            v[k] = __builtin_nontemporal_load(src + j * (CLY_CAP * 3) + pl * CLY_CAP + r);
     }
     bool of = false;
     #pragma unroll
