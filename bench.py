@@ -105,6 +105,23 @@ def make_workload(name, torch, rank=0, device=0, seed=0x434C59):
     return wl
 
 
+def measured_traffic(config):
+    """k_scan HBM bytes per launch (read + write) from the newest committed
+    profiles/*_traffic.json whose build and config match this library."""
+    import glob
+    from couloydb_amd import build_info
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
+        try:
+            t = json.load(open(f))
+        except ValueError:
+            continue
+        k = t.get("kernels", {}).get("k_scan")
+        if t.get("build") == build_info() and t.get("config") == config and k:
+            best = k.get("fetch_bytes", 0) + k.get("write_bytes", 0)
+    return best
+
+
 def cpu_baseline(wl, budget_s=12.0):
     """Oracle (C restatement) on the host cores over a bounded sample of the same
     workload: 'ref-algorithm' single thread over whole files; 'ref-faithful' =
@@ -207,8 +224,10 @@ def main():
         "kernel": {"k_scan_ms": round(kern_ms, 4), "k_resolve_ms": round(res_ms / args.steps, 4),
                    "passes": passes, "build": build_info()},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "note": "achieved = input bytes per k_scan launch / its HIP-event duration"},
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": measured_traffic(args.config),
+                     "note": "achieved = input bytes per k_scan launch / its HIP-event duration; traffic = "
+                             "k_scan HBM read+write bytes per launch from the committed rocprofv3 FETCH_SIZE/"
+                             "WRITE_SIZE passes of this build (profiles/*_traffic.json), null if none"},
         "parity_ok": ok,
     }
     if args.verify and rank == 0:
