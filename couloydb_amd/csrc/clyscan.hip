@@ -350,27 +350,6 @@ __device__ __forceinline__ uint32_t swar_ks(uint32_t W) {
     const uint32_t nz = ((W & 0x7f7f7f7fu) + 0x7f7f7f7fu) | W;
     return nz & ~(W << 7) & 0x80808080u;
 }
-// First q in [q0, b) whose bytes q+4, q+5 (type, data type) are <= 4
-// (word-parallel filter over the LDS window); b if none.
-__device__ int next_candidate(const CLY_LDS uint32_t* w32, int q0, int b) {
-    int i = (q0 + 4) >> 2;
-    uint32_t Li = swar_le4(w32[i]);
-    for (;;) {
-        const int qbase = 4 * i - 4;
-        if (qbase >= b) return b;
-        const uint32_t Wn = w32[i + 1];
-        const uint32_t Ln = swar_le4(Wn);
-        uint32_t c = Li & __builtin_amdgcn_alignbit(Ln, Li, 8);
-        if (qbase < q0) c &= ~0u << (8 * (q0 - qbase));
-        if (c) {
-            const int q = qbase + (__builtin_ctz(c) >> 3);
-            return q < b ? q : b;
-        }
-        i++;
-        Li = Ln;
-    }
-}
-
 // ---------------------------------------------------------------------------
 // Sub-tile context (wave-uniform, registers)
 struct Sub {
@@ -434,38 +413,129 @@ __device__ __forceinline__ void exact_walk(const Sub& T, int a, int b, int e, La
     }
 }
 
-__device__ __forceinline__ void spec_lane(const Sub& T, int lane, int q0, Spec& r) {
+// Candidate bits of stripe word m (positions 4m..4m+3 of the stripe starting at
+// window byte a): type and data type bytes <= 4 (bit 8j+7 for position 4m+j).
+__device__ __forceinline__ uint32_t cand_bits(const CLY_LDS uint32_t* w32, int a, int m) {
+    const int i = (a >> 2) + m + 1;
+    const uint32_t L1 = swar_le4(w32[i]), L2 = swar_le4(w32[i + 1]);
+    return L1 & __builtin_amdgcn_alignbit(L2, L1, 8);
+}
+
+// Speculative walk of one lane: the first candidate of its stripe (from the
+// word mask wm) whose chain of plain records leaves the stripe at an exit that
+// decodes as a plain record, the end of the file, or a position beyond the
+// window (left unchecked: the chain check of resolve() and the guess's own
+// deep check cover it).  Candidates whose key-size byte is odd or zero
+// (ks < 1) are skipped before decoding.
+__device__ __forceinline__ void spec_lane(const Sub& T, int lane, uint64_t wm, Spec& r) {
     r.s = -1; r.last = -1; r.c = 0; r.x = 0;
     const int a = lane * CLY_SUB;
     if (a >= T.dlen) return;
     const int b = a + CLY_SUB < T.dlen ? a + CLY_SUB : T.dlen;
     const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)T.w32;
-    for (int q = q0; q < b; q = next_candidate(T.w32, q + 1, b)) {
-        const uint32_t kb = w8[q + 6];                  // key-size varint: >= 1 needs an even nonzero first byte
-        if (kb == 0 || (kb & 1)) continue;
-        const Hdr h = hdr_at(T.w32, q, T.nrel, T.cbase + q);
-        if (!h.good) continue;
-        int64_t p = q;
-        int c = 1;
-        int64_t x = p + h.size;
-        bool ok = true;
-        while (x < b) {
-            const Hdr h2 = hdr_at(T.w32, (int)x, T.nrel, T.cbase + x);
-            if (!h2.good) { ok = false; break; }
-            p = x;
-            c++;
-            x = p + h2.size;
+    // (one flat loop over (word, bit): the nested form of this loop with the
+    // early return was miscompiled by the ROCm 7.2 toolchain - R.last came out -1)
+    uint32_t cm = 0;
+    int m = 0;
+    for (;;) {
+        if (cm == 0) {
+            if (wm == 0) break;
+            m = __builtin_ctzll(wm);
+            wm &= wm - 1;
+            cm = cand_bits(T.w32, a, m);
+            continue;
         }
-        if (!ok || x > T.nrel) continue;               // a chain past the end of the file is not a guess
-        if (x < T.nrel) {
-            const int64_t need = T.nrel - x < 26 ? T.nrel - x : 26;
-            Hdr e;
-            if (x + need <= T.win_len) e = hdr_at(T.w32, (int)x, T.nrel, T.cbase + x);
-            else hdr_global(T.gfile, T.cbase, x, T.nrel, e);
-            if (!e.good) continue;
+        {
+            const int q = a + 4 * m + (__builtin_ctz(cm) >> 3);
+            cm &= cm - 1;
+            if (q >= b) break;
+            const uint32_t kb = w8[q + 6];          // key-size varint: >= 1 needs an even nonzero first byte
+            if (kb == 0 || (kb & 1)) continue;
+            const Hdr h = hdr_at(T.w32, q, T.nrel, T.cbase + q);
+            if (!h.good) continue;
+            int64_t p = q;
+            int c = 1;
+            int64_t x = p + h.size;
+            bool ok = true;
+            while (x < b) {
+                const Hdr h2 = hdr_at(T.w32, (int)x, T.nrel, T.cbase + x);
+                if (!h2.good) { ok = false; break; }
+                p = x;
+                c++;
+                x = p + h2.size;
+            }
+            if (!ok || x > T.nrel) continue;           // a chain past the end of the file is not a guess
+            if (x < T.nrel && x + 26 <= T.win_len) {
+                const Hdr e = hdr_at(T.w32, (int)x, T.nrel, T.cbase + x);
+                if (!e.good) continue;
+            }
+            r.s = q; r.last = (int)p; r.c = c; r.x = x;
+            return;
         }
-        r.s = q; r.last = (int)p; r.c = c; r.x = x;
-        return;
+    }
+}
+
+// Second exit check of a speculative chain leaving its stripe at x: the record
+// at x and the one after it must decode as plain records.
+__device__ __forceinline__ int deep_check(const Sub& T, int64_t x) {
+    if (x >= T.nrel) return x == T.nrel;
+    Hdr e;
+    if (x + 26 <= T.win_len) e = hdr_at(T.w32, (int)x, T.nrel, T.cbase + x);
+    else hdr_global(T.gfile, T.cbase, x, T.nrel, e);
+    if (!e.good) return 0;
+    const int64_t x2 = x + e.size;
+    if (x2 >= T.nrel) return x2 == T.nrel;
+    Hdr f;
+    if (x2 + 26 <= T.win_len) f = hdr_at(T.w32, (int)x2, T.nrel, T.cbase + x2);
+    else hdr_global(T.gfile, T.cbase, x2, T.nrel, f);
+    return f.good ? 1 : 0;
+}
+
+// Speculation over the staged window: per lane the candidate word mask of its
+// stripe (register SWAR filter), then the candidate walks; the sub-tile guess.
+__device__ __forceinline__ void sub_spec(const Sub& T, int lane, Spec& sp, int& guess) {
+    const CLY_LDS uint32_t* w32 = T.w32;
+    uint64_t wm = 0;
+    const int a = lane * CLY_SUB;
+    if (a < T.dlen) {
+        uint32_t dw[CLY_NWD + 2];
+        const CLY_LDS u32x4* s4 = (const CLY_LDS u32x4*)(w32 + lane * CLY_NWD);
+        #pragma unroll
+        for (int i = 0; i < CLY_NWD / 4; i++) {
+            const u32x4 v = s4[i];
+            dw[4 * i] = v.x; dw[4 * i + 1] = v.y; dw[4 * i + 2] = v.z; dw[4 * i + 3] = v.w;
+        }
+        dw[CLY_NWD] = w32[lane * CLY_NWD + CLY_NWD];
+        dw[CLY_NWD + 1] = w32[lane * CLY_NWD + CLY_NWD + 1];
+        uint32_t wlo = 0, whi = 0;
+        uint32_t Ln = swar_le4(dw[CLY_NWD + 1]);
+        #pragma unroll
+        for (int m = CLY_NWD - 1; m >= 0; m--) {
+            const uint32_t Lm = swar_le4(dw[m + 1]);
+            const uint32_t cm = Lm & __builtin_amdgcn_alignbit(Ln, Lm, 8);
+            if (m < 32) wlo |= cm ? (1u << m) : 0u;
+            else whi |= cm ? (1u << (m - 32)) : 0u;
+            Ln = Lm;
+        }
+        wm = ((uint64_t)whi << 32) | wlo;
+    }
+    spec_lane(T, lane, wm, sp);
+    if (T.fof) { guess = 0; return; }
+    // guess: the first lane whose chain also survives a second exit check
+    // (a lane whose exit is where the stripe holding it starts its own chain is
+    // confirmed without it)
+    const bool ext = sp.s >= 0 && sp.x < T.dlen;
+    const int tl = ext ? (int)(sp.x / CLY_SUB) : lane;
+    const int ts = __shfl(sp.s, tl, 64);
+    const int conf = ext && ts == (int)sp.x;
+    unsigned long long m = __ballot(sp.s >= 0);
+    guess = -1;
+    while (m) {
+        const int k = __ffsll((long long)m) - 1;
+        int ok = conf;
+        if (lane == k && !ok) ok = deep_check(T, sp.x);
+        if (__shfl(ok, k, 64)) { guess = __shfl(sp.s, k, 64); break; }
+        m &= m - 1;
     }
 }
 
@@ -859,70 +929,6 @@ __device__ __forceinline__ void sub_setup(Sub& T, int64_t sidx, const DevFile& F
     T.fid = F.fid;
 }
 
-// Second exit check of a speculative chain leaving its stripe at x (x itself
-// decoded as a plain record): the record after x must decode as one too.
-__device__ __forceinline__ int deep_check(const Sub& T, int64_t x) {
-    if (x >= T.nrel) return x == T.nrel;
-    Hdr e;
-    if (x + 26 <= T.win_len) e = hdr_at(T.w32, (int)x, T.nrel, T.cbase + x);
-    else hdr_global(T.gfile, T.cbase, x, T.nrel, e);
-    if (!e.good) return 0;
-    const int64_t x2 = x + e.size;
-    if (x2 >= T.nrel) return x2 == T.nrel;
-    Hdr f;
-    if (x2 + 26 <= T.win_len) f = hdr_at(T.w32, (int)x2, T.nrel, T.cbase + x2);
-    else hdr_global(T.gfile, T.cbase, x2, T.nrel, f);
-    return f.good ? 1 : 0;
-}
-
-// Speculation over the staged window: per lane the first candidate (register
-// SWAR filter over its stripe), then the candidate walks; the sub-tile guess.
-__device__ __forceinline__ void sub_spec(const Sub& T, int lane, Spec& sp, int& guess) {
-    const CLY_LDS uint32_t* w32 = T.w32;
-    sp.s = -1; sp.last = -1; sp.c = 0; sp.x = 0;
-    int q0 = CLY_TS;
-    const int a = lane * CLY_SUB;
-    if (a < T.dlen) {
-        uint32_t dw[CLY_NWD + 2];
-        const CLY_LDS u32x4* s4 = (const CLY_LDS u32x4*)(w32 + lane * CLY_NWD);
-        #pragma unroll
-        for (int i = 0; i < CLY_NWD / 4; i++) {
-            const u32x4 v = s4[i];
-            dw[4 * i] = v.x; dw[4 * i + 1] = v.y; dw[4 * i + 2] = v.z; dw[4 * i + 3] = v.w;
-        }
-        dw[CLY_NWD] = w32[lane * CLY_NWD + CLY_NWD];
-        dw[CLY_NWD + 1] = w32[lane * CLY_NWD + CLY_NWD + 1];
-        int fm = CLY_NWD;
-        uint32_t Ln = swar_le4(dw[CLY_NWD + 1]);
-        #pragma unroll
-        for (int m = CLY_NWD - 1; m >= 0; m--) {
-            const uint32_t Lm = swar_le4(dw[m + 1]);
-            const uint32_t cm = Lm & __builtin_amdgcn_alignbit(Ln, Lm, 8);
-            fm = cm ? m : fm;
-            Ln = Lm;
-        }
-        if (fm < CLY_NWD) q0 = next_candidate(w32, a + 4 * fm, a + CLY_SUB < T.dlen ? a + CLY_SUB : T.dlen);
-    }
-    spec_lane(T, lane, q0, sp);
-    if (T.fof) { guess = 0; return; }
-    // guess: the first lane whose chain also survives a second exit check
-    // (a lane whose exit is where the stripe holding it starts its own chain is
-    // confirmed without it)
-    const bool ext = sp.s >= 0 && sp.x < T.dlen;
-    const int tl = ext ? (int)(sp.x / CLY_SUB) : lane;
-    const int ts = __shfl(sp.s, tl, 64);
-    const int conf = ext && ts == (int)sp.x;
-    unsigned long long m = __ballot(sp.s >= 0);
-    guess = -1;
-    while (m) {
-        const int k = __ffsll((long long)m) - 1;
-        int ok = conf;
-        if (lane == k && !ok) ok = deep_check(T, sp.x);
-        if (__shfl(ok, k, 64)) { guess = __shfl(sp.s, k, 64); break; }
-        m &= m - 1;
-    }
-}
-
 // Chain for the given final mode / entry.
 __device__ __forceinline__ void sub_chain(const Sub& T, const Spec& sp, int lane, int mode, int entry, Lane& L,
                                           Chain& R) {
@@ -1121,6 +1127,9 @@ __device__ __forceinline__ SubDesc make_desc(const Sub& T, const Chain& R) {
 
 // One sub-tile, start to end, for a chain given by (mode, entry) or, mode < 0,
 // by its own guess (mode -2: test mode, odd sub-tiles take a wrong guess).
+#ifndef CLY_EXP                 // timing experiments only (tools/exp_time.py): phases skipped, results wrong
+#define CLY_EXP 0
+#endif
 #define PF_N ((CLY_WIN / 16 + 63) / 64)       // 16-B pieces per lane of a prefetched window
 __device__ __forceinline__ void prefetch_issue(const uint8_t* src, int lane, u32x4 (&pf)[PF_N]) {
     const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
@@ -1155,7 +1164,11 @@ __device__ __forceinline__ void process_sub(int64_t sidx, int mode, int entry, c
     PROF(0);
     Spec sp;
     int guess = -1;
-    sub_spec(T, lane, sp, guess);
+    if (CLY_EXP & 4) {          // experiment: no speculation
+        sp.s = -1; sp.last = -1; sp.c = 0; sp.x = 0; guess = T.fof ? 0 : -1;
+    } else {
+        sub_spec(T, lane, sp, guess);
+    }
     if (pf_src) prefetch_issue(pf_src, lane, pf);
     PROF(1);
     Lane L;
@@ -1166,11 +1179,12 @@ __device__ __forceinline__ void process_sub(int64_t sidx, int mode, int entry, c
         entry = guess;
         if (force) mode = (sidx & 2) ? MODE_DEAD : MODE_PASS;
     }
+    if ((CLY_EXP & 8) && !T.fof) mode = MODE_PASS;    // experiment: no chain
     sub_chain(T, sp, lane, mode, entry, L, R);
     PROF(2);
-    stage_tuples(T, L, R, staging);                 // before the CRC phase patches the window
+    if (!(CLY_EXP & 1)) stage_tuples(T, L, R, staging);     // before the CRC phase patches the window
     PROF(3);
-    sub_crc(T, L, R, lane, smem, pool, 0, sums, g);
+    if (!(CLY_EXP & 2)) sub_crc(T, L, R, lane, smem, pool, 0, sums, g);
     PROF(4);
     d = make_desc(T, R);
     if (lane == 0) {
@@ -1790,8 +1804,8 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         HIPCK(hipStreamSynchronize(st));
         const uint32_t ncand = c->h_g->ncand, nfix = c->h_g->nfix;
         if (c->h_g->fail) break;
-        if (ncand == 0) break;
-        if (++rounds > FIX_ROUNDS || nfix == 0) {
+        if (ncand == 0 || CLY_EXP) break;         // (experiment builds: timing only)
+        if (++rounds > FIX_ROUNDS) {
             fprintf(stderr, "clyscan: chain resolution did not converge (%u candidates, %u fixes)\n", ncand, nfix);
             return CLY_ERR_NOREPAIR;
         }
@@ -1810,7 +1824,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
             fprintf(stderr, "\n");
             free(hf);
         }
-        if (rounds > SERIAL_AFTER) {
+        if (rounds > SERIAL_AFTER || nfix == 0) {
             // the parallel rounds did not settle: one exact serial walk per file
             hipLaunchKernelGGL(k_serial, dim3(nfiles), dim3(64), CLY_SCAN_LDS, st, c->d_files, c->d_cand, c->d_fck,
                                c->d_desc, c->d_sums, c->d_cols, c->d_staging, c->d_g);

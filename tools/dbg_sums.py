@@ -45,6 +45,16 @@ sc.lib.cly_dbg_descs(sc.ctx, desc.ctypes.data, n)
 sp = np.zeros(n, np.uint64)
 sc.lib.cly_dbg_subp.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
 sc.lib.cly_dbg_subp(sc.ctx, sp.ctypes.data, n)
+sdt = np.dtype([("evt_off", "<i8"), ("evt_gidx", "<u8"), ("open_pos", "<i8"), ("evt_status", "<i4"),
+                ("cnt", "<u4"), ("open_state", "<u4"), ("open_crc", "<u4"), ("head_raw", "<u4"), ("head_shift", "<u4"),
+                ("first4", "<u4"), ("head_len", "<u4"), ("flags", "<u4"), ("head_z", "<u4")])
+assert sdt.itemsize == sc.lib.cly_dbg_sumsize(), (sdt.itemsize, sc.lib.cly_dbg_sumsize())
+sums = np.zeros(n, sdt)
+sc.lib.cly_dbg_sums.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+sc.lib.cly_dbg_sums(sc.ctx, sums.ctypes.data, n)
+for i in range(lo, n):
+    print("sum %4d" % i, {k: (hex(int(sums[i][k])) if k in ("open_state", "open_crc", "head_raw", "first4") else int(sums[i][k]))
+                          for k in sdt.names})
 offs = [int(x["offset"]) for x in t]
 for i in range(lo, n):
     d = desc[i]
