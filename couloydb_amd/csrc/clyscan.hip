@@ -1198,7 +1198,9 @@ __device__ __forceinline__ void process_sub(int64_t sidx, int mode, int entry, c
 __global__ void __launch_bounds__(64 * CLY_NDW)
 k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ sub_prefix, int64_t nsub,
        SubDesc* descs, ChunkSum* sums, const uint32_t* __restrict__ cols, cly_tuple* staging, Globals* g, int gmode) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    // static LDS: its offsets are known when compiling, so table and window
+    // addresses need no base add (a dynamic extern array costs one v_add per lookup)
+    __shared__ __attribute__((aligned(16))) unsigned char smem_raw[CLY_SCAN_LDS];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
     init_tables(smem, cols);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1670,14 +1672,13 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     for (int n = 1; n < CLY_TS + 8; n++) hx[n] = cly_multmodp(x8, hx[n - 1]);
     HIPCK(hipMemcpy(c->d_x8n, hx, x8_bytes, hipMemcpyHostToDevice));
     free(hx);
-    HIPCK(hipFuncSetAttribute((const void*)k_scan, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CLY_SCAN_LDS));
     HIPCK(hipFuncSetAttribute((const void*)k_fix, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CLY_SCAN_LDS));
     HIPCK(hipFuncSetAttribute((const void*)k_serial, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CLY_SCAN_LDS));
     HIPCK(hipFuncSetAttribute((const void*)k_place, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)(CLY_NDW * CLY_WIN)));
     {
         int per_cu = 0, ncu = 0;
-        HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_scan, 64 * CLY_NDW, CLY_SCAN_LDS));
+        HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_scan, 64 * CLY_NDW, 0));
         HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
         if (per_cu < 1) per_cu = 1;
         c->scan_grid = per_cu * ncu;
@@ -1781,7 +1782,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     HIPCK(hipEventRecord(c->ev[0], st));
     int grid = c->scan_grid;
     if ((int64_t)grid * CLY_NDW > nsub) grid = (int)((nsub + CLY_NDW - 1) / CLY_NDW);
-    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * CLY_NDW), CLY_SCAN_LDS, st, c->d_files, nfiles, c->d_prefix, nsub,
+    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * CLY_NDW), 0, st, c->d_files, nfiles, c->d_prefix, nsub,
                        c->d_desc, c->d_sums, c->d_cols, c->d_staging, c->d_g, (c->dbg_flags & 2) ? -2 : -1);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[1], st));
