@@ -737,8 +737,10 @@ __device__ __forceinline__ void crc_phase(const Sub& T, const Lane& L, const Cha
             int p = L.ws;
             for (int r = 0; r < L.wc; r++, i++) {
                 pool[i] = (u32x2){(uint32_t)p | CP_REAL, lds_le32(w32, p)};
-                const Hdr h = hdr_at(w32, p, T.nrel, T.cbase + p);
-                p += (int)h.size;
+                if (r + 1 < L.wc) {
+                    const Hdr h = hdr_at(w32, p, T.nrel, T.cbase + p);
+                    p += (int)h.size;
+                }
             }
         }
         if (tcp) pool[i] = (u32x2){(uint32_t)L.wx, lds_le32(w32, (int)L.wx)};
