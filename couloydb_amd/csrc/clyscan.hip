@@ -392,6 +392,7 @@ struct Chain {                   // wave-uniform result of resolve()
 // (or is the end of the file).
 struct Spec {
     int s, last, c;
+    int v;                       // the exit was checked (else: beyond the window, unchecked)
     int64_t x;
 };
 
@@ -423,12 +424,12 @@ __device__ __forceinline__ uint32_t cand_bits(const CLY_LDS uint32_t* w32, int a
 
 // Speculative walk of one lane: the first candidate of its stripe (from the
 // word mask wm) whose chain of plain records leaves the stripe at an exit that
-// decodes as a plain record, the end of the file, or a position beyond the
-// window (left unchecked: the chain check of resolve() and the guess's own
-// deep check cover it).  Candidates whose key-size byte is odd or zero
-// (ks < 1) are skipped before decoding.
+// decodes as a plain record or is the end of the file; failing that, the first
+// whose exit lies beyond the window (left unchecked: the chain check of
+// resolve() and the guess's own deep check cover it).  Candidates whose
+// key-size byte is odd or zero (ks < 1) are skipped before decoding.
 __device__ __forceinline__ void spec_lane(const Sub& T, int lane, uint64_t wm, Spec& r) {
-    r.s = -1; r.last = -1; r.c = 0; r.x = 0;
+    r.s = -1; r.last = -1; r.c = 0; r.v = 0; r.x = 0;
     const int a = lane * CLY_SUB;
     if (a >= T.dlen) return;
     const int b = a + CLY_SUB < T.dlen ? a + CLY_SUB : T.dlen;
@@ -465,11 +466,18 @@ __device__ __forceinline__ void spec_lane(const Sub& T, int lane, uint64_t wm, S
                 x = p + h2.size;
             }
             if (!ok || x > T.nrel) continue;           // a chain past the end of the file is not a guess
-            if (x < T.nrel && x + 26 <= T.win_len) {
+            if (x < T.nrel && x + 26 > T.win_len) {
+                // exit beyond the window: kept unchecked as a fallback, but a
+                // later candidate with a checked exit wins (a false candidate
+                // must not hide the lane's true record)
+                if (r.s < 0) { r.s = q; r.last = (int)p; r.c = c; r.v = 0; r.x = x; }
+                continue;
+            }
+            if (x < T.nrel) {
                 const Hdr e = hdr_at(T.w32, (int)x, T.nrel, T.cbase + x);
                 if (!e.good) continue;
             }
-            r.s = q; r.last = (int)p; r.c = c; r.x = x;
+            r.s = q; r.last = (int)p; r.c = c; r.v = 1; r.x = x;
             return;
         }
     }
@@ -526,8 +534,8 @@ __device__ __forceinline__ void sub_spec(const Sub& T, int lane, Spec& sp, int& 
     // confirmed without it)
     const bool ext = sp.s >= 0 && sp.x < T.dlen;
     const int tl = ext ? (int)(sp.x / CLY_SUB) : lane;
-    const int ts = __shfl(sp.s, tl, 64);
-    const int conf = ext && ts == (int)sp.x;
+    const int ts = __shfl(sp.s, tl, 64), tv = __shfl(sp.v, tl, 64);
+    const int conf = ext && ts == (int)sp.x && tv;      // (an unchecked spec confirms nothing)
     unsigned long long m = __ballot(sp.s >= 0);
     guess = -1;
     while (m) {
@@ -1154,11 +1162,11 @@ __device__ __forceinline__ void prefetch_commit(CLY_LDS uint32_t* w32, int lane,
 // One sub-tile: window (already in LDS when `ready`), speculation, chain,
 // tuples, CRC, descriptor.  When pf_src is set, the window of the wave's next
 // sub-tile is loaded into pf[] on the way (after the phases that read HBM).
-__device__ __forceinline__ void process_sub(int64_t sidx, int mode, int entry, const DevFile& F, int lane,
+__device__ __forceinline__ bool process_sub(int64_t sidx, int mode, int entry, const DevFile& F, int lane,
                                             CLY_LDS uint8_t* smem, CLY_LDS uint32_t* w32, CLY_LDS u32x2* pool,
                                             SubDesc* descs, ChunkSum* sums, cly_tuple* staging, Globals* g,
                                             int prof_base, SubDesc& d, bool ready, const uint8_t* pf_src,
-                                            u32x4 (&pf)[PF_N]) {
+                                            u32x4 (&pf)[PF_N], bool tentative = false) {
     PROF_INIT();
     Sub T;
     sub_setup(T, sidx, F, w32);
@@ -1167,7 +1175,7 @@ __device__ __forceinline__ void process_sub(int64_t sidx, int mode, int entry, c
     Spec sp;
     int guess = -1;
     if (CLY_EXP & 4) {          // experiment: no speculation
-        sp.s = -1; sp.last = -1; sp.c = 0; sp.x = 0; guess = T.fof ? 0 : -1;
+        sp.s = -1; sp.last = -1; sp.c = 0; sp.v = 0; sp.x = 0; guess = T.fof ? 0 : -1;
     } else {
         sub_spec(T, lane, sp, guess);
     }
@@ -1184,6 +1192,12 @@ __device__ __forceinline__ void process_sub(int64_t sidx, int mode, int entry, c
     if ((CLY_EXP & 8) && !T.fof) mode = MODE_PASS;    // experiment: no chain
     sub_chain(T, sp, lane, mode, entry, L, R);
     PROF(2);
+    if (tentative && R.mode == MODE_NORMAL && R.term && !T.lof) {
+        // an uncertain fix whose chain ends inside the file: most likely a
+        // false entry; leave the sub-tile as it is (its state gets certain later)
+        d = descs[T.chunk];
+        return false;
+    }
     if (!(CLY_EXP & 1)) stage_tuples(T, L, R, staging);     // before the CRC phase patches the window
     PROF(3);
     if (!(CLY_EXP & 2)) sub_crc(T, L, R, lane, smem, pool, 0, sums, g);
@@ -1195,6 +1209,7 @@ __device__ __forceinline__ void process_sub(int64_t sidx, int mode, int entry, c
     }
     PROF(5);
     PROF_FLUSH(prof_base);
+    return true;
 }
 
 __global__ void __launch_bounds__(64 * CLY_NDW)
@@ -1261,7 +1276,8 @@ k_fix(const DevFile* __restrict__ files, const Fix* fixes, uint32_t nfix, uint32
         for (;;) {
             SubDesc d;
             u32x4 pf[PF_N];
-            process_sub(s, mode, entry, F, lane, smem, w32, pool, descs, sums, staging, g, 8, d, false, nullptr, pf);
+            if (!process_sub(s, mode, entry, F, lane, smem, w32, pool, descs, sums, staging, g, 8, d, false, nullptr, pf,
+                             pass == 1 && s == (int64_t)fx.s)) break;
             if (d.mode == MODE_DEAD || (d.mode == MODE_NORMAL && (d.flags & SD_TERM))) break;
             if (d.mode == MODE_NORMAL) x = d.x;
             if (++s >= s_end) break;
@@ -1365,7 +1381,7 @@ k_link2(LinkAgg* blk, int64_t nblk) {
 __global__ void __launch_bounds__(LINK_NT)
 k_link3(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ sub_prefix,
         const SubDesc* __restrict__ descs, int64_t nsub, const LinkAgg* __restrict__ blk, uint64_t* sub_P, Fix* cand,
-        uint32_t cand_cap, int32_t* fh, unsigned long long* fck, Globals* g) {
+        uint32_t cand_cap, int32_t* fh, unsigned long long* fck, uint32_t* cflag, uint32_t stamp, Globals* g) {
     const int64_t b0 = (int64_t)blockIdx.x * LINK_BLK + (int64_t)threadIdx.x * LINK_IT;
     LinkAgg v = link_ident();
     SubDesc d[LINK_IT];
@@ -1396,7 +1412,9 @@ k_link3(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
         if (!ok) {
             const uint32_t f = (uint32_t)find_file(sub_prefix, nfiles, s);
             // harmful: the wrong chain changes the state passed on (PASS and DEAD both pass it through)
-            if (live && mode >= 0 && (mode == MODE_NORMAL || d[i].mode == MODE_NORMAL)) atomicMin(&fh[f], (int32_t)s);
+            const bool harmful = live && mode >= 0 && (mode == MODE_NORMAL || d[i].mode == MODE_NORMAL);
+            if (harmful) atomicMin(&fh[f], (int32_t)s);
+            cflag[s] = 2 * stamp + (harmful ? 1u : 0u);
             const uint32_t k = atomicAdd(&g->ncand, 1u);
             if (k < cand_cap) {
                 Fix c;
@@ -1464,15 +1482,32 @@ k_serial(const DevFile* __restrict__ files, const Fix* __restrict__ cand, const 
 // Fix list of the round: every candidate up to and including the first harmful
 // sub-tile of its file (its state is certain); later candidates only when they
 // hold a wrong record chain (never turned into PASS / DEAD on an uncertain
-// state, which would discard a good guess).
+// state, which would discard a good guess: a false exit far ahead makes every
+// sub-tile up to it look covered).  Uncertain fixes run after the certain walks
+// and are dropped when their chain ends before the file does.
 __global__ void __launch_bounds__(LINK_NT)
-k_link4(const Fix* __restrict__ cand, const int32_t* __restrict__ fh, Fix* fixes, uint32_t* listed, uint32_t stamp,
-        Globals* g) {
+k_link4(const DevFile* __restrict__ files, const SubDesc* __restrict__ descs, const Fix* __restrict__ cand,
+        const int32_t* __restrict__ fh, const uint32_t* __restrict__ cflag, Fix* fixes, uint32_t* listed,
+        uint32_t stamp, Globals* g) {
     const uint32_t n = g->ncand;
     for (uint32_t i = blockIdx.x * LINK_NT + threadIdx.x; i < n; i += gridDim.x * LINK_NT) {
         const Fix c = cand[i];
         if (c.mode < 0) continue;
-        const bool certain = (int64_t)c.s <= (int64_t)fh[c.file];
+        // certain: no harmful candidate since the last sub-tile that agreed with
+        // its state on a record entry (its own exit then fixes the state), or
+        // since the file start; past 256 sub-tiles back: since the file start
+        bool certain = (int64_t)c.s <= (int64_t)fh[c.file];
+        if (!certain) {
+            const int64_t s_first = files[c.file].first_sub;
+            int64_t t = (int64_t)c.s - 1;
+            for (int k = 0; k < 256 && t >= s_first; k++, t--) {
+                const uint32_t cf = cflag[t];
+                if (cf == 2 * stamp + 1) break;                      // harmful candidate: uncertain
+                if (cf == 2 * stamp) continue;                       // harmless candidate
+                if (descs[t].mode == MODE_NORMAL) { certain = true; break; }   // agreed on an entry
+            }
+            if (t < s_first) certain = true;
+        }
         if (!certain && c.mode != MODE_NORMAL) continue;
         listed[c.s] = certain ? stamp : (stamp | LISTED_U);
         Fix e = c;
@@ -1622,6 +1657,7 @@ struct cly_ctx {
     Fix* d_fix;                  // fix list of a round
     Fix* d_cand;                 // candidates of a round
     uint32_t* d_listed;          // per sub-tile: stamp of the last round that listed it
+    uint32_t* d_cflag;           // per sub-tile: 2 stamp + harmful, for the candidates of a round
     int32_t* d_fh;               // per file: first harmful sub-tile of a round
     unsigned long long* d_fkey;  // per file: first event key (k_fin1)
     unsigned long long* d_fck;   // per file: first candidate key of a round
@@ -1695,7 +1731,7 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     hipStreamSynchronize(c->stream);
     hipFree(c->d_files); hipFree(c->d_prefix); hipFree(c->d_fout); hipFree(c->d_desc); hipFree(c->d_sums);
     hipFree(c->d_subP); hipFree(c->d_staging); hipFree(c->d_blk); hipFree(c->d_fix); hipFree(c->d_cand);
-    hipFree(c->d_listed); hipFree(c->d_fh); hipFree(c->d_fkey); hipFree(c->d_fck); hipFree(c->d_g); hipFree(c->d_cols); hipFree(c->d_x8n); hipFree(c->d_bytes); hipFree(c->d_tuples);
+    hipFree(c->d_listed); hipFree(c->d_cflag); hipFree(c->d_fh); hipFree(c->d_fkey); hipFree(c->d_fck); hipFree(c->d_g); hipFree(c->d_cols); hipFree(c->d_x8n); hipFree(c->d_bytes); hipFree(c->d_tuples);
     hipHostFree(c->h_files); hipHostFree(c->h_prefix); hipHostFree(c->h_fout); hipHostFree(c->h_g);
     for (int i = 0; i < 4; i++) hipEventDestroy(c->ev[i]);
     hipStreamDestroy(c->stream);
@@ -1729,7 +1765,7 @@ static int ensure_files(cly_ctx* c, int nfiles) {
 static int ensure_subs(cly_ctx* c, int64_t nsub) {
     if (nsub <= c->cap_subs) return CLY_OK;
     hipFree(c->d_desc); hipFree(c->d_sums); hipFree(c->d_subP); hipFree(c->d_staging); hipFree(c->d_blk);
-    hipFree(c->d_fix); hipFree(c->d_cand); hipFree(c->d_listed);
+    hipFree(c->d_fix); hipFree(c->d_cand); hipFree(c->d_listed); hipFree(c->d_cflag);
     const int64_t cap = nsub < 1024 ? 1024 : nsub;
     HIPCK(hipMalloc(&c->d_desc, sizeof(SubDesc) * cap));
     HIPCK(hipMalloc(&c->d_sums, sizeof(ChunkSum) * cap));
@@ -1740,6 +1776,8 @@ static int ensure_subs(cly_ctx* c, int64_t nsub) {
     HIPCK(hipMalloc(&c->d_cand, sizeof(Fix) * cap));
     HIPCK(hipMalloc(&c->d_listed, sizeof(uint32_t) * cap));
     HIPCK(hipMemset(c->d_listed, 0, sizeof(uint32_t) * cap));
+    HIPCK(hipMalloc(&c->d_cflag, sizeof(uint32_t) * cap));
+    HIPCK(hipMemset(c->d_cflag, 0, sizeof(uint32_t) * cap));
     c->stamp = 0;
     c->cap_subs = cap;
     return CLY_OK;
@@ -1799,15 +1837,17 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         hipLaunchKernelGGL(k_link1, dim3(nblk), dim3(LINK_NT), 0, st, c->d_desc, nsub, c->d_blk);
         hipLaunchKernelGGL(k_link2, dim3(1), dim3(LINK_NT), 0, st, c->d_blk, nblk);
         hipLaunchKernelGGL(k_link3, dim3(nblk), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_prefix, c->d_desc, nsub,
-                           c->d_blk, c->d_subP, c->d_cand, (uint32_t)c->cap_subs, c->d_fh, c->d_fck, c->d_g);
-        hipLaunchKernelGGL(k_link4, dim3(64), dim3(LINK_NT), 0, st, c->d_cand, c->d_fh, c->d_fix, c->d_listed, stamp,
+                           c->d_blk, c->d_subP, c->d_cand, (uint32_t)c->cap_subs, c->d_fh, c->d_fck, c->d_cflag, stamp,
+                           c->d_g);
+        hipLaunchKernelGGL(k_link4, dim3(64), dim3(LINK_NT), 0, st, c->d_files, c->d_desc, c->d_cand, c->d_fh, c->d_cflag,
+                           c->d_fix, c->d_listed, stamp,
                            c->d_g);
         HIPCK(hipGetLastError());
         HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
         HIPCK(hipStreamSynchronize(st));
         const uint32_t ncand = c->h_g->ncand, nfix = c->h_g->nfix;
         if (c->h_g->fail) break;
-        if (ncand == 0 || CLY_EXP) break;         // (experiment builds: timing only)
+        if (ncand == 0 || CLY_EXP || (c->dbg_flags & 16)) break;   // (experiment builds / debug: no fix rounds)
         if (++rounds > FIX_ROUNDS) {
             fprintf(stderr, "clyscan: chain resolution did not converge (%u candidates, %u fixes)\n", ncand, nfix);
             return CLY_ERR_NOREPAIR;
