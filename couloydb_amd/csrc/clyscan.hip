@@ -688,6 +688,7 @@ __device__ __forceinline__ void crc_patch_all(CLY_LDS uint8_t* smem, CLY_LDS uin
 }
 
 // Register of one lane over its stripe words d[] (patched), with the reset.
+template <bool OBSERVE>
 __device__ __forceinline__ void crc_loop(const CLY_LDS uint8_t* smem, const uint32_t* d, int rs, uint64_t chk,
                                          uint32_t lane_off, uint32_t& s_out, uint32_t& obs_out, uint32_t& err_out) {
     uint32_t s = 0, obs = 0, err = 0;
@@ -697,8 +698,10 @@ __device__ __forceinline__ void crc_loop(const CLY_LDS uint8_t* smem, const uint
         obs = r ? s : obs;
         const uint32_t x = (r ? 0u : s) ^ d[i];
         s = crc_word(smem, x, lane_off);
-        const uint32_t m = (uint32_t)(-(int32_t)((chk >> i) & 1));
-        err |= s & m;
+        if (OBSERVE) {
+            const uint32_t m = (uint32_t)(-(int32_t)((chk >> i) & 1));
+            err |= s & m;
+        }
     }
     s_out = s; obs_out = obs; err_out = err;
 }
@@ -785,7 +788,9 @@ __device__ __forceinline__ void crc_phase(const Sub& T, const Lane& L, const Cha
         if (lane == 0) d[0] = 0;                // head raw register counts from byte 4
     }
     uint32_t s, obs, err;
-    crc_loop(smem, d, rs, chk, lane_off, s, obs, err);
+    // (no lane with a second check point: the loop without observations)
+    if (__ballot(chk != 0)) crc_loop<true>(smem, d, rs, chk, lane_off, s, obs, err);
+    else crc_loop<false>(smem, d, rs, chk, lane_off, s, obs, err);
     // ---- segmented scan: element (c, v), S -> c ? v : A^SUB S ^ v
     int c = rs >= 0;
     uint32_t v = s;
