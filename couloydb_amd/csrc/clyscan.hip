@@ -394,6 +394,7 @@ struct Spec {
     int s, last, c;
     int v;                       // the exit was checked (else: beyond the window, unchecked)
     int64_t x;
+    Hdr h;                       // header of the record at s (reused for its tuple)
 };
 
 // Exact walk (ReadLogRecord semantics, any record or terminal) of the lane's
@@ -470,14 +471,14 @@ __device__ __forceinline__ void spec_lane(const Sub& T, int lane, uint64_t wm, S
                 // exit beyond the window: kept unchecked as a fallback, but a
                 // later candidate with a checked exit wins (a false candidate
                 // must not hide the lane's true record)
-                if (r.s < 0) { r.s = q; r.last = (int)p; r.c = c; r.v = 0; r.x = x; }
+                if (r.s < 0) { r.s = q; r.last = (int)p; r.c = c; r.v = 0; r.x = x; r.h = h; }
                 continue;
             }
             if (x < T.nrel) {
                 const Hdr e = hdr_at(T.w32, (int)x, T.nrel, T.cbase + x);
                 if (!e.good) continue;
             }
-            r.s = q; r.last = (int)p; r.c = c; r.v = 1; r.x = x;
+            r.s = q; r.last = (int)p; r.c = c; r.v = 1; r.x = x; r.h = h;
             return;
         }
     }
@@ -1028,9 +1029,9 @@ __device__ __forceinline__ void sub_crc(const Sub& T, const Lane& L, const Chain
 }
 
 // Tuple words of one record at window position p (index independent).
-__device__ __forceinline__ void tuple_words(const Sub& T, int p, u32x4& q0, u32x4& q1, u32x4& q2, int64_t& size) {
+__device__ __forceinline__ void tuple_words_h(const Sub& T, int p, const Hdr& h, u32x4& q0, u32x4& q1, u32x4& q2,
+                                              int64_t& size) {
     const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)T.w32;
-    const Hdr h = hdr_at(T.w32, p, T.nrel, T.cbase + p);
     int tn;
     const int64_t klim = h.ks < 11u ? (int64_t)h.ks : 11;
     const int64_t tx = go_varint(w8 + p + h.hsz, klim, tn);      // parseLogRecordKey, db.go:706-710
@@ -1044,6 +1045,10 @@ __device__ __forceinline__ void tuple_words(const Sub& T, int p, u32x4& q0, u32x
                      ((uint32_t)(tn < 0 ? 0xFF : tn) << 24),
                  h.crc};
     size = h.size;
+}
+__device__ __forceinline__ void tuple_words(const Sub& T, int p, u32x4& q0, u32x4& q1, u32x4& q2, int64_t& size) {
+    const Hdr h = hdr_at(T.w32, p, T.nrel, T.cbase + p);
+    tuple_words_h(T, p, h, q0, q1, q2, size);
 }
 
 __device__ __forceinline__ void put_tuple(cly_tuple* out, uint64_t idx, uint64_t out_cap, const u32x4& q0,
@@ -1112,7 +1117,8 @@ __device__ __forceinline__ void init_tables(CLY_LDS uint8_t* smem, const uint32_
 // fit).  The slot is three planes of CLY_CAP 16-B pieces (piece k of tuple i
 // at plane k, row i), so with one record per lane each store instruction
 // writes one contiguous run; k_copy interleaves the planes back.
-__device__ __forceinline__ void stage_tuples(const Sub& T, const Lane& L, const Chain& R, cly_tuple* staging) {
+__device__ __forceinline__ void stage_tuples(const Sub& T, const Spec& sp, const Lane& L, const Chain& R,
+                                             cly_tuple* staging) {
     if (R.mode != MODE_NORMAL || R.cnt > CLY_CAP) return;
     if (L.ws < 0) return;
     u32x4* slot = (u32x4*)staging + (uint64_t)T.chunk * (3 * CLY_CAP);
@@ -1120,7 +1126,8 @@ __device__ __forceinline__ void stage_tuples(const Sub& T, const Lane& L, const 
     for (int i = 0; i < L.wc; i++) {
         u32x4 q0, q1, q2;
         int64_t size;
-        tuple_words(T, p, q0, q1, q2, size);
+        if (i == 0 && p == sp.s) tuple_words_h(T, p, sp.h, q0, q1, q2, size);   // decoded by the speculation
+        else tuple_words(T, p, q0, q1, q2, size);
         const int r = (int)L.base + i;
         slot[r] = q0;
         slot[CLY_CAP + r] = q1;
@@ -1203,7 +1210,7 @@ __device__ __forceinline__ bool process_sub(int64_t sidx, int mode, int entry, c
         d = descs[T.chunk];
         return false;
     }
-    if (!(CLY_EXP & 1)) stage_tuples(T, L, R, staging);     // before the CRC phase patches the window
+    if (!(CLY_EXP & 1)) stage_tuples(T, sp, L, R, staging);     // before the CRC phase patches the window
     PROF(3);
     if (!(CLY_EXP & 2)) sub_crc(T, L, R, lane, smem, pool, 0, sums, g);
     PROF(4);
