@@ -1270,6 +1270,8 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
 __global__ void __launch_bounds__(64 * CLY_NDW)
 k_fix(const DevFile* __restrict__ files, const Fix* fixes, uint32_t nfix, uint32_t* listed, uint32_t stamp, int pass,
       SubDesc* descs, ChunkSum* sums, const uint32_t* __restrict__ cols, cly_tuple* staging, Globals* g) {
+    if (nfix == ~0u) nfix = __hip_atomic_load(&g->nfix, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (launched ahead)
+    if (blockIdx.x * CLY_NDW >= nfix) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
     init_tables(smem, cols);
@@ -1491,6 +1493,14 @@ k_serial(const DevFile* __restrict__ files, const Fix* __restrict__ cand, const 
     }
 }
 
+// Per-round reset of the link state (one launch instead of four memsets).
+__global__ void __launch_bounds__(LINK_NT)
+k_round_init(int32_t* fh, unsigned long long* fck, int nfiles, Globals* g) {
+    const int i = blockIdx.x * LINK_NT + threadIdx.x;
+    if (i == 0) { g->nfix = 0; g->ncand = 0; }
+    if (i < nfiles) { fh[i] = 0x7f7f7f7f; fck[i] = ~0ull; }
+}
+
 // Fix list of the round: every candidate up to and including the first harmful
 // sub-tile of its file (its state is certain); later candidates only when they
 // hold a wrong record chain (never turned into PASS / DEAD on an uncertain
@@ -1525,6 +1535,7 @@ k_link4(const DevFile* __restrict__ files, const SubDesc* __restrict__ descs, co
         Fix e = c;
         e.certain = certain;
         fixes[atomicAdd(&g->nfix, 1u)] = e;
+        atomicAdd(&g->fix_total, 1u);
     }
 }
 
@@ -1838,23 +1849,45 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
                        c->d_desc, c->d_sums, c->d_cols, c->d_staging, c->d_g, (c->dbg_flags & 2) ? -2 : -1);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[1], st));
-    // link scan, then fix rounds until every sub-tile holds the chain its state implies
-    uint32_t rounds = 0, fixes = 0;
-    for (;;) {
-        const uint32_t stamp = ++c->stamp;
-        HIPCK(hipMemsetAsync(&c->d_g->nfix, 0, sizeof(uint32_t), st));
-        HIPCK(hipMemsetAsync(&c->d_g->ncand, 0, sizeof(uint32_t), st));
-        HIPCK(hipMemsetAsync(c->d_fh, 0x7f, sizeof(int32_t) * nfiles, st));
-        HIPCK(hipMemsetAsync(c->d_fck, 0xff, sizeof(unsigned long long) * nfiles, st));
+    // link scan, then fix rounds until every sub-tile holds the chain its state
+    // implies.  The first fix round is launched without waiting for the first
+    // scan (k_fix reads the fix count itself), so the common case costs one
+    // host synchronisation.
+    uint32_t rounds = 0;
+    const int fix_grid = c->scan_grid < 64 ? c->scan_grid : 64;
+    auto link_round = [&](uint32_t stamp) -> int {
+        hipLaunchKernelGGL(k_round_init, dim3((nfiles + LINK_NT - 1) / LINK_NT), dim3(LINK_NT), 0, st, c->d_fh,
+                           c->d_fck, nfiles, c->d_g);
         hipLaunchKernelGGL(k_link1, dim3(nblk), dim3(LINK_NT), 0, st, c->d_desc, nsub, c->d_blk);
         hipLaunchKernelGGL(k_link2, dim3(1), dim3(LINK_NT), 0, st, c->d_blk, nblk);
         hipLaunchKernelGGL(k_link3, dim3(nblk), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_prefix, c->d_desc, nsub,
                            c->d_blk, c->d_subP, c->d_cand, (uint32_t)c->cap_subs, c->d_fh, c->d_fck, c->d_cflag, stamp,
                            c->d_g);
         hipLaunchKernelGGL(k_link4, dim3(64), dim3(LINK_NT), 0, st, c->d_files, c->d_desc, c->d_cand, c->d_fh, c->d_cflag,
-                           c->d_fix, c->d_listed, stamp,
-                           c->d_g);
+                           c->d_fix, c->d_listed, stamp, c->d_g);
         HIPCK(hipGetLastError());
+        return CLY_OK;
+    };
+    auto fix_round = [&](uint32_t stamp, uint32_t nfix) -> int {
+        int fgrid = nfix == ~0u ? fix_grid : (int)((nfix + CLY_NDW - 1) / CLY_NDW);
+        if (fgrid > c->scan_grid) fgrid = c->scan_grid;
+        for (int pass = 0; pass < 2; pass++)
+            hipLaunchKernelGGL(k_fix, dim3(fgrid), dim3(64 * CLY_NDW), CLY_SCAN_LDS, st, c->d_files, c->d_fix, nfix,
+                               c->d_listed, stamp, pass, c->d_desc, c->d_sums, c->d_cols, c->d_staging, c->d_g);
+        HIPCK(hipGetLastError());
+        return CLY_OK;
+    };
+    const bool ahead = !CLY_EXP && !(c->dbg_flags & (4 | 8 | 16));
+    {
+        const uint32_t stamp = ++c->stamp;
+        if ((rc = link_round(stamp))) return rc;
+        if (ahead) {
+            if ((rc = fix_round(stamp, ~0u))) return rc;
+            if ((rc = link_round(++c->stamp))) return rc;
+            rounds = 1;
+        }
+    }
+    for (;;) {
         HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
         HIPCK(hipStreamSynchronize(st));
         const uint32_t ncand = c->h_g->ncand, nfix = c->h_g->nfix;
@@ -1864,10 +1897,10 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
             fprintf(stderr, "clyscan: chain resolution did not converge (%u candidates, %u fixes)\n", ncand, nfix);
             return CLY_ERR_NOREPAIR;
         }
-        fixes += nfix;
+        const uint32_t stamp = c->stamp;
         if (c->dbg_flags & 4) {                          // debug trace of the fix rounds
             const uint32_t nshow = nfix < 64 ? nfix : 64;
-            Fix* hf = (Fix*)malloc(sizeof(Fix) * nshow);
+            Fix* hf = (Fix*)malloc(sizeof(Fix) * (nshow ? nshow : 1));
             HIPCK(hipMemcpy(hf, c->d_fix, sizeof(Fix) * nshow, hipMemcpyDeviceToHost));
             fprintf(stderr, "round %u: %u candidates, %u fixes:", rounds, ncand, nfix);
             for (uint32_t k = 0; k < nshow; k++) {
@@ -1884,13 +1917,9 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
             hipLaunchKernelGGL(k_serial, dim3(nfiles), dim3(64), CLY_SCAN_LDS, st, c->d_files, c->d_cand, c->d_fck,
                                c->d_desc, c->d_sums, c->d_cols, c->d_staging, c->d_g);
             HIPCK(hipGetLastError());
-            continue;
+        } else {
+            if ((rc = fix_round(stamp, nfix))) return rc;
         }
-        int fgrid = (int)((nfix + CLY_NDW - 1) / CLY_NDW);
-        if (fgrid > c->scan_grid) fgrid = c->scan_grid;
-        for (int pass = 0; pass < 2; pass++)
-            hipLaunchKernelGGL(k_fix, dim3(fgrid), dim3(64 * CLY_NDW), CLY_SCAN_LDS, st, c->d_files, c->d_fix, nfix,
-                               c->d_listed, stamp, pass, c->d_desc, c->d_sums, c->d_cols, c->d_staging, c->d_g);
         if (c->dbg_flags & 8) {                          // debug: descriptors and stamps after the round
             HIPCK(hipStreamSynchronize(st));
             const int64_t nd = nsub < 64 ? nsub : 64;
@@ -1904,7 +1933,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
                         hl[k] == stamp ? "w" : (hl[k] == (stamp | LISTED_U) ? "u" : ""));
             fprintf(stderr, "\n");
         }
-        HIPCK(hipGetLastError());
+        if ((rc = link_round(++c->stamp))) return rc;
     }
     HIPCK(hipEventRecord(c->ev[2], st));
     hipLaunchKernelGGL(k_copy, dim3((unsigned)((nsub + CP_SUBS - 1) / CP_SUBS)), dim3(CP_NT), 0, st, c->d_desc,
@@ -1942,7 +1971,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         total += c->h_fout[i].n_records;
     }
     if (needed) *needed = c->h_g->total;
-    c->h_g->fix_total = fixes;
+
     if (stats) {
         stats->scan_ms = ms_scan; stats->resolve_ms = ms_link + ms_tail; stats->total_ms = ms_scan + ms_link + ms_tail;
         stats->passes = 1 + rounds;
