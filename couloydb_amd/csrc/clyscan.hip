@@ -1149,6 +1149,9 @@ __device__ __forceinline__ SubDesc make_desc(const Sub& T, const Chain& R) {
 
 // One sub-tile, start to end, for a chain given by (mode, entry) or, mode < 0,
 // by its own guess (mode -2: test mode, odd sub-tiles take a wrong guess).
+#ifndef CLY_SRC_HASH
+#define CLY_SRC_HASH "unknown"
+#endif
 #ifndef CLY_EXP                 // timing experiments only (tools/exp_time.py): phases skipped, results wrong
 #define CLY_EXP 0
 #endif
@@ -2079,7 +2082,7 @@ extern "C" const char* cly_strerror(int code) {
 
 extern "C" const char* cly_build_info(void) {
     static char buf[200];
-    snprintf(buf, sizeof(buf), "clyscan gfx950 SUB=%d WAVES=%d TS=%d CAP=%d LDS=%d tables=16x", CLY_SUB, CLY_NDW, CLY_TS,
-             CLY_CAP, (int)CLY_SCAN_LDS);
+    snprintf(buf, sizeof(buf), "clyscan gfx950 SUB=%d WAVES=%d TS=%d CAP=%d LDS=%d tables=16x src=%s", CLY_SUB, CLY_NDW,
+             CLY_TS, CLY_CAP, (int)CLY_SCAN_LDS, CLY_SRC_HASH);
     return buf;
 }
