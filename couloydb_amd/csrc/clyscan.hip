@@ -87,15 +87,17 @@ struct FileOut {
 //   [LDS_WIN + k*WIN) window of wave k (sub-tile + halo, zero past the file end)
 //   [LDS_POOL ...)    per-wave check-point pools
 //   [LDS_KSNIB ...)   nibble tables of the Kogge-Stone shifts A^(SUB*2^k): 8 x 16 words each
-//   [LDS_HSCOL ...)   columns of the word shifts A^(4w)
+//   then nibble tables of A^(4b), b < 6, and A^(24a), a < HS_A: A^(4w) = A^(4b) A^(24a), w = 6a + b
 #define LDS_TAB 0
 #define LDS_INV 65536
 #define LDS_WIN (LDS_INV + 256)
 #define LDS_POOL (LDS_WIN + CLY_NDW * CLY_WIN)
 #define LDS_KSNIB (LDS_POOL + CLY_NDW * 192 * 8)
-#define LDS_HSCOL (LDS_KSNIB + CLY_KS_LEVELS * 128 * 4)
-#define CLY_SCAN_LDS (LDS_HSCOL + CLY_NWD * 32 * 4)
-#define CLY_COLS (CLY_KS_LEVELS * 128 + CLY_NWD * 32)            // words of the shift tables
+#define HS_A ((CLY_NWD + 5) / 6)
+#define NIB_HSB (CLY_KS_LEVELS * 128)                             // word offsets from LDS_KSNIB
+#define NIB_HSA (NIB_HSB + 6 * 128)
+#define CLY_COLS (NIB_HSA + HS_A * 128)                           // words of the shift tables
+#define CLY_SCAN_LDS (LDS_KSNIB + CLY_COLS * 4)
 
 // Per-sub-tile result of k_scan / k_fix, read by the link scan (16 B).
 struct SubDesc {
@@ -240,28 +242,24 @@ __device__ __forceinline__ uint32_t crc_unbyte(const CLY_LDS uint8_t* smem, uint
     const uint32_t t = *(const CLY_LDS uint32_t*)(smem + ((i << 8) | lane_off));
     return ((s ^ t) << 8) | i;
 }
-// M v for a linear map M given by its 32 columns M(1 << b) in LDS
-__device__ __forceinline__ uint32_t col_mul(const CLY_LDS uint8_t* smem, int col_byte_off, uint32_t v) {
-    const CLY_LDS u32x4* c4 = (const CLY_LDS u32x4*)(smem + col_byte_off);
-    uint32_t p = 0;
-    #pragma unroll
-    for (int q = 0; q < 8; q++) {
-        const u32x4 c = c4[q];
-        p ^= c.x & (uint32_t)__builtin_amdgcn_sbfe((int)v, 4 * q + 0, 1);
-        p ^= c.y & (uint32_t)__builtin_amdgcn_sbfe((int)v, 4 * q + 1, 1);
-        p ^= c.z & (uint32_t)__builtin_amdgcn_sbfe((int)v, 4 * q + 2, 1);
-        p ^= c.w & (uint32_t)__builtin_amdgcn_sbfe((int)v, 4 * q + 3, 1);
-    }
-    return p;
-}
 
-// A^(SUB*2^lvl) v by nibble tables: 8 lookups
-__device__ __forceinline__ uint32_t ks_mul(const CLY_LDS uint8_t* smem, int lvl, uint32_t v) {
-    const CLY_LDS uint32_t* t = (const CLY_LDS uint32_t*)(smem + LDS_KSNIB) + lvl * 128;
+// M v for a linear map M given by its nibble tables (word offset `off` from
+// LDS_KSNIB: 8 x 16 words, entry n*16+k = M (k << 4n)): 8 lookups
+__device__ __forceinline__ uint32_t nib_mul(const CLY_LDS uint8_t* smem, int off, uint32_t v) {
+    const CLY_LDS uint32_t* t = (const CLY_LDS uint32_t*)(smem + LDS_KSNIB) + off;
     uint32_t p = 0;
     #pragma unroll
     for (int n = 0; n < 8; n++) p ^= t[n * 16 + ((v >> (4 * n)) & 15u)];
     return p;
+}
+// A^(SUB*2^lvl) v
+__device__ __forceinline__ uint32_t ks_mul(const CLY_LDS uint8_t* smem, int lvl, uint32_t v) {
+    return nib_mul(smem, lvl * 128, v);
+}
+// A^(4w) v, w < NWD
+__device__ __forceinline__ uint32_t word_shift(const CLY_LDS uint8_t* smem, int w, uint32_t v) {
+    const int a = w / 6, b = w - 6 * a;
+    return nib_mul(smem, NIB_HSB + b * 128, nib_mul(smem, NIB_HSA + a * 128, v));
 }
 
 // ---------------------------------------------------------------------------
@@ -808,7 +806,7 @@ __device__ __forceinline__ void crc_phase(const Sub& T, const Lane& L, const Cha
     if (lane == 0) s_in = 0;
     out.end_state = __shfl(v, CLY_NT - 1, 64);
     // ---- reset checks: T = obs ^ A^(4 rs) S_in
-    const uint32_t y = col_mul(smem, LDS_HSCOL + (rs > 0 ? rs : 0) * 128, s_in);
+    const uint32_t y = word_shift(smem, rs > 0 ? rs : 0, s_in);
     const uint32_t Tv = obs ^ y;
     bool bad = err != 0;
     if (rs >= 0 && !rs_first) bad |= Tv != 0;
@@ -1720,9 +1718,10 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
             for (int nb = 0; nb < 8; nb++)
                 for (uint32_t v = 0; v < 16; v++) hc[lvl * 128 + nb * 16 + v] = cly_multmodp(xm, v << (4 * nb));
         }
-        for (int w = 0; w < CLY_NWD; w++) {
-            const uint32_t xm = cly_x8n((uint64_t)4 * w);
-            for (int b = 0; b < 32; b++) hc[CLY_KS_LEVELS * 128 + w * 32 + b] = cly_multmodp(xm, 1u << b);
+        for (int w = 0; w < 6 + HS_A; w++) {          // A^(4b), b < 6, then A^(24a), a < HS_A
+            const uint32_t xm = cly_x8n(w < 6 ? (uint64_t)4 * w : (uint64_t)24 * (w - 6));
+            for (int nb = 0; nb < 8; nb++)
+                for (uint32_t v = 0; v < 16; v++) hc[NIB_HSB + w * 128 + nb * 16 + v] = cly_multmodp(xm, v << (4 * nb));
         }
         HIPCK(hipMalloc(&c->d_cols, sizeof(uint32_t) * CLY_COLS));
         HIPCK(hipMemcpy(c->d_cols, hc, sizeof(uint32_t) * CLY_COLS, hipMemcpyHostToDevice));
