@@ -159,6 +159,44 @@ def cpu_baseline(wl, budget_s=12.0):
             "host_nproc": os.cpu_count()}
 
 
+def host_path(wl, sc, max_files=16):
+    """End-to-end rate of the host-memory entry cly_scan (the cgo path: mmap'd
+    files in, index tuples out): H2D of the file bytes, the scan, D2H of the
+    tuples.  Bounded to the first `max_files` files of the workload; pageable
+    buffers (what an mmap hands over) and page-locked buffers."""
+    import torch
+    from couloydb_amd import TUPLE_DTYPE, _abi
+    n = min(max_files, len(wl.dev_files))
+    pageable = [np.ascontiguousarray(wl.file_bytes(i)) for i in range(n)]
+    out_rec = {}
+    for kind in ("pageable", "pinned"):
+        bufs = pageable if kind == "pageable" else [torch.from_numpy(a).pin_memory().numpy() for a in pageable]
+        arr = (_abi.ClyFile * n)()
+        for i, a in enumerate(bufs):
+            arr[i].base, arr[i].len, arr[i].fid = a.ctypes.data, len(a), wl.dev_files[i][2]
+        cap = sum(len(a) for a in bufs) // 200 + 1024 if wl.name == "c2" else wl.expect_records + 1024
+        out = np.empty(cap, dtype=TUPLE_DTYPE)
+        first = (ctypes.c_uint64 * n)()
+        res = (_abi.ClyFileResult * n)()
+        need = ctypes.c_uint64()
+        st = _abi.ClyStats()
+        times = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            rc = sc.lib.cly_scan(sc.ctx, arr, n, out.ctypes.data, cap, first, res, ctypes.byref(need), ctypes.byref(st))
+            times.append(time.perf_counter() - t0)
+            if rc != 0:
+                return {"error": rc}
+        nbytes = sum(len(a) for a in bufs)
+        t = min(times[1:])
+        out_rec[kind] = {"value": round(nbytes / t / 2**30, 3), "unit": "GiB/s", "ms": round(t * 1e3, 2),
+                         "records": int(need.value), "tuple_bytes_d2h": int(need.value) * 48}
+        del bufs
+    out_rec["sample"] = "%d files, %.2f GiB; cly_scan (H2D + scan + D2H of the tuples), best of 2 after 1 warm-up" % (
+        n, sum(len(a) for a in pageable) / 2**30)
+    return out_rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -166,6 +204,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
     ap.add_argument("--verify", action="store_true", help="check one file against the oracle after timing")
     args = ap.parse_args()
 
@@ -239,6 +278,8 @@ def main():
         g = o[first[0]:first[0] + res[0].n_records]
         out["verify_file0"] = bool(len(g) == len(tt) and (g.view(np.uint8) == tt.view(np.uint8)).all()
                                    and so == res[0].status and eo == res[0].end_offset)
+    if rank == 0 and world == 1 and not args.no_host_path:
+        out["host_path"] = host_path(wl, sc)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(wl)
     if rank == 0:

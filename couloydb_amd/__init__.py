@@ -19,7 +19,7 @@ from . import _abi
 from ._abi import (END_EOF, END_TORN, END_ZERO, ERR_CRC, ERR_OFFSET, ERR_TRUNC5, ERR_VARINT,
                    TUPLE_DTYPE)
 
-__all__ = ["Scanner", "DataFile", "LogRecord", "LogPos", "ScanResult", "ScanError",
+__all__ = ["Scanner", "DataFile", "LogRecord", "LogPos", "ScanResult", "ScanError", "MergeResult",
            "ErrInvalidCRC", "TUPLE_DTYPE", "STATUS_NAMES"]
 
 # data/logRecord.go:10-16 / :20-26
@@ -109,6 +109,18 @@ class ScanResult:
             raise ScanError(st, "at offset %d" % self.end_offset[i])
 
 
+class MergeResult:
+    """Output of Scanner.merge: the merge DB's data files (fid k = files[k]), the
+    hint-index file, and the counters of cly_merge_result."""
+
+    def __init__(self, files, hint, r):
+        self.files = files
+        self.hint = hint
+        self.n_live = r.n_live
+        self.n_reencoded = r.n_reencoded
+        self.n_out_files = r.n_out_files
+
+
 class Scanner:
     """One GPU context (cly_ctx).  Not thread-safe; one per device."""
 
@@ -169,6 +181,48 @@ class Scanner:
         n = len(files)
         return ScanResult(files, out[:int(need.value)], [int(first[i]) for i in range(n)],
                           [res[i] for i in range(n)], st)
+
+    def merge(self, files, live, data_file_size):
+        """db.merge's rewrite loop (merge.go:90-143) on the device, host buffers
+        in and out (cly_merge).  live[i]: the index still points at the i-th
+        record of scan(files) (merge.go:104-132).  Returns a MergeResult."""
+        files = list(files)
+        arr = self._file_array(files)
+        lv = np.ascontiguousarray(live, dtype=np.uint8)
+        r = _abi.ClyMergeResult()
+        rc = self.lib.cly_merge(self.ctx, arr, len(files), lv.ctypes.data if len(lv) else None, len(lv),
+                                data_file_size, None, 0, None, None, 0, ctypes.byref(r))
+        if rc not in (0, _abi.ERR_CAPACITY):
+            raise (ErrInvalidCRC if rc == ERR_CRC else ScanError)(rc, "cly_merge")
+        nf = max(1, int(r.n_out_files))
+        stride = int(r.out_stride)
+        out = np.zeros(nf * stride, np.uint8)
+        lens = (ctypes.c_uint64 * nf)()
+        hint = np.zeros(max(1, int(r.hint_bytes)), np.uint8)
+        rc = self.lib.cly_merge(self.ctx, arr, len(files), lv.ctypes.data if len(lv) else None, len(lv),
+                                data_file_size, out.ctypes.data, nf, lens, hint.ctypes.data, len(hint),
+                                ctypes.byref(r))
+        if rc != 0:
+            raise (ErrInvalidCRC if rc == ERR_CRC else ScanError)(rc, "cly_merge")
+        outs = [out[k * stride:k * stride + int(lens[k])].tobytes() for k in range(int(r.n_out_files))]
+        return MergeResult(outs, hint[:int(r.hint_bytes)].tobytes(), r)
+
+    def merge_device(self, dev_files, d_tuples, file_first, results, d_live, data_file_size, d_out, out_max_files,
+                     d_hint, hint_cap, stream=None):
+        """Device-resident merge (cly_merge_device) over a scan_device result.
+        Returns (rc, out_file_lens, ClyMergeResult); rc CLY_ERR_CAPACITY leaves the
+        needs in the result."""
+        n = len(dev_files)
+        arr = (_abi.ClyFile * max(1, n))()
+        for i, (ptr, ln, fid) in enumerate(dev_files):
+            arr[i].base, arr[i].len, arr[i].fid = ptr, ln, fid
+        first = (ctypes.c_uint64 * max(1, n))(*file_first)
+        res = (_abi.ClyFileResult * max(1, n))(*results)
+        lens = (ctypes.c_uint64 * max(1, out_max_files))()
+        r = _abi.ClyMergeResult()
+        rc = self.lib.cly_merge_device(self.ctx, arr, n, d_tuples, first, res, d_live, data_file_size, d_out,
+                                       out_max_files, lens, d_hint, hint_cap, ctypes.byref(r), stream)
+        return rc, [int(lens[k]) for k in range(min(out_max_files, int(r.n_out_files)))], r
 
     def scan_device(self, dev_files, d_out, out_cap, stream=None):
         """Device-resident path: dev_files = [(device_ptr, len, fid)], d_out =

@@ -42,6 +42,13 @@ class ClyGenRec(ctypes.Structure):
                 ("_pad2", ctypes.c_int32)]
 
 
+class ClyMergeResult(ctypes.Structure):
+    _fields_ = [("n_live", ctypes.c_uint64), ("n_reencoded", ctypes.c_uint64),
+                ("hint_bytes", ctypes.c_uint64), ("out_stride", ctypes.c_uint64),
+                ("n_out_files", ctypes.c_uint32), ("_pad", ctypes.c_uint32),
+                ("merge_ms", ctypes.c_double)]
+
+
 # numpy view of cly_tuple (48 bytes)
 TUPLE_DTYPE = np.dtype([
     ("offset", "<i8"), ("expiration", "<i8"), ("tx_id", "<i8"),
@@ -56,7 +63,7 @@ GEN_DTYPE = np.dtype([("dst", "<u8"), ("key_index", "<u4"), ("value_len", "<u4")
 assert GEN_DTYPE.itemsize == 32
 
 SCAN_SYMBOLS = ["cly_ctx_create", "cly_ctx_destroy", "cly_scan_capacity", "cly_scan",
-                "cly_scan_device", "cly_strerror", "cly_build_info"]
+                "cly_scan_device", "cly_merge_device", "cly_merge", "cly_strerror", "cly_build_info"]
 GEN_SYMBOLS = ["cly_gen_record_size", "cly_gen_layout", "cly_gen_encode"]
 
 _libs = {}
@@ -90,6 +97,15 @@ def load_scan_lib(name="libclyscan.so"):
                                     P(ctypes.c_uint64), P(ClyFileResult), P(ctypes.c_uint64), P(ClyStats),
                                     ctypes.c_void_p]
     lib.cly_scan_device.restype = ctypes.c_int
+    lib.cly_merge_device.argtypes = [ctypes.c_void_p, P(ClyFile), ctypes.c_int, ctypes.c_void_p, P(ctypes.c_uint64),
+                                     P(ClyFileResult), ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                     ctypes.c_uint32, P(ctypes.c_uint64), ctypes.c_void_p, ctypes.c_uint64,
+                                     P(ClyMergeResult), ctypes.c_void_p]
+    lib.cly_merge_device.restype = ctypes.c_int
+    lib.cly_merge.argtypes = [ctypes.c_void_p, P(ClyFile), ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, P(ctypes.c_uint64),
+                              ctypes.c_void_p, ctypes.c_uint64, P(ClyMergeResult)]
+    lib.cly_merge.restype = ctypes.c_int
     lib.cly_strerror.argtypes = [ctypes.c_int]
     lib.cly_strerror.restype = ctypes.c_char_p
     lib.cly_build_info.argtypes = []

@@ -1,0 +1,705 @@
+// clymerge.hip — db.merge's rewrite loop on the device (gfx950), part of
+// libclyscan.so (C-ABI: cly_merge_device / cly_merge in include/clyscan.h).
+//
+// Reference (merge.go:90-143): for every record the scan of the old files
+// returns, in file order, look the realKey up in the index; when the index
+// still points at (fid, offset) the record is live and is re-appended to the
+// merge DB with Key = encodeKeyWithTxId(realKey, NO_TX_ID) (batch.go:120-127)
+// through appendLogRecord (db.go:368-413: EncodeLogRecord, a new file when
+// WriteOff+size > DataFileSize), and a hint record {realKey,
+// EncodeLogRecordPos(pos)} (data/dataFile.go:114-121, data/logRecord.go:117-124)
+// is written to the hint-index file.  The index lookup itself is the
+// caller's: it arrives as one live byte per scanned tuple.
+//
+// Device pipeline (one stream):
+//   k_mplan     per tuple: new record size (0 when dead), verbatim or re-encoded; block sums
+//   k_msums     exclusive scan of the block sums (one workgroup)
+//   k_mcompact  live records compacted in order: pre-rotation byte offset g
+//   k_mrot      appendLogRecord's rotation: first record of every output file
+//               (1024-ary searches over g, one workgroup)
+//   k_mplace    per live record: output file/offset, copy descriptor, 4-KiB
+//               block map, re-encoded header + CRC, hint record size
+//   k_msums, k_mhint   hint record offsets, hint records (header, realKey, pos, CRC)
+//   k_mcopy     output files by 4-KiB destination blocks: 16-B stores,
+//               funnel-shifted dword loads of the source
+// A live record whose key already is 0x00||realKey and whose header is the
+// canonical encoding (every non-transactional record the writer produces) is
+// byte-identical after EncodeLogRecord: it is copied as is, CRC included.
+// Other live records get a new header; their CRC is the stored one corrected
+// by the header+key difference, shifted over the value
+// (crc' = crc ^ A^(8 vs) (R(~0, X_old) ^ R(~0, X_new))), so the value bytes are
+// read only once, by the copy.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "scan_core.h"
+
+extern "C" hipStream_t cly_ctx_stream_internal(cly_ctx* c);
+extern "C" int cly_ctx_device_internal(cly_ctx* c);
+extern "C" void** cly_ctx_merge_slot_internal(cly_ctx* c);
+
+// Scratch buffers of the merge, kept in the context and grown on demand
+// (plain hipMalloc: no allocation inside a timed merge once warm).
+enum { MS_FB, MS_TOT, MS_PLAN, MS_BSUM, MS_ENT, MS_FSTART, MS_FLEN, MS_CP, MS_PRE, MS_BMAP, MS_HSZ, MS_N };
+struct MergeScratch { void* p[MS_N]; size_t cap[MS_N]; };
+extern "C" void cly_merge_scratch_free(void* v) {
+    MergeScratch* m = (MergeScratch*)v;
+    if (!m) return;
+    for (int i = 0; i < MS_N; i++) if (m->p[i]) hipFree(m->p[i]);
+    free(m);
+}
+template <class T>
+static hipError_t scratch(cly_ctx* ctx, int slot, size_t bytes, T** out) {
+    void** s = cly_ctx_merge_slot_internal(ctx);
+    if (!*s) *s = calloc(1, sizeof(MergeScratch));
+    MergeScratch* m = (MergeScratch*)*s;
+    if (bytes == 0) bytes = 16;
+    if (m->cap[slot] < bytes) {
+        if (m->p[slot]) { hipError_t e = hipFree(m->p[slot]); if (e != hipSuccess) return e; }
+        m->p[slot] = nullptr;
+        m->cap[slot] = 0;
+        const size_t want = bytes + bytes / 8;
+        hipError_t e = hipMalloc(&m->p[slot], want);
+        if (e != hipSuccess) return e;
+        m->cap[slot] = want;
+    }
+    *out = (T*)m->p[slot];
+    return hipSuccess;
+}
+
+#define M_NT 256
+#define M_IT 16
+#define M_BLK (M_NT * M_IT)          // tuples (or live records) per workgroup of the scans
+#define M_PRE 32                     // bytes per re-encoded prefix (crc..header, 0x00): <= 27
+#define M_CB 4096                    // destination block of k_mcopy
+#define M_CMAX 512                   // records starting in one block (>= M_CB / 10 + 2)
+#define PLAN_RE (1ull << 32)         // plan bit: re-encoded
+
+struct MSum { unsigned long long bytes, count; };
+struct MEnt { uint64_t g; uint32_t tuple, nsz; };
+struct MCopy { uint64_t dst, src; uint32_t size, pre; };
+struct MTot {                        // device totals, read back by the host
+    unsigned long long nl, bytes, hint_bytes, n_re;
+    uint32_t n_out, bad;
+};
+
+__device__ __forceinline__ uint64_t zz(int64_t x) {
+    const uint64_t u = (uint64_t)x << 1;
+    return x < 0 ? ~u : u;
+}
+__device__ __forceinline__ int uvlen(uint64_t u) {
+    int n = 1;
+    while (u >= 0x80) { u >>= 7; n++; }
+    return n;
+}
+__device__ __forceinline__ int put_uv(uint8_t* b, uint64_t u) {
+    int n = 0;
+    while (u >= 0x80) { b[n++] = (uint8_t)(u | 0x80); u >>= 7; }
+    b[n++] = (uint8_t)u;
+    return n;
+}
+__device__ __forceinline__ int find_file_u64(const uint64_t* first, int nfiles, uint64_t i) {
+    int lo = 0, hi = nfiles - 1;                      // largest f with first[f] <= i
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (first[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+__device__ __forceinline__ void crc_table_init(uint32_t* t) {
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        uint32_t s = (uint32_t)i;
+        for (int k = 0; k < 8; k++) s = (s & 1) ? (s >> 1) ^ CLY_POLY : s >> 1;
+        t[i] = s;
+    }
+    __syncthreads();
+}
+__device__ __forceinline__ uint32_t crc_upd(const uint32_t* t, uint32_t s, uint32_t b) {
+    return t[(s ^ b) & 0xff] ^ (s >> 8);
+}
+
+// Block-wide exclusive scan of (a, b) pairs over M_NT threads.
+__device__ __forceinline__ MSum block_excl(MSum v, MSum& total, MSum* sh) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    MSum inc = v;
+    #pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long a = __shfl_up(inc.bytes, d, 64), c = __shfl_up(inc.count, d, 64);
+        if (lane >= d) { inc.bytes += a; inc.count += c; }
+    }
+    if (lane == 63) sh[w] = inc;
+    __syncthreads();
+    MSum base = {0, 0};
+    total.bytes = 0; total.count = 0;
+    for (int k = 0; k < M_NT / 64; k++) {
+        if (k < w) { base.bytes += sh[k].bytes; base.count += sh[k].count; }
+        total.bytes += sh[k].bytes; total.count += sh[k].count;
+    }
+    __syncthreads();
+    MSum ex = {base.bytes + inc.bytes - v.bytes, base.count + inc.count - v.count};
+    return ex;
+}
+
+// ---- k_mplan: per tuple, the size of its merge record (0 = dead) ----------
+// Canonical check: EncodeLogRecord writes PutVarint(len(key)), PutVarint(len(value)),
+// PutVarint(exp) (data/logRecord.go:66-68); a record is kept byte for byte iff its
+// key already is varint(0)||realKey and its stored header bytes are that encoding.
+__global__ void __launch_bounds__(M_NT)
+k_mplan(const cly_tuple* __restrict__ tup, uint64_t T, const uint8_t* __restrict__ live,
+        const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases, int nfiles,
+        uint64_t* plan, MSum* bsum, uint64_t dfs, MTot* tot) {
+    __shared__ MSum sh[M_NT / 64];
+    MSum acc = {0, 0};
+    const uint64_t b0 = (uint64_t)blockIdx.x * M_BLK;
+    for (int k = 0; k < M_IT; k++) {
+        const uint64_t i = b0 + (uint64_t)k * M_NT + threadIdx.x;
+        if (i >= T) break;
+        uint64_t p = 0;
+        if (live[i]) {
+            const cly_tuple t = tup[i];
+            if (t.txid_len == 0xFF) { atomicOr(&tot->bad, 1u); plan[i] = 0; continue; }   // parseLogRecordKey panics
+            const uint32_t rk = t.key_size - t.txid_len;
+            const uint64_t nks = (uint64_t)rk + 1;
+            const int nh = 6 + uvlen(zz((int64_t)nks)) + uvlen(zz((int64_t)t.value_size)) + uvlen(zz(t.expiration));
+            const uint64_t nsz = (uint64_t)nh + nks + t.value_size;
+            bool verbatim = t.txid_len == 1 && t.tx_id == 0 && nh == t.header_size;
+            if (verbatim) {
+                const int f = find_file_u64(first, nfiles, i);
+                const uint8_t* h = (const uint8_t*)bases[f] + t.offset;
+                uint8_t cb[26];
+                int n = 6;
+                n += put_uv(cb + n, zz((int64_t)nks));
+                n += put_uv(cb + n, zz((int64_t)t.value_size));
+                n += put_uv(cb + n, zz(t.expiration));
+                for (int q = 6; q < n && verbatim; q++) verbatim = h[q] == cb[q];
+            }
+            if (nsz > dfs) atomicOr(&tot->bad, 2u);              // one record per file would not fit
+            p = nsz | (verbatim ? 0ull : PLAN_RE);
+            acc.bytes += nsz;
+            acc.count += 1;
+        }
+        plan[i] = p;
+    }
+    // block sum (order-free)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    #pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        acc.bytes += __shfl_xor(acc.bytes, d, 64);
+        acc.count += __shfl_xor(acc.count, d, 64);
+    }
+    if (lane == 0) sh[w] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        MSum s = {0, 0};
+        for (int k = 0; k < M_NT / 64; k++) { s.bytes += sh[k].bytes; s.count += sh[k].count; }
+        bsum[blockIdx.x] = s;
+    }
+}
+
+// ---- k_msums: exclusive scan of block sums (one workgroup of M_NT threads) --
+__global__ void __launch_bounds__(M_NT)
+k_msums(MSum* bsum, uint64_t nblk, unsigned long long* out_bytes, unsigned long long* out_count) {
+    __shared__ MSum sh[M_NT / 64];
+    MSum carry = {0, 0};
+    for (uint64_t b = 0; b < nblk; b += M_NT) {
+        const uint64_t i = b + threadIdx.x;
+        MSum v = i < nblk ? bsum[i] : MSum{0, 0};
+        MSum total;
+        MSum ex = block_excl(v, total, sh);
+        if (i < nblk) bsum[i] = MSum{carry.bytes + ex.bytes, carry.count + ex.count};
+        carry.bytes += total.bytes;
+        carry.count += total.count;
+    }
+    if (threadIdx.x == 0) {
+        if (out_bytes) *out_bytes = carry.bytes;
+        if (out_count) *out_count = carry.count;
+    }
+}
+
+// ---- k_mcompact: live records in order, with their pre-rotation offset -----
+__global__ void __launch_bounds__(M_NT)
+k_mcompact(const uint64_t* __restrict__ plan, uint64_t T, const MSum* __restrict__ bsum, MEnt* ent) {
+    __shared__ MSum sh[M_NT / 64];
+    const uint64_t b0 = (uint64_t)blockIdx.x * M_BLK;
+    MSum carry = bsum[blockIdx.x];
+    for (int k = 0; k < M_IT; k++) {
+        const uint64_t i = b0 + (uint64_t)k * M_NT + threadIdx.x;
+        if (b0 + (uint64_t)k * M_NT >= T) break;                 // (uniform)
+        const uint64_t p = i < T ? plan[i] : 0;
+        const uint32_t nsz = (uint32_t)p;
+        MSum v = {nsz, nsz ? 1ull : 0ull};
+        MSum total;
+        const MSum ex = block_excl(v, total, sh);
+        if (nsz) ent[carry.count + ex.count] = MEnt{carry.bytes + ex.bytes, (uint32_t)i, nsz};
+        carry.bytes += total.bytes;
+        carry.count += total.count;
+    }
+}
+
+// ---- k_mrot: appendLogRecord's file rotation (db.go:376-385) ----------------
+// File k starts at live record r_k; it holds r_k .. m-1 for the largest m with
+// g(m) - g(r_k) <= DataFileSize (g(nl) = total bytes), at least one record.
+// One workgroup; each search step probes M_ROT positions of the interval.
+#define M_ROT 1024
+__device__ __forceinline__ uint64_t g_at(const MEnt* e, uint64_t nl, uint64_t total, uint64_t m) {
+    return m < nl ? e[m].g : total;
+}
+__global__ void __launch_bounds__(M_ROT)
+k_mrot(const MEnt* __restrict__ e, MTot* tot, uint64_t dfs, uint32_t max_files, uint64_t* fstart, uint64_t* flen) {
+    const uint64_t nl = tot->nl, total = tot->bytes;
+    __shared__ uint64_t s_lo, s_hi;
+    uint64_t r = 0;
+    uint32_t k = 0;
+    while (r < nl) {
+        const uint64_t g0 = e[r].g, lim = g0 + dfs;
+        uint64_t lo = r + 1;                                    // g(r+1) - g(r) = size <= dfs (k_mplan)
+        uint64_t hi = r + dfs / 10 + 2;                         // merge records are >= 10 bytes
+        if (hi > nl) hi = nl;
+        if (hi < lo) hi = lo;
+        while (lo < hi) {                                       // invariant: g(lo) <= lim
+            const uint64_t span = hi - lo;
+            const uint64_t pos = lo + (span * (threadIdx.x + 1) + M_ROT - 1) / M_ROT;   // in (lo, hi]
+            const int ok = g_at(e, nl, total, pos) <= lim;
+            const int c = __syncthreads_count(ok);              // monotone: probes 0..c-1 are ok
+            if (threadIdx.x == (unsigned)c - 1) s_lo = pos;
+            if (threadIdx.x == (unsigned)c) s_hi = pos - 1;
+            if (threadIdx.x == 0) { if (c == 0) s_lo = lo; if (c == M_ROT) s_hi = hi; }
+            __syncthreads();
+            lo = s_lo; hi = s_hi;
+            __syncthreads();
+        }
+        if (threadIdx.x == 0 && k < max_files) {
+            fstart[k] = r;
+            flen[k] = g_at(e, nl, total, lo) - g0;
+        }
+        r = lo;
+        k++;
+    }
+    if (threadIdx.x == 0) {
+        if (k < max_files) fstart[k] = nl;
+        tot->n_out = k;
+    }
+}
+
+// ---- k_mplace: per live record, where it goes --------------------------------
+__global__ void __launch_bounds__(M_NT)
+k_mplace(const MEnt* __restrict__ e, const cly_tuple* __restrict__ tup, const uint64_t* __restrict__ plan,
+         const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases, int nfiles,
+         const uint64_t* __restrict__ fstart, MTot* tot, uint64_t stride, MCopy* cp, uint8_t* pre,
+         uint32_t* bmap, uint32_t* hsz, MSum* bsum) {
+    __shared__ uint32_t tab[256];
+    __shared__ MSum sh[M_NT / 64];
+    crc_table_init(tab);
+    const uint64_t nl = tot->nl;
+    const uint32_t nout = tot->n_out;
+    MSum acc = {0, 0};
+    unsigned long long nre = 0;
+    const uint64_t b0 = (uint64_t)blockIdx.x * M_BLK;
+    for (int it = 0; it < M_IT; it++) {
+        const uint64_t j = b0 + (uint64_t)it * M_NT + threadIdx.x;
+        if (j >= nl) break;
+        const MEnt m = e[j];
+        // output file: largest k with fstart[k] <= j
+        int lo = 0, hi = (int)nout - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (fstart[mid] <= j) lo = mid; else hi = mid - 1;
+        }
+        const uint64_t off = m.g - e[fstart[lo]].g;
+        const uint64_t dst = (uint64_t)lo * stride + off;
+        const cly_tuple t = tup[m.tuple];
+        const int f = find_file_u64(first, nfiles, m.tuple);
+        const uint8_t* F = (const uint8_t*)bases[f] + t.offset;
+        const uint32_t rk = t.key_size - t.txid_len;
+        MCopy c;
+        c.dst = dst;
+        c.size = m.nsz;
+        if (!(plan[m.tuple] & PLAN_RE)) {
+            c.src = (uint64_t)F;
+            c.pre = 0;
+        } else {
+            // new header: crc, type, dtype, varint(1+rk), varint(vs), varint(exp), then key byte 0x00
+            uint8_t h[M_PRE];
+            h[4] = t.type;
+            h[5] = t.data_type;
+            int n = 6;
+            n += put_uv(h + n, zz((int64_t)rk + 1));
+            n += put_uv(h + n, zz((int64_t)t.value_size));
+            n += put_uv(h + n, zz(t.expiration));
+            h[n] = 0x00;
+            const uint8_t* rkey = F + t.header_size + t.txid_len;
+            uint32_t ro = 0xFFFFFFFFu, rn = 0xFFFFFFFFu;
+            for (uint32_t q = 4; q < (uint32_t)t.header_size + t.key_size; q++) ro = crc_upd(tab, ro, F[q]);
+            for (int q = 4; q <= n; q++) rn = crc_upd(tab, rn, h[q]);
+            for (uint32_t q = 0; q < rk; q++) rn = crc_upd(tab, rn, rkey[q]);
+            const uint32_t crc = t.crc ^ cly_shift(ro ^ rn, t.value_size);
+            h[0] = (uint8_t)crc; h[1] = (uint8_t)(crc >> 8); h[2] = (uint8_t)(crc >> 16); h[3] = (uint8_t)(crc >> 24);
+            uint8_t* pj = pre + j * M_PRE;
+            for (int q = 0; q <= n; q++) pj[q] = h[q];
+            c.pre = (uint32_t)n + 1;
+            c.src = (uint64_t)rkey;
+            nre++;
+        }
+        cp[j] = c;
+        // blocks of k_mcopy whose first byte lies in this record
+        for (uint64_t b = (dst + M_CB - 1) / M_CB; b * M_CB < dst + c.size; b++) bmap[b] = (uint32_t)j;
+        // hint record: Key realKey, Value varint(fid)||varint(off), Type 0, DataType 0, Expiration 0
+        const int plen = uvlen(zz((int64_t)lo)) + uvlen(zz((int64_t)off));
+        const uint32_t hs = 6 + uvlen(zz((int64_t)rk)) + uvlen(zz((int64_t)plen)) + 1 + rk + plen;
+        hsz[j] = hs;
+        acc.bytes += hs;
+        acc.count += 1;
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    #pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        acc.bytes += __shfl_xor(acc.bytes, d, 64);
+        acc.count += __shfl_xor(acc.count, d, 64);
+        nre += __shfl_xor(nre, d, 64);
+    }
+    if (lane == 0 && nre) atomicAdd(&tot->n_re, nre);
+    if (lane == 0) sh[w] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        MSum s = {0, 0};
+        for (int k = 0; k < M_NT / 64; k++) { s.bytes += sh[k].bytes; s.count += sh[k].count; }
+        bsum[blockIdx.x] = s;
+    }
+}
+
+// ---- k_mhint: hint-index records (data/dataFile.go:114-121) -----------------
+__global__ void __launch_bounds__(M_NT)
+k_mhint(const MEnt* __restrict__ e, const MCopy* __restrict__ cp, const cly_tuple* __restrict__ tup,
+        const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases, int nfiles,
+        const uint32_t* __restrict__ hsz, const MSum* __restrict__ bsum, const MTot* tot, uint64_t stride,
+        uint8_t* hint, uint64_t hint_cap) {
+    __shared__ uint32_t tab[256];
+    __shared__ MSum sh[M_NT / 64];
+    crc_table_init(tab);
+    const uint64_t nl = tot->nl;
+    const uint64_t b0 = (uint64_t)blockIdx.x * M_BLK;
+    MSum carry = bsum[blockIdx.x];
+    for (int it = 0; it < M_IT; it++) {
+        if (b0 + (uint64_t)it * M_NT >= nl) break;
+        const uint64_t j = b0 + (uint64_t)it * M_NT + threadIdx.x;
+        const uint32_t hs = j < nl ? hsz[j] : 0;
+        MSum v = {hs, 0};
+        MSum total;
+        const MSum ex = block_excl(v, total, sh);
+        const uint64_t ho = carry.bytes + ex.bytes;
+        carry.bytes += total.bytes;
+        if (j >= nl || ho + hs > hint_cap) continue;
+        const MEnt m = e[j];
+        const cly_tuple t = tup[m.tuple];
+        const int f = find_file_u64(first, nfiles, m.tuple);
+        const uint8_t* rkey = (const uint8_t*)bases[f] + t.offset + t.header_size + t.txid_len;
+        const uint32_t rk = t.key_size - t.txid_len;
+        const uint64_t dst = cp[j].dst;
+        const uint64_t fid = dst / stride, off = dst - fid * stride;
+        uint8_t pv[20];
+        int pl = put_uv(pv, zz((int64_t)fid));
+        pl += put_uv(pv + pl, zz((int64_t)off));
+        uint8_t h[26];
+        h[4] = 0; h[5] = 0;
+        int n = 6;
+        n += put_uv(h + n, zz((int64_t)rk));
+        n += put_uv(h + n, zz((int64_t)pl));
+        h[n++] = 0;                                             // PutVarint(0) expiration
+        uint32_t s = 0xFFFFFFFFu;
+        for (int q = 4; q < n; q++) s = crc_upd(tab, s, h[q]);
+        uint8_t* o = hint + ho;
+        for (uint32_t q = 0; q < rk; q++) { const uint8_t b = rkey[q]; s = crc_upd(tab, s, b); o[n + q] = b; }
+        for (int q = 0; q < pl; q++) { s = crc_upd(tab, s, pv[q]); o[n + rk + q] = pv[q]; }
+        s = ~s;
+        h[0] = (uint8_t)s; h[1] = (uint8_t)(s >> 8); h[2] = (uint8_t)(s >> 16); h[3] = (uint8_t)(s >> 24);
+        for (int q = 0; q < n; q++) o[q] = h[q];
+    }
+}
+
+// ---- k_mcopy: one 4-KiB destination block per workgroup ----------------------
+__device__ __forceinline__ uint8_t src_byte(const MCopy& c, const uint8_t* pre_j, uint64_t r) {
+    return r < c.pre ? pre_j[r] : ((const uint8_t*)c.src)[r - c.pre];
+}
+__global__ void __launch_bounds__(M_NT)
+k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uint32_t* __restrict__ bmap,
+        const uint64_t* __restrict__ fstart, const uint64_t* __restrict__ flen, const MTot* tot, uint64_t stride,
+        uint64_t nblocks, uint8_t* out) {
+    __shared__ int64_t s_rel[M_CMAX];
+    __shared__ uint64_t s_src[M_CMAX];
+    __shared__ uint32_t s_size[M_CMAX], s_pre[M_CMAX];
+    const uint64_t bpf = stride / M_CB;
+    for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+        const uint64_t k = b / bpf;
+        const uint64_t B = b * M_CB, fo = B - k * stride;
+        const uint64_t L = flen[k];
+        if (fo >= L) continue;                                  // (uniform)
+        const uint32_t j0 = bmap[b];
+        uint64_t j1 = fstart[k + 1];
+        if (fo + M_CB < L && b + 1 < nblocks) j1 = (uint64_t)bmap[b + 1] + 1;
+        uint32_t cnt = (uint32_t)(j1 - j0);
+        if (cnt > M_CMAX) cnt = M_CMAX;
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < cnt; q += M_NT) {
+            const MCopy c = cp[j0 + q];
+            s_rel[q] = (int64_t)c.dst - (int64_t)B;
+            s_src[q] = c.src;
+            s_size[q] = c.size;
+            s_pre[q] = c.pre;
+        }
+        __syncthreads();
+        for (int part = 0; part < M_CB / 16 / M_NT; part++) {
+            const int64_t d = (int64_t)(part * M_NT + threadIdx.x) * 16;
+            if (fo + (uint64_t)d >= L) continue;
+            int lo = 0, hi = (int)cnt - 1;                      // last record with rel <= d
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_rel[mid] <= d) lo = mid; else hi = mid - 1;
+            }
+            const int64_t r0 = d - s_rel[lo];
+            uint32_t wv[4];
+            if (r0 >= (int64_t)s_pre[lo] && r0 + 16 <= (int64_t)s_size[lo]) {
+                // fast path: 16 body bytes of one record
+                const uint64_t sa = s_src[lo] + (uint64_t)(r0 - s_pre[lo]);
+                const uint32_t* w = (const uint32_t*)(sa & ~3ull);
+                const uint32_t sh = (uint32_t)(sa & 3) * 8;
+                uint32_t a[5];
+                #pragma unroll
+                for (int q = 0; q < 4; q++) a[q] = w[q];
+                a[4] = sh ? w[4] : 0u;
+                #pragma unroll
+                for (int q = 0; q < 4; q++) wv[q] = __builtin_amdgcn_alignbit(a[q + 1], a[q], sh);
+            } else {
+                int jj = lo;
+                #pragma unroll 1
+                for (int q = 0; q < 16; q++) {
+                    const int64_t pos = d + q;
+                    while (jj + 1 < (int)cnt && s_rel[jj + 1] <= pos) jj++;
+                    uint32_t byte = 0;
+                    const int64_t r = pos - s_rel[jj];
+                    if (fo + (uint64_t)pos < L && r >= 0 && r < (int64_t)s_size[jj]) {
+                        MCopy c;
+                        c.src = s_src[jj]; c.pre = s_pre[jj];
+                        byte = src_byte(c, pre + (uint64_t)(j0 + jj) * M_PRE, (uint64_t)r);
+                    }
+                    if ((q & 3) == 0) wv[q >> 2] = 0;
+                    wv[q >> 2] |= byte << (8 * (q & 3));
+                }
+            }
+            *(uint4*)(out + B + d) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// CLY_MERGE_DEBUG=1: synchronise after every kernel and name the one that failed
+static int merge_debug() {
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("CLY_MERGE_DEBUG"); v = e && *e == '1'; }
+    return v;
+}
+#define MDBG(st, name) do { if (merge_debug()) { hipError_t e_ = hipStreamSynchronize(st); \
+    if (e_ == hipSuccess) e_ = hipGetLastError(); \
+    fprintf(stderr, "clymerge: %s -> %s\n", name, hipGetErrorString(e_)); \
+    if (e_ != hipSuccess) { rc = CLY_ERR_DEVICE; goto done; } } } while (0)
+#define MCK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+    fprintf(stderr, "clymerge: %s failed: %s\n", #x, hipGetErrorString(e_)); rc = CLY_ERR_DEVICE; goto done; } } while (0)
+
+extern "C" int cly_merge_device(cly_ctx* ctx, const cly_file* files, int nfiles, const cly_tuple* d_tuples,
+                                const uint64_t* file_first, const cly_file_result* res, const uint8_t* d_live,
+                                uint64_t data_file_size, uint8_t* d_out, uint32_t out_max_files,
+                                uint64_t* out_file_len, uint8_t* d_hint, uint64_t hint_cap,
+                                cly_merge_result* mres, void* stream_v) {
+    if (!ctx || !mres || nfiles < 0 || (nfiles && (!files || !file_first || !res)) || data_file_size == 0)
+        return CLY_ERR_ARG;
+    memset(mres, 0, sizeof(*mres));
+    const uint64_t stride = (data_file_size + M_CB - 1) / M_CB * M_CB;
+    mres->out_stride = stride;
+    // the reference's merge stops with the scan's error (merge.go:94-99)
+    uint64_t T = 0;
+    for (int i = 0; i < nfiles; i++) {
+        if (res[i].status < 0) return res[i].status;
+        if (file_first[i] != T) return CLY_ERR_ARG;             // tuples of the files back to back
+        T += res[i].n_records;
+    }
+    if (T >= (1ull << 32)) return CLY_ERR_ARG;
+    if (hipSetDevice(cly_ctx_device_internal(ctx)) != hipSuccess) return CLY_ERR_DEVICE;
+    hipStream_t st = stream_v ? (hipStream_t)stream_v : cly_ctx_stream_internal(ctx);
+    int rc = CLY_OK;
+    uint64_t* h_fb = (uint64_t*)malloc(sizeof(uint64_t) * (2 * (size_t)nfiles + 2));
+    uint64_t *d_fb = nullptr, *d_plan = nullptr, *d_fstart = nullptr, *d_flen = nullptr;
+    MSum* d_bsum = nullptr;
+    MEnt* d_ent = nullptr;
+    MCopy* d_cp = nullptr;
+    uint8_t* d_pre = nullptr;
+    uint32_t *d_bmap = nullptr, *d_hsz = nullptr;
+    MTot* d_tot = nullptr;
+    MTot h_tot;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const uint64_t nblk = T / M_BLK + 1;
+    MCK(hipEventCreate(&e0));
+    MCK(hipEventCreate(&e1));
+    for (int i = 0; i < nfiles; i++) h_fb[i] = file_first[i];
+    h_fb[nfiles] = T;
+    for (int i = 0; i < nfiles; i++) h_fb[nfiles + 1 + i] = (uint64_t)files[i].base;
+    MCK(scratch(ctx, MS_FB, sizeof(uint64_t) * (2 * (size_t)nfiles + 2), &d_fb));
+    MCK(hipMemcpyAsync(d_fb, h_fb, sizeof(uint64_t) * (2 * (size_t)nfiles + 1), hipMemcpyHostToDevice, st));
+    MCK(scratch(ctx, MS_TOT, sizeof(MTot), &d_tot));
+    MCK(hipMemsetAsync(d_tot, 0, sizeof(MTot), st));
+    MCK(scratch(ctx, MS_PLAN, sizeof(uint64_t) * (T + 1), &d_plan));
+    MCK(scratch(ctx, MS_BSUM, sizeof(MSum) * nblk, &d_bsum));
+    MCK(scratch(ctx, MS_ENT, sizeof(MEnt) * (T + 1), &d_ent));
+    MCK(hipEventRecord(e0, st));
+    if (T) {
+        k_mplan<<<(unsigned)nblk, M_NT, 0, st>>>(d_tuples, T, d_live, d_fb, d_fb + nfiles + 1, nfiles, d_plan, d_bsum,
+                                                  data_file_size, d_tot);
+        MDBG(st, "k_mplan");
+        k_msums<<<1, M_NT, 0, st>>>(d_bsum, nblk, &d_tot->bytes, &d_tot->nl);
+        MDBG(st, "k_msums");
+        k_mcompact<<<(unsigned)nblk, M_NT, 0, st>>>(d_plan, T, d_bsum, d_ent);
+        MDBG(st, "k_mcompact");
+    }
+    MCK(hipMemcpyAsync(&h_tot, d_tot, sizeof(MTot), hipMemcpyDeviceToHost, st));
+    MCK(hipStreamSynchronize(st));
+    if (h_tot.bad & 1) { rc = CLY_ERR_VARINT; goto done; }
+    if (h_tot.bad & 2) { rc = CLY_ERR_ARG; goto done; }
+    mres->n_live = h_tot.nl;
+    if (h_tot.nl == 0) goto timing;
+    {
+        // n_out <= 2 total / dfs + 2: two neighbouring files hold more than dfs bytes
+        uint64_t fcap64 = 2 * h_tot.bytes / data_file_size + 4;
+        if (fcap64 > h_tot.nl + 2) fcap64 = h_tot.nl + 2;
+        const uint32_t fcap = (uint32_t)fcap64;
+        MCK(scratch(ctx, MS_FSTART, sizeof(uint64_t) * (fcap + 1), &d_fstart));
+        MCK(scratch(ctx, MS_FLEN, sizeof(uint64_t) * (fcap + 1), &d_flen));
+        k_mrot<<<1, M_ROT, 0, st>>>(d_ent, d_tot, data_file_size, fcap, d_fstart, d_flen);
+        MDBG(st, "k_mrot");
+        MCK(hipMemcpyAsync(&h_tot, d_tot, sizeof(MTot), hipMemcpyDeviceToHost, st));
+        MCK(hipStreamSynchronize(st));
+        mres->n_out_files = h_tot.n_out;
+        if (h_tot.n_out >= fcap) { rc = CLY_ERR_DEVICE; goto done; }   // cannot happen (bound above)
+        const uint64_t nl = h_tot.nl;
+        const uint64_t lblk = nl / M_BLK + 1;
+        const uint64_t nblocks = (uint64_t)h_tot.n_out * (stride / M_CB);
+        if (lblk > nblk) { rc = CLY_ERR_DEVICE; goto done; }    // cannot happen: nl <= T
+        MCK(scratch(ctx, MS_CP, sizeof(MCopy) * nl, &d_cp));
+        MCK(scratch(ctx, MS_PRE, (size_t)M_PRE * nl, &d_pre));
+        MCK(scratch(ctx, MS_BMAP, sizeof(uint32_t) * (nblocks + 1), &d_bmap));
+        MCK(scratch(ctx, MS_HSZ, sizeof(uint32_t) * nl, &d_hsz));
+        k_mplace<<<(unsigned)lblk, M_NT, 0, st>>>(d_ent, d_tuples, d_plan, d_fb, d_fb + nfiles + 1, nfiles, d_fstart,
+                                                   d_tot, stride, d_cp, d_pre, d_bmap, d_hsz, d_bsum);
+        MDBG(st, "k_mplace");
+        k_msums<<<1, M_NT, 0, st>>>(d_bsum, lblk, &d_tot->hint_bytes, nullptr);
+        MCK(hipMemcpyAsync(&h_tot, d_tot, sizeof(MTot), hipMemcpyDeviceToHost, st));
+        MCK(hipStreamSynchronize(st));
+        mres->hint_bytes = h_tot.hint_bytes;
+        mres->n_reencoded = h_tot.n_re;
+        if (h_tot.n_out > out_max_files || !d_out || h_tot.hint_bytes > hint_cap || !d_hint) {
+            rc = CLY_ERR_CAPACITY;
+            goto done;
+        }
+        k_mhint<<<(unsigned)lblk, M_NT, 0, st>>>(d_ent, d_cp, d_tuples, d_fb, d_fb + nfiles + 1, nfiles, d_hsz, d_bsum,
+                                                  d_tot, stride, d_hint, hint_cap);
+        MDBG(st, "k_mhint");
+        unsigned grid = nblocks < 65536 ? (unsigned)nblocks : 65536u;
+        k_mcopy<<<grid, M_NT, 0, st>>>(d_cp, d_pre, d_bmap, d_fstart, d_flen, d_tot, stride, nblocks, d_out);
+        MDBG(st, "k_mcopy");
+        MCK(hipGetLastError());
+        if (out_file_len) MCK(hipMemcpyAsync(out_file_len, d_flen, sizeof(uint64_t) * h_tot.n_out,
+                                             hipMemcpyDeviceToHost, st));
+    }
+timing:
+    MCK(hipEventRecord(e1, st));
+    MCK(hipEventSynchronize(e1));
+    {
+        float ms = 0;
+        MCK(hipEventElapsedTime(&ms, e0, e1));
+        mres->merge_ms = ms;
+    }
+done:
+    hipStreamSynchronize(st);
+    if (e0) hipEventDestroy(e0);
+    if (e1) hipEventDestroy(e1);
+    free(h_fb);
+    return rc;
+}
+
+// Host-memory entry (the cgo path): files in host memory (mmap), one live byte
+// per record of the scan (scan order), merge data files and hint file back to
+// host memory.  Scans the files on the device first (cly_scan_device).
+extern "C" int cly_merge(cly_ctx* ctx, const cly_file* files, int nfiles, const uint8_t* live, uint64_t n_live_bytes,
+                         uint64_t data_file_size, uint8_t* out, uint32_t out_max_files, uint64_t* out_file_len,
+                         uint8_t* hint, uint64_t hint_cap, cly_merge_result* mres) {
+    if (!ctx || !mres || nfiles < 0 || (nfiles && !files) || data_file_size == 0) return CLY_ERR_ARG;
+    memset(mres, 0, sizeof(*mres));
+    if (hipSetDevice(cly_ctx_device_internal(ctx)) != hipSuccess) return CLY_ERR_DEVICE;
+    hipStream_t st = cly_ctx_stream_internal(ctx);
+    int rc = CLY_OK;
+    const uint64_t stride = (data_file_size + M_CB - 1) / M_CB * M_CB;
+    uint64_t total = 0;
+    for (int i = 0; i < nfiles; i++) {
+        if (files[i].len >= (1ULL << 32)) return CLY_ERR_ARG;
+        total += (files[i].len + 4095) & ~4095ULL;
+    }
+    const int nf = nfiles ? nfiles : 1;
+    cly_file* df = (cly_file*)calloc(nf, sizeof(cly_file));
+    uint64_t* first = (uint64_t*)calloc(nf, sizeof(uint64_t));
+    cly_file_result* res = (cly_file_result*)calloc(nf, sizeof(cly_file_result));
+    uint8_t *d_bytes = nullptr, *d_live = nullptr, *d_out = nullptr, *d_hint = nullptr;
+    cly_tuple* d_tup = nullptr;
+    uint64_t need = 0, cap = 0, T = 0;
+    MCK(hipMalloc((void**)&d_bytes, total + 4096));
+    {
+        uint64_t off = 0;
+        for (int i = 0; i < nfiles; i++) {
+            df[i] = files[i];
+            df[i].base = d_bytes + off;
+            if (files[i].len) MCK(hipMemcpyAsync(d_bytes + off, files[i].base, files[i].len, hipMemcpyHostToDevice, st));
+            off += (files[i].len + 4095) & ~4095ULL;
+        }
+    }
+    cap = cly_scan_capacity(files, nfiles) + 16;
+    MCK(hipMalloc((void**)&d_tup, sizeof(cly_tuple) * cap));
+    rc = cly_scan_device(ctx, df, nfiles, d_tup, cap, first, res, &need, nullptr, nullptr);
+    if (rc == CLY_ERR_CAPACITY) {
+        hipFree(d_tup);
+        d_tup = nullptr;
+        cap = need + 16;
+        MCK(hipMalloc((void**)&d_tup, sizeof(cly_tuple) * cap));
+        rc = cly_scan_device(ctx, df, nfiles, d_tup, cap, first, res, &need, nullptr, nullptr);
+    }
+    if (rc != CLY_OK) goto done;
+    for (int i = 0; i < nfiles; i++) {
+        if (res[i].status < 0) { rc = res[i].status; goto done; }
+        T += res[i].n_records;
+    }
+    // tuples after a file's end may sit in the slots; the merge wants them back to back
+    {
+        uint64_t o = 0;
+        for (int i = 0; i < nfiles; i++) {
+            if (first[i] != o && res[i].n_records)
+                MCK(hipMemcpyAsync(d_tup + o, d_tup + first[i], sizeof(cly_tuple) * res[i].n_records,
+                                   hipMemcpyDeviceToDevice, st));
+            first[i] = o;
+            o += res[i].n_records;
+        }
+    }
+    if (n_live_bytes != T || (T && !live)) { rc = CLY_ERR_ARG; goto done; }
+    MCK(hipMalloc((void**)&d_live, T + 1));
+    if (T) MCK(hipMemcpyAsync(d_live, live, T, hipMemcpyHostToDevice, st));
+    if (out_max_files) MCK(hipMalloc((void**)&d_out, stride * out_max_files));
+    if (hint_cap) MCK(hipMalloc((void**)&d_hint, hint_cap));
+    rc = cly_merge_device(ctx, df, nfiles, d_tup, first, res, d_live, data_file_size, d_out, out_max_files,
+                          out_file_len, d_hint, hint_cap, mres, nullptr);
+    if (rc != CLY_OK) goto done;
+    for (uint32_t k = 0; k < mres->n_out_files; k++)
+        MCK(hipMemcpyAsync(out + k * stride, d_out + k * stride, out_file_len[k], hipMemcpyDeviceToHost, st));
+    if (mres->hint_bytes) MCK(hipMemcpyAsync(hint, d_hint, mres->hint_bytes, hipMemcpyDeviceToHost, st));
+    MCK(hipStreamSynchronize(st));
+done:
+    hipStreamSynchronize(st);
+    hipFree(d_bytes); hipFree(d_tup); hipFree(d_live); hipFree(d_out); hipFree(d_hint);
+    free(df); free(first); free(res);
+    return rc;
+}

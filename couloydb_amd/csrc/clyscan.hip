@@ -1697,7 +1697,9 @@ struct cly_ctx {
     uint8_t* d_bytes; uint64_t cap_bytes;          // host-path staging
     cly_tuple* d_tuples; uint64_t cap_tuples;
     int dbg_flags;
+    void* merge_scratch;         // clymerge.hip's buffers (grow-only)
 };
+extern "C" void cly_merge_scratch_free(void* p);
 
 extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     if (!out) return CLY_ERR_ARG;
@@ -1758,6 +1760,7 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     hipFree(c->d_subP); hipFree(c->d_staging); hipFree(c->d_blk); hipFree(c->d_fix); hipFree(c->d_cand);
     hipFree(c->d_listed); hipFree(c->d_cflag); hipFree(c->d_fh); hipFree(c->d_fkey); hipFree(c->d_fck); hipFree(c->d_g); hipFree(c->d_cols); hipFree(c->d_x8n); hipFree(c->d_bytes); hipFree(c->d_tuples);
     hipHostFree(c->h_files); hipHostFree(c->h_prefix); hipHostFree(c->h_fout); hipHostFree(c->h_g);
+    cly_merge_scratch_free(c->merge_scratch);
     for (int i = 0; i < 4; i++) hipEventDestroy(c->ev[i]);
     hipStreamDestroy(c->stream);
     free(c);
@@ -2034,6 +2037,11 @@ extern "C" int cly_scan(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
     HIPCK(hipStreamSynchronize(c->stream));
     return CLY_OK;
 }
+
+// Context accessors for the merge entries (clymerge.hip); not in the public header.
+extern "C" hipStream_t cly_ctx_stream_internal(cly_ctx* c) { return c->stream; }
+extern "C" int cly_ctx_device_internal(cly_ctx* c) { return c->device; }
+extern "C" void** cly_ctx_merge_slot_internal(cly_ctx* c) { return &c->merge_scratch; }
 
 // Debug / statistics (not part of include/clyscan.h)
 extern "C" int cly_dbg_sums(cly_ctx* c, void* out, int n) {

@@ -122,6 +122,49 @@ int cly_scan_device(cly_ctx* ctx, const cly_file* files, int nfiles,
                     uint64_t* file_first, cly_file_result* res,
                     uint64_t* needed, cly_stats* stats, void* stream);
 
+/* ---- merge rewrite (db.merge, merge.go:90-143) ----------------------------
+ * For every tuple of a scan whose live byte is set (the caller's index still
+ * points at (fid, offset): merge.go:104-132), re-append the record to the merge
+ * DB with Key = encodeKeyWithTxId(realKey, NO_TX_ID) (merge.go:129,
+ * batch.go:120-127) through appendLogRecord (db.go:368-413: EncodeLogRecord, a
+ * new file when WriteOff+size > data_file_size; the merge DB's first file is
+ * fid 0), and write the hint record {realKey, EncodeLogRecordPos(pos)}
+ * (merge.go:135, data/dataFile.go:114-121) to the hint-index file.
+ * Output data file k (fid k) is at out + k*out_stride, out_stride =
+ * data_file_size rounded up to 4 KiB; out_file_len[k] its length.  The
+ * merge-finished file (merge.go:150-163) is the caller's: one record.
+ * Returns CLY_OK; the scan's error status when a file's scan failed (the
+ * reference's merge returns it); CLY_ERR_VARINT when a tuple's txId varint
+ * overflowed (parseLogRecordKey panics); CLY_ERR_CAPACITY when out_max_files or
+ * hint_cap is too small (mres holds the need; out/hint may be NULL to query);
+ * CLY_ERR_ARG for a record larger than data_file_size.                         */
+typedef struct cly_merge_result {
+    uint64_t n_live;          /* records rewritten (= hint records)             */
+    uint64_t n_reencoded;     /* live records whose bytes change (tx records)   */
+    uint64_t hint_bytes;      /* length of the hint-index file                  */
+    uint64_t out_stride;      /* distance between output files in `out`        */
+    uint32_t n_out_files;     /* merge data files, fids 0 .. n_out_files-1      */
+    uint32_t _pad;
+    double   merge_ms;        /* device time of the merge kernels (device entry) */
+} cly_merge_result;
+
+/* Device-resident entry: files[i].base, d_tuples, d_live, d_out, d_hint are
+ * device memory; d_tuples/file_first/res as cly_scan_device returned them
+ * (files' tuples back to back); d_live[i] is the live byte of d_tuples[i].     */
+int cly_merge_device(cly_ctx* ctx, const cly_file* files, int nfiles,
+                     const cly_tuple* d_tuples, const uint64_t* file_first, const cly_file_result* res,
+                     const uint8_t* d_live, uint64_t data_file_size,
+                     uint8_t* d_out, uint32_t out_max_files, uint64_t* out_file_len,
+                     uint8_t* d_hint, uint64_t hint_cap, cly_merge_result* mres, void* stream);
+
+/* Host-memory entry (the cgo path): scans the files on the device, then
+ * merges; live[i] (n_live_bytes = number of records the scan returns, in scan
+ * order) is the index's verdict for the i-th record.                           */
+int cly_merge(cly_ctx* ctx, const cly_file* files, int nfiles,
+              const uint8_t* live, uint64_t n_live_bytes, uint64_t data_file_size,
+              uint8_t* out, uint32_t out_max_files, uint64_t* out_file_len,
+              uint8_t* hint, uint64_t hint_cap, cly_merge_result* mres);
+
 const char* cly_strerror(int code);
 
 /* Library build identification (gfx target, kernel configuration).            */

@@ -187,6 +187,74 @@ uint64_t clyo_encode_record(uint8_t* out, uint8_t type, uint8_t dtype,
 }
 
 /* ------------------------------------------------------------------------ */
+/* db.merge rewrite loop (merge.go:90-143) over the tuples of a scan, for the
+ * records the caller's index marks live (merge.go:104-132: index pos ==
+ * (fid, offset)).  Per live record, in scan order:
+ *   realKey, _ := parseLogRecordKey(Key)                 merge.go:102, db.go:706-710
+ *   Key = encodeKeyWithTxId(realKey, NO_TX_ID)            merge.go:129, batch.go:120-127
+ *   pos = mergeDb.appendLogRecord(rec)                    merge.go:130, db.go:368-413
+ *         (EncodeLogRecord; a new file when WriteOff+size > DataFileSize; the
+ *          merge DB starts empty, its first file is fid 0)
+ *   hintFile.WriteHintRecord(realKey, pos)                merge.go:135, data/dataFile.go:114-121
+ * A tuple whose txId varint overflowed (txid_len 0xFF) panics in the
+ * reference's parseLogRecordKey: CLYO_ERR_VARINT.  Output file k is written at
+ * out + k*data_file_size (a record larger than data_file_size: -12).          */
+int clyo_merge(const uint8_t* const* bases, const uint32_t* tuple_file, const clyo_tuple* tuples,
+               uint64_t ntuples, const uint8_t* live, uint64_t data_file_size,
+               uint8_t* out, uint32_t out_max_files, uint64_t* out_len,
+               uint8_t* hint, uint64_t hint_cap, clyo_merge_result* res) {
+    memset(res, 0, sizeof(*res));
+    for (uint64_t i = 0; i < ntuples; i++)
+        if (tuples[i].txid_len == 0xFF) return CLYO_ERR_VARINT;
+    int64_t fid = -1;                                    /* activityFile == nil */
+    uint64_t write_off = 0, hint_off = 0;
+    int cap_err = 0;
+    uint8_t* rec = NULL;
+    uint64_t rec_cap = 0;
+    for (uint64_t i = 0; i < ntuples; i++) {
+        if (!live[i]) continue;
+        const clyo_tuple* t = &tuples[i];
+        const uint8_t* F = bases[tuple_file[i]] + t->offset;
+        const uint8_t* key = F + t->header_size;
+        const uint64_t tl = t->txid_len;                 /* 0: Varint (0,0) on a short key, realKey = key */
+        const uint8_t* rk = key + tl;
+        const uint64_t rkl = t->key_size - tl;
+        const uint64_t need = 27 + rkl + t->value_size;
+        if (need > rec_cap) { free(rec); rec_cap = need * 2; rec = (uint8_t*)malloc(rec_cap); }
+        uint8_t* nk = (uint8_t*)malloc(rkl + 1);
+        nk[0] = 0x00;                                    /* PutVarint(0) */
+        if (rkl) memcpy(nk + 1, rk, rkl);
+        const uint64_t size = clyo_encode_record(rec, t->type, t->data_type, nk, rkl + 1,
+                                                 key + t->key_size, t->value_size, t->expiration);
+        free(nk);
+        if (size > data_file_size) { free(rec); return -12; }
+        if (fid < 0) fid = 0;                            /* setActivityFile: fid 0 */
+        if (write_off + size > data_file_size) { fid++; write_off = 0; }   /* db.go:376-385 */
+        if (size != t->size || memcmp(rec, F, size) != 0) res->n_reencoded++;
+        if ((uint64_t)fid < out_max_files) {
+            memcpy(out + (uint64_t)fid * data_file_size + write_off, rec, size);
+            out_len[fid] = write_off + size;
+        } else cap_err = 1;
+        /* hint record: Key = realKey, Value = EncodeLogRecordPos{fid, writeOff} */
+        uint8_t pv[20];
+        int pl = clyo_put_varint(pv, fid);
+        pl += clyo_put_varint(pv + pl, (int64_t)write_off);
+        uint8_t* hr = (uint8_t*)malloc(26 + rkl + pl);
+        const uint64_t hs = clyo_encode_record(hr, 0, 0, rk, rkl, pv, (uint64_t)pl, 0);
+        if (hint_off + hs <= hint_cap) memcpy(hint + hint_off, hr, hs);
+        else cap_err = 1;
+        free(hr);
+        hint_off += hs;
+        write_off += size;
+        res->n_live++;
+    }
+    free(rec);
+    res->n_out_files = (uint32_t)(fid + 1);
+    res->hint_bytes = hint_off;
+    return cap_err ? -10 : 0;
+}
+
+/* ------------------------------------------------------------------------ */
 /* "ref-faithful" CPU baseline: the reference's per-call I/O pattern.        */
 static int mmap_read(const char* path, uint8_t* dst, int64_t len, int64_t off, int* eof) {
     /* driver/mmap.go:25-32 -> x/exp/mmap Open (open, fstat, mmap, close) +

@@ -63,6 +63,20 @@ uint64_t clyo_encode_record(uint8_t* out, uint8_t type, uint8_t dtype,
                             const uint8_t* key, uint64_t klen,
                             const uint8_t* val, uint64_t vlen, int64_t expiration);
 
+/* db.merge rewrite loop (merge.go:90-143): live tuples re-encoded with a
+ * NO_TX_ID key into merge data files (appendLogRecord rotation, db.go:376-385)
+ * plus the hint-index records.  tuple_file[i] indexes bases.  Returns 0,
+ * CLYO_ERR_VARINT, -10 (capacity; *res holds the need) or -12 (a record larger
+ * than data_file_size). */
+typedef struct clyo_merge_result {
+    uint64_t n_live, n_reencoded, hint_bytes;
+    uint32_t n_out_files, _pad;
+} clyo_merge_result;
+int clyo_merge(const uint8_t* const* bases, const uint32_t* tuple_file, const clyo_tuple* tuples,
+               uint64_t ntuples, const uint8_t* live, uint64_t data_file_size,
+               uint8_t* out, uint32_t out_max_files, uint64_t* out_len,
+               uint8_t* hint, uint64_t hint_cap, clyo_merge_result* res);
+
 /* ---- CPU baselines for bench.py (cpu_baseline leg) ----------------------- */
 
 /* "ref-faithful": scans one on-disk file reproducing the reference's I/O

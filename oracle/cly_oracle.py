@@ -56,6 +56,10 @@ def lib():
         L.clyo_scan_files_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                          ctypes.c_int]
         L.clyo_scan_files_mt.restype = ctypes.c_uint64
+        L.clyo_merge.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_uint64, ctypes.c_void_p]
+        L.clyo_merge.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -110,3 +114,31 @@ def scan_files_mt(arrays, fids, nthreads):
     lens = (ctypes.c_uint64 * n)(*[len(a) for a in arrays])
     fa = (ctypes.c_uint32 * n)(*fids)
     return lib().clyo_scan_files_mt(bases, lens, fa, n, nthreads)
+
+
+class MergeResult(ctypes.Structure):
+    _fields_ = [("n_live", ctypes.c_uint64), ("n_reencoded", ctypes.c_uint64), ("hint_bytes", ctypes.c_uint64),
+                ("n_out_files", ctypes.c_uint32), ("_pad", ctypes.c_uint32)]
+
+
+def merge(arrays, tuples, tuple_file, live, data_file_size):
+    """db.merge rewrite (merge.go:90-143) -> (rc, [output file bytes], hint bytes, MergeResult)."""
+    tuples = np.ascontiguousarray(tuples, dtype=TUPLE_DTYPE)
+    tf = np.ascontiguousarray(tuple_file, dtype=np.uint32)
+    lv = np.ascontiguousarray(live, dtype=np.uint8)
+    n = len(tuples)
+    keep = [np.ascontiguousarray(a) if len(a) else np.zeros(1, np.uint8) for a in arrays]
+    bases = (ctypes.c_void_p * max(1, len(keep)))(*[a.ctypes.data for a in keep])
+    live_bytes = int(tuples["size"][lv != 0].astype(np.int64).sum()) if n else 0
+    max_files = live_bytes // max(1, data_file_size // 2) + 2
+    out = np.zeros(max_files * data_file_size, np.uint8)
+    out_len = np.zeros(max_files, np.uint64)
+    hint_cap = int(n * 48 + tuples["key_size"].astype(np.int64).sum()) + 64 if n else 64
+    hint = np.zeros(hint_cap, np.uint8)
+    r = MergeResult()
+    rc = lib().clyo_merge(bases, tf.ctypes.data if n else None, tuples.ctypes.data if n else None, n,
+                          lv.ctypes.data if n else None, data_file_size, out.ctypes.data, max_files,
+                          out_len.ctypes.data, hint.ctypes.data, hint_cap, ctypes.byref(r))
+    files = [out[k * data_file_size:k * data_file_size + int(out_len[k])].tobytes() for k in range(r.n_out_files)] \
+        if rc == 0 else []
+    return rc, files, hint[:r.hint_bytes].tobytes() if rc == 0 else b"", r

@@ -89,3 +89,95 @@ def compare(gpu_tuples, gpu_status, gpu_end, oracle_tuples, oracle_status, oracl
         bad = np.nonzero((g != o).any(axis=1))[0]
         assert bad.size == 0, "%s first differing tuple %d: gpu=%s oracle=%s" % (
             label, bad[0], gpu_tuples[bad[0]], oracle_tuples[bad[0]])
+
+
+def string_live_mask(file_bytes, tuples_per_file):
+    """The index db.loadIndex rebuilds (db.go:582-637: updateIndex for String
+    keys, tx records applied at their commit marker, rollback drops), then
+    merge.go:104-132's liveness test: a record is live iff the index still
+    points at its (fid, offset).  Non-String data types count as dead here (the
+    merge kernel takes the mask as given)."""
+    index, txbuf = {}, {}
+
+    def apply(rk, t):
+        if t["data_type"] != mg.STRING:
+            return
+        if t["type"] == mg.DELETED:
+            index.pop(rk, None)
+        else:
+            index[rk] = (int(t["fid"]), int(t["offset"]))
+
+    recs = []
+    for F, tt in zip(file_bytes, tuples_per_file):
+        for t in tt:
+            o, h, ks = int(t["offset"]), int(t["header_size"]), int(t["key_size"])
+            key = bytes(F[o + h:o + h + ks])
+            tx, n = mg.varint(key)
+            rk = key[n:] if n > 0 else key
+            recs.append((rk, t))
+            if tx == 0:
+                apply(rk, t)
+            elif t["type"] == mg.TXN_BEGIN:
+                pass
+            elif t["type"] == mg.TXN_COMMIT:
+                for r in txbuf.pop(tx, []):
+                    apply(*r)
+            elif t["type"] == mg.TXN_ROLLBACK:
+                txbuf.pop(tx, None)
+            else:
+                txbuf.setdefault(tx, []).append((rk, t))
+    return np.array([1 if (t["data_type"] == mg.STRING and index.get(rk) == (int(t["fid"]), int(t["offset"]))) else 0
+                     for rk, t in recs], dtype=np.uint8)
+
+
+def py_merge(file_bytes, tuples_per_file, live, data_file_size):
+    """Independent restatement of merge.go:90-143 (pure Python, small inputs):
+    -> ([merge data files], hint file bytes)."""
+    outs, hint = [], bytearray()
+    wo, i = 0, 0
+    for F, tt in zip(file_bytes, tuples_per_file):
+        for t in tt:
+            if live[i]:
+                o, h, ks, vs = int(t["offset"]), int(t["header_size"]), int(t["key_size"]), int(t["value_size"])
+                key = bytes(F[o + h:o + h + ks])
+                tx, n = mg.varint(key)
+                rk = key[n:] if n > 0 else key
+                rec = mg.encode_record(mg.put_varint(0) + rk, bytes(F[o + h + ks:o + h + ks + vs]),
+                                       int(t["type"]), int(t["data_type"]), int(t["expiration"]))
+                if not outs:
+                    outs.append(bytearray())
+                if wo + len(rec) > data_file_size:
+                    outs.append(bytearray())
+                    wo = 0
+                outs[-1] += rec
+                hint += mg.encode_record(rk, mg.put_varint(len(outs) - 1) + mg.put_varint(wo))
+                wo += len(rec)
+            i += 1
+    return [bytes(x) for x in outs], bytes(hint)
+
+
+def merge_corpus(seed, n_keys=300, rounds=3, tx_frac=0.3):
+    """A String-key workload with overwrites, deletes, committed and rolled-back
+    transactions (the shapes db.Put/Del/WriteBatch produce) -> record bytes."""
+    rng = random.Random(seed)
+    b = bytearray()
+    txid = 1000
+    for r in range(rounds):
+        for k in rng.sample(range(n_keys), n_keys * 2 // 3):
+            key = mg.test_key(k)
+            if rng.random() < tx_frac:
+                txid += 1
+                ops = [(key, rng.random() < 0.2)] + [(mg.test_key(rng.randrange(n_keys)), False)
+                                                     for _ in range(rng.randrange(0, 3))]
+                for kk, dele in ops:
+                    b += mg.encode_record(mg.key_tx(kk, txid), b"" if dele else rng.randbytes(rng.randrange(0, 300)),
+                                          mg.DELETED if dele else mg.NORMAL, mg.STRING,
+                                          rng.choice([0, 0, 1_700_000_000_000_000_000]))
+                end = mg.TXN_ROLLBACK if rng.random() < 0.15 else mg.TXN_COMMIT
+                b += mg.encode_record(mg.key_tx(b"txn-fin", txid), b"", end, mg.STRING, 0)
+            elif rng.random() < 0.2:
+                b += mg.encode_record(mg.key_tx(key, 0), b"", mg.DELETED, mg.STRING, 0)
+            else:
+                b += mg.encode_record(mg.key_tx(key, 0), rng.randbytes(rng.choice([0, 5, 50, 256, 900])),
+                                      mg.NORMAL, rng.choice([0, 0, 0, 1, 2, 3, 4]), 0)
+    return bytes(b)

@@ -1,0 +1,206 @@
+"""Merge rewrite (db.merge, merge.go:90-143).
+
+CPU: the oracle's C restatement (oracle/cly_oracle.c clyo_merge) against the
+independent pure-Python restatement (tests/gpu_util.py py_merge) on String-key
+workloads with overwrites, deletes and transactions, on every golden fixture
+(all records live) and on mixed corpora with random live masks.
+GPU (-m gpu): the HIP merge (cly_merge / cly_merge_device through the C-ABI)
+against the oracle, byte for byte: merge data files, hint-index file, counters.
+The reference ships no merge byte vectors: parity with the Go
+binary is pinned through the restatements only."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle import cly_oracle as co
+
+from .gpu_util import merge_corpus, mg, mixed_corpus, py_merge, string_live_mask
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+with open(os.path.join(GOLD, "golden.json")) as _f:
+    GOLDEN = json.load(_f)
+FIXTURES = sorted(k for k in GOLDEN if not k.startswith("_"))
+
+
+def split_files(b, nfiles, rng):
+    """Cut a record stream into data files at record boundaries (as appendLogRecord rotates)."""
+    _, _, recs = mg.scan(b, 0)
+    cuts = sorted(rng.sample(range(1, len(recs)), min(nfiles - 1, max(0, len(recs) - 1)))) if len(recs) > 1 else []
+    offs = [0] + [recs[c][0] for c in cuts] + [len(b)]
+    return [b[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
+
+
+def oracle_scan(files):
+    arrays = [np.frombuffer(f, np.uint8) for f in files]
+    tts, sts = [], []
+    for fid, a in enumerate(arrays):
+        t, st, _ = co.scan_file(a, fid)
+        tts.append(t)
+        sts.append(st)
+    return arrays, tts, sts
+
+
+def flat(tts):
+    tuples = np.concatenate(tts) if tts else np.zeros(0, co.TUPLE_DTYPE)
+    tf = np.concatenate([np.full(len(t), i, np.uint32) for i, t in enumerate(tts)]) if tts else np.zeros(0, np.uint32)
+    return tuples, tf
+
+
+def check_oracle(files, live, dfs):
+    arrays, tts, _ = oracle_scan(files)
+    tuples, tf = flat(tts)
+    rc, outs, hint, r = co.merge(arrays, tuples, tf, live, dfs)
+    assert rc == 0
+    p_outs, p_hint = py_merge(arrays, tts, live, dfs)
+    assert outs == p_outs
+    assert hint == p_hint
+    assert r.n_live == int(np.count_nonzero(live)) and r.n_out_files == len(p_outs)
+    return outs, hint, r
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("dfs", [1200, 4096, 1 << 20])
+def test_oracle_merge_string_workload(seed, dfs):
+    rng = random.Random(seed)
+    b = merge_corpus(seed, n_keys=200 + 50 * seed)
+    files = split_files(b, 1 + seed % 4, rng)
+    arrays, tts, _ = oracle_scan(files)
+    live = string_live_mask(arrays, tts)
+    _, _, r = check_oracle(files, live, dfs)
+    assert r.n_reencoded > 0 or seed % 2          # committed tx records get a NO_TX_ID key
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_oracle_merge_mixed_random_live(seed):
+    rng = np.random.default_rng(seed)
+    b = mixed_corpus(100 + seed, 60_000, tail=False)
+    files = split_files(b, 3, random.Random(seed))
+    arrays, tts, _ = oracle_scan(files)
+    live = (rng.random(sum(len(t) for t in tts)) < 0.6).astype(np.uint8)
+    check_oracle(files, live, 1 << 16)
+
+
+def test_oracle_merge_fixtures_all_live():
+    for name in FIXTURES:
+        g = GOLDEN[name]
+        if g["status"] < 0:
+            continue
+        with open(os.path.join(GOLD, name + ".cly"), "rb") as f:
+            b = f.read()
+        arrays, tts, _ = oracle_scan([b])
+        tuples, tf = flat(tts)
+        live = np.ones(len(tuples), np.uint8)
+        if len(tuples) and (tuples["txid_len"] == 0xFF).any():
+            rc, _, _, _ = co.merge(arrays, tuples, tf, live, 1 << 20)
+            assert rc == -3, name
+            continue
+        check_oracle([b], live, 1 << 20)
+
+
+def test_oracle_merge_rotation_exact_fit():
+    # records of 276 B, data file of exactly 3 records: rotation when WriteOff+size > DataFileSize
+    recs = b"".join(mg.encode_record(mg.key_tx(mg.test_key(i), 0), bytes(256)) for i in range(10))
+    live = np.ones(10, np.uint8)
+    outs, hint, r = check_oracle([recs], live, 3 * 276)
+    assert [len(o) for o in outs] == [828, 828, 828, 276]
+    assert r.n_reencoded == 0 and outs[0] == recs[:828]
+
+
+def test_oracle_merge_record_larger_than_file():
+    recs = mg.encode_record(mg.key_tx(mg.test_key(1), 0), bytes(500))
+    arrays, tts, _ = oracle_scan([recs])
+    tuples, tf = flat(tts)
+    rc, _, _, _ = co.merge(arrays, tuples, tf, np.ones(1, np.uint8), 100)
+    assert rc == -12
+
+
+# ---------------------------------------------------------------- GPU --------
+@pytest.fixture(scope="module")
+def scanner():
+    from couloydb_amd import Scanner
+    s = Scanner(0)
+    yield s
+    s.close()
+
+
+def gpu_vs_oracle(scanner, files, live, dfs):
+    from couloydb_amd import DataFile
+    arrays, tts, _ = oracle_scan(files)
+    tuples, tf = flat(tts)
+    rc, outs, hint, r = co.merge(arrays, tuples, tf, live, dfs)
+    assert rc == 0
+    m = scanner.merge([DataFile(a.copy(), i) for i, a in enumerate(arrays)], live, dfs)
+    assert m.n_out_files == r.n_out_files and m.n_live == r.n_live and m.n_reencoded == r.n_reencoded
+    for k, (g, o) in enumerate(zip(m.files, outs)):
+        assert len(g) == len(o), "file %d length gpu=%d oracle=%d" % (k, len(g), len(o))
+        if g != o:
+            d = next(i for i in range(len(g)) if g[i] != o[i])
+            raise AssertionError("merge file %d differs at byte %d" % (k, d))
+    assert m.hint == hint
+    return m
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("dfs", [1200, 4096, 1 << 20])
+def test_gpu_merge_string_workload(scanner, seed, dfs):
+    rng = random.Random(seed)
+    b = merge_corpus(seed, n_keys=200 + 50 * seed)
+    files = split_files(b, 1 + seed % 4, rng)
+    arrays, tts, _ = oracle_scan(files)
+    gpu_vs_oracle(scanner, files, string_live_mask(arrays, tts), dfs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(4))
+def test_gpu_merge_mixed_random_live(scanner, seed):
+    rng = np.random.default_rng(seed)
+    b = mixed_corpus(100 + seed, 200_000, tail=False)
+    files = split_files(b, 3, random.Random(seed))
+    arrays, tts, _ = oracle_scan(files)
+    live = (rng.random(sum(len(t) for t in tts)) < 0.6).astype(np.uint8)
+    gpu_vs_oracle(scanner, files, live, 1 << 16)
+
+
+@pytest.mark.gpu
+def test_gpu_merge_fixtures_all_live(scanner):
+    from couloydb_amd import DataFile, ScanError
+    for name in FIXTURES:
+        g = GOLDEN[name]
+        with open(os.path.join(GOLD, name + ".cly"), "rb") as f:
+            b = f.read()
+        arrays, tts, _ = oracle_scan([b])
+        tuples, _ = flat(tts)
+        live = np.ones(len(tuples), np.uint8)
+        if g["status"] < 0:
+            with pytest.raises(ScanError) as ei:          # merge.go:94-99 returns the scan's error
+                scanner.merge([DataFile(np.frombuffer(b, np.uint8).copy(), 0)], live, 1 << 20)
+            assert ei.value.code == g["status"], name
+            continue
+        if len(tuples) and (tuples["txid_len"] == 0xFF).any():
+            with pytest.raises(ScanError) as ei:
+                scanner.merge([DataFile(np.frombuffer(b, np.uint8).copy(), 0)], live, 1 << 20)
+            assert ei.value.code == -3, name
+            continue
+        gpu_vs_oracle(scanner, [b], live, 1 << 20)
+
+
+@pytest.mark.gpu
+def test_gpu_merge_rotation_and_verbatim(scanner):
+    recs = b"".join(mg.encode_record(mg.key_tx(mg.test_key(i), 0), bytes(256)) for i in range(5000))
+    live = (np.arange(5000) % 3 != 0).astype(np.uint8)
+    m = gpu_vs_oracle(scanner, [recs], live, 64 * 276 + 100)
+    assert m.n_reencoded == 0 and m.n_out_files > 50
+
+
+@pytest.mark.gpu
+def test_gpu_merge_big_records_and_empty(scanner):
+    rng = random.Random(7)
+    recs = b"".join(mg.encode_record(mg.key_tx(mg.test_key(i), i % 3), rng.randbytes(rng.randrange(0, 70000)))
+                    for i in range(60))
+    gpu_vs_oracle(scanner, [recs], np.ones(60, np.uint8), 1 << 20)
+    gpu_vs_oracle(scanner, [recs], np.zeros(60, np.uint8), 1 << 20)
