@@ -12,6 +12,9 @@ Workloads (BASELINE.json configs):
   c2 (default): 16 files x 256 MiB, key 0x00||%09d, 256-B random values -> 276-B records
   c1: one 64 MiB file of 1 KiB values (CPU plumbing config; also runnable here)
   c3: 32 GiB, Zipf(1.1) value lengths 64 B-64 KiB
+  c4: merge.go path, 32 GiB: keys 0..K-1 put, then k%4==0 overwritten and
+      k%4==2 deleted (50 % of the records dead); a step = scan + merge rewrite
+      (live filter, NO_TX_ID re-encode + CRC, file rotation, hint records)
 Data is synthetic (splitmix64 values), written on the GPU by libclygen.so, a
 restatement of EncodeLogRecord + appendLogRecord's file rotation.
 """
@@ -46,7 +49,7 @@ def _zipf_lengths(n, rng, s=1.1, nmax=65473):
     return (63 + r).astype(np.uint32)
 
 
-def make_workload(name, torch, rank=0, device=0, seed=0x434C59):
+def make_workload(name, torch, rank=0, device=0, seed=0x434C59, size=32 * 2**30):
     """Build the config's data files in HBM on `device`.  Returns a Workload with
     dev_files [(ptr, len, fid)], d_buf, d_out (uint8 tensor), out_cap, expect_records."""
     from couloydb_amd import _abi
@@ -61,17 +64,30 @@ def make_workload(name, torch, rank=0, device=0, seed=0x434C59):
     elif name == "c3":
         rng = np.random.default_rng(seed + 3)
         nfiles_target = 128
-        vl = _zipf_lengths(int(32 * 2**30 / 3500), rng)
+        vl = _zipf_lengths(int(size / 3500), rng)
         # trim/extend to ~32 GiB
         sizes = vl.astype(np.int64) + 20
         cum = np.cumsum(sizes)
-        vl = vl[: int(np.searchsorted(cum, 32 * 2**30 - nfiles_target * 70000))]
+        vl = vl[: int(np.searchsorted(cum, size - nfiles_target * 70000))]
+    elif name == "c4":
+        nfiles_target = 128
+        K = int(size / (276 + 276 / 4 + 19 / 4))
+        K -= K % 4
+        ph2 = np.arange(0, K, 2, dtype=np.int64)             # k%4==0 put, k%4==2 Del
+        keys = np.concatenate([np.arange(K, dtype=np.int64), ph2])
+        vl = np.concatenate([np.full(K, 256, np.uint32), np.where(ph2 % 4 == 0, 256, 0).astype(np.uint32)])
+        typ = np.concatenate([np.zeros(K, np.uint8), np.where(ph2 % 4 == 0, 0, 1).astype(np.uint8)])
+        live = np.concatenate([(np.arange(K) % 2 == 1), ph2 % 4 == 0]).astype(np.uint8)
     else:
         raise ValueError(name)
     n = len(vl)
     recs = np.zeros(n, dtype=_abi.GEN_DTYPE)
     recs["value_len"] = vl
-    recs["key_index"] = (np.arange(n, dtype=np.int64) + rank * n) % 1_000_000_000
+    if name == "c4":
+        recs["key_index"] = (keys + rank * K) % 1_000_000_000
+        recs["type"] = typ
+    else:
+        recs["key_index"] = (np.arange(n, dtype=np.int64) + rank * n) % 1_000_000_000
     maxf = 4096
     fo = (ctypes.c_uint64 * maxf)()
     fl = (ctypes.c_uint64 * maxf)()
@@ -95,6 +111,15 @@ def make_workload(name, torch, rank=0, device=0, seed=0x434C59):
     wl.bytes = int(sum(fl[i] for i in range(nf.value)))
     wl.expect_records = n
     wl.out_cap = n + 1024
+    if name == "c4":
+        wl.live_np = live
+        wl.live = torch.from_numpy(live).to(dev)
+        wl.n_live = int(live.sum())
+        live_bytes = int((recs["value_len"][live != 0].astype(np.int64) + 20).sum())
+        wl.merge_max_files = live_bytes // (DATA_FILE_SIZE - 65536) + 4
+        wl.d_merge = torch.empty(wl.merge_max_files * DATA_FILE_SIZE, dtype=torch.uint8, device=dev)
+        wl.hint_cap = wl.n_live * 40 + 4096
+        wl.d_hint = torch.empty(wl.hint_cap, dtype=torch.uint8, device=dev)
     wl.d_out = torch.empty(wl.out_cap * 48, dtype=torch.uint8, device=dev)
 
     def file_bytes(i):
@@ -140,6 +165,22 @@ def cpu_baseline(wl, budget_s=12.0):
         files.append(i)
         i += 1
     alg_gibs = nbytes / t_alg / 2**30
+    merge_part = None
+    if wl.name == "c4":
+        # scan + merge rewrite of the sampled files (file i's live bytes follow the
+        # scan order of the records before it)
+        t_m, mb, first_rec = 0.0, 0, 0
+        for i in range(min(len(files), 4)):
+            arr = wl.file_bytes(i)
+            t0 = time.perf_counter()
+            tt, _, _ = co.scan_file(arr, wl.dev_files[i][2])
+            rc, _, _, r = co.merge([arr], tt, np.zeros(len(tt), np.uint32), wl.live_np[first_rec:first_rec + len(tt)],
+                                   DATA_FILE_SIZE)
+            t_m += time.perf_counter() - t0
+            first_rec += len(tt)
+            mb += len(arr)
+        merge_part = {"value": round(mb / t_m / 2**30, 4), "unit": "GiB/s",
+                      "sample": "%d files: oracle scan + clyo_merge (merge.go:90-143 restated), 1 thread" % min(len(files), 4)}
     # ref-faithful on a bounded number of records of file 0
     arr = wl.file_bytes(0)
     with tempfile.TemporaryDirectory() as d:
@@ -156,7 +197,9 @@ def cpu_baseline(wl, budget_s=12.0):
             "ref_faithful": {"value": round(faithful_gibs, 5), "unit": "GiB/s",
                              "mrecords_per_s": round(nf / tf / 1e6, 4),
                              "sample": "first %d records of one file; per record fstat + 2x (open, mmap whole file, copy, munmap)" % nf},
-            "host_nproc": os.cpu_count()}
+            "host_nproc": os.cpu_count(),
+            **({"value": merge_part["value"], "sample": merge_part["sample"], "scan_only_value": round(alg_gibs, 4)}
+               if merge_part else {})}
 
 
 def host_path(wl, sc, max_files=16):
@@ -202,7 +245,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
     ap.add_argument("--verify", action="store_true", help="check one file against the oracle after timing")
@@ -221,14 +264,30 @@ def main():
     wl = make_workload(args.config, torch, rank=rank, device=local)
     sc = Scanner(local)
 
+    merge_ms = [0.0]
+    merge_info = {}
+
     def step():
-        return sc.scan_device(wl.dev_files, wl.d_out.data_ptr(), wl.out_cap)
+        r = sc.scan_device(wl.dev_files, wl.d_out.data_ptr(), wl.out_cap)
+        if args.config == "c4":
+            first, res, st, need = r
+            rc, lens, m = sc.merge_device(wl.dev_files, wl.d_out.data_ptr(), first, res, wl.live.data_ptr(),
+                                          DATA_FILE_SIZE, wl.d_merge.data_ptr(), wl.merge_max_files,
+                                          wl.d_hint.data_ptr(), wl.hint_cap)
+            if rc != 0:
+                raise RuntimeError("cly_merge_device failed: %d (need %d files, %d hint bytes)"
+                                   % (rc, m.n_out_files, m.hint_bytes))
+            merge_ms[0] += m.merge_ms
+            merge_info.update(n_live=int(m.n_live), n_reencoded=int(m.n_reencoded), n_out_files=int(m.n_out_files),
+                              hint_bytes=int(m.hint_bytes), out_bytes=int(sum(lens)), out_lens=lens)
+        return r
 
     for _ in range(args.warmup):
         step()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    merge_ms[0] = 0.0
     t0 = time.perf_counter()
     scan_ms, res_ms, passes, recs = 0.0, 0.0, 0, 0
     for _ in range(args.steps):
@@ -269,6 +328,25 @@ def main():
                              "WRITE_SIZE passes of this build (profiles/*_traffic.json), null if none"},
         "parity_ok": ok,
     }
+    if args.config == "c4":
+        mi = dict(merge_info)
+        lens = mi.pop("out_lens")
+        mms = merge_ms[0] / args.steps
+        mi["merge_ms"] = round(mms, 4)
+        mi["merge_io_gbs"] = round((mi["out_bytes"] * 2 + mi["hint_bytes"]) / (mms / 1e3) / 1e9, 1)
+        # size-independent checks: the live count, and a rescan of the merge output
+        # (every merged record decodes, keys carry NO_TX_ID, files end cleanly) and of the hint file
+        mfiles = [(wl.d_merge.data_ptr() + k * DATA_FILE_SIZE, lens[k], k) for k in range(len(lens))]
+        cap = mi["n_live"] + 1024
+        d2 = torch.empty(cap * 48, dtype=torch.uint8, device="cuda")
+        f2, r2, _, n2 = sc.scan_device(mfiles, d2.data_ptr(), cap)
+        hf = [(wl.d_hint.data_ptr(), mi["hint_bytes"], 0)]
+        f3, r3, _, n3 = sc.scan_device(hf, d2.data_ptr(), cap)
+        mi["rescan_ok"] = bool(n2 == mi["n_live"] and all(r.status == 0 for r in r2) and n3 == mi["n_live"]
+                               and r3[0].status == 0)
+        out["merge"] = mi
+        out["parity_ok"] = bool(ok and mi["n_live"] == wl.n_live and mi["rescan_ok"])
+        del d2
     if args.verify and rank == 0:
         from oracle import cly_oracle as co
         from couloydb_amd import TUPLE_DTYPE

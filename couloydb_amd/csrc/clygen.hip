@@ -135,8 +135,10 @@ __global__ void __launch_bounds__(256) k_gen_encode(uint8_t* __restrict__ buf, c
 extern "C" int cly_gen_encode(uint8_t* d_buf, const cly_gen_rec* d_recs, uint64_t nrecs, uint64_t seed) {
     if (!nrecs) return 0;
     const uint64_t blocks = (nrecs + 3) / 4;
-    for (uint64_t b0 = 0; b0 < blocks; b0 += (1u << 30)) {
-        const uint64_t nb = blocks - b0 < (1u << 30) ? blocks - b0 : (1u << 30);
+    // a launch's work-item count (grid x block) must stay below 2^32
+    const uint64_t per = 1u << 22;
+    for (uint64_t b0 = 0; b0 < blocks; b0 += per) {
+        const uint64_t nb = blocks - b0 < per ? blocks - b0 : per;
         hipLaunchKernelGGL(k_gen_encode, dim3((unsigned)nb), dim3(256), 0, 0, d_buf, d_recs + b0 * 4,
                            nrecs - b0 * 4, seed);
     }

@@ -204,3 +204,32 @@ def test_gpu_merge_big_records_and_empty(scanner):
                     for i in range(60))
     gpu_vs_oracle(scanner, [recs], np.ones(60, np.uint8), 1 << 20)
     gpu_vs_oracle(scanner, [recs], np.zeros(60, np.uint8), 1 << 20)
+
+
+@pytest.mark.gpu
+def test_gpu_merge_device_c4_shape():
+    """BASELINE config 4's shape (puts, k%4==0 overwritten, k%4==2 deleted: 50 %
+    of the records dead) at 600 MiB with the reference's 256 MiB data files,
+    through the device-resident entry, against the oracle byte for byte."""
+    import torch
+    import bench
+    from couloydb_amd import Scanner, TUPLE_DTYPE
+    wl = bench.make_workload("c4", torch, size=600 << 20)
+    with Scanner(0) as sc:
+        first, res, st, need = sc.scan_device(wl.dev_files, wl.d_out.data_ptr(), wl.out_cap)
+        assert all(r.status == 0 for r in res) and need == wl.expect_records
+        rc, lens, m = sc.merge_device(wl.dev_files, wl.d_out.data_ptr(), first, res, wl.live.data_ptr(),
+                                      bench.DATA_FILE_SIZE, wl.d_merge.data_ptr(), wl.merge_max_files,
+                                      wl.d_hint.data_ptr(), wl.hint_cap)
+        assert rc == 0 and m.n_live == wl.n_live and m.n_reencoded == 0
+    arrays = [wl.file_bytes(i) for i in range(len(wl.dev_files))]
+    tts = [co.scan_file(a, wl.dev_files[i][2])[0] for i, a in enumerate(arrays)]
+    tuples, tf = flat(tts)
+    got = wl.d_out[: need * 48].cpu().numpy().view(TUPLE_DTYPE)
+    assert (got.view(np.uint8) == tuples.view(np.uint8)).all()
+    rc, outs, hint, r = co.merge(arrays, tuples, tf, wl.live_np, bench.DATA_FILE_SIZE)
+    assert rc == 0 and r.n_out_files == m.n_out_files == len(lens)
+    for k in range(len(lens)):
+        o = wl.d_merge[k * bench.DATA_FILE_SIZE:k * bench.DATA_FILE_SIZE + lens[k]].cpu().numpy().tobytes()
+        assert o == outs[k], k
+    assert wl.d_hint[:m.hint_bytes].cpu().numpy().tobytes() == hint
