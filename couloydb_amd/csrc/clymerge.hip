@@ -165,7 +165,11 @@ k_mplan(const cly_tuple* __restrict__ tup, uint64_t T, const uint8_t* __restrict
             const int nh = 6 + uvlen(zz((int64_t)nks)) + uvlen(zz((int64_t)t.value_size)) + uvlen(zz(t.expiration));
             const uint64_t nsz = (uint64_t)nh + nks + t.value_size;
             bool verbatim = t.txid_len == 1 && t.tx_id == 0 && nh == t.header_size;
-            if (verbatim) {
+            // Equal header lengths mean the stored varints are the canonical ones
+            // (a longer-than-canonical encoding would make the header longer) unless
+            // a stored size varint was truncated by uint32() (data/logRecord.go:101,106),
+            // which needs >= 5 varint bytes: only then compare the bytes.
+            if (verbatim && (uvlen(zz((int64_t)nks)) >= 5 || uvlen(zz((int64_t)t.value_size)) >= 5)) {
                 const int f = find_file_u64(first, nfiles, i);
                 const uint8_t* h = (const uint8_t*)bases[f] + t.offset;
                 uint8_t cb[26];
@@ -370,6 +374,11 @@ k_mplace(const MEnt* __restrict__ e, const cly_tuple* __restrict__ tup, const ui
 }
 
 // ---- k_mhint: hint-index records (data/dataFile.go:114-121) -----------------
+// The hint records of a workgroup's 256 consecutive live records are contiguous
+// in the hint file: they are assembled in LDS and written out with aligned
+// dword stores (byte stores only at the two ends), unless they exceed the LDS
+// buffer (large keys), when each thread stores its own record's bytes.
+#define MH_BUF 12288
 __global__ void __launch_bounds__(M_NT)
 k_mhint(const MEnt* __restrict__ e, const MCopy* __restrict__ cp, const cly_tuple* __restrict__ tup,
         const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases, int nfiles,
@@ -377,117 +386,188 @@ k_mhint(const MEnt* __restrict__ e, const MCopy* __restrict__ cp, const cly_tupl
         uint8_t* hint, uint64_t hint_cap) {
     __shared__ uint32_t tab[256];
     __shared__ MSum sh[M_NT / 64];
+    __shared__ __attribute__((aligned(16))) uint8_t buf[MH_BUF + 16];
     crc_table_init(tab);
     const uint64_t nl = tot->nl;
     const uint64_t b0 = (uint64_t)blockIdx.x * M_BLK;
     MSum carry = bsum[blockIdx.x];
     for (int it = 0; it < M_IT; it++) {
-        if (b0 + (uint64_t)it * M_NT >= nl) break;
+        if (b0 + (uint64_t)it * M_NT >= nl) break;              // (uniform)
         const uint64_t j = b0 + (uint64_t)it * M_NT + threadIdx.x;
         const uint32_t hs = j < nl ? hsz[j] : 0;
         MSum v = {hs, 0};
         MSum total;
         const MSum ex = block_excl(v, total, sh);
-        const uint64_t ho = carry.bytes + ex.bytes;
+        const uint64_t H0 = carry.bytes;
+        const uint64_t ho = H0 + ex.bytes;
         carry.bytes += total.bytes;
-        if (j >= nl || ho + hs > hint_cap) continue;
-        const MEnt m = e[j];
-        const cly_tuple t = tup[m.tuple];
-        const int f = find_file_u64(first, nfiles, m.tuple);
-        const uint8_t* rkey = (const uint8_t*)bases[f] + t.offset + t.header_size + t.txid_len;
-        const uint32_t rk = t.key_size - t.txid_len;
-        const uint64_t dst = cp[j].dst;
-        const uint64_t fid = dst / stride, off = dst - fid * stride;
-        uint8_t pv[20];
-        int pl = put_uv(pv, zz((int64_t)fid));
-        pl += put_uv(pv + pl, zz((int64_t)off));
-        uint8_t h[26];
-        h[4] = 0; h[5] = 0;
-        int n = 6;
-        n += put_uv(h + n, zz((int64_t)rk));
-        n += put_uv(h + n, zz((int64_t)pl));
-        h[n++] = 0;                                             // PutVarint(0) expiration
-        uint32_t s = 0xFFFFFFFFu;
-        for (int q = 4; q < n; q++) s = crc_upd(tab, s, h[q]);
-        uint8_t* o = hint + ho;
-        for (uint32_t q = 0; q < rk; q++) { const uint8_t b = rkey[q]; s = crc_upd(tab, s, b); o[n + q] = b; }
-        for (int q = 0; q < pl; q++) { s = crc_upd(tab, s, pv[q]); o[n + rk + q] = pv[q]; }
-        s = ~s;
-        h[0] = (uint8_t)s; h[1] = (uint8_t)(s >> 8); h[2] = (uint8_t)(s >> 16); h[3] = (uint8_t)(s >> 24);
-        for (int q = 0; q < n; q++) o[q] = h[q];
+        const bool staged = total.bytes <= MH_BUF;              // (uniform)
+        if (j < nl && ho + hs <= hint_cap) {
+            const MEnt m = e[j];
+            const cly_tuple t = tup[m.tuple];
+            const int f = find_file_u64(first, nfiles, m.tuple);
+            const uint8_t* rkey = (const uint8_t*)bases[f] + t.offset + t.header_size + t.txid_len;
+            const uint32_t rk = t.key_size - t.txid_len;
+            const uint64_t dst = cp[j].dst;
+            const uint64_t fid = dst / stride, off = dst - fid * stride;
+            uint8_t pv[20];
+            int pl = put_uv(pv, zz((int64_t)fid));
+            pl += put_uv(pv + pl, zz((int64_t)off));
+            uint8_t h[26];
+            h[4] = 0; h[5] = 0;
+            int n = 6;
+            n += put_uv(h + n, zz((int64_t)rk));
+            n += put_uv(h + n, zz((int64_t)pl));
+            h[n++] = 0;                                         // PutVarint(0) expiration
+            uint32_t s = 0xFFFFFFFFu;
+            for (int q = 4; q < n; q++) s = crc_upd(tab, s, h[q]);
+            uint8_t* o = staged ? buf + (ho - H0) : hint + ho;
+            for (uint32_t q = 0; q < rk; q++) { const uint8_t c = rkey[q]; s = crc_upd(tab, s, c); o[n + q] = c; }
+            for (int q = 0; q < pl; q++) { s = crc_upd(tab, s, pv[q]); o[n + rk + q] = pv[q]; }
+            s = ~s;
+            h[0] = (uint8_t)s; h[1] = (uint8_t)(s >> 8); h[2] = (uint8_t)(s >> 16); h[3] = (uint8_t)(s >> 24);
+            for (int q = 0; q < n; q++) o[q] = h[q];
+        }
+        if (staged) {
+            __syncthreads();
+            uint64_t H1 = H0 + total.bytes;
+            if (H1 > hint_cap) H1 = hint_cap;
+            if (H1 > H0) {
+                // bytes [H0, H1): head bytes up to the first aligned dword, whole dwords, tail bytes
+                const uint64_t A0 = ((uint64_t)(uintptr_t)(hint + H0) + 3) & ~3ull;
+                const uint64_t a0 = A0 - (uint64_t)(uintptr_t)hint;          // first aligned offset
+                const uint64_t a1 = H0 + ((H1 - H0) > (a0 - H0) ? ((H1 - a0) & ~3ull) + (a0 - H0) : 0);
+                for (uint64_t x = H0 + threadIdx.x; x < H1 && x < a0; x += M_NT) hint[x] = buf[x - H0];
+                for (uint64_t x = a0 + 4 * (uint64_t)threadIdx.x; x + 4 <= a1; x += 4 * M_NT) {
+                    const uint64_t r = x - H0;
+                    const uint32_t wv = (uint32_t)buf[r] | ((uint32_t)buf[r + 1] << 8) | ((uint32_t)buf[r + 2] << 16) |
+                                        ((uint32_t)buf[r + 3] << 24);
+                    *(uint32_t*)(hint + x) = wv;
+                }
+                for (uint64_t x = (a1 > a0 ? a1 : a0) + threadIdx.x; x < H1; x += M_NT) hint[x] = buf[x - H0];
+            }
+            __syncthreads();
+        }
     }
 }
 
-// ---- k_mcopy: one 4-KiB destination block per workgroup ----------------------
-__device__ __forceinline__ uint8_t src_byte(const MCopy& c, const uint8_t* pre_j, uint64_t r) {
-    return r < c.pre ? pre_j[r] : ((const uint8_t*)c.src)[r - c.pre];
+// ---- k_mcopy: one 4-KiB destination block per wave ---------------------------
+// The wave loads the copy descriptors of the records covering its block into
+// LDS; lane l then writes the block's 16-B pieces l, l+64, l+128, l+192.  All
+// source loads of a lane are issued before any store (four pieces in flight).
+// A piece inside one record's body is 4-5 aligned dword loads funnel-shifted
+// into place (never a dword beyond the record's last byte); a piece that
+// straddles records, or touches a re-encoded prefix or the end of the file,
+// gathers its 16 bytes with independent byte loads.
+__device__ const uint8_t g_zero_byte = 0;
+#define MC_W 4                                   // waves per workgroup
+#define MC_P (M_CB / 16 / 64)                    // pieces per lane
+__device__ __forceinline__ void mc_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-__global__ void __launch_bounds__(M_NT)
+__global__ void __launch_bounds__(64 * MC_W)
 k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uint32_t* __restrict__ bmap,
         const uint64_t* __restrict__ fstart, const uint64_t* __restrict__ flen, const MTot* tot, uint64_t stride,
         uint64_t nblocks, uint8_t* out) {
-    __shared__ int64_t s_rel[M_CMAX];
-    __shared__ uint64_t s_src[M_CMAX];
-    __shared__ uint32_t s_size[M_CMAX], s_pre[M_CMAX];
+    __shared__ int32_t s_rel[MC_W][M_CMAX];
+    __shared__ uint64_t s_src[MC_W][M_CMAX];
+    __shared__ uint32_t s_end[MC_W][M_CMAX];      // size | pre << 24 would not hold big records: separate arrays
+    __shared__ uint8_t s_pre[MC_W][M_CMAX];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int32_t* rel = s_rel[w];
+    uint64_t* srcs = s_src[w];
+    uint32_t* sizes = s_end[w];
+    uint8_t* pres = s_pre[w];
     const uint64_t bpf = stride / M_CB;
-    for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    for (uint64_t b = (uint64_t)blockIdx.x * MC_W + w; b < nblocks; b += (uint64_t)gridDim.x * MC_W) {
         const uint64_t k = b / bpf;
         const uint64_t B = b * M_CB, fo = B - k * stride;
         const uint64_t L = flen[k];
-        if (fo >= L) continue;                                  // (uniform)
+        if (fo >= L) continue;                                  // (wave-uniform)
         const uint32_t j0 = bmap[b];
         uint64_t j1 = fstart[k + 1];
-        if (fo + M_CB < L && b + 1 < nblocks) j1 = (uint64_t)bmap[b + 1] + 1;
+        if (fo + M_CB < L) j1 = (uint64_t)bmap[b + 1] + 1;
         uint32_t cnt = (uint32_t)(j1 - j0);
         if (cnt > M_CMAX) cnt = M_CMAX;
-        __syncthreads();
-        for (uint32_t q = threadIdx.x; q < cnt; q += M_NT) {
+        mc_wave_sync();                                         // previous block's readers are done
+        for (uint32_t q = lane; q < cnt; q += 64) {
             const MCopy c = cp[j0 + q];
-            s_rel[q] = (int64_t)c.dst - (int64_t)B;
-            s_src[q] = c.src;
-            s_size[q] = c.size;
-            s_pre[q] = c.pre;
+            rel[q] = (int32_t)((int64_t)c.dst - (int64_t)B);   // >= -(record size) > -2^31
+            srcs[q] = c.src;
+            sizes[q] = c.size;
+            pres[q] = (uint8_t)c.pre;
         }
-        __syncthreads();
-        for (int part = 0; part < M_CB / 16 / M_NT; part++) {
-            const int64_t d = (int64_t)(part * M_NT + threadIdx.x) * 16;
+        mc_wave_sync();
+        uint32_t a[MC_P][5];
+        uint32_t fast = 0, gather = 0, shs = 0;
+        #pragma unroll
+        for (int p = 0; p < MC_P; p++) {
+            const int d = (p * 64 + lane) * 16;
             if (fo + (uint64_t)d >= L) continue;
             int lo = 0, hi = (int)cnt - 1;                      // last record with rel <= d
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
-                if (s_rel[mid] <= d) lo = mid; else hi = mid - 1;
+                if (rel[mid] <= d) lo = mid; else hi = mid - 1;
             }
-            const int64_t r0 = d - s_rel[lo];
-            uint32_t wv[4];
-            if (r0 >= (int64_t)s_pre[lo] && r0 + 16 <= (int64_t)s_size[lo]) {
-                // fast path: 16 body bytes of one record
-                const uint64_t sa = s_src[lo] + (uint64_t)(r0 - s_pre[lo]);
-                const uint32_t* w = (const uint32_t*)(sa & ~3ull);
-                const uint32_t sh = (uint32_t)(sa & 3) * 8;
-                uint32_t a[5];
+            const int r0 = d - rel[lo];
+            const int pr = pres[lo];
+            if (r0 >= pr && (int64_t)r0 + 16 <= (int64_t)sizes[lo]) {
+                const uint64_t sa = srcs[lo] + (uint64_t)(r0 - pr);
+                const uint32_t* wp = (const uint32_t*)(sa & ~3ull);
                 #pragma unroll
-                for (int q = 0; q < 4; q++) a[q] = w[q];
-                a[4] = sh ? w[4] : 0u;
-                #pragma unroll
-                for (int q = 0; q < 4; q++) wv[q] = __builtin_amdgcn_alignbit(a[q + 1], a[q], sh);
+                for (int q = 0; q < 4; q++) a[p][q] = wp[q];
+                a[p][4] = (sa & 3) ? wp[4] : 0u;
+                fast |= 1u << p;
+                shs |= (uint32_t)(sa & 3) << (2 * p);
             } else {
-                int jj = lo;
-                #pragma unroll 1
-                for (int q = 0; q < 16; q++) {
-                    const int64_t pos = d + q;
-                    while (jj + 1 < (int)cnt && s_rel[jj + 1] <= pos) jj++;
-                    uint32_t byte = 0;
-                    const int64_t r = pos - s_rel[jj];
-                    if (fo + (uint64_t)pos < L && r >= 0 && r < (int64_t)s_size[jj]) {
-                        MCopy c;
-                        c.src = s_src[jj]; c.pre = s_pre[jj];
-                        byte = src_byte(c, pre + (uint64_t)(j0 + jj) * M_PRE, (uint64_t)r);
-                    }
-                    if ((q & 3) == 0) wv[q >> 2] = 0;
-                    wv[q >> 2] |= byte << (8 * (q & 3));
-                }
+                gather |= 1u << p;
             }
-            *(uint4*)(out + B + d) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        }
+        #pragma unroll
+        for (int p = 0; p < MC_P; p++) {
+            if (!(fast & (1u << p))) continue;
+            const int d = (p * 64 + lane) * 16;
+            const uint32_t sh = ((shs >> (2 * p)) & 3) * 8;
+            uint32_t o[4];
+            #pragma unroll
+            for (int q = 0; q < 4; q++) o[q] = __builtin_amdgcn_alignbit(a[p][q + 1], a[p][q], sh);
+            *(uint4*)(out + B + d) = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        // gather pieces: byte q from its record (re-encoded prefix, body) or zero
+        // past the file end; the 16 loads of a piece are issued together
+        #pragma unroll 1
+        while (gather) {
+            const int p = __builtin_ctz(gather);
+            gather &= gather - 1;
+            const int d = (p * 64 + lane) * 16;
+            int jj = 0;
+            {
+                int lo = 0, hi = (int)cnt - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (rel[mid] <= d) lo = mid; else hi = mid - 1;
+                }
+                jj = lo;
+            }
+            const uint8_t* bp[16];
+            #pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const int pos = d + q;
+                while (jj + 1 < (int)cnt && rel[jj + 1] <= pos) jj++;
+                const int r = pos - rel[jj];
+                const uint8_t* ptr = &g_zero_byte;
+                if (fo + (uint64_t)pos < L && r >= 0 && (uint32_t)r < sizes[jj]) {
+                    const int pj = pres[jj];
+                    ptr = r < pj ? pre + (uint64_t)(j0 + jj) * M_PRE + r : (const uint8_t*)srcs[jj] + (r - pj);
+                }
+                bp[q] = ptr;
+            }
+            uint32_t v[4] = {0, 0, 0, 0};
+            #pragma unroll
+            for (int q = 0; q < 16; q++) v[q >> 2] |= (uint32_t)*bp[q] << (8 * (q & 3));
+            *(uint4*)(out + B + d) = make_uint4(v[0], v[1], v[2], v[3]);
         }
     }
 }
@@ -602,8 +682,9 @@ extern "C" int cly_merge_device(cly_ctx* ctx, const cly_file* files, int nfiles,
         k_mhint<<<(unsigned)lblk, M_NT, 0, st>>>(d_ent, d_cp, d_tuples, d_fb, d_fb + nfiles + 1, nfiles, d_hsz, d_bsum,
                                                   d_tot, stride, d_hint, hint_cap);
         MDBG(st, "k_mhint");
-        unsigned grid = nblocks < 65536 ? (unsigned)nblocks : 65536u;
-        k_mcopy<<<grid, M_NT, 0, st>>>(d_cp, d_pre, d_bmap, d_fstart, d_flen, d_tot, stride, nblocks, d_out);
+        const uint64_t wgs = (nblocks + MC_W - 1) / MC_W;
+        unsigned grid = wgs < 16384 ? (unsigned)wgs : 16384u;
+        k_mcopy<<<grid, 64 * MC_W, 0, st>>>(d_cp, d_pre, d_bmap, d_fstart, d_flen, d_tot, stride, nblocks, d_out);
         MDBG(st, "k_mcopy");
         MCK(hipGetLastError());
         if (out_file_len) MCK(hipMemcpyAsync(out_file_len, d_flen, sizeof(uint64_t) * h_tot.n_out,
