@@ -17,9 +17,9 @@ import numpy as np
 
 from . import _abi
 from ._abi import (END_EOF, END_TORN, END_ZERO, ERR_CRC, ERR_OFFSET, ERR_TRUNC5, ERR_VARINT,
-                   TUPLE_DTYPE)
+                   POS_DTYPE, TUPLE_DTYPE)
 
-__all__ = ["Scanner", "DataFile", "LogRecord", "LogPos", "ScanResult", "ScanError", "MergeResult",
+__all__ = ["POS_DTYPE", "Scanner", "DataFile", "LogRecord", "LogPos", "ScanResult", "ScanError", "MergeResult",
            "ErrInvalidCRC", "TUPLE_DTYPE", "STATUS_NAMES"]
 
 # data/logRecord.go:10-16 / :20-26
@@ -206,6 +206,28 @@ class Scanner:
             raise (ErrInvalidCRC if rc == ERR_CRC else ScanError)(rc, "cly_merge")
         outs = [out[k * stride:k * stride + int(lens[k])].tobytes() for k in range(int(r.n_out_files))]
         return MergeResult(outs, hint[:int(r.hint_bytes)].tobytes(), r)
+
+    def load_hint(self, hint_file):
+        """loadIndexFromHintFile (merge.go:257-287): scan the hint-index file and
+        decode each record's LogPos (DecodeLogRecordPos).  Returns (tuples,
+        positions[POS_DTYPE], status, end_offset); raises ScanError(ERR_VARINT)
+        where the reference's decode panics and ErrInvalidCRC on a corrupt record."""
+        arr = self._file_array([hint_file])
+        cap = int(self.lib.cly_scan_capacity(arr, 1)) + 16
+        out = np.zeros(cap, dtype=TUPLE_DTYPE)
+        pos = np.zeros(cap, dtype=POS_DTYPE)
+        n = ctypes.c_uint64()
+        res = _abi.ClyFileResult()
+        rc = self.lib.cly_hint_scan(self.ctx, arr, out.ctypes.data, pos.ctypes.data, cap, ctypes.byref(n),
+                                    ctypes.byref(res))
+        if rc != 0:
+            raise ScanError(rc, "cly_hint_scan (after %d records)" % n.value)
+        if res.status == ERR_CRC:
+            raise ErrInvalidCRC(res.status, "at offset %d" % res.end_offset)
+        if res.status < 0:
+            raise ScanError(res.status, "at offset %d" % res.end_offset)
+        k = int(n.value)
+        return out[:k], pos[:k], res.status, res.end_offset
 
     def merge_device(self, dev_files, d_tuples, file_first, results, d_live, data_file_size, d_out, out_max_files,
                      d_hint, hint_cap, stream=None):

@@ -49,6 +49,10 @@ class ClyMergeResult(ctypes.Structure):
                 ("merge_ms", ctypes.c_double)]
 
 
+# numpy view of cly_pos (16 bytes)
+POS_DTYPE = np.dtype([("offset", "<i8"), ("fid", "<u4"), ("_pad", "<u4")])
+
+
 # numpy view of cly_tuple (48 bytes)
 TUPLE_DTYPE = np.dtype([
     ("offset", "<i8"), ("expiration", "<i8"), ("tx_id", "<i8"),
@@ -63,7 +67,8 @@ GEN_DTYPE = np.dtype([("dst", "<u8"), ("key_index", "<u4"), ("value_len", "<u4")
 assert GEN_DTYPE.itemsize == 32
 
 SCAN_SYMBOLS = ["cly_ctx_create", "cly_ctx_destroy", "cly_scan_capacity", "cly_scan",
-                "cly_scan_device", "cly_merge_device", "cly_merge", "cly_strerror", "cly_build_info"]
+                "cly_scan_device", "cly_merge_device", "cly_merge", "cly_hint_positions_device", "cly_hint_scan",
+                "cly_strerror", "cly_build_info"]
 GEN_SYMBOLS = ["cly_gen_record_size", "cly_gen_layout", "cly_gen_encode"]
 
 _libs = {}
@@ -106,6 +111,12 @@ def load_scan_lib(name="libclyscan.so"):
                               ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, P(ctypes.c_uint64),
                               ctypes.c_void_p, ctypes.c_uint64, P(ClyMergeResult)]
     lib.cly_merge.restype = ctypes.c_int
+    lib.cly_hint_positions_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                              ctypes.c_void_p, P(ctypes.c_uint64), ctypes.c_void_p]
+    lib.cly_hint_positions_device.restype = ctypes.c_int
+    lib.cly_hint_scan.argtypes = [ctypes.c_void_p, P(ClyFile), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                  P(ctypes.c_uint64), P(ClyFileResult)]
+    lib.cly_hint_scan.restype = ctypes.c_int
     lib.cly_strerror.argtypes = [ctypes.c_int]
     lib.cly_strerror.restype = ctypes.c_char_p
     lib.cly_build_info.argtypes = []

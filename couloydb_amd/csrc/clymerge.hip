@@ -784,3 +784,94 @@ done:
     free(df); free(first); free(res);
     return rc;
 }
+
+// ---- hint-index load (loadIndexFromHintFile, merge.go:257-287) ---------------
+// DecodeLogRecordPos (data/logRecord.go:126-134) over the records of a scanned
+// hint file: Fid = uint32(Varint(value)), Offset = Varint(value[n:]).  A first
+// varint that overflows makes the reference panic (buf[index:] with index < 0):
+// the smallest such record index is reported.
+__global__ void __launch_bounds__(256)
+k_hintpos(const uint8_t* __restrict__ base, const cly_tuple* __restrict__ tup, uint64_t n, cly_pos* pos,
+          unsigned long long* first_bad) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const cly_tuple t = tup[i];
+        const uint8_t* v = base + t.offset + t.header_size + t.key_size;
+        int n1 = 0, n2 = 0;
+        const int64_t f = go_varint(v, (int64_t)t.value_size, n1);
+        cly_pos p;
+        p._pad = 0;
+        if (n1 < 0) {
+            atomicMin(first_bad, (unsigned long long)i);
+            p.fid = 0;
+            p.offset = 0;
+        } else {
+            p.fid = (uint32_t)f;
+            p.offset = go_varint(v + n1, (int64_t)t.value_size - n1, n2);
+        }
+        pos[i] = p;
+    }
+}
+
+extern "C" int cly_hint_positions_device(cly_ctx* ctx, const uint8_t* d_hint_file, const cly_tuple* d_tuples,
+                                         uint64_t n, cly_pos* d_pos, uint64_t* first_bad, void* stream_v) {
+    if (!ctx || (n && (!d_hint_file || !d_tuples || !d_pos))) return CLY_ERR_ARG;
+    if (first_bad) *first_bad = n;
+    if (!n) return CLY_OK;
+    if (hipSetDevice(cly_ctx_device_internal(ctx)) != hipSuccess) return CLY_ERR_DEVICE;
+    hipStream_t st = stream_v ? (hipStream_t)stream_v : cly_ctx_stream_internal(ctx);
+    int rc = CLY_OK;
+    unsigned long long* d_bad = nullptr;
+    unsigned long long h_bad = ~0ull;
+    const uint64_t blocks = (n + 255) / 256;
+    MCK(scratch(ctx, MS_TOT, sizeof(MTot), &d_bad));
+    MCK(hipMemcpyAsync(d_bad, &h_bad, sizeof(h_bad), hipMemcpyHostToDevice, st));
+    k_hintpos<<<(unsigned)(blocks < 65536 ? blocks : 65536), 256, 0, st>>>(d_hint_file, d_tuples, n, d_pos, d_bad);
+    MCK(hipGetLastError());
+    MCK(hipMemcpyAsync(&h_bad, d_bad, sizeof(h_bad), hipMemcpyDeviceToHost, st));
+    MCK(hipStreamSynchronize(st));
+    if (h_bad < n) {
+        if (first_bad) *first_bad = h_bad;
+        rc = CLY_ERR_VARINT;
+    }
+done:
+    return rc;
+}
+
+extern "C" int cly_hint_scan(cly_ctx* ctx, const cly_file* hint_file, cly_tuple* out, cly_pos* pos, uint64_t cap,
+                             uint64_t* n_out, cly_file_result* res) {
+    if (!ctx || !hint_file || !res || !n_out) return CLY_ERR_ARG;
+    *n_out = 0;
+    if (hipSetDevice(cly_ctx_device_internal(ctx)) != hipSuccess) return CLY_ERR_DEVICE;
+    hipStream_t st = cly_ctx_stream_internal(ctx);
+    int rc = CLY_OK;
+    uint8_t* d_bytes = nullptr;
+    cly_tuple* d_tup = nullptr;
+    cly_pos* d_pos = nullptr;
+    cly_file df = *hint_file;
+    uint64_t first = 0, need = 0, nrec = 0, bad = 0;
+    const uint64_t tcap = cly_scan_capacity(hint_file, 1) + 16;
+    MCK(hipMalloc((void**)&d_bytes, hint_file->len + 16));
+    if (hint_file->len) MCK(hipMemcpyAsync(d_bytes, hint_file->base, hint_file->len, hipMemcpyHostToDevice, st));
+    df.base = d_bytes;
+    MCK(hipMalloc((void**)&d_tup, sizeof(cly_tuple) * tcap));
+    rc = cly_scan_device(ctx, &df, 1, d_tup, tcap, &first, res, &need, nullptr, nullptr);
+    if (rc != CLY_OK) goto done;
+    nrec = res->n_records;
+    if (nrec) {
+        MCK(hipMalloc((void**)&d_pos, sizeof(cly_pos) * nrec));
+        rc = cly_hint_positions_device(ctx, d_bytes, d_tup + first, nrec, d_pos, &bad, nullptr);
+        if (rc == CLY_ERR_VARINT) nrec = bad;                  // the records before the panic
+        else if (rc != CLY_OK) goto done;
+    }
+    *n_out = nrec;
+    if (nrec > cap) { rc = CLY_ERR_CAPACITY; goto done; }
+    if (nrec) {
+        MCK(hipMemcpyAsync(out, d_tup + first, sizeof(cly_tuple) * nrec, hipMemcpyDeviceToHost, st));
+        MCK(hipMemcpyAsync(pos, d_pos, sizeof(cly_pos) * nrec, hipMemcpyDeviceToHost, st));
+        MCK(hipStreamSynchronize(st));
+    }
+done:
+    hipStreamSynchronize(st);
+    hipFree(d_bytes); hipFree(d_tup); hipFree(d_pos);
+    return rc;
+}

@@ -165,6 +165,29 @@ int cly_merge(cly_ctx* ctx, const cly_file* files, int nfiles,
               uint8_t* out, uint32_t out_max_files, uint64_t* out_file_len,
               uint8_t* hint, uint64_t hint_cap, cly_merge_result* mres);
 
+/* ---- hint-index load (db.loadIndexFromHintFile, merge.go:257-287) -------- */
+/* data.LogPos decoded from a hint record's value (DecodeLogRecordPos,
+ * data/logRecord.go:126-134).                                                   */
+typedef struct cly_pos {
+    int64_t  offset;          /* LogPos.Offset                                  */
+    uint32_t fid;             /* LogPos.Fid = uint32(first varint)              */
+    uint32_t _pad;
+} cly_pos;
+
+/* Device entry: d_pos[i] = DecodeLogRecordPos(value of d_tuples[i]) for the n
+ * tuples of a hint-file scan (cly_scan_device over d_hint_file).  Returns
+ * CLY_ERR_VARINT when a value's first varint overflows (the reference panics);
+ * *first_bad = the first such index (n if none).                              */
+int cly_hint_positions_device(cly_ctx* ctx, const uint8_t* d_hint_file, const cly_tuple* d_tuples,
+                              uint64_t n, cly_pos* d_pos, uint64_t* first_bad, void* stream);
+
+/* Host entry: scan a hint-index file (host memory) and decode every record's
+ * position: out[i] (Key = the realKey), pos[i].  *n_out = records returned
+ * (the loop's io.EOF end, or the records before a decode panic, with
+ * CLY_ERR_VARINT); res = the scan's per-file result (ErrInvalidCRC etc.).      */
+int cly_hint_scan(cly_ctx* ctx, const cly_file* hint_file, cly_tuple* out, cly_pos* pos, uint64_t cap,
+                  uint64_t* n_out, cly_file_result* res);
+
 const char* cly_strerror(int code);
 
 /* Library build identification (gfx target, kernel configuration).            */

@@ -186,6 +186,20 @@ uint64_t clyo_encode_record(uint8_t* out, uint8_t type, uint8_t dtype,
     return size;
 }
 
+/* DecodeLogRecordPos (data/logRecord.go:126-134): two Varints over the hint
+ * record's value; Fid = uint32(first).  A first varint that overflows moves
+ * the index negative and buf[index:] panics: CLYO_ERR_VARINT.  The second
+ * varint's n is ignored (overflow or short buffer give offset 0).            */
+int clyo_decode_pos(const uint8_t* buf, uint64_t len, uint32_t* fid, int64_t* offset) {
+    int n1, n2;
+    const int64_t f = clyo_varint(buf, (int64_t)len, &n1);
+    if (n1 < 0) return CLYO_ERR_VARINT;
+    const int64_t o = clyo_varint(buf + n1, (int64_t)len - n1, &n2);
+    *fid = (uint32_t)f;
+    *offset = o;
+    return 0;
+}
+
 /* ------------------------------------------------------------------------ */
 /* db.merge rewrite loop (merge.go:90-143) over the tuples of a scan, for the
  * records the caller's index marks live (merge.go:104-132: index pos ==

@@ -63,6 +63,10 @@ uint64_t clyo_encode_record(uint8_t* out, uint8_t type, uint8_t dtype,
                             const uint8_t* key, uint64_t klen,
                             const uint8_t* val, uint64_t vlen, int64_t expiration);
 
+/* DecodeLogRecordPos (data/logRecord.go:126-134): 0, or CLYO_ERR_VARINT where
+ * the reference panics. */
+int clyo_decode_pos(const uint8_t* buf, uint64_t len, uint32_t* fid, int64_t* offset);
+
 /* db.merge rewrite loop (merge.go:90-143): live tuples re-encoded with a
  * NO_TX_ID key into merge data files (appendLogRecord rotation, db.go:376-385)
  * plus the hint-index records.  tuple_file[i] indexes bases.  Returns 0,

@@ -60,6 +60,8 @@ def lib():
                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                                  ctypes.c_uint64, ctypes.c_void_p]
         L.clyo_merge.restype = ctypes.c_int
+        L.clyo_decode_pos.argtypes = [ctypes.c_void_p, ctypes.c_uint64, P(ctypes.c_uint32), P(ctypes.c_int64)]
+        L.clyo_decode_pos.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -142,3 +144,26 @@ def merge(arrays, tuples, tuple_file, live, data_file_size):
     files = [out[k * data_file_size:k * data_file_size + int(out_len[k])].tobytes() for k in range(r.n_out_files)] \
         if rc == 0 else []
     return rc, files, hint[:r.hint_bytes].tobytes() if rc == 0 else b"", r
+
+
+def decode_pos(value):
+    """DecodeLogRecordPos -> (rc, fid, offset)."""
+    a, p = _ptr(bytes(value) if value else b"\0")
+    f = ctypes.c_uint32()
+    o = ctypes.c_int64()
+    rc = lib().clyo_decode_pos(p, len(value), ctypes.byref(f), ctypes.byref(o))
+    return rc, f.value, o.value
+
+
+def hint_positions(data, tuples):
+    """loadIndexFromHintFile's per-record step (merge.go:272-284) over scanned
+    hint tuples -> (rc, fids uint32[], offsets int64[])."""
+    fids = np.zeros(len(tuples), np.uint32)
+    offs = np.zeros(len(tuples), np.int64)
+    for i, t in enumerate(tuples):
+        o = int(t["offset"]) + int(t["header_size"]) + int(t["key_size"])
+        rc, f, off = decode_pos(bytes(data[o:o + int(t["value_size"])]))
+        if rc:
+            return rc, fids[:i], offs[:i]
+        fids[i], offs[i] = f, off
+    return 0, fids, offs

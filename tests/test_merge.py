@@ -233,3 +233,76 @@ def test_gpu_merge_device_c4_shape():
         o = wl.d_merge[k * bench.DATA_FILE_SIZE:k * bench.DATA_FILE_SIZE + lens[k]].cpu().numpy().tobytes()
         assert o == outs[k], k
     assert wl.d_hint[:m.hint_bytes].cpu().numpy().tobytes() == hint
+
+
+# ------------------------------------------------ hint-index load (§8f row 2) --
+def py_decode_pos(v):
+    """DecodeLogRecordPos restated (data/logRecord.go:126-134)."""
+    f, n = mg.varint(v)
+    if n < 0:
+        return None
+    o, _ = mg.varint(v[n:])
+    return f & 0xFFFFFFFF, o
+
+
+POS_EDGE = [b"", bytes([0]), bytes([2, 0x80, 1]), bytes([3]), bytes([0xff] * 11), bytes([0x80] * 3),
+            bytes([4]) + bytes([0xff] * 11), bytes([0xfe, 0xff, 0xff, 0xff, 0x1f, 0x88, 0x04])]
+
+
+def test_oracle_decode_pos_edges():
+    for v in POS_EDGE:
+        rc, f, o = co.decode_pos(v)
+        want = py_decode_pos(v)
+        assert (rc == -3) == (want is None), v.hex()
+        if want is not None:
+            assert (f, o) == want, v.hex()
+
+
+def test_oracle_hint_of_merge_roundtrip():
+    b = merge_corpus(3, n_keys=400)
+    arrays, tts, _ = oracle_scan(split_files(b, 2, random.Random(3)))
+    live = string_live_mask(arrays, tts)
+    tuples, tf = flat(tts)
+    rc, outs, hint, r = co.merge(arrays, tuples, tf, live, 4096)
+    assert rc == 0
+    ht, st, end = co.scan_file(np.frombuffer(hint, np.uint8), 0)
+    assert st == 0 and end == len(hint) and len(ht) == r.n_live
+    rc, fids, offs = co.hint_positions(np.frombuffer(hint, np.uint8), ht)
+    assert rc == 0
+    for t, f, o in zip(ht, fids, offs):
+        # every position points at a merged record whose realKey is the hint key
+        hk = hint[int(t["offset"]) + int(t["header_size"]):][:int(t["key_size"])]
+        m = np.frombuffer(outs[f], np.uint8)
+        rec, _, _ = co.scan_file(m[o:], 0)
+        k0 = int(rec[0]["header_size"])
+        assert outs[f][o + k0:o + k0 + int(rec[0]["key_size"])] == b"\x00" + hk
+
+
+def hint_file_with(values):
+    return b"".join(mg.encode_record(mg.test_key(i), v) for i, v in enumerate(values))
+
+
+@pytest.mark.gpu
+def test_gpu_hint_scan(scanner):
+    from couloydb_amd import DataFile, ScanError
+    b = merge_corpus(5, n_keys=3000)
+    arrays, tts, _ = oracle_scan(split_files(b, 3, random.Random(5)))
+    live = string_live_mask(arrays, tts)
+    tuples, tf = flat(tts)
+    rc, outs, hint, r = co.merge(arrays, tuples, tf, live, 1 << 16)
+    files = [np.frombuffer(hint, np.uint8).copy(), np.frombuffer(hint_file_with(POS_EDGE[:4] + POS_EDGE[5:6]), np.uint8).copy()]
+    with open(os.path.join(GOLD, "hint_index.cly"), "rb") as f:
+        files.append(np.frombuffer(f.read(), np.uint8).copy())
+    for h in files:
+        t, st, end = co.scan_file(h, 0)
+        rc, fids, offs = co.hint_positions(h, t)
+        assert rc == 0
+        gt, gp, gst, gend = scanner.load_hint(DataFile(h, 0))
+        assert (gst, gend) == (st, end) and len(gt) == len(t)
+        assert (gt.view(np.uint8) == t.view(np.uint8)).all()
+        assert (gp["fid"] == fids).all() and (gp["offset"] == offs).all()
+    # a value whose first varint overflows: the reference panics at that record
+    bad = np.frombuffer(hint_file_with([bytes([2, 4]), bytes([6, 8]), bytes([0xff] * 11), bytes([2, 2])]), np.uint8).copy()
+    with pytest.raises(ScanError) as ei:
+        scanner.load_hint(DataFile(bad, 0))
+    assert ei.value.code == -3 and "after 2 records" in str(ei.value)
