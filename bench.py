@@ -358,6 +358,12 @@ def main():
                                    and so == res[0].status and eo == res[0].end_offset)
     if rank == 0 and world == 1 and not args.no_host_path:
         out["host_path"] = host_path(wl, sc)
+        hp = out["host_path"].get("pageable", {})
+        if hp and len(wl.dev_files) <= 16:
+            # the whole configuration went through the host entry: the record source
+            # of db.loadIndex (db.go:582-637) from mmap'd files to index tuples in host
+            # memory; the Go index inserts that consume the tuples stay Go's
+            out["index_load_wall_ms"] = hp["ms"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(wl)
     if rank == 0:
