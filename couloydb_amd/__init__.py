@@ -229,6 +229,35 @@ class Scanner:
         k = int(n.value)
         return out[:k], pos[:k], res.status, res.end_offset
 
+    def index(self, files):
+        """db.loadIndex's rebuild of the String/ListMeta indexes (db.go:511-637)
+        on the device, host buffers in (cly_index).  Returns (state per record in
+        scan order: IX_DEAD / IX_LIVE / IX_HOST, ClyIndexResult)."""
+        files = list(files)
+        arr = self._file_array(files)
+        cap = int(self.lib.cly_scan_capacity(arr, len(files))) + 16
+        state = np.zeros(cap, np.uint8)
+        n = ctypes.c_uint64()
+        r = _abi.ClyIndexResult()
+        rc = self.lib.cly_index(self.ctx, arr, len(files), state.ctypes.data, cap, ctypes.byref(n), ctypes.byref(r))
+        if rc != 0:
+            raise (ErrInvalidCRC if rc == ERR_CRC else ScanError)(rc, "cly_index")
+        return state[:int(n.value)], r
+
+    def index_device(self, dev_files, d_tuples, file_first, results, d_state, stream=None):
+        """Device-resident index rebuild over a scan_device result -> ClyIndexResult."""
+        n = len(dev_files)
+        arr = (_abi.ClyFile * max(1, n))()
+        for i, (ptr, ln, fid) in enumerate(dev_files):
+            arr[i].base, arr[i].len, arr[i].fid = ptr, ln, fid
+        first = (ctypes.c_uint64 * max(1, n))(*file_first)
+        res = (_abi.ClyFileResult * max(1, n))(*results)
+        r = _abi.ClyIndexResult()
+        rc = self.lib.cly_index_device(self.ctx, arr, n, d_tuples, first, res, d_state, ctypes.byref(r), stream)
+        if rc != 0:
+            raise (ErrInvalidCRC if rc == ERR_CRC else ScanError)(rc, "cly_index_device")
+        return r
+
     def merge_device(self, dev_files, d_tuples, file_first, results, d_live, data_file_size, d_out, out_max_files,
                      d_hint, hint_cap, stream=None):
         """Device-resident merge (cly_merge_device) over a scan_device result.

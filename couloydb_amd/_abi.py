@@ -42,6 +42,14 @@ class ClyGenRec(ctypes.Structure):
                 ("_pad2", ctypes.c_int32)]
 
 
+class ClyIndexResult(ctypes.Structure):
+    _fields_ = [("n_live", ctypes.c_uint64), ("n_applied", ctypes.c_uint64), ("n_host", ctypes.c_uint64),
+                ("n_collisions", ctypes.c_uint64), ("index_ms", ctypes.c_double)]
+
+
+IX_DEAD, IX_LIVE, IX_HOST = 0, 1, 2
+
+
 class ClyMergeResult(ctypes.Structure):
     _fields_ = [("n_live", ctypes.c_uint64), ("n_reencoded", ctypes.c_uint64),
                 ("hint_bytes", ctypes.c_uint64), ("out_stride", ctypes.c_uint64),
@@ -68,6 +76,7 @@ assert GEN_DTYPE.itemsize == 32
 
 SCAN_SYMBOLS = ["cly_ctx_create", "cly_ctx_destroy", "cly_scan_capacity", "cly_scan",
                 "cly_scan_device", "cly_merge_device", "cly_merge", "cly_hint_positions_device", "cly_hint_scan",
+                "cly_index_device", "cly_index",
                 "cly_strerror", "cly_build_info"]
 GEN_SYMBOLS = ["cly_gen_record_size", "cly_gen_layout", "cly_gen_encode"]
 
@@ -117,6 +126,12 @@ def load_scan_lib(name="libclyscan.so"):
     lib.cly_hint_scan.argtypes = [ctypes.c_void_p, P(ClyFile), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                   P(ctypes.c_uint64), P(ClyFileResult)]
     lib.cly_hint_scan.restype = ctypes.c_int
+    lib.cly_index_device.argtypes = [ctypes.c_void_p, P(ClyFile), ctypes.c_int, ctypes.c_void_p, P(ctypes.c_uint64),
+                                     P(ClyFileResult), ctypes.c_void_p, P(ClyIndexResult), ctypes.c_void_p]
+    lib.cly_index_device.restype = ctypes.c_int
+    lib.cly_index.argtypes = [ctypes.c_void_p, P(ClyFile), ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                              P(ctypes.c_uint64), P(ClyIndexResult)]
+    lib.cly_index.restype = ctypes.c_int
     lib.cly_strerror.argtypes = [ctypes.c_int]
     lib.cly_strerror.restype = ctypes.c_char_p
     lib.cly_build_info.argtypes = []

@@ -1,0 +1,460 @@
+// clyindex.hip — db.loadIndex's index rebuild on the device (gfx950), part of
+// libclyscan.so (C-ABI: cly_index_device in include/clyscan.h).
+//
+// Reference (db.go:511-637): every record of the scan, in fid/offset order,
+// goes through parseLogRecordKey (db.go:706-710); a record without a txId is
+// applied to the index at once (updateIndex, db.go:511-575); a record with a
+// txId is buffered until a TxnCommit marker of that txId applies the buffer in
+// order (a TxnRollback marker drops it, TxnBegin is ignored).  For the String
+// and ListMeta indexes the key is realKey itself: the last applied record of a
+// key decides, Put -> index[key] = (fid, offset), Deleted -> key absent.
+// Hash/List/Set keys are composite (decodeFieldKey, decodeListKey with
+// big.Float gob encodings, hashMemberKey's consistent hash): their records are
+// left to the host (state CLY_IX_HOST).
+//
+// Device pipeline:
+//   k_ixclass   per record: class (applied now / tx data / tx marker / host / none)
+//   select + radix sort of the tx records by txId (stable: scan order kept)
+//   k_ixtx      per tx record: its next marker in the same txId (segmented
+//               suffix scan), a committed data record is applied at its marker
+//   select + radix sort of the applied records by a 64-bit key hash
+//   segmented arg-max of the application order per hash group: the winner of
+//   each key; adjacent records of a group with different keys (a hash
+//   collision) send the group to an exact one-thread resolution
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "scan_core.h"
+
+extern "C" hipStream_t cly_ctx_stream_internal(cly_ctx* c);
+extern "C" int cly_ctx_device_internal(cly_ctx* c);
+
+#define IX_NONE 0xFFFFFFFFFFFFFFFFull
+enum { K_NONE = 0, K_APPLY = 1, K_TXDATA = 2, K_COMMIT = 3, K_ROLLBACK = 4, K_HOST = 5, K_HOSTTX = 6 };
+
+__device__ __forceinline__ int ix_file(const uint64_t* first, int nfiles, uint64_t i) {
+    int lo = 0, hi = nfiles - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (first[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+// realKey of tuple t (parseLogRecordKey: key[n:], n = 0 for a short varint)
+__device__ __forceinline__ const uint8_t* ix_rkey(const uint64_t* bases, int f, const cly_tuple& t, uint32_t& len) {
+    len = t.key_size - t.txid_len;
+    return (const uint8_t*)bases[f] + t.offset + t.header_size + t.txid_len;
+}
+// 64-bit hash of (index, realKey): FNV-1a over 8-byte words folded by a mix
+__device__ __forceinline__ uint64_t ix_hash(uint32_t index_kind, const uint8_t* k, uint32_t len) {
+    uint64_t h = 0xcbf29ce484222325ull ^ ((uint64_t)index_kind << 56) ^ len;
+    uint32_t q = 0;
+    for (; q + 8 <= len; q += 8) {
+        uint64_t w = 0;
+        #pragma unroll
+        for (int b = 0; b < 8; b++) w |= (uint64_t)k[q + b] << (8 * b);
+        h = (h ^ w) * 0x100000001b3ull;
+        h ^= h >> 29;
+    }
+    uint64_t w = 0;
+    for (int b = 0; q < len; q++, b++) w |= (uint64_t)k[q] << (8 * b);
+    h = (h ^ w) * 0x100000001b3ull;
+    h ^= h >> 32;
+    h *= 0xd6e8feb86659fd93ull;
+    h ^= h >> 32;
+    return h;
+}
+
+struct IxTot { unsigned long long n_live, n_applied, n_host, n_coll; uint32_t bad, _pad; };
+
+// class of each record; the index kind of an applied record: String 0, ListMeta 3
+__global__ void __launch_bounds__(256)
+k_ixclass(const cly_tuple* __restrict__ tup, uint64_t n, uint8_t* cls, uint8_t* state, uint64_t* txkey,
+          IxTot* tot) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const cly_tuple t = tup[i];
+        uint8_t c = K_NONE, s = CLY_IX_DEAD;
+        if (t.txid_len == 0xFF) atomicOr(&tot->bad, 1u);          // parseLogRecordKey panics
+        const bool idx = t.data_type == 0 || t.data_type == 3;     // String, ListMeta
+        const bool host = t.data_type == 1 || t.data_type == 2 || t.data_type == 4;
+        if (t.tx_id == 0) {                                        // updateIndex at once
+            if (idx) c = K_APPLY;
+            else if (host) { c = K_HOST; s = CLY_IX_HOST; }
+        } else if (t.type == 2) c = K_COMMIT;                      // LogRecordTxnCommit
+        else if (t.type == 3) c = K_ROLLBACK;                      // LogRecordTxnRollback
+        else if (t.type != 4) c = idx ? K_TXDATA : (host ? K_HOSTTX : K_NONE);   // buffered (Begin ignored)
+        cls[i] = c;
+        state[i] = s;
+        txkey[i] = (uint64_t)t.tx_id;
+    }
+}
+
+// per tx record (sorted by txId, scan order within): element of the segmented
+// suffix scan = (txId, position of the nearest marker at or after it)
+struct TxNext { uint64_t tx; uint64_t mpos; };
+struct TxNextOp {
+    __device__ __forceinline__ TxNext operator()(const TxNext& a, const TxNext& b) const {
+        // a precedes b in scan order (the scan runs backwards over the sorted records)
+        if (b.tx != a.tx) return b;
+        return TxNext{b.tx, b.mpos != IX_NONE ? b.mpos : a.mpos};
+    }
+};
+__global__ void __launch_bounds__(256)
+k_ixtxin(const uint64_t* __restrict__ stx, const uint32_t* __restrict__ sidx, const uint8_t* __restrict__ cls,
+         uint64_t m, TxNext* rev) {
+    for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < m; p += (uint64_t)gridDim.x * 256) {
+        const uint32_t i = sidx[p];
+        const uint8_t c = cls[i];
+        rev[m - 1 - p] = TxNext{stx[p], (c == K_COMMIT || c == K_ROLLBACK) ? p : IX_NONE};
+    }
+}
+// committed tx data records get their application order (marker position, own position)
+__global__ void __launch_bounds__(256)
+k_ixtx(const uint32_t* __restrict__ sidx, const uint8_t* __restrict__ cls, uint64_t m, const TxNext* __restrict__ nxt,
+       uint64_t* order, uint8_t* state) {
+    for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < m; p += (uint64_t)gridDim.x * 256) {
+        const uint32_t i = sidx[p];
+        const uint8_t c = cls[i];
+        if (c != K_TXDATA && c != K_HOSTTX) continue;
+        const uint64_t mp = nxt[m - 1 - p].mpos;
+        const bool committed = mp != IX_NONE && cls[sidx[mp]] == K_COMMIT;
+        if (c == K_HOSTTX) { if (committed) state[i] = CLY_IX_HOST; continue; }
+        if (committed) order[i] = ((uint64_t)sidx[mp] << 32) | i;
+    }
+}
+// applied records (now and at commit): order, hash
+__global__ void __launch_bounds__(256)
+k_ixapply(const cly_tuple* __restrict__ tup, uint64_t n, const uint8_t* __restrict__ cls, uint64_t* order,
+          const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases, int nfiles, uint64_t* hash,
+          uint8_t* flag, uint64_t hash_mask) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint8_t c = cls[i];
+        if (c == K_APPLY) order[i] = (i << 32) | i;
+        const uint64_t o = order[i];
+        const bool ap = (c == K_APPLY || c == K_TXDATA) && o != IX_NONE;
+        flag[i] = ap;
+        if (ap) {
+            const cly_tuple t = tup[i];
+            uint32_t len;
+            const uint8_t* k = ix_rkey(bases, ix_file(first, nfiles, i), t, len);
+            hash[i] = ix_hash(t.data_type, k, len) & hash_mask;
+        }
+    }
+}
+// arg-max of the order per hash group (segmented, forward)
+struct GMax { uint64_t h; uint64_t order; uint32_t idx; uint32_t head; };
+struct GMaxOp {
+    __device__ __forceinline__ GMax operator()(const GMax& a, const GMax& b) const {
+        if (b.h != a.h) return b;
+        return b.order > a.order ? b : GMax{b.h, a.order, a.idx, a.head};
+    }
+};
+__global__ void __launch_bounds__(256)
+k_ixgin(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, const uint64_t* __restrict__ order,
+        uint64_t m, GMax* g) {
+    for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < m; q += (uint64_t)gridDim.x * 256) {
+        const uint32_t i = sidx[q];
+        g[q] = GMax{sh[q], order[i], i, (uint32_t)q};
+    }
+}
+__device__ __forceinline__ bool ix_same_key(const cly_tuple* tup, const uint64_t* first, const uint64_t* bases,
+                                            int nfiles, uint32_t a, uint32_t b) {
+    const cly_tuple ta = tup[a], tb = tup[b];
+    if (ta.data_type != tb.data_type) return false;
+    uint32_t la, lb;
+    const uint8_t* ka = ix_rkey(bases, ix_file(first, nfiles, a), ta, la);
+    const uint8_t* kb = ix_rkey(bases, ix_file(first, nfiles, b), tb, lb);
+    if (la != lb) return false;
+    for (uint32_t q = 0; q < la; q++) if (ka[q] != kb[q]) return false;
+    return true;
+}
+// group ends: the winner (max order) decides the key; adjacent different keys
+// inside a group mark a hash collision (resolved exactly by k_ixcoll)
+__global__ void __launch_bounds__(256)
+k_ixwin(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, const GMax* __restrict__ g, uint64_t m,
+        const cly_tuple* __restrict__ tup, const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases,
+        int nfiles, uint8_t* state, uint8_t* coll, IxTot* tot) {
+    for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < m; q += (uint64_t)gridDim.x * 256) {
+        if (q > 0 && sh[q] == sh[q - 1] && !ix_same_key(tup, first, bases, nfiles, sidx[q], sidx[q - 1])) {
+            uint64_t h0 = q;
+            while (h0 > 0 && sh[h0 - 1] == sh[q]) h0--;
+            coll[h0] = 1;
+            atomicAdd(&tot->n_coll, 1ull);
+        }
+        if (q + 1 < m && sh[q + 1] == sh[q]) continue;         // not the group's last
+        const GMax w = g[q];
+        if (tup[w.idx].type != 1) state[w.idx] = CLY_IX_LIVE;   // LogRecordDeleted -> key absent
+    }
+}
+// exact resolution of a collided hash group (one thread): per distinct key the max order
+__global__ void __launch_bounds__(64)
+k_ixcoll(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, const uint64_t* __restrict__ order,
+         uint64_t m, const uint8_t* __restrict__ coll, const cly_tuple* __restrict__ tup,
+         const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases, int nfiles, uint8_t* state) {
+    const uint64_t q0 = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    if (q0 >= m || !coll[q0]) return;
+    uint64_t q1 = q0 + 1;
+    while (q1 < m && sh[q1] == sh[q0]) q1++;
+    for (uint64_t a = q0; a < q1; a++) state[sidx[a]] = CLY_IX_DEAD;
+    for (uint64_t a = q0; a < q1; a++) {
+        bool best = true;
+        for (uint64_t b = q0; b < q1 && best; b++)
+            if (b != a && order[sidx[b]] > order[sidx[a]] &&
+                ix_same_key(tup, first, bases, nfiles, sidx[a], sidx[b])) best = false;
+        if (best && tup[sidx[a]].type != 1) state[sidx[a]] = CLY_IX_LIVE;
+    }
+}
+__global__ void __launch_bounds__(256)
+k_ixcount(const uint8_t* __restrict__ state, const uint8_t* __restrict__ flag, uint64_t n, IxTot* tot) {
+    unsigned long long live = 0, host = 0, ap = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        live += state[i] == CLY_IX_LIVE;
+        host += state[i] == CLY_IX_HOST;
+        ap += flag[i];
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        live += __shfl_xor(live, d, 64);
+        host += __shfl_xor(host, d, 64);
+        ap += __shfl_xor(ap, d, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (live) atomicAdd(&tot->n_live, live);
+        if (host) atomicAdd(&tot->n_host, host);
+        if (ap) atomicAdd(&tot->n_applied, ap);
+    }
+}
+
+__global__ void __launch_bounds__(256)
+k_ixtxflag(const uint8_t* __restrict__ cls, uint64_t n, uint8_t* flag) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint8_t k = cls[i];
+        flag[i] = k == K_TXDATA || k == K_COMMIT || k == K_ROLLBACK || k == K_HOSTTX;
+    }
+}
+__global__ void __launch_bounds__(256)
+k_ixgather(const uint64_t* __restrict__ src, const uint32_t* __restrict__ sel, uint64_t m, uint64_t* dst) {
+    for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < m; p += (uint64_t)gridDim.x * 256)
+        dst[p] = src[sel[p]];
+}
+
+// ---------------------------------------------------------------------------
+#define ICK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+    fprintf(stderr, "clyindex: %s failed: %s\n", #x, hipGetErrorString(e_)); rc = CLY_ERR_DEVICE; goto done; } } while (0)
+
+static unsigned ix_grid(uint64_t n) { const uint64_t b = (n + 255) / 256; return (unsigned)(b < 16384 ? (b ? b : 1) : 16384); }
+
+extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles, const cly_tuple* d_tuples,
+                                const uint64_t* file_first, const cly_file_result* res, uint8_t* d_state,
+                                cly_index_result* ir, void* stream_v) {
+    if (!ctx || !ir || nfiles < 0 || (nfiles && (!files || !file_first || !res))) return CLY_ERR_ARG;
+    memset(ir, 0, sizeof(*ir));
+    uint64_t n = 0;
+    for (int i = 0; i < nfiles; i++) {
+        if (res[i].status < 0) return res[i].status;           // loadIndex returns the scan's error
+        if (file_first[i] != n) return CLY_ERR_ARG;
+        n += res[i].n_records;
+    }
+    if (n == 0) return CLY_OK;
+    if (n >= (1ull << 31) || !d_state) return CLY_ERR_ARG;
+    if (hipSetDevice(cly_ctx_device_internal(ctx)) != hipSuccess) return CLY_ERR_DEVICE;
+    hipStream_t st = stream_v ? (hipStream_t)stream_v : cly_ctx_stream_internal(ctx);
+    int rc = CLY_OK;
+    uint64_t* h_fb = (uint64_t*)malloc(sizeof(uint64_t) * (2 * (size_t)nfiles + 2));
+    for (int i = 0; i < nfiles; i++) { h_fb[i] = file_first[i]; h_fb[nfiles + 1 + i] = (uint64_t)files[i].base; }
+    h_fb[nfiles] = n;
+    uint64_t *d_fb = nullptr, *d_txkey = nullptr, *d_k2 = nullptr, *d_order = nullptr, *d_hash = nullptr;
+    uint32_t *d_sel = nullptr, *d_sidx = nullptr;
+    uint8_t *d_cls = nullptr, *d_flag = nullptr, *d_coll = nullptr;
+    TxNext *d_rev = nullptr, *d_nxt = nullptr;
+    GMax *d_g = nullptr, *d_g2 = nullptr;
+    IxTot* d_tot = nullptr;
+    IxTot h_tot;
+    unsigned long long* d_nsel = nullptr;
+    unsigned long long h_nsel = 0;
+    void* d_tmp = nullptr;
+    size_t tmp_bytes = 0, need = 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const unsigned grid = ix_grid(n);
+    hipcub::CountingInputIterator<uint32_t> cnt(0);
+    uint64_t m = 0, m2 = 0;
+    const uint64_t* d_first = nullptr;
+    const uint64_t* d_bases = nullptr;
+    ICK(hipEventCreate(&e0));
+    ICK(hipEventCreate(&e1));
+    ICK(hipMalloc((void**)&d_fb, sizeof(uint64_t) * (2 * (size_t)nfiles + 2)));
+    d_first = d_fb;
+    d_bases = d_fb + nfiles + 1;
+    ICK(hipMalloc((void**)&d_tot, sizeof(IxTot)));
+    ICK(hipMalloc((void**)&d_nsel, sizeof(unsigned long long)));
+    ICK(hipMalloc((void**)&d_cls, n));
+    ICK(hipMalloc((void**)&d_flag, n));
+    ICK(hipMalloc((void**)&d_coll, n));
+    ICK(hipMalloc((void**)&d_txkey, sizeof(uint64_t) * n));
+    ICK(hipMalloc((void**)&d_k2, sizeof(uint64_t) * n));
+    ICK(hipMalloc((void**)&d_order, sizeof(uint64_t) * n));
+    ICK(hipMalloc((void**)&d_hash, sizeof(uint64_t) * n));
+    ICK(hipMalloc((void**)&d_sel, sizeof(uint32_t) * n));
+    ICK(hipMalloc((void**)&d_sidx, sizeof(uint32_t) * n));
+    ICK(hipMalloc((void**)&d_rev, sizeof(TxNext) * n));
+    ICK(hipMalloc((void**)&d_nxt, sizeof(TxNext) * n));
+    ICK(hipMalloc((void**)&d_g, sizeof(GMax) * n));
+    ICK(hipMalloc((void**)&d_g2, sizeof(GMax) * n));
+    // temp storage: the largest of the select / sort / scan needs
+    ICK(hipcub::DeviceSelect::Flagged(nullptr, need, cnt, d_flag, d_sel, d_nsel, (int)n, st));
+    tmp_bytes = need;
+    ICK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, d_k2, d_txkey, d_sel, d_sidx, (int)n, 0, 64, st));
+    if (need > tmp_bytes) tmp_bytes = need;
+    ICK(hipcub::DeviceScan::InclusiveScan(nullptr, need, d_rev, d_nxt, TxNextOp(), (int)n, st));
+    if (need > tmp_bytes) tmp_bytes = need;
+    ICK(hipcub::DeviceScan::InclusiveScan(nullptr, need, d_g, d_g2, GMaxOp(), (int)n, st));
+    if (need > tmp_bytes) tmp_bytes = need;
+    ICK(hipMalloc(&d_tmp, tmp_bytes));
+    ICK(hipMemcpyAsync(d_fb, h_fb, sizeof(uint64_t) * (2 * (size_t)nfiles + 1), hipMemcpyHostToDevice, st));
+    ICK(hipMemsetAsync(d_tot, 0, sizeof(IxTot), st));
+    ICK(hipMemsetAsync(d_order, 0xff, sizeof(uint64_t) * n, st));
+    ICK(hipMemsetAsync(d_coll, 0, n, st));
+    ICK(hipEventRecord(e0, st));
+    k_ixclass<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_state, d_txkey, d_tot);
+    // ---- transactions: tx records sorted by txId (stable: scan order within a txId)
+    k_ixtxflag<<<grid, 256, 0, st>>>(d_cls, n, d_flag);
+    {
+        size_t tb = tmp_bytes;
+        ICK(hipcub::DeviceSelect::Flagged(d_tmp, tb, cnt, d_flag, d_sel, d_nsel, (int)n, st));
+    }
+    ICK(hipMemcpyAsync(&h_nsel, d_nsel, sizeof(h_nsel), hipMemcpyDeviceToHost, st));
+    ICK(hipStreamSynchronize(st));
+    m = h_nsel;
+    if (m) {
+        k_ixgather<<<ix_grid(m), 256, 0, st>>>(d_txkey, d_sel, m, d_k2);
+        {
+            size_t tb = tmp_bytes;
+            ICK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_k2, d_hash, d_sel, d_sidx, (int)m, 0, 64, st));
+        }
+        k_ixtxin<<<ix_grid(m), 256, 0, st>>>(d_hash, d_sidx, d_cls, m, d_rev);
+        {
+            size_t tb = tmp_bytes;
+            ICK(hipcub::DeviceScan::InclusiveScan(d_tmp, tb, d_rev, d_nxt, TxNextOp(), (int)m, st));
+        }
+        k_ixtx<<<ix_grid(m), 256, 0, st>>>(d_sidx, d_cls, m, d_nxt, d_order, d_state);
+    }
+    // ---- applied records: hash, sort, winner per key
+    {
+        // test hook: CLY_IX_HASH_MASK (hex) narrows the key hash so that collisions
+        // (resolved exactly by k_ixcoll) become common
+        uint64_t hm = ~0ull;
+        const char* e = getenv("CLY_IX_HASH_MASK");
+        if (e && *e) hm = strtoull(e, nullptr, 16);
+        k_ixapply<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_order, d_first, d_bases, nfiles, d_hash, d_flag, hm);
+    }
+    {
+        size_t tb = tmp_bytes;
+        ICK(hipcub::DeviceSelect::Flagged(d_tmp, tb, cnt, d_flag, d_sel, d_nsel, (int)n, st));
+    }
+    ICK(hipMemcpyAsync(&h_nsel, d_nsel, sizeof(h_nsel), hipMemcpyDeviceToHost, st));
+    ICK(hipStreamSynchronize(st));
+    m2 = h_nsel;
+    if (m2) {
+        k_ixgather<<<ix_grid(m2), 256, 0, st>>>(d_hash, d_sel, m2, d_k2);
+        {
+            size_t tb = tmp_bytes;
+            ICK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_k2, d_txkey, d_sel, d_sidx, (int)m2, 0, 64, st));
+        }
+        k_ixgin<<<ix_grid(m2), 256, 0, st>>>(d_txkey, d_sidx, d_order, m2, d_g);
+        {
+            size_t tb = tmp_bytes;
+            ICK(hipcub::DeviceScan::InclusiveScan(d_tmp, tb, d_g, d_g2, GMaxOp(), (int)m2, st));
+        }
+        k_ixwin<<<ix_grid(m2), 256, 0, st>>>(d_txkey, d_sidx, d_g2, m2, d_tuples, d_first, d_bases, nfiles, d_state,
+                                             d_coll, d_tot);
+        ICK(hipMemcpyAsync(&h_tot, d_tot, sizeof(IxTot), hipMemcpyDeviceToHost, st));
+        ICK(hipStreamSynchronize(st));
+        if (h_tot.n_coll)
+            k_ixcoll<<<(unsigned)((m2 + 63) / 64), 64, 0, st>>>(d_txkey, d_sidx, d_order, m2, d_coll, d_tuples, d_first,
+                                                                d_bases, nfiles, d_state);
+    }
+    k_ixcount<<<grid, 256, 0, st>>>(d_state, d_flag, n, d_tot);
+    ICK(hipGetLastError());
+    ICK(hipEventRecord(e1, st));
+    ICK(hipMemcpyAsync(&h_tot, d_tot, sizeof(IxTot), hipMemcpyDeviceToHost, st));
+    ICK(hipStreamSynchronize(st));
+    if (h_tot.bad) { rc = CLY_ERR_VARINT; goto done; }
+    ir->n_live = h_tot.n_live;
+    ir->n_applied = h_tot.n_applied;
+    ir->n_host = h_tot.n_host;
+    ir->n_collisions = h_tot.n_coll;
+    {
+        float ms = 0;
+        ICK(hipEventElapsedTime(&ms, e0, e1));
+        ir->index_ms = ms;
+    }
+done:
+    hipStreamSynchronize(st);
+    {
+        void* bufs[] = {d_fb, d_tot, d_nsel, d_cls, d_flag, d_coll, d_txkey, d_k2, d_order, d_hash, d_sel, d_sidx,
+                        d_rev, d_nxt, d_g, d_g2, d_tmp};
+        for (void* b : bufs) if (b) hipFree(b);
+    }
+    if (e0) hipEventDestroy(e0);
+    if (e1) hipEventDestroy(e1);
+    free(h_fb);
+    return rc;
+}
+
+// Host-memory entry: scan the files (host memory) on the device and rebuild
+// the String/ListMeta index state of every record; state[i] per record in scan
+// order (n_out = records).
+extern "C" int cly_index(cly_ctx* ctx, const cly_file* files, int nfiles, uint8_t* state, uint64_t cap,
+                         uint64_t* n_out, cly_index_result* ir) {
+    if (!ctx || !ir || !n_out || nfiles < 0 || (nfiles && !files)) return CLY_ERR_ARG;
+    memset(ir, 0, sizeof(*ir));
+    *n_out = 0;
+    if (hipSetDevice(cly_ctx_device_internal(ctx)) != hipSuccess) return CLY_ERR_DEVICE;
+    hipStream_t st = cly_ctx_stream_internal(ctx);
+    int rc = CLY_OK;
+    uint64_t total = 0;
+    for (int i = 0; i < nfiles; i++) {
+        if (files[i].len >= (1ULL << 32)) return CLY_ERR_ARG;
+        total += (files[i].len + 4095) & ~4095ULL;
+    }
+    const int nf = nfiles ? nfiles : 1;
+    cly_file* df = (cly_file*)calloc(nf, sizeof(cly_file));
+    uint64_t* first = (uint64_t*)calloc(nf, sizeof(uint64_t));
+    cly_file_result* res = (cly_file_result*)calloc(nf, sizeof(cly_file_result));
+    uint8_t *d_bytes = nullptr, *d_state = nullptr;
+    cly_tuple* d_tup = nullptr;
+    uint64_t need = 0, cap_t = 0, T = 0, off = 0;
+    ICK(hipMalloc((void**)&d_bytes, total + 4096));
+    for (int i = 0; i < nfiles; i++) {
+        df[i] = files[i];
+        df[i].base = d_bytes + off;
+        if (files[i].len) ICK(hipMemcpyAsync(d_bytes + off, files[i].base, files[i].len, hipMemcpyHostToDevice, st));
+        off += (files[i].len + 4095) & ~4095ULL;
+    }
+    cap_t = cly_scan_capacity(files, nfiles) + 16;
+    ICK(hipMalloc((void**)&d_tup, sizeof(cly_tuple) * cap_t));
+    rc = cly_scan_device(ctx, df, nfiles, d_tup, cap_t, first, res, &need, nullptr, nullptr);
+    if (rc != CLY_OK) goto done;
+    for (int i = 0; i < nfiles; i++) {
+        if (res[i].status < 0) { rc = res[i].status; goto done; }
+        if (first[i] != T && res[i].n_records)
+            ICK(hipMemcpyAsync(d_tup + T, d_tup + first[i], sizeof(cly_tuple) * res[i].n_records,
+                               hipMemcpyDeviceToDevice, st));
+        first[i] = T;
+        T += res[i].n_records;
+    }
+    *n_out = T;
+    if (T > cap) { rc = CLY_ERR_CAPACITY; goto done; }
+    ICK(hipMalloc((void**)&d_state, T + 1));
+    rc = cly_index_device(ctx, df, nfiles, d_tup, first, res, d_state, ir, nullptr);
+    if (rc != CLY_OK) goto done;
+    if (T) ICK(hipMemcpyAsync(state, d_state, T, hipMemcpyDeviceToHost, st));
+    ICK(hipStreamSynchronize(st));
+done:
+    hipStreamSynchronize(st);
+    hipFree(d_bytes); hipFree(d_tup); hipFree(d_state);
+    free(df); free(first); free(res);
+    return rc;
+}

@@ -188,6 +188,40 @@ int cly_hint_positions_device(cly_ctx* ctx, const uint8_t* d_hint_file, const cl
 int cly_hint_scan(cly_ctx* ctx, const cly_file* hint_file, cly_tuple* out, cly_pos* pos, uint64_t cap,
                   uint64_t* n_out, cly_file_result* res);
 
+/* ---- index rebuild (db.loadIndex, db.go:511-637) -------------------------
+ * Per record of a scan (scan order = fid order, offsets within), the state of
+ * the String and ListMeta indexes after the load: records without a txId are
+ * applied at once, records with a txId at their txId's next TxnCommit marker
+ * (a TxnRollback drops them, TxnBegin is ignored, no marker: never applied);
+ * the last applied record of a key decides (Put -> the index points at it,
+ * Deleted -> the key is absent).  Hash/List/Set records (composite index keys,
+ * db.go:524-572) are the host's: CLY_IX_HOST (tx records only when committed).
+ * A hint file loaded before (loadIndexFromHintFile) is not part of this.     */
+#define CLY_IX_DEAD 0         /* not the index's entry after the load         */
+#define CLY_IX_LIVE 1         /* the String/ListMeta index points here         */
+#define CLY_IX_HOST 2         /* Hash/List/Set record: indexed by the host     */
+typedef struct cly_index_result {
+    uint64_t n_live;          /* keys present (= records in state LIVE)         */
+    uint64_t n_applied;       /* String/ListMeta records updateIndex sees       */
+    uint64_t n_host;          /* records left to the host                       */
+    uint64_t n_collisions;    /* 64-bit key-hash collisions (resolved exactly)  */
+    double   index_ms;        /* device time                                    */
+} cly_index_result;
+
+/* Device entry over a cly_scan_device result (tuples back to back): d_state
+ * gets one byte per tuple.  The LIVE bytes are merge.go:104-132's liveness
+ * for String/ListMeta records (cly_merge_device's d_live once HOST bytes are
+ * replaced by the host's verdict).  Returns the scan's error status if a file
+ * failed (loadIndex returns it), CLY_ERR_VARINT if a txId varint overflowed. */
+int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
+                     const cly_tuple* d_tuples, const uint64_t* file_first, const cly_file_result* res,
+                     uint8_t* d_state, cly_index_result* ir, void* stream);
+
+/* Host-memory entry: scans the files (host memory) on the device, then the
+ * index rebuild; state[i] for the i-th record in scan order, *n_out records. */
+int cly_index(cly_ctx* ctx, const cly_file* files, int nfiles, uint8_t* state, uint64_t cap,
+              uint64_t* n_out, cly_index_result* ir);
+
 const char* cly_strerror(int code);
 
 /* Library build identification (gfx target, kernel configuration).            */

@@ -181,3 +181,49 @@ def merge_corpus(seed, n_keys=300, rounds=3, tx_frac=0.3):
                 b += mg.encode_record(mg.key_tx(key, 0), rng.randbytes(rng.choice([0, 5, 50, 256, 900])),
                                       mg.NORMAL, rng.choice([0, 0, 0, 1, 2, 3, 4]), 0)
     return bytes(b)
+
+
+def index_states(file_bytes, tuples_per_file):
+    """db.loadIndex (db.go:582-637) restated literally: a map of buffered tx
+    records per txId, updateIndex for String and ListMeta keys, then per record
+    the state the device index reports: 1 = the index points at it, 2 = a
+    Hash/List/Set record the host indexes (tx ones only once committed), 0
+    otherwise."""
+    recs = []
+    for F, tt in zip(file_bytes, tuples_per_file):
+        for t in tt:
+            o, h, ks = int(t["offset"]), int(t["header_size"]), int(t["key_size"])
+            key = bytes(F[o + h:o + h + ks])
+            tx, n = mg.varint(key)
+            recs.append((key[n:] if n > 0 else key, t, tx))
+    index = {mg.STRING: {}, mg.LISTMETA: {}}
+    state = [0] * len(recs)
+    txrecords = {}
+
+    def update(i):
+        rk, t, _ = recs[i]
+        dt = int(t["data_type"])
+        if dt in (mg.HASH, mg.LIST, mg.SET):
+            state[i] = 2
+        elif dt in index:
+            if int(t["type"]) == mg.DELETED:
+                index[dt].pop(rk, None)
+            else:
+                index[dt][rk] = i
+
+    for i, (rk, t, tx) in enumerate(recs):
+        if tx == 0:
+            update(i)
+        elif int(t["type"]) == mg.TXN_BEGIN:
+            pass
+        elif int(t["type"]) == mg.TXN_COMMIT:
+            for j in txrecords.pop(tx, []):
+                update(j)
+        elif int(t["type"]) == mg.TXN_ROLLBACK:
+            txrecords.pop(tx, None)
+        else:
+            txrecords.setdefault(tx, []).append(i)
+    for d in index.values():
+        for i in d.values():
+            state[i] = 1
+    return np.array(state, np.uint8)

@@ -1,0 +1,87 @@
+"""Index rebuild (db.loadIndex, db.go:511-637) on the
+device: per record the state of the String/ListMeta indexes after the load.
+
+CPU: the literal restatement (tests/gpu_util.py index_states, a map of tx
+buffers as db.go keeps it) against the independent liveness restatement used
+for merge (string_live_mask) on String workloads.  GPU (-m gpu): cly_index /
+cly_index_device against index_states, byte for byte, incl. forced key-hash
+collisions (CLY_IX_HASH_MASK) and the C4 shape through the device entry."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle import cly_oracle as co
+
+from .gpu_util import index_states, merge_corpus, mixed_corpus, string_live_mask
+from .test_merge import oracle_scan, split_files
+
+
+def test_index_restatements_agree():
+    for seed in range(6):
+        b = merge_corpus(seed, n_keys=150 + 40 * seed)
+        arrays, tts, _ = oracle_scan(split_files(b, 1 + seed % 3, random.Random(seed)))
+        st = index_states(arrays, tts)
+        live = string_live_mask(arrays, tts)
+        strings = np.concatenate([t["data_type"] == 0 for t in tts])
+        assert ((st == 1) & strings).sum() == live.sum()
+        assert (((st == 1) & strings) == (live == 1)).all()
+
+
+@pytest.fixture(scope="module")
+def scanner():
+    from couloydb_amd import Scanner
+    s = Scanner(0)
+    yield s
+    s.close()
+
+
+def gpu_vs_restatement(scanner, files):
+    from couloydb_amd import DataFile
+    arrays, tts, _ = oracle_scan(files)
+    want = index_states(arrays, tts)
+    got, r = scanner.index([DataFile(a.copy(), i) for i, a in enumerate(arrays)])
+    assert len(got) == len(want)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, "first differing record %d: gpu=%d want=%d" % (bad[0], got[bad[0]], want[bad[0]])
+    assert r.n_live == int((want == 1).sum()) and r.n_host == int((want == 2).sum())
+    return r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(6))
+def test_gpu_index_workload(scanner, seed):
+    b = merge_corpus(seed, n_keys=300 + 100 * seed, rounds=4)
+    gpu_vs_restatement(scanner, split_files(b, 1 + seed % 4, random.Random(seed)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(3))
+def test_gpu_index_mixed(scanner, seed):
+    b = mixed_corpus(200 + seed, 300_000, tail=False)
+    gpu_vs_restatement(scanner, split_files(b, 3, random.Random(seed)))
+
+
+@pytest.mark.gpu
+def test_gpu_index_forced_collisions(scanner, monkeypatch):
+    monkeypatch.setenv("CLY_IX_HASH_MASK", "f")
+    b = merge_corpus(11, n_keys=500, rounds=3)
+    r = gpu_vs_restatement(scanner, split_files(b, 2, random.Random(11)))
+    assert r.n_collisions > 0
+
+
+@pytest.mark.gpu
+def test_gpu_index_device_c4_shape():
+    """C4 shape (k%4==0 overwritten, k%4==2 deleted) at 600 MiB through the
+    device entry: the index's live records are exactly the workload's live mask."""
+    import torch
+    import bench
+    from couloydb_amd import Scanner
+    wl = bench.make_workload("c4", torch, size=600 << 20)
+    with Scanner(0) as sc:
+        first, res, st, need = sc.scan_device(wl.dev_files, wl.d_out.data_ptr(), wl.out_cap)
+        d_state = torch.empty(need, dtype=torch.uint8, device="cuda")
+        r = sc.index_device(wl.dev_files, wl.d_out.data_ptr(), first, res, d_state.data_ptr())
+    got = d_state.cpu().numpy()
+    assert (got == wl.live_np).all() and r.n_live == wl.n_live and r.n_host == 0
