@@ -17,7 +17,7 @@ import numpy as np
 
 from . import _abi
 from ._abi import (END_EOF, END_TORN, END_ZERO, ERR_CRC, ERR_OFFSET, ERR_TRUNC5, ERR_VARINT,
-                   POS_DTYPE, TUPLE_DTYPE)
+                   POS_DTYPE, REC_IN_DTYPE, TUPLE_DTYPE)
 
 __all__ = ["POS_DTYPE", "Scanner", "DataFile", "LogRecord", "LogPos", "ScanResult", "ScanError", "MergeResult",
            "ErrInvalidCRC", "TUPLE_DTYPE", "STATUS_NAMES"]
@@ -257,6 +257,17 @@ class Scanner:
         if rc != 0:
             raise (ErrInvalidCRC if rc == ERR_CRC else ScanError)(rc, "cly_index_device")
         return r
+
+    def append_device(self, d_recs, n, tx_id, commit, active_fid, write_off, data_file_size, d_out, out_max_files,
+                      d_pos, stream=None):
+        """Batched append (db.appendLogRecord over a batch, db.go:368-413; WriteBatch
+        with commit=True): d_recs = device array of n REC_IN_DTYPE records.
+        Returns (rc, region lengths, ClyAppendResult)."""
+        lens = (ctypes.c_uint64 * max(1, out_max_files))()
+        r = _abi.ClyAppendResult()
+        rc = self.lib.cly_append_device(self.ctx, d_recs, n, tx_id, 1 if commit else 0, active_fid, write_off,
+                                        data_file_size, d_out, out_max_files, lens, d_pos, ctypes.byref(r), stream)
+        return rc, [int(lens[k]) for k in range(min(out_max_files, int(r.n_out_files)))], r
 
     def merge_device(self, dev_files, d_tuples, file_first, results, d_live, data_file_size, d_out, out_max_files,
                      d_hint, hint_cap, stream=None):

@@ -50,6 +50,17 @@ class ClyIndexResult(ctypes.Structure):
 IX_DEAD, IX_LIVE, IX_HOST = 0, 1, 2
 
 
+class ClyAppendResult(ctypes.Structure):
+    _fields_ = [("bytes", ctypes.c_uint64), ("out_stride", ctypes.c_uint64), ("final_write_off", ctypes.c_uint64),
+                ("final_fid", ctypes.c_uint32), ("n_out_files", ctypes.c_uint32), ("append_ms", ctypes.c_double)]
+
+
+# numpy view of cly_rec_in (40 bytes)
+REC_IN_DTYPE = np.dtype([("key", "<u8"), ("value", "<u8"), ("key_len", "<u4"), ("value_len", "<u4"),
+                         ("expiration", "<i8"), ("type", "u1"), ("data_type", "u1"), ("_pad", "u1", (6,))])
+assert REC_IN_DTYPE.itemsize == 40
+
+
 class ClyMergeResult(ctypes.Structure):
     _fields_ = [("n_live", ctypes.c_uint64), ("n_reencoded", ctypes.c_uint64),
                 ("hint_bytes", ctypes.c_uint64), ("out_stride", ctypes.c_uint64),
@@ -76,7 +87,7 @@ assert GEN_DTYPE.itemsize == 32
 
 SCAN_SYMBOLS = ["cly_ctx_create", "cly_ctx_destroy", "cly_scan_capacity", "cly_scan",
                 "cly_scan_device", "cly_merge_device", "cly_merge", "cly_hint_positions_device", "cly_hint_scan",
-                "cly_index_device", "cly_index",
+                "cly_index_device", "cly_index", "cly_append_device",
                 "cly_strerror", "cly_build_info"]
 GEN_SYMBOLS = ["cly_gen_record_size", "cly_gen_layout", "cly_gen_encode"]
 
@@ -132,6 +143,11 @@ def load_scan_lib(name="libclyscan.so"):
     lib.cly_index.argtypes = [ctypes.c_void_p, P(ClyFile), ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
                               P(ctypes.c_uint64), P(ClyIndexResult)]
     lib.cly_index.restype = ctypes.c_int
+    lib.cly_append_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int,
+                                      ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+                                      ctypes.c_uint32, P(ctypes.c_uint64), ctypes.c_void_p, P(ClyAppendResult),
+                                      ctypes.c_void_p]
+    lib.cly_append_device.restype = ctypes.c_int
     lib.cly_strerror.argtypes = [ctypes.c_int]
     lib.cly_strerror.restype = ctypes.c_char_p
     lib.cly_build_info.argtypes = []

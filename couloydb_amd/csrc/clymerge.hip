@@ -34,6 +34,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <hipcub/hipcub.hpp>
+
 #include "scan_core.h"
 
 extern "C" hipStream_t cly_ctx_stream_internal(cly_ctx* c);
@@ -467,14 +469,19 @@ __device__ __forceinline__ void mc_wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// Template over the descriptor capacity per block (CMAX) and the prefix stride
+// (PRE); lo0 = first byte of region 0 that belongs to the output (appends
+// continue an active file: bytes below it are kept as they are).  fstart[k]
+// is the first descriptor of region k; flen[k] the region's end offset.
+template <int CMAX, int PRE>
 __global__ void __launch_bounds__(64 * MC_W)
 k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uint32_t* __restrict__ bmap,
-        const uint64_t* __restrict__ fstart, const uint64_t* __restrict__ flen, const MTot* tot, uint64_t stride,
-        uint64_t nblocks, uint8_t* out) {
-    __shared__ int32_t s_rel[MC_W][M_CMAX];
-    __shared__ uint64_t s_src[MC_W][M_CMAX];
-    __shared__ uint32_t s_end[MC_W][M_CMAX];      // size | pre << 24 would not hold big records: separate arrays
-    __shared__ uint8_t s_pre[MC_W][M_CMAX];
+        const uint64_t* __restrict__ fstart, const uint64_t* __restrict__ flen, uint64_t stride,
+        uint64_t nblocks, uint8_t* out, uint64_t lo0) {
+    __shared__ int32_t s_rel[MC_W][CMAX];
+    __shared__ uint64_t s_src[MC_W][CMAX];
+    __shared__ uint32_t s_end[MC_W][CMAX];
+    __shared__ uint8_t s_pre[MC_W][CMAX];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int32_t* rel = s_rel[w];
     uint64_t* srcs = s_src[w];
@@ -485,12 +492,13 @@ k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uin
         const uint64_t k = b / bpf;
         const uint64_t B = b * M_CB, fo = B - k * stride;
         const uint64_t L = flen[k];
-        if (fo >= L) continue;                                  // (wave-uniform)
+        const uint64_t keep = k == 0 ? lo0 : 0;
+        if (fo >= L || fo + M_CB <= keep || L <= keep) continue;  // (wave-uniform)
         const uint32_t j0 = bmap[b];
         uint64_t j1 = fstart[k + 1];
         if (fo + M_CB < L) j1 = (uint64_t)bmap[b + 1] + 1;
         uint32_t cnt = (uint32_t)(j1 - j0);
-        if (cnt > M_CMAX) cnt = M_CMAX;
+        if (cnt > CMAX) cnt = CMAX;
         mc_wave_sync();                                         // previous block's readers are done
         for (uint32_t q = lane; q < cnt; q += 64) {
             const MCopy c = cp[j0 + q];
@@ -505,7 +513,8 @@ k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uin
         #pragma unroll
         for (int p = 0; p < MC_P; p++) {
             const int d = (p * 64 + lane) * 16;
-            if (fo + (uint64_t)d >= L) continue;
+            if (fo + (uint64_t)d >= L || fo + (uint64_t)d + 16 <= keep) continue;
+            if (fo + (uint64_t)d < keep) { gather |= 1u << p; continue; }
             int lo = 0, hi = (int)cnt - 1;                      // last record with rel <= d
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
@@ -558,9 +567,11 @@ k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uin
                 while (jj + 1 < (int)cnt && rel[jj + 1] <= pos) jj++;
                 const int r = pos - rel[jj];
                 const uint8_t* ptr = &g_zero_byte;
-                if (fo + (uint64_t)pos < L && r >= 0 && (uint32_t)r < sizes[jj]) {
+                if (fo + (uint64_t)pos < keep) {
+                    ptr = out + B + pos;                        // an active file's existing bytes
+                } else if (fo + (uint64_t)pos < L && r >= 0 && (uint32_t)r < sizes[jj]) {
                     const int pj = pres[jj];
-                    ptr = r < pj ? pre + (uint64_t)(j0 + jj) * M_PRE + r : (const uint8_t*)srcs[jj] + (r - pj);
+                    ptr = r < pj ? pre + (uint64_t)(j0 + jj) * PRE + r : (const uint8_t*)srcs[jj] + (r - pj);
                 }
                 bp[q] = ptr;
             }
@@ -684,7 +695,8 @@ extern "C" int cly_merge_device(cly_ctx* ctx, const cly_file* files, int nfiles,
         MDBG(st, "k_mhint");
         const uint64_t wgs = (nblocks + MC_W - 1) / MC_W;
         unsigned grid = wgs < 16384 ? (unsigned)wgs : 16384u;
-        k_mcopy<<<grid, 64 * MC_W, 0, st>>>(d_cp, d_pre, d_bmap, d_fstart, d_flen, d_tot, stride, nblocks, d_out);
+        k_mcopy<M_CMAX, M_PRE><<<grid, 64 * MC_W, 0, st>>>(d_cp, d_pre, d_bmap, d_fstart, d_flen, stride, nblocks,
+                                                          d_out, 0);
         MDBG(st, "k_mcopy");
         MCK(hipGetLastError());
         if (out_file_len) MCK(hipMemcpyAsync(out_file_len, d_flen, sizeof(uint64_t) * h_tot.n_out,
@@ -873,5 +885,245 @@ extern "C" int cly_hint_scan(cly_ctx* ctx, const cly_file* hint_file, cly_tuple*
 done:
     hipStreamSynchronize(st);
     hipFree(d_bytes); hipFree(d_tup); hipFree(d_pos);
+    return rc;
+}
+
+// ===========================================================================
+// Batched append (the write path: db.appendLogRecord over a batch,
+// db.go:368-413, as WriteBatch.Commit issues it, batch.go:62-118): each
+// record's Key = encodeKeyWithTxId(key, txId) (batch.go:120-127; db.Put uses
+// NO_TX_ID), EncodeLogRecord (data/logRecord.go:57-84), the file rotation
+// continuing the active file at its WriteOff, and optionally WriteBatch's
+// commit marker {encodeKeyWithTxId(TX_COMMIT_KEY, txId), TxnCommit}.
+// Per record two copy descriptors: [header, txId varint, key] and [value].
+#define A_PRE 48                                   // header (<= 26) + txId varint (<= 10)
+#define A_CMAX 1024                                // descriptors starting in one 4-KiB block
+struct ARec {                                      // == cly_rec_in
+    const uint8_t* key;
+    const uint8_t* value;
+    uint32_t key_len, value_len;
+    int64_t expiration;
+    uint8_t type, data_type, _pad[6];
+};
+static_assert(sizeof(ARec) == 40, "cly_rec_in layout");
+__device__ const uint8_t g_commit_key = 0x04;      // public.TX_COMMIT_KEY
+
+__device__ __forceinline__ ARec a_rec(const ARec* recs, uint64_t n, uint64_t j) {
+    if (j < n) return recs[j];
+    ARec c;                                        // the commit marker
+    c.key = &g_commit_key; c.value = nullptr; c.key_len = 1; c.value_len = 0; c.expiration = 0;
+    c.type = 2; c.data_type = 0;
+    return c;
+}
+__device__ __forceinline__ int a_prefix(const ARec& r, int64_t tx, uint8_t* h) {
+    const int tl = uvlen(zz(tx));
+    h[4] = r.type;
+    h[5] = r.data_type;
+    int n = 6;
+    n += put_uv(h + n, zz((int64_t)r.key_len + tl));
+    n += put_uv(h + n, zz((int64_t)r.value_len));
+    n += put_uv(h + n, zz(r.expiration));
+    n += put_uv(h + n, zz(tx));
+    return n;                                      // header + txId varint
+}
+__global__ void __launch_bounds__(256)
+k_asize(const ARec* __restrict__ recs, uint64_t n, uint64_t nt, int64_t tx, uint64_t* sz, unsigned long long* mx) {
+    unsigned long long m = 0;
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < nt; j += (uint64_t)gridDim.x * 256) {
+        const ARec r = a_rec(recs, n, j);
+        uint8_t h[A_PRE];
+        sz[j] = (uint64_t)a_prefix(r, tx, h) + r.key_len + r.value_len;
+        m = sz[j] > m ? sz[j] : m;
+    }
+    if (m) atomicMax(mx, m);
+}
+// appendLogRecord's rotation from (active file, WriteOff): region 0 is the
+// active file (it may take no record), later regions are fresh files that
+// always take their first record (a record larger than DataFileSize alone).
+__global__ void __launch_bounds__(M_ROT)
+k_arot(const uint64_t* __restrict__ g, uint64_t nt, uint64_t total, uint64_t dfs, uint64_t woff, uint32_t max_files,
+       uint64_t* fstart, uint64_t* flen, uint32_t* n_out) {
+    __shared__ uint64_t s_lo, s_hi;
+    uint64_t r = 0;
+    uint32_t k = 0;
+    while (r < nt || k == 0) {
+        const uint64_t g0 = r < nt ? g[r] : total;
+        const uint64_t cap = k == 0 ? (woff < dfs ? dfs - woff : 0) : dfs;
+        const uint64_t lim = g0 + cap;
+        uint64_t lo = k == 0 ? r : r + 1;
+        uint64_t hi = r + cap / 9 + 2;
+        if (hi > nt) hi = nt;
+        if (hi < lo) hi = lo;
+        while (lo < hi) {
+            const uint64_t span = hi - lo;
+            const uint64_t pos = lo + (span * (threadIdx.x + 1) + M_ROT - 1) / M_ROT;
+            const int ok = (pos < nt ? g[pos] : total) <= lim;
+            const int c = __syncthreads_count(ok);
+            if (threadIdx.x == (unsigned)c - 1) s_lo = pos;
+            if (threadIdx.x == (unsigned)c) s_hi = pos - 1;
+            if (threadIdx.x == 0) { if (c == 0) s_lo = lo; if (c == M_ROT) s_hi = hi; }
+            __syncthreads();
+            lo = s_lo; hi = s_hi;
+            __syncthreads();
+        }
+        if (threadIdx.x == 0 && k < max_files) {
+            fstart[k] = r;
+            flen[k] = (k == 0 ? woff : 0) + ((lo < nt ? g[lo] : total) - g0);
+        }
+        r = lo;
+        k++;
+        if (r >= nt) break;
+    }
+    if (threadIdx.x == 0) {
+        if (k < max_files) fstart[k] = nt;
+        *n_out = k;
+    }
+}
+// per record: region, offset, LogPos, prefix with the CRC, copy descriptors, block map
+__global__ void __launch_bounds__(256)
+k_aplace(const ARec* __restrict__ recs, uint64_t n, uint64_t nt, int64_t tx, const uint64_t* __restrict__ g,
+         const uint64_t* __restrict__ fstart, const uint32_t* __restrict__ n_out_p, uint64_t woff, uint32_t fid0,
+         uint64_t stride, MCopy* cp, uint8_t* pre, uint32_t* bmap, cly_pos* pos) {
+    __shared__ uint32_t tab[256];
+    crc_table_init(tab);
+    const uint32_t nout = *n_out_p;
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < nt; j += (uint64_t)gridDim.x * 256) {
+        int lo = 0, hi = (int)nout - 1;                        // region: largest k with fstart[k] <= j
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (fstart[mid] <= j) lo = mid; else hi = mid - 1;
+        }
+        // region 0 may be empty (fstart[0] == fstart[1] == 0): take the last region starting at or before j
+        const uint64_t base = lo == 0 ? woff : 0;
+        const uint64_t off = base + (g[j] - g[fstart[lo]]);
+        const uint64_t dst = (uint64_t)lo * stride + off;
+        const ARec r = a_rec(recs, n, j);
+        uint8_t h[A_PRE];
+        const int np = a_prefix(r, tx, h);
+        uint32_t s = 0xFFFFFFFFu;
+        for (int q = 4; q < np; q++) s = crc_upd(tab, s, h[q]);
+        for (uint32_t q = 0; q < r.key_len; q++) s = crc_upd(tab, s, r.key[q]);
+        for (uint32_t q = 0; q < r.value_len; q++) s = crc_upd(tab, s, r.value[q]);
+        s = ~s;
+        h[0] = (uint8_t)s; h[1] = (uint8_t)(s >> 8); h[2] = (uint8_t)(s >> 16); h[3] = (uint8_t)(s >> 24);
+        uint8_t* pj = pre + (2 * j) * A_PRE;
+        for (int q = 0; q < np; q++) pj[q] = h[q];
+        const uint32_t ka = (uint32_t)np + r.key_len;
+        cp[2 * j] = MCopy{dst, (uint64_t)r.key, ka, (uint32_t)np};
+        cp[2 * j + 1] = MCopy{dst + ka, (uint64_t)r.value, r.value_len, 0};
+        const uint64_t size = (uint64_t)ka + r.value_len;
+        for (uint64_t b = (dst + M_CB - 1) / M_CB; b * M_CB < dst + ka; b++) bmap[b] = (uint32_t)(2 * j);
+        for (uint64_t b = (dst + ka + M_CB - 1) / M_CB; b * M_CB < dst + size; b++) bmap[b] = (uint32_t)(2 * j + 1);
+        if (j == fstart[0] && lo == 0 && woff % M_CB) bmap[woff / M_CB] = (uint32_t)(2 * j);   // the block WriteOff starts in
+        pos[j] = cly_pos{(int64_t)off, fid0 + (uint32_t)lo, 0};
+    }
+}
+
+__global__ void k_dscale(uint64_t* fstart, uint32_t m) {
+    for (uint32_t k = threadIdx.x; k < m; k += blockDim.x) fstart[k] *= 2;
+}
+
+extern "C" int cly_append_device(cly_ctx* ctx, const cly_rec_in* d_recs, uint64_t n, int64_t tx_id, int commit,
+                                 uint32_t active_fid, uint64_t write_off, uint64_t data_file_size, uint8_t* d_out,
+                                 uint32_t out_max_files, uint64_t* out_file_len, cly_pos* d_pos,
+                                 cly_append_result* ar, void* stream_v) {
+    if (!ctx || !ar || (n && !d_recs) || data_file_size == 0) return CLY_ERR_ARG;
+    memset(ar, 0, sizeof(*ar));
+    // regions are DataFileSize apart, or further when a record is larger (the
+    // reference writes such a record alone into a fresh file)
+    uint64_t stride = (data_file_size + M_CB - 1) / M_CB * M_CB;
+    ar->out_stride = stride;
+    const uint64_t nt = n + (commit ? 1 : 0);
+    if (nt == 0) { ar->n_out_files = 1; ar->final_fid = active_fid; ar->final_write_off = write_off; return CLY_OK; }
+    if (2 * nt >= (1ull << 32)) return CLY_ERR_ARG;
+    if (hipSetDevice(cly_ctx_device_internal(ctx)) != hipSuccess) return CLY_ERR_DEVICE;
+    hipStream_t st = stream_v ? (hipStream_t)stream_v : cly_ctx_stream_internal(ctx);
+    int rc = CLY_OK;
+    uint64_t *d_sz = nullptr, *d_g = nullptr, *d_fstart = nullptr, *d_flen = nullptr, *h_flen = nullptr;
+    uint32_t *d_nout = nullptr, *d_bmap = nullptr;
+    MCopy* d_cp = nullptr;
+    uint8_t* d_pre = nullptr;
+    void* d_tmp = nullptr;
+    size_t tb = 0;
+    uint32_t h_nout = 0;
+    uint64_t total = 0, last = 0, fcap = 0, nblocks = 0;
+    unsigned long long* d_mx = nullptr;
+    unsigned long long h_mx = 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const unsigned grid = (unsigned)((nt + 255) / 256 < 16384 ? (nt + 255) / 256 : 16384);
+    MCK(hipEventCreate(&e0));
+    MCK(hipEventCreate(&e1));
+    MCK(hipMalloc((void**)&d_sz, sizeof(uint64_t) * nt));
+    MCK(hipMalloc((void**)&d_g, sizeof(uint64_t) * nt));
+    MCK(hipMalloc((void**)&d_nout, sizeof(uint32_t)));
+    MCK(hipMalloc((void**)&d_mx, sizeof(unsigned long long)));
+    MCK(hipMemsetAsync(d_mx, 0, sizeof(unsigned long long), st));
+    MCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, d_sz, d_g, (int)nt, st));
+    MCK(hipMalloc(&d_tmp, tb + 16));
+    MCK(hipEventRecord(e0, st));
+    k_asize<<<grid, 256, 0, st>>>((const ARec*)d_recs, n, nt, tx_id, d_sz, d_mx);
+    MCK(hipcub::DeviceScan::ExclusiveSum(d_tmp, tb, d_sz, d_g, (int)nt, st));
+    MCK(hipMemcpyAsync(&last, d_sz + nt - 1, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    MCK(hipMemcpyAsync(&total, d_g + nt - 1, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    MCK(hipMemcpyAsync(&h_mx, d_mx, sizeof(h_mx), hipMemcpyDeviceToHost, st));
+    MCK(hipStreamSynchronize(st));
+    total += last;
+    {
+        // a region holds at most max(DataFileSize, one record, the active file's
+        // WriteOff): records beyond a full file start a new one
+        uint64_t need = data_file_size;
+        if (h_mx > need) need = h_mx;
+        if (write_off > need) need = write_off;
+        stride = (need + M_CB - 1) / M_CB * M_CB;
+        ar->out_stride = stride;
+    }
+    // two neighbouring regions hold more than DataFileSize bytes (the second
+    // exists because the first could not take its first record)
+    fcap = 2 * (total + write_off) / data_file_size + 4;
+    if (fcap > nt + 2) fcap = nt + 2;
+    MCK(hipMalloc((void**)&d_fstart, sizeof(uint64_t) * (fcap + 1)));
+    MCK(hipMalloc((void**)&d_flen, sizeof(uint64_t) * (fcap + 1)));
+    k_arot<<<1, M_ROT, 0, st>>>(d_g, nt, total, data_file_size, write_off, (uint32_t)fcap, d_fstart, d_flen, d_nout);
+    MCK(hipMemcpyAsync(&h_nout, d_nout, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    MCK(hipStreamSynchronize(st));
+    ar->n_out_files = h_nout;
+    ar->bytes = total;
+    if (h_nout > out_max_files || !d_out || !d_pos) { rc = CLY_ERR_CAPACITY; goto done; }
+    nblocks = (uint64_t)h_nout * (stride / M_CB);
+    MCK(hipMalloc((void**)&d_cp, sizeof(MCopy) * 2 * nt));
+    MCK(hipMalloc((void**)&d_pre, (size_t)A_PRE * 2 * nt));
+    MCK(hipMalloc((void**)&d_bmap, sizeof(uint32_t) * (nblocks + 1)));
+    k_aplace<<<grid, 256, 0, st>>>((const ARec*)d_recs, n, nt, tx_id, d_g, d_fstart, d_nout, write_off, active_fid,
+                                   stride, d_cp, d_pre, d_bmap, d_pos);
+    {
+        // k_mcopy's per-region first descriptor: 2 x the first record
+        k_dscale<<<1, 64, 0, st>>>(d_fstart, h_nout + 1);
+        const uint64_t wgs = (nblocks + MC_W - 1) / MC_W;
+        const unsigned cg = wgs < 16384 ? (unsigned)wgs : 16384u;
+        k_mcopy<A_CMAX, A_PRE><<<cg, 64 * MC_W, 0, st>>>(d_cp, d_pre, d_bmap, d_fstart, d_flen, stride, nblocks, d_out,
+                                                        write_off);
+    }
+    MCK(hipGetLastError());
+    MCK(hipEventRecord(e1, st));
+    h_flen = (uint64_t*)malloc(sizeof(uint64_t) * h_nout);
+    MCK(hipMemcpyAsync(h_flen, d_flen, sizeof(uint64_t) * h_nout, hipMemcpyDeviceToHost, st));
+    MCK(hipStreamSynchronize(st));
+    for (uint32_t k = 0; k < h_nout; k++) if (out_file_len) out_file_len[k] = h_flen[k];
+    ar->final_fid = active_fid + h_nout - 1;
+    ar->final_write_off = h_flen[h_nout - 1];
+    {
+        float ms = 0;
+        MCK(hipEventElapsedTime(&ms, e0, e1));
+        ar->append_ms = ms;
+    }
+done:
+    hipStreamSynchronize(st);
+    {
+        void* bufs[] = {d_sz, d_g, d_fstart, d_flen, d_nout, d_bmap, d_cp, d_pre, d_tmp, d_mx};
+        for (void* b : bufs) if (b) hipFree(b);
+    }
+    free(h_flen);
+    if (e0) hipEventDestroy(e0);
+    if (e1) hipEventDestroy(e1);
     return rc;
 }

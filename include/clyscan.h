@@ -222,6 +222,35 @@ int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
 int cly_index(cly_ctx* ctx, const cly_file* files, int nfiles, uint8_t* state, uint64_t cap,
               uint64_t* n_out, cly_index_result* ir);
 
+/* ---- batched append (the write path, db.appendLogRecord over a batch) ------
+ * db.go:368-413 as db.Put (NO_TX_ID) and WriteBatch.Commit (batch.go:62-118)
+ * issue it: Key = encodeKeyWithTxId(key, tx_id), EncodeLogRecord, a new file
+ * when WriteOff+size > data_file_size, continuing the active file at
+ * write_off; with `commit`, WriteBatch's marker {encodeKeyWithTxId(
+ * TX_COMMIT_KEY, tx_id), TxnCommit} follows the records.  Output region k is
+ * file active_fid+k at d_out + k*out_stride (region 0 holds the active file:
+ * its bytes below write_off are kept); d_pos[i] = the LogPos of record i
+ * (the marker's last).                                                        */
+typedef struct cly_rec_in {   /* one record to append (device pointers), 40 B  */
+    const uint8_t* key;
+    const uint8_t* value;
+    uint32_t key_len, value_len;
+    int64_t  expiration;
+    uint8_t  type, data_type, _pad[6];
+} cly_rec_in;
+typedef struct cly_append_result {
+    uint64_t bytes;           /* bytes appended                                 */
+    uint64_t out_stride;
+    uint64_t final_write_off; /* activityFile.WriteOff afterwards               */
+    uint32_t final_fid;       /* activityFile.FileId afterwards                 */
+    uint32_t n_out_files;     /* regions touched (the active file + new files)  */
+    double   append_ms;
+} cly_append_result;
+int cly_append_device(cly_ctx* ctx, const cly_rec_in* d_recs, uint64_t n, int64_t tx_id, int commit,
+                      uint32_t active_fid, uint64_t write_off, uint64_t data_file_size,
+                      uint8_t* d_out, uint32_t out_max_files, uint64_t* out_file_len, cly_pos* d_pos,
+                      cly_append_result* ar, void* stream);
+
 const char* cly_strerror(int code);
 
 /* Library build identification (gfx target, kernel configuration).            */

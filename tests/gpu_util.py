@@ -227,3 +227,21 @@ def index_states(file_bytes, tuples_per_file):
         for i in d.values():
             state[i] = 1
     return np.array(state, np.uint8)
+
+
+def py_append(records, tx_id, commit, active, write_off, data_file_size):
+    """appendLogRecord over a batch restated (db.go:368-413, batch.go:62-118):
+    records = [(key, value, type, dtype, exp)]; active = the active file's bytes
+    (its first write_off bytes are kept).  -> ([file bytes, active first], [(fid, off)])."""
+    files = [bytearray(active[:write_off])]
+    pos = []
+    recs = list(records)
+    if commit:
+        recs.append((b"\x04", b"", mg.TXN_COMMIT, mg.STRING, 0))       # public.TX_COMMIT_KEY
+    for key, value, typ, dt, exp in recs:
+        rec = mg.encode_record(mg.key_tx(key, tx_id), value, typ, dt, exp)
+        if len(files[-1]) + len(rec) > data_file_size:
+            files.append(bytearray())
+        pos.append((len(files) - 1, len(files[-1])))
+        files[-1] += rec
+    return [bytes(f) for f in files], pos
