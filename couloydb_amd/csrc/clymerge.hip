@@ -121,6 +121,45 @@ __device__ __forceinline__ void crc_table_init(uint32_t* t) {
 __device__ __forceinline__ uint32_t crc_upd(const uint32_t* t, uint32_t s, uint32_t b) {
     return t[(s ^ b) & 0xff] ^ (s >> 8);
 }
+// slicing-by-4 tables t4[k*256 + v] = A^(8k) T0[v] (t4[0..255] = T0)
+__device__ __forceinline__ void crc_table4_init(uint32_t* t4) {
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        uint32_t s = (uint32_t)i;
+        for (int k = 0; k < 8; k++) s = (s & 1) ? (s >> 1) ^ CLY_POLY : s >> 1;
+        t4[i] = s;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        uint32_t s = t4[i];
+        for (int k = 1; k < 4; k++) { s = t4[s & 0xff] ^ (s >> 8); t4[k * 256 + i] = s; }
+    }
+    __syncthreads();
+}
+// register over len bytes at p (any alignment): bytes up to a dword boundary,
+// then aligned dwords four at a time (loads in flight together), then the tail
+__device__ __forceinline__ uint32_t crc_span(const uint32_t* t4, uint32_t s, const uint8_t* p, uint64_t len) {
+    while (len && ((uintptr_t)p & 3)) { s = crc_upd(t4, s, *p++); len--; }
+    const uint32_t* w = (const uint32_t*)p;
+    uint64_t nw = len >> 2;
+    while (nw >= 4) {
+        const uint32_t a = w[0], b = w[1], c = w[2], d = w[3];
+        #pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t x = s ^ (k == 0 ? a : k == 1 ? b : k == 2 ? c : d);
+            s = t4[768 + (x & 0xff)] ^ t4[512 + ((x >> 8) & 0xff)] ^ t4[256 + ((x >> 16) & 0xff)] ^ t4[x >> 24];
+        }
+        w += 4;
+        nw -= 4;
+    }
+    while (nw) {
+        const uint32_t x = s ^ *w++;
+        s = t4[768 + (x & 0xff)] ^ t4[512 + ((x >> 8) & 0xff)] ^ t4[256 + ((x >> 16) & 0xff)] ^ t4[x >> 24];
+        nw--;
+    }
+    p = (const uint8_t*)w;
+    for (uint64_t q = 0; q < (len & 3); q++) s = crc_upd(t4, s, p[q]);
+    return s;
+}
 
 // Block-wide exclusive scan of (a, b) pairs over M_NT threads.
 __device__ __forceinline__ MSum block_excl(MSum v, MSum& total, MSum* sh) {
@@ -984,8 +1023,8 @@ __global__ void __launch_bounds__(256)
 k_aplace(const ARec* __restrict__ recs, uint64_t n, uint64_t nt, int64_t tx, const uint64_t* __restrict__ g,
          const uint64_t* __restrict__ fstart, const uint32_t* __restrict__ n_out_p, uint64_t woff, uint32_t fid0,
          uint64_t stride, MCopy* cp, uint8_t* pre, uint32_t* bmap, cly_pos* pos) {
-    __shared__ uint32_t tab[256];
-    crc_table_init(tab);
+    __shared__ uint32_t tab[1024];
+    crc_table4_init(tab);
     const uint32_t nout = *n_out_p;
     for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < nt; j += (uint64_t)gridDim.x * 256) {
         int lo = 0, hi = (int)nout - 1;                        // region: largest k with fstart[k] <= j
@@ -1002,8 +1041,8 @@ k_aplace(const ARec* __restrict__ recs, uint64_t n, uint64_t nt, int64_t tx, con
         const int np = a_prefix(r, tx, h);
         uint32_t s = 0xFFFFFFFFu;
         for (int q = 4; q < np; q++) s = crc_upd(tab, s, h[q]);
-        for (uint32_t q = 0; q < r.key_len; q++) s = crc_upd(tab, s, r.key[q]);
-        for (uint32_t q = 0; q < r.value_len; q++) s = crc_upd(tab, s, r.value[q]);
+        s = crc_span(tab, s, r.key, r.key_len);
+        s = crc_span(tab, s, r.value, r.value_len);
         s = ~s;
         h[0] = (uint8_t)s; h[1] = (uint8_t)(s >> 8); h[2] = (uint8_t)(s >> 16); h[3] = (uint8_t)(s >> 24);
         uint8_t* pj = pre + (2 * j) * A_PRE;
