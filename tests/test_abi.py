@@ -127,3 +127,28 @@ def test_gf_shift_algebra():
         bad, crc = subprocess.check_output([exe]).decode().split()
     assert bad == "0"
     assert int(crc, 16) == zlib.crc32(b"hello, world - couloydb log record")
+
+
+def test_path_struct_layouts():
+    """The merge / hint / index / append structs: ctypes and numpy views agree with the C compiler."""
+    src = r'''
+    #include <stdio.h>
+    #include <stddef.h>
+    #include "clyscan.h"
+    int main(void){ printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(cly_merge_result),
+      offsetof(cly_merge_result, merge_ms), sizeof(cly_pos), sizeof(cly_index_result), sizeof(cly_rec_in),
+      offsetof(cly_rec_in, expiration), offsetof(cly_rec_in, type), sizeof(cly_append_result),
+      offsetof(cly_append_result, append_ms)); return 0; }
+    '''
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "t")
+        subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe])
+        out = [int(x) for x in subprocess.check_output([exe]).decode().split()]
+    assert out[0] == ctypes.sizeof(_abi.ClyMergeResult) and out[1] == _abi.ClyMergeResult.merge_ms.offset
+    assert out[2] == _abi.POS_DTYPE.itemsize == 16
+    assert out[3] == ctypes.sizeof(_abi.ClyIndexResult)
+    assert out[4] == _abi.REC_IN_DTYPE.itemsize == 40
+    assert out[5] == _abi.REC_IN_DTYPE.fields["expiration"][1] and out[6] == _abi.REC_IN_DTYPE.fields["type"][1]
+    assert out[7] == ctypes.sizeof(_abi.ClyAppendResult) and out[8] == _abi.ClyAppendResult.append_ms.offset
