@@ -299,8 +299,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # CLY_BENCH_REHEARSE=1: every rank on GPU 0 over gloo (rehearses the N>1
+    # path on a one-GPU box; the driver's multi-GPU runs use RCCL, one GPU per rank)
+    rehearse = os.environ.get("CLY_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     if world > 1:
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group(backend="gloo")
+        else:
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
 
     from couloydb_amd import Scanner, build_info
@@ -362,7 +370,7 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt, scan_ms / args.steps], dtype=torch.float64, device="cuda")
+    t = torch.tensor([dt, scan_ms / args.steps], dtype=torch.float64, device="cpu" if rehearse else "cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt, kern_ms = float(t[0]), float(t[1])
