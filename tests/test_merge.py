@@ -306,3 +306,48 @@ def test_gpu_hint_scan(scanner):
     with pytest.raises(ScanError) as ei:
         scanner.load_hint(DataFile(bad, 0))
     assert ei.value.code == -3 and "after 2 records" in str(ei.value)
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_gpu_merge_c4_4gib_properties():
+    """C4 shape at 4 GiB (16 data files of 256 MiB): scan -> device index ->
+    merge -> rescans.  Size-independent properties: the index's live bytes are
+    the workload's; the merge output decodes cleanly into exactly the live
+    records, in order, with NO_TX_ID keys and the same values (verbatim copies:
+    the output sizes/CRCs equal the inputs'); the hint file decodes to one
+    position per live record, pointing at that record."""
+    import torch
+    import bench
+    from couloydb_amd import POS_DTYPE, Scanner, TUPLE_DTYPE
+    wl = bench.make_workload("c4", torch, size=4 << 30)
+    with Scanner(0) as sc:
+        first, res, st, need = sc.scan_device(wl.dev_files, wl.d_out.data_ptr(), wl.out_cap)
+        assert all(r.status == 0 for r in res) and need == wl.expect_records
+        d_state = torch.empty(need, dtype=torch.uint8, device="cuda")
+        ir = sc.index_device(wl.dev_files, wl.d_out.data_ptr(), first, res, d_state.data_ptr())
+        assert ir.n_live == wl.n_live and (d_state.cpu().numpy() == wl.live_np).all()
+        rc, lens, m = sc.merge_device(wl.dev_files, wl.d_out.data_ptr(), first, res, d_state.data_ptr(),
+                                      bench.DATA_FILE_SIZE, wl.d_merge.data_ptr(), wl.merge_max_files,
+                                      wl.d_hint.data_ptr(), wl.hint_cap)
+        assert rc == 0 and m.n_live == wl.n_live and m.n_reencoded == 0
+        stride = int(m.out_stride)
+        mfiles = [(wl.d_merge.data_ptr() + k * stride, lens[k], k) for k in range(len(lens))]
+        cap = m.n_live + 1024
+        d2 = torch.empty(cap * 48, dtype=torch.uint8, device="cuda")
+        f2, r2, _, n2 = sc.scan_device(mfiles, d2.data_ptr(), cap)
+        assert n2 == m.n_live and all(r.status == 0 and r.end_offset == lens[k] for k, r in enumerate(r2))
+        merged = d2[:n2 * 48].cpu().numpy().view(TUPLE_DTYPE)
+        d3 = torch.empty(cap * 48, dtype=torch.uint8, device="cuda")
+        f3, r3, _, n3 = sc.scan_device([(wl.d_hint.data_ptr(), m.hint_bytes, 0)], d3.data_ptr(), cap)
+        assert n3 == m.n_live and r3[0].status == 0
+        d_pos = torch.empty(n3 * 16, dtype=torch.uint8, device="cuda")
+        rc2 = sc.lib.cly_hint_positions_device(sc.ctx, wl.d_hint.data_ptr(), d3.data_ptr(), n3, d_pos.data_ptr(),
+                                               None, None)
+        assert rc2 == 0
+        pos = d_pos.cpu().numpy().view(POS_DTYPE)
+    src = wl.d_out[:need * 48].cpu().numpy().view(TUPLE_DTYPE)[wl.live_np != 0]
+    for f in ("size", "key_size", "value_size", "crc", "type", "data_type", "expiration"):
+        assert (merged[f] == src[f]).all(), f
+    assert (merged["tx_id"] == 0).all() and (merged["txid_len"] == 1).all()
+    assert (pos["fid"] == merged["fid"]).all() and (pos["offset"] == merged["offset"]).all()
