@@ -501,6 +501,8 @@ k_mhint(const MEnt* __restrict__ e, const MCopy* __restrict__ cp, const cly_tupl
 // straddles records, or touches a re-encoded prefix or the end of the file,
 // gathers its 16 bytes with independent byte loads.
 __device__ const uint8_t g_zero_byte = 0;
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));   // 16 B, dword-aligned
+#define CLY_GLB __attribute__((address_space(1)))                            // global (not flat) loads
 #define MC_W 4                                   // waves per workgroup
 #define MC_P (M_CB / 16 / 64)                    // pieces per lane
 __device__ __forceinline__ void mc_wave_sync() {
@@ -563,9 +565,9 @@ k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uin
             const int pr = pres[lo];
             if (r0 >= pr && (int64_t)r0 + 16 <= (int64_t)sizes[lo]) {
                 const uint64_t sa = srcs[lo] + (uint64_t)(r0 - pr);
-                const uint32_t* wp = (const uint32_t*)(sa & ~3ull);
-                #pragma unroll
-                for (int q = 0; q < 4; q++) a[p][q] = wp[q];
+                const CLY_GLB uint32_t* wp = (const CLY_GLB uint32_t*)(sa & ~3ull);
+                const u32x4a v4 = *(const CLY_GLB u32x4a*)wp;  // one dwordx4 at a dword-aligned address
+                a[p][0] = v4.x; a[p][1] = v4.y; a[p][2] = v4.z; a[p][3] = v4.w;
                 a[p][4] = (sa & 3) ? wp[4] : 0u;
                 fast |= 1u << p;
                 shs |= (uint32_t)(sa & 3) << (2 * p);
