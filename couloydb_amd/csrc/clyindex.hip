@@ -207,8 +207,11 @@ k_ixcoll(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, con
         if (best && tup[sidx[a]].type != 1) state[sidx[a]] = CLY_IX_LIVE;
     }
 }
+// counts: one atomic per workgroup and counter (a wave-level atomic on one
+// address from every wave serialises in L2)
 __global__ void __launch_bounds__(256)
 k_ixcount(const uint8_t* __restrict__ state, const uint8_t* __restrict__ flag, uint64_t n, IxTot* tot) {
+    __shared__ unsigned long long sh[3][4];
     unsigned long long live = 0, host = 0, ap = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         live += state[i] == CLY_IX_LIVE;
@@ -220,10 +223,13 @@ k_ixcount(const uint8_t* __restrict__ state, const uint8_t* __restrict__ flag, u
         host += __shfl_xor(host, d, 64);
         ap += __shfl_xor(ap, d, 64);
     }
-    if ((threadIdx.x & 63) == 0) {
-        if (live) atomicAdd(&tot->n_live, live);
-        if (host) atomicAdd(&tot->n_host, host);
-        if (ap) atomicAdd(&tot->n_applied, ap);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sh[0][w] = live; sh[1][w] = host; sh[2][w] = ap; }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const unsigned long long v = sh[threadIdx.x][0] + sh[threadIdx.x][1] + sh[threadIdx.x][2] + sh[threadIdx.x][3];
+        unsigned long long* dst = threadIdx.x == 0 ? &tot->n_live : threadIdx.x == 1 ? &tot->n_host : &tot->n_applied;
+        if (v) atomicAdd(dst, v);
     }
 }
 
@@ -375,7 +381,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
             k_ixcoll<<<(unsigned)((m2 + 63) / 64), 64, 0, st>>>(d_txkey, d_sidx, d_order, m2, d_coll, d_tuples, d_first,
                                                                 d_bases, nfiles, d_state);
     }
-    k_ixcount<<<grid, 256, 0, st>>>(d_state, d_flag, n, d_tot);
+    k_ixcount<<<ix_grid(n) < 1024 ? ix_grid(n) : 1024, 256, 0, st>>>(d_state, d_flag, n, d_tot);
     ICK(hipGetLastError());
     ICK(hipEventRecord(e1, st));
     ICK(hipMemcpyAsync(&h_tot, d_tot, sizeof(IxTot), hipMemcpyDeviceToHost, st));
