@@ -258,6 +258,36 @@ class Scanner:
             raise (ErrInvalidCRC if rc == ERR_CRC else ScanError)(rc, "cly_index_device")
         return r
 
+    def append(self, records, tx_id=0, commit=False, active_fid=0, write_off=0, data_file_size=256 << 20):
+        """appendLogRecord over a batch from host memory (cly_append): records =
+        [(key, value, type, data_type, expiration)].  Returns ([region bytes,
+        region 0 from write_off on], [(fid, offset)], ClyAppendResult)."""
+        n = len(records)
+        keep = []
+        ri = np.zeros(max(1, n), REC_IN_DTYPE)
+        for i, (k, v, typ, dt, exp) in enumerate(records):
+            kb, vb = np.frombuffer(k, np.uint8), np.frombuffer(v, np.uint8)
+            keep += [kb, vb]
+            ri[i]["key"], ri[i]["key_len"] = (kb.ctypes.data if len(kb) else 0), len(kb)
+            ri[i]["value"], ri[i]["value_len"] = (vb.ctypes.data if len(vb) else 0), len(vb)
+            ri[i]["type"], ri[i]["data_type"], ri[i]["expiration"] = typ, dt, exp
+        r = _abi.ClyAppendResult()
+        args = (self.ctx, ri.ctypes.data, n, tx_id, 1 if commit else 0, active_fid, write_off, data_file_size)
+        rc = self.lib.cly_append(*args, None, 0, None, None, ctypes.byref(r))
+        if rc not in (0, _abi.ERR_CAPACITY):
+            raise ScanError(rc, "cly_append")
+        nreg, stride = int(r.n_out_files), int(r.out_stride)
+        out = np.zeros(max(1, nreg) * stride, np.uint8)
+        lens = (ctypes.c_uint64 * max(1, nreg))()
+        pos = np.zeros(n + 2, POS_DTYPE)
+        rc = self.lib.cly_append(*args, out.ctypes.data, nreg, lens, pos.ctypes.data, ctypes.byref(r))
+        if rc != 0:
+            raise ScanError(rc, "cly_append")
+        regions = [out[k * stride + (write_off if k == 0 else 0):k * stride + int(lens[k])].tobytes()
+                   for k in range(nreg)]
+        nt = n + (1 if commit else 0)
+        return regions, [(int(p["fid"]), int(p["offset"])) for p in pos[:nt]], r
+
     def append_device(self, d_recs, n, tx_id, commit, active_fid, write_off, data_file_size, d_out, out_max_files,
                       d_pos, stream=None):
         """Batched append (db.appendLogRecord over a batch, db.go:368-413; WriteBatch

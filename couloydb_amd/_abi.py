@@ -87,7 +87,7 @@ assert GEN_DTYPE.itemsize == 32
 
 SCAN_SYMBOLS = ["cly_ctx_create", "cly_ctx_destroy", "cly_scan_capacity", "cly_scan",
                 "cly_scan_device", "cly_merge_device", "cly_merge", "cly_hint_positions_device", "cly_hint_scan",
-                "cly_index_device", "cly_index", "cly_append_device",
+                "cly_index_device", "cly_index", "cly_append_device", "cly_append",
                 "cly_strerror", "cly_build_info"]
 GEN_SYMBOLS = ["cly_gen_record_size", "cly_gen_layout", "cly_gen_encode"]
 
@@ -148,6 +148,10 @@ def load_scan_lib(name="libclyscan.so"):
                                       ctypes.c_uint32, P(ctypes.c_uint64), ctypes.c_void_p, P(ClyAppendResult),
                                       ctypes.c_void_p]
     lib.cly_append_device.restype = ctypes.c_int
+    lib.cly_append.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int,
+                               ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32,
+                               P(ctypes.c_uint64), ctypes.c_void_p, P(ClyAppendResult)]
+    lib.cly_append.restype = ctypes.c_int
     lib.cly_strerror.argtypes = [ctypes.c_int]
     lib.cly_strerror.restype = ctypes.c_char_p
     lib.cly_build_info.argtypes = []

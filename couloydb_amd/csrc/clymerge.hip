@@ -1168,3 +1168,63 @@ done:
     if (e1) hipEventDestroy(e1);
     return rc;
 }
+
+// Host-memory entry (the cgo path of the write side): records whose key and
+// value point into host memory; the encoded bytes come back per region (region
+// 0 from write_off on: out + write_off .. out + out_file_len[0]), positions in
+// pos[n (+1)].  A query call (out = NULL) returns the region count and stride.
+extern "C" int cly_append(cly_ctx* ctx, const cly_rec_in* recs, uint64_t n, int64_t tx_id, int commit,
+                          uint32_t active_fid, uint64_t write_off, uint64_t data_file_size, uint8_t* out,
+                          uint32_t out_max_files, uint64_t* out_file_len, cly_pos* pos, cly_append_result* ar) {
+    if (!ctx || !ar || (n && !recs) || data_file_size == 0) return CLY_ERR_ARG;
+    memset(ar, 0, sizeof(*ar));
+    if (hipSetDevice(cly_ctx_device_internal(ctx)) != hipSuccess) return CLY_ERR_DEVICE;
+    hipStream_t st = cly_ctx_stream_internal(ctx);
+    int rc = CLY_OK;
+    uint64_t blob = 0;
+    for (uint64_t i = 0; i < n; i++) blob += recs[i].key_len + recs[i].value_len;
+    uint8_t* h_blob = (uint8_t*)malloc(blob + 16);
+    cly_rec_in* h_recs = (cly_rec_in*)malloc(sizeof(cly_rec_in) * (n + 1));
+    uint8_t *d_blob = nullptr, *d_out = nullptr;
+    cly_rec_in* d_recs = nullptr;
+    cly_pos* d_pos = nullptr;
+    uint64_t o = 0;
+    const uint64_t nt = n + (commit ? 1 : 0);
+    cly_append_result q;
+    MCK(hipMalloc((void**)&d_blob, blob + 16));
+    for (uint64_t i = 0; i < n; i++) {
+        h_recs[i] = recs[i];
+        if (recs[i].key_len) memcpy(h_blob + o, recs[i].key, recs[i].key_len);
+        h_recs[i].key = d_blob + o;
+        o += recs[i].key_len;
+        if (recs[i].value_len) memcpy(h_blob + o, recs[i].value, recs[i].value_len);
+        h_recs[i].value = d_blob + o;
+        o += recs[i].value_len;
+    }
+    MCK(hipMalloc((void**)&d_recs, sizeof(cly_rec_in) * (n + 1)));
+    if (blob) MCK(hipMemcpyAsync(d_blob, h_blob, blob, hipMemcpyHostToDevice, st));
+    if (n) MCK(hipMemcpyAsync(d_recs, h_recs, sizeof(cly_rec_in) * n, hipMemcpyHostToDevice, st));
+    rc = cly_append_device(ctx, d_recs, n, tx_id, commit, active_fid, write_off, data_file_size, nullptr, 0, nullptr,
+                           nullptr, &q, nullptr);
+    *ar = q;
+    if (rc != CLY_OK && rc != CLY_ERR_CAPACITY) goto done;
+    if (!out || !pos || q.n_out_files > out_max_files) { rc = CLY_ERR_CAPACITY; goto done; }
+    MCK(hipMalloc((void**)&d_out, q.out_stride * q.n_out_files));
+    MCK(hipMalloc((void**)&d_pos, sizeof(cly_pos) * (nt + 1)));
+    rc = cly_append_device(ctx, d_recs, n, tx_id, commit, active_fid, write_off, data_file_size, d_out, q.n_out_files,
+                           out_file_len, d_pos, ar, nullptr);
+    if (rc != CLY_OK) goto done;
+    for (uint32_t k = 0; k < ar->n_out_files; k++) {
+        const uint64_t from = k == 0 ? write_off : 0;
+        if (out_file_len[k] > from)
+            MCK(hipMemcpyAsync(out + k * ar->out_stride + from, d_out + k * ar->out_stride + from,
+                               out_file_len[k] - from, hipMemcpyDeviceToHost, st));
+    }
+    if (nt) MCK(hipMemcpyAsync(pos, d_pos, sizeof(cly_pos) * nt, hipMemcpyDeviceToHost, st));
+    MCK(hipStreamSynchronize(st));
+done:
+    hipStreamSynchronize(st);
+    hipFree(d_blob); hipFree(d_recs); hipFree(d_out); hipFree(d_pos);
+    free(h_blob); free(h_recs);
+    return rc;
+}

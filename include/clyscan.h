@@ -250,6 +250,13 @@ int cly_append_device(cly_ctx* ctx, const cly_rec_in* d_recs, uint64_t n, int64_
                       uint32_t active_fid, uint64_t write_off, uint64_t data_file_size,
                       uint8_t* d_out, uint32_t out_max_files, uint64_t* out_file_len, cly_pos* d_pos,
                       cly_append_result* ar, void* stream);
+/* Host-memory entry (cgo): recs[i].key/value point to host memory; region k's
+ * bytes come back at out + k*out_stride (region 0 from write_off on), the
+ * positions in pos[].  out = NULL queries n_out_files and out_stride.        */
+int cly_append(cly_ctx* ctx, const cly_rec_in* recs, uint64_t n, int64_t tx_id, int commit,
+               uint32_t active_fid, uint64_t write_off, uint64_t data_file_size,
+               uint8_t* out, uint32_t out_max_files, uint64_t* out_file_len, cly_pos* pos,
+               cly_append_result* ar);
 
 const char* cly_strerror(int code);
 

@@ -121,3 +121,14 @@ def test_gpu_append_records_larger_than_a_file(scanner):
 @pytest.mark.gpu
 def test_gpu_append_tiny_records(scanner):
     gpu_append(scanner, batch(8, 20000, tiny=True), 0, False, b"", 0, 1 << 16)
+
+
+@pytest.mark.gpu
+def test_gpu_append_host_entry(scanner):
+    """cly_append (host buffers, the cgo path) against the restatement."""
+    active = random.Random(3).randbytes(3000)
+    recs = batch(12, 1500)
+    want, wpos = py_append(recs, 99, True, active, 2500, 20000)
+    regions, pos, r = scanner.append(recs, 99, True, 7, 2500, 20000)
+    assert regions[0] == want[0][2500:] and regions[1:] == want[1:]
+    assert [(f - 7, o) for f, o in pos] == wpos and r.final_fid == 7 + len(want) - 1
