@@ -25,6 +25,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+#include <thread>
+
 #include "scan_core.h"
 
 #ifndef CLY_EXP                 // timing experiments only (tools/exp_time.py): phases skipped, results wrong
@@ -2076,6 +2079,13 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     return CLY_OK;
 }
 
+// Host-memory entry.  Inputs of at least PIPE_MIN bytes go through a
+// pipeline: the files are split into groups of >= PIPE_GROUP bytes (whole
+// files); a copy thread moves group g+1 host->device while group g is scanned
+// and its tuples travel device->host (PCIe is full duplex), so the H2D stream
+// of the file bytes sets the pace.
+#define PIPE_MIN (256ull << 20)
+#define PIPE_GROUP (512ull << 20)
 extern "C" int cly_scan(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple* out, uint64_t out_cap,
                         uint64_t* file_first, cly_file_result* res, uint64_t* needed, cly_stats* stats) {
     if (!c || (!files && nfiles) || nfiles < 0 || !res || !file_first) return CLY_ERR_ARG;
@@ -2092,40 +2102,92 @@ extern "C" int cly_scan(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
         c->cap_bytes = total + 4096;
         HIPCK(hipMalloc(&c->d_bytes, c->cap_bytes));
     }
-    cly_file* df = (cly_file*)malloc(sizeof(cly_file) * nfiles);
-    uint64_t off = 0;
-    for (int i = 0; i < nfiles; i++) {
-        df[i] = files[i];
-        df[i].base = c->d_bytes + off;
-        if (files[i].len)
-            HIPCK(hipMemcpyAsync(c->d_bytes + off, files[i].base, files[i].len, hipMemcpyHostToDevice, c->stream));
-        off += (files[i].len + 4095) & ~4095ULL;
-    }
-    const uint64_t cap = cly_scan_capacity(files, nfiles) + 16;
+    const uint64_t cap = cly_scan_capacity(files, nfiles) + 16 * (uint64_t)nfiles + 16;
     if (cap > c->cap_tuples) {
         hipFree(c->d_tuples);
         c->cap_tuples = cap;
         HIPCK(hipMalloc(&c->d_tuples, sizeof(cly_tuple) * cap));
     }
-    uint64_t slots = 0;
-    int rc = cly_scan_device(c, df, nfiles, c->d_tuples, c->cap_tuples, file_first, res, &slots, stats, nullptr);
-    free(df);
-    uint64_t need = 0;
-    for (int i = 0; i < nfiles; i++) need += res[i].n_records;
-    if (needed) *needed = rc == CLY_ERR_CAPACITY ? slots : need;
-    if (rc != CLY_OK) return rc;
-    if (need > out_cap) return CLY_ERR_CAPACITY;
-    // per-file copies: the device buffer may hold tuples past an ErrInvalidCRC
-    uint64_t o = 0;
-    for (int i = 0; i < nfiles; i++) {
-        if (res[i].n_records)
-            HIPCK(hipMemcpyAsync(out + o, c->d_tuples + file_first[i], sizeof(cly_tuple) * res[i].n_records,
-                                 hipMemcpyDeviceToHost, c->stream));
-        file_first[i] = o;
-        o += res[i].n_records;
+    cly_file* df = (cly_file*)malloc(sizeof(cly_file) * nfiles);
+    uint64_t* goff = (uint64_t*)malloc(sizeof(uint64_t) * (nfiles + 1));   // device byte offset of each file
+    {
+        uint64_t off = 0;
+        for (int i = 0; i < nfiles; i++) {
+            df[i] = files[i];
+            df[i].base = c->d_bytes + off;
+            goff[i] = off;
+            off += (files[i].len + 4095) & ~4095ULL;
+        }
+        goff[nfiles] = off;
     }
-    HIPCK(hipStreamSynchronize(c->stream));
-    return CLY_OK;
+    // groups of whole files
+    int ng = 0;
+    int* gstart = (int*)malloc(sizeof(int) * (nfiles + 1));
+    {
+        uint64_t acc = 0;
+        gstart[ng++] = 0;
+        for (int i = 0; i < nfiles; i++) {
+            acc += files[i].len;
+            if (total >= PIPE_MIN && acc >= PIPE_GROUP && i + 1 < nfiles) { gstart[ng++] = i + 1; acc = 0; }
+        }
+        gstart[ng] = nfiles;
+    }
+    // the copy thread: group after group, each fully on the device before `ready` moves on
+    std::atomic<int> ready(0), copy_err(0);
+    std::thread copier([&]() {
+        if (hipSetDevice(c->device) != hipSuccess) { copy_err = 1; ready = ng; return; }
+        for (int g = 0; g < ng; g++) {
+            for (int i = gstart[g]; i < gstart[g + 1]; i++)
+                if (files[i].len && hipMemcpy(c->d_bytes + goff[i], files[i].base, files[i].len,
+                                              hipMemcpyHostToDevice) != hipSuccess) copy_err = 1;
+            ready.store(g + 1, std::memory_order_release);
+        }
+    });
+    int rc = CLY_OK;
+    uint64_t tbase = 0, o = 0, slots_total = 0, need = 0;
+    cly_stats st_acc;
+    memset(&st_acc, 0, sizeof(st_acc));
+    for (int g = 0; g < ng && rc == CLY_OK; g++) {
+        while (ready.load(std::memory_order_acquire) <= g) std::this_thread::yield();
+        if (copy_err) { rc = CLY_ERR_DEVICE; break; }
+        const int f0 = gstart[g], nf = gstart[g + 1] - gstart[g];
+        const uint64_t gcap = cly_scan_capacity(files + f0, nf) + 16;
+        uint64_t slots = 0;
+        cly_stats sg;
+        rc = cly_scan_device(c, df + f0, nf, c->d_tuples + tbase, gcap, file_first + f0, res + f0, &slots, &sg, nullptr);
+        if (rc == CLY_ERR_CAPACITY) slots_total += slots;
+        if (rc != CLY_OK) break;
+        st_acc.scan_ms += sg.scan_ms; st_acc.resolve_ms += sg.resolve_ms; st_acc.total_ms += sg.total_ms;
+        st_acc.passes = st_acc.passes > sg.passes ? st_acc.passes : sg.passes;
+        st_acc.n_chunks += sg.n_chunks; st_acc.bytes += sg.bytes; st_acc.records += sg.records;
+        // tuples of the group's files back to host memory (per file: the slots may hold
+        // tuples past an ErrInvalidCRC), while the next group is still coming in
+        for (int i = f0; i < f0 + nf; i++) {
+            need += res[i].n_records;
+            if (need > out_cap) { rc = CLY_ERR_CAPACITY; break; }
+            if (res[i].n_records &&
+                hipMemcpyAsync(out + o, c->d_tuples + tbase + file_first[i], sizeof(cly_tuple) * res[i].n_records,
+                               hipMemcpyDeviceToHost, c->stream) != hipSuccess) { rc = CLY_ERR_DEVICE; break; }
+            file_first[i] = o;
+            o += res[i].n_records;
+        }
+        tbase += gcap;
+    }
+    if (rc != CLY_OK) ready.store(ng);            // (the copier only reads `ready`'s own stores; it finishes its groups)
+    copier.join();                                // no return before this: the copier must be joined
+    if (hipStreamSynchronize(c->stream) != hipSuccess && rc == CLY_OK) rc = CLY_ERR_DEVICE;
+    free(df); free(goff); free(gstart);
+    if (stats) *stats = st_acc;
+    if (needed) {
+        if (rc == CLY_ERR_CAPACITY) {
+            uint64_t n_all = 0;
+            for (int i = 0; i < nfiles; i++) n_all += res[i].n_records;
+            *needed = slots_total > n_all ? slots_total : n_all;
+        } else {
+            *needed = need;
+        }
+    }
+    return rc;
 }
 
 // Context accessors for the merge entries (clymerge.hip); not in the public header.
