@@ -170,3 +170,25 @@ def test_config2_device_generated_properties():
     host = wl.file_bytes(3)
     t, st_o, end = co.scan_file(host, fid)
     compare(out[first[3]:first[3] + res[3].n_records], res[3].status, res[3].end_offset, t, st_o, end, "c2 file 3")
+
+
+@pytest.mark.slow
+def test_host_entry_pipelined_c2():
+    """cly_scan over host buffers of the whole C2 configuration (4 GiB, 16
+    files: the pipelined path, several groups): tuples back in host memory
+    equal the oracle's, file by file."""
+    torch = pytest.importorskip("torch")
+    from bench import make_workload
+    wl = make_workload("c2", torch)
+    files = [DataFile(np.ascontiguousarray(wl.file_bytes(i)), fid) for i, (_, _, fid) in enumerate(wl.dev_files)]
+    with Scanner(0) as sc:
+        r = sc.scan(files)
+    assert sum(r.n_records) == wl.expect_records
+    for i, f in enumerate(files):
+        assert r.status[i] == 0 and r.end_offset[i] == len(f.data)
+        if i in (0, 7, 15):
+            t, st, end = co.scan_file(f.data, f.fid)
+            compare(r.file_tuples(i), r.status[i], r.end_offset[i], t, st, end, "host c2 file %d" % i)
+        else:
+            t = r.file_tuples(i)
+            assert (t["offset"] == np.arange(len(t), dtype=np.int64) * 276).all() and (t["fid"] == f.fid).all()
