@@ -510,12 +510,40 @@ __device__ __forceinline__ void mc_wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// n bytes (0 < n <= 16) from byte address s as 16 bytes (bytes from n on
+// undefined): only the dwords that hold one of the n bytes are loaded.
+__device__ __forceinline__ void mc_part(uint64_t s, int n, uint32_t (&w)[4]) {
+    const CLY_GLB uint32_t* wp = (const CLY_GLB uint32_t*)(s & ~3ull);
+    const uint32_t sh = (uint32_t)(s & 3);
+    const int nd = (int)((sh + (uint32_t)n + 3) >> 2);
+    uint32_t t[5];
+    #pragma unroll
+    for (int q = 0; q < 5; q++) t[q] = q < nd ? wp[q] : 0u;
+    #pragma unroll
+    for (int q = 0; q < 4; q++) w[q] = __builtin_amdgcn_alignbit(t[q + 1], t[q], sh * 8);
+}
+__device__ __forceinline__ uint32_t mc_sel(const uint32_t (&b)[4], int k) {
+    return k == 0 ? b[0] : k == 1 ? b[1] : k == 2 ? b[2] : k == 3 ? b[3] : 0u;
+}
+// 16 bytes: x[0..nA) then y[0..16-nA)
+__device__ __forceinline__ void mc_join(const uint32_t (&x)[4], const uint32_t (&y)[4], int nA, uint32_t (&o)[4]) {
+    const int m = nA >> 2, r = nA & 3;
+    #pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t hi = mc_sel(y, j - m), lo = mc_sel(y, j - m - 1);
+        const uint32_t sj = r ? __builtin_amdgcn_alignbit(hi, lo, 32 - 8 * r) : hi;     // (y << 8 nA), dword j
+        const int kb = nA - 4 * j;                                                       // bytes of x in dword j
+        const uint32_t mk = kb >= 4 ? 0xFFFFFFFFu : kb <= 0 ? 0u : (1u << (8 * kb)) - 1u;
+        o[j] = (x[j] & mk) | (sj & ~mk);
+    }
+}
+
 // Template over the descriptor capacity per block (CMAX) and the prefix stride
 // (PRE); lo0 = first byte of region 0 that belongs to the output (appends
 // continue an active file: bytes below it are kept as they are).  fstart[k]
 // is the first descriptor of region k; flen[k] the region's end offset.
-template <int CMAX, int PRE>
-__global__ void __launch_bounds__(64 * MC_W)
+template <int CMAX, int PRE, bool TWO>
+__global__ void __launch_bounds__(64 * MC_W, 4)
 k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uint32_t* __restrict__ bmap,
         const uint64_t* __restrict__ fstart, const uint64_t* __restrict__ flen, uint64_t stride,
         uint64_t nblocks, uint8_t* out, uint64_t lo0) {
@@ -551,6 +579,8 @@ k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uin
         mc_wave_sync();
         uint32_t a[MC_P][5];
         uint32_t fast = 0, gather = 0, shs = 0;
+        int st_p = -1, st_n = 0;                                // the lane's (first) two-record piece
+        uint32_t xa[4], xb[4];
         #pragma unroll
         for (int p = 0; p < MC_P; p++) {
             const int d = (p * 64 + lane) * 16;
@@ -571,9 +601,36 @@ k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uin
                 a[p][4] = (sa & 3) ? wp[4] : 0u;
                 fast |= 1u << p;
                 shs |= (uint32_t)(sa & 3) << (2 * p);
+                continue;
+            }
+            // a piece across one record boundary: the tail of record lo, the head
+            // of record lo+1 (each from its body or wholly from its prefix slot)
+            const int nA = (int)sizes[lo] - r0;
+            bool two = TWO && st_p < 0 && nA > 0 && nA < 16 && lo + 1 < (int)cnt && rel[lo + 1] == d + nA &&
+                       fo + (uint64_t)d + 16 <= L && (int)sizes[lo + 1] >= 16 - nA;
+            uint64_t sA = 0, sB = 0;
+            if (two) {
+                if (r0 >= pr) sA = srcs[lo] + (uint64_t)(r0 - pr);
+                else if (r0 + nA <= pr) sA = (uint64_t)(pre + (uint64_t)(j0 + lo) * PRE + r0);
+                else two = false;
+                const int pb = pres[lo + 1];
+                if (pb == 0) sB = srcs[lo + 1];
+                else if (pb >= 16 - nA) sB = (uint64_t)(pre + (uint64_t)(j0 + lo + 1) * PRE);
+                else two = false;
+            }
+            if (two) {
+                mc_part(sA, nA, xa);
+                mc_part(sB, 16 - nA, xb);
+                st_p = p;
+                st_n = nA;
             } else {
                 gather |= 1u << p;
             }
+        }
+        if (st_p >= 0) {
+            uint32_t o[4];
+            mc_join(xa, xb, st_n, o);
+            *(uint4*)(out + B + (st_p * 64 + lane) * 16) = make_uint4(o[0], o[1], o[2], o[3]);
         }
         #pragma unroll
         for (int p = 0; p < MC_P; p++) {
@@ -736,7 +793,7 @@ extern "C" int cly_merge_device(cly_ctx* ctx, const cly_file* files, int nfiles,
         MDBG(st, "k_mhint");
         const uint64_t wgs = (nblocks + MC_W - 1) / MC_W;
         unsigned grid = wgs < 16384 ? (unsigned)wgs : 16384u;
-        k_mcopy<M_CMAX, M_PRE><<<grid, 64 * MC_W, 0, st>>>(d_cp, d_pre, d_bmap, d_fstart, d_flen, stride, nblocks,
+        k_mcopy<M_CMAX, M_PRE, true><<<grid, 64 * MC_W, 0, st>>>(d_cp, d_pre, d_bmap, d_fstart, d_flen, stride, nblocks,
                                                           d_out, 0);
         MDBG(st, "k_mcopy");
         MCK(hipGetLastError());
@@ -1141,7 +1198,7 @@ extern "C" int cly_append_device(cly_ctx* ctx, const cly_rec_in* d_recs, uint64_
         k_dscale<<<1, 64, 0, st>>>(d_fstart, h_nout + 1);
         const uint64_t wgs = (nblocks + MC_W - 1) / MC_W;
         const unsigned cg = wgs < 16384 ? (unsigned)wgs : 16384u;
-        k_mcopy<A_CMAX, A_PRE><<<cg, 64 * MC_W, 0, st>>>(d_cp, d_pre, d_bmap, d_fstart, d_flen, stride, nblocks, d_out,
+        k_mcopy<A_CMAX, A_PRE, false><<<cg, 64 * MC_W, 0, st>>>(d_cp, d_pre, d_bmap, d_fstart, d_flen, stride, nblocks, d_out,
                                                         write_off);
     }
     MCK(hipGetLastError());
