@@ -446,10 +446,13 @@ k_mhint(const MEnt* __restrict__ e, const MCopy* __restrict__ cp, const cly_tupl
         if (j < nl && ho + hs <= hint_cap) {
             const MEnt m = e[j];
             const cly_tuple t = tup[m.tuple];
-            const int f = find_file_u64(first, nfiles, m.tuple);
-            const uint8_t* rkey = (const uint8_t*)bases[f] + t.offset + t.header_size + t.txid_len;
+            // the copy descriptor already points into the record (verbatim: its
+            // start; re-encoded: its realKey): no file lookup
+            const MCopy c = cp[j];
+            const uint8_t* rkey = c.pre ? (const uint8_t*)c.src
+                                        : (const uint8_t*)c.src + t.header_size + t.txid_len;
             const uint32_t rk = t.key_size - t.txid_len;
-            const uint64_t dst = cp[j].dst;
+            const uint64_t dst = c.dst;
             const uint64_t fid = dst / stride, off = dst - fid * stride;
             uint8_t pv[20];
             int pl = put_uv(pv, zz((int64_t)fid));
