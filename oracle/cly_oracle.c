@@ -1,11 +1,13 @@
 /*
  * cly_oracle.c — TEST INFRASTRUCTURE ONLY (see cly_oracle.h).
  *
- * Scalar CPU restatement of the CouloyDB log-record scan.  Every function cites
- * the reference lines it follows (paths relative to the CouloyDB source tree).
- * Parity status: pinned by known-answer vectors + an independent Python
- * restatement (zlib.crc32) — not by running the Go reference, which cannot be
- * built here (no Go toolchain).
+ * Scalar CPU restatement of the CouloyDB log-record scan (ReadLogRecord loop),
+ * of db.merge's rewrite (clyo_merge) and of DecodeLogRecordPos
+ * (clyo_decode_pos).  Every function cites the reference lines it follows
+ * (paths relative to the CouloyDB source tree).  Parity status: pinned by
+ * known-answer vectors + independent Python restatements (zlib.crc32;
+ * tests/gpu_util.py for merge, index and append) — not by running the Go
+ * reference, which cannot be built here (no Go toolchain).
  */
 #define _GNU_SOURCE
 #include "cly_oracle.h"
