@@ -12,6 +12,8 @@ Workloads (BASELINE.json configs):
   c2 (default): 16 files x 256 MiB, key 0x00||%09d, 256-B random values -> 276-B records
   c1: one 64 MiB file of 1 KiB values (CPU plumbing config; also runnable here)
   c3: 32 GiB, Zipf(1.1) value lengths 64 B-64 KiB
+  c5: BASELINE config 5's per-GPU share: 32 GiB of the C2/C3 mix (one fid range
+      per rank; 8 ranks = 256 GiB)
   c4: merge.go path, 32 GiB: keys 0..K-1 put, then k%4==0 overwritten and
       k%4==2 deleted (50 % of the records dead); a step = scan + merge rewrite
       (live filter, NO_TX_ID re-encode + CRC, file rotation, hint records)
@@ -69,6 +71,17 @@ def make_workload(name, torch, rank=0, device=0, seed=0x434C59, size=32 * 2**30)
         sizes = vl.astype(np.int64) + 20
         cum = np.cumsum(sizes)
         vl = vl[: int(np.searchsorted(cum, size - nfiles_target * 70000))]
+    elif name == "c5":
+        # BASELINE config 5 per GPU: a 32-GiB fid range of the C2/C3 mix (16 GiB of
+        # 256-B values, then 16 GiB of Zipf value sizes); 8 GPUs -> 256 GiB
+        rng = np.random.default_rng(seed + 5)
+        nfiles_target = 128
+        half = size // 2
+        n2 = int(half // 276)
+        vz = _zipf_lengths(int(half / 3500), rng)
+        cum = np.cumsum(vz.astype(np.int64) + 20)
+        vz = vz[: int(np.searchsorted(cum, half - 64 * 70000))]
+        vl = np.concatenate([np.full(n2, 256, np.uint32), vz])
     elif name == "c4":
         nfiles_target = 128
         K = int(size / (276 + 276 / 4 + 19 / 4))
@@ -288,7 +301,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
     ap.add_argument("--verify", action="store_true", help="check one file against the oracle after timing")
