@@ -185,8 +185,10 @@ k_ixwin(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, cons
             atomicAdd(&tot->n_coll, 1ull);
         }
         if (q + 1 < m && sh[q + 1] == sh[q]) continue;         // not the group's last
-        const GMax w = g[q];
-        if (tup[w.idx].type != 1) state[w.idx] = CLY_IX_LIVE;   // LogRecordDeleted -> key absent
+        // g == nullptr: no tx record was applied, so the application order is the
+        // scan order, which the stable sort keeps inside a group: the last wins
+        const uint32_t w = g ? g[q].idx : sidx[q];
+        if (tup[w].type != 1) state[w] = CLY_IX_LIVE;           // LogRecordDeleted -> key absent
     }
 }
 // exact resolution of a collided hash group (one thread): per distinct key the max order
@@ -286,6 +288,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     const unsigned grid = ix_grid(n);
     hipcub::CountingInputIterator<uint32_t> cnt(0);
     uint64_t m = 0, m2 = 0;
+    int hbits = 64;
     const uint64_t* d_first = nullptr;
     const uint64_t* d_bases = nullptr;
     ICK(hipEventCreate(&e0));
@@ -350,9 +353,17 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     {
         // test hook: CLY_IX_HASH_MASK (hex) narrows the key hash so that collisions
         // (resolved exactly by k_ixcoll) become common
-        uint64_t hm = ~0ull;
+        // The key hash keeps hbits = log2(n) + 24 bits (multiple of 8, 32..64):
+        // expected colliding pairs n^2 / 2^(hbits+1) <= 2^-25 n stay ~0, and the
+        // radix sort makes hbits/8 passes instead of 8.
+        int lg = 0;
+        while (lg < 63 && (1ull << lg) < n) lg++;
+        hbits = (lg + 24 + 7) & ~7;
+        if (hbits < 32) hbits = 32;
+        if (hbits > 64) hbits = 64;
+        uint64_t hm = hbits == 64 ? ~0ull : (1ull << hbits) - 1;
         const char* e = getenv("CLY_IX_HASH_MASK");
-        if (e && *e) hm = strtoull(e, nullptr, 16);
+        if (e && *e) { hm = strtoull(e, nullptr, 16); hbits = hm ? 64 - __builtin_clzll(hm) : 1; }
         k_ixapply<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_order, d_first, d_bases, nfiles, d_hash, d_flag, hm);
     }
     {
@@ -366,15 +377,15 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
         k_ixgather<<<ix_grid(m2), 256, 0, st>>>(d_hash, d_sel, m2, d_k2);
         {
             size_t tb = tmp_bytes;
-            ICK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_k2, d_txkey, d_sel, d_sidx, (int)m2, 0, 64, st));
+            ICK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_k2, d_txkey, d_sel, d_sidx, (int)m2, 0, hbits, st));
         }
-        k_ixgin<<<ix_grid(m2), 256, 0, st>>>(d_txkey, d_sidx, d_order, m2, d_g);
-        {
+        if (m) {                    // tx records: application order != scan order, arg-max per group
+            k_ixgin<<<ix_grid(m2), 256, 0, st>>>(d_txkey, d_sidx, d_order, m2, d_g);
             size_t tb = tmp_bytes;
             ICK(hipcub::DeviceScan::InclusiveScan(d_tmp, tb, d_g, d_g2, GMaxOp(), (int)m2, st));
         }
-        k_ixwin<<<ix_grid(m2), 256, 0, st>>>(d_txkey, d_sidx, d_g2, m2, d_tuples, d_first, d_bases, nfiles, d_state,
-                                             d_coll, d_tot);
+        k_ixwin<<<ix_grid(m2), 256, 0, st>>>(d_txkey, d_sidx, m ? d_g2 : nullptr, m2, d_tuples, d_first, d_bases,
+                                             nfiles, d_state, d_coll, d_tot);
         ICK(hipMemcpyAsync(&h_tot, d_tot, sizeof(IxTot), hipMemcpyDeviceToHost, st));
         ICK(hipStreamSynchronize(st));
         if (h_tot.n_coll)
