@@ -33,6 +33,10 @@ extern "C" hipStream_t cly_ctx_stream_internal(cly_ctx* c);
 extern "C" int cly_ctx_device_internal(cly_ctx* c);
 
 #define IX_NONE 0xFFFFFFFFFFFFFFFFull
+// record index of a hash-sorted entry: bit 31 carries "LogRecordDeleted" so that
+// the winner's type needs no second (random) read of its tuple
+#define IX_DEL 0x80000000u
+#define IXI(x) ((x) & 0x7fffffffu)
 enum { K_NONE = 0, K_APPLY = 1, K_TXDATA = 2, K_COMMIT = 3, K_ROLLBACK = 4, K_HOST = 5, K_HOSTTX = 6 };
 
 __device__ __forceinline__ int ix_file(const uint64_t* first, int nfiles, uint64_t i) {
@@ -129,7 +133,7 @@ k_ixtx(const uint32_t* __restrict__ sidx, const uint8_t* __restrict__ cls, uint6
 __global__ void __launch_bounds__(256)
 k_ixapply(const cly_tuple* __restrict__ tup, uint64_t n, const uint8_t* __restrict__ cls, uint64_t* order,
           const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases, int nfiles, uint64_t* hash,
-          uint8_t* flag, uint64_t hash_mask) {
+          uint8_t* flag, uint8_t* del, uint64_t hash_mask) {
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         const uint8_t c = cls[i];
         if (c == K_APPLY) order[i] = (i << 32) | i;
@@ -141,6 +145,7 @@ k_ixapply(const cly_tuple* __restrict__ tup, uint64_t n, const uint8_t* __restri
             uint32_t len;
             const uint8_t* k = ix_rkey(bases, ix_file(first, nfiles, i), t, len);
             hash[i] = ix_hash(t.data_type, k, len) & hash_mask;
+            del[i] = t.type == 1;
         }
     }
 }
@@ -156,7 +161,7 @@ __global__ void __launch_bounds__(256)
 k_ixgin(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, const uint64_t* __restrict__ order,
         uint64_t m, GMax* g) {
     for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < m; q += (uint64_t)gridDim.x * 256) {
-        const uint32_t i = sidx[q];
+        const uint32_t i = IXI(sidx[q]);
         g[q] = GMax{sh[q], order[i], i, (uint32_t)q};
     }
 }
@@ -178,7 +183,7 @@ k_ixwin(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, cons
         const cly_tuple* __restrict__ tup, const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases,
         int nfiles, uint8_t* state, uint8_t* coll, IxTot* tot) {
     for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < m; q += (uint64_t)gridDim.x * 256) {
-        if (q > 0 && sh[q] == sh[q - 1] && !ix_same_key(tup, first, bases, nfiles, sidx[q], sidx[q - 1])) {
+        if (q > 0 && sh[q] == sh[q - 1] && !ix_same_key(tup, first, bases, nfiles, IXI(sidx[q]), IXI(sidx[q - 1]))) {
             uint64_t h0 = q;
             while (h0 > 0 && sh[h0 - 1] == sh[q]) h0--;
             coll[h0] = 1;
@@ -187,8 +192,9 @@ k_ixwin(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, cons
         if (q + 1 < m && sh[q + 1] == sh[q]) continue;         // not the group's last
         // g == nullptr: no tx record was applied, so the application order is the
         // scan order, which the stable sort keeps inside a group: the last wins
-        const uint32_t w = g ? g[q].idx : sidx[q];
-        if (tup[w].type != 1) state[w] = CLY_IX_LIVE;           // LogRecordDeleted -> key absent
+        const uint32_t w = g ? g[q].idx : IXI(sidx[q]);
+        const bool deleted = g ? tup[w].type == 1 : (sidx[q] & IX_DEL) != 0;
+        if (!deleted) state[w] = CLY_IX_LIVE;                   // LogRecordDeleted -> key absent
     }
 }
 // exact resolution of a collided hash group (one thread): per distinct key the max order
@@ -200,13 +206,14 @@ k_ixcoll(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, con
     if (q0 >= m || !coll[q0]) return;
     uint64_t q1 = q0 + 1;
     while (q1 < m && sh[q1] == sh[q0]) q1++;
-    for (uint64_t a = q0; a < q1; a++) state[sidx[a]] = CLY_IX_DEAD;
+    for (uint64_t a = q0; a < q1; a++) state[IXI(sidx[a])] = CLY_IX_DEAD;
     for (uint64_t a = q0; a < q1; a++) {
+        const uint32_t ia = IXI(sidx[a]);
         bool best = true;
         for (uint64_t b = q0; b < q1 && best; b++)
-            if (b != a && order[sidx[b]] > order[sidx[a]] &&
-                ix_same_key(tup, first, bases, nfiles, sidx[a], sidx[b])) best = false;
-        if (best && tup[sidx[a]].type != 1) state[sidx[a]] = CLY_IX_LIVE;
+            if (b != a && order[IXI(sidx[b])] > order[ia] &&
+                ix_same_key(tup, first, bases, nfiles, ia, IXI(sidx[b]))) best = false;
+        if (best && tup[ia].type != 1) state[ia] = CLY_IX_LIVE;
     }
 }
 // counts: one atomic per workgroup and counter (a wave-level atomic on one
@@ -247,6 +254,16 @@ k_ixgather(const uint64_t* __restrict__ src, const uint32_t* __restrict__ sel, u
     for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < m; p += (uint64_t)gridDim.x * 256)
         dst[p] = src[sel[p]];
 }
+// hash keys of the applied records and their indices with the IX_DEL bit
+__global__ void __launch_bounds__(256)
+k_ixgatherd(const uint64_t* __restrict__ src, const uint32_t* __restrict__ sel, const uint8_t* __restrict__ del,
+            uint64_t m, uint64_t* dst, uint32_t* selv) {
+    for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < m; p += (uint64_t)gridDim.x * 256) {
+        const uint32_t i = sel[p];
+        dst[p] = src[i];
+        selv[p] = i | (del[i] ? IX_DEL : 0u);
+    }
+}
 
 // ---------------------------------------------------------------------------
 #define ICK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
@@ -275,7 +292,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     h_fb[nfiles] = n;
     uint64_t *d_fb = nullptr, *d_txkey = nullptr, *d_k2 = nullptr, *d_order = nullptr, *d_hash = nullptr;
     uint32_t *d_sel = nullptr, *d_sidx = nullptr;
-    uint8_t *d_cls = nullptr, *d_flag = nullptr, *d_coll = nullptr;
+    uint8_t *d_cls = nullptr, *d_flag = nullptr, *d_coll = nullptr, *d_del = nullptr;
     TxNext *d_rev = nullptr, *d_nxt = nullptr;
     GMax *d_g = nullptr, *d_g2 = nullptr;
     IxTot* d_tot = nullptr;
@@ -301,6 +318,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     ICK(hipMalloc((void**)&d_cls, n));
     ICK(hipMalloc((void**)&d_flag, n));
     ICK(hipMalloc((void**)&d_coll, n));
+    ICK(hipMalloc((void**)&d_del, n));
     ICK(hipMalloc((void**)&d_txkey, sizeof(uint64_t) * n));
     ICK(hipMalloc((void**)&d_k2, sizeof(uint64_t) * n));
     ICK(hipMalloc((void**)&d_order, sizeof(uint64_t) * n));
@@ -364,7 +382,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
         uint64_t hm = hbits == 64 ? ~0ull : (1ull << hbits) - 1;
         const char* e = getenv("CLY_IX_HASH_MASK");
         if (e && *e) { hm = strtoull(e, nullptr, 16); hbits = hm ? 64 - __builtin_clzll(hm) : 1; }
-        k_ixapply<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_order, d_first, d_bases, nfiles, d_hash, d_flag, hm);
+        k_ixapply<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_order, d_first, d_bases, nfiles, d_hash, d_flag, d_del, hm);
     }
     {
         size_t tb = tmp_bytes;
@@ -374,10 +392,11 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     ICK(hipStreamSynchronize(st));
     m2 = h_nsel;
     if (m2) {
-        k_ixgather<<<ix_grid(m2), 256, 0, st>>>(d_hash, d_sel, m2, d_k2);
+        uint32_t* d_selv = (uint32_t*)d_rev;                  // free after the tx phase (n x 16 B)
+        k_ixgatherd<<<ix_grid(m2), 256, 0, st>>>(d_hash, d_sel, d_del, m2, d_k2, d_selv);
         {
             size_t tb = tmp_bytes;
-            ICK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_k2, d_txkey, d_sel, d_sidx, (int)m2, 0, hbits, st));
+            ICK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_k2, d_txkey, d_selv, d_sidx, (int)m2, 0, hbits, st));
         }
         if (m) {                    // tx records: application order != scan order, arg-max per group
             k_ixgin<<<ix_grid(m2), 256, 0, st>>>(d_txkey, d_sidx, d_order, m2, d_g);
@@ -410,7 +429,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
 done:
     hipStreamSynchronize(st);
     {
-        void* bufs[] = {d_fb, d_tot, d_nsel, d_cls, d_flag, d_coll, d_txkey, d_k2, d_order, d_hash, d_sel, d_sidx,
+        void* bufs[] = {d_fb, d_tot, d_nsel, d_cls, d_flag, d_coll, d_del, d_txkey, d_k2, d_order, d_hash, d_sel, d_sidx,
                         d_rev, d_nxt, d_g, d_g2, d_tmp};
         for (void* b : bufs) if (b) hipFree(b);
     }
