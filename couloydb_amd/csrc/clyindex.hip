@@ -72,12 +72,27 @@ __device__ __forceinline__ uint64_t ix_hash(uint32_t index_kind, const uint8_t* 
     return h;
 }
 
-struct IxTot { unsigned long long n_live, n_applied, n_host, n_coll; uint32_t bad, _pad; };
+struct IxTot { unsigned long long n_live, n_applied, n_host, n_coll, n_tx, n_now; uint32_t bad, _pad; };
+
+// sum of a and b over the workgroup (256 threads), one atomic per counter
+__device__ __forceinline__ void ix_wg_add2(unsigned long long a, unsigned long long b, unsigned long long* da,
+                                           unsigned long long* db) {
+    __shared__ unsigned long long sh[2][4];
+    for (int d = 32; d >= 1; d >>= 1) { a += __shfl_xor(a, d, 64); b += __shfl_xor(b, d, 64); }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sh[0][w] = a; sh[1][w] = b; }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        const unsigned long long v = sh[threadIdx.x][0] + sh[threadIdx.x][1] + sh[threadIdx.x][2] + sh[threadIdx.x][3];
+        if (v) atomicAdd(threadIdx.x == 0 ? da : db, v);
+    }
+}
 
 // class of each record; the index kind of an applied record: String 0, ListMeta 3
 __global__ void __launch_bounds__(256)
 k_ixclass(const cly_tuple* __restrict__ tup, uint64_t n, uint8_t* cls, uint8_t* state, uint64_t* txkey,
-          IxTot* tot) {
+          uint8_t* txflag, IxTot* tot) {
+    unsigned long long ntx = 0, nnow = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         const cly_tuple t = tup[i];
         uint8_t c = K_NONE, s = CLY_IX_DEAD;
@@ -93,7 +108,12 @@ k_ixclass(const cly_tuple* __restrict__ tup, uint64_t n, uint8_t* cls, uint8_t* 
         cls[i] = c;
         state[i] = s;
         txkey[i] = (uint64_t)t.tx_id;
+        const bool tx = c == K_TXDATA || c == K_COMMIT || c == K_ROLLBACK || c == K_HOSTTX;
+        txflag[i] = tx;
+        ntx += tx;
+        nnow += c == K_APPLY;
     }
+    ix_wg_add2(ntx, nnow, &tot->n_tx, &tot->n_now);
 }
 
 // per tx record (sorted by txId, scan order within): element of the segmented
@@ -243,13 +263,6 @@ k_ixcount(const uint8_t* __restrict__ state, const uint8_t* __restrict__ flag, u
 }
 
 __global__ void __launch_bounds__(256)
-k_ixtxflag(const uint8_t* __restrict__ cls, uint64_t n, uint8_t* flag) {
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-        const uint8_t k = cls[i];
-        flag[i] = k == K_TXDATA || k == K_COMMIT || k == K_ROLLBACK || k == K_HOSTTX;
-    }
-}
-__global__ void __launch_bounds__(256)
 k_ixgather(const uint64_t* __restrict__ src, const uint32_t* __restrict__ sel, uint64_t m, uint64_t* dst) {
     for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < m; p += (uint64_t)gridDim.x * 256)
         dst[p] = src[sel[p]];
@@ -259,7 +272,7 @@ __global__ void __launch_bounds__(256)
 k_ixgatherd(const uint64_t* __restrict__ src, const uint32_t* __restrict__ sel, const uint8_t* __restrict__ del,
             uint64_t m, uint64_t* dst, uint32_t* selv) {
     for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < m; p += (uint64_t)gridDim.x * 256) {
-        const uint32_t i = sel[p];
+        const uint32_t i = sel ? sel[p] : (uint32_t)p;        // sel == nullptr: every record is applied
         dst[p] = src[i];
         selv[p] = i | (del[i] ? IX_DEL : 0u);
     }
@@ -344,16 +357,17 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     ICK(hipMemsetAsync(d_order, 0xff, sizeof(uint64_t) * n, st));
     ICK(hipMemsetAsync(d_coll, 0, n, st));
     ICK(hipEventRecord(e0, st));
-    k_ixclass<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_state, d_txkey, d_tot);
+    k_ixclass<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_state, d_txkey, d_flag, d_tot);
+    ICK(hipMemcpyAsync(&h_tot, d_tot, sizeof(IxTot), hipMemcpyDeviceToHost, st));
+    ICK(hipStreamSynchronize(st));
     // ---- transactions: tx records sorted by txId (stable: scan order within a txId)
-    k_ixtxflag<<<grid, 256, 0, st>>>(d_cls, n, d_flag);
-    {
+    if (h_tot.n_tx) {
         size_t tb = tmp_bytes;
         ICK(hipcub::DeviceSelect::Flagged(d_tmp, tb, cnt, d_flag, d_sel, d_nsel, (int)n, st));
+        ICK(hipMemcpyAsync(&h_nsel, d_nsel, sizeof(h_nsel), hipMemcpyDeviceToHost, st));
+        ICK(hipStreamSynchronize(st));
+        m = h_nsel;
     }
-    ICK(hipMemcpyAsync(&h_nsel, d_nsel, sizeof(h_nsel), hipMemcpyDeviceToHost, st));
-    ICK(hipStreamSynchronize(st));
-    m = h_nsel;
     if (m) {
         k_ixgather<<<ix_grid(m), 256, 0, st>>>(d_txkey, d_sel, m, d_k2);
         {
@@ -384,16 +398,18 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
         if (e && *e) { hm = strtoull(e, nullptr, 16); hbits = hm ? 64 - __builtin_clzll(hm) : 1; }
         k_ixapply<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_order, d_first, d_bases, nfiles, d_hash, d_flag, d_del, hm);
     }
-    {
+    if (m == 0 && h_tot.n_now == n) {
+        m2 = n;                                                 // every record applied: no select
+    } else {
         size_t tb = tmp_bytes;
         ICK(hipcub::DeviceSelect::Flagged(d_tmp, tb, cnt, d_flag, d_sel, d_nsel, (int)n, st));
+        ICK(hipMemcpyAsync(&h_nsel, d_nsel, sizeof(h_nsel), hipMemcpyDeviceToHost, st));
+        ICK(hipStreamSynchronize(st));
+        m2 = h_nsel;
     }
-    ICK(hipMemcpyAsync(&h_nsel, d_nsel, sizeof(h_nsel), hipMemcpyDeviceToHost, st));
-    ICK(hipStreamSynchronize(st));
-    m2 = h_nsel;
     if (m2) {
         uint32_t* d_selv = (uint32_t*)d_rev;                  // free after the tx phase (n x 16 B)
-        k_ixgatherd<<<ix_grid(m2), 256, 0, st>>>(d_hash, d_sel, d_del, m2, d_k2, d_selv);
+        k_ixgatherd<<<ix_grid(m2), 256, 0, st>>>(d_hash, m2 == n ? nullptr : d_sel, d_del, m2, d_k2, d_selv);
         {
             size_t tb = tmp_bytes;
             ICK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_k2, d_txkey, d_selv, d_sidx, (int)m2, 0, hbits, st));
