@@ -72,6 +72,57 @@ __device__ __forceinline__ uint64_t ix_hash(uint32_t index_kind, const uint8_t* 
     return h;
 }
 
+// Key signature (16 B): the first min(len, 15) realKey bytes, zero-padded, and
+// in byte 15 the length (len <= 15) or 0x80 (longer), with the data type in
+// bits 4-6.  Injective for keys of <= 15 bytes, so two such records name the
+// same key iff their signatures are equal; equal signatures of longer keys
+// still need the byte comparison.  k_ixwin reads one 16-B signature per sorted
+// record instead of two tuples and two keys.
+#define IX_SIG_LONG 0x80u
+// ix_hash and the signature together.  A key of <= 15 bytes comes in as at most
+// five aligned dword loads (none past the dword of its last byte) joined by
+// alignbyte; the hash is ix_hash's, computed from those words.
+__device__ __forceinline__ uint64_t ix_hash_sig(uint32_t kind, const uint8_t* k, uint32_t len, uint4& sig) {
+    uint32_t v[4];
+    uint64_t h;
+    if (len <= 15) {
+        const uintptr_t a = (uintptr_t)k;
+        const uint32_t* base = (const uint32_t*)(a & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(a & 3);
+        const uint32_t nd = (sh + len + 3) >> 2;
+        uint32_t d[5];
+        #pragma unroll
+        for (int j = 0; j < 5; j++) d[j] = (uint32_t)j < nd ? base[j] : 0u;
+        #pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t w = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+            const uint32_t lo = 4u * i;
+            const uint32_t m = len >= lo + 4 ? 0xffffffffu : (len <= lo ? 0u : (1u << (8 * (len - lo))) - 1u);
+            v[i] = w & m;
+        }
+        h = 0xcbf29ce484222325ull ^ ((uint64_t)kind << 56) ^ len;
+        uint64_t tail = v[0] | ((uint64_t)v[1] << 32);
+        if (len >= 8) {
+            h = (h ^ tail) * 0x100000001b3ull;
+            h ^= h >> 29;
+            tail = v[2] | ((uint64_t)v[3] << 32);
+        }
+        h = (h ^ tail) * 0x100000001b3ull;
+        h ^= h >> 32;
+        h *= 0xd6e8feb86659fd93ull;
+        h ^= h >> 32;
+    } else {
+        h = ix_hash(kind, k, len);
+        #pragma unroll
+        for (int i = 0; i < 4; i++)
+            v[i] = k[4 * i] | ((uint32_t)k[4 * i + 1] << 8) | ((uint32_t)k[4 * i + 2] << 16) |
+                   (i < 3 ? (uint32_t)k[4 * i + 3] << 24 : 0u);
+    }
+    sig = make_uint4(v[0], v[1], v[2], v[3] | (((len <= 15 ? len : IX_SIG_LONG) | ((kind & 7u) << 4)) << 24));
+    return h;
+}
+__device__ __forceinline__ bool ix_sig_long(const uint4& s) { return (s.w >> 24) & IX_SIG_LONG; }
+
 struct IxTot { unsigned long long n_live, n_applied, n_host, n_coll, n_tx, n_now; uint32_t bad, _pad; };
 
 // sum of a and b over the workgroup (256 threads), one atomic per counter
@@ -153,7 +204,7 @@ k_ixtx(const uint32_t* __restrict__ sidx, const uint8_t* __restrict__ cls, uint6
 __global__ void __launch_bounds__(256)
 k_ixapply(const cly_tuple* __restrict__ tup, uint64_t n, const uint8_t* __restrict__ cls, uint64_t* order,
           const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases, int nfiles, uint64_t* hash,
-          uint8_t* flag, uint8_t* del, uint64_t hash_mask) {
+          uint8_t* flag, uint8_t* del, uint4* ksig, uint64_t hash_mask) {
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         const uint8_t c = cls[i];
         if (c == K_APPLY) order[i] = (i << 32) | i;
@@ -164,8 +215,10 @@ k_ixapply(const cly_tuple* __restrict__ tup, uint64_t n, const uint8_t* __restri
             const cly_tuple t = tup[i];
             uint32_t len;
             const uint8_t* k = ix_rkey(bases, ix_file(first, nfiles, i), t, len);
-            hash[i] = ix_hash(t.data_type, k, len) & hash_mask;
+            uint4 sg;
+            hash[i] = ix_hash_sig(t.data_type, k, len, sg) & hash_mask;
             del[i] = t.type == 1;
+            ksig[i] = sg;
         }
     }
 }
@@ -201,9 +254,16 @@ __device__ __forceinline__ bool ix_same_key(const cly_tuple* tup, const uint64_t
 __global__ void __launch_bounds__(256)
 k_ixwin(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, const GMax* __restrict__ g, uint64_t m,
         const cly_tuple* __restrict__ tup, const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases,
-        int nfiles, uint8_t* state, uint8_t* coll, IxTot* tot) {
+        int nfiles, const uint4* __restrict__ ksig, uint8_t* state, uint8_t* coll, IxTot* tot) {
     for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < m; q += (uint64_t)gridDim.x * 256) {
-        if (q > 0 && sh[q] == sh[q - 1] && !ix_same_key(tup, first, bases, nfiles, IXI(sidx[q]), IXI(sidx[q - 1]))) {
+        bool differ = false;
+        if (q > 0 && sh[q] == sh[q - 1]) {
+            const uint32_t a = IXI(sidx[q]), b = IXI(sidx[q - 1]);
+            const uint4 sa = ksig[a], sb = ksig[b];
+            differ = sa.x != sb.x || sa.y != sb.y || sa.z != sb.z || sa.w != sb.w;
+            if (!differ && ix_sig_long(sa)) differ = !ix_same_key(tup, first, bases, nfiles, a, b);
+        }
+        if (differ) {
             uint64_t h0 = q;
             while (h0 > 0 && sh[h0 - 1] == sh[q]) h0--;
             coll[h0] = 1;
@@ -306,6 +366,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     uint64_t *d_fb = nullptr, *d_txkey = nullptr, *d_k2 = nullptr, *d_order = nullptr, *d_hash = nullptr;
     uint32_t *d_sel = nullptr, *d_sidx = nullptr;
     uint8_t *d_cls = nullptr, *d_flag = nullptr, *d_coll = nullptr, *d_del = nullptr;
+    uint4* d_ksig = nullptr;
     TxNext *d_rev = nullptr, *d_nxt = nullptr;
     GMax *d_g = nullptr, *d_g2 = nullptr;
     IxTot* d_tot = nullptr;
@@ -332,6 +393,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     ICK(hipMalloc((void**)&d_flag, n));
     ICK(hipMalloc((void**)&d_coll, n));
     ICK(hipMalloc((void**)&d_del, n));
+    ICK(hipMalloc((void**)&d_ksig, sizeof(uint4) * n));
     ICK(hipMalloc((void**)&d_txkey, sizeof(uint64_t) * n));
     ICK(hipMalloc((void**)&d_k2, sizeof(uint64_t) * n));
     ICK(hipMalloc((void**)&d_order, sizeof(uint64_t) * n));
@@ -396,7 +458,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
         uint64_t hm = hbits == 64 ? ~0ull : (1ull << hbits) - 1;
         const char* e = getenv("CLY_IX_HASH_MASK");
         if (e && *e) { hm = strtoull(e, nullptr, 16); hbits = hm ? 64 - __builtin_clzll(hm) : 1; }
-        k_ixapply<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_order, d_first, d_bases, nfiles, d_hash, d_flag, d_del, hm);
+        k_ixapply<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_order, d_first, d_bases, nfiles, d_hash, d_flag, d_del, d_ksig, hm);
     }
     if (m == 0 && h_tot.n_now == n) {
         m2 = n;                                                 // every record applied: no select
@@ -420,7 +482,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
             ICK(hipcub::DeviceScan::InclusiveScan(d_tmp, tb, d_g, d_g2, GMaxOp(), (int)m2, st));
         }
         k_ixwin<<<ix_grid(m2), 256, 0, st>>>(d_txkey, d_sidx, m ? d_g2 : nullptr, m2, d_tuples, d_first, d_bases,
-                                             nfiles, d_state, d_coll, d_tot);
+                                             nfiles, d_ksig, d_state, d_coll, d_tot);
         ICK(hipMemcpyAsync(&h_tot, d_tot, sizeof(IxTot), hipMemcpyDeviceToHost, st));
         ICK(hipStreamSynchronize(st));
         if (h_tot.n_coll)
@@ -445,7 +507,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
 done:
     hipStreamSynchronize(st);
     {
-        void* bufs[] = {d_fb, d_tot, d_nsel, d_cls, d_flag, d_coll, d_del, d_txkey, d_k2, d_order, d_hash, d_sel, d_sidx,
+        void* bufs[] = {d_fb, d_tot, d_nsel, d_cls, d_flag, d_coll, d_del, d_ksig, d_txkey, d_k2, d_order, d_hash, d_sel, d_sidx,
                         d_rev, d_nxt, d_g, d_g2, d_tmp};
         for (void* b : bufs) if (b) hipFree(b);
     }
