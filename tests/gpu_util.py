@@ -156,18 +156,28 @@ def py_merge(file_bytes, tuples_per_file, live, data_file_size):
     return [bytes(x) for x in outs], bytes(hint)
 
 
-def merge_corpus(seed, n_keys=300, rounds=3, tx_frac=0.3):
+def varlen_key(k):
+    """Keys of 0..40 bytes: short ones (<= 15 B) repeat across k (more
+    overwrites), long ones share their first 15 bytes and differ after."""
+    n = k % 41
+    if n <= 15:
+        return (b"k%014d" % (k % 97))[:n]
+    return (b"0123456789abcde" + b"%026d" % k)[:n]
+
+
+def merge_corpus(seed, n_keys=300, rounds=3, tx_frac=0.3, key_fn=None):
     """A String-key workload with overwrites, deletes, committed and rolled-back
     transactions (the shapes db.Put/Del/WriteBatch produce) -> record bytes."""
     rng = random.Random(seed)
+    key_of = key_fn or mg.test_key
     b = bytearray()
     txid = 1000
     for r in range(rounds):
         for k in rng.sample(range(n_keys), n_keys * 2 // 3):
-            key = mg.test_key(k)
+            key = key_of(k)
             if rng.random() < tx_frac:
                 txid += 1
-                ops = [(key, rng.random() < 0.2)] + [(mg.test_key(rng.randrange(n_keys)), False)
+                ops = [(key, rng.random() < 0.2)] + [(key_of(rng.randrange(n_keys)), False)
                                                      for _ in range(rng.randrange(0, 3))]
                 for kk, dele in ops:
                     b += mg.encode_record(mg.key_tx(kk, txid), b"" if dele else rng.randbytes(rng.randrange(0, 300)),

@@ -72,6 +72,20 @@ def test_gpu_index_forced_collisions(scanner, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("tx_frac,mask", [(0.0, None), (0.0, "f"), (0.3, None), (0.3, "f")])
+def test_gpu_index_key_lengths(scanner, monkeypatch, tx_frac, mask):
+    """Keys of 0..40 bytes (the 16-B key signature is exact up to 15 bytes; longer
+    keys sharing their first 15 bytes need the byte comparison), without tx
+    records (scan order = application order) and with them, with the natural
+    hash and with a 4-bit one that puts most keys in one group."""
+    from .gpu_util import varlen_key
+    if mask:
+        monkeypatch.setenv("CLY_IX_HASH_MASK", mask)
+    b = merge_corpus(21, n_keys=600, rounds=4, tx_frac=tx_frac, key_fn=varlen_key)
+    gpu_vs_restatement(scanner, split_files(b, 3, random.Random(21)))
+
+
+@pytest.mark.gpu
 def test_gpu_index_device_c4_shape():
     """C4 shape (k%4==0 overwritten, k%4==2 deleted) at 600 MiB through the
     device entry: the index's live records are exactly the workload's live mask."""
