@@ -123,6 +123,20 @@ __device__ __forceinline__ uint64_t ix_hash_sig(uint32_t kind, const uint8_t* k,
 }
 __device__ __forceinline__ bool ix_sig_long(const uint4& s) { return (s.w >> 24) & IX_SIG_LONG; }
 
+// hash, signature and tombstone bit of applied record i; returns the bit
+__device__ __forceinline__ bool ix_apply_one(const cly_tuple& t, uint64_t i, const uint64_t* first,
+                                             const uint64_t* bases, int nfiles, uint64_t* hash, uint8_t* del,
+                                             uint4* ksig, uint64_t hash_mask) {
+    uint32_t len;
+    const uint8_t* k = ix_rkey(bases, ix_file(first, nfiles, i), t, len);
+    uint4 sg;
+    hash[i] = ix_hash_sig(t.data_type, k, len, sg) & hash_mask;
+    const bool dl = t.type == 1;
+    del[i] = dl;
+    ksig[i] = sg;
+    return dl;
+}
+
 struct IxTot { unsigned long long n_live, n_applied, n_host, n_coll, n_tx, n_now; uint32_t bad, _pad; };
 
 // sum of a and b over the workgroup (256 threads), one atomic per counter
@@ -142,7 +156,9 @@ __device__ __forceinline__ void ix_wg_add2(unsigned long long a, unsigned long l
 // class of each record; the index kind of an applied record: String 0, ListMeta 3
 __global__ void __launch_bounds__(256)
 k_ixclass(const cly_tuple* __restrict__ tup, uint64_t n, uint8_t* cls, uint8_t* state, uint64_t* txkey,
-          uint8_t* txflag, IxTot* tot) {
+          uint8_t* txflag, IxTot* tot, const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases,
+          int nfiles, uint64_t* order, uint64_t* hash, uint8_t* apflag, uint8_t* del, uint4* ksig, uint32_t* selv,
+          uint64_t hash_mask) {
     unsigned long long ntx = 0, nnow = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         const cly_tuple t = tup[i];
@@ -163,6 +179,14 @@ k_ixclass(const cly_tuple* __restrict__ tup, uint64_t n, uint8_t* cls, uint8_t* 
         txflag[i] = tx;
         ntx += tx;
         nnow += c == K_APPLY;
+        // a record without a txId is applied now: order = scan order, its hash,
+        // signature and tombstone bit come from this same pass over the tuples
+        if (c == K_APPLY) {
+            order[i] = (i << 32) | i;
+            const bool dl = ix_apply_one(t, i, first, bases, nfiles, hash, del, ksig, hash_mask);
+            selv[i] = (uint32_t)i | (dl ? IX_DEL : 0u);
+        }
+        apflag[i] = c == K_APPLY;
     }
     ix_wg_add2(ntx, nnow, &tot->n_tx, &tot->n_now);
 }
@@ -202,24 +226,13 @@ k_ixtx(const uint32_t* __restrict__ sidx, const uint8_t* __restrict__ cls, uint6
 }
 // applied records (now and at commit): order, hash
 __global__ void __launch_bounds__(256)
-k_ixapply(const cly_tuple* __restrict__ tup, uint64_t n, const uint8_t* __restrict__ cls, uint64_t* order,
-          const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases, int nfiles, uint64_t* hash,
-          uint8_t* flag, uint8_t* del, uint4* ksig, uint64_t hash_mask) {
+k_ixapply(const cly_tuple* __restrict__ tup, uint64_t n, const uint8_t* __restrict__ cls,
+          const uint64_t* __restrict__ order, const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases,
+          int nfiles, uint64_t* hash, uint8_t* apflag, uint8_t* del, uint4* ksig, uint64_t hash_mask) {
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-        const uint8_t c = cls[i];
-        if (c == K_APPLY) order[i] = (i << 32) | i;
-        const uint64_t o = order[i];
-        const bool ap = (c == K_APPLY || c == K_TXDATA) && o != IX_NONE;
-        flag[i] = ap;
-        if (ap) {
-            const cly_tuple t = tup[i];
-            uint32_t len;
-            const uint8_t* k = ix_rkey(bases, ix_file(first, nfiles, i), t, len);
-            uint4 sg;
-            hash[i] = ix_hash_sig(t.data_type, k, len, sg) & hash_mask;
-            del[i] = t.type == 1;
-            ksig[i] = sg;
-        }
+        if (cls[i] != K_TXDATA || order[i] == IX_NONE) continue;   // K_APPLY: done by k_ixclass
+        ix_apply_one(tup[i], i, first, bases, nfiles, hash, del, ksig, hash_mask);
+        apflag[i] = 1;
     }
 }
 // arg-max of the order per hash group (segmented, forward)
@@ -332,7 +345,7 @@ __global__ void __launch_bounds__(256)
 k_ixgatherd(const uint64_t* __restrict__ src, const uint32_t* __restrict__ sel, const uint8_t* __restrict__ del,
             uint64_t m, uint64_t* dst, uint32_t* selv) {
     for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < m; p += (uint64_t)gridDim.x * 256) {
-        const uint32_t i = sel ? sel[p] : (uint32_t)p;        // sel == nullptr: every record is applied
+        const uint32_t i = sel[p];
         dst[p] = src[i];
         selv[p] = i | (del[i] ? IX_DEL : 0u);
     }
@@ -365,8 +378,10 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     h_fb[nfiles] = n;
     uint64_t *d_fb = nullptr, *d_txkey = nullptr, *d_k2 = nullptr, *d_order = nullptr, *d_hash = nullptr;
     uint32_t *d_sel = nullptr, *d_sidx = nullptr;
-    uint8_t *d_cls = nullptr, *d_flag = nullptr, *d_coll = nullptr, *d_del = nullptr;
+    uint8_t *d_cls = nullptr, *d_flag = nullptr, *d_coll = nullptr, *d_del = nullptr, *d_apflag = nullptr;
     uint4* d_ksig = nullptr;
+    uint32_t* d_selv = nullptr;
+    uint64_t hm = ~0ull;
     TxNext *d_rev = nullptr, *d_nxt = nullptr;
     GMax *d_g = nullptr, *d_g2 = nullptr;
     IxTot* d_tot = nullptr;
@@ -393,6 +408,8 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     ICK(hipMalloc((void**)&d_flag, n));
     ICK(hipMalloc((void**)&d_coll, n));
     ICK(hipMalloc((void**)&d_del, n));
+    ICK(hipMalloc((void**)&d_apflag, n));
+    ICK(hipMalloc((void**)&d_selv, sizeof(uint32_t) * n));
     ICK(hipMalloc((void**)&d_ksig, sizeof(uint4) * n));
     ICK(hipMalloc((void**)&d_txkey, sizeof(uint64_t) * n));
     ICK(hipMalloc((void**)&d_k2, sizeof(uint64_t) * n));
@@ -419,7 +436,23 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     ICK(hipMemsetAsync(d_order, 0xff, sizeof(uint64_t) * n, st));
     ICK(hipMemsetAsync(d_coll, 0, n, st));
     ICK(hipEventRecord(e0, st));
-    k_ixclass<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_state, d_txkey, d_flag, d_tot);
+    {
+        // The key hash keeps hbits = log2(n) + 24 bits (multiple of 8, 32..64):
+        // expected colliding pairs n^2 / 2^(hbits+1) <= 2^-25 n stay ~0, and the
+        // radix sort makes hbits/8 passes instead of 8.
+        int lg = 0;
+        while (lg < 63 && (1ull << lg) < n) lg++;
+        hbits = (lg + 24 + 7) & ~7;
+        if (hbits < 32) hbits = 32;
+        if (hbits > 64) hbits = 64;
+        hm = hbits == 64 ? ~0ull : (1ull << hbits) - 1;
+        // test hook: CLY_IX_HASH_MASK (hex) narrows the key hash so that collisions
+        // (resolved exactly by k_ixcoll) become common
+        const char* e = getenv("CLY_IX_HASH_MASK");
+        if (e && *e) { hm = strtoull(e, nullptr, 16); hbits = hm ? 64 - __builtin_clzll(hm) : 1; }
+    }
+    k_ixclass<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_state, d_txkey, d_flag, d_tot, d_first, d_bases, nfiles,
+                                    d_order, d_hash, d_apflag, d_del, d_ksig, d_selv, hm);
     ICK(hipMemcpyAsync(&h_tot, d_tot, sizeof(IxTot), hipMemcpyDeviceToHost, st));
     ICK(hipStreamSynchronize(st));
     // ---- transactions: tx records sorted by txId (stable: scan order within a txId)
@@ -434,9 +467,10 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
         k_ixgather<<<ix_grid(m), 256, 0, st>>>(d_txkey, d_sel, m, d_k2);
         {
             size_t tb = tmp_bytes;
-            ICK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_k2, d_hash, d_sel, d_sidx, (int)m, 0, 64, st));
+            // sorted txIds into d_txkey (free after the gather; d_hash holds k_ixclass's hashes)
+            ICK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_k2, d_txkey, d_sel, d_sidx, (int)m, 0, 64, st));
         }
-        k_ixtxin<<<ix_grid(m), 256, 0, st>>>(d_hash, d_sidx, d_cls, m, d_rev);
+        k_ixtxin<<<ix_grid(m), 256, 0, st>>>(d_txkey, d_sidx, d_cls, m, d_rev);
         {
             size_t tb = tmp_bytes;
             ICK(hipcub::DeviceScan::InclusiveScan(d_tmp, tb, d_rev, d_nxt, TxNextOp(), (int)m, st));
@@ -444,37 +478,28 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
         k_ixtx<<<ix_grid(m), 256, 0, st>>>(d_sidx, d_cls, m, d_nxt, d_order, d_state);
     }
     // ---- applied records: hash, sort, winner per key
-    {
-        // test hook: CLY_IX_HASH_MASK (hex) narrows the key hash so that collisions
-        // (resolved exactly by k_ixcoll) become common
-        // The key hash keeps hbits = log2(n) + 24 bits (multiple of 8, 32..64):
-        // expected colliding pairs n^2 / 2^(hbits+1) <= 2^-25 n stay ~0, and the
-        // radix sort makes hbits/8 passes instead of 8.
-        int lg = 0;
-        while (lg < 63 && (1ull << lg) < n) lg++;
-        hbits = (lg + 24 + 7) & ~7;
-        if (hbits < 32) hbits = 32;
-        if (hbits > 64) hbits = 64;
-        uint64_t hm = hbits == 64 ? ~0ull : (1ull << hbits) - 1;
-        const char* e = getenv("CLY_IX_HASH_MASK");
-        if (e && *e) { hm = strtoull(e, nullptr, 16); hbits = hm ? 64 - __builtin_clzll(hm) : 1; }
-        k_ixapply<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_order, d_first, d_bases, nfiles, d_hash, d_flag, d_del, d_ksig, hm);
-    }
+    // (records without a txId were hashed by k_ixclass; committed tx data here)
+    if (m) k_ixapply<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_order, d_first, d_bases, nfiles, d_hash, d_apflag,
+                                           d_del, d_ksig, hm);
     if (m == 0 && h_tot.n_now == n) {
         m2 = n;                                                 // every record applied: no select
     } else {
         size_t tb = tmp_bytes;
-        ICK(hipcub::DeviceSelect::Flagged(d_tmp, tb, cnt, d_flag, d_sel, d_nsel, (int)n, st));
+        ICK(hipcub::DeviceSelect::Flagged(d_tmp, tb, cnt, d_apflag, d_sel, d_nsel, (int)n, st));
         ICK(hipMemcpyAsync(&h_nsel, d_nsel, sizeof(h_nsel), hipMemcpyDeviceToHost, st));
         ICK(hipStreamSynchronize(st));
         m2 = h_nsel;
     }
     if (m2) {
-        uint32_t* d_selv = (uint32_t*)d_rev;                  // free after the tx phase (n x 16 B)
-        k_ixgatherd<<<ix_grid(m2), 256, 0, st>>>(d_hash, m2 == n ? nullptr : d_sel, d_del, m2, d_k2, d_selv);
+        // every record applied now: k_ixclass wrote the sort input in place;
+        // otherwise gather the selected records' hashes and indices
+        const bool ident = m == 0 && m2 == n;
+        uint32_t* d_vin = ident ? d_selv : (uint32_t*)d_rev;    // d_rev is free after the tx phase
+        if (!ident) k_ixgatherd<<<ix_grid(m2), 256, 0, st>>>(d_hash, d_sel, d_del, m2, d_k2, d_vin);
         {
             size_t tb = tmp_bytes;
-            ICK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_k2, d_txkey, d_selv, d_sidx, (int)m2, 0, hbits, st));
+            ICK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, ident ? d_hash : d_k2, d_txkey, d_vin, d_sidx, (int)m2,
+                                                   0, hbits, st));
         }
         if (m) {                    // tx records: application order != scan order, arg-max per group
             k_ixgin<<<ix_grid(m2), 256, 0, st>>>(d_txkey, d_sidx, d_order, m2, d_g);
@@ -489,7 +514,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
             k_ixcoll<<<(unsigned)((m2 + 63) / 64), 64, 0, st>>>(d_txkey, d_sidx, d_order, m2, d_coll, d_tuples, d_first,
                                                                 d_bases, nfiles, d_state);
     }
-    k_ixcount<<<ix_grid(n) < 1024 ? ix_grid(n) : 1024, 256, 0, st>>>(d_state, d_flag, n, d_tot);
+    k_ixcount<<<ix_grid(n) < 1024 ? ix_grid(n) : 1024, 256, 0, st>>>(d_state, d_apflag, n, d_tot);
     ICK(hipGetLastError());
     ICK(hipEventRecord(e1, st));
     ICK(hipMemcpyAsync(&h_tot, d_tot, sizeof(IxTot), hipMemcpyDeviceToHost, st));
@@ -507,7 +532,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
 done:
     hipStreamSynchronize(st);
     {
-        void* bufs[] = {d_fb, d_tot, d_nsel, d_cls, d_flag, d_coll, d_del, d_ksig, d_txkey, d_k2, d_order, d_hash, d_sel, d_sidx,
+        void* bufs[] = {d_fb, d_tot, d_nsel, d_cls, d_flag, d_coll, d_del, d_apflag, d_selv, d_ksig, d_txkey, d_k2, d_order, d_hash, d_sel, d_sidx,
                         d_rev, d_nxt, d_g, d_g2, d_tmp};
         for (void* b : bufs) if (b) hipFree(b);
     }
