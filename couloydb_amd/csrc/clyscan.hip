@@ -1243,6 +1243,9 @@ __device__ __forceinline__ SubDesc make_desc(const Sub& T, const Chain& R) {
 
 // One sub-tile, start to end, for a chain given by (mode, entry) or, mode < 0,
 // by its own guess (mode -2: test mode, odd sub-tiles take a wrong guess).
+#ifndef CLY_SCHED
+#define CLY_SCHED "default"
+#endif
 #ifndef CLY_SRC_HASH
 #define CLY_SRC_HASH "unknown"
 #endif
@@ -2241,7 +2244,7 @@ extern "C" const char* cly_strerror(int code) {
 
 extern "C" const char* cly_build_info(void) {
     static char buf[200];
-    snprintf(buf, sizeof(buf), "clyscan gfx950 SUB=%d WAVES=%d TS=%d CAP=%d LDS=%d tables=16x src=%s", CLY_SUB, CLY_NDW,
-             CLY_TS, CLY_CAP, (int)CLY_SCAN_LDS, CLY_SRC_HASH);
+    snprintf(buf, sizeof(buf), "clyscan gfx950 SUB=%d WAVES=%d TS=%d CAP=%d LDS=%d tables=16x sched=%s src=%s", CLY_SUB,
+             CLY_NDW, CLY_TS, CLY_CAP, (int)CLY_SCAN_LDS, CLY_SCHED, CLY_SRC_HASH);
     return buf;
 }
