@@ -728,6 +728,7 @@ template <bool OBSERVE>
 __device__ __forceinline__ void crc_loop(const CLY_LDS uint8_t* smem, const uint32_t* d, int rs, uint64_t chk,
                                          uint32_t lane_off, uint32_t& s_out, uint32_t& obs_out, uint32_t& err_out) {
     uint32_t s = 0, obs = 0, err = 0;
+    const uint32_t chk_lo = (uint32_t)chk, chk_hi = (uint32_t)(chk >> 32);
 #if CLY_CRC_XB
     const CrcLane cl = crc_lane((int)__lane_id());
 #endif
@@ -742,7 +743,10 @@ __device__ __forceinline__ void crc_loop(const CLY_LDS uint8_t* smem, const uint
         s = crc_word(smem, x, lane_off);
 #endif
         if (OBSERVE) {
-            const uint32_t m = (uint32_t)(-(int32_t)((chk >> i) & 1));
+            // all-ones when word i holds a check point: one v_bfe_i32 (and the
+            // AND-OR below fuses) instead of and + cmp + cndmask per word
+            const uint32_t cw = i < 32 ? chk_lo : chk_hi;
+            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int32_t)cw, (uint32_t)(i & 31), 1u);
             err |= s & m;
         }
     }
