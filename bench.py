@@ -160,6 +160,9 @@ def measured_traffic(config):
     return best
 
 
+MT_THREADS = 16                 # the GPU box's CPU share per GPU
+
+
 def cpu_baseline(wl, budget_s=12.0):
     """Oracle (C restatement) on the host cores over a bounded sample of the same
     workload: 'ref-algorithm' single thread over whole files; 'ref-faithful' =
@@ -178,6 +181,18 @@ def cpu_baseline(wl, budget_s=12.0):
         files.append(i)
         i += 1
     alg_gibs = nbytes / t_alg / 2**30
+    # the same restatement with the files spread over MT_THREADS threads (the
+    # box's CPU share), over the first (up to) MT_THREADS sampled files
+    mt_files = files[:MT_THREADS]
+    mt_arrs = [wl.file_bytes(i) for i in mt_files]
+    t0 = time.perf_counter()
+    mt_rec = int(co.scan_files_mt(mt_arrs, [wl.dev_files[i][2] for i in mt_files], MT_THREADS))
+    t_mt = time.perf_counter() - t0
+    mt_bytes = sum(len(a) for a in mt_arrs)
+    del mt_arrs
+    multi = {"value": round(mt_bytes / t_mt / 2**30, 4), "unit": "GiB/s", "cores": MT_THREADS,
+             "mrecords_per_s": round(mt_rec / t_mt / 1e6, 3),
+             "sample": "%d files (%.2f GiB), one file per thread, clyo_scan_files_mt" % (len(mt_files), mt_bytes / 2**30)}
     merge_part = None
     if wl.name == "c4":
         # scan + merge rewrite of the sampled files (file i's live bytes follow the
@@ -211,6 +226,7 @@ def cpu_baseline(wl, budget_s=12.0):
                              "mrecords_per_s": round(nf / tf / 1e6, 4),
                              "sample": "first %d records of one file; per record fstat + 2x (open, mmap whole file, copy, munmap)" % nf},
             "host_nproc": os.cpu_count(),
+            "multi_thread": multi,
             **({"value": merge_part["value"], "sample": merge_part["sample"], "scan_only_value": round(alg_gibs, 4)}
                if merge_part else {})}
 
