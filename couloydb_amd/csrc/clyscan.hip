@@ -9,16 +9,25 @@
 // (data/logRecord.go:86-114), GetLogRecordCRC (data/logRecord.go:136-146) and
 // parseLogRecordKey (db.go:706-710).
 //
-// Launches per call (one HIP stream):
-//   k_scan  persistent, one workgroup per CU: CLY_NDW data waves + 1 coordinator
-//           wave.  Units (CLY_NDW sub-tiles of 64 stripes) are taken in ticket
-//           order; each data wave stages one sub-tile in LDS, speculates and
-//           resolves its record chain, checks every CRC and emits tuples; the
-//           coordinator composes the unit, runs the decoupled look-back over
-//           unit descriptors and hands out exact entries and output slots.
-//   k_fin   one workgroup per file: CRC of records that straddle sub-tiles, and
-//           the file's first event (ErrInvalidCRC / io.EOF variants / panics).
-// Design and data layout: DESIGN.md.
+// Layout: every file is cut into chunks of CLY_CH bytes, one
+// per lane; 64 consecutive chunks of a file are a tile, one per wave.
+//
+// k_scan (persistent, tiles in ticket order), per tile:
+//   A  each lane finds the first record start of its chunk (SWAR candidate
+//      filter over its bytes, then a walk of header gathers that must leave the
+//      chunk at a plausible header), and walks its records to the chunk end;
+//      the wave makes the lanes' chains agree (lane l+1 starts where lane l's
+//      chain leaves), re-walking exactly where they do not;
+//   L  decoupled look-back over tile descriptors: the chain state and record
+//      count entering the tile; a tile whose guessed entry is wrong re-resolves;
+//   C  every lane streams its chunk through a slicing-by-4 CRC register from
+//      HBM (16-B loads, 128 B per burst), re-walks its records, writes their
+//      tuples straight to their output slots and XORs one combined patch per
+//      record into the stream, so that the register of the whole file ends at
+//      zero iff every record's CRC matches; the tile's register is folded
+//      in-wave.
+// k_fin (one workgroup per file): folds the tile registers of the file and
+// checks it; k_locate (only when a file fails) finds the first bad record.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -30,1172 +39,86 @@
 
 #include "scan_core.h"
 
-#ifndef CLY_EXP                 // timing experiments only (tools/exp_time.py): phases skipped, results wrong
-#define CLY_EXP 0
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef unsigned long long u64;
+
+#define NONE32 0xFFFFFFFFu       // no position
+#define TERM_NONE 127            // the chain leaves the chunk (no terminal inside)
+#define LM_NONE 0                // no record starts in the chunk (the chain passes through it)
+#define LM_CHAIN 1               // the chain enters the chunk at E (a record start or its terminal)
+#define LM_DEAD 2                // the file's chain ended before the chunk
+#define LM_OFF 3                 // chunk beyond the end of the file
+#define NO_EV 0xFFFFu            // empty event slot
+#ifdef CLY_DEBUG
+#define DBG(...) do { if ((threadIdx.x & 63) == 0) printf(__VA_ARGS__); } while (0)
+#else
+#define DBG(...)
 #endif
-#define CLY_KS_LEVELS 6                          // Kogge-Stone levels over 64 lanes
-#define MODE_EMPTY 0                             // sub-tile beyond the end of its file
-#define MODE_NORMAL 1                            // the chain enters (or ends) inside the sub-tile
-#define MODE_PASS 2                              // one record covers the whole sub-tile
-#define MODE_DEAD 3                              // the file's chain ended in an earlier sub-tile
 
 struct DevFile {                 // 32 B
     const uint8_t* base;         // device pointer to the file's first byte (16-B aligned)
     uint64_t len;
     uint32_t fid;
-    uint32_t first_sub;          // global index of the file's first sub-tile
-    uint32_t nsub;               // sub-tiles of the file (>= 1)
+    uint32_t first_tile;         // global index of the file's first tile
+    uint32_t ntile;              // tiles of the file (>= 1)
     uint32_t _pad;
 };
+
+struct FileInfo {                // per file, zeroed per call (fail_key: all ones)
+    uint64_t first_index;        // global tuple index of the file's first record
+    uint64_t end_index;          // global index after the file's last record
+    uint32_t term_pos;           // terminal position T of the file's chain
+    int32_t  term_status;
+    uint32_t term_tile;          // global tile index holding T
+    uint32_t term_lane;
+    uint32_t expect;             // value the folded register must have (see k_fin)
+    uint32_t has_term;
+    u64      fail_key;           // (offset << 32) | index in file of the first CRC failure (k_locate)
+    uint32_t fold;               // k_fin: the folded register
+    uint32_t ok;                 // k_fin: fold == expect
+};
+
+// Tile descriptor: LOCAL (from the tile's own speculation) and INCL (the true
+// state after the tile), each published by its flag word, written last.
+struct TileDesc { u64 l[4]; u64 i[4]; };
+// l[0]: bit0 published | bit1 the chain ends in the tile | bit2 no chunk of the tile
+//       holds a boundary | bit3 first tile of its file | bit4 a record starts in the
+//       tile | records << 32
+// l[1]: G (the tile's guessed entry: its first boundary) | exit or terminal position << 32
+// l[2]: crc_last | P_last << 32 (last record start in the tile and its stored CRC)
+// l[3]: the smallest entry that passes the whole tile (tile end, or len + 1 for
+//       the tile holding the file's end)
+// i[0]: bit0 published | bit1 the file's chain ended | records before the next tile << 16
+// i[1]: X (chain position after the tile) | crc_last << 32
+// i[2]: P_last (start of the last record before the next tile, NONE32 if none)
+#define DF_PUB 1ull
+#define DF_TERM 2ull
+#define DF_NONE 4ull
+#define DF_FOF 8ull
+#define DF_REC 16ull
 
 struct Globals {                 // zeroed per call
     uint32_t ticket;
     uint32_t overflow;           // tuples beyond out_cap were dropped
-    uint32_t lb_timeout;         // a look-back / mailbox spin hit its bound (never expected)
-    uint32_t fail;               // an internal invariant was violated (never expected)
-    uint64_t total;              // tuple slots used (records + any past an ErrInvalidCRC)
-    uint32_t nfix;               // fix list length (this round)
-    uint32_t fix_total;          // statistics: all fixes of the call
-    uint32_t ncand;              // sub-tiles whose chain disagrees with the link (this round)
-    uint32_t novf;               // sub-tiles with more tuples than their staging slot
-    uint64_t prof[24];           // profiling build (-DCLY_PROF): summed cycles per phase
-};
-
-#ifdef CLY_PROF
-#define PROF_INIT() uint64_t prof_t = __builtin_amdgcn_s_memtime(); uint64_t prof_acc[12] = {0,0,0,0,0,0,0,0,0,0,0,0}
-#define PROF(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); prof_acc[i] += t_ - prof_t; prof_t = t_; } while (0)
-#define PROF_FLUSH(base) do { if (lane == 0) for (int i_ = 0; i_ < 6; i_++) atomicAdd((unsigned long long*)&g->prof[(base) + i_], (unsigned long long)prof_acc[i_]); } while (0)
-#else
-#define PROF_INIT()
-#define PROF(i)
-#define PROF_FLUSH(base)
-#endif
-
-struct SubDbg {                  // debug trace of one sub-tile (cly_dbg_enable)
-    int32_t mode, E, cnt, term, tst, last, lterm, eof_exit, k0, guess, bad, bpos;
-    int64_t tpos, xrel;
-};
-
-struct FileOut {
-    uint64_t n_records;
-    int64_t  end_offset;
-    int32_t  status;
-    int32_t  ok;
-    uint64_t first_index;
+    uint32_t fail;               // internal invariant / spin bound (never expected)
+    uint32_t refix;              // tiles whose guessed entry the look-back corrected
+    uint32_t slow_lanes;         // lanes that took the exact (slow) CRC path
+    uint32_t any_fail;           // a file's CRC fold failed (k_locate needed)
+    uint64_t total;              // records over all files
 };
 
 // ---------------------------------------------------------------------------
-// LDS layout of k_scan / k_fix (dynamic shared memory, byte offsets)
-//   [0, 65536)        CRC slicing-by-4 tables T0..T3, 16 replicas: dword
-//                     (i*64 + t*16 + r) = T_t[i] (replica r); lane l reads replica
-//                     l & 15, so one lookup instruction touches 16 banks x 2 lanes
-//   [65536, +256)     inverse of a zero-byte step (top byte of T0 -> index)
-//   [LDS_WIN + k*WIN) window of wave k (sub-tile + halo, zero past the file end)
-//   [LDS_POOL ...)    per-wave check-point pools
-//   [LDS_KSNIB ...)   nibble tables of the Kogge-Stone shifts A^(SUB*2^k): 8 x 16 words each
-//   then nibble tables of A^(4b), b < 6, and A^(24a), a < HS_A: A^(4w) = A^(4b) A^(24a), w = 6a + b
-#define LDS_TAB 0
+// LDS of k_scan / k_locate (static: compile-time offsets)
+//   [0, 65536)     CRC slicing-by-4 tables T0..T3, 16 replicas: dword (i*64 + t*16 + r)
+//   [65536, +256)  inverse of a zero-byte step (top byte of T0 -> index)
+//   [65792, ...)   nibble tables of A^(CLY_CH * 2^k), k < 7 (8 x 16 words each)
 #define LDS_INV 65536
-#define LDS_WIN (LDS_INV + 256)
-#define LDS_POOL (LDS_WIN + CLY_NDW * CLY_WIN)
-#define LDS_KSNIB (LDS_POOL + CLY_NDW * 192 * 8)
-#define HS_A ((CLY_NWD + 5) / 6)
-#define NIB_HSB (CLY_KS_LEVELS * 128)                             // word offsets from LDS_KSNIB
-#define NIB_HSA (NIB_HSB + 6 * 128)
-#define CLY_COLS (NIB_HSA + HS_A * 128)                           // words of the shift tables
-#define CLY_SCAN_LDS (LDS_KSNIB + CLY_COLS * 4)
+#define LDS_NIB (LDS_INV + 256)
+#define NIB_LEVELS 7                     // A^(CLY_CH * 2^k), k < 7 (k = 6: one tile)
+#define SCAN_LDS (LDS_NIB + NIB_LEVELS * 128 * 4)
 
-// Per-sub-tile result of k_scan / k_fix, read by the link scan (16 B).
-struct SubDesc {
-    int64_t  x;                  // global chain position after the sub-tile (MODE_NORMAL, not terminated)
-    uint32_t cnt;                // records of the sub-tile under its chain
-    int16_t  entry;              // sub-tile-relative entry of the chain (MODE_NORMAL)
-    uint8_t  mode;               // MODE_NORMAL / MODE_PASS / MODE_DEAD
-    uint8_t  flags;              // SD_*
-};
-#define SD_TERM 1                // the chain ends inside the sub-tile (incl. at the end of the file)
-#define SD_FOF 2                 // first sub-tile of its file
-#define SD_OVF 4                 // more tuples than the staging slot holds: k_place emits them from the data
-#define CLY_CAP 64               // tuples per sub-tile staging slot
-
-// Link-scan element: what a run of sub-tiles does to the chain state, for
-// each state it can be entered in (br[0]: chain live, br[1]: chain already
-// ended in this file).  A guessed chain counts only when entered live; the
-// first sub-tile of a file resets the state whatever it was.
-struct LinkBr {
-    int64_t  x;                  // chain position after the run (set)
-    uint64_t cnt;                // records the run adds
-    int32_t  set;                // the run fixes the state (else: passes it through)
-    int32_t  term;               // ... to ended
-};
-struct LinkAgg { LinkBr br[2]; };
-struct Fix {                     // a sub-tile whose chain disagrees with the state the link gives it
-    uint32_t s;
-    int32_t  mode, entry;        // the chain that state implies (mode < 0: not determined yet)
-    uint32_t file;
-    int64_t  x_in;               // chain position entering the sub-tile
-    uint32_t certain;            // the state is certain (no wrong chain before it in the file)
-    uint32_t _pad;
-};
-#define LISTED_U 0x80000000u     // listed[s] = stamp: certain fix or walked; stamp | LISTED_U: uncertain fix
-static_assert(CLY_SCAN_LDS <= 163840, "LDS budget");
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-// ---------------------------------------------------------------------------
-// small helpers
-__device__ __forceinline__ uint64_t ld_agent(const unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(unsigned long long* p, uint64_t v) {
-    __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int lds_ld_acq(const CLY_LDS int32_t* p) {
-    const int v = *(const volatile CLY_LDS int32_t*)p;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    return v;
-}
-__device__ __forceinline__ void lds_st_rel(CLY_LDS int32_t* p, int v) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    *(volatile CLY_LDS int32_t*)p = v;
-}
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-__device__ __forceinline__ int wave_min(int v) {
-    #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ int wave_max(int v) {
-    #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ int scan_max_incl(int v, int lane) {
-    #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) { const int u = __shfl_up(v, o, 64); if (lane >= o) v = max(v, u); }
-    return v;
-}
-__device__ __forceinline__ uint32_t scan_add_incl(uint32_t v, int lane) {
-    #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) { const uint32_t u = __shfl_up(v, o, 64); if (lane >= o) v += u; }
-    return v;
-}
-__device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t s) {
-    return __builtin_amdgcn_alignbyte(hi, lo, s);
-}
-// 4 bytes at LDS byte position p (any alignment)
-__device__ __forceinline__ uint32_t lds_le32(const CLY_LDS uint32_t* w32, int p) {
-    return alignb(w32[(p >> 2) + 1], w32[p >> 2], p & 3);
-}
-// struct copies to / from LDS (word by word: no generic-pointer flat access)
-template <class T> __device__ __forceinline__ T lds_get(const CLY_LDS T* p) {
-    static_assert(sizeof(T) % 4 == 0, "word-sized");
-    T v;
-    uint32_t* d = (uint32_t*)&v;
-    const CLY_LDS uint32_t* q = (const CLY_LDS uint32_t*)p;
-    #pragma unroll
-    for (int i = 0; i < (int)(sizeof(T) / 4); i++) d[i] = q[i];
-    return v;
-}
-template <class T> __device__ __forceinline__ void lds_put(CLY_LDS T* p, const T& v) {
-    const uint32_t* d = (const uint32_t*)&v;
-    CLY_LDS uint32_t* q = (CLY_LDS uint32_t*)p;
-    #pragma unroll
-    for (int i = 0; i < (int)(sizeof(T) / 4); i++) q[i] = d[i];
-}
-#define LDS_SPIN_MAX (1u << 26)
-#define LB_SPIN_MAX (1u << 24)
-
-// Wait until *p >= v (LDS mailbox), bounded.
-__device__ __forceinline__ bool lds_wait_ge(const CLY_LDS int32_t* p, int v, Globals* g) {
-    uint32_t n = 0;
-    while (lds_ld_acq(p) < v) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++n > LDS_SPIN_MAX) { atomicOr(&g->lb_timeout, 2u); return false; }
-    }
-    return true;
-}
-
-// ---------------------------------------------------------------------------
-// CRC-32 table step on a 4-byte word: s' = T3[x0]^T2[x1]^T1[x2]^T0[x3] where
-// x = s ^ data.  Lookup address = (byte << 8) | lane_off via one v_perm;
-// the table number goes into the ds_read offset field.
-__device__ __forceinline__ uint32_t tab_addr(uint32_t x, uint32_t lane_off, uint32_t k) {
-    return __builtin_amdgcn_perm(x, lane_off, 0x0c0c0000u | ((4u + k) << 8));
-}
-__device__ __forceinline__ uint32_t crc_word(const CLY_LDS uint8_t* smem, uint32_t x, uint32_t lane_off) {
-    const uint32_t a0 = tab_addr(x, lane_off, 0), a1 = tab_addr(x, lane_off, 1);
-    const uint32_t a2 = tab_addr(x, lane_off, 2), a3 = tab_addr(x, lane_off, 3);
-    const uint32_t t3 = *(const CLY_LDS uint32_t*)(smem + a0 + 3 * 64);
-    const uint32_t t2 = *(const CLY_LDS uint32_t*)(smem + a1 + 2 * 64);
-    const uint32_t t1 = *(const CLY_LDS uint32_t*)(smem + a2 + 1 * 64);
-    const uint32_t t0 = *(const CLY_LDS uint32_t*)(smem + a3 + 0 * 64);
-    return t3 ^ t2 ^ t1 ^ t0;
-}
-// Bank-conflict-free form of crc_word for the main loop.  Table slot k of
-// byte row v sits at v*256 + k*64 + replica*4 (replica = lane & 15), so for
-// ds_read_b32 (banks (a/4) mod 32 per 32-lane group) lanes l and l+16 hit the
-// same bank whenever they read the same slot.  Here lookup i of lanes with
-// bit 4 set reads slot i^1 instead of slot i (with the byte that slot takes):
-// the two half-groups always read slots 16 banks apart.
-#ifndef CLY_CRC_XB
-#define CLY_CRC_XB 1
-#endif
-struct CrcLane { uint32_t oe, oo, s0, s1, s2, s3; };
-__device__ __forceinline__ CrcLane crc_lane(int lane) {
-    const uint32_t r4 = (uint32_t)(lane & 15) * 4, h = (uint32_t)(lane >> 4) & 1u;
-    CrcLane c;
-    c.oe = r4 + 64 * h;                      // even lookups: offset field i*64
-    c.oo = r4 + 64 * (1 - h);                // odd lookups: offset field (i-1)*64
-    // lookup i reads slot i^h, which takes byte 3 - (i^h) of x
-    c.s0 = 0x0c0c0000u | ((4u + (3u - (0u ^ h))) << 8);
-    c.s1 = 0x0c0c0000u | ((4u + (3u - (1u ^ h))) << 8);
-    c.s2 = 0x0c0c0000u | ((4u + (3u - (2u ^ h))) << 8);
-    c.s3 = 0x0c0c0000u | ((4u + (3u - (3u ^ h))) << 8);
-    return c;
-}
-__device__ __forceinline__ uint32_t crc_word_xb(const CLY_LDS uint8_t* smem, uint32_t x, const CrcLane& c) {
-    const uint32_t a0 = __builtin_amdgcn_perm(x, c.oe, c.s0), a1 = __builtin_amdgcn_perm(x, c.oo, c.s1);
-    const uint32_t a2 = __builtin_amdgcn_perm(x, c.oe, c.s2), a3 = __builtin_amdgcn_perm(x, c.oo, c.s3);
-    const uint32_t t0 = *(const CLY_LDS uint32_t*)(smem + a0);
-    const uint32_t t1 = *(const CLY_LDS uint32_t*)(smem + a1);
-    const uint32_t t2 = *(const CLY_LDS uint32_t*)(smem + a2 + 128);
-    const uint32_t t3 = *(const CLY_LDS uint32_t*)(smem + a3 + 128);
-    return t0 ^ t1 ^ t2 ^ t3;
-}
-// one byte through the register (table T0, replica of lane_off)
-__device__ __forceinline__ uint32_t crc_byte(const CLY_LDS uint8_t* smem, uint32_t s, uint32_t b, uint32_t lane_off) {
-    const uint32_t i = (s ^ b) & 0xff;
-    return *(const CLY_LDS uint32_t*)(smem + ((i << 8) | lane_off)) ^ (s >> 8);
-}
-// inverse of one zero-byte step: s = A^-1 s'
-__device__ __forceinline__ uint32_t crc_unbyte(const CLY_LDS uint8_t* smem, uint32_t s, uint32_t lane_off) {
-    const uint32_t i = smem[LDS_INV + (s >> 24)];
-    const uint32_t t = *(const CLY_LDS uint32_t*)(smem + ((i << 8) | lane_off));
-    return ((s ^ t) << 8) | i;
-}
-
-// M v for a linear map M given by its nibble tables (word offset `off` from
-// LDS_KSNIB: 8 x 16 words, entry n*16+k = M (k << 4n)): 8 lookups
-__device__ __forceinline__ uint32_t nib_mul(const CLY_LDS uint8_t* smem, int off, uint32_t v) {
-    const CLY_LDS uint32_t* t = (const CLY_LDS uint32_t*)(smem + LDS_KSNIB) + off;
-    uint32_t p = 0;
-    #pragma unroll
-    for (int n = 0; n < 8; n++) p ^= t[n * 16 + ((v >> (4 * n)) & 15u)];
-    return p;
-}
-// A^(SUB*2^lvl) v
-__device__ __forceinline__ uint32_t ks_mul(const CLY_LDS uint8_t* smem, int lvl, uint32_t v) {
-    return nib_mul(smem, lvl * 128, v);
-}
-// A^(4w) v, w < NWD
-__device__ __forceinline__ uint32_t word_shift(const CLY_LDS uint8_t* smem, int w, uint32_t v) {
-    const int a = w / 6, b = w - 6 * a;
-    return nib_mul(smem, NIB_HSB + b * 128, nib_mul(smem, NIB_HSA + a * 128, v));
-}
-
-// ---------------------------------------------------------------------------
-// Header decode at window position p: fast path for headers whose three
-// varints are at most 4 bytes each and end within bytes 6..13 (every record
-// the writer produces except multi-byte expirations / huge sizes), else the
-// exact byte-loop form step_hdr.
-__device__ __noinline__ void hdr_slow(const CLY_LDS uint8_t* w8, int64_t p, int64_t nrel, int64_t p_abs, Hdr& h) {
-    h = step_hdr(w8, p, nrel, p_abs);
-}
-__device__ __forceinline__ uint32_t pack7(uint32_t s) {
-    return (s & 0x7fu) | ((s >> 1) & 0x3f80u) | ((s >> 2) & 0x1fc000u) | ((s >> 3) & 0xfe00000u);
-}
-__device__ __forceinline__ Hdr hdr_at(const CLY_LDS uint32_t* w32, int p, int64_t nrel, int64_t p_abs) {
-    int64_t m = nrel - p;
-    if (m > 26) m = 26;
-    if (m >= 14) {
-        const int wi = p >> 2;
-        const uint32_t s = p & 3;
-        const uint32_t a0 = w32[wi], a1 = w32[wi + 1], a2 = w32[wi + 2], a3 = w32[wi + 3], a4 = w32[wi + 4];
-        const uint32_t h0 = alignb(a1, a0, s), h1 = alignb(a2, a1, s), h2 = alignb(a3, a2, s), h3 = alignb(a4, a3, s);
-        const uint32_t lo = alignb(h2, h1, 2), hi = alignb(h3, h2, 2);       // bytes 6..9, 10..13
-        const uint64_t W = ((uint64_t)hi << 32) | lo;
-        const uint64_t T = ~W & 0x8080808080808080ull;
-        const uint64_t T2 = T & (T - 1), T3 = T2 & (T2 - 1);
-        const int e1 = __builtin_ctzll(T | (1ull << 63)) >> 3;
-        const int e2 = __builtin_ctzll(T2 | (1ull << 63)) >> 3;
-        const int e3 = __builtin_ctzll(T3 | (1ull << 63)) >> 3;
-        const int n1 = e1 + 1, n2 = e2 - e1, n3 = e3 - e2;
-        if (T3 != 0 && n1 <= 4 && n2 <= 4 && n3 <= 4 && 6 + e3 < m) {
-            const uint32_t u1 = pack7((uint32_t)W) & ((1u << (7 * n1)) - 1);
-            const uint32_t u2 = pack7((uint32_t)(W >> (8 * n1))) & ((1u << (7 * n2)) - 1);
-            const uint32_t u3 = pack7((uint32_t)(W >> (8 * (e2 + 1)))) & ((1u << (7 * n3)) - 1);
-            const int32_t v1 = (int32_t)(u1 >> 1) ^ -(int32_t)(u1 & 1);
-            const int32_t v2 = (int32_t)(u2 >> 1) ^ -(int32_t)(u2 & 1);
-            const int32_t v3 = (int32_t)(u3 >> 1) ^ -(int32_t)(u3 & 1);
-            Hdr h;
-            h.crc = h0;
-            h.type = h1 & 0xff;
-            h.dt = (h1 >> 8) & 0xff;
-            h.ks = (uint32_t)v1;
-            h.vs = (uint32_t)v2;
-            h.exp = v3;
-            h.hsz = 7 + e3;
-            h.size = 0;
-            h.good = false;
-            if (h.crc == 0 && h.ks == 0 && h.vs == 0) { h.status = CLY_END_ZERO; return h; }
-            const int64_t kv = (int64_t)h.ks + (int64_t)h.vs;
-            if (kv > 0 && nrel - (p + h.hsz) < kv) { h.status = CLY_END_TORN; return h; }
-            h.status = REC_OK;
-            h.size = h.hsz + kv;
-            h.good = h.type <= 4 && h.dt <= 4 && v1 >= 1 && v2 >= 0;
-            return h;
-        }
-    }
-    Hdr h;
-    hdr_slow((const CLY_LDS uint8_t*)w32, p, nrel, p_abs, h);
-    return h;
-}
-
-// Header at a position beyond the staged window (exit check of a long record):
-// read from global memory.
-__device__ __noinline__ void hdr_global(const uint8_t* gfile, int64_t cbase, int64_t x, int64_t nrel, Hdr& h) {
-    // bytes [x, x+26) from the dwords covering them (never past the file's last dword)
-    uint32_t wv[8];
-    const int64_t a = cbase + x, a0 = a & ~3ll;
-    const int64_t flen = cbase + nrel;
-    const uint32_t* gw = (const uint32_t*)(gfile + a0);
-    #pragma unroll
-    for (int k = 0; k < 8; k++) wv[k] = (a0 + 4 * k < flen) ? gw[k] : 0u;
-    uint8_t hb[28];
-    const int sh = (int)(a - a0);
-    const int64_t need = nrel - x < 26 ? nrel - x : 26;
-    #pragma unroll
-    for (int k = 0; k < 26; k++) {
-        const int q = k + sh;
-        hb[k] = k < need ? (uint8_t)(wv[q >> 2] >> (8 * (q & 3))) : 0;
-    }
-    h = step_hdr(hb, 0, nrel - x, cbase + x);
-}
-
-// SWAR byte masks (bit 7 of each byte): byte <= 4 (type/dtype), and
-// byte nonzero and even (first byte of the key-size varint of a record with ks >= 1).
-__device__ __forceinline__ uint32_t swar_le4(uint32_t W) { return ~(((W | 0x80808080u) - 0x05050505u) | W) & 0x80808080u; }
-__device__ __forceinline__ uint32_t swar_ks(uint32_t W) {
-    const uint32_t nz = ((W & 0x7f7f7f7fu) + 0x7f7f7f7fu) | W;
-    return nz & ~(W << 7) & 0x80808080u;
-}
-// ---------------------------------------------------------------------------
-// Sub-tile context (wave-uniform, registers)
-struct Sub {
-    const uint8_t* gfile;        // the file's bytes (HBM)
-    const CLY_LDS uint32_t* w32; // window
-    int64_t cbase;               // file offset of the sub-tile
-    int64_t nrel;                // bytes from the sub-tile start to the end of the file
-    int     dlen;                // data bytes in the sub-tile (<= TS)
-    int     win_len;             // bytes staged in the window
-    int     fof, lof;            // first / last sub-tile of its file
-    int64_t chunk;               // global sub-tile index (ChunkSum slot)
-    uint32_t fid;
-};
-
-// Per-lane chain state of a resolved sub-tile
-struct Lane {
-    int      ws;                 // first chain record starting in the stripe (-1 none)
-    int      wc;                 // chain records starting in the stripe
-    int      wl;                 // last of them
-    int64_t  wx;                 // exit of the stripe's chain part, or terminal position
-    int      wterm, wtst;        // terminal inside the stripe
-    int      pk;                 // last lane <= this one holding a chain record (-1 none)
-    uint32_t base;               // chain records before the stripe
-};
-struct Chain {                   // wave-uniform result of resolve()
-    int      mode;
-    int      E;                  // entry (sub-tile-relative)
-    int      k0;                 // lane of E
-    uint32_t cnt;                // records in the sub-tile
-    int      term, tst;          // the chain ends inside the sub-tile (incl. at the file end)
-    int64_t  tpos;               // terminal position
-    int64_t  xrel;               // exit when not terminated
-    int      last;               // start of the last record (-1 none)
-    int      lterm;              // lane of the terminal (CLY_NT none)
-    int      eof_exit;           // leaves the file's last sub-tile exactly at the end of the file
-};
-
-// Speculative walk of one lane: first candidate in its stripe whose chain of
-// plain records leaves the stripe at an exit that decodes as a plain record
-// (or is the end of the file).
-struct Spec {
-    int s, last, c;
-    int v;                       // the exit was checked (else: beyond the window, unchecked)
-    int64_t x;
-    Hdr h;                       // header of the record at s (reused for its tuple)
-};
-
-// Exact walk (ReadLogRecord semantics, any record or terminal) of the lane's
-// stripe [a, b) from position e.
-__device__ __forceinline__ void exact_walk(const Sub& T, int a, int b, int e, Lane& L) {
-    (void)a;
-    L.ws = e;
-    int64_t p = e;
-    int c = 0, last = -1;
-    for (;;) {
-        const Hdr h = hdr_at(T.w32, (int)p, T.nrel, T.cbase + p);
-        if (h.status != REC_OK) { L.wc = c; L.wl = last; L.wx = p; L.wterm = 1; L.wtst = h.status; return; }
-        c++;
-        last = (int)p;
-        const int64_t p2 = p + h.size;
-        if (p2 >= b) { L.wc = c; L.wl = last; L.wx = p2; L.wterm = 0; L.wtst = 0; return; }
-        p = p2;
-    }
-}
-
-// Candidate bits of stripe word m (positions 4m..4m+3 of the stripe starting at
-// window byte a): type and data type bytes <= 4 (bit 8j+7 for position 4m+j).
-__device__ __forceinline__ uint32_t cand_bits(const CLY_LDS uint32_t* w32, int a, int m) {
-    const int i = (a >> 2) + m + 1;
-    const uint32_t L1 = swar_le4(w32[i]), L2 = swar_le4(w32[i + 1]);
-    return L1 & __builtin_amdgcn_alignbit(L2, L1, 8);
-}
-
-// Speculative walk of one lane: the first candidate of its stripe (from the
-// word mask wm) whose chain of plain records leaves the stripe at an exit that
-// decodes as a plain record or is the end of the file; failing that, the first
-// whose exit lies beyond the window (left unchecked: the chain check of
-// resolve() and the guess's own deep check cover it).  Candidates whose
-// key-size byte is odd or zero (ks < 1) are skipped before decoding.
-__device__ __forceinline__ void spec_lane(const Sub& T, int lane, uint64_t wm, Spec& r) {
-    r.s = -1; r.last = -1; r.c = 0; r.v = 0; r.x = 0;
-    const int a = lane * CLY_SUB;
-    if (a >= T.dlen) return;
-    const int b = a + CLY_SUB < T.dlen ? a + CLY_SUB : T.dlen;
-    const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)T.w32;
-    // (one flat loop over (word, bit): the nested form of this loop with the
-    // early return was miscompiled by the ROCm 7.2 toolchain - R.last came out -1)
-    uint32_t cm = 0;
-    int m = 0;
-    for (;;) {
-        if (cm == 0) {
-            if (wm == 0) break;
-            m = __builtin_ctzll(wm);
-            wm &= wm - 1;
-            cm = cand_bits(T.w32, a, m);
-            continue;
-        }
-        {
-            const int q = a + 4 * m + (__builtin_ctz(cm) >> 3);
-            cm &= cm - 1;
-            if (q >= b) break;
-            const uint32_t kb = w8[q + 6];          // key-size varint: >= 1 needs an even nonzero first byte
-            if (kb == 0 || (kb & 1)) continue;
-            const Hdr h = hdr_at(T.w32, q, T.nrel, T.cbase + q);
-            if (!h.good) continue;
-            int64_t p = q;
-            int c = 1;
-            int64_t x = p + h.size;
-            bool ok = true;
-            while (x < b) {
-                const Hdr h2 = hdr_at(T.w32, (int)x, T.nrel, T.cbase + x);
-                if (!h2.good) { ok = false; break; }
-                p = x;
-                c++;
-                x = p + h2.size;
-            }
-            if (!ok || x > T.nrel) continue;           // a chain past the end of the file is not a guess
-            if (x < T.nrel && x + 26 > T.win_len) {
-                // exit beyond the window: kept unchecked as a fallback, but a
-                // later candidate with a checked exit wins (a false candidate
-                // must not hide the lane's true record)
-                if (r.s < 0) { r.s = q; r.last = (int)p; r.c = c; r.v = 0; r.x = x; r.h = h; }
-                continue;
-            }
-            if (x < T.nrel) {
-                const Hdr e = hdr_at(T.w32, (int)x, T.nrel, T.cbase + x);
-                if (!e.good) continue;
-            }
-            r.s = q; r.last = (int)p; r.c = c; r.v = 1; r.x = x; r.h = h;
-            return;
-        }
-    }
-}
-
-// Second exit check of a speculative chain leaving its stripe at x: the record
-// at x and the one after it must decode as plain records.
-__device__ __forceinline__ int deep_check(const Sub& T, int64_t x) {
-    if (x >= T.nrel) return x == T.nrel;
-    Hdr e;
-    if (x + 26 <= T.win_len) e = hdr_at(T.w32, (int)x, T.nrel, T.cbase + x);
-    else hdr_global(T.gfile, T.cbase, x, T.nrel, e);
-    if (!e.good) return 0;
-    const int64_t x2 = x + e.size;
-    if (x2 >= T.nrel) return x2 == T.nrel;
-    Hdr f;
-    if (x2 + 26 <= T.win_len) f = hdr_at(T.w32, (int)x2, T.nrel, T.cbase + x2);
-    else hdr_global(T.gfile, T.cbase, x2, T.nrel, f);
-    return f.good ? 1 : 0;
-}
-
-// Speculation over the staged window: per lane the candidate word mask of its
-// stripe (register SWAR filter), then the candidate walks; the sub-tile guess.
-__device__ __forceinline__ void sub_spec(const Sub& T, int lane, Spec& sp, int& guess) {
-    const CLY_LDS uint32_t* w32 = T.w32;
-    uint64_t wm = 0;
-    const int a = lane * CLY_SUB;
-    if (a < T.dlen) {
-        uint32_t dw[CLY_NWD + 2];
-        const CLY_LDS u32x4* s4 = (const CLY_LDS u32x4*)(w32 + lane * CLY_NWD);
-        #pragma unroll
-        for (int i = 0; i < CLY_NWD / 4; i++) {
-            const u32x4 v = s4[i];
-            dw[4 * i] = v.x; dw[4 * i + 1] = v.y; dw[4 * i + 2] = v.z; dw[4 * i + 3] = v.w;
-        }
-        dw[CLY_NWD] = w32[lane * CLY_NWD + CLY_NWD];
-        dw[CLY_NWD + 1] = w32[lane * CLY_NWD + CLY_NWD + 1];
-        uint32_t wlo = 0, whi = 0;
-        uint32_t Ln = swar_le4(dw[CLY_NWD + 1]);
-        #pragma unroll
-        for (int m = CLY_NWD - 1; m >= 0; m--) {
-            const uint32_t Lm = swar_le4(dw[m + 1]);
-            const uint32_t cm = Lm & __builtin_amdgcn_alignbit(Ln, Lm, 8);
-            if (m < 32) wlo |= cm ? (1u << m) : 0u;
-            else whi |= cm ? (1u << (m - 32)) : 0u;
-            Ln = Lm;
-        }
-        wm = ((uint64_t)whi << 32) | wlo;
-    }
-    spec_lane(T, lane, wm, sp);
-    if (T.fof) { guess = 0; return; }
-    // guess: the first lane whose chain also survives a second exit check
-    // (a lane whose exit is where the stripe holding it starts its own chain is
-    // confirmed without it)
-    const bool ext = sp.s >= 0 && sp.x < T.dlen;
-    const int tl = ext ? (int)(sp.x / CLY_SUB) : lane;
-    const int ts = __shfl(sp.s, tl, 64), tv = __shfl(sp.v, tl, 64);
-    const int conf = ext && ts == (int)sp.x && tv;      // (an unchecked spec confirms nothing)
-    unsigned long long m = __ballot(sp.s >= 0);
-    guess = -1;
-    while (m) {
-        const int k = __ffsll((long long)m) - 1;
-        int ok = conf;
-        if (lane == k && !ok) ok = deep_check(T, sp.x);
-        if (__shfl(ok, k, 64)) { guess = __shfl(sp.s, k, 64); break; }
-        m &= m - 1;
-    }
-}
-
-// resolve(E): the sub-tile's record chain from entry E (sub-tile-relative).
-__device__ __forceinline__ void resolve(const Sub& T, const Spec& sp, int lane, int E, Lane& L, Chain& R) {
-    R.mode = MODE_NORMAL; R.E = E; R.eof_exit = 0;
-    if (E >= T.dlen) {
-        // only in the file's last sub-tile: E is the end of the file (ReadLogRecord there: io.EOF)
-        L.ws = -1; L.wc = 0; L.wl = -1; L.wx = 0; L.wterm = 0; L.wtst = 0; L.pk = -1; L.base = 0;
-        const Hdr h = hdr_at(T.w32, E, T.nrel, T.cbase + E);
-        R.k0 = CLY_NT; R.cnt = 0; R.last = -1; R.lterm = CLY_NT; R.xrel = E; R.tpos = E;
-        R.term = h.status != REC_OK;
-        R.tst = h.status != REC_OK ? h.status : 0;
-        return;
-    }
-    const int k0 = E / CLY_SUB;
-    const int a = lane * CLY_SUB;
-    const int b = a + CLY_SUB < T.dlen ? a + CLY_SUB : T.dlen;
-    const bool in = a < T.dlen;
-    if (lane < k0 || !in) { L.ws = -1; L.wc = 0; }
-    else { L.ws = sp.s; L.wc = sp.c; }
-    L.wl = sp.last; L.wx = sp.x; L.wterm = 0; L.wtst = 0;
-    if (lane == k0 && L.ws != E) exact_walk(T, a, b, E, L);
-    int kill = __shfl(L.wterm, k0, 64) ? k0 : CLY_NT;
-    if (lane > kill) L.ws = -1;
-    for (int iter = 0;; iter++) {
-        L.pk = scan_max_incl(L.ws >= 0 ? lane : -1, lane);
-        const int j = __shfl_up(L.pk, 1, 64);
-        const int64_t Xj = __shfl(L.wx, j < 0 ? 0 : j, 64);
-        const int wtj = __shfl(L.wterm, j < 0 ? 0 : j, 64);
-        bool bad = false;
-        if (lane > k0 && in && j >= 0 && !wtj) {
-            if (L.ws >= 0) bad = Xj != (int64_t)L.ws;
-            else bad = Xj < (int64_t)b;
-        }
-        const unsigned long long bm = __ballot(bad);
-        if (!bm) break;
-        if (iter > CLY_NT + 1) break;                   // cannot happen: every fix advances
-        const int kstar = __ffsll((long long)bm) - 1;
-        const int jj = __shfl(L.pk, kstar - 1, 64);
-        const int64_t X = __shfl(L.wx, jj, 64);
-        const int K = X < T.dlen ? (int)(X / CLY_SUB) : CLY_NT;
-        if (lane > jj && lane < K) L.ws = -1;
-        if (K < CLY_NT) {
-            const int wsK = __shfl(L.ws, K, 64);
-            if (wsK != (int)X) {
-                if (lane == K) exact_walk(T, a, b, (int)X, L);
-                if (__shfl(L.wterm, K, 64) && lane > K) L.ws = -1;
-            }
-        }
-    }
-    const uint32_t cnt = L.ws >= 0 ? (uint32_t)L.wc : 0u;
-    const uint32_t incl = scan_add_incl(cnt, lane);
-    L.base = incl - cnt;
-    const int Ll = __shfl(L.pk, CLY_NT - 1, 64);
-    R.k0 = k0;
-    R.cnt = __shfl(incl, CLY_NT - 1, 64);
-    R.term = __shfl(L.wterm, Ll, 64);
-    R.tst = __shfl(L.wtst, Ll, 64);
-    R.lterm = R.term ? Ll : CLY_NT;
-    R.tpos = __shfl(L.wx, Ll, 64);
-    R.xrel = R.tpos;
-    R.last = __shfl(L.wl, Ll, 64);
-    if (!R.term && T.lof && R.xrel == T.nrel) {
-        // the chain leaves the file's last sub-tile exactly at the end of the
-        // file: the next ReadLogRecord there returns io.EOF
-        R.term = 1; R.tst = CLY_END_EOF; R.tpos = R.xrel; R.eof_exit = 1;
-        // the lane holding the end of the file owns that check point
-        const int lt = R.xrel < CLY_TS ? (int)(R.xrel / CLY_SUB) : CLY_NT;
-        R.lterm = lt;
-        if (lane == lt) { L.wterm = 1; L.wx = R.xrel; L.wtst = CLY_END_EOF; }
-    }
-}
-
-__device__ __forceinline__ void chain_none(Lane& L, Chain& R, int mode) {
-    L.ws = -1; L.wc = 0; L.wl = -1; L.wx = 0; L.wterm = 0; L.wtst = 0; L.pk = -1; L.base = 0;
-    R.mode = mode; R.E = CLY_TS; R.k0 = CLY_NT; R.cnt = 0; R.term = mode == MODE_DEAD; R.tst = 0; R.tpos = 0;
-    R.xrel = 0; R.last = -1; R.lterm = CLY_NT; R.eof_exit = 0;
-}
-
-// ---------------------------------------------------------------------------
-// CRC of every record of the resolved chain.
-//
-// Check points: every chain record start P (its predecessor's region ends at
-// P) and the terminal position.  XOR patches on the LDS window make one
-// uniform word loop verify all of them:
-//   W_a = word of P:     stored-CRC bytes (>= P) zeroed, and, when the record
-//                        ending at P started inside the sub-tile, Q = A^-j ~crc
-//                        XORed in, so that the register after W_a is zero iff
-//                        that record's CRC matches;
-//   W_b = W_a + 1:       rest of the stored CRC zeroed, 0xFF init on region bytes;
-//   W_c = W_a + 2:       0xFF init on the rest of the first 4 region bytes.
-// Each lane runs its stripe from register 0; the first check point whose W_b
-// lies in the stripe is a hard reset (the register before it is kept as
-// `obs`), later ones are observed directly (`chk` words).  A segmented
-// Kogge-Stone scan over lanes gives the register entering each stripe; the
-// reset check is obs ^ A^(4*rs) S_in.  All patches are XORs, so applying them
-// a second time restores the window.
-struct CrcOut {
-    uint32_t first4, open_crc, open_tail;   // pristine window values for the summary
-    int      bad;                // some check failed (localised by crc_locate)
-    uint32_t head_raw, head_z;   // Z_z(raw [4, E)) for k_fin
-    uint32_t end_state;          // register at the end of the sub-tile (lane 63's inclusive scan)
-};
-
-// Check points are collected (positions + the 4 bytes stored there) from the
-// pristine window into a per-wave pool before any patch is applied, in chain
-// order; patches, marks and the restore pass all read the pool.
-#define CP_POOL 192
-#define CP_REAL 0x10000u
-
-// Patch words of pool entry m (pos P, stored bytes c; cprev = previous entry's
-// stored bytes, or none for the sub-tile's first check point).
-__device__ __forceinline__ void crc_apply(CLY_LDS uint8_t* smem, CLY_LDS uint32_t* w32, uint32_t lane_off, uint32_t ent,
-                                          uint32_t c, bool has_prev, uint32_t cprev) {
-    const int P = (int)(ent & 0xffff);
-    const bool real = (ent & CP_REAL) != 0;
-    const int j = P & 3, wa = P >> 2;
-    const uint32_t lom = j ? (1u << (8 * j)) - 1 : 0u, him = ~lom;
-    uint32_t pa = j ? (c << (8 * j)) : c;
-    uint32_t pb = j ? (c >> (32 - 8 * j)) : 0u;
-    uint32_t pc = 0;
-    if (real) { pb ^= him; pc = lom; }
-    if (has_prev) {
-        uint32_t q = ~cprev;
-        for (int k = 0; k < j; k++) q = crc_unbyte(smem, q, lane_off);
-        pa ^= q;
-    }
-    __hip_atomic_fetch_xor(&w32[wa], pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    if (pb) __hip_atomic_fetch_xor(&w32[wa + 1], pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    if (pc) __hip_atomic_fetch_xor(&w32[wa + 2], pc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-}
-
-__device__ __forceinline__ void crc_patch_all(CLY_LDS uint8_t* smem, CLY_LDS uint32_t* w32, const CLY_LDS u32x2* pool,
-                                              int off, int n, uint32_t lane_off) {
-    for (int i = off; i < off + n; i++) {
-        const u32x2 e = pool[i];
-        const bool has_prev = i > 0;
-        const uint32_t cprev = has_prev ? pool[i - 1].y : 0u;
-        crc_apply(smem, w32, lane_off, e.x, e.y, has_prev, cprev);
-    }
-}
-
-// Register of one lane over its stripe words d[] (patched), with the reset.
-template <bool OBSERVE>
-__device__ __forceinline__ void crc_loop(const CLY_LDS uint8_t* smem, const uint32_t* d, int rs, uint64_t chk,
-                                         uint32_t lane_off, uint32_t& s_out, uint32_t& obs_out, uint32_t& err_out) {
-    uint32_t s = 0, obs = 0, err = 0;
-    const uint32_t chk_lo = (uint32_t)chk, chk_hi = (uint32_t)(chk >> 32);
-#if CLY_CRC_XB
-    const CrcLane cl = crc_lane((int)__lane_id());
-#endif
-    #pragma unroll
-    for (int i = 0; i < CLY_NWD; i++) {
-        const bool r = i == rs;
-        obs = r ? s : obs;
-        const uint32_t x = (r ? 0u : s) ^ d[i];
-#if CLY_CRC_XB
-        s = crc_word_xb(smem, x, cl);
-#else
-        s = crc_word(smem, x, lane_off);
-#endif
-        if (OBSERVE) {
-            // all-ones when word i holds a check point: one v_bfe_i32 (and the
-            // AND-OR below fuses) instead of and + cmp + cndmask per word
-            const uint32_t cw = i < 32 ? chk_lo : chk_hi;
-            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int32_t)cw, (uint32_t)(i & 31), 1u);
-            err |= s & m;
-        }
-    }
-    s_out = s; obs_out = obs; err_out = err;
-}
-
-// The same register without observations, as two independent chains over the
-// stripe's halves (twice the lookups in flight): the second half runs from 0
-// and the halves are joined by linearity, s = A^(4 H) s1 ^ s2 when the reset
-// (if any) is in the first half; with the reset in the second half the
-// register before it is A^(4 (rs - H)) s1 ^ ob, and s = s2.
-// (measured on C2: no gain over the single chain, 3.31 vs 3.25-3.29 ms; kept off)
-#ifndef CLY_CRC_SPLIT
-#define CLY_CRC_SPLIT 0
-#endif
-#define CRC_H (CLY_NWD / 2)
-__device__ __forceinline__ uint32_t word_shift(const CLY_LDS uint8_t* smem, int w, uint32_t v);
-__device__ __forceinline__ uint32_t nib_mul(const CLY_LDS uint8_t* smem, int off, uint32_t v);
-__device__ __forceinline__ void crc_loop_split(const CLY_LDS uint8_t* smem, const uint32_t* d, int rs, uint32_t lane_off,
-                                               uint32_t& s_out, uint32_t& obs_out) {
-    uint32_t sa = 0, sb = 0, oa = 0, ob = 0;
-#if CLY_CRC_XB
-    const CrcLane cl = crc_lane((int)__lane_id());
-#endif
-    #pragma unroll
-    for (int i = 0; i < CRC_H; i++) {
-        const bool ra = i == rs, rb = i + CRC_H == rs;
-        oa = ra ? sa : oa;
-        ob = rb ? sb : ob;
-        const uint32_t xa = (ra ? 0u : sa) ^ d[i];
-        const uint32_t xb = (rb ? 0u : sb) ^ d[i + CRC_H];
-#if CLY_CRC_XB
-        sa = crc_word_xb(smem, xa, cl);
-        sb = crc_word_xb(smem, xb, cl);
-#else
-        sa = crc_word(smem, xa, lane_off);
-        sb = crc_word(smem, xb, lane_off);
-#endif
-    }
-    if (rs >= CRC_H) {
-        obs_out = ob ^ word_shift(smem, rs - CRC_H, sa);
-        s_out = sb;
-    } else {
-        obs_out = oa;
-#if CRC_H % 6 == 0
-        s_out = nib_mul(smem, NIB_HSA + (CRC_H / 6) * 128, sa) ^ sb;     // A^(24 a) table, a = H/6
-#else
-        s_out = word_shift(smem, CRC_H, sa) ^ sb;
-#endif
-    }
-}
-
-__device__ __noinline__ void crc_slow(const CLY_LDS uint32_t* w32, int64_t nrel, int64_t cbase, int E, uint32_t cnt,
-                                      CLY_LDS uint8_t* smem, CrcOut& out);
-
-__device__ __forceinline__ void crc_phase(const Sub& T, const Lane& L, const Chain& R, int lane, CLY_LDS uint8_t* smem,
-                                       CLY_LDS uint32_t* w32, CLY_LDS u32x2* pool, CrcOut& out) {
-    const uint32_t lane_off = (uint32_t)(lane & 15) * 4;
-    out.bad = 0; out.head_raw = 0; out.head_z = 0; out.end_state = 0;
-    const bool normal = R.mode == MODE_NORMAL;
-    out.first4 = w32[0];
-    out.open_crc = 0; out.open_tail = 0xFFFFFFFFu;
-    if (normal && R.last >= 0) {
-        out.open_crc = lds_le32(w32, R.last);
-        const int ocs = R.last + 4;
-        if (ocs < CLY_TS && ocs + 4 > CLY_TS) {
-            const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)w32;
-            uint32_t st = 0xFFFFFFFFu;
-            for (int q = ocs; q < CLY_TS; q++) st = crc_byte(smem, st, w8[q], lane_off);
-            out.open_tail = st;
-        }
-    }
-    // ---- check points of this lane: chain records, then its terminal
-    const bool tcp = normal && L.wterm && L.wx < CLY_TS;
-    const int n = normal ? ((L.ws >= 0 ? L.wc : 0) + (tcp ? 1 : 0)) : 0;
-    const uint32_t incl = scan_add_incl((uint32_t)n, lane);
-    const int off = (int)(incl - (uint32_t)n);
-    const int total = (int)__shfl(incl, CLY_NT - 1, 64);
-    if (total > CP_POOL) {
-        if (lane == 0) {
-            CrcOut t;                               // (own object: `out` stays in registers)
-            crc_slow(w32, T.nrel, T.cbase, R.E, R.cnt, smem, t);
-            out.bad = t.bad; out.head_raw = t.head_raw; out.head_z = t.head_z; out.end_state = t.end_state;
-        }
-        out.bad = __shfl(out.bad, 0, 64); out.head_raw = __shfl(out.head_raw, 0, 64);
-        out.head_z = __shfl(out.head_z, 0, 64); out.end_state = __shfl(out.end_state, 0, 64);
-        return;
-    }
-    if (n && !(CLY_EXP & 64)) {
-        int i = off;
-        if (L.ws >= 0) {
-            int p = L.ws;
-            for (int r = 0; r < L.wc; r++, i++) {
-                pool[i] = (u32x2){(uint32_t)p | CP_REAL, lds_le32(w32, p)};
-                if (r + 1 < L.wc) {
-                    const Hdr h = hdr_at(w32, p, T.nrel, T.cbase + p);
-                    p += (int)h.size;
-                }
-            }
-        }
-        if (tcp) pool[i] = (u32x2){(uint32_t)L.wx, lds_le32(w32, (int)L.wx)};
-    }
-    wave_sync();
-    if (!(CLY_EXP & 64)) crc_patch_all(smem, w32, pool, off, n, lane_off);
-    wave_sync();
-    // ---- reset word and check mask (lane-local word indices)
-    const int w0 = lane * CLY_NWD;
-    int rs = -1, rs_first = 0;
-    uint64_t chk = 0;
-    if (off > 0) {
-        const int P = (int)(pool[off - 1].x & 0xffff);
-        if ((P >> 2) + 1 == w0) { rs = 0; rs_first = P == R.E; }
-    }
-    for (int i = off; i < off + n; i++) {
-        const int P = (int)(pool[i].x & 0xffff);
-        const int wa = (P >> 2) - w0;
-        if (rs < 0) {
-            if (wa + 1 < CLY_NWD) { rs = wa + 1; rs_first = P == R.E; }
-        } else {
-            chk |= 1ull << wa;
-        }
-    }
-    // ---- stripe words
-    uint32_t d[CLY_NWD];
-    {
-        const CLY_LDS u32x4* s4 = (const CLY_LDS u32x4*)(w32 + lane * CLY_NWD);
-        #pragma unroll
-        for (int i = 0; i < CLY_NWD / 4; i++) {
-            const u32x4 v = s4[i];
-            d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
-        }
-        if (lane == 0) d[0] = 0;                // head raw register counts from byte 4
-    }
-    uint32_t s, obs, err;
-    // (no lane with a second check point: the loop without observations)
-    if (CLY_EXP & 32) { s = d[0] ^ d[CLY_NWD - 1]; obs = d[1]; err = 0; }   // experiment: no CRC loop
-    else if (__ballot(chk != 0)) crc_loop<true>(smem, d, rs, chk, lane_off, s, obs, err);
-#if CLY_CRC_SPLIT
-    else { crc_loop_split(smem, d, rs, lane_off, s, obs); err = 0; }
-#else
-    else crc_loop<false>(smem, d, rs, chk, lane_off, s, obs, err);
-#endif
-    // ---- segmented scan: element (c, v), S -> c ? v : A^SUB S ^ v
-    int c = rs >= 0;
-    uint32_t v = s;
-    #pragma unroll
-    for (int lvl = 0; lvl < CLY_KS_LEVELS; lvl++) {
-        const int dd = 1 << lvl;
-        const bool fin_lane = c || lane < dd;
-        if (__ballot(!fin_lane) == 0ull) break;
-        const int pc = __shfl_up(c, dd, 64);
-        const uint32_t pv = __shfl_up(v, dd, 64);
-        if (!fin_lane) { v ^= ks_mul(smem, lvl, pv); c = pc; }
-    }
-    uint32_t s_in = __shfl_up(v, 1, 64);
-    if (lane == 0) s_in = 0;
-    out.end_state = __shfl(v, CLY_NT - 1, 64);
-    // ---- reset checks: T = obs ^ A^(4 rs) S_in
-    const uint32_t y = word_shift(smem, rs > 0 ? rs : 0, s_in);
-    const uint32_t Tv = obs ^ y;
-    bool bad = err != 0;
-    if (rs >= 0 && !rs_first) bad |= Tv != 0;
-    const unsigned long long hm = __ballot(rs >= 0 && rs_first);
-    if (hm) {
-        out.head_raw = __shfl(Tv, __ffsll((long long)hm) - 1, 64);
-        out.head_z = 4 - (R.E & 3);
-    } else if (normal && R.E < T.dlen) {
-        // the check point at E is in the sub-tile's last word (its reset word
-        // is outside): the register at the end is Z_z(raw [4, E))
-        out.head_raw = out.end_state;
-        out.head_z = 4 - (R.E & 3);
-    } else {
-        out.head_raw = out.end_state;     // no boundary: the whole sub-tile is head
-        out.head_z = (uint32_t)(CLY_TS - T.dlen);
-    }
-    // a later check point in the last word: observed at the end of the sub-tile
-    if (normal && total > 0) {
-        const int Pl = (int)(pool[total - 1].x & 0xffff);
-        if ((Pl >> 2) + 1 == CLY_NT * CLY_NWD && Pl != R.E && out.end_state != 0) bad = true;
-    }
-    out.bad = __ballot(bad && normal) != 0ull;
-    if (CLY_EXP & 96) out.bad = 0;                  // experiments: checks meaningless
-    // ---- restore the window for crc_locate (XOR patches are involutions);
-    // nothing else reads it after this phase
-    if (out.bad) {
-        crc_patch_all(smem, w32, pool, off, n, lane_off);
-        wave_sync();
-    }
-}
-
-// Slow path (more check points than the pool holds: sub-tiles of tiny
-// records): one lane recomputes everything byte-serially from the window.
-// (scalar arguments only: a struct passed by reference to a non-inlined
-// function is kept in scratch memory on every sub-tile)
-__device__ __noinline__ void crc_slow(const CLY_LDS uint32_t* w32, int64_t nrel, int64_t cbase, int E, uint32_t cnt,
-                                      CLY_LDS uint8_t* smem, CrcOut& out) {
-    const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)w32;
-    out.bad = 0;
-    // head: Z_z(raw [4, E))
-    uint32_t s = 0;
-    for (int q = 4; q < E; q++) s = crc_byte(smem, s, w8[q], 0);
-    const uint32_t z = 4 - (E & 3);
-    for (uint32_t k = 0; k < z; k++) s = crc_byte(smem, s, 0, 0);
-    out.head_raw = s;
-    out.head_z = z;
-    // records
-    int64_t p = E;
-    uint32_t last_state = 0xFFFFFFFFu;
-    for (uint32_t i = 0; i < cnt; i++) {
-        const Hdr h = hdr_at(w32, (int)p, nrel, cbase + p);
-        const int64_t e = p + h.size;
-        uint32_t r = 0xFFFFFFFFu;
-        const int64_t hi = e < CLY_TS ? e : CLY_TS;
-        for (int64_t q = p + 4; q < hi; q++) r = crc_byte(smem, r, w8[q], 0);
-        if (e < CLY_TS) { if (~r != h.crc) out.bad = 1; }
-        else last_state = r;
-        p = e;
-    }
-    out.end_state = last_state;
-}
-
-// Rare path: locate the first failing in-sub-tile record by a serial exact
-// walk (one lane) over the restored window.  Returns its position and local
-// index via (pos, idx); pos = -1 if none (cannot happen after a failed check).
-__device__ __noinline__ void crc_locate(const CLY_LDS uint32_t* w32, int64_t nrel, int64_t cbase, int E, uint32_t cnt,
-                                        CLY_LDS uint8_t* smem, int& pos, uint32_t& idx) {
-    pos = -1; idx = 0;
-    const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)w32;
-    int64_t p = E;
-    uint32_t i = 0;
-    while (p < CLY_TS && i < cnt) {
-        const Hdr h = hdr_at(w32, (int)p, nrel, cbase + p);
-        const int64_t e = p + h.size;
-        if (e >= CLY_TS) break;                        // no in-tile check point: k_fin
-        uint32_t s = 0xFFFFFFFFu;
-        for (int64_t q = p + 4; q < e; q++) s = crc_byte(smem, s, w8[q], 0);
-        if (~s != h.crc) { pos = (int)p; idx = i; return; }
-        p = e;
-        i++;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Staging: the sub-tile bytes (+halo) into the window.  Whole windows go by
-// LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction); a window cut
-// by the file end is staged through registers with a zero-filled tail.
-// Returns true when the window was issued by LDS-DMA and still has to be
-// waited for (stage_wait); the register path completes before returning.
-__device__ __forceinline__ bool stage(const Sub& T, int lane, CLY_LDS uint32_t* w32) {
-    const int wl = T.win_len;
-    const uint8_t* src = T.gfile + T.cbase;
-    if (wl == CLY_WIN) {
-        #pragma unroll
-        for (int k = 0; k < (CLY_WIN / 16 + 63) / 64; k++) {
-            const int slot0 = k * 64;
-            if (slot0 + lane < CLY_WIN / 16)
-                __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)(slot0 + lane) * 16),
-                                                 (CLY_LDS void*)((CLY_LDS char*)w32 + slot0 * 16), 16, 0, 0);
-        }
-        return true;
-    }
-    CLY_LDS u32x4* w4 = (CLY_LDS u32x4*)w32;
-    const int nvec = wl > 0 ? (wl >> 4) : 0;
-    const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
-    for (int i = lane; i < CLY_WIN / 16; i += 64) w4[i] = i < nvec ? s4[i] : (u32x4){0u, 0u, 0u, 0u};
-    wave_sync();
-    if (lane == 0 && wl > 0 && (wl & 15)) {
-        uint32_t v4[4] = {0, 0, 0, 0};
-        const uint8_t* b = src + (nvec << 4);
-        for (int k = 0; k < (wl & 15); k++) v4[k >> 2] |= (uint32_t)b[k] << (8 * (k & 3));
-        w4[nvec] = (u32x4){v4[0], v4[1], v4[2], v4[3]};
-    }
-    wave_sync();
-    return false;
-}
-__device__ __forceinline__ void stage_wait() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    wave_sync();
-}
-
-// ---------------------------------------------------------------------------
-// Data-wave pieces.
-// Geometry of global sub-tile sidx (file F).
-__device__ __forceinline__ void sub_setup(Sub& T, int64_t sidx, const DevFile& F, CLY_LDS uint32_t* w32) {
-    T.gfile = F.base;
-    T.w32 = w32;
-    T.cbase = (sidx - (int64_t)F.first_sub) * CLY_TS;
-    T.nrel = (int64_t)F.len - T.cbase;
-    T.dlen = (int)(T.nrel < CLY_TS ? (T.nrel > 0 ? T.nrel : 0) : CLY_TS);
-    T.win_len = (int)(T.nrel < CLY_WIN ? (T.nrel > 0 ? T.nrel : 0) : CLY_WIN);
-    T.fof = T.cbase == 0;
-    T.lof = T.cbase + CLY_TS >= (int64_t)F.len;
-    T.chunk = sidx;
-    T.fid = F.fid;
-}
-
-// Chain for the given final mode / entry.
-__device__ __forceinline__ void sub_chain(const Sub& T, const Spec& sp, int lane, int mode, int entry, Lane& L,
-                                          Chain& R) {
-    if (mode == MODE_NORMAL) resolve(T, sp, lane, entry, L, R);
-    else chain_none(L, R, mode);
-}
-
-// Per-sub-tile summary for k_fin (lane 0), with unit-relative record counts.
-__device__ __forceinline__ void sub_summary(const Sub& T, const Chain& R, const CrcOut& co, CLY_LDS uint8_t* smem,
-                                            uint32_t base, int bpos, uint32_t bidx, ChunkSum* sums, Globals* g) {
-    ChunkSum cs;
-    cs.evt_off = EVT_NONE; cs.evt_gidx = 0; cs.evt_status = 0; cs.cnt = 0;
-    cs.open_pos = -1; cs.open_state = 0; cs.open_crc = 0;
-    cs.first4 = co.first4;
-    cs.head_raw = 0; cs.head_len = 0; cs.head_shift = 0; cs.head_z = 0; cs.flags = 0;
-    if (R.mode == MODE_DEAD) {
-        cs.flags = SUM_DEAD;
-    } else if (R.mode == MODE_PASS) {
-        cs.head_len = (uint32_t)T.dlen;
-        cs.head_raw = co.end_state;
-        cs.head_z = (uint32_t)(CLY_TS - T.dlen);
-        if (T.lof) {
-            cs.flags |= SUM_CLOSES;
-            cs.evt_off = T.cbase + T.dlen;
-            cs.evt_gidx = base;
-            cs.evt_status = CLY_END_EOF;
-        }
-    } else {
-        cs.cnt = R.cnt;
-        cs.flags |= SUM_CLOSES;
-        cs.head_len = (uint32_t)(R.E < T.dlen ? R.E : T.dlen);
-        cs.head_raw = co.head_raw;
-        cs.head_z = co.head_z;
-        if (bpos >= 0) {
-            cs.evt_off = T.cbase + bpos;
-            cs.evt_gidx = base + bidx;
-            cs.evt_status = CLY_ERR_CRC;
-        } else if (co.bad) {
-            atomicMax(&g->fail, 5u);
-        }
-        if (R.term && bpos < 0) {
-            cs.evt_off = T.cbase + R.tpos;
-            cs.evt_gidx = base + R.cnt;
-            cs.evt_status = R.tst;
-        }
-        // the last record is open at the end of the sub-tile unless a check
-        // point follows it inside the sub-tile
-        if (R.cnt > 0 && R.last >= 0 && (!R.term || (R.eof_exit && R.tpos >= CLY_TS))) {
-            cs.flags |= SUM_OPEN;
-            cs.open_pos = T.cbase + R.last;
-            cs.open_crc = co.open_crc;
-            const int ocs = R.last + 4;
-            if (ocs >= CLY_TS) {
-                cs.open_state = 0xFFFFFFFFu;
-            } else if (ocs + 4 > CLY_TS) {
-                cs.open_state = co.open_tail;
-            } else {
-                cs.open_state = co.end_state;
-            }
-        }
-    }
-    cs.head_shift = cs.head_len > 4 ? cs.head_len - 4 + cs.head_z : 0;   // exponent; k_fin maps it
-    sums[T.chunk] = cs;
-}
-
-// CRC + first failure + summary of a resolved sub-tile.
-__device__ __forceinline__ void sub_crc(const Sub& T, const Lane& L, const Chain& R, int lane, CLY_LDS uint8_t* smem,
-                                        CLY_LDS u32x2* pool, uint32_t base, ChunkSum* sums, Globals* g) {
-    CrcOut co;
-    crc_phase(T, L, R, lane, smem, (CLY_LDS uint32_t*)T.w32, pool, co);
-    int bpos = -1;
-    uint32_t bidx = 0;
-    if (lane == 0) {
-        if (co.bad) {
-            int tp;
-            uint32_t ti;
-            crc_locate(T.w32, T.nrel, T.cbase, R.E, R.cnt, smem, tp, ti);
-            bpos = tp; bidx = ti;
-        }
-        sub_summary(T, R, co, smem, base, bpos, bidx, sums, g);
-    }
-}
-
-// Tuple words of one record at window position p (index independent).
-__device__ __forceinline__ void tuple_words_h(const Sub& T, int p, const Hdr& h, u32x4& q0, u32x4& q1, u32x4& q2,
-                                              int64_t& size) {
-    const CLY_LDS uint8_t* w8 = (const CLY_LDS uint8_t*)T.w32;
-    int tn;
-    const int64_t klim = h.ks < 11u ? (int64_t)h.ks : 11;
-    const int64_t tx = go_varint(w8 + p + h.hsz, klim, tn);      // parseLogRecordKey, db.go:706-710
-    const uint64_t off = (uint64_t)(T.cbase + p);
-    const uint64_t ex = (uint64_t)h.exp;
-    const uint64_t txv = tn < 0 ? 0ull : (uint64_t)tx;
-    q0 = (u32x4){(uint32_t)off, (uint32_t)(off >> 32), (uint32_t)ex, (uint32_t)(ex >> 32)};
-    q1 = (u32x4){(uint32_t)txv, (uint32_t)(txv >> 32), T.fid, (uint32_t)h.size};
-    q2 = (u32x4){h.ks, h.vs,
-                 (h.type & 0xff) | ((h.dt & 0xff) << 8) | ((uint32_t)(h.hsz & 0xff) << 16) |
-                     ((uint32_t)(tn < 0 ? 0xFF : tn) << 24),
-                 h.crc};
-    size = h.size;
-}
-__device__ __forceinline__ void tuple_words(const Sub& T, int p, u32x4& q0, u32x4& q1, u32x4& q2, int64_t& size) {
-    const Hdr h = hdr_at(T.w32, p, T.nrel, T.cbase + p);
-    tuple_words_h(T, p, h, q0, q1, q2, size);
-}
-
-__device__ __forceinline__ void put_tuple(cly_tuple* out, uint64_t idx, uint64_t out_cap, const u32x4& q0,
-                                          const u32x4& q1, const u32x4& q2, bool& of) {
-    if (idx < out_cap) {
-        u32x4* dst = (u32x4*)(out + idx);
-        dst[0] = q0; dst[1] = q1; dst[2] = q2;
-    } else {
-        of = true;
-    }
-}
-
-// Tuples of this lane's records, written directly (output slot known).
-__device__ __forceinline__ void emit_direct(const Sub& T, const Lane& L, uint64_t idx0, cly_tuple* out, uint64_t out_cap,
-                                            Globals* g) {
-    bool of = false;
-    if (L.ws >= 0) {
-        int p = L.ws;
-        for (int i = 0; i < L.wc; i++) {
-            u32x4 q0, q1, q2;
-            int64_t size;
-            tuple_words(T, p, q0, q1, q2, size);
-            put_tuple(out, idx0 + i, out_cap, q0, q1, q2, of);
-            p += (int)size;
-        }
-    }
-    if (of && g) atomicOr(&g->overflow, 1u);
-}
-
-// ---------------------------------------------------------------------------
-// Kernels.
-//   k_scan   every sub-tile independently: speculate, resolve the chain under
-//            its own guess, CRC, tuples into the sub-tile's staging slot
-//   k_link1/2/3   scan over sub-tile results: each guess is checked against the
-//            chain entering its sub-tile; output slot of every sub-tile
-//   k_fix    the (rare) sub-tiles whose guess was wrong, from their true entry
-//   k_place  staged tuples to their output slots
-//   k_fin    per file: straddling CRCs and the first event
-__device__ __forceinline__ int find_file(const uint32_t* __restrict__ sub_prefix, int nfiles, int64_t s) {
-    int lo = 0, hi = nfiles - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if ((int64_t)sub_prefix[mid] <= s) lo = mid; else hi = mid - 1;
-    }
-    return lo;
-}
-
-__device__ __forceinline__ void init_tables(CLY_LDS uint8_t* smem, const uint32_t* __restrict__ cols) {
-    // tables: entry i of T_t replicated 16x, dword (i*64 + t*16 + r)
+__device__ __forceinline__ void init_tables(CLY_LDS uint8_t* smem, const uint32_t* __restrict__ nib) {
     for (int i = threadIdx.x; i < 256; i += blockDim.x) {
         uint32_t cv = i;
         for (int k = 0; k < 8; k++) cv = (cv & 1) ? (cv >> 1) ^ CLY_POLY : cv >> 1;
@@ -1207,557 +130,969 @@ __device__ __forceinline__ void init_tables(CLY_LDS uint8_t* smem, const uint32_
             cv = (cv >> 8) ^ tl;
         }
     }
-    for (int i = threadIdx.x; i < CLY_COLS; i += blockDim.x) ((CLY_LDS uint32_t*)(smem + LDS_KSNIB))[i] = cols[i];
+    for (int i = threadIdx.x; i < NIB_LEVELS * 128; i += blockDim.x) ((CLY_LDS uint32_t*)(smem + LDS_NIB))[i] = nib[i];
     __syncthreads();
 }
 
-// Tuples of this lane's records into the sub-tile's staging slot (when they
-// fit).  The slot is three planes of CLY_CAP 16-B pieces (piece k of tuple i
-// at plane k, row i), so with one record per lane each store instruction
-// writes one contiguous run; k_copy interleaves the planes back.
-__device__ __forceinline__ void stage_tuples(const Sub& T, const Spec& sp, const Lane& L, const Chain& R,
-                                             cly_tuple* staging) {
-    if (R.mode != MODE_NORMAL || R.cnt > CLY_CAP) return;
-    if (L.ws < 0) return;
-    u32x4* slot = (u32x4*)staging + (uint64_t)T.chunk * (3 * CLY_CAP);
-    int p = L.ws;
-    for (int i = 0; i < L.wc; i++) {
-        u32x4 q0, q1, q2;
-        int64_t size;
-        if (i == 0 && p == sp.s) tuple_words_h(T, p, sp.h, q0, q1, q2, size);   // decoded by the speculation
-        else tuple_words(T, p, q0, q1, q2, size);
-        const int r = (int)L.base + i;
-        slot[r] = q0;
-        slot[CLY_CAP + r] = q1;
-        slot[2 * CLY_CAP + r] = q2;
-        p += (int)size;
-    }
+// One slicing-by-4 step s' = A^4 (s ^ word), bank-conflict-free: lookup i of
+// lanes with bit 4 set reads table slot i^1 (16 banks away) with the byte that
+// slot takes; table address = (byte << 8) | replica offset by one v_perm.
+struct CrcLane { uint32_t oe, oo, s0, s1, s2, s3, r4; };
+__device__ __forceinline__ CrcLane crc_lane(int lane) {
+    const uint32_t r4 = (uint32_t)(lane & 15) * 4, h = (uint32_t)(lane >> 4) & 1u;
+    CrcLane c;
+    c.r4 = r4;
+    c.oe = r4 + 64 * h;
+    c.oo = r4 + 64 * (1 - h);
+    c.s0 = 0x0c0c0000u | ((4u + (3u - (0u ^ h))) << 8);
+    c.s1 = 0x0c0c0000u | ((4u + (3u - (1u ^ h))) << 8);
+    c.s2 = 0x0c0c0000u | ((4u + (3u - (2u ^ h))) << 8);
+    c.s3 = 0x0c0c0000u | ((4u + (3u - (3u ^ h))) << 8);
+    return c;
 }
-
-__device__ __forceinline__ SubDesc make_desc(const Sub& T, const Chain& R) {
-    SubDesc d;
-    d.mode = (uint8_t)R.mode;
-    d.cnt = R.mode == MODE_NORMAL ? R.cnt : 0;
-    d.entry = (int16_t)(R.mode == MODE_NORMAL ? R.E : -1);
-    d.x = (R.mode == MODE_NORMAL && !R.term) ? T.chunk * (int64_t)CLY_TS + R.xrel : 0;
-    d.flags = (uint8_t)(((R.mode == MODE_NORMAL && R.term) ? SD_TERM : 0) | (T.fof ? SD_FOF : 0) |
-                        (d.cnt > CLY_CAP ? SD_OVF : 0));
-    return d;
+__device__ __forceinline__ uint32_t crc_word(const CLY_LDS uint8_t* smem, uint32_t x, const CrcLane& c) {
+    const uint32_t a0 = __builtin_amdgcn_perm(x, c.oe, c.s0), a1 = __builtin_amdgcn_perm(x, c.oo, c.s1);
+    const uint32_t a2 = __builtin_amdgcn_perm(x, c.oe, c.s2), a3 = __builtin_amdgcn_perm(x, c.oo, c.s3);
+    return *(const CLY_LDS uint32_t*)(smem + a0) ^ *(const CLY_LDS uint32_t*)(smem + a1) ^
+           *(const CLY_LDS uint32_t*)(smem + a2 + 128) ^ *(const CLY_LDS uint32_t*)(smem + a3 + 128);
 }
-
-// One sub-tile, start to end, for a chain given by (mode, entry) or, mode < 0,
-// by its own guess (mode -2: test mode, odd sub-tiles take a wrong guess).
-#ifndef CLY_SCHED
-#define CLY_SCHED "default"
-#endif
-#ifndef CLY_SRC_HASH
-#define CLY_SRC_HASH "unknown"
-#endif
-#define PF_N ((CLY_WIN / 16 + 63) / 64)       // 16-B pieces per lane of a prefetched window
-__device__ __forceinline__ void prefetch_issue(const uint8_t* src, int lane, u32x4 (&pf)[PF_N]) {
-    const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
+// inverse of one zero-byte step: s = A^-1 s'
+__device__ __forceinline__ uint32_t crc_unbyte(const CLY_LDS uint8_t* smem, uint32_t s, uint32_t r4) {
+    const uint32_t i = smem[LDS_INV + (s >> 24)];
+    const uint32_t t = *(const CLY_LDS uint32_t*)(smem + ((i << 8) | r4));
+    return ((s ^ t) << 8) | i;
+}
+// A^(CLY_CH * 2^lvl) v by nibble tables (entry n*16+k = M (k << 4n))
+__device__ __forceinline__ uint32_t nib_mul(const CLY_LDS uint8_t* smem, int lvl, uint32_t v) {
+    const CLY_LDS uint32_t* t = (const CLY_LDS uint32_t*)(smem + LDS_NIB) + lvl * 128;
+    uint32_t p = 0;
     #pragma unroll
-    for (int k = 0; k < PF_N; k++) {
-        const int slot = k * 64 + lane;
-        if (slot < CLY_WIN / 16) pf[k] = __builtin_nontemporal_load(s4 + slot);
-    }
-}
-__device__ __forceinline__ void prefetch_commit(CLY_LDS uint32_t* w32, int lane, const u32x4 (&pf)[PF_N]) {
-    CLY_LDS u32x4* w4 = (CLY_LDS u32x4*)w32;
-    #pragma unroll
-    for (int k = 0; k < PF_N; k++) {
-        const int slot = k * 64 + lane;
-        if (slot < CLY_WIN / 16) w4[slot] = pf[k];
-    }
-    wave_sync();
+    for (int n = 0; n < 8; n++) p ^= t[n * 16 + ((v >> (4 * n)) & 15u)];
+    return p;
 }
 
-// One sub-tile: window (already in LDS when `ready`), speculation, chain,
-// tuples, CRC, descriptor.  When pf_src is set, the window of the wave's next
-// sub-tile is loaded into pf[] on the way (after the phases that read HBM).
-__device__ __forceinline__ bool process_sub(int64_t sidx, int mode, int entry, const DevFile& F, int lane,
-                                            CLY_LDS uint8_t* smem, CLY_LDS uint32_t* w32, CLY_LDS u32x2* pool,
-                                            SubDesc* descs, ChunkSum* sums, cly_tuple* staging, Globals* g,
-                                            int prof_base, SubDesc& d, bool ready, const uint8_t* pf_src,
-                                            u32x4 (&pf)[PF_N], bool tentative = false) {
-    PROF_INIT();
-    Sub T;
-    sub_setup(T, sidx, F, w32);
-    if (!ready && stage(T, lane, w32)) stage_wait();
-    PROF(0);
-    Spec sp;
-    int guess = -1;
-    if (CLY_EXP & 4) {          // experiment: no speculation
-        sp.s = -1; sp.last = -1; sp.c = 0; sp.v = 0; sp.x = 0; guess = T.fof ? 0 : -1;
-    } else {
-        sub_spec(T, lane, sp, guess);
-    }
-    if (pf_src) prefetch_issue(pf_src, lane, pf);
-    PROF(1);
-    Lane L;
-    Chain R;
-    if (mode < 0) {
-        const bool force = mode == -2 && !T.fof && (sidx & 1);     // test mode: wrong guesses
-        mode = guess >= 0 ? MODE_NORMAL : MODE_PASS;
-        entry = guess;
-        if (force) mode = (sidx & 2) ? MODE_DEAD : MODE_PASS;
-    }
-    if ((CLY_EXP & 8) && !T.fof) mode = MODE_PASS;    // experiment: no chain
-    sub_chain(T, sp, lane, mode, entry, L, R);
-    PROF(2);
-    if (tentative && R.mode == MODE_NORMAL && R.term && !T.lof) {
-        // an uncertain fix whose chain ends inside the file: most likely a
-        // false entry; leave the sub-tile as it is (its state gets certain later)
-        d = descs[T.chunk];
-        return false;
-    }
-    if (!(CLY_EXP & 1)) stage_tuples(T, sp, L, R, staging);     // before the CRC phase patches the window
-    PROF(3);
-    if (!(CLY_EXP & 2)) sub_crc(T, L, R, lane, smem, pool, 0, sums, g);
-    PROF(4);
-    d = make_desc(T, R);
-    if (lane == 0) {
-        descs[T.chunk] = d;
-        if (d.flags & SD_OVF) atomicAdd(&g->novf, 1u);
-    }
-    PROF(5);
-    PROF_FLUSH(prof_base);
+// ---------------------------------------------------------------------------
+// Boundary patch.  A record starting at P (stored CRC c, the record before it
+// stored cq) changes the file's byte stream, as seen by the CRC register, by
+//   pa on word a = P>>2: the stored-CRC bytes [P, 4a+4) zeroed, and Q = A^-j ~cq
+//                  (j = P&3) XORed in, so that the register after word a is zero
+//                  iff the record ending at P has a good CRC (none at P = 0);
+//   pb on word a+1: the rest of the stored CRC zeroed, 0xFF (the init) on the
+//                  record's first region bytes [P+4, 4a+8);
+//   pc on word a+2: 0xFF on [4a+8, P+8).
+// XORing d into a word equals XORing A^4 d into the register after it, so the
+// three are one XOR delta' = A^8 pa ^ A^4 pb ^ pc on word a+2.  The register
+// of the whole patched file (everything from the chain's terminal T on zeroed,
+// Q of T's predecessor at T) is zero iff every record's CRC matches.
+__device__ __forceinline__ uint32_t q_of(const CLY_LDS uint8_t* smem, uint32_t cq, uint32_t j, uint32_t r4) {
+    uint32_t q = ~cq;
+    for (uint32_t k = 0; k < j; k++) q = crc_unbyte(smem, q, r4);
+    return q;
+}
+__device__ __forceinline__ uint32_t patch_delta(const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t P, uint32_t c,
+                                                uint32_t cq) {
+    const uint32_t j = P & 3, sh = 8 * j;
+    uint32_t pa = j ? (c << sh) : c;
+    if (P != 0) pa ^= q_of(smem, cq, j, cl.r4);
+    const uint32_t pb = (j ? (c >> (32 - sh)) : 0u) ^ (j ? (0xFFFFFFFFu << sh) : 0xFFFFFFFFu);
+    const uint32_t pc = j ? ((1u << sh) - 1u) : 0u;
+    return crc_word(smem, crc_word(smem, pa, cl) ^ pb, cl) ^ pc;
+}
+
+// ---------------------------------------------------------------------------
+// Header decode at file position p.  Fast path: 32 bytes gathered from
+// [p & ~3, +32) by two 16-B loads, varints of at most 4 bytes ending within
+// header bytes 6..13 (every record the writer produces except long
+// expirations); otherwise the exact byte-loop form over global memory.
+struct Gath { uint32_t w[8]; };
+__device__ __forceinline__ bool gath_ok(uint32_t p, uint64_t len) { return (uint64_t)(p & ~3u) + 32 <= len; }
+__device__ __forceinline__ void gath_issue(const uint8_t* base, uint32_t p, Gath& g) {
+    const u32x4u* q = (const u32x4u*)(base + (p & ~3u));
+    const u32x4u a = q[0], b = q[1];
+    g.w[0] = a.x; g.w[1] = a.y; g.w[2] = a.z; g.w[3] = a.w;
+    g.w[4] = b.x; g.w[5] = b.y; g.w[6] = b.z; g.w[7] = b.w;
+}
+__device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t s) {
+    return __builtin_amdgcn_alignbyte(hi, lo, s);
+}
+__device__ __forceinline__ uint32_t pack7(uint32_t s) {
+    return (s & 0x7fu) | ((s >> 1) & 0x3f80u) | ((s >> 2) & 0x1fc000u) | ((s >> 3) & 0xfe00000u);
+}
+__device__ __noinline__ void hdr_slow(const uint8_t* base, uint32_t p, uint64_t len, Hdr& h) {
+    h = step_hdr(base, (int64_t)p, (int64_t)len, (int64_t)p);
+}
+// header bytes 0..15 at p from a gather
+__device__ __forceinline__ bool hdr_fast(const Gath& g, uint32_t p, uint64_t len, Hdr& h) {
+    const uint64_t m64 = len - p;
+    const int m = m64 > 26 ? 26 : (int)m64;
+    if (m < 14) return false;
+    const uint32_t s = p & 3;
+    const uint32_t h0 = alignb(g.w[1], g.w[0], s), h1 = alignb(g.w[2], g.w[1], s), h2 = alignb(g.w[3], g.w[2], s),
+                   h3 = alignb(g.w[4], g.w[3], s);
+    const uint32_t lo = alignb(h2, h1, 2), hi = alignb(h3, h2, 2);       // bytes 6..9, 10..13
+    const uint64_t W = ((uint64_t)hi << 32) | lo;
+    const uint64_t T = ~W & 0x8080808080808080ull;
+    const uint64_t T2 = T & (T - 1), T3 = T2 & (T2 - 1);
+    const int e1 = __builtin_ctzll(T | (1ull << 63)) >> 3;
+    const int e2 = __builtin_ctzll(T2 | (1ull << 63)) >> 3;
+    const int e3 = __builtin_ctzll(T3 | (1ull << 63)) >> 3;
+    const int n1 = e1 + 1, n2 = e2 - e1, n3 = e3 - e2;
+    if (!(T3 != 0 && n1 <= 4 && n2 <= 4 && n3 <= 4 && 6 + e3 < m)) return false;
+    const uint32_t u1 = pack7((uint32_t)W) & ((1u << (7 * n1)) - 1);
+    const uint32_t u2 = pack7((uint32_t)(W >> (8 * n1))) & ((1u << (7 * n2)) - 1);
+    const uint32_t u3 = pack7((uint32_t)(W >> (8 * (e2 + 1)))) & ((1u << (7 * n3)) - 1);
+    const int32_t v1 = (int32_t)(u1 >> 1) ^ -(int32_t)(u1 & 1);
+    const int32_t v2 = (int32_t)(u2 >> 1) ^ -(int32_t)(u2 & 1);
+    const int32_t v3 = (int32_t)(u3 >> 1) ^ -(int32_t)(u3 & 1);
+    h.crc = h0;
+    h.key0 = (((7 + e3) >= 12 ? h3 : h2) >> (8 * ((7 + e3) & 3))) & 0xffu;
+    h.type = h1 & 0xff;
+    h.dt = (h1 >> 8) & 0xff;
+    h.ks = (uint32_t)v1;
+    h.vs = (uint32_t)v2;
+    h.exp = v3;
+    h.hsz = 7 + e3;
+    h.size = 0;
+    h.good = false;
+    if (h.crc == 0 && h.ks == 0 && h.vs == 0) { h.status = CLY_END_ZERO; return true; }
+    const int64_t kv = (int64_t)h.ks + (int64_t)h.vs;
+    if (kv > 0 && (int64_t)(len - (p + (uint32_t)h.hsz)) < kv) { h.status = CLY_END_TORN; return true; }
+    h.status = REC_OK;
+    h.size = h.hsz + kv;
+    h.good = h.type <= 4 && h.dt <= 4 && v1 >= 1 && v2 >= 0;
     return true;
 }
+// Header at p; `g` must hold the gather of p when gath_ok(p).
+__device__ __forceinline__ Hdr hdr_at(const uint8_t* base, uint32_t p, uint64_t len, const Gath& g) {
+    Hdr h;
+    if (gath_ok(p, len) && hdr_fast(g, p, len, h)) return h;
+    hdr_slow(base, p, len, h);
+    return h;
+}
+__device__ __forceinline__ Hdr hdr_load(const uint8_t* base, uint32_t p, uint64_t len) {
+    Gath g;
+    if (gath_ok(p, len)) gath_issue(base, p, g);
+    return hdr_at(base, p, len, g);
+}
 
-__global__ void __launch_bounds__(64 * CLY_NDW)
-k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ sub_prefix, int64_t nsub,
-       SubDesc* descs, ChunkSum* sums, const uint32_t* __restrict__ cols, cly_tuple* staging, Globals* g, int gmode) {
-    // static LDS: its offsets are known when compiling, so table and window
-    // addresses need no base add (a dynamic extern array costs one v_add per lookup)
-    __shared__ __attribute__((aligned(16))) unsigned char smem_raw[CLY_SCAN_LDS];
-    CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
-    init_tables(smem, cols);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    CLY_LDS uint32_t* w32 = (CLY_LDS uint32_t*)(smem + LDS_WIN + wave * CLY_WIN);
-    CLY_LDS u32x2* pool = (CLY_LDS u32x2*)(smem + LDS_POOL + wave * CP_POOL * 8);
-    const int64_t stride = (int64_t)gridDim.x * CLY_NDW;
-    int64_t s = (int64_t)blockIdx.x * CLY_NDW + wave;
-    if (s >= nsub) return;
-    int f = find_file(sub_prefix, nfiles, s);
-    DevFile F = files[f];
-    u32x4 pf[PF_N];
-    bool ready = false;
+// ---------------------------------------------------------------------------
+// Per-lane chain of one chunk [cb, ce) (file offsets; the file's last chunk
+// also owns position len, where ReadLogRecord returns io.EOF).
+struct Chunk {
+    const uint8_t* base;
+    uint64_t len;
+    uint32_t cb, ce;
+    bool last;                   // the file's last chunk
+    bool on;                     // the chunk exists (cb < len, or the empty file's chunk 0)
+};
+__device__ __forceinline__ bool in_chunk(const Chunk& K, uint32_t x) {
+    return (x >= K.cb && x < K.ce) || (K.last && (uint64_t)x == K.len);
+}
+struct LaneChain {
+    int      mode;               // LM_*
+    uint32_t E;                  // first boundary (record start or terminal)
+    uint32_t x;                  // exit (>= ce) or terminal position
+    int      term;               // terminal status, TERM_NONE if the chain leaves the chunk
+    uint32_t cnt;                // records starting in the chunk
+    uint32_t last, last_crc;     // last record start and its stored CRC
+    uint32_t prev_crc;           // stored CRC of the record before `last` (cnt >= 2)
+    uint32_t minsz;              // smallest record size
+};
+__device__ __forceinline__ void chain_set(LaneChain& L, int mode) {
+    L.mode = mode; L.E = NONE32; L.x = 0; L.term = TERM_NONE; L.cnt = 0; L.last = NONE32; L.last_crc = 0;
+    L.prev_crc = 0; L.minsz = 0xFFFFFFFFu;
+}
+
+// Walk from p: exact (ReadLogRecord semantics, every terminal) or speculative
+// (every record must be one the writer produces and the chain must leave the
+// chunk at a plausible header, or end at io.EOF at len).  Returns false when a
+// speculative chain is rejected.
+__device__ __noinline__ bool walk(const Chunk& K, uint32_t p, bool exact, LaneChain& L) {
+    chain_set(L, LM_CHAIN);
+    L.E = p;
     for (;;) {
-        if (ready) prefetch_commit(w32, lane, pf);
-        // the wave's next sub-tile (files in order: walk forward from f)
-        const int64_t s2 = s + stride;
-        int f2 = f;
-        DevFile F2 = F;
-        const uint8_t* src2 = nullptr;
-        if (s2 < nsub) {
-            while (s2 >= (int64_t)F2.first_sub + F2.nsub) F2 = files[++f2];
-            const int64_t cb2 = (s2 - (int64_t)F2.first_sub) * CLY_TS;
-            if ((int64_t)F2.len - cb2 >= CLY_WIN) src2 = F2.base + cb2;
+        if (!in_chunk(K, p)) {
+            L.x = p;
+            if (exact || (uint64_t)p == K.len) return true;
+            if ((uint64_t)p > K.len) return false;
+            const Hdr e = hdr_load(K.base, p, K.len);
+            return (e.status == REC_OK && e.good) || e.status == CLY_END_ZERO;
         }
-        SubDesc d;
-        process_sub(s, gmode, 0, F, lane, smem, w32, pool, descs, sums, staging, g, 0, d, ready, src2, pf);
-        if (s2 >= nsub) break;
-        s = s2; f = f2; F = F2;
-        ready = src2 != nullptr;
+        const Hdr h = hdr_load(K.base, p, K.len);
+        if (h.status != REC_OK) {
+            L.x = p; L.term = h.status;
+            return exact || (h.status == CLY_END_EOF && (uint64_t)p == K.len);
+        }
+        if (!exact && !h.good) return false;
+        L.cnt++;
+        L.prev_crc = L.last_crc;
+        L.last = p; L.last_crc = h.crc;
+        if ((uint32_t)h.size < L.minsz) L.minsz = (uint32_t)h.size;
+        p += (uint32_t)h.size;
     }
 }
 
-// Re-process the sub-tiles of the fix list from the chain the link gives them,
-// then walk on through the following sub-tiles of the file while the chain
-// stays live and disagrees with what they hold (stopping at a sub-tile listed
-// or walked this round).  Pass 0 takes the certain fixes, pass 1 the uncertain
-// ones that no pass-0 walk went through.
-__global__ void __launch_bounds__(64 * CLY_NDW)
-k_fix(const DevFile* __restrict__ files, const Fix* fixes, uint32_t nfix, uint32_t* listed, uint32_t stamp, int pass,
-      SubDesc* descs, ChunkSum* sums, const uint32_t* __restrict__ cols, cly_tuple* staging, Globals* g) {
-    if (nfix == ~0u) nfix = __hip_atomic_load(&g->nfix, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (launched ahead)
-    if (blockIdx.x * CLY_NDW >= nfix) return;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
-    init_tables(smem, cols);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    CLY_LDS uint32_t* w32 = (CLY_LDS uint32_t*)(smem + LDS_WIN + wave * CLY_WIN);
-    CLY_LDS u32x2* pool = (CLY_LDS u32x2*)(smem + LDS_POOL + wave * CP_POOL * 8);
-    for (uint32_t i = blockIdx.x * CLY_NDW + wave; i < nfix; i += gridDim.x * CLY_NDW) {
-        const Fix fx = fixes[i];
-        if ((int)fx.certain != (pass == 0)) continue;
-        // an uncertain fix gives way to a walk of the first pass that went through it
-        if (pass == 1 && __builtin_nontemporal_load(&listed[fx.s]) != (stamp | LISTED_U)) continue;
-        const DevFile F = files[fx.file];
-        const int64_t s_end = (int64_t)F.first_sub + F.nsub;
-        int64_t s = fx.s, x = fx.x_in;
-        int mode = fx.mode, entry = fx.entry;
-        for (;;) {
-            SubDesc d;
-            u32x4 pf[PF_N];
-            if (!process_sub(s, mode, entry, F, lane, smem, w32, pool, descs, sums, staging, g, 8, d, false, nullptr, pf,
-                             pass == 1 && s == (int64_t)fx.s)) break;
-            if (d.mode == MODE_DEAD || (d.mode == MODE_NORMAL && (d.flags & SD_TERM))) break;
-            if (d.mode == MODE_NORMAL) x = d.x;
-            if (++s >= s_end) break;
-            const uint32_t ls = __builtin_nontemporal_load(&listed[s]);
-            // certain-listed or walked this round: its own wave has it (pass 0
-            // walks through uncertain fixes, which then give way)
-            if (ls == stamp || (pass == 1 && ls == (stamp | LISTED_U))) break;
-            const int64_t rel = x - s * (int64_t)CLY_TS;
-            if (rel < 0) { if (lane == 0) atomicOr(&g->fail, 8u); break; }      // cannot happen
-            mode = rel >= CLY_TS ? MODE_PASS : MODE_NORMAL;
-            entry = rel >= CLY_TS ? 0 : (int)rel;
-            const SubDesc n = descs[s];
-            // walked (or already right for the walked chain): claimed for this round,
-            // so an uncertain fix listed there gives way
-            if (lane == 0) listed[s] = stamp;
-            if (n.mode == mode && (mode != MODE_NORMAL || n.entry == entry)) break;
+// SWAR byte masks (bit 7 of each byte): byte <= 4 (type / data type), byte
+// nonzero and even (first byte of the key-size varint of a record with ks >= 1).
+__device__ __forceinline__ uint32_t swar_le4(uint32_t W) { return ~(((W | 0x80808080u) - 0x05050505u) | W) & 0x80808080u; }
+__device__ __forceinline__ uint32_t swar_ks(uint32_t W) {
+    const uint32_t nz = ((W & 0x7f7f7f7fu) + 0x7f7f7f7fu) | W;
+    return nz & ~(W << 7) & 0x80808080u;
+}
+
+// 16-B piece at chunk-relative offset o (bytes past len read as zero; pieces
+// wholly past it are not loaded).
+__device__ __forceinline__ u32x4 piece(const Chunk& K, uint32_t o) {
+    const uint64_t a = (uint64_t)K.cb + o;
+    if (a + 16 <= K.len) return *(const u32x4*)(K.base + a);
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (a < K.len) {
+        v = *(const u32x4*)(K.base + a);
+        const uint32_t n = (uint32_t)(K.len - a);          // 1..15 valid bytes
+        #pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int lo = 4 * k;
+            const uint32_t m = (int)n >= lo + 4 ? 0xFFFFFFFFu : ((int)n <= lo ? 0u : ((1u << (8 * (n - lo))) - 1u));
+            v[k] &= m;
+        }
+    }
+    return v;
+}
+
+// Phase A for one lane: the chain of its chunk under its own guess.
+__device__ __noinline__ void phase_a(const Chunk& K, LaneChain& L) {
+    if (!K.on) { chain_set(L, LM_OFF); return; }
+    if (K.cb == 0) { walk(K, 0, true, L); return; }
+    chain_set(L, LM_NONE);
+    bool found = false;
+    for (int b = 0; b < CLY_NB; b++) {
+        if (found) continue;
+        uint32_t w[CLY_BW + 4];
+        #pragma unroll
+        for (int k = 0; k < CLY_BW / 4 + 1; k++) {
+            const u32x4 v = piece(K, (uint32_t)(b * CLY_BW * 4 + 16 * k));
+            w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+        }
+        // candidate positions of the burst, one bit each (4 per word)
+        uint32_t cmk[CLY_BW / 8];
+        #pragma unroll
+        for (int k = 0; k < CLY_BW / 8; k++) cmk[k] = 0;
+        #pragma unroll
+        for (int k = 0; k < CLY_BW; k++) {
+            // positions 4k..4k+3: bytes +4, +5 <= 4 and +6 even nonzero
+            const uint32_t L1 = swar_le4(w[k + 1]), L2 = swar_le4(w[k + 2]);
+            const uint32_t cm = L1 & __builtin_amdgcn_alignbit(L2, L1, 8) & swar_ks(alignb(w[k + 2], w[k + 1], 2));
+            const uint32_t nib = ((cm >> 7) & 1u) | ((cm >> 14) & 2u) | ((cm >> 21) & 4u) | ((cm >> 28) & 8u);
+            cmk[k >> 3] |= nib << (4 * (k & 7));
+        }
+        #pragma unroll
+        for (int k = 0; k < CLY_BW / 8; k++) {
+            uint32_t m = found ? 0u : cmk[k];
+            while (m) {
+                const uint32_t q = K.cb + (uint32_t)(b * CLY_BW * 4 + 32 * k) + (uint32_t)__builtin_ctz(m);
+                m &= m - 1;
+                if (q >= K.ce) { m = 0; break; }
+                LaneChain T;
+                if (walk(K, q, false, T)) { L = T; found = true; m = 0; }
+            }
         }
     }
 }
 
-// ---- link scan over sub-tiles (three passes of LINK_NT threads x LINK_IT items)
-#define LINK_NT 256
-#define LINK_IT 8
-#define LINK_BLK (LINK_NT * LINK_IT)
-__device__ __forceinline__ LinkAgg link_op(const LinkAgg& a, const LinkAgg& b) {
-    LinkAgg r;
+// ---------------------------------------------------------------------------
+// wave helpers
+__device__ __forceinline__ int scan_max_incl(int v, int lane) {
     #pragma unroll
-    for (int t = 0; t < 2; t++) {
-        const LinkBr& ra = a.br[t];
-        const LinkBr& rb = b.br[ra.set ? ra.term : t];
-        r.br[t].set = ra.set | rb.set;
-        r.br[t].x = rb.set ? rb.x : ra.x;
-        r.br[t].term = rb.set ? rb.term : ra.term;
-        r.br[t].cnt = ra.cnt + rb.cnt;
+    for (int o = 1; o < 64; o <<= 1) { const int u = __shfl_up(v, o, 64); if (lane >= o) v = max(v, u); }
+    return v;
+}
+__device__ __forceinline__ uint32_t scan_add_incl(uint32_t v, int lane) {
+    #pragma unroll
+    for (int o = 1; o < 64; o <<= 1) { const uint32_t u = __shfl_up(v, o, 64); if (lane >= o) v += u; }
+    return v;
+}
+__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, 64); }
+
+// In-wave agreement: lane l's chain must start where the chain of the nearest
+// chunk before it leaves (the tile's entry X0 for the first lanes; dead0: the
+// file's chain ended before the tile).  The lowest disagreeing lane is
+// re-walked exactly, until every lane agrees.
+__device__ __noinline__ void resolve(const Chunk& K, LaneChain& L, int lane, uint32_t X0, bool dead0, Globals* g) {
+    for (int iter = 0;; iter++) {
+        const bool isC = L.mode == LM_CHAIN;
+        const int pk = scan_max_incl(isC ? lane : -1, lane);
+        const int pu = __shfl_up(pk, 1, 64);            // (every lane: cross-lane reads outside conditionals)
+        const int j = lane > 0 ? pu : -1;
+        const uint32_t xj = shfl_u32(L.x, j < 0 ? 0 : j);
+        const int tj = __shfl(L.term, j < 0 ? 0 : j, 64);
+        const uint32_t Xin = j >= 0 ? xj : X0;
+        const bool din = j >= 0 ? tj != TERM_NONE : dead0;
+        bool bad = false;
+        if (L.mode != LM_OFF) {
+            if (din) bad = L.mode != LM_DEAD;
+            else if (L.mode == LM_CHAIN) bad = L.E != Xin;
+            else if (L.mode == LM_NONE) bad = in_chunk(K, Xin);
+            else bad = true;                                   // LM_DEAD under a live chain
+        }
+        const u64 bm = __ballot(bad);
+        if (!bm) return;
+        if (iter > 2 * CLY_NL + 2) { if (lane == 0) atomicOr(&g->fail, 1u); return; }
+        const int k = __ffsll((long long)bm) - 1;
+        if (lane == k) {
+            if (din) chain_set(L, LM_DEAD);
+            else if (!in_chunk(K, Xin)) chain_set(L, LM_NONE);
+            else walk(K, Xin, true, L);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Look-back: the chain state and record count entering a tile.
+struct LBState {
+    uint64_t count;              // records of all tiles before
+    uint32_t X;                  // chain position
+    uint32_t crc_last;           // stored CRC of the last record started before (its successor's Q)
+    uint32_t P_last;             // that record's start (NONE32: none in this file)
+    int      dead;               // the file's chain has ended
+};
+__device__ __forceinline__ u64 ld_agent(const u64* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_agent(u64* p, u64 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+#define SPIN_MAX (1u << 18)
+
+__device__ __forceinline__ LBState lb_virtual() {
+    LBState s;
+    s.count = 0; s.X = 0; s.crc_last = 0; s.P_last = NONE32; s.dead = 1;
+    return s;
+}
+__device__ __forceinline__ LBState lb_incl(u64 i0, u64 i1, u64 i2) {
+    LBState s;
+    s.dead = (i0 & DF_TERM) != 0;
+    s.count = i0 >> 16;
+    s.X = (uint32_t)i1; s.crc_last = (uint32_t)(i1 >> 32);
+    s.P_last = (uint32_t)i2;
+    return s;
+}
+// State after tile u given the state before it and u's LOCAL; false when the
+// tile's guess disagrees with the state (then only its INCL can tell).
+__device__ __forceinline__ bool lb_local(LBState& s, u64 l0, u64 l1, u64 l2, u64 l3) {
+    if (!(l0 & DF_FOF)) {
+        if (s.dead) return true;                                    // nothing of the file after its end
+        if (l0 & DF_NONE) return s.X >= (uint32_t)l3;              // the chain passes the tile
+        if (s.X != (uint32_t)l1) return false;
+    }
+    s.count += l0 >> 32;
+    s.dead = (l0 & DF_TERM) != 0;
+    s.X = (uint32_t)(l1 >> 32);
+    if (l0 & DF_REC) { s.crc_last = (uint32_t)l2; s.P_last = (uint32_t)(l2 >> 32); }
+    else if (l0 & DF_FOF) { s.crc_last = 0; s.P_last = NONE32; }
+    return true;
+}
+__device__ __forceinline__ u64 shfl64(u64 v, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+    return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ void bad_spin(Globals* g, uint32_t code) { atomicOr(&g->fail, code); }
+
+__device__ __noinline__ LBState look_back(const TileDesc* desc, int64_t t, int lane, Globals* g) {
+    // nearest tile before t with a published INCL (tile -1: nothing, dead)
+    int64_t k = -1;
+    for (int64_t base = t - 1; base >= 0; base -= 64) {
+        const int64_t u = base - lane;
+        const bool pub = u >= 0 && (ld_agent(&desc[u].i[0]) & DF_PUB);
+        const u64 bm = __ballot(pub);
+        if (bm) { k = base - (__ffsll((long long)bm) - 1); break; }
+    }
+    LBState s = lb_virtual();
+    if (k >= 0) s = lb_incl(ld_agent(&desc[k].i[0]), ld_agent(&desc[k].i[1]), ld_agent(&desc[k].i[2]));
+    // forward from it over the LOCALs (or INCLs) of k+1 .. t-1, 64 per round
+    for (int64_t u0 = k + 1; u0 < t; u0 += 64) {
+        const int64_t u = u0 + lane;
+        int got = u < t ? 0 : 3;                       // 1 LOCAL, 2 INCL
+        u64 w0 = 0;
+        for (uint32_t spin = 0;; spin++) {
+            if (got == 0) {
+                const u64 i0 = ld_agent(&desc[u].i[0]);
+                if (i0 & DF_PUB) { got = 2; w0 = i0; }
+                else {
+                    const u64 l0 = ld_agent(&desc[u].l[0]);
+                    if (l0 & DF_PUB) { got = 1; w0 = l0; }
+                }
+            }
+            if (__ballot(got == 0) == 0) break;
+            if (spin > SPIN_MAX) { if (lane == 0) bad_spin(g, 2u); return s; }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        u64 w1 = 0, w2 = 0, w3 = 0;
+        if (got == 2) { w1 = ld_agent(&desc[u].i[1]); w2 = ld_agent(&desc[u].i[2]); }
+        else if (got == 1) { w1 = ld_agent(&desc[u].l[1]); w2 = ld_agent(&desc[u].l[2]); w3 = ld_agent(&desc[u].l[3]); }
+        // the last INCL of the round overrides everything before it
+        const u64 bi = __ballot(got == 2);
+        int m = bi ? 63 - __clzll((long long)bi) : 0;
+        const int n = t - u0 < 64 ? (int)(t - u0) : 64;
+        if (bi) { s = lb_incl(shfl64(w0, m), shfl64(w1, m), shfl64(w2, m)); m++; }
+        for (; m < n; m++) {
+            const u64 a0 = shfl64(w0, m), a1 = shfl64(w1, m), a2 = shfl64(w2, m), a3 = shfl64(w3, m);
+            if (!lb_local(s, a0, a1, a2, a3)) {
+                // the tile's guess was wrong: wait for it to publish its true state
+                const TileDesc* d = &desc[u0 + m];
+                u64 i0 = 0;
+                for (uint32_t spin = 0;; spin++) {
+                    i0 = ld_agent(&d->i[0]);
+                    if (i0 & DF_PUB) break;
+                    if (spin > SPIN_MAX) { if (lane == 0) bad_spin(g, 4u); return s; }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                s = lb_incl(i0, ld_agent(&d->i[1]), ld_agent(&d->i[2]));
+            }
+        }
+    }
+    return s;
+}
+
+// ---------------------------------------------------------------------------
+// Inputs of phase C for one lane (after the tile's chain is final).
+struct LaneIn {
+    uint64_t base;               // global tuple index of the lane's first record
+    uint32_t crc_in;             // stored CRC of the record open when the chunk starts
+    uint32_t P_in;               // its start (NONE32 none)
+    bool     spill;              // P_in's patch reaches into this chunk
+};
+
+// The patch of the record start P (stored CRC c, predecessor's cq) on the
+// words [wlo, whi) (absolute word indices), combined onto the last of them it
+// touches; returns that word (NONE32: none in range).
+__device__ __forceinline__ uint32_t patch_part(const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t P, uint32_t c,
+                                               uint32_t cq, uint32_t wlo, uint32_t whi, uint32_t& delta) {
+    const uint32_t j = P & 3, sh = 8 * j, a = P >> 2;
+    uint32_t acc = 0, wl = NONE32;
+    if (a >= wlo && a < whi) {
+        uint32_t pa = j ? (c << sh) : c;
+        if (P != 0) pa ^= q_of(smem, cq, j, cl.r4);
+        acc = pa; wl = a;
+    }
+    if (a + 1 >= wlo && a + 1 < whi) {
+        const uint32_t pb = (j ? (c >> (32 - sh)) : 0u) ^ (j ? (0xFFFFFFFFu << sh) : 0xFFFFFFFFu);
+        acc = wl == NONE32 ? pb : (crc_word(smem, acc, cl) ^ pb);
+        wl = a + 1;
+    }
+    if (j && a + 2 >= wlo && a + 2 < whi) {
+        const uint32_t pc = (1u << sh) - 1u;
+        acc = wl == NONE32 ? pc : (crc_word(smem, acc, cl) ^ pc);
+        wl = a + 2;
+    }
+    delta = acc;
+    return wl;
+}
+
+// Tuple of the record at p (header h): 48 B, cly_tuple layout.
+__device__ __forceinline__ void put_tuple(cly_tuple* out, uint64_t idx, uint64_t out_cap, const Chunk& K, uint32_t p,
+                                          const Hdr& h, uint32_t fid, Globals* g) {
+    int tn;
+    int64_t tx;
+    if (h.key0 < 0x80 && h.ks >= 1) { tn = 1; tx = (int64_t)(h.key0 >> 1) ^ -(int64_t)(h.key0 & 1); }
+    else {
+        const int64_t klim = h.ks < 11u ? (int64_t)h.ks : 11;
+        tx = go_varint(K.base + p + h.hsz, klim, tn);                   // parseLogRecordKey, db.go:706-710
+    }
+    if (idx >= out_cap) { atomicOr(&g->overflow, 1u); return; }
+    const uint64_t off = p, ex = (uint64_t)h.exp, txv = tn < 0 ? 0ull : (uint64_t)tx;
+    u32x4* dst = (u32x4*)(out + idx);
+    dst[0] = (u32x4){(uint32_t)off, (uint32_t)(off >> 32), (uint32_t)ex, (uint32_t)(ex >> 32)};
+    dst[1] = (u32x4){(uint32_t)txv, (uint32_t)(txv >> 32), fid, (uint32_t)h.size};
+    dst[2] = (u32x4){h.ks, h.vs,
+                     (h.type & 0xff) | ((h.dt & 0xff) << 8) | ((uint32_t)(h.hsz & 0xff) << 16) |
+                         ((uint32_t)(tn < 0 ? 0xFF : tn) << 24),
+                     h.crc};
+}
+
+// ---------------------------------------------------------------------------
+// Phase C, uniform path: the chunk's 4-byte words through the register, each
+// record's combined patch XORed in at its word (events held in a 4-deep
+// per-lane queue that the walker keeps filled, a quarter-burst ahead).
+struct Evq { uint32_t an[4], dl[4]; };
+__device__ __forceinline__ void evq_push(Evq& q, uint32_t w, uint32_t d) {
+    if (q.an[0] == NO_EV) { q.an[0] = w; q.dl[0] = d; }
+    else if (q.an[1] == NO_EV) { q.an[1] = w; q.dl[1] = d; }
+    else if (q.an[2] == NO_EV) { q.an[2] = w; q.dl[2] = d; }
+    else { q.an[3] = w; q.dl[3] = d; }
+}
+__device__ __forceinline__ void evq_pop1(Evq& q) {
+    q.an[0] = q.an[1]; q.dl[0] = q.dl[1];
+    q.an[1] = q.an[2]; q.dl[1] = q.dl[2];
+    q.an[2] = q.an[3]; q.dl[2] = q.dl[3];
+    q.an[3] = NO_EV;
+}
+template <int KS>
+__device__ __forceinline__ uint32_t crc_quarter(const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t s, const u32x4& va,
+                                                const u32x4& vb, uint32_t w0, const Evq& q) {
+    const uint32_t w[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
+    #pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint32_t x = s ^ w[i];
+        #pragma unroll
+        for (int k = 0; k < KS; k++) x ^= q.an[k] == w0 + (uint32_t)i ? q.dl[k] : 0u;
+        s = crc_word(smem, x, cl);
+    }
+    return s;
+}
+struct Walker {
+    uint32_t p, cq, i;
+    Gath gt;
+};
+__device__ __forceinline__ void walker_step(const Chunk& K, Walker& W, uint32_t nrec, uint64_t base, uint32_t fid,
+                                            cly_tuple* out, uint64_t out_cap, const CLY_LDS uint8_t* smem,
+                                            const CrcLane& cl, Evq& q, Globals* g) {
+    const Hdr h = hdr_at(K.base, W.p, K.len, W.gt);
+    put_tuple(out, base + W.i, out_cap, K, W.p, h, fid, g);
+    uint32_t d;
+    const uint32_t wlo = K.cb >> 2;
+    const uint32_t w = patch_part(smem, cl, W.p, h.crc, W.cq, wlo, wlo + CLY_NW, d);
+    if (w != NONE32) evq_push(q, w - wlo, d);
+    W.cq = h.crc;
+    W.p += (uint32_t)h.size;
+    W.i++;
+    if (W.i < nrec && gath_ok(W.p, K.len)) gath_issue(K.base, W.p, W.gt);
+}
+
+__device__ __noinline__ uint32_t phase_c_fast(const Chunk& K, const LaneChain& L, const LaneIn& I, bool active, uint32_t fid,
+                                 cly_tuple* out, uint64_t out_cap, const CLY_LDS uint8_t* smem, const CrcLane& cl,
+                                 Globals* g) {
+    uint32_t s = 0;
+    Evq q;
+    #pragma unroll
+    for (int k = 0; k < 4; k++) { q.an[k] = NO_EV; q.dl[k] = 0; }
+    const uint32_t wlo = K.cb >> 2;
+    if (active && I.spill) {
+        uint32_t d;
+        const uint32_t w = patch_part(smem, cl, I.P_in, I.crc_in, 0u, wlo, wlo + CLY_NW, d);
+        if (w != NONE32) evq_push(q, w - wlo, d);
+    }
+    Walker W;
+    W.p = L.E; W.cq = I.crc_in; W.i = 0;
+    const uint32_t nrec = (active && L.mode == LM_CHAIN) ? L.cnt : 0u;
+    if (nrec && gath_ok(W.p, K.len)) gath_issue(K.base, W.p, W.gt);
+    const u32x4* src = (const u32x4*)(K.base + K.cb);
+    for (int b = 0; b < CLY_NB; b++) {
+        u32x4 v[CLY_BW / 4];
+        if (active) {
+            #pragma unroll
+            for (int k = 0; k < CLY_BW / 4; k++) v[k] = src[b * (CLY_BW / 4) + k];
+        } else {
+            #pragma unroll
+            for (int k = 0; k < CLY_BW / 4; k++) v[k] = (u32x4){0u, 0u, 0u, 0u};
+        }
+        #pragma unroll
+        for (int qq = 0; qq < CLY_BW / 8; qq++) {
+            const uint32_t w0 = (uint32_t)(b * CLY_BW + 8 * qq);
+            // every event of this quarter must be queued: step the walker while its
+            // next record's first patch word is near
+            for (;;) {
+                const bool need = W.i < nrec && q.an[3] == NO_EV && ((W.p >> 2) - wlo) < w0 + 16;
+                if (!__ballot(need)) break;
+                if (need) walker_step(K, W, nrec, I.base, fid, out, out_cap, smem, cl, q, g);
+            }
+            const uint32_t we = w0 + 8;
+            const uint32_t nh = (q.an[0] < we) + (q.an[1] < we) + (q.an[2] < we) + (q.an[3] < we);
+            if (__ballot(nh >= 3)) {
+                s = crc_quarter<4>(smem, cl, s, v[2 * qq], v[2 * qq + 1], w0, q);
+                for (int r = 0; r < 4; r++) if ((uint32_t)r < nh) evq_pop1(q);
+            } else if (__ballot(nh == 2)) {
+                s = crc_quarter<2>(smem, cl, s, v[2 * qq], v[2 * qq + 1], w0, q);
+                for (int r = 0; r < 2; r++) if ((uint32_t)r < nh) evq_pop1(q);
+            } else if (__ballot(nh == 1)) {
+                s = crc_quarter<1>(smem, cl, s, v[2 * qq], v[2 * qq + 1], w0, q);
+                if (nh) evq_pop1(q);
+            } else {
+                s = crc_quarter<0>(smem, cl, s, v[2 * qq], v[2 * qq + 1], w0, q);
+            }
+        }
+    }
+    return s;
+}
+
+// ---------------------------------------------------------------------------
+// Phase C, exact path (the lane holding the chain's terminal, lanes with
+// records shorter than 12 bytes, and k_locate): word by word with every
+// boundary's byte patches, everything from the terminal T on zeroed.  Starts
+// from register s0.  With `observe`, the first record whose check fails
+// (register after its end word != 0) is returned in fail_P / fail_i.
+struct Bnd { uint32_t P, c, q, start; uint64_t idx; int term; };
+__device__ __noinline__ uint32_t exact_lane(const Chunk& K, const LaneChain& L, const LaneIn& I, uint32_t s0, bool emit,
+                               bool observe, uint32_t fid, cly_tuple* out, uint64_t out_cap,
+                               const CLY_LDS uint8_t* smem, const CrcLane& cl, Globals* g, uint32_t& fail_P,
+                               uint64_t& fail_i, uint32_t& expect) {
+    uint32_t s = s0;
+    fail_P = NONE32; fail_i = 0; expect = 0;
+    Bnd bq[4];
+    int nb = 0;
+    if (I.spill) { bq[0].P = I.P_in; bq[0].c = I.crc_in; bq[0].q = 0; bq[0].term = 0; bq[0].start = NONE32; bq[0].idx = 0; nb = 1; }
+    const uint32_t T = (L.mode == LM_CHAIN && L.term != TERM_NONE) ? L.x : NONE32;
+    uint32_t wp = L.E, cq = I.crc_in, wi = 0, start = I.P_in;
+    uint64_t sidx = I.base - 1;
+    const uint32_t nrec = L.mode == LM_CHAIN ? L.cnt : 0u;
+    bool tpushed = T == NONE32;
+    for (uint32_t w = 0; w < CLY_NW; w++) {
+        const uint32_t A = K.cb + 4 * w;
+        // queue the boundaries whose first patch word is this one
+        for (;;) {
+            if (wi < nrec && (wp >> 2) == (A >> 2) && nb < 4) {
+                const Hdr h = hdr_load(K.base, wp, K.len);
+                if (emit) put_tuple(out, I.base + wi, out_cap, K, wp, h, fid, g);
+                Bnd& b = bq[nb++];
+                b.P = wp; b.c = h.crc; b.q = wp != 0 ? q_of(smem, cq, wp & 3, cl.r4) : 0u; b.term = 0;
+                b.start = start; b.idx = sidx;
+                start = wp; sidx = I.base + wi;
+                cq = h.crc; wp += (uint32_t)h.size; wi++;
+                continue;
+            }
+            if (!tpushed && wi >= nrec && (T >> 2) == (A >> 2) && nb < 4) {
+                Bnd& b = bq[nb++];
+                b.P = T; b.c = 0; b.q = T != 0 ? q_of(smem, cq, T & 3, cl.r4) : 0u; b.term = 1;
+                b.start = start; b.idx = sidx;
+                tpushed = true;
+                continue;
+            }
+            break;
+        }
+        uint32_t d = 0;
+        if ((uint64_t)A < K.len) {
+            d = *(const uint32_t*)(K.base + A);
+            const uint64_t n = K.len - A;
+            if (n < 4) d &= (1u << (8 * n)) - 1u;
+        }
+        if (T != NONE32 && A + 4 > T) d = A >= T ? 0u : (d & ((1u << (8 * (T - A))) - 1u));
+        uint32_t patch = 0;
+        for (int k = 0; k < nb; k++) {
+            const Bnd& b = bq[k];
+            #pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint32_t x = A + i;
+                uint32_t m = 0;
+                if (!b.term && x >= b.P && x < b.P + 4) m = (d >> (8 * i)) & 0xffu;          // stored CRC zeroed
+                if (!b.term && x >= b.P + 4 && x < b.P + 8) m ^= 0xffu;                     // init 0xFF
+                patch ^= m << (8 * i);
+            }
+            if ((b.P >> 2) == (A >> 2)) patch ^= b.q;
+        }
+        s = crc_word(smem, s ^ d ^ patch, cl);
+        if (observe && fail_P == NONE32) {
+            for (int k = 0; k < nb; k++)
+                if ((bq[k].P >> 2) == (A >> 2) && bq[k].P != 0 && bq[k].start != NONE32 && s != 0) {
+                    fail_P = bq[k].start; fail_i = bq[k].idx;
+                }
+        }
+        // retire boundaries whose patch span ended
+        int o = 0;
+        for (int k = 0; k < nb; k++) if (bq[k].P + 8 > A + 4 && !(bq[k].term && (bq[k].P >> 2) <= (A >> 2))) bq[o++] = bq[k];
+        nb = o;
+        if (nb == 4) { if (emit) atomicOr(&g->fail, 16u); }
+    }
+    // the terminal one word past a full chunk (T = len = chunk end): the register
+    // after the chunk must equal Q there
+    if (!tpushed) {
+        expect = T != 0 ? q_of(smem, cq, 0, cl.r4) : 0u;
+        if (observe && fail_P == NONE32 && s != expect && start != NONE32) { fail_P = start; fail_i = sidx; }
+    }
+    return s;
+}
+
+// ---------------------------------------------------------------------------
+// One tile: phase A, agreement, look-back, phase C, fold.
+__device__ __forceinline__ int find_file(const uint32_t* __restrict__ tprefix, int nfiles, uint32_t t) {
+    int lo = 0, hi = nfiles - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (tprefix[mid] <= t) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+__device__ __forceinline__ Chunk make_chunk(const DevFile& F, uint32_t tt, int lane) {
+    Chunk K;
+    K.base = F.base; K.len = F.len;
+    const uint64_t cb = (uint64_t)tt * CLY_TILE + (uint64_t)lane * CLY_CH;
+    K.cb = (uint32_t)cb;
+    K.ce = (uint32_t)(cb + CLY_CH < F.len ? cb + CLY_CH : F.len);
+    K.last = cb + CLY_CH >= F.len;
+    K.on = cb < F.len || cb == 0;
+    if (!K.on) { K.cb = 0xFFFFFFF0u; K.ce = 0xFFFFFFF0u; }
+    return K;
+}
+// Lane inputs from the final chain and the state entering the tile.
+__device__ __forceinline__ LaneIn lane_inputs(const Chunk& K, const LaneChain& L, const LBState& S, int lane,
+                                             uint32_t& tile_cnt) {
+    LaneIn I;
+    const uint32_t cnt = (L.mode == LM_CHAIN) ? L.cnt : 0u;
+    const uint32_t incl = scan_add_incl(cnt, lane);
+    tile_cnt = shfl_u32(incl, 63);
+    I.base = S.count + (incl - cnt);
+    const int pr = scan_max_incl(cnt > 0 ? lane : -1, lane);
+    const int pu = __shfl_up(pr, 1, 64);
+    const int j = lane > 0 ? pu : -1;
+    const uint32_t lc = shfl_u32(L.last_crc, j < 0 ? 0 : j), lp = shfl_u32(L.last, j < 0 ? 0 : j);
+    I.crc_in = j >= 0 ? lc : S.crc_last;
+    I.P_in = j >= 0 ? lp : S.P_last;
+    I.spill = K.on && (L.mode == LM_CHAIN || L.mode == LM_NONE) && I.P_in != NONE32 && I.P_in + 8 > K.cb &&
+              I.P_in < K.cb;
+    return I;
+}
+// Fold of the lanes' registers: sum over l of A^(CLY_CH (63 - l)) r_l (lane 0).
+__device__ __forceinline__ uint32_t tile_fold(const CLY_LDS uint8_t* smem, uint32_t r, int lane) {
+    #pragma unroll
+    for (int lvl = 0; lvl < 6; lvl++) {
+        const int d = 1 << lvl;
+        const uint32_t o = (uint32_t)__shfl_down((int)r, d, 64);
+        const uint32_t sh = nib_mul(smem, lvl, r);
+        if ((lane & (2 * d - 1)) == 0) r = sh ^ o;
     }
     return r;
 }
-__device__ __forceinline__ LinkAgg link_ident() {
-    LinkAgg e;
-    #pragma unroll
-    for (int t = 0; t < 2; t++) { e.br[t].x = 0; e.br[t].cnt = 0; e.br[t].set = 0; e.br[t].term = 0; }
-    return e;
-}
-__device__ __forceinline__ LinkAgg link_elem(const SubDesc& d) {
-    LinkAgg e = link_ident();
-    if (d.mode == MODE_NORMAL) {
-        const int32_t term = (d.flags & SD_TERM) != 0;
-        e.br[0].set = 1; e.br[0].x = d.x; e.br[0].term = term; e.br[0].cnt = d.cnt;
-        if (d.flags & SD_FOF) e.br[1] = e.br[0];
-    }
-    return e;
-}
-// Exclusive block scan of the threads' aggregates; returns the block total.
-__device__ __forceinline__ LinkAgg link_block_scan(LinkAgg v, LinkAgg& excl) {
-    __shared__ LinkAgg sh[LINK_NT];
-    const int t = threadIdx.x;
-    sh[t] = v;
-    __syncthreads();
-    for (int o = 1; o < LINK_NT; o <<= 1) {
-        LinkAgg u = link_ident();
-        if (t >= o) u = sh[t - o];
-        __syncthreads();
-        if (t >= o) sh[t] = link_op(u, sh[t]);
-        __syncthreads();
-    }
-    excl = t > 0 ? sh[t - 1] : link_ident();
-    const LinkAgg tot = sh[LINK_NT - 1];
-    __syncthreads();
-    return tot;
-}
 
-__global__ void __launch_bounds__(LINK_NT)
-k_link1(const SubDesc* __restrict__ descs, int64_t nsub, LinkAgg* blk) {
-    const int64_t b0 = (int64_t)blockIdx.x * LINK_BLK + (int64_t)threadIdx.x * LINK_IT;
-    LinkAgg v = link_ident();
-    for (int i = 0; i < LINK_IT; i++) if (b0 + i < nsub) v = link_op(v, link_elem(descs[b0 + i]));
-    LinkAgg ex;
-    const LinkAgg tot = link_block_scan(v, ex);
-    if (threadIdx.x == 0) blk[blockIdx.x] = tot;
-}
-
-// One block: exclusive scan of the block aggregates (in place).
-__global__ void __launch_bounds__(LINK_NT)
-k_link2(LinkAgg* blk, int64_t nblk) {
-    const int64_t per = (nblk + LINK_NT - 1) / LINK_NT;
-    const int64_t b0 = (int64_t)threadIdx.x * per;
-    LinkAgg v = link_ident();
-    for (int64_t i = 0; i < per; i++) if (b0 + i < nblk) v = link_op(v, blk[b0 + i]);
-    LinkAgg ex;
-    link_block_scan(v, ex);
-    LinkAgg run = ex;
-    for (int64_t i = 0; i < per; i++) {
-        if (b0 + i < nblk) { const LinkAgg a = blk[b0 + i]; blk[b0 + i] = run; run = link_op(run, a); }
-    }
-}
-
-// Per sub-tile: output slot, and whether its chain is the one the link state
-// implies; if not, a candidate (with the implied chain).  A wrong chain entered
-// live is "harmful" (it misleads the state of what follows): the first harmful
-// sub-tile of each file goes to fh[file].
-__global__ void __launch_bounds__(LINK_NT)
-k_link3(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ sub_prefix,
-        const SubDesc* __restrict__ descs, int64_t nsub, const LinkAgg* __restrict__ blk, uint64_t* sub_P, Fix* cand,
-        uint32_t cand_cap, int32_t* fh, unsigned long long* fck, uint32_t* cflag, uint32_t stamp, Globals* g) {
-    const int64_t b0 = (int64_t)blockIdx.x * LINK_BLK + (int64_t)threadIdx.x * LINK_IT;
-    LinkAgg v = link_ident();
-    SubDesc d[LINK_IT];
-    for (int i = 0; i < LINK_IT; i++) {
-        if (b0 + i < nsub) { d[i] = descs[b0 + i]; v = link_op(v, link_elem(d[i])); }
-    }
-    LinkAgg ex;
-    link_block_scan(v, ex);
-    LinkAgg run = link_op(blk[blockIdx.x], ex);
-    for (int i = 0; i < LINK_IT; i++) {
-        const int64_t s = b0 + i;
-        if (s >= nsub) break;
-        const LinkBr& st = run.br[1];          // state entering s (sub-tile 0 resets it)
-        sub_P[s] = st.cnt;
-        int mode, entry = 0;
-        int64_t x_in = st.x;
-        bool live = true;
-        if (d[i].flags & SD_FOF) { mode = MODE_NORMAL; entry = 0; x_in = s * (int64_t)CLY_TS; }
-        else if (!st.set) { mode = -1; atomicOr(&g->fail, 6u); }            // cannot happen
-        else if (st.term) { mode = MODE_DEAD; live = false; }
-        else {
-            const int64_t rel = st.x - s * (int64_t)CLY_TS;
-            if (rel >= CLY_TS) mode = MODE_PASS;
-            else if (rel < 0) mode = -1;       // a sub-tile before s is wrong (and a candidate)
-            else { mode = MODE_NORMAL; entry = (int)rel; }
-        }
-        const bool ok = mode >= 0 && d[i].mode == mode && (mode != MODE_NORMAL || d[i].entry == entry);
-        if (!ok) {
-            const uint32_t f = (uint32_t)find_file(sub_prefix, nfiles, s);
-            // harmful: the wrong chain changes the state passed on (PASS and DEAD both pass it through)
-            const bool harmful = live && mode >= 0 && (mode == MODE_NORMAL || d[i].mode == MODE_NORMAL);
-            if (harmful) atomicMin(&fh[f], (int32_t)s);
-            cflag[s] = 2 * stamp + (harmful ? 1u : 0u);
-            const uint32_t k = atomicAdd(&g->ncand, 1u);
-            if (k < cand_cap) {
-                Fix c;
-                c.s = (uint32_t)s; c.mode = mode; c.entry = entry; c.file = f; c.x_in = x_in;
-                c.certain = 0; c._pad = 0;
-                cand[k] = c;
-                atomicMin(&fck[f], ((unsigned long long)s << 32) | k);      // first candidate of the file
-            }
-        }
-        run = link_op(run, link_elem(d[i]));
-        if (s == nsub - 1) g->total = run.br[1].cnt;
-    }
-}
-
-// Serial resolution (after parallel rounds that did not converge): one wave per
-// file walks from the file's first candidate to its end, keeping the exact
-// chain state, and re-processes every sub-tile that disagrees with it.  The
-// descriptors are read 64 ahead (one per lane).
-__global__ void __launch_bounds__(64)
-k_serial(const DevFile* __restrict__ files, const Fix* __restrict__ cand, const unsigned long long* __restrict__ fck,
-         SubDesc* descs, ChunkSum* sums, const uint32_t* __restrict__ cols, cly_tuple* staging, Globals* g) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const unsigned long long key = fck[blockIdx.x];
-    if (key == ~0ull) return;
+__global__ void __launch_bounds__(512, 2)
+k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
+       TileDesc* desc, uint32_t* treg, FileInfo* finfo, const uint32_t* __restrict__ nib, cly_tuple* out,
+       uint64_t out_cap, Globals* g, uint32_t* dump) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
-    init_tables(smem, cols);
-    const int lane = threadIdx.x;
-    CLY_LDS uint32_t* w32 = (CLY_LDS uint32_t*)(smem + LDS_WIN);
-    CLY_LDS u32x2* pool = (CLY_LDS u32x2*)(smem + LDS_POOL);
-    const Fix c = cand[key & 0xffffffffull];
-    const DevFile F = files[blockIdx.x];
-    const int64_t s_end = (int64_t)F.first_sub + F.nsub;
-    if (c.mode < 0) { if (lane == 0) atomicOr(&g->fail, 9u); return; }      // cannot happen
-    int64_t s = c.s, x = c.x_in;
-    int mode = c.mode, entry = c.entry;
-    int64_t base = -1;
-    SubDesc ahead;
+    init_tables(smem, nib);
+    const int lane = threadIdx.x & 63;
+    const CrcLane cl = crc_lane(lane);
     for (;;) {
-        if (s >= base + 64) {
-            base = s;
-            if (s + lane < s_end) ahead = descs[s + lane];
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(&g->ticket, 1u);
+        t = (uint32_t)__builtin_amdgcn_readfirstlane((int)shfl_u32(t, 0));
+        if (t >= ntiles) break;
+        const int f = find_file(tprefix, nfiles, t);
+        const DevFile F = files[f];
+        const uint32_t tt = t - F.first_tile;
+        const bool fof = tt == 0;
+        const Chunk K = make_chunk(F, tt, lane);
+        DBG("t %u file %d start\n", t, f);
+        // ---- A: chains under the lanes' own guesses, made to agree
+        LaneChain L;
+        phase_a(K, L);
+        const uint32_t dbg_m0 = (uint32_t)L.mode, dbg_e0 = L.E;
+        uint32_t G = NONE32;
+        {
+            const u64 bm = __ballot(L.mode == LM_CHAIN);
+            if (bm) G = shfl_u32(L.E, __ffsll((long long)bm) - 1);
         }
-        const int k = (int)(s - base);
-        SubDesc d;
-        d.x = (int64_t)__shfl((long long)ahead.x, k, 64);
-        d.cnt = (uint32_t)__shfl((int)ahead.cnt, k, 64);
-        d.entry = (int16_t)__shfl((int)ahead.entry, k, 64);
-        d.mode = (uint8_t)__shfl((int)ahead.mode, k, 64);
-        d.flags = (uint8_t)__shfl((int)ahead.flags, k, 64);
-        if (!(d.mode == mode && (mode != MODE_NORMAL || d.entry == entry))) {
-            u32x4 pf[PF_N];
-            process_sub(s, mode, entry, F, lane, smem, w32, pool, descs, sums, staging, g, 8, d, false, nullptr, pf);
-        }
-        bool dead = mode == MODE_DEAD || (d.mode == MODE_NORMAL && (d.flags & SD_TERM));
-        if (d.mode == MODE_NORMAL && !dead) x = d.x;
-        if (++s >= s_end) break;
-        if (dead) { mode = MODE_DEAD; entry = 0; continue; }
-        const int64_t rel = x - s * (int64_t)CLY_TS;
-        if (rel < 0) { if (lane == 0) atomicOr(&g->fail, 10u); break; }    // cannot happen
-        mode = rel >= CLY_TS ? MODE_PASS : MODE_NORMAL;
-        entry = rel >= CLY_TS ? 0 : (int)rel;
-    }
-}
-
-// Per-round reset of the link state (one launch instead of four memsets).
-__global__ void __launch_bounds__(LINK_NT)
-k_round_init(int32_t* fh, unsigned long long* fck, int nfiles, Globals* g) {
-    const int i = blockIdx.x * LINK_NT + threadIdx.x;
-    if (i == 0) { g->nfix = 0; g->ncand = 0; }
-    if (i < nfiles) { fh[i] = 0x7f7f7f7f; fck[i] = ~0ull; }
-}
-
-// Fix list of the round: every candidate up to and including the first harmful
-// sub-tile of its file (its state is certain); later candidates only when they
-// hold a wrong record chain (never turned into PASS / DEAD on an uncertain
-// state, which would discard a good guess: a false exit far ahead makes every
-// sub-tile up to it look covered).  Uncertain fixes run after the certain walks
-// and are dropped when their chain ends before the file does.
-__global__ void __launch_bounds__(LINK_NT)
-k_link4(const DevFile* __restrict__ files, const SubDesc* __restrict__ descs, const Fix* __restrict__ cand,
-        const int32_t* __restrict__ fh, const uint32_t* __restrict__ cflag, Fix* fixes, uint32_t* listed,
-        uint32_t stamp, Globals* g) {
-    const uint32_t n = g->ncand;
-    for (uint32_t i = blockIdx.x * LINK_NT + threadIdx.x; i < n; i += gridDim.x * LINK_NT) {
-        const Fix c = cand[i];
-        if (c.mode < 0) continue;
-        // certain: no harmful candidate since the last sub-tile that agreed with
-        // its state on a record entry (its own exit then fixes the state), or
-        // since the file start; past 256 sub-tiles back: since the file start
-        bool certain = (int64_t)c.s <= (int64_t)fh[c.file];
-        if (!certain) {
-            const int64_t s_first = files[c.file].first_sub;
-            int64_t t = (int64_t)c.s - 1;
-            for (int k = 0; k < 256 && t >= s_first; k++, t--) {
-                const uint32_t cf = cflag[t];
-                if (cf == 2 * stamp + 1) break;                      // harmful candidate: uncertain
-                if (cf == 2 * stamp) continue;                       // harmless candidate
-                if (descs[t].mode == MODE_NORMAL) { certain = true; break; }   // agreed on an entry
+        DBG("t %u phase A done G %u\n", t, G);
+        resolve(K, L, lane, fof ? 0u : G, false, g);
+        DBG("t %u resolved\n", t);
+        const uint32_t dbg_m1 = (uint32_t)L.mode, dbg_e1 = L.E;
+        {
+            // LOCAL descriptor
+            const u64 bc = __ballot(L.mode == LM_CHAIN), br = __ballot(L.mode == LM_CHAIN && L.cnt > 0);
+            uint32_t tile_cnt = 0;
+            {
+                const uint32_t c = L.mode == LM_CHAIN ? L.cnt : 0u;
+                tile_cnt = shfl_u32(scan_add_incl(c, lane), 63);
             }
-            if (t < s_first) certain = true;
+            const int lc = bc ? 63 - __clzll((long long)bc) : 0, lr = br ? 63 - __clzll((long long)br) : 0;
+            const uint32_t X = shfl_u32(L.x, lc);
+            const int term = __shfl(L.term, lc, 64);
+            const uint32_t crc = shfl_u32(L.last_crc, lr), Pl = shfl_u32(L.last, lr);
+            if (lane == 0) {
+                const uint64_t tstart = (uint64_t)tt * CLY_TILE;
+                const uint32_t tend = tstart + CLY_TILE >= F.len ? (uint32_t)(F.len + 1) : (uint32_t)(tstart + CLY_TILE);
+                TileDesc* d = &desc[t];
+                st_agent(&d->l[1], (u64)G | ((u64)X << 32));
+                st_agent(&d->l[2], (u64)crc | ((u64)Pl << 32));
+                st_agent(&d->l[3], (u64)tend);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                u64 f0 = DF_PUB | ((u64)tile_cnt << 32);
+                if (bc && term != TERM_NONE) f0 |= DF_TERM;
+                if (!bc) f0 |= DF_NONE;
+                if (fof) f0 |= DF_FOF;
+                if (br) f0 |= DF_REC;
+                st_agent(&d->l[0], f0);
+            }
         }
-        if (!certain && c.mode != MODE_NORMAL) continue;
-        listed[c.s] = certain ? stamp : (stamp | LISTED_U);
-        Fix e = c;
-        e.certain = certain;
-        fixes[atomicAdd(&g->nfix, 1u)] = e;
-        atomicAdd(&g->fix_total, 1u);
+        // ---- L: the true state entering the tile
+        DBG("t %u local published\n", t);
+        LBState S = look_back(desc, (int64_t)t, lane, g);
+        DBG("t %u look-back done\n", t);
+        if (fof) { S.dead = 0; S.X = 0; S.crc_last = 0; S.P_last = NONE32; }
+        if (!fof && (S.dead || S.X != G) && lane == 0) atomicAdd(&g->refix, 1u);
+        resolve(K, L, lane, S.dead ? 0u : S.X, S.dead != 0, g);
+        uint32_t tile_cnt;
+        const LaneIn I = lane_inputs(K, L, S, lane, tile_cnt);
+        if (dump) {
+            // debug dump (CLY_DUMP): the final chain of every lane
+            uint32_t* o = dump + ((uint64_t)t * 64 + lane) * 12;
+            o[0] = (uint32_t)L.mode; o[1] = L.E; o[2] = L.x; o[3] = (uint32_t)L.term; o[4] = L.cnt;
+            o[5] = S.X | (S.dead ? 0x80000000u : 0u); o[6] = G; o[7] = (uint32_t)f;
+            o[8] = dbg_m0; o[9] = dbg_e0; o[10] = dbg_m1; o[11] = dbg_e1;
+        }
+        {
+            // INCL descriptor
+            LBState o = S;
+            o.count += tile_cnt;
+            const u64 bc = __ballot(L.mode == LM_CHAIN), br = __ballot(L.mode == LM_CHAIN && L.cnt > 0);
+            if (bc) {
+                const int lc = 63 - __clzll((long long)bc);
+                o.X = shfl_u32(L.x, lc);
+                o.dead = __shfl(L.term, lc, 64) != TERM_NONE;
+            }
+            if (br) {
+                const int lr = 63 - __clzll((long long)br);
+                o.crc_last = shfl_u32(L.last_crc, lr);
+                o.P_last = shfl_u32(L.last, lr);
+            }
+            if (lane == 0) {
+                TileDesc* d = &desc[t];
+                st_agent(&d->i[1], (u64)o.X | ((u64)o.crc_last << 32));
+                st_agent(&d->i[2], (u64)o.P_last);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                st_agent(&d->i[0], DF_PUB | (o.dead ? DF_TERM : 0ull) | (o.count << 16));
+                if (fof) finfo[f].first_index = S.count;
+                if (t == ntiles - 1) g->total = o.count;
+            }
+        }
+        // ---- C: CRC stream, tuples
+        const bool term_lane = L.mode == LM_CHAIN && L.term != TERM_NONE;
+        const bool slow = L.mode == LM_CHAIN && !term_lane && L.minsz < 12;
+        const bool fast = (L.mode == LM_CHAIN && !term_lane && !slow) || L.mode == LM_NONE;
+        DBG("t %u incl published\n", t);
+        uint32_t r = phase_c_fast(K, L, I, fast, F.fid, out, out_cap, smem, cl, g);
+        DBG("t %u phase C fast done\n", t);
+        if (term_lane || slow) {
+            uint32_t fp, ex;
+            uint64_t fi;
+            r = exact_lane(K, L, I, 0u, true, false, F.fid, out, out_cap, smem, cl, g, fp, fi, ex);
+            if (slow) atomicAdd(&g->slow_lanes, 1u);
+            if (term_lane) {
+                FileInfo* fo = &finfo[f];
+                fo->term_pos = L.x; fo->term_status = L.term; fo->term_tile = t; fo->term_lane = (uint32_t)lane;
+                fo->expect = ex; fo->end_index = I.base + L.cnt; fo->has_term = 1;
+            }
+        }
+        if (!fast && !term_lane && !slow) r = 0;
+        r = tile_fold(smem, r, lane);
+        if (lane == 0) treg[t] = r;
+        DBG("t %u done\n", t);
     }
 }
 
-// Staged tuples to their output slots: CP_SUBS sub-tiles per workgroup, one
-// 16-B piece per thread and step, all loads of a thread issued before its stores.
-#define CP_SUBS 16
-#define CP_NT 256
-#define CP_PER ((CP_SUBS * CLY_CAP * 3 + CP_NT - 1) / CP_NT)
-__global__ void __launch_bounds__(CP_NT)
-k_copy(const SubDesc* __restrict__ descs, const uint64_t* __restrict__ sub_P, const cly_tuple* __restrict__ staging,
-       cly_tuple* out, uint64_t out_cap, int64_t nsub, Globals* g) {
-    __shared__ uint32_t n_s[CP_SUBS];
-    __shared__ uint64_t p_s[CP_SUBS];
-    const int64_t s0 = (int64_t)blockIdx.x * CP_SUBS;
-    const int tid = threadIdx.x;
-    if (tid < CP_SUBS) {
-        const int64_t s = s0 + tid;
-        uint32_t n = 0;
-        uint64_t P = 0;
-        if (s < nsub) {
-            const SubDesc d = descs[s];
-            if (d.mode == MODE_NORMAL && !(d.flags & SD_OVF)) n = d.cnt * 3;
-            P = sub_P[s];
-        }
-        n_s[tid] = n;
-        p_s[tid] = P;
-    }
-    __syncthreads();
-    const u32x4* src = (const u32x4*)(staging + (uint64_t)s0 * CLY_CAP);
-    u32x4* dst = (u32x4*)out;
-    const uint64_t lim = out_cap * 3;
-    u32x4 v[CP_PER];
-    #pragma unroll
-    for (int k = 0; k < CP_PER; k++) {
-        const int e = k * CP_NT + tid, j = e / (CLY_CAP * 3), q = e - j * (CLY_CAP * 3);
-        const int r = q / 3, pl = q - 3 * r;                 // tuple r, piece pl (plane layout)
-        if (j < CP_SUBS && (uint32_t)q < n_s[j])
-            v[k] = __builtin_nontemporal_load(src + j * (CLY_CAP * 3) + pl * CLY_CAP + r);
-    }
-    bool of = false;
-    #pragma unroll
-    for (int k = 0; k < CP_PER; k++) {
-        const int e = k * CP_NT + tid, j = e / (CLY_CAP * 3), q = e - j * (CLY_CAP * 3);
-        if (j < CP_SUBS && (uint32_t)q < n_s[j]) {
-            const uint64_t i = p_s[j] * 3 + (uint64_t)q;
-            if (i < lim) dst[i] = v[k]; else of = true;
-        }
-    }
-    if (of) atomicOr(&g->overflow, 1u);
+// ---------------------------------------------------------------------------
+// k_fin: per file, the fold of its tile registers up to the terminal's tile
+// must equal A^(CLY_CH (63 - terminal lane)) expect.
+__device__ __forceinline__ uint32_t xpow_mul(const uint32_t* __restrict__ pw, uint64_t m, uint32_t v) {
+    for (int k = 0; m; k++, m >>= 1) if (m & 1) v = cly_multmodp(pw[k], v);
+    return v;
 }
-
-// Sub-tiles whose tuples did not fit the staging slot: re-read and emitted
-// (one wave per sub-tile; launched only when there are any).
-__global__ void __launch_bounds__(64 * CLY_NDW)
-k_place(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ sub_prefix, int64_t nsub,
-        const SubDesc* __restrict__ descs, const uint64_t* __restrict__ sub_P, const cly_tuple* __restrict__ staging,
-        cly_tuple* out, uint64_t out_cap, Globals* g) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    CLY_LDS uint32_t* w32 = (CLY_LDS uint32_t*)(smem + wave * CLY_WIN);
-    const int64_t stride = (int64_t)gridDim.x * CLY_NDW;
-    for (int64_t s = (int64_t)blockIdx.x * CLY_NDW + wave; s < nsub; s += stride) {
-        const SubDesc d = descs[s];
-        if (d.mode != MODE_NORMAL || d.cnt == 0) continue;
-        const uint64_t P = sub_P[s];
-        if (d.flags & SD_OVF) {
-            const DevFile F = files[find_file(sub_prefix, nfiles, s)];
-            Sub T;
-            sub_setup(T, s, F, w32);
-            if (stage(T, lane, w32)) stage_wait();
-            Spec sp;
-            int guess = -1;
-            sub_spec(T, lane, sp, guess);
-            Lane L;
-            Chain R;
-            sub_chain(T, sp, lane, MODE_NORMAL, d.entry, L, R);
-            emit_direct(T, L, P + L.base, out, out_cap, g);
-        }
-    }
-}
-
-// First event of every file: one thread per sub-tile (its in-tile event, or
-// the CRC failure of its open record), min-reduced per file on the key
-// (offset << 32 | sub-tile of the file); then one thread per file.
 #define FIN_NT 256
 __global__ void __launch_bounds__(FIN_NT)
-k_fin1(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ sub_prefix, int64_t nsub,
-       const ChunkSum* __restrict__ sums, const uint64_t* __restrict__ sub_P, const uint32_t* __restrict__ x8n,
-       unsigned long long* fkey) {
-    const int64_t s = (int64_t)blockIdx.x * FIN_NT + threadIdx.x;
-    if (s >= nsub) return;
-    const int f = find_file(sub_prefix, nfiles, s);
+k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __restrict__ treg,
+      const uint32_t* __restrict__ nib, const uint32_t* __restrict__ pw, Globals* g) {
+    __shared__ uint32_t tab[NIB_LEVELS * 128];
+    __shared__ uint32_t part[FIN_NT];
+    __shared__ uint32_t plen[FIN_NT];
+    for (int i = threadIdx.x; i < NIB_LEVELS * 128; i += FIN_NT) tab[i] = nib[i];
+    __syncthreads();
+    const int f = blockIdx.x;
     const DevFile F = files[f];
-    uint64_t gi = 0;
-    int32_t st = 0;
-    const int64_t i = s - (int64_t)F.first_sub;
-    const int64_t o = fin_chunk_event(sums, sub_P, x8n, F.first_sub, F.nsub, i, &gi, &st);
-    if (o != EVT_NONE) atomicMin(&fkey[f], ((unsigned long long)o << 32) | (unsigned long long)i);
-}
-__global__ void __launch_bounds__(FIN_NT)
-k_fin2(const DevFile* __restrict__ files, int nfiles, const ChunkSum* __restrict__ sums,
-       const uint64_t* __restrict__ sub_P, const uint32_t* __restrict__ x8n, const unsigned long long* fkey,
-       FileOut* __restrict__ fout) {
-    const int f = blockIdx.x * FIN_NT + threadIdx.x;
-    if (f >= nfiles) return;
-    const DevFile F = files[f];
-    const unsigned long long key = fkey[f];
-    FileOut fo;
-    fo.first_index = sub_P[F.first_sub];
-    fo.ok = key != ~0ull;
-    fo.n_records = 0; fo.end_offset = EVT_NONE; fo.status = 0;
-    if (fo.ok) {
-        uint64_t gi = 0;
-        int32_t st = 0;
-        const int64_t i = (int64_t)(key & 0xffffffffull);
-        fo.end_offset = fin_chunk_event(sums, sub_P, x8n, F.first_sub, F.nsub, i, &gi, &st);
-        fo.n_records = gi - fo.first_index;
-        fo.status = st;
+    FileInfo* fo = &finfo[f];
+    const uint32_t has = fo->has_term;
+    if (!has) {
+        if (threadIdx.x == 0) { atomicOr(&g->fail, 32u); fo->ok = 0; }
+        return;
     }
-    fout[f] = fo;
+    const uint32_t n = fo->term_tile - F.first_tile + 1;
+    const uint32_t per = (n + FIN_NT - 1) / FIN_NT;
+    const uint32_t lo = threadIdx.x * per, hi = lo + per < n ? lo + per : n;
+    uint32_t s = 0;
+    for (uint32_t i = lo; i < hi; i++) {
+        uint32_t p = 0;
+        #pragma unroll
+        for (int k = 0; k < 8; k++) p ^= tab[6 * 128 + k * 16 + ((s >> (4 * k)) & 15u)];
+        s = p ^ treg[F.first_tile + i];
+    }
+    part[threadIdx.x] = s;
+    plen[threadIdx.x] = hi > lo ? hi - lo : 0;
+    __syncthreads();
+    for (int d = 1; d < FIN_NT; d <<= 1) {
+        if ((threadIdx.x & (2 * d - 1)) == 0) {
+            part[threadIdx.x] = xpow_mul(pw, plen[threadIdx.x + d], part[threadIdx.x]) ^ part[threadIdx.x + d];
+            plen[threadIdx.x] += plen[threadIdx.x + d];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        // A^(CLY_CH (63 - lane)) expect
+        uint32_t e = fo->expect;
+        const uint32_t m = 63 - fo->term_lane;
+        for (int lvl = 0; lvl < 6; lvl++) {
+            if (m & (1u << lvl)) {
+                uint32_t p = 0;
+                for (int k = 0; k < 8; k++) p ^= tab[lvl * 128 + k * 16 + ((e >> (4 * k)) & 15u)];
+                e = p;
+            }
+        }
+        fo->fold = part[0];
+        fo->ok = part[0] == e;
+        fo->fail_key = ~0ull;
+        if (part[0] != e) atomicOr(&g->any_fail, 1u);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_locate (only after a failed fold): every tile of a failing file up to its
+// terminal re-derives its chain from the published states, the register
+// entering each chunk, and walks its records' checks from there; the first
+// failing record of the file wins (atomicMin on offset << 32 | index).
+__global__ void __launch_bounds__(512, 2)
+k_locate(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
+         const TileDesc* desc, const uint32_t* __restrict__ treg, FileInfo* finfo, const uint32_t* __restrict__ nib,
+         Globals* g) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS];
+    CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
+    init_tables(smem, nib);
+    const int lane = threadIdx.x & 63;
+    const CrcLane cl = crc_lane(lane);
+    for (uint32_t t = blockIdx.x * 8 + (threadIdx.x >> 6); t < ntiles; t += gridDim.x * 8) {
+        const int f = find_file(tprefix, nfiles, t);
+        const DevFile F = files[f];
+        FileInfo* fo = &finfo[f];
+        if (fo->ok || t > fo->term_tile) continue;
+        const uint32_t tt = t - F.first_tile;
+        const bool fof = tt == 0;
+        const Chunk K = make_chunk(F, tt, lane);
+        LBState S;
+        if (fof) { S = lb_virtual(); S.dead = 0; S.X = 0; S.count = fo->first_index; }
+        else S = lb_incl(desc[t - 1].i[0], desc[t - 1].i[1], desc[t - 1].i[2]);
+        if (S.dead) continue;
+        LaneChain L;
+        phase_a(K, L);
+        resolve(K, L, lane, S.X, false, g);
+        uint32_t tile_cnt;
+        const LaneIn I = lane_inputs(K, L, S, lane, tile_cnt);
+        // register entering the tile
+        uint32_t st = 0;
+        for (uint32_t i = F.first_tile; i < t; i++) st = nib_mul(smem, 6, st) ^ treg[i];
+        const bool live = L.mode == LM_CHAIN || L.mode == LM_NONE;
+        uint32_t fp, ex;
+        uint64_t fi;
+        uint32_t r = live ? exact_lane(K, L, I, 0u, false, false, F.fid, nullptr, 0, smem, cl, g, fp, fi, ex) : 0u;
+        // exclusive fold over the lanes, plus A^(CLY_CH l) st
+        uint32_t v = r;
+        #pragma unroll
+        for (int lvl = 0; lvl < 6; lvl++) {
+            const int d = 1 << lvl;
+            const uint32_t u = (uint32_t)__shfl_up((int)v, d, 64);
+            const uint32_t sh = nib_mul(smem, lvl, u);
+            if (lane >= d) v ^= sh;
+        }
+        uint32_t sin = (uint32_t)__shfl_up((int)v, 1, 64);
+        if (lane == 0) sin = 0;
+        uint32_t se = st;
+        for (int lvl = 0; lvl < 6; lvl++) if (lane & (1 << lvl)) se = nib_mul(smem, lvl, se);
+        sin ^= se;
+        if (live) {
+            exact_lane(K, L, I, sin, false, true, F.fid, nullptr, 0, smem, cl, g, fp, fi, ex);
+            if (fp != NONE32) atomicMin(&fo->fail_key, ((u64)fp << 32) | (u64)(fi - fo->first_index));
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1769,34 +1104,15 @@ struct cly_ctx {
     int device;
     hipStream_t stream;
     hipEvent_t ev[4];
-    DevFile* d_files; int cap_files;
-    uint32_t* d_prefix;
-    FileOut* d_fout;
-    int64_t cap_subs;
-    SubDesc* d_desc;
-    ChunkSum* d_sums;
-    uint64_t* d_subP;
-    cly_tuple* d_staging;
-    LinkAgg* d_blk;
-    Fix* d_fix;                  // fix list of a round
-    Fix* d_cand;                 // candidates of a round
-    uint32_t* d_listed;          // per sub-tile: stamp of the last round that listed it
-    uint32_t* d_cflag;           // per sub-tile: 2 stamp + harmful, for the candidates of a round
-    int32_t* d_fh;               // per file: first harmful sub-tile of a round
-    unsigned long long* d_fkey;  // per file: first event key (k_fin1)
-    unsigned long long* d_fck;   // per file: first candidate key of a round
-    uint32_t stamp;
-    Globals* d_g;
-    uint32_t* d_cols;            // columns of A^(SUB*2^k) (Kogge-Stone) and A^(4w) (head shifts)
-    uint32_t* d_x8n;
-    DevFile* h_files;
-    uint32_t* h_prefix;
-    FileOut* h_fout;
-    Globals* h_g;
+    DevFile* d_files; uint32_t* d_tprefix; FileInfo* d_finfo; int cap_files;
+    DevFile* h_files; uint32_t* h_tprefix; FileInfo* h_finfo;
+    TileDesc* d_desc; uint32_t* d_treg; int64_t cap_tiles;
+    Globals* d_g; Globals* h_g;
+    uint32_t* d_nib;             // nibble tables of A^(CLY_CH 2^k), k < NIB_LEVELS
+    uint32_t* d_pw;              // x^(8 CLY_TILE 2^k) mod P, k < 40
     int scan_grid;
     uint8_t* d_bytes; uint64_t cap_bytes;          // host-path staging
     cly_tuple* d_tuples; uint64_t cap_tuples;
-    int dbg_flags;
     void* merge_scratch;         // clymerge.hip's buffers (grow-only)
 };
 extern "C" void cly_merge_scratch_free(void* p);
@@ -1808,44 +1124,33 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) return CLY_ERR_DEVICE;
     HIPCK(hipSetDevice(device));
     cly_ctx* c = (cly_ctx*)calloc(1, sizeof(cly_ctx));
+    if (!c) return CLY_ERR_DEVICE;
     c->device = device;
     HIPCK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (int i = 0; i < 4; i++) HIPCK(hipEventCreate(&c->ev[i]));
     HIPCK(hipMalloc(&c->d_g, sizeof(Globals)));
     HIPCK(hipHostMalloc(&c->h_g, sizeof(Globals), hipHostMallocDefault));
     {
-        uint32_t* hc = (uint32_t*)calloc(CLY_COLS, sizeof(uint32_t));
-        for (int lvl = 0; lvl < CLY_KS_LEVELS; lvl++) {
-            const uint32_t xm = cly_x8n((uint64_t)CLY_SUB << lvl);
+        uint32_t hn[NIB_LEVELS * 128];
+        for (int lvl = 0; lvl < NIB_LEVELS; lvl++) {
+            const uint32_t xm = cly_x8n((uint64_t)CLY_CH << lvl);
             for (int nb = 0; nb < 8; nb++)
-                for (uint32_t v = 0; v < 16; v++) hc[lvl * 128 + nb * 16 + v] = cly_multmodp(xm, v << (4 * nb));
+                for (uint32_t v = 0; v < 16; v++) hn[lvl * 128 + nb * 16 + v] = cly_multmodp(xm, v << (4 * nb));
         }
-        for (int w = 0; w < 6 + HS_A; w++) {          // A^(4b), b < 6, then A^(24a), a < HS_A
-            const uint32_t xm = cly_x8n(w < 6 ? (uint64_t)4 * w : (uint64_t)24 * (w - 6));
-            for (int nb = 0; nb < 8; nb++)
-                for (uint32_t v = 0; v < 16; v++) hc[NIB_HSB + w * 128 + nb * 16 + v] = cly_multmodp(xm, v << (4 * nb));
-        }
-        HIPCK(hipMalloc(&c->d_cols, sizeof(uint32_t) * CLY_COLS));
-        HIPCK(hipMemcpy(c->d_cols, hc, sizeof(uint32_t) * CLY_COLS, hipMemcpyHostToDevice));
-        free(hc);
+        HIPCK(hipMalloc(&c->d_nib, sizeof(hn)));
+        HIPCK(hipMemcpy(c->d_nib, hn, sizeof(hn), hipMemcpyHostToDevice));
+        uint32_t hp[40];
+        hp[0] = cly_x8n((uint64_t)CLY_TILE);
+        for (int k = 1; k < 40; k++) hp[k] = cly_multmodp(hp[k - 1], hp[k - 1]);
+        HIPCK(hipMalloc(&c->d_pw, sizeof(hp)));
+        HIPCK(hipMemcpy(c->d_pw, hp, sizeof(hp), hipMemcpyHostToDevice));
     }
-    const size_t x8_bytes = sizeof(uint32_t) * (CLY_TS + 8);
-    HIPCK(hipMalloc(&c->d_x8n, x8_bytes));
-    uint32_t* hx = (uint32_t*)malloc(x8_bytes);
-    hx[0] = 1u << 31;
-    const uint32_t x8 = cly_x8n(1);
-    for (int n = 1; n < CLY_TS + 8; n++) hx[n] = cly_multmodp(x8, hx[n - 1]);
-    HIPCK(hipMemcpy(c->d_x8n, hx, x8_bytes, hipMemcpyHostToDevice));
-    free(hx);
-    HIPCK(hipFuncSetAttribute((const void*)k_fix, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CLY_SCAN_LDS));
-    HIPCK(hipFuncSetAttribute((const void*)k_serial, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CLY_SCAN_LDS));
-    HIPCK(hipFuncSetAttribute((const void*)k_place, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(CLY_NDW * CLY_WIN)));
     {
         int per_cu = 0, ncu = 0;
-        HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_scan, 64 * CLY_NDW, 0));
+        HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_scan, 512, 0));
         HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
         if (per_cu < 1) per_cu = 1;
+        if (per_cu > 2) per_cu = 2;
         c->scan_grid = per_cu * ncu;
     }
     *out = c;
@@ -1856,10 +1161,9 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
-    hipFree(c->d_files); hipFree(c->d_prefix); hipFree(c->d_fout); hipFree(c->d_desc); hipFree(c->d_sums);
-    hipFree(c->d_subP); hipFree(c->d_staging); hipFree(c->d_blk); hipFree(c->d_fix); hipFree(c->d_cand);
-    hipFree(c->d_listed); hipFree(c->d_cflag); hipFree(c->d_fh); hipFree(c->d_fkey); hipFree(c->d_fck); hipFree(c->d_g); hipFree(c->d_cols); hipFree(c->d_x8n); hipFree(c->d_bytes); hipFree(c->d_tuples);
-    hipHostFree(c->h_files); hipHostFree(c->h_prefix); hipHostFree(c->h_fout); hipHostFree(c->h_g);
+    hipFree(c->d_files); hipFree(c->d_tprefix); hipFree(c->d_finfo); hipFree(c->d_desc); hipFree(c->d_treg);
+    hipFree(c->d_g); hipFree(c->d_nib); hipFree(c->d_pw); hipFree(c->d_bytes); hipFree(c->d_tuples);
+    hipHostFree(c->h_files); hipHostFree(c->h_tprefix); hipHostFree(c->h_finfo); hipHostFree(c->h_g);
     cly_merge_scratch_free(c->merge_scratch);
     for (int i = 0; i < 4; i++) hipEventDestroy(c->ev[i]);
     hipStreamDestroy(c->stream);
@@ -1874,45 +1178,32 @@ extern "C" uint64_t cly_scan_capacity(const cly_file* files, int nfiles) {
 
 static int ensure_files(cly_ctx* c, int nfiles) {
     if (nfiles <= c->cap_files) return CLY_OK;
-    hipFree(c->d_files); hipFree(c->d_prefix); hipFree(c->d_fout); hipFree(c->d_fh); hipFree(c->d_fkey); hipFree(c->d_fck);
-    hipHostFree(c->h_files); hipHostFree(c->h_prefix); hipHostFree(c->h_fout);
+    hipFree(c->d_files); hipFree(c->d_tprefix); hipFree(c->d_finfo);
+    hipHostFree(c->h_files); hipHostFree(c->h_tprefix); hipHostFree(c->h_finfo);
+    c->d_files = nullptr; c->d_tprefix = nullptr; c->d_finfo = nullptr;
+    c->h_files = nullptr; c->h_tprefix = nullptr; c->h_finfo = nullptr;
+    c->cap_files = 0;
     const int cap = nfiles < 64 ? 64 : nfiles;
-    HIPCK(hipMalloc(&c->d_fh, sizeof(int32_t) * cap));
-    HIPCK(hipMalloc(&c->d_fkey, sizeof(unsigned long long) * cap));
-    HIPCK(hipMalloc(&c->d_fck, sizeof(unsigned long long) * cap));
     HIPCK(hipMalloc(&c->d_files, sizeof(DevFile) * cap));
-    HIPCK(hipMalloc(&c->d_prefix, sizeof(uint32_t) * (cap + 1)));
-    HIPCK(hipMalloc(&c->d_fout, sizeof(FileOut) * cap));
+    HIPCK(hipMalloc(&c->d_tprefix, sizeof(uint32_t) * (cap + 1)));
+    HIPCK(hipMalloc(&c->d_finfo, sizeof(FileInfo) * cap));
     HIPCK(hipHostMalloc(&c->h_files, sizeof(DevFile) * cap, hipHostMallocDefault));
-    HIPCK(hipHostMalloc(&c->h_prefix, sizeof(uint32_t) * (cap + 1), hipHostMallocDefault));
-    HIPCK(hipHostMalloc(&c->h_fout, sizeof(FileOut) * cap, hipHostMallocDefault));
+    HIPCK(hipHostMalloc(&c->h_tprefix, sizeof(uint32_t) * (cap + 1), hipHostMallocDefault));
+    HIPCK(hipHostMalloc(&c->h_finfo, sizeof(FileInfo) * cap, hipHostMallocDefault));
     c->cap_files = cap;
     return CLY_OK;
 }
 
-static int ensure_subs(cly_ctx* c, int64_t nsub) {
-    if (nsub <= c->cap_subs) return CLY_OK;
-    hipFree(c->d_desc); hipFree(c->d_sums); hipFree(c->d_subP); hipFree(c->d_staging); hipFree(c->d_blk);
-    hipFree(c->d_fix); hipFree(c->d_cand); hipFree(c->d_listed); hipFree(c->d_cflag);
-    const int64_t cap = nsub < 1024 ? 1024 : nsub;
-    HIPCK(hipMalloc(&c->d_desc, sizeof(SubDesc) * cap));
-    HIPCK(hipMalloc(&c->d_sums, sizeof(ChunkSum) * cap));
-    HIPCK(hipMalloc(&c->d_subP, sizeof(uint64_t) * cap));
-    HIPCK(hipMalloc(&c->d_staging, sizeof(cly_tuple) * CLY_CAP * cap));
-    HIPCK(hipMalloc(&c->d_blk, sizeof(LinkAgg) * (cap / LINK_BLK + 2)));
-    HIPCK(hipMalloc(&c->d_fix, sizeof(Fix) * cap));
-    HIPCK(hipMalloc(&c->d_cand, sizeof(Fix) * cap));
-    HIPCK(hipMalloc(&c->d_listed, sizeof(uint32_t) * cap));
-    HIPCK(hipMemset(c->d_listed, 0, sizeof(uint32_t) * cap));
-    HIPCK(hipMalloc(&c->d_cflag, sizeof(uint32_t) * cap));
-    HIPCK(hipMemset(c->d_cflag, 0, sizeof(uint32_t) * cap));
-    c->stamp = 0;
-    c->cap_subs = cap;
+static int ensure_tiles(cly_ctx* c, int64_t ntiles) {
+    if (ntiles <= c->cap_tiles) return CLY_OK;
+    hipFree(c->d_desc); hipFree(c->d_treg);
+    c->d_desc = nullptr; c->d_treg = nullptr; c->cap_tiles = 0;
+    const int64_t cap = ntiles < 1024 ? 1024 : ntiles;
+    HIPCK(hipMalloc(&c->d_desc, sizeof(TileDesc) * cap));
+    HIPCK(hipMalloc(&c->d_treg, sizeof(uint32_t) * cap));
+    c->cap_tiles = cap;
     return CLY_OK;
 }
-
-#define FIX_ROUNDS 8
-#define SERIAL_AFTER 2           // parallel fix rounds before the serial walk
 
 extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple* d_out, uint64_t out_cap,
                                uint64_t* file_first, cly_file_result* res, uint64_t* needed, cly_stats* stats,
@@ -1923,164 +1214,99 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     hipStream_t st = stream_v ? (hipStream_t)stream_v : c->stream;
     int rc = ensure_files(c, nfiles);
     if (rc) return rc;
-    int64_t nsub = 0;
+    int64_t ntiles = 0;
     uint64_t bytes = 0;
     for (int i = 0; i < nfiles; i++) {
-        if (files[i].len >= (1ULL << 32)) return CLY_ERR_ARG;
+        if (files[i].len >= 0xFFFFFFFFull) return CLY_ERR_ARG;
         if (files[i].len && (((uintptr_t)files[i].base) & 15)) return CLY_ERR_ARG;
-        const uint64_t ns = files[i].len ? (files[i].len + CLY_TS - 1) / CLY_TS : 1;
+        const uint64_t nt = files[i].len ? (files[i].len + CLY_TILE - 1) / CLY_TILE : 1;
         c->h_files[i].base = files[i].base;
         c->h_files[i].len = files[i].len;
         c->h_files[i].fid = files[i].fid;
-        c->h_files[i].first_sub = (uint32_t)nsub;
-        c->h_files[i].nsub = (uint32_t)ns;
+        c->h_files[i].first_tile = (uint32_t)ntiles;
+        c->h_files[i].ntile = (uint32_t)nt;
         c->h_files[i]._pad = 0;
-        c->h_prefix[i] = (uint32_t)nsub;
-        nsub += (int64_t)ns;
+        c->h_tprefix[i] = (uint32_t)ntiles;
+        ntiles += (int64_t)nt;
         bytes += files[i].len;
     }
-    if (nsub >= (1LL << 31)) return CLY_ERR_ARG;
-    c->h_prefix[nfiles] = (uint32_t)nsub;
-    rc = ensure_subs(c, nsub);
+    if (ntiles >= (1LL << 31)) return CLY_ERR_ARG;
+    c->h_tprefix[nfiles] = (uint32_t)ntiles;
+    rc = ensure_tiles(c, ntiles);
     if (rc) return rc;
     HIPCK(hipMemcpyAsync(c->d_files, c->h_files, sizeof(DevFile) * nfiles, hipMemcpyHostToDevice, st));
-    HIPCK(hipMemcpyAsync(c->d_prefix, c->h_prefix, sizeof(uint32_t) * (nfiles + 1), hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(c->d_tprefix, c->h_tprefix, sizeof(uint32_t) * (nfiles + 1), hipMemcpyHostToDevice, st));
+    HIPCK(hipMemsetAsync(c->d_desc, 0, sizeof(TileDesc) * ntiles, st));
+    HIPCK(hipMemsetAsync(c->d_finfo, 0, sizeof(FileInfo) * nfiles, st));
     HIPCK(hipMemsetAsync(c->d_g, 0, sizeof(Globals), st));
-    const int64_t nblk = (nsub + LINK_BLK - 1) / LINK_BLK;
-    HIPCK(hipEventRecord(c->ev[0], st));
     int grid = c->scan_grid;
-    if ((int64_t)grid * CLY_NDW > nsub) grid = (int)((nsub + CLY_NDW - 1) / CLY_NDW);
-    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * CLY_NDW), 0, st, c->d_files, nfiles, c->d_prefix, nsub,
-                       c->d_desc, c->d_sums, c->d_cols, c->d_staging, c->d_g, (c->dbg_flags & 2) ? -2 : -1);
+    if ((int64_t)grid * 8 > ntiles) grid = (int)((ntiles + 7) / 8);
+    HIPCK(hipEventRecord(c->ev[0], st));
+    // debug: CLY_DUMP=<path> appends every lane's final chain (8 u32 per lane) of each call
+    const char* dump_path = getenv("CLY_DUMP");
+    uint32_t* d_dump = nullptr;
+    if (dump_path) HIPCK(hipMalloc(&d_dump, sizeof(uint32_t) * 12 * 64 * ntiles));
+    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(512), 0, st, c->d_files, nfiles, c->d_tprefix, (uint32_t)ntiles,
+                       c->d_desc, c->d_treg, c->d_finfo, c->d_nib, d_out, out_cap, c->d_g, d_dump);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[1], st));
-    // link scan, then fix rounds until every sub-tile holds the chain its state
-    // implies.  The first fix round is launched without waiting for the first
-    // scan (k_fix reads the fix count itself), so the common case costs one
-    // host synchronisation.
-    uint32_t rounds = 0;
-    const int fix_grid = c->scan_grid < 64 ? c->scan_grid : 64;
-    auto link_round = [&](uint32_t stamp) -> int {
-        hipLaunchKernelGGL(k_round_init, dim3((nfiles + LINK_NT - 1) / LINK_NT), dim3(LINK_NT), 0, st, c->d_fh,
-                           c->d_fck, nfiles, c->d_g);
-        hipLaunchKernelGGL(k_link1, dim3(nblk), dim3(LINK_NT), 0, st, c->d_desc, nsub, c->d_blk);
-        hipLaunchKernelGGL(k_link2, dim3(1), dim3(LINK_NT), 0, st, c->d_blk, nblk);
-        hipLaunchKernelGGL(k_link3, dim3(nblk), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_prefix, c->d_desc, nsub,
-                           c->d_blk, c->d_subP, c->d_cand, (uint32_t)c->cap_subs, c->d_fh, c->d_fck, c->d_cflag, stamp,
-                           c->d_g);
-        hipLaunchKernelGGL(k_link4, dim3(64), dim3(LINK_NT), 0, st, c->d_files, c->d_desc, c->d_cand, c->d_fh, c->d_cflag,
-                           c->d_fix, c->d_listed, stamp, c->d_g);
-        HIPCK(hipGetLastError());
-        return CLY_OK;
-    };
-    auto fix_round = [&](uint32_t stamp, uint32_t nfix) -> int {
-        int fgrid = nfix == ~0u ? fix_grid : (int)((nfix + CLY_NDW - 1) / CLY_NDW);
-        if (fgrid > c->scan_grid) fgrid = c->scan_grid;
-        for (int pass = 0; pass < 2; pass++)
-            hipLaunchKernelGGL(k_fix, dim3(fgrid), dim3(64 * CLY_NDW), CLY_SCAN_LDS, st, c->d_files, c->d_fix, nfix,
-                               c->d_listed, stamp, pass, c->d_desc, c->d_sums, c->d_cols, c->d_staging, c->d_g);
-        HIPCK(hipGetLastError());
-        return CLY_OK;
-    };
-    const bool ahead = !CLY_EXP && !(c->dbg_flags & (4 | 8 | 16));
-    {
-        const uint32_t stamp = ++c->stamp;
-        if ((rc = link_round(stamp))) return rc;
-        if (ahead) {
-            if ((rc = fix_round(stamp, ~0u))) return rc;
-            if ((rc = link_round(++c->stamp))) return rc;
-            rounds = 1;
-        }
-    }
-    for (;;) {
-        HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
-        HIPCK(hipStreamSynchronize(st));
-        const uint32_t ncand = c->h_g->ncand, nfix = c->h_g->nfix;
-        if (c->h_g->fail) break;
-        if (ncand == 0 || CLY_EXP || (c->dbg_flags & 16)) break;   // (experiment builds / debug: no fix rounds)
-        if (++rounds > FIX_ROUNDS) {
-            fprintf(stderr, "clyscan: chain resolution did not converge (%u candidates, %u fixes)\n", ncand, nfix);
-            return CLY_ERR_NOREPAIR;
-        }
-        const uint32_t stamp = c->stamp;
-        if (c->dbg_flags & 4) {                          // debug trace of the fix rounds
-            const uint32_t nshow = nfix < 64 ? nfix : 64;
-            Fix* hf = (Fix*)malloc(sizeof(Fix) * (nshow ? nshow : 1));
-            HIPCK(hipMemcpy(hf, c->d_fix, sizeof(Fix) * nshow, hipMemcpyDeviceToHost));
-            fprintf(stderr, "round %u: %u candidates, %u fixes:", rounds, ncand, nfix);
-            for (uint32_t k = 0; k < nshow; k++) {
-                SubDesc d;
-                HIPCK(hipMemcpy(&d, c->d_desc + hf[k].s, sizeof(SubDesc), hipMemcpyDeviceToHost));
-                fprintf(stderr, " [s=%u%s want %d/%d have %d/%d cnt %u]", hf[k].s, hf[k].certain ? "C" : "", hf[k].mode,
-                        hf[k].entry, d.mode, d.entry, d.cnt);
-            }
-            fprintf(stderr, "\n");
-            free(hf);
-        }
-        if (rounds > SERIAL_AFTER || nfix == 0) {
-            // the parallel rounds did not settle: one exact serial walk per file
-            hipLaunchKernelGGL(k_serial, dim3(nfiles), dim3(64), CLY_SCAN_LDS, st, c->d_files, c->d_cand, c->d_fck,
-                               c->d_desc, c->d_sums, c->d_cols, c->d_staging, c->d_g);
-            HIPCK(hipGetLastError());
-        } else {
-            if ((rc = fix_round(stamp, nfix))) return rc;
-        }
-        if (c->dbg_flags & 8) {                          // debug: descriptors and stamps after the round
-            HIPCK(hipStreamSynchronize(st));
-            const int64_t nd = nsub < 64 ? nsub : 64;
-            SubDesc hd[64];
-            uint32_t hl[64];
-            HIPCK(hipMemcpy(hd, c->d_desc, sizeof(SubDesc) * nd, hipMemcpyDeviceToHost));
-            HIPCK(hipMemcpy(hl, c->d_listed, sizeof(uint32_t) * nd, hipMemcpyDeviceToHost));
-            fprintf(stderr, "  after (stamp %u):", stamp);
-            for (int64_t k = 0; k < nd; k++)
-                fprintf(stderr, " %lld:%d/%d/%u%s", (long long)k, hd[k].mode, hd[k].entry, hd[k].cnt,
-                        hl[k] == stamp ? "w" : (hl[k] == (stamp | LISTED_U) ? "u" : ""));
-            fprintf(stderr, "\n");
-        }
-        if ((rc = link_round(++c->stamp))) return rc;
-    }
-    HIPCK(hipEventRecord(c->ev[2], st));
-    hipLaunchKernelGGL(k_copy, dim3((unsigned)((nsub + CP_SUBS - 1) / CP_SUBS)), dim3(CP_NT), 0, st, c->d_desc,
-                       c->d_subP, c->d_staging, d_out, out_cap, nsub, c->d_g);
-    if (c->h_g->novf) {
-        hipLaunchKernelGGL(k_place, dim3(c->scan_grid), dim3(64 * CLY_NDW), CLY_NDW * CLY_WIN, st, c->d_files,
-                           nfiles, c->d_prefix, nsub, c->d_desc, c->d_subP, c->d_staging, d_out, out_cap, c->d_g);
-    }
-    HIPCK(hipMemsetAsync(c->d_fkey, 0xff, sizeof(unsigned long long) * nfiles, st));
-    hipLaunchKernelGGL(k_fin1, dim3((unsigned)((nsub + FIN_NT - 1) / FIN_NT)), dim3(FIN_NT), 0, st, c->d_files, nfiles,
-                       c->d_prefix, nsub, c->d_sums, c->d_subP, c->d_x8n, c->d_fkey);
-    hipLaunchKernelGGL(k_fin2, dim3((nfiles + FIN_NT - 1) / FIN_NT), dim3(FIN_NT), 0, st, c->d_files, nfiles, c->d_sums,
-                       c->d_subP, c->d_x8n, c->d_fkey, c->d_fout);
+    hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_finfo, c->d_treg, c->d_nib, c->d_pw,
+                       c->d_g);
     HIPCK(hipGetLastError());
-    HIPCK(hipEventRecord(c->ev[3], st));
+    HIPCK(hipEventRecord(c->ev[2], st));
     HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
-    HIPCK(hipMemcpyAsync(c->h_fout, c->d_fout, sizeof(FileOut) * nfiles, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
-    float ms_scan = 0, ms_link = 0, ms_tail = 0;
+    bool located = false;
+    if (c->h_g->any_fail && !c->h_g->fail) {
+        hipLaunchKernelGGL(k_locate, dim3(grid), dim3(512), 0, st, c->d_files, nfiles, c->d_tprefix, (uint32_t)ntiles,
+                           c->d_desc, c->d_treg, c->d_finfo, c->d_nib, c->d_g);
+        HIPCK(hipGetLastError());
+        located = true;
+    }
+    HIPCK(hipEventRecord(c->ev[3], st));
+    HIPCK(hipMemcpyAsync(c->h_finfo, c->d_finfo, sizeof(FileInfo) * nfiles, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    if (d_dump) {
+        const size_t nb = sizeof(uint32_t) * 12 * 64 * ntiles;
+        uint32_t* h = (uint32_t*)malloc(nb);
+        if (h && hipMemcpy(h, d_dump, nb, hipMemcpyDeviceToHost) == hipSuccess) {
+            FILE* fd = fopen(dump_path, "ab");
+            if (fd) { fwrite(h, 1, nb, fd); fclose(fd); }
+        }
+        free(h);
+        hipFree(d_dump);
+    }
+    float ms_scan = 0, ms_fin = 0, ms_loc = 0;
     HIPCK(hipEventElapsedTime(&ms_scan, c->ev[0], c->ev[1]));
-    HIPCK(hipEventElapsedTime(&ms_link, c->ev[1], c->ev[2]));
-    HIPCK(hipEventElapsedTime(&ms_tail, c->ev[2], c->ev[3]));
-    if ((c->h_g->lb_timeout || c->h_g->fail) && !CLY_EXP) {
-        fprintf(stderr, "clyscan: internal error (timeout %u, invariant %u)\n", c->h_g->lb_timeout, c->h_g->fail);
+    HIPCK(hipEventElapsedTime(&ms_fin, c->ev[1], c->ev[2]));
+    HIPCK(hipEventElapsedTime(&ms_loc, c->ev[2], c->ev[3]));
+    if (c->h_g->fail) {
+        fprintf(stderr, "clyscan: internal error (code %#x)\n", c->h_g->fail);
         return CLY_ERR_DEVICE;
     }
     uint64_t total = 0;
     for (int i = 0; i < nfiles; i++) {
-        if (!c->h_fout[i].ok && !CLY_EXP) { fprintf(stderr, "clyscan: internal error (file %d has no end event)\n", i); return CLY_ERR_DEVICE; }
-        file_first[i] = c->h_fout[i].first_index;
-        res[i].n_records = c->h_fout[i].n_records;
-        res[i].end_offset = c->h_fout[i].end_offset;
-        res[i].status = c->h_fout[i].status;
+        const FileInfo& fi = c->h_finfo[i];
+        file_first[i] = fi.first_index;
+        if (fi.ok) {
+            res[i].n_records = fi.end_index - fi.first_index;
+            res[i].end_offset = fi.term_pos;
+            res[i].status = fi.term_status;
+        } else {
+            if (fi.fail_key == ~0ull) { fprintf(stderr, "clyscan: internal error (file %d: no failing record)\n", i); return CLY_ERR_DEVICE; }
+            res[i].n_records = fi.fail_key & 0xffffffffull;
+            res[i].end_offset = (int64_t)(fi.fail_key >> 32);
+            res[i].status = CLY_ERR_CRC;
+        }
         res[i]._pad = 0;
-        total += c->h_fout[i].n_records;
+        total += res[i].n_records;
     }
     if (needed) *needed = c->h_g->total;
-
     if (stats) {
-        stats->scan_ms = ms_scan; stats->resolve_ms = ms_link + ms_tail; stats->total_ms = ms_scan + ms_link + ms_tail;
-        stats->passes = 1 + rounds;
-        stats->n_chunks = (uint32_t)nsub; stats->bytes = bytes; stats->records = total;
+        stats->scan_ms = ms_scan; stats->resolve_ms = ms_fin + ms_loc; stats->total_ms = ms_scan + ms_fin + ms_loc;
+        stats->passes = 1 + (c->h_g->refix ? 1 : 0) + (located ? 1 : 0);
+        stats->n_chunks = (uint32_t)(ntiles * CLY_NL); stats->bytes = bytes; stats->records = total;
     }
     if (c->h_g->overflow || c->h_g->total > out_cap) return CLY_ERR_CAPACITY;
     return CLY_OK;
@@ -2090,7 +1316,8 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
 // pipeline: the files are split into groups of >= PIPE_GROUP bytes (whole
 // files); a copy thread moves group g+1 host->device while group g is scanned
 // and its tuples travel device->host (PCIe is full duplex), so the H2D stream
-// of the file bytes sets the pace.
+// of the file bytes sets the pace.  On CLY_ERR_CAPACITY every group is still
+// scanned (nothing copied back) so that *needed is the exact record count.
 #define PIPE_MIN (256ull << 20)
 #define PIPE_GROUP (512ull << 20)
 extern "C" int cly_scan(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple* out, uint64_t out_cap,
@@ -2098,25 +1325,28 @@ extern "C" int cly_scan(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
     if (!c || (!files && nfiles) || nfiles < 0 || !res || !file_first) return CLY_ERR_ARG;
     if (nfiles == 0) { if (needed) *needed = 0; return CLY_OK; }
     HIPCK(hipSetDevice(c->device));
-    // pack the files into one device buffer, each at a 4 KiB-aligned offset
     uint64_t total = 0;
     for (int i = 0; i < nfiles; i++) {
-        if (files[i].len >= (1ULL << 32)) return CLY_ERR_ARG;
+        if (files[i].len >= 0xFFFFFFFFull) return CLY_ERR_ARG;
         total += (files[i].len + 4095) & ~4095ULL;
     }
     if (total + 4096 > c->cap_bytes) {
         hipFree(c->d_bytes);
+        c->d_bytes = nullptr; c->cap_bytes = 0;
+        HIPCK(hipMalloc(&c->d_bytes, total + 4096));
         c->cap_bytes = total + 4096;
-        HIPCK(hipMalloc(&c->d_bytes, c->cap_bytes));
     }
     const uint64_t cap = cly_scan_capacity(files, nfiles) + 16 * (uint64_t)nfiles + 16;
     if (cap > c->cap_tuples) {
         hipFree(c->d_tuples);
-        c->cap_tuples = cap;
+        c->d_tuples = nullptr; c->cap_tuples = 0;
         HIPCK(hipMalloc(&c->d_tuples, sizeof(cly_tuple) * cap));
+        c->cap_tuples = cap;
     }
     cly_file* df = (cly_file*)malloc(sizeof(cly_file) * nfiles);
     uint64_t* goff = (uint64_t*)malloc(sizeof(uint64_t) * (nfiles + 1));   // device byte offset of each file
+    int* gstart = (int*)malloc(sizeof(int) * (nfiles + 1));
+    if (!df || !goff || !gstart) { free(df); free(goff); free(gstart); return CLY_ERR_DEVICE; }
     {
         uint64_t off = 0;
         for (int i = 0; i < nfiles; i++) {
@@ -2127,9 +1357,7 @@ extern "C" int cly_scan(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
         }
         goff[nfiles] = off;
     }
-    // groups of whole files
     int ng = 0;
-    int* gstart = (int*)malloc(sizeof(int) * (nfiles + 1));
     {
         uint64_t acc = 0;
         gstart[ng++] = 0;
@@ -2151,19 +1379,21 @@ extern "C" int cly_scan(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
         }
     });
     int rc = CLY_OK;
-    uint64_t tbase = 0, o = 0, slots_total = 0, need = 0;
+    uint64_t tbase = 0, o = 0, need = 0;
+    bool over = false;
     cly_stats st_acc;
     memset(&st_acc, 0, sizeof(st_acc));
-    for (int g = 0; g < ng && rc == CLY_OK; g++) {
+    for (int g = 0; g < ng && (rc == CLY_OK || rc == CLY_ERR_CAPACITY); g++) {
         while (ready.load(std::memory_order_acquire) <= g) std::this_thread::yield();
         if (copy_err) { rc = CLY_ERR_DEVICE; break; }
         const int f0 = gstart[g], nf = gstart[g + 1] - gstart[g];
         const uint64_t gcap = cly_scan_capacity(files + f0, nf) + 16;
         uint64_t slots = 0;
         cly_stats sg;
-        rc = cly_scan_device(c, df + f0, nf, c->d_tuples + tbase, gcap, file_first + f0, res + f0, &slots, &sg, nullptr);
-        if (rc == CLY_ERR_CAPACITY) slots_total += slots;
-        if (rc != CLY_OK) break;
+        const int r = cly_scan_device(c, df + f0, nf, c->d_tuples + tbase, gcap, file_first + f0, res + f0, &slots, &sg,
+                                      nullptr);
+        if (r == CLY_ERR_CAPACITY) { over = true; need += slots; rc = CLY_ERR_CAPACITY; tbase += gcap; continue; }
+        if (r != CLY_OK) { rc = r; break; }
         st_acc.scan_ms += sg.scan_ms; st_acc.resolve_ms += sg.resolve_ms; st_acc.total_ms += sg.total_ms;
         st_acc.passes = st_acc.passes > sg.passes ? st_acc.passes : sg.passes;
         st_acc.n_chunks += sg.n_chunks; st_acc.bytes += sg.bytes; st_acc.records += sg.records;
@@ -2171,7 +1401,7 @@ extern "C" int cly_scan(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
         // tuples past an ErrInvalidCRC), while the next group is still coming in
         for (int i = f0; i < f0 + nf; i++) {
             need += res[i].n_records;
-            if (need > out_cap) { rc = CLY_ERR_CAPACITY; break; }
+            if (over || need > out_cap) { over = true; rc = CLY_ERR_CAPACITY; continue; }
             if (res[i].n_records &&
                 hipMemcpyAsync(out + o, c->d_tuples + tbase + file_first[i], sizeof(cly_tuple) * res[i].n_records,
                                hipMemcpyDeviceToHost, c->stream) != hipSuccess) { rc = CLY_ERR_DEVICE; break; }
@@ -2180,54 +1410,19 @@ extern "C" int cly_scan(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
         }
         tbase += gcap;
     }
-    if (rc != CLY_OK) ready.store(ng);            // (the copier only reads `ready`'s own stores; it finishes its groups)
+    if (rc != CLY_OK && rc != CLY_ERR_CAPACITY) ready.store(ng);
     copier.join();                                // no return before this: the copier must be joined
     if (hipStreamSynchronize(c->stream) != hipSuccess && rc == CLY_OK) rc = CLY_ERR_DEVICE;
     free(df); free(goff); free(gstart);
     if (stats) *stats = st_acc;
-    if (needed) {
-        if (rc == CLY_ERR_CAPACITY) {
-            uint64_t n_all = 0;
-            for (int i = 0; i < nfiles; i++) n_all += res[i].n_records;
-            *needed = slots_total > n_all ? slots_total : n_all;
-        } else {
-            *needed = need;
-        }
-    }
+    if (needed) *needed = need;
     return rc;
 }
 
-// Context accessors for the merge entries (clymerge.hip); not in the public header.
+// Context accessors for the merge / index entries (clymerge.hip, clyindex.hip); not in the public header.
 extern "C" hipStream_t cly_ctx_stream_internal(cly_ctx* c) { return c->stream; }
 extern "C" int cly_ctx_device_internal(cly_ctx* c) { return c->device; }
 extern "C" void** cly_ctx_merge_slot_internal(cly_ctx* c) { return &c->merge_scratch; }
-
-// Debug / statistics (not part of include/clyscan.h)
-extern "C" int cly_dbg_sums(cly_ctx* c, void* out, int n) {
-    HIPCK(hipDeviceSynchronize());
-    HIPCK(hipMemcpy(out, c->d_sums, sizeof(ChunkSum) * n, hipMemcpyDeviceToHost));
-    return n;
-}
-extern "C" int cly_dbg_sumsize(void) { return (int)sizeof(ChunkSum); }
-extern "C" int cly_dbg_descs(cly_ctx* c, void* out, int n) {
-    HIPCK(hipDeviceSynchronize());
-    HIPCK(hipMemcpy(out, c->d_desc, sizeof(SubDesc) * n, hipMemcpyDeviceToHost));
-    return n;
-}
-extern "C" int cly_dbg_subp(cly_ctx* c, uint64_t* out, int n) {
-    HIPCK(hipDeviceSynchronize());
-    HIPCK(hipMemcpy(out, c->d_subP, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
-    return n;
-}
-extern "C" int cly_dbg_stats(cly_ctx* c, uint32_t* out4) {
-    out4[0] = c->h_g->fix_total; out4[1] = 0; out4[2] = c->scan_grid; out4[3] = CLY_SCAN_LDS;
-    return 4;
-}
-extern "C" int cly_dbg_prof(cly_ctx* c, uint64_t* out24) {
-    for (int i = 0; i < 24; i++) out24[i] = c->h_g->prof[i];
-    return 24;
-}
-extern "C" int cly_dbg_enable(cly_ctx* c, int on) { c->dbg_flags = on; return 0; }
 
 extern "C" const char* cly_strerror(int code) {
     switch (code) {
@@ -2246,9 +1441,12 @@ extern "C" const char* cly_strerror(int code) {
     }
 }
 
+#ifndef CLY_SRC_HASH
+#define CLY_SRC_HASH "unknown"
+#endif
 extern "C" const char* cly_build_info(void) {
     static char buf[200];
-    snprintf(buf, sizeof(buf), "clyscan gfx950 SUB=%d WAVES=%d TS=%d CAP=%d LDS=%d tables=16x sched=%s src=%s", CLY_SUB,
-             CLY_NDW, CLY_TS, CLY_CAP, (int)CLY_SCAN_LDS, CLY_SCHED, CLY_SRC_HASH);
+    snprintf(buf, sizeof(buf), "clyscan gfx950 lane-chunk CH=%d TILE=%lld LDS=%d src=%s", CLY_CH, (long long)CLY_TILE,
+             (int)SCAN_LDS, CLY_SRC_HASH);
     return buf;
 }
