@@ -40,9 +40,13 @@
 #include "scan_core.h"
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(4)));
 typedef unsigned long long u64;
 
+#define CLY_GL __attribute__((address_space(1)))   // global memory (loads/stores as global_*, not flat_*)
+typedef const CLY_GL uint8_t* gbytes;
+typedef CLY_GL cly_tuple* gtuples;
 #define NONE32 0xFFFFFFFFu       // no position
 #define TERM_NONE 127            // the chain leaves the chunk (no terminal inside)
 #define LM_NONE 0                // no record starts in the chunk (the chain passes through it)
@@ -106,7 +110,20 @@ struct Globals {                 // zeroed per call
     uint32_t slow_lanes;         // lanes that took the exact (slow) CRC path
     uint32_t any_fail;           // a file's CRC fold failed (k_locate needed)
     uint64_t total;              // records over all files
+    uint64_t prof[12];           // profiling build (-DCLY_PROF): cycles per phase, summed over tiles; look-back counters
 };
+#ifdef CLY_PROF
+#define PROF_T0() uint64_t prof_t = __builtin_amdgcn_s_memtime()
+#define PROF(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long*)&g->prof[i], (unsigned long long)(t_ - prof_t)); prof_t = t_; } while (0)
+#else
+#define PROF_T0()
+#define PROF(i)
+#endif
+#ifdef CLY_PROF
+#define PCNT(i, n) do { if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long*)&g->prof[i], (unsigned long long)(n)); } while (0)
+#else
+#define PCNT(i, n)
+#endif
 
 // ---------------------------------------------------------------------------
 // LDS of k_scan / k_locate (static: compile-time offsets)
@@ -116,7 +133,10 @@ struct Globals {                 // zeroed per call
 #define LDS_INV 65536
 #define LDS_NIB (LDS_INV + 256)
 #define NIB_LEVELS 7                     // A^(CLY_CH * 2^k), k < 7 (k = 6: one tile)
-#define SCAN_LDS (LDS_NIB + NIB_LEVELS * 128 * 4)
+#define EVQ 10                   // events per lane in the LDS ring of phase C
+#define LDS_EVQ (LDS_NIB + NIB_LEVELS * 128 * 4)          // event rings: [wave][EVQ][64 lanes] x 8 B
+#define SCAN_WAVES 16
+#define SCAN_LDS (LDS_EVQ + SCAN_WAVES * EVQ * 64 * 8)
 
 __device__ __forceinline__ void init_tables(CLY_LDS uint8_t* smem, const uint32_t* __restrict__ nib) {
     for (int i = threadIdx.x; i < 256; i += blockDim.x) {
@@ -206,8 +226,8 @@ __device__ __forceinline__ uint32_t patch_delta(const CLY_LDS uint8_t* smem, con
 // expirations); otherwise the exact byte-loop form over global memory.
 struct Gath { uint32_t w[8]; };
 __device__ __forceinline__ bool gath_ok(uint32_t p, uint64_t len) { return (uint64_t)(p & ~3u) + 32 <= len; }
-__device__ __forceinline__ void gath_issue(const uint8_t* base, uint32_t p, Gath& g) {
-    const u32x4u* q = (const u32x4u*)(base + (p & ~3u));
+__device__ __forceinline__ void gath_issue(gbytes base, uint32_t p, Gath& g) {
+    const CLY_GL u32x4u* q = (const CLY_GL u32x4u*)(base + (p & ~3u));
     const u32x4u a = q[0], b = q[1];
     g.w[0] = a.x; g.w[1] = a.y; g.w[2] = a.z; g.w[3] = a.w;
     g.w[4] = b.x; g.w[5] = b.y; g.w[6] = b.z; g.w[7] = b.w;
@@ -218,7 +238,7 @@ __device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t s)
 __device__ __forceinline__ uint32_t pack7(uint32_t s) {
     return (s & 0x7fu) | ((s >> 1) & 0x3f80u) | ((s >> 2) & 0x1fc000u) | ((s >> 3) & 0xfe00000u);
 }
-__device__ __noinline__ void hdr_slow(const uint8_t* base, uint32_t p, uint64_t len, Hdr& h) {
+__device__ __noinline__ void hdr_slow(gbytes base, uint32_t p, uint64_t len, Hdr& h) {
     h = step_hdr(base, (int64_t)p, (int64_t)len, (int64_t)p);
 }
 // header bytes 0..15 at p from a gather
@@ -263,13 +283,13 @@ __device__ __forceinline__ bool hdr_fast(const Gath& g, uint32_t p, uint64_t len
     return true;
 }
 // Header at p; `g` must hold the gather of p when gath_ok(p).
-__device__ __forceinline__ Hdr hdr_at(const uint8_t* base, uint32_t p, uint64_t len, const Gath& g) {
+__device__ __forceinline__ Hdr hdr_at(gbytes base, uint32_t p, uint64_t len, const Gath& g) {
     Hdr h;
     if (gath_ok(p, len) && hdr_fast(g, p, len, h)) return h;
     hdr_slow(base, p, len, h);
     return h;
 }
-__device__ __forceinline__ Hdr hdr_load(const uint8_t* base, uint32_t p, uint64_t len) {
+__device__ __forceinline__ Hdr hdr_load(gbytes base, uint32_t p, uint64_t len) {
     Gath g;
     if (gath_ok(p, len)) gath_issue(base, p, g);
     return hdr_at(base, p, len, g);
@@ -279,7 +299,7 @@ __device__ __forceinline__ Hdr hdr_load(const uint8_t* base, uint32_t p, uint64_
 // Per-lane chain of one chunk [cb, ce) (file offsets; the file's last chunk
 // also owns position len, where ReadLogRecord returns io.EOF).
 struct Chunk {
-    const uint8_t* base;
+    gbytes base;
     uint64_t len;
     uint32_t cb, ce;
     bool last;                   // the file's last chunk
@@ -307,7 +327,7 @@ __device__ __forceinline__ void chain_set(LaneChain& L, int mode) {
 // (every record must be one the writer produces and the chain must leave the
 // chunk at a plausible header, or end at io.EOF at len).  Returns false when a
 // speculative chain is rejected.
-__device__ __noinline__ bool walk(const Chunk& K, uint32_t p, bool exact, LaneChain& L) {
+__device__ __forceinline__ bool walk(const Chunk& K, uint32_t p, bool exact, LaneChain& L) {
     chain_set(L, LM_CHAIN);
     L.E = p;
     for (;;) {
@@ -344,10 +364,10 @@ __device__ __forceinline__ uint32_t swar_ks(uint32_t W) {
 // wholly past it are not loaded).
 __device__ __forceinline__ u32x4 piece(const Chunk& K, uint32_t o) {
     const uint64_t a = (uint64_t)K.cb + o;
-    if (a + 16 <= K.len) return *(const u32x4*)(K.base + a);
+    if (a + 16 <= K.len) return *(const CLY_GL u32x4*)(K.base + a);
     u32x4 v = {0u, 0u, 0u, 0u};
     if (a < K.len) {
-        v = *(const u32x4*)(K.base + a);
+        v = *(const CLY_GL u32x4*)(K.base + a);
         const uint32_t n = (uint32_t)(K.len - a);          // 1..15 valid bytes
         #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -360,18 +380,28 @@ __device__ __forceinline__ u32x4 piece(const Chunk& K, uint32_t o) {
 }
 
 // Phase A for one lane: the chain of its chunk under its own guess.
-__device__ __noinline__ void phase_a(const Chunk& K, LaneChain& L) {
-    if (!K.on) { chain_set(L, LM_OFF); return; }
-    if (K.cb == 0) { walk(K, 0, true, L); return; }
+__device__ __noinline__ LaneChain phase_a(const Chunk K) {
+    LaneChain L;
+    if (!K.on) { chain_set(L, LM_OFF); return L; }
+    if (K.cb == 0) { walk(K, 0, true, L); return L; }
     chain_set(L, LM_NONE);
     bool found = false;
     for (int b = 0; b < CLY_NB; b++) {
         if (found) continue;
         uint32_t w[CLY_BW + 4];
-        #pragma unroll
-        for (int k = 0; k < CLY_BW / 4 + 1; k++) {
-            const u32x4 v = piece(K, (uint32_t)(b * CLY_BW * 4 + 16 * k));
-            w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+        if ((uint64_t)K.cb + (uint32_t)((b + 1) * CLY_BW * 4 + 16) <= K.len) {
+            const CLY_GL u32x4* src = (const CLY_GL u32x4*)(K.base + K.cb + (uint32_t)(b * CLY_BW * 4));
+            #pragma unroll
+            for (int k = 0; k < CLY_BW / 4 + 1; k++) {
+                const u32x4 v = src[k];
+                w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+            }
+        } else {
+            #pragma unroll
+            for (int k = 0; k < CLY_BW / 4 + 1; k++) {
+                const u32x4 v = piece(K, (uint32_t)(b * CLY_BW * 4 + 16 * k));
+                w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+            }
         }
         // candidate positions of the burst, one bit each (4 per word)
         uint32_t cmk[CLY_BW / 8];
@@ -397,6 +427,7 @@ __device__ __noinline__ void phase_a(const Chunk& K, LaneChain& L) {
             }
         }
     }
+    return L;
 }
 
 // ---------------------------------------------------------------------------
@@ -405,6 +436,11 @@ __device__ __forceinline__ int scan_max_incl(int v, int lane) {
     #pragma unroll
     for (int o = 1; o < 64; o <<= 1) { const int u = __shfl_up(v, o, 64); if (lane >= o) v = max(v, u); }
     return v;
+}
+__device__ __forceinline__ int scan_max_excl(int v, int lane) {
+    const int inc = scan_max_incl(v, lane);
+    const int up = __shfl_up(inc, 1, 64);
+    return lane > 0 ? up : -1;
 }
 __device__ __forceinline__ uint32_t scan_add_incl(uint32_t v, int lane) {
     #pragma unroll
@@ -417,7 +453,7 @@ __device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src) { return (uint
 // chunk before it leaves (the tile's entry X0 for the first lanes; dead0: the
 // file's chain ended before the tile).  The lowest disagreeing lane is
 // re-walked exactly, until every lane agrees.
-__device__ __noinline__ void resolve(const Chunk& K, LaneChain& L, int lane, uint32_t X0, bool dead0, Globals* g) {
+__device__ __noinline__ LaneChain resolve(const Chunk K, LaneChain L, int lane, uint32_t X0, bool dead0, Globals* g) {
     for (int iter = 0;; iter++) {
         const bool isC = L.mode == LM_CHAIN;
         const int pk = scan_max_incl(isC ? lane : -1, lane);
@@ -435,8 +471,8 @@ __device__ __noinline__ void resolve(const Chunk& K, LaneChain& L, int lane, uin
             else bad = true;                                   // LM_DEAD under a live chain
         }
         const u64 bm = __ballot(bad);
-        if (!bm) return;
-        if (iter > 2 * CLY_NL + 2) { if (lane == 0) atomicOr(&g->fail, 1u); return; }
+        if (!bm) return L;
+        if (iter > 2 * CLY_NL + 2) { if (lane == 0) atomicOr(&g->fail, 1u); return L; }
         const int k = __ffsll((long long)bm) - 1;
         if (lane == k) {
             if (din) chain_set(L, LM_DEAD);
@@ -455,8 +491,12 @@ struct LBState {
     uint32_t P_last;             // that record's start (NONE32: none in this file)
     int      dead;               // the file's chain has ended
 };
-__device__ __forceinline__ u64 ld_agent(const u64* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ void st_agent(u64* p, u64 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ u64 ld_agent(const u64* p) {
+    return __hip_atomic_load((const CLY_GL u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(u64* p, u64 v) {
+    __hip_atomic_store((CLY_GL u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 #define SPIN_MAX (1u << 18)
 
 __device__ __forceinline__ LBState lb_virtual() {
@@ -493,21 +533,31 @@ __device__ __forceinline__ u64 shfl64(u64 v, int src) {
 }
 __device__ __forceinline__ void bad_spin(Globals* g, uint32_t code) { atomicOr(&g->fail, code); }
 
+__device__ __forceinline__ int scan_max_excl(int v, int lane);
+
+// Look-back of tile t: the nearest published INCL before it, then the
+// LOCALs after it composed 64 tiles (one per lane) at a time.  Within a
+// window the chain position entering tile m is the exit of the nearest tile
+// before it that has a chain (or the window's entering state), "ended" is set
+// by the nearest tile whose chain terminates and cleared by the first tile of
+// a file; a tile whose guess disagrees with the position it is entered at
+// stops the window: its own INCL (published once it has re-resolved) is
+// awaited and the window goes on after it.
 __device__ __noinline__ LBState look_back(const TileDesc* desc, int64_t t, int lane, Globals* g) {
-    // nearest tile before t with a published INCL (tile -1: nothing, dead)
     int64_t k = -1;
     for (int64_t base = t - 1; base >= 0; base -= 64) {
         const int64_t u = base - lane;
         const bool pub = u >= 0 && (ld_agent(&desc[u].i[0]) & DF_PUB);
         const u64 bm = __ballot(pub);
+        PCNT(6, 1);
         if (bm) { k = base - (__ffsll((long long)bm) - 1); break; }
     }
     LBState s = lb_virtual();
     if (k >= 0) s = lb_incl(ld_agent(&desc[k].i[0]), ld_agent(&desc[k].i[1]), ld_agent(&desc[k].i[2]));
-    // forward from it over the LOCALs (or INCLs) of k+1 .. t-1, 64 per round
     for (int64_t u0 = k + 1; u0 < t; u0 += 64) {
         const int64_t u = u0 + lane;
-        int got = u < t ? 0 : 3;                       // 1 LOCAL, 2 INCL
+        const int n = t - u0 < 64 ? (int)(t - u0) : 64;
+        int got = lane < n ? 0 : 3;                    // 1 LOCAL, 2 INCL
         u64 w0 = 0;
         for (uint32_t spin = 0;; spin++) {
             if (got == 0) {
@@ -519,31 +569,83 @@ __device__ __noinline__ LBState look_back(const TileDesc* desc, int64_t t, int l
                 }
             }
             if (__ballot(got == 0) == 0) break;
+            PCNT(8, 1);
             if (spin > SPIN_MAX) { if (lane == 0) bad_spin(g, 2u); return s; }
             __builtin_amdgcn_s_sleep(2);
         }
+        PCNT(7, 1);
         u64 w1 = 0, w2 = 0, w3 = 0;
         if (got == 2) { w1 = ld_agent(&desc[u].i[1]); w2 = ld_agent(&desc[u].i[2]); }
         else if (got == 1) { w1 = ld_agent(&desc[u].l[1]); w2 = ld_agent(&desc[u].l[2]); w3 = ld_agent(&desc[u].l[3]); }
-        // the last INCL of the round overrides everything before it
-        const u64 bi = __ballot(got == 2);
-        int m = bi ? 63 - __clzll((long long)bi) : 0;
-        const int n = t - u0 < 64 ? (int)(t - u0) : 64;
-        if (bi) { s = lb_incl(shfl64(w0, m), shfl64(w1, m), shfl64(w2, m)); m++; }
-        for (; m < n; m++) {
-            const u64 a0 = shfl64(w0, m), a1 = shfl64(w1, m), a2 = shfl64(w2, m), a3 = shfl64(w3, m);
-            if (!lb_local(s, a0, a1, a2, a3)) {
-                // the tile's guess was wrong: wait for it to publish its true state
-                const TileDesc* d = &desc[u0 + m];
-                u64 i0 = 0;
-                for (uint32_t spin = 0;; spin++) {
-                    i0 = ld_agent(&d->i[0]);
-                    if (i0 & DF_PUB) break;
-                    if (spin > SPIN_MAX) { if (lane == 0) bad_spin(g, 4u); return s; }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                s = lb_incl(i0, ld_agent(&d->i[1]), ld_agent(&d->i[2]));
+        int m_lo = 0;
+        for (int round = 0;; round++) {
+            // the last INCL at or after m_lo overrides everything before it
+            const u64 bi = __ballot(got == 2 && lane >= m_lo);
+            if (bi) {
+                const int mi = 63 - __clzll((long long)bi);
+                s = lb_incl(shfl64(w0, mi), shfl64(w1, mi), shfl64(w2, mi));
+                m_lo = mi + 1;
             }
+            if (m_lo >= n) break;
+            const bool act = lane >= m_lo && lane < n;
+            const bool fof = act && (w0 & DF_FOF);
+            const bool none = act && !fof && (w0 & DF_NONE);
+            const bool chain = act && !none;
+            const bool term = chain && (w0 & DF_TERM);
+            const uint32_t G = (uint32_t)w1, Xo = (uint32_t)(w1 >> 32), tend = (uint32_t)w3;
+            // entering state of each lane
+            const int e = scan_max_excl((term || fof) ? lane : -1, lane);
+            const int j = scan_max_excl(chain ? lane : -1, lane);
+            const int te = __shfl((int)term, e < 0 ? 0 : e, 64);
+            const uint32_t xj = shfl_u32(Xo, j < 0 ? 0 : j);
+            const bool din = e >= 0 ? te != 0 : s.dead != 0;
+            const uint32_t Xin = j >= 0 ? xj : s.X;
+            const bool valid = !act || fof || din || (none ? Xin >= tend : Xin == G);
+            const u64 bad = __ballot(!valid);
+            const int ne = bad ? __ffsll((long long)bad) - 1 : n;      // lanes [m_lo, ne) compose
+            const bool in = act && lane < ne;
+            const bool applied = in && chain && (fof || !din);
+            const bool rec = applied && (fof || (w0 & DF_REC));
+            // state after each composed lane (inclusive scans)
+            const uint32_t cnt = applied ? (uint32_t)(w0 >> 32) : 0u;
+            const uint32_t ci = scan_add_incl(cnt, lane);
+            const int ei = scan_max_incl(in && (term || fof) ? lane : -1, lane);
+            const int ji = scan_max_incl(in && chain ? lane : -1, lane);
+            const int ri = scan_max_incl(rec ? lane : -1, lane);
+            const int tei = __shfl((int)term, ei < 0 ? 0 : ei, 64);
+            const uint32_t xji = shfl_u32(Xo, ji < 0 ? 0 : ji);
+            const u64 w0r = shfl64(w0, ri < 0 ? 0 : ri), w2r = shfl64(w2, ri < 0 ? 0 : ri);
+            LBState o = s;
+            o.count = s.count + ci;
+            if (ei >= 0) o.dead = tei != 0;
+            if (ji >= 0) o.X = xji;
+            if (ri >= 0) {
+                if (w0r & DF_REC) { o.crc_last = (uint32_t)w2r; o.P_last = (uint32_t)(w2r >> 32); }
+                else { o.crc_last = 0; o.P_last = NONE32; }
+            }
+            const int last = ne - 1;
+            if (last >= m_lo) {
+                s.count = shfl64(o.count, last);
+                s.X = shfl_u32(o.X, last);
+                s.dead = __shfl(o.dead, last, 64);
+                s.crc_last = shfl_u32(o.crc_last, last);
+                s.P_last = shfl_u32(o.P_last, last);
+            }
+            if (!bad) break;
+            // the tile at ne guessed wrong: wait for its true state
+            const TileDesc* d = &desc[u0 + ne];
+            u64 i0 = 0;
+            PCNT(9, 1);
+            for (uint32_t spin = 0;; spin++) {
+                i0 = ld_agent(&d->i[0]);
+                if (i0 & DF_PUB) break;
+                PCNT(10, 1);
+                if (spin > SPIN_MAX) { if (lane == 0) bad_spin(g, 4u); return s; }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            s = lb_incl(i0, ld_agent(&d->i[1]), ld_agent(&d->i[2]));
+            m_lo = ne + 1;
+            if (m_lo >= n) break;
         }
     }
     return s;
@@ -585,7 +687,7 @@ __device__ __forceinline__ uint32_t patch_part(const CLY_LDS uint8_t* smem, cons
 }
 
 // Tuple of the record at p (header h): 48 B, cly_tuple layout.
-__device__ __forceinline__ void put_tuple(cly_tuple* out, uint64_t idx, uint64_t out_cap, const Chunk& K, uint32_t p,
+__device__ __forceinline__ void put_tuple(gtuples out, uint64_t idx, uint64_t out_cap, const Chunk& K, uint32_t p,
                                           const Hdr& h, uint32_t fid, Globals* g) {
     int tn;
     int64_t tx;
@@ -596,7 +698,7 @@ __device__ __forceinline__ void put_tuple(cly_tuple* out, uint64_t idx, uint64_t
     }
     if (idx >= out_cap) { atomicOr(&g->overflow, 1u); return; }
     const uint64_t off = p, ex = (uint64_t)h.exp, txv = tn < 0 ? 0ull : (uint64_t)tx;
-    u32x4* dst = (u32x4*)(out + idx);
+    CLY_GL u32x4* dst = (CLY_GL u32x4*)(out + idx);
     dst[0] = (u32x4){(uint32_t)off, (uint32_t)(off >> 32), (uint32_t)ex, (uint32_t)(ex >> 32)};
     dst[1] = (u32x4){(uint32_t)txv, (uint32_t)(txv >> 32), fid, (uint32_t)h.size};
     dst[2] = (u32x4){h.ks, h.vs,
@@ -606,73 +708,63 @@ __device__ __forceinline__ void put_tuple(cly_tuple* out, uint64_t idx, uint64_t
 }
 
 // ---------------------------------------------------------------------------
-// Phase C, uniform path: the chunk's 4-byte words through the register, each
-// record's combined patch XORed in at its word (events held in a 4-deep
-// per-lane queue that the walker keeps filled, a quarter-burst ahead).
-struct Evq { uint32_t an[4], dl[4]; };
-__device__ __forceinline__ void evq_push(Evq& q, uint32_t w, uint32_t d) {
-    if (q.an[0] == NO_EV) { q.an[0] = w; q.dl[0] = d; }
-    else if (q.an[1] == NO_EV) { q.an[1] = w; q.dl[1] = d; }
-    else if (q.an[2] == NO_EV) { q.an[2] = w; q.dl[2] = d; }
-    else { q.an[3] = w; q.dl[3] = d; }
-}
-__device__ __forceinline__ void evq_pop1(Evq& q) {
-    q.an[0] = q.an[1]; q.dl[0] = q.dl[1];
-    q.an[1] = q.an[2]; q.dl[1] = q.dl[2];
-    q.an[2] = q.an[3]; q.dl[2] = q.dl[3];
-    q.an[3] = NO_EV;
-}
-template <int KS>
-__device__ __forceinline__ uint32_t crc_quarter(const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t s, const u32x4& va,
-                                                const u32x4& vb, uint32_t w0, const Evq& q) {
-    const uint32_t w[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
-    #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        uint32_t x = s ^ w[i];
-        #pragma unroll
-        for (int k = 0; k < KS; k++) x ^= q.an[k] == w0 + (uint32_t)i ? q.dl[k] : 0u;
-        s = crc_word(smem, x, cl);
-    }
-    return s;
-}
+// Phase C, uniform path.  Each record start P has one combined patch delta'
+// on one word of the stream (patch_part); the walker decodes the lane's
+// records (tuples written as it goes) and queues (word, delta') events in a
+// per-lane LDS ring, ahead of the stream.  Per 128-B burst the stream loads
+// the lane's 32 words, XORs in the burst's events, and runs the register
+// through them: the loop body is the plain slicing-by-4 step.
 struct Walker {
     uint32_t p, cq, i;
     Gath gt;
 };
 __device__ __forceinline__ void walker_step(const Chunk& K, Walker& W, uint32_t nrec, uint64_t base, uint32_t fid,
-                                            cly_tuple* out, uint64_t out_cap, const CLY_LDS uint8_t* smem,
-                                            const CrcLane& cl, Evq& q, Globals* g) {
+                                            gtuples out, uint64_t out_cap, const CLY_LDS uint8_t* smem,
+                                            const CrcLane& cl, uint32_t& w, uint32_t& d, Globals* g) {
     const Hdr h = hdr_at(K.base, W.p, K.len, W.gt);
     put_tuple(out, base + W.i, out_cap, K, W.p, h, fid, g);
-    uint32_t d;
     const uint32_t wlo = K.cb >> 2;
-    const uint32_t w = patch_part(smem, cl, W.p, h.crc, W.cq, wlo, wlo + CLY_NW, d);
-    if (w != NONE32) evq_push(q, w - wlo, d);
+    const uint32_t wa = patch_part(smem, cl, W.p, h.crc, W.cq, wlo, wlo + CLY_NW, d);
+    w = wa == NONE32 ? NONE32 : wa - wlo;
     W.cq = h.crc;
     W.p += (uint32_t)h.size;
     W.i++;
     if (W.i < nrec && gath_ok(W.p, K.len)) gath_issue(K.base, W.p, W.gt);
 }
 
-__device__ __noinline__ uint32_t phase_c_fast(const Chunk& K, const LaneChain& L, const LaneIn& I, bool active, uint32_t fid,
-                                 cly_tuple* out, uint64_t out_cap, const CLY_LDS uint8_t* smem, const CrcLane& cl,
-                                 Globals* g) {
-    uint32_t s = 0;
-    Evq q;
-    #pragma unroll
-    for (int k = 0; k < 4; k++) { q.an[k] = NO_EV; q.dl[k] = 0; }
+__device__ __noinline__ uint32_t phase_c_fast(const Chunk K, const LaneChain L, const LaneIn I, bool active, uint32_t fid,
+                                              gtuples out, uint64_t out_cap, const CLY_LDS uint8_t* smem,
+                                              CLY_LDS u32x2* evq, const CrcLane cl, Globals* g) {
+    // ring slot k of this lane: evq[k * 64]  (evq points at the wave's ring + lane)
+    uint32_t head = 0, tail = 0;
     const uint32_t wlo = K.cb >> 2;
     if (active && I.spill) {
         uint32_t d;
         const uint32_t w = patch_part(smem, cl, I.P_in, I.crc_in, 0u, wlo, wlo + CLY_NW, d);
-        if (w != NONE32) evq_push(q, w - wlo, d);
+        if (w != NONE32) { evq[0] = (u32x2){w - wlo, d}; tail = 1; }
     }
     Walker W;
     W.p = L.E; W.cq = I.crc_in; W.i = 0;
     const uint32_t nrec = (active && L.mode == LM_CHAIN) ? L.cnt : 0u;
     if (nrec && gath_ok(W.p, K.len)) gath_issue(K.base, W.p, W.gt);
-    const u32x4* src = (const u32x4*)(K.base + K.cb);
+    // next event in registers
+    uint32_t nw = NONE32, nd = 0;
+    uint32_t s = 0;
+    const CLY_GL u32x4* src = (const CLY_GL u32x4*)(K.base + K.cb);
+    #pragma unroll 1
     for (int b = 0; b < CLY_NB; b++) {
+        const uint32_t bend = (uint32_t)(b + 1) * CLY_BW;
+        // walker ahead: every event of this and the next burst queued (ring permitting)
+        for (;;) {
+            const bool need = W.i < nrec && tail - head < EVQ && ((W.p >> 2) - wlo) < bend + CLY_BW;
+            if (!__ballot(need)) break;
+            if (need) {
+                uint32_t w, d;
+                walker_step(K, W, nrec, I.base, fid, out, out_cap, smem, cl, w, d, g);
+                if (w != NONE32) { evq[(tail % EVQ) * 64] = (u32x2){w, d}; tail++; }
+            }
+        }
+        if (nw == NONE32 && head != tail) { const u32x2 e = evq[(head % EVQ) * 64]; nw = e.x; nd = e.y; head++; }
         u32x4 v[CLY_BW / 4];
         if (active) {
             #pragma unroll
@@ -681,30 +773,27 @@ __device__ __noinline__ uint32_t phase_c_fast(const Chunk& K, const LaneChain& L
             #pragma unroll
             for (int k = 0; k < CLY_BW / 4; k++) v[k] = (u32x4){0u, 0u, 0u, 0u};
         }
+        // the burst's events into its words
+        while (__ballot(nw < bend)) {
+            if (nw < bend) {
+                const uint32_t r = nw - (uint32_t)b * CLY_BW;
+                #pragma unroll
+                for (int k = 0; k < CLY_BW / 4; k++) {
+                    v[k].x ^= r == 4u * k ? nd : 0u;
+                    v[k].y ^= r == 4u * k + 1 ? nd : 0u;
+                    v[k].z ^= r == 4u * k + 2 ? nd : 0u;
+                    v[k].w ^= r == 4u * k + 3 ? nd : 0u;
+                }
+                nw = NONE32;
+                if (head != tail) { const u32x2 e = evq[(head % EVQ) * 64]; nw = e.x; nd = e.y; head++; }
+            }
+        }
         #pragma unroll
-        for (int qq = 0; qq < CLY_BW / 8; qq++) {
-            const uint32_t w0 = (uint32_t)(b * CLY_BW + 8 * qq);
-            // every event of this quarter must be queued: step the walker while its
-            // next record's first patch word is near
-            for (;;) {
-                const bool need = W.i < nrec && q.an[3] == NO_EV && ((W.p >> 2) - wlo) < w0 + 16;
-                if (!__ballot(need)) break;
-                if (need) walker_step(K, W, nrec, I.base, fid, out, out_cap, smem, cl, q, g);
-            }
-            const uint32_t we = w0 + 8;
-            const uint32_t nh = (q.an[0] < we) + (q.an[1] < we) + (q.an[2] < we) + (q.an[3] < we);
-            if (__ballot(nh >= 3)) {
-                s = crc_quarter<4>(smem, cl, s, v[2 * qq], v[2 * qq + 1], w0, q);
-                for (int r = 0; r < 4; r++) if ((uint32_t)r < nh) evq_pop1(q);
-            } else if (__ballot(nh == 2)) {
-                s = crc_quarter<2>(smem, cl, s, v[2 * qq], v[2 * qq + 1], w0, q);
-                for (int r = 0; r < 2; r++) if ((uint32_t)r < nh) evq_pop1(q);
-            } else if (__ballot(nh == 1)) {
-                s = crc_quarter<1>(smem, cl, s, v[2 * qq], v[2 * qq + 1], w0, q);
-                if (nh) evq_pop1(q);
-            } else {
-                s = crc_quarter<0>(smem, cl, s, v[2 * qq], v[2 * qq + 1], w0, q);
-            }
+        for (int k = 0; k < CLY_BW / 4; k++) {
+            s = crc_word(smem, s ^ v[k].x, cl);
+            s = crc_word(smem, s ^ v[k].y, cl);
+            s = crc_word(smem, s ^ v[k].z, cl);
+            s = crc_word(smem, s ^ v[k].w, cl);
         }
     }
     return s;
@@ -718,7 +807,7 @@ __device__ __noinline__ uint32_t phase_c_fast(const Chunk& K, const LaneChain& L
 // (register after its end word != 0) is returned in fail_P / fail_i.
 struct Bnd { uint32_t P, c, q, start; uint64_t idx; int term; };
 __device__ __noinline__ uint32_t exact_lane(const Chunk& K, const LaneChain& L, const LaneIn& I, uint32_t s0, bool emit,
-                               bool observe, uint32_t fid, cly_tuple* out, uint64_t out_cap,
+                               bool observe, uint32_t fid, gtuples out, uint64_t out_cap,
                                const CLY_LDS uint8_t* smem, const CrcLane& cl, Globals* g, uint32_t& fail_P,
                                uint64_t& fail_i, uint32_t& expect) {
     uint32_t s = s0;
@@ -756,7 +845,7 @@ __device__ __noinline__ uint32_t exact_lane(const Chunk& K, const LaneChain& L, 
         }
         uint32_t d = 0;
         if ((uint64_t)A < K.len) {
-            d = *(const uint32_t*)(K.base + A);
+            d = *(const CLY_GL uint32_t*)(K.base + A);
             const uint64_t n = K.len - A;
             if (n < 4) d &= (1u << (8 * n)) - 1u;
         }
@@ -808,7 +897,7 @@ __device__ __forceinline__ int find_file(const uint32_t* __restrict__ tprefix, i
 }
 __device__ __forceinline__ Chunk make_chunk(const DevFile& F, uint32_t tt, int lane) {
     Chunk K;
-    K.base = F.base; K.len = F.len;
+    K.base = (gbytes)F.base; K.len = F.len;
     const uint64_t cb = (uint64_t)tt * CLY_TILE + (uint64_t)lane * CLY_CH;
     K.cb = (uint32_t)cb;
     K.ce = (uint32_t)(cb + CLY_CH < F.len ? cb + CLY_CH : F.len);
@@ -847,82 +936,89 @@ __device__ __forceinline__ uint32_t tile_fold(const CLY_LDS uint8_t* smem, uint3
     return r;
 }
 
-__global__ void __launch_bounds__(512, 2)
+// Phase A of one tile: the lanes' chains under their own guesses, made to
+// agree, and the tile's LOCAL descriptor.
+struct TileA { LaneChain L; uint32_t G; };
+__device__ __noinline__ TileA tile_a(const Chunk K, uint32_t t, uint32_t tt, uint64_t flen, int lane, TileDesc* desc,
+                                     Globals* g) {
+    const bool fof = tt == 0;
+    TileA A;
+    A.L = phase_a(K);
+    A.G = NONE32;
+    {
+        const u64 bm = __ballot(A.L.mode == LM_CHAIN);
+        if (bm) A.G = shfl_u32(A.L.E, __ffsll((long long)bm) - 1);
+    }
+    A.L = resolve(K, A.L, lane, fof ? 0u : A.G, false, g);
+    const LaneChain& L = A.L;
+    const u64 bc = __ballot(L.mode == LM_CHAIN), br = __ballot(L.mode == LM_CHAIN && L.cnt > 0);
+    const uint32_t c = L.mode == LM_CHAIN ? L.cnt : 0u;
+    const uint32_t tile_cnt = shfl_u32(scan_add_incl(c, lane), 63);
+    const int lc = bc ? 63 - __clzll((long long)bc) : 0, lr = br ? 63 - __clzll((long long)br) : 0;
+    const uint32_t X = shfl_u32(L.x, lc);
+    const int term = __shfl(L.term, lc, 64);
+    const uint32_t crc = shfl_u32(L.last_crc, lr), Pl = shfl_u32(L.last, lr);
+    if (lane == 0) {
+        const uint64_t tstart = (uint64_t)tt * CLY_TILE;
+        const uint32_t tend = tstart + CLY_TILE >= flen ? (uint32_t)(flen + 1) : (uint32_t)(tstart + CLY_TILE);
+        TileDesc* d = &desc[t];
+        st_agent(&d->l[1], (u64)A.G | ((u64)X << 32));
+        st_agent(&d->l[2], (u64)crc | ((u64)Pl << 32));
+        st_agent(&d->l[3], (u64)tend);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        u64 f0 = DF_PUB | ((u64)tile_cnt << 32);
+        if (bc && term != TERM_NONE) f0 |= DF_TERM;
+        if (!bc) f0 |= DF_NONE;
+        if (fof) f0 |= DF_FOF;
+        if (br) f0 |= DF_REC;
+        st_agent(&d->l[0], f0);
+    }
+    return A;
+}
+__device__ __forceinline__ uint32_t take_tile(Globals* g, int lane) {
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(&g->ticket, 1u);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)shfl_u32(t, 0));
+}
+
+__global__ void __launch_bounds__(64 * SCAN_WAVES, 4)
 k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
-       TileDesc* desc, uint32_t* treg, FileInfo* finfo, const uint32_t* __restrict__ nib, cly_tuple* out,
+       TileDesc* desc, uint32_t* treg, FileInfo* finfo, const uint32_t* __restrict__ nib, cly_tuple* out_,
        uint64_t out_cap, Globals* g, uint32_t* dump) {
+    gtuples out = (gtuples)out_;
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
     init_tables(smem, nib);
     const int lane = threadIdx.x & 63;
     const CrcLane cl = crc_lane(lane);
+    CLY_LDS u32x2* evq = (CLY_LDS u32x2*)(smem + LDS_EVQ) + (threadIdx.x >> 6) * (EVQ * 64) + lane;
+    // Tiles are software-pipelined per wave: phase A of the wave's next tile
+    // (and its LOCAL) comes before phase C of the current one, so the
+    // look-back of the next tile finds its predecessors published.
+    uint32_t t = take_tile(g, lane);
+    if (t >= ntiles) return;
+    int f = find_file(tprefix, nfiles, t);
+    DevFile F = files[f];
+    uint32_t tt = t - F.first_tile;
+    Chunk K = make_chunk(F, tt, lane);
+    TileA A = tile_a(K, t, tt, F.len, lane, desc, g);
     for (;;) {
-        uint32_t t = 0;
-        if (lane == 0) t = atomicAdd(&g->ticket, 1u);
-        t = (uint32_t)__builtin_amdgcn_readfirstlane((int)shfl_u32(t, 0));
-        if (t >= ntiles) break;
-        const int f = find_file(tprefix, nfiles, t);
-        const DevFile F = files[f];
-        const uint32_t tt = t - F.first_tile;
+        PROF_T0();
         const bool fof = tt == 0;
-        const Chunk K = make_chunk(F, tt, lane);
-        DBG("t %u file %d start\n", t, f);
-        // ---- A: chains under the lanes' own guesses, made to agree
-        LaneChain L;
-        phase_a(K, L);
-        const uint32_t dbg_m0 = (uint32_t)L.mode, dbg_e0 = L.E;
-        uint32_t G = NONE32;
-        {
-            const u64 bm = __ballot(L.mode == LM_CHAIN);
-            if (bm) G = shfl_u32(L.E, __ffsll((long long)bm) - 1);
-        }
-        DBG("t %u phase A done G %u\n", t, G);
-        resolve(K, L, lane, fof ? 0u : G, false, g);
-        DBG("t %u resolved\n", t);
-        const uint32_t dbg_m1 = (uint32_t)L.mode, dbg_e1 = L.E;
-        {
-            // LOCAL descriptor
-            const u64 bc = __ballot(L.mode == LM_CHAIN), br = __ballot(L.mode == LM_CHAIN && L.cnt > 0);
-            uint32_t tile_cnt = 0;
-            {
-                const uint32_t c = L.mode == LM_CHAIN ? L.cnt : 0u;
-                tile_cnt = shfl_u32(scan_add_incl(c, lane), 63);
-            }
-            const int lc = bc ? 63 - __clzll((long long)bc) : 0, lr = br ? 63 - __clzll((long long)br) : 0;
-            const uint32_t X = shfl_u32(L.x, lc);
-            const int term = __shfl(L.term, lc, 64);
-            const uint32_t crc = shfl_u32(L.last_crc, lr), Pl = shfl_u32(L.last, lr);
-            if (lane == 0) {
-                const uint64_t tstart = (uint64_t)tt * CLY_TILE;
-                const uint32_t tend = tstart + CLY_TILE >= F.len ? (uint32_t)(F.len + 1) : (uint32_t)(tstart + CLY_TILE);
-                TileDesc* d = &desc[t];
-                st_agent(&d->l[1], (u64)G | ((u64)X << 32));
-                st_agent(&d->l[2], (u64)crc | ((u64)Pl << 32));
-                st_agent(&d->l[3], (u64)tend);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                u64 f0 = DF_PUB | ((u64)tile_cnt << 32);
-                if (bc && term != TERM_NONE) f0 |= DF_TERM;
-                if (!bc) f0 |= DF_NONE;
-                if (fof) f0 |= DF_FOF;
-                if (br) f0 |= DF_REC;
-                st_agent(&d->l[0], f0);
-            }
-        }
+        LaneChain L = A.L;
         // ---- L: the true state entering the tile
-        DBG("t %u local published\n", t);
         LBState S = look_back(desc, (int64_t)t, lane, g);
-        DBG("t %u look-back done\n", t);
+        PROF(1);
         if (fof) { S.dead = 0; S.X = 0; S.crc_last = 0; S.P_last = NONE32; }
-        if (!fof && (S.dead || S.X != G) && lane == 0) atomicAdd(&g->refix, 1u);
-        resolve(K, L, lane, S.dead ? 0u : S.X, S.dead != 0, g);
+        if (!fof && (S.dead || S.X != A.G) && lane == 0) atomicAdd(&g->refix, 1u);
+        L = resolve(K, L, lane, S.dead ? 0u : S.X, S.dead != 0, g);
         uint32_t tile_cnt;
         const LaneIn I = lane_inputs(K, L, S, lane, tile_cnt);
         if (dump) {
             // debug dump (CLY_DUMP): the final chain of every lane
-            uint32_t* o = dump + ((uint64_t)t * 64 + lane) * 12;
+            uint32_t* o = dump + ((uint64_t)t * 64 + lane) * 8;
             o[0] = (uint32_t)L.mode; o[1] = L.E; o[2] = L.x; o[3] = (uint32_t)L.term; o[4] = L.cnt;
-            o[5] = S.X | (S.dead ? 0x80000000u : 0u); o[6] = G; o[7] = (uint32_t)f;
-            o[8] = dbg_m0; o[9] = dbg_e0; o[10] = dbg_m1; o[11] = dbg_e1;
+            o[5] = S.X | (S.dead ? 0x80000000u : 0u); o[6] = A.G; o[7] = (uint32_t)f;
         }
         {
             // INCL descriptor
@@ -949,13 +1045,28 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                 if (t == ntiles - 1) g->total = o.count;
             }
         }
+        PROF(2);
+        // ---- A of the next tile
+        const uint32_t tn = take_tile(g, lane);
+        int fn = f;
+        DevFile Fn = F;
+        uint32_t ttn = 0;
+        Chunk Kn = K;
+        TileA An = A;
+        if (tn < ntiles) {
+            fn = find_file(tprefix, nfiles, tn);
+            Fn = files[fn];
+            ttn = tn - Fn.first_tile;
+            Kn = make_chunk(Fn, ttn, lane);
+            An = tile_a(Kn, tn, ttn, Fn.len, lane, desc, g);
+        }
+        PROF(0);
         // ---- C: CRC stream, tuples
         const bool term_lane = L.mode == LM_CHAIN && L.term != TERM_NONE;
         const bool slow = L.mode == LM_CHAIN && !term_lane && L.minsz < 12;
         const bool fast = (L.mode == LM_CHAIN && !term_lane && !slow) || L.mode == LM_NONE;
-        DBG("t %u incl published\n", t);
-        uint32_t r = phase_c_fast(K, L, I, fast, F.fid, out, out_cap, smem, cl, g);
-        DBG("t %u phase C fast done\n", t);
+        uint32_t r = phase_c_fast(K, L, I, fast, F.fid, out, out_cap, smem, evq, cl, g);
+        PROF(3);
         if (term_lane || slow) {
             uint32_t fp, ex;
             uint64_t fi;
@@ -968,9 +1079,12 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             }
         }
         if (!fast && !term_lane && !slow) r = 0;
+        PROF(4);
         r = tile_fold(smem, r, lane);
+        PROF(5);
         if (lane == 0) treg[t] = r;
-        DBG("t %u done\n", t);
+        if (tn >= ntiles) break;
+        t = tn; f = fn; F = Fn; tt = ttn; K = Kn; A = An;
     }
 }
 
@@ -1041,7 +1155,7 @@ k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __rest
 // terminal re-derives its chain from the published states, the register
 // entering each chunk, and walks its records' checks from there; the first
 // failing record of the file wins (atomicMin on offset << 32 | index).
-__global__ void __launch_bounds__(512, 2)
+__global__ void __launch_bounds__(512, 4)
 k_locate(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
          const TileDesc* desc, const uint32_t* __restrict__ treg, FileInfo* finfo, const uint32_t* __restrict__ nib,
          Globals* g) {
@@ -1062,9 +1176,8 @@ k_locate(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restri
         if (fof) { S = lb_virtual(); S.dead = 0; S.X = 0; S.count = fo->first_index; }
         else S = lb_incl(desc[t - 1].i[0], desc[t - 1].i[1], desc[t - 1].i[2]);
         if (S.dead) continue;
-        LaneChain L;
-        phase_a(K, L);
-        resolve(K, L, lane, S.X, false, g);
+        LaneChain L = phase_a(K);
+        L = resolve(K, L, lane, S.X, false, g);
         uint32_t tile_cnt;
         const LaneIn I = lane_inputs(K, L, S, lane, tile_cnt);
         // register entering the tile
@@ -1147,10 +1260,10 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     }
     {
         int per_cu = 0, ncu = 0;
-        HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_scan, 512, 0));
+        HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_scan, 64 * SCAN_WAVES, 0));
         HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
         if (per_cu < 1) per_cu = 1;
-        if (per_cu > 2) per_cu = 2;
+        if (per_cu > 1) per_cu = 1;
         c->scan_grid = per_cu * ncu;
     }
     *out = c;
@@ -1240,13 +1353,13 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     HIPCK(hipMemsetAsync(c->d_finfo, 0, sizeof(FileInfo) * nfiles, st));
     HIPCK(hipMemsetAsync(c->d_g, 0, sizeof(Globals), st));
     int grid = c->scan_grid;
-    if ((int64_t)grid * 8 > ntiles) grid = (int)((ntiles + 7) / 8);
+    if ((int64_t)grid * SCAN_WAVES > ntiles) grid = (int)((ntiles + SCAN_WAVES - 1) / SCAN_WAVES);
     HIPCK(hipEventRecord(c->ev[0], st));
     // debug: CLY_DUMP=<path> appends every lane's final chain (8 u32 per lane) of each call
     const char* dump_path = getenv("CLY_DUMP");
     uint32_t* d_dump = nullptr;
-    if (dump_path) HIPCK(hipMalloc(&d_dump, sizeof(uint32_t) * 12 * 64 * ntiles));
-    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(512), 0, st, c->d_files, nfiles, c->d_tprefix, (uint32_t)ntiles,
+    if (dump_path) HIPCK(hipMalloc(&d_dump, sizeof(uint32_t) * 8 * 64 * ntiles));
+    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * SCAN_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, (uint32_t)ntiles,
                        c->d_desc, c->d_treg, c->d_finfo, c->d_nib, d_out, out_cap, c->d_g, d_dump);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[1], st));
@@ -1258,7 +1371,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     HIPCK(hipStreamSynchronize(st));
     bool located = false;
     if (c->h_g->any_fail && !c->h_g->fail) {
-        hipLaunchKernelGGL(k_locate, dim3(grid), dim3(512), 0, st, c->d_files, nfiles, c->d_tprefix, (uint32_t)ntiles,
+        hipLaunchKernelGGL(k_locate, dim3(c->scan_grid), dim3(512), 0, st, c->d_files, nfiles, c->d_tprefix, (uint32_t)ntiles,
                            c->d_desc, c->d_treg, c->d_finfo, c->d_nib, c->d_g);
         HIPCK(hipGetLastError());
         located = true;
@@ -1268,7 +1381,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
     if (d_dump) {
-        const size_t nb = sizeof(uint32_t) * 12 * 64 * ntiles;
+        const size_t nb = sizeof(uint32_t) * 8 * 64 * ntiles;
         uint32_t* h = (uint32_t*)malloc(nb);
         if (h && hipMemcpy(h, d_dump, nb, hipMemcpyDeviceToHost) == hipSuccess) {
             FILE* fd = fopen(dump_path, "ab");
@@ -1423,6 +1536,12 @@ extern "C" int cly_scan(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
 extern "C" hipStream_t cly_ctx_stream_internal(cly_ctx* c) { return c->stream; }
 extern "C" int cly_ctx_device_internal(cly_ctx* c) { return c->device; }
 extern "C" void** cly_ctx_merge_slot_internal(cly_ctx* c) { return &c->merge_scratch; }
+
+// Profiling build only: the phase cycle counters of the last call.
+extern "C" int cly_dbg_prof(cly_ctx* c, uint64_t* out12) {
+    for (int i = 0; i < 12; i++) out12[i] = c->h_g->prof[i];
+    return 12;
+}
 
 extern "C" const char* cly_strerror(int code) {
     switch (code) {

@@ -21,7 +21,7 @@ with Scanner(0, lib=lib) as sc:
         sc.scan(files)
     except Exception as e:
         print("scan error", e)
-d = np.fromfile(dump, np.uint32).reshape(-1, 64, 12)
+d = np.fromfile(dump, np.uint32).reshape(-1, 64, 8)
 TILE = 64 * CH
 tile0 = 0
 for fi, f in enumerate(files):
@@ -38,7 +38,7 @@ for fi, f in enumerate(files):
             if cb >= n and cb != 0: continue
             ce = min(cb + CH, n); last = cb + CH >= n
             inb = [b for b in bset if (cb <= b < ce) or (last and b == n)]
-            mode, E, x, term, cnt, sx, G, ff, m0, e0, m1, e1 = [int(v) for v in d[tile0 + tt, l]]
+            mode, E, x, term, cnt, sx, G, ff = [int(v) for v in d[tile0 + tt, l]]; m0 = e0 = m1 = e1 = -1
             dead = cb > end
             exp_mode = 2 if dead else (1 if inb else 0)
             ok = mode == exp_mode and (mode != 1 or (E == inb[0] and cnt == len([b for b in inb if b != end]) ))
