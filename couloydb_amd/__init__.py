@@ -316,6 +316,16 @@ class Scanner:
                                        out_max_files, lens, d_hint, hint_cap, ctypes.byref(r), stream)
         return rc, [int(lens[k]) for k in range(min(out_max_files, int(r.n_out_files)))], r
 
+    KERNELS = ("k_spec", "link", "k_crc", "k_fin", "k_locate", "all")
+
+    def kernel_ms(self):
+        """Per-kernel HIP-event times (ms) of the last scan_device call: k_spec,
+        the link rounds (k_link + k_fbase + repairs), k_crc, k_term + k_fin,
+        k_locate, all."""
+        k = (ctypes.c_double * 6)()
+        self.lib.cly_dbg_kernel_ms(self.ctx, k)
+        return dict(zip(self.KERNELS, list(k)))
+
     def scan_device(self, dev_files, d_out, out_cap, stream=None):
         """Device-resident path: dev_files = [(device_ptr, len, fid)], d_out =
         device pointer of out_cap tuples.  Returns (file_first, results, stats, needed)."""

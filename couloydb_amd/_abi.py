@@ -95,8 +95,7 @@ _libs = {}
 
 
 def lib_path(name="libclyscan.so"):
-    """In-package library by name; an absolute path is taken as is (tests load
-    the CPU emulator tests/emu/libclyscan_emu*.so this way)."""
+    """In-package library by name; an absolute path is taken as is."""
     return name if os.path.isabs(name) else os.path.join(PKG_DIR, name)
 
 
@@ -113,6 +112,9 @@ def load_scan_lib(name="libclyscan.so"):
     lib.cly_ctx_create.restype = ctypes.c_int
     lib.cly_ctx_destroy.argtypes = [ctypes.c_void_p]
     lib.cly_ctx_destroy.restype = None
+    if hasattr(lib, "cly_dbg_kernel_ms"):
+        lib.cly_dbg_kernel_ms.argtypes = [ctypes.c_void_p, P(ctypes.c_double)]
+        lib.cly_dbg_kernel_ms.restype = ctypes.c_int
     lib.cly_scan_capacity.argtypes = [P(ClyFile), ctypes.c_int]
     lib.cly_scan_capacity.restype = ctypes.c_uint64
     lib.cly_scan.argtypes = [ctypes.c_void_p, P(ClyFile), ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,

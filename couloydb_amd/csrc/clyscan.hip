@@ -12,22 +12,26 @@
 // Layout: every file is cut into chunks of CLY_CH bytes, one
 // per lane; 64 consecutive chunks of a file are a tile, one per wave.
 //
-// k_scan (persistent, tiles in ticket order), per tile:
-//   A  each lane finds the first record start of its chunk (SWAR candidate
-//      filter over its bytes, then a walk of header gathers that must leave the
-//      chunk at a plausible header), and walks its records to the chunk end;
-//      the wave makes the lanes' chains agree (lane l+1 starts where lane l's
-//      chain leaves), re-walking exactly where they do not;
-//   L  decoupled look-back over tile descriptors: the chain state and record
-//      count entering the tile; a tile whose guessed entry is wrong re-resolves;
-//   C  every lane streams its chunk through a slicing-by-4 CRC register from
-//      HBM (16-B loads, 128 B per burst), re-walks its records, writes their
-//      tuples straight to their output slots and XORs one combined patch per
-//      record into the stream, so that the register of the whole file ends at
-//      zero iff every record's CRC matches; the tile's register is folded
-//      in-wave.
-// k_fin (one workgroup per file): folds the tile registers of the file and
-// checks it; k_locate (only when a file fails) finds the first bad record.
+// One call, all on one stream, no inter-workgroup waiting inside a kernel:
+//   k_spec   per tile: each lane finds the first record start of its chunk
+//            (SWAR candidate filter, then a walk of header gathers that must
+//            leave the chunk at a plausible header) and walks its records to
+//            the chunk end; the wave makes the lanes' chains agree under the
+//            tile's own guess of its entry; lane chains + the tile's LOCAL out;
+//   k_link   per file: the chain state entering every tile (record count,
+//            position, the record open at the tile start) from the LOCALs;
+//            tiles whose guess the state contradicts are listed;
+//   k_refix  (only for listed tiles) re-resolves them from the true entry,
+//            then k_link again;
+//   k_fbase  tuple index of each file's first record;
+//   k_crc    per tile: every lane streams its chunk through a slicing-by-4 CRC
+//            register (16-B loads, 128 B per burst) while a walker decodes its
+//            records one gather ahead, writes their tuples straight to their
+//            output slots and adds one shifted patch per record to the lane's
+//            register, so that the register of the whole file ends at zero iff
+//            every record's CRC matches; the tile's register is folded in-wave;
+//   k_fin    per file: folds the tile registers and checks them;
+//   k_locate (only when a file fails) finds the first bad record exactly.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -83,19 +87,15 @@ struct FileInfo {                // per file, zeroed per call (fail_key: all one
     uint32_t ok;                 // k_fin: fold == expect
 };
 
-// Tile descriptor: LOCAL (from the tile's own speculation) and INCL (the true
-// state after the tile), each published by its flag word, written last.
-struct TileDesc { u64 l[4]; u64 i[4]; };
-// l[0]: bit0 published | bit1 the chain ends in the tile | bit2 no chunk of the tile
-//       holds a boundary | bit3 first tile of its file | bit4 a record starts in the
+// Tile LOCAL (from the tile's own speculation), written by k_spec / k_refix:
+// l[0]: bit1 the chain ends in the tile | bit2 no chunk of the tile holds a
+//       boundary | bit3 first tile of its file | bit4 a record starts in the
 //       tile | records << 32
 // l[1]: G (the tile's guessed entry: its first boundary) | exit or terminal position << 32
 // l[2]: crc_last | P_last << 32 (last record start in the tile and its stored CRC)
 // l[3]: the smallest entry that passes the whole tile (tile end, or len + 1 for
 //       the tile holding the file's end)
-// i[0]: bit0 published | bit1 the file's chain ended | records before the next tile << 16
-// i[1]: X (chain position after the tile) | crc_last << 32
-// i[2]: P_last (start of the last record before the next tile, NONE32 if none)
+struct TileLocal { u64 l[4]; };
 #define DF_PUB 1ull
 #define DF_TERM 2ull
 #define DF_NONE 4ull
@@ -103,42 +103,29 @@ struct TileDesc { u64 l[4]; u64 i[4]; };
 #define DF_REC 16ull
 
 struct Globals {                 // zeroed per call
-    uint32_t ticket;
+    uint32_t nfix;               // tiles listed by k_link for k_refix (reset per link round)
     uint32_t overflow;           // tuples beyond out_cap were dropped
-    uint32_t fail;               // internal invariant / spin bound (never expected)
-    uint32_t refix;              // tiles whose guessed entry the look-back corrected
-    uint32_t slow_lanes;         // lanes that took the exact (slow) CRC path
+    uint32_t fail;               // internal invariant (never expected)
+    uint32_t refix;              // tiles re-resolved over all rounds
+    uint32_t rounds;             // link rounds
     uint32_t any_fail;           // a file's CRC fold failed (k_locate needed)
     uint64_t total;              // records over all files
-    uint64_t prof[12];           // profiling build (-DCLY_PROF): cycles per phase, summed over tiles; look-back counters
 };
-#ifdef CLY_PROF
-#define PROF_T0() uint64_t prof_t = __builtin_amdgcn_s_memtime()
-#define PROF(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long*)&g->prof[i], (unsigned long long)(t_ - prof_t)); prof_t = t_; } while (0)
-#else
-#define PROF_T0()
-#define PROF(i)
-#endif
-#ifdef CLY_PROF
-#define PCNT(i, n) do { if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long*)&g->prof[i], (unsigned long long)(n)); } while (0)
-#else
-#define PCNT(i, n)
-#endif
-
 // ---------------------------------------------------------------------------
-// LDS of k_scan / k_locate (static: compile-time offsets)
+// LDS of k_crc / k_locate (static: compile-time offsets)
 //   [0, 65536)     CRC slicing-by-4 tables T0..T3, 16 replicas: dword (i*64 + t*16 + r)
 //   [65536, +256)  inverse of a zero-byte step (top byte of T0 -> index)
-//   [65792, ...)   nibble tables of A^(CLY_CH * 2^k), k < 7 (8 x 16 words each)
+//   LDS_NIB        nibble tables of A^(CLY_CH * 2^k), k < 7 (8 x 16 words each)
+//   LDS_SH         nibble tables of A^(4 m), m < 16, then of A^(64 m), m <= CLY_NW / 16
 #define LDS_INV 65536
 #define LDS_NIB (LDS_INV + 256)
 #define NIB_LEVELS 7                     // A^(CLY_CH * 2^k), k < 7 (k = 6: one tile)
-#define EVQ 10                   // events per lane in the LDS ring of phase C
-#define LDS_EVQ (LDS_NIB + NIB_LEVELS * 128 * 4)          // event rings: [wave][EVQ][64 lanes] x 8 B
-#define SCAN_WAVES 16
-#define SCAN_LDS (LDS_EVQ + SCAN_WAVES * EVQ * 64 * 8)
+#define NSH (16 + CLY_NW / 16 + 1)       // shift tables
+#define LDS_SH (LDS_NIB + NIB_LEVELS * 128 * 4)
+#define NTAB ((NIB_LEVELS + NSH) * 128)  // words of nibble tables (copied from the context's buffer)
+#define SCAN_LDS (LDS_SH + NSH * 128 * 4)
 
-__device__ __forceinline__ void init_tables(CLY_LDS uint8_t* smem, const uint32_t* __restrict__ nib) {
+__device__ __forceinline__ void init_tables(CLY_LDS uint8_t* smem, const uint32_t* __restrict__ nib, int ntab = NTAB) {
     for (int i = threadIdx.x; i < 256; i += blockDim.x) {
         uint32_t cv = i;
         for (int k = 0; k < 8; k++) cv = (cv & 1) ? (cv >> 1) ^ CLY_POLY : cv >> 1;
@@ -150,7 +137,7 @@ __device__ __forceinline__ void init_tables(CLY_LDS uint8_t* smem, const uint32_
             cv = (cv >> 8) ^ tl;
         }
     }
-    for (int i = threadIdx.x; i < NIB_LEVELS * 128; i += blockDim.x) ((CLY_LDS uint32_t*)(smem + LDS_NIB))[i] = nib[i];
+    for (int i = threadIdx.x; i < ntab; i += blockDim.x) ((CLY_LDS uint32_t*)(smem + LDS_NIB))[i] = nib[i];
     __syncthreads();
 }
 
@@ -238,8 +225,8 @@ __device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t s)
 __device__ __forceinline__ uint32_t pack7(uint32_t s) {
     return (s & 0x7fu) | ((s >> 1) & 0x3f80u) | ((s >> 2) & 0x1fc000u) | ((s >> 3) & 0xfe00000u);
 }
-__device__ __noinline__ void hdr_slow(gbytes base, uint32_t p, uint64_t len, Hdr& h) {
-    h = step_hdr(base, (int64_t)p, (int64_t)len, (int64_t)p);
+__device__ __noinline__ Hdr hdr_slow(gbytes base, uint32_t p, uint64_t len) {
+    return step_hdr(base, (int64_t)p, (int64_t)len, (int64_t)p);
 }
 // header bytes 0..15 at p from a gather
 __device__ __forceinline__ bool hdr_fast(const Gath& g, uint32_t p, uint64_t len, Hdr& h) {
@@ -286,8 +273,7 @@ __device__ __forceinline__ bool hdr_fast(const Gath& g, uint32_t p, uint64_t len
 __device__ __forceinline__ Hdr hdr_at(gbytes base, uint32_t p, uint64_t len, const Gath& g) {
     Hdr h;
     if (gath_ok(p, len) && hdr_fast(g, p, len, h)) return h;
-    hdr_slow(base, p, len, h);
-    return h;
+    return hdr_slow(base, p, len);
 }
 __device__ __forceinline__ Hdr hdr_load(gbytes base, uint32_t p, uint64_t len) {
     Gath g;
@@ -380,7 +366,7 @@ __device__ __forceinline__ u32x4 piece(const Chunk& K, uint32_t o) {
 }
 
 // Phase A for one lane: the chain of its chunk under its own guess.
-__device__ __noinline__ LaneChain phase_a(const Chunk K) {
+__device__ __forceinline__ LaneChain phase_a(const Chunk K) {
     LaneChain L;
     if (!K.on) { chain_set(L, LM_OFF); return L; }
     if (K.cb == 0) { walk(K, 0, true, L); return L; }
@@ -453,7 +439,7 @@ __device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src) { return (uint
 // chunk before it leaves (the tile's entry X0 for the first lanes; dead0: the
 // file's chain ended before the tile).  The lowest disagreeing lane is
 // re-walked exactly, until every lane agrees.
-__device__ __noinline__ LaneChain resolve(const Chunk K, LaneChain L, int lane, uint32_t X0, bool dead0, Globals* g) {
+__device__ __forceinline__ LaneChain resolve(const Chunk K, LaneChain L, int lane, uint32_t X0, bool dead0, Globals* g) {
     for (int iter = 0;; iter++) {
         const bool isC = L.mode == LM_CHAIN;
         const int pk = scan_max_incl(isC ? lane : -1, lane);
@@ -483,175 +469,85 @@ __device__ __noinline__ LaneChain resolve(const Chunk K, LaneChain L, int lane, 
 }
 
 // ---------------------------------------------------------------------------
-// Look-back: the chain state and record count entering a tile.
+// ---------------------------------------------------------------------------
+// Chain state between tiles (k_link) and the per-lane chains (k_spec -> k_crc).
 struct LBState {
-    uint64_t count;              // records of all tiles before
+    uint64_t count;              // records before (file-relative in TileIn, absolute in k_crc)
     uint32_t X;                  // chain position
     uint32_t crc_last;           // stored CRC of the last record started before (its successor's Q)
     uint32_t P_last;             // that record's start (NONE32: none in this file)
     int      dead;               // the file's chain has ended
 };
-__device__ __forceinline__ u64 ld_agent(const u64* p) {
-    return __hip_atomic_load((const CLY_GL u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(u64* p, u64 v) {
-    __hip_atomic_store((CLY_GL u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-#define SPIN_MAX (1u << 18)
-
-__device__ __forceinline__ LBState lb_virtual() {
+// TileIn (k_link): the true state entering a tile, 32 B:
+//   w[0..1] count (file-relative), w[2] X, w[3] dead | fix << 1, w[4] crc_last, w[5] P_last
+struct TileIn { uint32_t w[8]; };
+#define TI_DEAD 1u
+#define TI_FIX 2u
+__device__ __forceinline__ LBState ti_load(const TileIn* p) {
+    const u32x4 a = ((const u32x4*)p)[0], b = ((const u32x4*)p)[1];
     LBState s;
-    s.count = 0; s.X = 0; s.crc_last = 0; s.P_last = NONE32; s.dead = 1;
+    s.count = ((uint64_t)a.y << 32) | a.x; s.X = a.z; s.dead = (a.w & TI_DEAD) != 0; s.crc_last = b.x; s.P_last = b.y;
     return s;
 }
-__device__ __forceinline__ LBState lb_incl(u64 i0, u64 i1, u64 i2) {
-    LBState s;
-    s.dead = (i0 & DF_TERM) != 0;
-    s.count = i0 >> 16;
-    s.X = (uint32_t)i1; s.crc_last = (uint32_t)(i1 >> 32);
-    s.P_last = (uint32_t)i2;
-    return s;
-}
-// State after tile u given the state before it and u's LOCAL; false when the
-// tile's guess disagrees with the state (then only its INCL can tell).
-__device__ __forceinline__ bool lb_local(LBState& s, u64 l0, u64 l1, u64 l2, u64 l3) {
-    if (!(l0 & DF_FOF)) {
-        if (s.dead) return true;                                    // nothing of the file after its end
-        if (l0 & DF_NONE) return s.X >= (uint32_t)l3;              // the chain passes the tile
-        if (s.X != (uint32_t)l1) return false;
-    }
-    s.count += l0 >> 32;
-    s.dead = (l0 & DF_TERM) != 0;
-    s.X = (uint32_t)(l1 >> 32);
-    if (l0 & DF_REC) { s.crc_last = (uint32_t)l2; s.P_last = (uint32_t)(l2 >> 32); }
-    else if (l0 & DF_FOF) { s.crc_last = 0; s.P_last = NONE32; }
-    return true;
-}
-__device__ __forceinline__ u64 shfl64(u64 v, int src) {
-    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
-    return ((u64)hi << 32) | lo;
-}
-__device__ __forceinline__ void bad_spin(Globals* g, uint32_t code) { atomicOr(&g->fail, code); }
-
-__device__ __forceinline__ int scan_max_excl(int v, int lane);
-
-// Look-back of tile t: the nearest published INCL before it, then the
-// LOCALs after it composed 64 tiles (one per lane) at a time.  Within a
-// window the chain position entering tile m is the exit of the nearest tile
-// before it that has a chain (or the window's entering state), "ended" is set
-// by the nearest tile whose chain terminates and cleared by the first tile of
-// a file; a tile whose guess disagrees with the position it is entered at
-// stops the window: its own INCL (published once it has re-resolved) is
-// awaited and the window goes on after it.
-__device__ __noinline__ LBState look_back(const TileDesc* desc, int64_t t, int lane, Globals* g) {
-    int64_t k = -1;
-    for (int64_t base = t - 1; base >= 0; base -= 64) {
-        const int64_t u = base - lane;
-        const bool pub = u >= 0 && (ld_agent(&desc[u].i[0]) & DF_PUB);
-        const u64 bm = __ballot(pub);
-        PCNT(6, 1);
-        if (bm) { k = base - (__ffsll((long long)bm) - 1); break; }
-    }
-    LBState s = lb_virtual();
-    if (k >= 0) s = lb_incl(ld_agent(&desc[k].i[0]), ld_agent(&desc[k].i[1]), ld_agent(&desc[k].i[2]));
-    for (int64_t u0 = k + 1; u0 < t; u0 += 64) {
-        const int64_t u = u0 + lane;
-        const int n = t - u0 < 64 ? (int)(t - u0) : 64;
-        int got = lane < n ? 0 : 3;                    // 1 LOCAL, 2 INCL
-        u64 w0 = 0;
-        for (uint32_t spin = 0;; spin++) {
-            if (got == 0) {
-                const u64 i0 = ld_agent(&desc[u].i[0]);
-                if (i0 & DF_PUB) { got = 2; w0 = i0; }
-                else {
-                    const u64 l0 = ld_agent(&desc[u].l[0]);
-                    if (l0 & DF_PUB) { got = 1; w0 = l0; }
-                }
-            }
-            if (__ballot(got == 0) == 0) break;
-            PCNT(8, 1);
-            if (spin > SPIN_MAX) { if (lane == 0) bad_spin(g, 2u); return s; }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        PCNT(7, 1);
-        u64 w1 = 0, w2 = 0, w3 = 0;
-        if (got == 2) { w1 = ld_agent(&desc[u].i[1]); w2 = ld_agent(&desc[u].i[2]); }
-        else if (got == 1) { w1 = ld_agent(&desc[u].l[1]); w2 = ld_agent(&desc[u].l[2]); w3 = ld_agent(&desc[u].l[3]); }
-        int m_lo = 0;
-        for (int round = 0;; round++) {
-            // the last INCL at or after m_lo overrides everything before it
-            const u64 bi = __ballot(got == 2 && lane >= m_lo);
-            if (bi) {
-                const int mi = 63 - __clzll((long long)bi);
-                s = lb_incl(shfl64(w0, mi), shfl64(w1, mi), shfl64(w2, mi));
-                m_lo = mi + 1;
-            }
-            if (m_lo >= n) break;
-            const bool act = lane >= m_lo && lane < n;
-            const bool fof = act && (w0 & DF_FOF);
-            const bool none = act && !fof && (w0 & DF_NONE);
-            const bool chain = act && !none;
-            const bool term = chain && (w0 & DF_TERM);
-            const uint32_t G = (uint32_t)w1, Xo = (uint32_t)(w1 >> 32), tend = (uint32_t)w3;
-            // entering state of each lane
-            const int e = scan_max_excl((term || fof) ? lane : -1, lane);
-            const int j = scan_max_excl(chain ? lane : -1, lane);
-            const int te = __shfl((int)term, e < 0 ? 0 : e, 64);
-            const uint32_t xj = shfl_u32(Xo, j < 0 ? 0 : j);
-            const bool din = e >= 0 ? te != 0 : s.dead != 0;
-            const uint32_t Xin = j >= 0 ? xj : s.X;
-            const bool valid = !act || fof || din || (none ? Xin >= tend : Xin == G);
-            const u64 bad = __ballot(!valid);
-            const int ne = bad ? __ffsll((long long)bad) - 1 : n;      // lanes [m_lo, ne) compose
-            const bool in = act && lane < ne;
-            const bool applied = in && chain && (fof || !din);
-            const bool rec = applied && (fof || (w0 & DF_REC));
-            // state after each composed lane (inclusive scans)
-            const uint32_t cnt = applied ? (uint32_t)(w0 >> 32) : 0u;
-            const uint32_t ci = scan_add_incl(cnt, lane);
-            const int ei = scan_max_incl(in && (term || fof) ? lane : -1, lane);
-            const int ji = scan_max_incl(in && chain ? lane : -1, lane);
-            const int ri = scan_max_incl(rec ? lane : -1, lane);
-            const int tei = __shfl((int)term, ei < 0 ? 0 : ei, 64);
-            const uint32_t xji = shfl_u32(Xo, ji < 0 ? 0 : ji);
-            const u64 w0r = shfl64(w0, ri < 0 ? 0 : ri), w2r = shfl64(w2, ri < 0 ? 0 : ri);
-            LBState o = s;
-            o.count = s.count + ci;
-            if (ei >= 0) o.dead = tei != 0;
-            if (ji >= 0) o.X = xji;
-            if (ri >= 0) {
-                if (w0r & DF_REC) { o.crc_last = (uint32_t)w2r; o.P_last = (uint32_t)(w2r >> 32); }
-                else { o.crc_last = 0; o.P_last = NONE32; }
-            }
-            const int last = ne - 1;
-            if (last >= m_lo) {
-                s.count = shfl64(o.count, last);
-                s.X = shfl_u32(o.X, last);
-                s.dead = __shfl(o.dead, last, 64);
-                s.crc_last = shfl_u32(o.crc_last, last);
-                s.P_last = shfl_u32(o.P_last, last);
-            }
-            if (!bad) break;
-            // the tile at ne guessed wrong: wait for its true state
-            const TileDesc* d = &desc[u0 + ne];
-            u64 i0 = 0;
-            PCNT(9, 1);
-            for (uint32_t spin = 0;; spin++) {
-                i0 = ld_agent(&d->i[0]);
-                if (i0 & DF_PUB) break;
-                PCNT(10, 1);
-                if (spin > SPIN_MAX) { if (lane == 0) bad_spin(g, 4u); return s; }
-                __builtin_amdgcn_s_sleep(2);
-            }
-            s = lb_incl(i0, ld_agent(&d->i[1]), ld_agent(&d->i[2]));
-            m_lo = ne + 1;
-            if (m_lo >= n) break;
-        }
-    }
-    return s;
+__device__ __forceinline__ void ti_store(TileIn* p, const LBState& s, bool fix) {
+    ((u32x4*)p)[0] = (u32x4){(uint32_t)s.count, (uint32_t)(s.count >> 32), s.X, (s.dead ? TI_DEAD : 0u) | (fix ? TI_FIX : 0u)};
+    ((u32x4*)p)[1] = (u32x4){s.crc_last, s.P_last, 0u, 0u};
 }
 
-// ---------------------------------------------------------------------------
+// Per-lane chains (structure of arrays over all lanes of the call, nl = 64 * ntiles):
+//   lanes[0*nl + i] mode | term << 8 | cnt << 16,  [1] E,  [2] x,  [3] last,  [4] last_crc
+#define LANE_WORDS 5
+__device__ __forceinline__ void lane_store(uint32_t* lanes, uint64_t nl, uint64_t i, const LaneChain& L) {
+    lanes[i] = (uint32_t)(L.mode & 0xff) | ((uint32_t)(L.term & 0xff) << 8) | (L.cnt << 16);
+    lanes[nl + i] = L.E;
+    lanes[2 * nl + i] = L.x;
+    lanes[3 * nl + i] = L.last;
+    lanes[4 * nl + i] = L.last_crc;
+}
+__device__ __forceinline__ LaneChain lane_load(const uint32_t* __restrict__ lanes, uint64_t nl, uint64_t i) {
+    LaneChain L;
+    const uint32_t m = lanes[i];
+    L.mode = (int)(m & 0xff);
+    L.term = (int)(int8_t)((m >> 8) & 0xff);
+    L.cnt = m >> 16;
+    L.E = lanes[nl + i];
+    L.x = lanes[2 * nl + i];
+    L.last = lanes[3 * nl + i];
+    L.last_crc = lanes[4 * nl + i];
+    L.prev_crc = 0;
+    L.minsz = 0xFFFFFFFFu;
+    return L;
+}
+
+// The tile's LOCAL (its chain under its own entry): flags | records << 32,
+// G | X << 32, crc_last | P_last << 32, tend.  Written by k_spec / k_refix.
+__device__ __forceinline__ void local_store(TileLocal* d, const LaneChain& L, uint32_t G, bool fof, uint32_t tt,
+                                            uint64_t flen, int lane) {
+    const u64 bc = __ballot(L.mode == LM_CHAIN), br = __ballot(L.mode == LM_CHAIN && L.cnt > 0);
+    const uint32_t c = L.mode == LM_CHAIN ? L.cnt : 0u;
+    const uint32_t tile_cnt = shfl_u32(scan_add_incl(c, lane), 63);
+    const int lc = bc ? 63 - __clzll((long long)bc) : 0, lr = br ? 63 - __clzll((long long)br) : 0;
+    const uint32_t X = shfl_u32(L.x, lc);
+    const int term = __shfl(L.term, lc, 64);
+    const uint32_t crc = shfl_u32(L.last_crc, lr), Pl = shfl_u32(L.last, lr);
+    const u64 bg = __ballot(L.mode == LM_CHAIN);
+    const uint32_t Gl = bg ? shfl_u32(L.E, __ffsll((long long)bg) - 1) : NONE32;
+    (void)G;
+    if (lane == 0) {
+        const uint64_t tstart = (uint64_t)tt * CLY_TILE;
+        const uint32_t tend = tstart + CLY_TILE >= flen ? (uint32_t)(flen + 1) : (uint32_t)(tstart + CLY_TILE);
+        u64 f0 = (u64)tile_cnt << 32;
+        if (bc && term != TERM_NONE) f0 |= DF_TERM;
+        if (!bc) f0 |= DF_NONE;
+        if (fof) f0 |= DF_FOF;
+        if (br) f0 |= DF_REC;
+        d->l[0] = f0;
+        d->l[1] = (u64)Gl | ((u64)X << 32);
+        d->l[2] = (u64)crc | ((u64)Pl << 32);
+        d->l[3] = (u64)tend;
+    }
+}
+
 // Inputs of phase C for one lane (after the tile's chain is final).
 struct LaneIn {
     uint64_t base;               // global tuple index of the lane's first record
@@ -708,86 +604,91 @@ __device__ __forceinline__ void put_tuple(gtuples out, uint64_t idx, uint64_t ou
 }
 
 // ---------------------------------------------------------------------------
-// Phase C, uniform path.  Each record start P has one combined patch delta'
-// on one word of the stream (patch_part); the walker decodes the lane's
-// records (tuples written as it goes) and queues (word, delta') events in a
-// per-lane LDS ring, ahead of the stream.  Per 128-B burst the stream loads
-// the lane's 32 words, XORs in the burst's events, and runs the register
-// through them: the loop body is the plain slicing-by-4 step.
+// ---------------------------------------------------------------------------
+// Phase C (k_crc), uniform path.  The lane streams its chunk through the CRC
+// register raw, in 128-B bursts: the loop body is the plain slicing-by-4 step.
+// Each record start P changes the stream by one combined patch delta' on one
+// word w of the chunk (patch_part); XORing delta' into word w changes the
+// register at the chunk end by A^(4 (NW - w)) delta', which the walker adds to
+// `pacc` (two nibble-table products, shift_words), so the stream itself never
+// sees the records.  The walker decodes the lane's records one gather ahead,
+// a record per burst at most, and writes their tuples.
+__device__ __forceinline__ uint32_t mat_mul(const CLY_LDS uint32_t* t, uint32_t v) {
+    uint32_t p = 0;
+    #pragma unroll
+    for (int n = 0; n < 8; n++) p ^= t[n * 16 + ((v >> (4 * n)) & 15u)];
+    return p;
+}
+// A^(4 m) v, 1 <= m <= CLY_NW
+__device__ __forceinline__ uint32_t shift_words(const CLY_LDS uint8_t* smem, uint32_t m, uint32_t v) {
+    const CLY_LDS uint32_t* t = (const CLY_LDS uint32_t*)(smem + LDS_SH);
+    v = mat_mul(t + (m & 15u) * 128, v);
+    return mat_mul(t + (16u + (m >> 4)) * 128, v);
+}
 struct Walker {
     uint32_t p, cq, i;
     Gath gt;
 };
 __device__ __forceinline__ void walker_step(const Chunk& K, Walker& W, uint32_t nrec, uint64_t base, uint32_t fid,
                                             gtuples out, uint64_t out_cap, const CLY_LDS uint8_t* smem,
-                                            const CrcLane& cl, uint32_t& w, uint32_t& d, Globals* g) {
+                                            const CrcLane& cl, uint32_t& pacc, Globals* g) {
     const Hdr h = hdr_at(K.base, W.p, K.len, W.gt);
     put_tuple(out, base + W.i, out_cap, K, W.p, h, fid, g);
     const uint32_t wlo = K.cb >> 2;
+    uint32_t d;
     const uint32_t wa = patch_part(smem, cl, W.p, h.crc, W.cq, wlo, wlo + CLY_NW, d);
-    w = wa == NONE32 ? NONE32 : wa - wlo;
+    if (wa != NONE32) pacc ^= shift_words(smem, CLY_NW - (wa - wlo), d);
     W.cq = h.crc;
     W.p += (uint32_t)h.size;
     W.i++;
     if (W.i < nrec && gath_ok(W.p, K.len)) gath_issue(K.base, W.p, W.gt);
 }
 
-__device__ __noinline__ uint32_t phase_c_fast(const Chunk K, const LaneChain L, const LaneIn I, bool active, uint32_t fid,
-                                              gtuples out, uint64_t out_cap, const CLY_LDS uint8_t* smem,
-                                              CLY_LDS u32x2* evq, const CrcLane cl, Globals* g) {
-    // ring slot k of this lane: evq[k * 64]  (evq points at the wave's ring + lane)
-    uint32_t head = 0, tail = 0;
+__device__ __forceinline__ uint32_t phase_c_fast(const Chunk& K, const LaneChain& L, const LaneIn& I, bool active,
+                                                 uint32_t fid, gtuples out, uint64_t out_cap,
+                                                 const CLY_LDS uint8_t* smem, const CrcLane& cl, Globals* g) {
     const uint32_t wlo = K.cb >> 2;
+    uint32_t pacc = 0;
     if (active && I.spill) {
         uint32_t d;
         const uint32_t w = patch_part(smem, cl, I.P_in, I.crc_in, 0u, wlo, wlo + CLY_NW, d);
-        if (w != NONE32) { evq[0] = (u32x2){w - wlo, d}; tail = 1; }
+        if (w != NONE32) pacc = shift_words(smem, CLY_NW - (w - wlo), d);
     }
     Walker W;
     W.p = L.E; W.cq = I.crc_in; W.i = 0;
+#ifdef CLY_XNOWALK
+    const uint32_t nrec = 0;                 // timing experiment: no walker
+#else
     const uint32_t nrec = (active && L.mode == LM_CHAIN) ? L.cnt : 0u;
+#endif
     if (nrec && gath_ok(W.p, K.len)) gath_issue(K.base, W.p, W.gt);
-    // next event in registers
-    uint32_t nw = NONE32, nd = 0;
     uint32_t s = 0;
     const CLY_GL u32x4* src = (const CLY_GL u32x4*)(K.base + K.cb);
+    const bool full = (uint64_t)K.cb + CLY_CH <= K.len;
     #pragma unroll 1
     for (int b = 0; b < CLY_NB; b++) {
-        const uint32_t bend = (uint32_t)(b + 1) * CLY_BW;
-        // walker ahead: every event of this and the next burst queued (ring permitting)
-        for (;;) {
-            const bool need = W.i < nrec && tail - head < EVQ && ((W.p >> 2) - wlo) < bend + CLY_BW;
-            if (!__ballot(need)) break;
-            if (need) {
-                uint32_t w, d;
-                walker_step(K, W, nrec, I.base, fid, out, out_cap, smem, cl, w, d, g);
-                if (w != NONE32) { evq[(tail % EVQ) * 64] = (u32x2){w, d}; tail++; }
-            }
-        }
-        if (nw == NONE32 && head != tail) { const u32x2 e = evq[(head % EVQ) * 64]; nw = e.x; nd = e.y; head++; }
         u32x4 v[CLY_BW / 4];
-        if (active) {
+        if (active && full) {
             #pragma unroll
             for (int k = 0; k < CLY_BW / 4; k++) v[k] = src[b * (CLY_BW / 4) + k];
+        } else if (active) {
+            #pragma unroll
+            for (int k = 0; k < CLY_BW / 4; k++) v[k] = piece(K, (uint32_t)(b * CLY_BW * 4 + 16 * k));
         } else {
             #pragma unroll
             for (int k = 0; k < CLY_BW / 4; k++) v[k] = (u32x4){0u, 0u, 0u, 0u};
         }
-        // the burst's events into its words
-        while (__ballot(nw < bend)) {
-            if (nw < bend) {
-                const uint32_t r = nw - (uint32_t)b * CLY_BW;
-                #pragma unroll
-                for (int k = 0; k < CLY_BW / 4; k++) {
-                    v[k].x ^= r == 4u * k ? nd : 0u;
-                    v[k].y ^= r == 4u * k + 1 ? nd : 0u;
-                    v[k].z ^= r == 4u * k + 2 ? nd : 0u;
-                    v[k].w ^= r == 4u * k + 3 ? nd : 0u;
-                }
-                nw = NONE32;
-                if (head != tail) { const u32x2 e = evq[(head % EVQ) * 64]; nw = e.x; nd = e.y; head++; }
-            }
+        // the records that start in this burst
+        const uint32_t bend = wlo + (uint32_t)(b + 1) * CLY_BW;
+        for (;;) {
+            const bool need = W.i < nrec && (W.p >> 2) < bend;
+            if (!__ballot(need)) break;
+            if (need) walker_step(K, W, nrec, I.base, fid, out, out_cap, smem, cl, pacc, g);
         }
+#ifdef CLY_XNOCRC
+        #pragma unroll
+        for (int k = 0; k < CLY_BW / 4; k++) s = s ^ v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;   // timing experiment
+#else
         #pragma unroll
         for (int k = 0; k < CLY_BW / 4; k++) {
             s = crc_word(smem, s ^ v[k].x, cl);
@@ -795,8 +696,9 @@ __device__ __noinline__ uint32_t phase_c_fast(const Chunk K, const LaneChain L, 
             s = crc_word(smem, s ^ v[k].z, cl);
             s = crc_word(smem, s ^ v[k].w, cl);
         }
+#endif
     }
-    return s;
+    return s ^ pacc;
 }
 
 // ---------------------------------------------------------------------------
@@ -806,15 +708,38 @@ __device__ __noinline__ uint32_t phase_c_fast(const Chunk K, const LaneChain L, 
 // from register s0.  With `observe`, the first record whose check fails
 // (register after its end word != 0) is returned in fail_P / fail_i.
 struct Bnd { uint32_t P, c, q, start; uint64_t idx; int term; };
-__device__ __noinline__ uint32_t exact_lane(const Chunk& K, const LaneChain& L, const LaneIn& I, uint32_t s0, bool emit,
+// Boundaries of exact_lane.  A record start P patches bytes [P, P+8) and a
+// record is at least 6 bytes (headerSize >= 6 for a decoded record), so at
+// most two record starts touch one word: two named slots (the older one drops
+// out when a third is pushed) plus one for the terminal; no array, so no
+// dynamic indexing and no scratch memory.
+__device__ __forceinline__ uint32_t bnd_patch(const Bnd& b, uint32_t A, uint32_t d) {
+    uint32_t patch = 0;
+    #pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t x = A + i;
+        uint32_t m = 0;
+        if (!b.term && x >= b.P && x < b.P + 4) m = (d >> (8 * i)) & 0xffu;          // stored CRC zeroed
+        if (!b.term && x >= b.P + 4 && x < b.P + 8) m ^= 0xffu;                     // init 0xFF
+        patch ^= m << (8 * i);
+    }
+    if ((b.P >> 2) == (A >> 2)) patch ^= b.q;
+    return patch;
+}
+__device__ __forceinline__ bool bnd_fails(const Bnd& b, uint32_t A, uint32_t s) {
+    return (b.P >> 2) == (A >> 2) && b.P != 0 && b.start != NONE32 && s != 0;
+}
+__device__ __forceinline__ uint32_t exact_lane(const Chunk& K, const LaneChain& L, const LaneIn& I, uint32_t s0, bool emit,
                                bool observe, uint32_t fid, gtuples out, uint64_t out_cap,
                                const CLY_LDS uint8_t* smem, const CrcLane& cl, Globals* g, uint32_t& fail_P,
-                               uint64_t& fail_i, uint32_t& expect) {
+                               uint64_t& fail_i, uint32_t& expect, const CLY_LDS uint32_t* wl = nullptr) {
     uint32_t s = s0;
     fail_P = NONE32; fail_i = 0; expect = 0;
-    Bnd bq[4];
-    int nb = 0;
-    if (I.spill) { bq[0].P = I.P_in; bq[0].c = I.crc_in; bq[0].q = 0; bq[0].term = 0; bq[0].start = NONE32; bq[0].idx = 0; nb = 1; }
+    Bnd rA, rB, tT;
+    bool vA = false, vB = false, vT = false;
+    rA.P = rB.P = tT.P = 0; rA.c = rB.c = tT.c = 0; rA.q = rB.q = tT.q = 0; rA.term = rB.term = 0; tT.term = 1;
+    rA.start = rB.start = tT.start = NONE32; rA.idx = rB.idx = tT.idx = 0;
+    if (I.spill) { rB.P = I.P_in; rB.c = I.crc_in; rB.q = 0; rB.start = NONE32; rB.idx = 0; vB = true; }
     const uint32_t T = (L.mode == LM_CHAIN && L.term != TERM_NONE) ? L.x : NONE32;
     uint32_t wp = L.E, cq = I.crc_in, wi = 0, start = I.P_in;
     uint64_t sidx = I.base - 1;
@@ -822,22 +747,21 @@ __device__ __noinline__ uint32_t exact_lane(const Chunk& K, const LaneChain& L, 
     bool tpushed = T == NONE32;
     for (uint32_t w = 0; w < CLY_NW; w++) {
         const uint32_t A = K.cb + 4 * w;
-        // queue the boundaries whose first patch word is this one
+        // the boundaries whose first patch word is this one
         for (;;) {
-            if (wi < nrec && (wp >> 2) == (A >> 2) && nb < 4) {
+            if (wi < nrec && (wp >> 2) == (A >> 2)) {
                 const Hdr h = hdr_load(K.base, wp, K.len);
                 if (emit) put_tuple(out, I.base + wi, out_cap, K, wp, h, fid, g);
-                Bnd& b = bq[nb++];
-                b.P = wp; b.c = h.crc; b.q = wp != 0 ? q_of(smem, cq, wp & 3, cl.r4) : 0u; b.term = 0;
-                b.start = start; b.idx = sidx;
+                rA = rB; vA = vB;
+                rB.P = wp; rB.c = h.crc; rB.q = wp != 0 ? q_of(smem, cq, wp & 3, cl.r4) : 0u;
+                rB.start = start; rB.idx = sidx; vB = true;
                 start = wp; sidx = I.base + wi;
                 cq = h.crc; wp += (uint32_t)h.size; wi++;
                 continue;
             }
-            if (!tpushed && wi >= nrec && (T >> 2) == (A >> 2) && nb < 4) {
-                Bnd& b = bq[nb++];
-                b.P = T; b.c = 0; b.q = T != 0 ? q_of(smem, cq, T & 3, cl.r4) : 0u; b.term = 1;
-                b.start = start; b.idx = sidx;
+            if (!tpushed && wi >= nrec && (T >> 2) == (A >> 2)) {
+                tT.P = T; tT.q = T != 0 ? q_of(smem, cq, T & 3, cl.r4) : 0u;
+                tT.start = start; tT.idx = sidx; vT = true;
                 tpushed = true;
                 continue;
             }
@@ -845,36 +769,22 @@ __device__ __noinline__ uint32_t exact_lane(const Chunk& K, const LaneChain& L, 
         }
         uint32_t d = 0;
         if ((uint64_t)A < K.len) {
-            d = *(const CLY_GL uint32_t*)(K.base + A);
+            d = wl ? wl[w] : *(const CLY_GL uint32_t*)(K.base + A);
             const uint64_t n = K.len - A;
             if (n < 4) d &= (1u << (8 * n)) - 1u;
         }
         if (T != NONE32 && A + 4 > T) d = A >= T ? 0u : (d & ((1u << (8 * (T - A))) - 1u));
         uint32_t patch = 0;
-        for (int k = 0; k < nb; k++) {
-            const Bnd& b = bq[k];
-            #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const uint32_t x = A + i;
-                uint32_t m = 0;
-                if (!b.term && x >= b.P && x < b.P + 4) m = (d >> (8 * i)) & 0xffu;          // stored CRC zeroed
-                if (!b.term && x >= b.P + 4 && x < b.P + 8) m ^= 0xffu;                     // init 0xFF
-                patch ^= m << (8 * i);
-            }
-            if ((b.P >> 2) == (A >> 2)) patch ^= b.q;
-        }
+        if (vA) patch ^= bnd_patch(rA, A, d);
+        if (vB) patch ^= bnd_patch(rB, A, d);
+        if (vT) patch ^= bnd_patch(tT, A, d);
         s = crc_word(smem, s ^ d ^ patch, cl);
         if (observe && fail_P == NONE32) {
-            for (int k = 0; k < nb; k++)
-                if ((bq[k].P >> 2) == (A >> 2) && bq[k].P != 0 && bq[k].start != NONE32 && s != 0) {
-                    fail_P = bq[k].start; fail_i = bq[k].idx;
-                }
+            if (vA && bnd_fails(rA, A, s)) { fail_P = rA.start; fail_i = rA.idx; }
+            if (vB && bnd_fails(rB, A, s)) { fail_P = rB.start; fail_i = rB.idx; }
+            if (vT && bnd_fails(tT, A, s)) { fail_P = tT.start; fail_i = tT.idx; }
         }
-        // retire boundaries whose patch span ended
-        int o = 0;
-        for (int k = 0; k < nb; k++) if (bq[k].P + 8 > A + 4 && !(bq[k].term && (bq[k].P >> 2) <= (A >> 2))) bq[o++] = bq[k];
-        nb = o;
-        if (nb == 4) { if (emit) atomicOr(&g->fail, 16u); }
+        if (vT && (tT.P >> 2) <= (A >> 2)) vT = false;
     }
     // the terminal one word past a full chunk (T = len = chunk end): the register
     // after the chunk must equal Q there
@@ -886,7 +796,10 @@ __device__ __noinline__ uint32_t exact_lane(const Chunk& K, const LaneChain& L, 
 }
 
 // ---------------------------------------------------------------------------
-// One tile: phase A, agreement, look-back, phase C, fold.
+// ---------------------------------------------------------------------------
+// Kernels of one call: k_spec (every tile on its own), k_link + k_fbase (the
+// chain state entering every tile), k_refix (tiles whose own entry was wrong;
+// then k_link again), k_crc (CRC stream + tuples), k_fin, k_locate.
 __device__ __forceinline__ int find_file(const uint32_t* __restrict__ tprefix, int nfiles, uint32_t t) {
     int lo = 0, hi = nfiles - 1;
     while (lo < hi) {
@@ -936,155 +849,282 @@ __device__ __forceinline__ uint32_t tile_fold(const CLY_LDS uint8_t* smem, uint3
     return r;
 }
 
-// Phase A of one tile: the lanes' chains under their own guesses, made to
-// agree, and the tile's LOCAL descriptor.
-struct TileA { LaneChain L; uint32_t G; };
-__device__ __noinline__ TileA tile_a(const Chunk K, uint32_t t, uint32_t tt, uint64_t flen, int lane, TileDesc* desc,
-                                     Globals* g) {
+// k_spec: one wave per tile.  Phase A (each lane's chain under its own guess),
+// the lanes made to agree under the tile's guess G (0 for a file's first
+// tile), the lane chains and the tile's LOCAL written out.
+#define SPEC_WAVES 4
+__global__ void __launch_bounds__(64 * SPEC_WAVES)
+k_spec(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
+       TileLocal* loc, uint32_t* lanes, Globals* g) {
+    const uint32_t t = blockIdx.x * SPEC_WAVES + (threadIdx.x >> 6);
+    if (t >= ntiles) return;
+    const int lane = threadIdx.x & 63;
+    const int f = find_file(tprefix, nfiles, t);
+    const DevFile F = files[f];
+    const uint32_t tt = t - F.first_tile;
+    const Chunk K = make_chunk(F, tt, lane);
     const bool fof = tt == 0;
-    TileA A;
-    A.L = phase_a(K);
-    A.G = NONE32;
+    const LaneChain L0 = phase_a(K);
+    LaneChain L = L0;
+    // The tile's guess: the first lane's chain, resolved over the tile; if it
+    // does not pass through the entry of the first lane whose own chain another
+    // lane confirms (its exit is the start of the chain of the lane it lands
+    // in, or it ends at the file's end), that entry instead.
+    uint32_t G = NONE32, Gc = NONE32;
     {
-        const u64 bm = __ballot(A.L.mode == LM_CHAIN);
-        if (bm) A.G = shfl_u32(A.L.E, __ffsll((long long)bm) - 1);
+        const bool isC = L.mode == LM_CHAIN;
+        const uint32_t tb = (uint32_t)((uint64_t)tt * CLY_TILE);
+        int m = -1;
+        if (isC && L.term == TERM_NONE && L.x >= tb && (uint64_t)(L.x - tb) < (uint64_t)CLY_TILE) m = (int)((L.x - tb) / CLY_CH);
+        const uint32_t Em = shfl_u32(L.E, m < 0 ? 0 : m);
+        const int mm = __shfl(L.mode, m < 0 ? 0 : m, 64);
+        const bool conf = isC && (L.term != TERM_NONE || (m > lane && mm == LM_CHAIN && Em == L.x));
+        const u64 bc = __ballot(conf), bm = __ballot(isC);
+        if (bc) Gc = shfl_u32(L.E, __ffsll((long long)bc) - 1);
+        if (bm) G = shfl_u32(L.E, __ffsll((long long)bm) - 1);
     }
-    A.L = resolve(K, A.L, lane, fof ? 0u : A.G, false, g);
-    const LaneChain& L = A.L;
-    const u64 bc = __ballot(L.mode == LM_CHAIN), br = __ballot(L.mode == LM_CHAIN && L.cnt > 0);
-    const uint32_t c = L.mode == LM_CHAIN ? L.cnt : 0u;
-    const uint32_t tile_cnt = shfl_u32(scan_add_incl(c, lane), 63);
-    const int lc = bc ? 63 - __clzll((long long)bc) : 0, lr = br ? 63 - __clzll((long long)br) : 0;
-    const uint32_t X = shfl_u32(L.x, lc);
-    const int term = __shfl(L.term, lc, 64);
-    const uint32_t crc = shfl_u32(L.last_crc, lr), Pl = shfl_u32(L.last, lr);
-    if (lane == 0) {
-        const uint64_t tstart = (uint64_t)tt * CLY_TILE;
-        const uint32_t tend = tstart + CLY_TILE >= flen ? (uint32_t)(flen + 1) : (uint32_t)(tstart + CLY_TILE);
-        TileDesc* d = &desc[t];
-        st_agent(&d->l[1], (u64)A.G | ((u64)X << 32));
-        st_agent(&d->l[2], (u64)crc | ((u64)Pl << 32));
-        st_agent(&d->l[3], (u64)tend);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        u64 f0 = DF_PUB | ((u64)tile_cnt << 32);
-        if (bc && term != TERM_NONE) f0 |= DF_TERM;
-        if (!bc) f0 |= DF_NONE;
-        if (fof) f0 |= DF_FOF;
-        if (br) f0 |= DF_REC;
-        st_agent(&d->l[0], f0);
+    L = resolve(K, L, lane, fof ? 0u : G, false, g);
+    if (!fof && Gc != NONE32 && Gc != G) {
+        const int m = (int)((Gc - (uint32_t)((uint64_t)tt * CLY_TILE)) / CLY_CH);
+        const bool merged = __shfl(L.mode, m, 64) == LM_CHAIN && shfl_u32(L.E, m) == Gc;
+        if (!merged) { G = Gc; L = resolve(K, L0, lane, G, false, g); }
     }
-    return A;
-}
-__device__ __forceinline__ uint32_t take_tile(Globals* g, int lane) {
-    uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(&g->ticket, 1u);
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)shfl_u32(t, 0));
+    const uint64_t nl = (uint64_t)ntiles * 64;
+    lane_store(lanes, nl, (uint64_t)t * 64 + lane, L);
+    local_store(&loc[t], L, G, fof, tt, F.len, lane);
 }
 
-__global__ void __launch_bounds__(64 * SCAN_WAVES, 4)
-k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
-       TileDesc* desc, uint32_t* treg, FileInfo* finfo, const uint32_t* __restrict__ nib, cly_tuple* out_,
-       uint64_t out_cap, Globals* g, uint32_t* dump) {
+// k_link: one workgroup per file.  Each thread composes a run of tiles
+// trusting their LOCALs (entered live at the run's first guess); thread 0
+// chains the runs; each thread then re-applies its run from the true entering
+// state, writing TileIn and listing the tiles whose LOCAL disagrees with it
+// (a chain tile entered live at X != G, a tile without boundaries entered
+// live at X < its end) for k_refix.
+#define LINK_NT 256
+struct Run { uint32_t X, crc, P, G0; uint64_t cnt; int dead, has, rec, fof; };
+__device__ __forceinline__ void apply_chain(LBState& s, u64 l0, u64 l1, u64 l2) {
+    s.count += l0 >> 32;
+    s.dead = (l0 & DF_TERM) != 0;
+    s.X = (uint32_t)(l1 >> 32);
+    if (l0 & DF_REC) { s.crc_last = (uint32_t)l2; s.P_last = (uint32_t)(l2 >> 32); }
+}
+__global__ void __launch_bounds__(LINK_NT)
+k_link(const DevFile* __restrict__ files, const TileLocal* __restrict__ loc, TileIn* tin, uint64_t* ftotal,
+       uint32_t* fixlist, Globals* g) {
+    __shared__ Run runs[LINK_NT];
+    __shared__ LBState ent[LINK_NT];
+    const int f = blockIdx.x;
+    const DevFile F = files[f];
+    const uint32_t nt = F.ntile, per = (nt + LINK_NT - 1) / LINK_NT;
+    const uint32_t lo = threadIdx.x * per, hi = lo + per < nt ? lo + per : nt;
+    {
+        Run r;
+        r.X = 0; r.crc = 0; r.P = NONE32; r.G0 = NONE32; r.cnt = 0; r.dead = 0; r.has = 0; r.rec = 0; r.fof = 0;
+        for (uint32_t u = lo; u < hi; u++) {
+            const TileLocal& d = loc[F.first_tile + u];
+            const u64 l0 = d.l[0], l1 = d.l[1], l2 = d.l[2];
+            if (l0 & DF_FOF) { r.fof = 1; r.has = 1; }
+            else if (!r.has) {
+                if (l0 & DF_NONE) continue;
+                r.has = 1; r.G0 = (uint32_t)l1;
+            } else if (r.dead || (l0 & DF_NONE)) continue;
+            r.cnt += l0 >> 32;
+            r.dead = (l0 & DF_TERM) != 0;
+            r.X = (uint32_t)(l1 >> 32);
+            if (l0 & DF_REC) { r.crc = (uint32_t)l2; r.P = (uint32_t)(l2 >> 32); r.rec = 1; }
+        }
+        runs[threadIdx.x] = r;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        LBState s;
+        s.count = 0; s.X = 0; s.crc_last = 0; s.P_last = NONE32; s.dead = 0;
+        const uint32_t nr = (nt + per - 1) / per;
+        for (uint32_t k = 0; k < nr; k++) {
+            ent[k] = s;
+            const Run& r = runs[k];
+            if (r.fof) { s.count = r.cnt; s.X = r.X; s.dead = r.dead; s.crc_last = r.rec ? r.crc : 0u; s.P_last = r.rec ? r.P : NONE32; }
+            else if (!s.dead && r.has) {
+                s.count += r.cnt; s.X = r.X; s.dead = r.dead;
+                if (r.rec) { s.crc_last = r.crc; s.P_last = r.P; }
+            }
+        }
+        ftotal[f] = s.count;
+    }
+    __shared__ uint32_t first_bad;
+    if (threadIdx.x == 0) first_bad = NONE32;
+    __syncthreads();
+    LBState s = ent[threadIdx.x];
+    for (uint32_t u = lo; u < hi; u++) {
+        const uint32_t t = F.first_tile + u;
+        const TileLocal& d = loc[t];
+        const u64 l0 = d.l[0], l1 = d.l[1], l2 = d.l[2], l3 = d.l[3];
+        bool bad = false;
+        if (l0 & DF_FOF) { s.count = 0; s.X = 0; s.dead = 0; s.crc_last = 0; s.P_last = NONE32; }
+        else if (!s.dead) {
+            if (l0 & DF_NONE) bad = s.X < (uint32_t)l3;
+            else bad = s.X != (uint32_t)l1;
+        }
+        ti_store(&tin[t], s, false);
+        if (bad) { atomicMin(&first_bad, t); break; }      // the state after it is not known
+        if ((l0 & DF_FOF) || (!s.dead && !(l0 & DF_NONE))) apply_chain(s, l0, l1, l2);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && first_bad != NONE32) {
+        // only the first contradicted tile of the file has a certain entry
+        const uint32_t k = atomicAdd(&g->nfix, 1u);
+        fixlist[k] = first_bad;
+    }
+}
+
+// k_fbase: tuple index of every file's first record (exclusive prefix over
+// the file totals) and the call's total.
+#define FB_NT 1024
+__global__ void __launch_bounds__(FB_NT)
+k_fbase(int nfiles, const uint64_t* __restrict__ ftotal, FileInfo* finfo, Globals* g) {
+    __shared__ uint64_t part[FB_NT];
+    __shared__ uint64_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int b = 0; b < nfiles; b += FB_NT) {
+        const int i = b + threadIdx.x;
+        const uint64_t v = i < nfiles ? ftotal[i] : 0;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (int d = 1; d < FB_NT; d <<= 1) {
+            const uint64_t o = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+            __syncthreads();
+            part[threadIdx.x] += o;
+            __syncthreads();
+        }
+        if (i < nfiles) finfo[i].first_index = carry + part[threadIdx.x] - v;
+        __syncthreads();
+        if (threadIdx.x == 0) carry += part[FB_NT - 1];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) g->total = carry;
+}
+
+// k_refix: one wave per listed tile: its lanes re-resolved from the entering
+// state k_link gave it; new lane chains and LOCAL.  Walks on into the next
+// tile of the file while that one's LOCAL disagrees with the new exit (and no
+// other wave has it listed).
+__global__ void __launch_bounds__(64 * SPEC_WAVES)
+k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
+        TileLocal* loc, const TileIn* __restrict__ tin, uint32_t* lanes, const uint32_t* __restrict__ fixlist,
+        Globals* g) {
+    const uint32_t k = blockIdx.x * SPEC_WAVES + (threadIdx.x >> 6);
+    if (k >= g->nfix) return;
+    const int lane = threadIdx.x & 63;
+    uint32_t t = fixlist[k];
+    const int f = find_file(tprefix, nfiles, t);
+    const DevFile F = files[f];
+    LBState S = ti_load(&tin[t]);
+    const uint64_t nl = (uint64_t)ntiles * 64;
+    for (;;) {
+        const uint32_t tt = t - F.first_tile;
+        const Chunk K = make_chunk(F, tt, lane);
+        LaneChain L = lane_load(lanes, nl, (uint64_t)t * 64 + lane);
+        L = resolve(K, L, lane, S.dead ? 0u : S.X, S.dead != 0, g);
+        lane_store(lanes, nl, (uint64_t)t * 64 + lane, L);
+        local_store(&loc[t], L, NONE32, tt == 0, tt, F.len, lane);
+        // state after the tile
+        const u64 bc = __ballot(L.mode == LM_CHAIN);
+        if (bc) {
+            const int lc = 63 - __clzll((long long)bc);
+            S.X = shfl_u32(L.x, lc);
+            S.dead = __shfl(L.term, lc, 64) != TERM_NONE;
+        }
+        if (S.dead || t + 1 >= F.first_tile + F.ntile) break;
+        // the next tile: consistent with the new exit?  else it is re-resolved too
+        const u64 n0 = loc[t + 1].l[0], n1 = loc[t + 1].l[1], n3 = loc[t + 1].l[3];
+        const bool ok = (n0 & DF_NONE) ? S.X >= (uint32_t)n3 : S.X == (uint32_t)n1;
+        if (ok) break;
+        t++;
+    }
+}
+
+// k_crc: the CRC stream and the tuples, tiles in grid-stride order.
+#define CRC_WAVES 16
+__global__ void __launch_bounds__(64 * CRC_WAVES)
+k_crc(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
+      const TileIn* __restrict__ tin, const uint32_t* __restrict__ lanes, uint32_t* treg, FileInfo* finfo,
+      const uint32_t* __restrict__ tabs, cly_tuple* out_, uint64_t out_cap, Globals* g) {
+    if (g->nfix) return;                    // the chain is not final yet (k_refix first)
     gtuples out = (gtuples)out_;
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
-    init_tables(smem, nib);
+    init_tables(smem, tabs);
     const int lane = threadIdx.x & 63;
     const CrcLane cl = crc_lane(lane);
-    CLY_LDS u32x2* evq = (CLY_LDS u32x2*)(smem + LDS_EVQ) + (threadIdx.x >> 6) * (EVQ * 64) + lane;
-    // Tiles are software-pipelined per wave: phase A of the wave's next tile
-    // (and its LOCAL) comes before phase C of the current one, so the
-    // look-back of the next tile finds its predecessors published.
-    uint32_t t = take_tile(g, lane);
-    if (t >= ntiles) return;
-    int f = find_file(tprefix, nfiles, t);
-    DevFile F = files[f];
-    uint32_t tt = t - F.first_tile;
-    Chunk K = make_chunk(F, tt, lane);
-    TileA A = tile_a(K, t, tt, F.len, lane, desc, g);
-    for (;;) {
-        PROF_T0();
-        const bool fof = tt == 0;
-        LaneChain L = A.L;
-        // ---- L: the true state entering the tile
-        LBState S = look_back(desc, (int64_t)t, lane, g);
-        PROF(1);
-        if (fof) { S.dead = 0; S.X = 0; S.crc_last = 0; S.P_last = NONE32; }
-        if (!fof && (S.dead || S.X != A.G) && lane == 0) atomicAdd(&g->refix, 1u);
-        L = resolve(K, L, lane, S.dead ? 0u : S.X, S.dead != 0, g);
+    const uint64_t nl = (uint64_t)ntiles * 64;
+    for (uint32_t t = blockIdx.x * CRC_WAVES + (threadIdx.x >> 6); t < ntiles; t += gridDim.x * CRC_WAVES) {
+        const int f = find_file(tprefix, nfiles, t);
+        const DevFile F = files[f];
+        LBState S = ti_load(&tin[t]);
+        if (S.dead) { if (lane == 0) treg[t] = 0; continue; }
+        S.count += finfo[f].first_index;
+        const uint32_t tt = t - F.first_tile;
+        const Chunk K = make_chunk(F, tt, lane);
+        const LaneChain L = lane_load(lanes, nl, (uint64_t)t * 64 + lane);
         uint32_t tile_cnt;
         const LaneIn I = lane_inputs(K, L, S, lane, tile_cnt);
-        if (dump) {
-            // debug dump (CLY_DUMP): the final chain of every lane
-            uint32_t* o = dump + ((uint64_t)t * 64 + lane) * 8;
-            o[0] = (uint32_t)L.mode; o[1] = L.E; o[2] = L.x; o[3] = (uint32_t)L.term; o[4] = L.cnt;
-            o[5] = S.X | (S.dead ? 0x80000000u : 0u); o[6] = A.G; o[7] = (uint32_t)f;
-        }
-        {
-            // INCL descriptor
-            LBState o = S;
-            o.count += tile_cnt;
-            const u64 bc = __ballot(L.mode == LM_CHAIN), br = __ballot(L.mode == LM_CHAIN && L.cnt > 0);
-            if (bc) {
-                const int lc = 63 - __clzll((long long)bc);
-                o.X = shfl_u32(L.x, lc);
-                o.dead = __shfl(L.term, lc, 64) != TERM_NONE;
-            }
-            if (br) {
-                const int lr = 63 - __clzll((long long)br);
-                o.crc_last = shfl_u32(L.last_crc, lr);
-                o.P_last = shfl_u32(L.last, lr);
-            }
-            if (lane == 0) {
-                TileDesc* d = &desc[t];
-                st_agent(&d->i[1], (u64)o.X | ((u64)o.crc_last << 32));
-                st_agent(&d->i[2], (u64)o.P_last);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                st_agent(&d->i[0], DF_PUB | (o.dead ? DF_TERM : 0ull) | (o.count << 16));
-                if (fof) finfo[f].first_index = S.count;
-                if (t == ntiles - 1) g->total = o.count;
-            }
-        }
-        PROF(2);
-        // ---- A of the next tile
-        const uint32_t tn = take_tile(g, lane);
-        int fn = f;
-        DevFile Fn = F;
-        uint32_t ttn = 0;
-        Chunk Kn = K;
-        TileA An = A;
-        if (tn < ntiles) {
-            fn = find_file(tprefix, nfiles, tn);
-            Fn = files[fn];
-            ttn = tn - Fn.first_tile;
-            Kn = make_chunk(Fn, ttn, lane);
-            An = tile_a(Kn, tn, ttn, Fn.len, lane, desc, g);
-        }
-        PROF(0);
-        // ---- C: CRC stream, tuples
         const bool term_lane = L.mode == LM_CHAIN && L.term != TERM_NONE;
-        const bool slow = L.mode == LM_CHAIN && !term_lane && L.minsz < 12;
-        const bool fast = (L.mode == LM_CHAIN && !term_lane && !slow) || L.mode == LM_NONE;
-        uint32_t r = phase_c_fast(K, L, I, fast, F.fid, out, out_cap, smem, evq, cl, g);
-        PROF(3);
-        if (term_lane || slow) {
-            uint32_t fp, ex;
-            uint64_t fi;
-            r = exact_lane(K, L, I, 0u, true, false, F.fid, out, out_cap, smem, cl, g, fp, fi, ex);
-            if (slow) atomicAdd(&g->slow_lanes, 1u);
-            if (term_lane) {
-                FileInfo* fo = &finfo[f];
-                fo->term_pos = L.x; fo->term_status = L.term; fo->term_tile = t; fo->term_lane = (uint32_t)lane;
-                fo->expect = ex; fo->end_index = I.base + L.cnt; fo->has_term = 1;
-            }
+        const bool fast = (L.mode == LM_CHAIN && !term_lane) || L.mode == LM_NONE;
+        uint32_t r = phase_c_fast(K, L, I, fast, F.fid, out, out_cap, smem, cl, g);
+        if (term_lane) {
+            // the lane holding the file's terminal: k_term (exact path) adds its register
+            FileInfo* fo = &finfo[f];
+            fo->term_pos = L.x; fo->term_status = L.term; fo->term_tile = t; fo->term_lane = (uint32_t)lane;
+            fo->end_index = I.base + L.cnt; fo->has_term = 1;
         }
-        if (!fast && !term_lane && !slow) r = 0;
-        PROF(4);
+        if (!fast) r = 0;
         r = tile_fold(smem, r, lane);
-        PROF(5);
         if (lane == 0) treg[t] = r;
-        if (tn >= ntiles) break;
-        t = tn; f = fn; F = Fn; tt = ttn; K = Kn; A = An;
+    }
+}
+
+// k_term: one wave per file: the lane holding the file's terminal T, word by
+// word (everything from T on zeroed), its tuples, and its register added to its
+// tile's (shifted to the tile end).
+__global__ void __launch_bounds__(64)
+k_term(const DevFile* __restrict__ files, const TileIn* __restrict__ tin, const uint32_t* __restrict__ lanes,
+       uint32_t ntiles, uint32_t* treg, FileInfo* finfo, const uint32_t* __restrict__ tabs, cly_tuple* out_,
+       uint64_t out_cap, Globals* g) {
+    if (g->nfix) return;
+    gtuples out = (gtuples)out_;
+    __shared__ __attribute__((aligned(16))) unsigned char smem_raw[LDS_SH + CLY_CH];
+    CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
+    init_tables(smem, tabs, NIB_LEVELS * 128);
+    const int lane = threadIdx.x & 63;
+    const int f = blockIdx.x;
+    FileInfo* fo = &finfo[f];
+    if (!fo->has_term) return;                         // k_fin reports it
+    const DevFile F = files[f];
+    const uint32_t t = fo->term_tile, tl = fo->term_lane;
+    LBState S = ti_load(&tin[t]);
+    S.count += fo->first_index;
+    const CrcLane cl = crc_lane(lane);
+    const Chunk K = make_chunk(F, t - F.first_tile, lane);
+    const LaneChain L = lane_load(lanes, (uint64_t)ntiles * 64, (uint64_t)t * 64 + lane);
+    uint32_t tile_cnt;
+    const LaneIn I = lane_inputs(K, L, S, lane, tile_cnt);
+    // the terminal lane's chunk into LDS (16 B per lane), read word by word from there
+    CLY_LDS u32x4* wl = (CLY_LDS u32x4*)(smem + LDS_SH);
+    {
+        Chunk Kt = K;
+        Kt.cb = (uint32_t)((uint64_t)(t - F.first_tile) * CLY_TILE + (uint64_t)tl * CLY_CH);
+        if (lane < CLY_CH / 16) wl[lane] = piece(Kt, 16u * (uint32_t)lane);
+    }
+    __syncthreads();
+    if ((uint32_t)lane == tl) {
+        uint32_t fp, ex;
+        uint64_t fi;
+        uint32_t r = exact_lane(K, L, I, 0u, true, false, F.fid, out, out_cap, smem, cl, g, fp, fi, ex,
+                                (const CLY_LDS uint32_t*)wl);
+        fo->expect = ex;
+        for (int lvl = 0; lvl < 6; lvl++) if ((63u - tl) & (1u << lvl)) r = nib_mul(smem, lvl, r);
+        treg[t] ^= r;
     }
 }
 
@@ -1102,6 +1142,7 @@ k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __rest
     __shared__ uint32_t tab[NIB_LEVELS * 128];
     __shared__ uint32_t part[FIN_NT];
     __shared__ uint32_t plen[FIN_NT];
+    if (g->nfix) return;                    // k_crc did not run (link repair first)
     for (int i = threadIdx.x; i < NIB_LEVELS * 128; i += FIN_NT) tab[i] = nib[i];
     __syncthreads();
     const int f = blockIdx.x;
@@ -1151,33 +1192,32 @@ k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __rest
 }
 
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
 // k_locate (only after a failed fold): every tile of a failing file up to its
-// terminal re-derives its chain from the published states, the register
-// entering each chunk, and walks its records' checks from there; the first
-// failing record of the file wins (atomicMin on offset << 32 | index).
-__global__ void __launch_bounds__(512, 4)
+// terminal takes its final lane chains, the register entering each chunk, and
+// walks its records' checks from there; the first failing record of the file
+// wins (atomicMin on offset << 32 | index).
+__global__ void __launch_bounds__(512, 2)
 k_locate(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
-         const TileDesc* desc, const uint32_t* __restrict__ treg, FileInfo* finfo, const uint32_t* __restrict__ nib,
-         Globals* g) {
+         const TileIn* __restrict__ tin, const uint32_t* __restrict__ lanes, const uint32_t* __restrict__ treg,
+         FileInfo* finfo, const uint32_t* __restrict__ tabs, Globals* g) {
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
-    init_tables(smem, nib);
+    init_tables(smem, tabs);
     const int lane = threadIdx.x & 63;
     const CrcLane cl = crc_lane(lane);
+    const uint64_t nl = (uint64_t)ntiles * 64;
     for (uint32_t t = blockIdx.x * 8 + (threadIdx.x >> 6); t < ntiles; t += gridDim.x * 8) {
         const int f = find_file(tprefix, nfiles, t);
         const DevFile F = files[f];
         FileInfo* fo = &finfo[f];
         if (fo->ok || t > fo->term_tile) continue;
-        const uint32_t tt = t - F.first_tile;
-        const bool fof = tt == 0;
-        const Chunk K = make_chunk(F, tt, lane);
-        LBState S;
-        if (fof) { S = lb_virtual(); S.dead = 0; S.X = 0; S.count = fo->first_index; }
-        else S = lb_incl(desc[t - 1].i[0], desc[t - 1].i[1], desc[t - 1].i[2]);
+        LBState S = ti_load(&tin[t]);
         if (S.dead) continue;
-        LaneChain L = phase_a(K);
-        L = resolve(K, L, lane, S.X, false, g);
+        S.count += fo->first_index;
+        const uint32_t tt = t - F.first_tile;
+        const Chunk K = make_chunk(F, tt, lane);
+        const LaneChain L = lane_load(lanes, nl, (uint64_t)t * 64 + lane);
         uint32_t tile_cnt;
         const LaneIn I = lane_inputs(K, L, S, lane, tile_cnt);
         // register entering the tile
@@ -1216,14 +1256,15 @@ k_locate(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restri
 struct cly_ctx {
     int device;
     hipStream_t stream;
-    hipEvent_t ev[4];
-    DevFile* d_files; uint32_t* d_tprefix; FileInfo* d_finfo; int cap_files;
+    hipEvent_t ev[8];
+    DevFile* d_files; uint32_t* d_tprefix; FileInfo* d_finfo; uint64_t* d_ftotal; int cap_files;
     DevFile* h_files; uint32_t* h_tprefix; FileInfo* h_finfo;
-    TileDesc* d_desc; uint32_t* d_treg; int64_t cap_tiles;
+    TileLocal* d_loc; TileIn* d_tin; uint32_t* d_treg; uint32_t* d_fix; uint32_t* d_lanes; int64_t cap_tiles;
     Globals* d_g; Globals* h_g;
-    uint32_t* d_nib;             // nibble tables of A^(CLY_CH 2^k), k < NIB_LEVELS
+    uint32_t* d_tabs;            // nibble tables: A^(CLY_CH 2^k), k < NIB_LEVELS; A^(4 m), m < 16; A^(64 m)
     uint32_t* d_pw;              // x^(8 CLY_TILE 2^k) mod P, k < 40
-    int scan_grid;
+    int crc_grid, loc_grid;
+    float kms[6];                // last call: k_spec, link rounds (k_link/k_fbase/k_refix), k_crc, k_fin, k_locate, all
     uint8_t* d_bytes; uint64_t cap_bytes;          // host-path staging
     cly_tuple* d_tuples; uint64_t cap_tuples;
     void* merge_scratch;         // clymerge.hip's buffers (grow-only)
@@ -1240,18 +1281,22 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     if (!c) return CLY_ERR_DEVICE;
     c->device = device;
     HIPCK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    for (int i = 0; i < 4; i++) HIPCK(hipEventCreate(&c->ev[i]));
+    for (int i = 0; i < 8; i++) HIPCK(hipEventCreate(&c->ev[i]));
     HIPCK(hipMalloc(&c->d_g, sizeof(Globals)));
     HIPCK(hipHostMalloc(&c->h_g, sizeof(Globals), hipHostMallocDefault));
     {
-        uint32_t hn[NIB_LEVELS * 128];
-        for (int lvl = 0; lvl < NIB_LEVELS; lvl++) {
-            const uint32_t xm = cly_x8n((uint64_t)CLY_CH << lvl);
+        static uint32_t hn[NTAB];
+        for (int lvl = 0; lvl < NIB_LEVELS + NSH; lvl++) {
+            uint64_t nbytes;
+            if (lvl < NIB_LEVELS) nbytes = (uint64_t)CLY_CH << lvl;                  // A^(CLY_CH 2^lvl)
+            else if (lvl < NIB_LEVELS + 16) nbytes = 4ull * (uint64_t)(lvl - NIB_LEVELS);   // A^(4 m)
+            else nbytes = 64ull * (uint64_t)(lvl - NIB_LEVELS - 16);                 // A^(64 m)
+            const uint32_t xm = cly_x8n(nbytes);
             for (int nb = 0; nb < 8; nb++)
                 for (uint32_t v = 0; v < 16; v++) hn[lvl * 128 + nb * 16 + v] = cly_multmodp(xm, v << (4 * nb));
         }
-        HIPCK(hipMalloc(&c->d_nib, sizeof(hn)));
-        HIPCK(hipMemcpy(c->d_nib, hn, sizeof(hn), hipMemcpyHostToDevice));
+        HIPCK(hipMalloc(&c->d_tabs, sizeof(hn)));
+        HIPCK(hipMemcpy(c->d_tabs, hn, sizeof(hn), hipMemcpyHostToDevice));
         uint32_t hp[40];
         hp[0] = cly_x8n((uint64_t)CLY_TILE);
         for (int k = 1; k < 40; k++) hp[k] = cly_multmodp(hp[k - 1], hp[k - 1]);
@@ -1259,12 +1304,13 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
         HIPCK(hipMemcpy(c->d_pw, hp, sizeof(hp), hipMemcpyHostToDevice));
     }
     {
-        int per_cu = 0, ncu = 0;
-        HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_scan, 64 * SCAN_WAVES, 0));
+        int ncu = 0;
         HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+        int per_cu = 0;
+        HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_crc, 64 * CRC_WAVES, 0));
         if (per_cu < 1) per_cu = 1;
-        if (per_cu > 1) per_cu = 1;
-        c->scan_grid = per_cu * ncu;
+        c->crc_grid = per_cu * ncu;
+        c->loc_grid = ncu * 2;
     }
     *out = c;
     return CLY_OK;
@@ -1274,11 +1320,12 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
-    hipFree(c->d_files); hipFree(c->d_tprefix); hipFree(c->d_finfo); hipFree(c->d_desc); hipFree(c->d_treg);
-    hipFree(c->d_g); hipFree(c->d_nib); hipFree(c->d_pw); hipFree(c->d_bytes); hipFree(c->d_tuples);
+    hipFree(c->d_files); hipFree(c->d_tprefix); hipFree(c->d_finfo); hipFree(c->d_ftotal);
+    hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_lanes);
+    hipFree(c->d_g); hipFree(c->d_tabs); hipFree(c->d_pw); hipFree(c->d_bytes); hipFree(c->d_tuples);
     hipHostFree(c->h_files); hipHostFree(c->h_tprefix); hipHostFree(c->h_finfo); hipHostFree(c->h_g);
     cly_merge_scratch_free(c->merge_scratch);
-    for (int i = 0; i < 4; i++) hipEventDestroy(c->ev[i]);
+    for (int i = 0; i < 8; i++) hipEventDestroy(c->ev[i]);
     hipStreamDestroy(c->stream);
     free(c);
 }
@@ -1291,15 +1338,16 @@ extern "C" uint64_t cly_scan_capacity(const cly_file* files, int nfiles) {
 
 static int ensure_files(cly_ctx* c, int nfiles) {
     if (nfiles <= c->cap_files) return CLY_OK;
-    hipFree(c->d_files); hipFree(c->d_tprefix); hipFree(c->d_finfo);
+    hipFree(c->d_files); hipFree(c->d_tprefix); hipFree(c->d_finfo); hipFree(c->d_ftotal);
     hipHostFree(c->h_files); hipHostFree(c->h_tprefix); hipHostFree(c->h_finfo);
-    c->d_files = nullptr; c->d_tprefix = nullptr; c->d_finfo = nullptr;
+    c->d_files = nullptr; c->d_tprefix = nullptr; c->d_finfo = nullptr; c->d_ftotal = nullptr;
     c->h_files = nullptr; c->h_tprefix = nullptr; c->h_finfo = nullptr;
     c->cap_files = 0;
     const int cap = nfiles < 64 ? 64 : nfiles;
     HIPCK(hipMalloc(&c->d_files, sizeof(DevFile) * cap));
     HIPCK(hipMalloc(&c->d_tprefix, sizeof(uint32_t) * (cap + 1)));
     HIPCK(hipMalloc(&c->d_finfo, sizeof(FileInfo) * cap));
+    HIPCK(hipMalloc(&c->d_ftotal, sizeof(uint64_t) * cap));
     HIPCK(hipHostMalloc(&c->h_files, sizeof(DevFile) * cap, hipHostMallocDefault));
     HIPCK(hipHostMalloc(&c->h_tprefix, sizeof(uint32_t) * (cap + 1), hipHostMallocDefault));
     HIPCK(hipHostMalloc(&c->h_finfo, sizeof(FileInfo) * cap, hipHostMallocDefault));
@@ -1309,11 +1357,15 @@ static int ensure_files(cly_ctx* c, int nfiles) {
 
 static int ensure_tiles(cly_ctx* c, int64_t ntiles) {
     if (ntiles <= c->cap_tiles) return CLY_OK;
-    hipFree(c->d_desc); hipFree(c->d_treg);
-    c->d_desc = nullptr; c->d_treg = nullptr; c->cap_tiles = 0;
+    hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_lanes);
+    c->d_loc = nullptr; c->d_tin = nullptr; c->d_treg = nullptr; c->d_fix = nullptr; c->d_lanes = nullptr;
+    c->cap_tiles = 0;
     const int64_t cap = ntiles < 1024 ? 1024 : ntiles;
-    HIPCK(hipMalloc(&c->d_desc, sizeof(TileDesc) * cap));
+    HIPCK(hipMalloc(&c->d_loc, sizeof(TileLocal) * cap));
+    HIPCK(hipMalloc(&c->d_tin, sizeof(TileIn) * cap));
     HIPCK(hipMalloc(&c->d_treg, sizeof(uint32_t) * cap));
+    HIPCK(hipMalloc(&c->d_fix, sizeof(uint32_t) * cap));
+    HIPCK(hipMalloc(&c->d_lanes, sizeof(uint32_t) * LANE_WORDS * 64 * cap));
     c->cap_tiles = cap;
     return CLY_OK;
 }
@@ -1349,51 +1401,111 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     if (rc) return rc;
     HIPCK(hipMemcpyAsync(c->d_files, c->h_files, sizeof(DevFile) * nfiles, hipMemcpyHostToDevice, st));
     HIPCK(hipMemcpyAsync(c->d_tprefix, c->h_tprefix, sizeof(uint32_t) * (nfiles + 1), hipMemcpyHostToDevice, st));
-    HIPCK(hipMemsetAsync(c->d_desc, 0, sizeof(TileDesc) * ntiles, st));
     HIPCK(hipMemsetAsync(c->d_finfo, 0, sizeof(FileInfo) * nfiles, st));
     HIPCK(hipMemsetAsync(c->d_g, 0, sizeof(Globals), st));
-    int grid = c->scan_grid;
-    if ((int64_t)grid * SCAN_WAVES > ntiles) grid = (int)((ntiles + SCAN_WAVES - 1) / SCAN_WAVES);
+    const uint32_t nt32 = (uint32_t)ntiles;
+    const int spec_grid = (int)((ntiles + SPEC_WAVES - 1) / SPEC_WAVES);
     HIPCK(hipEventRecord(c->ev[0], st));
-    // debug: CLY_DUMP=<path> appends every lane's final chain (8 u32 per lane) of each call
-    const char* dump_path = getenv("CLY_DUMP");
-    uint32_t* d_dump = nullptr;
-    if (dump_path) HIPCK(hipMalloc(&d_dump, sizeof(uint32_t) * 8 * 64 * ntiles));
-    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * SCAN_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, (uint32_t)ntiles,
-                       c->d_desc, c->d_treg, c->d_finfo, c->d_nib, d_out, out_cap, c->d_g, d_dump);
+    hipLaunchKernelGGL(k_spec, dim3(spec_grid), dim3(64 * SPEC_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
+                       c->d_loc, c->d_lanes, c->d_g);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[1], st));
-    hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_finfo, c->d_treg, c->d_nib, c->d_pw,
-                       c->d_g);
+    // link round 0, and the CRC kernels launched behind it: they return at once
+    // when the round listed tiles (g->nfix), and run again after the repair
+    hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, c->d_loc, c->d_tin, c->d_ftotal,
+                       c->d_fix, c->d_g);
+    hipLaunchKernelGGL(k_fbase, dim3(1), dim3(FB_NT), 0, st, nfiles, c->d_ftotal, c->d_finfo, c->d_g);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[2], st));
-    HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
-    HIPCK(hipStreamSynchronize(st));
+    auto launch_crc = [&]() -> int {
+        int grid = c->crc_grid;
+        if ((int64_t)grid * CRC_WAVES > ntiles) grid = (int)((ntiles + CRC_WAVES - 1) / CRC_WAVES);
+        hipLaunchKernelGGL(k_crc, dim3(grid), dim3(64 * CRC_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
+                           c->d_tin, c->d_lanes, c->d_treg, c->d_finfo, c->d_tabs, d_out, out_cap, c->d_g);
+        HIPCK(hipGetLastError());
+        HIPCK(hipEventRecord(c->ev[3], st));
+        hipLaunchKernelGGL(k_term, dim3(nfiles), dim3(64), 0, st, c->d_files, c->d_tin, c->d_lanes, nt32, c->d_treg,
+                           c->d_finfo, c->d_tabs, d_out, out_cap, c->d_g);
+        hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_finfo, c->d_treg, c->d_tabs,
+                           c->d_pw, c->d_g);
+        HIPCK(hipGetLastError());
+        HIPCK(hipEventRecord(c->ev[4], st));
+        HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
+        HIPCK(hipStreamSynchronize(st));
+        return CLY_OK;
+    };
+    int rc2 = launch_crc();
+    if (rc2) return rc2;
+    float ms_fix = 0;
+    uint32_t rounds = 1, refixed = 0;
+    if (c->h_g->nfix) {
+        // repair rounds: re-resolve the listed tiles from their true entry, link again
+        HIPCK(hipEventRecord(c->ev[5], st));
+        while (c->h_g->nfix) {
+            if (c->h_g->fail) break;
+            if (rounds > 4096) { fprintf(stderr, "clyscan: chain repair did not converge\n"); return CLY_ERR_NOREPAIR; }
+            const uint32_t nfix = c->h_g->nfix;
+            refixed += nfix;
+            if (getenv("CLY_TRACE") && (rounds < 6 || rounds % 200 == 0)) {
+                // debug: the listed tiles of this round, their entering state and LOCAL
+                static uint32_t hf[8];
+                static TileIn hti[8];
+                static TileLocal hl[8];
+                const uint32_t n = nfix < 8 ? nfix : 8;
+                hipMemcpy(hf, c->d_fix, 4 * n, hipMemcpyDeviceToHost);
+                fprintf(stderr, "round %u: %u listed\n", rounds, nfix);
+                for (uint32_t i = 0; i < n; i++) {
+                    hipMemcpy(&hti[i], c->d_tin + hf[i], sizeof(TileIn), hipMemcpyDeviceToHost);
+                    hipMemcpy(&hl[i], c->d_loc + hf[i], sizeof(TileLocal), hipMemcpyDeviceToHost);
+                    fprintf(stderr, "  tile %u: in X=%u dead=%u fix=%u | local flags=%#llx cnt=%llu G=%u X=%u tend=%llu\n", hf[i],
+                            hti[i].w[2], hti[i].w[3] & 1, hti[i].w[3] >> 1, (unsigned long long)(hl[i].l[0] & 0xff),
+                            (unsigned long long)(hl[i].l[0] >> 32), (uint32_t)hl[i].l[1], (uint32_t)(hl[i].l[1] >> 32),
+                            (unsigned long long)hl[i].l[3]);
+                }
+            }
+            hipLaunchKernelGGL(k_refix, dim3((nfix + SPEC_WAVES - 1) / SPEC_WAVES), dim3(64 * SPEC_WAVES), 0, st, c->d_files,
+                               nfiles, c->d_tprefix, nt32, c->d_loc, c->d_tin, c->d_lanes, c->d_fix, c->d_g);
+            HIPCK(hipGetLastError());
+            HIPCK(hipMemsetAsync(&c->d_g->nfix, 0, sizeof(uint32_t), st));
+            hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, c->d_loc, c->d_tin, c->d_ftotal,
+                               c->d_fix, c->d_g);
+            hipLaunchKernelGGL(k_fbase, dim3(1), dim3(FB_NT), 0, st, nfiles, c->d_ftotal, c->d_finfo, c->d_g);
+            HIPCK(hipGetLastError());
+            HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
+            HIPCK(hipStreamSynchronize(st));
+            rounds++;
+        }
+        HIPCK(hipEventRecord(c->ev[6], st));
+        HIPCK(hipEventSynchronize(c->ev[6]));
+        HIPCK(hipEventElapsedTime(&ms_fix, c->ev[5], c->ev[6]));
+        if (!c->h_g->fail) {
+            HIPCK(hipEventRecord(c->ev[2], st));
+            rc2 = launch_crc();
+            if (rc2) return rc2;
+        }
+    }
     bool located = false;
     if (c->h_g->any_fail && !c->h_g->fail) {
-        hipLaunchKernelGGL(k_locate, dim3(c->scan_grid), dim3(512), 0, st, c->d_files, nfiles, c->d_tprefix, (uint32_t)ntiles,
-                           c->d_desc, c->d_treg, c->d_finfo, c->d_nib, c->d_g);
+        HIPCK(hipMemcpyAsync(c->h_finfo, c->d_finfo, sizeof(FileInfo) * nfiles, hipMemcpyDeviceToHost, st));
+        HIPCK(hipStreamSynchronize(st));
+        hipLaunchKernelGGL(k_locate, dim3(c->loc_grid), dim3(512), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
+                           c->d_tin, c->d_lanes, c->d_treg, c->d_finfo, c->d_tabs, c->d_g);
         HIPCK(hipGetLastError());
         located = true;
     }
-    HIPCK(hipEventRecord(c->ev[3], st));
+    HIPCK(hipEventRecord(c->ev[7], st));
     HIPCK(hipMemcpyAsync(c->h_finfo, c->d_finfo, sizeof(FileInfo) * nfiles, hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
-    if (d_dump) {
-        const size_t nb = sizeof(uint32_t) * 8 * 64 * ntiles;
-        uint32_t* h = (uint32_t*)malloc(nb);
-        if (h && hipMemcpy(h, d_dump, nb, hipMemcpyDeviceToHost) == hipSuccess) {
-            FILE* fd = fopen(dump_path, "ab");
-            if (fd) { fwrite(h, 1, nb, fd); fclose(fd); }
-        }
-        free(h);
-        hipFree(d_dump);
-    }
-    float ms_scan = 0, ms_fin = 0, ms_loc = 0;
-    HIPCK(hipEventElapsedTime(&ms_scan, c->ev[0], c->ev[1]));
-    HIPCK(hipEventElapsedTime(&ms_fin, c->ev[1], c->ev[2]));
-    HIPCK(hipEventElapsedTime(&ms_loc, c->ev[2], c->ev[3]));
+    float ms_spec = 0, ms_link = 0, ms_crc = 0, ms_fin = 0, ms_loc = 0;
+    HIPCK(hipEventElapsedTime(&ms_spec, c->ev[0], c->ev[1]));
+    HIPCK(hipEventElapsedTime(&ms_link, c->ev[1], c->ev[2]));
+    HIPCK(hipEventElapsedTime(&ms_crc, c->ev[2], c->ev[3]));
+    HIPCK(hipEventElapsedTime(&ms_fin, c->ev[3], c->ev[4]));
+    HIPCK(hipEventElapsedTime(&ms_loc, c->ev[4], c->ev[7]));
+    if (rounds > 1) ms_link = 0;   // ev[2] was re-recorded after the repair: link time of round 0 not kept
+    c->kms[0] = ms_spec; c->kms[1] = ms_link + ms_fix; c->kms[2] = ms_crc; c->kms[3] = ms_fin; c->kms[4] = ms_loc;
+    c->kms[5] = ms_spec + ms_link + ms_fix + ms_crc + ms_fin + ms_loc;
     if (c->h_g->fail) {
         fprintf(stderr, "clyscan: internal error (code %#x)\n", c->h_g->fail);
         return CLY_ERR_DEVICE;
@@ -1417,8 +1529,9 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     }
     if (needed) *needed = c->h_g->total;
     if (stats) {
-        stats->scan_ms = ms_scan; stats->resolve_ms = ms_fin + ms_loc; stats->total_ms = ms_scan + ms_fin + ms_loc;
-        stats->passes = 1 + (c->h_g->refix ? 1 : 0) + (located ? 1 : 0);
+        stats->scan_ms = ms_spec + ms_crc; stats->resolve_ms = ms_link + ms_fix + ms_fin + ms_loc;
+        stats->total_ms = c->kms[5];
+        stats->passes = rounds + (located ? 1 : 0);
         stats->n_chunks = (uint32_t)(ntiles * CLY_NL); stats->bytes = bytes; stats->records = total;
     }
     if (c->h_g->overflow || c->h_g->total > out_cap) return CLY_ERR_CAPACITY;
@@ -1537,10 +1650,11 @@ extern "C" hipStream_t cly_ctx_stream_internal(cly_ctx* c) { return c->stream; }
 extern "C" int cly_ctx_device_internal(cly_ctx* c) { return c->device; }
 extern "C" void** cly_ctx_merge_slot_internal(cly_ctx* c) { return &c->merge_scratch; }
 
-// Profiling build only: the phase cycle counters of the last call.
-extern "C" int cly_dbg_prof(cly_ctx* c, uint64_t* out12) {
-    for (int i = 0; i < 12; i++) out12[i] = c->h_g->prof[i];
-    return 12;
+// Per-kernel times of the last cly_scan_device call (ms): k_spec, link rounds
+// (k_link + k_fbase + repair), k_crc, k_fin, k_locate, all.  Not in the public header.
+extern "C" int cly_dbg_kernel_ms(cly_ctx* c, double* out6) {
+    for (int i = 0; i < 6; i++) out6[i] = c->kms[i];
+    return 6;
 }
 
 extern "C" const char* cly_strerror(int code) {
@@ -1565,7 +1679,7 @@ extern "C" const char* cly_strerror(int code) {
 #endif
 extern "C" const char* cly_build_info(void) {
     static char buf[200];
-    snprintf(buf, sizeof(buf), "clyscan gfx950 lane-chunk CH=%d TILE=%lld LDS=%d src=%s", CLY_CH, (long long)CLY_TILE,
+    snprintf(buf, sizeof(buf), "clyscan gfx950 spec/link/crc CH=%d TILE=%lld LDS=%d src=%s", CLY_CH, (long long)CLY_TILE,
              (int)SCAN_LDS, CLY_SRC_HASH);
     return buf;
 }

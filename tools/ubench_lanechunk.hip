@@ -166,5 +166,11 @@ int main() {
     run<2048, 256, 1, 2>(d, n, out, grid, "lane chunk", head);
     run<2048, 64, 2, 1>(d, n, out, grid, "lane chunk", head);
     run<2048, 64, 2, 2>(d, n, out, grid, "lane chunk", head);
+    run<1024, 128, 1, 1>(d, n, out, grid, "lane chunk", head);
+    run<1024, 128, 2, 1>(d, n, out, grid, "lane chunk", head);
+    run<1024, 128, 2, 0>(d, n, out, grid, "lane chunk", head);
+    run<1024, 128, 3, 1>(d, n, out, grid, "lane chunk", head);
+    run<1024, 128, 2, 2>(d, n, out, grid, "lane chunk", head);
+    run<1024, 128, 2, 3>(d, n, out, grid, "lane chunk", head);
     return 0;
 }
