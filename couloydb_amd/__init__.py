@@ -316,6 +316,11 @@ class Scanner:
                                        out_max_files, lens, d_hint, hint_cap, ctypes.byref(r), stream)
         return rc, [int(lens[k]) for k in range(min(out_max_files, int(r.n_out_files)))], r
 
+    def set_clock(self, now_ns):
+        """loadIndex's time.Now() for the TTL sweep of the index entries
+        (UnixNano; 0 = the wall clock at each call)."""
+        self.lib.cly_ctx_set_clock(self.ctx, int(now_ns))
+
     KERNELS = ("k_spec", "link", "k_crc", "k_fin", "k_locate", "all")
 
     def kernel_ms(self):

@@ -85,7 +85,7 @@ GEN_DTYPE = np.dtype([("dst", "<u8"), ("key_index", "<u4"), ("value_len", "<u4")
                       ("value_mode", "u1"), ("_pad", "u1"), ("_pad2", "<i4")])
 assert GEN_DTYPE.itemsize == 32
 
-SCAN_SYMBOLS = ["cly_ctx_create", "cly_ctx_destroy", "cly_scan_capacity", "cly_scan",
+SCAN_SYMBOLS = ["cly_ctx_create", "cly_ctx_destroy", "cly_ctx_set_clock", "cly_scan_capacity", "cly_scan",
                 "cly_scan_device", "cly_merge_device", "cly_merge", "cly_hint_positions_device", "cly_hint_scan",
                 "cly_index_device", "cly_index", "cly_append_device", "cly_append",
                 "cly_strerror", "cly_build_info"]
@@ -115,6 +115,8 @@ def load_scan_lib(name="libclyscan.so"):
     if hasattr(lib, "cly_dbg_kernel_ms"):
         lib.cly_dbg_kernel_ms.argtypes = [ctypes.c_void_p, P(ctypes.c_double)]
         lib.cly_dbg_kernel_ms.restype = ctypes.c_int
+    lib.cly_ctx_set_clock.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    lib.cly_ctx_set_clock.restype = None
     lib.cly_scan_capacity.argtypes = [P(ClyFile), ctypes.c_int]
     lib.cly_scan_capacity.restype = ctypes.c_uint64
     lib.cly_scan.argtypes = [ctypes.c_void_p, P(ClyFile), ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,

@@ -30,6 +30,7 @@
 #include "scan_core.h"
 
 extern "C" hipStream_t cly_ctx_stream_internal(cly_ctx* c);
+extern "C" int64_t cly_ctx_now_internal(cly_ctx* c);
 extern "C" int cly_ctx_device_internal(cly_ctx* c);
 
 #define IX_NONE 0xFFFFFFFFFFFFFFFFull
@@ -262,12 +263,15 @@ __device__ __forceinline__ bool ix_same_key(const cly_tuple* tup, const uint64_t
     for (uint32_t q = 0; q < la; q++) if (ka[q] != kb[q]) return false;
     return true;
 }
+__device__ __forceinline__ bool ix_expired(const cly_tuple& t, int64_t now_ns) {
+    return t.data_type == 0 && t.expiration != 0 && t.expiration <= now_ns;
+}
 // group ends: the winner (max order) decides the key; adjacent different keys
 // inside a group mark a hash collision (resolved exactly by k_ixcoll)
 __global__ void __launch_bounds__(256)
 k_ixwin(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, const GMax* __restrict__ g, uint64_t m,
         const cly_tuple* __restrict__ tup, const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases,
-        int nfiles, const uint4* __restrict__ ksig, uint8_t* state, uint8_t* coll, IxTot* tot) {
+        int nfiles, const uint4* __restrict__ ksig, uint8_t* state, uint8_t* coll, IxTot* tot, int64_t now_ns) {
     for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < m; q += (uint64_t)gridDim.x * 256) {
         bool differ = false;
         if (q > 0 && sh[q] == sh[q - 1]) {
@@ -287,14 +291,17 @@ k_ixwin(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, cons
         // scan order, which the stable sort keeps inside a group: the last wins
         const uint32_t w = g ? g[q].idx : IXI(sidx[q]);
         const bool deleted = g ? tup[w].type == 1 : (sidx[q] & IX_DEL) != 0;
-        if (!deleted) state[w] = CLY_IX_LIVE;                   // LogRecordDeleted -> key absent
+        // LogRecordDeleted -> key absent; a String key whose winning put expired is
+        // db.Del'd by loadIndex's TTL sweep (db.go:639-651: not exp.After(now))
+        if (!deleted && !ix_expired(tup[w], now_ns)) state[w] = CLY_IX_LIVE;
     }
 }
 // exact resolution of a collided hash group (one thread): per distinct key the max order
 __global__ void __launch_bounds__(64)
 k_ixcoll(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, const uint64_t* __restrict__ order,
          uint64_t m, const uint8_t* __restrict__ coll, const cly_tuple* __restrict__ tup,
-         const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases, int nfiles, uint8_t* state) {
+         const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases, int nfiles, uint8_t* state,
+         int64_t now_ns) {
     const uint64_t q0 = (uint64_t)blockIdx.x * 64 + threadIdx.x;
     if (q0 >= m || !coll[q0]) return;
     uint64_t q1 = q0 + 1;
@@ -306,7 +313,7 @@ k_ixcoll(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, con
         for (uint64_t b = q0; b < q1 && best; b++)
             if (b != a && order[IXI(sidx[b])] > order[ia] &&
                 ix_same_key(tup, first, bases, nfiles, ia, IXI(sidx[b]))) best = false;
-        if (best && tup[ia].type != 1) state[ia] = CLY_IX_LIVE;
+        if (best && tup[ia].type != 1 && !ix_expired(tup[ia], now_ns)) state[ia] = CLY_IX_LIVE;
     }
 }
 // counts: one atomic per workgroup and counter (a wave-level atomic on one
@@ -362,6 +369,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
                                 cly_index_result* ir, void* stream_v) {
     if (!ctx || !ir || nfiles < 0 || (nfiles && (!files || !file_first || !res))) return CLY_ERR_ARG;
     memset(ir, 0, sizeof(*ir));
+    const int64_t now_ns = cly_ctx_now_internal(ctx);
     uint64_t n = 0;
     for (int i = 0; i < nfiles; i++) {
         if (res[i].status < 0) return res[i].status;           // loadIndex returns the scan's error
@@ -507,12 +515,12 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
             ICK(hipcub::DeviceScan::InclusiveScan(d_tmp, tb, d_g, d_g2, GMaxOp(), (int)m2, st));
         }
         k_ixwin<<<ix_grid(m2), 256, 0, st>>>(d_txkey, d_sidx, m ? d_g2 : nullptr, m2, d_tuples, d_first, d_bases,
-                                             nfiles, d_ksig, d_state, d_coll, d_tot);
+                                             nfiles, d_ksig, d_state, d_coll, d_tot, now_ns);
         ICK(hipMemcpyAsync(&h_tot, d_tot, sizeof(IxTot), hipMemcpyDeviceToHost, st));
         ICK(hipStreamSynchronize(st));
         if (h_tot.n_coll)
             k_ixcoll<<<(unsigned)((m2 + 63) / 64), 64, 0, st>>>(d_txkey, d_sidx, d_order, m2, d_coll, d_tuples, d_first,
-                                                                d_bases, nfiles, d_state);
+                                                                d_bases, nfiles, d_state, now_ns);
     }
     k_ixcount<<<ix_grid(n) < 1024 ? ix_grid(n) : 1024, 256, 0, st>>>(d_state, d_apflag, n, d_tot);
     ICK(hipGetLastError());

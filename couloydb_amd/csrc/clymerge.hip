@@ -198,7 +198,7 @@ k_mplan(const cly_tuple* __restrict__ tup, uint64_t T, const uint8_t* __restrict
         const uint64_t i = b0 + (uint64_t)k * M_NT + threadIdx.x;
         if (i >= T) break;
         uint64_t p = 0;
-        if (live[i]) {
+        if (live[i] == 1) {                 // CLY_IX_LIVE; a CLY_IX_HOST byte is not a verdict
             const cly_tuple t = tup[i];
             if (t.txid_len == 0xFF) { atomicOr(&tot->bad, 1u); plan[i] = 0; continue; }   // parseLogRecordKey panics
             const uint32_t rk = t.key_size - t.txid_len;

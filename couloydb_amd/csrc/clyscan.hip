@@ -37,6 +37,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <atomic>
 #include <thread>
@@ -101,6 +102,8 @@ struct TileLocal { u64 l[4]; };
 #define DF_NONE 4ull
 #define DF_FOF 8ull
 #define DF_REC 16ull
+#define DF_OVF 32ull             // the tile's record starts are not stored (more than POS_CAP)
+#define POS_CAP 2048             // stored record starts per tile (u16, tile-relative)
 
 struct Globals {                 // zeroed per call
     uint32_t nfix;               // tiles listed by k_link for k_refix (reset per link round)
@@ -116,11 +119,12 @@ struct Globals {                 // zeroed per call
 //   [0, 65536)     CRC slicing-by-4 tables T0..T3, 16 replicas: dword (i*64 + t*16 + r)
 //   [65536, +256)  inverse of a zero-byte step (top byte of T0 -> index)
 //   LDS_NIB        nibble tables of A^(CLY_CH * 2^k), k < 7 (8 x 16 words each)
-//   LDS_SH         nibble tables of A^(4 m), m < 16, then of A^(64 m), m <= CLY_NW / 16
+//   LDS_SH         nibble tables of A^(v 16^d) (v < 16, d < 4: a byte shift by one hex
+//                  digit each), then A^65536
 #define LDS_INV 65536
 #define LDS_NIB (LDS_INV + 256)
 #define NIB_LEVELS 7                     // A^(CLY_CH * 2^k), k < 7 (k = 6: one tile)
-#define NSH (16 + CLY_NW / 16 + 1)       // shift tables
+#define NSH 65                           // shift tables
 #define LDS_SH (LDS_NIB + NIB_LEVELS * 128 * 4)
 #define NTAB ((NIB_LEVELS + NSH) * 128)  // words of nibble tables (copied from the context's buffer)
 #define SCAN_LDS (LDS_SH + NSH * 128 * 4)
@@ -288,6 +292,7 @@ struct Chunk {
     gbytes base;
     uint64_t len;
     uint32_t cb, ce;
+    uint32_t tb;                 // file offset of the tile's first byte
     bool last;                   // the file's last chunk
     bool on;                     // the chunk exists (cb < len, or the empty file's chunk 0)
 };
@@ -313,7 +318,7 @@ __device__ __forceinline__ void chain_set(LaneChain& L, int mode) {
 // (every record must be one the writer produces and the chain must leave the
 // chunk at a plausible header, or end at io.EOF at len).  Returns false when a
 // speculative chain is rejected.
-__device__ __forceinline__ bool walk(const Chunk& K, uint32_t p, bool exact, LaneChain& L) {
+__device__ __forceinline__ bool walk_(const Chunk& K, uint32_t p, bool exact, LaneChain& L) {
     chain_set(L, LM_CHAIN);
     L.E = p;
     for (;;) {
@@ -336,6 +341,10 @@ __device__ __forceinline__ bool walk(const Chunk& K, uint32_t p, bool exact, Lan
         if ((uint32_t)h.size < L.minsz) L.minsz = (uint32_t)h.size;
         p += (uint32_t)h.size;
     }
+}
+
+__device__ __forceinline__ bool walk(const Chunk& K, uint32_t p, bool exact, LaneChain& L) {
+    return walk_(K, p, exact, L);
 }
 
 // SWAR byte masks (bit 7 of each byte): byte <= 4 (type / data type), byte
@@ -365,18 +374,15 @@ __device__ __forceinline__ u32x4 piece(const Chunk& K, uint32_t o) {
     return v;
 }
 
-// Phase A for one lane: the chain of its chunk under its own guess.
-__device__ __forceinline__ LaneChain phase_a(const Chunk K) {
-    LaneChain L;
-    if (!K.on) { chain_set(L, LM_OFF); return L; }
-    if (K.cb == 0) { walk(K, 0, true, L); return L; }
-    chain_set(L, LM_NONE);
-    bool found = false;
-    for (int b = 0; b < CLY_NB; b++) {
-        if (found) continue;
+// First candidate record start at or after chunk offset `from` (SWAR filter:
+// the type and data-type bytes are <= 4), NONE32 if none starts in the chunk.
+// The four candidate bits of a word are gathered by one multiply: bits 7, 15,
+// 23, 31 times 1 + 2^7 + 2^14 + 2^21 land in bits 28..31.
+__device__ __forceinline__ uint32_t first_cand(const Chunk& K, uint32_t from) {
+    for (uint32_t b = from / (CLY_BW * 4); b < (uint32_t)CLY_NB; b++) {
         uint32_t w[CLY_BW + 4];
-        if ((uint64_t)K.cb + (uint32_t)((b + 1) * CLY_BW * 4 + 16) <= K.len) {
-            const CLY_GL u32x4* src = (const CLY_GL u32x4*)(K.base + K.cb + (uint32_t)(b * CLY_BW * 4));
+        if ((uint64_t)K.cb + (b + 1) * CLY_BW * 4 + 16 <= K.len) {
+            const CLY_GL u32x4* src = (const CLY_GL u32x4*)(K.base + K.cb + b * CLY_BW * 4);
             #pragma unroll
             for (int k = 0; k < CLY_BW / 4 + 1; k++) {
                 const u32x4 v = src[k];
@@ -385,33 +391,49 @@ __device__ __forceinline__ LaneChain phase_a(const Chunk K) {
         } else {
             #pragma unroll
             for (int k = 0; k < CLY_BW / 4 + 1; k++) {
-                const u32x4 v = piece(K, (uint32_t)(b * CLY_BW * 4 + 16 * k));
+                const u32x4 v = piece(K, b * CLY_BW * 4 + 16 * k);
                 w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
             }
         }
-        // candidate positions of the burst, one bit each (4 per word)
         uint32_t cmk[CLY_BW / 8];
         #pragma unroll
         for (int k = 0; k < CLY_BW / 8; k++) cmk[k] = 0;
         #pragma unroll
         for (int k = 0; k < CLY_BW; k++) {
-            // positions 4k..4k+3: bytes +4, +5 <= 4 and +6 even nonzero
+            // positions 4k..4k+3: bytes +4 (type) and +5 (data type) <= 4
             const uint32_t L1 = swar_le4(w[k + 1]), L2 = swar_le4(w[k + 2]);
-            const uint32_t cm = L1 & __builtin_amdgcn_alignbit(L2, L1, 8) & swar_ks(alignb(w[k + 2], w[k + 1], 2));
-            const uint32_t nib = ((cm >> 7) & 1u) | ((cm >> 14) & 2u) | ((cm >> 21) & 4u) | ((cm >> 28) & 8u);
-            cmk[k >> 3] |= nib << (4 * (k & 7));
+            const uint32_t cm = L1 & __builtin_amdgcn_alignbit(L2, L1, 8);
+            cmk[k >> 3] |= ((cm * 0x204081u) >> 28) << (4 * (k & 7));
         }
+        const uint32_t base = b * CLY_BW * 4;
         #pragma unroll
         for (int k = 0; k < CLY_BW / 8; k++) {
-            uint32_t m = found ? 0u : cmk[k];
-            while (m) {
-                const uint32_t q = K.cb + (uint32_t)(b * CLY_BW * 4 + 32 * k) + (uint32_t)__builtin_ctz(m);
-                m &= m - 1;
-                if (q >= K.ce) { m = 0; break; }
-                LaneChain T;
-                if (walk(K, q, false, T)) { L = T; found = true; m = 0; }
+            const uint32_t lo = base + 32 * k;
+            uint32_t m = cmk[k];
+            if (from > lo) m = from - lo >= 32 ? 0u : (m & (0xFFFFFFFFu << (from - lo)));
+            if (m) {
+                const uint32_t q = K.cb + lo + (uint32_t)__builtin_ctz(m);
+                return q < K.ce ? q : NONE32;
             }
         }
+    }
+    return NONE32;
+}
+
+// Phase A for one lane: the chain of its chunk under its own guess (the first
+// candidate whose speculative walk holds).
+__device__ __forceinline__ LaneChain phase_a(const Chunk K) {
+    LaneChain L;
+    if (!K.on) { chain_set(L, LM_OFF); return L; }
+    if (K.cb == 0) { walk(K, 0, true, L); return L; }
+    chain_set(L, LM_NONE);
+    uint32_t from = 0;
+    for (int it = 0; it < CLY_CH; it++) {
+        const uint32_t q = first_cand(K, from);
+        if (q == NONE32) break;
+        LaneChain T;
+        if (walk(K, q, false, T)) { L = T; break; }
+        from = q + 1 - K.cb;
     }
     return L;
 }
@@ -522,7 +544,7 @@ __device__ __forceinline__ LaneChain lane_load(const uint32_t* __restrict__ lane
 // The tile's LOCAL (its chain under its own entry): flags | records << 32,
 // G | X << 32, crc_last | P_last << 32, tend.  Written by k_spec / k_refix.
 __device__ __forceinline__ void local_store(TileLocal* d, const LaneChain& L, uint32_t G, bool fof, uint32_t tt,
-                                            uint64_t flen, int lane) {
+                                            uint64_t flen, int lane, bool ovf) {
     const u64 bc = __ballot(L.mode == LM_CHAIN), br = __ballot(L.mode == LM_CHAIN && L.cnt > 0);
     const uint32_t c = L.mode == LM_CHAIN ? L.cnt : 0u;
     const uint32_t tile_cnt = shfl_u32(scan_add_incl(c, lane), 63);
@@ -541,6 +563,7 @@ __device__ __forceinline__ void local_store(TileLocal* d, const LaneChain& L, ui
         if (!bc) f0 |= DF_NONE;
         if (fof) f0 |= DF_FOF;
         if (br) f0 |= DF_REC;
+        if (ovf) f0 |= DF_OVF;
         d->l[0] = f0;
         d->l[1] = (u64)Gl | ((u64)X << 32);
         d->l[2] = (u64)crc | ((u64)Pl << 32);
@@ -611,57 +634,78 @@ __device__ __forceinline__ void put_tuple(gtuples out, uint64_t idx, uint64_t ou
 // word w of the chunk (patch_part); XORing delta' into word w changes the
 // register at the chunk end by A^(4 (NW - w)) delta', which the walker adds to
 // `pacc` (two nibble-table products, shift_words), so the stream itself never
-// sees the records.  The walker decodes the lane's records one gather ahead,
-// a record per burst at most, and writes their tuples.
+// sees the records.  The walker decodes the lane's records one gather ahead
+// and writes their tuples, before the stream.
 __device__ __forceinline__ uint32_t mat_mul(const CLY_LDS uint32_t* t, uint32_t v) {
     uint32_t p = 0;
     #pragma unroll
     for (int n = 0; n < 8; n++) p ^= t[n * 16 + ((v >> (4 * n)) & 15u)];
     return p;
 }
-// A^(4 m) v, 1 <= m <= CLY_NW
-__device__ __forceinline__ uint32_t shift_words(const CLY_LDS uint8_t* smem, uint32_t m, uint32_t v) {
+// A^m v (m bytes), 1 <= m <= 65536: one nibble-table product per hex digit of m
+__device__ __forceinline__ uint32_t shift_bytes(const CLY_LDS uint8_t* smem, uint32_t m, uint32_t v) {
     const CLY_LDS uint32_t* t = (const CLY_LDS uint32_t*)(smem + LDS_SH);
     v = mat_mul(t + (m & 15u) * 128, v);
-    return mat_mul(t + (16u + (m >> 4)) * 128, v);
+    v = mat_mul(t + (16u + ((m >> 4) & 15u)) * 128, v);
+    v = mat_mul(t + (32u + ((m >> 8) & 15u)) * 128, v);
+    v = mat_mul(t + (48u + ((m >> 12) & 15u)) * 128, v);
+    if (m >> 16) v = mat_mul(t + 64u * 128, v);
+    return v;
 }
+// The record start P (stored CRC c, the record before it stored cq) in the
+// file's byte stream, as the CRC register sees it: its stored CRC bytes zeroed
+// (XOR c into bytes [P, P+4)), the register checked against the previous
+// record's CRC (XOR ~cq into the register before byte P; not at P = 0) and the
+// record's own CRC started (XOR 0xFFFFFFFF into the register before byte P+4,
+// = XOR K4 = A^-4 0xFFFFFFFF before byte P).  All three are one register XOR
+// before byte P, whose effect at the tile end TE is A^(TE-P) applied to it;
+// bytes of the patch past TE belong to the next tile, and A^(TE-P) accounts
+// for them there exactly (the file fold shifts tile t by one tile more than
+// tile t+1).
+__device__ __forceinline__ uint32_t rec_patch(const CLY_LDS uint8_t* smem, uint32_t TE, uint32_t P, uint32_t c,
+                                              uint32_t cq, uint32_t K4) {
+    return shift_bytes(smem, TE - P, c ^ K4 ^ (P != 0 ? ~cq : 0u));
+}
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+    #pragma unroll
+    for (int o = 32; o; o >>= 1) v ^= (uint32_t)__shfl_xor((int)v, o, 64);
+    return v;
+}
+
 struct Walker {
     uint32_t p, cq, i;
     Gath gt;
 };
 __device__ __forceinline__ void walker_step(const Chunk& K, Walker& W, uint32_t nrec, uint64_t base, uint32_t fid,
                                             gtuples out, uint64_t out_cap, const CLY_LDS uint8_t* smem,
-                                            const CrcLane& cl, uint32_t& pacc, Globals* g) {
+                                            uint32_t K4, uint32_t& pacc, Globals* g) {
     const Hdr h = hdr_at(K.base, W.p, K.len, W.gt);
     put_tuple(out, base + W.i, out_cap, K, W.p, h, fid, g);
-    const uint32_t wlo = K.cb >> 2;
-    uint32_t d;
-    const uint32_t wa = patch_part(smem, cl, W.p, h.crc, W.cq, wlo, wlo + CLY_NW, d);
-    if (wa != NONE32) pacc ^= shift_words(smem, CLY_NW - (wa - wlo), d);
+    pacc ^= rec_patch(smem, K.tb + (uint32_t)CLY_TILE, W.p, h.crc, W.cq, K4);
     W.cq = h.crc;
     W.p += (uint32_t)h.size;
     W.i++;
     if (W.i < nrec && gath_ok(W.p, K.len)) gath_issue(K.base, W.p, W.gt);
 }
 
+// The raw CRC register of the lane's chunk (no patches), 128-B bursts; with
+// `walk` (tiles whose record starts were not stored) the lane first walks its
+// own records: tuples, and their patches into pacc.
 __device__ __forceinline__ uint32_t phase_c_fast(const Chunk& K, const LaneChain& L, const LaneIn& I, bool active,
-                                                 uint32_t fid, gtuples out, uint64_t out_cap,
-                                                 const CLY_LDS uint8_t* smem, const CrcLane& cl, Globals* g) {
-    const uint32_t wlo = K.cb >> 2;
-    uint32_t pacc = 0;
-    if (active && I.spill) {
-        uint32_t d;
-        const uint32_t w = patch_part(smem, cl, I.P_in, I.crc_in, 0u, wlo, wlo + CLY_NW, d);
-        if (w != NONE32) pacc = shift_words(smem, CLY_NW - (w - wlo), d);
+                                                 bool walk, uint32_t fid, gtuples out, uint64_t out_cap,
+                                                 const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t K4,
+                                                 uint32_t& pacc, Globals* g) {
+    if (walk) {
+        Walker W;
+        W.p = L.E; W.cq = I.crc_in; W.i = 0;
+        const uint32_t nrec = (active && L.mode == LM_CHAIN) ? L.cnt : 0u;
+        if (nrec && gath_ok(W.p, K.len)) gath_issue(K.base, W.p, W.gt);
+        for (;;) {
+            const bool need = W.i < nrec;
+            if (!__ballot(need)) break;
+            if (need) walker_step(K, W, nrec, I.base, fid, out, out_cap, smem, K4, pacc, g);
+        }
     }
-    Walker W;
-    W.p = L.E; W.cq = I.crc_in; W.i = 0;
-#ifdef CLY_XNOWALK
-    const uint32_t nrec = 0;                 // timing experiment: no walker
-#else
-    const uint32_t nrec = (active && L.mode == LM_CHAIN) ? L.cnt : 0u;
-#endif
-    if (nrec && gath_ok(W.p, K.len)) gath_issue(K.base, W.p, W.gt);
     uint32_t s = 0;
     const CLY_GL u32x4* src = (const CLY_GL u32x4*)(K.base + K.cb);
     const bool full = (uint64_t)K.cb + CLY_CH <= K.len;
@@ -678,13 +722,6 @@ __device__ __forceinline__ uint32_t phase_c_fast(const Chunk& K, const LaneChain
             #pragma unroll
             for (int k = 0; k < CLY_BW / 4; k++) v[k] = (u32x4){0u, 0u, 0u, 0u};
         }
-        // the records that start in this burst
-        const uint32_t bend = wlo + (uint32_t)(b + 1) * CLY_BW;
-        for (;;) {
-            const bool need = W.i < nrec && (W.p >> 2) < bend;
-            if (!__ballot(need)) break;
-            if (need) walker_step(K, W, nrec, I.base, fid, out, out_cap, smem, cl, pacc, g);
-        }
 #ifdef CLY_XNOCRC
         #pragma unroll
         for (int k = 0; k < CLY_BW / 4; k++) s = s ^ v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;   // timing experiment
@@ -698,7 +735,7 @@ __device__ __forceinline__ uint32_t phase_c_fast(const Chunk& K, const LaneChain
         }
 #endif
     }
-    return s ^ pacc;
+    return s;
 }
 
 // ---------------------------------------------------------------------------
@@ -814,6 +851,7 @@ __device__ __forceinline__ Chunk make_chunk(const DevFile& F, uint32_t tt, int l
     const uint64_t cb = (uint64_t)tt * CLY_TILE + (uint64_t)lane * CLY_CH;
     K.cb = (uint32_t)cb;
     K.ce = (uint32_t)(cb + CLY_CH < F.len ? cb + CLY_CH : F.len);
+    K.tb = (uint32_t)((uint64_t)tt * CLY_TILE);
     K.last = cb + CLY_CH >= F.len;
     K.on = cb < F.len || cb == 0;
     if (!K.on) { K.cb = 0xFFFFFFF0u; K.ce = 0xFFFFFFF0u; }
@@ -849,13 +887,35 @@ __device__ __forceinline__ uint32_t tile_fold(const CLY_LDS uint8_t* smem, uint3
     return r;
 }
 
+// The record starts of a lane's final chain into the tile's list (exact walk).
+__device__ __forceinline__ void emit_positions(const Chunk& K, const LaneChain& L, uint16_t* pos) {
+    if (L.mode != LM_CHAIN) return;
+    uint32_t p = L.E;
+    for (uint32_t i = 0; i < L.cnt; i++) {
+        pos[i] = (uint16_t)(p - K.tb);
+        const Hdr h = hdr_load(K.base, p, K.len);
+        p += (uint32_t)h.size;
+    }
+}
+// Record starts of the tile, in chain order, into pos[t * POS_CAP ...] (the
+// lanes re-walk their final chains; the headers are in L2 by now).  Returns
+// the overflow flag (more than POS_CAP records in the tile).
+__device__ __forceinline__ bool store_positions(const Chunk& K, const LaneChain& L, int lane, uint16_t* tpos) {
+    const uint32_t c = L.mode == LM_CHAIN ? L.cnt : 0u;
+    const uint32_t incl = scan_add_incl(c, lane);
+    const uint32_t tot = shfl_u32(incl, 63);
+    if (tot > POS_CAP) return true;
+    emit_positions(K, L, tpos + (incl - c));
+    return false;
+}
+
 // k_spec: one wave per tile.  Phase A (each lane's chain under its own guess),
 // the lanes made to agree under the tile's guess G (0 for a file's first
 // tile), the lane chains and the tile's LOCAL written out.
 #define SPEC_WAVES 4
 __global__ void __launch_bounds__(64 * SPEC_WAVES)
 k_spec(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
-       TileLocal* loc, uint32_t* lanes, Globals* g) {
+       TileLocal* loc, uint32_t* lanes, uint16_t* pos, Globals* g) {
     const uint32_t t = blockIdx.x * SPEC_WAVES + (threadIdx.x >> 6);
     if (t >= ntiles) return;
     const int lane = threadIdx.x & 63;
@@ -891,7 +951,8 @@ k_spec(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     }
     const uint64_t nl = (uint64_t)ntiles * 64;
     lane_store(lanes, nl, (uint64_t)t * 64 + lane, L);
-    local_store(&loc[t], L, G, fof, tt, F.len, lane);
+    const bool ovf = store_positions(K, L, lane, pos + (uint64_t)t * POS_CAP);
+    local_store(&loc[t], L, G, fof, tt, F.len, lane, ovf);
 }
 
 // k_link: one workgroup per file.  Each thread composes a run of tiles
@@ -1011,8 +1072,8 @@ k_fbase(int nfiles, const uint64_t* __restrict__ ftotal, FileInfo* finfo, Global
 // other wave has it listed).
 __global__ void __launch_bounds__(64 * SPEC_WAVES)
 k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
-        TileLocal* loc, const TileIn* __restrict__ tin, uint32_t* lanes, const uint32_t* __restrict__ fixlist,
-        Globals* g) {
+        TileLocal* loc, const TileIn* __restrict__ tin, uint32_t* lanes, uint16_t* pos,
+        const uint32_t* __restrict__ fixlist, Globals* g) {
     const uint32_t k = blockIdx.x * SPEC_WAVES + (threadIdx.x >> 6);
     if (k >= g->nfix) return;
     const int lane = threadIdx.x & 63;
@@ -1027,7 +1088,8 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
         LaneChain L = lane_load(lanes, nl, (uint64_t)t * 64 + lane);
         L = resolve(K, L, lane, S.dead ? 0u : S.X, S.dead != 0, g);
         lane_store(lanes, nl, (uint64_t)t * 64 + lane, L);
-        local_store(&loc[t], L, NONE32, tt == 0, tt, F.len, lane);
+        const bool ovf = store_positions(K, L, lane, pos + (uint64_t)t * POS_CAP);
+        local_store(&loc[t], L, NONE32, tt == 0, tt, F.len, lane, ovf);
         // state after the tile
         const u64 bc = __ballot(L.mode == LM_CHAIN);
         if (bc) {
@@ -1048,8 +1110,9 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
 #define CRC_WAVES 16
 __global__ void __launch_bounds__(64 * CRC_WAVES)
 k_crc(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
-      const TileIn* __restrict__ tin, const uint32_t* __restrict__ lanes, uint32_t* treg, FileInfo* finfo,
-      const uint32_t* __restrict__ tabs, cly_tuple* out_, uint64_t out_cap, Globals* g) {
+      const TileIn* __restrict__ tin, const TileLocal* __restrict__ loc, const uint32_t* __restrict__ lanes,
+      const uint16_t* __restrict__ pos, uint32_t* treg, FileInfo* finfo, const uint32_t* __restrict__ tabs,
+      cly_tuple* out_, uint64_t out_cap, Globals* g) {
     if (g->nfix) return;                    // the chain is not final yet (k_refix first)
     gtuples out = (gtuples)out_;
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS];
@@ -1057,6 +1120,8 @@ k_crc(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict_
     init_tables(smem, tabs);
     const int lane = threadIdx.x & 63;
     const CrcLane cl = crc_lane(lane);
+    uint32_t K4 = 0xFFFFFFFFu;              // A^-4 0xFFFFFFFF
+    for (int k = 0; k < 4; k++) K4 = crc_unbyte(smem, K4, cl.r4);
     const uint64_t nl = (uint64_t)ntiles * 64;
     for (uint32_t t = blockIdx.x * CRC_WAVES + (threadIdx.x >> 6); t < ntiles; t += gridDim.x * CRC_WAVES) {
         const int f = find_file(tprefix, nfiles, t);
@@ -1067,11 +1132,47 @@ k_crc(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict_
         const uint32_t tt = t - F.first_tile;
         const Chunk K = make_chunk(F, tt, lane);
         const LaneChain L = lane_load(lanes, nl, (uint64_t)t * 64 + lane);
+#ifdef CLY_XFORCEWALK
+        const bool ovf = true;                 // debug build: every tile on the lane walker
+#else
+        const bool ovf = (loc[t].l[0] & DF_OVF) != 0;
+#endif
         uint32_t tile_cnt;
         const LaneIn I = lane_inputs(K, L, S, lane, tile_cnt);
         const bool term_lane = L.mode == LM_CHAIN && L.term != TERM_NONE;
         const bool fast = (L.mode == LM_CHAIN && !term_lane) || L.mode == LM_NONE;
-        uint32_t r = phase_c_fast(K, L, I, fast, F.fid, out, out_cap, smem, cl, g);
+        uint32_t pacc = 0;
+        if (!ovf) {
+            // the tile's records before the terminal lane's, 64 at a time, record
+            // r on lane r % 64: independent header gathers, tuples written to
+            // consecutive slots
+            const u64 bt = __ballot(term_lane);
+            const uint32_t n_par = bt ? shfl_u32((uint32_t)(I.base - S.count), __ffsll((long long)bt) - 1) : tile_cnt;
+            const uint32_t TE = K.tb + (uint32_t)CLY_TILE;
+            const uint16_t* tp = pos + (uint64_t)t * POS_CAP;
+            uint32_t prev = S.crc_last;
+            for (uint32_t r0 = 0; r0 < n_par; r0 += 64) {
+                const uint32_t r = r0 + (uint32_t)lane;
+                const bool act = r < n_par;
+                uint32_t c = 0;
+                uint32_t P = 0;
+                Hdr h;
+                if (act) {
+                    P = K.tb + tp[r];
+                    Gath gt;
+                    if (gath_ok(P, K.len)) gath_issue(K.base, P, gt);
+                    h = hdr_at(K.base, P, K.len, gt);
+                    put_tuple(out, S.count + r, out_cap, K, P, h, F.fid, g);
+                    c = h.crc;
+                }
+                const uint32_t up = shfl_u32(c, lane > 0 ? lane - 1 : 0);
+                const uint32_t cq = lane > 0 ? up : prev;
+                if (act) pacc ^= rec_patch(smem, TE, P, c, cq, K4);
+                const uint32_t lastl = n_par - r0 - 1 < 63u ? n_par - r0 - 1 : 63u;
+                prev = shfl_u32(c, (int)lastl);
+            }
+        }
+        uint32_t r = phase_c_fast(K, L, I, fast, ovf, F.fid, out, out_cap, smem, cl, K4, pacc, g);
         if (term_lane) {
             // the lane holding the file's terminal: k_term (exact path) adds its register
             FileInfo* fo = &finfo[f];
@@ -1079,7 +1180,7 @@ k_crc(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict_
             fo->end_index = I.base + L.cnt; fo->has_term = 1;
         }
         if (!fast) r = 0;
-        r = tile_fold(smem, r, lane);
+        r = tile_fold(smem, r, lane) ^ wave_xor(pacc);
         if (lane == 0) treg[t] = r;
     }
 }
@@ -1108,7 +1209,8 @@ k_term(const DevFile* __restrict__ files, const TileIn* __restrict__ tin, const 
     const Chunk K = make_chunk(F, t - F.first_tile, lane);
     const LaneChain L = lane_load(lanes, (uint64_t)ntiles * 64, (uint64_t)t * 64 + lane);
     uint32_t tile_cnt;
-    const LaneIn I = lane_inputs(K, L, S, lane, tile_cnt);
+    LaneIn I = lane_inputs(K, L, S, lane, tile_cnt);
+    I.spill = false;        // the patch of a record before the lane is in k_crc's register (rec_patch)
     // the terminal lane's chunk into LDS (16 B per lane), read word by word from there
     CLY_LDS u32x4* wl = (CLY_LDS u32x4*)(smem + LDS_SH);
     {
@@ -1219,7 +1321,8 @@ k_locate(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restri
         const Chunk K = make_chunk(F, tt, lane);
         const LaneChain L = lane_load(lanes, nl, (uint64_t)t * 64 + lane);
         uint32_t tile_cnt;
-        const LaneIn I = lane_inputs(K, L, S, lane, tile_cnt);
+        LaneIn I = lane_inputs(K, L, S, lane, tile_cnt);
+        if (lane == 0) I.spill = false;     // a record of the previous tile: in treg[t - 1] (rec_patch)
         // register entering the tile
         uint32_t st = 0;
         for (uint32_t i = F.first_tile; i < t; i++) st = nib_mul(smem, 6, st) ^ treg[i];
@@ -1259,7 +1362,8 @@ struct cly_ctx {
     hipEvent_t ev[8];
     DevFile* d_files; uint32_t* d_tprefix; FileInfo* d_finfo; uint64_t* d_ftotal; int cap_files;
     DevFile* h_files; uint32_t* h_tprefix; FileInfo* h_finfo;
-    TileLocal* d_loc; TileIn* d_tin; uint32_t* d_treg; uint32_t* d_fix; uint32_t* d_lanes; int64_t cap_tiles;
+    TileLocal* d_loc; TileIn* d_tin; uint32_t* d_treg; uint32_t* d_fix; uint32_t* d_lanes; uint16_t* d_pos;
+    int64_t cap_tiles;
     Globals* d_g; Globals* h_g;
     uint32_t* d_tabs;            // nibble tables: A^(CLY_CH 2^k), k < NIB_LEVELS; A^(4 m), m < 16; A^(64 m)
     uint32_t* d_pw;              // x^(8 CLY_TILE 2^k) mod P, k < 40
@@ -1268,6 +1372,7 @@ struct cly_ctx {
     uint8_t* d_bytes; uint64_t cap_bytes;          // host-path staging
     cly_tuple* d_tuples; uint64_t cap_tuples;
     void* merge_scratch;         // clymerge.hip's buffers (grow-only)
+    int64_t now_ns;              // loadIndex's time.Now() for the TTL sweep (0: the wall clock per call)
 };
 extern "C" void cly_merge_scratch_free(void* p);
 
@@ -1289,8 +1394,10 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
         for (int lvl = 0; lvl < NIB_LEVELS + NSH; lvl++) {
             uint64_t nbytes;
             if (lvl < NIB_LEVELS) nbytes = (uint64_t)CLY_CH << lvl;                  // A^(CLY_CH 2^lvl)
-            else if (lvl < NIB_LEVELS + 16) nbytes = 4ull * (uint64_t)(lvl - NIB_LEVELS);   // A^(4 m)
-            else nbytes = 64ull * (uint64_t)(lvl - NIB_LEVELS - 16);                 // A^(64 m)
+            else if (lvl < NIB_LEVELS + 64) {                                        // A^(v 16^d)
+                const int k = lvl - NIB_LEVELS;
+                nbytes = (uint64_t)(k & 15) << (4 * (k >> 4));
+            } else nbytes = 65536;                                                   // A^65536
             const uint32_t xm = cly_x8n(nbytes);
             for (int nb = 0; nb < 8; nb++)
                 for (uint32_t v = 0; v < 16; v++) hn[lvl * 128 + nb * 16 + v] = cly_multmodp(xm, v << (4 * nb));
@@ -1322,7 +1429,7 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     hipStreamSynchronize(c->stream);
     hipFree(c->d_files); hipFree(c->d_tprefix); hipFree(c->d_finfo); hipFree(c->d_ftotal);
     hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_lanes);
-    hipFree(c->d_g); hipFree(c->d_tabs); hipFree(c->d_pw); hipFree(c->d_bytes); hipFree(c->d_tuples);
+    hipFree(c->d_pos); hipFree(c->d_g); hipFree(c->d_tabs); hipFree(c->d_pw); hipFree(c->d_bytes); hipFree(c->d_tuples);
     hipHostFree(c->h_files); hipHostFree(c->h_tprefix); hipHostFree(c->h_finfo); hipHostFree(c->h_g);
     cly_merge_scratch_free(c->merge_scratch);
     for (int i = 0; i < 8; i++) hipEventDestroy(c->ev[i]);
@@ -1357,8 +1464,9 @@ static int ensure_files(cly_ctx* c, int nfiles) {
 
 static int ensure_tiles(cly_ctx* c, int64_t ntiles) {
     if (ntiles <= c->cap_tiles) return CLY_OK;
-    hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_lanes);
+    hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_lanes); hipFree(c->d_pos);
     c->d_loc = nullptr; c->d_tin = nullptr; c->d_treg = nullptr; c->d_fix = nullptr; c->d_lanes = nullptr;
+    c->d_pos = nullptr;
     c->cap_tiles = 0;
     const int64_t cap = ntiles < 1024 ? 1024 : ntiles;
     HIPCK(hipMalloc(&c->d_loc, sizeof(TileLocal) * cap));
@@ -1366,6 +1474,7 @@ static int ensure_tiles(cly_ctx* c, int64_t ntiles) {
     HIPCK(hipMalloc(&c->d_treg, sizeof(uint32_t) * cap));
     HIPCK(hipMalloc(&c->d_fix, sizeof(uint32_t) * cap));
     HIPCK(hipMalloc(&c->d_lanes, sizeof(uint32_t) * LANE_WORDS * 64 * cap));
+    HIPCK(hipMalloc(&c->d_pos, sizeof(uint16_t) * POS_CAP * cap));
     c->cap_tiles = cap;
     return CLY_OK;
 }
@@ -1407,7 +1516,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     const int spec_grid = (int)((ntiles + SPEC_WAVES - 1) / SPEC_WAVES);
     HIPCK(hipEventRecord(c->ev[0], st));
     hipLaunchKernelGGL(k_spec, dim3(spec_grid), dim3(64 * SPEC_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
-                       c->d_loc, c->d_lanes, c->d_g);
+                       c->d_loc, c->d_lanes, c->d_pos, c->d_g);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[1], st));
     // link round 0, and the CRC kernels launched behind it: they return at once
@@ -1421,7 +1530,8 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         int grid = c->crc_grid;
         if ((int64_t)grid * CRC_WAVES > ntiles) grid = (int)((ntiles + CRC_WAVES - 1) / CRC_WAVES);
         hipLaunchKernelGGL(k_crc, dim3(grid), dim3(64 * CRC_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
-                           c->d_tin, c->d_lanes, c->d_treg, c->d_finfo, c->d_tabs, d_out, out_cap, c->d_g);
+                           c->d_tin, c->d_loc, c->d_lanes, c->d_pos, c->d_treg, c->d_finfo, c->d_tabs, d_out, out_cap,
+                           c->d_g);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[3], st));
         hipLaunchKernelGGL(k_term, dim3(nfiles), dim3(64), 0, st, c->d_files, c->d_tin, c->d_lanes, nt32, c->d_treg,
@@ -1464,7 +1574,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
                 }
             }
             hipLaunchKernelGGL(k_refix, dim3((nfix + SPEC_WAVES - 1) / SPEC_WAVES), dim3(64 * SPEC_WAVES), 0, st, c->d_files,
-                               nfiles, c->d_tprefix, nt32, c->d_loc, c->d_tin, c->d_lanes, c->d_fix, c->d_g);
+                               nfiles, c->d_tprefix, nt32, c->d_loc, c->d_tin, c->d_lanes, c->d_pos, c->d_fix, c->d_g);
             HIPCK(hipGetLastError());
             HIPCK(hipMemsetAsync(&c->d_g->nfix, 0, sizeof(uint32_t), st));
             hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, c->d_loc, c->d_tin, c->d_ftotal,
@@ -1616,10 +1726,17 @@ extern "C" int cly_scan(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
         const uint64_t gcap = cly_scan_capacity(files + f0, nf) + 16;
         uint64_t slots = 0;
         cly_stats sg;
-        const int r = cly_scan_device(c, df + f0, nf, c->d_tuples + tbase, gcap, file_first + f0, res + f0, &slots, &sg,
-                                      nullptr);
-        if (r == CLY_ERR_CAPACITY) { over = true; need += slots; rc = CLY_ERR_CAPACITY; tbase += gcap; continue; }
-        if (r != CLY_OK) { rc = r; break; }
+        cly_tuple* gout = c->d_tuples + tbase;
+        cly_tuple* big = nullptr;            // a group of exotic (< 9 B) records: its own buffer
+        int r = cly_scan_device(c, df + f0, nf, gout, gcap, file_first + f0, res + f0, &slots, &sg, nullptr);
+        if (r == CLY_ERR_CAPACITY && slots > gcap) {
+            if (hipStreamSynchronize(c->stream) != hipSuccess || hipMalloc(&big, sizeof(cly_tuple) * (slots + 16)) != hipSuccess) {
+                rc = CLY_ERR_DEVICE; break;
+            }
+            gout = big;
+            r = cly_scan_device(c, df + f0, nf, gout, slots + 16, file_first + f0, res + f0, &slots, &sg, nullptr);
+        }
+        if (r != CLY_OK) { hipFree(big); rc = r; break; }
         st_acc.scan_ms += sg.scan_ms; st_acc.resolve_ms += sg.resolve_ms; st_acc.total_ms += sg.total_ms;
         st_acc.passes = st_acc.passes > sg.passes ? st_acc.passes : sg.passes;
         st_acc.n_chunks += sg.n_chunks; st_acc.bytes += sg.bytes; st_acc.records += sg.records;
@@ -1629,11 +1746,12 @@ extern "C" int cly_scan(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
             need += res[i].n_records;
             if (over || need > out_cap) { over = true; rc = CLY_ERR_CAPACITY; continue; }
             if (res[i].n_records &&
-                hipMemcpyAsync(out + o, c->d_tuples + tbase + file_first[i], sizeof(cly_tuple) * res[i].n_records,
+                hipMemcpyAsync(out + o, gout + file_first[i], sizeof(cly_tuple) * res[i].n_records,
                                hipMemcpyDeviceToHost, c->stream) != hipSuccess) { rc = CLY_ERR_DEVICE; break; }
             file_first[i] = o;
             o += res[i].n_records;
         }
+        if (big) { if (hipStreamSynchronize(c->stream) != hipSuccess) rc = CLY_ERR_DEVICE; hipFree(big); }
         tbase += gcap;
     }
     if (rc != CLY_OK && rc != CLY_ERR_CAPACITY) ready.store(ng);
@@ -1647,6 +1765,13 @@ extern "C" int cly_scan(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
 
 // Context accessors for the merge / index entries (clymerge.hip, clyindex.hip); not in the public header.
 extern "C" hipStream_t cly_ctx_stream_internal(cly_ctx* c) { return c->stream; }
+extern "C" int64_t cly_ctx_now_internal(cly_ctx* c) {
+    if (c->now_ns) return c->now_ns;
+    struct timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    return (int64_t)ts.tv_sec * 1000000000ll + ts.tv_nsec;
+}
+extern "C" void cly_ctx_set_clock(cly_ctx* c, int64_t now_ns) { if (c) c->now_ns = now_ns; }
 extern "C" int cly_ctx_device_internal(cly_ctx* c) { return c->device; }
 extern "C" void** cly_ctx_merge_slot_internal(cly_ctx* c) { return &c->merge_scratch; }
 
@@ -1655,6 +1780,13 @@ extern "C" void** cly_ctx_merge_slot_internal(cly_ctx* c) { return &c->merge_scr
 extern "C" int cly_dbg_kernel_ms(cly_ctx* c, double* out6) {
     for (int i = 0; i < 6; i++) out6[i] = c->kms[i];
     return 6;
+}
+
+// Debug: the stored record starts of tile t (tile-relative) and the tile's LOCAL flags.
+extern "C" int cly_dbg_tile(cly_ctx* c, uint32_t t, uint16_t* pos_out, uint64_t* local4) {
+    hipMemcpy(pos_out, c->d_pos + (uint64_t)t * POS_CAP, sizeof(uint16_t) * POS_CAP, hipMemcpyDeviceToHost);
+    hipMemcpy(local4, c->d_loc + t, sizeof(TileLocal), hipMemcpyDeviceToHost);
+    return POS_CAP;
 }
 
 extern "C" const char* cly_strerror(int code) {

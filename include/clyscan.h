@@ -101,6 +101,10 @@ typedef struct cly_ctx cly_ctx;
 
 int  cly_ctx_create(int device, cly_ctx** out);
 void cly_ctx_destroy(cly_ctx* ctx);
+/* The clock of loadIndex's TTL sweep (db.go:639-651: a String key whose
+ * winning put has Expiration != 0 and not after time.Now() is db.Del'd):
+ * now_ns = UnixNano; 0 (the default) = the wall clock at each index call.    */
+void cly_ctx_set_clock(cly_ctx* ctx, int64_t now_ns);
 
 /* Upper bound on tuples for files whose records are >= 9 bytes (every record
  * the reference writer produces is).  Exotic records shorter than that make

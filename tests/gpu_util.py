@@ -193,12 +193,16 @@ def merge_corpus(seed, n_keys=300, rounds=3, tx_frac=0.3, key_fn=None):
     return bytes(b)
 
 
-def index_states(file_bytes, tuples_per_file):
-    """db.loadIndex (db.go:582-637) restated literally: a map of buffered tx
-    records per txId, updateIndex for String and ListMeta keys, then per record
-    the state the device index reports: 1 = the index points at it, 2 = a
-    Hash/List/Set record the host indexes (tx ones only once committed), 0
-    otherwise."""
+INDEX_NOW = 1_800_000_000_000_000_000      # the clock the index tests give loadIndex (UnixNano, 2027)
+
+
+def index_states(file_bytes, tuples_per_file, now_ns=INDEX_NOW):
+    """db.loadIndex (db.go:582-651) restated literally: a map of buffered tx
+    records per txId, updateIndex for String and ListMeta keys (with the
+    expirations map of String keys), the TTL sweep (a key whose expiration is
+    set and not after now is db.Del'd), then per record the state the device
+    index reports: 1 = the index points at it, 2 = a Hash/List/Set record the
+    host indexes (tx ones only once committed), 0 otherwise."""
     recs = []
     for F, tt in zip(file_bytes, tuples_per_file):
         for t in tt:
@@ -207,6 +211,7 @@ def index_states(file_bytes, tuples_per_file):
             tx, n = mg.varint(key)
             recs.append((key[n:] if n > 0 else key, t, tx))
     index = {mg.STRING: {}, mg.LISTMETA: {}}
+    expirations = {}
     state = [0] * len(recs)
     txrecords = {}
 
@@ -218,8 +223,12 @@ def index_states(file_bytes, tuples_per_file):
         elif dt in index:
             if int(t["type"]) == mg.DELETED:
                 index[dt].pop(rk, None)
+                if dt == mg.STRING:
+                    expirations.pop(rk, None)
             else:
                 index[dt][rk] = i
+                if dt == mg.STRING:
+                    expirations[rk] = int(t["expiration"])
 
     for i, (rk, t, tx) in enumerate(recs):
         if tx == 0:
@@ -233,6 +242,11 @@ def index_states(file_bytes, tuples_per_file):
             txrecords.pop(tx, None)
         else:
             txrecords.setdefault(tx, []).append(i)
+    # db.go:639-651: `if exp.After(time.Now()) ttl.add else db.Del(key)`
+    if now_ns is not None:
+        for rk, exp in expirations.items():
+            if exp != 0 and not exp > now_ns:
+                index[mg.STRING].pop(rk, None)
     for d in index.values():
         for i in d.values():
             state[i] = 1

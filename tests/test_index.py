@@ -14,15 +14,32 @@ import pytest
 
 from oracle import cly_oracle as co
 
-from .gpu_util import index_states, merge_corpus, mixed_corpus, string_live_mask
+from .gpu_util import INDEX_NOW, index_states, merge_corpus, mixed_corpus, string_live_mask
 from .test_merge import oracle_scan, split_files
+
+
+def test_ttl_sweep_restatement():
+    """db.go:639-651: after the load, a String key whose last put has an
+    expiration set and not after now is deleted; keys without one, with a later
+    one, or deleted afterwards are untouched; ListMeta keys have no TTL."""
+    import make_golden as mg
+    now = 1_000
+    recs = [(b"a", 0, mg.STRING), (b"b", 999, mg.STRING), (b"c", 1_000, mg.STRING), (b"d", 1_001, mg.STRING),
+            (b"e", 5, mg.STRING), (b"e", 0, mg.STRING), (b"f", 0, mg.STRING), (b"f", 5, mg.STRING),
+            (b"g", -1, mg.STRING), (b"h", 5, mg.LISTMETA)]
+    F = b"".join(mg.encode_record(mg.key_tx(k, 0), b"v", mg.NORMAL, dt, exp) for k, exp, dt in recs)
+    arr = np.frombuffer(F, np.uint8).copy()
+    tt, _, _ = co.scan_file(arr, 0)
+    st = index_states([arr], [tt], now_ns=now)
+    #         a  b  c  d  e(old) e  f(old) f  g  h
+    assert list(st) == [1, 0, 0, 1, 0, 1, 0, 0, 0, 1]
 
 
 def test_index_restatements_agree():
     for seed in range(6):
         b = merge_corpus(seed, n_keys=150 + 40 * seed)
         arrays, tts, _ = oracle_scan(split_files(b, 1 + seed % 3, random.Random(seed)))
-        st = index_states(arrays, tts)
+        st = index_states(arrays, tts, now_ns=None)
         live = string_live_mask(arrays, tts)
         strings = np.concatenate([t["data_type"] == 0 for t in tts])
         assert ((st == 1) & strings).sum() == live.sum()
@@ -33,6 +50,7 @@ def test_index_restatements_agree():
 def scanner():
     from couloydb_amd import Scanner
     s = Scanner(0)
+    s.set_clock(INDEX_NOW)
     yield s
     s.close()
 
