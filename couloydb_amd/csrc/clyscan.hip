@@ -308,10 +308,22 @@ struct LaneChain {
     uint32_t last, last_crc;     // last record start and its stored CRC
     uint32_t prev_crc;           // stored CRC of the record before `last` (cnt >= 2)
     uint32_t minsz;              // smallest record size
+    uint32_t pk[4];              // the first PK_N record starts, tile-relative u16 pairs (k_spec)
 };
+#define PK_N 8
 __device__ __forceinline__ void chain_set(LaneChain& L, int mode) {
     L.mode = mode; L.E = NONE32; L.x = 0; L.term = TERM_NONE; L.cnt = 0; L.last = NONE32; L.last_crc = 0;
     L.prev_crc = 0; L.minsz = 0xFFFFFFFFu;
+    L.pk[0] = L.pk[1] = L.pk[2] = L.pk[3] = 0;
+}
+// record start `rel` (tile-relative) as the chain's record number cnt (constant indices only)
+__device__ __forceinline__ void pk_put(LaneChain& L, uint32_t cnt, uint32_t rel) {
+    const uint32_t v = (rel & 0xFFFFu) << (16 * (cnt & 1));
+    const uint32_t q = cnt >> 1;                 // value selects, not indexed stores
+    L.pk[0] = L.pk[0] | (q == 0 ? v : 0u);
+    L.pk[1] = L.pk[1] | (q == 1 ? v : 0u);
+    L.pk[2] = L.pk[2] | (q == 2 ? v : 0u);
+    L.pk[3] = L.pk[3] | (q == 3 ? v : 0u);
 }
 
 // Walk from p: exact (ReadLogRecord semantics, every terminal) or speculative
@@ -335,6 +347,7 @@ __device__ __forceinline__ bool walk_(const Chunk& K, uint32_t p, bool exact, La
             return exact || (h.status == CLY_END_EOF && (uint64_t)p == K.len);
         }
         if (!exact && !h.good) return false;
+        pk_put(L, L.cnt, p - K.tb);
         L.cnt++;
         L.prev_crc = L.last_crc;
         L.last = p; L.last_crc = h.crc;
@@ -538,6 +551,7 @@ __device__ __forceinline__ LaneChain lane_load(const uint32_t* __restrict__ lane
     L.last_crc = lanes[4 * nl + i];
     L.prev_crc = 0;
     L.minsz = 0xFFFFFFFFu;
+    L.pk[0] = L.pk[1] = L.pk[2] = L.pk[3] = 0;       // not stored: callers re-walk for record starts
     return L;
 }
 
@@ -897,15 +911,24 @@ __device__ __forceinline__ void emit_positions(const Chunk& K, const LaneChain& 
         p += (uint32_t)h.size;
     }
 }
-// Record starts of the tile, in chain order, into pos[t * POS_CAP ...] (the
-// lanes re-walk their final chains; the headers are in L2 by now).  Returns
+// Record starts of the tile, in chain order, into pos[t * POS_CAP ...] (from
+// the chain's own packed starts; a lane with more than PK_N records re-walks
+// its chain, whose headers are in L2 by now).  Returns
 // the overflow flag (more than POS_CAP records in the tile).
-__device__ __forceinline__ bool store_positions(const Chunk& K, const LaneChain& L, int lane, uint16_t* tpos) {
+__device__ __forceinline__ bool store_positions(const Chunk& K, const LaneChain& L, int lane, uint16_t* tpos,
+                                                bool have_pk) {
     const uint32_t c = L.mode == LM_CHAIN ? L.cnt : 0u;
     const uint32_t incl = scan_add_incl(c, lane);
     const uint32_t tot = shfl_u32(incl, 63);
     if (tot > POS_CAP) return true;
-    emit_positions(K, L, tpos + (incl - c));
+    uint16_t* dst = tpos + (incl - c);
+    if (have_pk && c <= PK_N) {
+        #pragma unroll
+        for (uint32_t i = 0; i < PK_N; i++)
+            if (i < c) dst[i] = (uint16_t)(L.pk[i >> 1] >> (16 * (i & 1)));
+    } else {
+        emit_positions(K, L, dst);
+    }
     return false;
 }
 
@@ -913,7 +936,7 @@ __device__ __forceinline__ bool store_positions(const Chunk& K, const LaneChain&
 // the lanes made to agree under the tile's guess G (0 for a file's first
 // tile), the lane chains and the tile's LOCAL written out.
 #define SPEC_WAVES 4
-__global__ void __launch_bounds__(64 * SPEC_WAVES)
+__global__ void __launch_bounds__(64 * SPEC_WAVES, 5)
 k_spec(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
        TileLocal* loc, uint32_t* lanes, uint16_t* pos, Globals* g) {
     const uint32_t t = blockIdx.x * SPEC_WAVES + (threadIdx.x >> 6);
@@ -951,7 +974,7 @@ k_spec(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     }
     const uint64_t nl = (uint64_t)ntiles * 64;
     lane_store(lanes, nl, (uint64_t)t * 64 + lane, L);
-    const bool ovf = store_positions(K, L, lane, pos + (uint64_t)t * POS_CAP);
+    const bool ovf = store_positions(K, L, lane, pos + (uint64_t)t * POS_CAP, true);
     local_store(&loc[t], L, G, fof, tt, F.len, lane, ovf);
 }
 
@@ -1088,7 +1111,8 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
         LaneChain L = lane_load(lanes, nl, (uint64_t)t * 64 + lane);
         L = resolve(K, L, lane, S.dead ? 0u : S.X, S.dead != 0, g);
         lane_store(lanes, nl, (uint64_t)t * 64 + lane, L);
-        const bool ovf = store_positions(K, L, lane, pos + (uint64_t)t * POS_CAP);
+        // (lanes loaded from the lane arrays carry no packed starts: all re-walked)
+        const bool ovf = store_positions(K, L, lane, pos + (uint64_t)t * POS_CAP, false);
         local_store(&loc[t], L, NONE32, tt == 0, tt, F.len, lane, ovf);
         // state after the tile
         const u64 bc = __ballot(L.mode == LM_CHAIN);
