@@ -2,7 +2,7 @@
 """Benchmark: device-resident CouloyDB log-record scan (decode + CRC -> index tuples).
 
 Contract (see task spec): `python bench.py --gpus N --steps K --warmup W` prints ONE
-JSON line on rank 0.  A step = one full scan (k_spec, k_link, k_crc, k_term,
+JSON line on rank 0.  A step = one full scan (k_spec, k_link, k_crc,
 k_fin and the result read-back) of the configuration's data files, already resident in HBM.  For N>1
 each rank (one per GPU, launched by torch.distributed.run) scans its own fid
 range of the same per-GPU size (weak scaling, no collective on the data path;

@@ -325,7 +325,7 @@ class Scanner:
 
     def kernel_ms(self):
         """Per-kernel HIP-event times (ms) of the last scan_device call: k_spec,
-        the link rounds (k_link + k_fbase + repairs), k_crc, k_term + k_fin,
+        the link rounds (k_link + k_fbase + repairs), k_crc, k_fin,
         k_locate, all."""
         k = (ctypes.c_double * 6)()
         self.lib.cly_dbg_kernel_ms(self.ctx, k)

@@ -30,7 +30,8 @@
 //            output slots and adds one shifted patch per record to the lane's
 //            register, so that the register of the whole file ends at zero iff
 //            every record's CRC matches; the tile's register is folded in-wave;
-//   k_fin    per file: folds the tile registers and checks them;
+//   k_fin    per file: folds the tile registers up to the terminal's and checks
+//            that the fold is zero;
 //   k_locate (only when a file fails) finds the first bad record exactly.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -706,7 +707,7 @@ __device__ __forceinline__ void walker_step(const Chunk& K, Walker& W, uint32_t 
 // `walk` (tiles whose record starts were not stored) the lane first walks its
 // own records: tuples, and their patches into pacc.
 __device__ __forceinline__ uint32_t phase_c_fast(const Chunk& K, const LaneChain& L, const LaneIn& I, bool active,
-                                                 bool walk, uint32_t fid, gtuples out, uint64_t out_cap,
+                                                 bool walk, uint32_t slim, uint32_t fid, gtuples out, uint64_t out_cap,
                                                  const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t K4,
                                                  uint32_t& pacc, Globals* g) {
     if (walk) {
@@ -722,7 +723,10 @@ __device__ __forceinline__ uint32_t phase_c_fast(const Chunk& K, const LaneChain
     }
     uint32_t s = 0;
     const CLY_GL u32x4* src = (const CLY_GL u32x4*)(K.base + K.cb);
-    const bool full = (uint64_t)K.cb + CLY_CH <= K.len;
+    // the stream stops at slim (the terminal lane: T) or the file's end
+    Chunk Ks = K;
+    if ((uint64_t)slim < Ks.len) Ks.len = slim;
+    const bool full = (uint64_t)K.cb + CLY_CH <= Ks.len;
     #pragma unroll 1
     for (int b = 0; b < CLY_NB; b++) {
         u32x4 v[CLY_BW / 4];
@@ -731,7 +735,7 @@ __device__ __forceinline__ uint32_t phase_c_fast(const Chunk& K, const LaneChain
             for (int k = 0; k < CLY_BW / 4; k++) v[k] = src[b * (CLY_BW / 4) + k];
         } else if (active) {
             #pragma unroll
-            for (int k = 0; k < CLY_BW / 4; k++) v[k] = piece(K, (uint32_t)(b * CLY_BW * 4 + 16 * k));
+            for (int k = 0; k < CLY_BW / 4; k++) v[k] = piece(Ks, (uint32_t)(b * CLY_BW * 4 + 16 * k));
         } else {
             #pragma unroll
             for (int k = 0; k < CLY_BW / 4; k++) v[k] = (u32x4){0u, 0u, 0u, 0u};
@@ -1164,15 +1168,20 @@ k_crc(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict_
         uint32_t tile_cnt;
         const LaneIn I = lane_inputs(K, L, S, lane, tile_cnt);
         const bool term_lane = L.mode == LM_CHAIN && L.term != TERM_NONE;
-        const bool fast = (L.mode == LM_CHAIN && !term_lane) || L.mode == LM_NONE;
+        const bool live = L.mode == LM_CHAIN || L.mode == LM_NONE;
+        const uint32_t TE = K.tb + (uint32_t)CLY_TILE;
         uint32_t pacc = 0;
+        if (term_lane) {
+            // the chain's terminal T: the last record is checked there (XOR ~its CRC
+            // into the register before byte T; none when no record precedes T), and
+            // the stream stops at T (the bytes from T on are zeroed)
+            const uint32_t cT = L.cnt ? L.last_crc : I.crc_in;
+            if (L.cnt || I.P_in != NONE32) pacc = shift_bytes(smem, TE - L.x, ~cT);
+        }
         if (!ovf) {
-            // the tile's records before the terminal lane's, 64 at a time, record
-            // r on lane r % 64: independent header gathers, tuples written to
-            // consecutive slots
-            const u64 bt = __ballot(term_lane);
-            const uint32_t n_par = bt ? shfl_u32((uint32_t)(I.base - S.count), __ffsll((long long)bt) - 1) : tile_cnt;
-            const uint32_t TE = K.tb + (uint32_t)CLY_TILE;
+            // the tile's records, 64 at a time, record r on lane r % 64: independent
+            // header gathers, tuples written to consecutive slots
+            const uint32_t n_par = tile_cnt;
             const uint16_t* tp = pos + (uint64_t)t * POS_CAP;
             uint32_t prev = S.crc_last;
             for (uint32_t r0 = 0; r0 < n_par; r0 += 64) {
@@ -1196,63 +1205,19 @@ k_crc(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict_
                 prev = shfl_u32(c, (int)lastl);
             }
         }
-        uint32_t r = phase_c_fast(K, L, I, fast, ovf, F.fid, out, out_cap, smem, cl, K4, pacc, g);
+        uint32_t r = phase_c_fast(K, L, I, live, ovf, term_lane ? L.x : 0xFFFFFFFFu, F.fid, out, out_cap, smem, cl, K4,
+                                  pacc, g);
         if (term_lane) {
-            // the lane holding the file's terminal: k_term (exact path) adds its register
             FileInfo* fo = &finfo[f];
             fo->term_pos = L.x; fo->term_status = L.term; fo->term_tile = t; fo->term_lane = (uint32_t)lane;
-            fo->end_index = I.base + L.cnt; fo->has_term = 1;
+            fo->end_index = I.base + L.cnt; fo->has_term = 1; fo->expect = 0;
         }
-        if (!fast) r = 0;
+        if (!live) r = 0;
         r = tile_fold(smem, r, lane) ^ wave_xor(pacc);
         if (lane == 0) treg[t] = r;
     }
 }
 
-// k_term: one wave per file: the lane holding the file's terminal T, word by
-// word (everything from T on zeroed), its tuples, and its register added to its
-// tile's (shifted to the tile end).
-__global__ void __launch_bounds__(64)
-k_term(const DevFile* __restrict__ files, const TileIn* __restrict__ tin, const uint32_t* __restrict__ lanes,
-       uint32_t ntiles, uint32_t* treg, FileInfo* finfo, const uint32_t* __restrict__ tabs, cly_tuple* out_,
-       uint64_t out_cap, Globals* g) {
-    if (g->nfix) return;
-    gtuples out = (gtuples)out_;
-    __shared__ __attribute__((aligned(16))) unsigned char smem_raw[LDS_SH + CLY_CH];
-    CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
-    init_tables(smem, tabs, NIB_LEVELS * 128);
-    const int lane = threadIdx.x & 63;
-    const int f = blockIdx.x;
-    FileInfo* fo = &finfo[f];
-    if (!fo->has_term) return;                         // k_fin reports it
-    const DevFile F = files[f];
-    const uint32_t t = fo->term_tile, tl = fo->term_lane;
-    LBState S = ti_load(&tin[t]);
-    S.count += fo->first_index;
-    const CrcLane cl = crc_lane(lane);
-    const Chunk K = make_chunk(F, t - F.first_tile, lane);
-    const LaneChain L = lane_load(lanes, (uint64_t)ntiles * 64, (uint64_t)t * 64 + lane);
-    uint32_t tile_cnt;
-    LaneIn I = lane_inputs(K, L, S, lane, tile_cnt);
-    I.spill = false;        // the patch of a record before the lane is in k_crc's register (rec_patch)
-    // the terminal lane's chunk into LDS (16 B per lane), read word by word from there
-    CLY_LDS u32x4* wl = (CLY_LDS u32x4*)(smem + LDS_SH);
-    {
-        Chunk Kt = K;
-        Kt.cb = (uint32_t)((uint64_t)(t - F.first_tile) * CLY_TILE + (uint64_t)tl * CLY_CH);
-        if (lane < CLY_CH / 16) wl[lane] = piece(Kt, 16u * (uint32_t)lane);
-    }
-    __syncthreads();
-    if ((uint32_t)lane == tl) {
-        uint32_t fp, ex;
-        uint64_t fi;
-        uint32_t r = exact_lane(K, L, I, 0u, true, false, F.fid, out, out_cap, smem, cl, g, fp, fi, ex,
-                                (const CLY_LDS uint32_t*)wl);
-        fo->expect = ex;
-        for (int lvl = 0; lvl < 6; lvl++) if ((63u - tl) & (1u << lvl)) r = nib_mul(smem, lvl, r);
-        treg[t] ^= r;
-    }
-}
 
 // ---------------------------------------------------------------------------
 // k_fin: per file, the fold of its tile registers up to the terminal's tile
@@ -1558,8 +1523,6 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
                            c->d_g);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[3], st));
-        hipLaunchKernelGGL(k_term, dim3(nfiles), dim3(64), 0, st, c->d_files, c->d_tin, c->d_lanes, nt32, c->d_treg,
-                           c->d_finfo, c->d_tabs, d_out, out_cap, c->d_g);
         hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_finfo, c->d_treg, c->d_tabs,
                            c->d_pw, c->d_g);
         HIPCK(hipGetLastError());
