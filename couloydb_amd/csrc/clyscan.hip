@@ -106,8 +106,9 @@ struct TileLocal { u64 l[4]; };
 #define DF_OVF 32ull             // the tile's record starts are not stored (more than POS_CAP)
 #define POS_CAP 2048             // stored record starts per tile (u16, tile-relative)
 
+#define LINK_ROUNDS 3            // link rounds launched per call without a host wait (more: host loop)
 struct Globals {                 // zeroed per call
-    uint32_t nfix;               // tiles listed by k_link for k_refix (reset per link round)
+    uint32_t nfix[LINK_ROUNDS];  // tiles listed by k_link round r for k_refix round r + 1
     uint32_t overflow;           // tuples beyond out_cap were dropped
     uint32_t fail;               // internal invariant (never expected)
     uint32_t refix;              // tiles re-resolved over all rounds
@@ -982,85 +983,113 @@ k_spec(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     local_store(&loc[t], L, G, fof, tt, F.len, lane, ovf);
 }
 
-// k_link: one workgroup per file.  Each thread composes a run of tiles
-// trusting their LOCALs (entered live at the run's first guess); thread 0
-// chains the runs; each thread then re-applies its run from the true entering
-// state, writing TileIn and listing the tiles whose LOCAL disagrees with it
-// (a chain tile entered live at X != G, a tile without boundaries entered
-// live at X < its end) for k_refix.
-#define LINK_NT 256
-struct Run { uint32_t X, crc, P, G0; uint64_t cnt; int dead, has, rec, fof; };
-__device__ __forceinline__ void apply_chain(LBState& s, u64 l0, u64 l1, u64 l2) {
-    s.count += l0 >> 32;
-    s.dead = (l0 & DF_TERM) != 0;
-    s.X = (uint32_t)(l1 >> 32);
-    if (l0 & DF_REC) { s.crc_last = (uint32_t)l2; s.P_last = (uint32_t)(l2 >> 32); }
+// k_link: one workgroup per file: the chain state entering every tile.  A
+// tile's LOCAL, trusted, is a function of the state entering it: the first
+// tile of a file sets the state whatever it was (FOF); a tile without
+// boundaries passes the state on (ID); any other tile, entered live, sets
+// position, ended-ness and the last record and adds its records, and leaves a
+// dead state dead (CONST).  Each thread composes its run of tiles, a
+// Kogge-Stone scan over the threads' functions gives every run its entering
+// state, and each thread re-applies its run from there, writing TileIn and
+// checking the LOCALs against it: a chain tile entered live at X != G, or a
+// tile without boundaries entered live at X < its end, is contradicted; the
+// first contradicted tile of the file (the only one whose entry is certain)
+// is listed for k_refix.  Round r > 0 runs only if round r-1 listed tiles.
+#define LINK_NT 1024
+#define RF_ID 0
+#define RF_CONST 1
+#define RF_FOF 2
+struct RunF { uint32_t kind, X, crc, P, dead, rec; uint64_t cnt; };
+__device__ __forceinline__ RunF rf_tile(u64 l0, u64 l1, u64 l2) {
+    RunF f;
+    f.kind = (l0 & DF_FOF) ? RF_FOF : (l0 & DF_NONE) ? RF_ID : RF_CONST;
+    f.X = (uint32_t)(l1 >> 32);
+    f.dead = (l0 & DF_TERM) != 0;
+    f.cnt = l0 >> 32;
+    f.rec = (l0 & DF_REC) || (l0 & DF_FOF);
+    f.crc = (l0 & DF_REC) ? (uint32_t)l2 : 0u;
+    f.P = (l0 & DF_REC) ? (uint32_t)(l2 >> 32) : NONE32;
+    return f;
 }
+// g after f
+__device__ __forceinline__ RunF rf_then(const RunF& f, const RunF& g) {
+    if (g.kind == RF_FOF || f.kind == RF_ID) return g;
+    if (g.kind == RF_ID || f.dead) return f;
+    RunF h = f;
+    h.X = g.X; h.dead = g.dead; h.cnt = f.cnt + g.cnt;
+    if (g.rec) { h.crc = g.crc; h.P = g.P; h.rec = 1; }
+    return h;
+}
+__device__ __forceinline__ LBState rf_apply(const RunF& f, LBState s) {
+    if (f.kind == RF_ID || (f.kind == RF_CONST && s.dead)) return s;
+    s.count = (f.kind == RF_FOF ? 0 : s.count) + f.cnt;
+    s.X = f.X; s.dead = f.dead;
+    if (f.rec) { s.crc_last = f.crc; s.P_last = f.P; }
+    return s;
+}
+#define LINK_PER 4               // tiles per thread held in registers (more: re-read)
 __global__ void __launch_bounds__(LINK_NT)
 k_link(const DevFile* __restrict__ files, const TileLocal* __restrict__ loc, TileIn* tin, uint64_t* ftotal,
-       uint32_t* fixlist, Globals* g) {
-    __shared__ Run runs[LINK_NT];
-    __shared__ LBState ent[LINK_NT];
-    const int f = blockIdx.x;
+       uint32_t* fixlist, Globals* g, int round) {
+    if (round > 0 && g->nfix[round - 1] == 0) return;      // nothing changed since the last round
+    __shared__ RunF rf[2][LINK_NT];
+    __shared__ uint32_t first_bad;
+    const int f = blockIdx.x, tid = threadIdx.x;
     const DevFile F = files[f];
     const uint32_t nt = F.ntile, per = (nt + LINK_NT - 1) / LINK_NT;
-    const uint32_t lo = threadIdx.x * per, hi = lo + per < nt ? lo + per : nt;
-    {
-        Run r;
-        r.X = 0; r.crc = 0; r.P = NONE32; r.G0 = NONE32; r.cnt = 0; r.dead = 0; r.has = 0; r.rec = 0; r.fof = 0;
-        for (uint32_t u = lo; u < hi; u++) {
-            const TileLocal& d = loc[F.first_tile + u];
-            const u64 l0 = d.l[0], l1 = d.l[1], l2 = d.l[2];
-            if (l0 & DF_FOF) { r.fof = 1; r.has = 1; }
-            else if (!r.has) {
-                if (l0 & DF_NONE) continue;
-                r.has = 1; r.G0 = (uint32_t)l1;
-            } else if (r.dead || (l0 & DF_NONE)) continue;
-            r.cnt += l0 >> 32;
-            r.dead = (l0 & DF_TERM) != 0;
-            r.X = (uint32_t)(l1 >> 32);
-            if (l0 & DF_REC) { r.crc = (uint32_t)l2; r.P = (uint32_t)(l2 >> 32); r.rec = 1; }
-        }
-        runs[threadIdx.x] = r;
+    const uint32_t lo = tid * per < nt ? tid * per : nt, hi = lo + per < nt ? lo + per : nt;
+    const TileLocal* L0 = loc + F.first_tile;
+    u64 c0[LINK_PER], c1[LINK_PER], c2[LINK_PER], c3[LINK_PER];
+    #pragma unroll
+    for (int k = 0; k < LINK_PER; k++) {
+        c0[k] = c1[k] = c2[k] = c3[k] = 0;
+        if (lo + k < hi) { c0[k] = L0[lo + k].l[0]; c1[k] = L0[lo + k].l[1]; c2[k] = L0[lo + k].l[2]; c3[k] = L0[lo + k].l[3]; }
     }
+    RunF my;
+    my.kind = RF_ID; my.X = 0; my.crc = 0; my.P = NONE32; my.dead = 0; my.rec = 0; my.cnt = 0;
+    #pragma unroll
+    for (int k = 0; k < LINK_PER; k++)
+        if (lo + k < hi) my = rf_then(my, rf_tile(c0[k], c1[k], c2[k]));
+    for (uint32_t u = lo + LINK_PER; u < hi; u++) my = rf_then(my, rf_tile(L0[u].l[0], L0[u].l[1], L0[u].l[2]));
+    // inclusive Kogge-Stone scan of the run functions
+    int cur = 0;
+    rf[0][tid] = my;
+    if (tid == 0) first_bad = NONE32;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        LBState s;
-        s.count = 0; s.X = 0; s.crc_last = 0; s.P_last = NONE32; s.dead = 0;
-        const uint32_t nr = (nt + per - 1) / per;
-        for (uint32_t k = 0; k < nr; k++) {
-            ent[k] = s;
-            const Run& r = runs[k];
-            if (r.fof) { s.count = r.cnt; s.X = r.X; s.dead = r.dead; s.crc_last = r.rec ? r.crc : 0u; s.P_last = r.rec ? r.P : NONE32; }
-            else if (!s.dead && r.has) {
-                s.count += r.cnt; s.X = r.X; s.dead = r.dead;
-                if (r.rec) { s.crc_last = r.crc; s.P_last = r.P; }
-            }
-        }
-        ftotal[f] = s.count;
+    for (int d = 1; d < LINK_NT; d <<= 1) {
+        RunF v = rf[cur][tid];
+        if (tid >= d) v = rf_then(rf[cur][tid - d], v);
+        rf[cur ^ 1][tid] = v;
+        cur ^= 1;
+        __syncthreads();
     }
-    __shared__ uint32_t first_bad;
-    if (threadIdx.x == 0) first_bad = NONE32;
-    __syncthreads();
-    LBState s = ent[threadIdx.x];
-    for (uint32_t u = lo; u < hi; u++) {
-        const uint32_t t = F.first_tile + u;
-        const TileLocal& d = loc[t];
-        const u64 l0 = d.l[0], l1 = d.l[1], l2 = d.l[2], l3 = d.l[3];
+    LBState s;
+    s.count = 0; s.X = 0; s.crc_last = 0; s.P_last = NONE32; s.dead = 0;
+    if (tid > 0) s = rf_apply(rf[cur][tid - 1], s);
+    if (tid == LINK_NT - 1) {
+        LBState s0;
+        s0.count = 0; s0.X = 0; s0.crc_last = 0; s0.P_last = NONE32; s0.dead = 0;
+        ftotal[f] = rf_apply(rf[cur][tid], s0).count;
+    }
+    bool stop = false;
+    auto visit = [&](uint32_t u, u64 l0, u64 l1, u64 l2, u64 l3) {
         bool bad = false;
         if (l0 & DF_FOF) { s.count = 0; s.X = 0; s.dead = 0; s.crc_last = 0; s.P_last = NONE32; }
         else if (!s.dead) {
             if (l0 & DF_NONE) bad = s.X < (uint32_t)l3;
             else bad = s.X != (uint32_t)l1;
         }
-        ti_store(&tin[t], s, false);
-        if (bad) { atomicMin(&first_bad, t); break; }      // the state after it is not known
-        if ((l0 & DF_FOF) || (!s.dead && !(l0 & DF_NONE))) apply_chain(s, l0, l1, l2);
-    }
+        ti_store(&tin[F.first_tile + u], s, false);
+        if (bad) { atomicMin(&first_bad, F.first_tile + u); stop = true; return; }   // the state after it is not known
+        s = rf_apply(rf_tile(l0, l1, l2), s);
+    };
+    #pragma unroll
+    for (int k = 0; k < LINK_PER; k++)
+        if (!stop && lo + k < hi) visit(lo + k, c0[k], c1[k], c2[k], c3[k]);
+    for (uint32_t u = lo + LINK_PER; u < hi && !stop; u++) visit(u, L0[u].l[0], L0[u].l[1], L0[u].l[2], L0[u].l[3]);
     __syncthreads();
-    if (threadIdx.x == 0 && first_bad != NONE32) {
-        // only the first contradicted tile of the file has a certain entry
-        const uint32_t k = atomicAdd(&g->nfix, 1u);
+    if (tid == 0 && first_bad != NONE32) {
+        const uint32_t k = atomicAdd(&g->nfix[round], 1u);
         fixlist[k] = first_bad;
     }
 }
@@ -1069,7 +1098,8 @@ k_link(const DevFile* __restrict__ files, const TileLocal* __restrict__ loc, Til
 // the file totals) and the call's total.
 #define FB_NT 1024
 __global__ void __launch_bounds__(FB_NT)
-k_fbase(int nfiles, const uint64_t* __restrict__ ftotal, FileInfo* finfo, Globals* g) {
+k_fbase(int nfiles, const uint64_t* __restrict__ ftotal, FileInfo* finfo, Globals* g, int round) {
+    if (round > 0 && g->nfix[round - 1] == 0) return;
     __shared__ uint64_t part[FB_NT];
     __shared__ uint64_t carry;
     if (threadIdx.x == 0) carry = 0;
@@ -1100,9 +1130,9 @@ k_fbase(int nfiles, const uint64_t* __restrict__ ftotal, FileInfo* finfo, Global
 __global__ void __launch_bounds__(64 * SPEC_WAVES)
 k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
         TileLocal* loc, const TileIn* __restrict__ tin, uint32_t* lanes, uint16_t* pos,
-        const uint32_t* __restrict__ fixlist, Globals* g) {
+        const uint32_t* __restrict__ fixlist, Globals* g, int round) {
     const uint32_t k = blockIdx.x * SPEC_WAVES + (threadIdx.x >> 6);
-    if (k >= g->nfix) return;
+    if (k >= g->nfix[round - 1]) return;
     const int lane = threadIdx.x & 63;
     uint32_t t = fixlist[k];
     const int f = find_file(tprefix, nfiles, t);
@@ -1140,8 +1170,8 @@ __global__ void __launch_bounds__(64 * CRC_WAVES)
 k_crc(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
       const TileIn* __restrict__ tin, const TileLocal* __restrict__ loc, const uint32_t* __restrict__ lanes,
       const uint16_t* __restrict__ pos, uint32_t* treg, FileInfo* finfo, const uint32_t* __restrict__ tabs,
-      cly_tuple* out_, uint64_t out_cap, Globals* g) {
-    if (g->nfix) return;                    // the chain is not final yet (k_refix first)
+      cly_tuple* out_, uint64_t out_cap, Globals* g, int round) {
+    if (g->nfix[round]) return;             // the chain is not final yet (k_refix first)
     gtuples out = (gtuples)out_;
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
@@ -1229,11 +1259,11 @@ __device__ __forceinline__ uint32_t xpow_mul(const uint32_t* __restrict__ pw, ui
 #define FIN_NT 256
 __global__ void __launch_bounds__(FIN_NT)
 k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __restrict__ treg,
-      const uint32_t* __restrict__ nib, const uint32_t* __restrict__ pw, Globals* g) {
+      const uint32_t* __restrict__ nib, const uint32_t* __restrict__ pw, Globals* g, int round) {
     __shared__ uint32_t tab[NIB_LEVELS * 128];
     __shared__ uint32_t part[FIN_NT];
     __shared__ uint32_t plen[FIN_NT];
-    if (g->nfix) return;                    // k_crc did not run (link repair first)
+    if (g->nfix[round]) return;             // k_crc did not run (link repair first)
     for (int i = threadIdx.x; i < NIB_LEVELS * 128; i += FIN_NT) tab[i] = nib[i];
     __syncthreads();
     const int f = blockIdx.x;
@@ -1508,11 +1538,21 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
                        c->d_loc, c->d_lanes, c->d_pos, c->d_g);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[1], st));
-    // link round 0, and the CRC kernels launched behind it: they return at once
-    // when the round listed tiles (g->nfix), and run again after the repair
-    hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, c->d_loc, c->d_tin, c->d_ftotal,
-                       c->d_fix, c->d_g);
-    hipLaunchKernelGGL(k_fbase, dim3(1), dim3(FB_NT), 0, st, nfiles, c->d_ftotal, c->d_finfo, c->d_g);
+    // LINK_ROUNDS link rounds (round r > 0: k_refix of round r-1's listed tiles,
+    // then k_link; both return at once when round r-1 listed none), then the
+    // CRC kernels, which return at once if the last round still listed tiles;
+    // no host wait in between.  Files that need more rounds continue on a host
+    // loop (one wait per round).
+    const int RL = LINK_ROUNDS - 1;
+    const int fix_grid = (nfiles + SPEC_WAVES - 1) / SPEC_WAVES;   // at most one listed tile per file and round
+    for (int r = 0; r < LINK_ROUNDS; r++) {
+        if (r > 0)
+            hipLaunchKernelGGL(k_refix, dim3(fix_grid), dim3(64 * SPEC_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
+                               c->d_loc, c->d_tin, c->d_lanes, c->d_pos, c->d_fix, c->d_g, r);
+        hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, c->d_loc, c->d_tin, c->d_ftotal,
+                           c->d_fix, c->d_g, r);
+        hipLaunchKernelGGL(k_fbase, dim3(1), dim3(FB_NT), 0, st, nfiles, c->d_ftotal, c->d_finfo, c->d_g, r);
+    }
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[2], st));
     auto launch_crc = [&]() -> int {
@@ -1520,11 +1560,11 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         if ((int64_t)grid * CRC_WAVES > ntiles) grid = (int)((ntiles + CRC_WAVES - 1) / CRC_WAVES);
         hipLaunchKernelGGL(k_crc, dim3(grid), dim3(64 * CRC_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
                            c->d_tin, c->d_loc, c->d_lanes, c->d_pos, c->d_treg, c->d_finfo, c->d_tabs, d_out, out_cap,
-                           c->d_g);
+                           c->d_g, RL);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[3], st));
         hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_finfo, c->d_treg, c->d_tabs,
-                           c->d_pw, c->d_g);
+                           c->d_pw, c->d_g, RL);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[4], st));
         HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
@@ -1535,38 +1575,23 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     if (rc2) return rc2;
     float ms_fix = 0;
     uint32_t rounds = 1, refixed = 0;
-    if (c->h_g->nfix) {
-        // repair rounds: re-resolve the listed tiles from their true entry, link again
+    for (int r = 0; r < LINK_ROUNDS; r++) if (c->h_g->nfix[r]) { rounds++; refixed += c->h_g->nfix[r]; }
+    if (c->h_g->nfix[RL]) {
+        // more repair rounds on the host: round RL's list, k_link again into slot RL
         HIPCK(hipEventRecord(c->ev[5], st));
-        while (c->h_g->nfix) {
+        while (c->h_g->nfix[RL]) {
             if (c->h_g->fail) break;
             if (rounds > 4096) { fprintf(stderr, "clyscan: chain repair did not converge\n"); return CLY_ERR_NOREPAIR; }
-            const uint32_t nfix = c->h_g->nfix;
+            // k_refix reads slot RL - 1: move the count there, clear slot RL
+            const uint32_t nfix = c->h_g->nfix[RL];
             refixed += nfix;
-            if (getenv("CLY_TRACE") && (rounds < 6 || rounds % 200 == 0)) {
-                // debug: the listed tiles of this round, their entering state and LOCAL
-                static uint32_t hf[8];
-                static TileIn hti[8];
-                static TileLocal hl[8];
-                const uint32_t n = nfix < 8 ? nfix : 8;
-                hipMemcpy(hf, c->d_fix, 4 * n, hipMemcpyDeviceToHost);
-                fprintf(stderr, "round %u: %u listed\n", rounds, nfix);
-                for (uint32_t i = 0; i < n; i++) {
-                    hipMemcpy(&hti[i], c->d_tin + hf[i], sizeof(TileIn), hipMemcpyDeviceToHost);
-                    hipMemcpy(&hl[i], c->d_loc + hf[i], sizeof(TileLocal), hipMemcpyDeviceToHost);
-                    fprintf(stderr, "  tile %u: in X=%u dead=%u fix=%u | local flags=%#llx cnt=%llu G=%u X=%u tend=%llu\n", hf[i],
-                            hti[i].w[2], hti[i].w[3] & 1, hti[i].w[3] >> 1, (unsigned long long)(hl[i].l[0] & 0xff),
-                            (unsigned long long)(hl[i].l[0] >> 32), (uint32_t)hl[i].l[1], (uint32_t)(hl[i].l[1] >> 32),
-                            (unsigned long long)hl[i].l[3]);
-                }
-            }
-            hipLaunchKernelGGL(k_refix, dim3((nfix + SPEC_WAVES - 1) / SPEC_WAVES), dim3(64 * SPEC_WAVES), 0, st, c->d_files,
-                               nfiles, c->d_tprefix, nt32, c->d_loc, c->d_tin, c->d_lanes, c->d_pos, c->d_fix, c->d_g);
-            HIPCK(hipGetLastError());
-            HIPCK(hipMemsetAsync(&c->d_g->nfix, 0, sizeof(uint32_t), st));
+            HIPCK(hipMemcpyAsync(&c->d_g->nfix[RL - 1], &c->d_g->nfix[RL], sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+            HIPCK(hipMemsetAsync(&c->d_g->nfix[RL], 0, sizeof(uint32_t), st));
+            hipLaunchKernelGGL(k_refix, dim3(fix_grid), dim3(64 * SPEC_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
+                               c->d_loc, c->d_tin, c->d_lanes, c->d_pos, c->d_fix, c->d_g, RL);
             hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, c->d_loc, c->d_tin, c->d_ftotal,
-                               c->d_fix, c->d_g);
-            hipLaunchKernelGGL(k_fbase, dim3(1), dim3(FB_NT), 0, st, nfiles, c->d_ftotal, c->d_finfo, c->d_g);
+                               c->d_fix, c->d_g, RL);
+            hipLaunchKernelGGL(k_fbase, dim3(1), dim3(FB_NT), 0, st, nfiles, c->d_ftotal, c->d_finfo, c->d_g, RL);
             HIPCK(hipGetLastError());
             HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
             HIPCK(hipStreamSynchronize(st));
@@ -1600,7 +1625,8 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     HIPCK(hipEventElapsedTime(&ms_crc, c->ev[2], c->ev[3]));
     HIPCK(hipEventElapsedTime(&ms_fin, c->ev[3], c->ev[4]));
     HIPCK(hipEventElapsedTime(&ms_loc, c->ev[4], c->ev[7]));
-    if (rounds > 1) ms_link = 0;   // ev[2] was re-recorded after the repair: link time of round 0 not kept
+    if (ms_fix > 0) ms_link = 0;   // ev[2] was re-recorded after the host repair loop
+    c->h_g->refix = refixed;
     c->kms[0] = ms_spec; c->kms[1] = ms_link + ms_fix; c->kms[2] = ms_crc; c->kms[3] = ms_fin; c->kms[4] = ms_loc;
     c->kms[5] = ms_spec + ms_link + ms_fix + ms_crc + ms_fin + ms_loc;
     if (c->h_g->fail) {
