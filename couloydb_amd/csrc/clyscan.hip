@@ -219,6 +219,12 @@ __device__ __forceinline__ uint32_t patch_delta(const CLY_LDS uint8_t* smem, con
 // expirations); otherwise the exact byte-loop form over global memory.
 struct Gath { uint32_t w[8]; };
 __device__ __forceinline__ bool gath_ok(uint32_t p, uint64_t len) { return (uint64_t)(p & ~3u) + 32 <= len; }
+__device__ __forceinline__ void gath_issue_at(gbytes a, Gath& g) {     // a: 4-aligned, 32 readable bytes
+    const CLY_GL u32x4u* q = (const CLY_GL u32x4u*)a;
+    const u32x4u x = q[0], y = q[1];
+    g.w[0] = x.x; g.w[1] = x.y; g.w[2] = x.z; g.w[3] = x.w;
+    g.w[4] = y.x; g.w[5] = y.y; g.w[6] = y.z; g.w[7] = y.w;
+}
 __device__ __forceinline__ void gath_issue(gbytes base, uint32_t p, Gath& g) {
     const CLY_GL u32x4u* q = (const CLY_GL u32x4u*)(base + (p & ~3u));
     const u32x4u a = q[0], b = q[1];
@@ -1164,13 +1170,111 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
     }
 }
 
+// One record round of k_crc: record r = 64 k + lane of the tile (its start
+// from the tile's list), header decoded from its gather, tuple written, patch
+// added to pacc; cq chains the stored CRCs across lanes and rounds.
+__device__ __forceinline__ void round_finish(const Chunk& K, bool act, uint32_t P, const Gath& gt, uint64_t idx,
+                                             uint32_t TE, uint32_t fid, gtuples out, uint64_t out_cap,
+                                             const CLY_LDS uint8_t* smem, uint32_t K4, uint32_t last, uint32_t& prev,
+                                             uint32_t& pacc, Globals* g, int lane) {
+    uint32_t c = 0;
+    if (act) {
+        const Hdr h = hdr_at(K.base, P, K.len, gt);
+        put_tuple(out, idx, out_cap, K, P, h, fid, g);
+        c = h.crc;
+    }
+    const uint32_t up = shfl_u32(c, lane > 0 ? lane - 1 : 0);
+    const uint32_t cq = lane > 0 ? up : prev;
+    if (act) pacc ^= rec_patch(smem, TE, P, c, cq, K4);
+    prev = shfl_u32(c, (int)last);
+}
+// k_crc's tile body: the lane's raw CRC stream (128-B bursts) with the tile's
+// record rounds interleaved, one round after every RSTEP-th burst: the round's
+// header gathers are issued right after the burst's loads (so waiting for the
+// burst never waits for them) and used after the burst's CRC steps, which hide
+// their latency; all loads are issued unconditionally (a lane without a record
+// reads a zero block) so that the gathers' wait counts stay static.
+#define RSTEP (CLY_NB >= 4 ? CLY_NB / 4 : 1)
+#define NR_IN (CLY_NB / RSTEP)                     // rounds inside the burst loop
+__device__ __forceinline__ uint32_t tile_fused(const Chunk& K, const LaneChain& L, const LaneIn& I, const LBState& S,
+                                               bool active, uint32_t slim, const uint16_t* __restrict__ tp,
+                                               uint32_t n, uint32_t TE, uint32_t fid, gtuples out, uint64_t out_cap,
+                                               const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t K4,
+                                               uint32_t& pacc, gbytes zero32, Globals* g) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t nround = (n + 63) / 64;
+    uint32_t pr[NR_IN];
+    #pragma unroll
+    for (int k = 0; k < NR_IN; k++) {
+        const uint32_t r = 64u * k + lane;
+        pr[k] = tp[r < n ? r : 0];
+    }
+    uint32_t prev = S.crc_last;
+    uint32_t s = 0;
+    const CLY_GL u32x4* src = (const CLY_GL u32x4*)(K.base + K.cb);
+    Chunk Ks = K;
+    if ((uint64_t)slim < Ks.len) Ks.len = slim;
+    const bool full = (uint64_t)K.cb + CLY_CH <= Ks.len;
+    #pragma unroll
+    for (int b = 0; b < CLY_NB; b++) {
+        u32x4 v[CLY_BW / 4];
+        if (active && full) {
+            #pragma unroll
+            for (int k = 0; k < CLY_BW / 4; k++) v[k] = src[b * (CLY_BW / 4) + k];
+        } else if (active) {
+            #pragma unroll
+            for (int k = 0; k < CLY_BW / 4; k++) v[k] = piece(Ks, (uint32_t)(b * CLY_BW * 4 + 16 * k));
+        } else {
+            #pragma unroll
+            for (int k = 0; k < CLY_BW / 4; k++) v[k] = (u32x4){0u, 0u, 0u, 0u};
+        }
+        const int kr = b / RSTEP;
+        const bool rb = (b % RSTEP) == 0 && (uint32_t)kr < nround;
+        Gath gt;
+        uint32_t P = 0;
+        bool act = false;
+        if (rb) {
+            const uint32_t r = 64u * kr + lane;
+            act = r < n;
+            P = K.tb + pr[kr];
+            // every lane loads (a lane without a record, or too close to the file's
+            // end for a 32-B gather, reads the context's zero block)
+            gath_issue_at(act && gath_ok(P, K.len) ? K.base + (P & ~3u) : zero32, gt);
+        }
+        #pragma unroll
+        for (int k = 0; k < CLY_BW / 4; k++) {
+            s = crc_word(smem, s ^ v[k].x, cl);
+            s = crc_word(smem, s ^ v[k].y, cl);
+            s = crc_word(smem, s ^ v[k].z, cl);
+            s = crc_word(smem, s ^ v[k].w, cl);
+        }
+        if (rb) {
+            const uint32_t last = n - 64u * kr - 1 < 63u ? n - 64u * kr - 1 : 63u;
+            round_finish(K, act, P, gt, S.count + 64u * kr + lane, TE, fid, out, out_cap, smem, K4, last, prev, pacc,
+                         g, lane);
+        }
+    }
+    // rounds past the burst loop
+    for (uint32_t kr = NR_IN; kr < nround; kr++) {
+        const uint32_t r = 64u * kr + lane;
+        const bool act = r < n;
+        const uint32_t P = K.tb + tp[act ? r : 0];
+        Gath gt;
+        gath_issue_at(act && gath_ok(P, K.len) ? K.base + (P & ~3u) : zero32, gt);
+        const uint32_t last = n - 64u * kr - 1 < 63u ? n - 64u * kr - 1 : 63u;
+        round_finish(K, act, P, gt, S.count + r, TE, fid, out, out_cap, smem, K4, last, prev, pacc, g, lane);
+    }
+    (void)L; (void)I;
+    return s;
+}
+
 // k_crc: the CRC stream and the tuples, tiles in grid-stride order.
 #define CRC_WAVES 16
 __global__ void __launch_bounds__(64 * CRC_WAVES)
 k_crc(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
       const TileIn* __restrict__ tin, const TileLocal* __restrict__ loc, const uint32_t* __restrict__ lanes,
       const uint16_t* __restrict__ pos, uint32_t* treg, FileInfo* finfo, const uint32_t* __restrict__ tabs,
-      cly_tuple* out_, uint64_t out_cap, Globals* g, int round) {
+      cly_tuple* out_, uint64_t out_cap, Globals* g, int round, const uint8_t* __restrict__ zero32) {
     if (g->nfix[round]) return;             // the chain is not final yet (k_refix first)
     gtuples out = (gtuples)out_;
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS];
@@ -1208,35 +1312,11 @@ k_crc(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict_
             const uint32_t cT = L.cnt ? L.last_crc : I.crc_in;
             if (L.cnt || I.P_in != NONE32) pacc = shift_bytes(smem, TE - L.x, ~cT);
         }
-        if (!ovf) {
-            // the tile's records, 64 at a time, record r on lane r % 64: independent
-            // header gathers, tuples written to consecutive slots
-            const uint32_t n_par = tile_cnt;
-            const uint16_t* tp = pos + (uint64_t)t * POS_CAP;
-            uint32_t prev = S.crc_last;
-            for (uint32_t r0 = 0; r0 < n_par; r0 += 64) {
-                const uint32_t r = r0 + (uint32_t)lane;
-                const bool act = r < n_par;
-                uint32_t c = 0;
-                uint32_t P = 0;
-                Hdr h;
-                if (act) {
-                    P = K.tb + tp[r];
-                    Gath gt;
-                    if (gath_ok(P, K.len)) gath_issue(K.base, P, gt);
-                    h = hdr_at(K.base, P, K.len, gt);
-                    put_tuple(out, S.count + r, out_cap, K, P, h, F.fid, g);
-                    c = h.crc;
-                }
-                const uint32_t up = shfl_u32(c, lane > 0 ? lane - 1 : 0);
-                const uint32_t cq = lane > 0 ? up : prev;
-                if (act) pacc ^= rec_patch(smem, TE, P, c, cq, K4);
-                const uint32_t lastl = n_par - r0 - 1 < 63u ? n_par - r0 - 1 : 63u;
-                prev = shfl_u32(c, (int)lastl);
-            }
-        }
-        uint32_t r = phase_c_fast(K, L, I, live, ovf, term_lane ? L.x : 0xFFFFFFFFu, F.fid, out, out_cap, smem, cl, K4,
-                                  pacc, g);
+        uint32_t r;
+        if (!ovf) r = tile_fused(K, L, I, S, live, term_lane ? L.x : 0xFFFFFFFFu, pos + (uint64_t)t * POS_CAP, tile_cnt,
+                                 TE, F.fid, out, out_cap, smem, cl, K4, pacc, (gbytes)zero32, g);
+        else r = phase_c_fast(K, L, I, live, true, term_lane ? L.x : 0xFFFFFFFFu, F.fid, out, out_cap, smem, cl, K4,
+                              pacc, g);
         if (term_lane) {
             FileInfo* fo = &finfo[f];
             fo->term_pos = L.x; fo->term_status = L.term; fo->term_tile = t; fo->term_lane = (uint32_t)lane;
@@ -1386,6 +1466,7 @@ struct cly_ctx {
     Globals* d_g; Globals* h_g;
     uint32_t* d_tabs;            // nibble tables: A^(CLY_CH 2^k), k < NIB_LEVELS; A^(4 m), m < 16; A^(64 m)
     uint32_t* d_pw;              // x^(8 CLY_TILE 2^k) mod P, k < 40
+    uint8_t* d_zero;             // CLY_CH (>= 256) zero bytes: streams and gathers of lanes without data
     int crc_grid, loc_grid;
     float kms[6];                // last call: k_spec, link rounds (k_link/k_fbase/k_refix), k_crc, k_fin, k_locate, all
     uint8_t* d_bytes; uint64_t cap_bytes;          // host-path staging
@@ -1408,6 +1489,8 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     for (int i = 0; i < 8; i++) HIPCK(hipEventCreate(&c->ev[i]));
     HIPCK(hipMalloc(&c->d_g, sizeof(Globals)));
     HIPCK(hipHostMalloc(&c->h_g, sizeof(Globals), hipHostMallocDefault));
+    HIPCK(hipMalloc(&c->d_zero, CLY_CH < 256 ? 256 : CLY_CH));
+    HIPCK(hipMemset(c->d_zero, 0, CLY_CH < 256 ? 256 : CLY_CH));
     {
         static uint32_t hn[NTAB];
         for (int lvl = 0; lvl < NIB_LEVELS + NSH; lvl++) {
@@ -1448,7 +1531,7 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     hipStreamSynchronize(c->stream);
     hipFree(c->d_files); hipFree(c->d_tprefix); hipFree(c->d_finfo); hipFree(c->d_ftotal);
     hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_lanes);
-    hipFree(c->d_pos); hipFree(c->d_g); hipFree(c->d_tabs); hipFree(c->d_pw); hipFree(c->d_bytes); hipFree(c->d_tuples);
+    hipFree(c->d_pos); hipFree(c->d_g); hipFree(c->d_zero); hipFree(c->d_tabs); hipFree(c->d_pw); hipFree(c->d_bytes); hipFree(c->d_tuples);
     hipHostFree(c->h_files); hipHostFree(c->h_tprefix); hipHostFree(c->h_finfo); hipHostFree(c->h_g);
     cly_merge_scratch_free(c->merge_scratch);
     for (int i = 0; i < 8; i++) hipEventDestroy(c->ev[i]);
@@ -1560,7 +1643,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         if ((int64_t)grid * CRC_WAVES > ntiles) grid = (int)((ntiles + CRC_WAVES - 1) / CRC_WAVES);
         hipLaunchKernelGGL(k_crc, dim3(grid), dim3(64 * CRC_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
                            c->d_tin, c->d_loc, c->d_lanes, c->d_pos, c->d_treg, c->d_finfo, c->d_tabs, d_out, out_cap,
-                           c->d_g, RL);
+                           c->d_g, RL, c->d_zero);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[3], st));
         hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_finfo, c->d_treg, c->d_tabs,
