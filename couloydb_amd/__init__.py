@@ -321,6 +321,11 @@ class Scanner:
         (UnixNano; 0 = the wall clock at each call)."""
         self.lib.cly_ctx_set_clock(self.ctx, int(now_ns))
 
+    def open_db(self, path):
+        """NewCouloyDB's index load (db.go:442-655) from the `%09d.cly` files of
+        directory `path`, on this scanner's device (cly_db_open)."""
+        return LoadedDB(self, path)
+
     KERNELS = ("k_spec", "link", "k_crc", "k_fin", "k_locate", "all")
 
     def kernel_ms(self):
@@ -351,3 +356,62 @@ class Scanner:
 
 def build_info(lib="libclyscan.so"):
     return _abi.load_scan_lib(lib).cly_build_info().decode()
+
+
+class LoadedDB:
+    """The indexes NewCouloyDB holds after loadIndex (include/clyload.h):
+    String / ListMeta key -> LogPos, Hash (key, field) -> LogPos, and values by
+    position (getLogRecordByPos).  get/hget return the value bytes, or raise
+    KeyError for public.ErrKeyNotFound."""
+
+    def __init__(self, scanner, path):
+        self.lib = scanner.lib
+        self.db = ctypes.c_void_p()
+        self.stats = _abi.ClyLoadStats()
+        rc = self.lib.cly_db_open(scanner.ctx, os.fsencode(path), ctypes.byref(self.db), ctypes.byref(self.stats))
+        if rc != 0:
+            raise (ErrInvalidCRC if rc == ERR_CRC else ScanError)(rc, self.lib.cly_strerror(rc).decode())
+
+    def close(self):
+        if self.db:
+            self.lib.cly_db_close(self.db)
+            self.db = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _pos(self, rc, pos, what):
+        if rc == _abi.DB_NOT_FOUND:
+            raise KeyError(what)
+        if rc != 0:
+            raise ScanError(rc, self.lib.cly_strerror(rc).decode())
+        return LogPos(pos.fid, pos.offset)
+
+    def pos(self, key):
+        p = _abi.ClyPos()
+        return self._pos(self.lib.cly_db_get(self.db, key, len(key), ctypes.byref(p)), p, key)
+
+    def hpos(self, key, field):
+        p = _abi.ClyPos()
+        return self._pos(self.lib.cly_db_hget(self.db, key, len(key), field, len(field), ctypes.byref(p)), p,
+                         (key, field))
+
+    def value(self, pos):
+        p = _abi.ClyPos()
+        p.fid, p.offset = pos.fid, pos.offset
+        n = ctypes.c_uint64()
+        rc = self.lib.cly_db_value(self.db, ctypes.byref(p), None, 0, ctypes.byref(n))
+        buf = ctypes.create_string_buffer(max(1, n.value))
+        rc = self.lib.cly_db_value(self.db, ctypes.byref(p), buf, n.value, ctypes.byref(n))
+        if rc != 0:
+            raise ScanError(rc, self.lib.cly_strerror(rc).decode())
+        return buf.raw[:n.value]
+
+    def get(self, key):
+        return self.value(self.pos(key))
+
+    def hget(self, key, field):
+        return self.value(self.hpos(key, field))

@@ -90,6 +90,20 @@ SCAN_SYMBOLS = ["cly_ctx_create", "cly_ctx_destroy", "cly_ctx_set_clock", "cly_s
                 "cly_index_device", "cly_index", "cly_append_device", "cly_append",
                 "cly_strerror", "cly_build_info"]
 GEN_SYMBOLS = ["cly_gen_record_size", "cly_gen_layout", "cly_gen_encode"]
+LOAD_SYMBOLS = ["cly_db_open", "cly_db_close", "cly_db_get", "cly_db_listmeta", "cly_db_hget", "cly_db_value"]
+DB_NOT_FOUND = 1
+
+
+class ClyPos(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_int64), ("fid", ctypes.c_uint32), ("_pad", ctypes.c_uint32)]
+
+
+class ClyLoadStats(ctypes.Structure):
+    _fields_ = [("list_map_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double), ("scan_ms", ctypes.c_double),
+                ("index_ms", ctypes.c_double), ("insert_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("n_files", ctypes.c_uint64), ("bytes", ctypes.c_uint64), ("records", ctypes.c_uint64),
+                ("str_keys", ctypes.c_uint64), ("listmeta_keys", ctypes.c_uint64), ("hash_fields", ctypes.c_uint64),
+                ("active_fid", ctypes.c_uint32), ("_pad", ctypes.c_uint32), ("write_off", ctypes.c_int64)]
 
 _libs = {}
 
@@ -115,6 +129,19 @@ def load_scan_lib(name="libclyscan.so"):
     if hasattr(lib, "cly_dbg_kernel_ms"):
         lib.cly_dbg_kernel_ms.argtypes = [ctypes.c_void_p, P(ctypes.c_double)]
         lib.cly_dbg_kernel_ms.restype = ctypes.c_int
+    lib.cly_db_open.argtypes = [ctypes.c_void_p, ctypes.c_char_p, P(ctypes.c_void_p), ctypes.c_void_p]
+    lib.cly_db_open.restype = ctypes.c_int
+    lib.cly_db_close.argtypes = [ctypes.c_void_p]
+    lib.cly_db_close.restype = None
+    for fn in ("cly_db_get", "cly_db_listmeta"):
+        getattr(lib, fn).argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p]
+        getattr(lib, fn).restype = ctypes.c_int
+    lib.cly_db_hget.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
+                                ctypes.c_void_p]
+    lib.cly_db_hget.restype = ctypes.c_int
+    lib.cly_db_value.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                 P(ctypes.c_uint64)]
+    lib.cly_db_value.restype = ctypes.c_int
     lib.cly_ctx_set_clock.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     lib.cly_ctx_set_clock.restype = None
     lib.cly_scan_capacity.argtypes = [P(ClyFile), ctypes.c_int]

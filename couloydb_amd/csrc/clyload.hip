@@ -1,0 +1,290 @@
+// clyload.hip — the index load of NewCouloyDB on the device (host driver of
+// libclyscan; include/clyload.h).
+//
+// Restates, from data files on disk to a queryable index:
+//   NewCouloyDB -> loadDataFile (db.go:442-485: the `%09d.cly` files of the
+//   directory, fids ascending, the last one the active file)
+//   -> loadIndex (db.go:487-655: every record of every file in fid order,
+//   tx buffering by txId, updateIndex, the TTL sweep).
+// The files are mmap'd, copied to HBM, scanned (cly_scan_device) and the
+// String/ListMeta index state of every record is rebuilt on the device
+// (cly_index_device).  The tuples and states come back, and the host builds
+// what updateIndex puts in the MemTables (meta/memTable.go:15-30): the String
+// and ListMeta maps from the LIVE records, and the Hash maps (decodeFieldKey,
+// txnHash.go:249-251) by replaying the Hash records in application order (a
+// record without a txId at once, a tx record at its TxnCommit marker,
+// db.go:600-627).  List (gob-encoded big.Float sequence keys) and Set (consistent
+// hash of the member) indexes are not built here.
+//
+// The host inserts are timed separately from the device work.
+#include <hip/hip_runtime.h>
+#include <dirent.h>
+#include <fcntl.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/clyload.h"
+#include "scan_core.h"
+
+extern "C" hipStream_t cly_ctx_stream_internal(cly_ctx* c);
+extern "C" int cly_ctx_device_internal(cly_ctx* c);
+
+struct Mapped {
+    uint32_t fid;
+    const uint8_t* p;
+    uint64_t len;
+};
+
+struct cly_db {
+    std::vector<Mapped> files;
+    std::vector<cly_tuple> tuples;
+    std::vector<uint8_t> state;
+    std::vector<uint64_t> first;
+    std::unordered_map<std::string, cly_pos> str, listmeta;
+    std::unordered_map<std::string, std::unordered_map<std::string, cly_pos>> hash;
+};
+
+static double now_ms() {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
+static const uint8_t* file_of(const cly_db* db, uint32_t fid) {
+    for (const Mapped& m : db->files) if (m.fid == fid) return m.p;
+    return nullptr;
+}
+
+// realKey of tuple t (parseLogRecordKey, db.go:706-710)
+static std::string real_key(const cly_db* db, const cly_tuple& t) {
+    const uint8_t* f = file_of(db, t.fid);
+    const uint32_t tl = t.txid_len == 0xFF ? 0 : t.txid_len;
+    return std::string((const char*)f + t.offset + t.header_size + tl, t.key_size - tl);
+}
+
+// decodeFieldKey (txnHash.go:249-251 -> bytex.DecodeByteSlices)
+static bool field_key(const std::string& k, std::string& key, std::string& field) {
+    int n1 = 0, n2 = 0;
+    const int64_t ks = go_varint((const uint8_t*)k.data(), (int64_t)k.size(), n1);
+    if (n1 <= 0) return false;
+    go_varint((const uint8_t*)k.data() + n1, (int64_t)k.size() - n1, n2);
+    if (n2 <= 0) return false;
+    const int64_t idx = n1 + n2;
+    if (ks < 0 || idx + ks > (int64_t)k.size()) return false;
+    key = k.substr((size_t)idx, (size_t)ks);
+    field = k.substr((size_t)(idx + ks));
+    return true;
+}
+
+static int list_files(const char* dir, std::vector<Mapped>& out) {
+    DIR* d = opendir(dir);
+    if (!d) return CLY_ERR_ARG;
+    struct dirent* e;
+    std::vector<uint32_t> fids;
+    while ((e = readdir(d))) {
+        // data/dataFile.go:20-23 + public/preset.go:6: fmt.Sprintf("%09d", fid) + ".cly"
+        const size_t n = strlen(e->d_name);
+        if (n != 13 || strcmp(e->d_name + 9, ".cly") != 0) continue;
+        bool digits = true;
+        for (int i = 0; i < 9; i++) digits &= e->d_name[i] >= '0' && e->d_name[i] <= '9';
+        if (digits) fids.push_back((uint32_t)strtoul(std::string(e->d_name, 9).c_str(), nullptr, 10));
+    }
+    closedir(d);
+    std::sort(fids.begin(), fids.end());
+    for (uint32_t fid : fids) {
+        char path[4096];
+        snprintf(path, sizeof(path), "%s/%09u.cly", dir, fid);
+        const int fd = open(path, O_RDONLY);
+        if (fd < 0) return CLY_ERR_ARG;
+        struct stat sb;
+        if (fstat(fd, &sb) != 0) { close(fd); return CLY_ERR_ARG; }
+        Mapped m;
+        m.fid = fid;
+        m.len = (uint64_t)sb.st_size;
+        m.p = nullptr;
+        if (m.len) {
+            void* p = mmap(nullptr, m.len, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+            if (p == MAP_FAILED) { close(fd); return CLY_ERR_ARG; }
+            m.p = (const uint8_t*)p;
+        }
+        close(fd);
+        out.push_back(m);
+    }
+    return CLY_OK;
+}
+
+extern "C" void cly_db_close(cly_db* db) {
+    if (!db) return;
+    for (Mapped& m : db->files) if (m.p) munmap((void*)m.p, m.len);
+    delete db;
+}
+
+#define DCK(x) do { if ((x) != hipSuccess) { rc = CLY_ERR_DEVICE; goto done; } } while (0)
+
+extern "C" int cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load_stats* st) {
+    if (!ctx || !dir || !out) return CLY_ERR_ARG;
+    *out = nullptr;
+    cly_load_stats s;
+    memset(&s, 0, sizeof(s));
+    const double t0 = now_ms();
+    cly_db* db = new cly_db();
+    int rc = list_files(dir, db->files);
+    const int nf = (int)db->files.size();
+    uint8_t* d_bytes = nullptr;
+    cly_tuple* d_tup = nullptr;
+    uint8_t* d_state = nullptr;
+    std::vector<cly_file> hf(nf ? nf : 1), df(nf ? nf : 1);
+    std::vector<cly_file_result> res(nf ? nf : 1);
+    uint64_t total = 0, need = 0, cap = 0;
+    hipStream_t strm = cly_ctx_stream_internal(ctx);
+    double t1, t2, t3, t4, t5;
+    cly_index_result ir;
+    if (rc != CLY_OK) goto done;
+    t1 = now_ms();
+    s.list_map_ms = t1 - t0;
+    s.n_files = (uint64_t)nf;
+    if (nf) s.active_fid = db->files[nf - 1].fid;
+    DCK(hipSetDevice(cly_ctx_device_internal(ctx)));
+    for (int i = 0; i < nf; i++) {
+        hf[i].base = db->files[i].p; hf[i].len = db->files[i].len; hf[i].fid = db->files[i].fid;
+        total += (hf[i].len + 4095) & ~4095ull;
+        s.bytes += hf[i].len;
+    }
+    DCK(hipMalloc((void**)&d_bytes, total + 4096));
+    {
+        uint64_t off = 0;
+        for (int i = 0; i < nf; i++) {
+            df[i] = hf[i];
+            df[i].base = d_bytes + off;
+            if (hf[i].len) DCK(hipMemcpyAsync(d_bytes + off, hf[i].base, hf[i].len, hipMemcpyHostToDevice, strm));
+            off += (hf[i].len + 4095) & ~4095ull;
+        }
+    }
+    DCK(hipStreamSynchronize(strm));
+    t2 = now_ms();
+    s.h2d_ms = t2 - t1;
+    cap = cly_scan_capacity(hf.data(), nf) + 16;
+    DCK(hipMalloc((void**)&d_tup, sizeof(cly_tuple) * cap));
+    db->first.resize(nf ? nf : 1);
+    rc = cly_scan_device(ctx, df.data(), nf, d_tup, cap, db->first.data(), res.data(), &need, nullptr, nullptr);
+    if (rc != CLY_OK) goto done;
+    for (int i = 0; i < nf; i++)
+        if (res[i].status < 0) { rc = res[i].status; goto done; }         // loadIndex returns the read error
+    if (nf) s.write_off = res[nf - 1].end_offset;                         // db.go:632-634
+    t3 = now_ms();
+    s.scan_ms = t3 - t2;
+    DCK(hipMalloc((void**)&d_state, need ? need : 1));
+    rc = cly_index_device(ctx, df.data(), nf, d_tup, db->first.data(), res.data(), d_state, &ir, nullptr);
+    if (rc != CLY_OK) goto done;
+    db->tuples.resize(need);
+    db->state.resize(need);
+    if (need) {
+        DCK(hipMemcpyAsync(db->tuples.data(), d_tup, sizeof(cly_tuple) * need, hipMemcpyDeviceToHost, strm));
+        DCK(hipMemcpyAsync(db->state.data(), d_state, need, hipMemcpyDeviceToHost, strm));
+    }
+    DCK(hipStreamSynchronize(strm));
+    t4 = now_ms();
+    s.index_ms = t4 - t3;
+    s.records = need;
+    {
+        // MemTable inserts (updateIndex, db.go:511-575): String / ListMeta from the
+        // device's LIVE records; Hash replayed in application order
+        db->str.reserve((size_t)ir.n_live);
+        std::unordered_map<int64_t, std::vector<uint64_t>> txbuf;
+        auto hash_apply = [&](uint64_t i) {
+            const cly_tuple& t = db->tuples[i];
+            std::string key, field;
+            // updateIndex decodes log.Key: the realKey for a buffered tx record
+            // (db.go:620), but the key as stored, txId varint included, for a
+            // record applied at once (db.go:600-602, 523)
+            std::string k = real_key(db, t);
+            if (t.tx_id == 0 && t.txid_len != 0xFF) {
+                const uint8_t* f = file_of(db, t.fid);
+                k = std::string((const char*)f + t.offset + t.header_size, t.key_size);
+            }
+            if (!field_key(k, key, field)) return;
+            auto& idx = db->hash[key];
+            if (t.type == 1) idx.erase(field);                               // LogRecordDeleted
+            else { cly_pos p; p.offset = t.offset; p.fid = t.fid; p._pad = 0; idx[field] = p; }
+        };
+        for (uint64_t i = 0; i < need; i++) {
+            const cly_tuple& t = db->tuples[i];
+            if (db->state[i] == CLY_IX_LIVE) {
+                cly_pos p;
+                p.offset = t.offset; p.fid = t.fid; p._pad = 0;
+                (t.data_type == 3 ? db->listmeta : db->str)[real_key(db, t)] = p;
+            }
+            // the Hash records, and the tx markers that decide them
+            if (t.tx_id == 0) { if (t.data_type == 1) hash_apply(i); continue; }
+            if (t.type == 4) continue;                                        // TxnBegin
+            if (t.type == 2) {                                                // TxnCommit
+                auto it = txbuf.find(t.tx_id);
+                if (it != txbuf.end()) { for (uint64_t j : it->second) hash_apply(j); txbuf.erase(it); }
+            } else if (t.type == 3) txbuf.erase(t.tx_id);                    // TxnRollback
+            else if (t.data_type == 1) txbuf[t.tx_id].push_back(i);
+        }
+        s.str_keys = db->str.size();
+        s.listmeta_keys = db->listmeta.size();
+        for (auto& kv : db->hash) s.hash_fields += kv.second.size();
+    }
+    t5 = now_ms();
+    s.insert_ms = t5 - t4;
+    s.total_ms = t5 - t0;
+done:
+    hipFree(d_bytes); hipFree(d_tup); hipFree(d_state);
+    if (st) *st = s;
+    if (rc != CLY_OK) { cly_db_close(db); return rc; }
+    *out = db;
+    return CLY_OK;
+}
+
+static int found(const cly_pos* src, cly_pos* pos) {
+    if (pos) *pos = *src;
+    return CLY_OK;
+}
+
+extern "C" int cly_db_get(cly_db* db, const uint8_t* key, uint64_t klen, cly_pos* pos) {
+    if (!db) return CLY_ERR_ARG;
+    auto it = db->str.find(std::string((const char*)key, klen));
+    return it == db->str.end() ? CLY_DB_NOT_FOUND : found(&it->second, pos);
+}
+
+extern "C" int cly_db_listmeta(cly_db* db, const uint8_t* key, uint64_t klen, cly_pos* pos) {
+    if (!db) return CLY_ERR_ARG;
+    auto it = db->listmeta.find(std::string((const char*)key, klen));
+    return it == db->listmeta.end() ? CLY_DB_NOT_FOUND : found(&it->second, pos);
+}
+
+extern "C" int cly_db_hget(cly_db* db, const uint8_t* key, uint64_t klen, const uint8_t* field, uint64_t flen,
+                           cly_pos* pos) {
+    if (!db) return CLY_ERR_ARG;
+    auto h = db->hash.find(std::string((const char*)key, klen));
+    if (h == db->hash.end()) return CLY_DB_NOT_FOUND;
+    auto it = h->second.find(std::string((const char*)field, flen));
+    return it == h->second.end() ? CLY_DB_NOT_FOUND : found(&it->second, pos);
+}
+
+// getLogRecordByPos (db.go:680-704): the record at pos, its value.  The CRC
+// was checked by the load; the header is decoded again here.
+extern "C" int cly_db_value(cly_db* db, const cly_pos* pos, uint8_t* buf, uint64_t cap, uint64_t* vlen) {
+    if (!db || !pos || !vlen) return CLY_ERR_ARG;
+    const Mapped* m = nullptr;
+    for (const Mapped& f : db->files) if (f.fid == pos->fid) m = &f;
+    if (!m || pos->offset < 0 || (uint64_t)pos->offset >= m->len) return CLY_ERR_ARG;
+    const Hdr h = step_hdr(m->p, pos->offset, (int64_t)m->len, pos->offset);
+    if (h.status != REC_OK) return h.status;
+    *vlen = h.vs;
+    if (buf && cap >= h.vs) memcpy(buf, m->p + pos->offset + h.hsz + h.ks, h.vs);
+    return (buf && cap < h.vs) ? CLY_ERR_CAPACITY : CLY_OK;
+}

@@ -16,7 +16,7 @@
 #include "../../include/clyscan.h"
 #include "crc_gf.h"
 
-#define CLY_DEV __device__ __forceinline__
+#define CLY_DEV __host__ __device__ __forceinline__     // host too: clyload.hip's getLogRecordByPos
 #define CLY_LDS __attribute__((address_space(3)))
 
 #ifndef CLY_CH

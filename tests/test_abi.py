@@ -28,7 +28,7 @@ def declared_functions(header):
 
 
 @pytest.mark.parametrize("header,lib", [("clyscan.h", "libclyscan.so"), ("clyscan.h", "libclyscan_small.so"),
-                                        ("clygen.h", "libclygen.so")])
+                                        ("clyload.h", "libclyscan.so"), ("clygen.h", "libclygen.so")])
 def test_library_exports_header_symbols(header, lib):
     path = _abi.lib_path(lib)
     assert os.path.exists(path), "build the libraries first (__graft_entry__.build())"
@@ -37,7 +37,7 @@ def test_library_exports_header_symbols(header, lib):
     assert len(names) >= 3
     for n in names:
         assert hasattr(h, n), "%s missing from %s" % (n, lib)
-    expect = _abi.SCAN_SYMBOLS if header == "clyscan.h" else _abi.GEN_SYMBOLS
+    expect = {"clyscan.h": _abi.SCAN_SYMBOLS, "clyload.h": _abi.LOAD_SYMBOLS}.get(header, _abi.GEN_SYMBOLS)
     assert sorted(expect) == names
 
 
