@@ -66,11 +66,11 @@ def make_workload(name, torch, rank=0, device=0, seed=0x434C59, size=32 * 2**30)
     elif name == "c3":
         rng = np.random.default_rng(seed + 3)
         nfiles_target = 128
-        vl = _zipf_lengths(int(size / 3500), rng)
-        # trim/extend to ~32 GiB
-        sizes = vl.astype(np.int64) + 20
-        cum = np.cumsum(sizes)
-        vl = vl[: int(np.searchsorted(cum, size - nfiles_target * 70000))]
+        # enough draws for 32 GiB, cut where the records fill 128 files of
+        # DataFileSize (each file loses less than one record to the rotation)
+        vl = _zipf_lengths(int(size / 2000), rng)
+        cum = np.cumsum(vl.astype(np.int64) + 20)
+        vl = vl[: int(np.searchsorted(cum, size - nfiles_target * 40000))]
     elif name == "c5":
         # BASELINE config 5 per GPU: a 32-GiB fid range of the C2/C3 mix (16 GiB of
         # 256-B values, then 16 GiB of Zipf value sizes); 8 GPUs -> 256 GiB
@@ -78,9 +78,9 @@ def make_workload(name, torch, rank=0, device=0, seed=0x434C59, size=32 * 2**30)
         nfiles_target = 128
         half = size // 2
         n2 = int(half // 276)
-        vz = _zipf_lengths(int(half / 3500), rng)
+        vz = _zipf_lengths(int(half / 2000), rng)
         cum = np.cumsum(vz.astype(np.int64) + 20)
-        vz = vz[: int(np.searchsorted(cum, half - 64 * 70000))]
+        vz = vz[: int(np.searchsorted(cum, half - 64 * 40000))]
         vl = np.concatenate([np.full(n2, 256, np.uint32), vz])
     elif name == "c4":
         nfiles_target = 128

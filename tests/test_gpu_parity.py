@@ -192,3 +192,45 @@ def test_host_entry_pipelined_c2():
         else:
             t = r.file_tuples(i)
             assert (t["offset"] == np.arange(len(t), dtype=np.int64) * 276).all() and (t["fid"] == f.fid).all()
+
+
+def _device_file_checks(torch, wl, first, res, need):
+    """Size-independent properties of a device scan, checked on the device:
+    per file status io.EOF at its length, records back to back from offset 0
+    (offset[i+1] = offset[i] + size[i], the last ending at the file's end),
+    the file's fid; and the generator's record count."""
+    assert need == wl.expect_records
+    t = wl.d_out[: need * 48].view(torch.int64).view(need, 6)
+    u32 = wl.d_out[: need * 48].view(torch.int32).view(need, 12)
+    off, size, fidv = t[:, 0], u32[:, 7].to(torch.int64) & 0xFFFFFFFF, u32[:, 6].to(torch.int64) & 0xFFFFFFFF
+    for i, (ptr, ln, fid) in enumerate(wl.dev_files):
+        assert res[i].status == 0 and res[i].end_offset == ln, (i, res[i].status, res[i].end_offset, ln)
+        a, n = int(first[i]), int(res[i].n_records)
+        o, sz = off[a:a + n], size[a:a + n]
+        assert int(o[0]) == 0 and int(o[-1] + sz[-1]) == ln
+        assert bool((o[1:] == o[:-1] + sz[:-1]).all())
+        assert bool((fidv[a:a + n] == fid).all())
+
+
+@pytest.mark.slow
+def test_config3_device_generated_properties():
+    """BASELINE config 3 at full size: 128 files x 256 MiB = 32 GiB, value
+    lengths 64 B-64 KiB (Zipf 1.1, 14.6 % >= 4 KiB; tiles inside one record and
+    link repairs both occur), generated in HBM: the size-independent
+    properties over every file, and three whole files bit-exact against the
+    oracle (the first, the one holding the largest record, the last)."""
+    torch = pytest.importorskip("torch")
+    from bench import make_workload
+    wl = make_workload("c3", torch)
+    assert len(wl.dev_files) == 128 and wl.bytes > 31.9 * 2**30
+    with Scanner(0) as sc:
+        first, res, st, need = sc.scan_device(wl.dev_files, wl.d_out.data_ptr(), wl.out_cap)
+    _device_file_checks(torch, wl, first, res, need)
+    vs = wl.d_out[: need * 48].view(torch.int32).view(need, 12)[:, 9]
+    big = int(torch.argmax(vs).item())
+    fbig = max(i for i in range(len(first)) if first[i] <= big)
+    for i in sorted({0, fbig, len(wl.dev_files) - 1}):
+        ptr, ln, fid = wl.dev_files[i]
+        t, st_o, end = co.scan_file(wl.file_bytes(i), fid)
+        got = wl.d_out[first[i] * 48:(first[i] + res[i].n_records) * 48].cpu().numpy().view(TUPLE_DTYPE)
+        compare(got, res[i].status, res[i].end_offset, t, st_o, end, "c3 file %d" % i)
