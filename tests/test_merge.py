@@ -351,3 +351,31 @@ def test_gpu_merge_c4_4gib_properties():
         assert (merged[f] == src[f]).all(), f
     assert (merged["tx_id"] == 0).all() and (merged["txid_len"] == 1).all()
     assert (pos["fid"] == merged["fid"]).all() and (pos["offset"] == merged["offset"]).all()
+
+
+@pytest.mark.gpu
+def test_gpu_merge_repeated_calls_exact_scratch():
+    """Regression test of the round-1 fault (a second cly_merge_device call in
+    one process faulted in k_mplan while the scratch came from hipMallocAsync):
+    one context, exact-size scratch (CLY_MERGE_EXACT, no slack), merges of
+    growing and shrinking inputs back to back, each equal to the oracle."""
+    import subprocess
+    import sys
+    code = r'''
+import random, sys
+import numpy as np
+sys.path.insert(0, %r)
+from tests.test_merge import gpu_vs_oracle, split_files, oracle_scan
+from tests.gpu_util import merge_corpus, string_live_mask
+from couloydb_amd import Scanner
+with Scanner(0) as sc:
+    for k, n in enumerate([120, 900, 60, 1500, 300, 1500]):
+        b = merge_corpus(40 + k, n_keys=n)
+        files = split_files(b, 1 + k %% 3, random.Random(k))
+        arrays, tts, _ = oracle_scan(files)
+        gpu_vs_oracle(sc, files, string_live_mask(arrays, tts), 4096 if k %% 2 else 1 << 20)
+print("ok")
+''' % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CLY_MERGE_EXACT="1")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stderr[-2000:]
