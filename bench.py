@@ -191,6 +191,7 @@ def cpu_baseline(wl, budget_s=12.0):
     mt_bytes = sum(len(a) for a in mt_arrs)
     del mt_arrs
     multi = {"value": round(mt_bytes / t_mt / 2**30, 4), "unit": "GiB/s", "cores": MT_THREADS,
+             "cores_note": "the GPU box's CPU share per GPU (nproc reports the whole host)",
              "mrecords_per_s": round(mt_rec / t_mt / 1e6, 3),
              "sample": "%d files (%.2f GiB), one file per thread, clyo_scan_files_mt" % (len(mt_files), mt_bytes / 2**30)}
     merge_part = None
@@ -267,6 +268,33 @@ def host_path(wl, sc, max_files=16):
     out_rec["sample"] = "%d files, %.2f GiB; cly_scan (H2D + scan + D2H of the tuples), best of 2 after 1 warm-up" % (
         n, sum(len(a) for a in pageable) / 2**30)
     return out_rec
+
+
+def index_load_leg(wl, sc):
+    """NewCouloyDB's index load from files on disk through the device
+    (cly_db_open, include/clyload.h): the configuration's files written as
+    `%09d.cly` to a temporary directory, then list + mmap, H2D, scan, index
+    rebuild on the device, and the host String-index inserts (timed apart)."""
+    d = tempfile.mkdtemp(prefix="clyload_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    try:
+        for i, (_, ln, fid) in enumerate(wl.dev_files):
+            wl.file_bytes(i).tofile(os.path.join(d, "%09d.cly" % fid))
+        t0 = time.perf_counter()
+        db = sc.open_db(d)
+        wall = (time.perf_counter() - t0) * 1e3
+        s = db.stats
+        out = {"wall_ms": round(wall, 2), "list_map_ms": round(s.list_map_ms, 2), "h2d_ms": round(s.h2d_ms, 2),
+               "scan_ms": round(s.scan_ms, 2), "index_ms": round(s.index_ms, 2),
+               "host_insert_ms": round(s.insert_ms, 2), "files": int(s.n_files), "records": int(s.records),
+               "string_keys": int(s.str_keys),
+               "device_part_ms": round(s.h2d_ms + s.scan_ms + s.index_ms, 2),
+               "sample": "%d files (%.2f GiB) in %s; host index = hash-sharded open-addressing tables, 16 threads" % (
+                   s.n_files, s.bytes / 2**30, os.path.dirname(d))}
+        db.close()
+        return out
+    finally:
+        import shutil
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def append_leg(wl, sc, first, torch, reps=3):
@@ -471,10 +499,12 @@ def main():
         out["host_path"] = host_path(wl, sc)
         hp = out["host_path"].get("pageable", {})
         if hp and len(wl.dev_files) <= 16:
-            # the whole configuration went through the host entry: the record source
-            # of db.loadIndex (db.go:582-637) from mmap'd files to index tuples in host
-            # memory; the Go index inserts that consume the tuples stay Go's
-            out["index_load_wall_ms"] = hp["ms"]
+            # the record source of db.loadIndex (db.go:582-637) from mmap'd files to
+            # index tuples in host memory (the cgo path's rate)
+            out["host_scan_wall_ms"] = hp["ms"]
+    if args.config == "c2" and rank == 0 and world == 1 and not args.no_host_path:
+        out["index_load"] = index_load_leg(wl, sc)
+        out["index_load_wall_ms"] = out["index_load"]["wall_ms"]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(wl)
     if rank == 0:

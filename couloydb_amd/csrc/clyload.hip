@@ -10,7 +10,8 @@
 // String/ListMeta index state of every record is rebuilt on the device
 // (cly_index_device).  The tuples and states come back, and the host builds
 // what updateIndex puts in the MemTables (meta/memTable.go:15-30): the String
-// and ListMeta maps from the LIVE records, and the Hash maps (decodeFieldKey,
+// and ListMeta indexes from the LIVE records (open-addressing tables over the
+// mapped key bytes), and the Hash maps (decodeFieldKey,
 // txnHash.go:249-251) by replaying the Hash records in application order (a
 // record without a txId at once, a tx record at its TxnCommit marker,
 // db.go:600-627).  List (gob-encoded big.Float sequence keys) and Set (consistent
@@ -30,6 +31,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <thread>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -46,14 +48,47 @@ struct Mapped {
     uint64_t len;
 };
 
+// The String / ListMeta index: open-addressing tables of (key hash, tuple
+// index), sharded by the hash's top bits so that one thread builds each shard;
+// the key bytes stay in the mapped files.  The device already decided the one
+// live record of every key (last writer wins), so inserts never meet an equal
+// key and need no comparison.
+struct FlatShard {
+    std::vector<uint64_t> h;     // key hash | 1 (0 = empty)
+    std::vector<uint64_t> ti;    // tuple index
+    uint64_t mask = 0, n = 0;
+};
+static constexpr int FLAT_SHARD_BITS = 4;
+static constexpr int FLAT_SHARDS = 1 << FLAT_SHARD_BITS;
+struct FlatIndex {
+    FlatShard sh[FLAT_SHARDS];
+    uint64_t n = 0;
+};
+static inline int flat_shard(uint64_t h) { return (int)(h >> (64 - FLAT_SHARD_BITS)); }
 struct cly_db {
     std::vector<Mapped> files;
     std::vector<cly_tuple> tuples;
     std::vector<uint8_t> state;
     std::vector<uint64_t> first;
-    std::unordered_map<std::string, cly_pos> str, listmeta;
+    FlatIndex str, listmeta;
     std::unordered_map<std::string, std::unordered_map<std::string, cly_pos>> hash;
 };
+static inline uint64_t key_hash(const uint8_t* p, uint64_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xBF58476D1CE4E5B9ull);      // FNV-style, 8 bytes a step
+    uint64_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        memcpy(&w, p + i, 8);
+        h = (h ^ w) * 0x100000001B3ull;
+        h ^= h >> 29;
+    }
+    uint64_t w = 0;
+    memcpy(&w, p + i, n - i);
+    h = (h ^ w) * 0x100000001B3ull;
+    h ^= h >> 32;
+    h *= 0x94D049BB133111EBull;
+    return (h ^ (h >> 31)) | 1;
+}
 
 static double now_ms() {
     struct timespec ts;
@@ -62,15 +97,58 @@ static double now_ms() {
 }
 
 static const uint8_t* file_of(const cly_db* db, uint32_t fid) {
-    for (const Mapped& m : db->files) if (m.fid == fid) return m.p;
-    return nullptr;
+    // fids ascending in `files`: binary search
+    size_t lo = 0, hi = db->files.size();
+    while (lo < hi) {
+        const size_t mid = (lo + hi) / 2;
+        if (db->files[mid].fid < fid) lo = mid + 1; else hi = mid;
+    }
+    return lo < db->files.size() && db->files[lo].fid == fid ? db->files[lo].p : nullptr;
 }
 
 // realKey of tuple t (parseLogRecordKey, db.go:706-710)
-static std::string real_key(const cly_db* db, const cly_tuple& t) {
+static const uint8_t* real_key_ptr(const cly_db* db, const cly_tuple& t, uint64_t& len) {
     const uint8_t* f = file_of(db, t.fid);
     const uint32_t tl = t.txid_len == 0xFF ? 0 : t.txid_len;
-    return std::string((const char*)f + t.offset + t.header_size + tl, t.key_size - tl);
+    len = t.key_size - tl;
+    return f + t.offset + t.header_size + tl;
+}
+static std::string real_key(const cly_db* db, const cly_tuple& t) {
+    uint64_t n;
+    const uint8_t* p = real_key_ptr(db, t, n);
+    return std::string((const char*)p, n);
+}
+static void flat_init(FlatShard& x, uint64_t n) {
+    uint64_t cap = 16;
+    while (cap < 2 * n) cap <<= 1;
+    x.h.assign(cap, 0);
+    x.ti.assign(cap, 0);
+    x.mask = cap - 1;
+    x.n = 0;
+}
+static void flat_put(FlatShard& x, uint64_t h, uint64_t ti) {
+    uint64_t i = h & x.mask;
+    while (x.h[i]) i = (i + 1) & x.mask;
+    x.h[i] = h;
+    x.ti[i] = ti;
+    x.n++;
+}
+static void flat_build(cly_db* db, int nthreads);
+static int flat_get(const cly_db* db, const FlatIndex& xi, const uint8_t* key, uint64_t klen, cly_pos* pos) {
+    const uint64_t h = key_hash(key, klen);
+    const FlatShard& x = xi.sh[flat_shard(h)];
+    if (!x.mask) return CLY_DB_NOT_FOUND;
+    for (uint64_t i = h & x.mask; x.h[i]; i = (i + 1) & x.mask) {
+        if (x.h[i] != h) continue;
+        const cly_tuple& t = db->tuples[x.ti[i]];
+        uint64_t n;
+        const uint8_t* k = real_key_ptr(db, t, n);
+        if (n == klen && memcmp(k, key, n) == 0) {
+            if (pos) { pos->offset = t.offset; pos->fid = t.fid; pos->_pad = 0; }
+            return CLY_OK;
+        }
+    }
+    return CLY_DB_NOT_FOUND;
 }
 
 // decodeFieldKey (txnHash.go:249-251 -> bytex.DecodeByteSlices)
@@ -122,6 +200,52 @@ static int list_files(const char* dir, std::vector<Mapped>& out) {
         out.push_back(m);
     }
     return CLY_OK;
+}
+
+// Two passes over the LIVE tuples, each split over `nthreads` threads: hash the
+// keys and count them per shard, then let thread t fill shards t, t+T, ...
+static void flat_build(cly_db* db, int nthreads) {
+    const uint64_t need = db->tuples.size();
+    std::vector<uint64_t> hv(need);
+    std::vector<uint64_t> cnt((size_t)nthreads * 2 * FLAT_SHARDS, 0);
+    auto hash_part = [&](int t) {
+        const uint64_t a = need * t / nthreads, b = need * (t + 1) / nthreads;
+        uint64_t* c = &cnt[(size_t)t * 2 * FLAT_SHARDS];
+        for (uint64_t i = a; i < b; i++) {
+            hv[i] = 0;
+            if (db->state[i] != CLY_IX_LIVE) continue;
+            uint64_t n;
+            const uint8_t* k = real_key_ptr(db, db->tuples[i], n);
+            hv[i] = key_hash(k, n);
+            c[(db->tuples[i].data_type == 3) * FLAT_SHARDS + flat_shard(hv[i])]++;
+        }
+    };
+    auto fill_part = [&](int t) {
+        for (int kind = 0; kind < 2; kind++)
+            for (int sh = t; sh < FLAT_SHARDS; sh += nthreads) {
+                uint64_t n = 0;
+                for (int u = 0; u < nthreads; u++) n += cnt[(size_t)u * 2 * FLAT_SHARDS + kind * FLAT_SHARDS + sh];
+                flat_init((kind ? db->listmeta : db->str).sh[sh], n);
+            }
+        for (uint64_t i = 0; i < need; i++) {
+            const uint64_t h = hv[i];
+            if (!h || flat_shard(h) % nthreads != t) continue;
+            flat_put((db->tuples[i].data_type == 3 ? db->listmeta : db->str).sh[flat_shard(h)], h, i);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; t++) th.emplace_back(hash_part, t);
+    hash_part(0);
+    for (auto& x : th) x.join();
+    th.clear();
+    for (int t = 1; t < nthreads; t++) th.emplace_back(fill_part, t);
+    fill_part(0);
+    for (auto& x : th) x.join();
+    db->str.n = db->listmeta.n = 0;
+    for (int sh = 0; sh < FLAT_SHARDS; sh++) {
+        db->str.n += db->str.sh[sh].n;
+        db->listmeta.n += db->listmeta.sh[sh].n;
+    }
 }
 
 extern "C" void cly_db_close(cly_db* db) {
@@ -200,7 +324,7 @@ extern "C" int cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load
     {
         // MemTable inserts (updateIndex, db.go:511-575): String / ListMeta from the
         // device's LIVE records; Hash replayed in application order
-        db->str.reserve((size_t)ir.n_live);
+        flat_build(db, (int)std::min<unsigned>(FLAT_SHARDS, std::max(1u, std::thread::hardware_concurrency())));
         std::unordered_map<int64_t, std::vector<uint64_t>> txbuf;
         auto hash_apply = [&](uint64_t i) {
             const cly_tuple& t = db->tuples[i];
@@ -220,11 +344,6 @@ extern "C" int cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load
         };
         for (uint64_t i = 0; i < need; i++) {
             const cly_tuple& t = db->tuples[i];
-            if (db->state[i] == CLY_IX_LIVE) {
-                cly_pos p;
-                p.offset = t.offset; p.fid = t.fid; p._pad = 0;
-                (t.data_type == 3 ? db->listmeta : db->str)[real_key(db, t)] = p;
-            }
             // the Hash records, and the tx markers that decide them
             if (t.tx_id == 0) { if (t.data_type == 1) hash_apply(i); continue; }
             if (t.type == 4) continue;                                        // TxnBegin
@@ -234,8 +353,8 @@ extern "C" int cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load
             } else if (t.type == 3) txbuf.erase(t.tx_id);                    // TxnRollback
             else if (t.data_type == 1) txbuf[t.tx_id].push_back(i);
         }
-        s.str_keys = db->str.size();
-        s.listmeta_keys = db->listmeta.size();
+        s.str_keys = db->str.n;
+        s.listmeta_keys = db->listmeta.n;
         for (auto& kv : db->hash) s.hash_fields += kv.second.size();
     }
     t5 = now_ms();
@@ -256,14 +375,12 @@ static int found(const cly_pos* src, cly_pos* pos) {
 
 extern "C" int cly_db_get(cly_db* db, const uint8_t* key, uint64_t klen, cly_pos* pos) {
     if (!db) return CLY_ERR_ARG;
-    auto it = db->str.find(std::string((const char*)key, klen));
-    return it == db->str.end() ? CLY_DB_NOT_FOUND : found(&it->second, pos);
+    return flat_get(db, db->str, key, klen, pos);
 }
 
 extern "C" int cly_db_listmeta(cly_db* db, const uint8_t* key, uint64_t klen, cly_pos* pos) {
     if (!db) return CLY_ERR_ARG;
-    auto it = db->listmeta.find(std::string((const char*)key, klen));
-    return it == db->listmeta.end() ? CLY_DB_NOT_FOUND : found(&it->second, pos);
+    return flat_get(db, db->listmeta, key, klen, pos);
 }
 
 extern "C" int cly_db_hget(cly_db* db, const uint8_t* key, uint64_t klen, const uint8_t* field, uint64_t flen,
