@@ -230,9 +230,9 @@ class Scanner:
         return out[:k], pos[:k], res.status, res.end_offset
 
     def index(self, files):
-        """db.loadIndex's rebuild of the String/ListMeta indexes (db.go:511-637)
-        on the device, host buffers in (cly_index).  Returns (state per record in
-        scan order: IX_DEAD / IX_LIVE / IX_HOST, ClyIndexResult)."""
+        """db.loadIndex's rebuild of the five indexes (db.go:511-651) on the
+        device, host buffers in (cly_index).  Returns (state per record in scan
+        order: IX_DEAD / IX_LIVE / IX_LOADONLY, ClyIndexResult)."""
         files = list(files)
         arr = self._file_array(files)
         cap = int(self.lib.cly_scan_capacity(arr, len(files))) + 16
@@ -360,8 +360,9 @@ def build_info(lib="libclyscan.so"):
 
 class LoadedDB:
     """The indexes NewCouloyDB holds after loadIndex (include/clyload.h):
-    String / ListMeta key -> LogPos, Hash (key, field) -> LogPos, and values by
-    position (getLogRecordByPos).  get/hget return the value bytes, or raise
+    String / ListMeta key -> LogPos, Hash (key, field), List (key, seq gob
+    bytes) and Set (key, member) -> LogPos, and values by position
+    (getLogRecordByPos).  get/hget/lget/sget return the value bytes, or raise
     KeyError for public.ErrKeyNotFound."""
 
     def __init__(self, scanner, path):
@@ -399,6 +400,19 @@ class LoadedDB:
         return self._pos(self.lib.cly_db_hget(self.db, key, len(key), field, len(field), ctypes.byref(p)), p,
                          (key, field))
 
+    def lpos(self, key, seq):
+        p = _abi.ClyPos()
+        return self._pos(self.lib.cly_db_lget(self.db, key, len(key), seq, len(seq), ctypes.byref(p)), p, (key, seq))
+
+    def spos(self, key, member):
+        p = _abi.ClyPos()
+        return self._pos(self.lib.cly_db_sget(self.db, key, len(key), member, len(member), ctypes.byref(p)), p,
+                         (key, member))
+
+    def listmeta_pos(self, key):
+        p = _abi.ClyPos()
+        return self._pos(self.lib.cly_db_listmeta(self.db, key, len(key), ctypes.byref(p)), p, key)
+
     def value(self, pos):
         p = _abi.ClyPos()
         p.fid, p.offset = pos.fid, pos.offset
@@ -415,3 +429,22 @@ class LoadedDB:
 
     def hget(self, key, field):
         return self.value(self.hpos(key, field))
+
+    def lget(self, key, seq):
+        return self.value(self.lpos(key, seq))
+
+    def sget(self, key, member):
+        return self.value(self.spos(key, member))
+
+
+def index_key(lib, dtype, data):
+    """cly_index_key: the index key updateIndex derives from decoded key bytes
+    -> (P, R) bytes, or raises ValueError('panic') / returns None (no index)."""
+    out = ctypes.create_string_buffer(len(data) + 32)
+    plen = ctypes.c_uint32()
+    n = lib.cly_index_key(dtype, bytes(data), len(data), out, len(data) + 32, ctypes.byref(plen))
+    if n == -1:
+        raise ValueError("panic")
+    if n == -2:
+        return None
+    return out.raw[:plen.value], out.raw[plen.value:n]

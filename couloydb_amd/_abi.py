@@ -44,10 +44,11 @@ class ClyGenRec(ctypes.Structure):
 
 class ClyIndexResult(ctypes.Structure):
     _fields_ = [("n_live", ctypes.c_uint64), ("n_applied", ctypes.c_uint64), ("n_host", ctypes.c_uint64),
-                ("n_collisions", ctypes.c_uint64), ("index_ms", ctypes.c_double)]
+                ("n_collisions", ctypes.c_uint64), ("index_ms", ctypes.c_double),
+                ("n_loadonly", ctypes.c_uint64), ("n_merge_panic", ctypes.c_uint64)]
 
 
-IX_DEAD, IX_LIVE, IX_HOST = 0, 1, 2
+IX_DEAD, IX_LIVE, IX_HOST, IX_LOADONLY = 0, 1, 2, 3
 
 
 class ClyAppendResult(ctypes.Structure):
@@ -90,7 +91,8 @@ SCAN_SYMBOLS = ["cly_ctx_create", "cly_ctx_destroy", "cly_ctx_set_clock", "cly_s
                 "cly_index_device", "cly_index", "cly_append_device", "cly_append",
                 "cly_strerror", "cly_build_info"]
 GEN_SYMBOLS = ["cly_gen_record_size", "cly_gen_layout", "cly_gen_encode"]
-LOAD_SYMBOLS = ["cly_db_open", "cly_db_close", "cly_db_get", "cly_db_listmeta", "cly_db_hget", "cly_db_value"]
+LOAD_SYMBOLS = ["cly_db_open", "cly_db_close", "cly_db_get", "cly_db_listmeta", "cly_db_hget", "cly_db_lget",
+                "cly_db_sget", "cly_db_value", "cly_index_key"]
 DB_NOT_FOUND = 1
 
 
@@ -103,6 +105,7 @@ class ClyLoadStats(ctypes.Structure):
                 ("index_ms", ctypes.c_double), ("insert_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
                 ("n_files", ctypes.c_uint64), ("bytes", ctypes.c_uint64), ("records", ctypes.c_uint64),
                 ("str_keys", ctypes.c_uint64), ("listmeta_keys", ctypes.c_uint64), ("hash_fields", ctypes.c_uint64),
+                ("list_items", ctypes.c_uint64), ("set_members", ctypes.c_uint64),
                 ("active_fid", ctypes.c_uint32), ("_pad", ctypes.c_uint32), ("write_off", ctypes.c_int64)]
 
 _libs = {}
@@ -136,9 +139,13 @@ def load_scan_lib(name="libclyscan.so"):
     for fn in ("cly_db_get", "cly_db_listmeta"):
         getattr(lib, fn).argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p]
         getattr(lib, fn).restype = ctypes.c_int
-    lib.cly_db_hget.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
-                                ctypes.c_void_p]
-    lib.cly_db_hget.restype = ctypes.c_int
+    for fn in ("cly_db_hget", "cly_db_lget", "cly_db_sget"):
+        getattr(lib, fn).argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p,
+                                     ctypes.c_uint64, ctypes.c_void_p]
+        getattr(lib, fn).restype = ctypes.c_int
+    lib.cly_index_key.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                  P(ctypes.c_uint32)]
+    lib.cly_index_key.restype = ctypes.c_int64
     lib.cly_db_value.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                  P(ctypes.c_uint64)]
     lib.cly_db_value.restype = ctypes.c_int

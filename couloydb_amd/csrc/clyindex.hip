@@ -6,11 +6,13 @@
 // applied to the index at once (updateIndex, db.go:511-575); a record with a
 // txId is buffered until a TxnCommit marker of that txId applies the buffer in
 // order (a TxnRollback marker drops it, TxnBegin is ignored).  For the String
-// and ListMeta indexes the key is realKey itself: the last applied record of a
-// key decides, Put -> index[key] = (fid, offset), Deleted -> key absent.
-// Hash/List/Set keys are composite (decodeFieldKey, decodeListKey with
-// big.Float gob encodings, hashMemberKey's consistent hash): their records are
-// left to the host (state CLY_IX_HOST).
+// and ListMeta indexes the key is realKey itself; Hash/List/Set keys are
+// composite (decodeFieldKey, decodeListKey + the big.Float gob re-encoding,
+// hashMemberKey's CRC): ixkey.h derives them as (kind, P, R).  The last applied
+// record of a key decides, Put -> index[key] = (fid, offset), Deleted -> key
+// absent.  A winner whose key merge.go would look up differently (a Hash/List/
+// Set record without a txId: loadIndex decodes its stored key, merge its
+// realKey) is CLY_IX_LOADONLY: indexed, but not rewritten by a merge.
 //
 // Device pipeline:
 //   k_ixclass   per record: class (applied now / tx data / tx marker / host / none)
@@ -28,6 +30,7 @@
 #include <string.h>
 
 #include "scan_core.h"
+#include "ixkey.h"
 
 extern "C" hipStream_t cly_ctx_stream_internal(cly_ctx* c);
 extern "C" int64_t cly_ctx_now_internal(cly_ctx* c);
@@ -38,7 +41,7 @@ extern "C" int cly_ctx_device_internal(cly_ctx* c);
 // the winner's type needs no second (random) read of its tuple
 #define IX_DEL 0x80000000u
 #define IXI(x) ((x) & 0x7fffffffu)
-enum { K_NONE = 0, K_APPLY = 1, K_TXDATA = 2, K_COMMIT = 3, K_ROLLBACK = 4, K_HOST = 5, K_HOSTTX = 6 };
+enum { K_NONE = 0, K_APPLY = 1, K_TXDATA = 2, K_COMMIT = 3, K_ROLLBACK = 4 };
 
 __device__ __forceinline__ int ix_file(const uint64_t* first, int nfiles, uint64_t i) {
     int lo = 0, hi = nfiles - 1;
@@ -124,21 +127,68 @@ __device__ __forceinline__ uint64_t ix_hash_sig(uint32_t kind, const uint8_t* k,
 }
 __device__ __forceinline__ bool ix_sig_long(const uint4& s) { return (s.w >> 24) & IX_SIG_LONG; }
 
+__device__ __forceinline__ bool ix_composite(uint32_t dt) { return dt == 1 || dt == 2 || dt == 4; }
+// the key bytes of tuple t as stored
+__device__ __forceinline__ const uint8_t* ix_key_bytes(const uint64_t* bases, int f, const cly_tuple& t) {
+    return (const uint8_t*)bases[f] + t.offset + t.header_size;
+}
+// the index key of a Hash/List/Set record (ixkey.h) under loadIndex's decode
+// (merge = false) or merge.go's (merge = true)
+__device__ __forceinline__ bool ix_ckey(const uint64_t* bases, int f, const cly_tuple& t, bool merge, IxKey& k,
+                                        const uint8_t*& d) {
+    uint32_t off, len;
+    ixk_input(t, off, len, merge);
+    d = ix_key_bytes(bases, f, t) + off;
+    ixk_key(t.data_type, d, len, k);
+    return !k.panic;
+}
+__device__ __forceinline__ bool ix_ckey_eq(const IxKey& a, const uint8_t* da, const IxKey& b, const uint8_t* db) {
+    if (a.kind != b.kind || a.plen != b.plen || a.r_len != b.r_len) return false;
+    for (uint32_t q = 0; q < a.plen; q++) if (a.p[q] != b.p[q]) return false;
+    for (uint32_t q = 0; q < a.r_len; q++) if (da[a.r_off + q] != db[b.r_off + q]) return false;
+    return true;
+}
+// hash and signature of a composite key: ix_hash of R folded with P; the
+// signature is never injective (IX_SIG_LONG): equal ones are compared exactly
+__device__ __forceinline__ uint64_t ix_hash_ckey(const IxKey& k, const uint8_t* d, uint4& sig) {
+    uint64_t h = ix_hash(k.kind, d + k.r_off, k.r_len);
+    uint32_t pw[5] = {0, 0, 0, 0, 0};
+    for (uint32_t q = 0; q < k.plen; q++) pw[q >> 2] |= (uint32_t)k.p[q] << (8 * (q & 3));
+    #pragma unroll
+    for (int j = 0; j < 5; j += 2) {
+        const uint64_t w = pw[j] | (j + 1 < 5 ? (uint64_t)pw[j + 1] << 32 : 0ull);
+        h = (h ^ w ^ ((uint64_t)k.plen << 58)) * 0x100000001b3ull;
+        h ^= h >> 29;
+    }
+    h *= 0xd6e8feb86659fd93ull;
+    h ^= h >> 32;
+    sig = make_uint4(pw[0], pw[1], k.r_len, (pw[2] & 0xffffffu) | ((IX_SIG_LONG | ((k.kind & 7u) << 4)) << 24));
+    return h;
+}
+
 // hash, signature and tombstone bit of applied record i; returns the bit
 __device__ __forceinline__ bool ix_apply_one(const cly_tuple& t, uint64_t i, const uint64_t* first,
                                              const uint64_t* bases, int nfiles, uint64_t* hash, uint8_t* del,
-                                             uint4* ksig, uint64_t hash_mask) {
-    uint32_t len;
-    const uint8_t* k = ix_rkey(bases, ix_file(first, nfiles, i), t, len);
+                                             uint4* ksig, uint64_t hash_mask, uint32_t* bad) {
+    const int f = ix_file(first, nfiles, i);
     uint4 sg;
-    hash[i] = ix_hash_sig(t.data_type, k, len, sg) & hash_mask;
+    if (ix_composite(t.data_type)) {
+        IxKey k;
+        const uint8_t* d;
+        if (!ix_ckey(bases, f, t, false, k, d)) atomicOr(bad, 2u);     // updateIndex's decode panics
+        hash[i] = ix_hash_ckey(k, d, sg) & hash_mask;
+    } else {
+        uint32_t len;
+        const uint8_t* k = ix_rkey(bases, f, t, len);
+        hash[i] = ix_hash_sig(t.data_type, k, len, sg) & hash_mask;
+    }
     const bool dl = t.type == 1;
     del[i] = dl;
     ksig[i] = sg;
     return dl;
 }
 
-struct IxTot { unsigned long long n_live, n_applied, n_host, n_coll, n_tx, n_now; uint32_t bad, _pad; };
+struct IxTot { unsigned long long n_live, n_applied, n_loadonly, n_coll, n_tx, n_now, n_mpanic; uint32_t bad, _pad; };
 
 // sum of a and b over the workgroup (256 threads), one atomic per counter
 __device__ __forceinline__ void ix_wg_add2(unsigned long long a, unsigned long long b, unsigned long long* da,
@@ -154,7 +204,7 @@ __device__ __forceinline__ void ix_wg_add2(unsigned long long a, unsigned long l
     }
 }
 
-// class of each record; the index kind of an applied record: String 0, ListMeta 3
+// class of each record (every data type 0..4 is indexed; others: no-op)
 __global__ void __launch_bounds__(256)
 k_ixclass(const cly_tuple* __restrict__ tup, uint64_t n, uint8_t* cls, uint8_t* state, uint64_t* txkey,
           uint8_t* txflag, IxTot* tot, const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases,
@@ -163,20 +213,24 @@ k_ixclass(const cly_tuple* __restrict__ tup, uint64_t n, uint8_t* cls, uint8_t* 
     unsigned long long ntx = 0, nnow = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         const cly_tuple t = tup[i];
-        uint8_t c = K_NONE, s = CLY_IX_DEAD;
+        uint8_t c = K_NONE;
         if (t.txid_len == 0xFF) atomicOr(&tot->bad, 1u);          // parseLogRecordKey panics
-        const bool idx = t.data_type == 0 || t.data_type == 3;     // String, ListMeta
-        const bool host = t.data_type == 1 || t.data_type == 2 || t.data_type == 4;
+        const bool idx = t.data_type <= 4;                         // String Hash List ListMeta Set
         if (t.tx_id == 0) {                                        // updateIndex at once
             if (idx) c = K_APPLY;
-            else if (host) { c = K_HOST; s = CLY_IX_HOST; }
         } else if (t.type == 2) c = K_COMMIT;                      // LogRecordTxnCommit
         else if (t.type == 3) c = K_ROLLBACK;                      // LogRecordTxnRollback
-        else if (t.type != 4) c = idx ? K_TXDATA : (host ? K_HOSTTX : K_NONE);   // buffered (Begin ignored)
+        else if (t.type != 4 && idx) c = K_TXDATA;                 // buffered (Begin ignored)
+        // merge.go:101-126 decodes every Hash/List/Set record's realKey
+        if (ix_composite(t.data_type) && t.txid_len != 0xFF) {
+            IxKey k;
+            const uint8_t* d;
+            if (!ix_ckey(bases, ix_file(first, nfiles, i), t, true, k, d)) atomicAdd(&tot->n_mpanic, 1ull);
+        }
         cls[i] = c;
-        state[i] = s;
+        state[i] = CLY_IX_DEAD;
         txkey[i] = (uint64_t)t.tx_id;
-        const bool tx = c == K_TXDATA || c == K_COMMIT || c == K_ROLLBACK || c == K_HOSTTX;
+        const bool tx = c == K_TXDATA || c == K_COMMIT || c == K_ROLLBACK;
         txflag[i] = tx;
         ntx += tx;
         nnow += c == K_APPLY;
@@ -184,7 +238,7 @@ k_ixclass(const cly_tuple* __restrict__ tup, uint64_t n, uint8_t* cls, uint8_t* 
         // signature and tombstone bit come from this same pass over the tuples
         if (c == K_APPLY) {
             order[i] = (i << 32) | i;
-            const bool dl = ix_apply_one(t, i, first, bases, nfiles, hash, del, ksig, hash_mask);
+            const bool dl = ix_apply_one(t, i, first, bases, nfiles, hash, del, ksig, hash_mask, &tot->bad);
             selv[i] = (uint32_t)i | (dl ? IX_DEL : 0u);
         }
         apflag[i] = c == K_APPLY;
@@ -218,10 +272,9 @@ k_ixtx(const uint32_t* __restrict__ sidx, const uint8_t* __restrict__ cls, uint6
     for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < m; p += (uint64_t)gridDim.x * 256) {
         const uint32_t i = sidx[p];
         const uint8_t c = cls[i];
-        if (c != K_TXDATA && c != K_HOSTTX) continue;
+        if (c != K_TXDATA) continue;
         const uint64_t mp = nxt[m - 1 - p].mpos;
         const bool committed = mp != IX_NONE && cls[sidx[mp]] == K_COMMIT;
-        if (c == K_HOSTTX) { if (committed) state[i] = CLY_IX_HOST; continue; }
         if (committed) order[i] = ((uint64_t)sidx[mp] << 32) | i;
     }
 }
@@ -229,10 +282,11 @@ k_ixtx(const uint32_t* __restrict__ sidx, const uint8_t* __restrict__ cls, uint6
 __global__ void __launch_bounds__(256)
 k_ixapply(const cly_tuple* __restrict__ tup, uint64_t n, const uint8_t* __restrict__ cls,
           const uint64_t* __restrict__ order, const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases,
-          int nfiles, uint64_t* hash, uint8_t* apflag, uint8_t* del, uint4* ksig, uint64_t hash_mask) {
+          int nfiles, uint64_t* hash, uint8_t* apflag, uint8_t* del, uint4* ksig, uint64_t hash_mask,
+          uint32_t* bad) {
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         if (cls[i] != K_TXDATA || order[i] == IX_NONE) continue;   // K_APPLY: done by k_ixclass
-        ix_apply_one(tup[i], i, first, bases, nfiles, hash, del, ksig, hash_mask);
+        ix_apply_one(tup[i], i, first, bases, nfiles, hash, del, ksig, hash_mask, bad);
         apflag[i] = 1;
     }
 }
@@ -256,6 +310,13 @@ __device__ __forceinline__ bool ix_same_key(const cly_tuple* tup, const uint64_t
                                             int nfiles, uint32_t a, uint32_t b) {
     const cly_tuple ta = tup[a], tb = tup[b];
     if (ta.data_type != tb.data_type) return false;
+    if (ix_composite(ta.data_type)) {
+        IxKey x, y;
+        const uint8_t *dx, *dy;
+        ix_ckey(bases, ix_file(first, nfiles, a), ta, false, x, dx);
+        ix_ckey(bases, ix_file(first, nfiles, b), tb, false, y, dy);
+        return ix_ckey_eq(x, dx, y, dy);
+    }
     uint32_t la, lb;
     const uint8_t* ka = ix_rkey(bases, ix_file(first, nfiles, a), ta, la);
     const uint8_t* kb = ix_rkey(bases, ix_file(first, nfiles, b), tb, lb);
@@ -265,6 +326,20 @@ __device__ __forceinline__ bool ix_same_key(const cly_tuple* tup, const uint64_t
 }
 __device__ __forceinline__ bool ix_expired(const cly_tuple& t, int64_t now_ns) {
     return t.data_type == 0 && t.expiration != 0 && t.expiration <= now_ns;
+}
+// state of a key's winner w: LIVE, or LOADONLY when merge.go's lookup (the
+// realKey decoded, merge.go:101-126) names another key than loadIndex's (the
+// stored key decoded, for a Hash/List/Set record without a txId)
+__device__ __forceinline__ uint8_t ix_win_state(const cly_tuple* tup, const uint64_t* first, const uint64_t* bases,
+                                                int nfiles, uint32_t w) {
+    const cly_tuple t = tup[w];
+    if (!ix_composite(t.data_type) || t.tx_id != 0 || t.txid_len == 0) return CLY_IX_LIVE;
+    const int f = ix_file(first, nfiles, w);
+    IxKey x, y;
+    const uint8_t *dx, *dy;
+    ix_ckey(bases, f, t, false, x, dx);
+    if (!ix_ckey(bases, f, t, true, y, dy)) return CLY_IX_LOADONLY;
+    return ix_ckey_eq(x, dx, y, dy) ? CLY_IX_LIVE : CLY_IX_LOADONLY;
 }
 // group ends: the winner (max order) decides the key; adjacent different keys
 // inside a group mark a hash collision (resolved exactly by k_ixcoll)
@@ -293,7 +368,7 @@ k_ixwin(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, cons
         const bool deleted = g ? tup[w].type == 1 : (sidx[q] & IX_DEL) != 0;
         // LogRecordDeleted -> key absent; a String key whose winning put expired is
         // db.Del'd by loadIndex's TTL sweep (db.go:639-651: not exp.After(now))
-        if (!deleted && !ix_expired(tup[w], now_ns)) state[w] = CLY_IX_LIVE;
+        if (!deleted && !ix_expired(tup[w], now_ns)) state[w] = ix_win_state(tup, first, bases, nfiles, w);
     }
 }
 // exact resolution of a collided hash group (one thread): per distinct key the max order
@@ -313,7 +388,8 @@ k_ixcoll(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, con
         for (uint64_t b = q0; b < q1 && best; b++)
             if (b != a && order[IXI(sidx[b])] > order[ia] &&
                 ix_same_key(tup, first, bases, nfiles, ia, IXI(sidx[b]))) best = false;
-        if (best && tup[ia].type != 1 && !ix_expired(tup[ia], now_ns)) state[ia] = CLY_IX_LIVE;
+        if (best && tup[ia].type != 1 && !ix_expired(tup[ia], now_ns))
+            state[ia] = ix_win_state(tup, first, bases, nfiles, ia);
     }
 }
 // counts: one atomic per workgroup and counter (a wave-level atomic on one
@@ -323,8 +399,8 @@ k_ixcount(const uint8_t* __restrict__ state, const uint8_t* __restrict__ flag, u
     __shared__ unsigned long long sh[3][4];
     unsigned long long live = 0, host = 0, ap = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-        live += state[i] == CLY_IX_LIVE;
-        host += state[i] == CLY_IX_HOST;
+        live += state[i] == CLY_IX_LIVE || state[i] == CLY_IX_LOADONLY;
+        host += state[i] == CLY_IX_LOADONLY;
         ap += flag[i];
     }
     for (int d = 32; d >= 1; d >>= 1) {
@@ -337,7 +413,7 @@ k_ixcount(const uint8_t* __restrict__ state, const uint8_t* __restrict__ flag, u
     __syncthreads();
     if (threadIdx.x < 3) {
         const unsigned long long v = sh[threadIdx.x][0] + sh[threadIdx.x][1] + sh[threadIdx.x][2] + sh[threadIdx.x][3];
-        unsigned long long* dst = threadIdx.x == 0 ? &tot->n_live : threadIdx.x == 1 ? &tot->n_host : &tot->n_applied;
+        unsigned long long* dst = threadIdx.x == 0 ? &tot->n_live : threadIdx.x == 1 ? &tot->n_loadonly : &tot->n_applied;
         if (v) atomicAdd(dst, v);
     }
 }
@@ -488,7 +564,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     // ---- applied records: hash, sort, winner per key
     // (records without a txId were hashed by k_ixclass; committed tx data here)
     if (m) k_ixapply<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_order, d_first, d_bases, nfiles, d_hash, d_apflag,
-                                           d_del, d_ksig, hm);
+                                           d_del, d_ksig, hm, &d_tot->bad);
     if (m == 0 && h_tot.n_now == n) {
         m2 = n;                                                 // every record applied: no select
     } else {
@@ -530,7 +606,9 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     if (h_tot.bad) { rc = CLY_ERR_VARINT; goto done; }
     ir->n_live = h_tot.n_live;
     ir->n_applied = h_tot.n_applied;
-    ir->n_host = h_tot.n_host;
+    ir->n_host = 0;
+    ir->n_loadonly = h_tot.n_loadonly;
+    ir->n_merge_panic = h_tot.n_mpanic;
     ir->n_collisions = h_tot.n_coll;
     {
         float ms = 0;

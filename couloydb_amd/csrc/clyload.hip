@@ -7,15 +7,13 @@
 //   -> loadIndex (db.go:487-655: every record of every file in fid order,
 //   tx buffering by txId, updateIndex, the TTL sweep).
 // The files are mmap'd, copied to HBM, scanned (cly_scan_device) and the
-// String/ListMeta index state of every record is rebuilt on the device
+// index state of every record (all five indexes) is rebuilt on the device
 // (cly_index_device).  The tuples and states come back, and the host builds
-// what updateIndex puts in the MemTables (meta/memTable.go:15-30): the String
-// and ListMeta indexes from the LIVE records (open-addressing tables over the
-// mapped key bytes), and the Hash maps (decodeFieldKey,
-// txnHash.go:249-251) by replaying the Hash records in application order (a
-// record without a txId at once, a tx record at its TxnCommit marker,
-// db.go:600-627).  List (gob-encoded big.Float sequence keys) and Set (consistent
-// hash of the member) indexes are not built here.
+// what updateIndex puts in the MemTables (meta/memTable.go:15-30) from the
+// records the device marked as index entries: the String and ListMeta indexes
+// as open-addressing tables over the mapped key bytes, and the per-key Hash
+// (field), List (seq gob encoding) and Set (member hash) maps, keyed as
+// ixkey.h derives them (the same code as the device's).
 //
 // The host inserts are timed separately from the device work.
 #include <hip/hip_runtime.h>
@@ -38,6 +36,7 @@
 
 #include "../../include/clyload.h"
 #include "scan_core.h"
+#include "ixkey.h"
 
 extern "C" hipStream_t cly_ctx_stream_internal(cly_ctx* c);
 extern "C" int cly_ctx_device_internal(cly_ctx* c);
@@ -71,7 +70,8 @@ struct cly_db {
     std::vector<uint8_t> state;
     std::vector<uint64_t> first;
     FlatIndex str, listmeta;
-    std::unordered_map<std::string, std::unordered_map<std::string, cly_pos>> hash;
+    // getHashIndex / getListDataIndex / getSetIndex (index.go): realKey -> MemTable
+    std::unordered_map<std::string, std::unordered_map<std::string, cly_pos>> hash, list, set;
 };
 static inline uint64_t key_hash(const uint8_t* p, uint64_t n) {
     uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xBF58476D1CE4E5B9ull);      // FNV-style, 8 bytes a step
@@ -151,20 +151,6 @@ static int flat_get(const cly_db* db, const FlatIndex& xi, const uint8_t* key, u
     return CLY_DB_NOT_FOUND;
 }
 
-// decodeFieldKey (txnHash.go:249-251 -> bytex.DecodeByteSlices)
-static bool field_key(const std::string& k, std::string& key, std::string& field) {
-    int n1 = 0, n2 = 0;
-    const int64_t ks = go_varint((const uint8_t*)k.data(), (int64_t)k.size(), n1);
-    if (n1 <= 0) return false;
-    go_varint((const uint8_t*)k.data() + n1, (int64_t)k.size() - n1, n2);
-    if (n2 <= 0) return false;
-    const int64_t idx = n1 + n2;
-    if (ks < 0 || idx + ks > (int64_t)k.size()) return false;
-    key = k.substr((size_t)idx, (size_t)ks);
-    field = k.substr((size_t)(idx + ks));
-    return true;
-}
-
 static int list_files(const char* dir, std::vector<Mapped>& out) {
     DIR* d = opendir(dir);
     if (!d) return CLY_ERR_ARG;
@@ -213,7 +199,8 @@ static void flat_build(cly_db* db, int nthreads) {
         uint64_t* c = &cnt[(size_t)t * 2 * FLAT_SHARDS];
         for (uint64_t i = a; i < b; i++) {
             hv[i] = 0;
-            if (db->state[i] != CLY_IX_LIVE) continue;
+            const uint32_t dt = db->tuples[i].data_type;
+            if (db->state[i] != CLY_IX_LIVE || (dt != 0 && dt != 3)) continue;     // String / ListMeta
             uint64_t n;
             const uint8_t* k = real_key_ptr(db, db->tuples[i], n);
             hv[i] = key_hash(k, n);
@@ -322,40 +309,37 @@ extern "C" int cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load
     s.index_ms = t4 - t3;
     s.records = need;
     {
-        // MemTable inserts (updateIndex, db.go:511-575): String / ListMeta from the
-        // device's LIVE records; Hash replayed in application order
+        // MemTable inserts (updateIndex, db.go:511-575) for the records the
+        // device marked as index entries: String / ListMeta into the flat
+        // tables, Hash / List / Set into realKey -> (field | seqBuf | hashKey) maps
         flat_build(db, (int)std::min<unsigned>(FLAT_SHARDS, std::max(1u, std::thread::hardware_concurrency())));
-        std::unordered_map<int64_t, std::vector<uint64_t>> txbuf;
-        auto hash_apply = [&](uint64_t i) {
-            const cly_tuple& t = db->tuples[i];
-            std::string key, field;
-            // updateIndex decodes log.Key: the realKey for a buffered tx record
-            // (db.go:620), but the key as stored, txId varint included, for a
-            // record applied at once (db.go:600-602, 523)
-            std::string k = real_key(db, t);
-            if (t.tx_id == 0 && t.txid_len != 0xFF) {
-                const uint8_t* f = file_of(db, t.fid);
-                k = std::string((const char*)f + t.offset + t.header_size, t.key_size);
-            }
-            if (!field_key(k, key, field)) return;
-            auto& idx = db->hash[key];
-            if (t.type == 1) idx.erase(field);                               // LogRecordDeleted
-            else { cly_pos p; p.offset = t.offset; p.fid = t.fid; p._pad = 0; idx[field] = p; }
-        };
         for (uint64_t i = 0; i < need; i++) {
+            const uint8_t stt = db->state[i];
             const cly_tuple& t = db->tuples[i];
-            // the Hash records, and the tx markers that decide them
-            if (t.tx_id == 0) { if (t.data_type == 1) hash_apply(i); continue; }
-            if (t.type == 4) continue;                                        // TxnBegin
-            if (t.type == 2) {                                                // TxnCommit
-                auto it = txbuf.find(t.tx_id);
-                if (it != txbuf.end()) { for (uint64_t j : it->second) hash_apply(j); txbuf.erase(it); }
-            } else if (t.type == 3) txbuf.erase(t.tx_id);                    // TxnRollback
-            else if (t.data_type == 1) txbuf[t.tx_id].push_back(i);
+            if ((stt != CLY_IX_LIVE && stt != CLY_IX_LOADONLY) || !(t.data_type == 1 || t.data_type == 2 || t.data_type == 4))
+                continue;
+            uint32_t off, len;
+            ixk_input(t, off, len, false);
+            const uint8_t* d = file_of(db, t.fid) + t.offset + t.header_size + off;
+            IxKey k;
+            if (!ixk_key(t.data_type, d, len, k)) continue;      // (the device rejected a panicking decode)
+            cly_pos p;
+            p.offset = t.offset; p.fid = t.fid; p._pad = 0;
+            const uint8_t* r = d + k.r_off;
+            if (t.data_type == 1) {              // realKey = R[0:la], field = R[la:]
+                const uint32_t la = k.p[0] | ((uint32_t)k.p[1] << 8) | ((uint32_t)k.p[2] << 16) | ((uint32_t)k.p[3] << 24);
+                db->hash[std::string((const char*)r, la)][std::string((const char*)r + la, k.r_len - la)] = p;
+            } else if (t.data_type == 2) {       // realKey = R, seqBuf = P[1:]
+                db->list[std::string((const char*)r, k.r_len)][std::string((const char*)k.p + 1, k.plen - 1)] = p;
+            } else {                             // realKey = R, hashKey = P
+                db->set[std::string((const char*)r, k.r_len)][std::string((const char*)k.p, 4)] = p;
+            }
         }
         s.str_keys = db->str.n;
         s.listmeta_keys = db->listmeta.n;
         for (auto& kv : db->hash) s.hash_fields += kv.second.size();
+        for (auto& kv : db->list) s.list_items += kv.second.size();
+        for (auto& kv : db->set) s.set_members += kv.second.size();
     }
     t5 = now_ms();
     s.insert_ms = t5 - t4;
@@ -390,6 +374,50 @@ extern "C" int cly_db_hget(cly_db* db, const uint8_t* key, uint64_t klen, const 
     if (h == db->hash.end()) return CLY_DB_NOT_FOUND;
     auto it = h->second.find(std::string((const char*)field, flen));
     return it == h->second.end() ? CLY_DB_NOT_FOUND : found(&it->second, pos);
+}
+
+static int map_get(const std::unordered_map<std::string, std::unordered_map<std::string, cly_pos>>& m,
+                   const uint8_t* key, uint64_t klen, const std::string& sub, cly_pos* pos) {
+    auto h = m.find(std::string((const char*)key, klen));
+    if (h == m.end()) return CLY_DB_NOT_FOUND;
+    auto it = h->second.find(sub);
+    return it == h->second.end() ? CLY_DB_NOT_FOUND : found(&it->second, pos);
+}
+
+extern "C" int cly_db_lget(cly_db* db, const uint8_t* key, uint64_t klen, const uint8_t* seq, uint64_t slen,
+                           cly_pos* pos) {
+    if (!db || slen > 0xFFFFFFFFull) return CLY_ERR_ARG;
+    uint8_t c[IXK_PMAX];
+    const uint32_t n = ixk_gob_canon(seq, (uint32_t)slen, c);      // the index keys seq.GobEncode()
+    return map_get(db->list, key, klen, std::string((const char*)c, n), pos);
+}
+
+extern "C" int cly_db_sget(cly_db* db, const uint8_t* key, uint64_t klen, const uint8_t* member, uint64_t mlen,
+                           cly_pos* pos) {
+    if (!db || klen > 0xFFFFFFFFull || mlen > 0xFFFFFFFFull) return CLY_ERR_ARG;
+    uint8_t hdr[20], hk[4];                      // hashMemberKey(key, member), txnSet.go:149-153
+    int h = ixk_put_varint((int64_t)klen, hdr);
+    h += ixk_put_varint((int64_t)mlen, hdr + h);
+    uint32_t c = ixk_crc_bytes(0xFFFFFFFFu, hdr, (uint32_t)h);
+    c = ixk_crc_bytes(c, key, (uint32_t)klen);
+    c = ixk_crc_bytes(c, member, (uint32_t)mlen);
+    ixk_be32(hk, ~c);
+    return map_get(db->set, key, klen, std::string((const char*)hk, 4), pos);
+}
+
+// The index key updateIndex derives for a record of data type dtype from the
+// decoded key bytes d[0:n] (ixkey.h): writes P || R to out; returns its length,
+// -1 if the decode panics, -2 if dtype has no index, -3 if cap is too small.
+extern "C" int64_t cly_index_key(uint32_t dtype, const uint8_t* d, uint64_t n, uint8_t* out, uint64_t cap,
+                                 uint32_t* plen) {
+    if (n > 0xFFFFFFFFull) return -3;
+    IxKey k;
+    if (!ixk_key(dtype, d, (uint32_t)n, k)) return k.panic ? -1 : -2;
+    if ((uint64_t)k.plen + k.r_len > cap) return -3;
+    memcpy(out, k.p, k.plen);
+    memcpy(out + k.plen, d + k.r_off, k.r_len);
+    if (plen) *plen = k.plen;
+    return (int64_t)k.plen + k.r_len;
 }
 
 // getLogRecordByPos (db.go:680-704): the record at pos, its value.  The CRC

@@ -192,31 +192,45 @@ int cly_hint_positions_device(cly_ctx* ctx, const uint8_t* d_hint_file, const cl
 int cly_hint_scan(cly_ctx* ctx, const cly_file* hint_file, cly_tuple* out, cly_pos* pos, uint64_t cap,
                   uint64_t* n_out, cly_file_result* res);
 
-/* ---- index rebuild (db.loadIndex, db.go:511-637) -------------------------
+/* ---- index rebuild (db.loadIndex, db.go:511-651) -------------------------
  * Per record of a scan (scan order = fid order, offsets within), the state of
- * the String and ListMeta indexes after the load: records without a txId are
- * applied at once, records with a txId at their txId's next TxnCommit marker
- * (a TxnRollback drops them, TxnBegin is ignored, no marker: never applied);
- * the last applied record of a key decides (Put -> the index points at it,
- * Deleted -> the key is absent).  Hash/List/Set records (composite index keys,
- * db.go:524-572) are the host's: CLY_IX_HOST (tx records only when committed).
+ * the five indexes after the load: records without a txId are applied at
+ * once, records with a txId at their txId's next TxnCommit marker (a
+ * TxnRollback drops them, TxnBegin is ignored, no marker: never applied); the
+ * last applied record of a key decides (Put -> the index points at it,
+ * Deleted -> the key is absent); a String key whose winning put has expired
+ * (expiration set and <= the context clock, cly_ctx_set_clock) is dropped by
+ * the TTL sweep (db.go:639-651).  Keys: String/ListMeta realKey; Hash
+ * (key, field) = decodeFieldKey; List (key, seq.GobEncode()) = decodeListKey
+ * with big.Float's gob re-encoding; Set (key, hashMemberKey) — updateIndex
+ * decodes the stored key (txId varint included) of a record without a txId
+ * and the realKey of a committed tx record (db.go:521-572, 600-620).
  * A hint file loaded before (loadIndexFromHintFile) is not part of this.     */
 #define CLY_IX_DEAD 0         /* not the index's entry after the load         */
-#define CLY_IX_LIVE 1         /* the String/ListMeta index points here         */
-#define CLY_IX_HOST 2         /* Hash/List/Set record: indexed by the host     */
+#define CLY_IX_LIVE 1         /* an index points here, and merge.go's lookup
+                                 (merge.go:101-132) finds it: merge keeps it  */
+#define CLY_IX_HOST 2         /* (no longer emitted: every data type is built
+                                 on the device)                               */
+#define CLY_IX_LOADONLY 3     /* an index points here, but merge.go decodes the
+                                 realKey and looks up another key: a Hash/List/
+                                 Set record without a txId; merge drops it    */
 typedef struct cly_index_result {
-    uint64_t n_live;          /* keys present (= records in state LIVE)         */
-    uint64_t n_applied;       /* String/ListMeta records updateIndex sees       */
-    uint64_t n_host;          /* records left to the host                       */
+    uint64_t n_live;          /* index entries (= records LIVE or LOADONLY)     */
+    uint64_t n_applied;       /* records updateIndex sees                       */
+    uint64_t n_host;          /* 0 (kept for layout)                            */
     uint64_t n_collisions;    /* 64-bit key-hash collisions (resolved exactly)  */
     double   index_ms;        /* device time                                    */
+    uint64_t n_loadonly;      /* records in state LOADONLY                      */
+    uint64_t n_merge_panic;   /* Hash/List/Set records whose realKey decode
+                                 panics in merge.go (a merge would fail)      */
 } cly_index_result;
 
 /* Device entry over a cly_scan_device result (tuples back to back): d_state
  * gets one byte per tuple.  The LIVE bytes are merge.go:104-132's liveness
- * for String/ListMeta records (cly_merge_device's d_live once HOST bytes are
- * replaced by the host's verdict).  Returns the scan's error status if a file
- * failed (loadIndex returns it), CLY_ERR_VARINT if a txId varint overflowed. */
+ * (cly_merge_device's d_live takes d_state as is: it keeps state 1 only).
+ * Returns the scan's error status if a file failed (loadIndex returns it),
+ * CLY_ERR_VARINT if a txId varint overflowed or a Hash/List/Set key decode
+ * that updateIndex applies panics (a slice bound out of range in Go).      */
 int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
                      const cly_tuple* d_tuples, const uint64_t* file_first, const cly_file_result* res,
                      uint8_t* d_state, cly_index_result* ir, void* stream);

@@ -36,7 +36,7 @@ def fixed_records_file(n, value_len, seed=1, key_base=0, zero_values=False):
     return out.reshape(-1)
 
 
-def mixed_corpus(seed, target_bytes, corrupt=0, tail=True):
+def mixed_corpus(seed, target_bytes, corrupt=0, tail=True, dts=(0, 0, 0, 1, 2, 3, 4)):
     """Records of mixed shapes (tx ids, all types/dtypes, tombstones, header-like
     values, embedded records, long values spanning chunks)."""
     rng = random.Random(seed)
@@ -59,7 +59,7 @@ def mixed_corpus(seed, target_bytes, corrupt=0, tail=True):
         else:
             v = rng.randbytes(rng.randrange(0, 64))
         typ = rng.choice([0, 0, 0, 0, 1, 2, 3, 4])
-        dt = rng.choice([0, 0, 0, 1, 2, 3, 4])
+        dt = rng.choice(dts)
         exp = rng.choice([0, 0, 0, -1, 1 << 40, 1_697_000_000_000_000_000])
         b += mg.encode_record(mg.key_tx(mg.test_key(i), tx), v, typ, dt, exp)
         i += 1
@@ -189,55 +189,203 @@ def merge_corpus(seed, n_keys=300, rounds=3, tx_frac=0.3, key_fn=None):
                 b += mg.encode_record(mg.key_tx(key, 0), b"", mg.DELETED, mg.STRING, 0)
             else:
                 b += mg.encode_record(mg.key_tx(key, 0), rng.randbytes(rng.choice([0, 5, 50, 256, 900])),
-                                      mg.NORMAL, rng.choice([0, 0, 0, 1, 2, 3, 4]), 0)
+                                      mg.NORMAL, rng.choice([0, 0, 0, 3, 5, 6, 9]), 0)
+    return bytes(b)
+
+
+def _nc_varint(x, rng):
+    """binary.PutVarint(x), sometimes in a longer (non-minimal) form that
+    binary.Varint still reads as x."""
+    b = bytearray(mg.put_varint(x))
+    if rng.random() < 0.5 and len(b) < 9:
+        b[-1] |= 0x80
+        b += b"\x00"
+    return bytes(b)
+
+
+def seq_variant(v, rng):
+    """A gob buffer for list seq v: the writer's encoding, or another buffer of
+    the kinds GobDecode accepts (mode/accuracy bits, other precisions with or
+    without rounding, longer or zero-padded mantissas, the error forms)."""
+    from .index_keys import gob_encode_int
+    g = bytearray(gob_encode_int(v))
+    c = rng.randrange(14)
+    if c < 4:
+        return bytes(g)
+    if c == 4:                                   # accuracy / mode bits (reset by SetPrec)
+        g[1] |= rng.choice([0x10, 0x18, 0x20, 0xa0])
+    elif c == 5 and len(g) == 18:                # prec 64, low bits that round (or not)
+        g[2:6] = (64).to_bytes(4, "big")
+        m = int.from_bytes(g[10:18], "big") | rng.choice([0, 0x1, 0x3ff, 0x400, 0x7ff, 0xc00, 0x800])
+        g[10:18] = m.to_bytes(8, "big")
+    elif c == 6 and len(g) == 18:                # prec 24: no rounding, prec re-set to 53
+        g[2:6] = (24).to_bytes(4, "big")
+    elif c == 7 and len(g) == 18:                # two-word mantissa / leading zero bytes
+        g += bytes([rng.choice([0, 0, 5])]) * rng.choice([1, 8])
+        if rng.random() < 0.5:
+            g[10:10] = bytes(rng.randrange(1, 9))
+    elif c == 8:
+        return b""
+    elif c == 9:
+        return bytes(g[:rng.randrange(1, 6)])   # short: error, NewFloat(0)
+    elif c == 10:
+        g[0] = 2                                  # unsupported version
+    elif c == 11:
+        g[1] = (g[1] & ~0x06) | 0x04              # inf form
+    elif c == 12 and len(g) == 18:
+        return bytes(g[:rng.randrange(6, 10)])   # finite, shorter than 10 bytes
+    elif c == 13 and len(g) == 18:               # prec 200, all-ones low mantissa (carry)
+        g[2:6] = (200).to_bytes(4, "big")
+        g[10:18] = (int.from_bytes(g[10:18], "big") | ((1 << 11) - 1)).to_bytes(8, "big")
+        g += b"\xff" * rng.choice([0, 8])
+    return bytes(g)
+
+
+def typed_corpus(seed, n_ops=400, n_keys=12, tx_frac=0.6, nontx_frac=0.15, garbage=False):
+    """Records of all five data types as the reference's writers produce them
+    (Put/Del; HSet/HDel txnHash.go:9-90; LPush/RPush/LPop/RPop with their
+    ListMeta records txnList.go:96-232; SAdd/SRem txnSet.go:11-90) in committed,
+    rolled-back and unterminated transactions, plus records without a txId
+    (as a merge rewrites them) and equivalent non-canonical encodings of the
+    composite keys (longer varints, other gob forms of a list seq).
+    garbage=True adds rolled-back Hash/Set/List records whose keys do not decode
+    (merge.go would panic on them; loadIndex never decodes them)."""
+    from .index_keys import encode_list_meta
+    rng = random.Random(seed)
+    b = bytearray()
+    txid = 5000
+    lists = {}                                   # key -> [head, tail]
+
+    def rec(key, value, typ, dt, tx):
+        return mg.encode_record(mg.key_tx(key, tx), value, typ, dt, 0)
+
+    def ops_one(tx):
+        out = []
+        k = b"key%02d" % rng.randrange(n_keys)
+        what = rng.randrange(5)
+        dele = rng.random() < 0.25
+        if what == 0:                            # String / ListMeta by realKey
+            out.append(rec(k, b"" if dele else rng.randbytes(rng.randrange(0, 40)), mg.DELETED if dele else mg.NORMAL,
+                           rng.choice([mg.STRING, mg.STRING, mg.LISTMETA]), tx))
+        elif what == 1:                          # Hash
+            f = b"f%d" % rng.randrange(6)
+            key = _nc_varint(len(k), rng) + _nc_varint(rng.choice([len(f), len(f), 99, -3]), rng) + k + f
+            out.append(rec(key, b"" if dele else rng.randbytes(rng.randrange(0, 20)), mg.DELETED if dele else mg.NORMAL,
+                           mg.HASH, tx))
+        elif what == 2:                          # Set
+            m = b"m%d" % rng.randrange(6)
+            key = _nc_varint(len(k), rng) + _nc_varint(rng.choice([len(m), len(m), 7]), rng) + k + m
+            out.append(rec(key, b"" if dele else m, mg.DELETED if dele else mg.NORMAL, mg.SET, tx))
+        else:                                    # List push / pop + its ListMeta record
+            head, tail = lists.get(k, [1, 0])
+            left = rng.random() < 0.5
+            if dele and head <= tail:
+                seq = head if left else tail
+                prev, nxt = seq - 1, seq + 1
+                if left:
+                    head += 1
+                else:
+                    tail -= 1
+                typ, val = mg.DELETED, b""
+            else:
+                seq = head - 1 if left else tail + 1
+                prev, nxt = (seq - 1, head) if left else (tail, seq + 1)
+                if left:
+                    head = seq
+                else:
+                    tail = seq
+                typ, val = mg.NORMAL, rng.randbytes(rng.randrange(0, 20))
+            a, p, n = seq_variant(seq, rng), seq_variant(prev, rng), seq_variant(nxt, rng)
+            key = _nc_varint(len(a), rng) + _nc_varint(len(p), rng) + _nc_varint(len(n), rng) + a + p + n + k
+            out.append(rec(key, val, typ, mg.LIST, tx))
+            lists[k] = [head, tail]
+            out.append(rec(k, encode_list_meta(head, tail), mg.NORMAL, mg.LISTMETA, tx))
+        return out
+
+    while len(b) < 1 or n_ops > 0:
+        n_ops -= 1
+        r = rng.random()
+        if r < tx_frac:
+            txid += 1
+            body = []
+            for _ in range(rng.randrange(1, 5)):
+                body += ops_one(txid)
+            end = rng.random()
+            if garbage and rng.random() < 0.2:
+                body.append(rec(rng.choice([b"zz", b"\x7f\x7f", b"\x02"]), b"", mg.NORMAL,
+                                rng.choice([mg.HASH, mg.LIST, mg.SET]), txid))
+                end = 0.8                        # rolled back
+            if rng.random() < 0.3:
+                b += rec(mg.TX_BEGIN_KEY, b"", mg.TXN_BEGIN, mg.STRING, txid)
+            for x in body:
+                b += x
+            if end < 0.7:
+                b += rec(mg.TX_COMMIT_KEY, b"", mg.TXN_COMMIT, mg.STRING, txid)
+            elif end < 0.9:
+                b += rec(mg.TX_ROLLBACK_KEY, b"", mg.TXN_ROLLBACK, mg.STRING, txid)
+        elif r < tx_frac + nontx_frac:
+            for x in ops_one(0):
+                b += x
+        else:
+            for x in ops_one(0):
+                b += x
     return bytes(b)
 
 
 INDEX_NOW = 1_800_000_000_000_000_000      # the clock the index tests give loadIndex (UnixNano, 2027)
 
 
-def index_states(file_bytes, tuples_per_file, now_ns=INDEX_NOW):
+def index_states(file_bytes, tuples_per_file, now_ns=INDEX_NOW, merge_panics=None):
     """db.loadIndex (db.go:582-651) restated literally: a map of buffered tx
-    records per txId, updateIndex for String and ListMeta keys (with the
-    expirations map of String keys), the TTL sweep (a key whose expiration is
-    set and not after now is db.Del'd), then per record the state the device
-    index reports: 1 = the index points at it, 2 = a Hash/List/Set record the
-    host indexes (tx ones only once committed), 0 otherwise."""
+    records per txId, updateIndex for the five indexes (String/ListMeta by
+    realKey, Hash/List/Set by the composite keys of tests/index_keys.py decoded
+    from log.Key: the stored key for a record applied at once, the realKey for
+    a committed tx record), the expirations map of String keys and the TTL
+    sweep (a key whose expiration is set and not after now is db.Del'd).  Per
+    record the state the device index reports: 1 = an index points at it and
+    merge.go's lookup (merge.go:101-132, realKey decoded) finds it, 3 = an
+    index points at it under a key merge.go does not look up, 0 otherwise.
+    Raises index_keys.GoPanic where updateIndex's decode panics; merge_panics
+    (a list) receives the records whose merge.go decode panics."""
+    from .index_keys import GoPanic, index_key
     recs = []
     for F, tt in zip(file_bytes, tuples_per_file):
         for t in tt:
             o, h, ks = int(t["offset"]), int(t["header_size"]), int(t["key_size"])
             key = bytes(F[o + h:o + h + ks])
             tx, n = mg.varint(key)
-            recs.append((key[n:] if n > 0 else key, t, tx))
-    index = {mg.STRING: {}, mg.LISTMETA: {}}
+            recs.append((key, key[n:] if n > 0 else key, t, tx))
+    index = {}                      # index key -> record (all five indexes, flattened)
     expirations = {}
     state = [0] * len(recs)
     txrecords = {}
 
-    def update(i):
-        rk, t, _ = recs[i]
+    def update(i, log_key):
+        _, rk, t, _ = recs[i]
         dt = int(t["data_type"])
-        if dt in (mg.HASH, mg.LIST, mg.SET):
-            state[i] = 2
-        elif dt in index:
-            if int(t["type"]) == mg.DELETED:
-                index[dt].pop(rk, None)
-                if dt == mg.STRING:
-                    expirations.pop(rk, None)
-            else:
-                index[dt][rk] = i
-                if dt == mg.STRING:
-                    expirations[rk] = int(t["expiration"])
+        if dt in (mg.STRING, mg.LISTMETA):
+            ik = (dt, rk)           # updateIndex's key argument: the realKey
+        else:
+            ik = index_key(dt, log_key)
+            if ik is None:
+                return
+        if int(t["type"]) == mg.DELETED:
+            index.pop(ik, None)
+            if dt == mg.STRING:
+                expirations.pop(rk, None)
+        else:
+            index[ik] = i
+            if dt == mg.STRING:
+                expirations[rk] = int(t["expiration"])
 
-    for i, (rk, t, tx) in enumerate(recs):
+    for i, (key, rk, t, tx) in enumerate(recs):
         if tx == 0:
-            update(i)
+            update(i, key)
         elif int(t["type"]) == mg.TXN_BEGIN:
             pass
         elif int(t["type"]) == mg.TXN_COMMIT:
             for j in txrecords.pop(tx, []):
-                update(j)
+                update(j, recs[j][1])
         elif int(t["type"]) == mg.TXN_ROLLBACK:
             txrecords.pop(tx, None)
         else:
@@ -246,10 +394,21 @@ def index_states(file_bytes, tuples_per_file, now_ns=INDEX_NOW):
     if now_ns is not None:
         for rk, exp in expirations.items():
             if exp != 0 and not exp > now_ns:
-                index[mg.STRING].pop(rk, None)
-    for d in index.values():
-        for i in d.values():
-            state[i] = 1
+                index.pop((mg.STRING, rk), None)
+    for ik, i in index.items():
+        _, rk, t, _ = recs[i]
+        try:
+            mk = index_key(int(t["data_type"]), rk)
+        except GoPanic:
+            mk = None
+        state[i] = 1 if mk == ik else 3
+    if merge_panics is not None:
+        for i, (_, rk, t, _) in enumerate(recs):
+            if int(t["data_type"]) in (mg.HASH, mg.LIST, mg.SET):
+                try:
+                    index_key(int(t["data_type"]), rk)
+                except GoPanic:
+                    merge_panics.append(i)
     return np.array(state, np.uint8)
 
 

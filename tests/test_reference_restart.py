@@ -9,6 +9,7 @@ state the test asserts:
   TestDB_Reboot        db_test.go:214-261  10 000 keys, Get == key || 1024 zero bytes, 8 MiB files
   TestDB_TTL_Restart   ttl_test.go:55-88   PutWithExpiration(2 s); after 2 s the reloaded Get fails
   TestTxn_Hash_Restart txnHash_test.go:179-223  HGet(0,0), HGet(1,1) found; HGet(1,2) ErrKeyNotFound
+  TestTxn_List_Restart txnList_test.go:104-161  LPush/RPush 0..6; after reload LPop 3, LPop 2, RPop 6
 
 CPU: the same files through the oracle scan and the literal loadIndex
 restatement (index_states) give the asserted visible String keys.
@@ -59,6 +60,51 @@ def hash_files():
     HSet(1,2,2), HDel(1,2), Commit (the golden fixture txn_hash)."""
     with open(os.path.join(os.path.dirname(__file__), "golden", "txn_hash.cly"), "rb") as f:
         return [f.read()]
+
+
+def list_files():
+    """TestTxn_List_Restart's transaction, restated through txn.push
+    (txnList.go:96-160: per value a List record keyed encodeListKey(cur, prev,
+    next, key), then the ListMeta record encodeListMeta(head, tail); getListMeta
+    reads the txn's pending ListMeta, else head 1 / tail 0) between the Begin
+    and Commit markers of txn.go:258-283."""
+    from .index_keys import encode_list_key, encode_list_meta
+    tx = 1_700_000_000_000
+    k = mg.test_key(0)
+    head, tail = 1, 0
+    out = [(mg.TX_BEGIN_KEY, b"", mg.TXN_BEGIN, mg.STRING, 0)]
+    for vals, left in (([0], True), ([1], True), ([2, 3], True), ([4], False), ([5, 6], False)):
+        for v in vals:
+            if left:
+                cur = head - 1
+                prev, nxt = cur - 1, head
+                head = cur
+            else:
+                cur = tail + 1
+                prev, nxt = tail, cur + 1
+                tail = cur
+            out.append((encode_list_key(cur, prev, nxt, k), mg.test_key(v), mg.NORMAL, mg.LIST, 0))
+        out.append((k, encode_list_meta(head, tail), mg.NORMAL, mg.LISTMETA, 0))
+    out.append((mg.TX_COMMIT_KEY, b"", mg.TXN_COMMIT, mg.STRING, 0))
+    b = b"".join(mg.encode_record(mg.key_tx(key, tx), v, typ, dt, e) for key, v, typ, dt, e in out)
+    return [b]
+
+
+def gob_int(buf):
+    """The integer value of a writer's gob-encoded seq (GobDecode of an exact
+    integer Float)."""
+    if buf[1] & 0x06 == 0:
+        return 0
+    e = int.from_bytes(buf[6:10], "big")
+    v = int.from_bytes(buf[10:18], "big") >> (64 - e)
+    return -v if buf[1] & 1 else v
+
+
+def decode_list_meta(v):
+    """decodeListMeta (txnList.go:284-294) -> (head, tail)."""
+    hl, i = mg.varint(v)
+    _, j = mg.varint(v[i:])
+    return gob_int(v[i + j:i + j + hl]), gob_int(v[i + j + hl:])
 
 
 def test_reboot_restatement():
@@ -140,3 +186,71 @@ def test_gpu_load_rejects_corruption(scanner, tmp_path):
     write_dir(tmp_path, [bytes(b), files[1]])
     with pytest.raises(ErrInvalidCRC):
         scanner.open_db(str(tmp_path))
+
+
+def test_list_restatement():
+    from .index_keys import decode_list_key
+    files = list_files()
+    a = np.frombuffer(files[0], np.uint8).copy()
+    tt, st, _ = co.scan_file(a, 0)
+    assert st == 0 and len(tt) == 7 + 5 + 2
+    states = index_states([a], [tt])
+    assert int((states == 1).sum()) == 7 + 1                 # 7 list items + the last ListMeta
+    # the list order head..tail by following next from the ListMeta head
+    meta = [t for t in tt if t["data_type"] == mg.LISTMETA][-1]
+    o, h, ks, vs = (int(meta[x]) for x in ("offset", "header_size", "key_size", "value_size"))
+    head, tail = decode_list_meta(files[0][o + h + ks:o + h + ks + vs])
+    assert (head, tail) == (-3, 3)
+    by_seq = {}
+    for t in tt:
+        if t["data_type"] == mg.LIST:
+            o, h, ks, vs = (int(t[x]) for x in ("offset", "header_size", "key_size", "value_size"))
+            key = files[0][o + h:o + h + ks]
+            _, n = mg.varint(key)
+            _, seq = decode_list_key(key[n:])
+            by_seq[gob_int(seq)] = files[0][o + h + ks:o + h + ks + vs]
+    assert [by_seq[i] for i in range(head, tail + 1)] == [mg.test_key(x) for x in (3, 2, 1, 0, 4, 5, 6)]
+
+
+@pytest.mark.gpu
+def test_gpu_txn_list_restart(scanner, tmp_path):
+    """After reload: LPop -> key 3, LPop -> key 2, RPop -> key 6 (txn.pop,
+    txnList.go:162-232: head/tail from the ListMeta index, the item from the
+    List index by the seq's gob encoding, the next head from the item's key)."""
+    from .index_keys import decode_list_key, gob_encode_int
+    files = list_files()
+    write_dir(tmp_path, files)
+    scanner.set_clock(0)
+    with scanner.open_db(str(tmp_path)) as db:
+        assert db.stats.list_items == 7 and db.stats.listmeta_keys == 1
+        k = mg.test_key(0)
+        head, tail = decode_list_meta(db.value(db.listmeta_pos(k)))
+
+        tt, _, _ = co.scan_file(np.frombuffer(files[0], np.uint8).copy(), 0)
+        at = {int(t["offset"]): t for t in tt}
+
+        def pop(seq):
+            pos = db.lpos(k, gob_encode_int(seq))
+            t = at[pos.offset]
+            o, h, ks = pos.offset, int(t["header_size"]), int(t["key_size"])
+            key = files[pos.fid][o + h:o + h + ks]
+            _, n = mg.varint(key)
+            _, s = decode_list_key(key[n:])
+            # the prev/next seqs follow seq in the key (encodeListKey)
+            ln, idx = [], 0
+            for _ in range(3):
+                v, i = mg.varint(key[n + idx:])
+                ln.append(v)
+                idx += i
+            rest = key[n + idx + ln[0]:]
+            return db.value(pos), (gob_int(rest[:ln[1]]), gob_int(rest[ln[1]:ln[1] + ln[2]]))
+
+        v, (prev, nxt) = pop(head)
+        assert v == mg.test_key(3)
+        head = nxt
+        v, (prev, nxt) = pop(head)
+        assert v == mg.test_key(2)
+        v, (prev, nxt) = pop(tail)
+        assert v == mg.test_key(6)
+        with pytest.raises(KeyError):
+            db.lpos(k, gob_encode_int(tail + 1))
