@@ -122,11 +122,12 @@ struct Globals {                 // zeroed per call
 //   [65536, +256)  inverse of a zero-byte step (top byte of T0 -> index)
 //   LDS_NIB        nibble tables of A^(CLY_CH * 2^k), k < 7 (8 x 16 words each)
 //   LDS_SH         nibble tables of A^(v 16^d) (v < 16, d < 4: a byte shift by one hex
-//                  digit each), then A^65536
+//                  digit each), then A^65536 and A^(COAL_BLK - 64)
 #define LDS_INV 65536
+#define COAL_BLK 4096                    // k_crc's coalesced block (64 lanes x 64 B)
 #define LDS_NIB (LDS_INV + 256)
 #define NIB_LEVELS 7                     // A^(CLY_CH * 2^k), k < 7 (k = 6: one tile)
-#define NSH 65                           // shift tables
+#define NSH 66                           // shift tables (the last: A^(COAL_BLK - 64))
 #define LDS_SH (LDS_NIB + NIB_LEVELS * 128 * 4)
 #define NTAB ((NIB_LEVELS + NSH) * 128)  // words of nibble tables (copied from the context's buffer)
 #define SCAN_LDS (LDS_SH + NSH * 128 * 4)
@@ -1268,6 +1269,109 @@ __device__ __forceinline__ uint32_t tile_fused(const Chunk& K, const LaneChain& 
     return s;
 }
 
+// k_crc's tile stream, coalesced.  The tile is read in blocks of COAL_BLK =
+// 4 KiB: in block m, load k (k < 4) of lane i + 16 q (i < 16, q < 4) reads the
+// 16 B at 4096 m + 1024 k + 64 i + 16 q, so that each load instruction reads
+// 1 KiB of consecutive bytes (whole cache lines); a 4 x 4 transpose of 16-B
+// elements over the lane quarters (v_permlane32_swap, v_permlane16_swap) then
+// leaves lane L with the 64 consecutive bytes at 4096 m + 64 L.  Lane L's
+// register runs over its 16 segments, stepped by A^(4096 - 64) between them
+// (Horner), so A^(4096 - 64 (L + 1)) R_L is its share of the tile's raw
+// register at the tile end; bytes at or past `slim` (the chain's terminal T,
+// or the file end) read as zero.  The record rounds are interleaved as in
+// tile_fused.
+#define COAL_NB ((int)(CLY_TILE / COAL_BLK))
+#define COAL_RSTEP (COAL_NB >= 4 ? COAL_NB / 4 : 1)
+#define COAL_NR (COAL_NB / COAL_RSTEP)
+static_assert(CLY_TILE % COAL_BLK == 0, "tiles of whole 4-KiB blocks");
+__device__ __forceinline__ void swap32(uint32_t& a, uint32_t& b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+    a = r[0]; b = r[1];
+}
+__device__ __forceinline__ void swap16(uint32_t& a, uint32_t& b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+    a = r[0]; b = r[1];
+}
+// e[k] of lane quarter q -> e[j] of quarter q = what quarter j held in e[q]
+__device__ __forceinline__ void quad_transpose(u32x4* e) {
+    #pragma unroll
+    for (int c = 0; c < 4; c++) {
+        uint32_t a0 = e[0][c], a1 = e[1][c], a2 = e[2][c], a3 = e[3][c];
+        swap32(a0, a2); swap32(a1, a3);
+        swap16(a0, a1); swap16(a2, a3);
+        e[0][c] = a0; e[1][c] = a1; e[2][c] = a2; e[3][c] = a3;
+    }
+}
+__device__ __forceinline__ uint32_t tile_coal(const Chunk& K, const LBState& S, uint32_t slim,
+                                              const uint16_t* __restrict__ tp, uint32_t n, uint32_t TE, uint32_t fid,
+                                              gtuples out, uint64_t out_cap, const CLY_LDS uint8_t* smem,
+                                              const CrcLane& cl, uint32_t K4, uint32_t& pacc, gbytes zero32,
+                                              Globals* g) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t nround = (n + 63) / 64;
+    uint32_t pr[COAL_NR];
+    #pragma unroll
+    for (int k = 0; k < COAL_NR; k++) {
+        const uint32_t r = 64u * k + lane;
+        pr[k] = tp[r < n ? r : 0];
+    }
+    uint32_t prev = S.crc_last;
+    Chunk Kt = K;                                    // the tile as one chunk: piece() offsets are tile-relative
+    Kt.cb = K.tb;
+    if ((uint64_t)slim < Kt.len) Kt.len = slim;
+    const bool full = (uint64_t)K.tb + CLY_TILE <= Kt.len;
+    const uint32_t lo = 64u * (uint32_t)(lane & 15) + 16u * (uint32_t)(lane >> 4);
+    const CLY_GL u32x4* src = (const CLY_GL u32x4*)(K.base + K.tb + lo);
+    const CLY_LDS uint32_t* tblk = (const CLY_LDS uint32_t*)(smem + LDS_SH) + (NSH - 1) * 128;
+    uint32_t R = 0;
+    #pragma unroll
+    for (int m = 0; m < COAL_NB; m++) {
+        u32x4 e[4];
+        if (full) {
+            #pragma unroll
+            for (int k = 0; k < 4; k++) e[k] = src[(COAL_BLK * m + 1024 * k) / 16];
+        } else {
+            #pragma unroll
+            for (int k = 0; k < 4; k++) e[k] = piece(Kt, (uint32_t)(COAL_BLK * m + 1024 * k) + lo);
+        }
+        const int kr = m / COAL_RSTEP;
+        const bool rb = (m % COAL_RSTEP) == 0 && (uint32_t)kr < nround;
+        Gath gt;
+        uint32_t P = 0;
+        bool act = false;
+        if (rb) {
+            const uint32_t r = 64u * kr + lane;
+            act = r < n;
+            P = K.tb + pr[kr];
+            gath_issue_at(act && gath_ok(P, K.len) ? K.base + (P & ~3u) : zero32, gt);
+        }
+        quad_transpose(e);
+        if (m) R = mat_mul(tblk, R);
+        #pragma unroll
+        for (int k = 0; k < 4; k++) {
+            R = crc_word(smem, R ^ e[k].x, cl);
+            R = crc_word(smem, R ^ e[k].y, cl);
+            R = crc_word(smem, R ^ e[k].z, cl);
+            R = crc_word(smem, R ^ e[k].w, cl);
+        }
+        if (rb) {
+            const uint32_t last = n - 64u * kr - 1 < 63u ? n - 64u * kr - 1 : 63u;
+            round_finish(K, act, P, gt, S.count + 64u * kr + lane, TE, fid, out, out_cap, smem, K4, last, prev, pacc,
+                         g, lane);
+        }
+    }
+    for (uint32_t kr = COAL_NR; kr < nround; kr++) {
+        const uint32_t r = 64u * kr + lane;
+        const bool act = r < n;
+        const uint32_t P = K.tb + tp[act ? r : 0];
+        Gath gt;
+        gath_issue_at(act && gath_ok(P, K.len) ? K.base + (P & ~3u) : zero32, gt);
+        const uint32_t last = n - 64u * kr - 1 < 63u ? n - 64u * kr - 1 : 63u;
+        round_finish(K, act, P, gt, S.count + r, TE, fid, out, out_cap, smem, K4, last, prev, pacc, g, lane);
+    }
+    return shift_bytes(smem, COAL_BLK - 64u * (uint32_t)(lane + 1), R);
+}
+
 // k_crc: the CRC stream and the tuples, tiles in grid-stride order.
 #define CRC_WAVES 16
 __global__ void __launch_bounds__(64 * CRC_WAVES)
@@ -1313,17 +1417,24 @@ k_crc(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict_
             if (L.cnt || I.P_in != NONE32) pacc = shift_bytes(smem, TE - L.x, ~cT);
         }
         uint32_t r;
-        if (!ovf) r = tile_fused(K, L, I, S, live, term_lane ? L.x : 0xFFFFFFFFu, pos + (uint64_t)t * POS_CAP, tile_cnt,
-                                 TE, F.fid, out, out_cap, smem, cl, K4, pacc, (gbytes)zero32, g);
-        else r = phase_c_fast(K, L, I, live, true, term_lane ? L.x : 0xFFFFFFFFu, F.fid, out, out_cap, smem, cl, K4,
-                              pacc, g);
+        if (!ovf) {
+            // the tile's stream stops at the chain's terminal (if in this tile)
+            const uint64_t tm = __ballot(term_lane);
+            const uint32_t slim = tm ? (uint32_t)__shfl((int)L.x, __builtin_ctzll(tm), 64) : 0xFFFFFFFFu;
+            r = tile_coal(K, S, slim, pos + (uint64_t)t * POS_CAP, tile_cnt, TE, F.fid, out, out_cap, smem, cl, K4,
+                          pacc, (gbytes)zero32, g);
+        } else r = phase_c_fast(K, L, I, live, true, term_lane ? L.x : 0xFFFFFFFFu, F.fid, out, out_cap, smem, cl, K4,
+                                pacc, g);
         if (term_lane) {
             FileInfo* fo = &finfo[f];
             fo->term_pos = L.x; fo->term_status = L.term; fo->term_tile = t; fo->term_lane = (uint32_t)lane;
             fo->end_index = I.base + L.cnt; fo->has_term = 1; fo->expect = 0;
         }
-        if (!live) r = 0;
-        r = tile_fold(smem, r, lane) ^ wave_xor(pacc);
+        if (!ovf) r = wave_xor(r ^ pacc);               // lane shares already shifted to the tile end
+        else {
+            if (!live) r = 0;
+            r = tile_fold(smem, r, lane) ^ wave_xor(pacc);
+        }
         if (lane == 0) treg[t] = r;
     }
 }
@@ -1499,7 +1610,8 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
             else if (lvl < NIB_LEVELS + 64) {                                        // A^(v 16^d)
                 const int k = lvl - NIB_LEVELS;
                 nbytes = (uint64_t)(k & 15) << (4 * (k >> 4));
-            } else nbytes = 65536;                                                   // A^65536
+            } else if (lvl == NIB_LEVELS + 64) nbytes = 65536;                      // A^65536
+            else nbytes = COAL_BLK - 64;                                             // k_crc's block step
             const uint32_t xm = cly_x8n(nbytes);
             for (int nb = 0; nb < 8; nb++)
                 for (uint32_t v = 0; v < 16; v++) hn[lvl * 128 + nb * 16 + v] = cly_multmodp(xm, v << (4 * nb));
