@@ -35,6 +35,7 @@
 extern "C" hipStream_t cly_ctx_stream_internal(cly_ctx* c);
 extern "C" int64_t cly_ctx_now_internal(cly_ctx* c);
 extern "C" int cly_ctx_device_internal(cly_ctx* c);
+extern "C" hipError_t cly_ix_scratch_internal(cly_ctx* ctx, int k, size_t bytes, void** out);
 
 #define IX_NONE 0xFFFFFFFFFFFFFFFFull
 // record index of a hash-sorted entry: bit 31 carries "LogRecordDeleted" so that
@@ -56,24 +57,9 @@ __device__ __forceinline__ const uint8_t* ix_rkey(const uint64_t* bases, int f, 
     len = t.key_size - t.txid_len;
     return (const uint8_t*)bases[f] + t.offset + t.header_size + t.txid_len;
 }
-// 64-bit hash of (index, realKey): FNV-1a over 8-byte words folded by a mix
+// 64-bit hash of (index, key): ixkey.h's ixk_hash
 __device__ __forceinline__ uint64_t ix_hash(uint32_t index_kind, const uint8_t* k, uint32_t len) {
-    uint64_t h = 0xcbf29ce484222325ull ^ ((uint64_t)index_kind << 56) ^ len;
-    uint32_t q = 0;
-    for (; q + 8 <= len; q += 8) {
-        uint64_t w = 0;
-        #pragma unroll
-        for (int b = 0; b < 8; b++) w |= (uint64_t)k[q + b] << (8 * b);
-        h = (h ^ w) * 0x100000001b3ull;
-        h ^= h >> 29;
-    }
-    uint64_t w = 0;
-    for (int b = 0; q < len; q++, b++) w |= (uint64_t)k[q] << (8 * b);
-    h = (h ^ w) * 0x100000001b3ull;
-    h ^= h >> 32;
-    h *= 0xd6e8feb86659fd93ull;
-    h ^= h >> 32;
-    return h;
+    return ixk_hash(index_kind, k, len);
 }
 
 // Key signature (16 B): the first min(len, 15) realKey bytes, zero-padded, and
@@ -438,6 +424,28 @@ k_ixgatherd(const uint64_t* __restrict__ src, const uint32_t* __restrict__ sel, 
 #define ICK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
     fprintf(stderr, "clyindex: %s failed: %s\n", #x, hipGetErrorString(e_)); rc = CLY_ERR_DEVICE; goto done; } } while (0)
 
+// The key hash keeps hbits = log2(n) + 24 bits (multiple of 8, 32..64):
+// expected colliding pairs n^2 / 2^(hbits+1) <= 2^-25 n stay ~0, and the radix
+// sort makes hbits/8 passes instead of 8.  Test hook: CLY_IX_HASH_MASK (hex)
+// narrows the hash so that collisions (resolved exactly by k_ixcoll) are common.
+static uint64_t ix_hash_mask(uint64_t n, int& hbits) {
+    int lg = 0;
+    while (lg < 63 && (1ull << lg) < n) lg++;
+    hbits = (lg + 24 + 7) & ~7;
+    if (hbits < 32) hbits = 32;
+    if (hbits > 64) hbits = 64;
+    uint64_t hm = hbits == 64 ? ~0ull : (1ull << hbits) - 1;
+    const char* e = getenv("CLY_IX_HASH_MASK");
+    if (e && *e) { hm = strtoull(e, nullptr, 16); hbits = hm ? 64 - __builtin_clzll(hm) : 1; }
+    return hm;
+}
+extern "C" uint64_t cly_ix_hash_mask_internal(uint64_t n) { int hb; return ix_hash_mask(n, hb); }
+// The device buffer of the key hashes of the last cly_index_device call of
+// this context (n values: the records applied to an index; others undefined).
+extern "C" hipError_t cly_ix_hash_ptr_internal(cly_ctx* ctx, uint64_t n, void** out) {
+    return cly_ix_scratch_internal(ctx, 13, sizeof(uint64_t) * n, out);
+}
+
 static unsigned ix_grid(uint64_t n) { const uint64_t b = (n + 255) / 256; return (unsigned)(b < 16384 ? (b ? b : 1) : 16384); }
 
 extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles, const cly_tuple* d_tuples,
@@ -483,28 +491,28 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     const uint64_t* d_bases = nullptr;
     ICK(hipEventCreate(&e0));
     ICK(hipEventCreate(&e1));
-    ICK(hipMalloc((void**)&d_fb, sizeof(uint64_t) * (2 * (size_t)nfiles + 2)));
+    ICK(cly_ix_scratch_internal(ctx, 0, sizeof(uint64_t) * (2 * (size_t)nfiles + 2), (void**)&d_fb));
     d_first = d_fb;
     d_bases = d_fb + nfiles + 1;
-    ICK(hipMalloc((void**)&d_tot, sizeof(IxTot)));
-    ICK(hipMalloc((void**)&d_nsel, sizeof(unsigned long long)));
-    ICK(hipMalloc((void**)&d_cls, n));
-    ICK(hipMalloc((void**)&d_flag, n));
-    ICK(hipMalloc((void**)&d_coll, n));
-    ICK(hipMalloc((void**)&d_del, n));
-    ICK(hipMalloc((void**)&d_apflag, n));
-    ICK(hipMalloc((void**)&d_selv, sizeof(uint32_t) * n));
-    ICK(hipMalloc((void**)&d_ksig, sizeof(uint4) * n));
-    ICK(hipMalloc((void**)&d_txkey, sizeof(uint64_t) * n));
-    ICK(hipMalloc((void**)&d_k2, sizeof(uint64_t) * n));
-    ICK(hipMalloc((void**)&d_order, sizeof(uint64_t) * n));
-    ICK(hipMalloc((void**)&d_hash, sizeof(uint64_t) * n));
-    ICK(hipMalloc((void**)&d_sel, sizeof(uint32_t) * n));
-    ICK(hipMalloc((void**)&d_sidx, sizeof(uint32_t) * n));
-    ICK(hipMalloc((void**)&d_rev, sizeof(TxNext) * n));
-    ICK(hipMalloc((void**)&d_nxt, sizeof(TxNext) * n));
-    ICK(hipMalloc((void**)&d_g, sizeof(GMax) * n));
-    ICK(hipMalloc((void**)&d_g2, sizeof(GMax) * n));
+    ICK(cly_ix_scratch_internal(ctx, 1, sizeof(IxTot), (void**)&d_tot));
+    ICK(cly_ix_scratch_internal(ctx, 2, sizeof(unsigned long long), (void**)&d_nsel));
+    ICK(cly_ix_scratch_internal(ctx, 3, n, (void**)&d_cls));
+    ICK(cly_ix_scratch_internal(ctx, 4, n, (void**)&d_flag));
+    ICK(cly_ix_scratch_internal(ctx, 5, n, (void**)&d_coll));
+    ICK(cly_ix_scratch_internal(ctx, 6, n, (void**)&d_del));
+    ICK(cly_ix_scratch_internal(ctx, 7, n, (void**)&d_apflag));
+    ICK(cly_ix_scratch_internal(ctx, 8, sizeof(uint32_t) * n, (void**)&d_selv));
+    ICK(cly_ix_scratch_internal(ctx, 9, sizeof(uint4) * n, (void**)&d_ksig));
+    ICK(cly_ix_scratch_internal(ctx, 10, sizeof(uint64_t) * n, (void**)&d_txkey));
+    ICK(cly_ix_scratch_internal(ctx, 11, sizeof(uint64_t) * n, (void**)&d_k2));
+    ICK(cly_ix_scratch_internal(ctx, 12, sizeof(uint64_t) * n, (void**)&d_order));
+    ICK(cly_ix_scratch_internal(ctx, 13, sizeof(uint64_t) * n, (void**)&d_hash));
+    ICK(cly_ix_scratch_internal(ctx, 14, sizeof(uint32_t) * n, (void**)&d_sel));
+    ICK(cly_ix_scratch_internal(ctx, 15, sizeof(uint32_t) * n, (void**)&d_sidx));
+    ICK(cly_ix_scratch_internal(ctx, 16, sizeof(TxNext) * n, (void**)&d_rev));
+    ICK(cly_ix_scratch_internal(ctx, 17, sizeof(TxNext) * n, (void**)&d_nxt));
+    ICK(cly_ix_scratch_internal(ctx, 18, sizeof(GMax) * n, (void**)&d_g));
+    ICK(cly_ix_scratch_internal(ctx, 19, sizeof(GMax) * n, (void**)&d_g2));
     // temp storage: the largest of the select / sort / scan needs
     ICK(hipcub::DeviceSelect::Flagged(nullptr, need, cnt, d_flag, d_sel, d_nsel, (int)n, st));
     tmp_bytes = need;
@@ -514,27 +522,13 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     if (need > tmp_bytes) tmp_bytes = need;
     ICK(hipcub::DeviceScan::InclusiveScan(nullptr, need, d_g, d_g2, GMaxOp(), (int)n, st));
     if (need > tmp_bytes) tmp_bytes = need;
-    ICK(hipMalloc(&d_tmp, tmp_bytes));
+    ICK(cly_ix_scratch_internal(ctx, 20, tmp_bytes, &d_tmp));
     ICK(hipMemcpyAsync(d_fb, h_fb, sizeof(uint64_t) * (2 * (size_t)nfiles + 1), hipMemcpyHostToDevice, st));
     ICK(hipMemsetAsync(d_tot, 0, sizeof(IxTot), st));
     ICK(hipMemsetAsync(d_order, 0xff, sizeof(uint64_t) * n, st));
     ICK(hipMemsetAsync(d_coll, 0, n, st));
     ICK(hipEventRecord(e0, st));
-    {
-        // The key hash keeps hbits = log2(n) + 24 bits (multiple of 8, 32..64):
-        // expected colliding pairs n^2 / 2^(hbits+1) <= 2^-25 n stay ~0, and the
-        // radix sort makes hbits/8 passes instead of 8.
-        int lg = 0;
-        while (lg < 63 && (1ull << lg) < n) lg++;
-        hbits = (lg + 24 + 7) & ~7;
-        if (hbits < 32) hbits = 32;
-        if (hbits > 64) hbits = 64;
-        hm = hbits == 64 ? ~0ull : (1ull << hbits) - 1;
-        // test hook: CLY_IX_HASH_MASK (hex) narrows the key hash so that collisions
-        // (resolved exactly by k_ixcoll) become common
-        const char* e = getenv("CLY_IX_HASH_MASK");
-        if (e && *e) { hm = strtoull(e, nullptr, 16); hbits = hm ? 64 - __builtin_clzll(hm) : 1; }
-    }
+    hm = ix_hash_mask(n, hbits);
     k_ixclass<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_state, d_txkey, d_flag, d_tot, d_first, d_bases, nfiles,
                                     d_order, d_hash, d_apflag, d_del, d_ksig, d_selv, hm);
     ICK(hipMemcpyAsync(&h_tot, d_tot, sizeof(IxTot), hipMemcpyDeviceToHost, st));
@@ -616,12 +610,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
         ir->index_ms = ms;
     }
 done:
-    hipStreamSynchronize(st);
-    {
-        void* bufs[] = {d_fb, d_tot, d_nsel, d_cls, d_flag, d_coll, d_del, d_apflag, d_selv, d_ksig, d_txkey, d_k2, d_order, d_hash, d_sel, d_sidx,
-                        d_rev, d_nxt, d_g, d_g2, d_tmp};
-        for (void* b : bufs) if (b) hipFree(b);
-    }
+    hipStreamSynchronize(st);                     // (the buffers stay in the context's scratch)
     if (e0) hipEventDestroy(e0);
     if (e1) hipEventDestroy(e1);
     free(h_fb);

@@ -29,6 +29,8 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
+#include <memory>
 #include <thread>
 #include <string>
 #include <unordered_map>
@@ -40,6 +42,9 @@
 
 extern "C" hipStream_t cly_ctx_stream_internal(cly_ctx* c);
 extern "C" int cly_ctx_device_internal(cly_ctx* c);
+extern "C" uint64_t cly_ix_hash_mask_internal(uint64_t n);
+extern "C" hipError_t cly_ix_hash_ptr_internal(cly_ctx* ctx, uint64_t n, void** out);
+#define LOAD_PIECE (64ull << 20)
 
 struct Mapped {
     uint32_t fid;
@@ -63,17 +68,31 @@ struct FlatIndex {
     FlatShard sh[FLAT_SHARDS];
     uint64_t n = 0;
 };
-static inline int flat_shard(uint64_t h) { return (int)(h >> (64 - FLAT_SHARD_BITS)); }
+// shard = the top FLAT_SHARD_BITS of the hash's valid bits (the device hash keeps hbits)
+static inline int flat_shard(uint64_t h, int hshift) { return (int)((h >> hshift) & (FLAT_SHARDS - 1)); }
+// host array without value-initialisation (the device fills it)
+template <class T> struct HostArr {
+    std::unique_ptr<T[]> p;
+    uint64_t n = 0;
+    void alloc(uint64_t k) { p.reset(k ? new T[k] : nullptr); n = k; }
+    T& operator[](uint64_t i) { return p[i]; }
+    const T& operator[](uint64_t i) const { return p[i]; }
+    uint64_t size() const { return n; }
+    T* data() { return p.get(); }
+};
 struct cly_db {
     std::vector<Mapped> files;
-    std::vector<cly_tuple> tuples;
-    std::vector<uint8_t> state;
+    HostArr<cly_tuple> tuples;
+    HostArr<uint8_t> state;
+    HostArr<uint64_t> khash;     // the device index's key hash per record (String / ListMeta tables)
+    uint64_t hmask = ~0ull;
+    int hshift = 60;
     std::vector<uint64_t> first;
     FlatIndex str, listmeta;
     // getHashIndex / getListDataIndex / getSetIndex (index.go): realKey -> MemTable
     std::unordered_map<std::string, std::unordered_map<std::string, cly_pos>> hash, list, set;
 };
-static inline uint64_t key_hash(const uint8_t* p, uint64_t n) {
+[[maybe_unused]] static inline uint64_t key_hash(const uint8_t* p, uint64_t n) {
     uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xBF58476D1CE4E5B9ull);      // FNV-style, 8 bytes a step
     uint64_t i = 0;
     for (; i + 8 <= n; i += 8) {
@@ -88,6 +107,17 @@ static inline uint64_t key_hash(const uint8_t* p, uint64_t n) {
     h ^= h >> 32;
     h *= 0x94D049BB133111EBull;
     return (h ^ (h >> 31)) | 1;
+}
+
+// fn(t) on nthreads threads (t = 0 on the caller's)
+template <class F> static void par_run(int nthreads, F fn) {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; t++) th.emplace_back(fn, t);
+    fn(0);
+    for (auto& x : th) x.join();
+}
+static int load_threads() {
+    return (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
 }
 
 static double now_ms() {
@@ -134,9 +164,11 @@ static void flat_put(FlatShard& x, uint64_t h, uint64_t ti) {
     x.n++;
 }
 static void flat_build(cly_db* db, int nthreads);
-static int flat_get(const cly_db* db, const FlatIndex& xi, const uint8_t* key, uint64_t klen, cly_pos* pos) {
-    const uint64_t h = key_hash(key, klen);
-    const FlatShard& x = xi.sh[flat_shard(h)];
+static int flat_get(const cly_db* db, const FlatIndex& xi, uint32_t kind, const uint8_t* key, uint64_t klen,
+                    cly_pos* pos) {
+    if (klen > 0xFFFFFFFFull) return CLY_DB_NOT_FOUND;
+    const uint64_t h = (ixk_hash(kind, key, (uint32_t)klen) & db->hmask) | 1;
+    const FlatShard& x = xi.sh[flat_shard(h, db->hshift)];
     if (!x.mask) return CLY_DB_NOT_FOUND;
     for (uint64_t i = h & x.mask; x.h[i]; i = (i + 1) & x.mask) {
         if (x.h[i] != h) continue;
@@ -178,7 +210,7 @@ static int list_files(const char* dir, std::vector<Mapped>& out) {
         m.len = (uint64_t)sb.st_size;
         m.p = nullptr;
         if (m.len) {
-            void* p = mmap(nullptr, m.len, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+            void* p = mmap(nullptr, m.len, PROT_READ, MAP_PRIVATE, fd, 0);     // pages: faulted in by the copy threads
             if (p == MAP_FAILED) { close(fd); return CLY_ERR_ARG; }
             m.p = (const uint8_t*)p;
         }
@@ -188,8 +220,9 @@ static int list_files(const char* dir, std::vector<Mapped>& out) {
     return CLY_OK;
 }
 
-// Two passes over the LIVE tuples, each split over `nthreads` threads: hash the
-// keys and count them per shard, then let thread t fill shards t, t+T, ...
+// Two passes over the LIVE tuples, each split over `nthreads` threads: count
+// the records per shard (the key hashes are the device index's, downloaded),
+// then let thread t fill shards t, t+T, ...
 static void flat_build(cly_db* db, int nthreads) {
     const uint64_t need = db->tuples.size();
     std::vector<uint64_t> hv(need);
@@ -201,10 +234,8 @@ static void flat_build(cly_db* db, int nthreads) {
             hv[i] = 0;
             const uint32_t dt = db->tuples[i].data_type;
             if (db->state[i] != CLY_IX_LIVE || (dt != 0 && dt != 3)) continue;     // String / ListMeta
-            uint64_t n;
-            const uint8_t* k = real_key_ptr(db, db->tuples[i], n);
-            hv[i] = key_hash(k, n);
-            c[(db->tuples[i].data_type == 3) * FLAT_SHARDS + flat_shard(hv[i])]++;
+            hv[i] = (db->khash[i] & db->hmask) | 1;
+            c[(dt == 3) * FLAT_SHARDS + flat_shard(hv[i], db->hshift)]++;
         }
     };
     auto fill_part = [&](int t) {
@@ -216,8 +247,8 @@ static void flat_build(cly_db* db, int nthreads) {
             }
         for (uint64_t i = 0; i < need; i++) {
             const uint64_t h = hv[i];
-            if (!h || flat_shard(h) % nthreads != t) continue;
-            flat_put((db->tuples[i].data_type == 3 ? db->listmeta : db->str).sh[flat_shard(h)], h, i);
+            if (!h || flat_shard(h, db->hshift) % nthreads != t) continue;
+            flat_put((db->tuples[i].data_type == 3 ? db->listmeta : db->str).sh[flat_shard(h, db->hshift)], h, i);
         }
     };
     std::vector<std::thread> th;
@@ -274,15 +305,33 @@ extern "C" int cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load
     }
     DCK(hipMalloc((void**)&d_bytes, total + 4096));
     {
+        // the files' pages are faulted in and copied by load_threads() threads,
+        // 64-MiB pieces each (pageable copies from several threads overlap)
+        struct Piece { const uint8_t* src; uint8_t* dst; uint64_t len; };
+        std::vector<Piece> pieces;
         uint64_t off = 0;
         for (int i = 0; i < nf; i++) {
             df[i] = hf[i];
             df[i].base = d_bytes + off;
-            if (hf[i].len) DCK(hipMemcpyAsync(d_bytes + off, hf[i].base, hf[i].len, hipMemcpyHostToDevice, strm));
+            for (uint64_t a = 0; a < hf[i].len; a += LOAD_PIECE)
+                pieces.push_back({hf[i].base + a, d_bytes + off + a, std::min<uint64_t>(LOAD_PIECE, hf[i].len - a)});
             off += (hf[i].len + 4095) & ~4095ull;
         }
+        std::atomic<size_t> next(0);
+        std::atomic<int> err(0);
+        const int dev = cly_ctx_device_internal(ctx);
+        par_run(load_threads(), [&](int) {
+            if (hipSetDevice(dev) != hipSuccess) { err = 1; return; }
+            for (size_t k; (k = next.fetch_add(1)) < pieces.size();) {
+                const Piece& pc = pieces[k];
+                volatile uint8_t sink = 0;
+                for (uint64_t a = 0; a < pc.len; a += 4096) sink ^= pc.src[a];
+                (void)sink;
+                if (hipMemcpy(pc.dst, pc.src, pc.len, hipMemcpyHostToDevice) != hipSuccess) err = 1;
+            }
+        });
+        if (err) { rc = CLY_ERR_DEVICE; goto done; }
     }
-    DCK(hipStreamSynchronize(strm));
     t2 = now_ms();
     s.h2d_ms = t2 - t1;
     cap = cly_scan_capacity(hf.data(), nf) + 16;
@@ -298,13 +347,35 @@ extern "C" int cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load
     DCK(hipMalloc((void**)&d_state, need ? need : 1));
     rc = cly_index_device(ctx, df.data(), nf, d_tup, db->first.data(), res.data(), d_state, &ir, nullptr);
     if (rc != CLY_OK) goto done;
-    db->tuples.resize(need);
-    db->state.resize(need);
-    if (need) {
-        DCK(hipMemcpyAsync(db->tuples.data(), d_tup, sizeof(cly_tuple) * need, hipMemcpyDeviceToHost, strm));
-        DCK(hipMemcpyAsync(db->state.data(), d_state, need, hipMemcpyDeviceToHost, strm));
-    }
+    db->tuples.alloc(need);
+    db->state.alloc(need);
+    db->khash.alloc(need);
+    db->hmask = cly_ix_hash_mask_internal(need);
+    db->hshift = 64 - __builtin_clzll(db->hmask | 15) - FLAT_SHARD_BITS;
     DCK(hipStreamSynchronize(strm));
+    if (need) {
+        // tuples, states and key hashes back, in pieces from several threads
+        uint64_t* d_hash = nullptr;
+        DCK(cly_ix_hash_ptr_internal(ctx, need, (void**)&d_hash));
+        struct Piece { void* dst; const void* src; uint64_t len; };
+        std::vector<Piece> pieces;
+        auto add = [&](void* dst, const void* src, uint64_t len) {
+            for (uint64_t a = 0; a < len; a += LOAD_PIECE)
+                pieces.push_back({(uint8_t*)dst + a, (const uint8_t*)src + a, std::min<uint64_t>(LOAD_PIECE, len - a)});
+        };
+        add(db->tuples.data(), d_tup, sizeof(cly_tuple) * need);
+        add(db->state.data(), d_state, need);
+        add(db->khash.data(), d_hash, sizeof(uint64_t) * need);
+        std::atomic<size_t> next(0);
+        std::atomic<int> err(0);
+        const int dev = cly_ctx_device_internal(ctx);
+        par_run(load_threads(), [&](int) {
+            if (hipSetDevice(dev) != hipSuccess) { err = 1; return; }
+            for (size_t k; (k = next.fetch_add(1)) < pieces.size();)
+                if (hipMemcpy(pieces[k].dst, pieces[k].src, pieces[k].len, hipMemcpyDeviceToHost) != hipSuccess) err = 1;
+        });
+        if (err) { rc = CLY_ERR_DEVICE; goto done; }
+    }
     t4 = now_ms();
     s.index_ms = t4 - t3;
     s.records = need;
@@ -312,7 +383,7 @@ extern "C" int cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load
         // MemTable inserts (updateIndex, db.go:511-575) for the records the
         // device marked as index entries: String / ListMeta into the flat
         // tables, Hash / List / Set into realKey -> (field | seqBuf | hashKey) maps
-        flat_build(db, (int)std::min<unsigned>(FLAT_SHARDS, std::max(1u, std::thread::hardware_concurrency())));
+        flat_build(db, std::min(FLAT_SHARDS, load_threads()));
         for (uint64_t i = 0; i < need; i++) {
             const uint8_t stt = db->state[i];
             const cly_tuple& t = db->tuples[i];
@@ -359,12 +430,12 @@ static int found(const cly_pos* src, cly_pos* pos) {
 
 extern "C" int cly_db_get(cly_db* db, const uint8_t* key, uint64_t klen, cly_pos* pos) {
     if (!db) return CLY_ERR_ARG;
-    return flat_get(db, db->str, key, klen, pos);
+    return flat_get(db, db->str, 0, key, klen, pos);
 }
 
 extern "C" int cly_db_listmeta(cly_db* db, const uint8_t* key, uint64_t klen, cly_pos* pos) {
     if (!db) return CLY_ERR_ARG;
-    return flat_get(db, db->listmeta, key, klen, pos);
+    return flat_get(db, db->listmeta, 3, key, klen, pos);
 }
 
 extern "C" int cly_db_hget(cly_db* db, const uint8_t* key, uint64_t klen, const uint8_t* field, uint64_t flen,

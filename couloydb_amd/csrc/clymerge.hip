@@ -44,7 +44,10 @@ extern "C" void** cly_ctx_merge_slot_internal(cly_ctx* c);
 
 // Scratch buffers of the merge, kept in the context and grown on demand
 // (plain hipMalloc: no allocation inside a timed merge once warm).
-enum { MS_FB, MS_TOT, MS_PLAN, MS_BSUM, MS_ENT, MS_FSTART, MS_FLEN, MS_CP, MS_PRE, MS_BMAP, MS_HSZ, MS_N };
+enum { MS_FB, MS_TOT, MS_PLAN, MS_BSUM, MS_ENT, MS_FSTART, MS_FLEN, MS_CP, MS_PRE, MS_BMAP, MS_HSZ,
+       MS_A0 = 16, MS_AN = MS_A0 + 16,            // cly_append_device's buffers
+       MS_I0 = MS_AN, MS_IN = MS_I0 + 32,         // cly_index_device's buffers (clyindex.hip)
+       MS_N = MS_IN };
 struct MergeScratch { void* p[MS_N]; size_t cap[MS_N]; };
 extern "C" void cly_merge_scratch_free(void* v) {
     MergeScratch* m = (MergeScratch*)v;
@@ -72,6 +75,12 @@ static hipError_t scratch(cly_ctx* ctx, int slot, size_t bytes, T** out) {
     }
     *out = (T*)m->p[slot];
     return hipSuccess;
+}
+
+// for clyindex.hip: slot k of the index's range
+extern "C" hipError_t cly_ix_scratch_internal(cly_ctx* ctx, int k, size_t bytes, void** out) {
+    if (k < 0 || MS_I0 + k >= MS_IN) return hipErrorInvalidValue;
+    return scratch(ctx, MS_I0 + k, bytes, out);
 }
 
 #define M_NT 256
@@ -1157,13 +1166,13 @@ extern "C" int cly_append_device(cly_ctx* ctx, const cly_rec_in* d_recs, uint64_
     const unsigned grid = (unsigned)((nt + 255) / 256 < 16384 ? (nt + 255) / 256 : 16384);
     MCK(hipEventCreate(&e0));
     MCK(hipEventCreate(&e1));
-    MCK(hipMalloc((void**)&d_sz, sizeof(uint64_t) * nt));
-    MCK(hipMalloc((void**)&d_g, sizeof(uint64_t) * nt));
-    MCK(hipMalloc((void**)&d_nout, sizeof(uint32_t)));
-    MCK(hipMalloc((void**)&d_mx, sizeof(unsigned long long)));
+    MCK(scratch(ctx, MS_A0 + 0, sizeof(uint64_t) * nt, &d_sz));
+    MCK(scratch(ctx, MS_A0 + 1, sizeof(uint64_t) * nt, &d_g));
+    MCK(scratch(ctx, MS_A0 + 2, sizeof(uint32_t), &d_nout));
+    MCK(scratch(ctx, MS_A0 + 3, sizeof(unsigned long long), &d_mx));
     MCK(hipMemsetAsync(d_mx, 0, sizeof(unsigned long long), st));
     MCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, d_sz, d_g, (int)nt, st));
-    MCK(hipMalloc(&d_tmp, tb + 16));
+    MCK(scratch(ctx, MS_A0 + 4, tb + 16, (char**)&d_tmp));
     MCK(hipEventRecord(e0, st));
     k_asize<<<grid, 256, 0, st>>>((const ARec*)d_recs, n, nt, tx_id, d_sz, d_mx);
     MCK(hipcub::DeviceScan::ExclusiveSum(d_tmp, tb, d_sz, d_g, (int)nt, st));
@@ -1185,8 +1194,8 @@ extern "C" int cly_append_device(cly_ctx* ctx, const cly_rec_in* d_recs, uint64_
     // exists because the first could not take its first record)
     fcap = 2 * (total + write_off) / data_file_size + 4;
     if (fcap > nt + 2) fcap = nt + 2;
-    MCK(hipMalloc((void**)&d_fstart, sizeof(uint64_t) * (fcap + 1)));
-    MCK(hipMalloc((void**)&d_flen, sizeof(uint64_t) * (fcap + 1)));
+    MCK(scratch(ctx, MS_A0 + 5, sizeof(uint64_t) * (fcap + 1), &d_fstart));
+    MCK(scratch(ctx, MS_A0 + 6, sizeof(uint64_t) * (fcap + 1), &d_flen));
     k_arot<<<1, M_ROT, 0, st>>>(d_g, nt, total, data_file_size, write_off, (uint32_t)fcap, d_fstart, d_flen, d_nout);
     MCK(hipMemcpyAsync(&h_nout, d_nout, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     MCK(hipStreamSynchronize(st));
@@ -1194,9 +1203,9 @@ extern "C" int cly_append_device(cly_ctx* ctx, const cly_rec_in* d_recs, uint64_
     ar->bytes = total;
     if (h_nout > out_max_files || !d_out || !d_pos) { rc = CLY_ERR_CAPACITY; goto done; }
     nblocks = (uint64_t)h_nout * (stride / M_CB);
-    MCK(hipMalloc((void**)&d_cp, sizeof(MCopy) * 2 * nt));
-    MCK(hipMalloc((void**)&d_pre, (size_t)A_PRE * 2 * nt));
-    MCK(hipMalloc((void**)&d_bmap, sizeof(uint32_t) * (nblocks + 1)));
+    MCK(scratch(ctx, MS_A0 + 7, sizeof(MCopy) * 2 * nt, &d_cp));
+    MCK(scratch(ctx, MS_A0 + 8, (size_t)A_PRE * 2 * nt, &d_pre));
+    MCK(scratch(ctx, MS_A0 + 9, sizeof(uint32_t) * (nblocks + 1), &d_bmap));
     k_aplace<<<grid, 256, 0, st>>>((const ARec*)d_recs, n, nt, tx_id, d_g, d_fstart, d_nout, write_off, active_fid,
                                    stride, d_cp, d_pre, d_bmap, d_pos);
     {
@@ -1221,11 +1230,7 @@ extern "C" int cly_append_device(cly_ctx* ctx, const cly_rec_in* d_recs, uint64_
         ar->append_ms = ms;
     }
 done:
-    hipStreamSynchronize(st);
-    {
-        void* bufs[] = {d_sz, d_g, d_fstart, d_flen, d_nout, d_bmap, d_cp, d_pre, d_tmp, d_mx};
-        for (void* b : bufs) if (b) hipFree(b);
-    }
+    hipStreamSynchronize(st);                     // (the buffers stay in the context's scratch)
     free(h_flen);
     if (e0) hipEventDestroy(e0);
     if (e1) hipEventDestroy(e1);

@@ -201,3 +201,24 @@ CLY_DEV void ixk_input(const cly_tuple& t, uint32_t& off, uint32_t& len, bool me
     if (t.tx_id == 0 && !merge) { off = 0; len = t.key_size; }
     else { off = tl; len = t.key_size - tl; }
 }
+
+// 64-bit hash of (index kind, key bytes): FNV-1a over 8-byte words folded by a
+// mix; the device index sorts on it (clyindex.hip) and the load driver's String
+// / ListMeta tables use the same values (downloaded, not recomputed).
+CLY_DEV uint64_t ixk_hash(uint32_t kind, const uint8_t* k, uint32_t len) {
+    uint64_t h = 0xcbf29ce484222325ull ^ ((uint64_t)kind << 56) ^ len;
+    uint32_t q = 0;
+    for (; q + 8 <= len; q += 8) {
+        uint64_t w = 0;
+        for (int b = 0; b < 8; b++) w |= (uint64_t)k[q + b] << (8 * b);
+        h = (h ^ w) * 0x100000001b3ull;
+        h ^= h >> 29;
+    }
+    uint64_t w = 0;
+    for (int b = 0; q < len; q++, b++) w |= (uint64_t)k[q] << (8 * b);
+    h = (h ^ w) * 0x100000001b3ull;
+    h ^= h >> 32;
+    h *= 0xd6e8feb86659fd93ull;
+    h ^= h >> 32;
+    return h;
+}
