@@ -31,6 +31,7 @@
 #include <algorithm>
 #include <atomic>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <string>
 #include <unordered_map>
@@ -45,6 +46,11 @@ extern "C" int cly_ctx_device_internal(cly_ctx* c);
 extern "C" uint64_t cly_ix_hash_mask_internal(uint64_t n);
 extern "C" hipError_t cly_ix_hash_ptr_internal(cly_ctx* ctx, uint64_t n, void** out);
 #define LOAD_PIECE (64ull << 20)
+#define LOAD_STAGE (8ull << 20)            // page-locked staging buffer (two per copy thread)
+#define LOAD_THREADS_MAX 16
+// process-wide staging buffers of the file copies (allocated on first use)
+static std::mutex g_stage_mu;
+static void* g_stage[2 * LOAD_THREADS_MAX];
 
 struct Mapped {
     uint32_t fid;
@@ -117,7 +123,7 @@ template <class F> static void par_run(int nthreads, F fn) {
     for (auto& x : th) x.join();
 }
 static int load_threads() {
-    return (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+    return (int)std::min<unsigned>(LOAD_THREADS_MAX, std::max(1u, std::thread::hardware_concurrency()));
 }
 
 static double now_ms() {
@@ -163,7 +169,7 @@ static void flat_put(FlatShard& x, uint64_t h, uint64_t ti) {
     x.ti[i] = ti;
     x.n++;
 }
-static void flat_build(cly_db* db, int nthreads);
+static void flat_build(cly_db* db, int nthreads, std::vector<uint64_t>& composite);
 static int flat_get(const cly_db* db, const FlatIndex& xi, uint32_t kind, const uint8_t* key, uint64_t klen,
                     cly_pos* pos) {
     if (klen > 0xFFFFFFFFull) return CLY_DB_NOT_FOUND;
@@ -223,42 +229,73 @@ static int list_files(const char* dir, std::vector<Mapped>& out) {
 // Two passes over the LIVE tuples, each split over `nthreads` threads: count
 // the records per shard (the key hashes are the device index's, downloaded),
 // then let thread t fill shards t, t+T, ...
-static void flat_build(cly_db* db, int nthreads) {
+static void flat_build(cly_db* db, int nthreads, std::vector<uint64_t>& composite) {
     const uint64_t need = db->tuples.size();
-    std::vector<uint64_t> hv(need);
+    std::vector<std::vector<uint64_t>> comp(nthreads);
+    HostArr<uint64_t> hv;
+    hv.alloc(need);
     std::vector<uint64_t> cnt((size_t)nthreads * 2 * FLAT_SHARDS, 0);
     auto hash_part = [&](int t) {
         const uint64_t a = need * t / nthreads, b = need * (t + 1) / nthreads;
         uint64_t* c = &cnt[(size_t)t * 2 * FLAT_SHARDS];
         for (uint64_t i = a; i < b; i++) {
             hv[i] = 0;
+            const uint8_t st = db->state[i];
+            if (st != CLY_IX_LIVE && st != CLY_IX_LOADONLY) continue;
             const uint32_t dt = db->tuples[i].data_type;
-            if (db->state[i] != CLY_IX_LIVE || (dt != 0 && dt != 3)) continue;     // String / ListMeta
+            if (dt == 1 || dt == 2 || dt == 4) { comp[t].push_back(i); continue; }    // Hash / List / Set
+            if (st != CLY_IX_LIVE || (dt != 0 && dt != 3)) continue;               // String / ListMeta
             hv[i] = (db->khash[i] & db->hmask) | 1;
             c[(dt == 3) * FLAT_SHARDS + flat_shard(hv[i], db->hshift)]++;
+        }
+    };
+    std::vector<uint64_t> boff((size_t)nthreads * 2 * FLAT_SHARDS + 1, 0);
+    HostArr<uint64_t> bidx;
+    auto scatter_part = [&](int t) {
+        const uint64_t a = need * t / nthreads, b = need * (t + 1) / nthreads;
+        uint64_t w[2 * FLAT_SHARDS];
+        for (int ks = 0; ks < 2 * FLAT_SHARDS; ks++) w[ks] = boff[(size_t)ks * nthreads + t];
+        for (uint64_t i = a; i < b; i++) {
+            if (!hv[i]) continue;
+            const int ks = (db->tuples[i].data_type == 3) * FLAT_SHARDS + flat_shard(hv[i], db->hshift);
+            bidx[w[ks]++] = i;
         }
     };
     auto fill_part = [&](int t) {
         for (int kind = 0; kind < 2; kind++)
             for (int sh = t; sh < FLAT_SHARDS; sh += nthreads) {
-                uint64_t n = 0;
-                for (int u = 0; u < nthreads; u++) n += cnt[(size_t)u * 2 * FLAT_SHARDS + kind * FLAT_SHARDS + sh];
-                flat_init((kind ? db->listmeta : db->str).sh[sh], n);
+                const int ks = kind * FLAT_SHARDS + sh;
+                const uint64_t lo = boff[(size_t)ks * nthreads], hi = boff[(size_t)(ks + 1) * nthreads];
+                FlatShard& x = (kind ? db->listmeta : db->str).sh[sh];
+                flat_init(x, hi - lo);
+                for (uint64_t j = lo; j < hi; j++) flat_put(x, hv[bidx[j]], bidx[j]);
             }
-        for (uint64_t i = 0; i < need; i++) {
-            const uint64_t h = hv[i];
-            if (!h || flat_shard(h, db->hshift) % nthreads != t) continue;
-            flat_put((db->tuples[i].data_type == 3 ? db->listmeta : db->str).sh[flat_shard(h, db->hshift)], h, i);
-        }
     };
     std::vector<std::thread> th;
     for (int t = 1; t < nthreads; t++) th.emplace_back(hash_part, t);
     hash_part(0);
     for (auto& x : th) x.join();
     th.clear();
+    {
+        // bucket the records by (kind, shard): exclusive offsets over (kind, shard, thread)
+        uint64_t acc = 0;
+        for (int ks = 0; ks < 2 * FLAT_SHARDS; ks++)
+            for (int u = 0; u < nthreads; u++) {
+                boff[(size_t)ks * nthreads + u] = acc;
+                acc += cnt[(size_t)u * 2 * FLAT_SHARDS + ks];
+            }
+        boff[(size_t)nthreads * 2 * FLAT_SHARDS] = acc;
+        bidx.alloc(acc);
+    }
+    for (int t = 1; t < nthreads; t++) th.emplace_back(scatter_part, t);
+    scatter_part(0);
+    for (auto& x : th) x.join();
+    th.clear();
     for (int t = 1; t < nthreads; t++) th.emplace_back(fill_part, t);
     fill_part(0);
     for (auto& x : th) x.join();
+    composite.clear();
+    for (auto& v : comp) composite.insert(composite.end(), v.begin(), v.end());    // scan order
     db->str.n = db->listmeta.n = 0;
     for (int sh = 0; sh < FLAT_SHARDS; sh++) {
         db->str.n += db->str.sh[sh].n;
@@ -320,15 +357,40 @@ extern "C" int cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load
         std::atomic<size_t> next(0);
         std::atomic<int> err(0);
         const int dev = cly_ctx_device_internal(ctx);
-        par_run(load_threads(), [&](int) {
+        const int nt = load_threads();
+        std::lock_guard<std::mutex> lk(g_stage_mu);
+        if (!g_stage[0]) {
+            for (int k = 0; k < 2 * LOAD_THREADS_MAX; k++)
+                if (hipHostMalloc(&g_stage[k], LOAD_STAGE, hipHostMallocDefault) != hipSuccess) { g_stage[k] = nullptr; err = 1; }
+        }
+        if (err) { rc = CLY_ERR_DEVICE; goto done; }
+        par_run(nt, [&](int t) {
+            // thread t: pieces through its two page-locked staging buffers
+            // (CPU copy of one while the DMA of the other runs)
             if (hipSetDevice(dev) != hipSuccess) { err = 1; return; }
+            hipStream_t ts = nullptr;
+            hipEvent_t ev[2] = {nullptr, nullptr};
+            if (hipStreamCreateWithFlags(&ts, hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) != hipSuccess) { err = 1; return; }
+            int b = 0;
+            bool used[2] = {false, false};
             for (size_t k; (k = next.fetch_add(1)) < pieces.size();) {
                 const Piece& pc = pieces[k];
-                volatile uint8_t sink = 0;
-                for (uint64_t a = 0; a < pc.len; a += 4096) sink ^= pc.src[a];
-                (void)sink;
-                if (hipMemcpy(pc.dst, pc.src, pc.len, hipMemcpyHostToDevice) != hipSuccess) err = 1;
+                for (uint64_t a = 0; a < pc.len; a += LOAD_STAGE) {
+                    const uint64_t n = std::min<uint64_t>(LOAD_STAGE, pc.len - a);
+                    uint8_t* stg = (uint8_t*)g_stage[2 * t + b];
+                    if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) err = 1;
+                    memcpy(stg, pc.src + a, n);
+                    if (hipMemcpyAsync(pc.dst + a, stg, n, hipMemcpyHostToDevice, ts) != hipSuccess ||
+                        hipEventRecord(ev[b], ts) != hipSuccess) err = 1;
+                    used[b] = true;
+                    b ^= 1;
+                }
             }
+            if (hipStreamSynchronize(ts) != hipSuccess) err = 1;
+            hipEventDestroy(ev[0]); hipEventDestroy(ev[1]);
+            hipStreamDestroy(ts);
         });
         if (err) { rc = CLY_ERR_DEVICE; goto done; }
     }
@@ -369,10 +431,38 @@ extern "C" int cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load
         std::atomic<size_t> next(0);
         std::atomic<int> err(0);
         const int dev = cly_ctx_device_internal(ctx);
-        par_run(load_threads(), [&](int) {
+        std::lock_guard<std::mutex> lk(g_stage_mu);
+        par_run(load_threads(), [&](int t) {
+            // thread t: DMA into one staging buffer while the CPU copies the other out
             if (hipSetDevice(dev) != hipSuccess) { err = 1; return; }
-            for (size_t k; (k = next.fetch_add(1)) < pieces.size();)
-                if (hipMemcpy(pieces[k].dst, pieces[k].src, pieces[k].len, hipMemcpyDeviceToHost) != hipSuccess) err = 1;
+            hipStream_t ts = nullptr;
+            if (hipStreamCreateWithFlags(&ts, hipStreamNonBlocking) != hipSuccess) { err = 1; return; }
+            struct Pend { uint8_t* dst; uint64_t n; int b; };
+            Pend pend = {nullptr, 0, 0};
+            hipEvent_t ev[2] = {nullptr, nullptr};
+            if (hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) != hipSuccess) { err = 1; return; }
+            int b = 0;
+            auto drain = [&]() {
+                if (!pend.dst) return;
+                if (hipEventSynchronize(ev[pend.b]) != hipSuccess) err = 1;
+                memcpy(pend.dst, g_stage[2 * t + pend.b], pend.n);
+                pend.dst = nullptr;
+            };
+            for (size_t k; (k = next.fetch_add(1)) < pieces.size();) {
+                const Piece& pc = pieces[k];
+                for (uint64_t a = 0; a < pc.len; a += LOAD_STAGE) {
+                    const uint64_t n = std::min<uint64_t>(LOAD_STAGE, pc.len - a);
+                    if (hipMemcpyAsync(g_stage[2 * t + b], (const uint8_t*)pc.src + a, n, hipMemcpyDeviceToHost, ts) !=
+                            hipSuccess || hipEventRecord(ev[b], ts) != hipSuccess) err = 1;
+                    drain();
+                    pend = {(uint8_t*)pc.dst + a, n, b};
+                    b ^= 1;
+                }
+            }
+            drain();
+            hipEventDestroy(ev[0]); hipEventDestroy(ev[1]);
+            hipStreamDestroy(ts);
         });
         if (err) { rc = CLY_ERR_DEVICE; goto done; }
     }
@@ -383,12 +473,10 @@ extern "C" int cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load
         // MemTable inserts (updateIndex, db.go:511-575) for the records the
         // device marked as index entries: String / ListMeta into the flat
         // tables, Hash / List / Set into realKey -> (field | seqBuf | hashKey) maps
-        flat_build(db, std::min(FLAT_SHARDS, load_threads()));
-        for (uint64_t i = 0; i < need; i++) {
-            const uint8_t stt = db->state[i];
+        std::vector<uint64_t> composite;
+        flat_build(db, std::min(FLAT_SHARDS, load_threads()), composite);
+        for (uint64_t i : composite) {
             const cly_tuple& t = db->tuples[i];
-            if ((stt != CLY_IX_LIVE && stt != CLY_IX_LOADONLY) || !(t.data_type == 1 || t.data_type == 2 || t.data_type == 4))
-                continue;
             uint32_t off, len;
             ixk_input(t, off, len, false);
             const uint8_t* d = file_of(db, t.fid) + t.offset + t.header_size + off;
