@@ -748,10 +748,6 @@ __device__ __forceinline__ uint32_t phase_c_fast(const Chunk& K, const LaneChain
             #pragma unroll
             for (int k = 0; k < CLY_BW / 4; k++) v[k] = (u32x4){0u, 0u, 0u, 0u};
         }
-#ifdef CLY_XNOCRC
-        #pragma unroll
-        for (int k = 0; k < CLY_BW / 4; k++) s = s ^ v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;   // timing experiment
-#else
         #pragma unroll
         for (int k = 0; k < CLY_BW / 4; k++) {
             s = crc_word(smem, s ^ v[k].x, cl);
@@ -759,7 +755,6 @@ __device__ __forceinline__ uint32_t phase_c_fast(const Chunk& K, const LaneChain
             s = crc_word(smem, s ^ v[k].z, cl);
             s = crc_word(smem, s ^ v[k].w, cl);
         }
-#endif
     }
     return s;
 }
@@ -1398,11 +1393,7 @@ k_crc(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict_
         const uint32_t tt = t - F.first_tile;
         const Chunk K = make_chunk(F, tt, lane);
         const LaneChain L = lane_load(lanes, nl, (uint64_t)t * 64 + lane);
-#ifdef CLY_XFORCEWALK
-        const bool ovf = true;                 // debug build: every tile on the lane walker
-#else
         const bool ovf = (loc[t].l[0] & DF_OVF) != 0;
-#endif
         uint32_t tile_cnt;
         const LaneIn I = lane_inputs(K, L, S, lane, tile_cnt);
         const bool term_lane = L.mode == LM_CHAIN && L.term != TERM_NONE;
@@ -1988,13 +1979,6 @@ extern "C" void** cly_ctx_merge_slot_internal(cly_ctx* c) { return &c->merge_scr
 extern "C" int cly_dbg_kernel_ms(cly_ctx* c, double* out6) {
     for (int i = 0; i < 6; i++) out6[i] = c->kms[i];
     return 6;
-}
-
-// Debug: the stored record starts of tile t (tile-relative) and the tile's LOCAL flags.
-extern "C" int cly_dbg_tile(cly_ctx* c, uint32_t t, uint16_t* pos_out, uint64_t* local4) {
-    hipMemcpy(pos_out, c->d_pos + (uint64_t)t * POS_CAP, sizeof(uint16_t) * POS_CAP, hipMemcpyDeviceToHost);
-    hipMemcpy(local4, c->d_loc + t, sizeof(TileLocal), hipMemcpyDeviceToHost);
-    return POS_CAP;
 }
 
 extern "C" const char* cly_strerror(int code) {

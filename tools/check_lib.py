@@ -25,10 +25,6 @@ names = sorted(k for k in gold if not k.startswith("_"))
 FIELDS = ["offset", "expiration", "tx_id", "fid", "size", "key_size", "value_size", "type", "data_type",
           "header_size", "txid_len", "crc"]
 sc = Scanner(0, lib=lib)
-if "--force-redo" in sys.argv:            # odd sub-tiles start from wrong guesses: exercises link + fix rounds
-    import ctypes
-    sc.lib.cly_dbg_enable.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    sc.lib.cly_dbg_enable(sc.ctx, 2)
 bad = 0
 for n in names:
     g = gold[n]
