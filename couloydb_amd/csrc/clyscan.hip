@@ -1273,11 +1273,12 @@ __device__ __forceinline__ uint32_t tile_fused(const Chunk& K, const LaneChain& 
 // register runs over its 16 segments, stepped by A^(4096 - 64) between them
 // (Horner), so A^(4096 - 64 (L + 1)) R_L is its share of the tile's raw
 // register at the tile end; bytes at or past `slim` (the chain's terminal T,
-// or the file end) read as zero.  The record rounds are interleaved as in
-// tile_fused.
+// or the file end) read as zero.  Block m+1's loads are issued before block
+// m's CRC steps.  The record rounds are interleaved as in tile_fused.
 #define COAL_NB ((int)(CLY_TILE / COAL_BLK))
 #define COAL_RSTEP (COAL_NB >= 4 ? COAL_NB / 4 : 1)
 #define COAL_NR (COAL_NB / COAL_RSTEP)
+
 static_assert(CLY_TILE % COAL_BLK == 0, "tiles of whole 4-KiB blocks");
 __device__ __forceinline__ void swap32(uint32_t& a, uint32_t& b) {
     const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
@@ -1319,9 +1320,8 @@ __device__ __forceinline__ uint32_t tile_coal(const Chunk& K, const LBState& S, 
     const CLY_GL u32x4* src = (const CLY_GL u32x4*)(K.base + K.tb + lo);
     const CLY_LDS uint32_t* tblk = (const CLY_LDS uint32_t*)(smem + LDS_SH) + (NSH - 1) * 128;
     uint32_t R = 0;
-    #pragma unroll
-    for (int m = 0; m < COAL_NB; m++) {
-        u32x4 e[4];
+    u32x4 eb[2][4];
+    auto blk_load = [&](u32x4* e, int m) {
         if (full) {
             #pragma unroll
             for (int k = 0; k < 4; k++) e[k] = src[(COAL_BLK * m + 1024 * k) / 16];
@@ -1329,6 +1329,11 @@ __device__ __forceinline__ uint32_t tile_coal(const Chunk& K, const LBState& S, 
             #pragma unroll
             for (int k = 0; k < 4; k++) e[k] = piece(Kt, (uint32_t)(COAL_BLK * m + 1024 * k) + lo);
         }
+    };
+    blk_load(eb[0], 0);
+    #pragma unroll
+    for (int m = 0; m < COAL_NB; m++) {
+        u32x4* e = eb[m & 1];
         const int kr = m / COAL_RSTEP;
         const bool rb = (m % COAL_RSTEP) == 0 && (uint32_t)kr < nround;
         Gath gt;
@@ -1340,6 +1345,7 @@ __device__ __forceinline__ uint32_t tile_coal(const Chunk& K, const LBState& S, 
             P = K.tb + pr[kr];
             gath_issue_at(act && gath_ok(P, K.len) ? K.base + (P & ~3u) : zero32, gt);
         }
+        if (m + 1 < COAL_NB) blk_load(eb[(m + 1) & 1], m + 1);
         quad_transpose(e);
         if (m) R = mat_mul(tblk, R);
         #pragma unroll
