@@ -943,7 +943,7 @@ __device__ __forceinline__ bool store_positions(const Chunk& K, const LaneChain&
 // the lanes made to agree under the tile's guess G (0 for a file's first
 // tile), the lane chains and the tile's LOCAL written out.
 #define SPEC_WAVES 4
-__global__ void __launch_bounds__(64 * SPEC_WAVES, 5)
+__global__ void __launch_bounds__(64 * SPEC_WAVES, 6)   // 6 waves/SIMD (80 VGPRs): C3 k_spec -6 %
 k_spec(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
        TileLocal* loc, uint32_t* lanes, uint16_t* pos, Globals* g) {
     const uint32_t t = blockIdx.x * SPEC_WAVES + (threadIdx.x >> 6);
