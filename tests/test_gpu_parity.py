@@ -234,3 +234,35 @@ def test_config3_device_generated_properties():
         t, st_o, end = co.scan_file(wl.file_bytes(i), fid)
         got = wl.d_out[first[i] * 48:(first[i] + res[i].n_records) * 48].cpu().numpy().view(TUPLE_DTYPE)
         compare(got, res[i].status, res[i].end_offset, t, st_o, end, "c3 file %d" % i)
+
+
+@pytest.mark.gpu
+def test_gpu_host_scan_capacity_needed_exact():
+    """cly_scan (the pipelined host path, > 512 MiB so several groups) with a
+    too-small out_cap, and with out_cap = 0 as a size query: CLY_ERR_CAPACITY
+    and *needed equal to the true record count (never read res[]
+    of unscanned files); then the scan with exactly that capacity."""
+    import ctypes
+    from couloydb_amd import DataFile, Scanner, TUPLE_DTYPE, _abi
+    from .gpu_util import fixed_records_file
+    a = fixed_records_file(243_000, 256, seed=5)                 # 67 068 000 B
+    files = [DataFile(a, i) for i in range(12)]                  # 768 MiB: two pipeline groups
+    want = 12 * 243_000
+    with Scanner(0) as sc:
+        arr = sc._file_array(files)
+        first = (ctypes.c_uint64 * 12)()
+        res = (_abi.ClyFileResult * 12)()
+        need = ctypes.c_uint64()
+        for cap in (0, 10, want - 1):
+            out = np.zeros(max(cap, 1), dtype=TUPLE_DTYPE)
+            for i in range(12):                                  # garbage in res[]: must not be read
+                res[i].n_records = 0xDEADBEEF
+            rc = sc.lib.cly_scan(sc.ctx, arr, 12, out.ctypes.data, cap, first, res, ctypes.byref(need), None)
+            assert rc == _abi.ERR_CAPACITY and need.value == want, (cap, rc, need.value)
+        out = np.zeros(want, dtype=TUPLE_DTYPE)
+        rc = sc.lib.cly_scan(sc.ctx, arr, 12, out.ctypes.data, want, first, res, ctypes.byref(need), None)
+        assert rc == 0 and need.value == want
+        assert all(res[i].n_records == 243_000 and res[i].status == 0 for i in range(12))
+        assert [first[i] for i in range(12)] == [243_000 * i for i in range(12)]
+        assert (out["offset"][:243_000] == np.arange(243_000) * 276).all()
+        assert (out["fid"][243_000 * 11:] == 11).all()
