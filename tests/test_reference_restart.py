@@ -10,6 +10,9 @@ state the test asserts:
   TestDB_TTL_Restart   ttl_test.go:55-88   PutWithExpiration(2 s); after 2 s the reloaded Get fails
   TestTxn_Hash_Restart txnHash_test.go:179-223  HGet(0,0), HGet(1,1) found; HGet(1,2) ErrKeyNotFound
   TestTxn_List_Restart txnList_test.go:104-161  LPush/RPush 0..6; after reload LPop 3, LPop 2, RPop 6
+  TestDB_TTL_Reset     ttl_test.go:112-134 (as a reload): PutWithExpiration then Put; the second
+                       put's zero expiration resets the TTL (db.go:133-141, loadIndex's
+                       expirations map keeps the last put's, db.go:517) -> still there after expiry
 
 CPU: the same files through the oracle scan and the literal loadIndex
 restatement (index_states) give the asserted visible String keys.
@@ -105,6 +108,22 @@ def decode_list_meta(v):
     hl, i = mg.varint(v)
     _, j = mg.varint(v[i:])
     return gob_int(v[i + j:i + j + hl]), gob_int(v[i + j + hl:])
+
+
+def ttl_reset_files():
+    """TestDB_TTL_Reset's writes: PutWithExpiration(key0, v1, 100 ms), Put(key0, v2)."""
+    rng = random.Random(4)
+    v1, v2 = rng.randbytes(24), rng.randbytes(24)
+    files, _ = py_append([(mg.test_key(0), v1, mg.NORMAL, mg.STRING, TTL_EXP),
+                          (mg.test_key(0), v2, mg.NORMAL, mg.STRING, 0)], 0, False, b"", 0, 256 << 20)
+    return files, v2
+
+
+def test_ttl_reset_restatement():
+    files, _ = ttl_reset_files()
+    a = np.frombuffer(files[0], np.uint8).copy()
+    tt, _, _ = co.scan_file(a, 0)
+    assert list(index_states([a], [tt], now_ns=TTL_EXP + 10**9)) == [0, 1]
 
 
 def test_reboot_restatement():
@@ -254,3 +273,13 @@ def test_gpu_txn_list_restart(scanner, tmp_path):
         assert v == mg.test_key(6)
         with pytest.raises(KeyError):
             db.lpos(k, gob_encode_int(tail + 1))
+
+
+@pytest.mark.gpu
+def test_gpu_ttl_reset_restart(scanner, tmp_path):
+    files, v2 = ttl_reset_files()
+    write_dir(tmp_path, files)
+    scanner.set_clock(TTL_EXP + 10**9)           # reloaded after the first put's expiration
+    with scanner.open_db(str(tmp_path)) as db:
+        assert db.get(mg.test_key(0)) == v2
+    scanner.set_clock(0)
