@@ -361,7 +361,7 @@ extern "C" int cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load
         std::lock_guard<std::mutex> lk(g_stage_mu);
         if (!g_stage[0]) {
             for (int k = 0; k < 2 * LOAD_THREADS_MAX; k++)
-                if (hipHostMalloc(&g_stage[k], LOAD_STAGE, hipHostMallocDefault) != hipSuccess) { g_stage[k] = nullptr; err = 1; }
+                if (hipHostMalloc(&g_stage[k], LOAD_STAGE, hipHostMallocPortable) != hipSuccess) { g_stage[k] = nullptr; err = 1; }
         }
         if (err) { rc = CLY_ERR_DEVICE; goto done; }
         par_run(nt, [&](int t) {
