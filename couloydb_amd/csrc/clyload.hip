@@ -359,10 +359,11 @@ extern "C" int cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load
         const int dev = cly_ctx_device_internal(ctx);
         const int nt = load_threads();
         std::lock_guard<std::mutex> lk(g_stage_mu);
-        if (!g_stage[0]) {
-            for (int k = 0; k < 2 * LOAD_THREADS_MAX; k++)
-                if (hipHostMalloc(&g_stage[k], LOAD_STAGE, hipHostMallocPortable) != hipSuccess) { g_stage[k] = nullptr; err = 1; }
-        }
+        for (int k = 0; k < 2 * LOAD_THREADS_MAX; k++)          // (again after a failed allocation)
+            if (!g_stage[k] && hipHostMalloc(&g_stage[k], LOAD_STAGE, hipHostMallocPortable) != hipSuccess) {
+                g_stage[k] = nullptr;
+                err = 1;
+            }
         if (err) { rc = CLY_ERR_DEVICE; goto done; }
         par_run(nt, [&](int t) {
             // thread t: pieces through its two page-locked staging buffers
