@@ -10,5 +10,5 @@ while read -r set; do
   [[ -z "$set" ]] && continue
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $set --kernel-trace --output-format csv -d gpurun_out/pmc/p$i -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-path > gpurun_out/pmc/p$i.log 2>&1 || exit $?
-done < "${1:-tools/pmc_sets.txt}"
+done < "${1:-tools/pmc_sets_r2d.txt}"
 exit 0
