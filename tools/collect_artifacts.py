@@ -1,4 +1,4 @@
-"""Copy a gpu_artifacts.sh run (gpurun_out/art) into profiles/: the bench line,
+"""Copy a gpu_final.sh run (gpurun_out/art) into profiles/: the bench line,
 the rocprofv3 kernel stats of the same command, and the per-launch HBM traffic
 of each kernel from the FETCH_SIZE / WRITE_SIZE passes (FETCH_SIZE doubled, as
 MI355X_MICROARCH.md's HBM section prescribes for gfx950; both are in KB)."""
