@@ -1011,6 +1011,7 @@ done:
 // Per record two copy descriptors: [header, txId varint, key] and [value].
 #define A_PRE 48                                   // header (<= 26) + txId varint (<= 10)
 #define A_CMAX 1024                                // descriptors starting in one 4-KiB block
+#define A_SMALL_MIN 24                             // smallest record for the A_CMAX / 2 instance of k_mcopy
 struct ARec {                                      // == cly_rec_in
     const uint8_t* key;
     const uint8_t* value;
@@ -1041,14 +1042,16 @@ __device__ __forceinline__ int a_prefix(const ARec& r, int64_t tx, uint8_t* h) {
 }
 __global__ void __launch_bounds__(256)
 k_asize(const ARec* __restrict__ recs, uint64_t n, uint64_t nt, int64_t tx, uint64_t* sz, unsigned long long* mx) {
-    unsigned long long m = 0;
+    unsigned long long m = 0, mn = ~0ull;           // largest and smallest encoded record: mx[0], mx[1]
     for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < nt; j += (uint64_t)gridDim.x * 256) {
         const ARec r = a_rec(recs, n, j);
         uint8_t h[A_PRE];
         sz[j] = (uint64_t)a_prefix(r, tx, h) + r.key_len + r.value_len;
         m = sz[j] > m ? sz[j] : m;
+        mn = sz[j] < mn ? sz[j] : mn;
     }
     if (m) atomicMax(mx, m);
+    if (mn != ~0ull) atomicMin(mx + 1, mn);
 }
 // appendLogRecord's rotation from (active file, WriteOff): region 0 is the
 // active file (it may take no record), later regions are fresh files that
@@ -1161,7 +1164,7 @@ extern "C" int cly_append_device(cly_ctx* ctx, const cly_rec_in* d_recs, uint64_
     uint32_t h_nout = 0;
     uint64_t total = 0, last = 0, fcap = 0, nblocks = 0;
     unsigned long long* d_mx = nullptr;
-    unsigned long long h_mx = 0;
+    unsigned long long h_mx = 0, h_mn = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const unsigned grid = (unsigned)((nt + 255) / 256 < 16384 ? (nt + 255) / 256 : 16384);
     MCK(hipEventCreate(&e0));
@@ -1169,8 +1172,9 @@ extern "C" int cly_append_device(cly_ctx* ctx, const cly_rec_in* d_recs, uint64_
     MCK(scratch(ctx, MS_A0 + 0, sizeof(uint64_t) * nt, &d_sz));
     MCK(scratch(ctx, MS_A0 + 1, sizeof(uint64_t) * nt, &d_g));
     MCK(scratch(ctx, MS_A0 + 2, sizeof(uint32_t), &d_nout));
-    MCK(scratch(ctx, MS_A0 + 3, sizeof(unsigned long long), &d_mx));
+    MCK(scratch(ctx, MS_A0 + 3, 2 * sizeof(unsigned long long), &d_mx));
     MCK(hipMemsetAsync(d_mx, 0, sizeof(unsigned long long), st));
+    MCK(hipMemsetAsync(d_mx + 1, 0xff, sizeof(unsigned long long), st));
     MCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, d_sz, d_g, (int)nt, st));
     MCK(scratch(ctx, MS_A0 + 4, tb + 16, (char**)&d_tmp));
     MCK(hipEventRecord(e0, st));
@@ -1179,6 +1183,7 @@ extern "C" int cly_append_device(cly_ctx* ctx, const cly_rec_in* d_recs, uint64_
     MCK(hipMemcpyAsync(&last, d_sz + nt - 1, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     MCK(hipMemcpyAsync(&total, d_g + nt - 1, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     MCK(hipMemcpyAsync(&h_mx, d_mx, sizeof(h_mx), hipMemcpyDeviceToHost, st));
+    MCK(hipMemcpyAsync(&h_mn, d_mx + 1, sizeof(h_mn), hipMemcpyDeviceToHost, st));
     MCK(hipStreamSynchronize(st));
     total += last;
     {
@@ -1213,8 +1218,14 @@ extern "C" int cly_append_device(cly_ctx* ctx, const cly_rec_in* d_recs, uint64_
         k_dscale<<<1, 64, 0, st>>>(d_fstart, h_nout + 1);
         const uint64_t wgs = (nblocks + MC_W - 1) / MC_W;
         const unsigned cg = wgs < 16384 ? (unsigned)wgs : 16384u;
-        k_mcopy<A_CMAX, A_PRE, false><<<cg, 64 * MC_W, 0, st>>>(d_cp, d_pre, d_bmap, d_fstart, d_flen, stride, nblocks, d_out,
-                                                        write_off);
+        // records of >= A_SMALL_MIN bytes start at most 2 (4096 / 24 + 1) + 2 descriptors in a block:
+        // the 512-entry instance (half the LDS: 4 waves/SIMD instead of 2)
+        if (h_mn >= A_SMALL_MIN)
+            k_mcopy<A_CMAX / 2, A_PRE, false><<<cg, 64 * MC_W, 0, st>>>(d_cp, d_pre, d_bmap, d_fstart, d_flen, stride,
+                                                                     nblocks, d_out, write_off);
+        else
+            k_mcopy<A_CMAX, A_PRE, false><<<cg, 64 * MC_W, 0, st>>>(d_cp, d_pre, d_bmap, d_fstart, d_flen, stride,
+                                                                 nblocks, d_out, write_off);
     }
     MCK(hipGetLastError());
     MCK(hipEventRecord(e1, st));
