@@ -153,6 +153,18 @@ __device__ __forceinline__ uint32_t crc_span(const uint32_t* t4, uint32_t s, con
     while (len && ((uintptr_t)p & 3)) { s = crc_upd(t4, s, *p++); len--; }
     const uint32_t* w = (const uint32_t*)p;
     uint64_t nw = len >> 2;
+    while (nw >= 16) {                          // 16 independent loads in flight, then the steps
+        uint32_t v[16];
+        #pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = w[k];
+        #pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const uint32_t x = s ^ v[k];
+            s = t4[768 + (x & 0xff)] ^ t4[512 + ((x >> 8) & 0xff)] ^ t4[256 + ((x >> 16) & 0xff)] ^ t4[x >> 24];
+        }
+        w += 16;
+        nw -= 16;
+    }
     while (nw >= 4) {
         const uint32_t a = w[0], b = w[1], c = w[2], d = w[3];
         #pragma unroll
