@@ -547,9 +547,9 @@ static int map_get(const std::unordered_map<std::string, std::unordered_map<std:
 extern "C" int cly_db_lget(cly_db* db, const uint8_t* key, uint64_t klen, const uint8_t* seq, uint64_t slen,
                            cly_pos* pos) {
     if (!db || slen > 0xFFFFFFFFull) return CLY_ERR_ARG;
-    uint8_t c[IXK_PMAX];
-    const uint32_t n = ixk_gob_canon(seq, (uint32_t)slen, c);      // the index keys seq.GobEncode()
-    return map_get(db->list, key, klen, std::string((const char*)c, n), pos);
+    // the bytes as getListDataIndex(key).Get(seqBuf) takes them (seqBuf =
+    // seq.GobEncode() of the caller's Float, txnList.go:250-262): not re-decoded
+    return map_get(db->list, key, klen, std::string((const char*)seq, (size_t)slen), pos);
 }
 
 extern "C" int cly_db_sget(cly_db* db, const uint8_t* key, uint64_t klen, const uint8_t* member, uint64_t mlen,

@@ -43,7 +43,7 @@ int  cly_db_listmeta(cly_db* db, const uint8_t* key, uint64_t klen, cly_pos* pos
 int  cly_db_hget(cly_db* db, const uint8_t* key, uint64_t klen, const uint8_t* field, uint64_t flen,
                  cly_pos* pos);                                                         /* Hash     */
 int  cly_db_lget(cly_db* db, const uint8_t* key, uint64_t klen, const uint8_t* seq, uint64_t slen,
-                 cly_pos* pos);      /* List: getListDataIndex(key).Get(seq gob encoding)   */
+                 cly_pos* pos);      /* List: getListDataIndex(key).Get(seqBuf), seqBuf = seq.GobEncode() bytes as given */
 int  cly_db_sget(cly_db* db, const uint8_t* key, uint64_t klen, const uint8_t* member, uint64_t mlen,
                  cly_pos* pos);      /* Set: getSetIndex(key).Get(hashMemberKey(key, member)) */
 /* The index key updateIndex derives (db.go:511-575) for a record of data type

@@ -335,7 +335,7 @@ def typed_corpus(seed, n_ops=400, n_keys=12, tx_frac=0.6, nontx_frac=0.15, garba
 INDEX_NOW = 1_800_000_000_000_000_000      # the clock the index tests give loadIndex (UnixNano, 2027)
 
 
-def index_states(file_bytes, tuples_per_file, now_ns=INDEX_NOW, merge_panics=None):
+def index_states(file_bytes, tuples_per_file, now_ns=INDEX_NOW, merge_panics=None, out_index=None):
     """db.loadIndex (db.go:582-651) restated literally: a map of buffered tx
     records per txId, updateIndex for the five indexes (String/ListMeta by
     realKey, Hash/List/Set by the composite keys of tests/index_keys.py decoded
@@ -395,6 +395,9 @@ def index_states(file_bytes, tuples_per_file, now_ns=INDEX_NOW, merge_panics=Non
         for rk, exp in expirations.items():
             if exp != 0 and not exp > now_ns:
                 index.pop((mg.STRING, rk), None)
+    if out_index is not None:
+        out_index.update({ik: (recs[i][0], int(recs[i][2]["fid"]), int(recs[i][2]["offset"]), recs[i][3])
+                          for ik, i in index.items()})
     for ik, i in index.items():
         _, rk, t, _ = recs[i]
         try:

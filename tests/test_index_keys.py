@@ -11,6 +11,7 @@ GPU (-m gpu): cly_index / cly_index_device against index_states on typed
 corpora (all five data types, tx commit/rollback, records without a txId whose
 load and merge keys differ, forced hash collisions), the load/merge panics,
 and the merge of such files against the restatement."""
+import collections
 import random
 import struct
 import zlib
@@ -262,3 +263,40 @@ def test_gpu_merge_typed_from_device_states(scanner, seed):
     assert rc == 0
     m = scanner.merge([DataFile(a.copy(), i) for i, a in enumerate(arrays)], got, 4096)
     assert m.n_live == r.n_live and [bytes(x) for x in m.files] == [bytes(x) for x in outs] and m.hint == hint
+
+
+@pytest.mark.gpu
+def test_gpu_load_driver_composite_lookups(scanner, tmp_path):
+    """cly_db_open over typed corpus files: every entry of the restated
+    indexes (String, ListMeta, Hash (key, field), List (key, seq gob bytes),
+    Set (key, member)) is found at its record's position through the loader's
+    lookups, and the entry counts match."""
+    from .index_keys import decode_byte_slices
+    from .test_reference_restart import write_dir
+    files = split_files(typed_corpus(500, n_ops=1500, n_keys=20), 3, random.Random(5))
+    write_dir(tmp_path, files)
+    arrays, tts, _ = oracle_scan(files)
+    ix = {}
+    index_states(arrays, tts, out_index=ix)
+    counts = collections.Counter(k[0] for k in ix)
+    with scanner.open_db(str(tmp_path)) as db:
+        st = db.stats
+        assert (st.str_keys, st.listmeta_keys, st.hash_fields, st.list_items, st.set_members) == \
+            (counts[mg.STRING], counts[mg.LISTMETA], counts[mg.HASH], counts[mg.LIST], counts[mg.SET])
+        for ik, (key, fid, off, tx) in ix.items():
+            dt = ik[0]
+            if dt == mg.STRING:
+                p = db.pos(ik[1])
+            elif dt == mg.LISTMETA:
+                p = db.listmeta_pos(ik[1])
+            elif dt == mg.HASH:
+                p = db.hpos(ik[1], ik[2])
+            elif dt == mg.LIST:
+                p = db.lpos(ik[1], ik[2])
+            else:
+                _, n = mg.varint(key)
+                k, m = decode_byte_slices(key if tx == 0 else key[n:])      # the load key's member
+                p = db.spos(k, m)
+            assert (p.fid, p.offset) == (fid, off), (ik, fid, off)
+        with pytest.raises(KeyError):
+            db.hpos(b"no such key", b"f0")
