@@ -2,7 +2,7 @@
 """Benchmark: device-resident CouloyDB log-record scan (decode + CRC -> index tuples).
 
 Contract (see task spec): `python bench.py --gpus N --steps K --warmup W` prints ONE
-JSON line on rank 0.  A step = one full scan (k_spec, k_link, k_crc,
+JSON line on rank 0.  A step = one full scan (k_scan, k_link, k_emit,
 k_fin and the result read-back) of the configuration's data files, already resident in HBM.  For N>1
 each rank (one per GPU, launched by torch.distributed.run) scans its own fid
 range of the same per-GPU size (weak scaling, no collective on the data path;
@@ -144,7 +144,7 @@ def make_workload(name, torch, rank=0, device=0, seed=0x434C59, size=32 * 2**30)
 
 
 def measured_traffic(config):
-    """k_crc HBM bytes per launch (read + write) from the newest committed
+    """k_scan HBM bytes per launch (read + write) from the newest committed
     profiles/*_traffic.json whose build and config match this library."""
     import glob
     from couloydb_amd import build_info
@@ -154,7 +154,7 @@ def measured_traffic(config):
             t = json.load(open(f))
         except ValueError:
             continue
-        k = t.get("kernels", {}).get("k_crc")
+        k = t.get("kernels", {}).get("k_scan")
         if t.get("build") == build_info() and t.get("config") == config and k:
             best = k.get("fetch_bytes", 0) + k.get("write_bytes", 0)
     return best
@@ -430,7 +430,7 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt, scan_ms / args.steps, kms["k_crc"] / args.steps], dtype=torch.float64,
+    t = torch.tensor([dt, scan_ms / args.steps, kms["k_scan"] / args.steps], dtype=torch.float64,
                      device="cpu" if rehearse else "cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -439,7 +439,7 @@ def main():
     total_bytes = wl.bytes * world
     total_recs = recs * world
     value = total_bytes / (ms / 1e3) / 2**30
-    achieved = wl.bytes / (crc_ms / 1e3) / 1e9           # the dominant kernel, k_crc
+    achieved = wl.bytes / (crc_ms / 1e3) / 1e9           # the dominant kernel, k_scan
     step_gbs = wl.bytes / (ms / 1e3) / 1e9
     ok = all(r.status == 0 for r in res) and recs == wl.expect_records
     out = {
@@ -453,13 +453,13 @@ def main():
         "mrecords_per_s": round(total_recs / (ms / 1e3) / 1e6, 2),
         "kernel": {**{k + "_ms": round(v / args.steps, 4) for k, v in kms.items()},
                    "device_ms": round(scan_dev_ms, 4), "passes": passes, "build": build_info()},
-        "roofline": {"bound": "hbm", "kernel": "k_crc", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": "k_scan", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": measured_traffic(args.config),
                      "step_achieved": round(step_gbs, 1), "step_frac": round(step_gbs / HBM_PEAK_GBS, 4),
-                     "note": "achieved = input bytes per k_crc launch (it reads every byte of every file once) / "
+                     "note": "achieved = input bytes per k_scan launch (it reads every byte of every file once) / "
                              "its HIP-event duration; step_* = the same bytes / the whole step's wall time; "
-                             "traffic = k_crc HBM read+write bytes per launch from the committed rocprofv3 "
+                             "traffic = k_scan HBM read+write bytes per launch from the committed rocprofv3 "
                              "FETCH_SIZE/WRITE_SIZE passes of this build (profiles/*_traffic.json), null if none"},
         "parity_ok": ok,
     }

@@ -326,11 +326,11 @@ class Scanner:
         directory `path`, on this scanner's device (cly_db_open)."""
         return LoadedDB(self, path)
 
-    KERNELS = ("k_spec", "link", "k_crc", "k_fin", "k_locate", "all")
+    KERNELS = ("k_scan", "link", "k_emit", "k_fin", "k_locate", "all")
 
     def kernel_ms(self):
-        """Per-kernel HIP-event times (ms) of the last scan_device call: k_spec,
-        the link rounds (k_link + k_fbase + repairs), k_crc, k_fin,
+        """Per-kernel HIP-event times (ms) of the last scan_device call: k_scan,
+        the link rounds (k_link + k_fbase + repairs), k_emit, k_fin,
         k_locate, all."""
         k = (ctypes.c_double * 6)()
         self.lib.cly_dbg_kernel_ms(self.ctx, k)

@@ -9,30 +9,33 @@
 // (data/logRecord.go:86-114), GetLogRecordCRC (data/logRecord.go:136-146) and
 // parseLogRecordKey (db.go:706-710).
 //
-// Layout: every file is cut into chunks of CLY_CH bytes, one
-// per lane; 64 consecutive chunks of a file are a tile, one per wave.
+// Layout: a file is cut into tiles of CLY_NBLK blocks of
+// 4 KiB; one wave streams a tile block by block; in a block, lane L owns the
+// 64-B segment at 64 L.
 //
 // One call, all on one stream, no inter-workgroup waiting inside a kernel:
-//   k_spec   per tile: each lane finds the first record start of its chunk
-//            (SWAR candidate filter, then a walk of header gathers that must
-//            leave the chunk at a plausible header) and walks its records to
-//            the chunk end; the wave makes the lanes' chains agree under the
-//            tile's own guess of its entry; lane chains + the tile's LOCAL out;
-//   k_link   per file: the chain state entering every tile (record count,
-//            position, the record open at the tile start) from the LOCALs;
+//   k_scan   per tile, ONE read of its bytes: each block arrives by four
+//            coalesced 1-KiB loads (transposed over the lane quarters); the
+//            lanes find the record starts of their segments (SWAR candidate
+//            filter, header gathers that hit L2 because the wave has just
+//            loaded those lines, an in-wave agreement pass), XOR each record's
+//            CRC patch into their words in registers and run the words through
+//            a slicing-by-4 CRC register; a 16-B compact entry per record and
+//            the tile's chain summary (LOCAL) and CRC register go out.  The
+//            first tile of a file starts at offset 0; any other tile guesses
+//            its entry (its first plausible record start);
+//   k_link   per file: the chain state entering every tile from the LOCALs;
 //            tiles whose guess the state contradicts are listed;
-//   k_refix  (only for listed tiles) re-resolves them from the true entry,
+//   k_refix  (only for listed tiles) re-runs the tile body from the true entry,
 //            then k_link again;
 //   k_fbase  tuple index of each file's first record;
-//   k_crc    per tile: every lane streams its chunk through a slicing-by-4 CRC
-//            register (16-B loads, 128 B per burst) while a walker decodes its
-//            records one gather ahead, writes their tuples straight to their
-//            output slots and adds one shifted patch per record to the lane's
-//            register, so that the register of the whole file ends at zero iff
-//            every record's CRC matches; the tile's register is folded in-wave;
-//   k_fin    per file: folds the tile registers up to the terminal's and checks
-//            that the fold is zero;
-//   k_locate (only when a file fails) finds the first bad record exactly.
+//   k_emit   per tile: the 48-B tuples from the compact entries (tiles with
+//            more records than the compact list holds re-run the body and
+//            write tuples directly); the tile register gets the one patch
+//            term that needed the state entering it;
+//   k_fin    per file: folds the tile registers up to the terminal's tile and
+//            checks that the fold is zero (every record's CRC matches);
+//   k_locate (only when a file fails) checks the records' CRCs one by one.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -54,17 +57,12 @@ typedef unsigned long long u64;
 typedef const CLY_GL uint8_t* gbytes;
 typedef CLY_GL cly_tuple* gtuples;
 #define NONE32 0xFFFFFFFFu       // no position
-#define TERM_NONE 127            // the chain leaves the chunk (no terminal inside)
-#define LM_NONE 0                // no record starts in the chunk (the chain passes through it)
-#define LM_CHAIN 1               // the chain enters the chunk at E (a record start or its terminal)
-#define LM_DEAD 2                // the file's chain ended before the chunk
-#define LM_OFF 3                 // chunk beyond the end of the file
-#define NO_EV 0xFFFFu            // empty event slot
-#ifdef CLY_DEBUG
-#define DBG(...) do { if ((threadIdx.x & 63) == 0) printf(__VA_ARGS__); } while (0)
-#else
-#define DBG(...)
-#endif
+#define TERM_NONE 127            // the chain leaves the segment (no terminal inside)
+#define LM_NONE 0                // no record starts in the segment (the chain passes through it)
+#define LM_CHAIN 1               // the chain enters the segment at E (a record start or its terminal)
+#define LM_DEAD 2                // the file's chain ended before the segment
+#define LM_OFF 3                 // segment beyond the end of the file
+#define CAP_T ((uint32_t)(CLY_TILE / 128))   // compact entries kept per tile (more: k_emit re-walks)
 
 struct DevFile {                 // 32 B
     const uint8_t* base;         // device pointer to the file's first byte (16-B aligned)
@@ -75,36 +73,32 @@ struct DevFile {                 // 32 B
     uint32_t _pad;
 };
 
-struct FileInfo {                // per file, zeroed per call (fail_key: all ones)
+struct FileInfo {                // per file, zeroed per call (fail_key: all ones after k_fin)
     uint64_t first_index;        // global tuple index of the file's first record
     uint64_t end_index;          // global index after the file's last record
     uint32_t term_pos;           // terminal position T of the file's chain
     int32_t  term_status;
     uint32_t term_tile;          // global tile index holding T
-    uint32_t term_lane;
-    uint32_t expect;             // value the folded register must have (see k_fin)
     uint32_t has_term;
     u64      fail_key;           // (offset << 32) | index in file of the first CRC failure (k_locate)
     uint32_t fold;               // k_fin: the folded register
-    uint32_t ok;                 // k_fin: fold == expect
+    uint32_t ok;                 // k_fin: fold == 0
 };
 
-// Tile LOCAL (from the tile's own speculation), written by k_spec / k_refix:
-// l[0]: bit1 the chain ends in the tile | bit2 no chunk of the tile holds a
-//       boundary | bit3 first tile of its file | bit4 a record starts in the
-//       tile | records << 32
-// l[1]: G (the tile's guessed entry: its first boundary) | exit or terminal position << 32
+// Tile LOCAL (the tile's chain under its own entry), written by k_scan / k_refix:
+// l[0]: bit1 the chain ends in the tile | bit2 no boundary in the tile | bit3
+//       first tile of its file | bit4 a record starts in the tile | bit5 more
+//       records than the compact list holds | records << 32
+// l[1]: G (the tile's first boundary) | exit or terminal position << 32
 // l[2]: crc_last | P_last << 32 (last record start in the tile and its stored CRC)
 // l[3]: the smallest entry that passes the whole tile (tile end, or len + 1 for
-//       the tile holding the file's end)
+//       the tile holding the file's end) | terminal status (s8) << 32
 struct TileLocal { u64 l[4]; };
-#define DF_PUB 1ull
 #define DF_TERM 2ull
 #define DF_NONE 4ull
 #define DF_FOF 8ull
 #define DF_REC 16ull
-#define DF_OVF 32ull             // the tile's record starts are not stored (more than POS_CAP)
-#define POS_CAP 2048             // stored record starts per tile (u16, tile-relative)
+#define DF_OVF 32ull
 
 #define LINK_ROUNDS 3            // link rounds launched per call without a host wait (more: host loop)
 struct Globals {                 // zeroed per call
@@ -116,23 +110,28 @@ struct Globals {                 // zeroed per call
     uint32_t any_fail;           // a file's CRC fold failed (k_locate needed)
     uint64_t total;              // records over all files
 };
-// ---------------------------------------------------------------------------
-// LDS of k_crc / k_locate (static: compile-time offsets)
-//   [0, 65536)     CRC slicing-by-4 tables T0..T3, 16 replicas: dword (i*64 + t*16 + r)
-//   [65536, +256)  inverse of a zero-byte step (top byte of T0 -> index)
-//   LDS_NIB        nibble tables of A^(CLY_CH * 2^k), k < 7 (8 x 16 words each)
-//   LDS_SH         nibble tables of A^(v 16^d) (v < 16, d < 4: a byte shift by one hex
-//                  digit each), then A^65536 and A^(COAL_BLK - 64)
-#define LDS_INV 65536
-#define COAL_BLK 4096                    // k_crc's coalesced block (64 lanes x 64 B)
-#define LDS_NIB (LDS_INV + 256)
-#define NIB_LEVELS 7                     // A^(CLY_CH * 2^k), k < 7 (k = 6: one tile)
-#define NSH 66                           // shift tables (the last: A^(COAL_BLK - 64))
-#define LDS_SH (LDS_NIB + NIB_LEVELS * 128 * 4)
-#define NTAB ((NIB_LEVELS + NSH) * 128)  // words of nibble tables (copied from the context's buffer)
-#define SCAN_LDS (LDS_SH + NSH * 128 * 4)
 
-__device__ __forceinline__ void init_tables(CLY_LDS uint8_t* smem, const uint32_t* __restrict__ nib, int ntab = NTAB) {
+// ---------------------------------------------------------------------------
+// Nibble tables (the context's d_tabs, built on the host): 128 words each,
+// entry n*16 + v = M (v << 4n) for a matrix M = A^bytes.
+//   TAB_SCAN: A^(64 2^k), k < 6 (the lane fold), A^(CLY_BLK - 64) (the block step)
+//   TAB_SH:   A^(v 16^d), v < 16, d < 4 (one hex digit of a byte shift), A^65536
+//   TAB_TILE: A^CLY_TILE (k_fin)
+#define NIB_SCAN 7
+#define NIB_SH 65
+#define TAB_SCAN 0
+#define TAB_SH (NIB_SCAN * 128)
+#define TAB_TILE (TAB_SH + NIB_SH * 128)
+#define NTAB_ALL (TAB_TILE + 128)
+// LDS of k_scan / k_refix / k_locate (static: compile-time offsets)
+//   [0, 65536)  CRC slicing-by-4 tables T0..T3, 16 replicas: dword (i*64 + t*16 + r)
+//   LDS_INV     inverse of a zero-byte step (top byte of T0 -> index), 256 B
+//   LDS_NIB     the TAB_SCAN tables
+#define LDS_INV 65536
+#define LDS_NIB (LDS_INV + 256)
+#define SCAN_LDS (LDS_NIB + NIB_SCAN * 128 * 4)
+
+__device__ __forceinline__ void init_tables(CLY_LDS uint8_t* smem, const uint32_t* __restrict__ nib, int ntab) {
     for (int i = threadIdx.x; i < 256; i += blockDim.x) {
         uint32_t cv = i;
         for (int k = 0; k < 8; k++) cv = (cv & 1) ? (cv >> 1) ^ CLY_POLY : cv >> 1;
@@ -170,47 +169,38 @@ __device__ __forceinline__ uint32_t crc_word(const CLY_LDS uint8_t* smem, uint32
     return *(const CLY_LDS uint32_t*)(smem + a0) ^ *(const CLY_LDS uint32_t*)(smem + a1) ^
            *(const CLY_LDS uint32_t*)(smem + a2 + 128) ^ *(const CLY_LDS uint32_t*)(smem + a3 + 128);
 }
+// one byte through the register: T0[(s ^ b) & 0xff] ^ (s >> 8)
+__device__ __forceinline__ uint32_t crc_byte(const CLY_LDS uint8_t* smem, uint32_t s, uint32_t b, uint32_t r4) {
+    const uint32_t i = (s ^ b) & 0xffu;
+    return *(const CLY_LDS uint32_t*)(smem + ((i << 8) | r4)) ^ (s >> 8);
+}
 // inverse of one zero-byte step: s = A^-1 s'
 __device__ __forceinline__ uint32_t crc_unbyte(const CLY_LDS uint8_t* smem, uint32_t s, uint32_t r4) {
     const uint32_t i = smem[LDS_INV + (s >> 24)];
     const uint32_t t = *(const CLY_LDS uint32_t*)(smem + ((i << 8) | r4));
     return ((s ^ t) << 8) | i;
 }
-// A^(CLY_CH * 2^lvl) v by nibble tables (entry n*16+k = M (k << 4n))
-__device__ __forceinline__ uint32_t nib_mul(const CLY_LDS uint8_t* smem, int lvl, uint32_t v) {
-    const CLY_LDS uint32_t* t = (const CLY_LDS uint32_t*)(smem + LDS_NIB) + lvl * 128;
+// A^-j d (j < 4 zero bytes backwards)
+__device__ __forceinline__ uint32_t crc_unbytes(const CLY_LDS uint8_t* smem, uint32_t d, uint32_t j, uint32_t r4) {
+    for (uint32_t k = 0; k < j; k++) d = crc_unbyte(smem, d, r4);
+    return d;
+}
+// M v by a nibble table of M
+__device__ __forceinline__ uint32_t mat_mul(const CLY_LDS uint32_t* t, uint32_t v) {
     uint32_t p = 0;
     #pragma unroll
     for (int n = 0; n < 8; n++) p ^= t[n * 16 + ((v >> (4 * n)) & 15u)];
     return p;
 }
-
-// ---------------------------------------------------------------------------
-// Boundary patch.  A record starting at P (stored CRC c, the record before it
-// stored cq) changes the file's byte stream, as seen by the CRC register, by
-//   pa on word a = P>>2: the stored-CRC bytes [P, 4a+4) zeroed, and Q = A^-j ~cq
-//                  (j = P&3) XORed in, so that the register after word a is zero
-//                  iff the record ending at P has a good CRC (none at P = 0);
-//   pb on word a+1: the rest of the stored CRC zeroed, 0xFF (the init) on the
-//                  record's first region bytes [P+4, 4a+8);
-//   pc on word a+2: 0xFF on [4a+8, P+8).
-// XORing d into a word equals XORing A^4 d into the register after it, so the
-// three are one XOR delta' = A^8 pa ^ A^4 pb ^ pc on word a+2.  The register
-// of the whole patched file (everything from the chain's terminal T on zeroed,
-// Q of T's predecessor at T) is zero iff every record's CRC matches.
-__device__ __forceinline__ uint32_t q_of(const CLY_LDS uint8_t* smem, uint32_t cq, uint32_t j, uint32_t r4) {
-    uint32_t q = ~cq;
-    for (uint32_t k = 0; k < j; k++) q = crc_unbyte(smem, q, r4);
-    return q;
-}
-__device__ __forceinline__ uint32_t patch_delta(const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t P, uint32_t c,
-                                                uint32_t cq) {
-    const uint32_t j = P & 3, sh = 8 * j;
-    uint32_t pa = j ? (c << sh) : c;
-    if (P != 0) pa ^= q_of(smem, cq, j, cl.r4);
-    const uint32_t pb = (j ? (c >> (32 - sh)) : 0u) ^ (j ? (0xFFFFFFFFu << sh) : 0xFFFFFFFFu);
-    const uint32_t pc = j ? ((1u << sh) - 1u) : 0u;
-    return crc_word(smem, crc_word(smem, pa, cl) ^ pb, cl) ^ pc;
+// A^m v (m bytes), 1 <= m <= 65536: one nibble-table product per hex digit of m
+// (sh: the TAB_SH tables)
+__device__ __forceinline__ uint32_t shift_bytes(const CLY_LDS uint32_t* sh, uint32_t m, uint32_t v) {
+    v = mat_mul(sh + (m & 15u) * 128, v);
+    v = mat_mul(sh + (16u + ((m >> 4) & 15u)) * 128, v);
+    v = mat_mul(sh + (32u + ((m >> 8) & 15u)) * 128, v);
+    v = mat_mul(sh + (48u + ((m >> 12) & 15u)) * 128, v);
+    if (m >> 16) v = mat_mul(sh + 64u * 128, v);
+    return v;
 }
 
 // ---------------------------------------------------------------------------
@@ -220,12 +210,6 @@ __device__ __forceinline__ uint32_t patch_delta(const CLY_LDS uint8_t* smem, con
 // expirations); otherwise the exact byte-loop form over global memory.
 struct Gath { uint32_t w[8]; };
 __device__ __forceinline__ bool gath_ok(uint32_t p, uint64_t len) { return (uint64_t)(p & ~3u) + 32 <= len; }
-__device__ __forceinline__ void gath_issue_at(gbytes a, Gath& g) {     // a: 4-aligned, 32 readable bytes
-    const CLY_GL u32x4u* q = (const CLY_GL u32x4u*)a;
-    const u32x4u x = q[0], y = q[1];
-    g.w[0] = x.x; g.w[1] = x.y; g.w[2] = x.z; g.w[3] = x.w;
-    g.w[4] = y.x; g.w[5] = y.y; g.w[6] = y.z; g.w[7] = y.w;
-}
 __device__ __forceinline__ void gath_issue(gbytes base, uint32_t p, Gath& g) {
     const CLY_GL u32x4u* q = (const CLY_GL u32x4u*)(base + (p & ~3u));
     const u32x4u a = q[0], b = q[1];
@@ -237,9 +221,6 @@ __device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t s)
 }
 __device__ __forceinline__ uint32_t pack7(uint32_t s) {
     return (s & 0x7fu) | ((s >> 1) & 0x3f80u) | ((s >> 2) & 0x1fc000u) | ((s >> 3) & 0xfe00000u);
-}
-__device__ __noinline__ Hdr hdr_slow(gbytes base, uint32_t p, uint64_t len) {
-    return step_hdr(base, (int64_t)p, (int64_t)len, (int64_t)p);
 }
 // header bytes 0..15 at p from a gather
 __device__ __forceinline__ bool hdr_fast(const Gath& g, uint32_t p, uint64_t len, Hdr& h) {
@@ -282,110 +263,253 @@ __device__ __forceinline__ bool hdr_fast(const Gath& g, uint32_t p, uint64_t len
     h.good = h.type <= 4 && h.dt <= 4 && v1 >= 1 && v2 >= 0;
     return true;
 }
-// Header at p; `g` must hold the gather of p when gath_ok(p).
-__device__ __forceinline__ Hdr hdr_at(gbytes base, uint32_t p, uint64_t len, const Gath& g) {
+// The header at p: the 32-B gather from the wave's LDS copy of the block (and
+// the 64 bytes after it) when p lies there, else from global memory (L2);
+// the byte-loop form near the file's end.
+#define STG_BYTES (CLY_BLK + 64)                 // per-wave block stage: the block + 64 B after it
+__device__ __forceinline__ Hdr hdr_get(gbytes base, uint32_t p, uint64_t len, const CLY_LDS uint32_t* stg, uint32_t bs) {
     Hdr h;
-    if (gath_ok(p, len) && hdr_fast(g, p, len, h)) return h;
-    return hdr_slow(base, p, len);
+    if (gath_ok(p, len)) {
+        Gath g;
+        const uint32_t rel = (p & ~3u) - bs;
+        if (p >= bs && rel + 32 <= STG_BYTES) {
+            const CLY_LDS uint32_t* q = stg + (rel >> 2);
+            #pragma unroll
+            for (int k = 0; k < 8; k++) g.w[k] = q[k];
+        } else gath_issue(base, p, g);
+        if (hdr_fast(g, p, len, h)) return h;
+    }
+    return step_hdr(base, (int64_t)p, (int64_t)len, (int64_t)p);
 }
 __device__ __forceinline__ Hdr hdr_load(gbytes base, uint32_t p, uint64_t len) {
-    Gath g;
-    if (gath_ok(p, len)) gath_issue(base, p, g);
-    return hdr_at(base, p, len, g);
+    Hdr h;
+    if (gath_ok(p, len)) {
+        Gath g;
+        gath_issue(base, p, g);
+        if (hdr_fast(g, p, len, h)) return h;
+    }
+    return step_hdr(base, (int64_t)p, (int64_t)len, (int64_t)p);
 }
 
 // ---------------------------------------------------------------------------
-// Per-lane chain of one chunk [cb, ce) (file offsets; the file's last chunk
-// also owns position len, where ReadLogRecord returns io.EOF).
-struct Chunk {
+// A lane's segment [cb, ce) of one block (file offsets; the segment holding
+// the file's last byte also owns position len, where ReadLogRecord returns
+// io.EOF; so does the empty file's first segment).
+struct Seg {
     gbytes base;
     uint64_t len;
+    const CLY_LDS uint32_t* stg; // the wave's copy of the block
+    uint32_t bs;                 // the block's first byte
     uint32_t cb, ce;
-    uint32_t tb;                 // file offset of the tile's first byte
-    bool last;                   // the file's last chunk
-    bool on;                     // the chunk exists (cb < len, or the empty file's chunk 0)
+    bool last;                   // owns position len
+    bool on;                     // the segment exists (cb < len, or the empty file's segment 0)
 };
-__device__ __forceinline__ bool in_chunk(const Chunk& K, uint32_t x) {
+__device__ __forceinline__ Seg make_seg(const DevFile& F, uint32_t bs, int lane, const CLY_LDS uint32_t* stg) {
+    Seg K;
+    K.base = (gbytes)F.base; K.len = F.len;
+    K.stg = stg; K.bs = bs;
+    const uint64_t cb = (uint64_t)bs + (uint64_t)lane * CLY_SEG;
+    K.on = cb < F.len || cb == 0;
+    K.last = K.on && cb + CLY_SEG >= F.len;
+    K.cb = (uint32_t)cb;
+    K.ce = (uint32_t)(cb + CLY_SEG < F.len ? cb + CLY_SEG : F.len);
+    if (!K.on) { K.cb = 0xFFFFFFF0u; K.ce = 0xFFFFFFF0u; }
+    return K;
+}
+__device__ __forceinline__ bool in_seg(const Seg& K, uint32_t x) {
     return (x >= K.cb && x < K.ce) || (K.last && (uint64_t)x == K.len);
 }
-struct LaneChain {
+struct SegChain {
     int      mode;               // LM_*
     uint32_t E;                  // first boundary (record start or terminal)
-    uint32_t x;                  // exit (>= ce) or terminal position
-    int      term;               // terminal status, TERM_NONE if the chain leaves the chunk
-    uint32_t cnt;                // records starting in the chunk
+    uint32_t x;                  // exit (beyond the segment) or terminal position
+    int      term;               // terminal status, TERM_NONE if the chain leaves the segment
+    uint32_t cnt;                // records starting in the segment
     uint32_t last, last_crc;     // last record start and its stored CRC
-    uint32_t prev_crc;           // stored CRC of the record before `last` (cnt >= 2)
-    uint32_t minsz;              // smallest record size
-    uint32_t pk[4];              // the first PK_N record starts, tile-relative u16 pairs (k_spec)
 };
-#define PK_N 8
-__device__ __forceinline__ void chain_set(LaneChain& L, int mode) {
+__device__ __forceinline__ void sc_set(SegChain& L, int mode) {
     L.mode = mode; L.E = NONE32; L.x = 0; L.term = TERM_NONE; L.cnt = 0; L.last = NONE32; L.last_crc = 0;
-    L.prev_crc = 0; L.minsz = 0xFFFFFFFFu;
-    L.pk[0] = L.pk[1] = L.pk[2] = L.pk[3] = 0;
 }
-// record start `rel` (tile-relative) as the chain's record number cnt (constant indices only)
-__device__ __forceinline__ void pk_put(LaneChain& L, uint32_t cnt, uint32_t rel) {
-    const uint32_t v = (rel & 0xFFFFu) << (16 * (cnt & 1));
-    const uint32_t q = cnt >> 1;                 // value selects, not indexed stores
-    L.pk[0] = L.pk[0] | (q == 0 ? v : 0u);
-    L.pk[1] = L.pk[1] | (q == 1 ? v : 0u);
-    L.pk[2] = L.pk[2] | (q == 2 ? v : 0u);
-    L.pk[3] = L.pk[3] | (q == 3 ? v : 0u);
-}
-
 // Walk from p: exact (ReadLogRecord semantics, every terminal) or speculative
-// (every record must be one the writer produces and the chain must leave the
-// chunk at a plausible header, or end at io.EOF at len).  Returns false when a
-// speculative chain is rejected.
-__device__ __forceinline__ bool walk_(const Chunk& K, uint32_t p, bool exact, LaneChain& L) {
-    chain_set(L, LM_CHAIN);
+// (every record one the writer produces; a terminal only at io.EOF at len).
+// Returns false when a speculative chain is rejected.
+__device__ __forceinline__ bool seg_walk(const Seg& K, uint32_t p, bool exact, SegChain& L) {
+    sc_set(L, LM_CHAIN);
     L.E = p;
-    for (;;) {
-        if (!in_chunk(K, p)) {
-            L.x = p;
-            if (exact || (uint64_t)p == K.len) return true;
-            if ((uint64_t)p > K.len) return false;
-            const Hdr e = hdr_load(K.base, p, K.len);
-            return (e.status == REC_OK && e.good) || e.status == CLY_END_ZERO;
-        }
-        const Hdr h = hdr_load(K.base, p, K.len);
+    for (int it = 0; it < 16; it++) {            // records are >= 6 bytes: <= 12 steps per segment
+        if (!in_seg(K, p)) { L.x = p; return true; }
+        const Hdr h = hdr_get(K.base, p, K.len, K.stg, K.bs);
         if (h.status != REC_OK) {
             L.x = p; L.term = h.status;
             return exact || (h.status == CLY_END_EOF && (uint64_t)p == K.len);
         }
         if (!exact && !h.good) return false;
-        pk_put(L, L.cnt, p - K.tb);
         L.cnt++;
-        L.prev_crc = L.last_crc;
         L.last = p; L.last_crc = h.crc;
-        if ((uint32_t)h.size < L.minsz) L.minsz = (uint32_t)h.size;
         p += (uint32_t)h.size;
+    }
+    L.x = p;
+    return exact;
+}
+
+// SWAR byte mask (bit 7 of each byte): byte <= 4 (type / data type).
+__device__ __forceinline__ uint32_t swar_le4(uint32_t W) { return ~(((W | 0x80808080u) - 0x05050505u) | W) & 0x80808080u; }
+// Candidate record starts of a segment (bit i: position cb + i has type and data
+// type <= 4): its 16 words and the next 8 bytes (n0, n1).  The four candidate
+// bits of a word are gathered by one multiply: bits 7, 15, 23, 31 times
+// 1 + 2^7 + 2^14 + 2^21 land in bits 28..31.
+__device__ __forceinline__ u64 cand_mask(const uint32_t (&w)[16], uint32_t n0, uint32_t n1) {
+    uint32_t lo = 0, hi = 0;
+    uint32_t L1 = swar_le4(w[1]);
+    #pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint32_t y2 = k + 2 < 16 ? w[k + 2 < 16 ? k + 2 : 0] : (k + 2 == 16 ? n0 : n1);
+        const uint32_t L2 = swar_le4(y2);
+        const uint32_t cm = L1 & __builtin_amdgcn_alignbit(L2, L1, 8);
+        const uint32_t b4 = (cm * 0x204081u) >> 28;
+        if (k < 8) lo |= b4 << (4 * k); else hi |= b4 << (4 * (k - 8));
+        L1 = L2;
+    }
+    return ((u64)hi << 32) | lo;
+}
+
+// ---------------------------------------------------------------------------
+// wave helpers: DPP row shifts / row broadcasts (gfx9 encodings), readlane for
+// wave-uniform sources; no LDS round trips.
+#define DPP_ROW_SHR(n) (0x110 + (n))
+#define DPP_WF_SL1 0x130                 // lane i <- lane i+1
+#define DPP_WF_SR1 0x138                 // lane i <- lane i-1
+#define DPP_ROW_BCAST15 0x142
+#define DPP_ROW_BCAST31 0x143
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ uint32_t dppu(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, RM, 0xf, false);
+}
+__device__ __forceinline__ uint32_t rdl(uint32_t v, int lane) { return (uint32_t)__builtin_amdgcn_readlane((int)v, lane); }
+// inclusive prefix sum over the wave
+__device__ __forceinline__ uint32_t wave_add_incl(uint32_t v) {
+    v += dppu<DPP_ROW_SHR(1)>(0u, v);
+    v += dppu<DPP_ROW_SHR(2)>(0u, v);
+    v += dppu<DPP_ROW_SHR(4)>(0u, v);
+    v += dppu<DPP_ROW_SHR(8)>(0u, v);
+    v += dppu<DPP_ROW_BCAST15, 0xa>(0u, v);
+    v += dppu<DPP_ROW_BCAST31, 0xc>(0u, v);
+    return v;
+}
+// inclusive "last set": v of the highest lane <= this one whose f is set (f: 0/1; f' = any such lane)
+#define WL_STEP(CTRL, RM) { const uint32_t tv = dppu<CTRL, RM>(0u, v), tf = dppu<CTRL, RM>(0u, f); v = f ? v : tv; f |= tf; }
+__device__ __forceinline__ void wave_last_incl(uint32_t& v, uint32_t& f) {
+    WL_STEP(DPP_ROW_SHR(1), 0xf) WL_STEP(DPP_ROW_SHR(2), 0xf) WL_STEP(DPP_ROW_SHR(4), 0xf)
+    WL_STEP(DPP_ROW_SHR(8), 0xf) WL_STEP(DPP_ROW_BCAST15, 0xa) WL_STEP(DPP_ROW_BCAST31, 0xc)
+}
+__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, 64); }
+
+// In-wave agreement: lane l's chain must start where the chain of the nearest
+// segment before it leaves (the block's entry X0 for the first lanes); lanes
+// after the first lane whose chain ends in a terminal are not checked (they are
+// dead).  The lowest disagreeing lane is re-walked exactly, until every lane
+// agrees.
+__device__ __forceinline__ SegChain seg_resolve(const Seg& K, SegChain L, int lane, uint32_t X0, Globals* g) {
+    for (int iter = 0;; iter++) {
+        const bool isC = L.mode == LM_CHAIN;
+        uint32_t v = L.x, f = isC ? 1u : 0u;
+        wave_last_incl(v, f);
+        const uint32_t vp = dppu<DPP_WF_SR1>(0u, v), fp = dppu<DPP_WF_SR1>(0u, f);
+        const uint32_t Xin = fp ? vp : X0;
+        const u64 bt = __ballot(isC && L.term != TERM_NONE);
+        const int kT = bt ? __ffsll((long long)bt) - 1 : 64;
+        bool bad = false;
+        if (L.mode != LM_OFF && lane <= kT) bad = isC ? L.E != Xin : in_seg(K, Xin);
+        const u64 bm = __ballot(bad);
+        if (!bm) return L;
+        if (iter > 4 * CLY_NL) { if (lane == 0) atomicOr(&g->fail, 1u); return L; }
+        const int k = __ffsll((long long)bm) - 1;
+        if (lane == k) {
+            if (!in_seg(K, Xin)) sc_set(L, LM_NONE);
+            else seg_walk(K, Xin, true, L);
+        }
     }
 }
 
-__device__ __forceinline__ bool walk(const Chunk& K, uint32_t p, bool exact, LaneChain& L) {
-    return walk_(K, p, exact, L);
+// ---------------------------------------------------------------------------
+// Chain state between tiles (k_link).
+struct LBState {
+    uint64_t count;              // records before (file-relative in TileIn)
+    uint32_t X;                  // chain position
+    uint32_t crc_last;           // stored CRC of the last record started before (its successor's Q)
+    uint32_t P_last;             // that record's start (NONE32: none in this file)
+    int      dead;               // the file's chain has ended
+};
+// TileIn (k_link): the true state entering a tile, 32 B:
+//   w[0..1] count (file-relative), w[2] X, w[3] dead, w[4] crc_last, w[5] P_last
+struct TileIn { uint32_t w[8]; };
+#define TI_DEAD 1u
+__device__ __forceinline__ LBState ti_load(const TileIn* p) {
+    const u32x4 a = ((const u32x4*)p)[0], b = ((const u32x4*)p)[1];
+    LBState s;
+    s.count = ((uint64_t)a.y << 32) | a.x; s.X = a.z; s.dead = (a.w & TI_DEAD) != 0; s.crc_last = b.x; s.P_last = b.y;
+    return s;
+}
+__device__ __forceinline__ void ti_store(TileIn* p, const LBState& s) {
+    ((u32x4*)p)[0] = (u32x4){(uint32_t)s.count, (uint32_t)(s.count >> 32), s.X, s.dead ? TI_DEAD : 0u};
+    ((u32x4*)p)[1] = (u32x4){s.crc_last, s.P_last, 0u, 0u};
 }
 
-// SWAR byte masks (bit 7 of each byte): byte <= 4 (type / data type), byte
-// nonzero and even (first byte of the key-size varint of a record with ks >= 1).
-__device__ __forceinline__ uint32_t swar_le4(uint32_t W) { return ~(((W | 0x80808080u) - 0x05050505u) | W) & 0x80808080u; }
-__device__ __forceinline__ uint32_t swar_ks(uint32_t W) {
-    const uint32_t nz = ((W & 0x7f7f7f7fu) + 0x7f7f7f7fu) | W;
-    return nz & ~(W << 7) & 0x80808080u;
+// ---------------------------------------------------------------------------
+// Outputs of one record.  Tuple (48 B, cly_tuple layout):
+__device__ __forceinline__ void tuple_words(gbytes base, uint32_t p, const Hdr& h, uint32_t fid, u32x4& a, u32x4& b,
+                                            u32x4& c) {
+    int tn;
+    int64_t tx;
+    if (h.key0 < 0x80 && h.ks >= 1) { tn = 1; tx = (int64_t)(h.key0 >> 1) ^ -(int64_t)(h.key0 & 1); }
+    else {
+        const int64_t klim = h.ks < 11u ? (int64_t)h.ks : 11;
+        tx = go_varint(base + p + h.hsz, klim, tn);                     // parseLogRecordKey, db.go:706-710
+    }
+    const uint64_t off = p, ex = (uint64_t)h.exp, txv = tn < 0 ? 0ull : (uint64_t)tx;
+    a = (u32x4){(uint32_t)off, (uint32_t)(off >> 32), (uint32_t)ex, (uint32_t)(ex >> 32)};
+    b = (u32x4){(uint32_t)txv, (uint32_t)(txv >> 32), fid, (uint32_t)h.size};
+    c = (u32x4){h.ks, h.vs,
+                (h.type & 0xff) | ((h.dt & 0xff) << 8) | ((uint32_t)(h.hsz & 0xff) << 16) |
+                    ((uint32_t)(tn < 0 ? 0xFF : tn) << 24),
+                h.crc};
+}
+__device__ __forceinline__ void put_tuple(gtuples out, uint64_t idx, uint64_t out_cap, gbytes base, uint32_t p,
+                                          const Hdr& h, uint32_t fid, Globals* g) {
+    u32x4 a, b, c;
+    tuple_words(base, p, h, fid, a, b, c);
+    if (idx >= out_cap) { atomicOr(&g->overflow, 1u); return; }
+    CLY_GL u32x4* dst = (CLY_GL u32x4*)(out + idx);
+    dst[0] = a; dst[1] = b; dst[2] = c;
+}
+// Compact entry (16 B), k_scan -> k_emit.  Short form (bit 26 of w3; every
+// record the writer produces without a TTL or a txId >= 64): w0 crc,
+// w1 ks (24 bits) | hsz-6 << 24 | type << 29, w2 vs, w3 rel | dt << 16 |
+// key0 << 19 (the txId varint's single byte).  Long form: w3 = rel only
+// (k_emit decodes the header again).
+#define REC_SHORT (1u << 26)
+__device__ __forceinline__ void rec_store(uint32_t* dst, const Hdr& h, uint32_t rel) {
+    const bool sh = h.exp == 0 && h.key0 < 0x80u && h.ks >= 1u && h.ks < (1u << 24) && h.type < 8u && h.dt < 8u &&
+                    h.hsz >= 6 && h.hsz < 38;
+    u32x4 v = (u32x4){0u, 0u, 0u, rel};
+    if (sh) v = (u32x4){h.crc, h.ks | ((uint32_t)(h.hsz - 6) << 24) | (h.type << 29), h.vs,
+                        rel | (h.dt << 16) | (h.key0 << 19) | REC_SHORT};
+    *(CLY_GL u32x4*)dst = v;
 }
 
-// 16-B piece at chunk-relative offset o (bytes past len read as zero; pieces
-// wholly past it are not loaded).
-__device__ __forceinline__ u32x4 piece(const Chunk& K, uint32_t o) {
-    const uint64_t a = (uint64_t)K.cb + o;
-    if (a + 16 <= K.len) return *(const CLY_GL u32x4*)(K.base + a);
+// ---------------------------------------------------------------------------
+// Block loads.  Load k (of 4) of lane i + 16q reads the 16 B at
+// bs + 1024k + 64i + 16q, so that each load instruction reads 1 KiB of
+// consecutive bytes; a 4 x 4 transpose of 16-B elements over the lane quarters
+// (v_permlane32_swap, v_permlane16_swap) then leaves lane L with the 64 bytes
+// at bs + 64L.  Bytes at or past the file end read as zero (a 16-B load that
+// straddles it stays inside its 16-B-aligned block of the buffer).
+__device__ __forceinline__ u32x4 load16z(gbytes base, uint64_t a, uint64_t len) {
+    if (a + 16 <= len) return *(const CLY_GL u32x4*)(base + a);
     u32x4 v = {0u, 0u, 0u, 0u};
-    if (a < K.len) {
-        v = *(const CLY_GL u32x4*)(K.base + a);
-        const uint32_t n = (uint32_t)(K.len - a);          // 1..15 valid bytes
+    if (a < len) {
+        v = *(const CLY_GL u32x4*)(base + a);
+        const uint32_t n = (uint32_t)(len - a);          // 1..15 valid bytes
         #pragma unroll
         for (int k = 0; k < 4; k++) {
             const int lo = 4 * k;
@@ -395,469 +519,292 @@ __device__ __forceinline__ u32x4 piece(const Chunk& K, uint32_t o) {
     }
     return v;
 }
-
-// First candidate record start at or after chunk offset `from` (SWAR filter:
-// the type and data-type bytes are <= 4), NONE32 if none starts in the chunk.
-// The four candidate bits of a word are gathered by one multiply: bits 7, 15,
-// 23, 31 times 1 + 2^7 + 2^14 + 2^21 land in bits 28..31.
-__device__ __forceinline__ uint32_t first_cand(const Chunk& K, uint32_t from) {
-    for (uint32_t b = from / (CLY_BW * 4); b < (uint32_t)CLY_NB; b++) {
-        uint32_t w[CLY_BW + 4];
-        if ((uint64_t)K.cb + (b + 1) * CLY_BW * 4 + 16 <= K.len) {
-            const CLY_GL u32x4* src = (const CLY_GL u32x4*)(K.base + K.cb + b * CLY_BW * 4);
-            #pragma unroll
-            for (int k = 0; k < CLY_BW / 4 + 1; k++) {
-                const u32x4 v = src[k];
-                w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
-            }
-        } else {
-            #pragma unroll
-            for (int k = 0; k < CLY_BW / 4 + 1; k++) {
-                const u32x4 v = piece(K, b * CLY_BW * 4 + 16 * k);
-                w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
-            }
-        }
-        uint32_t cmk[CLY_BW / 8];
+// The block's loads, and the 64 bytes after it (16 B by each of lanes 0..3:
+// the tail of the wave's stage, for headers that start near the block's end).
+__device__ __forceinline__ void blk_issue(gbytes base, uint64_t flen, uint32_t bs, int lane, u32x4 (&e)[4], u32x4& hl) {
+    const uint32_t lo = 64u * (uint32_t)(lane & 15) + 16u * (uint32_t)(lane >> 4);
+    if ((uint64_t)bs + CLY_BLK <= flen) {
+        const CLY_GL u32x4* src = (const CLY_GL u32x4*)(base + bs + lo);
         #pragma unroll
-        for (int k = 0; k < CLY_BW / 8; k++) cmk[k] = 0;
+        for (int k = 0; k < 4; k++) e[k] = src[64 * k];
+    } else {
         #pragma unroll
-        for (int k = 0; k < CLY_BW; k++) {
-            // positions 4k..4k+3: bytes +4 (type) and +5 (data type) <= 4
-            const uint32_t L1 = swar_le4(w[k + 1]), L2 = swar_le4(w[k + 2]);
-            const uint32_t cm = L1 & __builtin_amdgcn_alignbit(L2, L1, 8);
-            cmk[k >> 3] |= ((cm * 0x204081u) >> 28) << (4 * (k & 7));
-        }
-        const uint32_t base = b * CLY_BW * 4;
-        #pragma unroll
-        for (int k = 0; k < CLY_BW / 8; k++) {
-            const uint32_t lo = base + 32 * k;
-            uint32_t m = cmk[k];
-            if (from > lo) m = from - lo >= 32 ? 0u : (m & (0xFFFFFFFFu << (from - lo)));
-            if (m) {
-                const uint32_t q = K.cb + lo + (uint32_t)__builtin_ctz(m);
-                return q < K.ce ? q : NONE32;
-            }
-        }
+        for (int k = 0; k < 4; k++) e[k] = load16z(base, (uint64_t)bs + 1024 * k + lo, flen);
     }
-    return NONE32;
+    hl = (u32x4){0u, 0u, 0u, 0u};
+    if (lane < 4) hl = load16z(base, (uint64_t)bs + CLY_BLK + 16 * lane, flen);
 }
-
-// Phase A for one lane: the chain of its chunk under its own guess (the first
-// candidate whose speculative walk holds).
-__device__ __forceinline__ LaneChain phase_a(const Chunk K) {
-    LaneChain L;
-    if (!K.on) { chain_set(L, LM_OFF); return L; }
-    if (K.cb == 0) { walk(K, 0, true, L); return L; }
-    chain_set(L, LM_NONE);
-    uint32_t from = 0;
-    for (int it = 0; it < CLY_CH; it++) {
-        const uint32_t q = first_cand(K, from);
-        if (q == NONE32) break;
-        LaneChain T;
-        if (walk(K, q, false, T)) { L = T; break; }
-        from = q + 1 - K.cb;
-    }
-    return L;
+__device__ __forceinline__ void swap32(uint32_t& a, uint32_t& b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+    a = r[0]; b = r[1];
 }
-
-// ---------------------------------------------------------------------------
-// wave helpers
-__device__ __forceinline__ int scan_max_incl(int v, int lane) {
+__device__ __forceinline__ void swap16(uint32_t& a, uint32_t& b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+    a = r[0]; b = r[1];
+}
+// e[k] of lane quarter q -> e[j] of quarter q = what quarter j held in e[q]
+__device__ __forceinline__ void quad_transpose(u32x4 (&e)[4]) {
     #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) { const int u = __shfl_up(v, o, 64); if (lane >= o) v = max(v, u); }
-    return v;
+    for (int c = 0; c < 4; c++) {
+        uint32_t a0 = e[0][c], a1 = e[1][c], a2 = e[2][c], a3 = e[3][c];
+        swap32(a0, a2); swap32(a1, a3);
+        swap16(a0, a1); swap16(a2, a3);
+        e[0][c] = a0; e[1][c] = a1; e[2][c] = a2; e[3][c] = a3;
+    }
 }
-__device__ __forceinline__ int scan_max_excl(int v, int lane) {
-    const int inc = scan_max_incl(v, lane);
-    const int up = __shfl_up(inc, 1, 64);
-    return lane > 0 ? up : -1;
-}
-__device__ __forceinline__ uint32_t scan_add_incl(uint32_t v, int lane) {
+__device__ __forceinline__ void patch_word(uint32_t (&w)[16], uint32_t k, uint32_t e) {
     #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) { const uint32_t u = __shfl_up(v, o, 64); if (lane >= o) v += u; }
-    return v;
-}
-__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, 64); }
-
-// In-wave agreement: lane l's chain must start where the chain of the nearest
-// chunk before it leaves (the tile's entry X0 for the first lanes; dead0: the
-// file's chain ended before the tile).  The lowest disagreeing lane is
-// re-walked exactly, until every lane agrees.
-__device__ __forceinline__ LaneChain resolve(const Chunk K, LaneChain L, int lane, uint32_t X0, bool dead0, Globals* g) {
-    for (int iter = 0;; iter++) {
-        const bool isC = L.mode == LM_CHAIN;
-        const int pk = scan_max_incl(isC ? lane : -1, lane);
-        const int pu = __shfl_up(pk, 1, 64);            // (every lane: cross-lane reads outside conditionals)
-        const int j = lane > 0 ? pu : -1;
-        const uint32_t xj = shfl_u32(L.x, j < 0 ? 0 : j);
-        const int tj = __shfl(L.term, j < 0 ? 0 : j, 64);
-        const uint32_t Xin = j >= 0 ? xj : X0;
-        const bool din = j >= 0 ? tj != TERM_NONE : dead0;
-        bool bad = false;
-        if (L.mode != LM_OFF) {
-            if (din) bad = L.mode != LM_DEAD;
-            else if (L.mode == LM_CHAIN) bad = L.E != Xin;
-            else if (L.mode == LM_NONE) bad = in_chunk(K, Xin);
-            else bad = true;                                   // LM_DEAD under a live chain
-        }
-        const u64 bm = __ballot(bad);
-        if (!bm) return L;
-        if (iter > 2 * CLY_NL + 2) { if (lane == 0) atomicOr(&g->fail, 1u); return L; }
-        const int k = __ffsll((long long)bm) - 1;
-        if (lane == k) {
-            if (din) chain_set(L, LM_DEAD);
-            else if (!in_chunk(K, Xin)) chain_set(L, LM_NONE);
-            else walk(K, Xin, true, L);
-        }
-    }
+    for (int i = 0; i < 16; i++) w[i] ^= (k == (uint32_t)i) ? e : 0u;
 }
 
 // ---------------------------------------------------------------------------
-// ---------------------------------------------------------------------------
-// Chain state between tiles (k_link) and the per-lane chains (k_spec -> k_crc).
-struct LBState {
-    uint64_t count;              // records before (file-relative in TileIn, absolute in k_crc)
-    uint32_t X;                  // chain position
-    uint32_t crc_last;           // stored CRC of the last record started before (its successor's Q)
-    uint32_t P_last;             // that record's start (NONE32: none in this file)
-    int      dead;               // the file's chain has ended
-};
-// TileIn (k_link): the true state entering a tile, 32 B:
-//   w[0..1] count (file-relative), w[2] X, w[3] dead | fix << 1, w[4] crc_last, w[5] P_last
-struct TileIn { uint32_t w[8]; };
-#define TI_DEAD 1u
-#define TI_FIX 2u
-__device__ __forceinline__ LBState ti_load(const TileIn* p) {
-    const u32x4 a = ((const u32x4*)p)[0], b = ((const u32x4*)p)[1];
-    LBState s;
-    s.count = ((uint64_t)a.y << 32) | a.x; s.X = a.z; s.dead = (a.w & TI_DEAD) != 0; s.crc_last = b.x; s.P_last = b.y;
-    return s;
-}
-__device__ __forceinline__ void ti_store(TileIn* p, const LBState& s, bool fix) {
-    ((u32x4*)p)[0] = (u32x4){(uint32_t)s.count, (uint32_t)(s.count >> 32), s.X, (s.dead ? TI_DEAD : 0u) | (fix ? TI_FIX : 0u)};
-    ((u32x4*)p)[1] = (u32x4){s.crc_last, s.P_last, 0u, 0u};
-}
-
-// Per-lane chains (structure of arrays over all lanes of the call, nl = 64 * ntiles):
-//   lanes[0*nl + i] mode | term << 8 | cnt << 16,  [1] E,  [2] x,  [3] last,  [4] last_crc
-#define LANE_WORDS 5
-__device__ __forceinline__ void lane_store(uint32_t* lanes, uint64_t nl, uint64_t i, const LaneChain& L) {
-    lanes[i] = (uint32_t)(L.mode & 0xff) | ((uint32_t)(L.term & 0xff) << 8) | (L.cnt << 16);
-    lanes[nl + i] = L.E;
-    lanes[2 * nl + i] = L.x;
-    lanes[3 * nl + i] = L.last;
-    lanes[4 * nl + i] = L.last_crc;
-}
-__device__ __forceinline__ LaneChain lane_load(const uint32_t* __restrict__ lanes, uint64_t nl, uint64_t i) {
-    LaneChain L;
-    const uint32_t m = lanes[i];
-    L.mode = (int)(m & 0xff);
-    L.term = (int)(int8_t)((m >> 8) & 0xff);
-    L.cnt = m >> 16;
-    L.E = lanes[nl + i];
-    L.x = lanes[2 * nl + i];
-    L.last = lanes[3 * nl + i];
-    L.last_crc = lanes[4 * nl + i];
-    L.prev_crc = 0;
-    L.minsz = 0xFFFFFFFFu;
-    L.pk[0] = L.pk[1] = L.pk[2] = L.pk[3] = 0;       // not stored: callers re-walk for record starts
-    return L;
-}
-
-// The tile's LOCAL (its chain under its own entry): flags | records << 32,
-// G | X << 32, crc_last | P_last << 32, tend.  Written by k_spec / k_refix.
-__device__ __forceinline__ void local_store(TileLocal* d, const LaneChain& L, uint32_t G, bool fof, uint32_t tt,
-                                            uint64_t flen, int lane, bool ovf) {
-    const u64 bc = __ballot(L.mode == LM_CHAIN), br = __ballot(L.mode == LM_CHAIN && L.cnt > 0);
-    const uint32_t c = L.mode == LM_CHAIN ? L.cnt : 0u;
-    const uint32_t tile_cnt = shfl_u32(scan_add_incl(c, lane), 63);
-    const int lc = bc ? 63 - __clzll((long long)bc) : 0, lr = br ? 63 - __clzll((long long)br) : 0;
-    const uint32_t X = shfl_u32(L.x, lc);
-    const int term = __shfl(L.term, lc, 64);
-    const uint32_t crc = shfl_u32(L.last_crc, lr), Pl = shfl_u32(L.last, lr);
-    const u64 bg = __ballot(L.mode == LM_CHAIN);
-    const uint32_t Gl = bg ? shfl_u32(L.E, __ffsll((long long)bg) - 1) : NONE32;
-    (void)G;
-    if (lane == 0) {
-        const uint64_t tstart = (uint64_t)tt * CLY_TILE;
-        const uint32_t tend = tstart + CLY_TILE >= flen ? (uint32_t)(flen + 1) : (uint32_t)(tstart + CLY_TILE);
-        u64 f0 = (u64)tile_cnt << 32;
-        if (bc && term != TERM_NONE) f0 |= DF_TERM;
-        if (!bc) f0 |= DF_NONE;
-        if (fof) f0 |= DF_FOF;
-        if (br) f0 |= DF_REC;
-        if (ovf) f0 |= DF_OVF;
-        d->l[0] = f0;
-        d->l[1] = (u64)Gl | ((u64)X << 32);
-        d->l[2] = (u64)crc | ((u64)Pl << 32);
-        d->l[3] = (u64)tend;
-    }
-}
-
-// Inputs of phase C for one lane (after the tile's chain is final).
-struct LaneIn {
-    uint64_t base;               // global tuple index of the lane's first record
-    uint32_t crc_in;             // stored CRC of the record open when the chunk starts
-    uint32_t P_in;               // its start (NONE32 none)
-    bool     spill;              // P_in's patch reaches into this chunk
-};
-
-// The patch of the record start P (stored CRC c, predecessor's cq) on the
-// words [wlo, whi) (absolute word indices), combined onto the last of them it
-// touches; returns that word (NONE32: none in range).
-__device__ __forceinline__ uint32_t patch_part(const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t P, uint32_t c,
-                                               uint32_t cq, uint32_t wlo, uint32_t whi, uint32_t& delta) {
-    const uint32_t j = P & 3, sh = 8 * j, a = P >> 2;
-    uint32_t acc = 0, wl = NONE32;
-    if (a >= wlo && a < whi) {
-        uint32_t pa = j ? (c << sh) : c;
-        if (P != 0) pa ^= q_of(smem, cq, j, cl.r4);
-        acc = pa; wl = a;
-    }
-    if (a + 1 >= wlo && a + 1 < whi) {
-        const uint32_t pb = (j ? (c >> (32 - sh)) : 0u) ^ (j ? (0xFFFFFFFFu << sh) : 0xFFFFFFFFu);
-        acc = wl == NONE32 ? pb : (crc_word(smem, acc, cl) ^ pb);
-        wl = a + 1;
-    }
-    if (j && a + 2 >= wlo && a + 2 < whi) {
-        const uint32_t pc = (1u << sh) - 1u;
-        acc = wl == NONE32 ? pc : (crc_word(smem, acc, cl) ^ pc);
-        wl = a + 2;
-    }
-    delta = acc;
-    return wl;
-}
-
-// Tuple of the record at p (header h): 48 B, cly_tuple layout.
-__device__ __forceinline__ void put_tuple(gtuples out, uint64_t idx, uint64_t out_cap, const Chunk& K, uint32_t p,
-                                          const Hdr& h, uint32_t fid, Globals* g) {
-    int tn;
-    int64_t tx;
-    if (h.key0 < 0x80 && h.ks >= 1) { tn = 1; tx = (int64_t)(h.key0 >> 1) ^ -(int64_t)(h.key0 & 1); }
-    else {
-        const int64_t klim = h.ks < 11u ? (int64_t)h.ks : 11;
-        tx = go_varint(K.base + p + h.hsz, klim, tn);                   // parseLogRecordKey, db.go:706-710
-    }
-    if (idx >= out_cap) { atomicOr(&g->overflow, 1u); return; }
-    const uint64_t off = p, ex = (uint64_t)h.exp, txv = tn < 0 ? 0ull : (uint64_t)tx;
-    CLY_GL u32x4* dst = (CLY_GL u32x4*)(out + idx);
-    dst[0] = (u32x4){(uint32_t)off, (uint32_t)(off >> 32), (uint32_t)ex, (uint32_t)(ex >> 32)};
-    dst[1] = (u32x4){(uint32_t)txv, (uint32_t)(txv >> 32), fid, (uint32_t)h.size};
-    dst[2] = (u32x4){h.ks, h.vs,
-                     (h.type & 0xff) | ((h.dt & 0xff) << 8) | ((uint32_t)(h.hsz & 0xff) << 16) |
-                         ((uint32_t)(tn < 0 ? 0xFF : tn) << 24),
-                     h.crc};
-}
-
-// ---------------------------------------------------------------------------
-// ---------------------------------------------------------------------------
-// Phase C (k_crc), uniform path.  The lane streams its chunk through the CRC
-// register raw, in 128-B bursts: the loop body is the plain slicing-by-4 step.
-// Each record start P changes the stream by one combined patch delta' on one
-// word w of the chunk (patch_part); XORing delta' into word w changes the
-// register at the chunk end by A^(4 (NW - w)) delta', which the walker adds to
-// `pacc` (two nibble-table products, shift_words), so the stream itself never
-// sees the records.  The walker decodes the lane's records one gather ahead
-// and writes their tuples, before the stream.
-__device__ __forceinline__ uint32_t mat_mul(const CLY_LDS uint32_t* t, uint32_t v) {
-    uint32_t p = 0;
-    #pragma unroll
-    for (int n = 0; n < 8; n++) p ^= t[n * 16 + ((v >> (4 * n)) & 15u)];
-    return p;
-}
-// A^m v (m bytes), 1 <= m <= 65536: one nibble-table product per hex digit of m
-__device__ __forceinline__ uint32_t shift_bytes(const CLY_LDS uint8_t* smem, uint32_t m, uint32_t v) {
-    const CLY_LDS uint32_t* t = (const CLY_LDS uint32_t*)(smem + LDS_SH);
-    v = mat_mul(t + (m & 15u) * 128, v);
-    v = mat_mul(t + (16u + ((m >> 4) & 15u)) * 128, v);
-    v = mat_mul(t + (32u + ((m >> 8) & 15u)) * 128, v);
-    v = mat_mul(t + (48u + ((m >> 12) & 15u)) * 128, v);
-    if (m >> 16) v = mat_mul(t + 64u * 128, v);
-    return v;
-}
-// The record start P (stored CRC c, the record before it stored cq) in the
-// file's byte stream, as the CRC register sees it: its stored CRC bytes zeroed
-// (XOR c into bytes [P, P+4)), the register checked against the previous
-// record's CRC (XOR ~cq into the register before byte P; not at P = 0) and the
-// record's own CRC started (XOR 0xFFFFFFFF into the register before byte P+4,
-// = XOR K4 = A^-4 0xFFFFFFFF before byte P).  All three are one register XOR
-// before byte P, whose effect at the tile end TE is A^(TE-P) applied to it;
-// bytes of the patch past TE belong to the next tile, and A^(TE-P) accounts
-// for them there exactly (the file fold shifts tile t by one tile more than
-// tile t+1).
-__device__ __forceinline__ uint32_t rec_patch(const CLY_LDS uint8_t* smem, uint32_t TE, uint32_t P, uint32_t c,
-                                              uint32_t cq, uint32_t K4) {
-    return shift_bytes(smem, TE - P, c ^ K4 ^ (P != 0 ? ~cq : 0u));
-}
-__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
-    #pragma unroll
-    for (int o = 32; o; o >>= 1) v ^= (uint32_t)__shfl_xor((int)v, o, 64);
-    return v;
-}
-
-struct Walker {
-    uint32_t p, cq, i;
-    Gath gt;
-};
-__device__ __forceinline__ void walker_step(const Chunk& K, Walker& W, uint32_t nrec, uint64_t base, uint32_t fid,
-                                            gtuples out, uint64_t out_cap, const CLY_LDS uint8_t* smem,
-                                            uint32_t K4, uint32_t& pacc, Globals* g) {
-    const Hdr h = hdr_at(K.base, W.p, K.len, W.gt);
-    put_tuple(out, base + W.i, out_cap, K, W.p, h, fid, g);
-    pacc ^= rec_patch(smem, K.tb + (uint32_t)CLY_TILE, W.p, h.crc, W.cq, K4);
-    W.cq = h.crc;
-    W.p += (uint32_t)h.size;
-    W.i++;
-    if (W.i < nrec && gath_ok(W.p, K.len)) gath_issue(K.base, W.p, W.gt);
-}
-
-// The raw CRC register of the lane's chunk (no patches), 128-B bursts; with
-// `walk` (tiles whose record starts were not stored) the lane first walks its
-// own records: tuples, and their patches into pacc.
-__device__ __forceinline__ uint32_t phase_c_fast(const Chunk& K, const LaneChain& L, const LaneIn& I, bool active,
-                                                 bool walk, uint32_t slim, uint32_t fid, gtuples out, uint64_t out_cap,
-                                                 const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t K4,
-                                                 uint32_t& pacc, Globals* g) {
-    if (walk) {
-        Walker W;
-        W.p = L.E; W.cq = I.crc_in; W.i = 0;
-        const uint32_t nrec = (active && L.mode == LM_CHAIN) ? L.cnt : 0u;
-        if (nrec && gath_ok(W.p, K.len)) gath_issue(K.base, W.p, W.gt);
-        for (;;) {
-            const bool need = W.i < nrec;
-            if (!__ballot(need)) break;
-            if (need) walker_step(K, W, nrec, I.base, fid, out, out_cap, smem, K4, pacc, g);
-        }
-    }
-    uint32_t s = 0;
-    const CLY_GL u32x4* src = (const CLY_GL u32x4*)(K.base + K.cb);
-    // the stream stops at slim (the terminal lane: T) or the file's end
-    Chunk Ks = K;
-    if ((uint64_t)slim < Ks.len) Ks.len = slim;
-    const bool full = (uint64_t)K.cb + CLY_CH <= Ks.len;
+// The tile body (k_scan, k_refix, k_emit's re-walk).  The wave streams the
+// tile's blocks in order; the chain position X is carried from block to block.
+//   BM_SPEC   k_scan: the entry of a tile other than its file's first is
+//             unknown; the first block with a plausible record start sets the
+//             tile's guess G (a candidate whose speculative walk holds and
+//             leaves at a candidate, or at a plausible header beyond the block);
+//   BM_EXACT  k_refix: the entry is the true state from k_link;
+//   BM_EMIT   k_emit: as BM_EXACT, tuples straight to their output slots (tiles
+//             whose compact list overflowed), no CRC.
+// CRC (not BM_EMIT): the record start P (stored CRC c, the record before it
+// stored cq) changes the file's byte stream, as the CRC register sees it, by
+// one register XOR d = c ^ K4 ^ ~cq before byte P (c zeroes the stored bytes,
+// K4 = A^-4 0xFFFFFFFF starts the record's CRC at P+4, ~cq checks the record
+// ending at P; no ~cq at P = 0); that is the XOR of A^-(P&3) d into the data
+// word at P & ~3, done in registers before the word enters the register.  At
+// the chain's terminal T: ~cq of the last record before T, and every byte from
+// T on zeroed.  The register of the whole patched file is then zero iff every
+// record's CRC matches.  The ~cq of the tile's FIRST boundary (tiles other
+// than a file's first) needs the state entering the tile: the tile XORs
+// 0xFFFFFFFF there, and k_emit adds A^(TE - G) crc_last (the rest of ~cq).
+#define BM_SPEC 0
+#define BM_EXACT 1
+#define BM_EMIT 2
+#ifndef CLY_EXP
+#define CLY_EXP 0                // timing experiments only (wrong results): 1 no record work, 3 candidate
+#endif                           // masks only, 2 no per-record outputs, 5 no agreement pass
+struct TileRes { uint32_t X; bool dead; };
+template <int BM>
+__device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint32_t tt, uint32_t X_in, bool dead_in,
+                                             const CLY_LDS uint8_t* smem, CLY_LDS uint32_t* stg, const CrcLane& cl,
+                                             uint32_t K4, TileLocal* loc, uint32_t* rec, uint32_t* treg, gtuples out,
+                                             uint64_t out_cap, uint64_t gbase, Globals* g) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t tb = (uint32_t)((uint64_t)tt * CLY_TILE);
+    const uint64_t flen = F.len;
+    const gbytes base = (gbytes)F.base;
+    const bool known0 = BM != BM_SPEC || tt == 0;
+    uint32_t X = tt == 0 ? 0u : (known0 ? X_in : NONE32);      // NONE32: entry unknown (BM_SPEC guess mode)
+    bool dead = tt != 0 && known0 && dead_in;
+    bool cq_known = tt == 0;     // the stored CRC before X is known (tile 0: no record before offset 0)
+    uint32_t cq = 0;
+    uint32_t G = NONE32, tcnt = 0, last_crc = 0, P_last = NONE32;
+    int term = TERM_NONE;
+    uint32_t R = 0, carry = 0;   // carry: register XOR due at the next block's first byte (T = block end)
+    const CLY_LDS uint32_t* nibt = (const CLY_LDS uint32_t*)(smem + LDS_NIB);
+    uint32_t* trec = rec + (uint64_t)t * CAP_T * 4;
+    u32x4 e[4], hl;
+    blk_issue(base, flen, tb, lane, e, hl);
     #pragma unroll 1
-    for (int b = 0; b < CLY_NB; b++) {
-        u32x4 v[CLY_BW / 4];
-        if (active && full) {
-            #pragma unroll
-            for (int k = 0; k < CLY_BW / 4; k++) v[k] = src[b * (CLY_BW / 4) + k];
-        } else if (active) {
-            #pragma unroll
-            for (int k = 0; k < CLY_BW / 4; k++) v[k] = piece(Ks, (uint32_t)(b * CLY_BW * 4 + 16 * k));
-        } else {
-            #pragma unroll
-            for (int k = 0; k < CLY_BW / 4; k++) v[k] = (u32x4){0u, 0u, 0u, 0u};
-        }
+    for (int m = 0; m < CLY_NBLK; m++) {
+        const uint32_t bs = tb + (uint32_t)m * CLY_BLK;
+        quad_transpose(e);
+        uint32_t w[16];
         #pragma unroll
-        for (int k = 0; k < CLY_BW / 4; k++) {
-            s = crc_word(smem, s ^ v[k].x, cl);
-            s = crc_word(smem, s ^ v[k].y, cl);
-            s = crc_word(smem, s ^ v[k].z, cl);
-            s = crc_word(smem, s ^ v[k].w, cl);
+        for (int k = 0; k < 4; k++) { w[4 * k] = e[k].x; w[4 * k + 1] = e[k].y; w[4 * k + 2] = e[k].z; w[4 * k + 3] = e[k].w; }
+        const u32x4 hc = hl;
+        if (m + 1 < CLY_NBLK && (BM != BM_EMIT || !dead)) blk_issue(base, flen, bs + CLY_BLK, lane, e, hl);
+        if (BM == BM_EMIT && dead) break;
+        uint32_t pend = 0;
+        const bool owned = X != NONE32 && (X < bs + CLY_BLK || ((uint64_t)X == flen && flen == (uint64_t)bs + CLY_BLK));
+        if (dead) {
+            #pragma unroll
+            for (int k = 0; k < 16; k++) w[k] = 0;
+        } else if (CLY_EXP != 1 && (X == NONE32 || owned)) {
+            // ---- record starts of the block; the headers are read from the
+            // wave's LDS copy of it (the stage)
+            {
+                CLY_LDS u32x4* sv = (CLY_LDS u32x4*)stg;
+                #pragma unroll
+                for (int k = 0; k < 4; k++) sv[4 * lane + k] = (u32x4){w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
+                if (lane < 4) sv[CLY_BLK / 16 + lane] = hc;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            const Seg K = make_seg(F, bs, lane, stg);
+            const uint32_t n0 = dppu<DPP_WF_SL1>(rdl(hc.x, 0), w[0]), n1 = dppu<DPP_WF_SL1>(rdl(hc.y, 0), w[1]);
+            u64 cm = 0;
+            if (K.on) {
+                cm = cand_mask(w, n0, n1);
+                const uint32_t nv = K.ce - K.cb;                    // valid positions
+                if (nv < 64) cm &= (1ull << nv) - 1ull;
+            }
+            if (CLY_EXP == 3) { w[0] ^= (uint32_t)cm ^ (uint32_t)(cm >> 32); X = bs + CLY_BLK + 100; G = tb; }
+            else {
+            SegChain L;
+            if (!K.on) sc_set(L, LM_OFF);
+            else if (X != NONE32) {
+                if (in_seg(K, X)) seg_walk(K, X, true, L);
+                else if (X > K.cb) sc_set(L, LM_NONE);
+                else {
+                    sc_set(L, LM_NONE);
+                    if (cm) { SegChain T; if (seg_walk(K, K.cb + (uint32_t)__builtin_ctzll(cm), false, T)) L = T; }
+                }
+            } else {
+                // guess mode: the first candidate whose walk holds and whose exit
+                // is a candidate of the block (or a plausible header beyond it)
+                sc_set(L, K.on ? LM_NONE : LM_OFF);
+                u64 mm = cm;
+                bool settled = !K.on || !mm;
+                for (int tr = 0; tr < 4; tr++) {
+                    const bool act = !settled;
+                    if (!__ballot(act)) break;
+                    SegChain T;
+                    sc_set(T, LM_NONE);
+                    bool ok = false;
+                    if (act) {
+                        const uint32_t q = K.cb + (uint32_t)__builtin_ctzll(mm);
+                        mm &= mm - 1;
+                        ok = seg_walk(K, q, false, T);
+                    }
+                    const bool chk_in = act && ok && T.term == TERM_NONE && T.x < bs + CLY_BLK;
+                    const uint32_t off = chk_in ? T.x - bs : 0u;
+                    const int tl = (int)(off >> 6);
+                    const uint32_t clo = shfl_u32((uint32_t)cm, tl), chi = shfl_u32((uint32_t)(cm >> 32), tl);
+                    if (act && ok && T.term == TERM_NONE) {
+                        if (chk_in) {
+                            const uint32_t b = off & 63u;
+                            ok = (((b < 32 ? clo >> b : chi >> (b - 32))) & 1u) != 0;
+                        } else {
+                            const Hdr eh = hdr_get(base, T.x, flen, stg, bs);
+                            ok = (eh.status == REC_OK && eh.good) || eh.status == CLY_END_ZERO ||
+                                 (eh.status == CLY_END_EOF && (uint64_t)T.x == flen);
+                        }
+                    }
+                    if (act && ok) { L = T; settled = true; }
+                    if (act && !ok && !mm) settled = true;
+                }
+            }
+            uint32_t X0 = X;
+            bool any = true;
+            if (X == NONE32) {
+                const u64 bc = __ballot(L.mode == LM_CHAIN);
+                any = bc != 0;
+                if (any) X0 = rdl(L.E, __ffsll((long long)bc) - 1);
+            }
+            if (any) {
+                if (CLY_EXP != 5) L = seg_resolve(K, L, lane, X0, g);
+                // the first terminal ends the chain: the lanes after it are dead
+                const u64 bt = __ballot(L.mode == LM_CHAIN && L.term != TERM_NONE);
+                const int kT = bt ? __ffsll((long long)bt) - 1 : 64;
+                if (lane > kT && L.mode != LM_OFF) sc_set(L, LM_DEAD);
+                const bool isC = L.mode == LM_CHAIN;
+                const uint32_t c = isC ? L.cnt : 0u;
+                const uint32_t incl = wave_add_incl(c);
+                const uint32_t bcnt = rdl(incl, 63), lex = incl - c;
+                // the stored CRC of the record before the lane's first one
+                uint32_t lv = L.last_crc, lf = c > 0 ? 1u : 0u;
+                wave_last_incl(lv, lf);
+                const uint32_t lvp = dppu<DPP_WF_SR1>(0u, lv), lfp = dppu<DPP_WF_SR1>(0u, lf);
+                uint32_t pcq = lfp ? lvp : cq;
+                bool pk = lfp ? true : cq_known;
+                // the lane's records: outputs and CRC patches (headers from the stage)
+                uint32_t p = L.E;
+                for (uint32_t i = 0; CLY_EXP != 2 && __ballot(i < c); i++) {
+                    if (i < c) {
+                        const Hdr h = hdr_get(base, p, flen, stg, bs);
+                        const uint32_t idx = tcnt + lex + i;
+                        if (BM == BM_EMIT) put_tuple(out, gbase + idx, out_cap, base, p, h, F.fid, g);
+                        else {
+                            if (idx < CAP_T) rec_store(trec + 4 * idx, h, p - tb);
+                            const uint32_t d = h.crc ^ K4 ^ (p == 0 ? 0u : (pk ? ~pcq : 0xFFFFFFFFu));
+                            patch_word(w, (p - K.cb) >> 2, crc_unbytes(smem, d, p & 3u, cl.r4));
+                        }
+                        pcq = h.crc; pk = true;
+                        p += (uint32_t)h.size;
+                    }
+                }
+                if (BM != BM_EMIT) {
+                    if (lane == kT) {
+                        const uint32_t T = L.x;
+                        const uint32_t dT = T == 0 ? 0u : (pk ? ~pcq : 0xFFFFFFFFu);
+                        #pragma unroll
+                        for (int k = 0; k < 16; k++) {
+                            const uint32_t a = K.cb + 4u * k;
+                            if (a >= T) w[k] = 0;
+                            else if (a + 4 > T) w[k] &= (1u << (8 * (T - a))) - 1u;
+                        }
+                        if (T < K.cb + CLY_SEG) patch_word(w, (T - K.cb) >> 2, crc_unbytes(smem, dT, T & 3u, cl.r4));
+                        else pend = dT;                         // T = len = the segment's end
+                    }
+                    if (lane > kT) {
+                        #pragma unroll
+                        for (int k = 0; k < 16; k++) w[k] = 0;
+                    }
+                }
+                // the chain after the block
+                if (bcnt) {
+                    const u64 br = __ballot(c > 0);
+                    const int lr = 63 - __clzll((long long)br);
+                    last_crc = rdl(L.last_crc, lr);
+                    P_last = rdl(L.last, lr);
+                    cq = last_crc; cq_known = true;
+                }
+                tcnt += bcnt;
+                const u64 bcc = __ballot(isC);
+                if (bcc) {
+                    if (G == NONE32) G = rdl(L.E, __ffsll((long long)bcc) - 1);
+                    X = rdl(L.x, 63 - __clzll((long long)bcc));
+                    if (bt) { dead = true; term = (int)rdl((uint32_t)L.term, kT); }
+                }
+            }
+            }
+        }
+        if (BM != BM_EMIT) {
+            // the register XOR of a terminal at a segment's end goes to the next
+            // segment's first word (the next block's, or the tile end)
+            w[0] ^= dppu<DPP_WF_SR1>(carry, pend);
+            carry = rdl(pend, 63);
+            if (m) R = mat_mul(nibt + 6 * 128, R);
+            #pragma unroll
+            for (int k = 0; k < 16; k++) R = crc_word(smem, R ^ w[k], cl);
         }
     }
-    return s;
+    TileRes res;
+    res.X = X; res.dead = dead;
+    if (BM != BM_EMIT) {
+        // fold of the lanes' registers to the tile end: sum over l of A^(64 (63 - l)) R_l
+        uint32_t r = R;
+        #pragma unroll
+        for (int lvl = 0; lvl < 6; lvl++) {
+            const int d = 1 << lvl;
+            const uint32_t o = (uint32_t)__shfl_down((int)r, d, 64);
+            const uint32_t sh = mat_mul(nibt + lvl * 128, r);
+            if ((lane & (2 * d - 1)) == 0) r = sh ^ o;
+        }
+        if (lane == 0) {
+            treg[t] = r ^ carry;
+            const uint64_t tstart = tb;
+            const uint32_t tend = tstart + CLY_TILE >= flen ? (uint32_t)(flen + 1) : (uint32_t)(tstart + CLY_TILE);
+            u64 f0 = (u64)tcnt << 32;
+            if (term != TERM_NONE) f0 |= DF_TERM;
+            if (G == NONE32) f0 |= DF_NONE;
+            if (tt == 0) f0 |= DF_FOF;
+            if (P_last != NONE32) f0 |= DF_REC;
+            if (tcnt > CAP_T) f0 |= DF_OVF;
+            TileLocal* d = &loc[t];
+            d->l[0] = f0;
+            d->l[1] = (u64)G | ((u64)X << 32);
+            d->l[2] = (u64)last_crc | ((u64)P_last << 32);
+            d->l[3] = (u64)tend | ((u64)(uint8_t)(int8_t)term << 32);
+        }
+    }
+    return res;
 }
 
 // ---------------------------------------------------------------------------
-// Phase C, exact path (the lane holding the chain's terminal, lanes with
-// records shorter than 12 bytes, and k_locate): word by word with every
-// boundary's byte patches, everything from the terminal T on zeroed.  Starts
-// from register s0.  With `observe`, the first record whose check fails
-// (register after its end word != 0) is returned in fail_P / fail_i.
-struct Bnd { uint32_t P, c, q, start; uint64_t idx; int term; };
-// Boundaries of exact_lane.  A record start P patches bytes [P, P+8) and a
-// record is at least 6 bytes (headerSize >= 6 for a decoded record), so at
-// most two record starts touch one word: two named slots (the older one drops
-// out when a third is pushed) plus one for the terminal; no array, so no
-// dynamic indexing and no scratch memory.
-__device__ __forceinline__ uint32_t bnd_patch(const Bnd& b, uint32_t A, uint32_t d) {
-    uint32_t patch = 0;
-    #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const uint32_t x = A + i;
-        uint32_t m = 0;
-        if (!b.term && x >= b.P && x < b.P + 4) m = (d >> (8 * i)) & 0xffu;          // stored CRC zeroed
-        if (!b.term && x >= b.P + 4 && x < b.P + 8) m ^= 0xffu;                     // init 0xFF
-        patch ^= m << (8 * i);
-    }
-    if ((b.P >> 2) == (A >> 2)) patch ^= b.q;
-    return patch;
-}
-__device__ __forceinline__ bool bnd_fails(const Bnd& b, uint32_t A, uint32_t s) {
-    return (b.P >> 2) == (A >> 2) && b.P != 0 && b.start != NONE32 && s != 0;
-}
-__device__ __forceinline__ uint32_t exact_lane(const Chunk& K, const LaneChain& L, const LaneIn& I, uint32_t s0, bool emit,
-                               bool observe, uint32_t fid, gtuples out, uint64_t out_cap,
-                               const CLY_LDS uint8_t* smem, const CrcLane& cl, Globals* g, uint32_t& fail_P,
-                               uint64_t& fail_i, uint32_t& expect, const CLY_LDS uint32_t* wl = nullptr) {
-    uint32_t s = s0;
-    fail_P = NONE32; fail_i = 0; expect = 0;
-    Bnd rA, rB, tT;
-    bool vA = false, vB = false, vT = false;
-    rA.P = rB.P = tT.P = 0; rA.c = rB.c = tT.c = 0; rA.q = rB.q = tT.q = 0; rA.term = rB.term = 0; tT.term = 1;
-    rA.start = rB.start = tT.start = NONE32; rA.idx = rB.idx = tT.idx = 0;
-    if (I.spill) { rB.P = I.P_in; rB.c = I.crc_in; rB.q = 0; rB.start = NONE32; rB.idx = 0; vB = true; }
-    const uint32_t T = (L.mode == LM_CHAIN && L.term != TERM_NONE) ? L.x : NONE32;
-    uint32_t wp = L.E, cq = I.crc_in, wi = 0, start = I.P_in;
-    uint64_t sidx = I.base - 1;
-    const uint32_t nrec = L.mode == LM_CHAIN ? L.cnt : 0u;
-    bool tpushed = T == NONE32;
-    for (uint32_t w = 0; w < CLY_NW; w++) {
-        const uint32_t A = K.cb + 4 * w;
-        // the boundaries whose first patch word is this one
-        for (;;) {
-            if (wi < nrec && (wp >> 2) == (A >> 2)) {
-                const Hdr h = hdr_load(K.base, wp, K.len);
-                if (emit) put_tuple(out, I.base + wi, out_cap, K, wp, h, fid, g);
-                rA = rB; vA = vB;
-                rB.P = wp; rB.c = h.crc; rB.q = wp != 0 ? q_of(smem, cq, wp & 3, cl.r4) : 0u;
-                rB.start = start; rB.idx = sidx; vB = true;
-                start = wp; sidx = I.base + wi;
-                cq = h.crc; wp += (uint32_t)h.size; wi++;
-                continue;
-            }
-            if (!tpushed && wi >= nrec && (T >> 2) == (A >> 2)) {
-                tT.P = T; tT.q = T != 0 ? q_of(smem, cq, T & 3, cl.r4) : 0u;
-                tT.start = start; tT.idx = sidx; vT = true;
-                tpushed = true;
-                continue;
-            }
-            break;
-        }
-        uint32_t d = 0;
-        if ((uint64_t)A < K.len) {
-            d = wl ? wl[w] : *(const CLY_GL uint32_t*)(K.base + A);
-            const uint64_t n = K.len - A;
-            if (n < 4) d &= (1u << (8 * n)) - 1u;
-        }
-        if (T != NONE32 && A + 4 > T) d = A >= T ? 0u : (d & ((1u << (8 * (T - A))) - 1u));
-        uint32_t patch = 0;
-        if (vA) patch ^= bnd_patch(rA, A, d);
-        if (vB) patch ^= bnd_patch(rB, A, d);
-        if (vT) patch ^= bnd_patch(tT, A, d);
-        s = crc_word(smem, s ^ d ^ patch, cl);
-        if (observe && fail_P == NONE32) {
-            if (vA && bnd_fails(rA, A, s)) { fail_P = rA.start; fail_i = rA.idx; }
-            if (vB && bnd_fails(rB, A, s)) { fail_P = rB.start; fail_i = rB.idx; }
-            if (vT && bnd_fails(tT, A, s)) { fail_P = tT.start; fail_i = tT.idx; }
-        }
-        if (vT && (tT.P >> 2) <= (A >> 2)) vT = false;
-    }
-    // the terminal one word past a full chunk (T = len = chunk end): the register
-    // after the chunk must equal Q there
-    if (!tpushed) {
-        expect = T != 0 ? q_of(smem, cq, 0, cl.r4) : 0u;
-        if (observe && fail_P == NONE32 && s != expect && start != NONE32) { fail_P = start; fail_i = sidx; }
-    }
-    return s;
-}
-
-// ---------------------------------------------------------------------------
-// ---------------------------------------------------------------------------
-// Kernels of one call: k_spec (every tile on its own), k_link + k_fbase (the
-// chain state entering every tile), k_refix (tiles whose own entry was wrong;
-// then k_link again), k_crc (CRC stream + tuples), k_fin, k_locate.
+// Kernels of one call.
 __device__ __forceinline__ int find_file(const uint32_t* __restrict__ tprefix, int nfiles, uint32_t t) {
     int lo = 0, hi = nfiles - 1;
     while (lo < hi) {
@@ -866,123 +813,30 @@ __device__ __forceinline__ int find_file(const uint32_t* __restrict__ tprefix, i
     }
     return lo;
 }
-__device__ __forceinline__ Chunk make_chunk(const DevFile& F, uint32_t tt, int lane) {
-    Chunk K;
-    K.base = (gbytes)F.base; K.len = F.len;
-    const uint64_t cb = (uint64_t)tt * CLY_TILE + (uint64_t)lane * CLY_CH;
-    K.cb = (uint32_t)cb;
-    K.ce = (uint32_t)(cb + CLY_CH < F.len ? cb + CLY_CH : F.len);
-    K.tb = (uint32_t)((uint64_t)tt * CLY_TILE);
-    K.last = cb + CLY_CH >= F.len;
-    K.on = cb < F.len || cb == 0;
-    if (!K.on) { K.cb = 0xFFFFFFF0u; K.ce = 0xFFFFFFF0u; }
-    return K;
-}
-// Lane inputs from the final chain and the state entering the tile.
-__device__ __forceinline__ LaneIn lane_inputs(const Chunk& K, const LaneChain& L, const LBState& S, int lane,
-                                             uint32_t& tile_cnt) {
-    LaneIn I;
-    const uint32_t cnt = (L.mode == LM_CHAIN) ? L.cnt : 0u;
-    const uint32_t incl = scan_add_incl(cnt, lane);
-    tile_cnt = shfl_u32(incl, 63);
-    I.base = S.count + (incl - cnt);
-    const int pr = scan_max_incl(cnt > 0 ? lane : -1, lane);
-    const int pu = __shfl_up(pr, 1, 64);
-    const int j = lane > 0 ? pu : -1;
-    const uint32_t lc = shfl_u32(L.last_crc, j < 0 ? 0 : j), lp = shfl_u32(L.last, j < 0 ? 0 : j);
-    I.crc_in = j >= 0 ? lc : S.crc_last;
-    I.P_in = j >= 0 ? lp : S.P_last;
-    I.spill = K.on && (L.mode == LM_CHAIN || L.mode == LM_NONE) && I.P_in != NONE32 && I.P_in + 8 > K.cb &&
-              I.P_in < K.cb;
-    return I;
-}
-// Fold of the lanes' registers: sum over l of A^(CLY_CH (63 - l)) r_l (lane 0).
-__device__ __forceinline__ uint32_t tile_fold(const CLY_LDS uint8_t* smem, uint32_t r, int lane) {
-    #pragma unroll
-    for (int lvl = 0; lvl < 6; lvl++) {
-        const int d = 1 << lvl;
-        const uint32_t o = (uint32_t)__shfl_down((int)r, d, 64);
-        const uint32_t sh = nib_mul(smem, lvl, r);
-        if ((lane & (2 * d - 1)) == 0) r = sh ^ o;
-    }
-    return r;
+__device__ __forceinline__ uint32_t k4_const(const CLY_LDS uint8_t* smem, uint32_t r4) {
+    uint32_t K4 = 0xFFFFFFFFu;              // A^-4 0xFFFFFFFF
+    for (int k = 0; k < 4; k++) K4 = crc_unbyte(smem, K4, r4);
+    return K4;
 }
 
-// The record starts of a lane's final chain into the tile's list (exact walk).
-__device__ __forceinline__ void emit_positions(const Chunk& K, const LaneChain& L, uint16_t* pos) {
-    if (L.mode != LM_CHAIN) return;
-    uint32_t p = L.E;
-    for (uint32_t i = 0; i < L.cnt; i++) {
-        pos[i] = (uint16_t)(p - K.tb);
-        const Hdr h = hdr_load(K.base, p, K.len);
-        p += (uint32_t)h.size;
-    }
-}
-// Record starts of the tile, in chain order, into pos[t * POS_CAP ...] (from
-// the chain's own packed starts; a lane with more than PK_N records re-walks
-// its chain, whose headers are in L2 by now).  Returns
-// the overflow flag (more than POS_CAP records in the tile).
-__device__ __forceinline__ bool store_positions(const Chunk& K, const LaneChain& L, int lane, uint16_t* tpos,
-                                                bool have_pk) {
-    const uint32_t c = L.mode == LM_CHAIN ? L.cnt : 0u;
-    const uint32_t incl = scan_add_incl(c, lane);
-    const uint32_t tot = shfl_u32(incl, 63);
-    if (tot > POS_CAP) return true;
-    uint16_t* dst = tpos + (incl - c);
-    if (have_pk && c <= PK_N) {
-        #pragma unroll
-        for (uint32_t i = 0; i < PK_N; i++)
-            if (i < c) dst[i] = (uint16_t)(L.pk[i >> 1] >> (16 * (i & 1)));
-    } else {
-        emit_positions(K, L, dst);
-    }
-    return false;
-}
-
-// k_spec: one wave per tile.  Phase A (each lane's chain under its own guess),
-// the lanes made to agree under the tile's guess G (0 for a file's first
-// tile), the lane chains and the tile's LOCAL written out.
-#define SPEC_WAVES 4
-__global__ void __launch_bounds__(64 * SPEC_WAVES, 6)   // 6 waves/SIMD (80 VGPRs): C3 k_spec -6 %
-k_spec(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
-       TileLocal* loc, uint32_t* lanes, uint16_t* pos, Globals* g) {
-    const uint32_t t = blockIdx.x * SPEC_WAVES + (threadIdx.x >> 6);
-    if (t >= ntiles) return;
+// k_scan: one wave per tile (grid-stride), every byte of every file read once.
+#define SCAN_WAVES 16
+#define SCAN_LDS_ALL (SCAN_LDS + SCAN_WAVES * STG_BYTES)     // tables + one block stage per wave
+__global__ void __launch_bounds__(64 * SCAN_WAVES)
+k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
+       TileLocal* loc, uint32_t* rec, uint32_t* treg, const uint32_t* __restrict__ tabs, Globals* g) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS_ALL];
+    CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
+    init_tables(smem, tabs + TAB_SCAN, NIB_SCAN * 128);
+    CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)(smem + SCAN_LDS + (threadIdx.x >> 6) * STG_BYTES);
     const int lane = threadIdx.x & 63;
-    const int f = find_file(tprefix, nfiles, t);
-    const DevFile F = files[f];
-    const uint32_t tt = t - F.first_tile;
-    const Chunk K = make_chunk(F, tt, lane);
-    const bool fof = tt == 0;
-    const LaneChain L0 = phase_a(K);
-    LaneChain L = L0;
-    // The tile's guess: the first lane's chain, resolved over the tile; if it
-    // does not pass through the entry of the first lane whose own chain another
-    // lane confirms (its exit is the start of the chain of the lane it lands
-    // in, or it ends at the file's end), that entry instead.
-    uint32_t G = NONE32, Gc = NONE32;
-    {
-        const bool isC = L.mode == LM_CHAIN;
-        const uint32_t tb = (uint32_t)((uint64_t)tt * CLY_TILE);
-        int m = -1;
-        if (isC && L.term == TERM_NONE && L.x >= tb && (uint64_t)(L.x - tb) < (uint64_t)CLY_TILE) m = (int)((L.x - tb) / CLY_CH);
-        const uint32_t Em = shfl_u32(L.E, m < 0 ? 0 : m);
-        const int mm = __shfl(L.mode, m < 0 ? 0 : m, 64);
-        const bool conf = isC && (L.term != TERM_NONE || (m > lane && mm == LM_CHAIN && Em == L.x));
-        const u64 bc = __ballot(conf), bm = __ballot(isC);
-        if (bc) Gc = shfl_u32(L.E, __ffsll((long long)bc) - 1);
-        if (bm) G = shfl_u32(L.E, __ffsll((long long)bm) - 1);
+    const CrcLane cl = crc_lane(lane);
+    const uint32_t K4 = k4_const(smem, cl.r4);
+    for (uint32_t t = blockIdx.x * SCAN_WAVES + (threadIdx.x >> 6); t < ntiles; t += gridDim.x * SCAN_WAVES) {
+        const int f = find_file(tprefix, nfiles, t);
+        const DevFile F = files[f];
+        tile_body<BM_SPEC>(F, t, t - F.first_tile, 0u, false, smem, stg, cl, K4, loc, rec, treg, nullptr, 0, 0, g);
     }
-    L = resolve(K, L, lane, fof ? 0u : G, false, g);
-    if (!fof && Gc != NONE32 && Gc != G) {
-        const int m = (int)((Gc - (uint32_t)((uint64_t)tt * CLY_TILE)) / CLY_CH);
-        const bool merged = __shfl(L.mode, m, 64) == LM_CHAIN && shfl_u32(L.E, m) == Gc;
-        if (!merged) { G = Gc; L = resolve(K, L0, lane, G, false, g); }
-    }
-    const uint64_t nl = (uint64_t)ntiles * 64;
-    lane_store(lanes, nl, (uint64_t)t * 64 + lane, L);
-    const bool ovf = store_positions(K, L, lane, pos + (uint64_t)t * POS_CAP, true);
-    local_store(&loc[t], L, G, fof, tt, F.len, lane, ovf);
 }
 
 // k_link: one workgroup per file: the chain state entering every tile.  A
@@ -1081,7 +935,7 @@ k_link(const DevFile* __restrict__ files, const TileLocal* __restrict__ loc, Til
             if (l0 & DF_NONE) bad = s.X < (uint32_t)l3;
             else bad = s.X != (uint32_t)l1;
         }
-        ti_store(&tin[F.first_tile + u], s, false);
+        ti_store(&tin[F.first_tile + u], s);
         if (bad) { atomicMin(&first_bad, F.first_tile + u); stop = true; return; }   // the state after it is not known
         s = rf_apply(rf_tile(l0, l1, l2), s);
     };
@@ -1125,38 +979,31 @@ k_fbase(int nfiles, const uint64_t* __restrict__ ftotal, FileInfo* finfo, Global
     if (threadIdx.x == 0) g->total = carry;
 }
 
-// k_refix: one wave per listed tile: its lanes re-resolved from the entering
-// state k_link gave it; new lane chains and LOCAL.  Walks on into the next
-// tile of the file while that one's LOCAL disagrees with the new exit (and no
-// other wave has it listed).
-__global__ void __launch_bounds__(64 * SPEC_WAVES)
-k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
-        TileLocal* loc, const TileIn* __restrict__ tin, uint32_t* lanes, uint16_t* pos,
+// k_refix: one wave per listed tile: the tile body again from the entering
+// state k_link gave it (new LOCAL, compact entries, register).  Walks on into
+// the next tile of the file while that one's LOCAL disagrees with the new exit.
+__global__ void __launch_bounds__(64 * SCAN_WAVES)
+k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, TileLocal* loc,
+        const TileIn* __restrict__ tin, uint32_t* rec, uint32_t* treg, const uint32_t* __restrict__ tabs,
         const uint32_t* __restrict__ fixlist, Globals* g, int round) {
-    const uint32_t k = blockIdx.x * SPEC_WAVES + (threadIdx.x >> 6);
+    if (g->nfix[round - 1] == 0) return;                   // (uniform: before the LDS setup's barrier)
+    __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS_ALL];
+    CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
+    init_tables(smem, tabs + TAB_SCAN, NIB_SCAN * 128);
+    CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)(smem + SCAN_LDS + (threadIdx.x >> 6) * STG_BYTES);
+    const uint32_t k = blockIdx.x * SCAN_WAVES + (threadIdx.x >> 6);
     if (k >= g->nfix[round - 1]) return;
     const int lane = threadIdx.x & 63;
+    const CrcLane cl = crc_lane(lane);
+    const uint32_t K4 = k4_const(smem, cl.r4);
     uint32_t t = fixlist[k];
     const int f = find_file(tprefix, nfiles, t);
     const DevFile F = files[f];
     LBState S = ti_load(&tin[t]);
-    const uint64_t nl = (uint64_t)ntiles * 64;
     for (;;) {
-        const uint32_t tt = t - F.first_tile;
-        const Chunk K = make_chunk(F, tt, lane);
-        LaneChain L = lane_load(lanes, nl, (uint64_t)t * 64 + lane);
-        L = resolve(K, L, lane, S.dead ? 0u : S.X, S.dead != 0, g);
-        lane_store(lanes, nl, (uint64_t)t * 64 + lane, L);
-        // (lanes loaded from the lane arrays carry no packed starts: all re-walked)
-        const bool ovf = store_positions(K, L, lane, pos + (uint64_t)t * POS_CAP, false);
-        local_store(&loc[t], L, NONE32, tt == 0, tt, F.len, lane, ovf);
-        // state after the tile
-        const u64 bc = __ballot(L.mode == LM_CHAIN);
-        if (bc) {
-            const int lc = 63 - __clzll((long long)bc);
-            S.X = shfl_u32(L.x, lc);
-            S.dead = __shfl(L.term, lc, 64) != TERM_NONE;
-        }
+        const TileRes r = tile_body<BM_EXACT>(F, t, t - F.first_tile, S.X, S.dead != 0, smem, stg, cl, K4, loc, rec,
+                                              treg, nullptr, 0, 0, g);
+        S.X = r.X; S.dead = r.dead;
         if (S.dead || t + 1 >= F.first_tile + F.ntile) break;
         // the next tile: consistent with the new exit?  else it is re-resolved too
         const u64 n0 = loc[t + 1].l[0], n1 = loc[t + 1].l[1], n3 = loc[t + 1].l[3];
@@ -1166,299 +1013,111 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
     }
 }
 
-// One record round of k_crc: record r = 64 k + lane of the tile (its start
-// from the tile's list), header decoded from its gather, tuple written, patch
-// added to pacc; cq chains the stored CRCs across lanes and rounds.
-__device__ __forceinline__ void round_finish(const Chunk& K, bool act, uint32_t P, const Gath& gt, uint64_t idx,
-                                             uint32_t TE, uint32_t fid, gtuples out, uint64_t out_cap,
-                                             const CLY_LDS uint8_t* smem, uint32_t K4, uint32_t last, uint32_t& prev,
-                                             uint32_t& pacc, Globals* g, int lane) {
-    uint32_t c = 0;
-    if (act) {
-        const Hdr h = hdr_at(K.base, P, K.len, gt);
-        put_tuple(out, idx, out_cap, K, P, h, fid, g);
-        c = h.crc;
-    }
-    const uint32_t up = shfl_u32(c, lane > 0 ? lane - 1 : 0);
-    const uint32_t cq = lane > 0 ? up : prev;
-    if (act) pacc ^= rec_patch(smem, TE, P, c, cq, K4);
-    prev = shfl_u32(c, (int)last);
-}
-// k_crc's tile body: the lane's raw CRC stream (128-B bursts) with the tile's
-// record rounds interleaved, one round after every RSTEP-th burst: the round's
-// header gathers are issued right after the burst's loads (so waiting for the
-// burst never waits for them) and used after the burst's CRC steps, which hide
-// their latency; all loads are issued unconditionally (a lane without a record
-// reads a zero block) so that the gathers' wait counts stay static.
-#define RSTEP (CLY_NB >= 4 ? CLY_NB / 4 : 1)
-#define NR_IN (CLY_NB / RSTEP)                     // rounds inside the burst loop
-__device__ __forceinline__ uint32_t tile_fused(const Chunk& K, const LaneChain& L, const LaneIn& I, const LBState& S,
-                                               bool active, uint32_t slim, const uint16_t* __restrict__ tp,
-                                               uint32_t n, uint32_t TE, uint32_t fid, gtuples out, uint64_t out_cap,
-                                               const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t K4,
-                                               uint32_t& pacc, gbytes zero32, Globals* g) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t nround = (n + 63) / 64;
-    uint32_t pr[NR_IN];
-    #pragma unroll
-    for (int k = 0; k < NR_IN; k++) {
-        const uint32_t r = 64u * k + lane;
-        pr[k] = tp[r < n ? r : 0];
-    }
-    uint32_t prev = S.crc_last;
-    uint32_t s = 0;
-    const CLY_GL u32x4* src = (const CLY_GL u32x4*)(K.base + K.cb);
-    Chunk Ks = K;
-    if ((uint64_t)slim < Ks.len) Ks.len = slim;
-    const bool full = (uint64_t)K.cb + CLY_CH <= Ks.len;
-    #pragma unroll
-    for (int b = 0; b < CLY_NB; b++) {
-        u32x4 v[CLY_BW / 4];
-        if (active && full) {
-            #pragma unroll
-            for (int k = 0; k < CLY_BW / 4; k++) v[k] = src[b * (CLY_BW / 4) + k];
-        } else if (active) {
-            #pragma unroll
-            for (int k = 0; k < CLY_BW / 4; k++) v[k] = piece(Ks, (uint32_t)(b * CLY_BW * 4 + 16 * k));
-        } else {
-            #pragma unroll
-            for (int k = 0; k < CLY_BW / 4; k++) v[k] = (u32x4){0u, 0u, 0u, 0u};
-        }
-        const int kr = b / RSTEP;
-        const bool rb = (b % RSTEP) == 0 && (uint32_t)kr < nround;
-        Gath gt;
-        uint32_t P = 0;
-        bool act = false;
-        if (rb) {
-            const uint32_t r = 64u * kr + lane;
-            act = r < n;
-            P = K.tb + pr[kr];
-            // every lane loads (a lane without a record, or too close to the file's
-            // end for a 32-B gather, reads the context's zero block)
-            gath_issue_at(act && gath_ok(P, K.len) ? K.base + (P & ~3u) : zero32, gt);
-        }
-        #pragma unroll
-        for (int k = 0; k < CLY_BW / 4; k++) {
-            s = crc_word(smem, s ^ v[k].x, cl);
-            s = crc_word(smem, s ^ v[k].y, cl);
-            s = crc_word(smem, s ^ v[k].z, cl);
-            s = crc_word(smem, s ^ v[k].w, cl);
-        }
-        if (rb) {
-            const uint32_t last = n - 64u * kr - 1 < 63u ? n - 64u * kr - 1 : 63u;
-            round_finish(K, act, P, gt, S.count + 64u * kr + lane, TE, fid, out, out_cap, smem, K4, last, prev, pacc,
-                         g, lane);
-        }
-    }
-    // rounds past the burst loop
-    for (uint32_t kr = NR_IN; kr < nround; kr++) {
-        const uint32_t r = 64u * kr + lane;
-        const bool act = r < n;
-        const uint32_t P = K.tb + tp[act ? r : 0];
-        Gath gt;
-        gath_issue_at(act && gath_ok(P, K.len) ? K.base + (P & ~3u) : zero32, gt);
-        const uint32_t last = n - 64u * kr - 1 < 63u ? n - 64u * kr - 1 : 63u;
-        round_finish(K, act, P, gt, S.count + r, TE, fid, out, out_cap, smem, K4, last, prev, pacc, g, lane);
-    }
-    (void)L; (void)I;
-    return s;
-}
-
-// k_crc's tile stream, coalesced.  The tile is read in blocks of COAL_BLK =
-// 4 KiB: in block m, load k (k < 4) of lane i + 16 q (i < 16, q < 4) reads the
-// 16 B at 4096 m + 1024 k + 64 i + 16 q, so that each load instruction reads
-// 1 KiB of consecutive bytes (whole cache lines); a 4 x 4 transpose of 16-B
-// elements over the lane quarters (v_permlane32_swap, v_permlane16_swap) then
-// leaves lane L with the 64 consecutive bytes at 4096 m + 64 L.  Lane L's
-// register runs over its 16 segments, stepped by A^(4096 - 64) between them
-// (Horner), so A^(4096 - 64 (L + 1)) R_L is its share of the tile's raw
-// register at the tile end; bytes at or past `slim` (the chain's terminal T,
-// or the file end) read as zero.  Block m+1's loads are issued before block
-// m's CRC steps.  The record rounds are interleaved as in tile_fused.
-#define COAL_NB ((int)(CLY_TILE / COAL_BLK))
-#define COAL_RSTEP (COAL_NB >= 4 ? COAL_NB / 4 : 1)
-#define COAL_NR (COAL_NB / COAL_RSTEP)
-
-static_assert(CLY_TILE % COAL_BLK == 0, "tiles of whole 4-KiB blocks");
-__device__ __forceinline__ void swap32(uint32_t& a, uint32_t& b) {
-    const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
-    a = r[0]; b = r[1];
-}
-__device__ __forceinline__ void swap16(uint32_t& a, uint32_t& b) {
-    const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
-    a = r[0]; b = r[1];
-}
-// e[k] of lane quarter q -> e[j] of quarter q = what quarter j held in e[q]
-__device__ __forceinline__ void quad_transpose(u32x4* e) {
-    #pragma unroll
-    for (int c = 0; c < 4; c++) {
-        uint32_t a0 = e[0][c], a1 = e[1][c], a2 = e[2][c], a3 = e[3][c];
-        swap32(a0, a2); swap32(a1, a3);
-        swap16(a0, a1); swap16(a2, a3);
-        e[0][c] = a0; e[1][c] = a1; e[2][c] = a2; e[3][c] = a3;
-    }
-}
-__device__ __forceinline__ uint32_t tile_coal(const Chunk& K, const LBState& S, uint32_t slim,
-                                              const uint16_t* __restrict__ tp, uint32_t n, uint32_t TE, uint32_t fid,
-                                              gtuples out, uint64_t out_cap, const CLY_LDS uint8_t* smem,
-                                              const CrcLane& cl, uint32_t K4, uint32_t& pacc, gbytes zero32,
-                                              Globals* g) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t nround = (n + 63) / 64;
-    uint32_t pr[COAL_NR];
-    #pragma unroll
-    for (int k = 0; k < COAL_NR; k++) {
-        const uint32_t r = 64u * k + lane;
-        pr[k] = tp[r < n ? r : 0];
-    }
-    uint32_t prev = S.crc_last;
-    Chunk Kt = K;                                    // the tile as one chunk: piece() offsets are tile-relative
-    Kt.cb = K.tb;
-    if ((uint64_t)slim < Kt.len) Kt.len = slim;
-    const bool full = (uint64_t)K.tb + CLY_TILE <= Kt.len;
-    const uint32_t lo = 64u * (uint32_t)(lane & 15) + 16u * (uint32_t)(lane >> 4);
-    const CLY_GL u32x4* src = (const CLY_GL u32x4*)(K.base + K.tb + lo);
-    const CLY_LDS uint32_t* tblk = (const CLY_LDS uint32_t*)(smem + LDS_SH) + (NSH - 1) * 128;
-    uint32_t R = 0;
-    u32x4 eb[2][4];
-    auto blk_load = [&](u32x4* e, int m) {
-        if (full) {
-            #pragma unroll
-            for (int k = 0; k < 4; k++) e[k] = src[(COAL_BLK * m + 1024 * k) / 16];
-        } else {
-            #pragma unroll
-            for (int k = 0; k < 4; k++) e[k] = piece(Kt, (uint32_t)(COAL_BLK * m + 1024 * k) + lo);
-        }
-    };
-    blk_load(eb[0], 0);
-    #pragma unroll
-    for (int m = 0; m < COAL_NB; m++) {
-        u32x4* e = eb[m & 1];
-        const int kr = m / COAL_RSTEP;
-        const bool rb = (m % COAL_RSTEP) == 0 && (uint32_t)kr < nround;
-        Gath gt;
-        uint32_t P = 0;
-        bool act = false;
-        if (rb) {
-            const uint32_t r = 64u * kr + lane;
-            act = r < n;
-            P = K.tb + pr[kr];
-            gath_issue_at(act && gath_ok(P, K.len) ? K.base + (P & ~3u) : zero32, gt);
-        }
-        if (m + 1 < COAL_NB) blk_load(eb[(m + 1) & 1], m + 1);
-        quad_transpose(e);
-        if (m) R = mat_mul(tblk, R);
-        #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            R = crc_word(smem, R ^ e[k].x, cl);
-            R = crc_word(smem, R ^ e[k].y, cl);
-            R = crc_word(smem, R ^ e[k].z, cl);
-            R = crc_word(smem, R ^ e[k].w, cl);
-        }
-        if (rb) {
-            const uint32_t last = n - 64u * kr - 1 < 63u ? n - 64u * kr - 1 : 63u;
-            round_finish(K, act, P, gt, S.count + 64u * kr + lane, TE, fid, out, out_cap, smem, K4, last, prev, pacc,
-                         g, lane);
-        }
-    }
-    for (uint32_t kr = COAL_NR; kr < nround; kr++) {
-        const uint32_t r = 64u * kr + lane;
-        const bool act = r < n;
-        const uint32_t P = K.tb + tp[act ? r : 0];
-        Gath gt;
-        gath_issue_at(act && gath_ok(P, K.len) ? K.base + (P & ~3u) : zero32, gt);
-        const uint32_t last = n - 64u * kr - 1 < 63u ? n - 64u * kr - 1 : 63u;
-        round_finish(K, act, P, gt, S.count + r, TE, fid, out, out_cap, smem, K4, last, prev, pacc, g, lane);
-    }
-    return shift_bytes(smem, COAL_BLK - 64u * (uint32_t)(lane + 1), R);
-}
-
-// k_crc: the CRC stream and the tuples, tiles in grid-stride order.
-#define CRC_WAVES 16
-__global__ void __launch_bounds__(64 * CRC_WAVES)
-k_crc(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
-      const TileIn* __restrict__ tin, const TileLocal* __restrict__ loc, const uint32_t* __restrict__ lanes,
-      const uint16_t* __restrict__ pos, uint32_t* treg, FileInfo* finfo, const uint32_t* __restrict__ tabs,
-      cly_tuple* out_, uint64_t out_cap, Globals* g, int round, const uint8_t* __restrict__ zero32) {
+// k_emit: per tile (one wave, grid-stride), after the chain is final: the
+// tuples from the compact entries (64 per round: coalesced 16-B reads, the 48-B
+// tuples assembled in the wave's LDS stage and written as whole 1-KiB runs),
+// the first-boundary patch term, and the file's terminal.
+#define EMIT_WAVES 16
+#define EMIT_LDS (NIB_SH * 128 * 4 + EMIT_WAVES * STG_BYTES)
+__global__ void __launch_bounds__(64 * EMIT_WAVES)
+k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
+       const TileIn* __restrict__ tin, const TileLocal* __restrict__ loc, const uint32_t* __restrict__ rec,
+       uint32_t* treg, FileInfo* finfo, const uint32_t* __restrict__ tabs, cly_tuple* out_, uint64_t out_cap,
+       Globals* g, int round) {
     if (g->nfix[round]) return;             // the chain is not final yet (k_refix first)
     gtuples out = (gtuples)out_;
-    __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS];
-    CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
-    init_tables(smem, tabs);
+    __shared__ __attribute__((aligned(16))) unsigned char smem_raw[EMIT_LDS];
+    CLY_LDS uint32_t* sht = (CLY_LDS uint32_t*)smem_raw;
+    for (int i = threadIdx.x; i < NIB_SH * 128; i += blockDim.x) sht[i] = tabs[TAB_SH + i];
+    __syncthreads();
+    CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)(smem_raw + NIB_SH * 128 * 4 + (threadIdx.x >> 6) * STG_BYTES);
+    CLY_LDS u32x4* sv = (CLY_LDS u32x4*)stg;
     const int lane = threadIdx.x & 63;
     const CrcLane cl = crc_lane(lane);
-    uint32_t K4 = 0xFFFFFFFFu;              // A^-4 0xFFFFFFFF
-    for (int k = 0; k < 4; k++) K4 = crc_unbyte(smem, K4, cl.r4);
-    const uint64_t nl = (uint64_t)ntiles * 64;
-    for (uint32_t t = blockIdx.x * CRC_WAVES + (threadIdx.x >> 6); t < ntiles; t += gridDim.x * CRC_WAVES) {
+    for (uint32_t t = blockIdx.x * EMIT_WAVES + (threadIdx.x >> 6); t < ntiles; t += gridDim.x * EMIT_WAVES) {
         const int f = find_file(tprefix, nfiles, t);
         const DevFile F = files[f];
         LBState S = ti_load(&tin[t]);
-        if (S.dead) { if (lane == 0) treg[t] = 0; continue; }
-        S.count += finfo[f].first_index;
-        const uint32_t tt = t - F.first_tile;
-        const Chunk K = make_chunk(F, tt, lane);
-        const LaneChain L = lane_load(lanes, nl, (uint64_t)t * 64 + lane);
-        const bool ovf = (loc[t].l[0] & DF_OVF) != 0;
-        uint32_t tile_cnt;
-        const LaneIn I = lane_inputs(K, L, S, lane, tile_cnt);
-        const bool term_lane = L.mode == LM_CHAIN && L.term != TERM_NONE;
-        const bool live = L.mode == LM_CHAIN || L.mode == LM_NONE;
-        const uint32_t TE = K.tb + (uint32_t)CLY_TILE;
-        uint32_t pacc = 0;
-        if (term_lane) {
-            // the chain's terminal T: the last record is checked there (XOR ~its CRC
-            // into the register before byte T; none when no record precedes T), and
-            // the stream stops at T (the bytes from T on are zeroed)
-            const uint32_t cT = L.cnt ? L.last_crc : I.crc_in;
-            if (L.cnt || I.P_in != NONE32) pacc = shift_bytes(smem, TE - L.x, ~cT);
+        if (S.dead) continue;
+        FileInfo* fo = &finfo[f];
+        const uint64_t gb = S.count + fo->first_index;
+        const u64 l0 = loc[t].l[0], l1 = loc[t].l[1], l3 = loc[t].l[3];
+        const uint32_t tt = t - F.first_tile, tb = (uint32_t)((uint64_t)tt * CLY_TILE);
+        const uint32_t n = (uint32_t)(l0 >> 32);
+        const gbytes base = (gbytes)F.base;
+        if (!(l0 & DF_OVF)) {
+            const uint32_t* trec = rec + (uint64_t)t * CAP_T * 4;
+            for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+                const uint32_t i = i0 + lane;
+                if (i < n) {
+                    const u32x4 v = *(const u32x4*)(trec + 4 * i);
+                    const uint32_t rel = v.w & 0xFFFFu, p = tb + rel;
+                    u32x4 a, b, c;
+                    if (v.w & REC_SHORT) {
+                        const uint32_t ks = v.y & 0xFFFFFFu, hsz = 6u + ((v.y >> 24) & 31u), type = v.y >> 29;
+                        const uint32_t dt = (v.w >> 16) & 7u, key0 = (v.w >> 19) & 0x7Fu;
+                        const uint64_t tx = (uint64_t)((int64_t)(key0 >> 1) ^ -(int64_t)(key0 & 1u));
+                        a = (u32x4){p, 0u, 0u, 0u};
+                        b = (u32x4){(uint32_t)tx, (uint32_t)(tx >> 32), F.fid, hsz + ks + v.z};
+                        c = (u32x4){ks, v.z, type | (dt << 8) | (hsz << 16) | (1u << 24), v.x};
+                    } else {
+                        const Hdr h = hdr_load(base, p, F.len);
+                        tuple_words(base, p, h, F.fid, a, b, c);
+                    }
+                    sv[3 * lane] = a; sv[3 * lane + 1] = b; sv[3 * lane + 2] = c;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                // the round's tuples are 48 (n - i0) contiguous bytes: 16-B pieces q = lane + 64 k
+                const uint32_t nr = n - i0 < 64 ? n - i0 : 64;
+                CLY_GL u32x4* dst = (CLY_GL u32x4*)(out + gb + i0);
+                #pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const uint32_t q = (uint32_t)lane + 64u * k;
+                    if (q < 3 * nr) {
+                        if (gb + i0 + q / 3 < out_cap) dst[q] = sv[q];
+                        else atomicOr(&g->overflow, 1u);
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        } else {
+            // more records than the compact list holds: the body again, tuples direct
+            tile_body<BM_EMIT>(F, t, tt, S.X, false, (const CLY_LDS uint8_t*)smem_raw, stg, cl, 0u, nullptr, nullptr,
+                               nullptr, out, out_cap, gb, g);
         }
-        uint32_t r;
-        if (!ovf) {
-            // the tile's stream stops at the chain's terminal (if in this tile)
-            const uint64_t tm = __ballot(term_lane);
-            const uint32_t slim = tm ? (uint32_t)__shfl((int)L.x, __builtin_ctzll(tm), 64) : 0xFFFFFFFFu;
-            r = tile_coal(K, S, slim, pos + (uint64_t)t * POS_CAP, tile_cnt, TE, F.fid, out, out_cap, smem, cl, K4,
-                          pacc, (gbytes)zero32, g);
-        } else r = phase_c_fast(K, L, I, live, true, term_lane ? L.x : 0xFFFFFFFFu, F.fid, out, out_cap, smem, cl, K4,
-                                pacc, g);
-        if (term_lane) {
-            FileInfo* fo = &finfo[f];
-            fo->term_pos = L.x; fo->term_status = L.term; fo->term_tile = t; fo->term_lane = (uint32_t)lane;
-            fo->end_index = I.base + L.cnt; fo->has_term = 1; fo->expect = 0;
+        if (lane == 0) {
+            const uint32_t G = (uint32_t)l1;
+            if (tt > 0 && !(l0 & DF_NONE)) treg[t] ^= shift_bytes(sht, tb + (uint32_t)CLY_TILE - G, S.crc_last);
+            if (l0 & DF_TERM) {
+                fo->term_pos = (uint32_t)(l1 >> 32);
+                fo->term_status = (int32_t)(int8_t)(uint8_t)(l3 >> 32);
+                fo->term_tile = t;
+                fo->end_index = gb + n;
+                fo->has_term = 1;
+            }
         }
-        if (!ovf) r = wave_xor(r ^ pacc);               // lane shares already shifted to the tile end
-        else {
-            if (!live) r = 0;
-            r = tile_fold(smem, r, lane) ^ wave_xor(pacc);
-        }
-        if (lane == 0) treg[t] = r;
     }
 }
 
-
 // ---------------------------------------------------------------------------
 // k_fin: per file, the fold of its tile registers up to the terminal's tile
-// must equal A^(CLY_CH (63 - terminal lane)) expect.
-__device__ __forceinline__ uint32_t xpow_mul(const uint32_t* __restrict__ pw, uint64_t m, uint32_t v) {
-    for (int k = 0; m; k++, m >>= 1) if (m & 1) v = cly_multmodp(pw[k], v);
-    return v;
-}
+// (sum over tiles t of A^(CLY_TILE (T - t)) treg[t]) must be zero.
 #define FIN_NT 256
 __global__ void __launch_bounds__(FIN_NT)
 k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __restrict__ treg,
-      const uint32_t* __restrict__ nib, const uint32_t* __restrict__ pw, Globals* g, int round) {
-    __shared__ uint32_t tab[NIB_LEVELS * 128];
+      const uint32_t* __restrict__ tabs, const uint32_t* __restrict__ pw, Globals* g, int round) {
+    __shared__ uint32_t tab[128];
     __shared__ uint32_t part[FIN_NT];
     __shared__ uint32_t plen[FIN_NT];
-    if (g->nfix[round]) return;             // k_crc did not run (link repair first)
-    for (int i = threadIdx.x; i < NIB_LEVELS * 128; i += FIN_NT) tab[i] = nib[i];
+    if (g->nfix[round]) return;             // k_emit did not run (link repair first)
+    for (int i = threadIdx.x; i < 128; i += FIN_NT) tab[i] = tabs[TAB_TILE + i];
     __syncthreads();
     const int f = blockIdx.x;
     const DevFile F = files[f];
     FileInfo* fo = &finfo[f];
-    const uint32_t has = fo->has_term;
-    if (!has) {
+    if (!fo->has_term) {
         if (threadIdx.x == 0) { atomicOr(&g->fail, 32u); fo->ok = 0; }
         return;
     }
@@ -1469,7 +1128,7 @@ k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __rest
     for (uint32_t i = lo; i < hi; i++) {
         uint32_t p = 0;
         #pragma unroll
-        for (int k = 0; k < 8; k++) p ^= tab[6 * 128 + k * 16 + ((s >> (4 * k)) & 15u)];
+        for (int k = 0; k < 8; k++) p ^= tab[k * 16 + ((s >> (4 * k)) & 15u)];
         s = p ^ treg[F.first_tile + i];
     }
     part[threadIdx.x] = s;
@@ -1477,84 +1136,50 @@ k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __rest
     __syncthreads();
     for (int d = 1; d < FIN_NT; d <<= 1) {
         if ((threadIdx.x & (2 * d - 1)) == 0) {
-            part[threadIdx.x] = xpow_mul(pw, plen[threadIdx.x + d], part[threadIdx.x]) ^ part[threadIdx.x + d];
+            uint32_t v = part[threadIdx.x];
+            for (uint32_t m = plen[threadIdx.x + d], k = 0; m; k++, m >>= 1) if (m & 1) v = cly_multmodp(pw[k], v);
+            part[threadIdx.x] = v ^ part[threadIdx.x + d];
             plen[threadIdx.x] += plen[threadIdx.x + d];
         }
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        // A^(CLY_CH (63 - lane)) expect
-        uint32_t e = fo->expect;
-        const uint32_t m = 63 - fo->term_lane;
-        for (int lvl = 0; lvl < 6; lvl++) {
-            if (m & (1u << lvl)) {
-                uint32_t p = 0;
-                for (int k = 0; k < 8; k++) p ^= tab[lvl * 128 + k * 16 + ((e >> (4 * k)) & 15u)];
-                e = p;
-            }
-        }
         fo->fold = part[0];
-        fo->ok = part[0] == e;
+        fo->ok = part[0] == 0;
         fo->fail_key = ~0ull;
-        if (part[0] != e) atomicOr(&g->any_fail, 1u);
+        if (part[0] != 0) atomicOr(&g->any_fail, 1u);
     }
 }
 
 // ---------------------------------------------------------------------------
-// ---------------------------------------------------------------------------
-// k_locate (only after a failed fold): every tile of a failing file up to its
-// terminal takes its final lane chains, the register entering each chunk, and
-// walks its records' checks from there; the first failing record of the file
-// wins (atomicMin on offset << 32 | index).
-__global__ void __launch_bounds__(512, 2)
-k_locate(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
-         const TileIn* __restrict__ tin, const uint32_t* __restrict__ lanes, const uint32_t* __restrict__ treg,
-         FileInfo* finfo, const uint32_t* __restrict__ tabs, Globals* g) {
+// k_locate (only after a failed fold): every tuple of a failing file gets its
+// CRC-32 computed alone (one lane per record, table steps from LDS) and
+// compared with the stored one; the first failing record of the file wins
+// (atomicMin on offset << 32 | index in file).
+__global__ void __launch_bounds__(1024)
+k_locate(const DevFile* __restrict__ files, int nfiles, FileInfo* finfo, const cly_tuple* __restrict__ tup,
+         uint64_t total, uint64_t out_cap, const uint32_t* __restrict__ tabs) {
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
-    init_tables(smem, tabs);
-    const int lane = threadIdx.x & 63;
-    const CrcLane cl = crc_lane(lane);
-    const uint64_t nl = (uint64_t)ntiles * 64;
-    for (uint32_t t = blockIdx.x * 8 + (threadIdx.x >> 6); t < ntiles; t += gridDim.x * 8) {
-        const int f = find_file(tprefix, nfiles, t);
-        const DevFile F = files[f];
-        FileInfo* fo = &finfo[f];
-        if (fo->ok || t > fo->term_tile) continue;
-        LBState S = ti_load(&tin[t]);
-        if (S.dead) continue;
-        S.count += fo->first_index;
-        const uint32_t tt = t - F.first_tile;
-        const Chunk K = make_chunk(F, tt, lane);
-        const LaneChain L = lane_load(lanes, nl, (uint64_t)t * 64 + lane);
-        uint32_t tile_cnt;
-        LaneIn I = lane_inputs(K, L, S, lane, tile_cnt);
-        if (lane == 0) I.spill = false;     // a record of the previous tile: in treg[t - 1] (rec_patch)
-        // register entering the tile
-        uint32_t st = 0;
-        for (uint32_t i = F.first_tile; i < t; i++) st = nib_mul(smem, 6, st) ^ treg[i];
-        const bool live = L.mode == LM_CHAIN || L.mode == LM_NONE;
-        uint32_t fp, ex;
-        uint64_t fi;
-        uint32_t r = live ? exact_lane(K, L, I, 0u, false, false, F.fid, nullptr, 0, smem, cl, g, fp, fi, ex) : 0u;
-        // exclusive fold over the lanes, plus A^(CLY_CH l) st
-        uint32_t v = r;
-        #pragma unroll
-        for (int lvl = 0; lvl < 6; lvl++) {
-            const int d = 1 << lvl;
-            const uint32_t u = (uint32_t)__shfl_up((int)v, d, 64);
-            const uint32_t sh = nib_mul(smem, lvl, u);
-            if (lane >= d) v ^= sh;
+    init_tables(smem, tabs + TAB_SCAN, 0);
+    const CrcLane cl = crc_lane(threadIdx.x & 63);
+    const uint64_t lim = total < out_cap ? total : out_cap;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += (uint64_t)gridDim.x * blockDim.x) {
+        int lo = 0, hi = nfiles - 1;                       // the last file whose first index is <= i
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (finfo[mid].first_index <= i) lo = mid; else hi = mid - 1;
         }
-        uint32_t sin = (uint32_t)__shfl_up((int)v, 1, 64);
-        if (lane == 0) sin = 0;
-        uint32_t se = st;
-        for (int lvl = 0; lvl < 6; lvl++) if (lane & (1 << lvl)) se = nib_mul(smem, lvl, se);
-        sin ^= se;
-        if (live) {
-            exact_lane(K, L, I, sin, false, true, F.fid, nullptr, 0, smem, cl, g, fp, fi, ex);
-            if (fp != NONE32) atomicMin(&fo->fail_key, ((u64)fp << 32) | (u64)(fi - fo->first_index));
-        }
+        FileInfo* fo = &finfo[lo];
+        if (fo->ok || i >= fo->end_index || i < fo->first_index) continue;
+        const cly_tuple T = tup[i];
+        const gbytes base = (gbytes)files[lo].base;
+        uint64_t a = (uint64_t)T.offset + 4, b = (uint64_t)T.offset + T.size;
+        uint32_t s = 0xFFFFFFFFu;
+        for (; a < b && (a & 3); a++) s = crc_byte(smem, s, base[a], cl.r4);
+        for (; a + 4 <= b; a += 4) s = crc_word(smem, s ^ *(const CLY_GL uint32_t*)(base + a), cl);
+        for (; a < b; a++) s = crc_byte(smem, s, base[a], cl.r4);
+        if (~s != T.crc) atomicMin(&fo->fail_key, ((u64)(uint64_t)T.offset << 32) | (u64)(i - fo->first_index));
     }
 }
 
@@ -1569,18 +1194,19 @@ struct cly_ctx {
     hipEvent_t ev[8];
     DevFile* d_files; uint32_t* d_tprefix; FileInfo* d_finfo; uint64_t* d_ftotal; int cap_files;
     DevFile* h_files; uint32_t* h_tprefix; FileInfo* h_finfo;
-    TileLocal* d_loc; TileIn* d_tin; uint32_t* d_treg; uint32_t* d_fix; uint32_t* d_lanes; uint16_t* d_pos;
+    TileLocal* d_loc; TileIn* d_tin; uint32_t* d_treg; uint32_t* d_fix; uint32_t* d_rec;
     int64_t cap_tiles;
     Globals* d_g; Globals* h_g;
-    uint32_t* d_tabs;            // nibble tables: A^(CLY_CH 2^k), k < NIB_LEVELS; A^(4 m), m < 16; A^(64 m)
+    uint32_t* d_tabs;            // nibble tables (TAB_SCAN, TAB_SH, TAB_TILE)
     uint32_t* d_pw;              // x^(8 CLY_TILE 2^k) mod P, k < 40
-    uint8_t* d_zero;             // CLY_CH (>= 256) zero bytes: streams and gathers of lanes without data
-    int crc_grid, loc_grid;
-    float kms[6];                // last call: k_spec, link rounds (k_link/k_fbase/k_refix), k_crc, k_fin, k_locate, all
+    int scan_grid, emit_grid, loc_grid;
+    float kms[6];                // last call: k_scan, link rounds (k_link/k_fbase/k_refix), k_emit, k_fin, k_locate, all
     uint8_t* d_bytes; uint64_t cap_bytes;          // host-path staging
     cly_tuple* d_tuples; uint64_t cap_tuples;
     void* merge_scratch;         // clymerge.hip's buffers (grow-only)
     int64_t now_ns;              // loadIndex's time.Now() for the TTL sweep (0: the wall clock per call)
+    int dbg;                     // cly_dbg_set: bit 0 = keep k_scan's LOCALs (before any repair) in d_dbg
+    TileLocal* d_dbg; int64_t cap_dbg;
 };
 extern "C" void cly_merge_scratch_free(void* p);
 
@@ -1597,21 +1223,20 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     for (int i = 0; i < 8; i++) HIPCK(hipEventCreate(&c->ev[i]));
     HIPCK(hipMalloc(&c->d_g, sizeof(Globals)));
     HIPCK(hipHostMalloc(&c->h_g, sizeof(Globals), hipHostMallocDefault));
-    HIPCK(hipMalloc(&c->d_zero, CLY_CH < 256 ? 256 : CLY_CH));
-    HIPCK(hipMemset(c->d_zero, 0, CLY_CH < 256 ? 256 : CLY_CH));
     {
-        static uint32_t hn[NTAB];
-        for (int lvl = 0; lvl < NIB_LEVELS + NSH; lvl++) {
+        static uint32_t hn[NTAB_ALL];
+        for (int k = 0; k < NIB_SCAN + NIB_SH + 1; k++) {
             uint64_t nbytes;
-            if (lvl < NIB_LEVELS) nbytes = (uint64_t)CLY_CH << lvl;                  // A^(CLY_CH 2^lvl)
-            else if (lvl < NIB_LEVELS + 64) {                                        // A^(v 16^d)
-                const int k = lvl - NIB_LEVELS;
-                nbytes = (uint64_t)(k & 15) << (4 * (k >> 4));
-            } else if (lvl == NIB_LEVELS + 64) nbytes = 65536;                      // A^65536
-            else nbytes = COAL_BLK - 64;                                             // k_crc's block step
+            if (k < 6) nbytes = (uint64_t)CLY_SEG << k;                              // A^(64 2^k)
+            else if (k == 6) nbytes = CLY_BLK - CLY_SEG;                             // the block step
+            else if (k < NIB_SCAN + 64) {                                            // A^(v 16^d)
+                const int s = k - NIB_SCAN;
+                nbytes = (uint64_t)(s & 15) << (4 * (s >> 4));
+            } else if (k == NIB_SCAN + 64) nbytes = 65536;                          // A^65536
+            else nbytes = (uint64_t)CLY_TILE;                                        // k_fin's tile step
             const uint32_t xm = cly_x8n(nbytes);
             for (int nb = 0; nb < 8; nb++)
-                for (uint32_t v = 0; v < 16; v++) hn[lvl * 128 + nb * 16 + v] = cly_multmodp(xm, v << (4 * nb));
+                for (uint32_t v = 0; v < 16; v++) hn[k * 128 + nb * 16 + v] = cly_multmodp(xm, v << (4 * nb));
         }
         HIPCK(hipMalloc(&c->d_tabs, sizeof(hn)));
         HIPCK(hipMemcpy(c->d_tabs, hn, sizeof(hn), hipMemcpyHostToDevice));
@@ -1625,10 +1250,14 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
         int ncu = 0;
         HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
         int per_cu = 0;
-        HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_crc, 64 * CRC_WAVES, 0));
+        HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_scan, 64 * SCAN_WAVES, 0));
         if (per_cu < 1) per_cu = 1;
-        c->crc_grid = per_cu * ncu;
-        c->loc_grid = ncu * 2;
+        c->scan_grid = per_cu * ncu;
+        per_cu = 0;
+        HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_emit, 64 * EMIT_WAVES, 0));
+        if (per_cu < 1) per_cu = 1;
+        c->emit_grid = per_cu * ncu;
+        c->loc_grid = ncu;
     }
     *out = c;
     return CLY_OK;
@@ -1639,8 +1268,8 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     hipFree(c->d_files); hipFree(c->d_tprefix); hipFree(c->d_finfo); hipFree(c->d_ftotal);
-    hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_lanes);
-    hipFree(c->d_pos); hipFree(c->d_g); hipFree(c->d_zero); hipFree(c->d_tabs); hipFree(c->d_pw); hipFree(c->d_bytes); hipFree(c->d_tuples);
+    hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_rec);
+    hipFree(c->d_g); hipFree(c->d_tabs); hipFree(c->d_pw); hipFree(c->d_bytes); hipFree(c->d_tuples); hipFree(c->d_dbg);
     hipHostFree(c->h_files); hipHostFree(c->h_tprefix); hipHostFree(c->h_finfo); hipHostFree(c->h_g);
     cly_merge_scratch_free(c->merge_scratch);
     for (int i = 0; i < 8; i++) hipEventDestroy(c->ev[i]);
@@ -1675,20 +1304,21 @@ static int ensure_files(cly_ctx* c, int nfiles) {
 
 static int ensure_tiles(cly_ctx* c, int64_t ntiles) {
     if (ntiles <= c->cap_tiles) return CLY_OK;
-    hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_lanes); hipFree(c->d_pos);
-    c->d_loc = nullptr; c->d_tin = nullptr; c->d_treg = nullptr; c->d_fix = nullptr; c->d_lanes = nullptr;
-    c->d_pos = nullptr;
+    hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_rec);
+    c->d_loc = nullptr; c->d_tin = nullptr; c->d_treg = nullptr; c->d_fix = nullptr; c->d_rec = nullptr;
     c->cap_tiles = 0;
     const int64_t cap = ntiles < 1024 ? 1024 : ntiles;
     HIPCK(hipMalloc(&c->d_loc, sizeof(TileLocal) * cap));
     HIPCK(hipMalloc(&c->d_tin, sizeof(TileIn) * cap));
     HIPCK(hipMalloc(&c->d_treg, sizeof(uint32_t) * cap));
     HIPCK(hipMalloc(&c->d_fix, sizeof(uint32_t) * cap));
-    HIPCK(hipMalloc(&c->d_lanes, sizeof(uint32_t) * LANE_WORDS * 64 * cap));
-    HIPCK(hipMalloc(&c->d_pos, sizeof(uint16_t) * POS_CAP * cap));
+    HIPCK(hipMalloc(&c->d_rec, sizeof(uint32_t) * 4 * (uint64_t)CAP_T * cap));
     c->cap_tiles = cap;
     return CLY_OK;
 }
+
+// the largest file length the tile arithmetic (u32 offsets) takes
+#define MAX_FILE_LEN (0xFFFFFFFFull - 2 * (uint64_t)CLY_TILE)
 
 extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple* d_out, uint64_t out_cap,
                                uint64_t* file_first, cly_file_result* res, uint64_t* needed, cly_stats* stats,
@@ -1702,7 +1332,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     int64_t ntiles = 0;
     uint64_t bytes = 0;
     for (int i = 0; i < nfiles; i++) {
-        if (files[i].len >= 0xFFFFFFFFull) return CLY_ERR_ARG;
+        if (files[i].len > MAX_FILE_LEN) return CLY_ERR_ARG;
         if (files[i].len && (((uintptr_t)files[i].base) & 15)) return CLY_ERR_ARG;
         const uint64_t nt = files[i].len ? (files[i].len + CLY_TILE - 1) / CLY_TILE : 1;
         c->h_files[i].base = files[i].base;
@@ -1724,35 +1354,43 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     HIPCK(hipMemsetAsync(c->d_finfo, 0, sizeof(FileInfo) * nfiles, st));
     HIPCK(hipMemsetAsync(c->d_g, 0, sizeof(Globals), st));
     const uint32_t nt32 = (uint32_t)ntiles;
-    const int spec_grid = (int)((ntiles + SPEC_WAVES - 1) / SPEC_WAVES);
+    int grid = c->scan_grid;
+    if ((int64_t)grid * SCAN_WAVES > ntiles) grid = (int)((ntiles + SCAN_WAVES - 1) / SCAN_WAVES);
     HIPCK(hipEventRecord(c->ev[0], st));
-    hipLaunchKernelGGL(k_spec, dim3(spec_grid), dim3(64 * SPEC_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
-                       c->d_loc, c->d_lanes, c->d_pos, c->d_g);
+    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * SCAN_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
+                       c->d_loc, c->d_rec, c->d_treg, c->d_tabs, c->d_g);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[1], st));
+    if (c->dbg & 1) {
+        if (c->cap_dbg < ntiles) {
+            hipFree(c->d_dbg); c->d_dbg = nullptr; c->cap_dbg = 0;
+            HIPCK(hipMalloc(&c->d_dbg, sizeof(TileLocal) * ntiles));
+            c->cap_dbg = ntiles;
+        }
+        HIPCK(hipMemcpyAsync(c->d_dbg, c->d_loc, sizeof(TileLocal) * ntiles, hipMemcpyDeviceToDevice, st));
+    }
     // LINK_ROUNDS link rounds (round r > 0: k_refix of round r-1's listed tiles,
-    // then k_link; both return at once when round r-1 listed none), then the
-    // CRC kernels, which return at once if the last round still listed tiles;
+    // then k_link; both return at once when round r-1 listed none), then
+    // k_emit/k_fin, which return at once if the last round still listed tiles;
     // no host wait in between.  Files that need more rounds continue on a host
     // loop (one wait per round).
     const int RL = LINK_ROUNDS - 1;
-    const int fix_grid = (nfiles + SPEC_WAVES - 1) / SPEC_WAVES;   // at most one listed tile per file and round
+    const int fix_grid = (nfiles + SCAN_WAVES - 1) / SCAN_WAVES;   // at most one listed tile per file and round
     for (int r = 0; r < LINK_ROUNDS; r++) {
         if (r > 0)
-            hipLaunchKernelGGL(k_refix, dim3(fix_grid), dim3(64 * SPEC_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
-                               c->d_loc, c->d_tin, c->d_lanes, c->d_pos, c->d_fix, c->d_g, r);
+            hipLaunchKernelGGL(k_refix, dim3(fix_grid), dim3(64 * SCAN_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix,
+                               c->d_loc, c->d_tin, c->d_rec, c->d_treg, c->d_tabs, c->d_fix, c->d_g, r);
         hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, c->d_loc, c->d_tin, c->d_ftotal,
                            c->d_fix, c->d_g, r);
         hipLaunchKernelGGL(k_fbase, dim3(1), dim3(FB_NT), 0, st, nfiles, c->d_ftotal, c->d_finfo, c->d_g, r);
     }
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[2], st));
-    auto launch_crc = [&]() -> int {
-        int grid = c->crc_grid;
-        if ((int64_t)grid * CRC_WAVES > ntiles) grid = (int)((ntiles + CRC_WAVES - 1) / CRC_WAVES);
-        hipLaunchKernelGGL(k_crc, dim3(grid), dim3(64 * CRC_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
-                           c->d_tin, c->d_loc, c->d_lanes, c->d_pos, c->d_treg, c->d_finfo, c->d_tabs, d_out, out_cap,
-                           c->d_g, RL, c->d_zero);
+    auto launch_emit = [&]() -> int {
+        int eg = c->emit_grid;
+        if ((int64_t)eg * EMIT_WAVES > ntiles) eg = (int)((ntiles + EMIT_WAVES - 1) / EMIT_WAVES);
+        hipLaunchKernelGGL(k_emit, dim3(eg), dim3(64 * EMIT_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
+                           c->d_tin, c->d_loc, c->d_rec, c->d_treg, c->d_finfo, c->d_tabs, d_out, out_cap, c->d_g, RL);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[3], st));
         hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_finfo, c->d_treg, c->d_tabs,
@@ -1763,8 +1401,17 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         HIPCK(hipStreamSynchronize(st));
         return CLY_OK;
     };
-    int rc2 = launch_crc();
+    int rc2 = launch_emit();
     if (rc2) return rc2;
+    if (CLY_EXP) {                           // timing experiments: the kernel times only
+        float a = 0, b = 0, e2 = 0, f2 = 0;
+        HIPCK(hipEventElapsedTime(&a, c->ev[0], c->ev[1])); HIPCK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+        HIPCK(hipEventElapsedTime(&e2, c->ev[2], c->ev[3])); HIPCK(hipEventElapsedTime(&f2, c->ev[3], c->ev[4]));
+        c->kms[0] = a; c->kms[1] = b; c->kms[2] = e2; c->kms[3] = f2; c->kms[4] = 0; c->kms[5] = a + b + e2 + f2;
+        for (int i = 0; i < nfiles; i++) { file_first[i] = 0; res[i].n_records = 0; res[i].end_offset = 0; res[i].status = 0; }
+        if (needed) *needed = 0;
+        return CLY_OK;
+    }
     float ms_fix = 0;
     uint32_t rounds = 1, refixed = 0;
     for (int r = 0; r < LINK_ROUNDS; r++) if (c->h_g->nfix[r]) { rounds++; refixed += c->h_g->nfix[r]; }
@@ -1779,8 +1426,8 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
             refixed += nfix;
             HIPCK(hipMemcpyAsync(&c->d_g->nfix[RL - 1], &c->d_g->nfix[RL], sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
             HIPCK(hipMemsetAsync(&c->d_g->nfix[RL], 0, sizeof(uint32_t), st));
-            hipLaunchKernelGGL(k_refix, dim3(fix_grid), dim3(64 * SPEC_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
-                               c->d_loc, c->d_tin, c->d_lanes, c->d_pos, c->d_fix, c->d_g, RL);
+            hipLaunchKernelGGL(k_refix, dim3(fix_grid), dim3(64 * SCAN_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix,
+                               c->d_loc, c->d_tin, c->d_rec, c->d_treg, c->d_tabs, c->d_fix, c->d_g, RL);
             hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, c->d_loc, c->d_tin, c->d_ftotal,
                                c->d_fix, c->d_g, RL);
             hipLaunchKernelGGL(k_fbase, dim3(1), dim3(FB_NT), 0, st, nfiles, c->d_ftotal, c->d_finfo, c->d_g, RL);
@@ -1794,16 +1441,14 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         HIPCK(hipEventElapsedTime(&ms_fix, c->ev[5], c->ev[6]));
         if (!c->h_g->fail) {
             HIPCK(hipEventRecord(c->ev[2], st));
-            rc2 = launch_crc();
+            rc2 = launch_emit();
             if (rc2) return rc2;
         }
     }
     bool located = false;
     if (c->h_g->any_fail && !c->h_g->fail) {
-        HIPCK(hipMemcpyAsync(c->h_finfo, c->d_finfo, sizeof(FileInfo) * nfiles, hipMemcpyDeviceToHost, st));
-        HIPCK(hipStreamSynchronize(st));
-        hipLaunchKernelGGL(k_locate, dim3(c->loc_grid), dim3(512), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
-                           c->d_tin, c->d_lanes, c->d_treg, c->d_finfo, c->d_tabs, c->d_g);
+        hipLaunchKernelGGL(k_locate, dim3(c->loc_grid), dim3(1024), 0, st, c->d_files, nfiles, c->d_finfo, d_out,
+                           c->h_g->total, out_cap, c->d_tabs);
         HIPCK(hipGetLastError());
         located = true;
     }
@@ -1811,16 +1456,16 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     HIPCK(hipMemcpyAsync(c->h_finfo, c->d_finfo, sizeof(FileInfo) * nfiles, hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
-    float ms_spec = 0, ms_link = 0, ms_crc = 0, ms_fin = 0, ms_loc = 0;
-    HIPCK(hipEventElapsedTime(&ms_spec, c->ev[0], c->ev[1]));
+    float ms_scan = 0, ms_link = 0, ms_emit = 0, ms_fin = 0, ms_loc = 0;
+    HIPCK(hipEventElapsedTime(&ms_scan, c->ev[0], c->ev[1]));
     HIPCK(hipEventElapsedTime(&ms_link, c->ev[1], c->ev[2]));
-    HIPCK(hipEventElapsedTime(&ms_crc, c->ev[2], c->ev[3]));
+    HIPCK(hipEventElapsedTime(&ms_emit, c->ev[2], c->ev[3]));
     HIPCK(hipEventElapsedTime(&ms_fin, c->ev[3], c->ev[4]));
     HIPCK(hipEventElapsedTime(&ms_loc, c->ev[4], c->ev[7]));
     if (ms_fix > 0) ms_link = 0;   // ev[2] was re-recorded after the host repair loop
     c->h_g->refix = refixed;
-    c->kms[0] = ms_spec; c->kms[1] = ms_link + ms_fix; c->kms[2] = ms_crc; c->kms[3] = ms_fin; c->kms[4] = ms_loc;
-    c->kms[5] = ms_spec + ms_link + ms_fix + ms_crc + ms_fin + ms_loc;
+    c->kms[0] = ms_scan; c->kms[1] = ms_link + ms_fix; c->kms[2] = ms_emit; c->kms[3] = ms_fin; c->kms[4] = ms_loc;
+    c->kms[5] = ms_scan + ms_link + ms_fix + ms_emit + ms_fin + ms_loc;
     if (c->h_g->fail) {
         fprintf(stderr, "clyscan: internal error (code %#x)\n", c->h_g->fail);
         return CLY_ERR_DEVICE;
@@ -1834,7 +1479,12 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
             res[i].end_offset = fi.term_pos;
             res[i].status = fi.term_status;
         } else {
-            if (fi.fail_key == ~0ull) { fprintf(stderr, "clyscan: internal error (file %d: no failing record)\n", i); return CLY_ERR_DEVICE; }
+            if (fi.fail_key == ~0ull) {
+                // a record's tuple was dropped (out_cap) before k_locate could check it
+                if (c->h_g->overflow || c->h_g->total > out_cap) return CLY_ERR_CAPACITY;
+                fprintf(stderr, "clyscan: internal error (file %d: no failing record)\n", i);
+                return CLY_ERR_DEVICE;
+            }
             res[i].n_records = fi.fail_key & 0xffffffffull;
             res[i].end_offset = (int64_t)(fi.fail_key >> 32);
             res[i].status = CLY_ERR_CRC;
@@ -1844,10 +1494,10 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     }
     if (needed) *needed = c->h_g->total;
     if (stats) {
-        stats->scan_ms = ms_spec + ms_crc; stats->resolve_ms = ms_link + ms_fix + ms_fin + ms_loc;
+        stats->scan_ms = ms_scan + ms_emit; stats->resolve_ms = ms_link + ms_fix + ms_fin + ms_loc;
         stats->total_ms = c->kms[5];
         stats->passes = rounds + (located ? 1 : 0);
-        stats->n_chunks = (uint32_t)(ntiles * CLY_NL); stats->bytes = bytes; stats->records = total;
+        stats->n_chunks = (uint32_t)(ntiles * CLY_NBLK * CLY_NL); stats->bytes = bytes; stats->records = total;
     }
     if (c->h_g->overflow || c->h_g->total > out_cap) return CLY_ERR_CAPACITY;
     return CLY_OK;
@@ -1868,7 +1518,7 @@ extern "C" int cly_scan(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
     HIPCK(hipSetDevice(c->device));
     uint64_t total = 0;
     for (int i = 0; i < nfiles; i++) {
-        if (files[i].len >= 0xFFFFFFFFull) return CLY_ERR_ARG;
+        if (files[i].len > MAX_FILE_LEN) return CLY_ERR_ARG;
         total += (files[i].len + 4095) & ~4095ULL;
     }
     if (total + 4096 > c->cap_bytes) {
@@ -1980,8 +1630,19 @@ extern "C" void cly_ctx_set_clock(cly_ctx* c, int64_t now_ns) { if (c) c->now_ns
 extern "C" int cly_ctx_device_internal(cly_ctx* c) { return c->device; }
 extern "C" void** cly_ctx_merge_slot_internal(cly_ctx* c) { return &c->merge_scratch; }
 
-// Per-kernel times of the last cly_scan_device call (ms): k_spec, link rounds
-// (k_link + k_fbase + repair), k_crc, k_fin, k_locate, all.  Not in the public header.
+// Per-kernel times of the last cly_scan_device call (ms): k_scan, link rounds
+// (k_link + k_fbase + repair), k_emit, k_fin, k_locate, all.  Not in the public header.
+// Debug (not in the public header): flags (bit 0: snapshot k_scan's tile
+// LOCALs); cly_dbg_tiles copies the snapshot (32 B per tile) and the final
+// TileIns (32 B per tile) of the last call to host memory.
+extern "C" void cly_dbg_set(cly_ctx* c, int flags) { c->dbg = flags; }
+extern "C" int cly_dbg_tiles(cly_ctx* c, void* loc_out, void* tin_out, int64_t ntiles) {
+    HIPCK(hipSetDevice(c->device));
+    if (loc_out && c->d_dbg && ntiles <= c->cap_dbg)
+        HIPCK(hipMemcpy(loc_out, c->d_dbg, sizeof(TileLocal) * ntiles, hipMemcpyDeviceToHost));
+    if (tin_out && ntiles <= c->cap_tiles) HIPCK(hipMemcpy(tin_out, c->d_tin, sizeof(TileIn) * ntiles, hipMemcpyDeviceToHost));
+    return CLY_OK;
+}
 extern "C" int cly_dbg_kernel_ms(cly_ctx* c, double* out6) {
     for (int i = 0; i < 6; i++) out6[i] = c->kms[i];
     return 6;
@@ -2009,7 +1670,7 @@ extern "C" const char* cly_strerror(int code) {
 #endif
 extern "C" const char* cly_build_info(void) {
     static char buf[200];
-    snprintf(buf, sizeof(buf), "clyscan gfx950 spec/link/crc CH=%d TILE=%lld LDS=%d src=%s", CLY_CH, (long long)CLY_TILE,
-             (int)SCAN_LDS, CLY_SRC_HASH);
+    snprintf(buf, sizeof(buf), "clyscan gfx950 scan/link/emit SEG=%d TILE=%lld CAP_T=%u LDS=%d src=%s", CLY_SEG,
+             (long long)CLY_TILE, (unsigned)CAP_T, (int)SCAN_LDS, CLY_SRC_HASH);
     return buf;
 }

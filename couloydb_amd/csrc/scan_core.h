@@ -7,9 +7,12 @@
 // parseLogRecordKey (db.go:706-710).
 //
 // Work decomposition of the scan:
-//   chunk  CLY_CH bytes of one file, owned by one lane
-//   tile   64 consecutive chunks of one file, owned by one wave; tiles are the
-//          unit of the decoupled look-back (record counts and chain state)
+//   segment  CLY_SEG = 64 consecutive bytes, owned by one lane for one block
+//   block    64 segments = 4 KiB, read by one wave with four coalesced 1-KiB
+//            load instructions and transposed so that lane L holds segment L
+//   tile     CLY_NBLK consecutive blocks of one file, owned by one wave, which
+//            streams them in order; tiles are the unit of the chain link
+//            (record counts and chain state between tiles, k_link)
 #pragma once
 #include <stdint.h>
 
@@ -19,16 +22,14 @@
 #define CLY_DEV __host__ __device__ __forceinline__     // host too: clyload.hip's getLogRecordByPos
 #define CLY_LDS __attribute__((address_space(3)))
 
-#ifndef CLY_CH
-#define CLY_CH 1024           // chunk bytes per lane (multiple of 16; the test build uses 64)
+#ifndef CLY_NBLK
+#define CLY_NBLK 16           // blocks per tile (the test build uses 2: 8-KiB tiles)
 #endif
-#define CLY_NL 64                             // lanes (chunks) per tile
-#define CLY_NW (CLY_CH / 4)                   // words per chunk
-#define CLY_TILE ((int64_t)CLY_NL * CLY_CH)   // tile bytes
-#define CLY_BW (CLY_NW < 32 ? CLY_NW : 32)    // words per load burst (128 B)
-#define CLY_NB (CLY_NW / CLY_BW)              // bursts per chunk
-static_assert(CLY_CH % 16 == 0 && CLY_CH >= 64, "chunk = 16-B pieces, >= 64 B");
-static_assert(CLY_NW % CLY_BW == 0 && CLY_BW % 8 == 0, "bursts of whole quarters");
+#define CLY_SEG 64                                // bytes per lane per block
+#define CLY_NL 64                                 // lanes (segments) per block
+#define CLY_BLK (CLY_NL * CLY_SEG)                // block bytes (4 KiB)
+#define CLY_TILE ((int64_t)CLY_NBLK * CLY_BLK)    // tile bytes
+static_assert(CLY_NBLK >= 1 && CLY_TILE <= 65536, "tile-relative record offsets are u16");
 
 #define REC_OK 100
 

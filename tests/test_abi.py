@@ -75,7 +75,7 @@ def test_capacity_bound():
 
 def test_build_info():
     s = _abi.load_scan_lib().cly_build_info().decode()
-    assert "gfx950" in s and "CH=" in s and "TILE=" in s
+    assert "gfx950" in s and "SEG=" in s and "TILE=" in s and "src=" in s
 
 
 def test_gen_record_size_and_layout():

@@ -1,4 +1,4 @@
-"""Per-kernel times (cly_dbg_kernel_ms: k_spec, link, k_crc, k_fin, k_locate,
+"""Per-kernel times (cly_dbg_kernel_ms: k_scan, link, k_emit, k_fin, k_locate,
 all) of alternative builds of libclyscan on C2 (or CLY_EXP_CONFIG), with a
 tuple/status check of every build against the first one:
 python tools/exp_kms.py libclyscan.so libclyscan_x.so ..."""
@@ -25,12 +25,12 @@ for rnd in range(2):
             sc.lib.cly_dbg_kernel_ms(sc.ctx, k)
             rows.append(list(k))
         torch.cuda.synchronize()
-        t64 = wl.d_out[: need * 48].view(torch.int64)
+        t64 = wl.d_out[: max(need, 1) * 48].view(torch.int64)
         sig = (tuple(first), tuple((r.status, r.end_offset, r.n_records) for r in res), int(need),
                int(t64.sum().item()), int((t64 * torch.arange(t64.numel(), device=t64.device)).sum().item()))
         if ref is None:
             ref = sig
         best = [min(r[i] for r in rows[1:]) for i in range(6)]
-        print("round %d %-26s spec %.3f link %.3f crc %.3f fin %.3f all %.3f  same=%s" %
+        print("round %d %-26s scan %.3f link %.3f emit %.3f fin %.3f all %.3f  same=%s" %
               (rnd, lib, best[0], best[1], best[2], best[3], best[5], sig == ref), flush=True)
         sc.close()
