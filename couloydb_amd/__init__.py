@@ -321,10 +321,12 @@ class Scanner:
         (UnixNano; 0 = the wall clock at each call)."""
         self.lib.cly_ctx_set_clock(self.ctx, int(now_ns))
 
-    def open_db(self, path):
-        """NewCouloyDB's index load (db.go:442-655) from the `%09d.cly` files of
-        directory `path`, on this scanner's device (cly_db_open)."""
-        return LoadedDB(self, path)
+    def open_db(self, path, data_file_size=0, apply_sweep=False):
+        """NewCouloyDB's index load (db.go:442-655, merge.go:240-287) from the
+        `*.cly`, hint-index and merge-finished files of directory `path`, on
+        this scanner's device (cly_db_open_opts).  apply_sweep: append the TTL
+        sweep's tombstones to the active file on disk, as db.Del does."""
+        return LoadedDB(self, path, data_file_size, apply_sweep)
 
     KERNELS = ("k_scan", "link", "k_emit", "k_fin", "k_locate", "all")
 
@@ -365,13 +367,29 @@ class LoadedDB:
     (getLogRecordByPos).  get/hget/lget/sget return the value bytes, or raise
     KeyError for public.ErrKeyNotFound."""
 
-    def __init__(self, scanner, path):
+    def __init__(self, scanner, path, data_file_size=0, apply_sweep=False):
         self.lib = scanner.lib
         self.db = ctypes.c_void_p()
         self.stats = _abi.ClyLoadStats()
-        rc = self.lib.cly_db_open(scanner.ctx, os.fsencode(path), ctypes.byref(self.db), ctypes.byref(self.stats))
+        opt = _abi.ClyDbOptions()
+        opt.data_file_size = data_file_size
+        opt.flags = _abi.DB_APPLY_SWEEP if apply_sweep else 0
+        rc = self.lib.cly_db_open_opts(scanner.ctx, os.fsencode(path), ctypes.byref(opt), ctypes.byref(self.db),
+                                       ctypes.byref(self.stats))
         if rc != 0:
             raise (ErrInvalidCRC if rc == ERR_CRC else ScanError)(rc, self.lib.cly_strerror(rc).decode())
+
+    def entries(self, kind):
+        """cly_db_entries of one kind (_abi.IT_*): [(key, sub, LogPos, expiration)]."""
+        n = int(self.lib.cly_db_count(self.db, kind))
+        arr = (_abi.ClyDbEntry * max(1, n))()
+        got = int(self.lib.cly_db_entries(self.db, kind, 0, arr, n))
+        out = []
+        for e in arr[:got]:
+            key = ctypes.string_at(e.key, e.key_len) if e.key_len else b""
+            sub = ctypes.string_at(e.sub, e.sub_len) if e.sub_len else b""
+            out.append((key, sub, LogPos(e.pos.fid, e.pos.offset), int(e.expiration)))
+        return out
 
     def close(self):
         if self.db:
@@ -418,6 +436,10 @@ class LoadedDB:
         p.fid, p.offset = pos.fid, pos.offset
         n = ctypes.c_uint64()
         rc = self.lib.cly_db_value(self.db, ctypes.byref(p), None, 0, ctypes.byref(n))
+        if rc == _abi.DB_NOT_FOUND:
+            raise KeyError(pos)
+        if rc != 0:
+            raise (ErrInvalidCRC if rc == ERR_CRC else ScanError)(rc, self.lib.cly_strerror(rc).decode())
         buf = ctypes.create_string_buffer(max(1, n.value))
         rc = self.lib.cly_db_value(self.db, ctypes.byref(p), buf, n.value, ctypes.byref(n))
         if rc != 0:

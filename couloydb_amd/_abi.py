@@ -91,9 +91,12 @@ SCAN_SYMBOLS = ["cly_ctx_create", "cly_ctx_destroy", "cly_ctx_set_clock", "cly_s
                 "cly_index_device", "cly_index", "cly_append_device", "cly_append",
                 "cly_strerror", "cly_build_info"]
 GEN_SYMBOLS = ["cly_gen_record_size", "cly_gen_layout", "cly_gen_encode"]
-LOAD_SYMBOLS = ["cly_db_open", "cly_db_close", "cly_db_get", "cly_db_listmeta", "cly_db_hget", "cly_db_lget",
-                "cly_db_sget", "cly_db_value", "cly_index_key"]
-DB_NOT_FOUND = 1
+LOAD_SYMBOLS = ["cly_db_open", "cly_db_open_opts", "cly_db_close", "cly_db_get", "cly_db_listmeta", "cly_db_hget",
+                "cly_db_lget", "cly_db_sget", "cly_db_value", "cly_index_key", "cly_db_count", "cly_db_entries"]
+DB_NOT_FOUND, DB_EOF = 1, 2
+ERR_DIR, ERR_MERGE_FIN = -14, -15
+IT_STRING, IT_LISTMETA, IT_HASH, IT_LIST, IT_SET, IT_EXPIRED = range(6)
+DB_APPLY_SWEEP = 1
 
 
 class ClyPos(ctypes.Structure):
@@ -106,7 +109,19 @@ class ClyLoadStats(ctypes.Structure):
                 ("n_files", ctypes.c_uint64), ("bytes", ctypes.c_uint64), ("records", ctypes.c_uint64),
                 ("str_keys", ctypes.c_uint64), ("listmeta_keys", ctypes.c_uint64), ("hash_fields", ctypes.c_uint64),
                 ("list_items", ctypes.c_uint64), ("set_members", ctypes.c_uint64),
-                ("active_fid", ctypes.c_uint32), ("_pad", ctypes.c_uint32), ("write_off", ctypes.c_int64)]
+                ("active_fid", ctypes.c_uint32), ("_pad", ctypes.c_uint32), ("write_off", ctypes.c_int64),
+                ("hint_records", ctypes.c_uint64), ("n_expired", ctypes.c_uint64),
+                ("write_off_loaded", ctypes.c_int64), ("active_fid_loaded", ctypes.c_uint32),
+                ("sweep_files", ctypes.c_uint32)]
+
+
+class ClyDbOptions(ctypes.Structure):
+    _fields_ = [("data_file_size", ctypes.c_uint64), ("flags", ctypes.c_uint32), ("_pad", ctypes.c_uint32)]
+
+
+class ClyDbEntry(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_void_p), ("key_len", ctypes.c_uint64), ("sub", ctypes.c_void_p),
+                ("sub_len", ctypes.c_uint64), ("pos", ClyPos), ("expiration", ctypes.c_int64)]
 
 _libs = {}
 
@@ -134,6 +149,13 @@ def load_scan_lib(name="libclyscan.so"):
         lib.cly_dbg_kernel_ms.restype = ctypes.c_int
     lib.cly_db_open.argtypes = [ctypes.c_void_p, ctypes.c_char_p, P(ctypes.c_void_p), ctypes.c_void_p]
     lib.cly_db_open.restype = ctypes.c_int
+    lib.cly_db_open_opts.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, P(ctypes.c_void_p),
+                                     ctypes.c_void_p]
+    lib.cly_db_open_opts.restype = ctypes.c_int
+    lib.cly_db_count.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.cly_db_count.restype = ctypes.c_uint64
+    lib.cly_db_entries.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]
+    lib.cly_db_entries.restype = ctypes.c_uint64
     lib.cly_db_close.argtypes = [ctypes.c_void_p]
     lib.cly_db_close.restype = None
     for fn in ("cly_db_get", "cly_db_listmeta"):

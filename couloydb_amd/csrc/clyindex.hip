@@ -354,7 +354,7 @@ k_ixwin(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, cons
         const bool deleted = g ? tup[w].type == 1 : (sidx[q] & IX_DEL) != 0;
         // LogRecordDeleted -> key absent; a String key whose winning put expired is
         // db.Del'd by loadIndex's TTL sweep (db.go:639-651: not exp.After(now))
-        if (!deleted && !ix_expired(tup[w], now_ns)) state[w] = ix_win_state(tup, first, bases, nfiles, w);
+        if (!deleted) state[w] = ix_expired(tup[w], now_ns) ? (uint8_t)CLY_IX_EXPIRED : ix_win_state(tup, first, bases, nfiles, w);
     }
 }
 // exact resolution of a collided hash group (one thread): per distinct key the max order
@@ -374,8 +374,8 @@ k_ixcoll(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, con
         for (uint64_t b = q0; b < q1 && best; b++)
             if (b != a && order[IXI(sidx[b])] > order[ia] &&
                 ix_same_key(tup, first, bases, nfiles, ia, IXI(sidx[b]))) best = false;
-        if (best && tup[ia].type != 1 && !ix_expired(tup[ia], now_ns))
-            state[ia] = ix_win_state(tup, first, bases, nfiles, ia);
+        if (best && tup[ia].type != 1)
+            state[ia] = ix_expired(tup[ia], now_ns) ? (uint8_t)CLY_IX_EXPIRED : ix_win_state(tup, first, bases, nfiles, ia);
     }
 }
 // counts: one atomic per workgroup and counter (a wave-level atomic on one

@@ -1,23 +1,30 @@
 // clyload.hip — the index load of NewCouloyDB on the device (host driver of
 // libclyscan; include/clyload.h).
 //
-// Restates, from data files on disk to a queryable index:
-//   NewCouloyDB -> loadDataFile (db.go:442-485: the `%09d.cly` files of the
-//   directory, fids ascending, the last one the active file)
-//   -> loadIndex (db.go:487-655: every record of every file in fid order,
-//   tx buffering by txId, updateIndex, the TTL sweep).
-// The files are mmap'd, copied to HBM, scanned (cly_scan_device) and the
-// index state of every record (all five indexes) is rebuilt on the device
-// (cly_index_device).  The tuples and states come back, and the host builds
-// what updateIndex puts in the MemTables (meta/memTable.go:15-30) from the
-// records the device marked as index entries: the String and ListMeta indexes
-// as open-addressing tables over the mapped key bytes, and the per-key Hash
-// (field), List (seq gob encoding) and Set (member hash) maps, keyed as
-// ixkey.h derives them (the same code as the device's).
+// Restates, from the files of a data directory to a queryable index:
+//   NewCouloyDB -> loadDataFile (db.go:442-485: the `*.cly` files, stems by
+//   strconv.Atoi, fids ascending, the last one the active file)
+//   -> loadIndexFromHintFile (merge.go:257-287: hint-index records into the
+//   String index first) -> loadIndex (db.go:487-655: merge-finished checked,
+//   every record of every file in fid order, tx buffering by txId,
+//   updateIndex, the TTL sweep's db.Del).
+// The files are mmap'd and copied to HBM; the hint file and the data files are
+// scanned in one cly_scan_device call, the hint records' positions decoded on
+// the device, and their tuples rewritten as String puts of their stored key
+// (no txId) so that the device index rebuild (cly_index_device) applies them
+// first and the data files' String records override them, last writer wins.
+// The tuples and states come back, and the host builds what updateIndex puts
+// in the MemTables (meta/memTable.go:15-30) from the records the device
+// marked as index entries: the String and ListMeta indexes as open-addressing
+// tables over the mapped key bytes, and the per-key Hash (field), List (seq
+// gob encoding) and Set (member hash) maps, keyed as ixkey.h derives them
+// (the same code as the device's).  The TTL sweep's tombstones follow
+// appendLogRecord's rotation rule (db.go:368-413).
 //
 // The host inserts are timed separately from the device work.
 #include <hip/hip_runtime.h>
 #include <dirent.h>
+#include <errno.h>
 #include <fcntl.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -57,6 +64,45 @@ struct Mapped {
     const uint8_t* p;
     uint64_t len;
 };
+// Go's strconv.Atoi (64-bit int): an optional sign, decimal digits, no overflow
+static bool go_atoi(const char* s, size_t n, int64_t& v) {
+    size_t i = 0;
+    bool neg = false;
+    if (n && (s[0] == '+' || s[0] == '-')) { neg = s[0] == '-'; i = 1; }
+    if (i == n) return false;
+    uint64_t x = 0;
+    for (; i < n; i++) {
+        if (s[i] < '0' || s[i] > '9') return false;
+        const uint64_t d = (uint64_t)(s[i] - '0');
+        if (x > (UINT64_MAX - d) / 10) return false;
+        x = x * 10 + d;
+    }
+    if (neg) { if (x > (uint64_t)INT64_MAX + 1) return false; v = (int64_t)(0 - x); }
+    else { if (x > (uint64_t)INT64_MAX) return false; v = (int64_t)x; }
+    return true;
+}
+// CRC-32/IEEE of a byte range (host; table-driven)
+static uint32_t host_crc(const uint8_t* p, uint64_t n) {
+    static uint32_t tab[256];
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (uint32_t i = 0; i < 256; i++) {
+            uint32_t c = i;
+            for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ CLY_POLY : c >> 1;
+            tab[i] = c;
+        }
+    });
+    uint32_t c = 0xFFFFFFFFu;
+    for (uint64_t i = 0; i < n; i++) c = tab[(c ^ p[i]) & 0xff] ^ (c >> 8);
+    return ~c;
+}
+// ReadLogRecord (data/dataFile.go:64-111) at off of a host buffer: the
+// header, and REC_OK only if the CRC matches (else CLY_ERR_CRC)
+static Hdr host_read_record(const uint8_t* p, uint64_t len, int64_t off) {
+    Hdr h = step_hdr(p, off, (int64_t)len, off);
+    if (h.status == REC_OK && host_crc(p + off + 4, (uint64_t)h.size - 4) != h.crc) h.status = CLY_ERR_CRC;
+    return h;
+}
 
 // The String / ListMeta index: open-addressing tables of (key hash, tuple
 // index), sharded by the hash's top bits so that one thread builds each shard;
@@ -88,6 +134,12 @@ template <class T> struct HostArr {
 };
 struct cly_db {
     std::vector<Mapped> files;
+    Mapped hint = {0, nullptr, 0};   // hint-index (tuples 0 .. n_hint-1 are its records)
+    uint64_t n_hint = 0;
+    std::vector<cly_pos> hint_pos;   // DecodeLogRecordPos of each hint record's value
+    std::vector<uint64_t> expired;   // tuple indices of the String winners the TTL sweep removed
+    std::vector<cly_db_entry> it[6]; // cly_db_entries, built on first use
+    bool it_built[6] = {false, false, false, false, false, false};
     HostArr<cly_tuple> tuples;
     HostArr<uint8_t> state;
     HostArr<uint64_t> khash;     // the device index's key hash per record (String / ListMeta tables)
@@ -142,17 +194,21 @@ static const uint8_t* file_of(const cly_db* db, uint32_t fid) {
     return lo < db->files.size() && db->files[lo].fid == fid ? db->files[lo].p : nullptr;
 }
 
-// realKey of tuple t (parseLogRecordKey, db.go:706-710)
-static const uint8_t* real_key_ptr(const cly_db* db, const cly_tuple& t, uint64_t& len) {
-    const uint8_t* f = file_of(db, t.fid);
+// realKey of tuple ti (parseLogRecordKey, db.go:706-710); a hint record's
+// stored key as it is (strIndex.Put(logRecord.Key), merge.go:283)
+static const uint8_t* real_key_ptr(const cly_db* db, uint64_t ti, uint64_t& len) {
+    const cly_tuple& t = db->tuples[ti];
+    const uint8_t* f = ti < db->n_hint ? db->hint.p : file_of(db, t.fid);
     const uint32_t tl = t.txid_len == 0xFF ? 0 : t.txid_len;
     len = t.key_size - tl;
     return f + t.offset + t.header_size + tl;
 }
-static std::string real_key(const cly_db* db, const cly_tuple& t) {
-    uint64_t n;
-    const uint8_t* p = real_key_ptr(db, t, n);
-    return std::string((const char*)p, n);
+// the LogPos an index entry at tuple ti holds
+static cly_pos pos_of(const cly_db* db, uint64_t ti) {
+    if (ti < db->n_hint) return db->hint_pos[ti];
+    cly_pos p;
+    p.offset = db->tuples[ti].offset; p.fid = db->tuples[ti].fid; p._pad = 0;
+    return p;
 }
 static void flat_init(FlatShard& x, uint64_t n) {
     uint64_t cap = 16;
@@ -178,49 +234,66 @@ static int flat_get(const cly_db* db, const FlatIndex& xi, uint32_t kind, const 
     if (!x.mask) return CLY_DB_NOT_FOUND;
     for (uint64_t i = h & x.mask; x.h[i]; i = (i + 1) & x.mask) {
         if (x.h[i] != h) continue;
-        const cly_tuple& t = db->tuples[x.ti[i]];
         uint64_t n;
-        const uint8_t* k = real_key_ptr(db, t, n);
+        const uint8_t* k = real_key_ptr(db, x.ti[i], n);
         if (n == klen && memcmp(k, key, n) == 0) {
-            if (pos) { pos->offset = t.offset; pos->fid = t.fid; pos->_pad = 0; }
+            if (pos) *pos = pos_of(db, x.ti[i]);
             return CLY_OK;
         }
     }
     return CLY_DB_NOT_FOUND;
 }
 
+static int map_file(const char* path, Mapped& m, bool& exists) {
+    m.p = nullptr; m.len = 0;
+    exists = false;
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return errno == ENOENT ? CLY_OK : CLY_ERR_ARG;
+    exists = true;
+    struct stat sb;
+    if (fstat(fd, &sb) != 0 || S_ISDIR(sb.st_mode)) { close(fd); return CLY_ERR_ARG; }
+    m.len = (uint64_t)sb.st_size;
+    if (m.len) {
+        void* p = mmap(nullptr, m.len, PROT_READ, MAP_PRIVATE, fd, 0);     // pages: faulted in by the copy threads
+        if (p == MAP_FAILED) { close(fd); m.len = 0; return CLY_ERR_ARG; }
+        m.p = (const uint8_t*)p;
+    }
+    close(fd);
+    return CLY_OK;
+}
+// loadDataFile's listing (db.go:442-470): entries ending in ".cly", stem =
+// the name up to its first '.', fid = strconv.Atoi(stem) (failure: "the data
+// dir maybe contaminated or damaged"), sort.Ints; the file read is
+// GetDataFileName(uint32(fid)) = "%09d.cly" (absent: read as empty; the
+// reference's OpenFile creates it empty).  A fid listed twice (say "7.cly" and
+// "000000007.cly") is read once: reading it again re-applies the same records
+// in the same order and leaves the same indexes.
 static int list_files(const char* dir, std::vector<Mapped>& out) {
     DIR* d = opendir(dir);
     if (!d) return CLY_ERR_ARG;
     struct dirent* e;
-    std::vector<uint32_t> fids;
+    std::vector<int64_t> fids;
+    int rc = CLY_OK;
     while ((e = readdir(d))) {
-        // data/dataFile.go:20-23 + public/preset.go:6: fmt.Sprintf("%09d", fid) + ".cly"
         const size_t n = strlen(e->d_name);
-        if (n != 13 || strcmp(e->d_name + 9, ".cly") != 0) continue;
-        bool digits = true;
-        for (int i = 0; i < 9; i++) digits &= e->d_name[i] >= '0' && e->d_name[i] <= '9';
-        if (digits) fids.push_back((uint32_t)strtoul(std::string(e->d_name, 9).c_str(), nullptr, 10));
+        if (n < 4 || strcmp(e->d_name + n - 4, ".cly") != 0) continue;
+        const char* dot = strchr(e->d_name, '.');
+        int64_t v;
+        if (!go_atoi(e->d_name, (size_t)(dot - e->d_name), v)) { rc = CLY_ERR_DIR; break; }
+        fids.push_back(v);
     }
     closedir(d);
+    if (rc != CLY_OK) return rc;
     std::sort(fids.begin(), fids.end());
-    for (uint32_t fid : fids) {
+    fids.erase(std::unique(fids.begin(), fids.end()), fids.end());
+    for (int64_t f : fids) {
         char path[4096];
+        const uint32_t fid = (uint32_t)f;
         snprintf(path, sizeof(path), "%s/%09u.cly", dir, fid);
-        const int fd = open(path, O_RDONLY);
-        if (fd < 0) return CLY_ERR_ARG;
-        struct stat sb;
-        if (fstat(fd, &sb) != 0) { close(fd); return CLY_ERR_ARG; }
         Mapped m;
+        bool exists;
+        if (map_file(path, m, exists) != CLY_OK) return CLY_ERR_ARG;
         m.fid = fid;
-        m.len = (uint64_t)sb.st_size;
-        m.p = nullptr;
-        if (m.len) {
-            void* p = mmap(nullptr, m.len, PROT_READ, MAP_PRIVATE, fd, 0);     // pages: faulted in by the copy threads
-            if (p == MAP_FAILED) { close(fd); return CLY_ERR_ARG; }
-            m.p = (const uint8_t*)p;
-        }
-        close(fd);
         out.push_back(m);
     }
     return CLY_OK;
@@ -306,166 +379,279 @@ static void flat_build(cly_db* db, int nthreads, std::vector<uint64_t>& composit
 extern "C" void cly_db_close(cly_db* db) {
     if (!db) return;
     for (Mapped& m : db->files) if (m.p) munmap((void*)m.p, m.len);
+    if (db->hint.p) munmap((void*)db->hint.p, db->hint.len);
     delete db;
 }
 
 #define DCK(x) do { if ((x) != hipSuccess) { rc = CLY_ERR_DEVICE; goto done; } } while (0)
 
+// A hint record's tuple as the index rebuild takes it: strIndex.Put of its
+// stored key (no txId prefix, merge.go:283), whatever its types, no TTL
+__global__ void k_hint_as_put(cly_tuple* t, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    t[i].tx_id = 0; t[i].txid_len = 0; t[i].type = 0; t[i].data_type = 0; t[i].expiration = 0;
+}
+
+// The files' bytes to the device: load_threads() threads fault the mapped
+// pages in and copy 64-MiB pieces through page-locked staging buffers (CPU
+// copy of one while the DMA of the other runs).
+static int copy_to_device(cly_ctx* ctx, const std::vector<cly_file>& hf, std::vector<cly_file>& df, uint8_t* d_bytes) {
+    struct Piece { const uint8_t* src; uint8_t* dst; uint64_t len; };
+    std::vector<Piece> pieces;
+    uint64_t off = 0;
+    for (size_t i = 0; i < hf.size(); i++) {
+        df[i] = hf[i];
+        df[i].base = d_bytes + off;
+        for (uint64_t a = 0; a < hf[i].len; a += LOAD_PIECE)
+            pieces.push_back({hf[i].base + a, d_bytes + off + a, std::min<uint64_t>(LOAD_PIECE, hf[i].len - a)});
+        off += (hf[i].len + 4095) & ~4095ull;
+    }
+    std::atomic<size_t> next(0);
+    std::atomic<int> err(0);
+    const int dev = cly_ctx_device_internal(ctx);
+    const int nt = load_threads();
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    for (int k = 0; k < 2 * LOAD_THREADS_MAX; k++)          // (again after a failed allocation)
+        if (!g_stage[k] && hipHostMalloc(&g_stage[k], LOAD_STAGE, hipHostMallocPortable) != hipSuccess) {
+            g_stage[k] = nullptr;
+            err = 1;
+        }
+    if (err) return CLY_ERR_DEVICE;
+    par_run(nt, [&](int t) {
+        if (hipSetDevice(dev) != hipSuccess) { err = 1; return; }
+        hipStream_t ts = nullptr;
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        if (hipStreamCreateWithFlags(&ts, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) != hipSuccess) { err = 1; return; }
+        int b = 0;
+        bool used[2] = {false, false};
+        for (size_t k; (k = next.fetch_add(1)) < pieces.size();) {
+            const Piece& pc = pieces[k];
+            for (uint64_t a = 0; a < pc.len; a += LOAD_STAGE) {
+                const uint64_t n = std::min<uint64_t>(LOAD_STAGE, pc.len - a);
+                uint8_t* stg = (uint8_t*)g_stage[2 * t + b];
+                if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) err = 1;
+                memcpy(stg, pc.src + a, n);
+                if (hipMemcpyAsync(pc.dst + a, stg, n, hipMemcpyHostToDevice, ts) != hipSuccess ||
+                    hipEventRecord(ev[b], ts) != hipSuccess) err = 1;
+                used[b] = true;
+                b ^= 1;
+            }
+        }
+        if (hipStreamSynchronize(ts) != hipSuccess) err = 1;
+        hipEventDestroy(ev[0]); hipEventDestroy(ev[1]);
+        hipStreamDestroy(ts);
+    });
+    return err ? CLY_ERR_DEVICE : CLY_OK;
+}
+
+// Device buffers back to host memory, in pieces from several threads (DMA
+// into one staging buffer while the CPU copies the other out).
+struct D2H { void* dst; const void* src; uint64_t len; };
+static int copy_to_host(cly_ctx* ctx, const std::vector<D2H>& parts) {
+    struct Piece { void* dst; const void* src; uint64_t len; };
+    std::vector<Piece> pieces;
+    for (const D2H& x : parts)
+        for (uint64_t a = 0; a < x.len; a += LOAD_PIECE)
+            pieces.push_back({(uint8_t*)x.dst + a, (const uint8_t*)x.src + a, std::min<uint64_t>(LOAD_PIECE, x.len - a)});
+    std::atomic<size_t> next(0);
+    std::atomic<int> err(0);
+    const int dev = cly_ctx_device_internal(ctx);
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    for (int k = 0; k < 2 * LOAD_THREADS_MAX; k++)
+        if (!g_stage[k] && hipHostMalloc(&g_stage[k], LOAD_STAGE, hipHostMallocPortable) != hipSuccess) {
+            g_stage[k] = nullptr;
+            err = 1;
+        }
+    if (err) return CLY_ERR_DEVICE;
+    par_run(load_threads(), [&](int t) {
+        if (hipSetDevice(dev) != hipSuccess) { err = 1; return; }
+        hipStream_t ts = nullptr;
+        if (hipStreamCreateWithFlags(&ts, hipStreamNonBlocking) != hipSuccess) { err = 1; return; }
+        struct Pend { uint8_t* dst; uint64_t n; int b; };
+        Pend pend = {nullptr, 0, 0};
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        if (hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) != hipSuccess) { err = 1; return; }
+        int b = 0;
+        auto drain = [&]() {
+            if (!pend.dst) return;
+            if (hipEventSynchronize(ev[pend.b]) != hipSuccess) err = 1;
+            memcpy(pend.dst, g_stage[2 * t + pend.b], pend.n);
+            pend.dst = nullptr;
+        };
+        for (size_t k; (k = next.fetch_add(1)) < pieces.size();) {
+            const Piece& pc = pieces[k];
+            for (uint64_t a = 0; a < pc.len; a += LOAD_STAGE) {
+                const uint64_t n = std::min<uint64_t>(LOAD_STAGE, pc.len - a);
+                if (hipMemcpyAsync(g_stage[2 * t + b], (const uint8_t*)pc.src + a, n, hipMemcpyDeviceToHost, ts) !=
+                        hipSuccess || hipEventRecord(ev[b], ts) != hipSuccess) err = 1;
+                drain();
+                pend = {(uint8_t*)pc.dst + a, n, b};
+                b ^= 1;
+            }
+        }
+        drain();
+        hipEventDestroy(ev[0]); hipEventDestroy(ev[1]);
+        hipStreamDestroy(ts);
+    });
+    return err ? CLY_ERR_DEVICE : CLY_OK;
+}
+
+// getNonMergeFileId (merge.go:240-255): the record at offset 0 of
+// merge-finished must read and its value be an integer.
+static int check_merge_finished(const char* dir) {
+    char path[4096];
+    snprintf(path, sizeof(path), "%s/merge-finished", dir);
+    Mapped m;
+    bool exists;
+    if (map_file(path, m, exists) != CLY_OK) return CLY_ERR_MERGE_FIN;
+    if (!exists) return CLY_OK;
+    int rc = CLY_OK;
+    const Hdr h = host_read_record(m.p, m.len, 0);
+    if (h.status == CLY_ERR_CRC) rc = CLY_ERR_CRC;                                 // ErrInvalidCRC
+    else if (h.status == CLY_ERR_TRUNC5 || h.status == CLY_ERR_VARINT) rc = h.status;    // the decode panics
+    else if (h.status != REC_OK) rc = CLY_ERR_MERGE_FIN;                           // io.EOF: an error here
+    else {
+        int64_t v;
+        if (!go_atoi((const char*)m.p + h.hsz + h.ks, h.vs, v)) rc = CLY_ERR_MERGE_FIN;
+    }
+    if (m.p) munmap((void*)m.p, m.len);
+    return rc;
+}
+
+// EncodeLogRecord (data/logRecord.go:57-84) of db.Del's tombstone for key:
+// {encodeKeyWithTxId(key, NO_TX_ID), LogRecordDeleted, String}
+static std::vector<uint8_t> tombstone(const uint8_t* key, uint64_t klen) {
+    std::vector<uint8_t> r(4 + 2 + 10 + 2 + 1 + klen);
+    uint8_t* p = r.data();
+    p[4] = 1; p[5] = 0;                                 // LogRecordDeleted, String
+    int n = 6;
+    n += ixk_put_varint((int64_t)klen + 1, p + n);      // key = 0x00 || key
+    n += ixk_put_varint(0, p + n);
+    n += ixk_put_varint(0, p + n);
+    p[n] = 0x00;
+    memcpy(p + n + 1, key, klen);
+    r.resize(n + 1 + klen);
+    const uint32_t c = host_crc(r.data() + 4, r.size() - 4);
+    r[0] = (uint8_t)c; r[1] = (uint8_t)(c >> 8); r[2] = (uint8_t)(c >> 16); r[3] = (uint8_t)(c >> 24);
+    return r;
+}
+
 extern "C" int cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load_stats* st) {
+    return cly_db_open_opts(ctx, dir, nullptr, out, st);
+}
+
+extern "C" int cly_db_open_opts(cly_ctx* ctx, const char* dir, const cly_db_options* opt, cly_db** out,
+                                cly_load_stats* st) {
     if (!ctx || !dir || !out) return CLY_ERR_ARG;
     *out = nullptr;
     cly_load_stats s;
     memset(&s, 0, sizeof(s));
+    const uint64_t dfs = opt && opt->data_file_size ? opt->data_file_size : (256ull << 20);
+    const bool apply = opt && (opt->flags & CLY_DB_APPLY_SWEEP);
     const double t0 = now_ms();
     cly_db* db = new cly_db();
     int rc = list_files(dir, db->files);
     const int nf = (int)db->files.size();
+    bool has_hint = false;
+    int nall = 0;                                // hint (file 0 when present) + data files
     uint8_t* d_bytes = nullptr;
     cly_tuple* d_tup = nullptr;
     uint8_t* d_state = nullptr;
-    std::vector<cly_file> hf(nf ? nf : 1), df(nf ? nf : 1);
-    std::vector<cly_file_result> res(nf ? nf : 1);
+    cly_pos* d_hpos = nullptr;
+    std::vector<cly_file> hf, df;
+    std::vector<cly_file_result> res;
+    std::vector<uint64_t> first;
     uint64_t total = 0, need = 0, cap = 0;
     hipStream_t strm = cly_ctx_stream_internal(ctx);
     double t1, t2, t3, t4, t5;
     cly_index_result ir;
     if (rc != CLY_OK) goto done;
+    {
+        char path[4096];
+        snprintf(path, sizeof(path), "%s/hint-index", dir);
+        if (map_file(path, db->hint, has_hint) != CLY_OK) { rc = CLY_ERR_ARG; goto done; }
+    }
+    if (nf) {
+        rc = check_merge_finished(dir);          // (loadIndex returns early without data files)
+        if (rc != CLY_OK) goto done;
+    }
     t1 = now_ms();
     s.list_map_ms = t1 - t0;
     s.n_files = (uint64_t)nf;
-    if (nf) s.active_fid = db->files[nf - 1].fid;
-    DCK(hipSetDevice(cly_ctx_device_internal(ctx)));
+    nall = nf + (has_hint ? 1 : 0);
+    hf.resize(nall ? nall : 1); df.resize(nall ? nall : 1); res.resize(nall ? nall : 1); first.resize(nall ? nall : 1);
+    if (has_hint) { hf[0].base = db->hint.p; hf[0].len = db->hint.len; hf[0].fid = 0; hf[0]._pad = 0; }
     for (int i = 0; i < nf; i++) {
-        hf[i].base = db->files[i].p; hf[i].len = db->files[i].len; hf[i].fid = db->files[i].fid;
-        total += (hf[i].len + 4095) & ~4095ull;
-        s.bytes += hf[i].len;
+        cly_file& f = hf[i + (has_hint ? 1 : 0)];
+        f.base = db->files[i].p; f.len = db->files[i].len; f.fid = db->files[i].fid; f._pad = 0;
+        s.bytes += f.len;
     }
+    for (int i = 0; i < nall; i++) total += (hf[i].len + 4095) & ~4095ull;
+    DCK(hipSetDevice(cly_ctx_device_internal(ctx)));
     DCK(hipMalloc((void**)&d_bytes, total + 4096));
-    {
-        // the files' pages are faulted in and copied by load_threads() threads,
-        // 64-MiB pieces each (pageable copies from several threads overlap)
-        struct Piece { const uint8_t* src; uint8_t* dst; uint64_t len; };
-        std::vector<Piece> pieces;
-        uint64_t off = 0;
-        for (int i = 0; i < nf; i++) {
-            df[i] = hf[i];
-            df[i].base = d_bytes + off;
-            for (uint64_t a = 0; a < hf[i].len; a += LOAD_PIECE)
-                pieces.push_back({hf[i].base + a, d_bytes + off + a, std::min<uint64_t>(LOAD_PIECE, hf[i].len - a)});
-            off += (hf[i].len + 4095) & ~4095ull;
-        }
-        std::atomic<size_t> next(0);
-        std::atomic<int> err(0);
-        const int dev = cly_ctx_device_internal(ctx);
-        const int nt = load_threads();
-        std::lock_guard<std::mutex> lk(g_stage_mu);
-        for (int k = 0; k < 2 * LOAD_THREADS_MAX; k++)          // (again after a failed allocation)
-            if (!g_stage[k] && hipHostMalloc(&g_stage[k], LOAD_STAGE, hipHostMallocPortable) != hipSuccess) {
-                g_stage[k] = nullptr;
-                err = 1;
-            }
-        if (err) { rc = CLY_ERR_DEVICE; goto done; }
-        par_run(nt, [&](int t) {
-            // thread t: pieces through its two page-locked staging buffers
-            // (CPU copy of one while the DMA of the other runs)
-            if (hipSetDevice(dev) != hipSuccess) { err = 1; return; }
-            hipStream_t ts = nullptr;
-            hipEvent_t ev[2] = {nullptr, nullptr};
-            if (hipStreamCreateWithFlags(&ts, hipStreamNonBlocking) != hipSuccess ||
-                hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) != hipSuccess) { err = 1; return; }
-            int b = 0;
-            bool used[2] = {false, false};
-            for (size_t k; (k = next.fetch_add(1)) < pieces.size();) {
-                const Piece& pc = pieces[k];
-                for (uint64_t a = 0; a < pc.len; a += LOAD_STAGE) {
-                    const uint64_t n = std::min<uint64_t>(LOAD_STAGE, pc.len - a);
-                    uint8_t* stg = (uint8_t*)g_stage[2 * t + b];
-                    if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) err = 1;
-                    memcpy(stg, pc.src + a, n);
-                    if (hipMemcpyAsync(pc.dst + a, stg, n, hipMemcpyHostToDevice, ts) != hipSuccess ||
-                        hipEventRecord(ev[b], ts) != hipSuccess) err = 1;
-                    used[b] = true;
-                    b ^= 1;
-                }
-            }
-            if (hipStreamSynchronize(ts) != hipSuccess) err = 1;
-            hipEventDestroy(ev[0]); hipEventDestroy(ev[1]);
-            hipStreamDestroy(ts);
-        });
-        if (err) { rc = CLY_ERR_DEVICE; goto done; }
-    }
+    rc = copy_to_device(ctx, hf, df, d_bytes);
+    if (rc != CLY_OK) goto done;
     t2 = now_ms();
     s.h2d_ms = t2 - t1;
-    cap = cly_scan_capacity(hf.data(), nf) + 16;
+    cap = cly_scan_capacity(hf.data(), nall) + 16;
     DCK(hipMalloc((void**)&d_tup, sizeof(cly_tuple) * cap));
-    db->first.resize(nf ? nf : 1);
-    rc = cly_scan_device(ctx, df.data(), nf, d_tup, cap, db->first.data(), res.data(), &need, nullptr, nullptr);
-    if (rc != CLY_OK) goto done;
-    for (int i = 0; i < nf; i++)
-        if (res[i].status < 0) { rc = res[i].status; goto done; }         // loadIndex returns the read error
-    if (nf) s.write_off = res[nf - 1].end_offset;                         // db.go:632-634
+    if (nall) {
+        rc = cly_scan_device(ctx, df.data(), nall, d_tup, cap, first.data(), res.data(), &need, nullptr, nullptr);
+        if (rc == CLY_ERR_CAPACITY && need > cap) {
+            // records shorter than 9 B: the exact need, scanned again
+            hipFree(d_tup); d_tup = nullptr;
+            cap = need + 16;
+            DCK(hipMalloc((void**)&d_tup, sizeof(cly_tuple) * cap));
+            rc = cly_scan_device(ctx, df.data(), nall, d_tup, cap, first.data(), res.data(), &need, nullptr, nullptr);
+        }
+        if (rc != CLY_OK) goto done;
+    }
+    for (int i = 0; i < nall; i++)
+        if (res[i].status < 0) { rc = res[i].status; goto done; }         // loadIndexFromHintFile / loadIndex return it
+    if (has_hint) {
+        db->n_hint = res[0].n_records;
+        s.hint_records = db->n_hint;
+        if (db->n_hint) {
+            uint64_t bad = 0;
+            DCK(hipMalloc((void**)&d_hpos, sizeof(cly_pos) * db->n_hint));
+            rc = cly_hint_positions_device(ctx, df[0].base, d_tup, db->n_hint, d_hpos, &bad, nullptr);
+            if (rc != CLY_OK) goto done;                                   // DecodeLogRecordPos panics
+            hipLaunchKernelGGL(k_hint_as_put, dim3((unsigned)((db->n_hint + 255) / 256)), dim3(256), 0, strm, d_tup,
+                               db->n_hint);
+            DCK(hipGetLastError());
+        }
+    }
+    if (nf) {
+        s.active_fid_loaded = db->files[nf - 1].fid;
+        s.write_off_loaded = res[nall - 1].end_offset;                    // db.go:632-634
+    }
     t3 = now_ms();
     s.scan_ms = t3 - t2;
     DCK(hipMalloc((void**)&d_state, need ? need : 1));
-    rc = cly_index_device(ctx, df.data(), nf, d_tup, db->first.data(), res.data(), d_state, &ir, nullptr);
-    if (rc != CLY_OK) goto done;
+    if (nall) {
+        rc = cly_index_device(ctx, df.data(), nall, d_tup, first.data(), res.data(), d_state, &ir, nullptr);
+        if (rc != CLY_OK) goto done;
+    }
     db->tuples.alloc(need);
     db->state.alloc(need);
     db->khash.alloc(need);
+    db->hint_pos.resize(db->n_hint);
     db->hmask = cly_ix_hash_mask_internal(need);
     db->hshift = 64 - __builtin_clzll(db->hmask | 15) - FLAT_SHARD_BITS;
     DCK(hipStreamSynchronize(strm));
     if (need) {
-        // tuples, states and key hashes back, in pieces from several threads
         uint64_t* d_hash = nullptr;
         DCK(cly_ix_hash_ptr_internal(ctx, need, (void**)&d_hash));
-        struct Piece { void* dst; const void* src; uint64_t len; };
-        std::vector<Piece> pieces;
-        auto add = [&](void* dst, const void* src, uint64_t len) {
-            for (uint64_t a = 0; a < len; a += LOAD_PIECE)
-                pieces.push_back({(uint8_t*)dst + a, (const uint8_t*)src + a, std::min<uint64_t>(LOAD_PIECE, len - a)});
-        };
-        add(db->tuples.data(), d_tup, sizeof(cly_tuple) * need);
-        add(db->state.data(), d_state, need);
-        add(db->khash.data(), d_hash, sizeof(uint64_t) * need);
-        std::atomic<size_t> next(0);
-        std::atomic<int> err(0);
-        const int dev = cly_ctx_device_internal(ctx);
-        std::lock_guard<std::mutex> lk(g_stage_mu);
-        par_run(load_threads(), [&](int t) {
-            // thread t: DMA into one staging buffer while the CPU copies the other out
-            if (hipSetDevice(dev) != hipSuccess) { err = 1; return; }
-            hipStream_t ts = nullptr;
-            if (hipStreamCreateWithFlags(&ts, hipStreamNonBlocking) != hipSuccess) { err = 1; return; }
-            struct Pend { uint8_t* dst; uint64_t n; int b; };
-            Pend pend = {nullptr, 0, 0};
-            hipEvent_t ev[2] = {nullptr, nullptr};
-            if (hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) != hipSuccess) { err = 1; return; }
-            int b = 0;
-            auto drain = [&]() {
-                if (!pend.dst) return;
-                if (hipEventSynchronize(ev[pend.b]) != hipSuccess) err = 1;
-                memcpy(pend.dst, g_stage[2 * t + pend.b], pend.n);
-                pend.dst = nullptr;
-            };
-            for (size_t k; (k = next.fetch_add(1)) < pieces.size();) {
-                const Piece& pc = pieces[k];
-                for (uint64_t a = 0; a < pc.len; a += LOAD_STAGE) {
-                    const uint64_t n = std::min<uint64_t>(LOAD_STAGE, pc.len - a);
-                    if (hipMemcpyAsync(g_stage[2 * t + b], (const uint8_t*)pc.src + a, n, hipMemcpyDeviceToHost, ts) !=
-                            hipSuccess || hipEventRecord(ev[b], ts) != hipSuccess) err = 1;
-                    drain();
-                    pend = {(uint8_t*)pc.dst + a, n, b};
-                    b ^= 1;
-                }
-            }
-            drain();
-            hipEventDestroy(ev[0]); hipEventDestroy(ev[1]);
-            hipStreamDestroy(ts);
-        });
-        if (err) { rc = CLY_ERR_DEVICE; goto done; }
+        std::vector<D2H> parts = {{db->tuples.data(), d_tup, sizeof(cly_tuple) * need},
+                                  {db->state.data(), d_state, need},
+                                  {db->khash.data(), d_hash, sizeof(uint64_t) * need}};
+        if (db->n_hint) parts.push_back({db->hint_pos.data(), d_hpos, sizeof(cly_pos) * db->n_hint});
+        rc = copy_to_host(ctx, parts);
+        if (rc != CLY_OK) goto done;
     }
     t4 = now_ms();
     s.index_ms = t4 - t3;
@@ -501,11 +687,43 @@ extern "C" int cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load
         for (auto& kv : db->list) s.list_items += kv.second.size();
         for (auto& kv : db->set) s.set_members += kv.second.size();
     }
+    {
+        // the TTL sweep's db.Del (db.go:639-651, 186-215): a tombstone per swept
+        // key appended by appendLogRecord's rule (db.go:368-413)
+        for (uint64_t i = db->n_hint; i < need; i++)
+            if (db->state[i] == CLY_IX_EXPIRED) db->expired.push_back(i);
+        s.n_expired = db->expired.size();
+        uint32_t afid = s.active_fid_loaded;
+        int64_t woff = s.write_off_loaded;
+        int fd = -1;
+        for (uint64_t i : db->expired) {
+            uint64_t kl;
+            const uint8_t* k = real_key_ptr(db, i, kl);
+            const std::vector<uint8_t> rec = tombstone(k, kl);
+            if ((uint64_t)woff + rec.size() > dfs) {                      // setActivityFile: fid + 1
+                afid++; woff = 0; s.sweep_files++;
+                if (fd >= 0) { close(fd); fd = -1; }
+            }
+            if (apply) {
+                if (fd < 0) {
+                    char path[4096];
+                    snprintf(path, sizeof(path), "%s/%09u.cly", dir, afid);
+                    fd = open(path, O_CREAT | O_RDWR | O_APPEND, 0644);    // driver/fileIO: O_APPEND
+                    if (fd < 0) { rc = CLY_ERR_ARG; goto done; }
+                }
+                if (write(fd, rec.data(), rec.size()) != (ssize_t)rec.size()) { close(fd); rc = CLY_ERR_ARG; goto done; }
+            }
+            woff += (int64_t)rec.size();
+        }
+        if (fd >= 0) close(fd);
+        s.active_fid = afid;
+        s.write_off = woff;
+    }
     t5 = now_ms();
     s.insert_ms = t5 - t4;
     s.total_ms = t5 - t0;
 done:
-    hipFree(d_bytes); hipFree(d_tup); hipFree(d_state);
+    hipFree(d_bytes); hipFree(d_tup); hipFree(d_state); hipFree(d_hpos);
     if (st) *st = s;
     if (rc != CLY_OK) { cly_db_close(db); return rc; }
     *out = db;
@@ -580,16 +798,84 @@ extern "C" int64_t cly_index_key(uint32_t dtype, const uint8_t* d, uint64_t n, u
     return (int64_t)k.plen + k.r_len;
 }
 
-// getLogRecordByPos (db.go:680-704): the record at pos, its value.  The CRC
-// was checked by the load; the header is decoded again here.
+// getLogRecordByPos (db.go:680-704): the record at pos (ReadLogRecord, CRC
+// included), its value; a LogRecordDeleted or an unknown fid is
+// ErrKeyNotFound.
 extern "C" int cly_db_value(cly_db* db, const cly_pos* pos, uint8_t* buf, uint64_t cap, uint64_t* vlen) {
     if (!db || !pos || !vlen) return CLY_ERR_ARG;
+    *vlen = 0;
     const Mapped* m = nullptr;
     for (const Mapped& f : db->files) if (f.fid == pos->fid) m = &f;
-    if (!m || pos->offset < 0 || (uint64_t)pos->offset >= m->len) return CLY_ERR_ARG;
-    const Hdr h = step_hdr(m->p, pos->offset, (int64_t)m->len, pos->offset);
-    if (h.status != REC_OK) return h.status;
+    if (!m) return CLY_DB_NOT_FOUND;                                  // dataFile == nil
+    if (pos->offset < 0) return CLY_ERR_OFFSET;                       // mmap ReadAt: invalid offset
+    const Hdr h = host_read_record(m->p, m->len, pos->offset);
+    if (h.status == CLY_END_EOF || h.status == CLY_END_ZERO || h.status == CLY_END_TORN) return CLY_DB_EOF;
+    if (h.status != REC_OK) return h.status;                          // ErrInvalidCRC, the panics
+    if (h.type == 1) return CLY_DB_NOT_FOUND;                         // LogRecordDeleted
     *vlen = h.vs;
     if (buf && cap >= h.vs) memcpy(buf, m->p + pos->offset + h.hsz + h.ks, h.vs);
     return (buf && cap < h.vs) ? CLY_ERR_CAPACITY : CLY_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Enumeration (cly_db_count / cly_db_entries), built on first use.
+static void build_entries(cly_db* db, int kind) {
+    std::vector<cly_db_entry>& v = db->it[kind];
+    v.clear();
+    auto flat = [&](const FlatIndex& xi, bool str) {
+        for (int sh = 0; sh < FLAT_SHARDS; sh++) {
+            const FlatShard& x = xi.sh[sh];
+            for (uint64_t i = 0; i <= x.mask && x.mask; i++) {
+                if (!x.h[i]) continue;
+                cly_db_entry e;
+                memset(&e, 0, sizeof(e));
+                e.key = real_key_ptr(db, x.ti[i], e.key_len);
+                e.pos = pos_of(db, x.ti[i]);
+                e.expiration = str && x.ti[i] >= db->n_hint ? db->tuples[x.ti[i]].expiration : 0;
+                v.push_back(e);
+            }
+        }
+    };
+    auto maps = [&](const std::unordered_map<std::string, std::unordered_map<std::string, cly_pos>>& m) {
+        for (const auto& kv : m)
+            for (const auto& sub : kv.second) {
+                cly_db_entry e;
+                memset(&e, 0, sizeof(e));
+                e.key = (const uint8_t*)kv.first.data(); e.key_len = kv.first.size();
+                e.sub = (const uint8_t*)sub.first.data(); e.sub_len = sub.first.size();
+                e.pos = sub.second;
+                v.push_back(e);
+            }
+    };
+    switch (kind) {
+        case CLY_IT_STRING: flat(db->str, true); break;
+        case CLY_IT_LISTMETA: flat(db->listmeta, false); break;
+        case CLY_IT_HASH: maps(db->hash); break;
+        case CLY_IT_LIST: maps(db->list); break;
+        case CLY_IT_SET: maps(db->set); break;
+        case CLY_IT_EXPIRED:
+            for (uint64_t i : db->expired) {
+                cly_db_entry e;
+                memset(&e, 0, sizeof(e));
+                e.key = real_key_ptr(db, i, e.key_len);
+                e.pos = pos_of(db, i);
+                e.expiration = db->tuples[i].expiration;
+                v.push_back(e);
+            }
+            break;
+    }
+    db->it_built[kind] = true;
+}
+extern "C" uint64_t cly_db_count(cly_db* db, int kind) {
+    if (!db || kind < 0 || kind > CLY_IT_EXPIRED) return 0;
+    if (!db->it_built[kind]) build_entries(db, kind);
+    return db->it[kind].size();
+}
+extern "C" uint64_t cly_db_entries(cly_db* db, int kind, uint64_t first, cly_db_entry* out, uint64_t n) {
+    if (!db || !out || kind < 0 || kind > CLY_IT_EXPIRED) return 0;
+    if (!db->it_built[kind]) build_entries(db, kind);
+    const std::vector<cly_db_entry>& v = db->it[kind];
+    uint64_t k = 0;
+    for (; k < n && first + k < v.size(); k++) out[k] = v[first + k];
+    return k;
 }

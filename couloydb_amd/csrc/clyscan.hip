@@ -28,7 +28,6 @@
 //            tiles whose guess the state contradicts are listed;
 //   k_refix  (only for listed tiles) re-runs the tile body from the true entry,
 //            then k_link again;
-//   k_fbase  tuple index of each file's first record;
 //   k_emit   per tile: the 48-B tuples from the compact entries (tiles with
 //            more records than the compact list holds re-run the body and
 //            write tuples directly); the tile register gets the one patch
@@ -100,9 +99,9 @@ struct TileLocal { u64 l[4]; };
 #define DF_REC 16ull
 #define DF_OVF 32ull
 
-#define LINK_ROUNDS 3            // link rounds launched per call without a host wait (more: host loop)
 struct Globals {                 // zeroed per call
-    uint32_t nfix[LINK_ROUNDS];  // tiles listed by k_link round r for k_refix round r + 1
+    uint32_t nfix[2];            // tiles listed by a k_link round (slot r & 1) for the next k_refix
+    uint32_t link_done;          // k_link workgroups finished (the last one computes the file bases)
     uint32_t overflow;           // tuples beyond out_cap were dropped
     uint32_t fail;               // internal invariant (never expected)
     uint32_t refix;              // tiles re-resolved over all rounds
@@ -450,6 +449,7 @@ __device__ __forceinline__ LBState ti_load(const TileIn* p) {
     s.count = ((uint64_t)a.y << 32) | a.x; s.X = a.z; s.dead = (a.w & TI_DEAD) != 0; s.crc_last = b.x; s.P_last = b.y;
     return s;
 }
+#define TI_FIX 2u                // listed for k_refix this round
 __device__ __forceinline__ void ti_store(TileIn* p, const LBState& s) {
     ((u32x4*)p)[0] = (u32x4){(uint32_t)s.count, (uint32_t)(s.count >> 32), s.X, s.dead ? TI_DEAD : 0u};
     ((u32x4*)p)[1] = (u32x4){s.crc_last, s.P_last, 0u, 0u};
@@ -585,6 +585,179 @@ __device__ __forceinline__ void patch_word(uint32_t (&w)[16], uint32_t k, uint32
 #define CLY_EXP 0                // timing experiments only (wrong results): 1 no record work, 3 candidate
 #endif                           // masks only, 2 no per-record outputs, 5 no agreement pass
 struct TileRes { uint32_t X; bool dead; };
+// The chain state a wave carries through its tile (wave-uniform).
+struct TState {
+    uint32_t X;                  // chain position (next boundary); NONE32: entry unknown (guess mode)
+    bool dead;                   // the chain has ended (terminal found)
+    bool cq_known;               // cq is the stored CRC before X (else: the tile's first boundary, deferred)
+    uint32_t cq;
+    uint32_t G, tcnt, last_crc, P_last;
+    int term;
+    uint32_t s_last, s_prev;     // sizes of the last two records (0: none yet)
+    uint32_t Tb;                 // terminal position in the current block (NONE32: none)
+    uint32_t tpatch;             // its patch word (XORed after the bytes from Tb on are zeroed)
+    uint32_t carry_next;         // register XOR due at the next block's first byte (terminal at the block end)
+};
+// The block's outputs for record k of a round (lane k), and its CRC patch XORed
+// into the stage word holding P (ds_xor: record starts are >= 6 B apart).
+template <int BM>
+__device__ __forceinline__ void rec_out(const DevFile& F, gbytes base, uint32_t p, const Hdr& h, uint32_t idx, uint32_t tb,
+                                        uint32_t bs, uint32_t dq, CLY_LDS uint32_t* stg, const CLY_LDS uint8_t* smem,
+                                        const CrcLane& cl, uint32_t K4, uint32_t* trec, gtuples out, uint64_t out_cap,
+                                        uint64_t gbase, Globals* g) {
+    if (BM == BM_EMIT) put_tuple(out, gbase + idx, out_cap, base, p, h, F.fid, g);
+    else {
+        if (idx < CAP_T) rec_store(trec + 4 * idx, h, p - tb);
+        const uint32_t d = h.crc ^ K4 ^ dq;
+        stg[(p - bs) >> 2] ^= crc_unbytes(smem, d, p & 3u, cl.r4);   // one writer per word (starts are >= 6 B apart)
+    }
+}
+// The terminal T (found by lane src): the bytes from T on read as zero, and
+// ~cq of the record before it (dT) is XORed in before byte T (into the word
+// holding T, after the zeroing), or at the next block's first byte when T is
+// the block's end.
+template <int BM>
+__device__ __forceinline__ void term_patch(TState& S, uint32_t T, uint32_t dT, uint32_t bs, const CLY_LDS uint8_t* smem,
+                                           const CrcLane& cl, int src) {
+    S.Tb = T;
+    if (BM == BM_EMIT) return;
+    if (T < bs + CLY_BLK) S.tpatch = rdl(crc_unbytes(smem, dT, T & 3u, cl.r4), src);
+    else S.carry_next = rdl(dT, src);
+}
+
+// Exact predictive walk (entry X known and in this block): lane k decodes the
+// header at the position the last two record sizes predict for the k-th record
+// from X (sizes alternating b, a, b, ... with a = the last size, b = the one
+// before).  Lanes 0 .. kb-1 whose sizes match the prediction are records of the
+// chain, and so is lane kb (the first mismatch) when its header is a record:
+// its true size gives the next X; a terminal at kb ends the chain.  Every round
+// is exact and advances by at least one record.  Returns false when the round
+// budget runs out with X still in the block (the caller's general pass goes on).
+template <int BM>
+__device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t tb, uint32_t bs, CLY_LDS uint32_t* stg,
+                                          const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t K4, uint32_t* trec,
+                                          gtuples out, uint64_t out_cap, uint64_t gbase, Globals* g, int lane) {
+    const gbytes base = (gbytes)F.base;
+    const uint64_t flen = F.len, bend = (uint64_t)bs + CLY_BLK;
+    for (int round = 0; round < 4; round++) {
+        const uint64_t X = S.X;
+        const bool owned = X < bend || (X == flen && flen == bend);
+        if (S.dead || !owned) return true;
+        uint32_t a = S.s_last, b = S.s_prev ? S.s_prev : S.s_last;
+        if (!a) {                                  // no size yet: the record at X sets the stride
+            const Hdr h0 = hdr_get(base, (uint32_t)X, flen, stg, bs);
+            a = b = h0.status == REC_OK ? (uint32_t)h0.size : 64u;
+        }
+        const uint32_t k = (uint32_t)lane;
+        const uint64_t P = X + (uint64_t)((k + 1) >> 1) * b + (uint64_t)(k >> 1) * a;
+        const bool act = P < bend || (P == flen && flen == bend);
+        Hdr h;
+        h.status = CLY_END_EOF; h.size = 0; h.crc = 0;
+        if (act) h = hdr_get(base, (uint32_t)P, flen, stg, bs);
+        const uint32_t expect = (k & 1) ? a : b;
+        const bool rec = act && h.status == REC_OK;
+        const u64 brk = __ballot(!(rec && (uint64_t)h.size == expect));
+        const int kb = brk ? __ffsll((long long)brk) - 1 : 64;
+        const bool acc = (int)k < kb || ((int)k == kb && rec);
+        const u64 ba = __ballot(acc);
+        const int n = __popcll(ba);
+        // the stored CRC of each record's predecessor
+        const uint32_t up = dppu<DPP_WF_SR1>(0u, h.crc);
+        const uint32_t dq = k == 0 ? (S.cq_known ? ~S.cq : 0xFFFFFFFFu) : ~up;
+        if (acc) rec_out<BM>(F, base, (uint32_t)P, h, S.tcnt + k, tb, bs, P == 0 ? 0u : dq, stg, smem, cl, K4, trec, out,
+                              out_cap, gbase, g);
+        if (S.G == NONE32) S.G = (uint32_t)X;
+        if (n) {
+            const int kl = n - 1;
+            S.last_crc = rdl(h.crc, kl);
+            S.P_last = rdl((uint32_t)P, kl);
+            const uint32_t sl = rdl((uint32_t)h.size, kl);
+            S.s_prev = kl ? rdl((uint32_t)h.size, kl - 1) : S.s_last;
+            S.s_last = sl;
+            S.cq = S.last_crc; S.cq_known = true;
+            S.X = S.P_last + sl;
+            S.tcnt += (uint32_t)n;
+        }
+        if (kb < 64 && !((ba >> kb) & 1ull) && ((__ballot(act) >> kb) & 1ull)) {
+            // lane kb is the chain's terminal (its header is not a record)
+            const int st = (int)rdl((uint32_t)h.status, kb);
+            {
+                const uint32_t T = rdl((uint32_t)P, kb);
+                const uint32_t dT = T == 0 ? 0u : rdl(dq, kb);
+                term_patch<BM>(S, T, dT, bs, smem, cl, kb);
+                S.X = T; S.dead = true; S.term = st;
+                return true;
+            }
+        }
+    }
+    const uint64_t X = S.X;
+    return S.dead || !(X < bend || (X == flen && flen == bend));
+}
+
+// Guess mode (a tile other than its file's first, entry unknown): every
+// lane's first candidate record start in its 64-B segment whose speculative
+// walk holds, validated at the walk's exit (a candidate of the block, or a
+// plausible header beyond it).  The tile's guessed entry G is the first such
+// start whose exit was confirmed inside the block, else the first such start;
+// NONE32 when the block holds none.  k_link checks the guess.
+__device__ __forceinline__ uint32_t guess_entry(const DevFile& F, uint32_t bs, CLY_LDS uint32_t* stg, const u32x4& hc,
+                                                int lane) {
+    const CLY_LDS u32x4* sv = (const CLY_LDS u32x4*)stg;
+    const gbytes base = (gbytes)F.base;
+    const uint64_t flen = F.len;
+    const Seg K = make_seg(F, bs, lane, stg);
+    uint32_t wv[16];
+    #pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const u32x4 v = sv[4 * lane + k];
+        wv[4 * k] = v.x; wv[4 * k + 1] = v.y; wv[4 * k + 2] = v.z; wv[4 * k + 3] = v.w;
+    }
+    const uint32_t n0 = dppu<DPP_WF_SL1>(rdl(hc.x, 0), wv[0]), n1 = dppu<DPP_WF_SL1>(rdl(hc.y, 0), wv[1]);
+    u64 cm = 0;
+    if (K.on) {
+        cm = cand_mask(wv, n0, n1);
+        const uint32_t nv = K.ce - K.cb;                    // valid positions
+        if (nv < 64) cm &= (1ull << nv) - 1ull;
+    }
+    uint32_t E = NONE32;
+    bool conf_in = false;
+    u64 mm = cm;
+    bool settled = !K.on || !mm;
+    for (int tr = 0; tr < 4; tr++) {
+        const bool act = !settled;
+        if (!__ballot(act)) break;
+        SegChain T;
+        sc_set(T, LM_NONE);
+        bool ok = false;
+        if (act) {
+            const uint32_t q = K.cb + (uint32_t)__builtin_ctzll(mm);
+            mm &= mm - 1;
+            ok = seg_walk(K, q, false, T);
+        }
+        const bool chk_in = act && ok && T.term == TERM_NONE && T.x < bs + CLY_BLK;
+        const uint32_t off = chk_in ? T.x - bs : 0u;
+        const int tl = (int)(off >> 6);
+        const uint32_t clo = shfl_u32((uint32_t)cm, tl), chi = shfl_u32((uint32_t)(cm >> 32), tl);
+        bool in = act && ok && T.term != TERM_NONE;          // walk ended at io.EOF at len
+        if (act && ok && T.term == TERM_NONE) {
+            if (chk_in) {
+                const uint32_t bb = off & 63u;
+                ok = (((bb < 32 ? clo >> bb : chi >> (bb - 32))) & 1u) != 0;
+                in = ok;
+            } else {
+                const Hdr eh = hdr_get(base, T.x, flen, stg, bs);
+                ok = (eh.status == REC_OK && eh.good) || eh.status == CLY_END_ZERO ||
+                     (eh.status == CLY_END_EOF && (uint64_t)T.x == flen);
+            }
+        }
+        if (act && ok) { E = T.E; conf_in = in; settled = true; }
+        if (act && !ok && !mm) settled = true;
+    }
+    const u64 bin = __ballot(E != NONE32 && conf_in), ball = __ballot(E != NONE32);
+    if (!ball) return NONE32;
+    return rdl(E, __ffsll((long long)(bin ? bin : ball)) - 1);
+}
+
 template <int BM>
 __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint32_t tt, uint32_t X_in, bool dead_in,
                                              const CLY_LDS uint8_t* smem, CLY_LDS uint32_t* stg, const CrcLane& cl,
@@ -595,184 +768,161 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     const uint64_t flen = F.len;
     const gbytes base = (gbytes)F.base;
     const bool known0 = BM != BM_SPEC || tt == 0;
-    uint32_t X = tt == 0 ? 0u : (known0 ? X_in : NONE32);      // NONE32: entry unknown (BM_SPEC guess mode)
-    bool dead = tt != 0 && known0 && dead_in;
-    bool cq_known = tt == 0;     // the stored CRC before X is known (tile 0: no record before offset 0)
-    uint32_t cq = 0;
-    uint32_t G = NONE32, tcnt = 0, last_crc = 0, P_last = NONE32;
-    int term = TERM_NONE;
-    uint32_t R = 0, carry = 0;   // carry: register XOR due at the next block's first byte (T = block end)
+    TState S;
+    S.X = tt == 0 ? 0u : (known0 ? X_in : NONE32);
+    S.dead = tt != 0 && known0 && dead_in;
+    S.cq_known = tt == 0;        // tile 0: no record before offset 0
+    S.cq = 0; S.G = NONE32; S.tcnt = 0; S.last_crc = 0; S.P_last = NONE32; S.term = TERM_NONE;
+    S.s_last = 0; S.s_prev = 0; S.Tb = NONE32; S.tpatch = 0; S.carry_next = 0;
+    uint32_t R = 0, carry = 0;   // carry: register XOR due at this block's first byte
     const CLY_LDS uint32_t* nibt = (const CLY_LDS uint32_t*)(smem + LDS_NIB);
     uint32_t* trec = rec + (uint64_t)t * CAP_T * 4;
+    CLY_LDS u32x4* sv = (CLY_LDS u32x4*)stg;
     u32x4 e[4], hl;
     blk_issue(base, flen, tb, lane, e, hl);
     #pragma unroll 1
     for (int m = 0; m < CLY_NBLK; m++) {
         const uint32_t bs = tb + (uint32_t)m * CLY_BLK;
+        const uint64_t bend = (uint64_t)bs + CLY_BLK;
         quad_transpose(e);
         uint32_t w[16];
         #pragma unroll
         for (int k = 0; k < 4; k++) { w[4 * k] = e[k].x; w[4 * k + 1] = e[k].y; w[4 * k + 2] = e[k].z; w[4 * k + 3] = e[k].w; }
         const u32x4 hc = hl;
-        if (m + 1 < CLY_NBLK && (BM != BM_EMIT || !dead)) blk_issue(base, flen, bs + CLY_BLK, lane, e, hl);
-        if (BM == BM_EMIT && dead) break;
-        uint32_t pend = 0;
-        const bool owned = X != NONE32 && (X < bs + CLY_BLK || ((uint64_t)X == flen && flen == (uint64_t)bs + CLY_BLK));
-        if (dead) {
+        if (m + 1 < CLY_NBLK && (BM != BM_EMIT || !S.dead)) blk_issue(base, flen, bs + CLY_BLK, lane, e, hl);
+        if (BM == BM_EMIT && S.dead) break;
+        S.Tb = NONE32;
+        const bool owned = S.X != NONE32 && ((uint64_t)S.X < bend || ((uint64_t)S.X == flen && flen == bend));
+        if (S.dead) {
             #pragma unroll
             for (int k = 0; k < 16; k++) w[k] = 0;
-        } else if (CLY_EXP != 1 && (X == NONE32 || owned)) {
-            // ---- record starts of the block; the headers are read from the
-            // wave's LDS copy of it (the stage)
-            {
-                CLY_LDS u32x4* sv = (CLY_LDS u32x4*)stg;
+        } else if (CLY_EXP != 1 && (S.X == NONE32 || owned)) {
+            // ---- record starts of the block; headers are read from the wave's
+            // LDS copy of it (the stage), patches XORed into the stage
+            #pragma unroll
+            for (int k = 0; k < 4; k++) sv[4 * lane + k] = (u32x4){w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
+            if (lane < 4) sv[CLY_BLK / 16 + lane] = hc;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (S.X == NONE32) S.X = guess_entry(F, bs, stg, hc, lane);     // the tile's guessed entry
+            bool done = true;
+            if (S.X != NONE32) done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, trec, out, out_cap, gbase, g, lane);
+            if (!done) {
+                // ---- general pass (the predictive walk's round budget ran out):
+                // every lane's first candidate record start in its 64-B segment
+                // after X, then agreement
+                const Seg K = make_seg(F, bs, lane, stg);
+                uint32_t wv[16];
                 #pragma unroll
-                for (int k = 0; k < 4; k++) sv[4 * lane + k] = (u32x4){w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
-                if (lane < 4) sv[CLY_BLK / 16 + lane] = hc;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
-            const Seg K = make_seg(F, bs, lane, stg);
-            const uint32_t n0 = dppu<DPP_WF_SL1>(rdl(hc.x, 0), w[0]), n1 = dppu<DPP_WF_SL1>(rdl(hc.y, 0), w[1]);
-            u64 cm = 0;
-            if (K.on) {
-                cm = cand_mask(w, n0, n1);
-                const uint32_t nv = K.ce - K.cb;                    // valid positions
-                if (nv < 64) cm &= (1ull << nv) - 1ull;
-            }
-            if (CLY_EXP == 3) { w[0] ^= (uint32_t)cm ^ (uint32_t)(cm >> 32); X = bs + CLY_BLK + 100; G = tb; }
-            else {
-            SegChain L;
-            if (!K.on) sc_set(L, LM_OFF);
-            else if (X != NONE32) {
-                if (in_seg(K, X)) seg_walk(K, X, true, L);
+                for (int k = 0; k < 4; k++) {
+                    const u32x4 v = sv[4 * lane + k];
+                    wv[4 * k] = v.x; wv[4 * k + 1] = v.y; wv[4 * k + 2] = v.z; wv[4 * k + 3] = v.w;
+                }
+                const uint32_t n0 = dppu<DPP_WF_SL1>(rdl(hc.x, 0), wv[0]), n1 = dppu<DPP_WF_SL1>(rdl(hc.y, 0), wv[1]);
+                u64 cm = 0;
+                if (K.on) {
+                    cm = cand_mask(wv, n0, n1);
+                    const uint32_t nv = K.ce - K.cb;                    // valid positions
+                    if (nv < 64) cm &= (1ull << nv) - 1ull;
+                }
+                SegChain L;
+                const uint32_t X = S.X;
+                if (!K.on) sc_set(L, LM_OFF);
+                else if (in_seg(K, X)) seg_walk(K, X, true, L);
                 else if (X > K.cb) sc_set(L, LM_NONE);
                 else {
                     sc_set(L, LM_NONE);
                     if (cm) { SegChain T; if (seg_walk(K, K.cb + (uint32_t)__builtin_ctzll(cm), false, T)) L = T; }
                 }
-            } else {
-                // guess mode: the first candidate whose walk holds and whose exit
-                // is a candidate of the block (or a plausible header beyond it)
-                sc_set(L, K.on ? LM_NONE : LM_OFF);
-                u64 mm = cm;
-                bool settled = !K.on || !mm;
-                for (int tr = 0; tr < 4; tr++) {
-                    const bool act = !settled;
-                    if (!__ballot(act)) break;
-                    SegChain T;
-                    sc_set(T, LM_NONE);
-                    bool ok = false;
-                    if (act) {
-                        const uint32_t q = K.cb + (uint32_t)__builtin_ctzll(mm);
-                        mm &= mm - 1;
-                        ok = seg_walk(K, q, false, T);
-                    }
-                    const bool chk_in = act && ok && T.term == TERM_NONE && T.x < bs + CLY_BLK;
-                    const uint32_t off = chk_in ? T.x - bs : 0u;
-                    const int tl = (int)(off >> 6);
-                    const uint32_t clo = shfl_u32((uint32_t)cm, tl), chi = shfl_u32((uint32_t)(cm >> 32), tl);
-                    if (act && ok && T.term == TERM_NONE) {
-                        if (chk_in) {
-                            const uint32_t b = off & 63u;
-                            ok = (((b < 32 ? clo >> b : chi >> (b - 32))) & 1u) != 0;
-                        } else {
-                            const Hdr eh = hdr_get(base, T.x, flen, stg, bs);
-                            ok = (eh.status == REC_OK && eh.good) || eh.status == CLY_END_ZERO ||
-                                 (eh.status == CLY_END_EOF && (uint64_t)T.x == flen);
+                {
+                    if (CLY_EXP != 5) L = seg_resolve(K, L, lane, X, g);
+                    // the first terminal ends the chain: the lanes after it are dead
+                    const u64 bt = __ballot(L.mode == LM_CHAIN && L.term != TERM_NONE);
+                    const int kT = bt ? __ffsll((long long)bt) - 1 : 64;
+                    if (lane > kT && L.mode != LM_OFF) sc_set(L, LM_DEAD);
+                    const bool isC = L.mode == LM_CHAIN;
+                    const uint32_t c = isC ? L.cnt : 0u;
+                    const uint32_t incl = wave_add_incl(c);
+                    const uint32_t bcnt = rdl(incl, 63), lex = incl - c;
+                    // the stored CRC of the record before the lane's first one
+                    uint32_t lv = L.last_crc, lf = c > 0 ? 1u : 0u;
+                    wave_last_incl(lv, lf);
+                    const uint32_t lvp = dppu<DPP_WF_SR1>(0u, lv), lfp = dppu<DPP_WF_SR1>(0u, lf);
+                    uint32_t pcq = lfp ? lvp : S.cq;
+                    bool pk = lfp ? true : S.cq_known;
+                    // the lane's records: outputs and CRC patches (headers from the stage)
+                    uint32_t p = L.E, psz = 0, ppsz = 0;
+                    for (uint32_t i = 0; CLY_EXP != 2 && __ballot(i < c); i++) {
+                        if (i < c) {
+                            const Hdr h = hdr_get(base, p, flen, stg, bs);
+                            rec_out<BM>(F, base, p, h, S.tcnt + lex + i, tb, bs, p == 0 ? 0u : (pk ? ~pcq : 0xFFFFFFFFu),
+                                        stg, smem, cl, K4, trec, out, out_cap, gbase, g);
+                            pcq = h.crc; pk = true;
+                            ppsz = psz; psz = (uint32_t)h.size;
+                            p += (uint32_t)h.size;
                         }
                     }
-                    if (act && ok) { L = T; settled = true; }
-                    if (act && !ok && !mm) settled = true;
-                }
-            }
-            uint32_t X0 = X;
-            bool any = true;
-            if (X == NONE32) {
-                const u64 bc = __ballot(L.mode == LM_CHAIN);
-                any = bc != 0;
-                if (any) X0 = rdl(L.E, __ffsll((long long)bc) - 1);
-            }
-            if (any) {
-                if (CLY_EXP != 5) L = seg_resolve(K, L, lane, X0, g);
-                // the first terminal ends the chain: the lanes after it are dead
-                const u64 bt = __ballot(L.mode == LM_CHAIN && L.term != TERM_NONE);
-                const int kT = bt ? __ffsll((long long)bt) - 1 : 64;
-                if (lane > kT && L.mode != LM_OFF) sc_set(L, LM_DEAD);
-                const bool isC = L.mode == LM_CHAIN;
-                const uint32_t c = isC ? L.cnt : 0u;
-                const uint32_t incl = wave_add_incl(c);
-                const uint32_t bcnt = rdl(incl, 63), lex = incl - c;
-                // the stored CRC of the record before the lane's first one
-                uint32_t lv = L.last_crc, lf = c > 0 ? 1u : 0u;
-                wave_last_incl(lv, lf);
-                const uint32_t lvp = dppu<DPP_WF_SR1>(0u, lv), lfp = dppu<DPP_WF_SR1>(0u, lf);
-                uint32_t pcq = lfp ? lvp : cq;
-                bool pk = lfp ? true : cq_known;
-                // the lane's records: outputs and CRC patches (headers from the stage)
-                uint32_t p = L.E;
-                for (uint32_t i = 0; CLY_EXP != 2 && __ballot(i < c); i++) {
-                    if (i < c) {
-                        const Hdr h = hdr_get(base, p, flen, stg, bs);
-                        const uint32_t idx = tcnt + lex + i;
-                        if (BM == BM_EMIT) put_tuple(out, gbase + idx, out_cap, base, p, h, F.fid, g);
-                        else {
-                            if (idx < CAP_T) rec_store(trec + 4 * idx, h, p - tb);
-                            const uint32_t d = h.crc ^ K4 ^ (p == 0 ? 0u : (pk ? ~pcq : 0xFFFFFFFFu));
-                            patch_word(w, (p - K.cb) >> 2, crc_unbytes(smem, d, p & 3u, cl.r4));
-                        }
-                        pcq = h.crc; pk = true;
-                        p += (uint32_t)h.size;
-                    }
-                }
-                if (BM != BM_EMIT) {
-                    if (lane == kT) {
-                        const uint32_t T = L.x;
+                    if (kT < 64) {
+                        const uint32_t T = rdl(L.x, kT);
                         const uint32_t dT = T == 0 ? 0u : (pk ? ~pcq : 0xFFFFFFFFu);
-                        #pragma unroll
-                        for (int k = 0; k < 16; k++) {
-                            const uint32_t a = K.cb + 4u * k;
-                            if (a >= T) w[k] = 0;
-                            else if (a + 4 > T) w[k] &= (1u << (8 * (T - a))) - 1u;
-                        }
-                        if (T < K.cb + CLY_SEG) patch_word(w, (T - K.cb) >> 2, crc_unbytes(smem, dT, T & 3u, cl.r4));
-                        else pend = dT;                         // T = len = the segment's end
+                        term_patch<BM>(S, T, dT, bs, smem, cl, kT);
                     }
-                    if (lane > kT) {
-                        #pragma unroll
-                        for (int k = 0; k < 16; k++) w[k] = 0;
+                    // the chain after the block
+                    if (bcnt) {
+                        const u64 br = __ballot(c > 0);
+                        const int lr = 63 - __clzll((long long)br);
+                        S.last_crc = rdl(L.last_crc, lr);
+                        S.P_last = rdl(L.last, lr);
+                        S.cq = S.last_crc; S.cq_known = true;
+                        // sizes of the last two records (the one before may be in an earlier lane)
+                        const uint32_t cl_ = rdl(c, lr);
+                        S.s_last = rdl(psz, lr);
+                        S.s_prev = cl_ >= 2 ? rdl(ppsz, lr) : (bcnt >= 2 ? 0u : S.s_last);
                     }
-                }
-                // the chain after the block
-                if (bcnt) {
-                    const u64 br = __ballot(c > 0);
-                    const int lr = 63 - __clzll((long long)br);
-                    last_crc = rdl(L.last_crc, lr);
-                    P_last = rdl(L.last, lr);
-                    cq = last_crc; cq_known = true;
-                }
-                tcnt += bcnt;
-                const u64 bcc = __ballot(isC);
-                if (bcc) {
-                    if (G == NONE32) G = rdl(L.E, __ffsll((long long)bcc) - 1);
-                    X = rdl(L.x, 63 - __clzll((long long)bcc));
-                    if (bt) { dead = true; term = (int)rdl((uint32_t)L.term, kT); }
+                    S.tcnt += bcnt;
+                    const u64 bcc = __ballot(isC);
+                    if (bcc) {
+                        if (S.G == NONE32) S.G = rdl(L.E, __ffsll((long long)bcc) - 1);
+                        S.X = rdl(L.x, 63 - __clzll((long long)bcc));
+                        if (bt) { S.dead = true; S.term = (int)rdl((uint32_t)L.term, kT); }
+                    }
                 }
             }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (BM != BM_EMIT) {
+                #pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const u32x4 v = sv[4 * lane + k];
+                    w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+                }
             }
         }
         if (BM != BM_EMIT) {
-            // the register XOR of a terminal at a segment's end goes to the next
-            // segment's first word (the next block's, or the tile end)
-            w[0] ^= dppu<DPP_WF_SR1>(carry, pend);
-            carry = rdl(pend, 63);
+            // bytes from the terminal on read as zero
+            if (S.Tb != NONE32) {
+                const uint32_t cb = bs + 64u * (uint32_t)lane, T = S.Tb;
+                #pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const uint32_t a = cb + 4u * k;
+                    if (a >= T) w[k] = 0;
+                    else if (a + 4 > T) w[k] &= (1u << (8 * (T - a))) - 1u;
+                }
+                if ((uint64_t)T < bend) {
+                    const uint32_t wi = ((T & ~3u) - bs) >> 2;
+                    if ((uint32_t)lane == (wi >> 4)) patch_word(w, wi & 15u, S.tpatch);
+                }
+            }
+            if (lane == 0) w[0] ^= carry;
+            carry = S.carry_next;
+            S.carry_next = 0;
             if (m) R = mat_mul(nibt + 6 * 128, R);
             #pragma unroll
             for (int k = 0; k < 16; k++) R = crc_word(smem, R ^ w[k], cl);
         }
     }
     TileRes res;
-    res.X = X; res.dead = dead;
+    res.X = S.X; res.dead = S.dead;
     if (BM != BM_EMIT) {
         // fold of the lanes' registers to the tile end: sum over l of A^(64 (63 - l)) R_l
         uint32_t r = R;
@@ -787,17 +937,17 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
             treg[t] = r ^ carry;
             const uint64_t tstart = tb;
             const uint32_t tend = tstart + CLY_TILE >= flen ? (uint32_t)(flen + 1) : (uint32_t)(tstart + CLY_TILE);
-            u64 f0 = (u64)tcnt << 32;
-            if (term != TERM_NONE) f0 |= DF_TERM;
-            if (G == NONE32) f0 |= DF_NONE;
+            u64 f0 = (u64)S.tcnt << 32;
+            if (S.term != TERM_NONE) f0 |= DF_TERM;
+            if (S.G == NONE32) f0 |= DF_NONE;
             if (tt == 0) f0 |= DF_FOF;
-            if (P_last != NONE32) f0 |= DF_REC;
-            if (tcnt > CAP_T) f0 |= DF_OVF;
+            if (S.P_last != NONE32) f0 |= DF_REC;
+            if (S.tcnt > CAP_T) f0 |= DF_OVF;
             TileLocal* d = &loc[t];
             d->l[0] = f0;
-            d->l[1] = (u64)G | ((u64)X << 32);
-            d->l[2] = (u64)last_crc | ((u64)P_last << 32);
-            d->l[3] = (u64)tend | ((u64)(uint8_t)(int8_t)term << 32);
+            d->l[1] = (u64)S.G | ((u64)S.X << 32);
+            d->l[2] = (u64)S.last_crc | ((u64)S.P_last << 32);
+            d->l[3] = (u64)tend | ((u64)(uint8_t)(int8_t)S.term << 32);
         }
     }
     return res;
@@ -848,10 +998,14 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
 // Kogge-Stone scan over the threads' functions gives every run its entering
 // state, and each thread re-applies its run from there, writing TileIn and
 // checking the LOCALs against it: a chain tile entered live at X != G, or a
-// tile without boundaries entered live at X < its end, is contradicted; the
-// first contradicted tile of the file (the only one whose entry is certain)
-// is listed for k_refix.  Round r > 0 runs only if round r-1 listed tiles.
+// tile without boundaries entered live at X < its end, is contradicted.  A
+// contradicted tile whose predecessor is not contradicted is listed for
+// k_refix (its entry X is the predecessor's own exit; a wrong guess rarely
+// spoils more than its own tile).  The workgroup that finishes last also
+// computes every file's first tuple index (exclusive prefix over the files'
+// record totals) and the call's total.
 #define LINK_NT 1024
+#define LINK_MAXT 8192           // tiles per file tracked in the contradiction bitmask (512 MiB files)
 #define RF_ID 0
 #define RF_CONST 1
 #define RF_FOF 2
@@ -885,11 +1039,14 @@ __device__ __forceinline__ LBState rf_apply(const RunF& f, LBState s) {
 }
 #define LINK_PER 4               // tiles per thread held in registers (more: re-read)
 __global__ void __launch_bounds__(LINK_NT)
-k_link(const DevFile* __restrict__ files, const TileLocal* __restrict__ loc, TileIn* tin, uint64_t* ftotal,
-       uint32_t* fixlist, Globals* g, int round) {
-    if (round > 0 && g->nfix[round - 1] == 0) return;      // nothing changed since the last round
+k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restrict__ loc, TileIn* tin,
+       uint64_t* ftotal, FileInfo* finfo, uint32_t* fixlist, Globals* g, int slot) {
     __shared__ RunF rf[2][LINK_NT];
-    __shared__ uint32_t first_bad;
+    __shared__ uint32_t badm[LINK_MAXT / 32];
+    __shared__ uint32_t bad_far;             // a contradicted tile beyond the bitmask (listed alone)
+    __shared__ uint64_t part[LINK_NT];
+    __shared__ uint64_t carry;
+    __shared__ int last;
     const int f = blockIdx.x, tid = threadIdx.x;
     const DevFile F = files[f];
     const uint32_t nt = F.ntile, per = (nt + LINK_NT - 1) / LINK_NT;
@@ -910,7 +1067,8 @@ k_link(const DevFile* __restrict__ files, const TileLocal* __restrict__ loc, Til
     // inclusive Kogge-Stone scan of the run functions
     int cur = 0;
     rf[0][tid] = my;
-    if (tid == 0) first_bad = NONE32;
+    for (int i = tid; i < LINK_MAXT / 32; i += LINK_NT) badm[i] = 0;
+    if (tid == 0) bad_far = NONE32;
     __syncthreads();
     for (int d = 1; d < LINK_NT; d <<= 1) {
         RunF v = rf[cur][tid];
@@ -927,7 +1085,6 @@ k_link(const DevFile* __restrict__ files, const TileLocal* __restrict__ loc, Til
         s0.count = 0; s0.X = 0; s0.crc_last = 0; s0.P_last = NONE32; s0.dead = 0;
         ftotal[f] = rf_apply(rf[cur][tid], s0).count;
     }
-    bool stop = false;
     auto visit = [&](uint32_t u, u64 l0, u64 l1, u64 l2, u64 l3) {
         bool bad = false;
         if (l0 & DF_FOF) { s.count = 0; s.X = 0; s.dead = 0; s.crc_last = 0; s.P_last = NONE32; }
@@ -936,63 +1093,87 @@ k_link(const DevFile* __restrict__ files, const TileLocal* __restrict__ loc, Til
             else bad = s.X != (uint32_t)l1;
         }
         ti_store(&tin[F.first_tile + u], s);
-        if (bad) { atomicMin(&first_bad, F.first_tile + u); stop = true; return; }   // the state after it is not known
+        if (bad) {
+            if (u < LINK_MAXT) atomicOr(&badm[u >> 5], 1u << (u & 31));
+            else atomicMin(&bad_far, u);
+        }
         s = rf_apply(rf_tile(l0, l1, l2), s);
     };
     #pragma unroll
     for (int k = 0; k < LINK_PER; k++)
-        if (!stop && lo + k < hi) visit(lo + k, c0[k], c1[k], c2[k], c3[k]);
-    for (uint32_t u = lo + LINK_PER; u < hi && !stop; u++) visit(u, L0[u].l[0], L0[u].l[1], L0[u].l[2], L0[u].l[3]);
+        if (lo + k < hi) visit(lo + k, c0[k], c1[k], c2[k], c3[k]);
+    for (uint32_t u = lo + LINK_PER; u < hi; u++) visit(u, L0[u].l[0], L0[u].l[1], L0[u].l[2], L0[u].l[3]);
     __syncthreads();
-    if (tid == 0 && first_bad != NONE32) {
-        const uint32_t k = atomicAdd(&g->nfix[round], 1u);
-        fixlist[k] = first_bad;
+    // list the contradicted tiles whose predecessor is not contradicted
+    for (uint32_t u = lo; u < hi && u < LINK_MAXT; u++) {
+        const bool bu = (badm[u >> 5] >> (u & 31)) & 1u;
+        const bool bp = u > 0 && ((badm[(u - 1) >> 5] >> ((u - 1) & 31)) & 1u);
+        if (bu && !bp) {
+            const uint32_t k = atomicAdd(&g->nfix[slot], 1u);
+            fixlist[k] = F.first_tile + u;
+            tin[F.first_tile + u].w[3] |= TI_FIX;
+        }
     }
-}
-
-// k_fbase: tuple index of every file's first record (exclusive prefix over
-// the file totals) and the call's total.
-#define FB_NT 1024
-__global__ void __launch_bounds__(FB_NT)
-k_fbase(int nfiles, const uint64_t* __restrict__ ftotal, FileInfo* finfo, Globals* g, int round) {
-    if (round > 0 && g->nfix[round - 1] == 0) return;
-    __shared__ uint64_t part[FB_NT];
-    __shared__ uint64_t carry;
-    if (threadIdx.x == 0) carry = 0;
+    if (tid == 0 && bad_far != NONE32) {
+        bool any_near = false;
+        for (int i = 0; i < LINK_MAXT / 32; i++) any_near |= badm[i] != 0;
+        if (!any_near) {
+            const uint32_t k = atomicAdd(&g->nfix[slot], 1u);
+            fixlist[k] = F.first_tile + bad_far;
+            tin[F.first_tile + bad_far].w[3] |= TI_FIX;
+        }
+    }
+    // the workgroup that finishes last: the file bases (its acquire sees every
+    // workgroup's ftotal: each released it before its arrival)
     __syncthreads();
-    for (int b = 0; b < nfiles; b += FB_NT) {
-        const int i = b + threadIdx.x;
-        const uint64_t v = i < nfiles ? ftotal[i] : 0;
-        part[threadIdx.x] = v;
+    if (tid == LINK_NT - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = atomicAdd(&g->link_done, 1u) == (uint32_t)gridDim.x - 1;
+        if (last) { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+        carry = 0;
+    }
+    __syncthreads();
+    if (!last) return;
+    for (int b = 0; b < nfiles; b += LINK_NT) {
+        const int i = b + tid;
+        const uint64_t v = i < nfiles ? __hip_atomic_load(&ftotal[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        part[tid] = v;
         __syncthreads();
-        for (int d = 1; d < FB_NT; d <<= 1) {
-            const uint64_t o = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+        for (int d = 1; d < LINK_NT; d <<= 1) {
+            const uint64_t o = tid >= d ? part[tid - d] : 0;
             __syncthreads();
-            part[threadIdx.x] += o;
+            part[tid] += o;
             __syncthreads();
         }
-        if (i < nfiles) finfo[i].first_index = carry + part[threadIdx.x] - v;
+        if (i < nfiles) finfo[i].first_index = carry + part[tid] - v;
         __syncthreads();
-        if (threadIdx.x == 0) carry += part[FB_NT - 1];
+        if (tid == 0) carry += part[LINK_NT - 1];
         __syncthreads();
     }
-    if (threadIdx.x == 0) g->total = carry;
+    if (tid == 0) { g->total = carry; g->link_done = 0; }
 }
 
 // k_refix: one wave per listed tile: the tile body again from the entering
 // state k_link gave it (new LOCAL, compact entries, register).  Walks on into
-// the next tile of the file while that one's LOCAL disagrees with the new exit.
+// the next tile of the file while that one's LOCAL disagrees with the new exit
+// (and is not listed itself).
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
 k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, TileLocal* loc,
         const TileIn* __restrict__ tin, uint32_t* rec, uint32_t* treg, const uint32_t* __restrict__ tabs,
-        const uint32_t* __restrict__ fixlist, Globals* g, int round) {
-    if (g->nfix[round - 1] == 0) return;                   // (uniform: before the LDS setup's barrier)
+        const uint32_t* __restrict__ fixlist, Globals* g, int slot) {
+    if (g->nfix[slot] == 0) return;                        // (uniform: before the LDS setup's barrier)
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS_ALL];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
     init_tables(smem, tabs + TAB_SCAN, NIB_SCAN * 128);
     CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)(smem + SCAN_LDS + (threadIdx.x >> 6) * STG_BYTES);
     const uint32_t k = blockIdx.x * SCAN_WAVES + (threadIdx.x >> 6);
-    if (k >= g->nfix[round - 1]) return;
+    if (k >= g->nfix[slot]) return;
     const int lane = threadIdx.x & 63;
     const CrcLane cl = crc_lane(lane);
     const uint32_t K4 = k4_const(smem, cl.r4);
@@ -1006,6 +1187,8 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
         S.X = r.X; S.dead = r.dead;
         if (S.dead || t + 1 >= F.first_tile + F.ntile) break;
         // the next tile: consistent with the new exit?  else it is re-resolved too
+        // (unless it is listed itself: its own wave has it)
+        if (tin[t + 1].w[3] & TI_FIX) break;
         const u64 n0 = loc[t + 1].l[0], n1 = loc[t + 1].l[1], n3 = loc[t + 1].l[3];
         const bool ok = (n0 & DF_NONE) ? S.X >= (uint32_t)n3 : S.X == (uint32_t)n1;
         if (ok) break;
@@ -1023,8 +1206,8 @@ __global__ void __launch_bounds__(64 * EMIT_WAVES)
 k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
        const TileIn* __restrict__ tin, const TileLocal* __restrict__ loc, const uint32_t* __restrict__ rec,
        uint32_t* treg, FileInfo* finfo, const uint32_t* __restrict__ tabs, cly_tuple* out_, uint64_t out_cap,
-       Globals* g, int round) {
-    if (g->nfix[round]) return;             // the chain is not final yet (k_refix first)
+       Globals* g, int slot) {
+    if (g->nfix[slot]) return;              // the chain is not final yet (k_refix first)
     gtuples out = (gtuples)out_;
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[EMIT_LDS];
     CLY_LDS uint32_t* sht = (CLY_LDS uint32_t*)smem_raw;
@@ -1107,11 +1290,11 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
 #define FIN_NT 256
 __global__ void __launch_bounds__(FIN_NT)
 k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __restrict__ treg,
-      const uint32_t* __restrict__ tabs, const uint32_t* __restrict__ pw, Globals* g, int round) {
+      const uint32_t* __restrict__ tabs, const uint32_t* __restrict__ pw, Globals* g, int slot) {
     __shared__ uint32_t tab[128];
     __shared__ uint32_t part[FIN_NT];
     __shared__ uint32_t plen[FIN_NT];
-    if (g->nfix[round]) return;             // k_emit did not run (link repair first)
+    if (g->nfix[slot]) return;              // k_emit did not run (link repair first)
     for (int i = threadIdx.x; i < 128; i += FIN_NT) tab[i] = tabs[TAB_TILE + i];
     __syncthreads();
     const int f = blockIdx.x;
@@ -1200,7 +1383,7 @@ struct cly_ctx {
     uint32_t* d_tabs;            // nibble tables (TAB_SCAN, TAB_SH, TAB_TILE)
     uint32_t* d_pw;              // x^(8 CLY_TILE 2^k) mod P, k < 40
     int scan_grid, emit_grid, loc_grid;
-    float kms[6];                // last call: k_scan, link rounds (k_link/k_fbase/k_refix), k_emit, k_fin, k_locate, all
+    float kms[6];                // last call: k_scan, link rounds (k_link/k_refix), k_emit, k_fin, k_locate, all
     uint8_t* d_bytes; uint64_t cap_bytes;          // host-path staging
     cly_tuple* d_tuples; uint64_t cap_tuples;
     void* merge_scratch;         // clymerge.hip's buffers (grow-only)
@@ -1369,32 +1552,23 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         }
         HIPCK(hipMemcpyAsync(c->d_dbg, c->d_loc, sizeof(TileLocal) * ntiles, hipMemcpyDeviceToDevice, st));
     }
-    // LINK_ROUNDS link rounds (round r > 0: k_refix of round r-1's listed tiles,
-    // then k_link; both return at once when round r-1 listed none), then
-    // k_emit/k_fin, which return at once if the last round still listed tiles;
-    // no host wait in between.  Files that need more rounds continue on a host
-    // loop (one wait per round).
-    const int RL = LINK_ROUNDS - 1;
-    const int fix_grid = (nfiles + SCAN_WAVES - 1) / SCAN_WAVES;   // at most one listed tile per file and round
-    for (int r = 0; r < LINK_ROUNDS; r++) {
-        if (r > 0)
-            hipLaunchKernelGGL(k_refix, dim3(fix_grid), dim3(64 * SCAN_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix,
-                               c->d_loc, c->d_tin, c->d_rec, c->d_treg, c->d_tabs, c->d_fix, c->d_g, r);
-        hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, c->d_loc, c->d_tin, c->d_ftotal,
-                           c->d_fix, c->d_g, r);
-        hipLaunchKernelGGL(k_fbase, dim3(1), dim3(FB_NT), 0, st, nfiles, c->d_ftotal, c->d_finfo, c->d_g, r);
-    }
+    // the link (k_link: chain states, contradicted tiles, file bases), then
+    // k_emit/k_fin, which return at once if the link listed tiles; only then
+    // the host waits.  Repair rounds (k_refix + k_link) follow on the host loop.
+    hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_loc, c->d_tin, c->d_ftotal,
+                       c->d_finfo, c->d_fix, c->d_g, 0);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[2], st));
+    int slot = 0;
     auto launch_emit = [&]() -> int {
         int eg = c->emit_grid;
         if ((int64_t)eg * EMIT_WAVES > ntiles) eg = (int)((ntiles + EMIT_WAVES - 1) / EMIT_WAVES);
         hipLaunchKernelGGL(k_emit, dim3(eg), dim3(64 * EMIT_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
-                           c->d_tin, c->d_loc, c->d_rec, c->d_treg, c->d_finfo, c->d_tabs, d_out, out_cap, c->d_g, RL);
+                           c->d_tin, c->d_loc, c->d_rec, c->d_treg, c->d_finfo, c->d_tabs, d_out, out_cap, c->d_g, slot);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[3], st));
         hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_finfo, c->d_treg, c->d_tabs,
-                           c->d_pw, c->d_g, RL);
+                           c->d_pw, c->d_g, slot);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[4], st));
         HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
@@ -1414,26 +1588,24 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     }
     float ms_fix = 0;
     uint32_t rounds = 1, refixed = 0;
-    for (int r = 0; r < LINK_ROUNDS; r++) if (c->h_g->nfix[r]) { rounds++; refixed += c->h_g->nfix[r]; }
-    if (c->h_g->nfix[RL]) {
-        // more repair rounds on the host: round RL's list, k_link again into slot RL
+    if (c->h_g->nfix[slot]) {
         HIPCK(hipEventRecord(c->ev[5], st));
-        while (c->h_g->nfix[RL]) {
+        while (c->h_g->nfix[slot]) {
             if (c->h_g->fail) break;
             if (rounds > 4096) { fprintf(stderr, "clyscan: chain repair did not converge\n"); return CLY_ERR_NOREPAIR; }
-            // k_refix reads slot RL - 1: move the count there, clear slot RL
-            const uint32_t nfix = c->h_g->nfix[RL];
+            const uint32_t nfix = c->h_g->nfix[slot];
             refixed += nfix;
-            HIPCK(hipMemcpyAsync(&c->d_g->nfix[RL - 1], &c->d_g->nfix[RL], sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-            HIPCK(hipMemsetAsync(&c->d_g->nfix[RL], 0, sizeof(uint32_t), st));
-            hipLaunchKernelGGL(k_refix, dim3(fix_grid), dim3(64 * SCAN_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix,
-                               c->d_loc, c->d_tin, c->d_rec, c->d_treg, c->d_tabs, c->d_fix, c->d_g, RL);
-            hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, c->d_loc, c->d_tin, c->d_ftotal,
-                               c->d_fix, c->d_g, RL);
-            hipLaunchKernelGGL(k_fbase, dim3(1), dim3(FB_NT), 0, st, nfiles, c->d_ftotal, c->d_finfo, c->d_g, RL);
+            const int ns = slot ^ 1;
+            HIPCK(hipMemsetAsync(&c->d_g->nfix[ns], 0, sizeof(uint32_t), st));
+            hipLaunchKernelGGL(k_refix, dim3((nfix + SCAN_WAVES - 1) / SCAN_WAVES), dim3(64 * SCAN_WAVES), 0, st,
+                               c->d_files, nfiles, c->d_tprefix, c->d_loc, c->d_tin, c->d_rec, c->d_treg, c->d_tabs,
+                               c->d_fix, c->d_g, slot);
+            hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_loc, c->d_tin,
+                               c->d_ftotal, c->d_finfo, c->d_fix, c->d_g, ns);
             HIPCK(hipGetLastError());
             HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
             HIPCK(hipStreamSynchronize(st));
+            slot = ns;
             rounds++;
         }
         HIPCK(hipEventRecord(c->ev[6], st));
@@ -1661,6 +1833,8 @@ extern "C" const char* cly_strerror(int code) {
         case CLY_ERR_DEVICE: return "HIP device error";
         case CLY_ERR_ARG: return "invalid argument";
         case CLY_ERR_NOREPAIR: return "internal: chain resolution failed";
+        case -14: return "the data dir maybe contaminated or damaged";            // CLY_ERR_DIR (clyload.h)
+        case -15: return "merge-finished: no readable record / value not an integer";   // CLY_ERR_MERGE_FIN
         default: return "unknown status";
     }
 }

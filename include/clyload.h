@@ -1,16 +1,43 @@
 /* clyload.h — NewCouloyDB's index load on the device, from data files on disk
  * (libclyscan.so; couloydb_amd/csrc/clyload.hip).
  *
- * Replaces NewCouloyDB -> loadDataFile -> loadIndex (db.go:44-115, 442-485,
- * 487-655) up to "index built": the directory's `%09d.cly` files (fids
- * ascending, the last the active file) are mmap'd, copied to the device,
- * scanned (cly_scan_device) and their String/ListMeta index state rebuilt
- * (cly_index_device, incl. tx commit/rollback and the TTL sweep at the
- * context's clock, cly_ctx_set_clock); the host then holds the String,
- * ListMeta, Hash, List and Set indexes (key -> LogPos) that updateIndex builds
- * in the MemTables (meta/memTable.go:15-30, index.go).
- * A read error of the scan (ErrInvalidCRC etc.) fails the open with its
- * status, as NewCouloyDB does.                                                */
+ * Replaces NewCouloyDB -> loadDataFile -> loadIndexFromHintFile -> loadIndex
+ * (db.go:44-115, 442-485, 487-655; merge.go:240-287) up to "index built":
+ *   - the directory's data files: every entry named `*.cly` whose stem (the
+ *     name up to its first '.') strconv.Atoi parses (any other such name fails
+ *     the open with CLY_ERR_DIR, db.go:451-457), fids ascending, the file read
+ *     being "%09d.cly" of uint32(fid) (an absent one reads as empty: the
+ *     reference creates it empty), the last fid the active file;
+ *   - `hint-index` (when present, even without data files): every record's
+ *     key -> DecodeLogRecordPos(value) into the String index first
+ *     (merge.go:257-287, strIndex.Put of the stored key, whatever its record's
+ *     types), so that the data files' String Put/Del records override it;
+ *   - `merge-finished` (when present and data files exist): its record at
+ *     offset 0 must read (ReadLogRecord) and its value must be an integer
+ *     (strconv.Atoi), else the open fails (merge.go:240-255, db.go:492-502);
+ *     the data files are read in full either way (db.go:502 discards
+ *     deleteLessThan's result);
+ *   - the files are mmap'd, copied to the device, scanned (cly_scan_device),
+ *     all five indexes rebuilt on the device (cly_index_device: tx
+ *     commit/rollback, last writer wins, the TTL sweep at the context's clock,
+ *     cly_ctx_set_clock); the host then holds the String, ListMeta, Hash, List
+ *     and Set indexes (key -> LogPos) that updateIndex builds in the MemTables
+ *     (meta/memTable.go:15-30, index.go);
+ *   - the TTL sweep's db.Del (db.go:639-651, 186-215): every String key whose
+ *     winning put has expired leaves the index, and its tombstone record
+ *     {0x00 || key, LogRecordDeleted} is appended to the active file by
+ *     appendLogRecord's rule (a new file fid+1 when WriteOff + size >
+ *     DataFileSize); cly_db_open_opts with CLY_DB_APPLY_SWEEP writes those
+ *     records to disk (O_APPEND, as the FileIO writer does), and the stats
+ *     report the active file and WriteOff after the sweep either way.  The
+ *     reference issues the Del calls in Go map order; the library uses scan
+ *     order (the set of records and WriteOff agree whenever no rotation falls
+ *     between two of them).
+ * Read errors fail the open with their status (ErrInvalidCRC etc.), as
+ * NewCouloyDB does.  Out of scope (the Go caller's): loadMergeFiles' moving of
+ * the merge directory (merge.go:195-238), the file lock, and scheduling the TTL
+ * jobs of keys that expire later (cly_db_entries lists them with their
+ * expiration).                                                                */
 #ifndef CLYLOAD_H
 #define CLYLOAD_H
 #include "clyscan.h"
@@ -19,6 +46,11 @@ extern "C" {
 #endif
 
 #define CLY_DB_NOT_FOUND 1    /* public.ErrKeyNotFound                           */
+#define CLY_DB_EOF       2    /* cly_db_value: ReadLogRecord at pos returned io.EOF */
+#define CLY_ERR_DIR     -14   /* "the data dir maybe contaminated or damaged":
+                                 a *.cly name whose stem strconv.Atoi rejects   */
+#define CLY_ERR_MERGE_FIN -15 /* merge-finished's record at 0 does not read, or
+                                 its value is not an integer (getNonMergeFileId) */
 
 typedef struct cly_db cly_db;
 typedef struct cly_load_stats {
@@ -30,12 +62,27 @@ typedef struct cly_load_stats {
     double   total_ms;
     uint64_t n_files, bytes, records;
     uint64_t str_keys, listmeta_keys, hash_fields, list_items, set_members;
-    uint32_t active_fid;      /* activityFile.FileId                             */
+    uint32_t active_fid;      /* activityFile.FileId after the open (TTL sweep included) */
     uint32_t _pad;
-    int64_t  write_off;       /* activityFile.WriteOff (db.go:632-634)           */
+    int64_t  write_off;       /* activityFile.WriteOff after the open (db.go:632-634 + the sweep's appends) */
+    uint64_t hint_records;    /* hint-index records loaded                        */
+    uint64_t n_expired;       /* String keys the TTL sweep db.Del'd               */
+    int64_t  write_off_loaded;/* WriteOff as loadIndex leaves it (before the sweep) */
+    uint32_t active_fid_loaded;
+    uint32_t sweep_files;     /* new data files the sweep's appends opened        */
 } cly_load_stats;
 
+/* NewCouloyDB's Options the open uses.                                        */
+typedef struct cly_db_options {
+    uint64_t data_file_size;  /* Options.DataFileSize (0: 256 MiB, options.go:32) */
+    uint32_t flags;           /* CLY_DB_APPLY_SWEEP: write the sweep's tombstones */
+    uint32_t _pad;
+} cly_db_options;
+#define CLY_DB_APPLY_SWEEP 1u
+
+/* cly_db_open = cly_db_open_opts with default options (nothing written).    */
 int  cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load_stats* st);
+int  cly_db_open_opts(cly_ctx* ctx, const char* dir, const cly_db_options* opt, cly_db** out, cly_load_stats* st);
 void cly_db_close(cly_db* db);
 /* Index lookups: CLY_OK with *pos, or CLY_DB_NOT_FOUND.                      */
 int  cly_db_get(cly_db* db, const uint8_t* key, uint64_t klen, cly_pos* pos);          /* String   */
@@ -55,8 +102,35 @@ int  cly_db_sget(cly_db* db, const uint8_t* key, uint64_t klen, const uint8_t* m
  * index, -3 if cap is too small.                                             */
 int64_t cly_index_key(uint32_t dtype, const uint8_t* d, uint64_t n, uint8_t* out, uint64_t cap, uint32_t* plen);
 /* getLogRecordByPos (db.go:680-704): the value of the record at pos into buf
- * (*vlen = its length; CLY_ERR_CAPACITY if cap is too small).                */
+ * (*vlen = its length, 0 on any error; CLY_ERR_CAPACITY if cap is too small).
+ * CLY_DB_NOT_FOUND when pos.Fid is not a data file of the db or the record is
+ * a LogRecordDeleted; CLY_DB_EOF when ReadLogRecord returns io.EOF there;
+ * CLY_ERR_CRC on a checksum mismatch; CLY_ERR_OFFSET for a negative offset;
+ * the panics' codes (CLY_ERR_TRUNC5, CLY_ERR_VARINT).                        */
 int  cly_db_value(cly_db* db, const cly_pos* pos, uint8_t* buf, uint64_t cap, uint64_t* vlen);
+
+/* Enumeration of what the load produced (for bulk-loading the caller's
+ * MemTables and TTL queue).  Pointers stay valid until cly_db_close; the order
+ * within a kind is unspecified (the MemTables sort).  Not thread-safe.        */
+#define CLY_IT_STRING   0     /* key = realKey, pos, expiration (0 = none; else the
+                                 UnixNano the reference's ttl job fires at)   */
+#define CLY_IT_LISTMETA 1     /* key, pos                                       */
+#define CLY_IT_HASH     2     /* key, sub = field, pos                          */
+#define CLY_IT_LIST     3     /* key, sub = seq.GobEncode() bytes, pos          */
+#define CLY_IT_SET      4     /* key, sub = hashMemberKey (4 B), pos            */
+#define CLY_IT_EXPIRED  5     /* key: the String keys the TTL sweep db.Del'd, in
+                                 the order their tombstones are appended      */
+typedef struct cly_db_entry {
+    const uint8_t* key;
+    uint64_t       key_len;
+    const uint8_t* sub;
+    uint64_t       sub_len;
+    cly_pos        pos;
+    int64_t        expiration;
+} cly_db_entry;
+uint64_t cly_db_count(cly_db* db, int kind);
+/* entries first .. first+n-1 of a kind into out; returns how many were written */
+uint64_t cly_db_entries(cly_db* db, int kind, uint64_t first, cly_db_entry* out, uint64_t n);
 
 #ifdef __cplusplus
 }

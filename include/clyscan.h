@@ -214,6 +214,9 @@ int cly_hint_scan(cly_ctx* ctx, const cly_file* hint_file, cly_tuple* out, cly_p
 #define CLY_IX_LOADONLY 3     /* an index points here, but merge.go decodes the
                                  realKey and looks up another key: a Hash/List/
                                  Set record without a txId; merge drops it    */
+#define CLY_IX_EXPIRED 4      /* a String key's winning put, removed by the TTL
+                                 sweep (db.Del: a tombstone goes to the active
+                                 file); no index entry                        */
 typedef struct cly_index_result {
     uint64_t n_live;          /* index entries (= records LIVE or LOADONLY)     */
     uint64_t n_applied;       /* records updateIndex sees                       */

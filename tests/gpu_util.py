@@ -335,7 +335,26 @@ def typed_corpus(seed, n_ops=400, n_keys=12, tx_frac=0.6, nontx_frac=0.15, garba
 INDEX_NOW = 1_800_000_000_000_000_000      # the clock the index tests give loadIndex (UnixNano, 2027)
 
 
-def index_states(file_bytes, tuples_per_file, now_ns=INDEX_NOW, merge_panics=None, out_index=None):
+def hint_entries(hint_bytes):
+    """loadIndexFromHintFile's reading (merge.go:257-287) restated: the hint
+    file's records in order -> [(stored key, fid, offset)] (DecodeLogRecordPos
+    of each value, data/logRecord.go:126-134)."""
+    out, off = [], 0
+    while True:
+        st, t = mg.read_log_record(hint_bytes, off)
+        if st is not None:
+            break
+        h, ks = t["header_size"], t["key_size"]
+        key = bytes(hint_bytes[off + h:off + h + ks])
+        val = bytes(hint_bytes[off + h + ks:off + t["size"]])
+        fid, n = mg.varint(val)
+        o, _ = mg.varint(val[n:])
+        out.append((key, fid & 0xFFFFFFFF, o))
+        off += t["size"]
+    return out
+
+
+def index_states(file_bytes, tuples_per_file, now_ns=INDEX_NOW, merge_panics=None, out_index=None, preload=None):
     """db.loadIndex (db.go:582-651) restated literally: a map of buffered tx
     records per txId, updateIndex for the five indexes (String/ListMeta by
     realKey, Hash/List/Set by the composite keys of tests/index_keys.py decoded
@@ -344,9 +363,13 @@ def index_states(file_bytes, tuples_per_file, now_ns=INDEX_NOW, merge_panics=Non
     sweep (a key whose expiration is set and not after now is db.Del'd).  Per
     record the state the device index reports: 1 = an index points at it and
     merge.go's lookup (merge.go:101-132, realKey decoded) finds it, 3 = an
-    index points at it under a key merge.go does not look up, 0 otherwise.
+    index points at it under a key merge.go does not look up, 4 = the winning
+    put of a String key the TTL sweep removes, 0 otherwise.
     Raises index_keys.GoPanic where updateIndex's decode panics; merge_panics
-    (a list) receives the records whose merge.go decode panics."""
+    (a list) receives the records whose merge.go decode panics.  preload: the
+    hint file's [(key, fid, offset)] put into the String index before the data
+    files (loadIndexFromHintFile); a key the data files Put or Del later is
+    theirs (out_index holds (key, fid, offset, 0) for the other ones)."""
     from .index_keys import GoPanic, index_key
     recs = []
     for F, tt in zip(file_bytes, tuples_per_file):
@@ -356,6 +379,8 @@ def index_states(file_bytes, tuples_per_file, now_ns=INDEX_NOW, merge_panics=Non
             tx, n = mg.varint(key)
             recs.append((key, key[n:] if n > 0 else key, t, tx))
     index = {}                      # index key -> record (all five indexes, flattened)
+    pre = {k: (f, o) for k, f, o in (preload or [])}
+    touched = set()                 # String keys a data-file record Put or Del
     expirations = {}
     state = [0] * len(recs)
     txrecords = {}
@@ -369,6 +394,8 @@ def index_states(file_bytes, tuples_per_file, now_ns=INDEX_NOW, merge_panics=Non
             ik = index_key(dt, log_key)
             if ik is None:
                 return
+        if dt == mg.STRING:
+            touched.add(rk)
         if int(t["type"]) == mg.DELETED:
             index.pop(ik, None)
             if dt == mg.STRING:
@@ -390,12 +417,17 @@ def index_states(file_bytes, tuples_per_file, now_ns=INDEX_NOW, merge_panics=Non
             txrecords.pop(tx, None)
         else:
             txrecords.setdefault(tx, []).append(i)
-    # db.go:639-651: `if exp.After(time.Now()) ttl.add else db.Del(key)`
+    # db.go:639-651: `if exp.After(time.Now()) ttl.add else db.Del(key)`; the
+    # device marks the swept key's winning put 4 (CLY_IX_EXPIRED)
+    swept = []
     if now_ns is not None:
         for rk, exp in expirations.items():
             if exp != 0 and not exp > now_ns:
-                index.pop((mg.STRING, rk), None)
+                i = index.pop((mg.STRING, rk), None)
+                if i is not None:
+                    swept.append(i)
     if out_index is not None:
+        out_index.update({(mg.STRING, k): (k, f, o, 0) for k, (f, o) in pre.items() if k not in touched})
         out_index.update({ik: (recs[i][0], int(recs[i][2]["fid"]), int(recs[i][2]["offset"]), recs[i][3])
                           for ik, i in index.items()})
     for ik, i in index.items():
@@ -405,6 +437,8 @@ def index_states(file_bytes, tuples_per_file, now_ns=INDEX_NOW, merge_panics=Non
         except GoPanic:
             mk = None
         state[i] = 1 if mk == ik else 3
+    for i in swept:
+        state[i] = 4
     if merge_panics is not None:
         for i, (_, rk, t, _) in enumerate(recs):
             if int(t["data_type"]) in (mg.HASH, mg.LIST, mg.SET):

@@ -32,8 +32,9 @@ def test_ttl_sweep_restatement():
     arr = np.frombuffer(F, np.uint8).copy()
     tt, _, _ = co.scan_file(arr, 0)
     st = index_states([arr], [tt], now_ns=now)
+    # swept winners are state 4 (CLY_IX_EXPIRED: db.Del appends their tombstones)
     #         a  b  c  d  e(old) e  f(old) f  g  h
-    assert list(st) == [1, 0, 0, 1, 0, 1, 0, 0, 0, 1]
+    assert list(st) == [1, 4, 4, 1, 0, 1, 0, 4, 4, 1]
 
 
 def test_index_restatements_agree():

@@ -143,7 +143,7 @@ def test_ttl_restatement():
     files, _ = ttl_files()
     a = np.frombuffer(files[0], np.uint8).copy()
     tt, _, _ = co.scan_file(a, 0)
-    assert list(index_states([a], [tt], now_ns=TTL_EXP)) == [0]          # expired at reload: db.Del
+    assert list(index_states([a], [tt], now_ns=TTL_EXP)) == [4]          # expired at reload: db.Del (CLY_IX_EXPIRED)
     assert list(index_states([a], [tt], now_ns=TTL_EXP - 1)) == [1]      # still pending: ttl.add
 
 
