@@ -210,6 +210,21 @@ def cpu_baseline(wl, budget_s=12.0):
             mb += len(arr)
         merge_part = {"value": round(mb / t_m / 2**30, 4), "unit": "GiB/s",
                       "sample": "%d files: oracle scan + clyo_merge (merge.go:90-143 restated), 1 thread" % min(len(files), 4)}
+    index_part = None
+    if wl.name == "c2":
+        # db.loadIndex (String index, tx buffering, TTL pass) over all of the
+        # configuration's files in memory, one thread as the reference: the CPU
+        # side of index_load_wall_ms
+        arrs = [wl.file_bytes(i) for i in range(len(wl.dev_files))]
+        t0 = time.perf_counter()
+        rc, lr = co.load_index(arrs, [f for _, _, f in wl.dev_files], time.time_ns())
+        t_li = time.perf_counter() - t0
+        index_part = {"wall_ms": round(t_li * 1e3, 1), "rc": rc, "records": int(lr.records),
+                      "str_keys": int(lr.str_keys), "cores": 1,
+                      "sample": "all %d files (%.2f GiB) in memory; oracle clyo_load_index (db.go:487-651 String/"
+                                "ListMeta restated, open-addressing tables keyed into the file bytes)"
+                                % (len(arrs), sum(len(a) for a in arrs) / 2**30)}
+        del arrs
     # ref-faithful on a bounded number of records of file 0
     arr = wl.file_bytes(0)
     with tempfile.TemporaryDirectory() as d:
@@ -227,6 +242,7 @@ def cpu_baseline(wl, budget_s=12.0):
                              "mrecords_per_s": round(nf / tf / 1e6, 4),
                              "sample": "first %d records of one file; per record fstat + 2x (open, mmap whole file, copy, munmap)" % nf},
             "host_nproc": os.cpu_count(),
+            **({"index_load": index_part} if index_part else {}),
             "multi_thread": multi,
             **({"value": merge_part["value"], "sample": merge_part["sample"], "scan_only_value": round(alg_gibs, 4)}
                if merge_part else {})}

@@ -598,19 +598,18 @@ struct TState {
     uint32_t tpatch;             // its patch word (XORed after the bytes from Tb on are zeroed)
     uint32_t carry_next;         // register XOR due at the next block's first byte (terminal at the block end)
 };
-// The block's outputs for record k of a round (lane k), and its CRC patch XORed
-// into the stage word holding P (ds_xor: record starts are >= 6 B apart).
+// The block's outputs for record k of a round (lane k); returns its CRC patch,
+// to be XORed into the stage word holding P (one writer per word: record
+// starts are >= 7 B apart) once no header read of the stage can still see
+// that word (the tail of the record before P shares it).
 template <int BM>
-__device__ __forceinline__ void rec_out(const DevFile& F, gbytes base, uint32_t p, const Hdr& h, uint32_t idx, uint32_t tb,
-                                        uint32_t bs, uint32_t dq, CLY_LDS uint32_t* stg, const CLY_LDS uint8_t* smem,
-                                        const CrcLane& cl, uint32_t K4, uint32_t* trec, gtuples out, uint64_t out_cap,
-                                        uint64_t gbase, Globals* g) {
-    if (BM == BM_EMIT) put_tuple(out, gbase + idx, out_cap, base, p, h, F.fid, g);
-    else {
-        if (idx < CAP_T) rec_store(trec + 4 * idx, h, p - tb);
-        const uint32_t d = h.crc ^ K4 ^ dq;
-        stg[(p - bs) >> 2] ^= crc_unbytes(smem, d, p & 3u, cl.r4);   // one writer per word (starts are >= 6 B apart)
-    }
+__device__ __forceinline__ uint32_t rec_out(const DevFile& F, gbytes base, uint32_t p, const Hdr& h, uint32_t idx,
+                                            uint32_t tb, uint32_t dq, const CLY_LDS uint8_t* smem, const CrcLane& cl,
+                                            uint32_t K4, uint32_t* trec, gtuples out, uint64_t out_cap, uint64_t gbase,
+                                            Globals* g) {
+    if (BM == BM_EMIT) { put_tuple(out, gbase + idx, out_cap, base, p, h, F.fid, g); return 0u; }
+    if (idx < CAP_T) rec_store(trec + 4 * idx, h, p - tb);
+    return crc_unbytes(smem, h.crc ^ K4 ^ dq, p & 3u, cl.r4);
 }
 // The terminal T (found by lane src): the bytes from T on read as zero, and
 // ~cq of the record before it (dT) is XORed in before byte T (into the word
@@ -664,8 +663,12 @@ __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t 
         // the stored CRC of each record's predecessor
         const uint32_t up = dppu<DPP_WF_SR1>(0u, h.crc);
         const uint32_t dq = k == 0 ? (S.cq_known ? ~S.cq : 0xFFFFFFFFu) : ~up;
-        if (acc) rec_out<BM>(F, base, (uint32_t)P, h, S.tcnt + k, tb, bs, P == 0 ? 0u : dq, stg, smem, cl, K4, trec, out,
-                              out_cap, gbase, g);
+        // every lane of the round has read its header: the patches may go in
+        if (acc) {
+            const uint32_t pv = rec_out<BM>(F, base, (uint32_t)P, h, S.tcnt + k, tb, P == 0 ? 0u : dq, smem, cl, K4,
+                                            trec, out, out_cap, gbase, g);
+            if (BM != BM_EMIT) stg[((uint32_t)P - bs) >> 2] ^= pv;
+        }
         if (S.G == NONE32) S.G = (uint32_t)X;
         if (n) {
             const int kl = n - 1;
@@ -851,17 +854,24 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                     uint32_t pcq = lfp ? lvp : S.cq;
                     bool pk = lfp ? true : S.cq_known;
                     // the lane's records: outputs and CRC patches (headers from the stage)
-                    uint32_t p = L.E, psz = 0, ppsz = 0;
+                    // (the patch of a lane's first record waits for the loop's end: the
+                    // lane before reads its last header, whose tail shares that word,
+                    // in a later iteration)
+                    uint32_t p = L.E, psz = 0, ppsz = 0, p0w = 0, p0v = 0;
                     for (uint32_t i = 0; CLY_EXP != 2 && __ballot(i < c); i++) {
                         if (i < c) {
                             const Hdr h = hdr_get(base, p, flen, stg, bs);
-                            rec_out<BM>(F, base, p, h, S.tcnt + lex + i, tb, bs, p == 0 ? 0u : (pk ? ~pcq : 0xFFFFFFFFu),
-                                        stg, smem, cl, K4, trec, out, out_cap, gbase, g);
+                            const uint32_t pv = rec_out<BM>(F, base, p, h, S.tcnt + lex + i, tb,
+                                                            p == 0 ? 0u : (pk ? ~pcq : 0xFFFFFFFFu), smem, cl, K4, trec,
+                                                            out, out_cap, gbase, g);
+                            if (i == 0) { p0w = (p - bs) >> 2; p0v = pv; }
+                            else if (BM != BM_EMIT) stg[(p - bs) >> 2] ^= pv;
                             pcq = h.crc; pk = true;
                             ppsz = psz; psz = (uint32_t)h.size;
                             p += (uint32_t)h.size;
                         }
                     }
+                    if (BM != BM_EMIT && c > 0) stg[p0w] ^= p0v;
                     if (kT < 64) {
                         const uint32_t T = rdl(L.x, kT);
                         const uint32_t dT = T == 0 ? 0u : (pk ? ~pcq : 0xFFFFFFFFu);

@@ -391,3 +391,158 @@ uint64_t clyo_scan_files_mt(const uint8_t* const* bases, const uint64_t* lens,
     for (int i = 0; i < nthreads; i++) { pthread_join(th[i], NULL); total += args[i].records; }
     return total;
 }
+
+/* ------------------------------------------------------------------------ */
+/* db.loadIndex (db.go:487-651) for the String and ListMeta data types: the
+ * CPU baseline of the index-load wall time.  One thread, as the reference
+ * (one goroutine walks the fids in order).  The reference's indexes are
+ * meta.MemTable trees and Go maps holding copies of the keys; this restatement
+ * uses open-addressing hash tables whose keys point into the file bytes, which
+ * can only make the baseline faster.  Records of the Hash/List/Set types are
+ * not restated here (the benchmark workloads hold none): their presence returns
+ * CLYO_LI_UNSUPPORTED.                                                       */
+typedef struct {
+    const uint8_t* key; uint32_t klen, fid;
+    int64_t off, exp;
+    uint8_t used, live;
+} li_ent;
+typedef struct { li_ent* t; uint64_t cap, used; } li_map;
+
+static uint64_t li_hash(const uint8_t* p, uint32_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
+    while (n >= 8) {
+        uint64_t w; memcpy(&w, p, 8);
+        h = (h ^ w) * 0xBF58476D1CE4E5B9ull; h ^= h >> 31;
+        p += 8; n -= 8;
+    }
+    uint64_t w = 0;
+    memcpy(&w, p, n);
+    h = (h ^ w) * 0x94D049BB133111EBull; h ^= h >> 29;
+    return h;
+}
+
+static li_ent* li_find(li_map* m, const uint8_t* k, uint32_t n, int insert);
+static void li_grow(li_map* m) {
+    li_map g = {(li_ent*)calloc(m->cap * 2, sizeof(li_ent)), m->cap * 2, 0};
+    for (uint64_t i = 0; i < m->cap; i++)
+        if (m->t[i].used) { li_ent* e = li_find(&g, m->t[i].key, m->t[i].klen, 1); *e = m->t[i]; }
+    free(m->t);
+    *m = g;
+}
+static li_ent* li_find(li_map* m, const uint8_t* k, uint32_t n, int insert) {
+    if (insert && (m->used + 1) * 2 > m->cap) li_grow(m);
+    uint64_t i = li_hash(k, n) & (m->cap - 1);
+    for (;; i = (i + 1) & (m->cap - 1)) {
+        li_ent* e = &m->t[i];
+        if (!e->used) {
+            if (!insert) return NULL;
+            e->used = 1; e->key = k; e->klen = n; e->live = 0;
+            m->used++;
+            return e;
+        }
+        if (e->klen == n && memcmp(e->key, k, n) == 0) return e;
+    }
+}
+
+/* updateIndex (db.go:511-571), String and ListMeta cases */
+static int li_update(li_map* str, li_map* lmeta, const uint8_t* key, uint32_t klen, uint8_t type,
+                     uint8_t dtype, int64_t exp, uint32_t fid, int64_t off) {
+    li_map* m;
+    if (dtype == 0) m = str;                             /* data.String :513-520 */
+    else if (dtype == 3) m = lmeta;                      /* data.ListMeta :549-554 */
+    else if (dtype <= 4) return CLYO_LI_UNSUPPORTED;     /* Hash / List / Set */
+    else return 0;                                       /* no case: nothing */
+    if (type == 1) {                                     /* LogRecordDeleted: Del (+ delete(expirations)) */
+        li_ent* e = li_find(m, key, klen, 0);
+        if (e) e->live = 0;
+        return 0;
+    }
+    li_ent* e = li_find(m, key, klen, 1);                /* Put(key, pos); expirations[key] = exp */
+    e->live = 1; e->fid = fid; e->off = off; e->exp = exp;
+    return 0;
+}
+
+typedef struct { const uint8_t* key; uint32_t klen, fid; int64_t off, exp; uint8_t type, dtype; int64_t next; } li_txrec;
+typedef struct { int64_t txid, head, tail; uint8_t used, live; } li_tx;
+
+int clyo_load_index(const uint8_t* const* bases, const uint64_t* lens, const uint32_t* fids, int nfiles,
+                    int64_t now_ns, clyo_load_result* r) {
+    memset(r, 0, sizeof(*r));
+    li_map str = {(li_ent*)calloc(1 << 16, sizeof(li_ent)), 1 << 16, 0};
+    li_map lmeta = {(li_ent*)calloc(1 << 10, sizeof(li_ent)), 1 << 10, 0};
+    uint64_t tcap = 1 << 10, tused = 0, rcap = 1 << 12, rn = 0;
+    li_tx* tx = (li_tx*)calloc(tcap, sizeof(li_tx));
+    li_txrec* recs = (li_txrec*)malloc(rcap * sizeof(li_txrec));
+    int rc = 0;
+    for (int f = 0; f < nfiles && rc == 0; f++) {       /* db.go:582 for i, fid := range fids */
+        const uint8_t* F = bases[f];
+        uint64_t off = 0;
+        for (;;) {
+            clyo_tuple t;
+            int s = clyo_read_log_record(F, lens[f], off, &t);   /* :592 */
+            if (s != CLYO_REC) {
+                if (s < 0) rc = s;                       /* :594-597 non-EOF error */
+                break;
+            }
+            r->records++;
+            if (t.txid_len == 0xFF) { rc = CLYO_ERR_VARINT; break; }   /* key[n:] with n<0 */
+            const uint8_t* rk = F + off + t.header_size + t.txid_len;  /* parseLogRecordKey :706-710 */
+            const uint32_t rkl = t.key_size - t.txid_len;
+            if (t.tx_id == 0) {                          /* NO_TX_ID: :604-606 */
+                rc = li_update(&str, &lmeta, rk, rkl, t.type, t.data_type, t.expiration, fids[f], (int64_t)off);
+                r->applied++;
+            } else {
+                /* txRecords map (:578), keyed by txId: open addressing on int64 */
+                if ((tused + 1) * 2 > tcap) {
+                    li_tx* g = (li_tx*)calloc(tcap * 2, sizeof(li_tx));
+                    for (uint64_t i = 0; i < tcap; i++) if (tx[i].used) {
+                        uint64_t j = ((uint64_t)tx[i].txid * 0x9E3779B97F4A7C15ull) & (tcap * 2 - 1);
+                        while (g[j].used) j = (j + 1) & (tcap * 2 - 1);
+                        g[j] = tx[i];
+                    }
+                    free(tx); tx = g; tcap *= 2;
+                }
+                uint64_t j = ((uint64_t)t.tx_id * 0x9E3779B97F4A7C15ull) & (tcap - 1);
+                while (tx[j].used && tx[j].txid != t.tx_id) j = (j + 1) & (tcap - 1);
+                li_tx* e = &tx[j];
+                if (t.type == 4) {                       /* TxnBegin: nothing (:609) */
+                } else if (t.type == 2) {                /* TxnCommit: apply in order, delete (:611-616) */
+                    if (e->used && e->live)
+                        for (int64_t q = e->head; q >= 0 && rc == 0; q = recs[q].next) {
+                            rc = li_update(&str, &lmeta, recs[q].key, recs[q].klen, recs[q].type, recs[q].dtype,
+                                           recs[q].exp, recs[q].fid, recs[q].off);
+                            r->applied++;
+                        }
+                    if (e->used) e->live = 0;
+                } else if (t.type == 3) {                /* TxnRollback: delete (:617-618) */
+                    if (e->used) e->live = 0;
+                } else {                                 /* buffer (Key = realKey) :620-625 */
+                    if (!e->used) { e->used = 1; e->txid = t.tx_id; tused++; }
+                    if (!e->live) { e->live = 1; e->head = e->tail = -1; }
+                    if (rn == rcap) { rcap *= 2; recs = (li_txrec*)realloc(recs, rcap * sizeof(li_txrec)); }
+                    recs[rn] = (li_txrec){rk, rkl, fids[f], (int64_t)off, t.expiration, t.type, t.data_type, -1};
+                    if (e->tail >= 0) recs[e->tail].next = (int64_t)rn; else e->head = (int64_t)rn;
+                    e->tail = (int64_t)rn++;
+                }
+            }
+            if (rc) break;
+            off += t.size;                               /* :629 */
+        }
+        if (f == nfiles - 1) r->write_off = (int64_t)off;   /* :633-635 */
+    }
+    /* TTL (:638-649): expired keys are deleted (db.Del), the others scheduled */
+    for (uint64_t i = 0; i < str.cap && rc == 0; i++) {
+        li_ent* e = &str.t[i];
+        if (!e->used || !e->live) continue;
+        if (e->exp != 0) {
+            if (e->exp > now_ns) r->with_ttl++;
+            else { r->expired++; e->live = 0; }
+        }
+        if (e->live) r->str_keys++;
+    }
+    for (uint64_t i = 0; i < lmeta.cap; i++) r->listmeta_keys += lmeta.t[i].used && lmeta.t[i].live;
+    for (uint64_t i = 0; i < tcap; i++) r->tx_pending += tx[i].used && tx[i].live;
+    free(str.t); free(lmeta.t); free(tx); free(recs);
+    r->status = rc;
+    return rc;
+}

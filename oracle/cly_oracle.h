@@ -97,6 +97,20 @@ int64_t clyo_scan_path_faithful(const char* path, uint32_t fid, uint64_t max_rec
 uint64_t clyo_scan_files_mt(const uint8_t* const* bases, const uint64_t* lens,
                             const uint32_t* fids, int nfiles, int nthreads);
 
+/* db.loadIndex (db.go:487-651) for the String and ListMeta types, one thread:
+ * tx buffering by txId (:578, :604-626), last-writer-wins Put/Del (:511-554),
+ * WriteOff of the last file (:633-635) and the TTL pass (:638-649, keys whose
+ * expiration <= now_ns are deleted).  Returns 0, a scan error status, or
+ * CLYO_LI_UNSUPPORTED for a Hash/List/Set record. */
+enum { CLYO_LI_UNSUPPORTED = -20 };
+typedef struct clyo_load_result {
+    uint64_t records, applied, str_keys, listmeta_keys, expired, with_ttl, tx_pending;
+    int64_t  write_off;
+    int32_t  status, _pad;
+} clyo_load_result;
+int clyo_load_index(const uint8_t* const* bases, const uint64_t* lens, const uint32_t* fids, int nfiles,
+                    int64_t now_ns, clyo_load_result* r);
+
 #ifdef __cplusplus
 }
 #endif

@@ -62,6 +62,9 @@ def lib():
         L.clyo_merge.restype = ctypes.c_int
         L.clyo_decode_pos.argtypes = [ctypes.c_void_p, ctypes.c_uint64, P(ctypes.c_uint32), P(ctypes.c_int64)]
         L.clyo_decode_pos.restype = ctypes.c_int
+        L.clyo_load_index.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                      ctypes.c_int64, ctypes.c_void_p]
+        L.clyo_load_index.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -116,6 +119,27 @@ def scan_files_mt(arrays, fids, nthreads):
     lens = (ctypes.c_uint64 * n)(*[len(a) for a in arrays])
     fa = (ctypes.c_uint32 * n)(*fids)
     return lib().clyo_scan_files_mt(bases, lens, fa, n, nthreads)
+
+
+class LoadResult(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("records", "applied", "str_keys", "listmeta_keys", "expired",
+                                               "with_ttl", "tx_pending")] + \
+               [("write_off", ctypes.c_int64), ("status", ctypes.c_int32), ("_pad", ctypes.c_int32)]
+
+
+LI_UNSUPPORTED = -20
+
+
+def load_index(arrays, fids, now_ns):
+    """clyo_load_index: db.loadIndex (String/ListMeta) over the files in fid
+    order -> (rc, LoadResult)."""
+    n = len(arrays)
+    bases = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrays])
+    lens = (ctypes.c_uint64 * n)(*[len(a) for a in arrays])
+    fa = (ctypes.c_uint32 * n)(*fids)
+    r = LoadResult()
+    rc = lib().clyo_load_index(bases, lens, fa, n, now_ns, ctypes.byref(r))
+    return rc, r
 
 
 class MergeResult(ctypes.Structure):

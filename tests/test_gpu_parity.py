@@ -100,6 +100,34 @@ def test_shapes_vs_oracle(scanner, shape):
     compare(r.file_tuples(0), r.status[0], r.end_offset[0], t, st, end, shape)
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_tiny_records_irregular(scanner, seed):
+    """Records whose key+value is <= 3 bytes (commit markers: the header, the
+    txId varint and the key share the 4-B word of the next record's start)
+    among irregular sizes, so that blocks take the general pass: every header
+    must be read before the next record's CRC patch lands in the stage."""
+    import random
+
+    import make_golden as mg
+    rng = random.Random(seed)
+    b = bytearray()
+    while len(b) < 400_000:
+        if rng.random() < 0.6:
+            tx = rng.choice([0, 1, 5, 63, 64, 6453, 100_000])
+            key = mg.key_tx(bytes([rng.randrange(256)]) if rng.random() < 0.7 else b"", tx)[:3]
+            val = rng.randbytes(max(0, rng.randrange(4) - len(key)))
+            b += mg.encode_record(key, val, rng.choice([0, 1, 2, 3, 4]), rng.choice([0, 0, 1, 3]), 0)
+        else:
+            b += mg.encode_record(mg.key_tx(rng.randbytes(rng.randrange(1, 30)), 0),
+                                  rng.randbytes(rng.choice([0, 7, 33, 120])), 0, 0, 0)
+    data = np.frombuffer(bytes(b), np.uint8).copy()
+    f = DataFile(data, 9)
+    r = scanner.scan([f])
+    t, st, end = co.scan_file(data, 9)
+    assert len(t) > 8000 and st == 0
+    compare(r.file_tuples(0), r.status[0], r.end_offset[0], t, st, end, "tiny %d" % seed)
+
+
 @pytest.mark.parametrize("cut", [0, 1, 4, 5, 6, 13, 27, 31])
 def test_tails_at_chunk_boundaries(scanner, cut):
     # lengths around chunk multiples for both builds (32 KiB and 2 KiB chunks)

@@ -130,3 +130,26 @@ def test_gpu_index_device_c4_shape():
         r = sc.index_device(wl.dev_files, wl.d_out.data_ptr(), first, res, d_state.data_ptr())
     got = d_state.cpu().numpy()
     assert (got == wl.live_np).all() and r.n_live == wl.n_live and r.n_host == 0 and r.n_loadonly == 0
+
+
+def test_c_load_index_restatement():
+    """oracle clyo_load_index (the CPU baseline of the index-load time) against
+    the literal restatement: live String / ListMeta keys, swept keys, WriteOff."""
+    import make_golden as mg
+    for seed in range(6):
+        b = merge_corpus(seed, n_keys=150 + 40 * seed)
+        arrays, tts, _ = oracle_scan(split_files(b, 1 + seed % 3, random.Random(seed)))
+        st = index_states(arrays, tts)
+        dts = np.concatenate([t["data_type"] for t in tts])
+        rc, r = co.load_index(arrays, list(range(len(arrays))), INDEX_NOW)
+        assert rc == 0
+        assert r.records == len(st)
+        assert r.str_keys == int(((st == 1) & (dts == mg.STRING)).sum())
+        assert r.listmeta_keys == int(((st == 1) & (dts == mg.LISTMETA)).sum())
+        assert r.expired == int((st == 4).sum())
+        assert r.write_off == len(arrays[-1])
+    # Hash / List / Set records are outside this restatement
+    from .gpu_util import typed_corpus
+    arr = np.frombuffer(typed_corpus(1), np.uint8).copy()
+    rc, _ = co.load_index([arr], [0], INDEX_NOW)
+    assert rc == co.LI_UNSUPPORTED
