@@ -368,14 +368,20 @@ class LoadedDB:
     KeyError for public.ErrKeyNotFound."""
 
     def __init__(self, scanner, path, data_file_size=0, apply_sweep=False):
-        self.lib = scanner.lib
+        scanners = list(scanner) if isinstance(scanner, (list, tuple)) else [scanner]
+        self.lib = scanners[0].lib
         self.db = ctypes.c_void_p()
         self.stats = _abi.ClyLoadStats()
         opt = _abi.ClyDbOptions()
         opt.data_file_size = data_file_size
         opt.flags = _abi.DB_APPLY_SWEEP if apply_sweep else 0
-        rc = self.lib.cly_db_open_opts(scanner.ctx, os.fsencode(path), ctypes.byref(opt), ctypes.byref(self.db),
-                                       ctypes.byref(self.stats))
+        if len(scanners) == 1:
+            rc = self.lib.cly_db_open_opts(scanners[0].ctx, os.fsencode(path), ctypes.byref(opt),
+                                           ctypes.byref(self.db), ctypes.byref(self.stats))
+        else:
+            ctxs = (ctypes.c_void_p * len(scanners))(*[sc.ctx.value for sc in scanners])
+            rc = self.lib.cly_db_open_multi(ctxs, len(scanners), os.fsencode(path), ctypes.byref(opt),
+                                            ctypes.byref(self.db), ctypes.byref(self.stats))
         if rc != 0:
             raise (ErrInvalidCRC if rc == ERR_CRC else ScanError)(rc, self.lib.cly_strerror(rc).decode())
 
@@ -470,3 +476,10 @@ def index_key(lib, dtype, data):
     if n == -2:
         return None
     return out.raw[:plen.value], out.raw[plen.value:n]
+
+
+def open_db_multi(scanners, path, data_file_size=0, apply_sweep=False):
+    """The index load with the files sharded by fid range over several scanners
+    (one per GPU, or several on one): cly_db_open_multi; the index is rebuilt on
+    scanners[0]'s device."""
+    return LoadedDB(list(scanners), path, data_file_size, apply_sweep)

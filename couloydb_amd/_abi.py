@@ -91,7 +91,7 @@ SCAN_SYMBOLS = ["cly_ctx_create", "cly_ctx_destroy", "cly_ctx_set_clock", "cly_s
                 "cly_index_device", "cly_index", "cly_append_device", "cly_append",
                 "cly_strerror", "cly_build_info"]
 GEN_SYMBOLS = ["cly_gen_record_size", "cly_gen_layout", "cly_gen_encode"]
-LOAD_SYMBOLS = ["cly_db_open", "cly_db_open_opts", "cly_db_close", "cly_db_get", "cly_db_listmeta", "cly_db_hget",
+LOAD_SYMBOLS = ["cly_db_open", "cly_db_open_opts", "cly_db_open_multi", "cly_db_close", "cly_db_get", "cly_db_listmeta", "cly_db_hget",
                 "cly_db_lget", "cly_db_sget", "cly_db_value", "cly_index_key", "cly_db_count", "cly_db_entries"]
 DB_NOT_FOUND, DB_EOF = 1, 2
 ERR_DIR, ERR_MERGE_FIN = -14, -15
@@ -112,7 +112,7 @@ class ClyLoadStats(ctypes.Structure):
                 ("active_fid", ctypes.c_uint32), ("_pad", ctypes.c_uint32), ("write_off", ctypes.c_int64),
                 ("hint_records", ctypes.c_uint64), ("n_expired", ctypes.c_uint64),
                 ("write_off_loaded", ctypes.c_int64), ("active_fid_loaded", ctypes.c_uint32),
-                ("sweep_files", ctypes.c_uint32)]
+                ("sweep_files", ctypes.c_uint32), ("n_shards", ctypes.c_uint32), ("_pad2", ctypes.c_uint32)]
 
 
 class ClyDbOptions(ctypes.Structure):
@@ -152,6 +152,9 @@ def load_scan_lib(name="libclyscan.so"):
     lib.cly_db_open_opts.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, P(ctypes.c_void_p),
                                      ctypes.c_void_p]
     lib.cly_db_open_opts.restype = ctypes.c_int
+    lib.cly_db_open_multi.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_void_p,
+                                      P(ctypes.c_void_p), ctypes.c_void_p]
+    lib.cly_db_open_multi.restype = ctypes.c_int
     lib.cly_db_count.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.cly_db_count.restype = ctypes.c_uint64
     lib.cly_db_entries.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]

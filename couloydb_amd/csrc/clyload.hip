@@ -393,10 +393,22 @@ __global__ void k_hint_as_put(cly_tuple* t, uint64_t n) {
     t[i].tx_id = 0; t[i].txid_len = 0; t[i].type = 0; t[i].data_type = 0; t[i].expiration = 0;
 }
 
-// The files' bytes to the device: load_threads() threads fault the mapped
-// pages in and copy 64-MiB pieces through page-locked staging buffers (CPU
-// copy of one while the DMA of the other runs).
-static int copy_to_device(cly_ctx* ctx, const std::vector<cly_file>& hf, std::vector<cly_file>& df, uint8_t* d_bytes) {
+// Page-locked staging buffers (two per copy thread), allocated once; the
+// caller holds g_stage_mu.
+static int stage_ready() {
+    for (int k = 0; k < 2 * LOAD_THREADS_MAX; k++)          // (again after a failed allocation)
+        if (!g_stage[k] && hipHostMalloc(&g_stage[k], LOAD_STAGE, hipHostMallocPortable) != hipSuccess) {
+            g_stage[k] = nullptr;
+            return CLY_ERR_DEVICE;
+        }
+    return CLY_OK;
+}
+// The files' bytes to device dev: nt threads (staging buffers of threads t0 ..
+// t0+nt-1) fault the mapped pages in and copy 64-MiB pieces through the
+// page-locked staging buffers (CPU copy of one while the DMA of the other
+// runs).  The caller holds g_stage_mu.
+static int copy_to_device(int dev, const std::vector<cly_file>& hf, std::vector<cly_file>& df, uint8_t* d_bytes,
+                          int t0, int nt) {
     struct Piece { const uint8_t* src; uint8_t* dst; uint64_t len; };
     std::vector<Piece> pieces;
     uint64_t off = 0;
@@ -409,15 +421,6 @@ static int copy_to_device(cly_ctx* ctx, const std::vector<cly_file>& hf, std::ve
     }
     std::atomic<size_t> next(0);
     std::atomic<int> err(0);
-    const int dev = cly_ctx_device_internal(ctx);
-    const int nt = load_threads();
-    std::lock_guard<std::mutex> lk(g_stage_mu);
-    for (int k = 0; k < 2 * LOAD_THREADS_MAX; k++)          // (again after a failed allocation)
-        if (!g_stage[k] && hipHostMalloc(&g_stage[k], LOAD_STAGE, hipHostMallocPortable) != hipSuccess) {
-            g_stage[k] = nullptr;
-            err = 1;
-        }
-    if (err) return CLY_ERR_DEVICE;
     par_run(nt, [&](int t) {
         if (hipSetDevice(dev) != hipSuccess) { err = 1; return; }
         hipStream_t ts = nullptr;
@@ -431,7 +434,7 @@ static int copy_to_device(cly_ctx* ctx, const std::vector<cly_file>& hf, std::ve
             const Piece& pc = pieces[k];
             for (uint64_t a = 0; a < pc.len; a += LOAD_STAGE) {
                 const uint64_t n = std::min<uint64_t>(LOAD_STAGE, pc.len - a);
-                uint8_t* stg = (uint8_t*)g_stage[2 * t + b];
+                uint8_t* stg = (uint8_t*)g_stage[2 * (t0 + t) + b];
                 if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) err = 1;
                 memcpy(stg, pc.src + a, n);
                 if (hipMemcpyAsync(pc.dst + a, stg, n, hipMemcpyHostToDevice, ts) != hipSuccess ||
@@ -460,12 +463,7 @@ static int copy_to_host(cly_ctx* ctx, const std::vector<D2H>& parts) {
     std::atomic<int> err(0);
     const int dev = cly_ctx_device_internal(ctx);
     std::lock_guard<std::mutex> lk(g_stage_mu);
-    for (int k = 0; k < 2 * LOAD_THREADS_MAX; k++)
-        if (!g_stage[k] && hipHostMalloc(&g_stage[k], LOAD_STAGE, hipHostMallocPortable) != hipSuccess) {
-            g_stage[k] = nullptr;
-            err = 1;
-        }
-    if (err) return CLY_ERR_DEVICE;
+    if (stage_ready() != CLY_OK) return CLY_ERR_DEVICE;
     par_run(load_threads(), [&](int t) {
         if (hipSetDevice(dev) != hipSuccess) { err = 1; return; }
         hipStream_t ts = nullptr;
@@ -541,13 +539,64 @@ static std::vector<uint8_t> tombstone(const uint8_t* key, uint64_t klen) {
 }
 
 extern "C" int cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load_stats* st) {
-    return cly_db_open_opts(ctx, dir, nullptr, out, st);
+    return cly_db_open_multi(&ctx, 1, dir, nullptr, out, st);
 }
-
 extern "C" int cly_db_open_opts(cly_ctx* ctx, const char* dir, const cly_db_options* opt, cly_db** out,
                                 cly_load_stats* st) {
-    if (!ctx || !dir || !out) return CLY_ERR_ARG;
+    return cly_db_open_multi(&ctx, 1, dir, opt, out, st);
+}
+
+// One shard of the load: a contiguous range [f0, f1) of the open's files (the
+// hint-index first when present, then the data files by fid), copied to its
+// context's device and scanned there.
+struct LoadShard {
+    cly_ctx* ctx = nullptr;
+    int dev = 0, f0 = 0, f1 = 0;
+    uint8_t* d_bytes = nullptr;
+    cly_tuple* d_tup = nullptr;
+    uint64_t cap = 0, need = 0;
+    std::vector<cly_file> df;
+    std::vector<cly_file_result> res;
+    std::vector<uint64_t> first;
+    int rc = CLY_OK;
+    double t_copy = 0, t_scan = 0;
+};
+static void shard_load(LoadShard& S, const std::vector<cly_file>& hf, int t0, int nt) {
+    const int n = S.f1 - S.f0;
+    const std::vector<cly_file> h(hf.begin() + S.f0, hf.begin() + S.f1);
+    S.df.resize(n); S.res.resize(n); S.first.resize(n);
+    if (hipSetDevice(S.dev) != hipSuccess) { S.rc = CLY_ERR_DEVICE; return; }
+    uint64_t total = 0;
+    for (const cly_file& f : h) total += (f.len + 4095) & ~4095ull;
+    if (hipMalloc((void**)&S.d_bytes, total + 4096) != hipSuccess) { S.d_bytes = nullptr; S.rc = CLY_ERR_DEVICE; return; }
+    S.rc = copy_to_device(S.dev, h, S.df, S.d_bytes, t0, nt);
+    S.t_copy = now_ms();
+    if (S.rc != CLY_OK) return;
+    S.cap = cly_scan_capacity(h.data(), n) + 16;
+    if (hipMalloc((void**)&S.d_tup, sizeof(cly_tuple) * S.cap) != hipSuccess) { S.d_tup = nullptr; S.rc = CLY_ERR_DEVICE; return; }
+    S.rc = cly_scan_device(S.ctx, S.df.data(), n, S.d_tup, S.cap, S.first.data(), S.res.data(), &S.need, nullptr, nullptr);
+    if (S.rc == CLY_ERR_CAPACITY && S.need > S.cap) {
+        // records shorter than 9 B: the exact need, scanned again
+        hipFree(S.d_tup); S.d_tup = nullptr;
+        S.cap = S.need + 16;
+        if (hipMalloc((void**)&S.d_tup, sizeof(cly_tuple) * S.cap) != hipSuccess) { S.d_tup = nullptr; S.rc = CLY_ERR_DEVICE; return; }
+        S.rc = cly_scan_device(S.ctx, S.df.data(), n, S.d_tup, S.cap, S.first.data(), S.res.data(), &S.need, nullptr,
+                               nullptr);
+    }
+    S.t_scan = now_ms();
+}
+static void shard_free(LoadShard& S) {
+    if (!S.d_bytes && !S.d_tup) return;
+    if (hipSetDevice(S.dev) == hipSuccess) { hipFree(S.d_bytes); hipFree(S.d_tup); }
+    S.d_bytes = nullptr; S.d_tup = nullptr;
+}
+
+extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir, const cly_db_options* opt,
+                                 cly_db** out, cly_load_stats* st) {
+    if (!ctxs || nctx < 1 || nctx > LOAD_THREADS_MAX || !dir || !out) return CLY_ERR_ARG;
+    for (int k = 0; k < nctx; k++) if (!ctxs[k]) return CLY_ERR_ARG;
     *out = nullptr;
+    cly_ctx* ctx = ctxs[0];                      // the index is rebuilt on the first context
     cly_load_stats s;
     memset(&s, 0, sizeof(s));
     const uint64_t dfs = opt && opt->data_file_size ? opt->data_file_size : (256ull << 20);
@@ -556,18 +605,20 @@ extern "C" int cly_db_open_opts(cly_ctx* ctx, const char* dir, const cly_db_opti
     cly_db* db = new cly_db();
     int rc = list_files(dir, db->files);
     const int nf = (int)db->files.size();
+    const int dev0 = cly_ctx_device_internal(ctx);
     bool has_hint = false;
     int nall = 0;                                // hint (file 0 when present) + data files
-    uint8_t* d_bytes = nullptr;
-    cly_tuple* d_tup = nullptr;
+    cly_tuple* d_tup = nullptr;                  // every tuple, in file order, on the first context's device
+    bool own_tup = false;
     uint8_t* d_state = nullptr;
     cly_pos* d_hpos = nullptr;
     std::vector<cly_file> hf, df;
     std::vector<cly_file_result> res;
     std::vector<uint64_t> first;
-    uint64_t total = 0, need = 0, cap = 0;
+    std::vector<LoadShard> sh(nctx);
+    uint64_t need = 0;
     hipStream_t strm = cly_ctx_stream_internal(ctx);
-    double t1, t2, t3, t4, t5;
+    double t1, t2 = 0, t3, t4, t5;
     cly_index_result ir;
     if (rc != CLY_OK) goto done;
     {
@@ -583,32 +634,85 @@ extern "C" int cly_db_open_opts(cly_ctx* ctx, const char* dir, const cly_db_opti
     s.list_map_ms = t1 - t0;
     s.n_files = (uint64_t)nf;
     nall = nf + (has_hint ? 1 : 0);
-    hf.resize(nall ? nall : 1); df.resize(nall ? nall : 1); res.resize(nall ? nall : 1); first.resize(nall ? nall : 1);
+    hf.resize(nall);
     if (has_hint) { hf[0].base = db->hint.p; hf[0].len = db->hint.len; hf[0].fid = 0; hf[0]._pad = 0; }
     for (int i = 0; i < nf; i++) {
         cly_file& f = hf[i + (has_hint ? 1 : 0)];
         f.base = db->files[i].p; f.len = db->files[i].len; f.fid = db->files[i].fid; f._pad = 0;
         s.bytes += f.len;
     }
-    for (int i = 0; i < nall; i++) total += (hf[i].len + 4095) & ~4095ull;
-    DCK(hipSetDevice(cly_ctx_device_internal(ctx)));
-    DCK(hipMalloc((void**)&d_bytes, total + 4096));
-    rc = copy_to_device(ctx, hf, df, d_bytes);
-    if (rc != CLY_OK) goto done;
-    t2 = now_ms();
-    s.h2d_ms = t2 - t1;
-    cap = cly_scan_capacity(hf.data(), nall) + 16;
-    DCK(hipMalloc((void**)&d_tup, sizeof(cly_tuple) * cap));
+    {
+        // contiguous file ranges balanced by bytes (each file weighs len + 4 KiB):
+        // a file goes to the shard its weight's midpoint falls in; file 0 to
+        // shard 0 (a single non-empty shard is then the first context's)
+        uint64_t tot = 0, acc = 0;
+        for (const cly_file& f : hf) tot += f.len + 4096;
+        int f = 0;
+        for (int k = 0; k < nctx; k++) {
+            sh[k].ctx = ctxs[k];
+            sh[k].dev = cly_ctx_device_internal(ctxs[k]);
+            sh[k].f0 = f;
+            const uint64_t target = tot / (uint64_t)nctx * (uint64_t)(k + 1) + (k + 1 == nctx ? tot : 0);
+            while (f < nall && (f == 0 || acc + (hf[f].len + 4096) / 2 <= target)) acc += hf[f++].len + 4096;
+            sh[k].f1 = f;
+        }
+        s.n_shards = 0;
+        for (const LoadShard& S : sh) s.n_shards += S.f1 > S.f0;
+    }
     if (nall) {
-        rc = cly_scan_device(ctx, df.data(), nall, d_tup, cap, first.data(), res.data(), &need, nullptr, nullptr);
-        if (rc == CLY_ERR_CAPACITY && need > cap) {
-            // records shorter than 9 B: the exact need, scanned again
-            hipFree(d_tup); d_tup = nullptr;
-            cap = need + 16;
-            DCK(hipMalloc((void**)&d_tup, sizeof(cly_tuple) * cap));
-            rc = cly_scan_device(ctx, df.data(), nall, d_tup, cap, first.data(), res.data(), &need, nullptr, nullptr);
+        // the shards in parallel, one host thread each (load_threads() copy
+        // threads shared out), each on its own context's device and stream
+        std::lock_guard<std::mutex> lk(g_stage_mu);
+        if (stage_ready() != CLY_OK) { rc = CLY_ERR_DEVICE; goto done; }
+        const int nt = load_threads(), ntk = std::max(1, nt / (int)s.n_shards);
+        std::vector<std::thread> th;
+        int slot = 0;
+        for (LoadShard& S : sh) {
+            if (S.f1 == S.f0) continue;
+            th.emplace_back(shard_load, std::ref(S), std::cref(hf), slot, ntk);
+            slot += ntk;
+        }
+        for (auto& x : th) x.join();
+        for (const LoadShard& S : sh) {
+            if (S.f1 == S.f0) continue;
+            if (S.rc != CLY_OK && rc == CLY_OK) rc = S.rc;
+            t2 = std::max(t2, S.t_copy);
         }
         if (rc != CLY_OK) goto done;
+    } else t2 = t1;
+    s.h2d_ms = t2 - t1;
+    // the shards' results in file order; their tuples gathered on the first
+    // context's device (peer copies), whose index reads every shard's file bytes
+    // in place (peer access when a shard is on another device)
+    df.resize(nall); res.resize(nall); first.resize(nall);
+    for (const LoadShard& S : sh) {
+        for (int i = S.f0; i < S.f1; i++) {
+            df[i] = S.df[i - S.f0];
+            res[i] = S.res[i - S.f0];
+            first[i] = need + S.first[i - S.f0];
+        }
+        need += S.need;
+    }
+    DCK(hipSetDevice(dev0));
+    if (s.n_shards <= 1) {
+        d_tup = sh[0].d_tup;
+    } else {
+        DCK(hipMalloc((void**)&d_tup, sizeof(cly_tuple) * (need + 16)));
+        own_tup = true;
+        uint64_t off = 0;
+        for (const LoadShard& S : sh) {
+            if (S.f1 == S.f0) continue;
+            if (S.dev != dev0) {
+                int can = 0;
+                DCK(hipDeviceCanAccessPeer(&can, dev0, S.dev));
+                if (!can) { rc = CLY_ERR_DEVICE; goto done; }
+                const hipError_t e = hipDeviceEnablePeerAccess(S.dev, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) { rc = CLY_ERR_DEVICE; goto done; }
+                (void)hipGetLastError();
+            }
+            if (S.need) DCK(hipMemcpyPeerAsync(d_tup + off, dev0, S.d_tup, S.dev, sizeof(cly_tuple) * S.need, strm));
+            off += S.need;
+        }
     }
     for (int i = 0; i < nall; i++)
         if (res[i].status < 0) { rc = res[i].status; goto done; }         // loadIndexFromHintFile / loadIndex return it
@@ -629,6 +733,7 @@ extern "C" int cly_db_open_opts(cly_ctx* ctx, const char* dir, const cly_db_opti
         s.active_fid_loaded = db->files[nf - 1].fid;
         s.write_off_loaded = res[nall - 1].end_offset;                    // db.go:632-634
     }
+    DCK(hipStreamSynchronize(strm));
     t3 = now_ms();
     s.scan_ms = t3 - t2;
     DCK(hipMalloc((void**)&d_state, need ? need : 1));
@@ -723,7 +828,10 @@ extern "C" int cly_db_open_opts(cly_ctx* ctx, const char* dir, const cly_db_opti
     s.insert_ms = t5 - t4;
     s.total_ms = t5 - t0;
 done:
-    hipFree(d_bytes); hipFree(d_tup); hipFree(d_state); hipFree(d_hpos);
+    (void)hipSetDevice(dev0);
+    if (own_tup) hipFree(d_tup);
+    hipFree(d_state); hipFree(d_hpos);
+    for (LoadShard& S : sh) shard_free(S);
     if (st) *st = s;
     if (rc != CLY_OK) { cly_db_close(db); return rc; }
     *out = db;

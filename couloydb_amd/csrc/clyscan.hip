@@ -184,6 +184,17 @@ __device__ __forceinline__ uint32_t crc_unbytes(const CLY_LDS uint8_t* smem, uin
     for (uint32_t k = 0; k < j; k++) d = crc_unbyte(smem, d, r4);
     return d;
 }
+// A^k d (k < 4 zero bytes forwards): (d >> 8k) ^ sum_{i<k} T_{k-1-i}[byte i of d],
+// k independent lookups (T_t = the slicing tables, dword (i*64 + t*16 + r))
+__device__ __forceinline__ uint32_t crc_fwd(const CLY_LDS uint8_t* smem, uint32_t d, uint32_t k, uint32_t r4) {
+    const uint32_t b0 = d & 0xffu, b1 = (d >> 8) & 0xffu, b2 = (d >> 16) & 0xffu;
+    const uint32_t t = k - 1u;                                    // table of byte 0 (k >= 1)
+    uint32_t v = k == 3u ? d >> 24 : (k == 2u ? d >> 16 : d >> 8);
+    v ^= *(const CLY_LDS uint32_t*)(smem + ((b0 << 8) | (t << 6) | r4));
+    if (k >= 2u) v ^= *(const CLY_LDS uint32_t*)(smem + ((b1 << 8) | ((t - 1u) << 6) | r4));
+    if (k >= 3u) v ^= *(const CLY_LDS uint32_t*)(smem + ((b2 << 8) | r4));
+    return v;
+}
 // M v by a nibble table of M
 __device__ __forceinline__ uint32_t mat_mul(const CLY_LDS uint32_t* t, uint32_t v) {
     uint32_t p = 0;
@@ -584,6 +595,17 @@ __device__ __forceinline__ void patch_word(uint32_t (&w)[16], uint32_t k, uint32
 #ifndef CLY_EXP
 #define CLY_EXP 0                // timing experiments only (wrong results): 1 no record work, 3 candidate
 #endif                           // masks only, 2 no per-record outputs, 5 no agreement pass
+#ifndef CLY_PROF
+#define CLY_PROF 0               // experiment builds: per-section cycle counts of k_scan's tile body
+#endif
+#if CLY_PROF
+__device__ unsigned long long g_prof[8];
+#define PT(i) do { if (BM == BM_SPEC) { const uint64_t n_ = __builtin_amdgcn_s_memtime(); pacc[i] += n_ - pt; pt = n_; } } while (0)
+#define PC(i) do { if (BM == BM_SPEC) pacc[i]++; } while (0)
+#else
+#define PT(i) do {} while (0)
+#define PC(i) do {} while (0)
+#endif
 struct TileRes { uint32_t X; bool dead; };
 // The chain state a wave carries through its tile (wave-uniform).
 struct TState {
@@ -602,15 +624,22 @@ struct TState {
 // to be XORed into the stage word holding P (one writer per word: record
 // starts are >= 7 B apart) once no header read of the stage can still see
 // that word (the tail of the record before P shares it).
+// The register XOR d due before byte P goes into the data: into P's word as
+// is when P is word-aligned, else as A^(4 - (P & 3)) d into the word after
+// it (the register after P's word); pw = that word's index in the block
+// (1024: the next block's first word, carried).
 template <int BM>
 __device__ __forceinline__ uint32_t rec_out(const DevFile& F, gbytes base, uint32_t p, const Hdr& h, uint32_t idx,
-                                            uint32_t tb, uint32_t dq, const CLY_LDS uint8_t* smem, const CrcLane& cl,
-                                            uint32_t K4, uint32_t* trec, gtuples out, uint64_t out_cap, uint64_t gbase,
-                                            Globals* g) {
-    if (BM == BM_EMIT) { put_tuple(out, gbase + idx, out_cap, base, p, h, F.fid, g); return 0u; }
+                                            uint32_t tb, uint32_t bs, uint32_t dq, const CLY_LDS uint8_t* smem,
+                                            const CrcLane& cl, uint32_t K4, uint32_t* trec, gtuples out,
+                                            uint64_t out_cap, uint64_t gbase, Globals* g, uint32_t& pw) {
+    if (BM == BM_EMIT) { put_tuple(out, gbase + idx, out_cap, base, p, h, F.fid, g); pw = 0; return 0u; }
     if (idx < CAP_T) rec_store(trec + 4 * idx, h, p - tb);
-    return crc_unbytes(smem, h.crc ^ K4 ^ dq, p & 3u, cl.r4);
+    const uint32_t d = h.crc ^ K4 ^ dq, j = p & 3u;
+    pw = ((p - bs) >> 2) + (j ? 1u : 0u);
+    return j ? crc_fwd(smem, d, 4u - j, cl.r4) : d;
 }
+#define PW_CARRY (CLY_BLK / 4)
 // The terminal T (found by lane src): the bytes from T on read as zero, and
 // ~cq of the record before it (dT) is XORed in before byte T (into the word
 // holding T, after the zeroing), or at the next block's first byte when T is
@@ -621,7 +650,7 @@ __device__ __forceinline__ void term_patch(TState& S, uint32_t T, uint32_t dT, u
     S.Tb = T;
     if (BM == BM_EMIT) return;
     if (T < bs + CLY_BLK) S.tpatch = rdl(crc_unbytes(smem, dT, T & 3u, cl.r4), src);
-    else S.carry_next = rdl(dT, src);
+    else S.carry_next ^= rdl(dT, src);
 }
 
 // Exact predictive walk (entry X known and in this block): lane k decodes the
@@ -664,10 +693,15 @@ __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t 
         const uint32_t up = dppu<DPP_WF_SR1>(0u, h.crc);
         const uint32_t dq = k == 0 ? (S.cq_known ? ~S.cq : 0xFFFFFFFFu) : ~up;
         // every lane of the round has read its header: the patches may go in
+        uint32_t pw = 0, pv = 0;
         if (acc) {
-            const uint32_t pv = rec_out<BM>(F, base, (uint32_t)P, h, S.tcnt + k, tb, P == 0 ? 0u : dq, smem, cl, K4,
-                                            trec, out, out_cap, gbase, g);
-            if (BM != BM_EMIT) stg[((uint32_t)P - bs) >> 2] ^= pv;
+            pv = rec_out<BM>(F, base, (uint32_t)P, h, S.tcnt + k, tb, bs, P == 0 ? 0u : dq, smem, cl, K4, trec, out,
+                             out_cap, gbase, g, pw);
+            if (BM != BM_EMIT && pw < PW_CARRY) stg[pw] ^= pv;
+        }
+        if (BM != BM_EMIT) {
+            const u64 bc = __ballot(acc && pw == PW_CARRY);
+            if (bc) S.carry_next ^= rdl(pv, __ffsll((long long)bc) - 1);
         }
         if (S.G == NONE32) S.G = (uint32_t)X;
         if (n) {
@@ -782,6 +816,9 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     uint32_t* trec = rec + (uint64_t)t * CAP_T * 4;
     CLY_LDS u32x4* sv = (CLY_LDS u32x4*)stg;
     u32x4 e[4], hl;
+#if CLY_PROF
+    uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = __builtin_amdgcn_s_memtime();
+#endif
     blk_issue(base, flen, tb, lane, e, hl);
     #pragma unroll 1
     for (int m = 0; m < CLY_NBLK; m++) {
@@ -791,6 +828,7 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
         uint32_t w[16];
         #pragma unroll
         for (int k = 0; k < 4; k++) { w[4 * k] = e[k].x; w[4 * k + 1] = e[k].y; w[4 * k + 2] = e[k].z; w[4 * k + 3] = e[k].w; }
+        PT(0);
         const u32x4 hc = hl;
         if (m + 1 < CLY_NBLK && (BM != BM_EMIT || !S.dead)) blk_issue(base, flen, bs + CLY_BLK, lane, e, hl);
         if (BM == BM_EMIT && S.dead) break;
@@ -807,10 +845,13 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
             if (lane < 4) sv[CLY_BLK / 16 + lane] = hc;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (S.X == NONE32) S.X = guess_entry(F, bs, stg, hc, lane);     // the tile's guessed entry
+            if (S.X == NONE32) { S.X = guess_entry(F, bs, stg, hc, lane); PC(6); }    // the tile's guessed entry
+            PT(1);
             bool done = true;
             if (S.X != NONE32) done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, trec, out, out_cap, gbase, g, lane);
+            PT(2);
             if (!done) {
+                PC(7);
                 // ---- general pass (the predictive walk's round budget ran out):
                 // every lane's first candidate record start in its 64-B segment
                 // after X, then agreement
@@ -857,21 +898,27 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                     // (the patch of a lane's first record waits for the loop's end: the
                     // lane before reads its last header, whose tail shares that word,
                     // in a later iteration)
-                    uint32_t p = L.E, psz = 0, ppsz = 0, p0w = 0, p0v = 0;
+                    uint32_t p = L.E, psz = 0, ppsz = 0, p0w = PW_CARRY + 1, p0v = 0, cv = 0;
                     for (uint32_t i = 0; CLY_EXP != 2 && __ballot(i < c); i++) {
                         if (i < c) {
                             const Hdr h = hdr_get(base, p, flen, stg, bs);
-                            const uint32_t pv = rec_out<BM>(F, base, p, h, S.tcnt + lex + i, tb,
+                            uint32_t pw;
+                            const uint32_t pv = rec_out<BM>(F, base, p, h, S.tcnt + lex + i, tb, bs,
                                                             p == 0 ? 0u : (pk ? ~pcq : 0xFFFFFFFFu), smem, cl, K4, trec,
-                                                            out, out_cap, gbase, g);
-                            if (i == 0) { p0w = (p - bs) >> 2; p0v = pv; }
-                            else if (BM != BM_EMIT) stg[(p - bs) >> 2] ^= pv;
+                                                            out, out_cap, gbase, g, pw);
+                            if (pw == PW_CARRY) cv = pv;
+                            else if (i == 0) { p0w = pw; p0v = pv; }
+                            else if (BM != BM_EMIT) stg[pw] ^= pv;
                             pcq = h.crc; pk = true;
                             ppsz = psz; psz = (uint32_t)h.size;
                             p += (uint32_t)h.size;
                         }
                     }
-                    if (BM != BM_EMIT && c > 0) stg[p0w] ^= p0v;
+                    if (BM != BM_EMIT) {
+                        if (p0w < PW_CARRY) stg[p0w] ^= p0v;
+                        const u64 bc = __ballot(cv != 0);
+                        if (bc) S.carry_next ^= rdl(cv, __ffsll((long long)bc) - 1);
+                    }
                     if (kT < 64) {
                         const uint32_t T = rdl(L.x, kT);
                         const uint32_t dT = T == 0 ? 0u : (pk ? ~pcq : 0xFFFFFFFFu);
@@ -898,6 +945,7 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                     }
                 }
             }
+            PT(3);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             if (BM != BM_EMIT) {
@@ -930,6 +978,7 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
             #pragma unroll
             for (int k = 0; k < 16; k++) R = crc_word(smem, R ^ w[k], cl);
         }
+        PT(4);
     }
     TileRes res;
     res.X = S.X; res.dead = S.dead;
@@ -959,6 +1008,11 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
             d->l[2] = (u64)S.last_crc | ((u64)S.P_last << 32);
             d->l[3] = (u64)tend | ((u64)(uint8_t)(int8_t)S.term << 32);
         }
+        PT(5);
+#if CLY_PROF
+        if (lane == 0)
+            for (int i = 0; i < 8; i++) atomicAdd(&g_prof[i], (unsigned long long)pacc[i]);
+#endif
     }
     return res;
 }
@@ -1818,6 +1872,15 @@ extern "C" void** cly_ctx_merge_slot_internal(cly_ctx* c) { return &c->merge_scr
 // LOCALs); cly_dbg_tiles copies the snapshot (32 B per tile) and the final
 // TileIns (32 B per tile) of the last call to host memory.
 extern "C" void cly_dbg_set(cly_ctx* c, int flags) { c->dbg = flags; }
+#if CLY_PROF
+// experiment builds: the section cycle sums of k_scan since the last call (reset)
+extern "C" int cly_dbg_prof(cly_ctx* c, unsigned long long* out8) {
+    hipStreamSynchronize(c->stream);
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 extern "C" int cly_dbg_tiles(cly_ctx* c, void* loc_out, void* tin_out, int64_t ntiles) {
     HIPCK(hipSetDevice(c->device));
     if (loc_out && c->d_dbg && ntiles <= c->cap_dbg)

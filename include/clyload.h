@@ -70,6 +70,8 @@ typedef struct cly_load_stats {
     int64_t  write_off_loaded;/* WriteOff as loadIndex leaves it (before the sweep) */
     uint32_t active_fid_loaded;
     uint32_t sweep_files;     /* new data files the sweep's appends opened        */
+    uint32_t n_shards;        /* contexts that loaded files (cly_db_open_multi)   */
+    uint32_t _pad2;
 } cly_load_stats;
 
 /* NewCouloyDB's Options the open uses.                                        */
@@ -83,6 +85,19 @@ typedef struct cly_db_options {
 /* cly_db_open = cly_db_open_opts with default options (nothing written).    */
 int  cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load_stats* st);
 int  cly_db_open_opts(cly_ctx* ctx, const char* dir, const cly_db_options* opt, cly_db** out, cly_load_stats* st);
+/* The same open over nctx contexts (one per GPU; several may share one): the
+ * files (hint-index first, then the data files by fid) are cut into nctx
+ * contiguous ranges balanced by bytes, and each context copies its range to
+ * its device and scans it (cly_scan_device), all in parallel.  The tuples are
+ * then gathered in fid order on ctxs[0]'s device, whose index rebuild reads
+ * every range's bytes in place (peer access between devices): loadIndex's
+ * single pass over the fids (db.go:582-637) with its tx buffers, so a
+ * transaction whose records and commit fall in different ranges resolves as
+ * in one pass.  Result identical to cly_db_open_opts(ctxs[0], ...).
+ * CLY_ERR_DEVICE when a range's device cannot be reached from ctxs[0]'s.
+ * 1 <= nctx <= 16.                                                            */
+int  cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir, const cly_db_options* opt, cly_db** out,
+                       cly_load_stats* st);
 void cly_db_close(cly_db* db);
 /* Index lookups: CLY_OK with *pos, or CLY_DB_NOT_FOUND.                      */
 int  cly_db_get(cly_db* db, const uint8_t* key, uint64_t klen, cly_pos* pos);          /* String   */

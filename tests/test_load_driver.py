@@ -276,3 +276,58 @@ def test_gpu_value_statuses(scanner, tmp_path):
         with pytest.raises(ScanError) as e:
             db.value(LogPos(0, -1))
         assert e.value.code == _abi.ERR_OFFSET
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nctx", [2, 3, 5])
+def test_gpu_open_multi_matches_single(scanner, tmp_path, nctx):
+    """cly_db_open_multi: the merged directory's files sharded by fid range over
+    nctx contexts (all on device 0 here; one per GPU on a node) give the same
+    index, counts, WriteOff and entries as the one-context open."""
+    from couloydb_amd import Scanner, _abi, open_db_multi
+    files, hint = merged_dir(7, tmp_path, new_ops=900)
+    ix = restated_index(files, hint)
+    scanner.set_clock(INDEX_NOW)
+    extra = [Scanner(0) for _ in range(nctx - 1)]
+    try:
+        for sc in extra:
+            sc.set_clock(INDEX_NOW)
+        with scanner.open_db(str(tmp_path)) as one, open_db_multi([scanner] + extra, str(tmp_path)) as db:
+            assert 1 < db.stats.n_shards <= nctx and one.stats.n_shards == 1
+            for f in ("records", "hint_records", "n_files", "write_off", "active_fid", "str_keys", "hash_fields",
+                      "list_items", "set_members", "n_expired"):
+                assert getattr(db.stats, f) == getattr(one.stats, f), f
+            check_lookups(db, ix)
+            for kind in range(6):
+                assert sorted(db.entries(kind)) == sorted(one.entries(kind)), kind
+    finally:
+        for sc in extra:
+            sc.close()
+
+
+@pytest.mark.gpu
+def test_gpu_open_multi_tx_across_shards(scanner, tmp_path):
+    """A transaction whose records end file 1 and whose commit opens file 2 (the
+    two shards' boundary) applies; a rolled-back one split the same way does
+    not; a tx begun in shard 0 and never finished stays out."""
+    from couloydb_amd import Scanner, open_db_multi
+    pad = lambda i, n: b"".join(mg.encode_record(mg.key_tx(b"p%d-%d" % (i, j), 0), b"x" * 200) for j in range(n))
+    f0 = pad(0, 40) + mg.encode_record(mg.key_tx(b"u", 91), b"never")
+    f1 = pad(1, 38) + mg.encode_record(mg.key_tx(b"a", 77), b"va") + mg.encode_record(mg.key_tx(b"b", 78), b"vb") + \
+        mg.encode_record(mg.key_tx(b"c", 77), b"vc")
+    f2 = mg.encode_record(mg.key_tx(mg.TX_COMMIT_KEY, 77), b"", mg.TXN_COMMIT) + \
+        mg.encode_record(mg.key_tx(mg.TX_ROLLBACK_KEY, 78), b"", mg.TXN_ROLLBACK) + pad(2, 40)
+    f3 = pad(3, 41)
+    write_dir(tmp_path, [f0, f1, f2, f3])
+    other = Scanner(0)
+    try:
+        with open_db_multi([scanner, other], str(tmp_path)) as db:
+            assert db.stats.n_shards == 2
+            assert db.get(b"a") == b"va" and db.get(b"c") == b"vc"
+            for k in (b"b", b"u"):
+                with pytest.raises(KeyError):
+                    db.get(k)
+            assert db.stats.str_keys == 40 + 38 + 40 + 41 + 2
+            assert db.stats.write_off == len(f3) and db.stats.active_fid == 3
+    finally:
+        other.close()
