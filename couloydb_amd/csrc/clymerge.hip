@@ -439,20 +439,36 @@ k_mplace(const MEnt* __restrict__ e, const cly_tuple* __restrict__ tup, const ui
 }
 
 // ---- k_mhint: hint-index records (data/dataFile.go:114-121) -----------------
-// The hint records of a workgroup's 256 consecutive live records are contiguous
-// in the hint file: they are assembled in LDS and written out with aligned
-// dword stores (byte stores only at the two ends), unless they exceed the LDS
-// buffer (large keys), when each thread stores its own record's bytes.
+// Record of live record j: crc(4) 0 0 varint(rk) varint(pl) 0x00 realKey pos,
+// pos = varint(fid) varint(off) (EncodeLogRecordPos), CRC over bytes 4 .. end.
+// The records of a workgroup's 256 consecutive live records are contiguous in
+// the hint file: each thread writes its bytes into an LDS stage laid out at
+// the output's 16-B phase (header and pos from registers, realKey from aligned
+// dword loads), then computes its CRC slicing-by-4 from the stage, and the
+// workgroup stores the stage with 16-B stores.  A workgroup whose records
+// exceed the stage (large keys) writes to global directly, CRC byte by byte.
 #define MH_BUF 12288
+#define CLY_GLB __attribute__((address_space(1)))            // global (not flat) loads
+// Go's PutUvarint of u (< 2^56) packed little-endian, *n bytes
+__device__ __forceinline__ uint64_t uv_pack(uint64_t u, int& n) {
+    uint64_t r = 0;
+    int k = 0;
+    while (u >= 0x80) { r |= ((u & 0x7f) | 0x80) << (8 * k); u >>= 7; k++; }
+    n = k + 1;
+    return r | (u << (8 * k));
+}
+__device__ __forceinline__ uint32_t byte_of(uint64_t lo, uint64_t hi, int q) {
+    return (uint32_t)((q < 8 ? lo >> (8 * q) : hi >> (8 * (q - 8))) & 0xffu);
+}
 __global__ void __launch_bounds__(M_NT)
 k_mhint(const MEnt* __restrict__ e, const MCopy* __restrict__ cp, const cly_tuple* __restrict__ tup,
         const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases, int nfiles,
         const uint32_t* __restrict__ hsz, const MSum* __restrict__ bsum, const MTot* tot, uint64_t stride,
         uint8_t* hint, uint64_t hint_cap) {
-    __shared__ uint32_t tab[256];
+    __shared__ uint32_t t4[1024];
     __shared__ MSum sh[M_NT / 64];
-    __shared__ __attribute__((aligned(16))) uint8_t buf[MH_BUF + 16];
-    crc_table_init(tab);
+    __shared__ __attribute__((aligned(16))) uint8_t buf[MH_BUF + 48];
+    crc_table4_init(t4);
     const uint64_t nl = tot->nl;
     const uint64_t b0 = (uint64_t)blockIdx.x * M_BLK;
     MSum carry = bsum[blockIdx.x];
@@ -467,52 +483,101 @@ k_mhint(const MEnt* __restrict__ e, const MCopy* __restrict__ cp, const cly_tupl
         const uint64_t ho = H0 + ex.bytes;
         carry.bytes += total.bytes;
         const bool staged = total.bytes <= MH_BUF;              // (uniform)
-        if (j < nl && ho + hs <= hint_cap) {
+        const uint32_t ph = (uint32_t)((uintptr_t)(hint + H0) & 15u);   // the stage's 16-B phase
+        const uint32_t o = ph + (uint32_t)(ho - H0);            // the record's stage offset
+        const bool mine = j < nl && ho + hs <= hint_cap;
+        uint32_t s = 0xFFFFFFFFu;
+        if (mine) {
             const MEnt m = e[j];
             const cly_tuple t = tup[m.tuple];
             // the copy descriptor already points into the record (verbatim: its
             // start; re-encoded: its realKey): no file lookup
             const MCopy c = cp[j];
-            const uint8_t* rkey = c.pre ? (const uint8_t*)c.src
-                                        : (const uint8_t*)c.src + t.header_size + t.txid_len;
+            const uint8_t* rkey = c.pre ? (const uint8_t*)c.src : (const uint8_t*)c.src + t.header_size + t.txid_len;
             const uint32_t rk = t.key_size - t.txid_len;
-            const uint64_t dst = c.dst;
-            const uint64_t fid = dst / stride, off = dst - fid * stride;
-            uint8_t pv[20];
-            int pl = put_uv(pv, zz((int64_t)fid));
-            pl += put_uv(pv + pl, zz((int64_t)off));
-            uint8_t h[26];
-            h[4] = 0; h[5] = 0;
-            int n = 6;
-            n += put_uv(h + n, zz((int64_t)rk));
-            n += put_uv(h + n, zz((int64_t)pl));
-            h[n++] = 0;                                         // PutVarint(0) expiration
-            uint32_t s = 0xFFFFFFFFu;
-            for (int q = 4; q < n; q++) s = crc_upd(tab, s, h[q]);
-            uint8_t* o = staged ? buf + (ho - H0) : hint + ho;
-            for (uint32_t q = 0; q < rk; q++) { const uint8_t c = rkey[q]; s = crc_upd(tab, s, c); o[n + q] = c; }
-            for (int q = 0; q < pl; q++) { s = crc_upd(tab, s, pv[q]); o[n + rk + q] = pv[q]; }
+            const uint64_t fid = c.dst / stride, off = c.dst - fid * stride;
+            int nf, nofs, nk;
+            const uint64_t pf = uv_pack(zz((int64_t)fid), nf), po = uv_pack(zz((int64_t)off), nofs);
+            const int pl = nf + nofs;                            // <= 10
+            const uint64_t pvl = nf < 8 ? pf | (po << (8 * nf)) : pf;
+            const uint64_t pvh = nf < 8 ? (nf ? po >> (64 - 8 * nf) : 0) : po;   // (nf >= 1)
+            const uint64_t kv = uv_pack(zz((int64_t)rk), nk);    // nk <= 5
+            // header bytes 0..n-1 (crc bytes 0..3 later): 0 0 varint(rk) 2pl 0
+            const int n = 8 + nk;
+            uint64_t hl = kv << 48, hh = kv >> 16;
+            const uint64_t tailb = (uint64_t)(2 * pl);           // varint(zz(pl)): one byte
+            if (6 + nk < 8) hl |= tailb << (8 * (6 + nk)); else hh |= tailb << (8 * (6 + nk - 8));
+            auto put = [&](uint32_t q, uint32_t bv) {
+                if (staged) buf[o + q] = (uint8_t)bv;
+                else { hint[ho + q] = (uint8_t)bv; s = crc_upd(t4, s, bv); }
+            };
+            #pragma unroll
+            for (int q = 4; q < 14; q++)
+                if (q < n) put((uint32_t)q, byte_of(hl, hh, q));
+            // realKey: aligned dwords holding its bytes, shifted into place
+            const uintptr_t ka = (uintptr_t)rkey;
+            const CLY_GLB uint32_t* kw = (const CLY_GLB uint32_t*)(ka & ~(uintptr_t)3);
+            const uint32_t kb = (uint32_t)(ka & 3);
+            uint32_t prev = rk ? kw[0] : 0u;
+            for (uint32_t q = 0, k = 0; q < rk; q += 4, k++) {
+                const uint32_t nxt = 4 * (k + 1) < kb + rk ? kw[k + 1] : 0u;
+                const uint32_t x = __builtin_amdgcn_alignbit(nxt, prev, 8 * kb);
+                #pragma unroll
+                for (int i = 0; i < 4; i++)
+                    if (q + i < rk) put((uint32_t)n + q + i, (x >> (8 * i)) & 0xffu);
+                prev = nxt;
+            }
+            #pragma unroll
+            for (int q = 0; q < 10; q++)
+                if (q < pl) put((uint32_t)n + rk + q, byte_of(pvl, pvh, q));
+        }
+        if (staged) {
+            __syncthreads();
+            if (mine) {
+                // CRC of bytes 4 .. hs-1 from the stage: aligned dword reads, shifted
+                const uint32_t bb = o + 4, sh8 = 8 * (bb & 3);
+                const uint32_t* w = (const uint32_t*)(buf + (bb & ~3u));
+                const uint32_t nb = hs - 4, nw = nb >> 2;
+                uint32_t w0 = w[0];
+                uint32_t k = 0;
+                for (; k < nw; k++) {
+                    const uint32_t w1 = w[k + 1];
+                    const uint32_t x = s ^ __builtin_amdgcn_alignbit(w1, w0, sh8);
+                    s = t4[768 + (x & 0xff)] ^ t4[512 + ((x >> 8) & 0xff)] ^ t4[256 + ((x >> 16) & 0xff)] ^ t4[x >> 24];
+                    w0 = w1;
+                }
+                const uint32_t x = __builtin_amdgcn_alignbit(w[k + 1], w0, sh8);
+                #pragma unroll
+                for (int i = 0; i < 3; i++)
+                    if ((uint32_t)i < (nb & 3u)) s = crc_upd(t4, s, (x >> (8 * i)) & 0xffu);
+            }
+        }
+        if (mine) {
             s = ~s;
-            h[0] = (uint8_t)s; h[1] = (uint8_t)(s >> 8); h[2] = (uint8_t)(s >> 16); h[3] = (uint8_t)(s >> 24);
-            for (int q = 0; q < n; q++) o[q] = h[q];
+            #pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (staged) buf[o + q] = (uint8_t)(s >> (8 * q));
+                else hint[ho + q] = (uint8_t)(s >> (8 * q));
+            }
         }
         if (staged) {
             __syncthreads();
             uint64_t H1 = H0 + total.bytes;
             if (H1 > hint_cap) H1 = hint_cap;
             if (H1 > H0) {
-                // bytes [H0, H1): head bytes up to the first aligned dword, whole dwords, tail bytes
-                const uint64_t A0 = ((uint64_t)(uintptr_t)(hint + H0) + 3) & ~3ull;
-                const uint64_t a0 = A0 - (uint64_t)(uintptr_t)hint;          // first aligned offset
-                const uint64_t a1 = H0 + ((H1 - H0) > (a0 - H0) ? ((H1 - a0) & ~3ull) + (a0 - H0) : 0);
-                for (uint64_t x = H0 + threadIdx.x; x < H1 && x < a0; x += M_NT) hint[x] = buf[x - H0];
-                for (uint64_t x = a0 + 4 * (uint64_t)threadIdx.x; x + 4 <= a1; x += 4 * M_NT) {
-                    const uint64_t r = x - H0;
-                    const uint32_t wv = (uint32_t)buf[r] | ((uint32_t)buf[r + 1] << 8) | ((uint32_t)buf[r + 2] << 16) |
-                                        ((uint32_t)buf[r + 3] << 24);
-                    *(uint32_t*)(hint + x) = wv;
+                // 16-B chunks of [H0 - ph, H1): whole ones with one store, the two
+                // partial ones byte by byte
+                const uint64_t C0 = H0 - ph, nch = (H1 - C0 + 15) >> 4;
+                for (uint64_t ci = threadIdx.x; ci < nch; ci += M_NT) {
+                    const uint64_t c = C0 + 16 * ci;
+                    const uint32_t lo = (uint32_t)(16 * ci);
+                    if (c >= H0 && c + 16 <= H1) {
+                        *(uint4*)(hint + c) = *(const uint4*)(buf + lo);
+                    } else {
+                        for (int q = 0; q < 16; q++)
+                            if (c + q >= H0 && c + q < H1) hint[c + q] = buf[lo + q];
+                    }
                 }
-                for (uint64_t x = (a1 > a0 ? a1 : a0) + threadIdx.x; x < H1; x += M_NT) hint[x] = buf[x - H0];
             }
             __syncthreads();
         }
@@ -529,7 +594,6 @@ k_mhint(const MEnt* __restrict__ e, const MCopy* __restrict__ cp, const cly_tupl
 // gathers its 16 bytes with independent byte loads.
 __device__ const uint8_t g_zero_byte = 0;
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));   // 16 B, dword-aligned
-#define CLY_GLB __attribute__((address_space(1)))                            // global (not flat) loads
 #define MC_W 4                                   // waves per workgroup
 #define MC_P (M_CB / 16 / 64)                    // pieces per lane
 __device__ __forceinline__ void mc_wave_sync() {

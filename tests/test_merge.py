@@ -207,6 +207,22 @@ def test_gpu_merge_big_records_and_empty(scanner):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kmax", [3, 60, 400])
+def test_gpu_merge_hint_key_lengths(scanner, kmax):
+    """Hint records of realKeys from 0 bytes up to kmax (k_mhint: the LDS stage
+    of a workgroup's records, and the direct path when they exceed it), with
+    txId prefixes of 1-3 bytes (re-encoded records) and without."""
+    rng = random.Random(kmax)
+    recs = []
+    for i in range(3000):
+        key = rng.randbytes(rng.randrange(0, kmax + 1))
+        recs.append(mg.encode_record(mg.key_tx(key, rng.choice([0, 0, 5, 300, 70000])), rng.randbytes(rng.randrange(0, 40))))
+    b = b"".join(recs)
+    live = (np.random.default_rng(kmax).random(3000) < 0.8).astype(np.uint8)
+    gpu_vs_oracle(scanner, split_files(b, 2, rng), live, 1 << 16)
+
+
+@pytest.mark.gpu
 def test_gpu_merge_device_c4_shape():
     """BASELINE config 4's shape (puts, k%4==0 overwritten, k%4==2 deleted: 50 %
     of the records dead) at 600 MiB with the reference's 256 MiB data files,
