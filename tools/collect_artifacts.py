@@ -33,5 +33,5 @@ for i, (counter, scale) in enumerate((("FETCH_SIZE", 2.0), ("WRITE_SIZE", 1.0)),
 traffic["note"] = ("per-launch averages; fetch_bytes = FETCH_SIZE x 1024 x 2 (gfx950 half-count correction), "
                    "write_bytes = WRITE_SIZE x 1024")
 json.dump(traffic, open(os.path.join(prof, "%s_traffic.json" % tag), "w"), indent=1)
-ks = traffic["kernels"].get("k_crc", {})
-print("bench", bench["value"], bench["unit"], "k_crc", bench["kernel"]["k_crc_ms"], "ms; traffic", ks)
+ks = traffic["kernels"].get("k_scan", {})
+print("bench", bench["value"], bench["unit"], "k_scan", bench["kernel"].get("k_scan_ms"), "ms; traffic", ks)
