@@ -55,6 +55,12 @@ typedef unsigned long long u64;
 #define CLY_GL __attribute__((address_space(1)))   // global memory (loads/stores as global_*, not flat_*)
 typedef const CLY_GL uint8_t* gbytes;
 typedef CLY_GL cly_tuple* gtuples;
+// Buffer resources (SGPRs) for the block loads and the compact-entry stores:
+// 32-bit offsets only, no 64-bit addresses held in VGPRs across a block
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t mk_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
 #define NONE32 0xFFFFFFFFu       // no position
 #define TERM_NONE 127            // the chain leaves the segment (no terminal inside)
 #define LM_NONE 0                // no record starts in the segment (the chain passes through it)
@@ -214,17 +220,20 @@ __device__ __forceinline__ uint32_t shift_bytes(const CLY_LDS uint32_t* sh, uint
 }
 
 // ---------------------------------------------------------------------------
-// Header decode at file position p.  Fast path: 32 bytes gathered from
-// [p & ~3, +32) by two 16-B loads, varints of at most 4 bytes ending within
+// Header decode at file position p.  Fast path: 20 bytes gathered from
+// [p & ~3, +20) (a 16-B and a 4-B load), varints of at most 4 bytes ending within
 // header bytes 6..13 (every record the writer produces except long
 // expirations); otherwise the exact byte-loop form over global memory.
 struct Gath { uint32_t w[8]; };
 __device__ __forceinline__ bool gath_ok(uint32_t p, uint64_t len) { return (uint64_t)(p & ~3u) + 32 <= len; }
+// (only the 5 dwords hdr_fast reads: a loaded register left unread would keep
+// a pending load on it, and the register's next writer would wait for it)
 __device__ __forceinline__ void gath_issue(gbytes base, uint32_t p, Gath& g) {
     const CLY_GL u32x4u* q = (const CLY_GL u32x4u*)(base + (p & ~3u));
-    const u32x4u a = q[0], b = q[1];
+    const u32x4u a = q[0];
     g.w[0] = a.x; g.w[1] = a.y; g.w[2] = a.z; g.w[3] = a.w;
-    g.w[4] = b.x; g.w[5] = b.y; g.w[6] = b.z; g.w[7] = b.w;
+    g.w[4] = ((const CLY_GL uint32_t*)q)[4];
+    g.w[5] = g.w[6] = g.w[7] = 0u;
 }
 __device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t s) {
     return __builtin_amdgcn_alignbyte(hi, lo, s);
@@ -273,24 +282,46 @@ __device__ __forceinline__ bool hdr_fast(const Gath& g, uint32_t p, uint64_t len
     h.good = h.type <= 4 && h.dt <= 4 && v1 >= 1 && v2 >= 0;
     return true;
 }
-// The header at p: the 32-B gather from the wave's LDS copy of the block (and
-// the 64 bytes after it) when p lies there, else from global memory (L2);
-// the byte-loop form near the file's end.
-#define STG_BYTES (CLY_BLK + 64)                 // per-wave block stage: the block + 64 B after it
-__device__ __forceinline__ Hdr hdr_get(gbytes base, uint32_t p, uint64_t len, const CLY_LDS uint32_t* stg, uint32_t bs) {
+// The wave's block stage in LDS: the block and the 32 bytes after it, each
+// 64-B segment at an 80-B stride whose last 16 B repeat the
+// next segment's first 16 B.  The stride spreads the lanes' 16-B stores and
+// loads of their own segments over all banks (ds_write_b128: 8 lanes of 4
+// dwords at 20 L mod 32; ds_read_b128: 16 lanes at 20 L mod 64), and the copy
+// makes any 5 consecutive dwords of the logical stream 5 consecutive dwords of
+// the stage.  Logical dword d (of the block) is stage dword d + 4 (d >> 4).
+#define STG_STRIDE 80
+#define STG_BYTES (CLY_NL * STG_STRIDE + 32)     // + the 32 B after the block (segment 64's first two chunks)
+#define STG_SPAN (CLY_BLK + 32)                  // logical bytes the stage holds
+__device__ __forceinline__ uint32_t stg_dw(uint32_t d) { return d + ((d >> 4) << 2); }
+// byte view of the stage for step_hdr / go_varint (logical offsets)
+struct StgBytes {
+    const CLY_LDS uint8_t* s;
+    uint32_t o;
+    __device__ __forceinline__ uint32_t operator[](int64_t i) const {
+        const uint32_t a = o + (uint32_t)i;
+        return s[a + ((a >> 6) << 4)];
+    }
+    __device__ __forceinline__ StgBytes operator+(int64_t n) const { return StgBytes{s, o + (uint32_t)n}; }
+};
+// The header at p (bs <= p, p - bs + 26 <= STG_SPAN: every position the block
+// body decodes) from the stage only: no global load inside the block body, so
+// the next block's loads stay in flight (a vmcnt wait for a gather would wait
+// for them too).  Fast form from 5 dwords; the byte-loop form otherwise.
+__device__ __forceinline__ Hdr hdr_get(uint32_t p, uint64_t len, const CLY_LDS uint32_t* stg, uint32_t bs) {
     Hdr h;
-    if (gath_ok(p, len)) {
+    const uint32_t rel = p - bs;
+    {
         Gath g;
-        const uint32_t rel = (p & ~3u) - bs;
-        if (p >= bs && rel + 32 <= STG_BYTES) {
-            const CLY_LDS uint32_t* q = stg + (rel >> 2);
-            #pragma unroll
-            for (int k = 0; k < 8; k++) g.w[k] = q[k];
-        } else gath_issue(base, p, g);
+        const CLY_LDS uint32_t* q = stg + stg_dw(rel >> 2);
+        #pragma unroll
+        for (int k = 0; k < 5; k++) g.w[k] = q[k];
         if (hdr_fast(g, p, len, h)) return h;
     }
-    return step_hdr(base, (int64_t)p, (int64_t)len, (int64_t)p);
+    return step_hdr(StgBytes{(const CLY_LDS uint8_t*)stg, 0u}, (int64_t)rel, (int64_t)(len - bs), (int64_t)p);
 }
+__device__ __forceinline__ bool in_stage(uint32_t p, uint32_t bs) { return p >= bs && p - bs + 26 <= STG_SPAN; }
+// The header at p from global memory (k_emit's long entries; guess-mode exit
+// checks beyond the stage)
 __device__ __forceinline__ Hdr hdr_load(gbytes base, uint32_t p, uint64_t len) {
     Hdr h;
     if (gath_ok(p, len)) {
@@ -348,7 +379,7 @@ __device__ __forceinline__ bool seg_walk(const Seg& K, uint32_t p, bool exact, S
     L.E = p;
     for (int it = 0; it < 16; it++) {            // records are >= 6 bytes: <= 12 steps per segment
         if (!in_seg(K, p)) { L.x = p; return true; }
-        const Hdr h = hdr_get(K.base, p, K.len, K.stg, K.bs);
+        const Hdr h = hdr_get(p, K.len, K.stg, K.bs);
         if (h.status != REC_OK) {
             L.x = p; L.term = h.status;
             return exact || (h.status == CLY_END_EOF && (uint64_t)p == K.len);
@@ -499,13 +530,13 @@ __device__ __forceinline__ void put_tuple(gtuples out, uint64_t idx, uint64_t ou
 // key0 << 19 (the txId varint's single byte).  Long form: w3 = rel only
 // (k_emit decodes the header again).
 #define REC_SHORT (1u << 26)
-__device__ __forceinline__ void rec_store(uint32_t* dst, const Hdr& h, uint32_t rel) {
+__device__ __forceinline__ void rec_store(rsrc_t trs, uint32_t idx, const Hdr& h, uint32_t rel) {
     const bool sh = h.exp == 0 && h.key0 < 0x80u && h.ks >= 1u && h.ks < (1u << 24) && h.type < 8u && h.dt < 8u &&
                     h.hsz >= 6 && h.hsz < 38;
     u32x4 v = (u32x4){0u, 0u, 0u, rel};
     if (sh) v = (u32x4){h.crc, h.ks | ((uint32_t)(h.hsz - 6) << 24) | (h.type << 29), h.vs,
                         rel | (h.dt << 16) | (h.key0 << 19) | REC_SHORT};
-    *(CLY_GL u32x4*)dst = v;
+    __builtin_amdgcn_raw_buffer_store_b128(v, trs, (int)(idx * 16u), 0, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -530,20 +561,20 @@ __device__ __forceinline__ u32x4 load16z(gbytes base, uint64_t a, uint64_t len) 
     }
     return v;
 }
-// The block's loads, and the 64 bytes after it (16 B by each of lanes 0..3:
+// The block's loads, and the 32 bytes after it (16 B by each of lanes 0, 1:
 // the tail of the wave's stage, for headers that start near the block's end).
-__device__ __forceinline__ void blk_issue(gbytes base, uint64_t flen, uint32_t bs, int lane, u32x4 (&e)[4], u32x4& hl) {
-    const uint32_t lo = 64u * (uint32_t)(lane & 15) + 16u * (uint32_t)(lane >> 4);
+__device__ __forceinline__ void blk_issue(gbytes base, rsrc_t frs, uint64_t flen, uint32_t bs, int lane, u32x4 (&e)[4],
+                                          u32x4& hl) {
+    const uint32_t off = bs + 64u * (uint32_t)(lane & 15) + 16u * (uint32_t)(lane >> 4);
     if ((uint64_t)bs + CLY_BLK <= flen) {
-        const CLY_GL u32x4* src = (const CLY_GL u32x4*)(base + bs + lo);
         #pragma unroll
-        for (int k = 0; k < 4; k++) e[k] = src[64 * k];
+        for (int k = 0; k < 4; k++) e[k] = __builtin_amdgcn_raw_buffer_load_b128(frs, (int)(off + 1024u * k), 0, 0);
     } else {
         #pragma unroll
-        for (int k = 0; k < 4; k++) e[k] = load16z(base, (uint64_t)bs + 1024 * k + lo, flen);
+        for (int k = 0; k < 4; k++) e[k] = load16z(base, (uint64_t)(off + 1024u * k), flen);
     }
     hl = (u32x4){0u, 0u, 0u, 0u};
-    if (lane < 4) hl = load16z(base, (uint64_t)bs + CLY_BLK + 16 * lane, flen);
+    if (lane < 2) hl = load16z(base, (uint64_t)bs + CLY_BLK + 16 * lane, flen);
 }
 __device__ __forceinline__ void swap32(uint32_t& a, uint32_t& b) {
     const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
@@ -593,7 +624,8 @@ __device__ __forceinline__ void patch_word(uint32_t (&w)[16], uint32_t k, uint32
 #define BM_EXACT 1
 #define BM_EMIT 2
 #ifndef CLY_EXP
-#define CLY_EXP 0                // timing experiments only (wrong results): 1 no record work, 3 candidate
+#define CLY_EXP 0                // timing experiments only (wrong results): 1 no record work, 6 no CRC
+                                 // table steps, 7 neither, 3 candidate
 #endif                           // masks only, 2 no per-record outputs, 5 no agreement pass
 #ifndef CLY_PROF
 #define CLY_PROF 0               // experiment builds: per-section cycle counts of k_scan's tile body
@@ -631,10 +663,10 @@ struct TState {
 template <int BM>
 __device__ __forceinline__ uint32_t rec_out(const DevFile& F, gbytes base, uint32_t p, const Hdr& h, uint32_t idx,
                                             uint32_t tb, uint32_t bs, uint32_t dq, const CLY_LDS uint8_t* smem,
-                                            const CrcLane& cl, uint32_t K4, uint32_t* trec, gtuples out,
+                                            const CrcLane& cl, uint32_t K4, rsrc_t trs, gtuples out,
                                             uint64_t out_cap, uint64_t gbase, Globals* g, uint32_t& pw) {
     if (BM == BM_EMIT) { put_tuple(out, gbase + idx, out_cap, base, p, h, F.fid, g); pw = 0; return 0u; }
-    if (idx < CAP_T) rec_store(trec + 4 * idx, h, p - tb);
+    if (idx < CAP_T) rec_store(trs, idx, h, p - tb);
     const uint32_t d = h.crc ^ K4 ^ dq, j = p & 3u;
     pw = ((p - bs) >> 2) + (j ? 1u : 0u);
     return j ? crc_fwd(smem, d, 4u - j, cl.r4) : d;
@@ -663,7 +695,7 @@ __device__ __forceinline__ void term_patch(TState& S, uint32_t T, uint32_t dT, u
 // budget runs out with X still in the block (the caller's general pass goes on).
 template <int BM>
 __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t tb, uint32_t bs, CLY_LDS uint32_t* stg,
-                                          const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t K4, uint32_t* trec,
+                                          const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t K4, rsrc_t trs,
                                           gtuples out, uint64_t out_cap, uint64_t gbase, Globals* g, int lane) {
     const gbytes base = (gbytes)F.base;
     const uint64_t flen = F.len, bend = (uint64_t)bs + CLY_BLK;
@@ -673,7 +705,7 @@ __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t 
         if (S.dead || !owned) return true;
         uint32_t a = S.s_last, b = S.s_prev ? S.s_prev : S.s_last;
         if (!a) {                                  // no size yet: the record at X sets the stride
-            const Hdr h0 = hdr_get(base, (uint32_t)X, flen, stg, bs);
+            const Hdr h0 = hdr_get((uint32_t)X, flen, stg, bs);
             a = b = h0.status == REC_OK ? (uint32_t)h0.size : 64u;
         }
         const uint32_t k = (uint32_t)lane;
@@ -681,7 +713,7 @@ __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t 
         const bool act = P < bend || (P == flen && flen == bend);
         Hdr h;
         h.status = CLY_END_EOF; h.size = 0; h.crc = 0;
-        if (act) h = hdr_get(base, (uint32_t)P, flen, stg, bs);
+        if (act) h = hdr_get((uint32_t)P, flen, stg, bs);
         const uint32_t expect = (k & 1) ? a : b;
         const bool rec = act && h.status == REC_OK;
         const u64 brk = __ballot(!(rec && (uint64_t)h.size == expect));
@@ -695,9 +727,9 @@ __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t 
         // every lane of the round has read its header: the patches may go in
         uint32_t pw = 0, pv = 0;
         if (acc) {
-            pv = rec_out<BM>(F, base, (uint32_t)P, h, S.tcnt + k, tb, bs, P == 0 ? 0u : dq, smem, cl, K4, trec, out,
+            pv = rec_out<BM>(F, base, (uint32_t)P, h, S.tcnt + k, tb, bs, P == 0 ? 0u : dq, smem, cl, K4, trs, out,
                              out_cap, gbase, g, pw);
-            if (BM != BM_EMIT && pw < PW_CARRY) stg[pw] ^= pv;
+            if (BM != BM_EMIT && pw < PW_CARRY) stg[stg_dw(pw)] ^= pv;
         }
         if (BM != BM_EMIT) {
             const u64 bc = __ballot(acc && pw == PW_CARRY);
@@ -737,16 +769,20 @@ __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t 
 // plausible header beyond it).  The tile's guessed entry G is the first such
 // start whose exit was confirmed inside the block, else the first such start;
 // NONE32 when the block holds none.  k_link checks the guess.
+// a header a chain may continue at: a record the writer produces, a zero
+// header, or the end of the file
+__device__ __forceinline__ bool hdr_plausible(const Hdr& h, uint32_t x, uint64_t flen) {
+    return (h.status == REC_OK && h.good) || h.status == CLY_END_ZERO || (h.status == CLY_END_EOF && (uint64_t)x == flen);
+}
 __device__ __forceinline__ uint32_t guess_entry(const DevFile& F, uint32_t bs, CLY_LDS uint32_t* stg, const u32x4& hc,
                                                 int lane) {
     const CLY_LDS u32x4* sv = (const CLY_LDS u32x4*)stg;
-    const gbytes base = (gbytes)F.base;
     const uint64_t flen = F.len;
     const Seg K = make_seg(F, bs, lane, stg);
     uint32_t wv[16];
     #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const u32x4 v = sv[4 * lane + k];
+        const u32x4 v = sv[5 * lane + k];
         wv[4 * k] = v.x; wv[4 * k + 1] = v.y; wv[4 * k + 2] = v.z; wv[4 * k + 3] = v.w;
     }
     const uint32_t n0 = dppu<DPP_WF_SL1>(rdl(hc.x, 0), wv[0]), n1 = dppu<DPP_WF_SL1>(rdl(hc.y, 0), wv[1]);
@@ -780,11 +816,30 @@ __device__ __forceinline__ uint32_t guess_entry(const DevFile& F, uint32_t bs, C
             if (chk_in) {
                 const uint32_t bb = off & 63u;
                 ok = (((bb < 32 ? clo >> bb : chi >> (bb - 32))) & 1u) != 0;
+                if (ok) {
+                    // two more hops from the stage: the exit's header, and the
+                    // header after that record when it is in the stage too (a
+                    // false start rarely passes three headers)
+                    const Hdr h1 = hdr_get(T.x, flen, stg, bs);
+                    ok = hdr_plausible(h1, T.x, flen);
+                    if (ok && h1.status == REC_OK) {
+                        const uint64_t x2 = (uint64_t)T.x + (uint64_t)h1.size;
+                        if (x2 < 0xFFFFFFFFull && in_stage((uint32_t)x2, bs))
+                            ok = hdr_plausible(hdr_get((uint32_t)x2, flen, stg, bs), (uint32_t)x2, flen);
+                    }
+                }
                 in = ok;
             } else {
-                const Hdr eh = hdr_get(base, T.x, flen, stg, bs);
-                ok = (eh.status == REC_OK && eh.good) || eh.status == CLY_END_ZERO ||
-                     (eh.status == CLY_END_EOF && (uint64_t)T.x == flen);
+                // the exit's header from the stage, or (beyond it) from global
+                // memory: the one global read of the block body, in guess blocks
+                // only (its wait also waits for the next block's loads)
+                Hdr eh;
+                if (in_stage(T.x, bs)) eh = hdr_get(T.x, flen, stg, bs);
+                else {
+                    eh = hdr_load((gbytes)F.base, T.x, flen);
+                    __builtin_amdgcn_s_waitcnt(0);          // every load of this path done here, not at a join
+                }
+                ok = hdr_plausible(eh, T.x, flen);
             }
         }
         if (act && ok) { E = T.E; conf_in = in; settled = true; }
@@ -813,13 +868,14 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     S.s_last = 0; S.s_prev = 0; S.Tb = NONE32; S.tpatch = 0; S.carry_next = 0;
     uint32_t R = 0, carry = 0;   // carry: register XOR due at this block's first byte
     const CLY_LDS uint32_t* nibt = (const CLY_LDS uint32_t*)(smem + LDS_NIB);
-    uint32_t* trec = rec + (uint64_t)t * CAP_T * 4;
+    const rsrc_t trs = mk_rsrc(rec + (uint64_t)t * CAP_T * 4, CAP_T * 16u);      // the tile's compact entries
+    const rsrc_t frs = mk_rsrc(F.base, (uint32_t)flen);
     CLY_LDS u32x4* sv = (CLY_LDS u32x4*)stg;
     u32x4 e[4], hl;
 #if CLY_PROF
     uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = __builtin_amdgcn_s_memtime();
 #endif
-    blk_issue(base, flen, tb, lane, e, hl);
+    blk_issue(base, frs, flen, tb, lane, e, hl);
     #pragma unroll 1
     for (int m = 0; m < CLY_NBLK; m++) {
         const uint32_t bs = tb + (uint32_t)m * CLY_BLK;
@@ -830,25 +886,36 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
         for (int k = 0; k < 4; k++) { w[4 * k] = e[k].x; w[4 * k + 1] = e[k].y; w[4 * k + 2] = e[k].z; w[4 * k + 3] = e[k].w; }
         PT(0);
         const u32x4 hc = hl;
-        if (m + 1 < CLY_NBLK && (BM != BM_EMIT || !S.dead)) blk_issue(base, flen, bs + CLY_BLK, lane, e, hl);
+        if (m + 1 < CLY_NBLK && (BM != BM_EMIT || !S.dead)) blk_issue(base, frs, flen, bs + CLY_BLK, lane, e, hl);
         if (BM == BM_EMIT && S.dead) break;
         S.Tb = NONE32;
         const bool owned = S.X != NONE32 && ((uint64_t)S.X < bend || ((uint64_t)S.X == flen && flen == bend));
         if (S.dead) {
             #pragma unroll
             for (int k = 0; k < 16; k++) w[k] = 0;
-        } else if (CLY_EXP != 1 && (S.X == NONE32 || owned)) {
+        } else if (CLY_EXP != 1 && CLY_EXP != 7 && (S.X == NONE32 || owned)) {
             // ---- record starts of the block; headers are read from the wave's
             // LDS copy of it (the stage), patches XORed into the stage
-            #pragma unroll
-            for (int k = 0; k < 4; k++) sv[4 * lane + k] = (u32x4){w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
-            if (lane < 4) sv[CLY_BLK / 16 + lane] = hc;
+            {
+                // segment L, then its copy of the next segment's first 16 B (lane 63:
+                // the 32 B after the block, held by lanes 0 and 1, copied and stored)
+                const uint32_t t0x = rdl(hc.x, 0), t0y = rdl(hc.y, 0), t0z = rdl(hc.z, 0), t0w = rdl(hc.w, 0);
+                #pragma unroll
+                for (int k = 0; k < 4; k++) sv[5 * lane + k] = (u32x4){w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
+                const u32x4 nx = (u32x4){dppu<DPP_WF_SL1>(t0x, w[0]), dppu<DPP_WF_SL1>(t0y, w[1]),
+                                         dppu<DPP_WF_SL1>(t0z, w[2]), dppu<DPP_WF_SL1>(t0w, w[3])};
+                sv[5 * lane + 4] = nx;
+                if (lane == CLY_NL - 1) {
+                    sv[5 * lane + 5] = nx;
+                    sv[5 * lane + 6] = (u32x4){rdl(hc.x, 1), rdl(hc.y, 1), rdl(hc.z, 1), rdl(hc.w, 1)};
+                }
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             if (S.X == NONE32) { S.X = guess_entry(F, bs, stg, hc, lane); PC(6); }    // the tile's guessed entry
             PT(1);
             bool done = true;
-            if (S.X != NONE32) done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, trec, out, out_cap, gbase, g, lane);
+            if (S.X != NONE32) done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, trs, out, out_cap, gbase, g, lane);
             PT(2);
             if (!done) {
                 PC(7);
@@ -859,7 +926,7 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                 uint32_t wv[16];
                 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    const u32x4 v = sv[4 * lane + k];
+                    const u32x4 v = sv[5 * lane + k];
                     wv[4 * k] = v.x; wv[4 * k + 1] = v.y; wv[4 * k + 2] = v.z; wv[4 * k + 3] = v.w;
                 }
                 const uint32_t n0 = dppu<DPP_WF_SL1>(rdl(hc.x, 0), wv[0]), n1 = dppu<DPP_WF_SL1>(rdl(hc.y, 0), wv[1]);
@@ -901,21 +968,21 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                     uint32_t p = L.E, psz = 0, ppsz = 0, p0w = PW_CARRY + 1, p0v = 0, cv = 0;
                     for (uint32_t i = 0; CLY_EXP != 2 && __ballot(i < c); i++) {
                         if (i < c) {
-                            const Hdr h = hdr_get(base, p, flen, stg, bs);
+                            const Hdr h = hdr_get(p, flen, stg, bs);
                             uint32_t pw;
                             const uint32_t pv = rec_out<BM>(F, base, p, h, S.tcnt + lex + i, tb, bs,
-                                                            p == 0 ? 0u : (pk ? ~pcq : 0xFFFFFFFFu), smem, cl, K4, trec,
+                                                            p == 0 ? 0u : (pk ? ~pcq : 0xFFFFFFFFu), smem, cl, K4, trs,
                                                             out, out_cap, gbase, g, pw);
                             if (pw == PW_CARRY) cv = pv;
                             else if (i == 0) { p0w = pw; p0v = pv; }
-                            else if (BM != BM_EMIT) stg[pw] ^= pv;
+                            else if (BM != BM_EMIT) stg[stg_dw(pw)] ^= pv;
                             pcq = h.crc; pk = true;
                             ppsz = psz; psz = (uint32_t)h.size;
                             p += (uint32_t)h.size;
                         }
                     }
                     if (BM != BM_EMIT) {
-                        if (p0w < PW_CARRY) stg[p0w] ^= p0v;
+                        if (p0w < PW_CARRY) stg[stg_dw(p0w)] ^= p0v;
                         const u64 bc = __ballot(cv != 0);
                         if (bc) S.carry_next ^= rdl(cv, __ffsll((long long)bc) - 1);
                     }
@@ -951,7 +1018,7 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
             if (BM != BM_EMIT) {
                 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    const u32x4 v = sv[4 * lane + k];
+                    const u32x4 v = sv[5 * lane + k];
                     w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
                 }
             }
@@ -976,7 +1043,7 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
             S.carry_next = 0;
             if (m) R = mat_mul(nibt + 6 * 128, R);
             #pragma unroll
-            for (int k = 0; k < 16; k++) R = crc_word(smem, R ^ w[k], cl);
+            for (int k = 0; k < 16; k++) R = (CLY_EXP == 6 || CLY_EXP == 7) ? R ^ w[k] : crc_word(smem, R ^ w[k], cl);
         }
         PT(4);
     }
@@ -1027,6 +1094,7 @@ __device__ __forceinline__ int find_file(const uint32_t* __restrict__ tprefix, i
     }
     return lo;
 }
+#define CLY_K4 0x9226F562u        // A^-4 0xFFFFFFFF (k4_const)
 __device__ __forceinline__ uint32_t k4_const(const CLY_LDS uint8_t* smem, uint32_t r4) {
     uint32_t K4 = 0xFFFFFFFFu;              // A^-4 0xFFFFFFFF
     for (int k = 0; k < 4; k++) K4 = crc_unbyte(smem, K4, r4);
@@ -1245,6 +1313,29 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
     const int f = find_file(tprefix, nfiles, t);
     const DevFile F = files[f];
     LBState S = ti_load(&tin[t]);
+    {
+        // Suffix: the true entry is the start of the guessed chain's record j
+        // (a false start that runs into the true chain).  The chain from there
+        // on is the tile's own: drop the first j records (count, entry; k_emit
+        // skips their compact entries and corrects the register) instead of
+        // walking the tile again.
+        const u64 l0 = loc[t].l[0], l1 = loc[t].l[1];
+        const uint32_t n = (uint32_t)(l0 >> 32), tb = (t - F.first_tile) * (uint32_t)CLY_TILE;
+        if (!S.dead && !(l0 & (DF_NONE | DF_FOF | DF_OVF)) && n > 1 && ((loc[t].l[3] >> 40) & 0xFFFFu) == 0) {
+            const uint32_t nn = n < 64u ? n : 64u;
+            const uint32_t rel = (uint32_t)lane < nn ? (rec[((uint64_t)t * CAP_T + lane) * 4 + 3] & 0xFFFFu) : 0xFFFFFu;
+            const u64 bm = __ballot(lane >= 1 && tb + rel == S.X);
+            if (bm) {
+                const uint32_t j = (uint32_t)__ffsll((long long)bm) - 1;
+                if (lane == 0) {
+                    loc[t].l[0] = (l0 & 0xFFFFFFFFull) | ((u64)(n - j) << 32);
+                    loc[t].l[1] = (u64)S.X | (l1 & 0xFFFFFFFF00000000ull);
+                    loc[t].l[3] |= (u64)j << 40;
+                }
+                return;
+            }
+        }
+    }
     for (;;) {
         const TileRes r = tile_body<BM_EXACT>(F, t, t - F.first_tile, S.X, S.dead != 0, smem, stg, cl, K4, loc, rec,
                                               treg, nullptr, 0, 0, g);
@@ -1291,9 +1382,10 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         const u64 l0 = loc[t].l[0], l1 = loc[t].l[1], l3 = loc[t].l[3];
         const uint32_t tt = t - F.first_tile, tb = (uint32_t)((uint64_t)tt * CLY_TILE);
         const uint32_t n = (uint32_t)(l0 >> 32);
+        const uint32_t skip = (uint32_t)(l3 >> 40) & 0xFFFFu;              // k_refix's suffix (records dropped)
         const gbytes base = (gbytes)F.base;
         if (!(l0 & DF_OVF)) {
-            const uint32_t* trec = rec + (uint64_t)t * CAP_T * 4;
+            const uint32_t* trec = rec + ((uint64_t)t * CAP_T + skip) * 4;
             for (uint32_t i0 = 0; i0 < n; i0 += 64) {
                 const uint32_t i = i0 + lane;
                 if (i < n) {
@@ -1336,6 +1428,21 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         }
         if (lane == 0) {
             const uint32_t G = (uint32_t)l1;
+            if (skip) {
+                // the dropped records' patches out, and the new first record's
+                // predecessor term (its deferred ~cq is completed below)
+                const uint32_t* r0 = rec + (uint64_t)t * CAP_T * 4;
+                const uint32_t TE = tb + (uint32_t)CLY_TILE;
+                uint32_t corr = 0, q = 0xFFFFFFFFu, cp = 0;
+                for (uint32_t i = 0; i <= skip; i++) {
+                    const u32x4 v = *(const u32x4*)(r0 + 4 * i);
+                    const uint32_t Pi = tb + (v.w & 0xFFFFu);
+                    const uint32_t ci = (v.w & REC_SHORT) ? v.x : hdr_load(base, Pi, F.len).crc;
+                    corr ^= shift_bytes(sht, TE - Pi, i < skip ? (ci ^ CLY_K4 ^ q) : cp);
+                    q = ~ci; cp = ci;
+                }
+                treg[t] ^= corr;
+            }
             if (tt > 0 && !(l0 & DF_NONE)) treg[t] ^= shift_bytes(sht, tb + (uint32_t)CLY_TILE - G, S.crc_last);
             if (l0 & DF_TERM) {
                 fo->term_pos = (uint32_t)(l1 >> 32);
@@ -1405,7 +1512,10 @@ k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __rest
 // (atomicMin on offset << 32 | index in file).
 __global__ void __launch_bounds__(1024)
 k_locate(const DevFile* __restrict__ files, int nfiles, FileInfo* finfo, const cly_tuple* __restrict__ tup,
-         uint64_t total, uint64_t out_cap, const uint32_t* __restrict__ tabs) {
+         uint64_t out_cap, const uint32_t* __restrict__ tabs, const Globals* g, int slot) {
+    // (launched after every k_fin: returns at once unless a fold failed and the chain is final)
+    if (!g->any_fail || g->nfix[slot] || g->fail) return;
+    const uint64_t total = g->total;
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
     init_tables(smem, tabs + TAB_SCAN, 0);
@@ -1635,6 +1745,12 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
                            c->d_pw, c->d_g, slot);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[4], st));
+        hipLaunchKernelGGL(k_locate, dim3(c->loc_grid), dim3(1024), 0, st, c->d_files, nfiles, c->d_finfo, d_out,
+                           out_cap, c->d_tabs, c->d_g, slot);
+        HIPCK(hipGetLastError());
+        HIPCK(hipEventRecord(c->ev[7], st));
+        // one read-back and one wait for the whole call when no repair round is needed
+        HIPCK(hipMemcpyAsync(c->h_finfo, c->d_finfo, sizeof(FileInfo) * nfiles, hipMemcpyDeviceToHost, st));
         HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
         HIPCK(hipStreamSynchronize(st));
         return CLY_OK;
@@ -1681,17 +1797,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
             if (rc2) return rc2;
         }
     }
-    bool located = false;
-    if (c->h_g->any_fail && !c->h_g->fail) {
-        hipLaunchKernelGGL(k_locate, dim3(c->loc_grid), dim3(1024), 0, st, c->d_files, nfiles, c->d_finfo, d_out,
-                           c->h_g->total, out_cap, c->d_tabs);
-        HIPCK(hipGetLastError());
-        located = true;
-    }
-    HIPCK(hipEventRecord(c->ev[7], st));
-    HIPCK(hipMemcpyAsync(c->h_finfo, c->d_finfo, sizeof(FileInfo) * nfiles, hipMemcpyDeviceToHost, st));
-    HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
-    HIPCK(hipStreamSynchronize(st));
+    const bool located = c->h_g->any_fail && !c->h_g->fail;       // k_locate did its work
     float ms_scan = 0, ms_link = 0, ms_emit = 0, ms_fin = 0, ms_loc = 0;
     HIPCK(hipEventElapsedTime(&ms_scan, c->ev[0], c->ev[1]));
     HIPCK(hipEventElapsedTime(&ms_link, c->ev[1], c->ev[2]));

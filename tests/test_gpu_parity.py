@@ -156,6 +156,46 @@ def test_false_merge_fixtures(scanner, name):
         compare(r.file_tuples(0), r.status[0], r.end_offset[0], t, st, end, name)
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_false_starts_chaining_into_true_records(scanner, seed):
+    """Every value embeds a well-formed header whose record size ends exactly
+    where the next true record starts: a tile whose entry guess takes such a
+    false start runs into the true chain (k_refix's suffix shortcut drops the
+    false record, k_emit skips its compact entry and corrects the register)."""
+    import random
+
+    import make_golden as mg
+    rng = random.Random(seed)
+    b = bytearray()
+    i = 0
+    while len(b) < 600_000:
+        vlen = rng.choice([150, 276, 300, 777, 2000])
+        key = mg.key_tx(mg.test_key(i), 0)
+        hdr_len = len(mg.encode_record(key, b"")) - len(key)
+        o = rng.randrange(0, vlen - 40)
+        start_v = len(b) + hdr_len + len(key)
+        rec_end = start_v + vlen
+        fpos = start_v + o
+        ks = 10
+        body_len = rec_end - fpos
+        for hsz in range(9, 20):
+            vs = body_len - hsz - ks
+            fh = rng.randbytes(4) + bytes([rng.randrange(5), rng.randrange(5)]) + mg.put_varint(ks) + \
+                mg.put_varint(vs) + mg.put_varint(0)
+            if len(fh) == hsz:
+                break
+        v = bytearray(rng.randbytes(vlen))
+        v[o:o + len(fh)] = fh
+        b += mg.encode_record(key, bytes(v))
+        i += 1
+    data = np.frombuffer(bytes(b), np.uint8).copy()
+    f = DataFile(data, 4)
+    r = scanner.scan([f])
+    t, st, end = co.scan_file(data, 4)
+    assert st == 0 and len(t) == i
+    compare(r.file_tuples(0), r.status[0], r.end_offset[0], t, st, end, "false starts %d" % seed)
+
+
 def test_bitflips_everywhere_small(scanner):
     base = fixed_records_file(60, 200, seed=5)
     rng = np.random.default_rng(0)
