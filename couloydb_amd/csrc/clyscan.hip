@@ -1172,7 +1172,8 @@ __device__ __forceinline__ LBState rf_apply(const RunF& f, LBState s) {
 #define LINK_PER 4               // tiles per thread held in registers (more: re-read)
 __global__ void __launch_bounds__(LINK_NT)
 k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restrict__ loc, TileIn* tin,
-       uint64_t* ftotal, FileInfo* finfo, uint32_t* fixlist, Globals* g, int slot) {
+       uint64_t* ftotal, FileInfo* finfo, uint32_t* fixlist, Globals* g, int slot, int guard) {
+    if (guard >= 0 && g->nfix[guard] == 0) return;  // (device round: nothing was re-resolved)
     __shared__ RunF rf[2][LINK_NT];
     __shared__ uint32_t badm[LINK_MAXT / 32];
     __shared__ uint32_t bad_far;             // a contradicted tile beyond the bitmask (listed alone)
@@ -1291,6 +1292,7 @@ k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restric
     if (tid == 0) { g->total = carry; g->link_done = 0; }
 }
 
+#define REFIX_GRID 64             // workgroups of the device repair round (16 listed tiles each)
 // k_refix: one wave per listed tile: the tile body again from the entering
 // state k_link gave it (new LOCAL, compact entries, register).  Walks on into
 // the next tile of the file while that one's LOCAL disagrees with the new exit
@@ -1549,6 +1551,7 @@ struct cly_ctx {
     int device;
     hipStream_t stream;
     hipEvent_t ev[8];
+    uint8_t* d_call; uint8_t* h_call; size_t call_bytes;     // the per-call block (ensure_files)
     DevFile* d_files; uint32_t* d_tprefix; FileInfo* d_finfo; uint64_t* d_ftotal; int cap_files;
     DevFile* h_files; uint32_t* h_tprefix; FileInfo* h_finfo;
     TileLocal* d_loc; TileIn* d_tin; uint32_t* d_treg; uint32_t* d_fix; uint32_t* d_rec;
@@ -1578,8 +1581,6 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     c->device = device;
     HIPCK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (int i = 0; i < 8; i++) HIPCK(hipEventCreate(&c->ev[i]));
-    HIPCK(hipMalloc(&c->d_g, sizeof(Globals)));
-    HIPCK(hipHostMalloc(&c->h_g, sizeof(Globals), hipHostMallocDefault));
     {
         static uint32_t hn[NTAB_ALL];
         for (int k = 0; k < NIB_SCAN + NIB_SH + 1; k++) {
@@ -1624,10 +1625,10 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
-    hipFree(c->d_files); hipFree(c->d_tprefix); hipFree(c->d_finfo); hipFree(c->d_ftotal);
+    hipFree(c->d_call); hipFree(c->d_ftotal);
     hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_rec);
-    hipFree(c->d_g); hipFree(c->d_tabs); hipFree(c->d_pw); hipFree(c->d_bytes); hipFree(c->d_tuples); hipFree(c->d_dbg);
-    hipHostFree(c->h_files); hipHostFree(c->h_tprefix); hipHostFree(c->h_finfo); hipHostFree(c->h_g);
+    hipFree(c->d_tabs); hipFree(c->d_pw); hipFree(c->d_bytes); hipFree(c->d_tuples); hipFree(c->d_dbg);
+    hipHostFree(c->h_call);
     cly_merge_scratch_free(c->merge_scratch);
     for (int i = 0; i < 8; i++) hipEventDestroy(c->ev[i]);
     hipStreamDestroy(c->stream);
@@ -1640,21 +1641,27 @@ extern "C" uint64_t cly_scan_capacity(const cly_file* files, int nfiles) {
     return cap;
 }
 
+// The per-call block, one device allocation and its page-locked mirror:
+// [Globals | FileInfo x cap | DevFile x cap | tprefix x (cap + 1)], so that a
+// call moves its inputs (and zeroes the outputs) with one copy in and reads
+// the results back with one copy out.
+static inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 static int ensure_files(cly_ctx* c, int nfiles) {
     if (nfiles <= c->cap_files) return CLY_OK;
-    hipFree(c->d_files); hipFree(c->d_tprefix); hipFree(c->d_finfo); hipFree(c->d_ftotal);
-    hipHostFree(c->h_files); hipHostFree(c->h_tprefix); hipHostFree(c->h_finfo);
-    c->d_files = nullptr; c->d_tprefix = nullptr; c->d_finfo = nullptr; c->d_ftotal = nullptr;
-    c->h_files = nullptr; c->h_tprefix = nullptr; c->h_finfo = nullptr;
+    hipFree(c->d_call); hipFree(c->d_ftotal); hipHostFree(c->h_call);
+    c->d_call = nullptr; c->h_call = nullptr; c->d_ftotal = nullptr;
     c->cap_files = 0;
     const int cap = nfiles < 64 ? 64 : nfiles;
-    HIPCK(hipMalloc(&c->d_files, sizeof(DevFile) * cap));
-    HIPCK(hipMalloc(&c->d_tprefix, sizeof(uint32_t) * (cap + 1)));
-    HIPCK(hipMalloc(&c->d_finfo, sizeof(FileInfo) * cap));
+    const size_t o_fi = al16(sizeof(Globals)), o_f = o_fi + al16(sizeof(FileInfo) * cap);
+    const size_t o_tp = o_f + al16(sizeof(DevFile) * cap), tot = o_tp + al16(sizeof(uint32_t) * (cap + 1));
+    HIPCK(hipMalloc(&c->d_call, tot));
     HIPCK(hipMalloc(&c->d_ftotal, sizeof(uint64_t) * cap));
-    HIPCK(hipHostMalloc(&c->h_files, sizeof(DevFile) * cap, hipHostMallocDefault));
-    HIPCK(hipHostMalloc(&c->h_tprefix, sizeof(uint32_t) * (cap + 1), hipHostMallocDefault));
-    HIPCK(hipHostMalloc(&c->h_finfo, sizeof(FileInfo) * cap, hipHostMallocDefault));
+    HIPCK(hipHostMalloc(&c->h_call, tot, hipHostMallocDefault));
+    c->d_g = (Globals*)c->d_call; c->h_g = (Globals*)c->h_call;
+    c->d_finfo = (FileInfo*)(c->d_call + o_fi); c->h_finfo = (FileInfo*)(c->h_call + o_fi);
+    c->d_files = (DevFile*)(c->d_call + o_f); c->h_files = (DevFile*)(c->h_call + o_f);
+    c->d_tprefix = (uint32_t*)(c->d_call + o_tp); c->h_tprefix = (uint32_t*)(c->h_call + o_tp);
+    c->call_bytes = tot;
     c->cap_files = cap;
     return CLY_OK;
 }
@@ -1706,10 +1713,9 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     c->h_tprefix[nfiles] = (uint32_t)ntiles;
     rc = ensure_tiles(c, ntiles);
     if (rc) return rc;
-    HIPCK(hipMemcpyAsync(c->d_files, c->h_files, sizeof(DevFile) * nfiles, hipMemcpyHostToDevice, st));
-    HIPCK(hipMemcpyAsync(c->d_tprefix, c->h_tprefix, sizeof(uint32_t) * (nfiles + 1), hipMemcpyHostToDevice, st));
-    HIPCK(hipMemsetAsync(c->d_finfo, 0, sizeof(FileInfo) * nfiles, st));
-    HIPCK(hipMemsetAsync(c->d_g, 0, sizeof(Globals), st));
+    memset(c->h_g, 0, sizeof(Globals));
+    memset(c->h_finfo, 0, sizeof(FileInfo) * nfiles);
+    HIPCK(hipMemcpyAsync(c->d_call, c->h_call, c->call_bytes, hipMemcpyHostToDevice, st));
     const uint32_t nt32 = (uint32_t)ntiles;
     int grid = c->scan_grid;
     if ((int64_t)grid * SCAN_WAVES > ntiles) grid = (int)((ntiles + SCAN_WAVES - 1) / SCAN_WAVES);
@@ -1730,10 +1736,16 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     // k_emit/k_fin, which return at once if the link listed tiles; only then
     // the host waits.  Repair rounds (k_refix + k_link) follow on the host loop.
     hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_loc, c->d_tin, c->d_ftotal,
-                       c->d_finfo, c->d_fix, c->d_g, 0);
+                       c->d_finfo, c->d_fix, c->d_g, 0, -1);
+    // one repair round on the device, without a host wait: k_refix and
+    // k_link return at once when the first link listed no tile
+    hipLaunchKernelGGL(k_refix, dim3(REFIX_GRID), dim3(64 * SCAN_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix,
+                       c->d_loc, c->d_tin, c->d_rec, c->d_treg, c->d_tabs, c->d_fix, c->d_g, 0);
+    hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_loc, c->d_tin, c->d_ftotal,
+                       c->d_finfo, c->d_fix, c->d_g, 1, 0);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[2], st));
-    int slot = 0;
+    int slot = 1;
     auto launch_emit = [&]() -> int {
         int eg = c->emit_grid;
         if ((int64_t)eg * EMIT_WAVES > ntiles) eg = (int)((ntiles + EMIT_WAVES - 1) / EMIT_WAVES);
@@ -1750,8 +1762,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[7], st));
         // one read-back and one wait for the whole call when no repair round is needed
-        HIPCK(hipMemcpyAsync(c->h_finfo, c->d_finfo, sizeof(FileInfo) * nfiles, hipMemcpyDeviceToHost, st));
-        HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
+        HIPCK(hipMemcpyAsync(c->h_call, c->d_call, (uint8_t*)(c->h_finfo + nfiles) - c->h_call, hipMemcpyDeviceToHost, st));
         HIPCK(hipStreamSynchronize(st));
         return CLY_OK;
     };
@@ -1768,6 +1779,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     }
     float ms_fix = 0;
     uint32_t rounds = 1, refixed = 0;
+    if (c->h_g->nfix[0]) { rounds++; refixed += c->h_g->nfix[0]; }          // the device round
     if (c->h_g->nfix[slot]) {
         HIPCK(hipEventRecord(c->ev[5], st));
         while (c->h_g->nfix[slot]) {
@@ -1781,7 +1793,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
                                c->d_files, nfiles, c->d_tprefix, c->d_loc, c->d_tin, c->d_rec, c->d_treg, c->d_tabs,
                                c->d_fix, c->d_g, slot);
             hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_loc, c->d_tin,
-                               c->d_ftotal, c->d_finfo, c->d_fix, c->d_g, ns);
+                               c->d_ftotal, c->d_finfo, c->d_fix, c->d_g, ns, -1);
             HIPCK(hipGetLastError());
             HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
             HIPCK(hipStreamSynchronize(st));
