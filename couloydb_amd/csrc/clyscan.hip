@@ -1086,6 +1086,9 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
 
 // ---------------------------------------------------------------------------
 // Kernels of one call.
+// the wave's index in its workgroup, as a wave-uniform (SGPR) value: tile
+// indices, file descriptors and buffer resources derived from it stay scalar
+__device__ __forceinline__ uint32_t wave_id() { return (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 __device__ __forceinline__ int find_file(const uint32_t* __restrict__ tprefix, int nfiles, uint32_t t) {
     int lo = 0, hi = nfiles - 1;
     while (lo < hi) {
@@ -1110,11 +1113,11 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS_ALL];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
     init_tables(smem, tabs + TAB_SCAN, NIB_SCAN * 128);
-    CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)(smem + SCAN_LDS + (threadIdx.x >> 6) * STG_BYTES);
+    CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)(smem + SCAN_LDS + wave_id() * STG_BYTES);
     const int lane = threadIdx.x & 63;
     const CrcLane cl = crc_lane(lane);
     const uint32_t K4 = k4_const(smem, cl.r4);
-    for (uint32_t t = blockIdx.x * SCAN_WAVES + (threadIdx.x >> 6); t < ntiles; t += gridDim.x * SCAN_WAVES) {
+    for (uint32_t t = blockIdx.x * SCAN_WAVES + wave_id(); t < ntiles; t += gridDim.x * SCAN_WAVES) {
         const int f = find_file(tprefix, nfiles, t);
         const DevFile F = files[f];
         tile_body<BM_SPEC>(F, t, t - F.first_tile, 0u, false, smem, stg, cl, K4, loc, rec, treg, nullptr, 0, 0, g);
@@ -1305,8 +1308,8 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS_ALL];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
     init_tables(smem, tabs + TAB_SCAN, NIB_SCAN * 128);
-    CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)(smem + SCAN_LDS + (threadIdx.x >> 6) * STG_BYTES);
-    const uint32_t k = blockIdx.x * SCAN_WAVES + (threadIdx.x >> 6);
+    CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)(smem + SCAN_LDS + wave_id() * STG_BYTES);
+    const uint32_t k = blockIdx.x * SCAN_WAVES + wave_id();
     if (k >= g->nfix[slot]) return;
     const int lane = threadIdx.x & 63;
     const CrcLane cl = crc_lane(lane);
@@ -1370,11 +1373,11 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     CLY_LDS uint32_t* sht = (CLY_LDS uint32_t*)smem_raw;
     for (int i = threadIdx.x; i < NIB_SH * 128; i += blockDim.x) sht[i] = tabs[TAB_SH + i];
     __syncthreads();
-    CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)(smem_raw + NIB_SH * 128 * 4 + (threadIdx.x >> 6) * STG_BYTES);
+    CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)(smem_raw + NIB_SH * 128 * 4 + wave_id() * STG_BYTES);
     CLY_LDS u32x4* sv = (CLY_LDS u32x4*)stg;
     const int lane = threadIdx.x & 63;
     const CrcLane cl = crc_lane(lane);
-    for (uint32_t t = blockIdx.x * EMIT_WAVES + (threadIdx.x >> 6); t < ntiles; t += gridDim.x * EMIT_WAVES) {
+    for (uint32_t t = blockIdx.x * EMIT_WAVES + wave_id(); t < ntiles; t += gridDim.x * EMIT_WAVES) {
         const int f = find_file(tprefix, nfiles, t);
         const DevFile F = files[f];
         LBState S = ti_load(&tin[t]);
