@@ -642,7 +642,7 @@ k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uin
     __shared__ uint64_t s_src[MC_W][CMAX];
     __shared__ uint32_t s_end[MC_W][CMAX];
     __shared__ uint8_t s_pre[MC_W][CMAX];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;   // (scalar: block indices in SGPRs)
     int32_t* rel = s_rel[w];
     uint64_t* srcs = s_src[w];
     uint32_t* sizes = s_end[w];
