@@ -59,10 +59,15 @@ extern "C" hipError_t cly_ix_hash_ptr_internal(cly_ctx* ctx, uint64_t n, void** 
 static std::mutex g_stage_mu;
 static void* g_stage[2 * LOAD_THREADS_MAX];
 
+// db->state bytes: the index state (low nibble) and the record's data type
+// (high nibble; k_state_dt)
+#define ST_STATE(b) ((uint8_t)((b) & 15))
+#define ST_DT(b) ((uint32_t)((b) >> 4))
 struct Mapped {
     uint32_t fid;
     const uint8_t* p;
     uint64_t len;
+    int fd = -1;                 // kept open: the copy to HBM preads it (no page faults on the mapping)
 };
 // Go's strconv.Atoi (64-bit int): an optional sign, decimal digits, no overflow
 static bool go_atoi(const char* s, size_t n, int64_t& v) {
@@ -254,9 +259,11 @@ static int map_file(const char* path, Mapped& m, bool& exists) {
     if (fstat(fd, &sb) != 0 || S_ISDIR(sb.st_mode)) { close(fd); return CLY_ERR_ARG; }
     m.len = (uint64_t)sb.st_size;
     if (m.len) {
-        void* p = mmap(nullptr, m.len, PROT_READ, MAP_PRIVATE, fd, 0);     // pages: faulted in by the copy threads
+        void* p = mmap(nullptr, m.len, PROT_READ, MAP_PRIVATE, fd, 0);     // for the host's key reads
         if (p == MAP_FAILED) { close(fd); m.len = 0; return CLY_ERR_ARG; }
         m.p = (const uint8_t*)p;
+        m.fd = fd;
+        return CLY_OK;
     }
     close(fd);
     return CLY_OK;
@@ -313,9 +320,9 @@ static void flat_build(cly_db* db, int nthreads, std::vector<uint64_t>& composit
         uint64_t* c = &cnt[(size_t)t * 2 * FLAT_SHARDS];
         for (uint64_t i = a; i < b; i++) {
             hv[i] = 0;
-            const uint8_t st = db->state[i];
+            const uint8_t st = ST_STATE(db->state[i]);
             if (st != CLY_IX_LIVE && st != CLY_IX_LOADONLY) continue;
-            const uint32_t dt = db->tuples[i].data_type;
+            const uint32_t dt = ST_DT(db->state[i]);
             if (dt == 1 || dt == 2 || dt == 4) { comp[t].push_back(i); continue; }    // Hash / List / Set
             if (st != CLY_IX_LIVE || (dt != 0 && dt != 3)) continue;               // String / ListMeta
             hv[i] = (db->khash[i] & db->hmask) | 1;
@@ -330,7 +337,7 @@ static void flat_build(cly_db* db, int nthreads, std::vector<uint64_t>& composit
         for (int ks = 0; ks < 2 * FLAT_SHARDS; ks++) w[ks] = boff[(size_t)ks * nthreads + t];
         for (uint64_t i = a; i < b; i++) {
             if (!hv[i]) continue;
-            const int ks = (db->tuples[i].data_type == 3) * FLAT_SHARDS + flat_shard(hv[i], db->hshift);
+            const int ks = (ST_DT(db->state[i]) == 3) * FLAT_SHARDS + flat_shard(hv[i], db->hshift);
             bidx[w[ks]++] = i;
         }
     };
@@ -378,12 +385,23 @@ static void flat_build(cly_db* db, int nthreads, std::vector<uint64_t>& composit
 
 extern "C" void cly_db_close(cly_db* db) {
     if (!db) return;
-    for (Mapped& m : db->files) if (m.p) munmap((void*)m.p, m.len);
+    for (Mapped& m : db->files) { if (m.p) munmap((void*)m.p, m.len); if (m.fd >= 0) close(m.fd); }
     if (db->hint.p) munmap((void*)db->hint.p, db->hint.len);
+    if (db->hint.fd >= 0) close(db->hint.fd);
     delete db;
 }
 
 #define DCK(x) do { if ((x) != hipSuccess) { rc = CLY_ERR_DEVICE; goto done; } } while (0)
+
+// The host table build's per-record class byte: the index state (low nibble)
+// and the data type (high nibble, 7 for any type above 6), so that the build
+// reads 1 B per record instead of the 48-B tuple
+__global__ void k_state_dt(uint8_t* state, const cly_tuple* t, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t dt = t[i].data_type;
+    state[i] = (uint8_t)(state[i] | ((dt < 7 ? dt : 7) << 4));
+}
 
 // A hint record's tuple as the index rebuild takes it: strIndex.Put of its
 // stored key (no txId prefix, merge.go:283), whatever its types, no TTL
@@ -407,16 +425,17 @@ static int stage_ready() {
 // t0+nt-1) fault the mapped pages in and copy 64-MiB pieces through the
 // page-locked staging buffers (CPU copy of one while the DMA of the other
 // runs).  The caller holds g_stage_mu.
-static int copy_to_device(int dev, const std::vector<cly_file>& hf, std::vector<cly_file>& df, uint8_t* d_bytes,
-                          int t0, int nt) {
-    struct Piece { const uint8_t* src; uint8_t* dst; uint64_t len; };
+static int copy_to_device(int dev, const std::vector<cly_file>& hf, const int* fds, std::vector<cly_file>& df,
+                          uint8_t* d_bytes, int t0, int nt) {
+    struct Piece { const uint8_t* src; uint8_t* dst; uint64_t len; int fd; uint64_t foff; };
     std::vector<Piece> pieces;
     uint64_t off = 0;
     for (size_t i = 0; i < hf.size(); i++) {
         df[i] = hf[i];
         df[i].base = d_bytes + off;
         for (uint64_t a = 0; a < hf[i].len; a += LOAD_PIECE)
-            pieces.push_back({hf[i].base + a, d_bytes + off + a, std::min<uint64_t>(LOAD_PIECE, hf[i].len - a)});
+            pieces.push_back({hf[i].base + a, d_bytes + off + a, std::min<uint64_t>(LOAD_PIECE, hf[i].len - a),
+                              fds ? fds[i] : -1, a});
         off += (hf[i].len + 4095) & ~4095ull;
     }
     std::atomic<size_t> next(0);
@@ -436,7 +455,14 @@ static int copy_to_device(int dev, const std::vector<cly_file>& hf, std::vector<
                 const uint64_t n = std::min<uint64_t>(LOAD_STAGE, pc.len - a);
                 uint8_t* stg = (uint8_t*)g_stage[2 * (t0 + t) + b];
                 if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) err = 1;
-                memcpy(stg, pc.src + a, n);
+                if (pc.fd >= 0) {
+                    // read(2) from the page cache straight into the staging buffer
+                    for (uint64_t got = 0; got < n;) {
+                        const ssize_t r = pread(pc.fd, stg + got, n - got, (off_t)(pc.foff + a + got));
+                        if (r <= 0) { memcpy(stg + got, pc.src + a + got, n - got); break; }
+                        got += (uint64_t)r;
+                    }
+                } else memcpy(stg, pc.src + a, n);
                 if (hipMemcpyAsync(pc.dst + a, stg, n, hipMemcpyHostToDevice, ts) != hipSuccess ||
                     hipEventRecord(ev[b], ts) != hipSuccess) err = 1;
                 used[b] = true;
@@ -453,7 +479,7 @@ static int copy_to_device(int dev, const std::vector<cly_file>& hf, std::vector<
 // Device buffers back to host memory, in pieces from several threads (DMA
 // into one staging buffer while the CPU copies the other out).
 struct D2H { void* dst; const void* src; uint64_t len; };
-static int copy_to_host(cly_ctx* ctx, const std::vector<D2H>& parts) {
+static int copy_to_host(cly_ctx* ctx, const std::vector<D2H>& parts, int t0, int nt) {
     struct Piece { void* dst; const void* src; uint64_t len; };
     std::vector<Piece> pieces;
     for (const D2H& x : parts)
@@ -464,7 +490,9 @@ static int copy_to_host(cly_ctx* ctx, const std::vector<D2H>& parts) {
     const int dev = cly_ctx_device_internal(ctx);
     std::lock_guard<std::mutex> lk(g_stage_mu);
     if (stage_ready() != CLY_OK) return CLY_ERR_DEVICE;
-    par_run(load_threads(), [&](int t) {
+    // (threads t0 .. t0+nt-1, each with its own two staging buffers)
+    par_run(nt, [&, t0](int tl) {
+        const int t = t0 + tl;
         if (hipSetDevice(dev) != hipSuccess) { err = 1; return; }
         hipStream_t ts = nullptr;
         if (hipStreamCreateWithFlags(&ts, hipStreamNonBlocking) != hipSuccess) { err = 1; return; }
@@ -517,6 +545,7 @@ static int check_merge_finished(const char* dir) {
         if (!go_atoi((const char*)m.p + h.hsz + h.ks, h.vs, v)) rc = CLY_ERR_MERGE_FIN;
     }
     if (m.p) munmap((void*)m.p, m.len);
+    if (m.fd >= 0) close(m.fd);
     return rc;
 }
 
@@ -561,7 +590,7 @@ struct LoadShard {
     int rc = CLY_OK;
     double t_copy = 0, t_scan = 0;
 };
-static void shard_load(LoadShard& S, const std::vector<cly_file>& hf, int t0, int nt) {
+static void shard_load(LoadShard& S, const std::vector<cly_file>& hf, const std::vector<int>& fds, int t0, int nt) {
     const int n = S.f1 - S.f0;
     const std::vector<cly_file> h(hf.begin() + S.f0, hf.begin() + S.f1);
     S.df.resize(n); S.res.resize(n); S.first.resize(n);
@@ -569,7 +598,7 @@ static void shard_load(LoadShard& S, const std::vector<cly_file>& hf, int t0, in
     uint64_t total = 0;
     for (const cly_file& f : h) total += (f.len + 4095) & ~4095ull;
     if (hipMalloc((void**)&S.d_bytes, total + 4096) != hipSuccess) { S.d_bytes = nullptr; S.rc = CLY_ERR_DEVICE; return; }
-    S.rc = copy_to_device(S.dev, h, S.df, S.d_bytes, t0, nt);
+    S.rc = copy_to_device(S.dev, h, fds.data() + S.f0, S.df, S.d_bytes, t0, nt);
     S.t_copy = now_ms();
     if (S.rc != CLY_OK) return;
     S.cap = cly_scan_capacity(h.data(), n) + 16;
@@ -613,6 +642,7 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
     uint8_t* d_state = nullptr;
     cly_pos* d_hpos = nullptr;
     std::vector<cly_file> hf, df;
+    std::vector<int> hfd;                        // the files' descriptors (pread by the copy threads)
     std::vector<cly_file_result> res;
     std::vector<uint64_t> first;
     std::vector<LoadShard> sh(nctx);
@@ -635,10 +665,12 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
     s.n_files = (uint64_t)nf;
     nall = nf + (has_hint ? 1 : 0);
     hf.resize(nall);
-    if (has_hint) { hf[0].base = db->hint.p; hf[0].len = db->hint.len; hf[0].fid = 0; hf[0]._pad = 0; }
+    hfd.assign(nall, -1);
+    if (has_hint) { hf[0].base = db->hint.p; hf[0].len = db->hint.len; hf[0].fid = 0; hf[0]._pad = 0; hfd[0] = db->hint.fd; }
     for (int i = 0; i < nf; i++) {
         cly_file& f = hf[i + (has_hint ? 1 : 0)];
         f.base = db->files[i].p; f.len = db->files[i].len; f.fid = db->files[i].fid; f._pad = 0;
+        hfd[i + (has_hint ? 1 : 0)] = db->files[i].fd;
         s.bytes += f.len;
     }
     {
@@ -669,7 +701,7 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
         int slot = 0;
         for (LoadShard& S : sh) {
             if (S.f1 == S.f0) continue;
-            th.emplace_back(shard_load, std::ref(S), std::cref(hf), slot, ntk);
+            th.emplace_back(shard_load, std::ref(S), std::cref(hf), std::cref(hfd), slot, ntk);
             slot += ntk;
         }
         for (auto& x : th) x.join();
@@ -749,13 +781,17 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
     db->hshift = 64 - __builtin_clzll(db->hmask | 15) - FLAT_SHARD_BITS;
     DCK(hipStreamSynchronize(strm));
     if (need) {
+        // the class bytes and key hashes first (what the table build reads); the
+        // tuples (what lookups read) come back while the host builds the tables
         uint64_t* d_hash = nullptr;
         DCK(cly_ix_hash_ptr_internal(ctx, need, (void**)&d_hash));
-        std::vector<D2H> parts = {{db->tuples.data(), d_tup, sizeof(cly_tuple) * need},
-                                  {db->state.data(), d_state, need},
+        hipLaunchKernelGGL(k_state_dt, dim3((unsigned)((need + 255) / 256)), dim3(256), 0, strm, d_state, d_tup, need);
+        DCK(hipGetLastError());
+        DCK(hipStreamSynchronize(strm));
+        std::vector<D2H> parts = {{db->state.data(), d_state, need},
                                   {db->khash.data(), d_hash, sizeof(uint64_t) * need}};
         if (db->n_hint) parts.push_back({db->hint_pos.data(), d_hpos, sizeof(cly_pos) * db->n_hint});
-        rc = copy_to_host(ctx, parts);
+        rc = copy_to_host(ctx, parts, 0, load_threads());
         if (rc != CLY_OK) goto done;
     }
     t4 = now_ms();
@@ -766,7 +802,18 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
         // device marked as index entries: String / ListMeta into the flat
         // tables, Hash / List / Set into realKey -> (field | seqBuf | hashKey) maps
         std::vector<uint64_t> composite;
-        flat_build(db, std::min(FLAT_SHARDS, load_threads()), composite);
+        int trc = CLY_OK;
+        {
+            // the tuples' read-back on copy threads 8..15 beside the build's threads 0..7
+            const int nb = std::max(1, std::min(FLAT_SHARDS, load_threads()) / 2);
+            std::thread tcopy([&]() {
+                if (need) trc = copy_to_host(ctx, {{db->tuples.data(), d_tup, sizeof(cly_tuple) * need}}, nb,
+                                             std::max(1, load_threads() - nb));
+            });
+            flat_build(db, nb, composite);
+            tcopy.join();
+        }
+        if (trc != CLY_OK) { rc = trc; goto done; }
         for (uint64_t i : composite) {
             const cly_tuple& t = db->tuples[i];
             uint32_t off, len;
@@ -796,7 +843,7 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
         // the TTL sweep's db.Del (db.go:639-651, 186-215): a tombstone per swept
         // key appended by appendLogRecord's rule (db.go:368-413)
         for (uint64_t i = db->n_hint; i < need; i++)
-            if (db->state[i] == CLY_IX_EXPIRED) db->expired.push_back(i);
+            if (ST_STATE(db->state[i]) == CLY_IX_EXPIRED) db->expired.push_back(i);
         s.n_expired = db->expired.size();
         uint32_t afid = s.active_fid_loaded;
         int64_t woff = s.write_off_loaded;

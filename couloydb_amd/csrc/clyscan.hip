@@ -624,7 +624,7 @@ __device__ __forceinline__ void patch_word(uint32_t (&w)[16], uint32_t k, uint32
 #define BM_EXACT 1
 #define BM_EMIT 2
 #ifndef CLY_EXP
-#define CLY_EXP 0                // timing experiments only (wrong results): 1 no record work, 6 no CRC
+#define CLY_EXP 0                // timing experiments only (wrong results): 1 no record work, 6 no CRC, 8 no pred_walk
                                  // table steps, 7 neither, 3 candidate
 #endif                           // masks only, 2 no per-record outputs, 5 no agreement pass
 #ifndef CLY_PROF
@@ -651,6 +651,12 @@ struct TState {
     uint32_t Tb;                 // terminal position in the current block (NONE32: none)
     uint32_t tpatch;             // its patch word (XORed after the bytes from Tb on are zeroed)
     uint32_t carry_next;         // register XOR due at the next block's first byte (terminal at the block end)
+    // stride reference (stride_round): header bytes 4..15 of the last record
+    // (ref1..3) under the masks of its bytes 4..hsz, and the uniform words of
+    // its compact entry; valid while ref_ok
+    bool ref_ok;
+    uint32_t ref_s;              // the reference record's size (the stride)
+    uint32_t ref1, ref2, ref3, msk1, msk2, msk3, rw1, rw2, rw3;
 };
 // The block's outputs for record k of a round (lane k); returns its CRC patch,
 // to be XORed into the stage word holding P (one writer per word: record
@@ -763,6 +769,83 @@ __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t 
     return S.dead || !(X < bend || (X == flen && flen == bend));
 }
 
+// Stride round (regular data: the last two records had the same size; s =
+// the reference record's size): lane k takes X + k s; a record there whose
+// header bytes 4..hsz equal the reference's (type, data type, the three
+// varints and the first key byte) is a record of size s with the same fields,
+// so no decode is needed, only its stored CRC.  Lanes up to the first one that differs (or leaves the block, or
+// would pass the file's end) are records; the rest of the block goes to
+// pred_walk from there.
+template <int BM>
+__device__ __forceinline__ void stride_round(const DevFile& F, TState& S, uint32_t tb, uint32_t bs,
+                                             CLY_LDS uint32_t* stg, const CLY_LDS uint8_t* smem, const CrcLane& cl,
+                                             uint32_t K4, rsrc_t trs, int lane) {
+    const uint32_t X = S.X, s = S.ref_s, k = (uint32_t)lane;
+    const uint64_t bend = (uint64_t)bs + CLY_BLK;
+    if (S.dead || (uint64_t)X >= bend) return;
+    const uint64_t P64 = (uint64_t)X + (uint64_t)k * s;
+    const bool act = P64 < bend && P64 + s <= F.len;
+    const uint32_t P = act ? (uint32_t)P64 : X;
+    const CLY_LDS uint32_t* q = stg + stg_dw((P - bs) >> 2);
+    const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4], sh = P & 3u;
+    const uint32_t crc = alignb(w1, w0, sh), h1 = alignb(w2, w1, sh), h2 = alignb(w3, w2, sh), h3 = alignb(w4, w3, sh);
+    const bool match = act && (((h1 ^ S.ref1) & S.msk1) | ((h2 ^ S.ref2) & S.msk2) | ((h3 ^ S.ref3) & S.msk3)) == 0u;
+    const u64 bm = __ballot(!match);
+    const uint32_t kb = bm ? (uint32_t)__ffsll((long long)bm) - 1 : 64u;
+    if (kb == 0) return;
+    const uint32_t up = dppu<DPP_WF_SR1>(0u, crc);
+    const uint32_t dq = k == 0 ? (S.cq_known ? ~S.cq : 0xFFFFFFFFu) : ~up;
+    uint32_t pw = 0, pv = 0;
+    if (k < kb) {
+        if (S.tcnt + k < CAP_T)
+            __builtin_amdgcn_raw_buffer_store_b128((u32x4){crc, S.rw1, S.rw2, (P - tb) | S.rw3}, trs,
+                                                   (int)((S.tcnt + k) * 16u), 0, 0);
+        const uint32_t d = crc ^ K4 ^ dq, j = P & 3u;
+        pw = ((P - bs) >> 2) + (j ? 1u : 0u);
+        pv = j ? crc_fwd(smem, d, 4u - j, cl.r4) : d;
+        if (pw < PW_CARRY) stg[stg_dw(pw)] ^= pv;
+    }
+    const u64 bc = __ballot(k < kb && pw == PW_CARRY);
+    if (bc) S.carry_next ^= rdl(pv, __ffsll((long long)bc) - 1);
+    if (S.G == NONE32) S.G = X;
+    S.last_crc = rdl(crc, (int)kb - 1);
+    S.P_last = X + (kb - 1) * s;
+    S.cq = S.last_crc; S.cq_known = true;
+    S.X = S.P_last + s;
+    S.tcnt += kb;
+    S.s_prev = kb >= 2 ? s : S.s_last;
+    S.s_last = s;
+}
+// The stride reference from the last record (after pred_walk accepted
+// records): taken when the last two sizes are equal and the last record is in
+// the stage and has a short compact entry with its header in bytes 0..15.
+__device__ __forceinline__ void stride_ref(const DevFile& F, TState& S, uint32_t bs, const CLY_LDS uint32_t* stg) {
+    S.ref_ok = false;
+    if (S.dead || !S.s_last || S.s_last != S.s_prev || S.P_last == NONE32 || S.P_last < bs) return;
+    const uint32_t P = S.P_last;
+    const Hdr h = hdr_get(P, F.len, stg, bs);
+    const bool sh = h.status == REC_OK && h.exp == 0 && h.key0 < 0x80u && h.ks >= 1u && h.ks < (1u << 24) &&
+                    h.type < 8u && h.dt < 8u && h.hsz >= 6 && h.hsz <= 15 && (uint32_t)h.size == S.s_last;
+    if (!sh) return;
+    const CLY_LDS uint32_t* q = stg + stg_dw((P - bs) >> 2);
+    const uint32_t w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4], a = P & 3u;
+    S.ref1 = __builtin_amdgcn_readfirstlane(alignb(w2, w1, a));
+    S.ref2 = __builtin_amdgcn_readfirstlane(alignb(w3, w2, a));
+    S.ref3 = __builtin_amdgcn_readfirstlane(alignb(w4, w3, a));
+    const uint32_t hz = (uint32_t)h.hsz;                       // bytes 4..hz compared
+    auto msk = [&](uint32_t b0) {                              // bytes b0..b0+3
+        uint32_t m = 0;
+        for (uint32_t b = 0; b < 4; b++) if (b0 + b <= hz) m |= 0xFFu << (8 * b);
+        return m;
+    };
+    S.msk1 = msk(4); S.msk2 = msk(8); S.msk3 = msk(12);
+    S.rw1 = h.ks | ((uint32_t)(h.hsz - 6) << 24) | (h.type << 29);
+    S.rw2 = h.vs;
+    S.rw3 = (h.dt << 16) | (h.key0 << 19) | REC_SHORT;
+    S.ref_s = (uint32_t)h.size;
+    S.ref_ok = true;
+}
+
 // Guess mode (a tile other than its file's first, entry unknown): every
 // lane's first candidate record start in its 64-B segment whose speculative
 // walk holds, validated at the walk's exit (a candidate of the block, or a
@@ -866,6 +949,7 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     S.cq_known = tt == 0;        // tile 0: no record before offset 0
     S.cq = 0; S.G = NONE32; S.tcnt = 0; S.last_crc = 0; S.P_last = NONE32; S.term = TERM_NONE;
     S.s_last = 0; S.s_prev = 0; S.Tb = NONE32; S.tpatch = 0; S.carry_next = 0;
+    S.ref_ok = false; S.ref_s = 0; S.ref1 = S.ref2 = S.ref3 = S.msk1 = S.msk2 = S.msk3 = S.rw1 = S.rw2 = S.rw3 = 0;
     uint32_t R = 0, carry = 0;   // carry: register XOR due at this block's first byte
     const CLY_LDS uint32_t* nibt = (const CLY_LDS uint32_t*)(smem + LDS_NIB);
     const rsrc_t trs = mk_rsrc(rec + (uint64_t)t * CAP_T * 4, CAP_T * 16u);      // the tile's compact entries
@@ -915,7 +999,12 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
             if (S.X == NONE32) { S.X = guess_entry(F, bs, stg, hc, lane); PC(6); }    // the tile's guessed entry
             PT(1);
             bool done = true;
-            if (S.X != NONE32) done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, trs, out, out_cap, gbase, g, lane);
+            if (S.X != NONE32 && CLY_EXP != 8) {
+                if (BM != BM_EMIT && S.ref_ok) stride_round<BM>(F, S, tb, bs, stg, smem, cl, K4, trs, lane);
+                const uint32_t c0 = S.tcnt;
+                done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, trs, out, out_cap, gbase, g, lane);
+                if (BM != BM_EMIT && S.tcnt != c0) stride_ref(F, S, bs, stg);
+            }
             PT(2);
             if (!done) {
                 PC(7);
