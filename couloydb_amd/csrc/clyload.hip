@@ -425,8 +425,43 @@ static int stage_ready() {
 // t0+nt-1) fault the mapped pages in and copy 64-MiB pieces through the
 // page-locked staging buffers (CPU copy of one while the DMA of the other
 // runs).  The caller holds g_stage_mu.
+// Experiment switches of the load path (CLY_H2D_MODE: 0 memcpy from the
+// mapping into the staging buffers, 1 pread into them, 2 the mapping
+// registered and copied by DMA directly; CLY_LOAD_OVERLAP: 1 the tuples'
+// read-back beside the table build).  Measured on C2 (tools/exp_load.py): H2D
+// 86-90 ms (0), 92-97 (1), 156-163 (2); wall 216-232 ms with the overlap.
+static int g_h2d_mode = 0, g_overlap = 0;
+static void load_switches() {
+    const char* a = getenv("CLY_H2D_MODE");
+    const char* b = getenv("CLY_LOAD_OVERLAP");
+    g_h2d_mode = a ? atoi(a) : 0;
+    g_overlap = b ? atoi(b) : 1;
+}
 static int copy_to_device(int dev, const std::vector<cly_file>& hf, const int* fds, std::vector<cly_file>& df,
                           uint8_t* d_bytes, int t0, int nt) {
+    if (g_h2d_mode == 2) {
+        // the mapped files registered (page-locked in place) and copied by DMA
+        int err = 0;
+        uint64_t off = 0;
+        if (hipSetDevice(dev) != hipSuccess) return CLY_ERR_DEVICE;
+        hipStream_t ts = nullptr;
+        if (hipStreamCreateWithFlags(&ts, hipStreamNonBlocking) != hipSuccess) return CLY_ERR_DEVICE;
+        std::vector<const void*> reg;
+        for (size_t i = 0; i < hf.size(); i++) {
+            df[i] = hf[i];
+            df[i].base = d_bytes + off;
+            if (hf[i].len) {
+                if (hipHostRegister((void*)hf[i].base, hf[i].len, hipHostRegisterReadOnly) != hipSuccess) { err = 1; break; }
+                reg.push_back(hf[i].base);
+                if (hipMemcpyAsync(d_bytes + off, hf[i].base, hf[i].len, hipMemcpyHostToDevice, ts) != hipSuccess) err = 1;
+            }
+            off += (hf[i].len + 4095) & ~4095ull;
+        }
+        if (hipStreamSynchronize(ts) != hipSuccess) err = 1;
+        for (const void* p : reg) hipHostUnregister((void*)p);
+        hipStreamDestroy(ts);
+        return err ? CLY_ERR_DEVICE : CLY_OK;
+    }
     struct Piece { const uint8_t* src; uint8_t* dst; uint64_t len; int fd; uint64_t foff; };
     std::vector<Piece> pieces;
     uint64_t off = 0;
@@ -455,7 +490,7 @@ static int copy_to_device(int dev, const std::vector<cly_file>& hf, const int* f
                 const uint64_t n = std::min<uint64_t>(LOAD_STAGE, pc.len - a);
                 uint8_t* stg = (uint8_t*)g_stage[2 * (t0 + t) + b];
                 if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) err = 1;
-                if (pc.fd >= 0) {
+                if (pc.fd >= 0 && g_h2d_mode == 1) {
                     // read(2) from the page cache straight into the staging buffer
                     for (uint64_t got = 0; got < n;) {
                         const ssize_t r = pread(pc.fd, stg + got, n - got, (off_t)(pc.foff + a + got));
@@ -626,6 +661,7 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
     for (int k = 0; k < nctx; k++) if (!ctxs[k]) return CLY_ERR_ARG;
     *out = nullptr;
     cly_ctx* ctx = ctxs[0];                      // the index is rebuilt on the first context
+    load_switches();
     cly_load_stats s;
     memset(&s, 0, sizeof(s));
     const uint64_t dfs = opt && opt->data_file_size ? opt->data_file_size : (256ull << 20);
@@ -803,7 +839,7 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
         // tables, Hash / List / Set into realKey -> (field | seqBuf | hashKey) maps
         std::vector<uint64_t> composite;
         int trc = CLY_OK;
-        {
+        if (g_overlap) {
             // the tuples' read-back on copy threads 8..15 beside the build's threads 0..7
             const int nb = std::max(1, std::min(FLAT_SHARDS, load_threads()) / 2);
             std::thread tcopy([&]() {
@@ -812,6 +848,9 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
             });
             flat_build(db, nb, composite);
             tcopy.join();
+        } else {
+            flat_build(db, std::min(FLAT_SHARDS, load_threads()), composite);
+            if (need) trc = copy_to_host(ctx, {{db->tuples.data(), d_tup, sizeof(cly_tuple) * need}}, 0, load_threads());
         }
         if (trc != CLY_OK) { rc = trc; goto done; }
         for (uint64_t i : composite) {
