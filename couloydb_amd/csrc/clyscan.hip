@@ -627,6 +627,9 @@ __device__ __forceinline__ void patch_word(uint32_t (&w)[16], uint32_t k, uint32
 #define CLY_EXP 0                // timing experiments only (wrong results): 1 no record work, 6 no CRC, 8 no pred_walk
                                  // table steps, 7 neither, 3 candidate
 #endif                           // masks only, 2 no per-record outputs, 5 no agreement pass
+#ifndef CLY_PW_ROUNDS
+#define CLY_PW_ROUNDS 4          // pred_walk rounds per block before the general pass
+#endif
 #ifndef CLY_PROF
 #define CLY_PROF 0               // experiment builds: per-section cycle counts of k_scan's tile body
 #endif
@@ -705,7 +708,7 @@ __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t 
                                           gtuples out, uint64_t out_cap, uint64_t gbase, Globals* g, int lane) {
     const gbytes base = (gbytes)F.base;
     const uint64_t flen = F.len, bend = (uint64_t)bs + CLY_BLK;
-    for (int round = 0; round < 4; round++) {
+    for (int round = 0; round < CLY_PW_ROUNDS; round++) {
         const uint64_t X = S.X;
         const bool owned = X < bend || (X == flen && flen == bend);
         if (S.dead || !owned) return true;
