@@ -332,7 +332,7 @@ class Scanner:
 
     def kernel_ms(self):
         """Per-kernel HIP-event times (ms) of the last scan_device call: k_scan,
-        the link rounds (k_link + k_fbase + repairs), k_emit, k_fin,
+        the link rounds (k_link, the device repair round, host-driven repairs), k_emit, k_fin,
         k_locate, all."""
         k = (ctypes.c_double * 6)()
         self.lib.cly_dbg_kernel_ms(self.ctx, k)
