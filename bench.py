@@ -182,16 +182,22 @@ def cpu_baseline(wl, budget_s=12.0):
         i += 1
     alg_gibs = nbytes / t_alg / 2**30
     # the same restatement with the files spread over MT_THREADS threads (the
-    # box's CPU share), over the first (up to) MT_THREADS sampled files
-    mt_files = files[:MT_THREADS]
+    # box's CPU share), over the configuration's first MT_THREADS files (one
+    # file per thread)
+    mt_files = list(range(min(MT_THREADS, len(wl.dev_files))))
     mt_arrs = [wl.file_bytes(i) for i in mt_files]
     t0 = time.perf_counter()
     mt_rec = int(co.scan_files_mt(mt_arrs, [wl.dev_files[i][2] for i in mt_files], MT_THREADS))
     t_mt = time.perf_counter() - t0
     mt_bytes = sum(len(a) for a in mt_arrs)
     del mt_arrs
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     multi = {"value": round(mt_bytes / t_mt / 2**30, 4), "unit": "GiB/s", "cores": MT_THREADS,
-             "cores_note": "the GPU box's CPU share per GPU (nproc reports the whole host)",
+             "cores_note": "the GPU box's CPU share per GPU (OMP_NUM_THREADS/MAX_JOBS are 16 there; nproc and "
+                           "the affinity mask report the whole host, %s CPUs)" % affinity,
              "mrecords_per_s": round(mt_rec / t_mt / 1e6, 3),
              "sample": "%d files (%.2f GiB), one file per thread, clyo_scan_files_mt" % (len(mt_files), mt_bytes / 2**30)}
     merge_part = None
