@@ -628,7 +628,7 @@ __device__ __forceinline__ void patch_word(uint32_t (&w)[16], uint32_t k, uint32
                                  // table steps, 7 neither, 3 candidate
 #endif                           // masks only, 2 no per-record outputs, 5 no agreement pass
 #ifndef CLY_PW_ROUNDS
-#define CLY_PW_ROUNDS 4          // pred_walk rounds per block before the general pass
+#define CLY_PW_ROUNDS 1          // pred_walk rounds per block before the general pass (C3: 1 round 12.7 ms, 2 13.6, 4 15.4)
 #endif
 #ifndef CLY_PROF
 #define CLY_PROF 0               // experiment builds: per-section cycle counts of k_scan's tile body
