@@ -94,7 +94,7 @@ GEN_SYMBOLS = ["cly_gen_record_size", "cly_gen_layout", "cly_gen_encode"]
 LOAD_SYMBOLS = ["cly_db_open", "cly_db_open_opts", "cly_db_open_multi", "cly_db_close", "cly_db_get", "cly_db_listmeta", "cly_db_hget",
                 "cly_db_lget", "cly_db_sget", "cly_db_value", "cly_index_key", "cly_db_count", "cly_db_entries"]
 DB_NOT_FOUND, DB_EOF = 1, 2
-ERR_DIR, ERR_MERGE_FIN = -14, -15
+ERR_DIR, ERR_MERGE_FIN, ERR_KEY_EMPTY = -14, -15, -16
 IT_STRING, IT_LISTMETA, IT_HASH, IT_LIST, IT_SET, IT_EXPIRED = range(6)
 DB_APPLY_SWEEP = 1
 

@@ -67,7 +67,7 @@ struct Mapped {
     uint32_t fid;
     const uint8_t* p;
     uint64_t len;
-    int fd = -1;                 // kept open: the copy to HBM preads it (no page faults on the mapping)
+    int fd = -1;                 // kept open only for CLY_H2D_MODE=1 (the copy to HBM preads it)
 };
 // Go's strconv.Atoi (64-bit int): an optional sign, decimal digits, no overflow
 static bool go_atoi(const char* s, size_t n, int64_t& v) {
@@ -138,7 +138,8 @@ template <class T> struct HostArr {
     T* data() { return p.get(); }
 };
 struct cly_db {
-    std::vector<Mapped> files;
+    std::vector<Mapped> files;       // in loadIndex's order (fids as sort.Ints orders the stems)
+    std::unordered_map<uint32_t, uint32_t> fid_ix;   // uint32(fid) -> its file
     Mapped hint = {0, nullptr, 0};   // hint-index (tuples 0 .. n_hint-1 are its records)
     uint64_t n_hint = 0;
     std::vector<cly_pos> hint_pos;   // DecodeLogRecordPos of each hint record's value
@@ -190,13 +191,8 @@ static double now_ms() {
 }
 
 static const uint8_t* file_of(const cly_db* db, uint32_t fid) {
-    // fids ascending in `files`: binary search
-    size_t lo = 0, hi = db->files.size();
-    while (lo < hi) {
-        const size_t mid = (lo + hi) / 2;
-        if (db->files[mid].fid < fid) lo = mid + 1; else hi = mid;
-    }
-    return lo < db->files.size() && db->files[lo].fid == fid ? db->files[lo].p : nullptr;
+    const auto it = db->fid_ix.find(fid);
+    return it == db->fid_ix.end() ? nullptr : db->files[it->second].p;
 }
 
 // realKey of tuple ti (parseLogRecordKey, db.go:706-710); a hint record's
@@ -249,6 +245,8 @@ static int flat_get(const cly_db* db, const FlatIndex& xi, uint32_t kind, const 
     return CLY_DB_NOT_FOUND;
 }
 
+static int g_h2d_mode = 0, g_overlap = 0;
+static void load_switches();
 static int map_file(const char* path, Mapped& m, bool& exists) {
     m.p = nullptr; m.len = 0;
     exists = false;
@@ -262,7 +260,8 @@ static int map_file(const char* path, Mapped& m, bool& exists) {
         void* p = mmap(nullptr, m.len, PROT_READ, MAP_PRIVATE, fd, 0);     // for the host's key reads
         if (p == MAP_FAILED) { close(fd); m.len = 0; return CLY_ERR_ARG; }
         m.p = (const uint8_t*)p;
-        m.fd = fd;
+        if (g_h2d_mode == 1) m.fd = fd;
+        else close(fd);
         return CLY_OK;
     }
     close(fd);
@@ -272,10 +271,11 @@ static int map_file(const char* path, Mapped& m, bool& exists) {
 // the name up to its first '.', fid = strconv.Atoi(stem) (failure: "the data
 // dir maybe contaminated or damaged"), sort.Ints; the file read is
 // GetDataFileName(uint32(fid)) = "%09d.cly" (absent: read as empty; the
-// reference's OpenFile creates it empty).  A fid listed twice (say "7.cly" and
-// "000000007.cly") is read once: reading it again re-applies the same records
-// in the same order and leaves the same indexes.
-static int list_files(const char* dir, std::vector<Mapped>& out) {
+// reference's OpenFile creates it empty).  A file listed twice (say "7.cly" and
+// "000000007.cly", or "-1.cly" and "4294967295.cly": the same uint32 fid) is
+// read once, at its first place in the order: reading it again re-applies the
+// same records and leaves the same indexes.
+static int list_files(const char* dir, std::vector<Mapped>& out, std::unordered_map<uint32_t, uint32_t>& ix) {
     DIR* d = opendir(dir);
     if (!d) return CLY_ERR_ARG;
     struct dirent* e;
@@ -296,11 +296,13 @@ static int list_files(const char* dir, std::vector<Mapped>& out) {
     for (int64_t f : fids) {
         char path[4096];
         const uint32_t fid = (uint32_t)f;
+        if (ix.count(fid)) continue;
         snprintf(path, sizeof(path), "%s/%09u.cly", dir, fid);
         Mapped m;
         bool exists;
         if (map_file(path, m, exists) != CLY_OK) return CLY_ERR_ARG;
         m.fid = fid;
+        ix[fid] = (uint32_t)out.size();
         out.push_back(m);
     }
     return CLY_OK;
@@ -430,12 +432,14 @@ static int stage_ready() {
 // registered and copied by DMA directly; CLY_LOAD_OVERLAP: 1 the tuples'
 // read-back beside the table build).  Measured on C2 (tools/exp_load.py): H2D
 // 86-90 ms (0), 92-97 (1), 156-163 (2); wall 216-232 ms with the overlap.
-static int g_h2d_mode = 0, g_overlap = 0;
-static void load_switches() {
-    const char* a = getenv("CLY_H2D_MODE");
-    const char* b = getenv("CLY_LOAD_OVERLAP");
-    g_h2d_mode = a ? atoi(a) : 0;
-    g_overlap = b ? atoi(b) : 1;
+static void load_switches() {            // read once per process (opens may run concurrently)
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const char* a = getenv("CLY_H2D_MODE");
+        const char* b = getenv("CLY_LOAD_OVERLAP");
+        g_h2d_mode = a ? atoi(a) : 0;
+        g_overlap = b ? atoi(b) : 1;
+    });
 }
 static int copy_to_device(int dev, const std::vector<cly_file>& hf, const int* fds, std::vector<cly_file>& df,
                           uint8_t* d_bytes, int t0, int nt) {
@@ -658,17 +662,21 @@ static void shard_free(LoadShard& S) {
 extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir, const cly_db_options* opt,
                                  cly_db** out, cly_load_stats* st) {
     if (!ctxs || nctx < 1 || nctx > LOAD_THREADS_MAX || !dir || !out) return CLY_ERR_ARG;
-    for (int k = 0; k < nctx; k++) if (!ctxs[k]) return CLY_ERR_ARG;
+    for (int k = 0; k < nctx; k++) {
+        if (!ctxs[k]) return CLY_ERR_ARG;
+        for (int q = 0; q < k; q++) if (ctxs[q] == ctxs[k]) return CLY_ERR_ARG;   // one scan per context at a time
+    }
     *out = nullptr;
     cly_ctx* ctx = ctxs[0];                      // the index is rebuilt on the first context
     load_switches();
     cly_load_stats s;
     memset(&s, 0, sizeof(s));
-    const uint64_t dfs = opt && opt->data_file_size ? opt->data_file_size : (256ull << 20);
+    uint64_t dfs = opt && opt->data_file_size ? opt->data_file_size : (256ull << 20);
+    if (dfs < 64) dfs = 64;                      // checkOptions (db.go:433-438)
     const bool apply = opt && (opt->flags & CLY_DB_APPLY_SWEEP);
     const double t0 = now_ms();
     cly_db* db = new cly_db();
-    int rc = list_files(dir, db->files);
+    int rc = list_files(dir, db->files, db->fid_ix);
     const int nf = (int)db->files.size();
     const int dev0 = cly_ctx_device_internal(ctx);
     bool has_hint = false;
@@ -691,10 +699,6 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
         char path[4096];
         snprintf(path, sizeof(path), "%s/hint-index", dir);
         if (map_file(path, db->hint, has_hint) != CLY_OK) { rc = CLY_ERR_ARG; goto done; }
-    }
-    if (nf) {
-        rc = check_merge_finished(dir);          // (loadIndex returns early without data files)
-        if (rc != CLY_OK) goto done;
     }
     t1 = now_ms();
     s.list_map_ms = t1 - t0;
@@ -782,8 +786,10 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
             off += S.need;
         }
     }
-    for (int i = 0; i < nall; i++)
-        if (res[i].status < 0) { rc = res[i].status; goto done; }         // loadIndexFromHintFile / loadIndex return it
+    // the errors in the reference's order: loadIndexFromHintFile first (its
+    // loop: ReadLogRecord, then DecodeLogRecordPos of that record; merge.go:
+    // 270-285), then loadIndex's merge-finished check (db.go:492-499), then
+    // the data files in fid order
     if (has_hint) {
         db->n_hint = res[0].n_records;
         s.hint_records = db->n_hint;
@@ -796,7 +802,14 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
                                db->n_hint);
             DCK(hipGetLastError());
         }
+        if (res[0].status < 0) { rc = res[0].status; goto done; }
     }
+    if (nf) {
+        rc = check_merge_finished(dir);          // (loadIndex returns early without data files)
+        if (rc != CLY_OK) goto done;
+    }
+    for (int i = has_hint ? 1 : 0; i < nall; i++)
+        if (res[i].status < 0) { rc = res[i].status; goto done; }         // loadIndex returns it
     if (nf) {
         s.active_fid_loaded = db->files[nf - 1].fid;
         s.write_off_loaded = res[nall - 1].end_offset;                    // db.go:632-634
@@ -884,6 +897,14 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
         for (uint64_t i = db->n_hint; i < need; i++)
             if (ST_STATE(db->state[i]) == CLY_IX_EXPIRED) db->expired.push_back(i);
         s.n_expired = db->expired.size();
+        // db.Del refuses an empty key (db.go:186-188) and loadIndex returns
+        // that error (db.go:646-649): the open fails (the reference may have
+        // appended other keys' tombstones first, in Go map order; none here)
+        for (uint64_t i : db->expired) {
+            uint64_t kl;
+            real_key_ptr(db, i, kl);
+            if (kl == 0) { rc = CLY_ERR_KEY_EMPTY; goto done; }
+        }
         uint32_t afid = s.active_fid_loaded;
         int64_t woff = s.write_off_loaded;
         int fd = -1;

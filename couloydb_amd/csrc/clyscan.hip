@@ -17,24 +17,31 @@
 //   k_scan   per tile, ONE read of its bytes: each block arrives by four
 //            coalesced 1-KiB loads (transposed over the lane quarters); the
 //            lanes find the record starts of their segments (SWAR candidate
-//            filter, header gathers that hit L2 because the wave has just
-//            loaded those lines, an in-wave agreement pass), XOR each record's
-//            CRC patch into their words in registers and run the words through
-//            a slicing-by-4 CRC register; a 16-B compact entry per record and
-//            the tile's chain summary (LOCAL) and CRC register go out.  The
-//            first tile of a file starts at offset 0; any other tile guesses
-//            its entry (its first plausible record start);
+//            filter, header gathers from the wave's LDS copy of the block, an
+//            in-wave agreement pass), XOR each record's CRC patch into the
+//            copy, and run their 64-B segments through a slicing-by-4 CRC
+//            register from zero.  Out go: a 16-B compact entry per record, the
+//            segment registers (4 B per 64 B), and per record the register of
+//            its segment before the word that holds its patch (its snapshot),
+//            plus the tile's chain summary (LOCAL).  The first tile of a file
+//            starts at offset 0; any other tile guesses its entry;
 //   k_link   per file: the chain state entering every tile from the LOCALs;
 //            tiles whose guess the state contradicts are listed;
 //   k_refix  (only for listed tiles) re-runs the tile body from the true entry,
 //            then k_link again;
 //   k_emit   per tile: the 48-B tuples from the compact entries (tiles with
 //            more records than the compact list holds re-run the body and
-//            write tuples directly); the tile register gets the one patch
-//            term that needed the state entering it;
-//   k_fin    per file: folds the tile registers up to the terminal's tile and
-//            checks that the fold is zero (every record's CRC matches);
-//   k_locate (only when a file fails) checks the records' CRCs one by one.
+//            write tuples directly); a scan of the segment registers gives
+//            the stream register at every segment start, from which every
+//            record that ends inside the tile is checked against its own
+//            stored CRC (data/dataFile.go:105-109);
+//   k_fin    per file: a segmented scan of the tiles' exit registers gives the
+//            register entering every tile; the record that crosses into a
+//            tile is checked there;
+//   k_ovf    (only for tiles whose compact list overflowed) checks those
+//            tiles' records one by one.
+// Every record is checked on its own, so a file fails exactly at the first
+// record whose CRC differs, as ReadLogRecord's loop does.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -78,16 +85,15 @@ struct DevFile {                 // 32 B
     uint32_t _pad;
 };
 
-struct FileInfo {                // per file, zeroed per call (fail_key: all ones after k_fin)
+struct FileInfo {                // per file, zeroed per call (fail_key: all ones)
     uint64_t first_index;        // global tuple index of the file's first record
     uint64_t end_index;          // global index after the file's last record
     uint32_t term_pos;           // terminal position T of the file's chain
     int32_t  term_status;
     uint32_t term_tile;          // global tile index holding T
     uint32_t has_term;
-    u64      fail_key;           // (offset << 32) | index in file of the first CRC failure (k_locate)
-    uint32_t fold;               // k_fin: the folded register
-    uint32_t ok;                 // k_fin: fold == 0
+    u64      fail_key;           // (offset << 32) | index in file of the first record whose CRC fails (atomicMin)
+    uint32_t _r0, _r1;
 };
 
 // Tile LOCAL (the tile's chain under its own entry), written by k_scan / k_refix:
@@ -112,31 +118,34 @@ struct Globals {                 // zeroed per call
     uint32_t fail;               // internal invariant (never expected)
     uint32_t refix;              // tiles re-resolved over all rounds
     uint32_t rounds;             // link rounds
-    uint32_t any_fail;           // a file's CRC fold failed (k_locate needed)
+    uint32_t n_ovf;              // tiles listed by k_emit for k_ovf (compact list overflowed)
     uint64_t total;              // records over all files
 };
 
 // ---------------------------------------------------------------------------
 // Nibble tables (the context's d_tabs, built on the host): 128 words each,
 // entry n*16 + v = M (v << 4n) for a matrix M = A^bytes.
-//   TAB_SCAN: A^(64 2^k), k < 6 (the lane fold), A^(CLY_BLK - 64) (the block step)
 //   TAB_SH:   A^(v 16^d), v < 16, d < 4 (one hex digit of a byte shift), A^65536
 //   TAB_TILE: A^CLY_TILE (k_fin)
-#define NIB_SCAN 7
+//   TAB_EM:   k_emit's: A^(4k), k = 1..16 (a shift inside a segment; k = 16 is
+//             the segment step A^64), A^1..A^3, and A^(RUN_BYTES 2^l), l < 6
+//             (the lanes' runs of segments)
 #define NIB_SH 65
-#define TAB_SCAN 0
-#define TAB_SH (NIB_SCAN * 128)
-#define TAB_TILE (TAB_SH + NIB_SH * 128)
-#define NTAB_ALL (TAB_TILE + 128)
-// LDS of k_scan / k_refix / k_locate (static: compile-time offsets)
+#define TAB_SH 0
+#define TAB_TILE (NIB_SH * 128)
+#define TAB_EM (TAB_TILE + 128)
+#define EM_F4 0                   // A^(4k): table k - 1
+#define EM_F1 16                  // A^1, A^2, A^3: tables 16, 17, 18
+#define EM_RUN 19                 // A^(RUN_BYTES 2^l): table 19 + l
+#define NEM 25
+#define NTAB_ALL (TAB_EM + NEM * 128)
+// LDS of k_scan / k_refix / k_ovf (static: compile-time offsets)
 //   [0, 65536)  CRC slicing-by-4 tables T0..T3, 16 replicas: dword (i*64 + t*16 + r)
 //   LDS_INV     inverse of a zero-byte step (top byte of T0 -> index), 256 B
-//   LDS_NIB     the TAB_SCAN tables
 #define LDS_INV 65536
-#define LDS_NIB (LDS_INV + 256)
-#define SCAN_LDS (LDS_NIB + NIB_SCAN * 128 * 4)
+#define SCAN_LDS (LDS_INV + 256)
 
-__device__ __forceinline__ void init_tables(CLY_LDS uint8_t* smem, const uint32_t* __restrict__ nib, int ntab) {
+__device__ __forceinline__ void init_tables(CLY_LDS uint8_t* smem) {
     for (int i = threadIdx.x; i < 256; i += blockDim.x) {
         uint32_t cv = i;
         for (int k = 0; k < 8; k++) cv = (cv & 1) ? (cv >> 1) ^ CLY_POLY : cv >> 1;
@@ -148,7 +157,6 @@ __device__ __forceinline__ void init_tables(CLY_LDS uint8_t* smem, const uint32_
             cv = (cv >> 8) ^ tl;
         }
     }
-    for (int i = threadIdx.x; i < ntab; i += blockDim.x) ((CLY_LDS uint32_t*)(smem + LDS_NIB))[i] = nib[i];
     __syncthreads();
 }
 
@@ -612,35 +620,31 @@ __device__ __forceinline__ void patch_word(uint32_t (&w)[16], uint32_t k, uint32
 // CRC (not BM_EMIT): the record start P (stored CRC c, the record before it
 // stored cq) changes the file's byte stream, as the CRC register sees it, by
 // one register XOR d = c ^ K4 ^ ~cq before byte P (c zeroes the stored bytes,
-// K4 = A^-4 0xFFFFFFFF starts the record's CRC at P+4, ~cq checks the record
-// ending at P; no ~cq at P = 0); that is the XOR of A^-(P&3) d into the data
-// word at P & ~3, done in registers before the word enters the register.  At
-// the chain's terminal T: ~cq of the last record before T, and every byte from
-// T on zeroed.  The register of the whole patched file is then zero iff every
-// record's CRC matches.  The ~cq of the tile's FIRST boundary (tiles other
-// than a file's first) needs the state entering the tile: the tile XORs
-// 0xFFFFFFFF there, and k_emit adds A^(TE - G) crc_last (the rest of ~cq).
+// K4 = A^-4 0xFFFFFFFF starts the record's CRC at P+4, ~cq closes the record
+// ending at P; no ~cq at P = 0); it goes into the data as A^(4-j) d into the
+// word after P's (j = P & 3; into P's own word when j = 0): the patch word
+// W(P).  At the chain's terminal T: ~cq of the last record before T, and every
+// byte from T on zeroed.  In this patched stream the register entering W(P),
+// when every record before P matches its CRC, is a known value exp_pre(P)
+// (~cq, or A^(4-j) (~cq ^ the j-byte-shifted head of c)); so record i matches
+// iff the register entering W(P_{i+1}) is exp_pre(P_{i+1}), and the last one
+// iff the register is zero after T.  Each lane runs its 64-B segment from a
+// zero register and keeps, for every patch word in it, the register before
+// that word (the snapshot); the register of the stream at any patch word is
+// then A^(W - segment start) (the stream register entering the segment) ^ the
+// snapshot, and the stream registers entering the segments follow from the
+// segment registers alone (k_emit's scan).  The ~cq of the tile's FIRST
+// boundary (tiles other than a file's first) needs the state entering the
+// tile: the tile XORs 0xFFFFFFFF there and k_emit accounts for the difference.
 #define BM_SPEC 0
 #define BM_EXACT 1
 #define BM_EMIT 2
-#ifndef CLY_EXP
-#define CLY_EXP 0                // timing experiments only (wrong results): 1 no record work, 6 no CRC, 8 no pred_walk
-                                 // table steps, 7 neither, 3 candidate
-#endif                           // masks only, 2 no per-record outputs, 5 no agreement pass
-#ifndef CLY_PW_ROUNDS
-#define CLY_PW_ROUNDS 1          // pred_walk rounds per block before the general pass (C3: 1 round 12.7 ms, 2 13.6, 4 15.4)
-#endif
-#ifndef CLY_PROF
-#define CLY_PROF 0               // experiment builds: per-section cycle counts of k_scan's tile body
-#endif
-#if CLY_PROF
-__device__ unsigned long long g_prof[8];
-#define PT(i) do { if (BM == BM_SPEC) { const uint64_t n_ = __builtin_amdgcn_s_memtime(); pacc[i] += n_ - pt; pt = n_; } } while (0)
-#define PC(i) do { if (BM == BM_SPEC) pacc[i]++; } while (0)
-#else
-#define PT(i) do {} while (0)
-#define PC(i) do {} while (0)
-#endif
+#define PW_ROUNDS 1              // pred_walk rounds per block before the general pass (C3: 1 round 12.7 ms, 2 13.6, 4 15.4)
+// Per-tile CRC outputs of the tile body: the segment registers (one per 64-B
+// segment of the tile, stream order) and the records' snapshots (indexed like
+// the compact entries; boundary CAP_T is the last one kept)
+#define NSEG (CLY_NBLK * CLY_NL)         // segments per tile
+#define SNAP_T (CAP_T + 4)               // snapshot words per tile (CAP_T + 1 used)
 struct TileRes { uint32_t X; bool dead; };
 // The chain state a wave carries through its tile (wave-uniform).
 struct TState {
@@ -653,7 +657,8 @@ struct TState {
     uint32_t s_last, s_prev;     // sizes of the last two records (0: none yet)
     uint32_t Tb;                 // terminal position in the current block (NONE32: none)
     uint32_t tpatch;             // its patch word (XORed after the bytes from Tb on are zeroed)
-    uint32_t carry_next;         // register XOR due at the next block's first byte (terminal at the block end)
+    uint32_t carry_next;         // register XOR due at the next block's first byte (a patch word past the block)
+    bool cmark_next;             // ... and it is a record start's patch (its snapshot is the next block's word 0)
     // stride reference (stride_round): header bytes 4..15 of the last record
     // (ref1..3) under the masks of its bytes 4..hsz, and the uniform words of
     // its compact entry; valid while ref_ok
@@ -681,6 +686,12 @@ __device__ __forceinline__ uint32_t rec_out(const DevFile& F, gbytes base, uint3
     return j ? crc_fwd(smem, d, 4u - j, cl.r4) : d;
 }
 #define PW_CARRY (CLY_BLK / 4)
+// The block's patch-word mask (per wave, in LDS: bit k of word L = word k of
+// segment L holds a record start's patch), built by the lanes that place the
+// patches; the segment lanes read it to know where to keep snapshots.
+__device__ __forceinline__ void mark_pw(CLY_LDS uint32_t* mk, uint32_t pw) {
+    __atomic_fetch_or(mk + (pw >> 4), 1u << (pw & 15u), __ATOMIC_RELAXED);
+}
 // The terminal T (found by lane src): the bytes from T on read as zero, and
 // ~cq of the record before it (dT) is XORed in before byte T (into the word
 // holding T, after the zeroing), or at the next block's first byte when T is
@@ -705,10 +716,11 @@ __device__ __forceinline__ void term_patch(TState& S, uint32_t T, uint32_t dT, u
 template <int BM>
 __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t tb, uint32_t bs, CLY_LDS uint32_t* stg,
                                           const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t K4, rsrc_t trs,
-                                          gtuples out, uint64_t out_cap, uint64_t gbase, Globals* g, int lane) {
+                                          gtuples out, uint64_t out_cap, uint64_t gbase, Globals* g, int lane,
+                                          CLY_LDS uint32_t* mk) {
     const gbytes base = (gbytes)F.base;
     const uint64_t flen = F.len, bend = (uint64_t)bs + CLY_BLK;
-    for (int round = 0; round < CLY_PW_ROUNDS; round++) {
+    for (int round = 0; round < PW_ROUNDS; round++) {
         const uint64_t X = S.X;
         const bool owned = X < bend || (X == flen && flen == bend);
         if (S.dead || !owned) return true;
@@ -738,11 +750,11 @@ __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t 
         if (acc) {
             pv = rec_out<BM>(F, base, (uint32_t)P, h, S.tcnt + k, tb, bs, P == 0 ? 0u : dq, smem, cl, K4, trs, out,
                              out_cap, gbase, g, pw);
-            if (BM != BM_EMIT && pw < PW_CARRY) stg[stg_dw(pw)] ^= pv;
+            if (BM != BM_EMIT && pw < PW_CARRY) { stg[stg_dw(pw)] ^= pv; mark_pw(mk, pw); }
         }
         if (BM != BM_EMIT) {
             const u64 bc = __ballot(acc && pw == PW_CARRY);
-            if (bc) S.carry_next ^= rdl(pv, __ffsll((long long)bc) - 1);
+            if (bc) { S.carry_next ^= rdl(pv, __ffsll((long long)bc) - 1); S.cmark_next = true; }
         }
         if (S.G == NONE32) S.G = (uint32_t)X;
         if (n) {
@@ -782,7 +794,7 @@ __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t 
 template <int BM>
 __device__ __forceinline__ void stride_round(const DevFile& F, TState& S, uint32_t tb, uint32_t bs,
                                              CLY_LDS uint32_t* stg, const CLY_LDS uint8_t* smem, const CrcLane& cl,
-                                             uint32_t K4, rsrc_t trs, int lane) {
+                                             uint32_t K4, rsrc_t trs, int lane, CLY_LDS uint32_t* mk) {
     const uint32_t X = S.X, s = S.ref_s, k = (uint32_t)lane;
     const uint64_t bend = (uint64_t)bs + CLY_BLK;
     if (S.dead || (uint64_t)X >= bend) return;
@@ -806,10 +818,10 @@ __device__ __forceinline__ void stride_round(const DevFile& F, TState& S, uint32
         const uint32_t d = crc ^ K4 ^ dq, j = P & 3u;
         pw = ((P - bs) >> 2) + (j ? 1u : 0u);
         pv = j ? crc_fwd(smem, d, 4u - j, cl.r4) : d;
-        if (pw < PW_CARRY) stg[stg_dw(pw)] ^= pv;
+        if (pw < PW_CARRY) { stg[stg_dw(pw)] ^= pv; mark_pw(mk, pw); }
     }
     const u64 bc = __ballot(k < kb && pw == PW_CARRY);
-    if (bc) S.carry_next ^= rdl(pv, __ffsll((long long)bc) - 1);
+    if (bc) { S.carry_next ^= rdl(pv, __ffsll((long long)bc) - 1); S.cmark_next = true; }
     if (S.G == NONE32) S.G = X;
     S.last_crc = rdl(crc, (int)kb - 1);
     S.P_last = X + (kb - 1) * s;
@@ -938,8 +950,9 @@ __device__ __forceinline__ uint32_t guess_entry(const DevFile& F, uint32_t bs, C
 
 template <int BM>
 __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint32_t tt, uint32_t X_in, bool dead_in,
-                                             const CLY_LDS uint8_t* smem, CLY_LDS uint32_t* stg, const CrcLane& cl,
-                                             uint32_t K4, TileLocal* loc, uint32_t* rec, uint32_t* treg, gtuples out,
+                                             const CLY_LDS uint8_t* smem, CLY_LDS uint32_t* stg, CLY_LDS uint32_t* mk,
+                                             const CrcLane& cl, uint32_t K4, TileLocal* loc, uint32_t* rec,
+                                             uint32_t* seg, uint32_t* snap, uint32_t* treg, gtuples out,
                                              uint64_t out_cap, uint64_t gbase, Globals* g) {
     const int lane = threadIdx.x & 63;
     const uint32_t tb = (uint32_t)((uint64_t)tt * CLY_TILE);
@@ -951,17 +964,17 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     S.dead = tt != 0 && known0 && dead_in;
     S.cq_known = tt == 0;        // tile 0: no record before offset 0
     S.cq = 0; S.G = NONE32; S.tcnt = 0; S.last_crc = 0; S.P_last = NONE32; S.term = TERM_NONE;
-    S.s_last = 0; S.s_prev = 0; S.Tb = NONE32; S.tpatch = 0; S.carry_next = 0;
+    S.s_last = 0; S.s_prev = 0; S.Tb = NONE32; S.tpatch = 0; S.carry_next = 0; S.cmark_next = false;
     S.ref_ok = false; S.ref_s = 0; S.ref1 = S.ref2 = S.ref3 = S.msk1 = S.msk2 = S.msk3 = S.rw1 = S.rw2 = S.rw3 = 0;
-    uint32_t R = 0, carry = 0;   // carry: register XOR due at this block's first byte
-    const CLY_LDS uint32_t* nibt = (const CLY_LDS uint32_t*)(smem + LDS_NIB);
+    uint32_t carry = 0;          // register XOR due at this block's first byte
+    bool cmark = false;          // ... a record start's patch (marked as word 0 of the block)
+    uint32_t nb = 0;             // snapshots taken so far (= records whose patch word was passed)
     const rsrc_t trs = mk_rsrc(rec + (uint64_t)t * CAP_T * 4, CAP_T * 16u);      // the tile's compact entries
     const rsrc_t frs = mk_rsrc(F.base, (uint32_t)flen);
+    const rsrc_t srs = mk_rsrc(seg + (uint64_t)t * NSEG, BM == BM_EMIT ? 0u : NSEG * 4u);            // segment registers
+    const rsrc_t nrs = mk_rsrc(snap + (uint64_t)t * SNAP_T, BM == BM_EMIT ? 0u : (CAP_T + 1) * 4u);  // snapshots
     CLY_LDS u32x4* sv = (CLY_LDS u32x4*)stg;
     u32x4 e[4], hl;
-#if CLY_PROF
-    uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = __builtin_amdgcn_s_memtime();
-#endif
     blk_issue(base, frs, flen, tb, lane, e, hl);
     #pragma unroll 1
     for (int m = 0; m < CLY_NBLK; m++) {
@@ -971,16 +984,16 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
         uint32_t w[16];
         #pragma unroll
         for (int k = 0; k < 4; k++) { w[4 * k] = e[k].x; w[4 * k + 1] = e[k].y; w[4 * k + 2] = e[k].z; w[4 * k + 3] = e[k].w; }
-        PT(0);
         const u32x4 hc = hl;
         if (m + 1 < CLY_NBLK && (BM != BM_EMIT || !S.dead)) blk_issue(base, frs, flen, bs + CLY_BLK, lane, e, hl);
         if (BM == BM_EMIT && S.dead) break;
+        if (BM != BM_EMIT) mk[lane] = (lane == 0 && cmark) ? 1u : 0u;       // the block's patch words (carried: word 0)
         S.Tb = NONE32;
         const bool owned = S.X != NONE32 && ((uint64_t)S.X < bend || ((uint64_t)S.X == flen && flen == bend));
         if (S.dead) {
             #pragma unroll
             for (int k = 0; k < 16; k++) w[k] = 0;
-        } else if (CLY_EXP != 1 && CLY_EXP != 7 && (S.X == NONE32 || owned)) {
+        } else if (S.X == NONE32 || owned) {
             // ---- record starts of the block; headers are read from the wave's
             // LDS copy of it (the stage), patches XORed into the stage
             {
@@ -999,18 +1012,15 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (S.X == NONE32) { S.X = guess_entry(F, bs, stg, hc, lane); PC(6); }    // the tile's guessed entry
-            PT(1);
+            if (S.X == NONE32) S.X = guess_entry(F, bs, stg, hc, lane);    // the tile's guessed entry
             bool done = true;
-            if (S.X != NONE32 && CLY_EXP != 8) {
-                if (BM != BM_EMIT && S.ref_ok) stride_round<BM>(F, S, tb, bs, stg, smem, cl, K4, trs, lane);
+            if (S.X != NONE32) {
+                if (BM != BM_EMIT && S.ref_ok) stride_round<BM>(F, S, tb, bs, stg, smem, cl, K4, trs, lane, mk);
                 const uint32_t c0 = S.tcnt;
-                done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, trs, out, out_cap, gbase, g, lane);
+                done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, trs, out, out_cap, gbase, g, lane, mk);
                 if (BM != BM_EMIT && S.tcnt != c0) stride_ref(F, S, bs, stg);
             }
-            PT(2);
             if (!done) {
-                PC(7);
                 // ---- general pass (the predictive walk's round budget ran out):
                 // every lane's first candidate record start in its 64-B segment
                 // after X, then agreement
@@ -1038,7 +1048,7 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                     if (cm) { SegChain T; if (seg_walk(K, K.cb + (uint32_t)__builtin_ctzll(cm), false, T)) L = T; }
                 }
                 {
-                    if (CLY_EXP != 5) L = seg_resolve(K, L, lane, X, g);
+                    L = seg_resolve(K, L, lane, X, g);
                     // the first terminal ends the chain: the lanes after it are dead
                     const u64 bt = __ballot(L.mode == LM_CHAIN && L.term != TERM_NONE);
                     const int kT = bt ? __ffsll((long long)bt) - 1 : 64;
@@ -1058,25 +1068,26 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                     // lane before reads its last header, whose tail shares that word,
                     // in a later iteration)
                     uint32_t p = L.E, psz = 0, ppsz = 0, p0w = PW_CARRY + 1, p0v = 0, cv = 0;
-                    for (uint32_t i = 0; CLY_EXP != 2 && __ballot(i < c); i++) {
+                    bool cf = false;
+                    for (uint32_t i = 0; __ballot(i < c); i++) {
                         if (i < c) {
                             const Hdr h = hdr_get(p, flen, stg, bs);
                             uint32_t pw;
                             const uint32_t pv = rec_out<BM>(F, base, p, h, S.tcnt + lex + i, tb, bs,
                                                             p == 0 ? 0u : (pk ? ~pcq : 0xFFFFFFFFu), smem, cl, K4, trs,
                                                             out, out_cap, gbase, g, pw);
-                            if (pw == PW_CARRY) cv = pv;
+                            if (pw == PW_CARRY) { cv = pv; cf = true; }
                             else if (i == 0) { p0w = pw; p0v = pv; }
-                            else if (BM != BM_EMIT) stg[stg_dw(pw)] ^= pv;
+                            else if (BM != BM_EMIT) { stg[stg_dw(pw)] ^= pv; mark_pw(mk, pw); }
                             pcq = h.crc; pk = true;
                             ppsz = psz; psz = (uint32_t)h.size;
                             p += (uint32_t)h.size;
                         }
                     }
                     if (BM != BM_EMIT) {
-                        if (p0w < PW_CARRY) stg[stg_dw(p0w)] ^= p0v;
-                        const u64 bc = __ballot(cv != 0);
-                        if (bc) S.carry_next ^= rdl(cv, __ffsll((long long)bc) - 1);
+                        if (p0w < PW_CARRY) { stg[stg_dw(p0w)] ^= p0v; mark_pw(mk, p0w); }
+                        const u64 bc = __ballot(cf);
+                        if (bc) { S.carry_next ^= rdl(cv, __ffsll((long long)bc) - 1); S.cmark_next = true; }
                     }
                     if (kT < 64) {
                         const uint32_t T = rdl(L.x, kT);
@@ -1104,7 +1115,6 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                     }
                 }
             }
-            PT(3);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             if (BM != BM_EMIT) {
@@ -1131,47 +1141,60 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                 }
             }
             if (lane == 0) w[0] ^= carry;
-            carry = S.carry_next;
-            S.carry_next = 0;
-            if (m) R = mat_mul(nibt + 6 * 128, R);
+            // the segment's register from zero; w[k] becomes the register entering word k
+            uint32_t R = 0;
             #pragma unroll
-            for (int k = 0; k < 16; k++) R = (CLY_EXP == 6 || CLY_EXP == 7) ? R ^ w[k] : crc_word(smem, R ^ w[k], cl);
+            for (int k = 0; k < 16; k++) { const uint32_t x = R; R = crc_word(smem, R ^ w[k], cl); w[k] = x; }
+            __builtin_amdgcn_raw_buffer_store_b32(R, srs, (int)(((uint32_t)m * CLY_NL + (uint32_t)lane) * 4u), 0, 0);
+            // snapshots: the registers entering the marked words, in position
+            // order = record order (one patch word per record start), through
+            // the stage (the block's bytes there are no longer needed)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t mm = mk[lane];
+            if (__ballot(mm != 0u)) {
+                #pragma unroll
+                for (int k = 0; k < 4; k++) sv[5 * lane + k] = (u32x4){w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint32_t c = (uint32_t)__builtin_popcount(mm), incl = wave_add_incl(c);
+                uint32_t r = nb + incl - c, q = mm;
+                nb += rdl(incl, 63);
+                while (__ballot(q != 0u)) {
+                    if (q) {
+                        const uint32_t k = (uint32_t)__builtin_ctz(q);
+                        q &= q - 1u;
+                        __builtin_amdgcn_raw_buffer_store_b32(stg[20u * (uint32_t)lane + k], nrs, (int)(r * 4u), 0, 0);
+                        r++;
+                    }
+                }
+            }
+            carry = S.carry_next; cmark = S.cmark_next;
+            S.carry_next = 0; S.cmark_next = false;
         }
-        PT(4);
     }
     TileRes res;
     res.X = S.X; res.dead = S.dead;
-    if (BM != BM_EMIT) {
-        // fold of the lanes' registers to the tile end: sum over l of A^(64 (63 - l)) R_l
-        uint32_t r = R;
-        #pragma unroll
-        for (int lvl = 0; lvl < 6; lvl++) {
-            const int d = 1 << lvl;
-            const uint32_t o = (uint32_t)__shfl_down((int)r, d, 64);
-            const uint32_t sh = mat_mul(nibt + lvl * 128, r);
-            if ((lane & (2 * d - 1)) == 0) r = sh ^ o;
-        }
-        if (lane == 0) {
-            treg[t] = r ^ carry;
-            const uint64_t tstart = tb;
-            const uint32_t tend = tstart + CLY_TILE >= flen ? (uint32_t)(flen + 1) : (uint32_t)(tstart + CLY_TILE);
-            u64 f0 = (u64)S.tcnt << 32;
-            if (S.term != TERM_NONE) f0 |= DF_TERM;
-            if (S.G == NONE32) f0 |= DF_NONE;
-            if (tt == 0) f0 |= DF_FOF;
-            if (S.P_last != NONE32) f0 |= DF_REC;
-            if (S.tcnt > CAP_T) f0 |= DF_OVF;
-            TileLocal* d = &loc[t];
-            d->l[0] = f0;
-            d->l[1] = (u64)S.G | ((u64)S.X << 32);
-            d->l[2] = (u64)S.last_crc | ((u64)S.P_last << 32);
-            d->l[3] = (u64)tend | ((u64)(uint8_t)(int8_t)S.term << 32);
-        }
-        PT(5);
-#if CLY_PROF
-        if (lane == 0)
-            for (int i = 0; i < 8; i++) atomicAdd(&g_prof[i], (unsigned long long)pacc[i]);
-#endif
+    if (BM != BM_EMIT && lane == 0) {
+        // a record start whose patch word is the tile's end: its snapshot is
+        // the (empty) segment after the tile's, zero; the patch itself is the
+        // register XOR due at the tile end
+        if (cmark) __builtin_amdgcn_raw_buffer_store_b32(0u, nrs, (int)(nb * 4u), 0, 0);
+        treg[2 * t] = carry;
+        if (nb + (cmark ? 1u : 0u) != S.tcnt) atomicOr(&g->fail, 64u);      // one snapshot per record
+        const uint64_t tstart = tb;
+        const uint32_t tend = tstart + CLY_TILE >= flen ? (uint32_t)(flen + 1) : (uint32_t)(tstart + CLY_TILE);
+        u64 f0 = (u64)S.tcnt << 32;
+        if (S.term != TERM_NONE) f0 |= DF_TERM;
+        if (S.G == NONE32) f0 |= DF_NONE;
+        if (tt == 0) f0 |= DF_FOF;
+        if (S.P_last != NONE32) f0 |= DF_REC;
+        if (S.tcnt > CAP_T) f0 |= DF_OVF;
+        TileLocal* d = &loc[t];
+        d->l[0] = f0;
+        d->l[1] = (u64)S.G | ((u64)S.X << 32);
+        d->l[2] = (u64)S.last_crc | ((u64)S.P_last << 32);
+        d->l[3] = (u64)tend | ((u64)(uint8_t)(int8_t)S.term << 32);
     }
     return res;
 }
@@ -1198,21 +1221,30 @@ __device__ __forceinline__ uint32_t k4_const(const CLY_LDS uint8_t* smem, uint32
 
 // k_scan: one wave per tile (grid-stride), every byte of every file read once.
 #define SCAN_WAVES 16
-#define SCAN_LDS_ALL (SCAN_LDS + SCAN_WAVES * STG_BYTES)     // tables + one block stage per wave
+#define MK_BYTES (CLY_NL * 4)                                 // a wave's patch-word mask
+#define SCAN_LDS_ALL (SCAN_LDS + SCAN_WAVES * (STG_BYTES + MK_BYTES))   // tables + per wave a block stage and a mask
+__device__ __forceinline__ CLY_LDS uint32_t* wave_stage(CLY_LDS uint8_t* smem) {
+    return (CLY_LDS uint32_t*)(smem + SCAN_LDS + wave_id() * STG_BYTES);
+}
+__device__ __forceinline__ CLY_LDS uint32_t* wave_mask(CLY_LDS uint8_t* smem) {
+    return (CLY_LDS uint32_t*)(smem + SCAN_LDS + SCAN_WAVES * STG_BYTES + wave_id() * MK_BYTES);
+}
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
 k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
-       TileLocal* loc, uint32_t* rec, uint32_t* treg, const uint32_t* __restrict__ tabs, Globals* g) {
+       TileLocal* loc, uint32_t* rec, uint32_t* seg, uint32_t* snap, uint32_t* treg, Globals* g) {
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS_ALL];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
-    init_tables(smem, tabs + TAB_SCAN, NIB_SCAN * 128);
-    CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)(smem + SCAN_LDS + wave_id() * STG_BYTES);
+    init_tables(smem);
+    CLY_LDS uint32_t* stg = wave_stage(smem);
+    CLY_LDS uint32_t* mk = wave_mask(smem);
     const int lane = threadIdx.x & 63;
     const CrcLane cl = crc_lane(lane);
     const uint32_t K4 = k4_const(smem, cl.r4);
     for (uint32_t t = blockIdx.x * SCAN_WAVES + wave_id(); t < ntiles; t += gridDim.x * SCAN_WAVES) {
         const int f = find_file(tprefix, nfiles, t);
         const DevFile F = files[f];
-        tile_body<BM_SPEC>(F, t, t - F.first_tile, 0u, false, smem, stg, cl, K4, loc, rec, treg, nullptr, 0, 0, g);
+        tile_body<BM_SPEC>(F, t, t - F.first_tile, 0u, false, smem, stg, mk, cl, K4, loc, rec, seg, snap, treg, nullptr,
+                           0, 0, g);
     }
 }
 
@@ -1394,13 +1426,14 @@ k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restric
 // (and is not listed itself).
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
 k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, TileLocal* loc,
-        const TileIn* __restrict__ tin, uint32_t* rec, uint32_t* treg, const uint32_t* __restrict__ tabs,
+        const TileIn* __restrict__ tin, uint32_t* rec, uint32_t* seg, uint32_t* snap, uint32_t* treg,
         const uint32_t* __restrict__ fixlist, Globals* g, int slot) {
     if (g->nfix[slot] == 0) return;                        // (uniform: before the LDS setup's barrier)
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS_ALL];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
-    init_tables(smem, tabs + TAB_SCAN, NIB_SCAN * 128);
-    CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)(smem + SCAN_LDS + wave_id() * STG_BYTES);
+    init_tables(smem);
+    CLY_LDS uint32_t* stg = wave_stage(smem);
+    CLY_LDS uint32_t* mk = wave_mask(smem);
     const uint32_t k = blockIdx.x * SCAN_WAVES + wave_id();
     if (k >= g->nfix[slot]) return;
     const int lane = threadIdx.x & 63;
@@ -1420,8 +1453,8 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
         const uint32_t n = (uint32_t)(l0 >> 32), tb = (t - F.first_tile) * (uint32_t)CLY_TILE;
         if (!S.dead && !(l0 & (DF_NONE | DF_FOF | DF_OVF)) && n > 1 && ((loc[t].l[3] >> 40) & 0xFFFFu) == 0) {
             const uint32_t nn = n < 64u ? n : 64u;
-            const uint32_t rel = (uint32_t)lane < nn ? (rec[((uint64_t)t * CAP_T + lane) * 4 + 3] & 0xFFFFu) : 0xFFFFFu;
-            const u64 bm = __ballot(lane >= 1 && tb + rel == S.X);
+            const uint32_t rel = (uint32_t)lane < nn ? (rec[((uint64_t)t * CAP_T + lane) * 4 + 3] & 0xFFFFu) : 0u;
+            const u64 bm = __ballot(lane >= 1 && (uint32_t)lane < nn && tb + rel == S.X);
             if (bm) {
                 const uint32_t j = (uint32_t)__ffsll((long long)bm) - 1;
                 if (lane == 0) {
@@ -1434,8 +1467,8 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
         }
     }
     for (;;) {
-        const TileRes r = tile_body<BM_EXACT>(F, t, t - F.first_tile, S.X, S.dead != 0, smem, stg, cl, K4, loc, rec,
-                                              treg, nullptr, 0, 0, g);
+        const TileRes r = tile_body<BM_EXACT>(F, t, t - F.first_tile, S.X, S.dead != 0, smem, stg, mk, cl, K4, loc, rec,
+                                              seg, snap, treg, nullptr, 0, 0, g);
         S.X = r.X; S.dead = r.dead;
         if (S.dead || t + 1 >= F.first_tile + F.ntile) break;
         // the next tile: consistent with the new exit?  else it is re-resolved too
@@ -1450,29 +1483,75 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
 
 // k_emit: per tile (one wave, grid-stride), after the chain is final: the
 // tuples from the compact entries (64 per round: coalesced 16-B reads, the 48-B
-// tuples assembled in the wave's LDS stage and written as whole 1-KiB runs),
-// the first-boundary patch term, and the file's terminal.
+// tuples assembled in the wave's LDS and written as whole 1-KiB runs), and the
+// tile's CRC verdicts.
+//   The scan: lane L owns the run of RUN consecutive segments at L RUN_BYTES;
+//   a Horner pass over their registers gives the run as a function of the
+//   register entering it (x -> A^RUN_BYTES x ^ v, or a constant when the run
+//   holds the reset below), a Kogge-Stone scan over the lanes composes the
+//   runs, and a second Horner pass gives the register entering every segment
+//   (gin, LDS).  The stream is reset at the tile's first boundary G: past G's
+//   patch word the register is what it is when the record ending at G matches
+//   its CRC (k_fin checks that record: it knows the register entering the
+//   tile); so no state from earlier tiles is needed here.
+//   Record r of the tile ends at the patch word W of record r + 1; the register
+//   entering W is A^(W - segment start) gin ^ the snapshot, and must equal
+//   exp_pre (data/dataFile.go:105-109: the record's own CRC).  The record that
+//   ends at the chain's terminal matches iff the register at the tile's end is
+//   zero (every byte from the terminal on is zero, and its patch closes the
+//   record).  Outputs per tile for k_fin: the register at the tile's end (a
+//   tile with a boundary: under the reset; a tile without one: its own, from
+//   zero) and the straddling record's check value (dev).
+#define RUN (CLY_NBLK)                          // segments per lane in k_emit's scan
+#define RUN_BYTES (RUN * CLY_SEG)
 #define EMIT_WAVES 16
-#define EMIT_LDS (NIB_SH * 128 * 4 + EMIT_WAVES * STG_BYTES)
+#define GIN_WORDS (NSEG + 4)                    // the register entering each segment (+ the tile's end)
+#define TUP_BYTES (64 * 48)                     // a round's tuples
+#define EW_RAW (GIN_WORDS * 4 + TUP_BYTES > STG_BYTES ? GIN_WORDS * 4 + TUP_BYTES : STG_BYTES)
+#define EW_BYTES ((EW_RAW + 15) & ~15)
+#define EMIT_LDS (NEM * 128 * 4 + EMIT_WAVES * EW_BYTES)
+static_assert(CLY_NL * RUN == NSEG, "one run of segments per lane");
+__device__ __forceinline__ uint32_t gin_at(uint32_t sg) {      // LDS word of segment sg's entering register
+    return sg < NSEG ? (sg % RUN) * 64u + sg / RUN : NSEG;
+}
+// A^(4k) v, 0 <= k <= 16 (k = 16: the segment step A^64)
+__device__ __forceinline__ uint32_t em_f4(const CLY_LDS uint32_t* emt, uint32_t k, uint32_t v) {
+    return k ? mat_mul(emt + (EM_F4 + k - 1u) * 128u, v) : v;
+}
+// A^(4-j) v, 1 <= j <= 3
+__device__ __forceinline__ uint32_t em_fj(const CLY_LDS uint32_t* emt, uint32_t j, uint32_t v) {
+    return mat_mul(emt + (EM_F1 + 3u - j) * 128u, v);
+}
+// The register entering the patch word of a record start P (j = P & 3) when
+// the record before it (stored CRC cq) matches: ~cq at P, then for j != 0 the
+// 4 - j first bytes of the new record's stored CRC c in the same word.
+__device__ __forceinline__ uint32_t exp_pre(const CLY_LDS uint32_t* emt, uint32_t j, uint32_t cq, uint32_t c) {
+    return j ? em_fj(emt, j, ~cq ^ (c & ((1u << (8u * (4u - j))) - 1u))) : ~cq;
+}
+__device__ __forceinline__ uint32_t entry_crc(gbytes base, uint64_t len, uint32_t tb, const u32x4& v) {
+    return (v.w & REC_SHORT) ? v.x : hdr_load(base, tb + (v.w & 0xFFFFu), len).crc;
+}
 __global__ void __launch_bounds__(64 * EMIT_WAVES)
 k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
        const TileIn* __restrict__ tin, const TileLocal* __restrict__ loc, const uint32_t* __restrict__ rec,
-       uint32_t* treg, FileInfo* finfo, const uint32_t* __restrict__ tabs, cly_tuple* out_, uint64_t out_cap,
-       Globals* g, int slot) {
+       const uint32_t* __restrict__ seg, const uint32_t* __restrict__ snap, uint32_t* treg, FileInfo* finfo,
+       const uint32_t* __restrict__ tabs, cly_tuple* out_, uint64_t out_cap, u32x4* ovf, Globals* g, int slot) {
     if (g->nfix[slot]) return;              // the chain is not final yet (k_refix first)
     gtuples out = (gtuples)out_;
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[EMIT_LDS];
-    CLY_LDS uint32_t* sht = (CLY_LDS uint32_t*)smem_raw;
-    for (int i = threadIdx.x; i < NIB_SH * 128; i += blockDim.x) sht[i] = tabs[TAB_SH + i];
+    CLY_LDS uint32_t* emt = (CLY_LDS uint32_t*)smem_raw;
+    for (int i = threadIdx.x; i < NEM * 128; i += blockDim.x) emt[i] = tabs[TAB_EM + i];
     __syncthreads();
-    CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)(smem_raw + NIB_SH * 128 * 4 + wave_id() * STG_BYTES);
-    CLY_LDS u32x4* sv = (CLY_LDS u32x4*)stg;
+    CLY_LDS uint8_t* wreg = (CLY_LDS uint8_t*)smem_raw + NEM * 128 * 4 + wave_id() * EW_BYTES;
+    CLY_LDS uint32_t* gin = (CLY_LDS uint32_t*)wreg;                  // the scan (tiles with compact entries)
+    CLY_LDS u32x4* sv = (CLY_LDS u32x4*)(wreg + GIN_WORDS * 4);       // a round's tuples
+    CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)wreg;                  // the re-walk's stage (overflowed tiles)
     const int lane = threadIdx.x & 63;
     const CrcLane cl = crc_lane(lane);
     for (uint32_t t = blockIdx.x * EMIT_WAVES + wave_id(); t < ntiles; t += gridDim.x * EMIT_WAVES) {
         const int f = find_file(tprefix, nfiles, t);
         const DevFile F = files[f];
-        LBState S = ti_load(&tin[t]);
+        const LBState S = ti_load(&tin[t]);
         if (S.dead) continue;
         FileInfo* fo = &finfo[f];
         const uint64_t gb = S.count + fo->first_index;
@@ -1481,8 +1560,84 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         const uint32_t n = (uint32_t)(l0 >> 32);
         const uint32_t skip = (uint32_t)(l3 >> 40) & 0xFFFFu;              // k_refix's suffix (records dropped)
         const gbytes base = (gbytes)F.base;
+        const bool none = (l0 & DF_NONE) != 0, term = (l0 & DF_TERM) != 0;
+        const bool gterm = !none && term && n == 0;                         // the first boundary is the terminal
+        const bool grec = !none && !gterm;                                  // ... a record start
+        const uint32_t* trec = rec + ((uint64_t)t * CAP_T + skip) * 4;
+        const uint32_t* tsnap = snap + (uint64_t)t * SNAP_T + skip;
+        // ---- G (a record start): its patch word WG, the register entering WG
+        // when the record ending at G matches (expG), and injG: what the reset
+        // XORs in at WG relative to the tile's own stream (expG ^ the snapshot
+        // ^ the difference between the ~cq the tile applied at G and the true one)
+        const uint32_t G = (uint32_t)l1;
+        uint32_t WG = 0, sigG = NSEG + 1, expG = 0, injG = 0, DG = 0, sG = 0;
+        if (grec) {
+            const u32x4 vg = *(const u32x4*)trec;
+            const uint32_t cG = entry_crc(base, F.len, tb, vg);
+            const uint32_t jG = G & 3u;
+            WG = jG ? (G & ~3u) + 4u : G;
+            sigG = (WG - tb) >> 6;
+            sG = tsnap[0];
+            if (tt > 0) {
+                uint32_t dqa = 0xFFFFFFFFu;                                 // guess mode / k_refix: cq unknown at G
+                if (skip) dqa = ~entry_crc(base, F.len, tb, *(const u32x4*)(trec - 4));   // the dropped record before G
+                const uint32_t dd = dqa ^ ~S.crc_last;
+                DG = jG ? em_fj(emt, jG, dd) : dd;
+                expG = exp_pre(emt, jG, S.crc_last, cG);
+            }
+            injG = expG ^ sG ^ DG;
+        }
+        // ---- the scan
+        uint32_t sr[RUN];
+        {
+            const uint32_t* sp = seg + (uint64_t)t * NSEG + (uint32_t)lane * RUN;
+            #pragma unroll
+            for (int k = 0; k < RUN; k += 4) {
+                const u32x4 q = *(const u32x4*)(sp + k);
+                sr[k] = q.x; sr[k + 1] = q.y; sr[k + 2] = q.z; sr[k + 3] = q.w;
+            }
+        }
+        // the exit register of segment sigG under the reset: its register from
+        // zero, with injG XORed in before WG (= A^(segment end - WG) injG)
+        const uint32_t xG = grec && sigG < NSEG ? em_f4(emt, (64u * (sigG + 1u) - (WG - tb)) >> 2, injG) : 0u;
+        uint32_t x = 0, rc = 0;
+        #pragma unroll
+        for (int k = 0; k < RUN; k++) {
+            const uint32_t sg = (uint32_t)lane * RUN + k;
+            if (sg == sigG) { x = sr[k] ^ xG; rc = 1; }
+            else x = mat_mul(emt + (EM_F4 + 15) * 128, x) ^ sr[k];
+        }
+        #pragma unroll
+        for (int l = 0; l < 6; l++) {
+            const int d = 1 << l;
+            const uint32_t px = (uint32_t)__shfl_up((int)x, d, 64), pc = (uint32_t)__shfl_up((int)rc, d, 64);
+            if (lane >= d && !rc) { x = mat_mul(emt + (EM_RUN + l) * 128, px) ^ x; rc = pc; }
+        }
+        uint32_t y = (uint32_t)__shfl_up((int)x, 1, 64), Lg = 0;
+        if (lane == 0) y = 0;
+        #pragma unroll
+        for (int k = 0; k < RUN; k++) {
+            const uint32_t sg = (uint32_t)lane * RUN + k;
+            gin[k * 64 + lane] = y;
+            if (sg == sigG) { Lg = em_f4(emt, (WG - tb - 64u * sg) >> 2, y) ^ sG; y = sr[k] ^ xG; }
+            else y = mat_mul(emt + (EM_F4 + 15) * 128, y) ^ sr[k];
+        }
+        const uint32_t gte = rdl(y, 63);                                    // the register at the tile's end
+        if (lane == 0) gin[NSEG] = gte;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t cout = treg[2 * t];                                  // the register XOR due at the tile's end
+        uint32_t ex = gte, dev = 0;
+        if (gterm) { ex = 0; dev = gte ^ cout; }
+        else if (grec) {
+            const uint32_t LG = sigG < NSEG ? rdl(Lg, (int)(sigG / RUN)) : gte ^ sG;   // the tile's own register entering WG
+            ex = sigG < NSEG ? gte ^ cout : expG ^ cout ^ DG;
+            dev = LG ^ expG;
+            if (term && ex != 0u && lane == 0)                              // the record ending at the terminal
+                atomicMin(&fo->fail_key, ((u64)(uint32_t)(loc[t].l[2] >> 32) << 32) | (S.count + n - 1));
+        }
+        // ---- tuples, and the records that end inside the tile
         if (!(l0 & DF_OVF)) {
-            const uint32_t* trec = rec + ((uint64_t)t * CAP_T + skip) * 4;
             for (uint32_t i0 = 0; i0 < n; i0 += 64) {
                 const uint32_t i = i0 + lane;
                 if (i < n) {
@@ -1501,6 +1656,17 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                         tuple_words(base, p, h, F.fid, a, b, c);
                     }
                     sv[3 * lane] = a; sv[3 * lane + 1] = b; sv[3 * lane + 2] = c;
+                    if (i + 1 < n) {
+                        // record i ends at record i + 1's patch word W
+                        const u32x4 v2 = *(const u32x4*)(trec + 4 * (i + 1));
+                        const uint32_t P2 = tb + (v2.w & 0xFFFFu), j = P2 & 3u;
+                        const uint32_t W = j ? (P2 & ~3u) + 4u : P2, sg = (W - tb) >> 6;
+                        const uint32_t bv = sg == sigG ? injG : gin[gin_at(sg)];
+                        const uint32_t k4 = sg == sigG ? (W - WG) >> 2 : (W - tb - 64u * sg) >> 2;
+                        const uint32_t pre = em_f4(emt, k4, bv) ^ tsnap[i + 1];
+                        if (pre != exp_pre(emt, j, c.w, entry_crc(base, F.len, tb, v2)))
+                            atomicMin(&fo->fail_key, ((u64)p << 32) | (S.count + i));
+                    }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1519,29 +1685,19 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
         } else {
-            // more records than the compact list holds: the body again, tuples direct
-            tile_body<BM_EMIT>(F, t, tt, S.X, false, (const CLY_LDS uint8_t*)smem_raw, stg, cl, 0u, nullptr, nullptr,
-                               nullptr, out, out_cap, gb, g);
+            // more records than the compact list holds: the body again, tuples
+            // direct; k_ovf checks these records one by one
+            tile_body<BM_EMIT>(F, t, tt, S.X, false, (const CLY_LDS uint8_t*)emt, stg, nullptr, cl, 0u, nullptr,
+                               nullptr, nullptr, nullptr, nullptr, out, out_cap, gb, g);
+            if (lane == 0) {
+                const uint32_t k = atomicAdd(&g->n_ovf, 1u);
+                ovf[k] = (u32x4){(uint32_t)f, n, (uint32_t)gb, (uint32_t)(gb >> 32)};
+            }
         }
         if (lane == 0) {
-            const uint32_t G = (uint32_t)l1;
-            if (skip) {
-                // the dropped records' patches out, and the new first record's
-                // predecessor term (its deferred ~cq is completed below)
-                const uint32_t* r0 = rec + (uint64_t)t * CAP_T * 4;
-                const uint32_t TE = tb + (uint32_t)CLY_TILE;
-                uint32_t corr = 0, q = 0xFFFFFFFFu, cp = 0;
-                for (uint32_t i = 0; i <= skip; i++) {
-                    const u32x4 v = *(const u32x4*)(r0 + 4 * i);
-                    const uint32_t Pi = tb + (v.w & 0xFFFFu);
-                    const uint32_t ci = (v.w & REC_SHORT) ? v.x : hdr_load(base, Pi, F.len).crc;
-                    corr ^= shift_bytes(sht, TE - Pi, i < skip ? (ci ^ CLY_K4 ^ q) : cp);
-                    q = ~ci; cp = ci;
-                }
-                treg[t] ^= corr;
-            }
-            if (tt > 0 && !(l0 & DF_NONE)) treg[t] ^= shift_bytes(sht, tb + (uint32_t)CLY_TILE - G, S.crc_last);
-            if (l0 & DF_TERM) {
+            treg[2 * t] = ex;
+            treg[2 * t + 1] = dev;
+            if (term) {
                 fo->term_pos = (uint32_t)(l1 >> 32);
                 fo->term_status = (int32_t)(int8_t)(uint8_t)(l3 >> 32);
                 fo->term_tile = t;
@@ -1553,87 +1709,123 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// k_fin: per file, the fold of its tile registers up to the terminal's tile
-// (sum over tiles t of A^(CLY_TILE (T - t)) treg[t]) must be zero.
+// k_fin: per file (FIN_NT threads), after k_emit: the register entering every
+// tile up to the terminal's, as a segmented scan over the tiles (a tile with a
+// boundary fixes the register at its end to its exit value; a tile without one
+// passes it on as A^CLY_TILE r ^ its own register), and in every tile after the
+// first that has a boundary, the check of the record that crosses into it
+// (its start: the last record before the tile, TileIn): A^CLY_TILE (the
+// register entering the tile) must equal the tile's dev shifted to its end,
+// with the patches of records k_refix dropped in front of G taken out.
 #define FIN_NT 256
+__device__ __forceinline__ uint32_t shift_b(const CLY_LDS uint32_t* sh, uint32_t m, uint32_t v) {
+    return m ? shift_bytes(sh, m, v) : v;
+}
 __global__ void __launch_bounds__(FIN_NT)
 k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __restrict__ treg,
+      const TileLocal* __restrict__ loc, const TileIn* __restrict__ tin, const uint32_t* __restrict__ rec,
       const uint32_t* __restrict__ tabs, const uint32_t* __restrict__ pw, Globals* g, int slot) {
-    __shared__ uint32_t tab[128];
-    __shared__ uint32_t part[FIN_NT];
-    __shared__ uint32_t plen[FIN_NT];
+    __shared__ uint32_t tabl[NIB_SH * 128 + 128];           // TAB_SH, TAB_TILE
+    __shared__ uint32_t px[FIN_NT], pc[FIN_NT];
+    __shared__ uint32_t mlev[8];
     if (g->nfix[slot]) return;              // k_emit did not run (link repair first)
-    for (int i = threadIdx.x; i < 128; i += FIN_NT) tab[i] = tabs[TAB_TILE + i];
-    __syncthreads();
-    const int f = blockIdx.x;
+    for (int i = threadIdx.x; i < NIB_SH * 128 + 128; i += FIN_NT) tabl[i] = tabs[TAB_SH + i];
+    const CLY_LDS uint32_t* sht = (const CLY_LDS uint32_t*)tabl;
+    const CLY_LDS uint32_t* tilet = sht + NIB_SH * 128;
+    const int f = blockIdx.x, tid = threadIdx.x;
     const DevFile F = files[f];
     FileInfo* fo = &finfo[f];
     if (!fo->has_term) {
-        if (threadIdx.x == 0) { atomicOr(&g->fail, 32u); fo->ok = 0; }
+        if (tid == 0) atomicOr(&g->fail, 32u);
         return;
     }
-    const uint32_t n = fo->term_tile - F.first_tile + 1;
-    const uint32_t per = (n + FIN_NT - 1) / FIN_NT;
-    const uint32_t lo = threadIdx.x * per, hi = lo + per < n ? lo + per : n;
-    uint32_t s = 0;
-    for (uint32_t i = lo; i < hi; i++) {
-        uint32_t p = 0;
-        #pragma unroll
-        for (int k = 0; k < 8; k++) p ^= tab[k * 16 + ((s >> (4 * k)) & 15u)];
-        s = p ^ treg[F.first_tile + i];
+    const uint32_t ft = F.first_tile, nt = fo->term_tile - ft + 1;
+    const uint32_t per = (nt + FIN_NT - 1) / FIN_NT;
+    const uint32_t lo = tid * per < nt ? tid * per : nt, hi = lo + per < nt ? lo + per : nt;
+    if (tid == 0) {                         // A^(CLY_TILE per 2^l): the shift of a level of the scan
+        uint32_t m = 1u << 31;
+        for (uint32_t b = per, k = 0; b; b >>= 1, k++) if (b & 1) m = cly_multmodp(pw[k], m);
+        for (int l = 0; l < 8; l++) { mlev[l] = m; m = cly_multmodp(m, m); }
     }
-    part[threadIdx.x] = s;
-    plen[threadIdx.x] = hi > lo ? hi - lo : 0;
     __syncthreads();
-    for (int d = 1; d < FIN_NT; d <<= 1) {
-        if ((threadIdx.x & (2 * d - 1)) == 0) {
-            uint32_t v = part[threadIdx.x];
-            for (uint32_t m = plen[threadIdx.x + d], k = 0; m; k++, m >>= 1) if (m & 1) v = cly_multmodp(pw[k], v);
-            part[threadIdx.x] = v ^ part[threadIdx.x + d];
-            plen[threadIdx.x] += plen[threadIdx.x + d];
-        }
+    uint32_t x = 0, c = 0;
+    for (uint32_t u = lo; u < hi; u++) {
+        const uint32_t v = treg[2 * (ft + u)];
+        if (!(loc[ft + u].l[0] & DF_NONE)) { x = v; c = 1; }
+        else x = mat_mul(tilet, x) ^ v;
+    }
+    px[tid] = x; pc[tid] = c;
+    __syncthreads();
+    for (int l = 0; (1 << l) < FIN_NT; l++) {
+        const int d = 1 << l;
+        uint32_t ox = 0, oc = 0;
+        if (tid >= d) { ox = px[tid - d]; oc = pc[tid - d]; }
+        __syncthreads();
+        if (tid >= d && !c) { x = cly_multmodp(mlev[l], ox) ^ x; c = oc; }
+        px[tid] = x; pc[tid] = c;
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
-        fo->fold = part[0];
-        fo->ok = part[0] == 0;
-        fo->fail_key = ~0ull;
-        if (part[0] != 0) atomicOr(&g->any_fail, 1u);
+    uint32_t y = tid ? px[tid - 1] : 0u;
+    const gbytes base = (gbytes)F.base;
+    for (uint32_t u = lo; u < hi; u++) {
+        const uint32_t t = ft + u;
+        const u64 l0 = loc[t].l[0];
+        const uint32_t v = treg[2 * t];
+        if (l0 & DF_NONE) { y = mat_mul(tilet, y) ^ v; continue; }
+        if (u > 0) {
+            const LBState S = ti_load(&tin[t]);
+            const uint32_t n = (uint32_t)(l0 >> 32), G = (uint32_t)loc[t].l[1];
+            const uint32_t tb = (uint32_t)((uint64_t)u * CLY_TILE), TE = tb + (uint32_t)CLY_TILE;
+            uint32_t dev = treg[2 * t + 1];
+            if ((l0 & DF_TERM) && n == 0) dev ^= shift_b(sht, TE - G, S.crc_last);     // G is the terminal
+            else {
+                const uint32_t WG = (G & 3u) ? (G & ~3u) + 4u : G;
+                dev = shift_b(sht, TE - WG, dev);
+                const uint32_t skip = (uint32_t)(loc[t].l[3] >> 40) & 0xFFFFu;
+                uint32_t q = 0xFFFFFFFFu;
+                for (uint32_t i = 0; i < skip; i++) {                     // the dropped records' patches
+                    const u32x4 e = *(const u32x4*)(rec + ((uint64_t)t * CAP_T + i) * 4);
+                    const uint32_t Pi = tb + (e.w & 0xFFFFu), ci = entry_crc(base, F.len, tb, e);
+                    dev ^= shift_b(sht, TE - Pi, ci ^ CLY_K4 ^ q);
+                    q = ~ci;
+                }
+            }
+            if (mat_mul(tilet, y) != dev)
+                atomicMin(&fo->fail_key, ((u64)S.P_last << 32) | (uint64_t)(S.count - 1));
+        }
+        y = v;
     }
 }
 
 // ---------------------------------------------------------------------------
-// k_locate (only after a failed fold): every tuple of a failing file gets its
-// CRC-32 computed alone (one lane per record, table steps from LDS) and
-// compared with the stored one; the first failing record of the file wins
-// (atomicMin on offset << 32 | index in file).
+// k_ovf (only for tiles whose compact list overflowed; k_emit lists them): every
+// record of such a tile gets its CRC-32 computed alone (one lane per record,
+// table steps from LDS) and compared with the stored one (data/logRecord.go:
+// 136-146, data/dataFile.go:105-109); the first failing record of a file wins.
 __global__ void __launch_bounds__(1024)
-k_locate(const DevFile* __restrict__ files, int nfiles, FileInfo* finfo, const cly_tuple* __restrict__ tup,
-         uint64_t out_cap, const uint32_t* __restrict__ tabs, const Globals* g, int slot) {
-    // (launched after every k_fin: returns at once unless a fold failed and the chain is final)
-    if (!g->any_fail || g->nfix[slot] || g->fail) return;
-    const uint64_t total = g->total;
+k_ovf(const DevFile* __restrict__ files, FileInfo* finfo, const cly_tuple* __restrict__ tup, uint64_t out_cap,
+      const u32x4* __restrict__ ovf, const Globals* g, int slot) {
+    if (!g->n_ovf || g->nfix[slot] || g->fail) return;     // (uniform: before the LDS setup's barrier)
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
-    init_tables(smem, tabs + TAB_SCAN, 0);
+    init_tables(smem);
     const CrcLane cl = crc_lane(threadIdx.x & 63);
-    const uint64_t lim = total < out_cap ? total : out_cap;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += (uint64_t)gridDim.x * blockDim.x) {
-        int lo = 0, hi = nfiles - 1;                       // the last file whose first index is <= i
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (finfo[mid].first_index <= i) lo = mid; else hi = mid - 1;
+    const uint32_t nl = g->n_ovf;
+    for (uint32_t k = blockIdx.x; k < nl; k += gridDim.x) {
+        const u32x4 e = ovf[k];
+        FileInfo* fo = &finfo[e.x];
+        const gbytes base = (gbytes)files[e.x].base;
+        const uint64_t gb = ((uint64_t)e.w << 32) | e.z;
+        for (uint32_t i = threadIdx.x; i < e.y; i += blockDim.x) {
+            if (gb + i >= out_cap) break;
+            const cly_tuple T = tup[gb + i];
+            uint64_t a = (uint64_t)T.offset + 4, b = (uint64_t)T.offset + T.size;
+            uint32_t s = 0xFFFFFFFFu;
+            for (; a < b && (a & 3); a++) s = crc_byte(smem, s, base[a], cl.r4);
+            for (; a + 4 <= b; a += 4) s = crc_word(smem, s ^ *(const CLY_GL uint32_t*)(base + a), cl);
+            for (; a < b; a++) s = crc_byte(smem, s, base[a], cl.r4);
+            if (~s != T.crc) atomicMin(&fo->fail_key, ((u64)(uint64_t)T.offset << 32) | (u64)(gb + i - fo->first_index));
         }
-        FileInfo* fo = &finfo[lo];
-        if (fo->ok || i >= fo->end_index || i < fo->first_index) continue;
-        const cly_tuple T = tup[i];
-        const gbytes base = (gbytes)files[lo].base;
-        uint64_t a = (uint64_t)T.offset + 4, b = (uint64_t)T.offset + T.size;
-        uint32_t s = 0xFFFFFFFFu;
-        for (; a < b && (a & 3); a++) s = crc_byte(smem, s, base[a], cl.r4);
-        for (; a + 4 <= b; a += 4) s = crc_word(smem, s ^ *(const CLY_GL uint32_t*)(base + a), cl);
-        for (; a < b; a++) s = crc_byte(smem, s, base[a], cl.r4);
-        if (~s != T.crc) atomicMin(&fo->fail_key, ((u64)(uint64_t)T.offset << 32) | (u64)(i - fo->first_index));
     }
 }
 
@@ -1650,12 +1842,13 @@ struct cly_ctx {
     DevFile* d_files; uint32_t* d_tprefix; FileInfo* d_finfo; uint64_t* d_ftotal; int cap_files;
     DevFile* h_files; uint32_t* h_tprefix; FileInfo* h_finfo;
     TileLocal* d_loc; TileIn* d_tin; uint32_t* d_treg; uint32_t* d_fix; uint32_t* d_rec;
+    uint32_t* d_seg; uint32_t* d_snap; u32x4* d_ovf;   // segment registers, snapshots, k_ovf's list
     int64_t cap_tiles;
     Globals* d_g; Globals* h_g;
-    uint32_t* d_tabs;            // nibble tables (TAB_SCAN, TAB_SH, TAB_TILE)
+    uint32_t* d_tabs;            // nibble tables (TAB_SH, TAB_TILE, TAB_EM)
     uint32_t* d_pw;              // x^(8 CLY_TILE 2^k) mod P, k < 40
     int scan_grid, emit_grid, loc_grid;
-    float kms[6];                // last call: k_scan, link rounds (k_link/k_refix), k_emit, k_fin, k_locate, all
+    float kms[6];                // last call: k_scan, link rounds (k_link/k_refix), k_emit, k_fin, k_ovf, all
     uint8_t* d_bytes; uint64_t cap_bytes;          // host-path staging
     cly_tuple* d_tuples; uint64_t cap_tuples;
     void* merge_scratch;         // clymerge.hip's buffers (grow-only)
@@ -1678,15 +1871,17 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     for (int i = 0; i < 8; i++) HIPCK(hipEventCreate(&c->ev[i]));
     {
         static uint32_t hn[NTAB_ALL];
-        for (int k = 0; k < NIB_SCAN + NIB_SH + 1; k++) {
+        for (int k = 0; k < NTAB_ALL / 128; k++) {
             uint64_t nbytes;
-            if (k < 6) nbytes = (uint64_t)CLY_SEG << k;                              // A^(64 2^k)
-            else if (k == 6) nbytes = CLY_BLK - CLY_SEG;                             // the block step
-            else if (k < NIB_SCAN + 64) {                                            // A^(v 16^d)
-                const int s = k - NIB_SCAN;
-                nbytes = (uint64_t)(s & 15) << (4 * (s >> 4));
-            } else if (k == NIB_SCAN + 64) nbytes = 65536;                          // A^65536
-            else nbytes = (uint64_t)CLY_TILE;                                        // k_fin's tile step
+            if (k < 64) nbytes = (uint64_t)(k & 15) << (4 * (k >> 4));               // A^(v 16^d)
+            else if (k == 64) nbytes = 65536;                                        // A^65536
+            else if (k == 65) nbytes = (uint64_t)CLY_TILE;                           // k_fin's tile step
+            else {
+                const int e = k - 66;                                                // TAB_EM
+                if (e < EM_F1) nbytes = 4ull * (uint64_t)(e + 1);                    // A^(4k), k = 1..16
+                else if (e < EM_RUN) nbytes = (uint64_t)(e - EM_F1 + 1);             // A^1..A^3
+                else nbytes = (uint64_t)RUN_BYTES << (e - EM_RUN);                   // A^(RUN_BYTES 2^l)
+            }
             const uint32_t xm = cly_x8n(nbytes);
             for (int nb = 0; nb < 8; nb++)
                 for (uint32_t v = 0; v < 16; v++) hn[k * 128 + nb * 16 + v] = cly_multmodp(xm, v << (4 * nb));
@@ -1722,6 +1917,7 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     hipStreamSynchronize(c->stream);
     hipFree(c->d_call); hipFree(c->d_ftotal);
     hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_rec);
+    hipFree(c->d_seg); hipFree(c->d_snap); hipFree(c->d_ovf);
     hipFree(c->d_tabs); hipFree(c->d_pw); hipFree(c->d_bytes); hipFree(c->d_tuples); hipFree(c->d_dbg);
     hipHostFree(c->h_call);
     cly_merge_scratch_free(c->merge_scratch);
@@ -1764,12 +1960,17 @@ static int ensure_files(cly_ctx* c, int nfiles) {
 static int ensure_tiles(cly_ctx* c, int64_t ntiles) {
     if (ntiles <= c->cap_tiles) return CLY_OK;
     hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_rec);
+    hipFree(c->d_seg); hipFree(c->d_snap); hipFree(c->d_ovf);
     c->d_loc = nullptr; c->d_tin = nullptr; c->d_treg = nullptr; c->d_fix = nullptr; c->d_rec = nullptr;
+    c->d_seg = nullptr; c->d_snap = nullptr; c->d_ovf = nullptr;
     c->cap_tiles = 0;
     const int64_t cap = ntiles < 1024 ? 1024 : ntiles;
     HIPCK(hipMalloc(&c->d_loc, sizeof(TileLocal) * cap));
     HIPCK(hipMalloc(&c->d_tin, sizeof(TileIn) * cap));
-    HIPCK(hipMalloc(&c->d_treg, sizeof(uint32_t) * cap));
+    HIPCK(hipMalloc(&c->d_treg, sizeof(uint32_t) * 2 * cap));
+    HIPCK(hipMalloc(&c->d_seg, sizeof(uint32_t) * NSEG * (uint64_t)cap));
+    HIPCK(hipMalloc(&c->d_snap, sizeof(uint32_t) * SNAP_T * (uint64_t)cap));
+    HIPCK(hipMalloc(&c->d_ovf, sizeof(u32x4) * cap));
     HIPCK(hipMalloc(&c->d_fix, sizeof(uint32_t) * cap));
     HIPCK(hipMalloc(&c->d_rec, sizeof(uint32_t) * 4 * (uint64_t)CAP_T * cap));
     c->cap_tiles = cap;
@@ -1810,13 +2011,14 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     if (rc) return rc;
     memset(c->h_g, 0, sizeof(Globals));
     memset(c->h_finfo, 0, sizeof(FileInfo) * nfiles);
+    for (int i = 0; i < nfiles; i++) c->h_finfo[i].fail_key = ~0ull;
     HIPCK(hipMemcpyAsync(c->d_call, c->h_call, c->call_bytes, hipMemcpyHostToDevice, st));
     const uint32_t nt32 = (uint32_t)ntiles;
     int grid = c->scan_grid;
     if ((int64_t)grid * SCAN_WAVES > ntiles) grid = (int)((ntiles + SCAN_WAVES - 1) / SCAN_WAVES);
     HIPCK(hipEventRecord(c->ev[0], st));
     hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * SCAN_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
-                       c->d_loc, c->d_rec, c->d_treg, c->d_tabs, c->d_g);
+                       c->d_loc, c->d_rec, c->d_seg, c->d_snap, c->d_treg, c->d_g);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[1], st));
     if (c->dbg & 1) {
@@ -1835,7 +2037,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     // one repair round on the device, without a host wait: k_refix and
     // k_link return at once when the first link listed no tile
     hipLaunchKernelGGL(k_refix, dim3(REFIX_GRID), dim3(64 * SCAN_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix,
-                       c->d_loc, c->d_tin, c->d_rec, c->d_treg, c->d_tabs, c->d_fix, c->d_g, 0);
+                       c->d_loc, c->d_tin, c->d_rec, c->d_seg, c->d_snap, c->d_treg, c->d_fix, c->d_g, 0);
     hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_loc, c->d_tin, c->d_ftotal,
                        c->d_finfo, c->d_fix, c->d_g, 1, 0);
     HIPCK(hipGetLastError());
@@ -1845,15 +2047,16 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         int eg = c->emit_grid;
         if ((int64_t)eg * EMIT_WAVES > ntiles) eg = (int)((ntiles + EMIT_WAVES - 1) / EMIT_WAVES);
         hipLaunchKernelGGL(k_emit, dim3(eg), dim3(64 * EMIT_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
-                           c->d_tin, c->d_loc, c->d_rec, c->d_treg, c->d_finfo, c->d_tabs, d_out, out_cap, c->d_g, slot);
+                           c->d_tin, c->d_loc, c->d_rec, c->d_seg, c->d_snap, c->d_treg, c->d_finfo, c->d_tabs, d_out,
+                           out_cap, c->d_ovf, c->d_g, slot);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[3], st));
-        hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_finfo, c->d_treg, c->d_tabs,
-                           c->d_pw, c->d_g, slot);
+        hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_finfo, c->d_treg, c->d_loc,
+                           c->d_tin, c->d_rec, c->d_tabs, c->d_pw, c->d_g, slot);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[4], st));
-        hipLaunchKernelGGL(k_locate, dim3(c->loc_grid), dim3(1024), 0, st, c->d_files, nfiles, c->d_finfo, d_out,
-                           out_cap, c->d_tabs, c->d_g, slot);
+        hipLaunchKernelGGL(k_ovf, dim3(c->loc_grid), dim3(1024), 0, st, c->d_files, c->d_finfo, d_out, out_cap,
+                           c->d_ovf, c->d_g, slot);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[7], st));
         // one read-back and one wait for the whole call when no repair round is needed
@@ -1863,15 +2066,6 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     };
     int rc2 = launch_emit();
     if (rc2) return rc2;
-    if (CLY_EXP) {                           // timing experiments: the kernel times only
-        float a = 0, b = 0, e2 = 0, f2 = 0;
-        HIPCK(hipEventElapsedTime(&a, c->ev[0], c->ev[1])); HIPCK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
-        HIPCK(hipEventElapsedTime(&e2, c->ev[2], c->ev[3])); HIPCK(hipEventElapsedTime(&f2, c->ev[3], c->ev[4]));
-        c->kms[0] = a; c->kms[1] = b; c->kms[2] = e2; c->kms[3] = f2; c->kms[4] = 0; c->kms[5] = a + b + e2 + f2;
-        for (int i = 0; i < nfiles; i++) { file_first[i] = 0; res[i].n_records = 0; res[i].end_offset = 0; res[i].status = 0; }
-        if (needed) *needed = 0;
-        return CLY_OK;
-    }
     float ms_fix = 0;
     uint32_t rounds = 1, refixed = 0;
     if (c->h_g->nfix[0]) { rounds++; refixed += c->h_g->nfix[0]; }          // the device round
@@ -1885,8 +2079,8 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
             const int ns = slot ^ 1;
             HIPCK(hipMemsetAsync(&c->d_g->nfix[ns], 0, sizeof(uint32_t), st));
             hipLaunchKernelGGL(k_refix, dim3((nfix + SCAN_WAVES - 1) / SCAN_WAVES), dim3(64 * SCAN_WAVES), 0, st,
-                               c->d_files, nfiles, c->d_tprefix, c->d_loc, c->d_tin, c->d_rec, c->d_treg, c->d_tabs,
-                               c->d_fix, c->d_g, slot);
+                               c->d_files, nfiles, c->d_tprefix, c->d_loc, c->d_tin, c->d_rec, c->d_seg, c->d_snap,
+                               c->d_treg, c->d_fix, c->d_g, slot);
             hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_loc, c->d_tin,
                                c->d_ftotal, c->d_finfo, c->d_fix, c->d_g, ns, -1);
             HIPCK(hipGetLastError());
@@ -1904,7 +2098,6 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
             if (rc2) return rc2;
         }
     }
-    const bool located = c->h_g->any_fail && !c->h_g->fail;       // k_locate did its work
     float ms_scan = 0, ms_link = 0, ms_emit = 0, ms_fin = 0, ms_loc = 0;
     HIPCK(hipEventElapsedTime(&ms_scan, c->ev[0], c->ev[1]));
     HIPCK(hipEventElapsedTime(&ms_link, c->ev[1], c->ev[2]));
@@ -1923,17 +2116,11 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     for (int i = 0; i < nfiles; i++) {
         const FileInfo& fi = c->h_finfo[i];
         file_first[i] = fi.first_index;
-        if (fi.ok) {
+        if (fi.fail_key == ~0ull) {              // every record matches its CRC
             res[i].n_records = fi.end_index - fi.first_index;
             res[i].end_offset = fi.term_pos;
             res[i].status = fi.term_status;
-        } else {
-            if (fi.fail_key == ~0ull) {
-                // a record's tuple was dropped (out_cap) before k_locate could check it
-                if (c->h_g->overflow || c->h_g->total > out_cap) return CLY_ERR_CAPACITY;
-                fprintf(stderr, "clyscan: internal error (file %d: no failing record)\n", i);
-                return CLY_ERR_DEVICE;
-            }
+        } else {                                 // the first record whose CRC fails
             res[i].n_records = fi.fail_key & 0xffffffffull;
             res[i].end_offset = (int64_t)(fi.fail_key >> 32);
             res[i].status = CLY_ERR_CRC;
@@ -1945,7 +2132,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     if (stats) {
         stats->scan_ms = ms_scan + ms_emit; stats->resolve_ms = ms_link + ms_fix + ms_fin + ms_loc;
         stats->total_ms = c->kms[5];
-        stats->passes = rounds + (located ? 1 : 0);
+        stats->passes = rounds;
         stats->n_chunks = (uint32_t)(ntiles * CLY_NBLK * CLY_NL); stats->bytes = bytes; stats->records = total;
     }
     if (c->h_g->overflow || c->h_g->total > out_cap) return CLY_ERR_CAPACITY;
@@ -2080,20 +2267,11 @@ extern "C" int cly_ctx_device_internal(cly_ctx* c) { return c->device; }
 extern "C" void** cly_ctx_merge_slot_internal(cly_ctx* c) { return &c->merge_scratch; }
 
 // Per-kernel times of the last cly_scan_device call (ms): k_scan, link rounds
-// (k_link + k_fbase + repair), k_emit, k_fin, k_locate, all.  Not in the public header.
+// (k_link + repair), k_emit, k_fin, k_ovf, all.  Not in the public header.
 // Debug (not in the public header): flags (bit 0: snapshot k_scan's tile
 // LOCALs); cly_dbg_tiles copies the snapshot (32 B per tile) and the final
 // TileIns (32 B per tile) of the last call to host memory.
 extern "C" void cly_dbg_set(cly_ctx* c, int flags) { c->dbg = flags; }
-#if CLY_PROF
-// experiment builds: the section cycle sums of k_scan since the last call (reset)
-extern "C" int cly_dbg_prof(cly_ctx* c, unsigned long long* out8) {
-    hipStreamSynchronize(c->stream);
-    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
-}
-#endif
 extern "C" int cly_dbg_tiles(cly_ctx* c, void* loc_out, void* tin_out, int64_t ntiles) {
     HIPCK(hipSetDevice(c->device));
     if (loc_out && c->d_dbg && ntiles <= c->cap_dbg)
@@ -2121,6 +2299,7 @@ extern "C" const char* cly_strerror(int code) {
         case CLY_ERR_NOREPAIR: return "internal: chain resolution failed";
         case -14: return "the data dir maybe contaminated or damaged";            // CLY_ERR_DIR (clyload.h)
         case -15: return "merge-finished: no readable record / value not an integer";   // CLY_ERR_MERGE_FIN
+        case -16: return "the key can not be empty";                              // CLY_ERR_KEY_EMPTY (clyload.h)
         default: return "unknown status";
     }
 }

@@ -34,7 +34,9 @@
  *     order (the set of records and WriteOff agree whenever no rotation falls
  *     between two of them).
  * Read errors fail the open with their status (ErrInvalidCRC etc.), as
- * NewCouloyDB does.  Out of scope (the Go caller's): loadMergeFiles' moving of
+ * NewCouloyDB does, in its order: the hint file's (a record that does not
+ * read, or whose position does not decode), then merge-finished's, then the
+ * data files' in fid order.  Out of scope (the Go caller's): loadMergeFiles' moving of
  * the merge directory (merge.go:195-238), the file lock, and scheduling the TTL
  * jobs of keys that expire later (cly_db_entries lists them with their
  * expiration).                                                                */
@@ -51,6 +53,9 @@ extern "C" {
                                  a *.cly name whose stem strconv.Atoi rejects   */
 #define CLY_ERR_MERGE_FIN -15 /* merge-finished's record at 0 does not read, or
                                  its value is not an integer (getNonMergeFileId) */
+#define CLY_ERR_KEY_EMPTY -16 /* public.ErrKeyIsEmpty: the TTL sweep's db.Del of an
+                                 expired String key whose realKey is empty
+                                 (db.go:186-188, returned by loadIndex db.go:646-649) */
 
 typedef struct cly_db cly_db;
 typedef struct cly_load_stats {
@@ -95,7 +100,10 @@ int  cly_db_open_opts(cly_ctx* ctx, const char* dir, const cly_db_options* opt, 
  * transaction whose records and commit fall in different ranges resolves as
  * in one pass.  Result identical to cly_db_open_opts(ctxs[0], ...).
  * CLY_ERR_DEVICE when a range's device cannot be reached from ctxs[0]'s.
- * 1 <= nctx <= 16.                                                            */
+ * 1 <= nctx <= 16, each context listed once (CLY_ERR_ARG otherwise: a context
+ * runs one scan at a time; several contexts may share a device).  The path
+ * with contexts on different devices (peer copies of the tuples, peer reads
+ * by the index rebuild) has not been run on a multi-GPU node.                */
 int  cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir, const cly_db_options* opt, cly_db** out,
                        cly_load_stats* st);
 void cly_db_close(cly_db* db);

@@ -76,6 +76,134 @@ def crc32(b):
     return zlib.crc32(b) & 0xFFFFFFFF
 
 
+# ---- GF(2) arithmetic of the CRC-32 register (fixture construction only) ----
+# Register convention: the reflected register Go's crc32.Update keeps; one zero
+# byte through it is the linear map A: s -> T0[s & 0xff] ^ (s >> 8), and A^n is
+# multiplication by x^(8n) mod P (bit 31 = x^0).
+POLY = 0xEDB88320
+
+
+def gf_mul(a, b):
+    p = 0
+    for k in range(31, -1, -1):
+        if a & (1 << k):
+            p ^= b
+        b = (b >> 1) ^ POLY if b & 1 else b >> 1
+    return p
+
+
+def gf_x8n(n):
+    p, sq = 1 << 31, 1 << 23
+    while n:
+        if n & 1:
+            p = gf_mul(sq, p)
+        sq = gf_mul(sq, sq)
+        n >>= 1
+    return p
+
+
+def crc_shift(v, n):
+    """A^n v: the register v after n zero bytes."""
+    return gf_mul(gf_x8n(n), v) if n else v
+
+
+def _t0(i):
+    for _ in range(8):
+        i = (i >> 1) ^ POLY if i & 1 else i >> 1
+    return i
+
+
+_T0 = [_t0(i) for i in range(256)]
+_T0_INV = {t >> 24: i for i, t in enumerate(_T0)}
+
+
+def crc_unshift(v, n):
+    """A^-n v (the top byte of T0 is a permutation of the index)."""
+    for _ in range(n):
+        i = _T0_INV[v >> 24]
+        v = (((v ^ _T0[i]) << 8) & 0xFFFFFFFF) | i
+    return v
+
+
+def record_bounds(F):
+    """(offset, size) of every record the reader returns."""
+    out, off = [], 0
+    while True:
+        st, t = read_log_record(F, off)
+        if st is not None:
+            return out
+        out.append((off, t["size"]))
+        off += t["size"]
+
+
+def file_fold(F):
+    """The per-file linear fold of the records' CRC residues, each shifted to the
+    end of the file: sum_k A^(E - end_k) (crc32(record k) ^ stored_k).  A GF(2)
+    sum, so two non-zero residues can cancel; a verdict taken from this fold
+    alone misses such files, while ReadLogRecord checks every record
+    (data/dataFile.go:105-109)."""
+    recs = record_bounds_lenient(F)
+    E = recs[-1][0] + recs[-1][1] if recs else 0
+    s = 0
+    for off, size in recs:
+        res = crc32(F[off + 4: off + size]) ^ struct.unpack_from("<I", F, off)[0]
+        if res:
+            s ^= crc_shift(res, E - off - size)
+    return s
+
+
+def record_bounds_lenient(F):
+    """Record framing only (header sizes), ignoring the CRC: the chain a decoder
+    that does not stop at ErrInvalidCRC would walk."""
+    out, off = [], 0
+    while True:
+        hb = F[off:off + 26]
+        if len(hb) <= 5:
+            return out
+        idx = 6
+        ks, a = varint(hb[idx:]); idx += a
+        vs, b = varint(hb[idx:]); idx += b
+        _, c = varint(hb[idx:]); idx += c
+        if a <= 0 or b <= 0 or c <= 0:
+            return out
+        size = idx + (ks & 0xFFFFFFFF) + (vs & 0xFFFFFFFF)
+        if off + size > len(F) or (struct.unpack_from("<I", F, off)[0] == 0 and ks == 0 and vs == 0):
+            return out
+        out.append((off, size))
+        off += size
+
+
+def cancel_stored(F, i, j, delta):
+    """XOR delta into record i's stored CRC and A^(end_j - end_i) delta into record
+    j's: both records fail their own CRC check, yet their residues cancel in the
+    per-file fold.  The reference stops at record i with ErrInvalidCRC."""
+    b = bytearray(F)
+    recs = record_bounds_lenient(F)
+    (oi, si), (oj, sj) = recs[i], recs[j]
+    d2 = crc_shift(delta, (oj + sj) - (oi + si))
+    struct.pack_into("<I", b, oi, struct.unpack_from("<I", b, oi)[0] ^ delta)
+    struct.pack_into("<I", b, oj, struct.unpack_from("<I", b, oj)[0] ^ d2)
+    return bytes(b)
+
+
+def cancel_payload(F, i, pos_i, bit, j):
+    """Flip one payload bit of record i (at offset pos_i inside it) and XOR into
+    the last 4 payload bytes of record j the word whose CRC syndrome cancels the
+    first in the per-file fold (4 bytes at the record end change the register
+    by A^4 v, so v = A^-4 of the wanted residue)."""
+    b = bytearray(F)
+    recs = record_bounds_lenient(F)
+    (oi, si), (oj, sj) = recs[i], recs[j]
+    before = crc32(bytes(b[oi + 4: oi + si]))
+    b[oi + pos_i] ^= 1 << bit
+    res_i = crc32(bytes(b[oi + 4: oi + si])) ^ before
+    want = crc_shift(res_i, (oj + sj) - (oi + si))
+    v = crc_unshift(want, 4)
+    w = struct.unpack_from("<I", b, oj + sj - 4)[0] ^ v
+    struct.pack_into("<I", b, oj + sj - 4, w)
+    return bytes(b)
+
+
 # ---- writer side -----------------------------------------------------------
 def encode_record(key, value, typ=NORMAL, dtype=STRING, exp=0):
     hdr = bytes([typ, dtype]) + put_varint(len(key)) + put_varint(len(value)) + put_varint(exp)
@@ -280,6 +408,26 @@ def fixtures():
     fx["six_tail"] = good + raw(b"", b"", typ=1, dt=2)
     # big keys
     fx["big_record"] = encode_record(key_tx(bytes(range(256)) * 4, 0), bytes(rng.getrandbits(8) for _ in range(70000)))
+
+    # 13. CRC residues that cancel in a per-file linear fold: two (or three)
+    # records fail their own check, the file's fold of residues is zero.  The
+    # reference returns ErrInvalidCRC at the first of them (dataFile.go:105-109).
+    c2 = b"".join(encode_record(key_tx(test_key(i), 0), bytes(rng.getrandbits(8) for _ in range(256)))
+                  for i in range(300))                                   # C2 shape, 82 800 B: > one 64-KiB tile
+    fx["crc_cancel_near"] = cancel_stored(c2, 2, 5, 0x1D)
+    fx["crc_cancel_far"] = cancel_stored(c2, 3, 260, 0x80000001)
+    fx["crc_cancel_payload"] = cancel_payload(c2, 10, 130, 3, 200)
+    three = cancel_stored(c2, 40, 41, 0xDEADBEEF)                        # i, i+1 cancel ...
+    fx["crc_cancel_three"] = cancel_stored(three, 41, 250, 0x00C0FFEE)  # ... and a third pair on top
+    tiny = bytearray()
+    for i in range(2000):                                                # 11-14 B records, unaligned starts
+        tiny += encode_record(key_tx(bytes([i & 0xFF]), 0), bytes(rng.getrandbits(8) for _ in range(i % 4)))
+    fx["crc_cancel_tiny"] = cancel_stored(bytes(tiny), 700, 701, 0x5A5A5A5A)
+    fx["crc_cancel_tiny_far"] = cancel_payload(bytes(tiny), 101, 10, 0, 1903)
+    for name in ("crc_cancel_near", "crc_cancel_far", "crc_cancel_payload", "crc_cancel_three",
+                 "crc_cancel_tiny", "crc_cancel_tiny_far"):
+        assert file_fold(fx[name]) == 0, name                            # the fold passes ...
+        assert scan(fx[name], 0)[0] == ERR_CRC, name                     # ... the reference does not
     return fx
 
 

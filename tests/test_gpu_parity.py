@@ -211,6 +211,64 @@ def test_bitflips_everywhere_small(scanner):
         compare(r.file_tuples(i), r.status[i], r.end_offset[i], t, st, end, "flip %d" % i)
 
 
+def _cancel_corpus(seed):
+    """A file and record pairs (i, j) for the CRC-cancellation cases: C2-shape
+    records, tiny unaligned records, mixed corpora, and big records spanning
+    tiles."""
+    import random
+
+    import make_golden as mg
+    rng = random.Random(seed)
+    kind = seed % 4
+    if kind == 0:
+        data = fixed_records_file(9000, 256, seed=seed).tobytes()             # 2.5 MB, 276-B records
+    elif kind == 1:
+        b = bytearray()
+        for i in range(60000):                                                # 11-14 B records
+            b += mg.encode_record(mg.key_tx(bytes([i & 0xFF]), 0), rng.randbytes(i % 4))
+        data = bytes(b)
+    elif kind == 2:
+        data = mixed_corpus(seed * 13, 1_500_000, tail=False)
+    else:
+        b = bytearray()
+        for i in range(120):                                                  # 2 KiB .. 100 KiB values
+            b += mg.encode_record(mg.key_tx(mg.test_key(i), 0), rng.randbytes(rng.choice([2000, 30000, 100000])))
+        data = bytes(b)
+    return data, rng
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_crc_residues_that_cancel(scanner, seed):
+    """Two (or three) records fail their own CRC while their residues cancel in
+    any per-file linear fold (stored-CRC deltas d and A^(end_j - end_i) d, or a
+    payload flip compensated in a later record's last word).  ReadLogRecord's
+    loop stops at the first of them with ErrInvalidCRC (data/dataFile.go:105-109);
+    so must the scan.  Pairs: adjacent, a few records apart, across tiles."""
+    import make_golden as mg
+    data, rng = _cancel_corpus(seed)
+    recs = mg.record_bounds_lenient(data)
+    n = len(recs)
+    files = []
+    for k in range(6):
+        i = rng.randrange(0, n - 2)
+        j = min(n - 1, i + rng.choice([1, 1, 2, 5, 40, n]))
+        if j <= i:
+            continue
+        if seed % 4 == 0 and k % 2:
+            d = mg.cancel_payload(data, i, rng.randrange(14, 270), rng.randrange(8), j)
+        else:
+            d = mg.cancel_stored(data, i, j, rng.randrange(1, 1 << 32))
+        if k == 5 and j + 1 < n:                                              # a third record on top
+            d = mg.cancel_stored(d, j, rng.randrange(j + 1, n), rng.randrange(1, 1 << 32))
+        assert mg.file_fold(d) == 0
+        files.append(DataFile(np.frombuffer(d, np.uint8).copy(), 50 + k))
+    r = scanner.scan(files)
+    for i, f in enumerate(files):
+        t, st, end = co.scan_file(f.data, f.fid)
+        assert st == _abi.ERR_CRC
+        compare(r.file_tuples(i), r.status[i], r.end_offset[i], t, st, end, "cancel seed %d file %d" % (seed, i))
+
+
 @pytest.mark.slow
 def test_config2_device_generated_properties():
     """BASELINE config 2 at full size (16 x 256 MiB, 256-B values), generated in

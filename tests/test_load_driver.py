@@ -331,3 +331,107 @@ def test_gpu_open_multi_tx_across_shards(scanner, tmp_path):
             assert db.stats.write_off == len(f3) and db.stats.active_fid == 3
     finally:
         other.close()
+
+
+@pytest.mark.gpu
+def test_gpu_ttl_sweep_empty_key(scanner, tmp_path):
+    """An expired String put whose realKey is empty: the sweep's db.Del("")
+    returns ErrKeyIsEmpty (db.go:186-188) and loadIndex returns it
+    (db.go:646-649), so NewCouloyDB fails.  A live empty key does not."""
+    from couloydb_amd import ScanError, _abi
+    F = mg.encode_record(mg.key_tx(b"a", 0), b"1", mg.NORMAL, mg.STRING, 5) + \
+        mg.encode_record(mg.key_tx(b"", 0), b"2", mg.NORMAL, mg.STRING, 5)
+    write_dir(tmp_path, [F])
+    scanner.set_clock(10)
+    try:
+        with pytest.raises(ScanError) as e:
+            scanner.open_db(str(tmp_path))
+        assert e.value.code == _abi.ERR_KEY_EMPTY
+        scanner.set_clock(3)                                      # not expired yet: no Del
+        with scanner.open_db(str(tmp_path)) as db:
+            assert db.get(b"") == b"2" and db.stats.n_expired == 0
+    finally:
+        scanner.set_clock(0)
+
+
+@pytest.mark.gpu
+def test_gpu_open_error_order(scanner, tmp_path):
+    """NewCouloyDB's error order (db.go:472-485, merge.go:257-287, db.go:492-499):
+    the hint file's first failure (a record that does not read, or a value that
+    does not decode, whichever comes first in its loop), then merge-finished,
+    then the data files."""
+    from couloydb_amd import ScanError, _abi
+    good = [mg.encode_record(b"k%d" % i, mg.put_varint(0) + mg.put_varint(10 * i)) for i in range(5)]
+    panic = mg.encode_record(b"bad", b"\xff" * 10 + b"\x02")       # DecodeLogRecordPos: varint overflow
+    crc_bad = bytearray(mg.encode_record(b"k9", mg.put_varint(0) + mg.put_varint(9)))
+    crc_bad[-1] ^= 1
+    data_bad = bytearray(mg.encode_record(mg.key_tx(b"x", 0), b"v"))
+    data_bad[-1] ^= 1
+    write_dir(tmp_path, [bytes(data_bad)])
+    mf = os.path.join(tmp_path, "merge-finished")
+    hf = os.path.join(tmp_path, "hint-index")
+    with open(mf, "wb") as f:
+        f.write(b"")                                               # does not read: ERR_MERGE_FIN
+    cases = [
+        (good[0] + bytes(crc_bad) + good[1], _abi.ERR_CRC),        # hint CRC before merge-finished
+        (good[0] + panic + bytes(crc_bad), _abi.ERR_VARINT),       # hint decode panic before its later CRC error
+        (good[0] + bytes(crc_bad) + panic, _abi.ERR_CRC),          # ... and after it
+        (b"".join(good), _abi.ERR_MERGE_FIN),                      # a good hint: merge-finished next
+    ]
+    for hint, code in cases:
+        with open(hf, "wb") as f:
+            f.write(hint)
+        with pytest.raises(ScanError) as e:
+            scanner.open_db(str(tmp_path))
+        assert e.value.code == code, (code, e.value.code)
+    with open(mf, "wb") as f:
+        f.write(mg.encode_record(mg.MERGE_FIN_KEY, b"0"))
+    with pytest.raises(ScanError) as e:                            # then the data file's CRC error
+        scanner.open_db(str(tmp_path))
+    assert e.value.code == _abi.ERR_CRC
+
+
+@pytest.mark.gpu
+def test_gpu_dir_listing_uint32_fids(scanner, tmp_path):
+    """Stems Atoi accepts but uint32() wraps: "-1.cly" is fid 4294967295 (read
+    from 4294967295.cly, sort.Ints puts it first), listed once with the
+    spelled-out name; lookups into it and into fid 3 both resolve."""
+    a = mg.encode_record(mg.key_tx(b"a", 0), b"from-max")
+    b = mg.encode_record(mg.key_tx(b"b", 0), b"from-3")
+    with open(os.path.join(tmp_path, "4294967295.cly"), "wb") as f:
+        f.write(a)
+    with open(os.path.join(tmp_path, "-1.cly"), "wb") as f:
+        f.write(b"never read")
+    with open(os.path.join(tmp_path, "000000003.cly"), "wb") as f:
+        f.write(b)
+    with scanner.open_db(str(tmp_path)) as db:
+        assert db.stats.n_files == 2
+        assert db.get(b"a") == b"from-max" and db.get(b"b") == b"from-3"
+        assert db.stats.active_fid == 0xFFFFFFFF                   # the last in sort.Ints order
+
+
+@pytest.mark.gpu
+def test_gpu_data_file_size_clamp(scanner, tmp_path):
+    """checkOptions raises DataFileSize below 64 to 64 (db.go:436-438): the
+    sweep's rotation with DataFileSize 1 equals the one with 64."""
+    recs = [mg.encode_record(mg.key_tx(mg.test_key(i), 0), b"x" * 3, mg.NORMAL, mg.STRING, 5) for i in range(9)]
+    write_dir(tmp_path, [b"".join(recs)])
+    scanner.set_clock(10)
+    try:
+        with scanner.open_db(str(tmp_path), data_file_size=1) as db1, \
+                scanner.open_db(str(tmp_path), data_file_size=64) as db64:
+            assert (db1.stats.active_fid, db1.stats.write_off, db1.stats.sweep_files) == \
+                (db64.stats.active_fid, db64.stats.write_off, db64.stats.sweep_files)
+            assert db64.stats.sweep_files >= 1
+    finally:
+        scanner.set_clock(0)
+
+
+@pytest.mark.gpu
+def test_gpu_open_multi_rejects_repeated_context(scanner, tmp_path):
+    """A context listed twice would run two scans on one context at once."""
+    from couloydb_amd import ScanError, _abi, open_db_multi
+    write_dir(tmp_path, [mg.encode_record(mg.key_tx(b"k", 0), b"v")])
+    with pytest.raises(ScanError) as e:
+        open_db_multi([scanner, scanner], str(tmp_path))
+    assert e.value.code == _abi.ERR_ARG
