@@ -125,6 +125,7 @@ class Scanner:
     """One GPU context (cly_ctx).  Not thread-safe; one per device."""
 
     def __init__(self, device=0, lib="libclyscan.so"):
+        self.lib_name = lib
         self.lib = _abi.load_scan_lib(lib)
         self.ctx = ctypes.c_void_p()
         rc = self.lib.cly_ctx_create(device, ctypes.byref(self.ctx))

@@ -586,16 +586,23 @@ k_mhint(const MEnt* __restrict__ e, const MCopy* __restrict__ cp, const cly_tupl
 
 // ---- k_mcopy: one 4-KiB destination block per wave ---------------------------
 // The wave loads the copy descriptors of the records covering its block into
-// LDS; lane l then writes the block's 16-B pieces l, l+64, l+128, l+192.  All
-// source loads of a lane are issued before any store (four pieces in flight).
-// A piece inside one record's body is 4-5 aligned dword loads funnel-shifted
-// into place (never a dword beyond the record's last byte); a piece that
-// straddles records, or touches a re-encoded prefix or the end of the file,
-// gathers its 16 bytes with independent byte loads.
+// LDS and builds the block's piece map: for each 16-B piece, the last record
+// starting at or before it (each record marks the first piece at or after its
+// start with an LDS max, then a prefix max over the 256 pieces: four per lane
+// plus a DPP max-scan across the wave).  Lane l then writes pieces l, l+64,
+// l+128, l+192 (each store instruction covers 1 KiB): a piece inside one
+// record's body is one dwordx4 load at a dword-aligned address (+ one dword
+// when the source is not dword-aligned) funnel-shifted into place, all issued
+// before any store; a lane's first piece across two records is assembled
+// from two partial loads; any other piece (more than one boundary, a
+// re-encoded prefix, the end of the file, an append's kept bytes) gathers its
+// 16 bytes one by one.
 __device__ const uint8_t g_zero_byte = 0;
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));   // 16 B, dword-aligned
+typedef uint32_t mc_u32x4 __attribute__((ext_vector_type(4)));
 #define MC_W 4                                   // waves per workgroup
 #define MC_P (M_CB / 16 / 64)                    // pieces per lane
+#define MC_NPIECE (M_CB / 16)
 __device__ __forceinline__ void mc_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -628,6 +635,20 @@ __device__ __forceinline__ void mc_join(const uint32_t (&x)[4], const uint32_t (
         o[j] = (x[j] & mk) | (sj & ~mk);
     }
 }
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ uint32_t mc_dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xf, false);
+}
+// inclusive max over the wave (DPP row shifts and row broadcasts; 0 = identity)
+__device__ __forceinline__ uint32_t mc_wave_max_incl(uint32_t v) {
+    v = max(v, mc_dpp<0x111>(v));
+    v = max(v, mc_dpp<0x112>(v));
+    v = max(v, mc_dpp<0x114>(v));
+    v = max(v, mc_dpp<0x118>(v));
+    v = max(v, mc_dpp<0x142, 0xa>(v));
+    v = max(v, mc_dpp<0x143, 0xc>(v));
+    return v;
+}
 
 // Template over the descriptor capacity per block (CMAX) and the prefix stride
 // (PRE); lo0 = first byte of region 0 that belongs to the output (appends
@@ -638,15 +659,13 @@ __global__ void __launch_bounds__(64 * MC_W, 4)
 k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uint32_t* __restrict__ bmap,
         const uint64_t* __restrict__ fstart, const uint64_t* __restrict__ flen, uint64_t stride,
         uint64_t nblocks, uint8_t* out, uint64_t lo0) {
-    __shared__ int32_t s_rel[MC_W][CMAX];
-    __shared__ uint64_t s_src[MC_W][CMAX];
-    __shared__ uint32_t s_end[MC_W][CMAX];
+    __shared__ mc_u32x4 s_desc[MC_W][CMAX];              // source (lo, hi), rel (dst - block start), size
     __shared__ uint8_t s_pre[MC_W][CMAX];
+    __shared__ mc_u32x4 s_map[MC_W][MC_NPIECE / 4];      // piece -> descriptor
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;   // (scalar: block indices in SGPRs)
-    int32_t* rel = s_rel[w];
-    uint64_t* srcs = s_src[w];
-    uint32_t* sizes = s_end[w];
+    mc_u32x4* desc = s_desc[w];
     uint8_t* pres = s_pre[w];
+    uint32_t* map = (uint32_t*)s_map[w];
     const uint64_t bpf = stride / M_CB;
     for (uint64_t b = (uint64_t)blockIdx.x * MC_W + w; b < nblocks; b += (uint64_t)gridDim.x * MC_W) {
         const uint64_t k = b / bpf;
@@ -660,107 +679,114 @@ k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uin
         uint32_t cnt = (uint32_t)(j1 - j0);
         if (cnt > CMAX) cnt = CMAX;
         mc_wave_sync();                                         // previous block's readers are done
+        s_map[w][lane] = (mc_u32x4){0u, 0u, 0u, 0u};
+        mc_wave_sync();
         for (uint32_t q = lane; q < cnt; q += 64) {
             const MCopy c = cp[j0 + q];
-            rel[q] = (int32_t)((int64_t)c.dst - (int64_t)B);   // >= -(record size) > -2^31
-            srcs[q] = c.src;
-            sizes[q] = c.size;
+            const int32_t rel = (int32_t)((int64_t)c.dst - (int64_t)B);   // >= -(record size) > -2^31
+            desc[q] = (mc_u32x4){(uint32_t)c.src, (uint32_t)(c.src >> 32), (uint32_t)rel, c.size};
             pres[q] = (uint8_t)c.pre;
+            const int32_t pi = rel <= 0 ? 0 : (rel + 15) >> 4;  // the first piece at or after the record's start
+            if (pi < MC_NPIECE) __atomic_fetch_max(map + pi, q, __ATOMIC_RELAXED);
         }
         mc_wave_sync();
+        {
+            mc_u32x4 v = s_map[w][lane];
+            v.y = max(v.y, v.x); v.z = max(v.z, v.y); v.w = max(v.w, v.z);
+            const uint32_t incl = mc_wave_max_incl(v.w);
+            const uint32_t ex = mc_dpp<0x138>(incl);            // lane - 1's (lane 0: 0)
+            v.x = max(v.x, ex); v.y = max(v.y, ex); v.z = max(v.z, ex); v.w = max(v.w, ex);
+            s_map[w][lane] = v;
+        }
+        mc_wave_sync();
+        const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(out + B, (short)0, (int)M_CB, 0x00020000);
         uint32_t a[MC_P][5];
-        uint32_t fast = 0, gather = 0, shs = 0;
-        int st_p = -1, st_n = 0;                                // the lane's (first) two-record piece
-        uint32_t xa[4], xb[4];
+        uint32_t fast = 0, slow = 0, shs = 0;
         #pragma unroll
         for (int p = 0; p < MC_P; p++) {
-            const int d = (p * 64 + lane) * 16;
+            const int P = p * 64 + lane, d = P * 16;
             if (fo + (uint64_t)d >= L || fo + (uint64_t)d + 16 <= keep) continue;
-            if (fo + (uint64_t)d < keep) { gather |= 1u << p; continue; }
-            int lo = 0, hi = (int)cnt - 1;                      // last record with rel <= d
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (rel[mid] <= d) lo = mid; else hi = mid - 1;
-            }
-            const int r0 = d - rel[lo];
-            const int pr = pres[lo];
-            if (r0 >= pr && (int64_t)r0 + 16 <= (int64_t)sizes[lo]) {
-                const uint64_t sa = srcs[lo] + (uint64_t)(r0 - pr);
+            if (fo + (uint64_t)d < keep) { slow |= 1u << p; continue; }
+            const uint32_t r = map[P];
+            const mc_u32x4 D = desc[r];
+            const int r0 = d - (int32_t)D.z, pr = pres[r];
+            if (r0 >= pr && (int64_t)r0 + 16 <= (int64_t)D.w) {
+                const uint64_t sa = (((uint64_t)D.y << 32) | D.x) + (uint64_t)(r0 - pr);
                 const CLY_GLB uint32_t* wp = (const CLY_GLB uint32_t*)(sa & ~3ull);
                 const u32x4a v4 = *(const CLY_GLB u32x4a*)wp;  // one dwordx4 at a dword-aligned address
                 a[p][0] = v4.x; a[p][1] = v4.y; a[p][2] = v4.z; a[p][3] = v4.w;
                 a[p][4] = (sa & 3) ? wp[4] : 0u;
                 fast |= 1u << p;
                 shs |= (uint32_t)(sa & 3) << (2 * p);
-                continue;
-            }
-            // a piece across one record boundary: the tail of record lo, the head
-            // of record lo+1 (each from its body or wholly from its prefix slot)
-            const int nA = (int)sizes[lo] - r0;
-            bool two = TWO && st_p < 0 && nA > 0 && nA < 16 && lo + 1 < (int)cnt && rel[lo + 1] == d + nA &&
-                       fo + (uint64_t)d + 16 <= L && (int)sizes[lo + 1] >= 16 - nA;
-            uint64_t sA = 0, sB = 0;
-            if (two) {
-                if (r0 >= pr) sA = srcs[lo] + (uint64_t)(r0 - pr);
-                else if (r0 + nA <= pr) sA = (uint64_t)(pre + (uint64_t)(j0 + lo) * PRE + r0);
-                else two = false;
-                const int pb = pres[lo + 1];
-                if (pb == 0) sB = srcs[lo + 1];
-                else if (pb >= 16 - nA) sB = (uint64_t)(pre + (uint64_t)(j0 + lo + 1) * PRE);
-                else two = false;
-            }
-            if (two) {
-                mc_part(sA, nA, xa);
-                mc_part(sB, 16 - nA, xb);
-                st_p = p;
-                st_n = nA;
             } else {
-                gather |= 1u << p;
+                slow |= 1u << p;
             }
         }
-        if (st_p >= 0) {
-            uint32_t o[4];
-            mc_join(xa, xb, st_n, o);
-            *(uint4*)(out + B + (st_p * 64 + lane) * 16) = make_uint4(o[0], o[1], o[2], o[3]);
+        // the lane's first slow piece: across exactly one record boundary, the
+        // tail of record r (body or prefix) then the head of record r + 1
+        if (TWO && slow) {
+            const int p = __builtin_ctz(slow);
+            const int P = p * 64 + lane, d = P * 16;
+            bool two = fo + (uint64_t)d >= keep && fo + (uint64_t)d + 16 <= L;
+            const uint32_t r = two ? map[P] : 0u;
+            two = two && r + 1 < cnt;
+            uint64_t sA = 0, sB = 0;
+            int nA = 0;
+            if (two) {
+                const mc_u32x4 D = desc[r], E = desc[r + 1];
+                const int r0 = d - (int32_t)D.z, pr = pres[r], pb = pres[r + 1];
+                nA = (int)D.w - r0;
+                two = nA > 0 && nA < 16 && (int32_t)E.z == d + nA && (int)E.w >= 16 - nA;
+                if (r0 >= pr) sA = (((uint64_t)D.y << 32) | D.x) + (uint64_t)(r0 - pr);
+                else if (r0 + nA <= pr) sA = (uint64_t)(pre + (uint64_t)(j0 + r) * PRE + r0);
+                else two = false;
+                if (pb == 0) sB = ((uint64_t)E.y << 32) | E.x;
+                else if (pb >= 16 - nA) sB = (uint64_t)(pre + (uint64_t)(j0 + r + 1) * PRE);
+                else two = false;
+            }
+            if (two) {
+                uint32_t xa[4], xb[4], o[4];
+                mc_part(sA, nA, xa);
+                mc_part(sB, 16 - nA, xb);
+                mc_join(xa, xb, nA, o);
+                __builtin_amdgcn_raw_buffer_store_b128((mc_u32x4){o[0], o[1], o[2], o[3]}, ors, d, 0, 0);
+                slow &= slow - 1;
+            }
         }
         #pragma unroll
         for (int p = 0; p < MC_P; p++) {
             if (!(fast & (1u << p))) continue;
             const int d = (p * 64 + lane) * 16;
             const uint32_t sh = ((shs >> (2 * p)) & 3) * 8;
-            uint32_t o[4];
-            #pragma unroll
-            for (int q = 0; q < 4; q++) o[q] = __builtin_amdgcn_alignbit(a[p][q + 1], a[p][q], sh);
-            *(uint4*)(out + B + d) = make_uint4(o[0], o[1], o[2], o[3]);
+            mc_u32x4 o;
+            o.x = __builtin_amdgcn_alignbit(a[p][1], a[p][0], sh);
+            o.y = __builtin_amdgcn_alignbit(a[p][2], a[p][1], sh);
+            o.z = __builtin_amdgcn_alignbit(a[p][3], a[p][2], sh);
+            o.w = __builtin_amdgcn_alignbit(a[p][4], a[p][3], sh);
+            __builtin_amdgcn_raw_buffer_store_b128(o, ors, d, 0, 0);
         }
         // gather pieces: byte q from its record (re-encoded prefix, body) or zero
         // past the file end; the 16 loads of a piece are issued together
         #pragma unroll 1
-        while (gather) {
-            const int p = __builtin_ctz(gather);
-            gather &= gather - 1;
+        while (slow) {
+            const int p = __builtin_ctz(slow);
+            slow &= slow - 1;
             const int d = (p * 64 + lane) * 16;
-            int jj = 0;
-            {
-                int lo = 0, hi = (int)cnt - 1;
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (rel[mid] <= d) lo = mid; else hi = mid - 1;
-                }
-                jj = lo;
-            }
+            int jj = (int)map[d >> 4];
             const uint8_t* bp[16];
             #pragma unroll
             for (int q = 0; q < 16; q++) {
                 const int pos = d + q;
-                while (jj + 1 < (int)cnt && rel[jj + 1] <= pos) jj++;
-                const int r = pos - rel[jj];
+                while (jj + 1 < (int)cnt && (int32_t)desc[jj + 1].z <= pos) jj++;
+                const mc_u32x4 D = desc[jj];
+                const int r = pos - (int32_t)D.z;
                 const uint8_t* ptr = &g_zero_byte;
                 if (fo + (uint64_t)pos < keep) {
                     ptr = out + B + pos;                        // an active file's existing bytes
-                } else if (fo + (uint64_t)pos < L && r >= 0 && (uint32_t)r < sizes[jj]) {
+                } else if (fo + (uint64_t)pos < L && r >= 0 && (uint32_t)r < D.w) {
                     const int pj = pres[jj];
-                    ptr = r < pj ? pre + (uint64_t)(j0 + jj) * PRE + r : (const uint8_t*)srcs[jj] + (r - pj);
+                    ptr = r < pj ? pre + (uint64_t)(j0 + jj) * PRE + r
+                                 : (const uint8_t*)(((uint64_t)D.y << 32) | D.x) + (r - pj);
                 }
                 bp[q] = ptr;
             }

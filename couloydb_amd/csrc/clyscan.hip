@@ -1484,39 +1484,50 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
 // k_emit: per tile (one wave, grid-stride), after the chain is final: the
 // tuples from the compact entries (64 per round: coalesced 16-B reads, the 48-B
 // tuples assembled in the wave's LDS and written as whole 1-KiB runs), and the
-// tile's CRC verdicts.
-//   The scan: lane L owns the run of RUN consecutive segments at L RUN_BYTES;
-//   a Horner pass over their registers gives the run as a function of the
-//   register entering it (x -> A^RUN_BYTES x ^ v, or a constant when the run
-//   holds the reset below), a Kogge-Stone scan over the lanes composes the
-//   runs, and a second Horner pass gives the register entering every segment
-//   (gin, LDS).  The stream is reset at the tile's first boundary G: past G's
-//   patch word the register is what it is when the record ending at G matches
-//   its CRC (k_fin checks that record: it knows the register entering the
-//   tile); so no state from earlier tiles is needed here.
-//   Record r of the tile ends at the patch word W of record r + 1; the register
-//   entering W is A^(W - segment start) gin ^ the snapshot, and must equal
-//   exp_pre (data/dataFile.go:105-109: the record's own CRC).  The record that
-//   ends at the chain's terminal matches iff the register at the tile's end is
-//   zero (every byte from the terminal on is zero, and its patch closes the
-//   record).  Outputs per tile for k_fin: the register at the tile's end (a
-//   tile with a boundary: under the reset; a tile without one: its own, from
-//   zero) and the straddling record's check value (dev).
+// tile's CRC verdicts from its segment registers (loaded into LDS) and the
+// records' snapshots.
+//   Past a record start P (patch word W) the stream's register, when every
+//   record before P matches its CRC, is known: XORing v = snapshot ^
+//   exp_pre(P) into the segment's own register at W gives it (the reset).  So
+//   record r is checked from its own segments alone: the reset exit of the
+//   segment holding W_r, Horner steps x -> A^64 x ^ S over the segments up to
+//   the one holding W_{r+1}, then A^(W_{r+1} - segment start) x ^ snapshot
+//   must equal exp_pre(P_{r+1}) (data/dataFile.go:105-109: the record's own
+//   CRC).  The record that ends at the chain's terminal matches iff the
+//   register is zero at the end of the terminal's segment (every byte from the
+//   terminal on is zero, and its patch closes the record).  The tile's first
+//   boundary G is reset the same way with the ~cq the tile could not know (the
+//   record ending at G is k_fin's: it knows the register entering the tile).
+//   Tiles of long records (one spanning more than SHORT_KMAX segments), of many
+//   short ones, without a record start, or whose compact list overflowed take
+//   the tile-wide scan instead: lane L owns the run of RUN consecutive
+//   segments at L RUN_BYTES; a Horner pass gives each run as a function of the
+//   register entering it (constant past the reset), a Kogge-Stone scan over
+//   the lanes composes them, a second Horner pass gives the register entering
+//   every segment (gin), and every record is checked from gin.
+//   Outputs per tile for k_fin: the register at the tile's end (a tile with a
+//   boundary: past the reset; a tile without one: its own, from zero) and the
+//   crossing record's check value dev.
 #define RUN (CLY_NBLK)                          // segments per lane in k_emit's scan
 #define RUN_BYTES (RUN * CLY_SEG)
 #define EMIT_WAVES 16
-#define GIN_WORDS (NSEG + 4)                    // the register entering each segment (+ the tile's end)
+#define SHORT_MAXN 256                          // records per tile of the per-record path
+#define SHORT_KMAX 32                           // segments one record may span there
+#define GIN_WORDS (NSEG + 4)                    // segment registers / the scan (+ the tile's end)
 #define TUP_BYTES (64 * 48)                     // a round's tuples
 #define EW_RAW (GIN_WORDS * 4 + TUP_BYTES > STG_BYTES ? GIN_WORDS * 4 + TUP_BYTES : STG_BYTES)
 #define EW_BYTES ((EW_RAW + 15) & ~15)
 #define EMIT_LDS (NEM * 128 * 4 + EMIT_WAVES * EW_BYTES)
 static_assert(CLY_NL * RUN == NSEG, "one run of segments per lane");
-__device__ __forceinline__ uint32_t gin_at(uint32_t sg) {      // LDS word of segment sg's entering register
+__device__ __forceinline__ uint32_t gin_at(uint32_t sg) {      // LDS word of segment sg (lane-transposed)
     return sg < NSEG ? (sg % RUN) * 64u + sg / RUN : NSEG;
 }
 // A^(4k) v, 0 <= k <= 16 (k = 16: the segment step A^64)
 __device__ __forceinline__ uint32_t em_f4(const CLY_LDS uint32_t* emt, uint32_t k, uint32_t v) {
     return k ? mat_mul(emt + (EM_F4 + k - 1u) * 128u, v) : v;
+}
+__device__ __forceinline__ uint32_t em_a64(const CLY_LDS uint32_t* emt, uint32_t v) {
+    return mat_mul(emt + (EM_F4 + 15) * 128, v);
 }
 // A^(4-j) v, 1 <= j <= 3
 __device__ __forceinline__ uint32_t em_fj(const CLY_LDS uint32_t* emt, uint32_t j, uint32_t v) {
@@ -1531,6 +1542,22 @@ __device__ __forceinline__ uint32_t exp_pre(const CLY_LDS uint32_t* emt, uint32_
 __device__ __forceinline__ uint32_t entry_crc(gbytes base, uint64_t len, uint32_t tb, const u32x4& v) {
     return (v.w & REC_SHORT) ? v.x : hdr_load(base, tb + (v.w & 0xFFFFu), len).crc;
 }
+__device__ __forceinline__ uint32_t patch_word_of(uint32_t P) { return (P & 3u) ? (P & ~3u) + 4u : P; }
+// the fields of record i's check (per-record path): its start's patch word
+// Wr in segment sa with reset value inj; its end W2 in segment sb (kind 1: a
+// record start, expected register expn, snapshot s2; kind 2: the terminal's
+// segment end, expected zero; kind 3: the tile's end)
+struct RecChk { uint32_t sa, sb, Wr, W2, inj, s2, expn, kind; };
+__device__ __forceinline__ uint32_t chk_eval(const CLY_LDS uint32_t* emt, const CLY_LDS uint32_t* gin,
+                                             const RecChk& q, uint32_t tb) {
+    // the register entering W2 (kind 1), or at the end of segment sb - 1 (kinds 2, 3)
+    if (q.sb == q.sa) return q.s2 ^ em_f4(emt, (q.W2 - q.Wr) >> 2, q.inj);
+    uint32_t x = gin[gin_at(q.sa)] ^ em_f4(emt, (64u * (q.sa + 1u) - (q.Wr - tb)) >> 2, q.inj);
+    const uint32_t steps = q.sb - q.sa - 1u;
+    for (uint32_t k = 0; __ballot(k < steps); k++)
+        if (k < steps) x = em_a64(emt, x) ^ gin[gin_at(q.sa + 1u + k)];
+    return em_f4(emt, (q.W2 - tb - 64u * q.sb) >> 2, x) ^ q.s2;
+}
 __global__ void __launch_bounds__(64 * EMIT_WAVES)
 k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
        const TileIn* __restrict__ tin, const TileLocal* __restrict__ loc, const uint32_t* __restrict__ rec,
@@ -1543,7 +1570,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     for (int i = threadIdx.x; i < NEM * 128; i += blockDim.x) emt[i] = tabs[TAB_EM + i];
     __syncthreads();
     CLY_LDS uint8_t* wreg = (CLY_LDS uint8_t*)smem_raw + NEM * 128 * 4 + wave_id() * EW_BYTES;
-    CLY_LDS uint32_t* gin = (CLY_LDS uint32_t*)wreg;                  // the scan (tiles with compact entries)
+    CLY_LDS uint32_t* gin = (CLY_LDS uint32_t*)wreg;                  // segment registers, then the scan
     CLY_LDS u32x4* sv = (CLY_LDS u32x4*)(wreg + GIN_WORDS * 4);       // a round's tuples
     CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)wreg;                  // the re-walk's stage (overflowed tiles)
     const int lane = threadIdx.x & 63;
@@ -1556,15 +1583,37 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         FileInfo* fo = &finfo[f];
         const uint64_t gb = S.count + fo->first_index;
         const u64 l0 = loc[t].l[0], l1 = loc[t].l[1], l3 = loc[t].l[3];
-        const uint32_t tt = t - F.first_tile, tb = (uint32_t)((uint64_t)tt * CLY_TILE);
+        const uint32_t tt = t - F.first_tile, tb = (uint32_t)((uint64_t)tt * CLY_TILE), TE = tb + (uint32_t)CLY_TILE;
         const uint32_t n = (uint32_t)(l0 >> 32);
         const uint32_t skip = (uint32_t)(l3 >> 40) & 0xFFFFu;              // k_refix's suffix (records dropped)
         const gbytes base = (gbytes)F.base;
-        const bool none = (l0 & DF_NONE) != 0, term = (l0 & DF_TERM) != 0;
+        const bool none = (l0 & DF_NONE) != 0, term = (l0 & DF_TERM) != 0, ovfl = (l0 & DF_OVF) != 0;
         const bool gterm = !none && term && n == 0;                         // the first boundary is the terminal
         const bool grec = !none && !gterm;                                  // ... a record start
+        const uint32_t T = (uint32_t)(l1 >> 32);                            // the terminal (term)
         const uint32_t* trec = rec + ((uint64_t)t * CAP_T + skip) * 4;
         const uint32_t* tsnap = snap + (uint64_t)t * SNAP_T + skip;
+        const uint32_t cout = treg[2 * t];                                  // the register XOR due at the tile's end
+        // the tile's segment registers into LDS (lane-transposed: lane L's run)
+        uint32_t sr[RUN];
+        {
+            const uint32_t* sp = seg + (uint64_t)t * NSEG + (uint32_t)lane * RUN;
+            if (RUN % 4 == 0) {
+                #pragma unroll
+                for (int k = 0; k < RUN; k += 4) {
+                    const u32x4 q = *(const u32x4*)(sp + k);
+                    sr[k] = q.x; sr[k + 1 < RUN ? k + 1 : 0] = q.y;
+                    sr[k + 2 < RUN ? k + 2 : 0] = q.z; sr[k + 3 < RUN ? k + 3 : 0] = q.w;
+                }
+            } else {
+                #pragma unroll
+                for (int k = 0; k < RUN; k++) sr[k] = sp[k];
+            }
+            #pragma unroll
+            for (int k = 0; k < RUN; k++) gin[k * 64 + lane] = sr[k];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
         // ---- G (a record start): its patch word WG, the register entering WG
         // when the record ending at G matches (expG), and injG: what the reset
         // XORs in at WG relative to the tile's own stream (expG ^ the snapshot
@@ -1575,7 +1624,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             const u32x4 vg = *(const u32x4*)trec;
             const uint32_t cG = entry_crc(base, F.len, tb, vg);
             const uint32_t jG = G & 3u;
-            WG = jG ? (G & ~3u) + 4u : G;
+            WG = patch_word_of(G);
             sigG = (WG - tb) >> 6;
             sG = tsnap[0];
             if (tt > 0) {
@@ -1587,62 +1636,24 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             }
             injG = expG ^ sG ^ DG;
         }
-        // ---- the scan
-        uint32_t sr[RUN];
-        {
-            const uint32_t* sp = seg + (uint64_t)t * NSEG + (uint32_t)lane * RUN;
-            #pragma unroll
-            for (int k = 0; k < RUN; k += 4) {
-                const u32x4 q = *(const u32x4*)(sp + k);
-                sr[k] = q.x; sr[k + 1] = q.y; sr[k + 2] = q.z; sr[k + 3] = q.w;
-            }
+        bool full = !grec || ovfl || n > SHORT_MAXN || sigG >= NSEG || (tt > 0 && sigG > SHORT_KMAX);
+        uint32_t ex = 0, dev = 0;
+        if (!full && tt > 0) {
+            // the tile's own register entering WG (from zero at the tile's start)
+            uint32_t x = 0;
+            for (uint32_t k = 0; k < sigG; k++) x = em_a64(emt, x) ^ gin[gin_at(k)];
+            dev = em_f4(emt, (WG - tb - 64u * sigG) >> 2, x) ^ sG ^ expG;
         }
-        // the exit register of segment sigG under the reset: its register from
-        // zero, with injG XORed in before WG (= A^(segment end - WG) injG)
-        const uint32_t xG = grec && sigG < NSEG ? em_f4(emt, (64u * (sigG + 1u) - (WG - tb)) >> 2, injG) : 0u;
-        uint32_t x = 0, rc = 0;
-        #pragma unroll
-        for (int k = 0; k < RUN; k++) {
-            const uint32_t sg = (uint32_t)lane * RUN + k;
-            if (sg == sigG) { x = sr[k] ^ xG; rc = 1; }
-            else x = mat_mul(emt + (EM_F4 + 15) * 128, x) ^ sr[k];
-        }
-        #pragma unroll
-        for (int l = 0; l < 6; l++) {
-            const int d = 1 << l;
-            const uint32_t px = (uint32_t)__shfl_up((int)x, d, 64), pc = (uint32_t)__shfl_up((int)rc, d, 64);
-            if (lane >= d && !rc) { x = mat_mul(emt + (EM_RUN + l) * 128, px) ^ x; rc = pc; }
-        }
-        uint32_t y = (uint32_t)__shfl_up((int)x, 1, 64), Lg = 0;
-        if (lane == 0) y = 0;
-        #pragma unroll
-        for (int k = 0; k < RUN; k++) {
-            const uint32_t sg = (uint32_t)lane * RUN + k;
-            gin[k * 64 + lane] = y;
-            if (sg == sigG) { Lg = em_f4(emt, (WG - tb - 64u * sg) >> 2, y) ^ sG; y = sr[k] ^ xG; }
-            else y = mat_mul(emt + (EM_F4 + 15) * 128, y) ^ sr[k];
-        }
-        const uint32_t gte = rdl(y, 63);                                    // the register at the tile's end
-        if (lane == 0) gin[NSEG] = gte;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t cout = treg[2 * t];                                  // the register XOR due at the tile's end
-        uint32_t ex = gte, dev = 0;
-        if (gterm) { ex = 0; dev = gte ^ cout; }
-        else if (grec) {
-            const uint32_t LG = sigG < NSEG ? rdl(Lg, (int)(sigG / RUN)) : gte ^ sG;   // the tile's own register entering WG
-            ex = sigG < NSEG ? gte ^ cout : expG ^ cout ^ DG;
-            dev = LG ^ expG;
-            if (term && ex != 0u && lane == 0)                              // the record ending at the terminal
-                atomicMin(&fo->fail_key, ((u64)(uint32_t)(loc[t].l[2] >> 32) << 32) | (S.count + n - 1));
-        }
-        // ---- tuples, and the records that end inside the tile
-        if (!(l0 & DF_OVF)) {
+        // ---- tuples, and on the per-record path the records' checks
+        if (!ovfl) {
             for (uint32_t i0 = 0; i0 < n; i0 += 64) {
                 const uint32_t i = i0 + lane;
+                RecChk q = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+                uint32_t p = 0;
                 if (i < n) {
                     const u32x4 v = *(const u32x4*)(trec + 4 * i);
-                    const uint32_t rel = v.w & 0xFFFFu, p = tb + rel;
+                    const uint32_t rel = v.w & 0xFFFFu;
+                    p = tb + rel;
                     u32x4 a, b, c;
                     if (v.w & REC_SHORT) {
                         const uint32_t ks = v.y & 0xFFFFFFu, hsz = 6u + ((v.y >> 24) & 31u), type = v.y >> 29;
@@ -1656,16 +1667,41 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                         tuple_words(base, p, h, F.fid, a, b, c);
                     }
                     sv[3 * lane] = a; sv[3 * lane + 1] = b; sv[3 * lane + 2] = c;
-                    if (i + 1 < n) {
-                        // record i ends at record i + 1's patch word W
-                        const u32x4 v2 = *(const u32x4*)(trec + 4 * (i + 1));
-                        const uint32_t P2 = tb + (v2.w & 0xFFFFu), j = P2 & 3u;
-                        const uint32_t W = j ? (P2 & ~3u) + 4u : P2, sg = (W - tb) >> 6;
-                        const uint32_t bv = sg == sigG ? injG : gin[gin_at(sg)];
-                        const uint32_t k4 = sg == sigG ? (W - WG) >> 2 : (W - tb - 64u * sg) >> 2;
-                        const uint32_t pre = em_f4(emt, k4, bv) ^ tsnap[i + 1];
-                        if (pre != exp_pre(emt, j, c.w, entry_crc(base, F.len, tb, v2)))
+                    if (!full) {
+                        const uint32_t cr = c.w;                            // this record's stored CRC
+                        q.Wr = patch_word_of(p);
+                        q.sa = (q.Wr - tb) >> 6;
+                        if (i == 0) q.inj = injG;
+                        else q.inj = tsnap[i] ^ exp_pre(emt, p & 3u, entry_crc(base, F.len, tb,
+                                                                           *(const u32x4*)(trec + 4 * (i - 1))), cr);
+                        if (i + 1 < n) {                                    // ends at the next record's patch word
+                            const u32x4 v2 = *(const u32x4*)(trec + 4 * (i + 1));
+                            const uint32_t P2 = tb + (v2.w & 0xFFFFu);
+                            q.W2 = patch_word_of(P2);
+                            q.sb = (q.W2 - tb) >> 6;
+                            q.s2 = tsnap[i + 1];
+                            q.expn = exp_pre(emt, P2 & 3u, cr, entry_crc(base, F.len, tb, v2));
+                            q.kind = 1;
+                        } else if (term && T < TE) {                        // at the terminal's segment end
+                            q.sb = (((T & ~3u) - tb) >> 6) + 1u;
+                            q.W2 = tb + 64u * q.sb;
+                            q.kind = 2;
+                        } else {                                            // at the tile's end
+                            q.sb = NSEG;
+                            q.W2 = TE;
+                            q.kind = 3;
+                        }
+                    }
+                }
+                if (!full) {
+                    if (__ballot(q.kind != 0 && q.sb > q.sa + SHORT_KMAX + 1u)) full = true;     // (uniform)
+                    else {
+                        const uint32_t val = q.kind ? chk_eval(emt, gin, q, tb) : 0u;
+                        if ((q.kind == 1 && val != q.expn) || (q.kind == 2 && val != 0u) ||
+                            (q.kind == 3 && term && (val ^ cout) != 0u))
                             atomicMin(&fo->fail_key, ((u64)p << 32) | (S.count + i));
+                        const u64 bl = __ballot(q.kind == 3);
+                        if (bl) ex = rdl(val, __ffsll((long long)bl) - 1) ^ cout;
                     }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1675,9 +1711,9 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                 CLY_GL u32x4* dst = (CLY_GL u32x4*)(out + gb + i0);
                 #pragma unroll
                 for (int k = 0; k < 3; k++) {
-                    const uint32_t q = (uint32_t)lane + 64u * k;
-                    if (q < 3 * nr) {
-                        if (gb + i0 + q / 3 < out_cap) dst[q] = sv[q];
+                    const uint32_t qq = (uint32_t)lane + 64u * k;
+                    if (qq < 3 * nr) {
+                        if (gb + i0 + qq / 3 < out_cap) dst[qq] = sv[qq];
                         else atomicOr(&g->overflow, 1u);
                     }
                 }
@@ -1693,12 +1729,70 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                 const uint32_t k = atomicAdd(&g->n_ovf, 1u);
                 ovf[k] = (u32x4){(uint32_t)f, n, (uint32_t)gb, (uint32_t)(gb >> 32)};
             }
+            // the segment registers again (the re-walk used this LDS as its stage)
+            #pragma unroll
+            for (int k = 0; k < RUN; k++) gin[k * 64 + lane] = sr[k];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (full) {
+            // ---- the tile-wide scan; the exit register of segment sigG under
+            // the reset: its register from zero, with injG XORed in before WG
+            const uint32_t xG = grec && sigG < NSEG ? em_f4(emt, (64u * (sigG + 1u) - (WG - tb)) >> 2, injG) : 0u;
+            uint32_t x = 0, rc = 0;
+            #pragma unroll
+            for (int k = 0; k < RUN; k++) {
+                const uint32_t sg = (uint32_t)lane * RUN + k;
+                if (sg == sigG) { x = sr[k] ^ xG; rc = 1; }
+                else x = em_a64(emt, x) ^ sr[k];
+            }
+            #pragma unroll
+            for (int l = 0; l < 6; l++) {
+                const int d = 1 << l;
+                const uint32_t px = (uint32_t)__shfl_up((int)x, d, 64), pc = (uint32_t)__shfl_up((int)rc, d, 64);
+                if (lane >= d && !rc) { x = mat_mul(emt + (EM_RUN + l) * 128, px) ^ x; rc = pc; }
+            }
+            uint32_t y = (uint32_t)__shfl_up((int)x, 1, 64), Lg = 0;
+            if (lane == 0) y = 0;
+            #pragma unroll
+            for (int k = 0; k < RUN; k++) {
+                const uint32_t sg = (uint32_t)lane * RUN + k;
+                gin[k * 64 + lane] = y;
+                if (sg == sigG) { Lg = em_f4(emt, (WG - tb - 64u * sg) >> 2, y) ^ sG; y = sr[k] ^ xG; }
+                else y = em_a64(emt, y) ^ sr[k];
+            }
+            const uint32_t gte = rdl(y, 63);                                // the register at the tile's end
+            if (lane == 0) gin[NSEG] = gte;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            ex = gte;
+            if (gterm) { ex = 0; dev = gte ^ cout; }
+            else if (grec) {
+                const uint32_t LG = sigG < NSEG ? rdl(Lg, (int)(sigG / RUN)) : gte ^ sG;   // the tile's own register entering WG
+                ex = sigG < NSEG ? gte ^ cout : expG ^ cout ^ DG;
+                dev = LG ^ expG;
+                if (term && ex != 0u && lane == 0)                          // the record ending at the terminal
+                    atomicMin(&fo->fail_key, ((u64)(uint32_t)(loc[t].l[2] >> 32) << 32) | (S.count + n - 1));
+                if (!ovfl) {
+                    // every record that ends at a record start inside the tile
+                    for (uint32_t i = lane; i + 1 < n; i += 64) {
+                        const u32x4 v = *(const u32x4*)(trec + 4 * i), v2 = *(const u32x4*)(trec + 4 * (i + 1));
+                        const uint32_t p = tb + (v.w & 0xFFFFu), P2 = tb + (v2.w & 0xFFFFu);
+                        const uint32_t W = patch_word_of(P2), sg = (W - tb) >> 6;
+                        const uint32_t bv = sg == sigG ? injG : gin[gin_at(sg)];
+                        const uint32_t k4 = sg == sigG ? (W - WG) >> 2 : (W - tb - 64u * sg) >> 2;
+                        const uint32_t pre = em_f4(emt, k4, bv) ^ tsnap[i + 1];
+                        if (pre != exp_pre(emt, P2 & 3u, entry_crc(base, F.len, tb, v), entry_crc(base, F.len, tb, v2)))
+                            atomicMin(&fo->fail_key, ((u64)p << 32) | (S.count + i));
+                    }
+                }
+            }
         }
         if (lane == 0) {
             treg[2 * t] = ex;
             treg[2 * t + 1] = dev;
             if (term) {
-                fo->term_pos = (uint32_t)(l1 >> 32);
+                fo->term_pos = T;
                 fo->term_status = (int32_t)(int8_t)(uint8_t)(l3 >> 32);
                 fo->term_tile = t;
                 fo->end_index = gb + n;

@@ -196,6 +196,43 @@ def test_false_starts_chaining_into_true_records(scanner, seed):
     compare(r.file_tuples(0), r.status[0], r.end_offset[0], t, st, end, "false starts %d" % seed)
 
 
+@pytest.mark.parametrize("nfalse", [3, 20])
+def test_refix_suffix_entry_at_sentinel_offset(scanner, nfalse):
+    """a record spanning many tiles ends exactly 0xFFFFF bytes past
+    the start of a middle tile that holds a short false chain (embedded
+    records).  The true entry of that tile is then tb + 0xFFFFF, the value the
+    suffix shortcut gave lanes without a compact entry; it must re-walk the
+    tile instead of taking the shortcut."""
+    import random
+
+    import make_golden as mg
+    tile = 8192 if "small" in scanner.lib_name else 65536
+    rng = random.Random(nfalse)
+    head = mg.encode_record(mg.key_tx(mg.test_key(0), 0), rng.randbytes(100))
+    t = 2                                                     # the middle tile
+    tb = t * tile
+    key = mg.key_tx(mg.test_key(1), 0)
+    vlen = tb + 0xFFFFF - len(head) - len(key)
+    for _ in range(3):                                        # the header's length depends on vlen's varint
+        hdr = len(mg.encode_record(key, b"")) - 1 + len(mg.put_varint(vlen)) - len(key)
+        vlen = tb + 0xFFFFF - len(head) - hdr - len(key)
+    vstart = len(head) + hdr + len(key)
+    value = bytearray(rng.randbytes(vlen))
+    emb = b"".join(mg.encode_record(mg.key_tx(mg.test_key(900 + j), 0), rng.randbytes(rng.randrange(5, 60)))
+                   for j in range(nfalse))
+    o = tb + 40 - vstart
+    value[o:o + len(emb)] = emb
+    big = mg.encode_record(key, bytes(value))
+    tail = mg.encode_record(mg.key_tx(mg.test_key(2), 0), b"after")
+    data = np.frombuffer(head + big + tail, np.uint8).copy()
+    assert len(head) + len(big) == tb + 0xFFFFF
+    f = DataFile(data, 6)
+    r = scanner.scan([f])
+    tt, st, end = co.scan_file(data, 6)
+    assert st == 0 and len(tt) == 3
+    compare(r.file_tuples(0), r.status[0], r.end_offset[0], tt, st, end, "sentinel %d" % nfalse)
+
+
 def test_bitflips_everywhere_small(scanner):
     base = fixed_records_file(60, 200, seed=5)
     rng = np.random.default_rng(0)
@@ -360,6 +397,30 @@ def test_config3_device_generated_properties():
         t, st_o, end = co.scan_file(wl.file_bytes(i), fid)
         got = wl.d_out[first[i] * 48:(first[i] + res[i].n_records) * 48].cpu().numpy().view(TUPLE_DTYPE)
         compare(got, res[i].status, res[i].end_offset, t, st_o, end, "c3 file %d" % i)
+
+
+@pytest.mark.slow
+def test_config5_per_gpu_share_properties():
+    """BASELINE config 5's per-GPU share (one rank's 32-GiB fid range of the
+    256-GiB C2/C3 mix, 128 files), generated in HBM exactly as bench.py --config
+    c5 builds it: the size-independent properties over every file, and the
+    first file, the file holding the largest record and the last file bit-exact
+    against the oracle."""
+    torch = pytest.importorskip("torch")
+    from bench import make_workload
+    wl = make_workload("c5", torch)
+    assert 120 <= len(wl.dev_files) <= 136 and wl.bytes > 31.9 * 2**30
+    with Scanner(0) as sc:
+        first, res, st, need = sc.scan_device(wl.dev_files, wl.d_out.data_ptr(), wl.out_cap)
+    _device_file_checks(torch, wl, first, res, need)
+    vs = wl.d_out[: need * 48].view(torch.int32).view(need, 12)[:, 9]
+    big = int(torch.argmax(vs).item())
+    fbig = max(i for i in range(len(first)) if first[i] <= big)
+    for i in sorted({0, fbig, len(wl.dev_files) - 1}):
+        ptr, ln, fid = wl.dev_files[i]
+        t, st_o, end = co.scan_file(wl.file_bytes(i), fid)
+        got = wl.d_out[first[i] * 48:(first[i] + res[i].n_records) * 48].cpu().numpy().view(TUPLE_DTYPE)
+        compare(got, res[i].status, res[i].end_offset, t, st_o, end, "c5 file %d" % i)
 
 
 @pytest.mark.gpu
