@@ -198,17 +198,6 @@ __device__ __forceinline__ uint32_t crc_unbytes(const CLY_LDS uint8_t* smem, uin
     for (uint32_t k = 0; k < j; k++) d = crc_unbyte(smem, d, r4);
     return d;
 }
-// A^k d (k < 4 zero bytes forwards): (d >> 8k) ^ sum_{i<k} T_{k-1-i}[byte i of d],
-// k independent lookups (T_t = the slicing tables, dword (i*64 + t*16 + r))
-__device__ __forceinline__ uint32_t crc_fwd(const CLY_LDS uint8_t* smem, uint32_t d, uint32_t k, uint32_t r4) {
-    const uint32_t b0 = d & 0xffu, b1 = (d >> 8) & 0xffu, b2 = (d >> 16) & 0xffu;
-    const uint32_t t = k - 1u;                                    // table of byte 0 (k >= 1)
-    uint32_t v = k == 3u ? d >> 24 : (k == 2u ? d >> 16 : d >> 8);
-    v ^= *(const CLY_LDS uint32_t*)(smem + ((b0 << 8) | (t << 6) | r4));
-    if (k >= 2u) v ^= *(const CLY_LDS uint32_t*)(smem + ((b1 << 8) | ((t - 1u) << 6) | r4));
-    if (k >= 3u) v ^= *(const CLY_LDS uint32_t*)(smem + ((b2 << 8) | r4));
-    return v;
-}
 // M v by a nibble table of M
 __device__ __forceinline__ uint32_t mat_mul(const CLY_LDS uint32_t* t, uint32_t v) {
     uint32_t p = 0;
@@ -617,25 +606,23 @@ __device__ __forceinline__ void patch_word(uint32_t (&w)[16], uint32_t k, uint32
 //   BM_EXACT  k_refix: the entry is the true state from k_link;
 //   BM_EMIT   k_emit: as BM_EXACT, tuples straight to their output slots (tiles
 //             whose compact list overflowed), no CRC.
-// CRC (not BM_EMIT): the record start P (stored CRC c, the record before it
-// stored cq) changes the file's byte stream, as the CRC register sees it, by
-// one register XOR d = c ^ K4 ^ ~cq before byte P (c zeroes the stored bytes,
-// K4 = A^-4 0xFFFFFFFF starts the record's CRC at P+4, ~cq closes the record
-// ending at P; no ~cq at P = 0); it goes into the data as A^(4-j) d into the
-// word after P's (j = P & 3; into P's own word when j = 0): the patch word
-// W(P).  At the chain's terminal T: ~cq of the last record before T, and every
-// byte from T on zeroed.  In this patched stream the register entering W(P),
-// when every record before P matches its CRC, is a known value exp_pre(P)
-// (~cq, or A^(4-j) (~cq ^ the j-byte-shifted head of c)); so record i matches
-// iff the register entering W(P_{i+1}) is exp_pre(P_{i+1}), and the last one
-// iff the register is zero after T.  Each lane runs its 64-B segment from a
-// zero register and keeps, for every patch word in it, the register before
-// that word (the snapshot); the register of the stream at any patch word is
-// then A^(W - segment start) (the stream register entering the segment) ^ the
-// snapshot, and the stream registers entering the segments follow from the
-// segment registers alone (k_emit's scan).  The ~cq of the tile's FIRST
-// boundary (tiles other than a file's first) needs the state entering the
-// tile: the tile XORs 0xFFFFFFFF there and k_emit accounts for the difference.
+// CRC (not BM_EMIT): GetLogRecordCRC of the record at P is the CRC-32 of
+// F[P+4 : P+size] (data/logRecord.go:136-146).  In the CRC register's terms
+// the stream from P on, started from the register c ^ K4 (c = the stored CRC
+// at P, K4 = A^-4 0xFFFFFFFF), holds 0xFFFFFFFF after the 4 stored bytes and
+// ~crc at the record's end; the record matches iff that register is ~c there.
+// Each lane runs its 64-B segment's raw words from a zero register (the
+// segment register S) and keeps, at every record start's patch word W (P's
+// own word when P is word-aligned, else the next one), the register entering W
+// (the snapshot).  From these alone (linearity) k_emit gets the register
+// entering the next record's patch word as it is when the walk restarts at
+// P with the known register exp_post(P) entering W (the reset), and compares
+// it with the value a matching record leaves (exp_pre).  The chain's terminal
+// T is closed in the data instead: ~cq of the record before it is XORed in
+// before byte T and every byte from T on reads as zero, so the last record
+// matches iff the register is zero after T (the tile's first boundary XORs
+// 0xFFFFFFFF there when the record before it is in an earlier tile; k_fin
+// completes it).
 #define BM_SPEC 0
 #define BM_EXACT 1
 #define BM_EMIT 2
@@ -666,24 +653,18 @@ struct TState {
     uint32_t ref_s;              // the reference record's size (the stride)
     uint32_t ref1, ref2, ref3, msk1, msk2, msk3, rw1, rw2, rw3;
 };
-// The block's outputs for record k of a round (lane k); returns its CRC patch,
-// to be XORed into the stage word holding P (one writer per word: record
-// starts are >= 7 B apart) once no header read of the stage can still see
-// that word (the tail of the record before P shares it).
-// The register XOR d due before byte P goes into the data: into P's word as
-// is when P is word-aligned, else as A^(4 - (P & 3)) d into the word after
-// it (the register after P's word); pw = that word's index in the block
-// (1024: the next block's first word, carried).
+// The block's outputs for record k of a round (lane k): its compact entry
+// (k_scan, k_refix) or its tuple (k_emit's re-walk).  Returns the record's
+// patch word as an index in the block: the word whose entering register its
+// CRC check reads (P's own word when P is word-aligned, else the word after
+// it; PW_CARRY: the next block's first word).
 template <int BM>
 __device__ __forceinline__ uint32_t rec_out(const DevFile& F, gbytes base, uint32_t p, const Hdr& h, uint32_t idx,
-                                            uint32_t tb, uint32_t bs, uint32_t dq, const CLY_LDS uint8_t* smem,
-                                            const CrcLane& cl, uint32_t K4, rsrc_t trs, gtuples out,
-                                            uint64_t out_cap, uint64_t gbase, Globals* g, uint32_t& pw) {
-    if (BM == BM_EMIT) { put_tuple(out, gbase + idx, out_cap, base, p, h, F.fid, g); pw = 0; return 0u; }
+                                            uint32_t tb, uint32_t bs, rsrc_t trs, gtuples out, uint64_t out_cap,
+                                            uint64_t gbase, Globals* g) {
+    if (BM == BM_EMIT) { put_tuple(out, gbase + idx, out_cap, base, p, h, F.fid, g); return 0u; }
     if (idx < CAP_T) rec_store(trs, idx, h, p - tb);
-    const uint32_t d = h.crc ^ K4 ^ dq, j = p & 3u;
-    pw = ((p - bs) >> 2) + (j ? 1u : 0u);
-    return j ? crc_fwd(smem, d, 4u - j, cl.r4) : d;
+    return ((p - bs) >> 2) + ((p & 3u) ? 1u : 0u);
 }
 #define PW_CARRY (CLY_BLK / 4)
 // The block's patch-word mask (per wave, in LDS: bit k of word L = word k of
@@ -745,17 +726,12 @@ __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t 
         // the stored CRC of each record's predecessor
         const uint32_t up = dppu<DPP_WF_SR1>(0u, h.crc);
         const uint32_t dq = k == 0 ? (S.cq_known ? ~S.cq : 0xFFFFFFFFu) : ~up;
-        // every lane of the round has read its header: the patches may go in
-        uint32_t pw = 0, pv = 0;
+        uint32_t pw = 0;
         if (acc) {
-            pv = rec_out<BM>(F, base, (uint32_t)P, h, S.tcnt + k, tb, bs, P == 0 ? 0u : dq, smem, cl, K4, trs, out,
-                             out_cap, gbase, g, pw);
-            if (BM != BM_EMIT && pw < PW_CARRY) { stg[stg_dw(pw)] ^= pv; mark_pw(mk, pw); }
+            pw = rec_out<BM>(F, base, (uint32_t)P, h, S.tcnt + k, tb, bs, trs, out, out_cap, gbase, g);
+            if (BM != BM_EMIT && pw < PW_CARRY) mark_pw(mk, pw);
         }
-        if (BM != BM_EMIT) {
-            const u64 bc = __ballot(acc && pw == PW_CARRY);
-            if (bc) { S.carry_next ^= rdl(pv, __ffsll((long long)bc) - 1); S.cmark_next = true; }
-        }
+        if (BM != BM_EMIT && __ballot(acc && pw == PW_CARRY)) S.cmark_next = true;
         if (S.G == NONE32) S.G = (uint32_t)X;
         if (n) {
             const int kl = n - 1;
@@ -808,20 +784,15 @@ __device__ __forceinline__ void stride_round(const DevFile& F, TState& S, uint32
     const u64 bm = __ballot(!match);
     const uint32_t kb = bm ? (uint32_t)__ffsll((long long)bm) - 1 : 64u;
     if (kb == 0) return;
-    const uint32_t up = dppu<DPP_WF_SR1>(0u, crc);
-    const uint32_t dq = k == 0 ? (S.cq_known ? ~S.cq : 0xFFFFFFFFu) : ~up;
-    uint32_t pw = 0, pv = 0;
+    uint32_t pw = 0;
     if (k < kb) {
         if (S.tcnt + k < CAP_T)
             __builtin_amdgcn_raw_buffer_store_b128((u32x4){crc, S.rw1, S.rw2, (P - tb) | S.rw3}, trs,
                                                    (int)((S.tcnt + k) * 16u), 0, 0);
-        const uint32_t d = crc ^ K4 ^ dq, j = P & 3u;
-        pw = ((P - bs) >> 2) + (j ? 1u : 0u);
-        pv = j ? crc_fwd(smem, d, 4u - j, cl.r4) : d;
-        if (pw < PW_CARRY) { stg[stg_dw(pw)] ^= pv; mark_pw(mk, pw); }
+        pw = ((P - bs) >> 2) + ((P & 3u) ? 1u : 0u);
+        if (pw < PW_CARRY) mark_pw(mk, pw);
     }
-    const u64 bc = __ballot(k < kb && pw == PW_CARRY);
-    if (bc) { S.carry_next ^= rdl(pv, __ffsll((long long)bc) - 1); S.cmark_next = true; }
+    if (__ballot(k < kb && pw == PW_CARRY)) S.cmark_next = true;
     if (S.G == NONE32) S.G = X;
     S.last_crc = rdl(crc, (int)kb - 1);
     S.P_last = X + (kb - 1) * s;
@@ -1063,32 +1034,21 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                     const uint32_t lvp = dppu<DPP_WF_SR1>(0u, lv), lfp = dppu<DPP_WF_SR1>(0u, lf);
                     uint32_t pcq = lfp ? lvp : S.cq;
                     bool pk = lfp ? true : S.cq_known;
-                    // the lane's records: outputs and CRC patches (headers from the stage)
-                    // (the patch of a lane's first record waits for the loop's end: the
-                    // lane before reads its last header, whose tail shares that word,
-                    // in a later iteration)
-                    uint32_t p = L.E, psz = 0, ppsz = 0, p0w = PW_CARRY + 1, p0v = 0, cv = 0;
+                    // the lane's records: outputs and patch-word marks (headers from the stage)
+                    uint32_t p = L.E, psz = 0, ppsz = 0;
                     bool cf = false;
                     for (uint32_t i = 0; __ballot(i < c); i++) {
                         if (i < c) {
                             const Hdr h = hdr_get(p, flen, stg, bs);
-                            uint32_t pw;
-                            const uint32_t pv = rec_out<BM>(F, base, p, h, S.tcnt + lex + i, tb, bs,
-                                                            p == 0 ? 0u : (pk ? ~pcq : 0xFFFFFFFFu), smem, cl, K4, trs,
-                                                            out, out_cap, gbase, g, pw);
-                            if (pw == PW_CARRY) { cv = pv; cf = true; }
-                            else if (i == 0) { p0w = pw; p0v = pv; }
-                            else if (BM != BM_EMIT) { stg[stg_dw(pw)] ^= pv; mark_pw(mk, pw); }
+                            const uint32_t pw = rec_out<BM>(F, base, p, h, S.tcnt + lex + i, tb, bs, trs, out,
+                                                            out_cap, gbase, g);
+                            if (BM != BM_EMIT) { if (pw == PW_CARRY) cf = true; else mark_pw(mk, pw); }
                             pcq = h.crc; pk = true;
                             ppsz = psz; psz = (uint32_t)h.size;
                             p += (uint32_t)h.size;
                         }
                     }
-                    if (BM != BM_EMIT) {
-                        if (p0w < PW_CARRY) { stg[stg_dw(p0w)] ^= p0v; mark_pw(mk, p0w); }
-                        const u64 bc = __ballot(cf);
-                        if (bc) { S.carry_next ^= rdl(cv, __ffsll((long long)bc) - 1); S.cmark_next = true; }
-                    }
+                    if (BM != BM_EMIT && __ballot(cf)) S.cmark_next = true;
                     if (kT < 64) {
                         const uint32_t T = rdl(L.x, kT);
                         const uint32_t dT = T == 0 ? 0u : (pk ? ~pcq : 0xFFFFFFFFu);
@@ -1113,15 +1073,6 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                         S.X = rdl(L.x, 63 - __clzll((long long)bcc));
                         if (bt) { S.dead = true; S.term = (int)rdl((uint32_t)L.term, kT); }
                     }
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (BM != BM_EMIT) {
-                #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const u32x4 v = sv[5 * lane + k];
-                    w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
                 }
             }
         }
@@ -1486,28 +1437,32 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
 // tuples assembled in the wave's LDS and written as whole 1-KiB runs), and the
 // tile's CRC verdicts from its segment registers (loaded into LDS) and the
 // records' snapshots.
-//   Past a record start P (patch word W) the stream's register, when every
-//   record before P matches its CRC, is known: XORing v = snapshot ^
-//   exp_pre(P) into the segment's own register at W gives it (the reset).  So
-//   record r is checked from its own segments alone: the reset exit of the
+//   The reset at a record start P (patch word W, stored CRC c): the register
+//   entering W as the walk restarts at P is exp_post(P) (c ^ K4 at P, then the
+//   4 - j bytes of c up to W), so XORing v = snapshot ^ exp_post into the
+//   segment's own register at W gives the stream's register from there on.
+//   Record r is checked from its own segments alone: the reset exit of the
 //   segment holding W_r, Horner steps x -> A^64 x ^ S over the segments up to
 //   the one holding W_{r+1}, then A^(W_{r+1} - segment start) x ^ snapshot
-//   must equal exp_pre(P_{r+1}) (data/dataFile.go:105-109: the record's own
-//   CRC).  The record that ends at the chain's terminal matches iff the
-//   register is zero at the end of the terminal's segment (every byte from the
-//   terminal on is zero, and its patch closes the record).  The tile's first
-//   boundary G is reset the same way with the ~cq the tile could not know (the
-//   record ending at G is k_fin's: it knows the register entering the tile).
+//   must equal exp_pre(P_{r+1}) = the register a matching record leaves there
+//   (~c_r at P_{r+1}, then the 4 - j bytes of c_{r+1}; data/dataFile.go:
+//   105-109).  The record that ends at the chain's terminal matches iff the
+//   register is zero at the end of the terminal's segment (k_scan closed it
+//   there).  The record that crosses into the tile is k_fin's, which knows the
+//   register entering the tile: the tile gives it its own register entering
+//   its first patch word (dev, with exp_pre folded in).
 //   Tiles of long records (one spanning more than SHORT_KMAX segments), of many
 //   short ones, without a record start, or whose compact list overflowed take
-//   the tile-wide scan instead: lane L owns the run of RUN consecutive
-//   segments at L RUN_BYTES; a Horner pass gives each run as a function of the
-//   register entering it (constant past the reset), a Kogge-Stone scan over
-//   the lanes composes them, a second Horner pass gives the register entering
-//   every segment (gin), and every record is checked from gin.
+//   the tile-wide scan instead: every segment whose last boundary is a record
+//   start gets its reset exit (a constant), lane L owns the run of RUN
+//   consecutive segments at L RUN_BYTES; a Horner pass gives each run as a
+//   function of the register entering it, a Kogge-Stone scan over the lanes
+//   composes them, a second Horner pass gives the register entering every
+//   segment (gin), and every record is checked from gin.
 //   Outputs per tile for k_fin: the register at the tile's end (a tile with a
-//   boundary: past the reset; a tile without one: its own, from zero) and the
-//   crossing record's check value dev.
+//   record start: past its last reset; a tile without one: its own, from
+//   zero; a tile whose compact list overflowed: none, k_ovf checks its
+//   records) and dev.
 #define RUN (CLY_NBLK)                          // segments per lane in k_emit's scan
 #define RUN_BYTES (RUN * CLY_SEG)
 #define EMIT_WAVES 16
@@ -1515,7 +1470,8 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
 #define SHORT_KMAX 32                           // segments one record may span there
 #define GIN_WORDS (NSEG + 4)                    // segment registers / the scan (+ the tile's end)
 #define TUP_BYTES (64 * 48)                     // a round's tuples
-#define EW_RAW (GIN_WORDS * 4 + TUP_BYTES > STG_BYTES ? GIN_WORDS * 4 + TUP_BYTES : STG_BYTES)
+#define FLG_BYTES (NSEG / 8)                    // segments that hold a reset (tile-wide scan)
+#define EW_RAW (GIN_WORDS * 4 + TUP_BYTES + FLG_BYTES > STG_BYTES ? GIN_WORDS * 4 + TUP_BYTES + FLG_BYTES : STG_BYTES)
 #define EW_BYTES ((EW_RAW + 15) & ~15)
 #define EMIT_LDS (NEM * 128 * 4 + EMIT_WAVES * EW_BYTES)
 static_assert(CLY_NL * RUN == NSEG, "one run of segments per lane");
@@ -1538,6 +1494,13 @@ __device__ __forceinline__ uint32_t em_fj(const CLY_LDS uint32_t* emt, uint32_t 
 // 4 - j first bytes of the new record's stored CRC c in the same word.
 __device__ __forceinline__ uint32_t exp_pre(const CLY_LDS uint32_t* emt, uint32_t j, uint32_t cq, uint32_t c) {
     return j ? em_fj(emt, j, ~cq ^ (c & ((1u << (8u * (4u - j))) - 1u))) : ~cq;
+}
+// The register entering the patch word of a record start P (stored CRC c) as
+// the walk restarts at P: c ^ K4 at P; for j != 0 the 4 - j bytes of c up to
+// the word boundary, A^(4-j) (c ^ K4 ^ (c's low bytes)) = (c >> 8 (4-j)) ^
+// A^(4-j) K4 (kj[j]).
+__device__ __forceinline__ uint32_t exp_post(uint32_t j, uint32_t c, const uint32_t (&kj)[4]) {
+    return j ? (c >> (8u * (4u - j))) ^ (j == 1 ? kj[1] : j == 2 ? kj[2] : kj[3]) : c ^ kj[0];
 }
 __device__ __forceinline__ uint32_t entry_crc(gbytes base, uint64_t len, uint32_t tb, const u32x4& v) {
     return (v.w & REC_SHORT) ? v.x : hdr_load(base, tb + (v.w & 0xFFFFu), len).crc;
@@ -1572,9 +1535,12 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     CLY_LDS uint8_t* wreg = (CLY_LDS uint8_t*)smem_raw + NEM * 128 * 4 + wave_id() * EW_BYTES;
     CLY_LDS uint32_t* gin = (CLY_LDS uint32_t*)wreg;                  // segment registers, then the scan
     CLY_LDS u32x4* sv = (CLY_LDS u32x4*)(wreg + GIN_WORDS * 4);       // a round's tuples
+    CLY_LDS uint32_t* flg = (CLY_LDS uint32_t*)(wreg + GIN_WORDS * 4 + TUP_BYTES);   // reset segments (bitmap)
     CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)wreg;                  // the re-walk's stage (overflowed tiles)
     const int lane = threadIdx.x & 63;
     const CrcLane cl = crc_lane(lane);
+    uint32_t kj[4];
+    kj[0] = CLY_K4; kj[1] = em_fj(emt, 1, CLY_K4); kj[2] = em_fj(emt, 2, CLY_K4); kj[3] = em_fj(emt, 3, CLY_K4);
     for (uint32_t t = blockIdx.x * EMIT_WAVES + wave_id(); t < ntiles; t += gridDim.x * EMIT_WAVES) {
         const int f = find_file(tprefix, nfiles, t);
         const DevFile F = files[f];
@@ -1614,27 +1580,15 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        // ---- G (a record start): its patch word WG, the register entering WG
-        // when the record ending at G matches (expG), and injG: what the reset
-        // XORs in at WG relative to the tile's own stream (expG ^ the snapshot
-        // ^ the difference between the ~cq the tile applied at G and the true one)
+        // ---- G (a record start): its patch word WG, its snapshot, and the
+        // register entering WG when the record ending at G matches (expG)
         const uint32_t G = (uint32_t)l1;
-        uint32_t WG = 0, sigG = NSEG + 1, expG = 0, injG = 0, DG = 0, sG = 0;
+        uint32_t WG = 0, sigG = NSEG + 1, expG = 0, sG = 0;
         if (grec) {
-            const u32x4 vg = *(const u32x4*)trec;
-            const uint32_t cG = entry_crc(base, F.len, tb, vg);
-            const uint32_t jG = G & 3u;
             WG = patch_word_of(G);
             sigG = (WG - tb) >> 6;
             sG = tsnap[0];
-            if (tt > 0) {
-                uint32_t dqa = 0xFFFFFFFFu;                                 // guess mode / k_refix: cq unknown at G
-                if (skip) dqa = ~entry_crc(base, F.len, tb, *(const u32x4*)(trec - 4));   // the dropped record before G
-                const uint32_t dd = dqa ^ ~S.crc_last;
-                DG = jG ? em_fj(emt, jG, dd) : dd;
-                expG = exp_pre(emt, jG, S.crc_last, cG);
-            }
-            injG = expG ^ sG ^ DG;
+            if (tt > 0) expG = exp_pre(emt, G & 3u, S.crc_last, entry_crc(base, F.len, tb, *(const u32x4*)trec));
         }
         bool full = !grec || ovfl || n > SHORT_MAXN || sigG >= NSEG || (tt > 0 && sigG > SHORT_KMAX);
         uint32_t ex = 0, dev = 0;
@@ -1671,9 +1625,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                         const uint32_t cr = c.w;                            // this record's stored CRC
                         q.Wr = patch_word_of(p);
                         q.sa = (q.Wr - tb) >> 6;
-                        if (i == 0) q.inj = injG;
-                        else q.inj = tsnap[i] ^ exp_pre(emt, p & 3u, entry_crc(base, F.len, tb,
-                                                                           *(const u32x4*)(trec + 4 * (i - 1))), cr);
+                        q.inj = tsnap[i] ^ exp_post(p & 3u, cr, kj);
                         if (i + 1 < n) {                                    // ends at the next record's patch word
                             const u32x4 v2 = *(const u32x4*)(trec + 4 * (i + 1));
                             const uint32_t P2 = tb + (v2.w & 0xFFFFu);
@@ -1736,15 +1688,43 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         if (full) {
-            // ---- the tile-wide scan; the exit register of segment sigG under
-            // the reset: its register from zero, with injG XORed in before WG
-            const uint32_t xG = grec && sigG < NSEG ? em_f4(emt, (64u * (sigG + 1u) - (WG - tb)) >> 2, injG) : 0u;
-            uint32_t x = 0, rc = 0;
+            // ---- the tile-wide scan: the segments whose last boundary is a
+            // record start get their reset exit (flagged: a constant in the scan)
+            if (lane < NSEG / 32) flg[lane] = 0u;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint32_t wlast = 0, clast = 0, plast = 0;                       // (the tile's last record start)
+            if (grec && !ovfl) {
+                for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+                    const uint32_t i = i0 + (uint32_t)lane;
+                    if (i < n) {
+                        const u32x4 v = *(const u32x4*)(trec + 4 * i);
+                        const uint32_t P = tb + (v.w & 0xFFFFu), W = patch_word_of(P), sg = (W - tb) >> 6;
+                        bool lastin = true;
+                        if (i + 1 < n) lastin = ((patch_word_of(tb + (trec[4 * (i + 1) + 3] & 0xFFFFu)) - tb) >> 6) != sg;
+                        if (sg < NSEG && lastin) {
+                            const uint32_t inj = tsnap[i] ^ exp_post(P & 3u, entry_crc(base, F.len, tb, v), kj);
+                            gin[gin_at(sg)] ^= em_f4(emt, (64u * (sg + 1u) - (W - tb)) >> 2, inj);
+                            __atomic_fetch_or(flg + (sg >> 5), 1u << (sg & 31u), __ATOMIC_RELAXED);
+                        }
+                    }
+                }
+                const u32x4 vl = *(const u32x4*)(trec + 4 * (n - 1));
+                plast = tb + (vl.w & 0xFFFFu);
+                wlast = patch_word_of(plast);
+                clast = entry_crc(base, F.len, tb, vl);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            uint32_t x = 0, rc = 0, fl = 0;
             #pragma unroll
             for (int k = 0; k < RUN; k++) {
                 const uint32_t sg = (uint32_t)lane * RUN + k;
-                if (sg == sigG) { x = sr[k] ^ xG; rc = 1; }
-                else x = em_a64(emt, x) ^ sr[k];
+                sr[k] = gin[k * 64 + lane];
+                const uint32_t fk = (flg[sg >> 5] >> (sg & 31u)) & 1u;
+                fl |= fk << k;
+                x = fk ? sr[k] : em_a64(emt, x) ^ sr[k];
+                rc |= fk;
             }
             #pragma unroll
             for (int l = 0; l < 6; l++) {
@@ -1752,14 +1732,12 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                 const uint32_t px = (uint32_t)__shfl_up((int)x, d, 64), pc = (uint32_t)__shfl_up((int)rc, d, 64);
                 if (lane >= d && !rc) { x = mat_mul(emt + (EM_RUN + l) * 128, px) ^ x; rc = pc; }
             }
-            uint32_t y = (uint32_t)__shfl_up((int)x, 1, 64), Lg = 0;
+            uint32_t y = (uint32_t)__shfl_up((int)x, 1, 64);
             if (lane == 0) y = 0;
             #pragma unroll
             for (int k = 0; k < RUN; k++) {
-                const uint32_t sg = (uint32_t)lane * RUN + k;
                 gin[k * 64 + lane] = y;
-                if (sg == sigG) { Lg = em_f4(emt, (WG - tb - 64u * sg) >> 2, y) ^ sG; y = sr[k] ^ xG; }
-                else y = em_a64(emt, y) ^ sr[k];
+                y = ((fl >> k) & 1u) ? sr[k] : em_a64(emt, y) ^ sr[k];
             }
             const uint32_t gte = rdl(y, 63);                                // the register at the tile's end
             if (lane == 0) gin[NSEG] = gte;
@@ -1768,21 +1746,23 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             ex = gte;
             if (gterm) { ex = 0; dev = gte ^ cout; }
             else if (grec) {
-                const uint32_t LG = sigG < NSEG ? rdl(Lg, (int)(sigG / RUN)) : gte ^ sG;   // the tile's own register entering WG
-                ex = sigG < NSEG ? gte ^ cout : expG ^ cout ^ DG;
-                dev = LG ^ expG;
-                if (term && ex != 0u && lane == 0)                          // the record ending at the terminal
-                    atomicMin(&fo->fail_key, ((u64)(uint32_t)(loc[t].l[2] >> 32) << 32) | (S.count + n - 1));
+                // the tile's own register entering WG (no reset before G)
+                dev = (sigG < NSEG ? em_f4(emt, (WG - tb - 64u * sigG) >> 2, gin[gin_at(sigG)]) : gte) ^ sG ^ expG;
                 if (!ovfl) {
+                    // past the last record start: its reset at the tile's end
+                    // when its patch word is there, else the scan's register
+                    ex = wlast == TE ? exp_post(plast & 3u, clast, kj) : gte ^ cout;
+                    if (term && ex != 0u && lane == 0)                      // the record ending at the terminal
+                        atomicMin(&fo->fail_key, ((u64)(uint32_t)(loc[t].l[2] >> 32) << 32) | (S.count + n - 1));
                     // every record that ends at a record start inside the tile
                     for (uint32_t i = lane; i + 1 < n; i += 64) {
                         const u32x4 v = *(const u32x4*)(trec + 4 * i), v2 = *(const u32x4*)(trec + 4 * (i + 1));
                         const uint32_t p = tb + (v.w & 0xFFFFu), P2 = tb + (v2.w & 0xFFFFu);
-                        const uint32_t W = patch_word_of(P2), sg = (W - tb) >> 6;
-                        const uint32_t bv = sg == sigG ? injG : gin[gin_at(sg)];
-                        const uint32_t k4 = sg == sigG ? (W - WG) >> 2 : (W - tb - 64u * sg) >> 2;
-                        const uint32_t pre = em_f4(emt, k4, bv) ^ tsnap[i + 1];
-                        if (pre != exp_pre(emt, P2 & 3u, entry_crc(base, F.len, tb, v), entry_crc(base, F.len, tb, v2)))
+                        const uint32_t W = patch_word_of(p), W2 = patch_word_of(P2), sg = (W - tb) >> 6, sg2 = (W2 - tb) >> 6;
+                        const uint32_t c1 = entry_crc(base, F.len, tb, v), c2 = entry_crc(base, F.len, tb, v2);
+                        const uint32_t pre = sg2 == sg ? tsnap[i + 1] ^ em_f4(emt, (W2 - W) >> 2, tsnap[i] ^ exp_post(p & 3u, c1, kj))
+                                                       : em_f4(emt, (W2 - tb - 64u * sg2) >> 2, gin[gin_at(sg2)]) ^ tsnap[i + 1];
+                        if (pre != exp_pre(emt, P2 & 3u, c1, c2))
                             atomicMin(&fo->fail_key, ((u64)p << 32) | (S.count + i));
                     }
                 }
@@ -1806,21 +1786,22 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
 // k_fin: per file (FIN_NT threads), after k_emit: the register entering every
 // tile up to the terminal's, as a segmented scan over the tiles (a tile with a
 // boundary fixes the register at its end to its exit value; a tile without one
-// passes it on as A^CLY_TILE r ^ its own register), and in every tile after the
-// first that has a boundary, the check of the record that crosses into it
-// (its start: the last record before the tile, TileIn): A^CLY_TILE (the
-// register entering the tile) must equal the tile's dev shifted to its end,
-// with the patches of records k_refix dropped in front of G taken out.
+// passes it on as A^CLY_TILE r ^ its own register; a tile whose compact list
+// overflowed leaves it unknown: k_ovf checks the records that start there),
+// and in every tile after the first that has a boundary, the check of the
+// record that crosses into it (its start: the last record before the tile,
+// TileIn): A^CLY_TILE (the register entering the tile) must equal the tile's
+// dev shifted to its end.
 #define FIN_NT 256
 __device__ __forceinline__ uint32_t shift_b(const CLY_LDS uint32_t* sh, uint32_t m, uint32_t v) {
     return m ? shift_bytes(sh, m, v) : v;
 }
 __global__ void __launch_bounds__(FIN_NT)
 k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __restrict__ treg,
-      const TileLocal* __restrict__ loc, const TileIn* __restrict__ tin, const uint32_t* __restrict__ rec,
-      const uint32_t* __restrict__ tabs, const uint32_t* __restrict__ pw, Globals* g, int slot) {
+      const TileLocal* __restrict__ loc, const TileIn* __restrict__ tin, const uint32_t* __restrict__ tabs,
+      const uint32_t* __restrict__ pw, Globals* g, int slot) {
     __shared__ uint32_t tabl[NIB_SH * 128 + 128];           // TAB_SH, TAB_TILE
-    __shared__ uint32_t px[FIN_NT], pc[FIN_NT];
+    __shared__ uint32_t px[FIN_NT], pc[FIN_NT], pu[FIN_NT];
     __shared__ uint32_t mlev[8];
     if (g->nfix[slot]) return;              // k_emit did not run (link repair first)
     for (int i = threadIdx.x; i < NIB_SH * 128 + 128; i += FIN_NT) tabl[i] = tabs[TAB_SH + i];
@@ -1842,52 +1823,42 @@ k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __rest
         for (int l = 0; l < 8; l++) { mlev[l] = m; m = cly_multmodp(m, m); }
     }
     __syncthreads();
-    uint32_t x = 0, c = 0;
+    uint32_t x = 0, c = 0, un = 0;
     for (uint32_t u = lo; u < hi; u++) {
+        const u64 l0 = loc[ft + u].l[0];
         const uint32_t v = treg[2 * (ft + u)];
-        if (!(loc[ft + u].l[0] & DF_NONE)) { x = v; c = 1; }
+        if (!(l0 & DF_NONE)) { x = v; c = 1; un = (l0 & DF_OVF) ? 1u : 0u; }
         else x = mat_mul(tilet, x) ^ v;
     }
-    px[tid] = x; pc[tid] = c;
+    px[tid] = x; pc[tid] = c; pu[tid] = un;
     __syncthreads();
     for (int l = 0; (1 << l) < FIN_NT; l++) {
         const int d = 1 << l;
-        uint32_t ox = 0, oc = 0;
-        if (tid >= d) { ox = px[tid - d]; oc = pc[tid - d]; }
+        uint32_t ox = 0, oc = 0, ou = 0;
+        if (tid >= d) { ox = px[tid - d]; oc = pc[tid - d]; ou = pu[tid - d]; }
         __syncthreads();
-        if (tid >= d && !c) { x = cly_multmodp(mlev[l], ox) ^ x; c = oc; }
-        px[tid] = x; pc[tid] = c;
+        if (tid >= d && !c) { x = cly_multmodp(mlev[l], ox) ^ x; c = oc; un = ou; }
+        px[tid] = x; pc[tid] = c; pu[tid] = un;
         __syncthreads();
     }
-    uint32_t y = tid ? px[tid - 1] : 0u;
-    const gbytes base = (gbytes)F.base;
+    uint32_t y = tid ? px[tid - 1] : 0u, yu = tid ? pu[tid - 1] : 0u;
     for (uint32_t u = lo; u < hi; u++) {
         const uint32_t t = ft + u;
         const u64 l0 = loc[t].l[0];
         const uint32_t v = treg[2 * t];
         if (l0 & DF_NONE) { y = mat_mul(tilet, y) ^ v; continue; }
-        if (u > 0) {
+        if (u > 0 && !yu) {
             const LBState S = ti_load(&tin[t]);
             const uint32_t n = (uint32_t)(l0 >> 32), G = (uint32_t)loc[t].l[1];
             const uint32_t tb = (uint32_t)((uint64_t)u * CLY_TILE), TE = tb + (uint32_t)CLY_TILE;
             uint32_t dev = treg[2 * t + 1];
             if ((l0 & DF_TERM) && n == 0) dev ^= shift_b(sht, TE - G, S.crc_last);     // G is the terminal
-            else {
-                const uint32_t WG = (G & 3u) ? (G & ~3u) + 4u : G;
-                dev = shift_b(sht, TE - WG, dev);
-                const uint32_t skip = (uint32_t)(loc[t].l[3] >> 40) & 0xFFFFu;
-                uint32_t q = 0xFFFFFFFFu;
-                for (uint32_t i = 0; i < skip; i++) {                     // the dropped records' patches
-                    const u32x4 e = *(const u32x4*)(rec + ((uint64_t)t * CAP_T + i) * 4);
-                    const uint32_t Pi = tb + (e.w & 0xFFFFu), ci = entry_crc(base, F.len, tb, e);
-                    dev ^= shift_b(sht, TE - Pi, ci ^ CLY_K4 ^ q);
-                    q = ~ci;
-                }
-            }
+            else dev = shift_b(sht, TE - patch_word_of(G), dev);
             if (mat_mul(tilet, y) != dev)
                 atomicMin(&fo->fail_key, ((u64)S.P_last << 32) | (uint64_t)(S.count - 1));
         }
         y = v;
+        yu = (l0 & DF_OVF) ? 1u : 0u;
     }
 }
 
@@ -2146,7 +2117,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[3], st));
         hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_finfo, c->d_treg, c->d_loc,
-                           c->d_tin, c->d_rec, c->d_tabs, c->d_pw, c->d_g, slot);
+                           c->d_tin, c->d_tabs, c->d_pw, c->d_g, slot);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[4], st));
         hipLaunchKernelGGL(k_ovf, dim3(c->loc_grid), dim3(1024), 0, st, c->d_files, c->d_finfo, d_out, out_cap,
