@@ -112,7 +112,8 @@ class ClyLoadStats(ctypes.Structure):
                 ("active_fid", ctypes.c_uint32), ("_pad", ctypes.c_uint32), ("write_off", ctypes.c_int64),
                 ("hint_records", ctypes.c_uint64), ("n_expired", ctypes.c_uint64),
                 ("write_off_loaded", ctypes.c_int64), ("active_fid_loaded", ctypes.c_uint32),
-                ("sweep_files", ctypes.c_uint32), ("n_shards", ctypes.c_uint32), ("_pad2", ctypes.c_uint32)]
+                ("sweep_files", ctypes.c_uint32), ("n_shards", ctypes.c_uint32), ("_pad2", ctypes.c_uint32),
+                ("tuple_slots", ctypes.c_uint64)]
 
 
 class ClyDbOptions(ctypes.Structure):

@@ -52,6 +52,9 @@ extern "C" hipStream_t cly_ctx_stream_internal(cly_ctx* c);
 extern "C" int cly_ctx_device_internal(cly_ctx* c);
 extern "C" uint64_t cly_ix_hash_mask_internal(uint64_t n);
 extern "C" hipError_t cly_ix_hash_ptr_internal(cly_ctx* ctx, uint64_t n, void** out);
+extern "C" int cly_scan_device_alloc_internal(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple** d_out,
+                                              uint64_t* cap, uint64_t* file_first, cly_file_result* res,
+                                              uint64_t* needed);
 #define LOAD_PIECE (64ull << 20)
 #define LOAD_STAGE (8ull << 20)            // page-locked staging buffer (two per copy thread)
 #define LOAD_THREADS_MAX 16
@@ -67,7 +70,6 @@ struct Mapped {
     uint32_t fid;
     const uint8_t* p;
     uint64_t len;
-    int fd = -1;                 // kept open only for CLY_H2D_MODE=1 (the copy to HBM preads it)
 };
 // Go's strconv.Atoi (64-bit int): an optional sign, decimal digits, no overflow
 static bool go_atoi(const char* s, size_t n, int64_t& v) {
@@ -109,24 +111,6 @@ static Hdr host_read_record(const uint8_t* p, uint64_t len, int64_t off) {
     return h;
 }
 
-// The String / ListMeta index: open-addressing tables of (key hash, tuple
-// index), sharded by the hash's top bits so that one thread builds each shard;
-// the key bytes stay in the mapped files.  The device already decided the one
-// live record of every key (last writer wins), so inserts never meet an equal
-// key and need no comparison.
-struct FlatShard {
-    std::vector<uint64_t> h;     // key hash | 1 (0 = empty)
-    std::vector<uint64_t> ti;    // tuple index
-    uint64_t mask = 0, n = 0;
-};
-static constexpr int FLAT_SHARD_BITS = 4;
-static constexpr int FLAT_SHARDS = 1 << FLAT_SHARD_BITS;
-struct FlatIndex {
-    FlatShard sh[FLAT_SHARDS];
-    uint64_t n = 0;
-};
-// shard = the top FLAT_SHARD_BITS of the hash's valid bits (the device hash keeps hbits)
-static inline int flat_shard(uint64_t h, int hshift) { return (int)((h >> hshift) & (FLAT_SHARDS - 1)); }
 // host array without value-initialisation (the device fills it)
 template <class T> struct HostArr {
     std::unique_ptr<T[]> p;
@@ -137,6 +121,30 @@ template <class T> struct HostArr {
     uint64_t size() const { return n; }
     T* data() { return p.get(); }
 };
+// The String / ListMeta index: open-addressing tables sharded by the key
+// hash's top valid bits, built on the device (k_flat_count, k_flat_insert)
+// and read back whole; the key bytes stay in the mapped files.  A slot is
+// 8 B: 0 empty, else tag << 40 | (tuple index + 1), the tag 24 bits of a
+// remix of the hash (a lookup compares keys only on equal tags); probing
+// starts at hash & mask.  The device already decided the one live record of
+// every key (last writer wins), so inserts never meet an equal key.
+struct FlatShard {
+    HostArr<uint64_t> s;
+    uint64_t mask = 0, n = 0;    // (mask 0: no slots)
+};
+static constexpr int FLAT_SHARD_BITS = 4;
+static constexpr int FLAT_SHARDS = 1 << FLAT_SHARD_BITS;
+#define FLAT_TI_BITS 40
+#define FLAT_TI_MASK ((1ull << FLAT_TI_BITS) - 1)
+struct FlatIndex {
+    FlatShard sh[FLAT_SHARDS];
+    uint64_t n = 0;
+};
+// shard = the top FLAT_SHARD_BITS of the hash's valid bits (the device hash keeps hbits)
+__host__ __device__ static inline int flat_shard(uint64_t h, int hshift) { return (int)((h >> hshift) & (FLAT_SHARDS - 1)); }
+__host__ __device__ static inline uint64_t flat_tag(uint64_t h) { return (h * 0x9E3779B97F4A7C15ull) >> 40; }
+// the slot's tuple index, or ~0 for an empty slot
+static inline uint64_t flat_ti(uint64_t v) { return v ? (v & FLAT_TI_MASK) - 1 : ~0ull; }
 struct cly_db {
     std::vector<Mapped> files;       // in loadIndex's order (fids as sort.Ints orders the stems)
     std::unordered_map<uint32_t, uint32_t> fid_ix;   // uint32(fid) -> its file
@@ -148,7 +156,6 @@ struct cly_db {
     bool it_built[6] = {false, false, false, false, false, false};
     HostArr<cly_tuple> tuples;
     HostArr<uint8_t> state;
-    HostArr<uint64_t> khash;     // the device index's key hash per record (String / ListMeta tables)
     uint64_t hmask = ~0ull;
     int hshift = 60;
     std::vector<uint64_t> first;
@@ -211,42 +218,32 @@ static cly_pos pos_of(const cly_db* db, uint64_t ti) {
     p.offset = db->tuples[ti].offset; p.fid = db->tuples[ti].fid; p._pad = 0;
     return p;
 }
-static void flat_init(FlatShard& x, uint64_t n) {
+// slots of a shard of n keys: a power of two >= 1.5 n (at least 16; none for no key)
+static uint64_t flat_cap(uint64_t n) {
+    if (!n) return 0;
     uint64_t cap = 16;
-    while (cap < 2 * n) cap <<= 1;
-    x.h.assign(cap, 0);
-    x.ti.assign(cap, 0);
-    x.mask = cap - 1;
-    x.n = 0;
+    while (cap < n + n / 2) cap <<= 1;
+    return cap;
 }
-static void flat_put(FlatShard& x, uint64_t h, uint64_t ti) {
-    uint64_t i = h & x.mask;
-    while (x.h[i]) i = (i + 1) & x.mask;
-    x.h[i] = h;
-    x.ti[i] = ti;
-    x.n++;
-}
-static void flat_build(cly_db* db, int nthreads, std::vector<uint64_t>& composite);
 static int flat_get(const cly_db* db, const FlatIndex& xi, uint32_t kind, const uint8_t* key, uint64_t klen,
                     cly_pos* pos) {
     if (klen > 0xFFFFFFFFull) return CLY_DB_NOT_FOUND;
-    const uint64_t h = (ixk_hash(kind, key, (uint32_t)klen) & db->hmask) | 1;
+    const uint64_t h = (ixk_hash(kind, key, (uint32_t)klen) & db->hmask) | 1, tg = flat_tag(h);
     const FlatShard& x = xi.sh[flat_shard(h, db->hshift)];
     if (!x.mask) return CLY_DB_NOT_FOUND;
-    for (uint64_t i = h & x.mask; x.h[i]; i = (i + 1) & x.mask) {
-        if (x.h[i] != h) continue;
+    for (uint64_t i = h & x.mask, v; (v = x.s[i]); i = (i + 1) & x.mask) {
+        if ((v >> FLAT_TI_BITS) != tg) continue;
         uint64_t n;
-        const uint8_t* k = real_key_ptr(db, x.ti[i], n);
+        const uint64_t ti = flat_ti(v);
+        const uint8_t* k = real_key_ptr(db, ti, n);
         if (n == klen && memcmp(k, key, n) == 0) {
-            if (pos) *pos = pos_of(db, x.ti[i]);
+            if (pos) *pos = pos_of(db, ti);
             return CLY_OK;
         }
     }
     return CLY_DB_NOT_FOUND;
 }
 
-static int g_h2d_mode = 0, g_overlap = 0;
-static void load_switches();
 static int map_file(const char* path, Mapped& m, bool& exists) {
     m.p = nullptr; m.len = 0;
     exists = false;
@@ -260,8 +257,7 @@ static int map_file(const char* path, Mapped& m, bool& exists) {
         void* p = mmap(nullptr, m.len, PROT_READ, MAP_PRIVATE, fd, 0);     // for the host's key reads
         if (p == MAP_FAILED) { close(fd); m.len = 0; return CLY_ERR_ARG; }
         m.p = (const uint8_t*)p;
-        if (g_h2d_mode == 1) m.fd = fd;
-        else close(fd);
+        close(fd);
         return CLY_OK;
     }
     close(fd);
@@ -314,88 +310,64 @@ static int list_files(const char* dir, std::vector<Mapped>& out, std::unordered_
     return CLY_OK;
 }
 
-// Two passes over the LIVE tuples, each split over `nthreads` threads: count
-// the records per shard (the key hashes are the device index's, downloaded),
-// then let thread t fill shards t, t+T, ...
-static void flat_build(cly_db* db, int nthreads, std::vector<uint64_t>& composite) {
-    const uint64_t need = db->tuples.size();
+// The records the flat tables take: a String or ListMeta key's live record
+// (dt 0 / 3; class byte = state | dt << 4, k_state_dt); -1 for the others
+__device__ static inline int flat_ks(uint8_t b, uint64_t h, int hshift) {
+    const uint32_t st = b & 15u, dt = b >> 4;
+    if (st != CLY_IX_LIVE || (dt != 0 && dt != 3)) return -1;
+    return (dt == 3 ? FLAT_SHARDS : 0) + flat_shard(h, hshift);
+}
+// keys per (kind, shard)
+__global__ void k_flat_count(const uint8_t* __restrict__ state, const uint64_t* __restrict__ hash, uint64_t n,
+                             uint64_t hmask, int hshift, unsigned long long* cnt) {
+    __shared__ unsigned int c[2 * FLAT_SHARDS];
+    if (threadIdx.x < 2 * FLAT_SHARDS) c[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t b = state[i];
+        if ((b & 15u) != CLY_IX_LIVE) continue;
+        const int ks = flat_ks(b, (hash[i] & hmask) | 1, hshift);
+        if (ks >= 0) atomicAdd(&c[ks], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 2 * FLAT_SHARDS && c[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], (unsigned long long)c[threadIdx.x]);
+}
+// the inserts: linear probing from hash & mask, a slot claimed by CAS on 0
+// (geo: per (kind, shard) its first slot and its mask)
+__global__ void k_flat_insert(const uint8_t* __restrict__ state, const uint64_t* __restrict__ hash, uint64_t n,
+                              uint64_t hmask, int hshift, const uint64_t* __restrict__ geo, unsigned long long* slots) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t b = state[i];
+        if ((b & 15u) != CLY_IX_LIVE) continue;
+        const uint64_t h = (hash[i] & hmask) | 1;
+        const int ks = flat_ks(b, h, hshift);
+        if (ks < 0) continue;
+        const uint64_t base = geo[2 * ks], m = geo[2 * ks + 1];
+        const unsigned long long v = (unsigned long long)((flat_tag(h) << FLAT_TI_BITS) | (i + 1));
+        for (uint64_t j = h & m; atomicCAS(&slots[base + j], 0ull, v) != 0ull; j = (j + 1) & m) {}
+    }
+}
+// Hash / List / Set records an index points at (scan order), from the class bytes
+static void composite_list(const cly_db* db, int nthreads, std::vector<uint64_t>& composite) {
+    const uint64_t need = db->state.size();
     std::vector<std::vector<uint64_t>> comp(nthreads);
-    HostArr<uint64_t> hv;
-    hv.alloc(need);
-    std::vector<uint64_t> cnt((size_t)nthreads * 2 * FLAT_SHARDS, 0);
-    auto hash_part = [&](int t) {
+    par_run(nthreads, [&](int t) {
         const uint64_t a = need * t / nthreads, b = need * (t + 1) / nthreads;
-        uint64_t* c = &cnt[(size_t)t * 2 * FLAT_SHARDS];
         for (uint64_t i = a; i < b; i++) {
-            hv[i] = 0;
             const uint8_t st = ST_STATE(db->state[i]);
             if (st != CLY_IX_LIVE && st != CLY_IX_LOADONLY) continue;
             const uint32_t dt = ST_DT(db->state[i]);
-            if (dt == 1 || dt == 2 || dt == 4) { comp[t].push_back(i); continue; }    // Hash / List / Set
-            if (st != CLY_IX_LIVE || (dt != 0 && dt != 3)) continue;               // String / ListMeta
-            hv[i] = (db->khash[i] & db->hmask) | 1;
-            c[(dt == 3) * FLAT_SHARDS + flat_shard(hv[i], db->hshift)]++;
+            if (dt == 1 || dt == 2 || dt == 4) comp[t].push_back(i);
         }
-    };
-    std::vector<uint64_t> boff((size_t)nthreads * 2 * FLAT_SHARDS + 1, 0);
-    HostArr<uint64_t> bidx;
-    auto scatter_part = [&](int t) {
-        const uint64_t a = need * t / nthreads, b = need * (t + 1) / nthreads;
-        uint64_t w[2 * FLAT_SHARDS];
-        for (int ks = 0; ks < 2 * FLAT_SHARDS; ks++) w[ks] = boff[(size_t)ks * nthreads + t];
-        for (uint64_t i = a; i < b; i++) {
-            if (!hv[i]) continue;
-            const int ks = (ST_DT(db->state[i]) == 3) * FLAT_SHARDS + flat_shard(hv[i], db->hshift);
-            bidx[w[ks]++] = i;
-        }
-    };
-    auto fill_part = [&](int t) {
-        for (int kind = 0; kind < 2; kind++)
-            for (int sh = t; sh < FLAT_SHARDS; sh += nthreads) {
-                const int ks = kind * FLAT_SHARDS + sh;
-                const uint64_t lo = boff[(size_t)ks * nthreads], hi = boff[(size_t)(ks + 1) * nthreads];
-                FlatShard& x = (kind ? db->listmeta : db->str).sh[sh];
-                flat_init(x, hi - lo);
-                for (uint64_t j = lo; j < hi; j++) flat_put(x, hv[bidx[j]], bidx[j]);
-            }
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < nthreads; t++) th.emplace_back(hash_part, t);
-    hash_part(0);
-    for (auto& x : th) x.join();
-    th.clear();
-    {
-        // bucket the records by (kind, shard): exclusive offsets over (kind, shard, thread)
-        uint64_t acc = 0;
-        for (int ks = 0; ks < 2 * FLAT_SHARDS; ks++)
-            for (int u = 0; u < nthreads; u++) {
-                boff[(size_t)ks * nthreads + u] = acc;
-                acc += cnt[(size_t)u * 2 * FLAT_SHARDS + ks];
-            }
-        boff[(size_t)nthreads * 2 * FLAT_SHARDS] = acc;
-        bidx.alloc(acc);
-    }
-    for (int t = 1; t < nthreads; t++) th.emplace_back(scatter_part, t);
-    scatter_part(0);
-    for (auto& x : th) x.join();
-    th.clear();
-    for (int t = 1; t < nthreads; t++) th.emplace_back(fill_part, t);
-    fill_part(0);
-    for (auto& x : th) x.join();
+    });
     composite.clear();
-    for (auto& v : comp) composite.insert(composite.end(), v.begin(), v.end());    // scan order
-    db->str.n = db->listmeta.n = 0;
-    for (int sh = 0; sh < FLAT_SHARDS; sh++) {
-        db->str.n += db->str.sh[sh].n;
-        db->listmeta.n += db->listmeta.sh[sh].n;
-    }
+    for (auto& v : comp) composite.insert(composite.end(), v.begin(), v.end());
 }
 
 extern "C" void cly_db_close(cly_db* db) {
     if (!db) return;
-    for (Mapped& m : db->files) { if (m.p) munmap((void*)m.p, m.len); if (m.fd >= 0) close(m.fd); }
+    for (Mapped& m : db->files) if (m.p) munmap((void*)m.p, m.len);
     if (db->hint.p) munmap((void*)db->hint.p, db->hint.len);
-    if (db->hint.fd >= 0) close(db->hint.fd);
     delete db;
 }
 
@@ -433,54 +405,16 @@ static int stage_ready() {
 // t0+nt-1) fault the mapped pages in and copy 64-MiB pieces through the
 // page-locked staging buffers (CPU copy of one while the DMA of the other
 // runs).  The caller holds g_stage_mu.
-// Experiment switches of the load path (CLY_H2D_MODE: 0 memcpy from the
-// mapping into the staging buffers, 1 pread into them, 2 the mapping
-// registered and copied by DMA directly; CLY_LOAD_OVERLAP: 1 the tuples'
-// read-back beside the table build).  Measured on C2 (tools/exp_load.py): H2D
-// 86-90 ms (0), 92-97 (1), 156-163 (2); wall 216-232 ms with the overlap.
-static void load_switches() {            // read once per process (opens may run concurrently)
-    static std::once_flag once;
-    std::call_once(once, [] {
-        const char* a = getenv("CLY_H2D_MODE");
-        const char* b = getenv("CLY_LOAD_OVERLAP");
-        g_h2d_mode = a ? atoi(a) : 0;
-        g_overlap = b ? atoi(b) : 1;
-    });
-}
-static int copy_to_device(int dev, const std::vector<cly_file>& hf, const int* fds, std::vector<cly_file>& df,
-                          uint8_t* d_bytes, int t0, int nt) {
-    if (g_h2d_mode == 2) {
-        // the mapped files registered (page-locked in place) and copied by DMA
-        int err = 0;
-        uint64_t off = 0;
-        if (hipSetDevice(dev) != hipSuccess) return CLY_ERR_DEVICE;
-        hipStream_t ts = nullptr;
-        if (hipStreamCreateWithFlags(&ts, hipStreamNonBlocking) != hipSuccess) return CLY_ERR_DEVICE;
-        std::vector<const void*> reg;
-        for (size_t i = 0; i < hf.size(); i++) {
-            df[i] = hf[i];
-            df[i].base = d_bytes + off;
-            if (hf[i].len) {
-                if (hipHostRegister((void*)hf[i].base, hf[i].len, hipHostRegisterReadOnly) != hipSuccess) { err = 1; break; }
-                reg.push_back(hf[i].base);
-                if (hipMemcpyAsync(d_bytes + off, hf[i].base, hf[i].len, hipMemcpyHostToDevice, ts) != hipSuccess) err = 1;
-            }
-            off += (hf[i].len + 4095) & ~4095ull;
-        }
-        if (hipStreamSynchronize(ts) != hipSuccess) err = 1;
-        for (const void* p : reg) hipHostUnregister((void*)p);
-        hipStreamDestroy(ts);
-        return err ? CLY_ERR_DEVICE : CLY_OK;
-    }
-    struct Piece { const uint8_t* src; uint8_t* dst; uint64_t len; int fd; uint64_t foff; };
+static int copy_to_device(int dev, const std::vector<cly_file>& hf, std::vector<cly_file>& df, uint8_t* d_bytes,
+                          int t0, int nt) {
+    struct Piece { const uint8_t* src; uint8_t* dst; uint64_t len; };
     std::vector<Piece> pieces;
     uint64_t off = 0;
     for (size_t i = 0; i < hf.size(); i++) {
         df[i] = hf[i];
         df[i].base = d_bytes + off;
         for (uint64_t a = 0; a < hf[i].len; a += LOAD_PIECE)
-            pieces.push_back({hf[i].base + a, d_bytes + off + a, std::min<uint64_t>(LOAD_PIECE, hf[i].len - a),
-                              fds ? fds[i] : -1, a});
+            pieces.push_back({hf[i].base + a, d_bytes + off + a, std::min<uint64_t>(LOAD_PIECE, hf[i].len - a)});
         off += (hf[i].len + 4095) & ~4095ull;
     }
     std::atomic<size_t> next(0);
@@ -500,14 +434,7 @@ static int copy_to_device(int dev, const std::vector<cly_file>& hf, const int* f
                 const uint64_t n = std::min<uint64_t>(LOAD_STAGE, pc.len - a);
                 uint8_t* stg = (uint8_t*)g_stage[2 * (t0 + t) + b];
                 if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) err = 1;
-                if (pc.fd >= 0 && g_h2d_mode == 1) {
-                    // read(2) from the page cache straight into the staging buffer
-                    for (uint64_t got = 0; got < n;) {
-                        const ssize_t r = pread(pc.fd, stg + got, n - got, (off_t)(pc.foff + a + got));
-                        if (r <= 0) { memcpy(stg + got, pc.src + a + got, n - got); break; }
-                        got += (uint64_t)r;
-                    }
-                } else memcpy(stg, pc.src + a, n);
+                memcpy(stg, pc.src + a, n);
                 if (hipMemcpyAsync(pc.dst + a, stg, n, hipMemcpyHostToDevice, ts) != hipSuccess ||
                     hipEventRecord(ev[b], ts) != hipSuccess) err = 1;
                 used[b] = true;
@@ -524,7 +451,7 @@ static int copy_to_device(int dev, const std::vector<cly_file>& hf, const int* f
 // Device buffers back to host memory, in pieces from several threads (DMA
 // into one staging buffer while the CPU copies the other out).
 struct D2H { void* dst; const void* src; uint64_t len; };
-static int copy_to_host(cly_ctx* ctx, const std::vector<D2H>& parts, int t0, int nt) {
+static int copy_to_host(cly_ctx* ctx, const std::vector<D2H>& parts, int t0, int nt, bool lock = true) {
     struct Piece { void* dst; const void* src; uint64_t len; };
     std::vector<Piece> pieces;
     for (const D2H& x : parts)
@@ -533,7 +460,8 @@ static int copy_to_host(cly_ctx* ctx, const std::vector<D2H>& parts, int t0, int
     std::atomic<size_t> next(0);
     std::atomic<int> err(0);
     const int dev = cly_ctx_device_internal(ctx);
-    std::lock_guard<std::mutex> lk(g_stage_mu);
+    std::unique_lock<std::mutex> lk(g_stage_mu, std::defer_lock);     // (lock = false: the caller holds it)
+    if (lock) lk.lock();
     if (stage_ready() != CLY_OK) return CLY_ERR_DEVICE;
     // (threads t0 .. t0+nt-1, each with its own two staging buffers)
     par_run(nt, [&, t0](int tl) {
@@ -590,7 +518,6 @@ static int check_merge_finished(const char* dir) {
         if (!go_atoi((const char*)m.p + h.hsz + h.ks, h.vs, v)) rc = CLY_ERR_MERGE_FIN;
     }
     if (m.p) munmap((void*)m.p, m.len);
-    if (m.fd >= 0) close(m.fd);
     return rc;
 }
 
@@ -610,6 +537,71 @@ static std::vector<uint8_t> tombstone(const uint8_t* key, uint64_t klen) {
     const uint32_t c = host_crc(r.data() + 4, r.size() - 4);
     r[0] = (uint8_t)c; r[1] = (uint8_t)(c >> 8); r[2] = (uint8_t)(c >> 16); r[3] = (uint8_t)(c >> 24);
     return r;
+}
+
+// The index rebuild on the device (cly_index_device), then the String /
+// ListMeta tables: keys per shard counted, slots laid out, inserts, and the
+// class bytes, the slots and the hint positions read back on copy threads
+// 0 .. nb-1 (the caller holds g_stage_mu).
+static int flat_device(cly_ctx* ctx, cly_db* db, const cly_file* df, int nall, const cly_tuple* d_tup,
+                       const std::vector<uint64_t>& first, const std::vector<cly_file_result>& res, uint8_t* d_state,
+                       const cly_pos* d_hpos, uint64_t need, cly_index_result& ir, int nb) {
+    hipStream_t strm = cly_ctx_stream_internal(ctx);
+    if (nall) {
+        const int rc = cly_index_device(ctx, df, nall, d_tup, first.data(), res.data(), d_state, &ir, nullptr);
+        if (rc != CLY_OK) return rc;
+    }
+    if (!need) return hipStreamSynchronize(strm) == hipSuccess ? CLY_OK : CLY_ERR_DEVICE;
+    int rc = CLY_OK;
+    uint64_t* d_hash = nullptr;
+    unsigned long long* d_cnt = nullptr;
+    unsigned long long* d_slots = nullptr;
+    uint64_t* d_geo = nullptr;
+    unsigned long long cnt[2 * FLAT_SHARDS];
+    uint64_t geo[4 * FLAT_SHARDS], tot = 0;
+    const unsigned grid = (unsigned)std::min<uint64_t>((need + 255) / 256, 8192);
+    std::vector<D2H> parts = {{db->state.data(), d_state, need}};
+    DCK(cly_ix_hash_ptr_internal(ctx, need, (void**)&d_hash));
+    DCK(hipMalloc((void**)&d_cnt, sizeof(cnt) + sizeof(geo)));
+    d_geo = (uint64_t*)(d_cnt + 2 * FLAT_SHARDS);
+    DCK(hipMemsetAsync(d_cnt, 0, sizeof(cnt), strm));
+    hipLaunchKernelGGL(k_state_dt, dim3((unsigned)((need + 255) / 256)), dim3(256), 0, strm, d_state, d_tup, need);
+    hipLaunchKernelGGL(k_flat_count, dim3(grid), dim3(256), 0, strm, d_state, d_hash, need, db->hmask, db->hshift, d_cnt);
+    DCK(hipGetLastError());
+    DCK(hipMemcpyAsync(cnt, d_cnt, sizeof(cnt), hipMemcpyDeviceToHost, strm));
+    DCK(hipStreamSynchronize(strm));
+    for (int ks = 0; ks < 2 * FLAT_SHARDS; ks++) {
+        const uint64_t cap = flat_cap(cnt[ks]);
+        FlatShard& x = (ks >= FLAT_SHARDS ? db->listmeta : db->str).sh[ks % FLAT_SHARDS];
+        x.s.alloc(cap);
+        x.mask = cap ? cap - 1 : 0;
+        x.n = cnt[ks];
+        geo[2 * ks] = tot; geo[2 * ks + 1] = x.mask;
+        if (cap) parts.push_back({x.s.data(), nullptr, cap * 8});     // (its source once the slots exist)
+        tot += cap;
+    }
+    DCK(hipMalloc((void**)&d_slots, 8 * (tot ? tot : 1)));
+    {
+        size_t k = 1;
+        for (int ks = 0; ks < 2 * FLAT_SHARDS; ks++)
+            if (cnt[ks]) parts[k++].src = d_slots + geo[2 * ks];
+    }
+    DCK(hipMemsetAsync(d_slots, 0, 8 * tot, strm));
+    DCK(hipMemcpyAsync(d_geo, geo, sizeof(uint64_t) * 4 * FLAT_SHARDS, hipMemcpyHostToDevice, strm));
+    hipLaunchKernelGGL(k_flat_insert, dim3(grid), dim3(256), 0, strm, d_state, d_hash, need, db->hmask, db->hshift, d_geo,
+                       d_slots);
+    DCK(hipGetLastError());
+    DCK(hipStreamSynchronize(strm));
+    if (db->n_hint) parts.push_back({db->hint_pos.data(), d_hpos, sizeof(cly_pos) * db->n_hint});
+    rc = copy_to_host(ctx, parts, 0, nb, false);
+    db->str.n = db->listmeta.n = 0;
+    for (int sh = 0; sh < FLAT_SHARDS; sh++) {
+        db->str.n += db->str.sh[sh].n;
+        db->listmeta.n += db->listmeta.sh[sh].n;
+    }
+done:
+    hipFree(d_cnt); hipFree(d_slots);
+    return rc;
 }
 
 extern "C" int cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load_stats* st) {
@@ -635,7 +627,7 @@ struct LoadShard {
     int rc = CLY_OK;
     double t_copy = 0, t_scan = 0;
 };
-static void shard_load(LoadShard& S, const std::vector<cly_file>& hf, const std::vector<int>& fds, int t0, int nt) {
+static void shard_load(LoadShard& S, const std::vector<cly_file>& hf, int t0, int nt) {
     const int n = S.f1 - S.f0;
     const std::vector<cly_file> h(hf.begin() + S.f0, hf.begin() + S.f1);
     S.df.resize(n); S.res.resize(n); S.first.resize(n);
@@ -643,20 +635,11 @@ static void shard_load(LoadShard& S, const std::vector<cly_file>& hf, const std:
     uint64_t total = 0;
     for (const cly_file& f : h) total += (f.len + 4095) & ~4095ull;
     if (hipMalloc((void**)&S.d_bytes, total + 4096) != hipSuccess) { S.d_bytes = nullptr; S.rc = CLY_ERR_DEVICE; return; }
-    S.rc = copy_to_device(S.dev, h, fds.data() + S.f0, S.df, S.d_bytes, t0, nt);
+    S.rc = copy_to_device(S.dev, h, S.df, S.d_bytes, t0, nt);
     S.t_copy = now_ms();
     if (S.rc != CLY_OK) return;
-    S.cap = cly_scan_capacity(h.data(), n) + 16;
-    if (hipMalloc((void**)&S.d_tup, sizeof(cly_tuple) * S.cap) != hipSuccess) { S.d_tup = nullptr; S.rc = CLY_ERR_DEVICE; return; }
-    S.rc = cly_scan_device(S.ctx, S.df.data(), n, S.d_tup, S.cap, S.first.data(), S.res.data(), &S.need, nullptr, nullptr);
-    if (S.rc == CLY_ERR_CAPACITY && S.need > S.cap) {
-        // records shorter than 9 B: the exact need, scanned again
-        hipFree(S.d_tup); S.d_tup = nullptr;
-        S.cap = S.need + 16;
-        if (hipMalloc((void**)&S.d_tup, sizeof(cly_tuple) * S.cap) != hipSuccess) { S.d_tup = nullptr; S.rc = CLY_ERR_DEVICE; return; }
-        S.rc = cly_scan_device(S.ctx, S.df.data(), n, S.d_tup, S.cap, S.first.data(), S.res.data(), &S.need, nullptr,
-                               nullptr);
-    }
+    // the tuple buffer sized by the exact record count, once the link knows it
+    S.rc = cly_scan_device_alloc_internal(S.ctx, S.df.data(), n, &S.d_tup, &S.cap, S.first.data(), S.res.data(), &S.need);
     S.t_scan = now_ms();
 }
 static void shard_free(LoadShard& S) {
@@ -674,7 +657,6 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
     }
     *out = nullptr;
     cly_ctx* ctx = ctxs[0];                      // the index is rebuilt on the first context
-    load_switches();
     cly_load_stats s;
     memset(&s, 0, sizeof(s));
     uint64_t dfs = opt && opt->data_file_size ? opt->data_file_size : (256ull << 20);
@@ -692,7 +674,6 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
     uint8_t* d_state = nullptr;
     cly_pos* d_hpos = nullptr;
     std::vector<cly_file> hf, df;
-    std::vector<int> hfd;                        // the files' descriptors (pread by the copy threads)
     std::vector<cly_file_result> res;
     std::vector<uint64_t> first;
     std::vector<LoadShard> sh(nctx);
@@ -711,12 +692,10 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
     s.n_files = (uint64_t)nf;
     nall = nf + (has_hint ? 1 : 0);
     hf.resize(nall);
-    hfd.assign(nall, -1);
-    if (has_hint) { hf[0].base = db->hint.p; hf[0].len = db->hint.len; hf[0].fid = 0; hf[0]._pad = 0; hfd[0] = db->hint.fd; }
+    if (has_hint) { hf[0].base = db->hint.p; hf[0].len = db->hint.len; hf[0].fid = 0; hf[0]._pad = 0; }
     for (int i = 0; i < nf; i++) {
         cly_file& f = hf[i + (has_hint ? 1 : 0)];
         f.base = db->files[i].p; f.len = db->files[i].len; f.fid = db->files[i].fid; f._pad = 0;
-        hfd[i + (has_hint ? 1 : 0)] = db->files[i].fd;
         s.bytes += f.len;
     }
     {
@@ -747,7 +726,7 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
         int slot = 0;
         for (LoadShard& S : sh) {
             if (S.f1 == S.f0) continue;
-            th.emplace_back(shard_load, std::ref(S), std::cref(hf), std::cref(hfd), slot, ntk);
+            th.emplace_back(shard_load, std::ref(S), std::cref(hf), slot, ntk);
             slot += ntk;
         }
         for (auto& x : th) x.join();
@@ -755,6 +734,7 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
             if (S.f1 == S.f0) continue;
             if (S.rc != CLY_OK && rc == CLY_OK) rc = S.rc;
             t2 = std::max(t2, S.t_copy);
+            s.tuple_slots += S.cap;
         }
         if (rc != CLY_OK) goto done;
     } else t2 = t1;
@@ -824,29 +804,26 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
     t3 = now_ms();
     s.scan_ms = t3 - t2;
     DCK(hipMalloc((void**)&d_state, need ? need : 1));
-    if (nall) {
-        rc = cly_index_device(ctx, df.data(), nall, d_tup, first.data(), res.data(), d_state, &ir, nullptr);
-        if (rc != CLY_OK) goto done;
-    }
     db->tuples.alloc(need);
     db->state.alloc(need);
-    db->khash.alloc(need);
     db->hint_pos.resize(db->n_hint);
     db->hmask = cly_ix_hash_mask_internal(need);
     db->hshift = 64 - __builtin_clzll(db->hmask | 15) - FLAT_SHARD_BITS;
-    DCK(hipStreamSynchronize(strm));
-    if (need) {
-        // the class bytes and key hashes first (what the table build reads); the
-        // tuples (what lookups read) come back while the host builds the tables
-        uint64_t* d_hash = nullptr;
-        DCK(cly_ix_hash_ptr_internal(ctx, need, (void**)&d_hash));
-        hipLaunchKernelGGL(k_state_dt, dim3((unsigned)((need + 255) / 256)), dim3(256), 0, strm, d_state, d_tup, need);
-        DCK(hipGetLastError());
-        DCK(hipStreamSynchronize(strm));
-        std::vector<D2H> parts = {{db->state.data(), d_state, need},
-                                  {db->khash.data(), d_hash, sizeof(uint64_t) * need}};
-        if (db->n_hint) parts.push_back({db->hint_pos.data(), d_hpos, sizeof(cly_pos) * db->n_hint});
-        rc = copy_to_host(ctx, parts, 0, load_threads());
+    {
+        // the tuples (what lookups read) come back on copy threads nb.. from now
+        // on, beside the index rebuild and the tables' build on the device and
+        // their read-back on threads 0 .. nb-1
+        std::unique_lock<std::mutex> lk(g_stage_mu);
+        if (stage_ready() != CLY_OK) { rc = CLY_ERR_DEVICE; goto done; }
+        const int nt = load_threads(), nb = std::max(1, nt / 2);
+        int trc = CLY_OK;
+        std::thread tcopy([&]() {
+            if (need) trc = copy_to_host(ctx, {{db->tuples.data(), d_tup, sizeof(cly_tuple) * need}}, nb,
+                                         std::max(1, nt - nb), false);
+        });
+        rc = flat_device(ctx, db, nall ? df.data() : nullptr, nall, d_tup, first, res, d_state, d_hpos, need, ir, nb);
+        tcopy.join();
+        if (rc == CLY_OK) rc = trc;
         if (rc != CLY_OK) goto done;
     }
     t4 = now_ms();
@@ -854,24 +831,11 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
     s.records = need;
     {
         // MemTable inserts (updateIndex, db.go:511-575) for the records the
-        // device marked as index entries: String / ListMeta into the flat
-        // tables, Hash / List / Set into realKey -> (field | seqBuf | hashKey) maps
+        // device marked as index entries: String / ListMeta are in the flat
+        // tables already; Hash / List / Set go into realKey -> (field | seqBuf |
+        // hashKey) maps
         std::vector<uint64_t> composite;
-        int trc = CLY_OK;
-        if (g_overlap) {
-            // the tuples' read-back on copy threads 8..15 beside the build's threads 0..7
-            const int nb = std::max(1, std::min(FLAT_SHARDS, load_threads()) / 2);
-            std::thread tcopy([&]() {
-                if (need) trc = copy_to_host(ctx, {{db->tuples.data(), d_tup, sizeof(cly_tuple) * need}}, nb,
-                                             std::max(1, load_threads() - nb));
-            });
-            flat_build(db, nb, composite);
-            tcopy.join();
-        } else {
-            flat_build(db, std::min(FLAT_SHARDS, load_threads()), composite);
-            if (need) trc = copy_to_host(ctx, {{db->tuples.data(), d_tup, sizeof(cly_tuple) * need}}, 0, load_threads());
-        }
-        if (trc != CLY_OK) { rc = trc; goto done; }
+        composite_list(db, load_threads(), composite);
         for (uint64_t i : composite) {
             const cly_tuple& t = db->tuples[i];
             uint32_t off, len;
@@ -1047,12 +1011,13 @@ static void build_entries(cly_db* db, int kind) {
         for (int sh = 0; sh < FLAT_SHARDS; sh++) {
             const FlatShard& x = xi.sh[sh];
             for (uint64_t i = 0; i <= x.mask && x.mask; i++) {
-                if (!x.h[i]) continue;
+                const uint64_t ti = flat_ti(x.s[i]);
+                if (ti == ~0ull) continue;
                 cly_db_entry e;
                 memset(&e, 0, sizeof(e));
-                e.key = real_key_ptr(db, x.ti[i], e.key_len);
-                e.pos = pos_of(db, x.ti[i]);
-                e.expiration = str && x.ti[i] >= db->n_hint ? db->tuples[x.ti[i]].expiration : 0;
+                e.key = real_key_ptr(db, ti, e.key_len);
+                e.pos = pos_of(db, ti);
+                e.expiration = str && ti >= db->n_hint ? db->tuples[ti].expiration : 0;
                 v.push_back(e);
             }
         }

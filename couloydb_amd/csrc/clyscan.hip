@@ -74,7 +74,7 @@ __device__ __forceinline__ rsrc_t mk_rsrc(const void* p, uint32_t bytes) {
 #define LM_CHAIN 1               // the chain enters the segment at E (a record start or its terminal)
 #define LM_DEAD 2                // the file's chain ended before the segment
 #define LM_OFF 3                 // segment beyond the end of the file
-#define CAP_T ((uint32_t)(CLY_TILE / 128))   // compact entries kept per tile (more: k_emit re-walks)
+#define CAP_T ((uint32_t)(CLY_TILE / 128))   // compact entries kept per tile (more: k_ovf re-walks)
 
 struct DevFile {                 // 32 B
     const uint8_t* base;         // device pointer to the file's first byte (16-B aligned)
@@ -489,9 +489,10 @@ __device__ __forceinline__ LBState ti_load(const TileIn* p) {
     return s;
 }
 #define TI_FIX 2u                // listed for k_refix this round
-__device__ __forceinline__ void ti_store(TileIn* p, const LBState& s) {
+// (word 6: the tile's file, for k_emit)
+__device__ __forceinline__ void ti_store(TileIn* p, const LBState& s, uint32_t f) {
     ((u32x4*)p)[0] = (u32x4){(uint32_t)s.count, (uint32_t)(s.count >> 32), s.X, s.dead ? TI_DEAD : 0u};
-    ((u32x4*)p)[1] = (u32x4){s.crc_last, s.P_last, 0u, 0u};
+    ((u32x4*)p)[1] = (u32x4){s.crc_last, s.P_last, f, 0u};
 }
 
 // ---------------------------------------------------------------------------
@@ -527,13 +528,40 @@ __device__ __forceinline__ void put_tuple(gtuples out, uint64_t idx, uint64_t ou
 // key0 << 19 (the txId varint's single byte).  Long form: w3 = rel only
 // (k_emit decodes the header again).
 #define REC_SHORT (1u << 26)
-__device__ __forceinline__ void rec_store(rsrc_t trs, uint32_t idx, const Hdr& h, uint32_t rel) {
+// Where a block's compact entries and snapshots go (k_scan, k_refix): the
+// wave's LDS buffers (entries c0 .. c0 + RB - 1 of the block, snapshots from
+// n0 on), written to global memory at the top of the next block, after the
+// wait for its loads, and before the loads of the block after it are issued:
+// stores issued in the block body would sit between a block's prefetch and
+// its wait (vmcnt counts loads and stores in one ordered counter), and every
+// block would wait for its own last stores.  Entries beyond the buffers go
+// out directly.
+#define RB 32
+struct RecSink { rsrc_t trs, nrs; CLY_LDS u32x4* rb; CLY_LDS uint32_t* sb; uint32_t c0, n0; FileInfo* fo; };
+__device__ __forceinline__ void rec_put(const RecSink& rs, uint32_t idx, const u32x4& v) {
+    const uint32_t j = idx - rs.c0;
+    if (j < RB) rs.rb[j] = v;
+    else if (idx < CAP_T) __builtin_amdgcn_raw_buffer_store_b128(v, rs.trs, (int)(idx * 16u), 0, 0);
+}
+__device__ __forceinline__ void snap_put(const RecSink& rs, uint32_t r, uint32_t v) {
+    const uint32_t j = r - rs.n0;
+    if (j < RB) rs.sb[j] = v;
+    else __builtin_amdgcn_raw_buffer_store_b32(v, rs.nrs, (int)(r * 4u), 0, 0);
+}
+// the buffered outputs of a block whose entries end at c1 and snapshots at n1
+__device__ __forceinline__ void sink_flush(const RecSink& rs, uint32_t c1, uint32_t n1, int lane) {
+    const uint32_t ne = c1 - rs.c0, ns = n1 - rs.n0, l = (uint32_t)lane;
+    if (l < ne && l < RB && rs.c0 + l < CAP_T)
+        __builtin_amdgcn_raw_buffer_store_b128(rs.rb[l], rs.trs, (int)((rs.c0 + l) * 16u), 0, 0);
+    if (l < ns && l < RB) __builtin_amdgcn_raw_buffer_store_b32(rs.sb[l], rs.nrs, (int)((rs.n0 + l) * 4u), 0, 0);
+}
+__device__ __forceinline__ void rec_store(const RecSink& rs, uint32_t idx, const Hdr& h, uint32_t rel) {
     const bool sh = h.exp == 0 && h.key0 < 0x80u && h.ks >= 1u && h.ks < (1u << 24) && h.type < 8u && h.dt < 8u &&
                     h.hsz >= 6 && h.hsz < 38;
     u32x4 v = (u32x4){0u, 0u, 0u, rel};
     if (sh) v = (u32x4){h.crc, h.ks | ((uint32_t)(h.hsz - 6) << 24) | (h.type << 29), h.vs,
                         rel | (h.dt << 16) | (h.key0 << 19) | REC_SHORT};
-    __builtin_amdgcn_raw_buffer_store_b128(v, trs, (int)(idx * 16u), 0, 0);
+    rec_put(rs, idx, v);
 }
 
 // ---------------------------------------------------------------------------
@@ -573,6 +601,11 @@ __device__ __forceinline__ void blk_issue(gbytes base, rsrc_t frs, uint64_t flen
     hl = (u32x4){0u, 0u, 0u, 0u};
     if (lane < 2) hl = load16z(base, (uint64_t)bs + CLY_BLK + 16 * lane, flen);
 }
+// the first block of tile tt of file F (its loads are issued by the caller of
+// tile_body, so that a wave's next tile streams in under its current one)
+__device__ __forceinline__ void tile_issue(const DevFile& F, uint32_t tt, int lane, u32x4 (&e)[4], u32x4& hl) {
+    blk_issue((gbytes)F.base, mk_rsrc(F.base, (uint32_t)F.len), F.len, (uint32_t)((uint64_t)tt * CLY_TILE), lane, e, hl);
+}
 __device__ __forceinline__ void swap32(uint32_t& a, uint32_t& b) {
     const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
     a = r[0]; b = r[1];
@@ -597,15 +630,15 @@ __device__ __forceinline__ void patch_word(uint32_t (&w)[16], uint32_t k, uint32
 }
 
 // ---------------------------------------------------------------------------
-// The tile body (k_scan, k_refix, k_emit's re-walk).  The wave streams the
+// The tile body (k_scan, k_refix, k_ovf's re-walk).  The wave streams the
 // tile's blocks in order; the chain position X is carried from block to block.
 //   BM_SPEC   k_scan: the entry of a tile other than its file's first is
 //             unknown; the first block with a plausible record start sets the
 //             tile's guess G (a candidate whose speculative walk holds and
 //             leaves at a candidate, or at a plausible header beyond the block);
 //   BM_EXACT  k_refix: the entry is the true state from k_link;
-//   BM_EMIT   k_emit: as BM_EXACT, tuples straight to their output slots (tiles
-//             whose compact list overflowed), no CRC.
+//   BM_EMIT   k_ovf: as BM_EXACT, tuples straight to their output slots (tiles
+//             whose compact list overflowed), each record's CRC checked alone.
 // CRC (not BM_EMIT): GetLogRecordCRC of the record at P is the CRC-32 of
 // F[P+4 : P+size] (data/logRecord.go:136-146).  In the CRC register's terms
 // the stream from P on, started from the register c ^ K4 (c = the stored CRC
@@ -653,17 +686,31 @@ struct TState {
     uint32_t ref_s;              // the reference record's size (the stride)
     uint32_t ref1, ref2, ref3, msk1, msk2, msk3, rw1, rw2, rw3;
 };
+// k_ovf's record check: the CRC-32 of F[P+4 : P+size], byte-serial in the lane
+__device__ __forceinline__ void rec_crc_check(const CLY_LDS uint8_t* smem, const CrcLane& cl, gbytes base, uint32_t p,
+                                              const Hdr& h, FileInfo* fo, uint64_t gidx) {
+    uint64_t a = (uint64_t)p + 4, b = (uint64_t)p + h.size;
+    uint32_t s = 0xFFFFFFFFu;
+    for (; a < b && (a & 3); a++) s = crc_byte(smem, s, base[a], cl.r4);
+    for (; a + 4 <= b; a += 4) s = crc_word(smem, s ^ *(const CLY_GL uint32_t*)(base + a), cl);
+    for (; a < b; a++) s = crc_byte(smem, s, base[a], cl.r4);
+    if (~s != h.crc) atomicMin(&fo->fail_key, ((u64)p << 32) | (u64)(gidx - fo->first_index));
+}
 // The block's outputs for record k of a round (lane k): its compact entry
-// (k_scan, k_refix) or its tuple (k_emit's re-walk).  Returns the record's
-// patch word as an index in the block: the word whose entering register its
-// CRC check reads (P's own word when P is word-aligned, else the word after
-// it; PW_CARRY: the next block's first word).
+// (k_scan, k_refix), or its tuple and CRC check (k_ovf's re-walk).  Returns
+// the record's patch word as an index in the block: the word whose entering
+// register its CRC check reads (P's own word when P is word-aligned, else the
+// word after it; PW_CARRY: the next block's first word).
 template <int BM>
 __device__ __forceinline__ uint32_t rec_out(const DevFile& F, gbytes base, uint32_t p, const Hdr& h, uint32_t idx,
-                                            uint32_t tb, uint32_t bs, rsrc_t trs, gtuples out, uint64_t out_cap,
-                                            uint64_t gbase, Globals* g) {
-    if (BM == BM_EMIT) { put_tuple(out, gbase + idx, out_cap, base, p, h, F.fid, g); return 0u; }
-    if (idx < CAP_T) rec_store(trs, idx, h, p - tb);
+                                            uint32_t tb, uint32_t bs, const RecSink& rs, gtuples out, uint64_t out_cap,
+                                            uint64_t gbase, Globals* g, const CLY_LDS uint8_t* smem, const CrcLane& cl) {
+    if (BM == BM_EMIT) {
+        put_tuple(out, gbase + idx, out_cap, base, p, h, F.fid, g);
+        rec_crc_check(smem, cl, base, p, h, rs.fo, gbase + idx);
+        return 0u;
+    }
+    rec_store(rs, idx, h, p - tb);
     return ((p - bs) >> 2) + ((p & 3u) ? 1u : 0u);
 }
 #define PW_CARRY (CLY_BLK / 4)
@@ -696,7 +743,7 @@ __device__ __forceinline__ void term_patch(TState& S, uint32_t T, uint32_t dT, u
 // budget runs out with X still in the block (the caller's general pass goes on).
 template <int BM>
 __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t tb, uint32_t bs, CLY_LDS uint32_t* stg,
-                                          const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t K4, rsrc_t trs,
+                                          const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t K4, const RecSink& rs,
                                           gtuples out, uint64_t out_cap, uint64_t gbase, Globals* g, int lane,
                                           CLY_LDS uint32_t* mk) {
     const gbytes base = (gbytes)F.base;
@@ -728,7 +775,7 @@ __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t 
         const uint32_t dq = k == 0 ? (S.cq_known ? ~S.cq : 0xFFFFFFFFu) : ~up;
         uint32_t pw = 0;
         if (acc) {
-            pw = rec_out<BM>(F, base, (uint32_t)P, h, S.tcnt + k, tb, bs, trs, out, out_cap, gbase, g);
+            pw = rec_out<BM>(F, base, (uint32_t)P, h, S.tcnt + k, tb, bs, rs, out, out_cap, gbase, g, smem, cl);
             if (BM != BM_EMIT && pw < PW_CARRY) mark_pw(mk, pw);
         }
         if (BM != BM_EMIT && __ballot(acc && pw == PW_CARRY)) S.cmark_next = true;
@@ -770,7 +817,7 @@ __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t 
 template <int BM>
 __device__ __forceinline__ void stride_round(const DevFile& F, TState& S, uint32_t tb, uint32_t bs,
                                              CLY_LDS uint32_t* stg, const CLY_LDS uint8_t* smem, const CrcLane& cl,
-                                             uint32_t K4, rsrc_t trs, int lane, CLY_LDS uint32_t* mk) {
+                                             uint32_t K4, const RecSink& rs, int lane, CLY_LDS uint32_t* mk) {
     const uint32_t X = S.X, s = S.ref_s, k = (uint32_t)lane;
     const uint64_t bend = (uint64_t)bs + CLY_BLK;
     if (S.dead || (uint64_t)X >= bend) return;
@@ -786,9 +833,7 @@ __device__ __forceinline__ void stride_round(const DevFile& F, TState& S, uint32
     if (kb == 0) return;
     uint32_t pw = 0;
     if (k < kb) {
-        if (S.tcnt + k < CAP_T)
-            __builtin_amdgcn_raw_buffer_store_b128((u32x4){crc, S.rw1, S.rw2, (P - tb) | S.rw3}, trs,
-                                                   (int)((S.tcnt + k) * 16u), 0, 0);
+        rec_put(rs, S.tcnt + k, (u32x4){crc, S.rw1, S.rw2, (P - tb) | S.rw3});
         pw = ((P - bs) >> 2) + ((P & 3u) ? 1u : 0u);
         if (pw < PW_CARRY) mark_pw(mk, pw);
     }
@@ -922,9 +967,10 @@ __device__ __forceinline__ uint32_t guess_entry(const DevFile& F, uint32_t bs, C
 template <int BM>
 __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint32_t tt, uint32_t X_in, bool dead_in,
                                              const CLY_LDS uint8_t* smem, CLY_LDS uint32_t* stg, CLY_LDS uint32_t* mk,
-                                             const CrcLane& cl, uint32_t K4, TileLocal* loc, uint32_t* rec,
-                                             uint32_t* seg, uint32_t* snap, uint32_t* treg, gtuples out,
-                                             uint64_t out_cap, uint64_t gbase, Globals* g) {
+                                             CLY_LDS uint8_t* wbuf, const CrcLane& cl, uint32_t K4, TileLocal* loc,
+                                             uint32_t* rec, uint32_t* seg, uint32_t* snap, uint32_t* treg, gtuples out,
+                                             uint64_t out_cap, uint64_t gbase, Globals* g, FileInfo* fo,
+                                             u32x4 (&e)[4], u32x4& hl, const uint8_t* nbase, uint32_t nlen, uint32_t ntb) {
     const int lane = threadIdx.x & 63;
     const uint32_t tb = (uint32_t)((uint64_t)tt * CLY_TILE);
     const uint64_t flen = F.len;
@@ -944,9 +990,11 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     const rsrc_t frs = mk_rsrc(F.base, (uint32_t)flen);
     const rsrc_t srs = mk_rsrc(seg + (uint64_t)t * NSEG, BM == BM_EMIT ? 0u : NSEG * 4u);            // segment registers
     const rsrc_t nrs = mk_rsrc(snap + (uint64_t)t * SNAP_T, BM == BM_EMIT ? 0u : (CAP_T + 1) * 4u);  // snapshots
+    RecSink rs;
+    rs.trs = trs; rs.nrs = nrs; rs.c0 = 0; rs.n0 = 0; rs.fo = fo;
+    rs.rb = (CLY_LDS u32x4*)wbuf; rs.sb = (CLY_LDS uint32_t*)(wbuf + RB * 16);
+    uint32_t Rp = 0;             // the previous block's segment register (stored with its flush)
     CLY_LDS u32x4* sv = (CLY_LDS u32x4*)stg;
-    u32x4 e[4], hl;
-    blk_issue(base, frs, flen, tb, lane, e, hl);
     #pragma unroll 1
     for (int m = 0; m < CLY_NBLK; m++) {
         const uint32_t bs = tb + (uint32_t)m * CLY_BLK;
@@ -956,7 +1004,20 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
         #pragma unroll
         for (int k = 0; k < 4; k++) { w[4 * k] = e[k].x; w[4 * k + 1] = e[k].y; w[4 * k + 2] = e[k].z; w[4 * k + 3] = e[k].w; }
         const u32x4 hc = hl;
+        if (BM != BM_EMIT) {
+            // the previous block's outputs, now that this block's loads are in
+            if (m > 0) {
+                sink_flush(rs, S.tcnt, nb, lane);
+                __builtin_amdgcn_raw_buffer_store_b32(Rp, srs, (int)(((uint32_t)(m - 1) * CLY_NL + (uint32_t)lane) * 4u), 0, 0);
+            }
+            rs.c0 = S.tcnt; rs.n0 = nb;
+        }
         if (m + 1 < CLY_NBLK && (BM != BM_EMIT || !S.dead)) blk_issue(base, frs, flen, bs + CLY_BLK, lane, e, hl);
+        else if (m + 1 == CLY_NBLK && nbase) {                                 // the wave's next tile
+            uint32_t nl = nlen, nt = ntb;
+            asm volatile("" : "+s"(nl), "+s"(nt));     // (keeps its tail masks from being hoisted out of the loop)
+            blk_issue((gbytes)nbase, mk_rsrc(nbase, nl), nl, nt, lane, e, hl);
+        }
         if (BM == BM_EMIT && S.dead) break;
         if (BM != BM_EMIT) mk[lane] = (lane == 0 && cmark) ? 1u : 0u;       // the block's patch words (carried: word 0)
         S.Tb = NONE32;
@@ -986,9 +1047,9 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
             if (S.X == NONE32) S.X = guess_entry(F, bs, stg, hc, lane);    // the tile's guessed entry
             bool done = true;
             if (S.X != NONE32) {
-                if (BM != BM_EMIT && S.ref_ok) stride_round<BM>(F, S, tb, bs, stg, smem, cl, K4, trs, lane, mk);
+                if (BM != BM_EMIT && S.ref_ok) stride_round<BM>(F, S, tb, bs, stg, smem, cl, K4, rs, lane, mk);
                 const uint32_t c0 = S.tcnt;
-                done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, trs, out, out_cap, gbase, g, lane, mk);
+                done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, rs, out, out_cap, gbase, g, lane, mk);
                 if (BM != BM_EMIT && S.tcnt != c0) stride_ref(F, S, bs, stg);
             }
             if (!done) {
@@ -1040,8 +1101,8 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                     for (uint32_t i = 0; __ballot(i < c); i++) {
                         if (i < c) {
                             const Hdr h = hdr_get(p, flen, stg, bs);
-                            const uint32_t pw = rec_out<BM>(F, base, p, h, S.tcnt + lex + i, tb, bs, trs, out,
-                                                            out_cap, gbase, g);
+                            const uint32_t pw = rec_out<BM>(F, base, p, h, S.tcnt + lex + i, tb, bs, rs, out,
+                                                            out_cap, gbase, g, smem, cl);
                             if (BM != BM_EMIT) { if (pw == PW_CARRY) cf = true; else mark_pw(mk, pw); }
                             pcq = h.crc; pk = true;
                             ppsz = psz; psz = (uint32_t)h.size;
@@ -1096,7 +1157,7 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
             uint32_t R = 0;
             #pragma unroll
             for (int k = 0; k < 16; k++) { const uint32_t x = R; R = crc_word(smem, R ^ w[k], cl); w[k] = x; }
-            __builtin_amdgcn_raw_buffer_store_b32(R, srs, (int)(((uint32_t)m * CLY_NL + (uint32_t)lane) * 4u), 0, 0);
+            Rp = R;
             // snapshots: the registers entering the marked words, in position
             // order = record order (one patch word per record start), through
             // the stage (the block's bytes there are no longer needed)
@@ -1115,7 +1176,7 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                     if (q) {
                         const uint32_t k = (uint32_t)__builtin_ctz(q);
                         q &= q - 1u;
-                        __builtin_amdgcn_raw_buffer_store_b32(stg[20u * (uint32_t)lane + k], nrs, (int)(r * 4u), 0, 0);
+                        snap_put(rs, r, stg[20u * (uint32_t)lane + k]);
                         r++;
                     }
                 }
@@ -1126,6 +1187,10 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     }
     TileRes res;
     res.X = S.X; res.dead = S.dead;
+    if (BM != BM_EMIT) {
+        sink_flush(rs, S.tcnt, nb, lane);
+        __builtin_amdgcn_raw_buffer_store_b32(Rp, srs, (int)(((uint32_t)(CLY_NBLK - 1) * CLY_NL + (uint32_t)lane) * 4u), 0, 0);
+    }
     if (BM != BM_EMIT && lane == 0) {
         // a record start whose patch word is the tile's end: its snapshot is
         // the (empty) segment after the tile's, zero; the patch itself is the
@@ -1173,12 +1238,17 @@ __device__ __forceinline__ uint32_t k4_const(const CLY_LDS uint8_t* smem, uint32
 // k_scan: one wave per tile (grid-stride), every byte of every file read once.
 #define SCAN_WAVES 16
 #define MK_BYTES (CLY_NL * 4)                                 // a wave's patch-word mask
-#define SCAN_LDS_ALL (SCAN_LDS + SCAN_WAVES * (STG_BYTES + MK_BYTES))   // tables + per wave a block stage and a mask
+#define SINK_BYTES (RB * 16 + RB * 4)                        // a wave's RecSink buffers
+#define SCAN_LDS_ALL (SCAN_LDS + SCAN_WAVES * (STG_BYTES + MK_BYTES + SINK_BYTES))   // tables + per wave a block stage, a mask, the sink
+static_assert(SCAN_LDS_ALL <= 160 * 1024, "k_scan's LDS");
 __device__ __forceinline__ CLY_LDS uint32_t* wave_stage(CLY_LDS uint8_t* smem) {
     return (CLY_LDS uint32_t*)(smem + SCAN_LDS + wave_id() * STG_BYTES);
 }
 __device__ __forceinline__ CLY_LDS uint32_t* wave_mask(CLY_LDS uint8_t* smem) {
     return (CLY_LDS uint32_t*)(smem + SCAN_LDS + SCAN_WAVES * STG_BYTES + wave_id() * MK_BYTES);
+}
+__device__ __forceinline__ CLY_LDS uint8_t* wave_sink(CLY_LDS uint8_t* smem) {
+    return smem + SCAN_LDS + SCAN_WAVES * (STG_BYTES + MK_BYTES) + wave_id() * SINK_BYTES;
 }
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
 k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
@@ -1191,11 +1261,29 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     const int lane = threadIdx.x & 63;
     const CrcLane cl = crc_lane(lane);
     const uint32_t K4 = k4_const(smem, cl.r4);
-    for (uint32_t t = blockIdx.x * SCAN_WAVES + wave_id(); t < ntiles; t += gridDim.x * SCAN_WAVES) {
-        const int f = find_file(tprefix, nfiles, t);
+    const uint32_t stride = gridDim.x * SCAN_WAVES;
+    uint32_t t = blockIdx.x * SCAN_WAVES + wave_id();
+    if (t >= ntiles) return;
+    int f = find_file(tprefix, nfiles, t);
+    u32x4 e[4], hl;
+    {
         const DevFile F = files[f];
-        tile_body<BM_SPEC>(F, t, t - F.first_tile, 0u, false, smem, stg, mk, cl, K4, loc, rec, seg, snap, treg, nullptr,
-                           0, 0, g);
+        tile_issue(F, t - F.first_tile, lane, e, hl);
+    }
+    for (;;) {
+        const uint32_t tn = t + stride;
+        const int fn = tn < ntiles ? find_file(tprefix, nfiles, tn) : -1;
+        const uint8_t* nbase = nullptr;
+        uint32_t nlen = 0, ntb = 0;
+        if (fn >= 0) {
+            nbase = files[fn].base; nlen = (uint32_t)files[fn].len;
+            ntb = (tn - files[fn].first_tile) * (uint32_t)CLY_TILE;
+        }
+        const DevFile F = files[f];
+        tile_body<BM_SPEC>(F, t, t - F.first_tile, 0u, false, smem, stg, mk, wave_sink(smem), cl, K4, loc, rec, seg, snap,
+                           treg, nullptr, 0, 0, g, nullptr, e, hl, nbase, nlen, ntb);
+        if (fn < 0) break;
+        t = tn; f = fn;
     }
 }
 
@@ -1303,7 +1391,7 @@ k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restric
             if (l0 & DF_NONE) bad = s.X < (uint32_t)l3;
             else bad = s.X != (uint32_t)l1;
         }
-        ti_store(&tin[F.first_tile + u], s);
+        ti_store(&tin[F.first_tile + u], s, (uint32_t)f);
         if (bad) {
             if (u < LINK_MAXT) atomicOr(&badm[u >> 5], 1u << (u & 31));
             else atomicMin(&bad_far, u);
@@ -1418,8 +1506,10 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
         }
     }
     for (;;) {
-        const TileRes r = tile_body<BM_EXACT>(F, t, t - F.first_tile, S.X, S.dead != 0, smem, stg, mk, cl, K4, loc, rec,
-                                              seg, snap, treg, nullptr, 0, 0, g);
+        u32x4 e[4], hl;
+        tile_issue(F, t - F.first_tile, lane, e, hl);
+        const TileRes r = tile_body<BM_EXACT>(F, t, t - F.first_tile, S.X, S.dead != 0, smem, stg, mk, wave_sink(smem), cl,
+                                              K4, loc, rec, seg, snap, treg, nullptr, 0, 0, g, nullptr, e, hl, nullptr, 0u, 0u);
         S.X = r.X; S.dead = r.dead;
         if (S.dead || t + 1 >= F.first_tile + F.ntile) break;
         // the next tile: consistent with the new exit?  else it is re-resolved too
@@ -1465,15 +1555,14 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
 //   records) and dev.
 #define RUN (CLY_NBLK)                          // segments per lane in k_emit's scan
 #define RUN_BYTES (RUN * CLY_SEG)
-#define EMIT_WAVES 16
+#define EMIT_WAVES 4
 #define SHORT_MAXN 256                          // records per tile of the per-record path
 #define SHORT_KMAX 32                           // segments one record may span there
 #define GIN_WORDS (NSEG + 4)                    // segment registers / the scan (+ the tile's end)
-#define TUP_BYTES (64 * 48)                     // a round's tuples
 #define FLG_BYTES (NSEG / 8)                    // segments that hold a reset (tile-wide scan)
-#define EW_RAW (GIN_WORDS * 4 + TUP_BYTES + FLG_BYTES > STG_BYTES ? GIN_WORDS * 4 + TUP_BYTES + FLG_BYTES : STG_BYTES)
-#define EW_BYTES ((EW_RAW + 15) & ~15)
-#define EMIT_LDS (NEM * 128 * 4 + EMIT_WAVES * EW_BYTES)
+#define EW_BYTES ((GIN_WORDS * 4 + FLG_BYTES + 15) & ~15)
+#define EMIT_KJ (NEM * 128)                    // kj[4] after the tables (words)
+#define EMIT_LDS (NEM * 128 * 4 + 16 + EMIT_WAVES * EW_BYTES)
 static_assert(CLY_NL * RUN == NSEG, "one run of segments per lane");
 __device__ __forceinline__ uint32_t gin_at(uint32_t sg) {      // LDS word of segment sg (lane-transposed)
     return sg < NSEG ? (sg % RUN) * 64u + sg / RUN : NSEG;
@@ -1498,9 +1587,9 @@ __device__ __forceinline__ uint32_t exp_pre(const CLY_LDS uint32_t* emt, uint32_
 // The register entering the patch word of a record start P (stored CRC c) as
 // the walk restarts at P: c ^ K4 at P; for j != 0 the 4 - j bytes of c up to
 // the word boundary, A^(4-j) (c ^ K4 ^ (c's low bytes)) = (c >> 8 (4-j)) ^
-// A^(4-j) K4 (kj[j]).
-__device__ __forceinline__ uint32_t exp_post(uint32_t j, uint32_t c, const uint32_t (&kj)[4]) {
-    return j ? (c >> (8u * (4u - j))) ^ (j == 1 ? kj[1] : j == 2 ? kj[2] : kj[3]) : c ^ kj[0];
+// A^(4-j) K4 (kj[j], in LDS: a lane-indexed register array would live in scratch).
+__device__ __forceinline__ uint32_t exp_post(uint32_t j, uint32_t c, const CLY_LDS uint32_t* kj) {
+    return (j ? c >> (8u * (4u - j)) : c) ^ kj[j];
 }
 __device__ __forceinline__ uint32_t entry_crc(gbytes base, uint64_t len, uint32_t tb, const u32x4& v) {
     return (v.w & REC_SHORT) ? v.x : hdr_load(base, tb + (v.w & 0xFFFFu), len).crc;
@@ -1532,20 +1621,18 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     CLY_LDS uint32_t* emt = (CLY_LDS uint32_t*)smem_raw;
     for (int i = threadIdx.x; i < NEM * 128; i += blockDim.x) emt[i] = tabs[TAB_EM + i];
     __syncthreads();
-    CLY_LDS uint8_t* wreg = (CLY_LDS uint8_t*)smem_raw + NEM * 128 * 4 + wave_id() * EW_BYTES;
+    CLY_LDS uint32_t* kj = emt + EMIT_KJ;
+    if (threadIdx.x < 4) kj[threadIdx.x] = threadIdx.x ? em_fj(emt, threadIdx.x, CLY_K4) : CLY_K4;
+    __syncthreads();
+    CLY_LDS uint8_t* wreg = (CLY_LDS uint8_t*)smem_raw + NEM * 128 * 4 + 16 + wave_id() * EW_BYTES;
     CLY_LDS uint32_t* gin = (CLY_LDS uint32_t*)wreg;                  // segment registers, then the scan
-    CLY_LDS u32x4* sv = (CLY_LDS u32x4*)(wreg + GIN_WORDS * 4);       // a round's tuples
-    CLY_LDS uint32_t* flg = (CLY_LDS uint32_t*)(wreg + GIN_WORDS * 4 + TUP_BYTES);   // reset segments (bitmap)
-    CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)wreg;                  // the re-walk's stage (overflowed tiles)
+    CLY_LDS uint32_t* flg = (CLY_LDS uint32_t*)(wreg + GIN_WORDS * 4);   // reset segments (bitmap)
     const int lane = threadIdx.x & 63;
-    const CrcLane cl = crc_lane(lane);
-    uint32_t kj[4];
-    kj[0] = CLY_K4; kj[1] = em_fj(emt, 1, CLY_K4); kj[2] = em_fj(emt, 2, CLY_K4); kj[3] = em_fj(emt, 3, CLY_K4);
     for (uint32_t t = blockIdx.x * EMIT_WAVES + wave_id(); t < ntiles; t += gridDim.x * EMIT_WAVES) {
-        const int f = find_file(tprefix, nfiles, t);
-        const DevFile F = files[f];
         const LBState S = ti_load(&tin[t]);
         if (S.dead) continue;
+        const int f = (int)__builtin_amdgcn_readfirstlane(((const uint32_t*)&tin[t])[6]);
+        const DevFile F = files[f];
         FileInfo* fo = &finfo[f];
         const uint64_t gb = S.count + fo->first_index;
         const u64 l0 = loc[t].l[0], l1 = loc[t].l[1], l3 = loc[t].l[3];
@@ -1620,7 +1707,10 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                         const Hdr h = hdr_load(base, p, F.len);
                         tuple_words(base, p, h, F.fid, a, b, c);
                     }
-                    sv[3 * lane] = a; sv[3 * lane + 1] = b; sv[3 * lane + 2] = c;
+                    if (gb + i < out_cap) {
+                        CLY_GL u32x4* dst = (CLY_GL u32x4*)(out + gb + i);
+                        dst[0] = a; dst[1] = b; dst[2] = c;
+                    } else atomicOr(&g->overflow, 1u);
                     if (!full) {
                         const uint32_t cr = c.w;                            // this record's stored CRC
                         q.Wr = patch_word_of(p);
@@ -1656,36 +1746,12 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                         if (bl) ex = rdl(val, __ffsll((long long)bl) - 1) ^ cout;
                     }
                 }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                // the round's tuples are 48 (n - i0) contiguous bytes: 16-B pieces q = lane + 64 k
-                const uint32_t nr = n - i0 < 64 ? n - i0 : 64;
-                CLY_GL u32x4* dst = (CLY_GL u32x4*)(out + gb + i0);
-                #pragma unroll
-                for (int k = 0; k < 3; k++) {
-                    const uint32_t qq = (uint32_t)lane + 64u * k;
-                    if (qq < 3 * nr) {
-                        if (gb + i0 + qq / 3 < out_cap) dst[qq] = sv[qq];
-                        else atomicOr(&g->overflow, 1u);
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
-        } else {
-            // more records than the compact list holds: the body again, tuples
-            // direct; k_ovf checks these records one by one
-            tile_body<BM_EMIT>(F, t, tt, S.X, false, (const CLY_LDS uint8_t*)emt, stg, nullptr, cl, 0u, nullptr,
-                               nullptr, nullptr, nullptr, nullptr, out, out_cap, gb, g);
-            if (lane == 0) {
-                const uint32_t k = atomicAdd(&g->n_ovf, 1u);
-                ovf[k] = (u32x4){(uint32_t)f, n, (uint32_t)gb, (uint32_t)(gb >> 32)};
-            }
-            // the segment registers again (the re-walk used this LDS as its stage)
-            #pragma unroll
-            for (int k = 0; k < RUN; k++) gin[k * 64 + lane] = sr[k];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else if (lane == 0) {
+            // more records than the compact list holds: k_ovf walks the tile
+            // again, writes its tuples and checks its records one by one
+            const uint32_t k = atomicAdd(&g->n_ovf, 1u);
+            ovf[k] = (u32x4){(uint32_t)f, t, (uint32_t)gb, (uint32_t)(gb >> 32)};
         }
         if (full) {
             // ---- the tile-wide scan: the segments whose last boundary is a
@@ -1863,34 +1929,33 @@ k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __rest
 }
 
 // ---------------------------------------------------------------------------
-// k_ovf (only for tiles whose compact list overflowed; k_emit lists them): every
-// record of such a tile gets its CRC-32 computed alone (one lane per record,
-// table steps from LDS) and compared with the stored one (data/logRecord.go:
-// 136-146, data/dataFile.go:105-109); the first failing record of a file wins.
-__global__ void __launch_bounds__(1024)
-k_ovf(const DevFile* __restrict__ files, FileInfo* finfo, const cly_tuple* __restrict__ tup, uint64_t out_cap,
-      const u32x4* __restrict__ ovf, const Globals* g, int slot) {
+// k_ovf (only for tiles whose compact list overflowed; k_emit lists them): one
+// wave per listed tile walks it again from its final entry (tile_body,
+// BM_EMIT), writes every record's tuple to its slot and computes the record's
+// CRC-32 alone (one lane per record, table steps from LDS), compared with the
+// stored one (data/logRecord.go:136-146, data/dataFile.go:105-109); the first
+// failing record of a file wins.
+#define OVF_LDS (SCAN_LDS + SCAN_WAVES * STG_BYTES)
+__global__ void __launch_bounds__(64 * SCAN_WAVES)
+k_ovf(const DevFile* __restrict__ files, FileInfo* finfo, const TileIn* __restrict__ tin, cly_tuple* out_,
+      uint64_t out_cap, const u32x4* __restrict__ ovf, Globals* g, int slot) {
     if (!g->n_ovf || g->nfix[slot] || g->fail) return;     // (uniform: before the LDS setup's barrier)
-    __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS];
+    __shared__ __attribute__((aligned(16))) unsigned char smem_raw[OVF_LDS];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
     init_tables(smem);
+    CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)(smem + SCAN_LDS + wave_id() * STG_BYTES);
     const CrcLane cl = crc_lane(threadIdx.x & 63);
     const uint32_t nl = g->n_ovf;
-    for (uint32_t k = blockIdx.x; k < nl; k += gridDim.x) {
+    for (uint32_t k = blockIdx.x * SCAN_WAVES + wave_id(); k < nl; k += gridDim.x * SCAN_WAVES) {
         const u32x4 e = ovf[k];
-        FileInfo* fo = &finfo[e.x];
-        const gbytes base = (gbytes)files[e.x].base;
+        const DevFile F = files[e.x];
+        const uint32_t t = e.y;
         const uint64_t gb = ((uint64_t)e.w << 32) | e.z;
-        for (uint32_t i = threadIdx.x; i < e.y; i += blockDim.x) {
-            if (gb + i >= out_cap) break;
-            const cly_tuple T = tup[gb + i];
-            uint64_t a = (uint64_t)T.offset + 4, b = (uint64_t)T.offset + T.size;
-            uint32_t s = 0xFFFFFFFFu;
-            for (; a < b && (a & 3); a++) s = crc_byte(smem, s, base[a], cl.r4);
-            for (; a + 4 <= b; a += 4) s = crc_word(smem, s ^ *(const CLY_GL uint32_t*)(base + a), cl);
-            for (; a < b; a++) s = crc_byte(smem, s, base[a], cl.r4);
-            if (~s != T.crc) atomicMin(&fo->fail_key, ((u64)(uint64_t)T.offset << 32) | (u64)(gb + i - fo->first_index));
-        }
+        const LBState S = ti_load(&tin[t]);
+        u32x4 blk[4], hl;
+        tile_issue(F, t - F.first_tile, threadIdx.x & 63, blk, hl);
+        tile_body<BM_EMIT>(F, t, t - F.first_tile, S.X, false, smem, stg, nullptr, nullptr, cl, 0u, nullptr, nullptr,
+                           nullptr, nullptr, nullptr, (gtuples)out_, out_cap, gb, g, &finfo[e.x], blk, hl, nullptr, 0u, 0u);
     }
 }
 
@@ -2045,10 +2110,14 @@ static int ensure_tiles(cly_ctx* c, int64_t ntiles) {
 // the largest file length the tile arithmetic (u32 offsets) takes
 #define MAX_FILE_LEN (0xFFFFFFFFull - 2 * (uint64_t)CLY_TILE)
 
-extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple* d_out, uint64_t out_cap,
-                               uint64_t* file_first, cly_file_result* res, uint64_t* needed, cly_stats* stats,
-                               void* stream_v) {
+// alloc != nullptr: the output is allocated here (hipMalloc, the caller frees
+// it) once the link knows the exact record count, so that it holds exactly
+// needed + 16 tuples (d_out and out_cap are ignored).
+static int scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple* d_out, uint64_t out_cap,
+                       uint64_t* file_first, cly_file_result* res, uint64_t* needed, cly_stats* stats, void* stream_v,
+                       cly_tuple** alloc, uint64_t* alloc_cap) {
     if (!c || (!files && nfiles) || nfiles < 0 || !res || !file_first) return CLY_ERR_ARG;
+    if (alloc) { *alloc = nullptr; d_out = nullptr; out_cap = 0; }
     if (nfiles == 0) { if (needed) *needed = 0; return CLY_OK; }
     HIPCK(hipSetDevice(c->device));
     hipStream_t st = stream_v ? (hipStream_t)stream_v : c->stream;
@@ -2120,7 +2189,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
                            c->d_tin, c->d_tabs, c->d_pw, c->d_g, slot);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[4], st));
-        hipLaunchKernelGGL(k_ovf, dim3(c->loc_grid), dim3(1024), 0, st, c->d_files, c->d_finfo, d_out, out_cap,
+        hipLaunchKernelGGL(k_ovf, dim3(c->loc_grid), dim3(64 * SCAN_WAVES), 0, st, c->d_files, c->d_finfo, c->d_tin, d_out, out_cap,
                            c->d_ovf, c->d_g, slot);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[7], st));
@@ -2129,7 +2198,21 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         HIPCK(hipStreamSynchronize(st));
         return CLY_OK;
     };
-    int rc2 = launch_emit();
+    // (alloc: the output once the count is final, after any repair rounds)
+    auto emit_alloc = [&]() -> int {
+        out_cap = c->h_g->total + 16;
+        HIPCK(hipMalloc((void**)alloc, sizeof(cly_tuple) * out_cap));
+        d_out = *alloc;
+        if (alloc_cap) *alloc_cap = out_cap;
+        return launch_emit();
+    };
+    int rc2 = CLY_OK;
+    if (!alloc) rc2 = launch_emit();
+    else {
+        HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
+        HIPCK(hipStreamSynchronize(st));
+        if (!c->h_g->nfix[slot] && !c->h_g->fail) rc2 = emit_alloc();
+    }
     if (rc2) return rc2;
     float ms_fix = 0;
     uint32_t rounds = 1, refixed = 0;
@@ -2159,7 +2242,7 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
         HIPCK(hipEventElapsedTime(&ms_fix, c->ev[5], c->ev[6]));
         if (!c->h_g->fail) {
             HIPCK(hipEventRecord(c->ev[2], st));
-            rc2 = launch_emit();
+            rc2 = alloc ? emit_alloc() : launch_emit();
             if (rc2) return rc2;
         }
     }
@@ -2202,6 +2285,21 @@ extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cl
     }
     if (c->h_g->overflow || c->h_g->total > out_cap) return CLY_ERR_CAPACITY;
     return CLY_OK;
+}
+extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple* d_out, uint64_t out_cap,
+                               uint64_t* file_first, cly_file_result* res, uint64_t* needed, cly_stats* stats,
+                               void* stream_v) {
+    return scan_device(c, files, nfiles, d_out, out_cap, file_first, res, needed, stats, stream_v, nullptr, nullptr);
+}
+// The open's scan (clyload.hip; not in the public header): the tuple buffer
+// sized by the exact record count (*d_out, *cap slots; the caller frees it).
+extern "C" int cly_scan_device_alloc_internal(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple** d_out,
+                                              uint64_t* cap, uint64_t* file_first, cly_file_result* res,
+                                              uint64_t* needed) {
+    if (!d_out) return CLY_ERR_ARG;
+    const int rc = scan_device(c, files, nfiles, nullptr, 0, file_first, res, needed, nullptr, nullptr, d_out, cap);
+    if (rc != CLY_OK && *d_out) { hipFree(*d_out); *d_out = nullptr; }
+    return rc;
 }
 
 // Host-memory entry.  Inputs of at least PIPE_MIN bytes go through a

@@ -77,6 +77,7 @@ typedef struct cly_load_stats {
     uint32_t sweep_files;     /* new data files the sweep's appends opened        */
     uint32_t n_shards;        /* contexts that loaded files (cly_db_open_multi)   */
     uint32_t _pad2;
+    uint64_t tuple_slots;     /* device tuple slots the scans allocated (exact: records + 16 per shard) */
 } cly_load_stats;
 
 /* NewCouloyDB's Options the open uses.                                        */

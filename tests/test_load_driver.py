@@ -435,3 +435,25 @@ def test_gpu_open_multi_rejects_repeated_context(scanner, tmp_path):
     with pytest.raises(ScanError) as e:
         open_db_multi([scanner, scanner], str(tmp_path))
     assert e.value.code == _abi.ERR_ARG
+
+
+@pytest.mark.gpu
+def test_gpu_open_tuple_alloc_exact(scanner, tmp_path):
+    """The open's device tuple buffer is sized by the exact record count the
+    link finds (records + 16 per shard), not by a bytes/9 bound: checked on a
+    C3-shaped corpus (bench.make_workload("c3") at 192 MiB: Zipf value sizes
+    64 B-64 KiB), where bytes/9 would be ~40x the records; every String key
+    is found at its record."""
+    import torch
+    import bench
+    wl = bench.make_workload("c3", torch, size=192 << 20)
+    for i, (_, ln, fid) in enumerate(wl.dev_files):
+        wl.file_bytes(i).tofile(str(tmp_path / ("%09d.cly" % fid)))
+    with scanner.open_db(str(tmp_path)) as db:
+        st = db.stats
+        assert st.records == wl.expect_records
+        assert st.tuple_slots == st.records + 16 * st.n_shards
+        assert st.tuple_slots <= 1.1 * st.records
+        assert st.str_keys == st.records
+    del wl
+    torch.cuda.empty_cache()

@@ -1,0 +1,10 @@
+#!/bin/bash
+# full GPU suite, then C2 kernel stats of the built library
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/r4d
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -q -x --timeout 300 --timeout-method thread -m gpu > gpurun_out/r4d/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/r4d/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+CFG=c2 bash tools/gpu_xp.sh libclyscan.so "$@"

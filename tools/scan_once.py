@@ -12,7 +12,11 @@ n = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 lib = sys.argv[3] if len(sys.argv) > 3 else "libclyscan.so"
 wl = make_workload(cfg, torch)
 sc = Scanner(0, lib=lib)
+st = need = None
 for _ in range(n):
-    first, res, st, need = sc.scan_device(wl.dev_files, wl.d_out.data_ptr(), wl.out_cap)
+    try:
+        first, res, st, need = sc.scan_device(wl.dev_files, wl.d_out.data_ptr(), wl.out_cap)
+    except Exception as e:  # experiment builds that break the chain: the kernel times still count
+        print("scan error:", e, flush=True)
 torch.cuda.synchronize()
-print(cfg, lib, "need", need, "passes", st.passes, sc.kernel_ms(), flush=True)
+print(cfg, lib, "need", need, "passes", st.passes if st else None, sc.kernel_ms(), flush=True)
