@@ -182,15 +182,18 @@ def cpu_baseline(wl, budget_s=12.0):
         i += 1
     alg_gibs = nbytes / t_alg / 2**30
     # the same restatement with the files spread over MT_THREADS threads (the
-    # box's CPU share), over the configuration's first MT_THREADS files (one
-    # file per thread)
-    mt_files = list(range(min(MT_THREADS, len(wl.dev_files))))
-    mt_arrs = [wl.file_bytes(i) for i in mt_files]
-    t0 = time.perf_counter()
-    mt_rec = int(co.scan_files_mt(mt_arrs, [wl.dev_files[i][2] for i in mt_files], MT_THREADS))
-    t_mt = time.perf_counter() - t0
-    mt_bytes = sum(len(a) for a in mt_arrs)
-    del mt_arrs
+    # box's CPU share), over ALL the configuration's files: groups of
+    # MT_THREADS files (one file per thread), only the scans timed
+    t_mt, mt_rec, mt_bytes = 0.0, 0, 0
+    nf_all = len(wl.dev_files)
+    for g0 in range(0, nf_all, MT_THREADS):
+        grp = list(range(g0, min(g0 + MT_THREADS, nf_all)))
+        arrs = [wl.file_bytes(i) for i in grp]
+        t0 = time.perf_counter()
+        mt_rec += int(co.scan_files_mt(arrs, [wl.dev_files[i][2] for i in grp], MT_THREADS))
+        t_mt += time.perf_counter() - t0
+        mt_bytes += sum(len(a) for a in arrs)
+        del arrs
     try:
         affinity = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
@@ -199,7 +202,8 @@ def cpu_baseline(wl, budget_s=12.0):
              "cores_note": "the GPU box's CPU share per GPU (OMP_NUM_THREADS/MAX_JOBS are 16 there; nproc and "
                            "the affinity mask report the whole host, %s CPUs)" % affinity,
              "mrecords_per_s": round(mt_rec / t_mt / 1e6, 3),
-             "sample": "%d files (%.2f GiB), one file per thread, clyo_scan_files_mt" % (len(mt_files), mt_bytes / 2**30)}
+             "sample": "all %d files (%.2f GiB) in groups of %d, one file per thread, %d threads, clyo_scan_files_mt" % (
+                 nf_all, mt_bytes / 2**30, MT_THREADS, MT_THREADS)}
     merge_part = None
     if wl.name == "c4":
         # scan + merge rewrite of the sampled files (file i's live bytes follow the

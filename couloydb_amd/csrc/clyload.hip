@@ -552,6 +552,7 @@ static int flat_device(cly_ctx* ctx, cly_db* db, const cly_file* df, int nall, c
         if (rc != CLY_OK) return rc;
     }
     if (!need) return hipStreamSynchronize(strm) == hipSuccess ? CLY_OK : CLY_ERR_DEVICE;
+    if (need >= FLAT_TI_MASK) return CLY_ERR_ARG;                 // (a slot holds a 40-bit tuple index)
     int rc = CLY_OK;
     uint64_t* d_hash = nullptr;
     unsigned long long* d_cnt = nullptr;

@@ -44,7 +44,7 @@ extern "C" void** cly_ctx_merge_slot_internal(cly_ctx* c);
 
 // Scratch buffers of the merge, kept in the context and grown on demand
 // (plain hipMalloc: no allocation inside a timed merge once warm).
-enum { MS_FB, MS_TOT, MS_PLAN, MS_BSUM, MS_ENT, MS_FSTART, MS_FLEN, MS_CP, MS_PRE, MS_BMAP, MS_HSZ,
+enum { MS_FB, MS_TOT, MS_PLAN, MS_BSUM, MS_ENT, MS_FSTART, MS_FLEN, MS_CP, MS_PRE, MS_BMAP, MS_HSZ, MS_KEYS,
        MS_A0 = 16, MS_AN = MS_A0 + 16,            // cly_append_device's buffers
        MS_I0 = MS_AN, MS_IN = MS_I0 + 32,         // cly_index_device's buffers (clyindex.hip)
        MS_N = MS_IN };
@@ -93,7 +93,14 @@ extern "C" hipError_t cly_ix_scratch_internal(cly_ctx* ctx, int k, size_t bytes,
 
 struct MSum { unsigned long long bytes, count; };
 struct MEnt { uint64_t g; uint32_t tuple, nsz; };
+// pre: the re-encoded prefix's bytes (bits 0-7; 0: verbatim from src); for
+// the merge also the realKey's offset from src (bits 8-15) and its length
+// (bits 16-31, 0xFFFF: longer), for the hint records
 struct MCopy { uint64_t dst, src; uint32_t size, pre; };
+#define MC_PRE(x) ((x) & 0xFFu)
+#define MC_KOFF(x) (((x) >> 8) & 0xFFu)
+#define MC_RK(x) ((x) >> 16)
+#define MH_KEY 16                    // realKey bytes k_mcopy keeps per live record for k_mhint
 struct MTot {                        // device totals, read back by the host
     unsigned long long nl, bytes, hint_bytes, n_re;
     uint32_t n_out, bad;
@@ -385,9 +392,10 @@ k_mplace(const MEnt* __restrict__ e, const cly_tuple* __restrict__ tup, const ui
         MCopy c;
         c.dst = dst;
         c.size = m.nsz;
+        const uint32_t kx = (rk < 0xFFFFu ? rk : 0xFFFFu) << 16;
         if (!(plan[m.tuple] & PLAN_RE)) {
             c.src = (uint64_t)F;
-            c.pre = 0;
+            c.pre = kx | ((uint32_t)(t.header_size + t.txid_len) << 8);
         } else {
             // new header: crc, type, dtype, varint(1+rk), varint(vs), varint(exp), then key byte 0x00
             uint8_t h[M_PRE];
@@ -407,7 +415,7 @@ k_mplace(const MEnt* __restrict__ e, const cly_tuple* __restrict__ tup, const ui
             h[0] = (uint8_t)crc; h[1] = (uint8_t)(crc >> 8); h[2] = (uint8_t)(crc >> 16); h[3] = (uint8_t)(crc >> 24);
             uint8_t* pj = pre + j * M_PRE;
             for (int q = 0; q <= n; q++) pj[q] = h[q];
-            c.pre = (uint32_t)n + 1;
+            c.pre = kx | ((uint32_t)n + 1);
             c.src = (uint64_t)rkey;
             nre++;
         }
@@ -462,9 +470,8 @@ __device__ __forceinline__ uint32_t byte_of(uint64_t lo, uint64_t hi, int q) {
 }
 __global__ void __launch_bounds__(M_NT)
 k_mhint(const MEnt* __restrict__ e, const MCopy* __restrict__ cp, const cly_tuple* __restrict__ tup,
-        const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases, int nfiles,
-        const uint32_t* __restrict__ hsz, const MSum* __restrict__ bsum, const MTot* tot, uint64_t stride,
-        uint8_t* hint, uint64_t hint_cap) {
+        const uint4* __restrict__ keys, const uint32_t* __restrict__ hsz, const MSum* __restrict__ bsum,
+        const MTot* tot, uint64_t stride, uint8_t* hint, uint64_t hint_cap) {
     __shared__ uint32_t t4[1024];
     __shared__ MSum sh[M_NT / 64];
     __shared__ __attribute__((aligned(16))) uint8_t buf[MH_BUF + 48];
@@ -488,13 +495,16 @@ k_mhint(const MEnt* __restrict__ e, const MCopy* __restrict__ cp, const cly_tupl
         const bool mine = j < nl && ho + hs <= hint_cap;
         uint32_t s = 0xFFFFFFFFu;
         if (mine) {
-            const MEnt m = e[j];
-            const cly_tuple t = tup[m.tuple];
-            // the copy descriptor already points into the record (verbatim: its
-            // start; re-encoded: its realKey): no file lookup
+            // the copy descriptor locates the realKey (its first MH_KEY bytes
+            // are in keys[j], kept by k_mcopy); the tuple only for keys of 64 KiB on
             const MCopy c = cp[j];
-            const uint8_t* rkey = c.pre ? (const uint8_t*)c.src : (const uint8_t*)c.src + t.header_size + t.txid_len;
-            const uint32_t rk = t.key_size - t.txid_len;
+            const uint8_t* rkey = (const uint8_t*)c.src + MC_KOFF(c.pre);
+            uint32_t rk = MC_RK(c.pre);
+            if (rk == 0xFFFFu) {
+                const cly_tuple t = tup[e[j].tuple];
+                rk = t.key_size - t.txid_len;
+            }
+            const uint4 k4 = rk <= MH_KEY ? keys[j] : make_uint4(0, 0, 0, 0);
             const uint64_t fid = c.dst / stride, off = c.dst - fid * stride;
             int nf, nofs, nk;
             const uint64_t pf = uv_pack(zz((int64_t)fid), nf), po = uv_pack(zz((int64_t)off), nofs);
@@ -514,18 +524,26 @@ k_mhint(const MEnt* __restrict__ e, const MCopy* __restrict__ cp, const cly_tupl
             #pragma unroll
             for (int q = 4; q < 14; q++)
                 if (q < n) put((uint32_t)q, byte_of(hl, hh, q));
-            // realKey: aligned dwords holding its bytes, shifted into place
-            const uintptr_t ka = (uintptr_t)rkey;
-            const CLY_GLB uint32_t* kw = (const CLY_GLB uint32_t*)(ka & ~(uintptr_t)3);
-            const uint32_t kb = (uint32_t)(ka & 3);
-            uint32_t prev = rk ? kw[0] : 0u;
-            for (uint32_t q = 0, k = 0; q < rk; q += 4, k++) {
-                const uint32_t nxt = 4 * (k + 1) < kb + rk ? kw[k + 1] : 0u;
-                const uint32_t x = __builtin_amdgcn_alignbit(nxt, prev, 8 * kb);
+            if (rk <= MH_KEY) {
+                // realKey from k_mcopy's copy
+                const uint32_t kd[4] = {k4.x, k4.y, k4.z, k4.w};
                 #pragma unroll
-                for (int i = 0; i < 4; i++)
-                    if (q + i < rk) put((uint32_t)n + q + i, (x >> (8 * i)) & 0xffu);
-                prev = nxt;
+                for (int q = 0; q < MH_KEY; q++)
+                    if ((uint32_t)q < rk) put((uint32_t)n + q, (kd[q >> 2] >> (8 * (q & 3))) & 0xffu);
+            } else {
+                // realKey: aligned dwords holding its bytes, shifted into place
+                const uintptr_t ka = (uintptr_t)rkey;
+                const CLY_GLB uint32_t* kw = (const CLY_GLB uint32_t*)(ka & ~(uintptr_t)3);
+                const uint32_t kb = (uint32_t)(ka & 3);
+                uint32_t prev = kw[0];
+                for (uint32_t q = 0, k = 0; q < rk; q += 4, k++) {
+                    const uint32_t nxt = 4 * (k + 1) < kb + rk ? kw[k + 1] : 0u;
+                    const uint32_t x = __builtin_amdgcn_alignbit(nxt, prev, 8 * kb);
+                    #pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        if (q + i < rk) put((uint32_t)n + q + i, (x >> (8 * i)) & 0xffu);
+                    prev = nxt;
+                }
             }
             #pragma unroll
             for (int q = 0; q < 10; q++)
@@ -658,7 +676,7 @@ template <int CMAX, int PRE, bool TWO>
 __global__ void __launch_bounds__(64 * MC_W, 4)
 k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uint32_t* __restrict__ bmap,
         const uint64_t* __restrict__ fstart, const uint64_t* __restrict__ flen, uint64_t stride,
-        uint64_t nblocks, uint8_t* out, uint64_t lo0) {
+        uint64_t nblocks, uint8_t* out, uint64_t lo0, uint4* keys) {
     __shared__ mc_u32x4 s_desc[MC_W][CMAX];              // source (lo, hi), rel (dst - block start), size
     __shared__ uint8_t s_pre[MC_W][CMAX];
     __shared__ mc_u32x4 s_map[MC_W][MC_NPIECE / 4];      // piece -> descriptor
@@ -795,6 +813,22 @@ k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uin
             for (int q = 0; q < 16; q++) v[q >> 2] |= (uint32_t)*bp[q] << (8 * (q & 3));
             *(uint4*)(out + B + d) = make_uint4(v[0], v[1], v[2], v[3]);
         }
+        if (keys) {
+            // the merge's hint records: the first MH_KEY realKey bytes of every
+            // record starting in the block, re-read from the source lines the
+            // block's loads just brought into L2 (k_mhint then reads 16 B per
+            // record instead of a line of the file)
+            for (uint32_t q = lane; q < cnt; q += 64) {
+                if ((int32_t)desc[q].z < 0) continue;               // started in an earlier block
+                const uint32_t px = cp[j0 + q].pre;
+                if (MC_RK(px) > MH_KEY) continue;
+                const mc_u32x4 D = desc[q];
+                uint32_t kw[4];
+                kw[0] = kw[1] = kw[2] = kw[3] = 0u;
+                if (MC_RK(px)) mc_part((((uint64_t)D.y << 32) | D.x) + MC_KOFF(px), (int)MC_RK(px), kw);   // (its bytes only)
+                keys[j0 + q] = make_uint4(kw[0], kw[1], kw[2], kw[3]);
+            }
+        }
     }
 }
 
@@ -840,6 +874,7 @@ extern "C" int cly_merge_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     MCopy* d_cp = nullptr;
     uint8_t* d_pre = nullptr;
     uint32_t *d_bmap = nullptr, *d_hsz = nullptr;
+    uint4* d_keys = nullptr;
     MTot* d_tot = nullptr;
     MTot h_tot;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -905,14 +940,15 @@ extern "C" int cly_merge_device(cly_ctx* ctx, const cly_file* files, int nfiles,
             rc = CLY_ERR_CAPACITY;
             goto done;
         }
-        k_mhint<<<(unsigned)lblk, M_NT, 0, st>>>(d_ent, d_cp, d_tuples, d_fb, d_fb + nfiles + 1, nfiles, d_hsz, d_bsum,
-                                                  d_tot, stride, d_hint, hint_cap);
-        MDBG(st, "k_mhint");
+        MCK(scratch(ctx, MS_KEYS, sizeof(uint4) * nl, &d_keys));
         const uint64_t wgs = (nblocks + MC_W - 1) / MC_W;
         unsigned grid = wgs < 16384 ? (unsigned)wgs : 16384u;
         k_mcopy<M_CMAX, M_PRE, true><<<grid, 64 * MC_W, 0, st>>>(d_cp, d_pre, d_bmap, d_fstart, d_flen, stride, nblocks,
-                                                          d_out, 0);
+                                                          d_out, 0, d_keys);
         MDBG(st, "k_mcopy");
+        k_mhint<<<(unsigned)lblk, M_NT, 0, st>>>(d_ent, d_cp, d_tuples, d_keys, d_hsz, d_bsum, d_tot, stride, d_hint,
+                                                  hint_cap);
+        MDBG(st, "k_mhint");
         MCK(hipGetLastError());
         if (out_file_len) MCK(hipMemcpyAsync(out_file_len, d_flen, sizeof(uint64_t) * h_tot.n_out,
                                              hipMemcpyDeviceToHost, st));
@@ -1324,10 +1360,10 @@ extern "C" int cly_append_device(cly_ctx* ctx, const cly_rec_in* d_recs, uint64_
         // the 512-entry instance (half the LDS: 4 waves/SIMD instead of 2)
         if (h_mn >= A_SMALL_MIN)
             k_mcopy<A_CMAX / 2, A_PRE, false><<<cg, 64 * MC_W, 0, st>>>(d_cp, d_pre, d_bmap, d_fstart, d_flen, stride,
-                                                                     nblocks, d_out, write_off);
+                                                                     nblocks, d_out, write_off, nullptr);
         else
             k_mcopy<A_CMAX, A_PRE, false><<<cg, 64 * MC_W, 0, st>>>(d_cp, d_pre, d_bmap, d_fstart, d_flen, stride,
-                                                                 nblocks, d_out, write_off);
+                                                                 nblocks, d_out, write_off, nullptr);
     }
     MCK(hipGetLastError());
     MCK(hipEventRecord(e1, st));

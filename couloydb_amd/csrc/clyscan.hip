@@ -1687,12 +1687,32 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         }
         // ---- tuples, and on the per-record path the records' checks
         if (!ovfl) {
+            // a round's compact entries and snapshots, loaded one round ahead;
+            // the next record's come from lane + 1 (lane 63 loads its own)
+            const u32x4* trec4 = (const u32x4*)trec;
+            const u32x4 z4 = (u32x4){0u, 0u, 0u, 0u};
+            auto ld = [&](uint32_t j0, u32x4& v, uint32_t& sv, u32x4& vx, uint32_t& sx) {
+                const uint32_t j = j0 + (uint32_t)lane;
+                v = j < n ? trec4[j] : z4;
+                sv = j < n ? tsnap[j] : 0u;
+                vx = z4; sx = 0u;
+                if (lane == 63 && j + 1 < n) { vx = trec4[j + 1]; sx = tsnap[j + 1]; }
+            };
+            u32x4 vc, vx;
+            uint32_t sc, sx;
+            ld(0u, vc, sc, vx, sx);
             for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+                u32x4 vN = z4, vxN = z4;
+                uint32_t sN = 0, sxN = 0;
+                if (i0 + 64 < n) ld(i0 + 64, vN, sN, vxN, sxN);
                 const uint32_t i = i0 + lane;
+                const u32x4 v2n = (u32x4){dppu<DPP_WF_SL1>(vx.x, vc.x), dppu<DPP_WF_SL1>(vx.y, vc.y),
+                                          dppu<DPP_WF_SL1>(vx.z, vc.z), dppu<DPP_WF_SL1>(vx.w, vc.w)};
+                const uint32_t s2n = dppu<DPP_WF_SL1>(sx, sc);
                 RecChk q = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
                 uint32_t p = 0;
                 if (i < n) {
-                    const u32x4 v = *(const u32x4*)(trec + 4 * i);
+                    const u32x4 v = vc;
                     const uint32_t rel = v.w & 0xFFFFu;
                     p = tb + rel;
                     u32x4 a, b, c;
@@ -1715,13 +1735,13 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                         const uint32_t cr = c.w;                            // this record's stored CRC
                         q.Wr = patch_word_of(p);
                         q.sa = (q.Wr - tb) >> 6;
-                        q.inj = tsnap[i] ^ exp_post(p & 3u, cr, kj);
+                        q.inj = sc ^ exp_post(p & 3u, cr, kj);
                         if (i + 1 < n) {                                    // ends at the next record's patch word
-                            const u32x4 v2 = *(const u32x4*)(trec + 4 * (i + 1));
+                            const u32x4 v2 = v2n;
                             const uint32_t P2 = tb + (v2.w & 0xFFFFu);
                             q.W2 = patch_word_of(P2);
                             q.sb = (q.W2 - tb) >> 6;
-                            q.s2 = tsnap[i + 1];
+                            q.s2 = s2n;
                             q.expn = exp_pre(emt, P2 & 3u, cr, entry_crc(base, F.len, tb, v2));
                             q.kind = 1;
                         } else if (term && T < TE) {                        // at the terminal's segment end
@@ -1746,6 +1766,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                         if (bl) ex = rdl(val, __ffsll((long long)bl) - 1) ^ cout;
                     }
                 }
+                vc = vN; sc = sN; vx = vxN; sx = sxN;
             }
         } else if (lane == 0) {
             // more records than the compact list holds: k_ovf walks the tile
