@@ -42,6 +42,7 @@ extern "C" hipError_t cly_ix_scratch_internal(cly_ctx* ctx, int k, size_t bytes,
 // the winner's type needs no second (random) read of its tuple
 #define IX_DEL 0x80000000u
 #define IXI(x) ((x) & 0x7fffffffu)
+#define IX_WIN 7                     // a key's winner, its final state not yet decided (k_ixwinfix)
 enum { K_NONE = 0, K_APPLY = 1, K_TXDATA = 2, K_COMMIT = 3, K_ROLLBACK = 4 };
 
 __device__ __forceinline__ int ix_file(const uint64_t* first, int nfiles, uint64_t i) {
@@ -354,7 +355,19 @@ k_ixwin(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, cons
         const bool deleted = g ? tup[w].type == 1 : (sidx[q] & IX_DEL) != 0;
         // LogRecordDeleted -> key absent; a String key whose winning put expired is
         // db.Del'd by loadIndex's TTL sweep (db.go:639-651: not exp.After(now))
-        if (!deleted) state[w] = ix_expired(tup[w], now_ns) ? (uint8_t)CLY_IX_EXPIRED : ix_win_state(tup, first, bases, nfiles, w);
+        // (the winner's final state from its tuple: k_ixwinfix, in scan order)
+        if (!deleted) state[w] = IX_WIN;
+    }
+}
+// the winners' states (LIVE, LOADONLY or EXPIRED) in scan order: the tuples
+// read as consecutive runs instead of one line per sorted winner
+__global__ void __launch_bounds__(256)
+k_ixwinfix(const cly_tuple* __restrict__ tup, uint64_t n, const uint64_t* __restrict__ first,
+           const uint64_t* __restrict__ bases, int nfiles, uint8_t* state, int64_t now_ns) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        if (state[i] != IX_WIN) continue;
+        state[i] = ix_expired(tup[i], now_ns) ? (uint8_t)CLY_IX_EXPIRED
+                                              : ix_win_state(tup, first, bases, nfiles, (uint32_t)i);
     }
 }
 // exact resolution of a collided hash group (one thread): per distinct key the max order
@@ -591,6 +604,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
         if (h_tot.n_coll)
             k_ixcoll<<<(unsigned)((m2 + 63) / 64), 64, 0, st>>>(d_txkey, d_sidx, d_order, m2, d_coll, d_tuples, d_first,
                                                                 d_bases, nfiles, d_state, now_ns);
+        k_ixwinfix<<<ix_grid(n), 256, 0, st>>>(d_tuples, n, d_first, d_bases, nfiles, d_state, now_ns);
     }
     k_ixcount<<<ix_grid(n) < 1024 ? ix_grid(n) : 1024, 256, 0, st>>>(d_state, d_apflag, n, d_tot);
     ICK(hipGetLastError());

@@ -453,3 +453,33 @@ def test_gpu_host_scan_capacity_needed_exact():
         assert [first[i] for i in range(12)] == [243_000 * i for i in range(12)]
         assert (out["offset"][:243_000] == np.arange(243_000) * 276).all()
         assert (out["fid"][243_000 * 11:] == 11).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_gpu_largest_file_offsets_past_2gib(corrupt):
+    """One data file of 4.28 GB (the largest this build takes is MAX_FILE_LEN =
+    4 GiB - 128 KiB: Options.SetDataFileSizeGB(1..3) files, options.go:70-71):
+    record offsets past 2^31 and 2^32 - 2^25 come out as the reference's int64
+    offsets, bit-exact against the oracle, and a record whose value byte is
+    flipped at ~3.45 GB stops the file there with ErrInvalidCRC."""
+    torch = pytest.importorskip("torch")
+    base = fixed_records_file(100_000, 256, seed=9)            # 27.6 MB, 276-B records
+    arr = np.tile(base, 155)                                   # 4 278 000 000 B, 15.5 M records
+    k = 12_500_000
+    if corrupt:
+        arr[k * 276 + 100] ^= 0x40
+    d = torch.from_numpy(arr).cuda()
+    n = len(arr) // 276
+    out = torch.empty((n + 64) * 48, dtype=torch.uint8, device="cuda")
+    with Scanner(0) as sc:
+        first, res, st, need = sc.scan_device([(d.data_ptr(), len(arr), 7)], out.data_ptr(), n + 64)
+    got = out[: need * 48].cpu().numpy().view(TUPLE_DTYPE)
+    t, st_o, end = co.scan_file(arr, 7)
+    compare(got[: res[0].n_records], res[0].status, res[0].end_offset, t, st_o, end, "4.28 GB file")
+    if corrupt:
+        assert res[0].status == _abi.ERR_CRC and res[0].n_records == k
+    else:
+        assert res[0].status == 0 and res[0].n_records == n and res[0].end_offset == len(arr)
+        assert int(got["offset"][-1]) == (n - 1) * 276 > 2**32 - 2**25
