@@ -683,6 +683,7 @@ struct TState {
     // (ref1..3) under the masks of its bytes 4..hsz, and the uniform words of
     // its compact entry; valid while ref_ok
     bool ref_ok;
+    bool pw_poor;                // the last pred_walk round took < 3 records and left the block unfinished
     uint32_t ref_s;              // the reference record's size (the stride)
     uint32_t ref1, ref2, ref3, msk1, msk2, msk3, rw1, rw2, rw3;
 };
@@ -983,6 +984,7 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     S.cq = 0; S.G = NONE32; S.tcnt = 0; S.last_crc = 0; S.P_last = NONE32; S.term = TERM_NONE;
     S.s_last = 0; S.s_prev = 0; S.Tb = NONE32; S.tpatch = 0; S.carry_next = 0; S.cmark_next = false;
     S.ref_ok = false; S.ref_s = 0; S.ref1 = S.ref2 = S.ref3 = S.msk1 = S.msk2 = S.msk3 = S.rw1 = S.rw2 = S.rw3 = 0;
+    S.pw_poor = false;
     uint32_t carry = 0;          // register XOR due at this block's first byte
     bool cmark = false;          // ... a record start's patch (marked as word 0 of the block)
     uint32_t nb = 0;             // snapshots taken so far (= records whose patch word was passed)
@@ -1048,9 +1050,17 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
             bool done = true;
             if (S.X != NONE32) {
                 if (BM != BM_EMIT && S.ref_ok) stride_round<BM>(F, S, tb, bs, stg, smem, cl, K4, rs, lane, mk);
-                const uint32_t c0 = S.tcnt;
-                done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, rs, out, out_cap, gbase, g, lane, mk);
-                if (BM != BM_EMIT && S.tcnt != c0) stride_ref(F, S, bs, stg);
+                if (S.pw_poor) {
+                    // irregular records: the general pass directly (a predictive
+                    // round would take one record and leave the block to it)
+                    const uint64_t X = S.X;
+                    done = S.dead || !(X < bend || (X == flen && flen == bend));
+                } else {
+                    const uint32_t c0 = S.tcnt;
+                    done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, rs, out, out_cap, gbase, g, lane, mk);
+                    if (BM != BM_EMIT && S.tcnt != c0) stride_ref(F, S, bs, stg);
+                    S.pw_poor = !done && S.tcnt - c0 < 3;
+                }
             }
             if (!done) {
                 // ---- general pass (the predictive walk's round budget ran out):
@@ -1133,6 +1143,11 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                         if (S.G == NONE32) S.G = rdl(L.E, __ffsll((long long)bcc) - 1);
                         S.X = rdl(L.x, 63 - __clzll((long long)bcc));
                         if (bt) { S.dead = true; S.term = (int)rdl((uint32_t)L.term, kT); }
+                    }
+                    if (S.pw_poor && S.s_last && S.s_last == S.s_prev) {
+                        // regular sizes again: the predictive rounds and the stride reference back
+                        S.pw_poor = false;
+                        if (BM != BM_EMIT) stride_ref(F, S, bs, stg);
                     }
                 }
             }

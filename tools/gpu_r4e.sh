@@ -14,3 +14,5 @@ timeout -k 10 400 python -u bench.py --config c4 --no-host-path --no-cpu-baselin
 timeout -s KILL 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4e/c4_stats -o run -- python3 bench.py --config c4 --steps 3 --warmup 1 --no-host-path --no-cpu-baseline > gpurun_out/r4e/c4_stats.log 2>&1 || exit $?
 timeout -k 10 400 python -u bench.py --config c3 --no-host-path --no-cpu-baseline > gpurun_out/r4e/bench_c3.json 2> gpurun_out/r4e/bench_c3.err || exit $?
 echo done
+CFG=c3 bash tools/gpu_xp.sh libclyscan.so libclyscan_head.so || exit $?
+echo done2

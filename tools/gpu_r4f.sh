@@ -1,0 +1,22 @@
+#!/bin/bash
+# profiles of the final build: C2 and C4 kernel stats, SQ instruction passes,
+# HBM traffic passes (FETCH_SIZE and WRITE_SIZE each in a run of its own)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+D=gpurun_out/r4f
+mkdir -p $D
+export TMPDIR=/tmp
+S1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS"
+S2="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT"
+timeout -s KILL 200 rocprofv3 --kernel-trace --stats --output-format csv -d $D/c2_stats -o run -- python3 tools/scan_once.py c2 10 > $D/c2_stats.log 2>&1 || exit $?
+i=0
+for s in "$S1" "$S2" "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -s KILL 200 rocprofv3 --pmc $s --kernel-trace --output-format csv -d $D/c2_p$i -o run -- python3 tools/scan_once.py c2 2 > $D/c2_p$i.log 2>&1 || exit $?
+done
+i=0
+for s in "$S2" "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -s KILL 300 rocprofv3 --pmc $s --kernel-trace --output-format csv -d $D/c4_p$i -o run -- python3 bench.py --config c4 --steps 1 --warmup 1 --no-host-path --no-cpu-baseline > $D/c4_p$i.log 2>&1 || exit $?
+done
+echo done
