@@ -1496,42 +1496,50 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
     uint32_t t = fixlist[k];
     const int f = find_file(tprefix, nfiles, t);
     const DevFile F = files[f];
-    LBState S = ti_load(&tin[t]);
-    {
+    // a run of listed tiles is walked by the wave of its first one: the
+    // entry of a later one is the walk's exit, not its stale TileIn
+    if (t > F.first_tile && (tin[t - 1].w[3] & TI_FIX)) return;
+    const LBState S0 = ti_load(&tin[t]);
+    uint32_t X = S0.X;
+    bool dead = S0.dead != 0;
+    for (;;) {
         // Suffix: the true entry is the start of the guessed chain's record j
         // (a false start that runs into the true chain).  The chain from there
         // on is the tile's own: drop the first j records (count, entry; k_emit
-        // skips their compact entries and corrects the register) instead of
-        // walking the tile again.
+        // skips their compact entries and snapshots) instead of walking the
+        // tile again; its exit stays.
         const u64 l0 = loc[t].l[0], l1 = loc[t].l[1];
         const uint32_t n = (uint32_t)(l0 >> 32), tb = (t - F.first_tile) * (uint32_t)CLY_TILE;
-        if (!S.dead && !(l0 & (DF_NONE | DF_FOF | DF_OVF)) && n > 1 && ((loc[t].l[3] >> 40) & 0xFFFFu) == 0) {
+        bool shortcut = false;
+        if (!dead && !(l0 & (DF_NONE | DF_FOF | DF_OVF)) && n > 1 && ((loc[t].l[3] >> 40) & 0xFFFFu) == 0) {
             const uint32_t nn = n < 64u ? n : 64u;
             const uint32_t rel = (uint32_t)lane < nn ? (rec[((uint64_t)t * CAP_T + lane) * 4 + 3] & 0xFFFFu) : 0u;
-            const u64 bm = __ballot(lane >= 1 && (uint32_t)lane < nn && tb + rel == S.X);
+            const u64 bm = __ballot(lane >= 1 && (uint32_t)lane < nn && tb + rel == X);
             if (bm) {
                 const uint32_t j = (uint32_t)__ffsll((long long)bm) - 1;
                 if (lane == 0) {
                     loc[t].l[0] = (l0 & 0xFFFFFFFFull) | ((u64)(n - j) << 32);
-                    loc[t].l[1] = (u64)S.X | (l1 & 0xFFFFFFFF00000000ull);
+                    loc[t].l[1] = (u64)X | (l1 & 0xFFFFFFFF00000000ull);
                     loc[t].l[3] |= (u64)j << 40;
                 }
-                return;
+                X = (uint32_t)(l1 >> 32);
+                dead = (l0 & DF_TERM) != 0;
+                shortcut = true;
             }
         }
-    }
-    for (;;) {
-        u32x4 e[4], hl;
-        tile_issue(F, t - F.first_tile, lane, e, hl);
-        const TileRes r = tile_body<BM_EXACT>(F, t, t - F.first_tile, S.X, S.dead != 0, smem, stg, mk, wave_sink(smem), cl,
-                                              K4, loc, rec, seg, snap, treg, nullptr, 0, 0, g, nullptr, e, hl, nullptr, 0u, 0u);
-        S.X = r.X; S.dead = r.dead;
-        if (S.dead || t + 1 >= F.first_tile + F.ntile) break;
-        // the next tile: consistent with the new exit?  else it is re-resolved too
-        // (unless it is listed itself: its own wave has it)
-        if (tin[t + 1].w[3] & TI_FIX) break;
+        if (!shortcut) {
+            u32x4 e[4], hl;
+            tile_issue(F, t - F.first_tile, lane, e, hl);
+            const TileRes r = tile_body<BM_EXACT>(F, t, t - F.first_tile, X, dead, smem, stg, mk, wave_sink(smem), cl,
+                                                  K4, loc, rec, seg, snap, treg, nullptr, 0, 0, g, nullptr, e, hl,
+                                                  nullptr, 0u, 0u);
+            X = r.X; dead = r.dead;
+        }
+        if (dead || t + 1 >= F.first_tile + F.ntile) break;
+        // the next tile (listed or not: a listed one's own wave left it to
+        // this walk): consistent with the new exit?  else it is re-resolved too
         const u64 n0 = loc[t + 1].l[0], n1 = loc[t + 1].l[1], n3 = loc[t + 1].l[3];
-        const bool ok = (n0 & DF_NONE) ? S.X >= (uint32_t)n3 : S.X == (uint32_t)n1;
+        const bool ok = (n0 & DF_NONE) ? X >= (uint32_t)n3 : X == (uint32_t)n1;
         if (ok) break;
         t++;
     }
