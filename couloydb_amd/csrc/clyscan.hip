@@ -1536,8 +1536,10 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
             X = r.X; dead = r.dead;
         }
         if (dead || t + 1 >= F.first_tile + F.ntile) break;
-        // the next tile (listed or not: a listed one's own wave left it to
-        // this walk): consistent with the new exit?  else it is re-resolved too
+        // a listed next tile whose predecessor is not listed has a wave of its
+        // own (it starts a run); any other next tile: consistent with the new
+        // exit?  else it is re-resolved here too
+        if ((tin[t + 1].w[3] & TI_FIX) && !(tin[t].w[3] & TI_FIX)) break;
         const u64 n0 = loc[t + 1].l[0], n1 = loc[t + 1].l[1], n3 = loc[t + 1].l[3];
         const bool ok = (n0 & DF_NONE) ? X >= (uint32_t)n3 : X == (uint32_t)n1;
         if (ok) break;
