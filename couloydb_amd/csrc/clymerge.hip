@@ -819,7 +819,8 @@ k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uin
             // block's loads just brought into L2 (k_mhint then reads 16 B per
             // record instead of a line of the file)
             for (uint32_t q = lane; q < cnt; q += 64) {
-                if ((int32_t)desc[q].z < 0) continue;               // started in an earlier block
+                const int32_t rl = (int32_t)desc[q].z;
+                if (rl < 0 || rl >= M_CB) continue;                  // starts in another block
                 const uint32_t px = cp[j0 + q].pre;
                 if (MC_RK(px) > MH_KEY) continue;
                 const mc_u32x4 D = desc[q];
