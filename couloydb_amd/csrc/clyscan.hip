@@ -528,32 +528,16 @@ __device__ __forceinline__ void put_tuple(gtuples out, uint64_t idx, uint64_t ou
 // key0 << 19 (the txId varint's single byte).  Long form: w3 = rel only
 // (k_emit decodes the header again).
 #define REC_SHORT (1u << 26)
-// Where a block's compact entries and snapshots go (k_scan, k_refix): the
-// wave's LDS buffers (entries c0 .. c0 + RB - 1 of the block, snapshots from
-// n0 on), written to global memory at the top of the next block, after the
-// wait for its loads, and before the loads of the block after it are issued:
-// stores issued in the block body would sit between a block's prefetch and
-// its wait (vmcnt counts loads and stores in one ordered counter), and every
-// block would wait for its own last stores.  Entries beyond the buffers go
-// out directly.
-#define RB 32
-struct RecSink { rsrc_t trs, nrs; CLY_LDS u32x4* rb; CLY_LDS uint32_t* sb; uint32_t c0, n0; FileInfo* fo; };
+// Where a block's compact entries and snapshots go (k_scan, k_refix): stored
+// as they are made (an LDS sink flushed at the next block's top, after its
+// loads, measured 1.6 % slower on C2 and 3.3 % on C4), and the file record
+// checks of k_ovf's re-walk
+struct RecSink { rsrc_t trs, nrs; FileInfo* fo; };
 __device__ __forceinline__ void rec_put(const RecSink& rs, uint32_t idx, const u32x4& v) {
-    const uint32_t j = idx - rs.c0;
-    if (j < RB) rs.rb[j] = v;
-    else if (idx < CAP_T) __builtin_amdgcn_raw_buffer_store_b128(v, rs.trs, (int)(idx * 16u), 0, 0);
+    if (idx < CAP_T) __builtin_amdgcn_raw_buffer_store_b128(v, rs.trs, (int)(idx * 16u), 0, 0);
 }
 __device__ __forceinline__ void snap_put(const RecSink& rs, uint32_t r, uint32_t v) {
-    const uint32_t j = r - rs.n0;
-    if (j < RB) rs.sb[j] = v;
-    else __builtin_amdgcn_raw_buffer_store_b32(v, rs.nrs, (int)(r * 4u), 0, 0);
-}
-// the buffered outputs of a block whose entries end at c1 and snapshots at n1
-__device__ __forceinline__ void sink_flush(const RecSink& rs, uint32_t c1, uint32_t n1, int lane) {
-    const uint32_t ne = c1 - rs.c0, ns = n1 - rs.n0, l = (uint32_t)lane;
-    if (l < ne && l < RB && rs.c0 + l < CAP_T)
-        __builtin_amdgcn_raw_buffer_store_b128(rs.rb[l], rs.trs, (int)((rs.c0 + l) * 16u), 0, 0);
-    if (l < ns && l < RB) __builtin_amdgcn_raw_buffer_store_b32(rs.sb[l], rs.nrs, (int)((rs.n0 + l) * 4u), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(v, rs.nrs, (int)(r * 4u), 0, 0);
 }
 __device__ __forceinline__ void rec_store(const RecSink& rs, uint32_t idx, const Hdr& h, uint32_t rel) {
     const bool sh = h.exp == 0 && h.key0 < 0x80u && h.ks >= 1u && h.ks < (1u << 24) && h.type < 8u && h.dt < 8u &&
@@ -683,7 +667,6 @@ struct TState {
     // (ref1..3) under the masks of its bytes 4..hsz, and the uniform words of
     // its compact entry; valid while ref_ok
     bool ref_ok;
-    bool pw_poor;                // the last pred_walk round took < 3 records and left the block unfinished
     uint32_t ref_s;              // the reference record's size (the stride)
     uint32_t ref1, ref2, ref3, msk1, msk2, msk3, rw1, rw2, rw3;
 };
@@ -968,7 +951,7 @@ __device__ __forceinline__ uint32_t guess_entry(const DevFile& F, uint32_t bs, C
 template <int BM>
 __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint32_t tt, uint32_t X_in, bool dead_in,
                                              const CLY_LDS uint8_t* smem, CLY_LDS uint32_t* stg, CLY_LDS uint32_t* mk,
-                                             CLY_LDS uint8_t* wbuf, const CrcLane& cl, uint32_t K4, TileLocal* loc,
+                                             const CrcLane& cl, uint32_t K4, TileLocal* loc,
                                              uint32_t* rec, uint32_t* seg, uint32_t* snap, uint32_t* treg, gtuples out,
                                              uint64_t out_cap, uint64_t gbase, Globals* g, FileInfo* fo,
                                              u32x4 (&e)[4], u32x4& hl, const uint8_t* nbase, uint32_t nlen, uint32_t ntb) {
@@ -984,7 +967,6 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     S.cq = 0; S.G = NONE32; S.tcnt = 0; S.last_crc = 0; S.P_last = NONE32; S.term = TERM_NONE;
     S.s_last = 0; S.s_prev = 0; S.Tb = NONE32; S.tpatch = 0; S.carry_next = 0; S.cmark_next = false;
     S.ref_ok = false; S.ref_s = 0; S.ref1 = S.ref2 = S.ref3 = S.msk1 = S.msk2 = S.msk3 = S.rw1 = S.rw2 = S.rw3 = 0;
-    S.pw_poor = false;
     uint32_t carry = 0;          // register XOR due at this block's first byte
     bool cmark = false;          // ... a record start's patch (marked as word 0 of the block)
     uint32_t nb = 0;             // snapshots taken so far (= records whose patch word was passed)
@@ -993,9 +975,8 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     const rsrc_t srs = mk_rsrc(seg + (uint64_t)t * NSEG, BM == BM_EMIT ? 0u : NSEG * 4u);            // segment registers
     const rsrc_t nrs = mk_rsrc(snap + (uint64_t)t * SNAP_T, BM == BM_EMIT ? 0u : (CAP_T + 1) * 4u);  // snapshots
     RecSink rs;
-    rs.trs = trs; rs.nrs = nrs; rs.c0 = 0; rs.n0 = 0; rs.fo = fo;
-    rs.rb = (CLY_LDS u32x4*)wbuf; rs.sb = (CLY_LDS uint32_t*)(wbuf + RB * 16);
-    uint32_t Rp = 0;             // the previous block's segment register (stored with its flush)
+    rs.trs = trs; rs.nrs = nrs; rs.fo = fo;
+    uint32_t Rp = 0;             // the previous block's segment register (stored at the next block's top)
     CLY_LDS u32x4* sv = (CLY_LDS u32x4*)stg;
     #pragma unroll 1
     for (int m = 0; m < CLY_NBLK; m++) {
@@ -1008,11 +989,8 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
         const u32x4 hc = hl;
         if (BM != BM_EMIT) {
             // the previous block's outputs, now that this block's loads are in
-            if (m > 0) {
-                sink_flush(rs, S.tcnt, nb, lane);
+            if (m > 0)
                 __builtin_amdgcn_raw_buffer_store_b32(Rp, srs, (int)(((uint32_t)(m - 1) * CLY_NL + (uint32_t)lane) * 4u), 0, 0);
-            }
-            rs.c0 = S.tcnt; rs.n0 = nb;
         }
         if (m + 1 < CLY_NBLK && (BM != BM_EMIT || !S.dead)) blk_issue(base, frs, flen, bs + CLY_BLK, lane, e, hl);
         else if (m + 1 == CLY_NBLK && nbase) {                                 // the wave's next tile
@@ -1050,17 +1028,9 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
             bool done = true;
             if (S.X != NONE32) {
                 if (BM != BM_EMIT && S.ref_ok) stride_round<BM>(F, S, tb, bs, stg, smem, cl, K4, rs, lane, mk);
-                if (S.pw_poor) {
-                    // irregular records: the general pass directly (a predictive
-                    // round would take one record and leave the block to it)
-                    const uint64_t X = S.X;
-                    done = S.dead || !(X < bend || (X == flen && flen == bend));
-                } else {
-                    const uint32_t c0 = S.tcnt;
-                    done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, rs, out, out_cap, gbase, g, lane, mk);
-                    if (BM != BM_EMIT && S.tcnt != c0) stride_ref(F, S, bs, stg);
-                    S.pw_poor = !done && S.tcnt - c0 < 3;
-                }
+                const uint32_t c0 = S.tcnt;
+                done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, rs, out, out_cap, gbase, g, lane, mk);
+                if (BM != BM_EMIT && S.tcnt != c0) stride_ref(F, S, bs, stg);
             }
             if (!done) {
                 // ---- general pass (the predictive walk's round budget ran out):
@@ -1144,11 +1114,6 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                         S.X = rdl(L.x, 63 - __clzll((long long)bcc));
                         if (bt) { S.dead = true; S.term = (int)rdl((uint32_t)L.term, kT); }
                     }
-                    if (S.pw_poor && S.s_last && S.s_last == S.s_prev) {
-                        // regular sizes again: the predictive rounds and the stride reference back
-                        S.pw_poor = false;
-                        if (BM != BM_EMIT) stride_ref(F, S, bs, stg);
-                    }
                 }
             }
         }
@@ -1203,7 +1168,6 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     TileRes res;
     res.X = S.X; res.dead = S.dead;
     if (BM != BM_EMIT) {
-        sink_flush(rs, S.tcnt, nb, lane);
         __builtin_amdgcn_raw_buffer_store_b32(Rp, srs, (int)(((uint32_t)(CLY_NBLK - 1) * CLY_NL + (uint32_t)lane) * 4u), 0, 0);
     }
     if (BM != BM_EMIT && lane == 0) {
@@ -1253,17 +1217,13 @@ __device__ __forceinline__ uint32_t k4_const(const CLY_LDS uint8_t* smem, uint32
 // k_scan: one wave per tile (grid-stride), every byte of every file read once.
 #define SCAN_WAVES 16
 #define MK_BYTES (CLY_NL * 4)                                 // a wave's patch-word mask
-#define SINK_BYTES (RB * 16 + RB * 4)                        // a wave's RecSink buffers
-#define SCAN_LDS_ALL (SCAN_LDS + SCAN_WAVES * (STG_BYTES + MK_BYTES + SINK_BYTES))   // tables + per wave a block stage, a mask, the sink
+#define SCAN_LDS_ALL (SCAN_LDS + SCAN_WAVES * (STG_BYTES + MK_BYTES))   // tables + per wave a block stage and a mask
 static_assert(SCAN_LDS_ALL <= 160 * 1024, "k_scan's LDS");
 __device__ __forceinline__ CLY_LDS uint32_t* wave_stage(CLY_LDS uint8_t* smem) {
     return (CLY_LDS uint32_t*)(smem + SCAN_LDS + wave_id() * STG_BYTES);
 }
 __device__ __forceinline__ CLY_LDS uint32_t* wave_mask(CLY_LDS uint8_t* smem) {
     return (CLY_LDS uint32_t*)(smem + SCAN_LDS + SCAN_WAVES * STG_BYTES + wave_id() * MK_BYTES);
-}
-__device__ __forceinline__ CLY_LDS uint8_t* wave_sink(CLY_LDS uint8_t* smem) {
-    return smem + SCAN_LDS + SCAN_WAVES * (STG_BYTES + MK_BYTES) + wave_id() * SINK_BYTES;
 }
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
 k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
@@ -1295,7 +1255,7 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             ntb = (tn - files[fn].first_tile) * (uint32_t)CLY_TILE;
         }
         const DevFile F = files[f];
-        tile_body<BM_SPEC>(F, t, t - F.first_tile, 0u, false, smem, stg, mk, wave_sink(smem), cl, K4, loc, rec, seg, snap,
+        tile_body<BM_SPEC>(F, t, t - F.first_tile, 0u, false, smem, stg, mk, cl, K4, loc, rec, seg, snap,
                            treg, nullptr, 0, 0, g, nullptr, e, hl, nbase, nlen, ntb);
         if (fn < 0) break;
         t = tn; f = fn;
@@ -1530,7 +1490,7 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
         if (!shortcut) {
             u32x4 e[4], hl;
             tile_issue(F, t - F.first_tile, lane, e, hl);
-            const TileRes r = tile_body<BM_EXACT>(F, t, t - F.first_tile, X, dead, smem, stg, mk, wave_sink(smem), cl,
+            const TileRes r = tile_body<BM_EXACT>(F, t, t - F.first_tile, X, dead, smem, stg, mk, cl,
                                                   K4, loc, rec, seg, snap, treg, nullptr, 0, 0, g, nullptr, e, hl,
                                                   nullptr, 0u, 0u);
             X = r.X; dead = r.dead;
@@ -1904,7 +1864,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
 // record that crosses into it (its start: the last record before the tile,
 // TileIn): A^CLY_TILE (the register entering the tile) must equal the tile's
 // dev shifted to its end.
-#define FIN_NT 256
+#define FIN_NT 1024
 __device__ __forceinline__ uint32_t shift_b(const CLY_LDS uint32_t* sh, uint32_t m, uint32_t v) {
     return m ? shift_bytes(sh, m, v) : v;
 }
@@ -1914,7 +1874,7 @@ k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __rest
       const uint32_t* __restrict__ pw, Globals* g, int slot) {
     __shared__ uint32_t tabl[NIB_SH * 128 + 128];           // TAB_SH, TAB_TILE
     __shared__ uint32_t px[FIN_NT], pc[FIN_NT], pu[FIN_NT];
-    __shared__ uint32_t mlev[8];
+    __shared__ uint32_t mlev[16];
     if (g->nfix[slot]) return;              // k_emit did not run (link repair first)
     for (int i = threadIdx.x; i < NIB_SH * 128 + 128; i += FIN_NT) tabl[i] = tabs[TAB_SH + i];
     const CLY_LDS uint32_t* sht = (const CLY_LDS uint32_t*)tabl;
@@ -1932,7 +1892,7 @@ k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __rest
     if (tid == 0) {                         // A^(CLY_TILE per 2^l): the shift of a level of the scan
         uint32_t m = 1u << 31;
         for (uint32_t b = per, k = 0; b; b >>= 1, k++) if (b & 1) m = cly_multmodp(pw[k], m);
-        for (int l = 0; l < 8; l++) { mlev[l] = m; m = cly_multmodp(m, m); }
+        for (int l = 0; (1 << l) < FIN_NT; l++) { mlev[l] = m; m = cly_multmodp(m, m); }
     }
     __syncthreads();
     uint32_t x = 0, c = 0, un = 0;
@@ -2000,7 +1960,7 @@ k_ovf(const DevFile* __restrict__ files, FileInfo* finfo, const TileIn* __restri
         const LBState S = ti_load(&tin[t]);
         u32x4 blk[4], hl;
         tile_issue(F, t - F.first_tile, threadIdx.x & 63, blk, hl);
-        tile_body<BM_EMIT>(F, t, t - F.first_tile, S.X, false, smem, stg, nullptr, nullptr, cl, 0u, nullptr, nullptr,
+        tile_body<BM_EMIT>(F, t, t - F.first_tile, S.X, false, smem, stg, nullptr, cl, 0u, nullptr, nullptr,
                            nullptr, nullptr, nullptr, (gtuples)out_, out_cap, gb, g, &finfo[e.x], blk, hl, nullptr, 0u, 0u);
     }
 }
