@@ -1540,12 +1540,13 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
 //   records) and dev.
 #define RUN (CLY_NBLK)                          // segments per lane in k_emit's scan
 #define RUN_BYTES (RUN * CLY_SEG)
-#define EMIT_WAVES 4
+#define EMIT_WAVES 8
 #define SHORT_MAXN 256                          // records per tile of the per-record path
 #define SHORT_KMAX 32                           // segments one record may span there
 #define GIN_WORDS (NSEG + 4)                    // segment registers / the scan (+ the tile's end)
 #define FLG_BYTES (NSEG / 8)                    // segments that hold a reset (tile-wide scan)
-#define EW_BYTES ((GIN_WORDS * 4 + FLG_BYTES + 15) & ~15)
+#define TUP_BYTES (64 * 48)                     // a round's tuples (stored as contiguous 1-KiB runs)
+#define EW_BYTES ((GIN_WORDS * 4 + FLG_BYTES + TUP_BYTES + 15) & ~15)
 #define EMIT_KJ (NEM * 128)                    // kj[4] after the tables (words)
 #define EMIT_LDS (NEM * 128 * 4 + 16 + EMIT_WAVES * EW_BYTES)
 static_assert(CLY_NL * RUN == NSEG, "one run of segments per lane");
@@ -1612,6 +1613,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     CLY_LDS uint8_t* wreg = (CLY_LDS uint8_t*)smem_raw + NEM * 128 * 4 + 16 + wave_id() * EW_BYTES;
     CLY_LDS uint32_t* gin = (CLY_LDS uint32_t*)wreg;                  // segment registers, then the scan
     CLY_LDS uint32_t* flg = (CLY_LDS uint32_t*)(wreg + GIN_WORDS * 4);   // reset segments (bitmap)
+    CLY_LDS u32x4* sv = (CLY_LDS u32x4*)(wreg + ((GIN_WORDS * 4 + FLG_BYTES + 15) & ~15));   // a round's tuples
     const int lane = threadIdx.x & 63;
     for (uint32_t t = blockIdx.x * EMIT_WAVES + wave_id(); t < ntiles; t += gridDim.x * EMIT_WAVES) {
         const LBState S = ti_load(&tin[t]);
@@ -1712,10 +1714,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                         const Hdr h = hdr_load(base, p, F.len);
                         tuple_words(base, p, h, F.fid, a, b, c);
                     }
-                    if (gb + i < out_cap) {
-                        CLY_GL u32x4* dst = (CLY_GL u32x4*)(out + gb + i);
-                        dst[0] = a; dst[1] = b; dst[2] = c;
-                    } else atomicOr(&g->overflow, 1u);
+                    sv[3 * lane] = a; sv[3 * lane + 1] = b; sv[3 * lane + 2] = c;
                     if (!full) {
                         const uint32_t cr = c.w;                            // this record's stored CRC
                         q.Wr = patch_word_of(p);
@@ -1751,6 +1750,23 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                         if (bl) ex = rdl(val, __ffsll((long long)bl) - 1) ^ cout;
                     }
                 }
+                // the round's tuples are 48 (n - i0) contiguous bytes: 16-B pieces q = lane + 64 k
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                {
+                    const uint32_t nr = n - i0 < 64 ? n - i0 : 64;
+                    CLY_GL u32x4* dst = (CLY_GL u32x4*)(out + gb + i0);
+                    #pragma unroll
+                    for (int k = 0; k < 3; k++) {
+                        const uint32_t qq = (uint32_t)lane + 64u * k;
+                        if (qq < 3 * nr) {
+                            if (gb + i0 + qq / 3 < out_cap) dst[qq] = sv[qq];
+                            else atomicOr(&g->overflow, 1u);
+                        }
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 vc = vN; sc = sN; vx = vxN; sx = sxN;
             }
         } else if (lane == 0) {

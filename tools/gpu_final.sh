@@ -1,11 +1,17 @@
 #!/bin/bash
-# profiles of the final build: C2 and C4 kernel stats, SQ instruction passes,
-# HBM traffic passes (FETCH_SIZE and WRITE_SIZE each in a run of its own)
+# round-end artifacts: GPU suite, the default bench (C2 + host path + index load),
+# C3/C4 benches, then kernel stats, SQ passes and HBM traffic passes (C2, C4)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-D=gpurun_out/r4f
+D=gpurun_out/fin
 mkdir -p $D
 export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -q -x --timeout 300 --timeout-method thread -m gpu > $D/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 $D/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u bench.py > $D/bench_c2.json 2> $D/bench_c2.err || exit $?
+timeout -k 10 400 python -u bench.py --config c4 --no-host-path --no-cpu-baseline > $D/bench_c4.json 2> $D/bench_c4.err || exit $?
+timeout -k 10 400 python -u bench.py --config c3 --no-host-path --no-cpu-baseline > $D/bench_c3.json 2> $D/bench_c3.err || exit $?
 S1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS"
 S2="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT"
 timeout -s KILL 200 rocprofv3 --kernel-trace --stats --output-format csv -d $D/c2_stats -o run -- python3 tools/scan_once.py c2 10 > $D/c2_stats.log 2>&1 || exit $?
@@ -14,6 +20,7 @@ for s in "$S1" "$S2" "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -s KILL 200 rocprofv3 --pmc $s --kernel-trace --output-format csv -d $D/c2_p$i -o run -- python3 tools/scan_once.py c2 2 > $D/c2_p$i.log 2>&1 || exit $?
 done
+timeout -s KILL 400 rocprofv3 --kernel-trace --stats --output-format csv -d $D/c4_stats -o run -- python3 bench.py --config c4 --steps 3 --warmup 1 --no-host-path --no-cpu-baseline > $D/c4_stats.log 2>&1 || exit $?
 i=0
 for s in "$S2" "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
