@@ -1548,10 +1548,13 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
 #define TUP_BYTES (64 * 48)                     // a round's tuples (stored as contiguous 1-KiB runs)
 #define EW_BYTES ((GIN_WORDS * 4 + FLG_BYTES + TUP_BYTES + 15) & ~15)
 #define EMIT_KJ (NEM * 128)                    // kj[4] after the tables (words)
-#define EMIT_LDS (NEM * 128 * 4 + 16 + EMIT_WAVES * EW_BYTES)
+#define EMIT_LDS (NEM * 128 * 4 + 16 + 4096 + EMIT_WAVES * EW_BYTES)
 static_assert(CLY_NL * RUN == NSEG, "one run of segments per lane");
-__device__ __forceinline__ uint32_t gin_at(uint32_t sg) {      // LDS word of segment sg (lane-transposed)
-    return sg < NSEG ? (sg % RUN) * 64u + sg / RUN : NSEG;
+// LDS word of segment sg: plain (the per-record path: neighbouring records'
+// segments in different banks) or lane-transposed (the tile-wide scan: lane
+// L's run of RUN segments in one bank column)
+__device__ __forceinline__ uint32_t gin_at(uint32_t sg, bool plain) {
+    return sg < NSEG ? (plain ? sg : (sg % RUN) * 64u + sg / RUN) : NSEG;
 }
 // A^(4k) v, 0 <= k <= 16 (k = 16: the segment step A^64)
 __device__ __forceinline__ uint32_t em_f4(const CLY_LDS uint32_t* emt, uint32_t k, uint32_t v) {
@@ -1559,6 +1562,12 @@ __device__ __forceinline__ uint32_t em_f4(const CLY_LDS uint32_t* emt, uint32_t 
 }
 __device__ __forceinline__ uint32_t em_a64(const CLY_LDS uint32_t* emt, uint32_t v) {
     return mat_mul(emt + (EM_F4 + 15) * 128, v);
+}
+// A^64 v by byte tables (4 lookups; k_emit keeps them after the nibble tables)
+#define EMIT_A64B (NEM * 128 + 4)                       // words: after the nibble tables and kj
+__device__ __forceinline__ uint32_t em_a64b(const CLY_LDS uint32_t* emt, uint32_t v) {
+    const CLY_LDS uint32_t* bt = emt + EMIT_A64B;
+    return bt[v & 255u] ^ bt[256 + ((v >> 8) & 255u)] ^ bt[512 + ((v >> 16) & 255u)] ^ bt[768 + (v >> 24)];
 }
 // A^(4-j) v, 1 <= j <= 3
 __device__ __forceinline__ uint32_t em_fj(const CLY_LDS uint32_t* emt, uint32_t j, uint32_t v) {
@@ -1589,11 +1598,12 @@ struct RecChk { uint32_t sa, sb, Wr, W2, inj, s2, expn, kind; };
 __device__ __forceinline__ uint32_t chk_eval(const CLY_LDS uint32_t* emt, const CLY_LDS uint32_t* gin,
                                              const RecChk& q, uint32_t tb) {
     // the register entering W2 (kind 1), or at the end of segment sb - 1 (kinds 2, 3)
+    // (gin in the plain layout)
     if (q.sb == q.sa) return q.s2 ^ em_f4(emt, (q.W2 - q.Wr) >> 2, q.inj);
-    uint32_t x = gin[gin_at(q.sa)] ^ em_f4(emt, (64u * (q.sa + 1u) - (q.Wr - tb)) >> 2, q.inj);
+    uint32_t x = gin[q.sa] ^ em_f4(emt, (64u * (q.sa + 1u) - (q.Wr - tb)) >> 2, q.inj);
     const uint32_t steps = q.sb - q.sa - 1u;
     for (uint32_t k = 0; __ballot(k < steps); k++)
-        if (k < steps) x = em_a64(emt, x) ^ gin[gin_at(q.sa + 1u + k)];
+        if (k < steps) x = em_a64b(emt, x) ^ gin[q.sa + 1u + k];
     return em_f4(emt, (q.W2 - tb - 64u * q.sb) >> 2, x) ^ q.s2;
 }
 __global__ void __launch_bounds__(64 * EMIT_WAVES)
@@ -1609,8 +1619,13 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     __syncthreads();
     CLY_LDS uint32_t* kj = emt + EMIT_KJ;
     if (threadIdx.x < 4) kj[threadIdx.x] = threadIdx.x ? em_fj(emt, threadIdx.x, CLY_K4) : CLY_K4;
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {       // A^64 by bytes from its nibble table
+        const CLY_LDS uint32_t* a = emt + (EM_F4 + 15) * 128;
+        const int b = i >> 8, x = i & 255;
+        emt[EMIT_A64B + i] = a[(2 * b) * 16 + (x & 15)] ^ a[(2 * b + 1) * 16 + (x >> 4)];
+    }
     __syncthreads();
-    CLY_LDS uint8_t* wreg = (CLY_LDS uint8_t*)smem_raw + NEM * 128 * 4 + 16 + wave_id() * EW_BYTES;
+    CLY_LDS uint8_t* wreg = (CLY_LDS uint8_t*)smem_raw + NEM * 128 * 4 + 16 + 4096 + wave_id() * EW_BYTES;
     CLY_LDS uint32_t* gin = (CLY_LDS uint32_t*)wreg;                  // segment registers, then the scan
     CLY_LDS uint32_t* flg = (CLY_LDS uint32_t*)(wreg + GIN_WORDS * 4);   // reset segments (bitmap)
     CLY_LDS u32x4* sv = (CLY_LDS u32x4*)(wreg + ((GIN_WORDS * 4 + FLG_BYTES + 15) & ~15));   // a round's tuples
@@ -1649,10 +1664,6 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                 #pragma unroll
                 for (int k = 0; k < RUN; k++) sr[k] = sp[k];
             }
-            #pragma unroll
-            for (int k = 0; k < RUN; k++) gin[k * 64 + lane] = sr[k];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         // ---- G (a record start): its patch word WG, its snapshot, and the
         // register entering WG when the record ending at G matches (expG)
@@ -1665,11 +1676,24 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             if (tt > 0) expG = exp_pre(emt, G & 3u, S.crc_last, entry_crc(base, F.len, tb, *(const u32x4*)trec));
         }
         bool full = !grec || ovfl || n > SHORT_MAXN || sigG >= NSEG || (tt > 0 && sigG > SHORT_KMAX);
+        // the segment registers into LDS: plain for the per-record path,
+        // lane-transposed for the tile-wide scan
+        bool plain = !full;
+        if (plain) {
+            #pragma unroll
+            for (int k = 0; k < RUN; k += 4)
+                *(CLY_LDS u32x4*)(gin + (uint32_t)lane * RUN + k) = (u32x4){sr[k], sr[k + 1], sr[k + 2], sr[k + 3]};
+        } else {
+            #pragma unroll
+            for (int k = 0; k < RUN; k++) gin[k * 64 + lane] = sr[k];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         uint32_t ex = 0, dev = 0;
         if (!full && tt > 0) {
             // the tile's own register entering WG (from zero at the tile's start)
             uint32_t x = 0;
-            for (uint32_t k = 0; k < sigG; k++) x = em_a64(emt, x) ^ gin[gin_at(k)];
+            for (uint32_t k = 0; k < sigG; k++) x = em_a64b(emt, x) ^ gin[k];
             dev = em_f4(emt, (WG - tb - 64u * sigG) >> 2, x) ^ sG ^ expG;
         }
         // ---- tuples, and on the per-record path the records' checks
@@ -1776,6 +1800,12 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             ovf[k] = (u32x4){(uint32_t)f, t, (uint32_t)gb, (uint32_t)(gb >> 32)};
         }
         if (full) {
+            if (plain) {
+                // (a record spanning too many segments turned the tile over to the scan)
+                #pragma unroll
+                for (int k = 0; k < RUN; k++) gin[k * 64 + lane] = sr[k];
+                plain = false;
+            }
             // ---- the tile-wide scan: the segments whose last boundary is a
             // record start get their reset exit (flagged: a constant in the scan)
             if (lane < NSEG / 32) flg[lane] = 0u;
@@ -1792,7 +1822,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                         if (i + 1 < n) lastin = ((patch_word_of(tb + (trec[4 * (i + 1) + 3] & 0xFFFFu)) - tb) >> 6) != sg;
                         if (sg < NSEG && lastin) {
                             const uint32_t inj = tsnap[i] ^ exp_post(P & 3u, entry_crc(base, F.len, tb, v), kj);
-                            gin[gin_at(sg)] ^= em_f4(emt, (64u * (sg + 1u) - (W - tb)) >> 2, inj);
+                            gin[gin_at(sg, false)] ^= em_f4(emt, (64u * (sg + 1u) - (W - tb)) >> 2, inj);
                             __atomic_fetch_or(flg + (sg >> 5), 1u << (sg & 31u), __ATOMIC_RELAXED);
                         }
                     }
@@ -1811,7 +1841,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                 sr[k] = gin[k * 64 + lane];
                 const uint32_t fk = (flg[sg >> 5] >> (sg & 31u)) & 1u;
                 fl |= fk << k;
-                x = fk ? sr[k] : em_a64(emt, x) ^ sr[k];
+                x = fk ? sr[k] : em_a64b(emt, x) ^ sr[k];
                 rc |= fk;
             }
             #pragma unroll
@@ -1825,7 +1855,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             #pragma unroll
             for (int k = 0; k < RUN; k++) {
                 gin[k * 64 + lane] = y;
-                y = ((fl >> k) & 1u) ? sr[k] : em_a64(emt, y) ^ sr[k];
+                y = ((fl >> k) & 1u) ? sr[k] : em_a64b(emt, y) ^ sr[k];
             }
             const uint32_t gte = rdl(y, 63);                                // the register at the tile's end
             if (lane == 0) gin[NSEG] = gte;
@@ -1835,7 +1865,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             if (gterm) { ex = 0; dev = gte ^ cout; }
             else if (grec) {
                 // the tile's own register entering WG (no reset before G)
-                dev = (sigG < NSEG ? em_f4(emt, (WG - tb - 64u * sigG) >> 2, gin[gin_at(sigG)]) : gte) ^ sG ^ expG;
+                dev = (sigG < NSEG ? em_f4(emt, (WG - tb - 64u * sigG) >> 2, gin[gin_at(sigG, false)]) : gte) ^ sG ^ expG;
                 if (!ovfl) {
                     // past the last record start: its reset at the tile's end
                     // when its patch word is there, else the scan's register
@@ -1849,7 +1879,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                         const uint32_t W = patch_word_of(p), W2 = patch_word_of(P2), sg = (W - tb) >> 6, sg2 = (W2 - tb) >> 6;
                         const uint32_t c1 = entry_crc(base, F.len, tb, v), c2 = entry_crc(base, F.len, tb, v2);
                         const uint32_t pre = sg2 == sg ? tsnap[i + 1] ^ em_f4(emt, (W2 - W) >> 2, tsnap[i] ^ exp_post(p & 3u, c1, kj))
-                                                       : em_f4(emt, (W2 - tb - 64u * sg2) >> 2, gin[gin_at(sg2)]) ^ tsnap[i + 1];
+                                                       : em_f4(emt, (W2 - tb - 64u * sg2) >> 2, gin[gin_at(sg2, false)]) ^ tsnap[i + 1];
                         if (pre != exp_pre(emt, P2 & 3u, c1, c2))
                             atomicMin(&fo->fail_key, ((u64)p << 32) | (S.count + i));
                     }
