@@ -1541,7 +1541,7 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
 #define RUN (CLY_NBLK)                          // segments per lane in k_emit's scan
 #define RUN_BYTES (RUN * CLY_SEG)
 #define EMIT_WAVES 8
-#define SHORT_MAXN 256                          // records per tile of the per-record path
+#define SHORT_MAXN CAP_T                        // records per tile of the per-record path (all a compact list holds)
 #define SHORT_KMAX 32                           // segments one record may span there
 #define GIN_WORDS (NSEG + 4)                    // segment registers / the scan (+ the tile's end)
 #define FLG_BYTES (NSEG / 8)                    // segments that hold a reset (tile-wide scan)
