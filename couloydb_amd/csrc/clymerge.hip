@@ -616,6 +616,7 @@ k_mhint(const MEnt* __restrict__ e, const MCopy* __restrict__ cp, const cly_tupl
 // re-encoded prefix, the end of the file, an append's kept bytes) gathers its
 // 16 bytes one by one.
 __device__ const uint8_t g_zero_byte = 0;
+__device__ const uint32_t g_zero_words[4] = {0u, 0u, 0u, 0u};
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));   // 16 B, dword-aligned
 typedef uint32_t mc_u32x4 __attribute__((ext_vector_type(4)));
 #define MC_W 4                                   // waves per workgroup
@@ -637,6 +638,19 @@ __device__ __forceinline__ void mc_part(uint64_t s, int n, uint32_t (&w)[4]) {
     for (int q = 0; q < 5; q++) t[q] = q < nd ? wp[q] : 0u;
     #pragma unroll
     for (int q = 0; q < 4; q++) w[q] = __builtin_amdgcn_alignbit(t[q + 1], t[q], sh * 8);
+}
+// the same in two halves: the loads (issued with no branch: a lane that needs
+// none, or fewer than five dwords, loads zero words), then the funnel shift
+__device__ __forceinline__ void mc_load(uint64_t s, int n, bool on, uint32_t (&t)[5]) {
+    const CLY_GLB uint32_t* wp = (const CLY_GLB uint32_t*)(s & ~3ull);
+    const int nd = on ? (int)(((uint32_t)(s & 3) + (uint32_t)n + 3) >> 2) : 0;
+    #pragma unroll
+    for (int q = 0; q < 5; q++) t[q] = *(q < nd ? wp + q : (const CLY_GLB uint32_t*)g_zero_words);
+}
+__device__ __forceinline__ void mc_align(const uint32_t (&t)[5], uint64_t s, uint32_t (&w)[4]) {
+    const uint32_t sh = (uint32_t)(s & 3) * 8;
+    #pragma unroll
+    for (int q = 0; q < 4; q++) w[q] = __builtin_amdgcn_alignbit(t[q + 1], t[q], sh);
 }
 __device__ __forceinline__ uint32_t mc_sel(const uint32_t (&b)[4], int k) {
     return k == 0 ? b[0] : k == 1 ? b[1] : k == 2 ? b[2] : k == 3 ? b[3] : 0u;
@@ -668,6 +682,44 @@ __device__ __forceinline__ uint32_t mc_wave_max_incl(uint32_t v) {
     return v;
 }
 
+// A destination block's place: its region's end L and kept prefix, its first
+// descriptor j0 and descriptor count (ok = false: nothing of it is written).
+struct McBlk { bool ok; uint32_t j0, cnt; uint64_t fo, L, keep; };
+// lanes 0 and 1: bmap[b + lane], and flen[k] (lane 0) / fstart[k + 1] (lane 1)
+__device__ __forceinline__ void mc_info_load(uint64_t b, uint64_t nblocks, uint64_t bpf, const uint32_t* bmap,
+                                             const uint64_t* fstart, const uint64_t* flen, int lane, uint32_t& vb,
+                                             uint64_t& vf) {
+    vb = 0u; vf = 0u;
+    if (b < nblocks && lane < 2) {
+        const uint64_t k = b / bpf;
+        vb = bmap[b + (uint64_t)lane];
+        vf = lane ? fstart[k + 1] : flen[k];
+    }
+}
+// the loaded descriptor's registers are needed here (the compiler's wait for them)
+__device__ __forceinline__ void mc_pin(const MCopy& c) {
+    asm volatile("" ::"v"(c.dst), "v"(c.src), "v"(c.size), "v"(c.pre));
+}
+template <int CMAX>
+__device__ __forceinline__ McBlk mc_info_use(uint64_t b, uint64_t nblocks, uint64_t bpf, uint64_t stride, uint64_t lo0,
+                                             uint32_t vb, uint64_t vf) {
+    McBlk r;
+    r.ok = false; r.j0 = 0; r.cnt = 0; r.fo = 0; r.L = 0; r.keep = 0;
+    if (b >= nblocks) return r;
+    const uint64_t k = b / bpf;
+    r.fo = b * M_CB - k * stride;
+    r.L = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(vf >> 32), 0) << 32) | __builtin_amdgcn_readlane((uint32_t)vf, 0);
+    r.keep = k == 0 ? lo0 : 0;
+    if (r.fo >= r.L || r.fo + M_CB <= r.keep || r.L <= r.keep) return r;
+    r.j0 = __builtin_amdgcn_readlane(vb, 0);
+    uint64_t j1 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(vf >> 32), 1) << 32) | __builtin_amdgcn_readlane((uint32_t)vf, 1);
+    if (r.fo + M_CB < r.L) j1 = (uint64_t)__builtin_amdgcn_readlane(vb, 1) + 1;
+    const uint64_t n = j1 - r.j0;
+    r.cnt = n > (uint64_t)CMAX ? (uint32_t)CMAX : (uint32_t)n;
+    r.ok = true;
+    return r;
+}
+
 // Template over the descriptor capacity per block (CMAX) and the prefix stride
 // (PRE); lo0 = first byte of region 0 that belongs to the output (appends
 // continue an active file: bytes below it are kept as they are).  fstart[k]
@@ -684,23 +736,43 @@ k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uin
     mc_u32x4* desc = s_desc[w];
     uint8_t* pres = s_pre[w];
     uint32_t* map = (uint32_t*)s_map[w];
-    const uint64_t bpf = stride / M_CB;
-    for (uint64_t b = (uint64_t)blockIdx.x * MC_W + w; b < nblocks; b += (uint64_t)gridDim.x * MC_W) {
-        const uint64_t k = b / bpf;
-        const uint64_t B = b * M_CB, fo = B - k * stride;
-        const uint64_t L = flen[k];
-        const uint64_t keep = k == 0 ? lo0 : 0;
-        if (fo >= L || fo + M_CB <= keep || L <= keep) continue;  // (wave-uniform)
-        const uint32_t j0 = bmap[b];
-        uint64_t j1 = fstart[k + 1];
-        if (fo + M_CB < L) j1 = (uint64_t)bmap[b + 1] + 1;
-        uint32_t cnt = (uint32_t)(j1 - j0);
-        if (cnt > CMAX) cnt = CMAX;
+    const uint64_t bpf = stride / M_CB, step = (uint64_t)gridDim.x * MC_W;
+    // A block's loads depend on each other (bmap -> descriptors -> source
+    // bytes).  The wave loads its next block's descriptors (the first 64, one
+    // per lane) and the bmap / flen / fstart words of the block after that
+    // while it copies the current block, as vector loads issued before the
+    // block's source loads: one wait for those (vmcnt counts loads and stores
+    // in issue order) finds all of them in, before any store of the block.
+    uint64_t b = (uint64_t)blockIdx.x * MC_W + w;
+    uint32_t vb;
+    uint64_t vf;
+    mc_info_load(b, nblocks, bpf, bmap, fstart, flen, lane, vb, vf);
+    McBlk cur = mc_info_use<CMAX>(b, nblocks, bpf, stride, lo0, vb, vf);
+    MCopy cq = {0, 0, 0, 0};
+    if (cur.ok && (uint32_t)lane < cur.cnt) cq = cp[cur.j0 + lane];
+    mc_info_load(b + step, nblocks, bpf, bmap, fstart, flen, lane, vb, vf);
+    McBlk nx = mc_info_use<CMAX>(b + step, nblocks, bpf, stride, lo0, vb, vf);
+    mc_pin(cq);
+    for (; b < nblocks; b += step) {
+        MCopy cn = {0, 0, 0, 0};
+        if (nx.ok && (uint32_t)lane < nx.cnt) cn = cp[nx.j0 + lane];
+        mc_info_load(b + 2 * step, nblocks, bpf, bmap, fstart, flen, lane, vb, vf);
+        const MCopy cl = cq;
+        const McBlk cb = cur;
+        McBlk nx2;
+        if (!cb.ok) {                                           // (wave-uniform)
+            mc_pin(cn);
+            nx2 = mc_info_use<CMAX>(b + 2 * step, nblocks, bpf, stride, lo0, vb, vf);
+            cur = nx; cq = cn; nx = nx2;
+            continue;
+        }
+        const uint64_t B = b * M_CB, fo = cb.fo, L = cb.L, keep = cb.keep;
+        const uint32_t j0 = cb.j0, cnt = cb.cnt;
         mc_wave_sync();                                         // previous block's readers are done
         s_map[w][lane] = (mc_u32x4){0u, 0u, 0u, 0u};
         mc_wave_sync();
         for (uint32_t q = lane; q < cnt; q += 64) {
-            const MCopy c = cp[j0 + q];
+            const MCopy c = q < 64 ? cl : cp[j0 + q];
             const int32_t rel = (int32_t)((int64_t)c.dst - (int64_t)B);   // >= -(record size) > -2^31
             desc[q] = (mc_u32x4){(uint32_t)c.src, (uint32_t)(c.src >> 32), (uint32_t)rel, c.size};
             pres[q] = (uint8_t)c.pre;
@@ -720,36 +792,42 @@ k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uin
         const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(out + B, (short)0, (int)M_CB, 0x00020000);
         uint32_t a[MC_P][5];
         uint32_t fast = 0, slow = 0, shs = 0;
+        // (branch-free: every lane loads every piece, a piece that is not a
+        // fast one from a zero word, so that the loads land in a[][] directly
+        // and all of them are in flight together)
         #pragma unroll
         for (int p = 0; p < MC_P; p++) {
             const int P = p * 64 + lane, d = P * 16;
-            if (fo + (uint64_t)d >= L || fo + (uint64_t)d + 16 <= keep) continue;
-            if (fo + (uint64_t)d < keep) { slow |= 1u << p; continue; }
+            const bool out_ = fo + (uint64_t)d >= L || fo + (uint64_t)d + 16 <= keep;
+            const bool kept = fo + (uint64_t)d < keep;
             const uint32_t r = map[P];
             const mc_u32x4 D = desc[r];
             const int r0 = d - (int32_t)D.z, pr = pres[r];
-            if (r0 >= pr && (int64_t)r0 + 16 <= (int64_t)D.w) {
-                const uint64_t sa = (((uint64_t)D.y << 32) | D.x) + (uint64_t)(r0 - pr);
-                const CLY_GLB uint32_t* wp = (const CLY_GLB uint32_t*)(sa & ~3ull);
-                const u32x4a v4 = *(const CLY_GLB u32x4a*)wp;  // one dwordx4 at a dword-aligned address
-                a[p][0] = v4.x; a[p][1] = v4.y; a[p][2] = v4.z; a[p][3] = v4.w;
-                a[p][4] = (sa & 3) ? wp[4] : 0u;
-                fast |= 1u << p;
-                shs |= (uint32_t)(sa & 3) << (2 * p);
-            } else {
-                slow |= 1u << p;
-            }
+            const bool isf = !out_ && !kept && r0 >= pr && (int64_t)r0 + 16 <= (int64_t)D.w;
+            const uint64_t sa = isf ? (((uint64_t)D.y << 32) | D.x) + (uint64_t)(r0 - pr) : (uint64_t)g_zero_words;
+            const CLY_GLB uint32_t* wp = (const CLY_GLB uint32_t*)(sa & ~3ull);
+            const u32x4a v4 = *(const CLY_GLB u32x4a*)wp;      // one dwordx4 at a dword-aligned address
+            a[p][0] = v4.x; a[p][1] = v4.y; a[p][2] = v4.z; a[p][3] = v4.w;
+            a[p][4] = wp[(sa & 3) ? 4 : 0];                      // (dword 0 again when not needed)
+            fast |= (isf ? 1u : 0u) << p;
+            slow |= (!out_ && !isf ? 1u : 0u) << p;
+            shs |= (uint32_t)(sa & 3) << (2 * p);
         }
         // the lane's first slow piece: across exactly one record boundary, the
         // tail of record r (body or prefix) then the head of record r + 1
-        if (TWO && slow) {
+        uint32_t ta[5], tb[5];
+        uint64_t sA = 0, sB = 0;
+        int d2 = -1, n2 = 0;                                    // the piece assembled from two records
+        if (TWO) {
+          bool two = false;
+          int nA = 0, d = 0;
+          if (slow) {
             const int p = __builtin_ctz(slow);
-            const int P = p * 64 + lane, d = P * 16;
-            bool two = fo + (uint64_t)d >= keep && fo + (uint64_t)d + 16 <= L;
+            const int P = p * 64 + lane;
+            d = P * 16;
+            two = fo + (uint64_t)d >= keep && fo + (uint64_t)d + 16 <= L;
             const uint32_t r = two ? map[P] : 0u;
             two = two && r + 1 < cnt;
-            uint64_t sA = 0, sB = 0;
-            int nA = 0;
             if (two) {
                 const mc_u32x4 D = desc[r], E = desc[r + 1];
                 const int r0 = d - (int32_t)D.z, pr = pres[r], pb = pres[r + 1];
@@ -762,14 +840,43 @@ k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uin
                 else if (pb >= 16 - nA) sB = (uint64_t)(pre + (uint64_t)(j0 + r + 1) * PRE);
                 else two = false;
             }
-            if (two) {
-                uint32_t xa[4], xb[4], o[4];
-                mc_part(sA, nA, xa);
-                mc_part(sB, 16 - nA, xb);
-                mc_join(xa, xb, nA, o);
-                __builtin_amdgcn_raw_buffer_store_b128((mc_u32x4){o[0], o[1], o[2], o[3]}, ors, d, 0, 0);
-                slow &= slow - 1;
+          }
+          mc_load(sA, nA, two, ta);
+          mc_load(sB, 16 - nA, two, tb);
+          if (two) { d2 = d; n2 = nA; }
+        }
+        // the merge's hint records: the first MH_KEY realKey bytes of every
+        // record starting in the block, re-read from the source lines the
+        // block's loads bring into L2 (k_mhint then reads 16 B per record
+        // instead of a line of the file); the first 64 records' loads here
+        uint32_t tk[5];
+        uint64_t sk = 0;
+        bool kst = false;
+        if (keys) {
+            bool kon = false;
+            if ((uint32_t)lane < cnt) {
+                const mc_u32x4 D = desc[lane];
+                if ((int32_t)D.z >= 0 && (int32_t)D.z < M_CB && MC_RK(cl.pre) <= MH_KEY) {   // starts in the block
+                    kst = true;
+                    kon = MC_RK(cl.pre) != 0;
+                    sk = (((uint64_t)D.y << 32) | D.x) + MC_KOFF(cl.pre);
+                }
             }
+            mc_load(sk, (int)MC_RK(cl.pre), kon, tk);
+        }
+        // the block's loads are in, and with them the next blocks' descriptors
+        // and words (issued before them)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        mc_pin(cn);
+        nx2 = mc_info_use<CMAX>(b + 2 * step, nblocks, bpf, stride, lo0, vb, vf);
+        cur = nx; cq = cn; nx = nx2;
+        if (TWO && d2 >= 0) {
+            uint32_t xa[4], xb[4], o[4];
+            mc_align(ta, sA, xa);
+            mc_align(tb, sB, xb);
+            mc_join(xa, xb, n2, o);
+            __builtin_amdgcn_raw_buffer_store_b128((mc_u32x4){o[0], o[1], o[2], o[3]}, ors, d2, 0, 0);
+            slow &= slow - 1;
         }
         #pragma unroll
         for (int p = 0; p < MC_P; p++) {
@@ -814,11 +921,12 @@ k_mcopy(const MCopy* __restrict__ cp, const uint8_t* __restrict__ pre, const uin
             *(uint4*)(out + B + d) = make_uint4(v[0], v[1], v[2], v[3]);
         }
         if (keys) {
-            // the merge's hint records: the first MH_KEY realKey bytes of every
-            // record starting in the block, re-read from the source lines the
-            // block's loads just brought into L2 (k_mhint then reads 16 B per
-            // record instead of a line of the file)
-            for (uint32_t q = lane; q < cnt; q += 64) {
+            if (kst) {
+                uint32_t kw[4];
+                mc_align(tk, sk, kw);
+                keys[j0 + lane] = make_uint4(kw[0], kw[1], kw[2], kw[3]);
+            }
+            for (uint32_t q = lane + 64; q < cnt; q += 64) {
                 const int32_t rl = (int32_t)desc[q].z;
                 if (rl < 0 || rl >= M_CB) continue;                  // starts in another block
                 const uint32_t px = cp[j0 + q].pre;
