@@ -86,6 +86,7 @@ extern "C" hipError_t cly_ix_scratch_internal(cly_ctx* ctx, int k, size_t bytes,
 #define M_NT 256
 #define M_IT 16
 #define M_BLK (M_NT * M_IT)          // tuples (or live records) per workgroup of the scans
+#define MP_FILES 512                 // input / output files whose bounds k_mplace keeps in LDS
 #define M_PRE 32                     // bytes per re-encoded prefix (crc..header, 0x00): <= 27
 #define M_CB 4096                    // destination block of k_mcopy
 #define M_CMAX 512                   // records starting in one block (>= M_CB / 10 + 2)
@@ -367,9 +368,16 @@ k_mplace(const MEnt* __restrict__ e, const cly_tuple* __restrict__ tup, const ui
          uint32_t* bmap, uint32_t* hsz, MSum* bsum) {
     __shared__ uint32_t tab[256];
     __shared__ MSum sh[M_NT / 64];
+    // the two searches per record (input file of its tuple, output file of the
+    // record) and the output files' first offsets, from LDS when they fit
+    __shared__ uint64_t s_first[MP_FILES], s_fst[MP_FILES], s_fg[MP_FILES];
     crc_table_init(tab);
     const uint64_t nl = tot->nl;
     const uint32_t nout = tot->n_out;
+    const bool lds_in = nfiles <= MP_FILES, lds_out = nout <= MP_FILES;
+    if (lds_in) for (int i = threadIdx.x; i < nfiles; i += M_NT) s_first[i] = first[i];
+    if (lds_out) for (uint32_t i = threadIdx.x; i < nout; i += M_NT) { s_fst[i] = fstart[i]; s_fg[i] = e[fstart[i]].g; }
+    __syncthreads();
     MSum acc = {0, 0};
     unsigned long long nre = 0;
     const uint64_t b0 = (uint64_t)blockIdx.x * M_BLK;
@@ -381,12 +389,12 @@ k_mplace(const MEnt* __restrict__ e, const cly_tuple* __restrict__ tup, const ui
         int lo = 0, hi = (int)nout - 1;
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
-            if (fstart[mid] <= j) lo = mid; else hi = mid - 1;
+            if ((lds_out ? s_fst[mid] : fstart[mid]) <= j) lo = mid; else hi = mid - 1;
         }
-        const uint64_t off = m.g - e[fstart[lo]].g;
+        const uint64_t off = m.g - (lds_out ? s_fg[lo] : e[fstart[lo]].g);
         const uint64_t dst = (uint64_t)lo * stride + off;
         const cly_tuple t = tup[m.tuple];
-        const int f = find_file_u64(first, nfiles, m.tuple);
+        const int f = find_file_u64(lds_in ? s_first : first, nfiles, m.tuple);
         const uint8_t* F = (const uint8_t*)bases[f] + t.offset;
         const uint32_t rk = t.key_size - t.txid_len;
         MCopy c;
