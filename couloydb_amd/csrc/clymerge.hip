@@ -326,6 +326,7 @@ __device__ __forceinline__ uint64_t g_at(const MEnt* e, uint64_t nl, uint64_t to
 __global__ void __launch_bounds__(M_ROT)
 k_mrot(const MEnt* __restrict__ e, MTot* tot, uint64_t dfs, uint32_t max_files, uint64_t* fstart, uint64_t* flen) {
     const uint64_t nl = tot->nl, total = tot->bytes;
+    const uint64_t mean = nl ? (total / nl > 0 ? total / nl : 1) : 1;   // bytes per merge record
     __shared__ uint64_t s_lo, s_hi;
     uint64_t r = 0;
     uint32_t k = 0;
@@ -335,9 +336,20 @@ k_mrot(const MEnt* __restrict__ e, MTot* tot, uint64_t dfs, uint32_t max_files, 
         uint64_t hi = r + dfs / 10 + 2;                         // merge records are >= 10 bytes
         if (hi > nl) hi = nl;
         if (hi < lo) hi = lo;
+        // first round: M_ROT consecutive positions around the end the mean
+        // record size predicts (one round when the end is among them); then
+        // evenly spread probes
+        uint64_t guess = r + dfs / mean;
+        bool first = true;
         while (lo < hi) {                                       // invariant: g(lo) <= lim
             const uint64_t span = hi - lo;
-            const uint64_t pos = lo + (span * (threadIdx.x + 1) + M_ROT - 1) / M_ROT;   // in (lo, hi]
+            uint64_t pos = lo + (span * (threadIdx.x + 1) + M_ROT - 1) / M_ROT;   // in (lo, hi]
+            if (first) {
+                const uint64_t q = guess + threadIdx.x;         // guess - M_ROT/2 .. guess + M_ROT/2 - 1, clamped
+                pos = q < lo + 1 + M_ROT / 2 ? lo + 1 : q - M_ROT / 2;
+                if (pos > hi) pos = hi;
+                first = false;
+            }
             const int ok = g_at(e, nl, total, pos) <= lim;
             const int c = __syncthreads_count(ok);              // monotone: probes 0..c-1 are ok
             if (threadIdx.x == (unsigned)c - 1) s_lo = pos;
