@@ -45,6 +45,7 @@ extern "C" void** cly_ctx_merge_slot_internal(cly_ctx* c);
 // Scratch buffers of the merge, kept in the context and grown on demand
 // (plain hipMalloc: no allocation inside a timed merge once warm).
 enum { MS_FB, MS_TOT, MS_PLAN, MS_BSUM, MS_ENT, MS_FSTART, MS_FLEN, MS_CP, MS_PRE, MS_BMAP, MS_HSZ, MS_KEYS,
+       MS_PK, MS_PKC,
        MS_A0 = 16, MS_AN = MS_A0 + 16,            // cly_append_device's buffers
        MS_I0 = MS_AN, MS_IN = MS_I0 + 32,         // cly_index_device's buffers (clyindex.hip)
        MS_N = MS_IN };
@@ -91,6 +92,9 @@ extern "C" hipError_t cly_ix_scratch_internal(cly_ctx* ctx, int k, size_t bytes,
 #define M_CB 4096                    // destination block of k_mcopy
 #define M_CMAX 512                   // records starting in one block (>= M_CB / 10 + 2)
 #define PLAN_RE (1ull << 32)         // plan bit: re-encoded
+// k_mplan -> k_mcompact -> k_mplace, per live record: file offset (bits 0-31),
+// header + txId bytes (32-39), realKey length (40-55); PK_SLOW: read the tuple
+#define PK_SLOW (1ull << 56)
 
 struct MSum { unsigned long long bytes, count; };
 struct MEnt { uint64_t g; uint32_t tuple, nsz; };
@@ -222,17 +226,17 @@ __device__ __forceinline__ MSum block_excl(MSum v, MSum& total, MSum* sh) {
 __global__ void __launch_bounds__(M_NT)
 k_mplan(const cly_tuple* __restrict__ tup, uint64_t T, const uint8_t* __restrict__ live,
         const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases, int nfiles,
-        uint64_t* plan, MSum* bsum, uint64_t dfs, MTot* tot) {
+        uint64_t* plan, uint64_t* pk, MSum* bsum, uint64_t dfs, MTot* tot) {
     __shared__ MSum sh[M_NT / 64];
     MSum acc = {0, 0};
     const uint64_t b0 = (uint64_t)blockIdx.x * M_BLK;
     for (int k = 0; k < M_IT; k++) {
         const uint64_t i = b0 + (uint64_t)k * M_NT + threadIdx.x;
         if (i >= T) break;
-        uint64_t p = 0;
+        uint64_t p = 0, pkv = 0;               // (every slot written: whole lines)
         if (live[i] == 1) {                 // CLY_IX_LIVE; a CLY_IX_HOST byte is not a verdict
             const cly_tuple t = tup[i];
-            if (t.txid_len == 0xFF) { atomicOr(&tot->bad, 1u); plan[i] = 0; continue; }   // parseLogRecordKey panics
+            if (t.txid_len == 0xFF) { atomicOr(&tot->bad, 1u); plan[i] = 0; pk[i] = 0; continue; }   // parseLogRecordKey panics
             const uint32_t rk = t.key_size - t.txid_len;
             const uint64_t nks = (uint64_t)rk + 1;
             const int nh = 6 + uvlen(zz((int64_t)nks)) + uvlen(zz((int64_t)t.value_size)) + uvlen(zz(t.expiration));
@@ -254,10 +258,15 @@ k_mplan(const cly_tuple* __restrict__ tup, uint64_t T, const uint8_t* __restrict
             }
             if (nsz > dfs) atomicOr(&tot->bad, 2u);              // one record per file would not fit
             p = nsz | (verbatim ? 0ull : PLAN_RE);
+            // what k_mplace needs of a copied record, so that it reads no tuple
+            const uint32_t hx = (uint32_t)t.header_size + t.txid_len;
+            const bool esc = !verbatim || rk >= 0xFFFFu || hx > 0xFFu || (uint64_t)t.offset >= (1ull << 32);
+            pkv = esc ? PK_SLOW : (uint64_t)t.offset | ((uint64_t)hx << 32) | ((uint64_t)rk << 40);
             acc.bytes += nsz;
             acc.count += 1;
         }
         plan[i] = p;
+        pk[i] = pkv;
     }
     // block sum (order-free)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -297,7 +306,8 @@ k_msums(MSum* bsum, uint64_t nblk, unsigned long long* out_bytes, unsigned long 
 
 // ---- k_mcompact: live records in order, with their pre-rotation offset -----
 __global__ void __launch_bounds__(M_NT)
-k_mcompact(const uint64_t* __restrict__ plan, uint64_t T, const MSum* __restrict__ bsum, MEnt* ent) {
+k_mcompact(const uint64_t* __restrict__ plan, const uint64_t* __restrict__ pk, uint64_t T,
+           const MSum* __restrict__ bsum, MEnt* ent, uint64_t* pkc) {
     __shared__ MSum sh[M_NT / 64];
     const uint64_t b0 = (uint64_t)blockIdx.x * M_BLK;
     MSum carry = bsum[blockIdx.x];
@@ -309,7 +319,10 @@ k_mcompact(const uint64_t* __restrict__ plan, uint64_t T, const MSum* __restrict
         MSum v = {nsz, nsz ? 1ull : 0ull};
         MSum total;
         const MSum ex = block_excl(v, total, sh);
-        if (nsz) ent[carry.count + ex.count] = MEnt{carry.bytes + ex.bytes, (uint32_t)i, nsz};
+        if (nsz) {
+            ent[carry.count + ex.count] = MEnt{carry.bytes + ex.bytes, (uint32_t)i, nsz};
+            pkc[carry.count + ex.count] = pk[i];
+        }
         carry.bytes += total.bytes;
         carry.count += total.count;
     }
@@ -374,7 +387,8 @@ k_mrot(const MEnt* __restrict__ e, MTot* tot, uint64_t dfs, uint32_t max_files, 
 
 // ---- k_mplace: per live record, where it goes --------------------------------
 __global__ void __launch_bounds__(M_NT)
-k_mplace(const MEnt* __restrict__ e, const cly_tuple* __restrict__ tup, const uint64_t* __restrict__ plan,
+k_mplace(const MEnt* __restrict__ e, const uint64_t* __restrict__ pkc, const cly_tuple* __restrict__ tup,
+         const uint64_t* __restrict__ plan,
          const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases, int nfiles,
          const uint64_t* __restrict__ fstart, MTot* tot, uint64_t stride, MCopy* cp, uint8_t* pre,
          uint32_t* bmap, uint32_t* hsz, MSum* bsum) {
@@ -405,13 +419,22 @@ k_mplace(const MEnt* __restrict__ e, const cly_tuple* __restrict__ tup, const ui
         }
         const uint64_t off = m.g - (lds_out ? s_fg[lo] : e[fstart[lo]].g);
         const uint64_t dst = (uint64_t)lo * stride + off;
-        const cly_tuple t = tup[m.tuple];
         const int f = find_file_u64(lds_in ? s_first : first, nfiles, m.tuple);
-        const uint8_t* F = (const uint8_t*)bases[f] + t.offset;
-        const uint32_t rk = t.key_size - t.txid_len;
+        const uint64_t q = pkc[j];
         MCopy c;
         c.dst = dst;
         c.size = m.nsz;
+        uint32_t rk;
+        if (!(q & PK_SLOW)) {
+            // a record copied byte for byte: its file offset and header sizes
+            // from k_mplan (no tuple read)
+            rk = (uint32_t)(q >> 40) & 0xFFFFu;
+            c.src = bases[f] + (uint32_t)q;
+            c.pre = (rk << 16) | ((uint32_t)((q >> 32) & 0xFFu) << 8);
+        } else {
+        const cly_tuple t = tup[m.tuple];
+        const uint8_t* F = (const uint8_t*)bases[f] + t.offset;
+        rk = t.key_size - t.txid_len;
         const uint32_t kx = (rk < 0xFFFFu ? rk : 0xFFFFu) << 16;
         if (!(plan[m.tuple] & PLAN_RE)) {
             c.src = (uint64_t)F;
@@ -438,6 +461,7 @@ k_mplace(const MEnt* __restrict__ e, const cly_tuple* __restrict__ tup, const ui
             c.pre = kx | ((uint32_t)n + 1);
             c.src = (uint64_t)rkey;
             nre++;
+        }
         }
         cp[j] = c;
         // blocks of k_mcopy whose first byte lies in this record
@@ -997,7 +1021,7 @@ extern "C" int cly_merge_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     hipStream_t st = stream_v ? (hipStream_t)stream_v : cly_ctx_stream_internal(ctx);
     int rc = CLY_OK;
     uint64_t* h_fb = (uint64_t*)malloc(sizeof(uint64_t) * (2 * (size_t)nfiles + 2));
-    uint64_t *d_fb = nullptr, *d_plan = nullptr, *d_fstart = nullptr, *d_flen = nullptr;
+    uint64_t *d_fb = nullptr, *d_plan = nullptr, *d_fstart = nullptr, *d_flen = nullptr, *d_pk = nullptr, *d_pkc = nullptr;
     MSum* d_bsum = nullptr;
     MEnt* d_ent = nullptr;
     MCopy* d_cp = nullptr;
@@ -1020,14 +1044,16 @@ extern "C" int cly_merge_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     MCK(scratch(ctx, MS_PLAN, sizeof(uint64_t) * (T + 1), &d_plan));
     MCK(scratch(ctx, MS_BSUM, sizeof(MSum) * nblk, &d_bsum));
     MCK(scratch(ctx, MS_ENT, sizeof(MEnt) * (T + 1), &d_ent));
+    MCK(scratch(ctx, MS_PK, sizeof(uint64_t) * (T + 1), &d_pk));
+    MCK(scratch(ctx, MS_PKC, sizeof(uint64_t) * (T + 1), &d_pkc));
     MCK(hipEventRecord(e0, st));
     if (T) {
-        k_mplan<<<(unsigned)nblk, M_NT, 0, st>>>(d_tuples, T, d_live, d_fb, d_fb + nfiles + 1, nfiles, d_plan, d_bsum,
+        k_mplan<<<(unsigned)nblk, M_NT, 0, st>>>(d_tuples, T, d_live, d_fb, d_fb + nfiles + 1, nfiles, d_plan, d_pk, d_bsum,
                                                   data_file_size, d_tot);
         MDBG(st, "k_mplan");
         k_msums<<<1, M_NT, 0, st>>>(d_bsum, nblk, &d_tot->bytes, &d_tot->nl);
         MDBG(st, "k_msums");
-        k_mcompact<<<(unsigned)nblk, M_NT, 0, st>>>(d_plan, T, d_bsum, d_ent);
+        k_mcompact<<<(unsigned)nblk, M_NT, 0, st>>>(d_plan, d_pk, T, d_bsum, d_ent, d_pkc);
         MDBG(st, "k_mcompact");
     }
     MCK(hipMemcpyAsync(&h_tot, d_tot, sizeof(MTot), hipMemcpyDeviceToHost, st));
@@ -1057,7 +1083,7 @@ extern "C" int cly_merge_device(cly_ctx* ctx, const cly_file* files, int nfiles,
         MCK(scratch(ctx, MS_PRE, (size_t)M_PRE * nl, &d_pre));
         MCK(scratch(ctx, MS_BMAP, sizeof(uint32_t) * (nblocks + 1), &d_bmap));
         MCK(scratch(ctx, MS_HSZ, sizeof(uint32_t) * nl, &d_hsz));
-        k_mplace<<<(unsigned)lblk, M_NT, 0, st>>>(d_ent, d_tuples, d_plan, d_fb, d_fb + nfiles + 1, nfiles, d_fstart,
+        k_mplace<<<(unsigned)lblk, M_NT, 0, st>>>(d_ent, d_pkc, d_tuples, d_plan, d_fb, d_fb + nfiles + 1, nfiles, d_fstart,
                                                    d_tot, stride, d_cp, d_pre, d_bmap, d_hsz, d_bsum);
         MDBG(st, "k_mplace");
         k_msums<<<1, M_NT, 0, st>>>(d_bsum, lblk, &d_tot->hint_bytes, nullptr);
