@@ -4,9 +4,13 @@
 Contract (see task spec): `python bench.py --gpus N --steps K --warmup W` prints ONE
 JSON line on rank 0.  A step = one full scan (k_scan, k_link, k_emit,
 k_fin and the result read-back) of the configuration's data files, already resident in HBM.  For N>1
-each rank (one per GPU, launched by torch.distributed.run) scans its own fid
-range of the same per-GPU size (weak scaling, no collective on the data path;
-the barrier and the max-over-ranks timing use torch.distributed).
+each rank (one per GPU) scans its own fid range of the same per-GPU size
+(weak scaling, no collective on the data path; the barrier and the
+max-over-ranks timing use torch.distributed).  Ranks: either an outer
+`python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`
+(WORLD_SIZE must equal --gpus), or plain `python bench.py --gpus N`, which
+starts the N ranks itself (a torch.distributed.run child, 127.0.0.1) before any
+GPU call and exits with their status.
 
 Workloads (BASELINE.json configs):
   c2 (default): 16 files x 256 MiB, key 0x00||%09d, 256-B random values -> 276-B records
@@ -375,6 +379,62 @@ def append_leg(wl, sc, first, torch, reps=3):
     return res
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` run without an outer launcher: start N rank
+    processes (one per GPU) through torch.distributed.run as a CHILD process
+    (this process never touches the GPU, so no exec after GPU init), let rank 0
+    print the JSON line on the inherited stdout, and return the launcher's exit
+    status."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_protocol(args, rank, world):
+    """--dry-protocol: the rank protocol alone on the CPU (gloo; no GPU, no
+    workload): warmup, barrier, K timed no-op steps, barrier, MAX over ranks,
+    one line from rank 0 carrying n_gpus and every rank's pid.  The CPU tests
+    use it to check the launcher (tests/test_bench_launch.py)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group(backend="gloo")
+    for _ in range(args.warmup):
+        time.sleep(0.001)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001)
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    pids = [os.getpid()]
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        pids = [None] * world
+        dist.all_gather_object(pids, os.getpid())
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(float(t[0]) / max(1, args.steps) * 1e3, 4),
+                          "dry_protocol": True, "rank_pids": pids}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -384,13 +444,28 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
     ap.add_argument("--verify", action="store_true", help="check one file against the oracle after timing")
+    ap.add_argument("--dry-protocol", action="store_true", help="rank protocol only, on the CPU (launcher tests)")
     args = ap.parse_args()
-
-    import torch
-    import torch.distributed as dist
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    # Ranks: under torch.distributed.run WORLD_SIZE is set and must equal
+    # --gpus; without it, --gpus N > 1 starts its own N ranks (before any GPU
+    # call in this process) and exits with their status.
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        print("bench.py: WORLD_SIZE=%s but --gpus %d" % (env_world, args.gpus), file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_protocol:
+        dry_protocol(args, rank, world)
+        return
+
+    import torch
+    import torch.distributed as dist
     # CLY_BENCH_REHEARSE=1: every rank on GPU 0 over gloo (rehearses the N>1
     # path on a one-GPU box; the driver's multi-GPU runs use RCCL, one GPU per rank)
     rehearse = os.environ.get("CLY_BENCH_REHEARSE") == "1"
