@@ -269,9 +269,10 @@ static int map_file(const char* path, Mapped& m, bool& exists) {
 // GetDataFileName(uint32(fid)) = "%09d.cly" (absent: read as empty; the
 // reference's OpenFile creates it empty).  A file listed twice (say "7.cly" and
 // "000000007.cly", or "-1.cly" and "4294967295.cly": the same uint32 fid) is
-// read once, at its last place in the order: the reference's second reading
-// re-applies its records after the files between (and makes it the active file
-// when it is last), which is the state a single reading there leaves.
+// read at every place sort.Ints puts it, as loadDataFile/loadIndex do
+// (db.go:449-464, 587-631): each place opens %09d of the uint32 fid, so every
+// reading sees the same file, and transactions spanning the places resolve as
+// the reference's do.
 static int list_files(const char* dir, std::vector<Mapped>& out, std::unordered_map<uint32_t, uint32_t>& ix) {
     DIR* d = opendir(dir);
     if (!d) return CLY_ERR_ARG;
@@ -289,14 +290,8 @@ static int list_files(const char* dir, std::vector<Mapped>& out, std::unordered_
     closedir(d);
     if (rc != CLY_OK) return rc;
     std::sort(fids.begin(), fids.end());
-    fids.erase(std::unique(fids.begin(), fids.end()), fids.end());
-    std::vector<uint32_t> order;                 // uint32 fids, each at its last place
-    {
-        std::unordered_map<uint32_t, size_t> lastpos;
-        for (size_t k = 0; k < fids.size(); k++) lastpos[(uint32_t)fids[k]] = k;
-        for (size_t k = 0; k < fids.size(); k++)
-            if (lastpos[(uint32_t)fids[k]] == k) order.push_back((uint32_t)fids[k]);
-    }
+    std::vector<uint32_t> order;                 // every listing, in sort.Ints order
+    for (int64_t v : fids) order.push_back((uint32_t)v);
     for (uint32_t fid : order) {
         char path[4096];
         snprintf(path, sizeof(path), "%s/%09u.cly", dir, fid);

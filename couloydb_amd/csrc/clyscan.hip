@@ -1680,9 +1680,15 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         // lane-transposed for the tile-wide scan
         bool plain = !full;
         if (plain) {
-            #pragma unroll
-            for (int k = 0; k < RUN; k += 4)
-                *(CLY_LDS u32x4*)(gin + (uint32_t)lane * RUN + k) = (u32x4){sr[k], sr[k + 1], sr[k + 2], sr[k + 3]};
+            if (RUN % 4 == 0) {
+                #pragma unroll
+                for (int k = 0; k < RUN; k += 4)
+                    *(CLY_LDS u32x4*)(gin + (uint32_t)lane * RUN + k) =
+                        (u32x4){sr[k], sr[k + 1 < RUN ? k + 1 : 0], sr[k + 2 < RUN ? k + 2 : 0], sr[k + 3 < RUN ? k + 3 : 0]};
+            } else {
+                #pragma unroll
+                for (int k = 0; k < RUN; k++) gin[(uint32_t)lane * RUN + k] = sr[k];
+            }
         } else {
             #pragma unroll
             for (int k = 0; k < RUN; k++) gin[k * 64 + lane] = sr[k];

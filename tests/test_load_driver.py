@@ -235,7 +235,8 @@ def test_gpu_ttl_sweep_rotation(scanner, tmp_path):
 @pytest.mark.gpu
 def test_gpu_dir_listing_atoi(scanner, tmp_path):
     """loadDataFile's listing: stems by strconv.Atoi ("+1" and "0001" name fid
-    1, read from 000000001.cly); a stem Atoi rejects fails the open."""
+    1, read from 000000001.cly, once per listing: sort.Ints keeps the four
+    fid-1 entries, db.go:449-464); a stem Atoi rejects fails the open."""
     from couloydb_amd import ScanError, _abi
     a = mg.encode_record(mg.key_tx(b"a", 0), b"1")
     b = mg.encode_record(mg.key_tx(b"a", 0), b"2")
@@ -247,7 +248,7 @@ def test_gpu_dir_listing_atoi(scanner, tmp_path):
         with open(os.path.join(tmp_path, alias), "wb") as f:
             f.write(b"garbage")                                   # never read: fid 1 opens 000000001.cly
     with scanner.open_db(str(tmp_path)) as db:
-        assert db.get(b"a") == b"2" and db.stats.n_files == 2 and db.stats.active_fid == 1
+        assert db.get(b"a") == b"2" and db.stats.n_files == 5 and db.stats.active_fid == 1
     with open(os.path.join(tmp_path, "x7.cly"), "wb") as f:
         f.write(b"")
     with pytest.raises(ScanError) as e:
@@ -394,8 +395,9 @@ def test_gpu_open_error_order(scanner, tmp_path):
 @pytest.mark.gpu
 def test_gpu_dir_listing_uint32_fids(scanner, tmp_path):
     """Stems Atoi accepts but uint32() wraps: "-1.cly" is fid 4294967295 (read
-    from 4294967295.cly, sort.Ints puts it first), listed once with the
-    spelled-out name; lookups into it and into fid 3 both resolve."""
+    from 4294967295.cly; sort.Ints puts it first, and the spelled-out name
+    last, so that file is read twice); lookups into it and into fid 3 both
+    resolve."""
     a = mg.encode_record(mg.key_tx(b"a", 0), b"from-max")
     b = mg.encode_record(mg.key_tx(b"b", 0), b"from-3")
     with open(os.path.join(tmp_path, "4294967295.cly"), "wb") as f:
@@ -405,9 +407,36 @@ def test_gpu_dir_listing_uint32_fids(scanner, tmp_path):
     with open(os.path.join(tmp_path, "000000003.cly"), "wb") as f:
         f.write(b)
     with scanner.open_db(str(tmp_path)) as db:
-        assert db.stats.n_files == 2
+        assert db.stats.n_files == 3
         assert db.get(b"a") == b"from-max" and db.get(b"b") == b"from-3"
         assert db.stats.active_fid == 0xFFFFFFFF                   # the last in sort.Ints order
+
+
+@pytest.mark.gpu
+def test_gpu_dir_listing_tx_across_repeated_file(scanner, tmp_path):
+    """A transaction whose data records sit in a file read at two places of
+    the listing ("-1.cly" first, "4294967295.cly" last) and whose commit marker
+    sits in a file between them: the first reading buffers the records, the
+    marker applies them (loadIndex, db.go:603-627), the second reading buffers
+    them again without a marker.  The key is therefore found; a single reading
+    at the last place would leave it uncommitted."""
+    tx = 77
+    data = mg.encode_record(mg.key_tx(b"k", tx), b"in-tx")
+    fin = mg.encode_record(mg.key_tx(mg.TX_COMMIT_KEY, tx), b"", mg.TXN_COMMIT)
+    with open(os.path.join(tmp_path, "4294967295.cly"), "wb") as f:
+        f.write(data)
+    with open(os.path.join(tmp_path, "-1.cly"), "wb") as f:
+        f.write(b"never read")
+    with open(os.path.join(tmp_path, "000000003.cly"), "wb") as f:
+        f.write(fin)
+    files = [np.frombuffer(b, np.uint8) for b in (data, fin, data)]
+    tpf = [co.scan_file(F, fid)[0] for F, fid in zip(files, [0xFFFFFFFF, 3, 0xFFFFFFFF])]
+    ix = {}
+    index_states(files, tpf, out_index=ix)
+    assert (mg.STRING, b"k") in ix                                # the restatement finds the key too
+    with scanner.open_db(str(tmp_path)) as db:
+        assert db.stats.n_files == 3
+        assert db.get(b"k") == b"in-tx"
 
 
 @pytest.mark.gpu
