@@ -113,7 +113,8 @@ class ClyLoadStats(ctypes.Structure):
                 ("hint_records", ctypes.c_uint64), ("n_expired", ctypes.c_uint64),
                 ("write_off_loaded", ctypes.c_int64), ("active_fid_loaded", ctypes.c_uint32),
                 ("sweep_files", ctypes.c_uint32), ("n_shards", ctypes.c_uint32), ("_pad2", ctypes.c_uint32),
-                ("tuple_slots", ctypes.c_uint64)]
+                ("tuple_slots", ctypes.c_uint64), ("order_ms", ctypes.c_double), ("order_rounds", ctypes.c_uint32),
+                ("_pad3", ctypes.c_uint32)]
 
 
 class ClyDbOptions(ctypes.Structure):

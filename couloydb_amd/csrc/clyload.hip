@@ -52,6 +52,9 @@ extern "C" hipStream_t cly_ctx_stream_internal(cly_ctx* c);
 extern "C" int cly_ctx_device_internal(cly_ctx* c);
 extern "C" uint64_t cly_ix_hash_mask_internal(uint64_t n);
 extern "C" hipError_t cly_ix_hash_ptr_internal(cly_ctx* ctx, uint64_t n, void** out);
+extern "C" int cly_order_keys_internal(hipStream_t st, const cly_tuple* d_tup, uint64_t n, const uint8_t* d_state,
+                                       uint32_t dt, const uint64_t* first, const uint64_t* bases, int nf,
+                                       uint32_t** d_ord_out, uint64_t* m_out, uint32_t* rounds_out);
 extern "C" int cly_scan_device_alloc_internal(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple** d_out,
                                               uint64_t* cap, uint64_t* file_first, cly_file_result* res,
                                               uint64_t* needed);
@@ -160,6 +163,12 @@ struct cly_db {
     int hshift = 60;
     std::vector<uint64_t> first;
     FlatIndex str, listmeta;
+    // the String (0) and ListMeta (1) winners as tuple indices, ascending by
+    // key (bytes.Compare; clyorder.hip): the BTree order of the enumeration
+    HostArr<uint32_t> ord[2];
+    uint64_t n_ord[2] = {0, 0};
+    // the Hash / List / Set entries in (key, sub) order, built at the open
+    std::vector<cly_db_entry> comp[3];
     // getHashIndex / getListDataIndex / getSetIndex (index.go): realKey -> MemTable
     std::unordered_map<std::string, std::unordered_map<std::string, cly_pos>> hash, list, set;
 };
@@ -540,7 +549,7 @@ static std::vector<uint8_t> tombstone(const uint8_t* key, uint64_t klen) {
 // 0 .. nb-1 (the caller holds g_stage_mu).
 static int flat_device(cly_ctx* ctx, cly_db* db, const cly_file* df, int nall, const cly_tuple* d_tup,
                        const std::vector<uint64_t>& first, const std::vector<cly_file_result>& res, uint8_t* d_state,
-                       const cly_pos* d_hpos, uint64_t need, cly_index_result& ir, int nb) {
+                       const cly_pos* d_hpos, uint64_t need, cly_index_result& ir, int nb, cly_load_stats& s) {
     hipStream_t strm = cly_ctx_stream_internal(ctx);
     if (nall) {
         const int rc = cly_index_device(ctx, df, nall, d_tup, first.data(), res.data(), d_state, &ir, nullptr);
@@ -553,6 +562,7 @@ static int flat_device(cly_ctx* ctx, cly_db* db, const cly_file* df, int nall, c
     unsigned long long* d_cnt = nullptr;
     unsigned long long* d_slots = nullptr;
     uint64_t* d_geo = nullptr;
+    uint32_t* d_ord[2] = {nullptr, nullptr};
     unsigned long long cnt[2 * FLAT_SHARDS];
     uint64_t geo[4 * FLAT_SHARDS], tot = 0;
     const unsigned grid = (unsigned)std::min<uint64_t>((need + 255) / 256, 8192);
@@ -587,6 +597,22 @@ static int flat_device(cly_ctx* ctx, cly_db* db, const cly_file* df, int nall, c
     hipLaunchKernelGGL(k_flat_insert, dim3(grid), dim3(256), 0, strm, d_state, d_hash, need, db->hmask, db->hshift, d_geo,
                        d_slots);
     DCK(hipGetLastError());
+    {
+        // the MemTable order: String (dt 0) and ListMeta (dt 3) winners by key
+        const double to = now_ms();
+        std::vector<uint64_t> bases(nall);
+        for (int i = 0; i < nall; i++) bases[i] = (uint64_t)(uintptr_t)df[i].base;
+        for (int k = 0; k < 2; k++) {
+            uint32_t rounds = 0;
+            rc = cly_order_keys_internal(strm, d_tup, need, d_state, k ? 3u : 0u, first.data(), bases.data(), nall,
+                                         &d_ord[k], &db->n_ord[k], &rounds);
+            if (rc != CLY_OK) goto done;
+            s.order_rounds = std::max(s.order_rounds, rounds);
+            db->ord[k].alloc(db->n_ord[k]);
+            if (db->n_ord[k]) parts.push_back({db->ord[k].data(), d_ord[k], sizeof(uint32_t) * db->n_ord[k]});
+        }
+        s.order_ms = now_ms() - to;
+    }
     DCK(hipStreamSynchronize(strm));
     if (db->n_hint) parts.push_back({db->hint_pos.data(), d_hpos, sizeof(cly_pos) * db->n_hint});
     rc = copy_to_host(ctx, parts, 0, nb, false);
@@ -596,7 +622,7 @@ static int flat_device(cly_ctx* ctx, cly_db* db, const cly_file* df, int nall, c
         db->listmeta.n += db->listmeta.sh[sh].n;
     }
 done:
-    hipFree(d_cnt); hipFree(d_slots);
+    hipFree(d_cnt); hipFree(d_slots); hipFree(d_ord[0]); hipFree(d_ord[1]);
     return rc;
 }
 
@@ -817,7 +843,7 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
             if (need) trc = copy_to_host(ctx, {{db->tuples.data(), d_tup, sizeof(cly_tuple) * need}}, nb,
                                          std::max(1, nt - nb), false);
         });
-        rc = flat_device(ctx, db, nall ? df.data() : nullptr, nall, d_tup, first, res, d_state, d_hpos, need, ir, nb);
+        rc = flat_device(ctx, db, nall ? df.data() : nullptr, nall, d_tup, first, res, d_state, d_hpos, need, ir, nb, s);
         tcopy.join();
         if (rc == CLY_OK) rc = trc;
         if (rc != CLY_OK) goto done;
@@ -850,6 +876,31 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
             } else {                             // realKey = R, hashKey = P
                 db->set[std::string((const char*)r, k.r_len)][std::string((const char*)k.p, 4)] = p;
             }
+        }
+        // the per-key MemTables' fill order: keys ascending, subs ascending
+        // inside a key (bytes.Compare; google/btree keeps the same order)
+        const std::unordered_map<std::string, std::unordered_map<std::string, cly_pos>>* cm[3] = {&db->hash, &db->list,
+                                                                                                   &db->set};
+        for (int k = 0; k < 3; k++) {
+            std::vector<cly_db_entry>& v = db->comp[k];
+            v.clear();
+            for (const auto& kv : *cm[k])
+                for (const auto& sub : kv.second) {
+                    cly_db_entry e;
+                    memset(&e, 0, sizeof(e));
+                    e.key = (const uint8_t*)kv.first.data(); e.key_len = kv.first.size();
+                    e.sub = (const uint8_t*)sub.first.data(); e.sub_len = sub.first.size();
+                    e.pos = sub.second;
+                    v.push_back(e);
+                }
+            auto bcmp = [](const uint8_t* a, uint64_t na, const uint8_t* b, uint64_t nb) {
+                const int c = memcmp(a, b, std::min(na, nb));
+                return c ? c : (na < nb ? -1 : na > nb ? 1 : 0);
+            };
+            std::sort(v.begin(), v.end(), [&](const cly_db_entry& a, const cly_db_entry& b) {
+                const int c = bcmp(a.key, a.key_len, b.key, b.key_len);
+                return c ? c < 0 : bcmp(a.sub, a.sub_len, b.sub, b.sub_len) < 0;
+            });
         }
         s.str_keys = db->str.n;
         s.listmeta_keys = db->listmeta.n;
@@ -1003,38 +1054,25 @@ extern "C" int cly_db_value(cly_db* db, const cly_pos* pos, uint8_t* buf, uint64
 static void build_entries(cly_db* db, int kind) {
     std::vector<cly_db_entry>& v = db->it[kind];
     v.clear();
-    auto flat = [&](const FlatIndex& xi, bool str) {
-        for (int sh = 0; sh < FLAT_SHARDS; sh++) {
-            const FlatShard& x = xi.sh[sh];
-            for (uint64_t i = 0; i <= x.mask && x.mask; i++) {
-                const uint64_t ti = flat_ti(x.s[i]);
-                if (ti == ~0ull) continue;
-                cly_db_entry e;
-                memset(&e, 0, sizeof(e));
-                e.key = real_key_ptr(db, ti, e.key_len);
-                e.pos = pos_of(db, ti);
-                e.expiration = str && ti >= db->n_hint ? db->tuples[ti].expiration : 0;
-                v.push_back(e);
-            }
+    // String / ListMeta: the device's key order (db->ord)
+    auto ordered = [&](int k, bool str) {
+        v.reserve(db->n_ord[k]);
+        for (uint64_t j = 0; j < db->n_ord[k]; j++) {
+            const uint64_t ti = db->ord[k][j];
+            cly_db_entry e;
+            memset(&e, 0, sizeof(e));
+            e.key = real_key_ptr(db, ti, e.key_len);
+            e.pos = pos_of(db, ti);
+            e.expiration = str && ti >= db->n_hint ? db->tuples[ti].expiration : 0;
+            v.push_back(e);
         }
     };
-    auto maps = [&](const std::unordered_map<std::string, std::unordered_map<std::string, cly_pos>>& m) {
-        for (const auto& kv : m)
-            for (const auto& sub : kv.second) {
-                cly_db_entry e;
-                memset(&e, 0, sizeof(e));
-                e.key = (const uint8_t*)kv.first.data(); e.key_len = kv.first.size();
-                e.sub = (const uint8_t*)sub.first.data(); e.sub_len = sub.first.size();
-                e.pos = sub.second;
-                v.push_back(e);
-            }
-    };
     switch (kind) {
-        case CLY_IT_STRING: flat(db->str, true); break;
-        case CLY_IT_LISTMETA: flat(db->listmeta, false); break;
-        case CLY_IT_HASH: maps(db->hash); break;
-        case CLY_IT_LIST: maps(db->list); break;
-        case CLY_IT_SET: maps(db->set); break;
+        case CLY_IT_STRING: ordered(0, true); break;
+        case CLY_IT_LISTMETA: ordered(1, false); break;
+        case CLY_IT_HASH: v = db->comp[0]; break;
+        case CLY_IT_LIST: v = db->comp[1]; break;
+        case CLY_IT_SET: v = db->comp[2]; break;
         case CLY_IT_EXPIRED:
             for (uint64_t i : db->expired) {
                 cly_db_entry e;

@@ -78,6 +78,9 @@ typedef struct cly_load_stats {
     uint32_t n_shards;        /* contexts that loaded files (cly_db_open_multi)   */
     uint32_t _pad2;
     uint64_t tuple_slots;     /* device tuple slots the scans allocated (exact: records + 16 per shard) */
+    double   order_ms;        /* the String / ListMeta winners sorted by key on the device (part of index_ms) */
+    uint32_t order_rounds;    /* refinement rounds of that sort (keys of 16+ bytes sharing 15-byte prefixes) */
+    uint32_t _pad3;
 } cly_load_stats;
 
 /* NewCouloyDB's Options the open uses.                                        */
@@ -134,8 +137,13 @@ int64_t cly_index_key(uint32_t dtype, const uint8_t* d, uint64_t n, uint8_t* out
 int  cly_db_value(cly_db* db, const cly_pos* pos, uint8_t* buf, uint64_t cap, uint64_t* vlen);
 
 /* Enumeration of what the load produced (for bulk-loading the caller's
- * MemTables and TTL queue).  Pointers stay valid until cly_db_close; the order
- * within a kind is unspecified (the MemTables sort).  Not thread-safe.        */
+ * MemTables and TTL queue).  Pointers stay valid until cly_db_close.  The
+ * order is the reference BTree's (meta/btree.go:64-66, bytes.Compare): String
+ * and ListMeta entries ascending by key (sorted on the device during the
+ * open); Hash / List / Set entries grouped by key, the keys ascending, and
+ * inside a key ascending by sub (field, seq gob bytes, member hash) — each
+ * group is one getHashIndex(key) / getListDataIndex / getSetIndex MemTable.
+ * CLY_IT_EXPIRED keeps the sweep's order.  Not thread-safe.                  */
 #define CLY_IT_STRING   0     /* key = realKey, pos, expiration (0 = none; else the
                                  UnixNano the reference's ttl job fires at)   */
 #define CLY_IT_LISTMETA 1     /* key, pos                                       */

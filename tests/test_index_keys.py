@@ -300,3 +300,71 @@ def test_gpu_load_driver_composite_lookups(scanner, tmp_path):
             assert (p.fid, p.offset) == (fid, off), (ik, fid, off)
         with pytest.raises(KeyError):
             db.hpos(b"no such key", b"f0")
+
+
+@pytest.mark.gpu
+def test_gpu_entries_in_btree_order(scanner, tmp_path):
+    """The enumeration in the reference BTree's order (meta/btree.go:64-66,
+    bytes.Compare; MemTable.Iterator): String and ListMeta entries (sorted on
+    the device during the open) equal Python's sorted() of the restated
+    index's keys with the same positions; Hash / List / Set entries equal
+    sorted() of their (key, sub) pairs."""
+    from couloydb_amd import _abi
+    from .test_reference_restart import write_dir
+    files = split_files(typed_corpus(501, n_ops=1500, n_keys=20), 3, random.Random(6))
+    write_dir(tmp_path, files)
+    arrays, tts, _ = oracle_scan(files)
+    ix = {}
+    index_states(arrays, tts, out_index=ix)
+    with scanner.open_db(str(tmp_path)) as db:
+        for kind, dt in ((_abi.IT_STRING, mg.STRING), (_abi.IT_LISTMETA, mg.LISTMETA)):
+            got = [(e[0], (e[2].fid, e[2].offset)) for e in db.entries(kind)]
+            want = sorted((ik[1], (v[1], v[2])) for ik, v in ix.items() if ik[0] == dt)
+            assert got == want, kind
+        for kind, dt in ((_abi.IT_HASH, mg.HASH), (_abi.IT_LIST, mg.LIST), (_abi.IT_SET, mg.SET)):
+            got = [(e[0], e[1], (e[2].fid, e[2].offset)) for e in db.entries(kind)]
+            want = sorted((ik[1], ik[2], (v[1], v[2])) for ik, v in ix.items() if ik[0] == dt)
+            assert got == want, kind
+
+
+@pytest.mark.gpu
+def test_gpu_string_order_long_keys(scanner, tmp_path):
+    """The device key sort's refinement rounds: keys of 0-40 bytes sharing
+    long prefixes (15-byte round-0 window, then 7-byte rounds), keys that are
+    prefixes of others, zero bytes at the window edges, a txId-prefixed
+    committed write and overwrites/deletes; the String enumeration equals
+    sorted() of the live keys, every position the last writer's."""
+    from couloydb_amd import _abi
+    from .test_reference_restart import write_dir
+    rng = random.Random(11)
+    stems = [b"", b"user:profile:00", b"user:profile:00\x00", b"user:profile:0000000:",
+             b"a" * 22, b"a" * 23, b"\x00" * 16, b"zz"]
+    keys = set()
+    while len(keys) < 3000:
+        st = rng.choice(stems)
+        tail = bytes(rng.choice(b"\x00\x01ab\xff") for _ in range(rng.randrange(0, 20)))
+        k = (st + tail)[:rng.choice([40, 15, 16, 22, 23, 29, 30, 40])]
+        if k:
+            keys.add(k)
+    keys = sorted(keys)
+    rng.shuffle(keys)
+    b = bytearray()
+    live = {}
+    for r, k in enumerate(keys + keys[:500]):
+        if r % 7 == 3:
+            b += mg.encode_record(mg.key_tx(k, 0), b"", mg.DELETED)
+            live.pop(k, None)
+        else:
+            live[k] = len(b)
+            b += mg.encode_record(mg.key_tx(k, 0), b"v%d" % r)
+    tx = 9
+    k = b"user:profile:00\x00\x00\x00\x00\x00\x00\x00\x00tx"
+    off = len(b)
+    b += mg.encode_record(mg.key_tx(k, tx), b"t")
+    b += mg.encode_record(mg.key_tx(mg.TX_COMMIT_KEY, tx), b"", mg.TXN_COMMIT)
+    live[k] = off
+    write_dir(tmp_path, [bytes(b)])
+    with scanner.open_db(str(tmp_path)) as db:
+        got = [(e[0], e[2].offset) for e in db.entries(_abi.IT_STRING)]
+        assert got == sorted(live.items())
+        assert db.stats.order_rounds >= 2
