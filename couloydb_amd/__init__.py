@@ -329,12 +329,13 @@ class Scanner:
         sweep's tombstones to the active file on disk, as db.Del does."""
         return LoadedDB(self, path, data_file_size, apply_sweep)
 
-    KERNELS = ("k_scan", "link", "k_emit", "k_fin", "k_ovf", "all")
+    KERNELS = ("k_scan", "link", "k_emit", "k_fin", "retry", "all")
 
     def kernel_ms(self):
         """Per-kernel HIP-event times (ms) of the last scan_device call: k_scan,
         the link rounds (k_link, the device repair round, host-driven repairs), k_emit, k_fin,
-        k_ovf, all."""
+        the attempts run again with a larger spill pool (0 unless a tile held more than CAP_T
+        records and the pool was short), all."""
         k = (ctypes.c_double * 6)()
         self.lib.cly_dbg_kernel_ms(self.ctx, k)
         return dict(zip(self.KERNELS, list(k)))

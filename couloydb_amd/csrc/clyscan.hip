@@ -29,17 +29,15 @@
 //            tiles whose guess the state contradicts are listed;
 //   k_refix  (only for listed tiles) re-runs the tile body from the true entry,
 //            then k_link again;
-//   k_emit   per tile: the 48-B tuples from the compact entries (tiles with
-//            more records than the compact list holds re-run the body and
-//            write tuples directly); a scan of the segment registers gives
+//   k_emit   per tile: the 48-B tuples from the compact entries (a tile of
+//            more than CAP_T records keeps the rest in spill chunks taken
+//            from a per-call pool); a scan of the segment registers gives
 //            the stream register at every segment start, from which every
 //            record that ends inside the tile is checked against its own
 //            stored CRC (data/dataFile.go:105-109);
 //   k_fin    per file: a segmented scan of the tiles' exit registers gives the
 //            register entering every tile; the record that crosses into a
-//            tile is checked there;
-//   k_ovf    (only for tiles whose compact list overflowed) checks those
-//            tiles' records one by one.
+//            tile is checked there.
 // Every record is checked on its own, so a file fails exactly at the first
 // record whose CRC differs, as ReadLogRecord's loop does.
 #include <hip/hip_runtime.h>
@@ -49,6 +47,7 @@
 #include <string.h>
 #include <time.h>
 
+#include <algorithm>
 #include <atomic>
 #include <thread>
 
@@ -74,7 +73,18 @@ __device__ __forceinline__ rsrc_t mk_rsrc(const void* p, uint32_t bytes) {
 #define LM_CHAIN 1               // the chain enters the segment at E (a record start or its terminal)
 #define LM_DEAD 2                // the file's chain ended before the segment
 #define LM_OFF 3                 // segment beyond the end of the file
-#define CAP_T ((uint32_t)(CLY_TILE / 128))   // compact entries kept per tile (more: k_ovf re-walks)
+#define CAP_T ((uint32_t)(CLY_TILE / 128))   // compact entries in a tile's own area (more: spill chunks)
+#define CAP_SHIFT (__builtin_ctz(CAP_T))
+// Spill: records CAP_T.. of a tile go to chunks of CAP_T entries (and their
+// snapshots) taken from a per-call pool; a tile's chunk table holds up to
+// NCH_MAX chunk ids and, in word CH_NWORD, how many it took.  Records are at
+// least 9 bytes (header of 4 + 1 + 1 + three 1-byte varints) except at a
+// file's end, so a tile holds at most CLY_TILE / 9 + 1 <= (NCH_MAX + 1) CAP_T.
+#define NCH_MAX 14
+#define CH_WORDS 16
+#define CH_NWORD 15
+static_assert((NCH_MAX + 1) * (CLY_TILE / 128) >= CLY_TILE / 9 + 1, "spill chunks per tile");
+static_assert((CAP_T & (CAP_T - 1)) == 0 && CAP_T >= 64, "CAP_T: a power of two, >= a round of 64 records");
 
 struct DevFile {                 // 32 B
     const uint8_t* base;         // device pointer to the file's first byte (16-B aligned)
@@ -109,7 +119,6 @@ struct TileLocal { u64 l[4]; };
 #define DF_NONE 4ull
 #define DF_FOF 8ull
 #define DF_REC 16ull
-#define DF_OVF 32ull
 
 struct Globals {                 // zeroed per call
     uint32_t nfix[2];            // tiles listed by a k_link round (slot r & 1) for the next k_refix
@@ -118,7 +127,10 @@ struct Globals {                 // zeroed per call
     uint32_t fail;               // internal invariant (never expected)
     uint32_t refix;              // tiles re-resolved over all rounds
     uint32_t rounds;             // link rounds
-    uint32_t n_ovf;              // tiles listed by k_emit for k_ovf (compact list overflowed)
+    uint32_t spill_next;         // spill chunks taken
+    uint32_t spill_cap;          // spill chunks in the pool (set by the host)
+    uint32_t spill_over;         // a chunk was refused (the host grows the pool and runs the call again)
+    uint32_t _g0;
     uint64_t total;              // records over all files
 };
 
@@ -139,7 +151,7 @@ struct Globals {                 // zeroed per call
 #define EM_RUN 19                 // A^(RUN_BYTES 2^l): table 19 + l
 #define NEM 25
 #define NTAB_ALL (TAB_EM + NEM * 128)
-// LDS of k_scan / k_refix / k_ovf (static: compile-time offsets)
+// LDS of k_scan / k_refix (static: compile-time offsets)
 //   [0, 65536)  CRC slicing-by-4 tables T0..T3, 16 replicas: dword (i*64 + t*16 + r)
 //   LDS_INV     inverse of a zero-byte step (top byte of T0 -> index), 256 B
 #define LDS_INV 65536
@@ -514,14 +526,6 @@ __device__ __forceinline__ void tuple_words(gbytes base, uint32_t p, const Hdr& 
                     ((uint32_t)(tn < 0 ? 0xFF : tn) << 24),
                 h.crc};
 }
-__device__ __forceinline__ void put_tuple(gtuples out, uint64_t idx, uint64_t out_cap, gbytes base, uint32_t p,
-                                          const Hdr& h, uint32_t fid, Globals* g) {
-    u32x4 a, b, c;
-    tuple_words(base, p, h, fid, a, b, c);
-    if (idx >= out_cap) { atomicOr(&g->overflow, 1u); return; }
-    CLY_GL u32x4* dst = (CLY_GL u32x4*)(out + idx);
-    dst[0] = a; dst[1] = b; dst[2] = c;
-}
 // Compact entry (16 B), k_scan -> k_emit.  Short form (bit 26 of w3; every
 // record the writer produces without a TTL or a txId >= 64): w0 crc,
 // w1 ks (24 bits) | hsz-6 << 24 | type << 29, w2 vs, w3 rel | dt << 16 |
@@ -532,12 +536,27 @@ __device__ __forceinline__ void put_tuple(gtuples out, uint64_t idx, uint64_t ou
 // as they are made (an LDS sink flushed at the next block's top, after its
 // loads, measured 1.6 % slower on C2 and 3.3 % on C4), and the file record
 // checks of k_ovf's re-walk
-struct RecSink { rsrc_t trs, nrs; FileInfo* fo; };
+struct RecSink {
+    rsrc_t trs, nrs;             // the tile's own entries and snapshots
+    CLY_GL u32x4* sp_rec;        // the spill pool: entries, snapshots (chunk c at c CAP_T)
+    CLY_GL uint32_t* sp_snap;
+    CLY_LDS uint32_t* chk;       // the wave's copy of the tile's chunk ids
+    uint32_t* ctab;              // the tile's chunk table (CH_WORDS words)
+    Globals* g;
+};
 __device__ __forceinline__ void rec_put(const RecSink& rs, uint32_t idx, const u32x4& v) {
     if (idx < CAP_T) __builtin_amdgcn_raw_buffer_store_b128(v, rs.trs, (int)(idx * 16u), 0, 0);
+    else {
+        const uint32_t c = rs.chk[(idx >> CAP_SHIFT) - 1u];
+        if (c != NONE32) rs.sp_rec[(uint64_t)c * CAP_T + (idx & (CAP_T - 1u))] = v;
+    }
 }
 __device__ __forceinline__ void snap_put(const RecSink& rs, uint32_t r, uint32_t v) {
-    __builtin_amdgcn_raw_buffer_store_b32(v, rs.nrs, (int)(r * 4u), 0, 0);
+    if (r < CAP_T) __builtin_amdgcn_raw_buffer_store_b32(v, rs.nrs, (int)(r * 4u), 0, 0);
+    else {
+        const uint32_t c = rs.chk[(r >> CAP_SHIFT) - 1u];
+        if (c != NONE32) rs.sp_snap[(uint64_t)c * CAP_T + (r & (CAP_T - 1u))] = v;
+    }
 }
 __device__ __forceinline__ void rec_store(const RecSink& rs, uint32_t idx, const Hdr& h, uint32_t rel) {
     const bool sh = h.exp == 0 && h.key0 < 0x80u && h.ks >= 1u && h.ks < (1u << 24) && h.type < 8u && h.dt < 8u &&
@@ -614,16 +633,14 @@ __device__ __forceinline__ void patch_word(uint32_t (&w)[16], uint32_t k, uint32
 }
 
 // ---------------------------------------------------------------------------
-// The tile body (k_scan, k_refix, k_ovf's re-walk).  The wave streams the
+// The tile body (k_scan, k_refix).  The wave streams the
 // tile's blocks in order; the chain position X is carried from block to block.
 //   BM_SPEC   k_scan: the entry of a tile other than its file's first is
 //             unknown; the first block with a plausible record start sets the
 //             tile's guess G (a candidate whose speculative walk holds and
 //             leaves at a candidate, or at a plausible header beyond the block);
-//   BM_EXACT  k_refix: the entry is the true state from k_link;
-//   BM_EMIT   k_ovf: as BM_EXACT, tuples straight to their output slots (tiles
-//             whose compact list overflowed), each record's CRC checked alone.
-// CRC (not BM_EMIT): GetLogRecordCRC of the record at P is the CRC-32 of
+//   BM_EXACT  k_refix: the entry is the true state from k_link.
+// CRC: GetLogRecordCRC of the record at P is the CRC-32 of
 // F[P+4 : P+size] (data/logRecord.go:136-146).  In the CRC register's terms
 // the stream from P on, started from the register c ^ K4 (c = the stored CRC
 // at P, K4 = A^-4 0xFFFFFFFF), holds 0xFFFFFFFF after the 4 stored bytes and
@@ -642,7 +659,6 @@ __device__ __forceinline__ void patch_word(uint32_t (&w)[16], uint32_t k, uint32
 // completes it).
 #define BM_SPEC 0
 #define BM_EXACT 1
-#define BM_EMIT 2
 #define PW_ROUNDS 1              // pred_walk rounds per block before the general pass (C3: 1 round 12.7 ms, 2 13.6, 4 15.4)
 // Per-tile CRC outputs of the tile body: the segment registers (one per 64-B
 // segment of the tile, stream order) and the records' snapshots (indexed like
@@ -666,34 +682,18 @@ struct TState {
     // stride reference (stride_round): header bytes 4..15 of the last record
     // (ref1..3) under the masks of its bytes 4..hsz, and the uniform words of
     // its compact entry; valid while ref_ok
+    uint32_t nch;                // spill chunks the records so far need
+    uint32_t nch_have;           // chunks the tile holds (k_refix reuses k_scan's)
     bool ref_ok;
     uint32_t ref_s;              // the reference record's size (the stride)
     uint32_t ref1, ref2, ref3, msk1, msk2, msk3, rw1, rw2, rw3;
 };
-// k_ovf's record check: the CRC-32 of F[P+4 : P+size], byte-serial in the lane
-__device__ __forceinline__ void rec_crc_check(const CLY_LDS uint8_t* smem, const CrcLane& cl, gbytes base, uint32_t p,
-                                              const Hdr& h, FileInfo* fo, uint64_t gidx) {
-    uint64_t a = (uint64_t)p + 4, b = (uint64_t)p + h.size;
-    uint32_t s = 0xFFFFFFFFu;
-    for (; a < b && (a & 3); a++) s = crc_byte(smem, s, base[a], cl.r4);
-    for (; a + 4 <= b; a += 4) s = crc_word(smem, s ^ *(const CLY_GL uint32_t*)(base + a), cl);
-    for (; a < b; a++) s = crc_byte(smem, s, base[a], cl.r4);
-    if (~s != h.crc) atomicMin(&fo->fail_key, ((u64)p << 32) | (u64)(gidx - fo->first_index));
-}
-// The block's outputs for record k of a round (lane k): its compact entry
-// (k_scan, k_refix), or its tuple and CRC check (k_ovf's re-walk).  Returns
-// the record's patch word as an index in the block: the word whose entering
-// register its CRC check reads (P's own word when P is word-aligned, else the
-// word after it; PW_CARRY: the next block's first word).
-template <int BM>
-__device__ __forceinline__ uint32_t rec_out(const DevFile& F, gbytes base, uint32_t p, const Hdr& h, uint32_t idx,
-                                            uint32_t tb, uint32_t bs, const RecSink& rs, gtuples out, uint64_t out_cap,
-                                            uint64_t gbase, Globals* g, const CLY_LDS uint8_t* smem, const CrcLane& cl) {
-    if (BM == BM_EMIT) {
-        put_tuple(out, gbase + idx, out_cap, base, p, h, F.fid, g);
-        rec_crc_check(smem, cl, base, p, h, rs.fo, gbase + idx);
-        return 0u;
-    }
+// The block's outputs for record k of a round (lane k): its compact entry.
+// Returns the record's patch word as an index in the block: the word whose
+// entering register its CRC check reads (P's own word when P is word-aligned,
+// else the word after it; PW_CARRY: the next block's first word).
+__device__ __forceinline__ uint32_t rec_out(uint32_t p, const Hdr& h, uint32_t idx, uint32_t tb, uint32_t bs,
+                                            const RecSink& rs) {
     rec_store(rs, idx, h, p - tb);
     return ((p - bs) >> 2) + ((p & 3u) ? 1u : 0u);
 }
@@ -712,9 +712,31 @@ template <int BM>
 __device__ __forceinline__ void term_patch(TState& S, uint32_t T, uint32_t dT, uint32_t bs, const CLY_LDS uint8_t* smem,
                                            const CrcLane& cl, int src) {
     S.Tb = T;
-    if (BM == BM_EMIT) return;
     if (T < bs + CLY_BLK) S.tpatch = rdl(crc_unbytes(smem, dT, T & 3u, cl.r4), src);
     else S.carry_next ^= rdl(dT, src);
+}
+
+// The spill chunks for record indices < hi (wave-uniform): a chunk the tile
+// does not hold yet comes from the pool (lane 0); a refused one (pool full)
+// is NONE32 and the call is run again with a larger pool.
+__device__ __forceinline__ void spill_ensure(TState& S, uint32_t hi, const RecSink& rs, int lane) {
+    if (hi <= (S.nch + 1u) * CAP_T) return;
+    while (hi > (S.nch + 1u) * CAP_T) {
+        if (S.nch >= S.nch_have) {
+            if (lane == 0) {
+                uint32_t id = NONE32;
+                if (S.nch < NCH_MAX) {
+                    id = atomicAdd(&rs.g->spill_next, 1u);
+                    if (id >= rs.g->spill_cap) { atomicOr(&rs.g->spill_over, 1u); id = NONE32; }
+                } else atomicOr(&rs.g->fail, 128u);                  // (records >= 9 B: never)
+                if (S.nch < NCH_MAX) { rs.chk[S.nch] = id; rs.ctab[S.nch] = id; }
+            }
+            S.nch_have = S.nch + 1u;
+        }
+        S.nch++;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Exact predictive walk (entry X known and in this block): lane k decodes the
@@ -728,9 +750,7 @@ __device__ __forceinline__ void term_patch(TState& S, uint32_t T, uint32_t dT, u
 template <int BM>
 __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t tb, uint32_t bs, CLY_LDS uint32_t* stg,
                                           const CLY_LDS uint8_t* smem, const CrcLane& cl, uint32_t K4, const RecSink& rs,
-                                          gtuples out, uint64_t out_cap, uint64_t gbase, Globals* g, int lane,
-                                          CLY_LDS uint32_t* mk) {
-    const gbytes base = (gbytes)F.base;
+                                          int lane, CLY_LDS uint32_t* mk) {
     const uint64_t flen = F.len, bend = (uint64_t)bs + CLY_BLK;
     for (int round = 0; round < PW_ROUNDS; round++) {
         const uint64_t X = S.X;
@@ -758,11 +778,12 @@ __device__ __forceinline__ bool pred_walk(const DevFile& F, TState& S, uint32_t 
         const uint32_t up = dppu<DPP_WF_SR1>(0u, h.crc);
         const uint32_t dq = k == 0 ? (S.cq_known ? ~S.cq : 0xFFFFFFFFu) : ~up;
         uint32_t pw = 0;
+        spill_ensure(S, S.tcnt + (uint32_t)n, rs, lane);
         if (acc) {
-            pw = rec_out<BM>(F, base, (uint32_t)P, h, S.tcnt + k, tb, bs, rs, out, out_cap, gbase, g, smem, cl);
-            if (BM != BM_EMIT && pw < PW_CARRY) mark_pw(mk, pw);
+            pw = rec_out((uint32_t)P, h, S.tcnt + k, tb, bs, rs);
+            if (pw < PW_CARRY) mark_pw(mk, pw);
         }
-        if (BM != BM_EMIT && __ballot(acc && pw == PW_CARRY)) S.cmark_next = true;
+        if (__ballot(acc && pw == PW_CARRY)) S.cmark_next = true;
         if (S.G == NONE32) S.G = (uint32_t)X;
         if (n) {
             const int kl = n - 1;
@@ -816,6 +837,7 @@ __device__ __forceinline__ void stride_round(const DevFile& F, TState& S, uint32
     const uint32_t kb = bm ? (uint32_t)__ffsll((long long)bm) - 1 : 64u;
     if (kb == 0) return;
     uint32_t pw = 0;
+    spill_ensure(S, S.tcnt + kb, rs, lane);
     if (k < kb) {
         rec_put(rs, S.tcnt + k, (u32x4){crc, S.rw1, S.rw2, (P - tb) | S.rw3});
         pw = ((P - bs) >> 2) + ((P & 3u) ? 1u : 0u);
@@ -952,9 +974,10 @@ template <int BM>
 __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint32_t tt, uint32_t X_in, bool dead_in,
                                              const CLY_LDS uint8_t* smem, CLY_LDS uint32_t* stg, CLY_LDS uint32_t* mk,
                                              const CrcLane& cl, uint32_t K4, TileLocal* loc,
-                                             uint32_t* rec, uint32_t* seg, uint32_t* snap, uint32_t* treg, gtuples out,
-                                             uint64_t out_cap, uint64_t gbase, Globals* g, FileInfo* fo,
-                                             u32x4 (&e)[4], u32x4& hl, const uint8_t* nbase, uint32_t nlen, uint32_t ntb) {
+                                             uint32_t* rec, uint32_t* seg, uint32_t* snap, uint32_t* treg,
+                                             CLY_LDS uint32_t* chk, uint32_t* chunks, u32x4* sp_rec, uint32_t* sp_snap,
+                                             Globals* g, u32x4 (&e)[4], u32x4& hl, const uint8_t* nbase, uint32_t nlen,
+                                             uint32_t ntb) {
     const int lane = threadIdx.x & 63;
     const uint32_t tb = (uint32_t)((uint64_t)tt * CLY_TILE);
     const uint64_t flen = F.len;
@@ -967,15 +990,25 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     S.cq = 0; S.G = NONE32; S.tcnt = 0; S.last_crc = 0; S.P_last = NONE32; S.term = TERM_NONE;
     S.s_last = 0; S.s_prev = 0; S.Tb = NONE32; S.tpatch = 0; S.carry_next = 0; S.cmark_next = false;
     S.ref_ok = false; S.ref_s = 0; S.ref1 = S.ref2 = S.ref3 = S.msk1 = S.msk2 = S.msk3 = S.rw1 = S.rw2 = S.rw3 = 0;
+    uint32_t* ctab = chunks + (uint64_t)t * CH_WORDS;
+    S.nch = 0;
+    // k_scan starts the tile's chunk list; k_refix reuses the chunks k_scan took
+    S.nch_have = BM == BM_SPEC ? 0u : __builtin_amdgcn_readfirstlane(ctab[CH_NWORD]);
+    if (BM != BM_SPEC) {
+        if ((uint32_t)lane < S.nch_have) chk[lane] = ctab[lane];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     uint32_t carry = 0;          // register XOR due at this block's first byte
     bool cmark = false;          // ... a record start's patch (marked as word 0 of the block)
     uint32_t nb = 0;             // snapshots taken so far (= records whose patch word was passed)
     const rsrc_t trs = mk_rsrc(rec + (uint64_t)t * CAP_T * 4, CAP_T * 16u);      // the tile's compact entries
     const rsrc_t frs = mk_rsrc(F.base, (uint32_t)flen);
-    const rsrc_t srs = mk_rsrc(seg + (uint64_t)t * NSEG, BM == BM_EMIT ? 0u : NSEG * 4u);            // segment registers
-    const rsrc_t nrs = mk_rsrc(snap + (uint64_t)t * SNAP_T, BM == BM_EMIT ? 0u : (CAP_T + 1) * 4u);  // snapshots
+    const rsrc_t srs = mk_rsrc(seg + (uint64_t)t * NSEG, NSEG * 4u);           // segment registers
+    const rsrc_t nrs = mk_rsrc(snap + (uint64_t)t * SNAP_T, CAP_T * 4u);       // snapshots
     RecSink rs;
-    rs.trs = trs; rs.nrs = nrs; rs.fo = fo;
+    rs.trs = trs; rs.nrs = nrs; rs.sp_rec = (CLY_GL u32x4*)sp_rec; rs.sp_snap = (CLY_GL uint32_t*)sp_snap;
+    rs.chk = chk; rs.ctab = ctab; rs.g = g;
     uint32_t Rp = 0;             // the previous block's segment register (stored at the next block's top)
     CLY_LDS u32x4* sv = (CLY_LDS u32x4*)stg;
     #pragma unroll 1
@@ -987,19 +1020,16 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
         #pragma unroll
         for (int k = 0; k < 4; k++) { w[4 * k] = e[k].x; w[4 * k + 1] = e[k].y; w[4 * k + 2] = e[k].z; w[4 * k + 3] = e[k].w; }
         const u32x4 hc = hl;
-        if (BM != BM_EMIT) {
-            // the previous block's outputs, now that this block's loads are in
-            if (m > 0)
-                __builtin_amdgcn_raw_buffer_store_b32(Rp, srs, (int)(((uint32_t)(m - 1) * CLY_NL + (uint32_t)lane) * 4u), 0, 0);
-        }
-        if (m + 1 < CLY_NBLK && (BM != BM_EMIT || !S.dead)) blk_issue(base, frs, flen, bs + CLY_BLK, lane, e, hl);
+        // the previous block's outputs, now that this block's loads are in
+        if (m > 0)
+            __builtin_amdgcn_raw_buffer_store_b32(Rp, srs, (int)(((uint32_t)(m - 1) * CLY_NL + (uint32_t)lane) * 4u), 0, 0);
+        if (m + 1 < CLY_NBLK) blk_issue(base, frs, flen, bs + CLY_BLK, lane, e, hl);
         else if (m + 1 == CLY_NBLK && nbase) {                                 // the wave's next tile
             uint32_t nl = nlen, nt = ntb;
             asm volatile("" : "+s"(nl), "+s"(nt));     // (keeps its tail masks from being hoisted out of the loop)
             blk_issue((gbytes)nbase, mk_rsrc(nbase, nl), nl, nt, lane, e, hl);
         }
-        if (BM == BM_EMIT && S.dead) break;
-        if (BM != BM_EMIT) mk[lane] = (lane == 0 && cmark) ? 1u : 0u;       // the block's patch words (carried: word 0)
+        mk[lane] = (lane == 0 && cmark) ? 1u : 0u;       // the block's patch words (carried: word 0)
         S.Tb = NONE32;
         const bool owned = S.X != NONE32 && ((uint64_t)S.X < bend || ((uint64_t)S.X == flen && flen == bend));
         if (S.dead) {
@@ -1027,10 +1057,10 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
             if (S.X == NONE32) S.X = guess_entry(F, bs, stg, hc, lane);    // the tile's guessed entry
             bool done = true;
             if (S.X != NONE32) {
-                if (BM != BM_EMIT && S.ref_ok) stride_round<BM>(F, S, tb, bs, stg, smem, cl, K4, rs, lane, mk);
+                if (S.ref_ok) stride_round<BM>(F, S, tb, bs, stg, smem, cl, K4, rs, lane, mk);
                 const uint32_t c0 = S.tcnt;
-                done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, rs, out, out_cap, gbase, g, lane, mk);
-                if (BM != BM_EMIT && S.tcnt != c0) stride_ref(F, S, bs, stg);
+                done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, rs, lane, mk);
+                if (S.tcnt != c0) stride_ref(F, S, bs, stg);
             }
             if (!done) {
                 // ---- general pass (the predictive walk's round budget ran out):
@@ -1078,18 +1108,18 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                     // the lane's records: outputs and patch-word marks (headers from the stage)
                     uint32_t p = L.E, psz = 0, ppsz = 0;
                     bool cf = false;
+                    spill_ensure(S, S.tcnt + bcnt, rs, lane);
                     for (uint32_t i = 0; __ballot(i < c); i++) {
                         if (i < c) {
                             const Hdr h = hdr_get(p, flen, stg, bs);
-                            const uint32_t pw = rec_out<BM>(F, base, p, h, S.tcnt + lex + i, tb, bs, rs, out,
-                                                            out_cap, gbase, g, smem, cl);
-                            if (BM != BM_EMIT) { if (pw == PW_CARRY) cf = true; else mark_pw(mk, pw); }
+                            const uint32_t pw = rec_out(p, h, S.tcnt + lex + i, tb, bs, rs);
+                            if (pw == PW_CARRY) cf = true; else mark_pw(mk, pw);
                             pcq = h.crc; pk = true;
                             ppsz = psz; psz = (uint32_t)h.size;
                             p += (uint32_t)h.size;
                         }
                     }
-                    if (BM != BM_EMIT && __ballot(cf)) S.cmark_next = true;
+                    if (__ballot(cf)) S.cmark_next = true;
                     if (kT < 64) {
                         const uint32_t T = rdl(L.x, kT);
                         const uint32_t dT = T == 0 ? 0u : (pk ? ~pcq : 0xFFFFFFFFu);
@@ -1117,7 +1147,7 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                 }
             }
         }
-        if (BM != BM_EMIT) {
+        {
             // bytes from the terminal on read as zero
             if (S.Tb != NONE32) {
                 const uint32_t cb = bs + 64u * (uint32_t)lane, T = S.Tb;
@@ -1167,14 +1197,13 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     }
     TileRes res;
     res.X = S.X; res.dead = S.dead;
-    if (BM != BM_EMIT) {
-        __builtin_amdgcn_raw_buffer_store_b32(Rp, srs, (int)(((uint32_t)(CLY_NBLK - 1) * CLY_NL + (uint32_t)lane) * 4u), 0, 0);
-    }
-    if (BM != BM_EMIT && lane == 0) {
-        // a record start whose patch word is the tile's end: its snapshot is
-        // the (empty) segment after the tile's, zero; the patch itself is the
-        // register XOR due at the tile end
-        if (cmark) __builtin_amdgcn_raw_buffer_store_b32(0u, nrs, (int)(nb * 4u), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(Rp, srs, (int)(((uint32_t)(CLY_NBLK - 1) * CLY_NL + (uint32_t)lane) * 4u), 0, 0);
+    // a record start whose patch word is the tile's end: its snapshot is
+    // the (empty) segment after the tile's, zero; the patch itself is the
+    // register XOR due at the tile end
+    if (cmark && lane == 0) snap_put(rs, nb, 0u);
+    if (lane == 0) {
+        ctab[CH_NWORD] = S.nch_have;
         treg[2 * t] = carry;
         if (nb + (cmark ? 1u : 0u) != S.tcnt) atomicOr(&g->fail, 64u);      // one snapshot per record
         const uint64_t tstart = tb;
@@ -1184,7 +1213,6 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
         if (S.G == NONE32) f0 |= DF_NONE;
         if (tt == 0) f0 |= DF_FOF;
         if (S.P_last != NONE32) f0 |= DF_REC;
-        if (S.tcnt > CAP_T) f0 |= DF_OVF;
         TileLocal* d = &loc[t];
         d->l[0] = f0;
         d->l[1] = (u64)S.G | ((u64)S.X << 32);
@@ -1217,7 +1245,8 @@ __device__ __forceinline__ uint32_t k4_const(const CLY_LDS uint8_t* smem, uint32
 // k_scan: one wave per tile (grid-stride), every byte of every file read once.
 #define SCAN_WAVES 16
 #define MK_BYTES (CLY_NL * 4)                                 // a wave's patch-word mask
-#define SCAN_LDS_ALL (SCAN_LDS + SCAN_WAVES * (STG_BYTES + MK_BYTES))   // tables + per wave a block stage and a mask
+#define CHK_BYTES (CH_WORDS * 4)                              // a wave's copy of its tile's spill chunk ids
+#define SCAN_LDS_ALL (SCAN_LDS + SCAN_WAVES * (STG_BYTES + MK_BYTES + CHK_BYTES))   // tables + per wave a stage, a mask, chunk ids
 static_assert(SCAN_LDS_ALL <= 160 * 1024, "k_scan's LDS");
 __device__ __forceinline__ CLY_LDS uint32_t* wave_stage(CLY_LDS uint8_t* smem) {
     return (CLY_LDS uint32_t*)(smem + SCAN_LDS + wave_id() * STG_BYTES);
@@ -1225,14 +1254,19 @@ __device__ __forceinline__ CLY_LDS uint32_t* wave_stage(CLY_LDS uint8_t* smem) {
 __device__ __forceinline__ CLY_LDS uint32_t* wave_mask(CLY_LDS uint8_t* smem) {
     return (CLY_LDS uint32_t*)(smem + SCAN_LDS + SCAN_WAVES * STG_BYTES + wave_id() * MK_BYTES);
 }
+__device__ __forceinline__ CLY_LDS uint32_t* wave_chk(CLY_LDS uint8_t* smem) {
+    return (CLY_LDS uint32_t*)(smem + SCAN_LDS + SCAN_WAVES * (STG_BYTES + MK_BYTES) + wave_id() * CHK_BYTES);
+}
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
 k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
-       TileLocal* loc, uint32_t* rec, uint32_t* seg, uint32_t* snap, uint32_t* treg, Globals* g) {
+       TileLocal* loc, uint32_t* rec, uint32_t* seg, uint32_t* snap, uint32_t* treg, uint32_t* chunks, u32x4* sp_rec,
+       uint32_t* sp_snap, Globals* g) {
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS_ALL];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
     init_tables(smem);
     CLY_LDS uint32_t* stg = wave_stage(smem);
     CLY_LDS uint32_t* mk = wave_mask(smem);
+    CLY_LDS uint32_t* chk = wave_chk(smem);
     const int lane = threadIdx.x & 63;
     const CrcLane cl = crc_lane(lane);
     const uint32_t K4 = k4_const(smem, cl.r4);
@@ -1255,8 +1289,8 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             ntb = (tn - files[fn].first_tile) * (uint32_t)CLY_TILE;
         }
         const DevFile F = files[f];
-        tile_body<BM_SPEC>(F, t, t - F.first_tile, 0u, false, smem, stg, mk, cl, K4, loc, rec, seg, snap,
-                           treg, nullptr, 0, 0, g, nullptr, e, hl, nbase, nlen, ntb);
+        tile_body<BM_SPEC>(F, t, t - F.first_tile, 0u, false, smem, stg, mk, cl, K4, loc, rec, seg, snap, treg, chk,
+                           chunks, sp_rec, sp_snap, g, e, hl, nbase, nlen, ntb);
         if (fn < 0) break;
         t = tn; f = fn;
     }
@@ -1441,13 +1475,14 @@ k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restric
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
 k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, TileLocal* loc,
         const TileIn* __restrict__ tin, uint32_t* rec, uint32_t* seg, uint32_t* snap, uint32_t* treg,
-        const uint32_t* __restrict__ fixlist, Globals* g, int slot) {
+        uint32_t* chunks, u32x4* sp_rec, uint32_t* sp_snap, const uint32_t* __restrict__ fixlist, Globals* g, int slot) {
     if (g->nfix[slot] == 0) return;                        // (uniform: before the LDS setup's barrier)
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS_ALL];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
     init_tables(smem);
     CLY_LDS uint32_t* stg = wave_stage(smem);
     CLY_LDS uint32_t* mk = wave_mask(smem);
+    CLY_LDS uint32_t* chk = wave_chk(smem);
     const uint32_t k = blockIdx.x * SCAN_WAVES + wave_id();
     if (k >= g->nfix[slot]) return;
     const int lane = threadIdx.x & 63;
@@ -1471,7 +1506,7 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
         const u64 l0 = loc[t].l[0], l1 = loc[t].l[1];
         const uint32_t n = (uint32_t)(l0 >> 32), tb = (t - F.first_tile) * (uint32_t)CLY_TILE;
         bool shortcut = false;
-        if (!dead && !(l0 & (DF_NONE | DF_FOF | DF_OVF)) && n > 1 && ((loc[t].l[3] >> 40) & 0xFFFFu) == 0) {
+        if (!dead && !(l0 & (DF_NONE | DF_FOF)) && n > 1 && ((loc[t].l[3] >> 40) & 0xFFFFu) == 0) {
             const uint32_t nn = n < 64u ? n : 64u;
             const uint32_t rel = (uint32_t)lane < nn ? (rec[((uint64_t)t * CAP_T + lane) * 4 + 3] & 0xFFFFu) : 0u;
             const u64 bm = __ballot(lane >= 1 && (uint32_t)lane < nn && tb + rel == X);
@@ -1490,9 +1525,9 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
         if (!shortcut) {
             u32x4 e[4], hl;
             tile_issue(F, t - F.first_tile, lane, e, hl);
-            const TileRes r = tile_body<BM_EXACT>(F, t, t - F.first_tile, X, dead, smem, stg, mk, cl,
-                                                  K4, loc, rec, seg, snap, treg, nullptr, 0, 0, g, nullptr, e, hl,
-                                                  nullptr, 0u, 0u);
+            const TileRes r = tile_body<BM_EXACT>(F, t, t - F.first_tile, X, dead, smem, stg, mk, cl, K4, loc, rec,
+                                                  seg, snap, treg, chk, chunks, sp_rec, sp_snap, g, e, hl, nullptr,
+                                                  0u, 0u);
             X = r.X; dead = r.dead;
         }
         if (dead || t + 1 >= F.first_tile + F.ntile) break;
@@ -1526,9 +1561,8 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
 //   there).  The record that crosses into the tile is k_fin's, which knows the
 //   register entering the tile: the tile gives it its own register entering
 //   its first patch word (dev, with exp_pre folded in).
-//   Tiles of long records (one spanning more than SHORT_KMAX segments), of many
-//   short ones, without a record start, or whose compact list overflowed take
-//   the tile-wide scan instead: every segment whose last boundary is a record
+//   Tiles of long records (one spanning more than SHORT_KMAX segments) or
+//   without a record start take the tile-wide scan instead: every segment whose last boundary is a record
 //   start gets its reset exit (a constant), lane L owns the run of RUN
 //   consecutive segments at L RUN_BYTES; a Horner pass gives each run as a
 //   function of the register entering it, a Kogge-Stone scan over the lanes
@@ -1536,12 +1570,10 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
 //   segment (gin), and every record is checked from gin.
 //   Outputs per tile for k_fin: the register at the tile's end (a tile with a
 //   record start: past its last reset; a tile without one: its own, from
-//   zero; a tile whose compact list overflowed: none, k_ovf checks its
-//   records) and dev.
+//   zero) and dev.
 #define RUN (CLY_NBLK)                          // segments per lane in k_emit's scan
 #define RUN_BYTES (RUN * CLY_SEG)
 #define EMIT_WAVES 8
-#define SHORT_MAXN CAP_T                        // records per tile of the per-record path (all a compact list holds)
 #define SHORT_KMAX 32                           // segments one record may span there
 #define GIN_WORDS (NSEG + 4)                    // segment registers / the scan (+ the tile's end)
 #define FLG_BYTES (NSEG / 8)                    // segments that hold a reset (tile-wide scan)
@@ -1590,6 +1622,24 @@ __device__ __forceinline__ uint32_t entry_crc(gbytes base, uint64_t len, uint32_
     return (v.w & REC_SHORT) ? v.x : hdr_load(base, tb + (v.w & 0xFFFFu), len).crc;
 }
 __device__ __forceinline__ uint32_t patch_word_of(uint32_t P) { return (P & 3u) ? (P & ~3u) + 4u : P; }
+// A tile's compact entries and snapshots as k_emit reads them: index i (after
+// k_refix's suffix skip) in the tile's own area below CAP_T, else in its spill
+// chunks
+struct EntSrc {
+    const u32x4* tile; const uint32_t* tsnap;
+    const u32x4* sp_rec; const uint32_t* sp_snap; const uint32_t* ctab;
+    uint32_t skip;
+    __device__ __forceinline__ u32x4 ent(uint32_t i) const {
+        const uint32_t a = i + skip;
+        if (a < CAP_T) return tile[a];
+        return sp_rec[(uint64_t)ctab[(a >> CAP_SHIFT) - 1u] * CAP_T + (a & (CAP_T - 1u))];
+    }
+    __device__ __forceinline__ uint32_t snap(uint32_t i) const {
+        const uint32_t a = i + skip;
+        if (a < CAP_T) return tsnap[a];
+        return sp_snap[(uint64_t)ctab[(a >> CAP_SHIFT) - 1u] * CAP_T + (a & (CAP_T - 1u))];
+    }
+};
 // the fields of record i's check (per-record path): its start's patch word
 // Wr in segment sa with reset value inj; its end W2 in segment sb (kind 1: a
 // record start, expected register expn, snapshot s2; kind 2: the terminal's
@@ -1610,8 +1660,9 @@ __global__ void __launch_bounds__(64 * EMIT_WAVES)
 k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
        const TileIn* __restrict__ tin, const TileLocal* __restrict__ loc, const uint32_t* __restrict__ rec,
        const uint32_t* __restrict__ seg, const uint32_t* __restrict__ snap, uint32_t* treg, FileInfo* finfo,
-       const uint32_t* __restrict__ tabs, cly_tuple* out_, uint64_t out_cap, u32x4* ovf, Globals* g, int slot) {
-    if (g->nfix[slot]) return;              // the chain is not final yet (k_refix first)
+       const uint32_t* __restrict__ tabs, cly_tuple* out_, uint64_t out_cap, const uint32_t* __restrict__ chunks,
+       const u32x4* __restrict__ sp_rec, const uint32_t* __restrict__ sp_snap, Globals* g, int slot) {
+    if (g->nfix[slot] || g->spill_over) return;     // the chain is not final yet (k_refix first) / run again
     gtuples out = (gtuples)out_;
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[EMIT_LDS];
     CLY_LDS uint32_t* emt = (CLY_LDS uint32_t*)smem_raw;
@@ -1642,12 +1693,13 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         const uint32_t n = (uint32_t)(l0 >> 32);
         const uint32_t skip = (uint32_t)(l3 >> 40) & 0xFFFFu;              // k_refix's suffix (records dropped)
         const gbytes base = (gbytes)F.base;
-        const bool none = (l0 & DF_NONE) != 0, term = (l0 & DF_TERM) != 0, ovfl = (l0 & DF_OVF) != 0;
+        const bool none = (l0 & DF_NONE) != 0, term = (l0 & DF_TERM) != 0;
         const bool gterm = !none && term && n == 0;                         // the first boundary is the terminal
         const bool grec = !none && !gterm;                                  // ... a record start
         const uint32_t T = (uint32_t)(l1 >> 32);                            // the terminal (term)
-        const uint32_t* trec = rec + ((uint64_t)t * CAP_T + skip) * 4;
-        const uint32_t* tsnap = snap + (uint64_t)t * SNAP_T + skip;
+        EntSrc E;
+        E.tile = (const u32x4*)(rec + (uint64_t)t * CAP_T * 4); E.tsnap = snap + (uint64_t)t * SNAP_T;
+        E.sp_rec = sp_rec; E.sp_snap = sp_snap; E.ctab = chunks + (uint64_t)t * CH_WORDS; E.skip = skip;
         const uint32_t cout = treg[2 * t];                                  // the register XOR due at the tile's end
         // the tile's segment registers into LDS (lane-transposed: lane L's run)
         uint32_t sr[RUN];
@@ -1672,10 +1724,10 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         if (grec) {
             WG = patch_word_of(G);
             sigG = (WG - tb) >> 6;
-            sG = tsnap[0];
-            if (tt > 0) expG = exp_pre(emt, G & 3u, S.crc_last, entry_crc(base, F.len, tb, *(const u32x4*)trec));
+            sG = E.snap(0);
+            if (tt > 0) expG = exp_pre(emt, G & 3u, S.crc_last, entry_crc(base, F.len, tb, E.ent(0)));
         }
-        bool full = !grec || ovfl || n > SHORT_MAXN || sigG >= NSEG || (tt > 0 && sigG > SHORT_KMAX);
+        bool full = !grec || sigG >= NSEG || (tt > 0 && sigG > SHORT_KMAX);
         // the segment registers into LDS: plain for the per-record path,
         // lane-transposed for the tile-wide scan
         bool plain = !full;
@@ -1703,17 +1755,16 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             dev = em_f4(emt, (WG - tb - 64u * sigG) >> 2, x) ^ sG ^ expG;
         }
         // ---- tuples, and on the per-record path the records' checks
-        if (!ovfl) {
+        {
             // a round's compact entries and snapshots, loaded one round ahead;
             // the next record's come from lane + 1 (lane 63 loads its own)
-            const u32x4* trec4 = (const u32x4*)trec;
             const u32x4 z4 = (u32x4){0u, 0u, 0u, 0u};
             auto ld = [&](uint32_t j0, u32x4& v, uint32_t& sv, u32x4& vx, uint32_t& sx) {
                 const uint32_t j = j0 + (uint32_t)lane;
-                v = j < n ? trec4[j] : z4;
-                sv = j < n ? tsnap[j] : 0u;
+                v = j < n ? E.ent(j) : z4;
+                sv = j < n ? E.snap(j) : 0u;
                 vx = z4; sx = 0u;
-                if (lane == 63 && j + 1 < n) { vx = trec4[j + 1]; sx = tsnap[j + 1]; }
+                if (lane == 63 && j + 1 < n) { vx = E.ent(j + 1); sx = E.snap(j + 1); }
             };
             u32x4 vc, vx;
             uint32_t sc, sx;
@@ -1799,11 +1850,6 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 vc = vN; sc = sN; vx = vxN; sx = sxN;
             }
-        } else if (lane == 0) {
-            // more records than the compact list holds: k_ovf walks the tile
-            // again, writes its tuples and checks its records one by one
-            const uint32_t k = atomicAdd(&g->n_ovf, 1u);
-            ovf[k] = (u32x4){(uint32_t)f, t, (uint32_t)gb, (uint32_t)(gb >> 32)};
         }
         if (full) {
             if (plain) {
@@ -1818,22 +1864,22 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             uint32_t wlast = 0, clast = 0, plast = 0;                       // (the tile's last record start)
-            if (grec && !ovfl) {
+            if (grec) {
                 for (uint32_t i0 = 0; i0 < n; i0 += 64) {
                     const uint32_t i = i0 + (uint32_t)lane;
                     if (i < n) {
-                        const u32x4 v = *(const u32x4*)(trec + 4 * i);
+                        const u32x4 v = E.ent(i);
                         const uint32_t P = tb + (v.w & 0xFFFFu), W = patch_word_of(P), sg = (W - tb) >> 6;
                         bool lastin = true;
-                        if (i + 1 < n) lastin = ((patch_word_of(tb + (trec[4 * (i + 1) + 3] & 0xFFFFu)) - tb) >> 6) != sg;
+                        if (i + 1 < n) lastin = ((patch_word_of(tb + (E.ent(i + 1).w & 0xFFFFu)) - tb) >> 6) != sg;
                         if (sg < NSEG && lastin) {
-                            const uint32_t inj = tsnap[i] ^ exp_post(P & 3u, entry_crc(base, F.len, tb, v), kj);
+                            const uint32_t inj = E.snap(i) ^ exp_post(P & 3u, entry_crc(base, F.len, tb, v), kj);
                             gin[gin_at(sg, false)] ^= em_f4(emt, (64u * (sg + 1u) - (W - tb)) >> 2, inj);
                             __atomic_fetch_or(flg + (sg >> 5), 1u << (sg & 31u), __ATOMIC_RELAXED);
                         }
                     }
                 }
-                const u32x4 vl = *(const u32x4*)(trec + 4 * (n - 1));
+                const u32x4 vl = E.ent(n - 1);
                 plast = tb + (vl.w & 0xFFFFu);
                 wlast = patch_word_of(plast);
                 clast = entry_crc(base, F.len, tb, vl);
@@ -1872,7 +1918,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             else if (grec) {
                 // the tile's own register entering WG (no reset before G)
                 dev = (sigG < NSEG ? em_f4(emt, (WG - tb - 64u * sigG) >> 2, gin[gin_at(sigG, false)]) : gte) ^ sG ^ expG;
-                if (!ovfl) {
+                {
                     // past the last record start: its reset at the tile's end
                     // when its patch word is there, else the scan's register
                     ex = wlast == TE ? exp_post(plast & 3u, clast, kj) : gte ^ cout;
@@ -1880,12 +1926,13 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                         atomicMin(&fo->fail_key, ((u64)(uint32_t)(loc[t].l[2] >> 32) << 32) | (S.count + n - 1));
                     // every record that ends at a record start inside the tile
                     for (uint32_t i = lane; i + 1 < n; i += 64) {
-                        const u32x4 v = *(const u32x4*)(trec + 4 * i), v2 = *(const u32x4*)(trec + 4 * (i + 1));
+                        const u32x4 v = E.ent(i), v2 = E.ent(i + 1);
                         const uint32_t p = tb + (v.w & 0xFFFFu), P2 = tb + (v2.w & 0xFFFFu);
                         const uint32_t W = patch_word_of(p), W2 = patch_word_of(P2), sg = (W - tb) >> 6, sg2 = (W2 - tb) >> 6;
                         const uint32_t c1 = entry_crc(base, F.len, tb, v), c2 = entry_crc(base, F.len, tb, v2);
-                        const uint32_t pre = sg2 == sg ? tsnap[i + 1] ^ em_f4(emt, (W2 - W) >> 2, tsnap[i] ^ exp_post(p & 3u, c1, kj))
-                                                       : em_f4(emt, (W2 - tb - 64u * sg2) >> 2, gin[gin_at(sg2, false)]) ^ tsnap[i + 1];
+                        const uint32_t s1 = E.snap(i), s2 = E.snap(i + 1);
+                        const uint32_t pre = sg2 == sg ? s2 ^ em_f4(emt, (W2 - W) >> 2, s1 ^ exp_post(p & 3u, c1, kj))
+                                                       : em_f4(emt, (W2 - tb - 64u * sg2) >> 2, gin[gin_at(sg2, false)]) ^ s2;
                         if (pre != exp_pre(emt, P2 & 3u, c1, c2))
                             atomicMin(&fo->fail_key, ((u64)p << 32) | (S.count + i));
                     }
@@ -1910,9 +1957,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
 // k_fin: per file (FIN_NT threads), after k_emit: the register entering every
 // tile up to the terminal's, as a segmented scan over the tiles (a tile with a
 // boundary fixes the register at its end to its exit value; a tile without one
-// passes it on as A^CLY_TILE r ^ its own register; a tile whose compact list
-// overflowed leaves it unknown: k_ovf checks the records that start there),
-// and in every tile after the first that has a boundary, the check of the
+// passes it on as A^CLY_TILE r ^ its own register), and in every tile after the first that has a boundary, the check of the
 // record that crosses into it (its start: the last record before the tile,
 // TileIn): A^CLY_TILE (the register entering the tile) must equal the tile's
 // dev shifted to its end.
@@ -1925,9 +1970,9 @@ k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __rest
       const TileLocal* __restrict__ loc, const TileIn* __restrict__ tin, const uint32_t* __restrict__ tabs,
       const uint32_t* __restrict__ pw, Globals* g, int slot) {
     __shared__ uint32_t tabl[NIB_SH * 128 + 128];           // TAB_SH, TAB_TILE
-    __shared__ uint32_t px[FIN_NT], pc[FIN_NT], pu[FIN_NT];
+    __shared__ uint32_t px[FIN_NT], pc[FIN_NT];
     __shared__ uint32_t mlev[16];
-    if (g->nfix[slot]) return;              // k_emit did not run (link repair first)
+    if (g->nfix[slot] || g->spill_over) return;     // k_emit did not run
     for (int i = threadIdx.x; i < NIB_SH * 128 + 128; i += FIN_NT) tabl[i] = tabs[TAB_SH + i];
     const CLY_LDS uint32_t* sht = (const CLY_LDS uint32_t*)tabl;
     const CLY_LDS uint32_t* tilet = sht + NIB_SH * 128;
@@ -1947,31 +1992,31 @@ k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __rest
         for (int l = 0; (1 << l) < FIN_NT; l++) { mlev[l] = m; m = cly_multmodp(m, m); }
     }
     __syncthreads();
-    uint32_t x = 0, c = 0, un = 0;
+    uint32_t x = 0, c = 0;
     for (uint32_t u = lo; u < hi; u++) {
         const u64 l0 = loc[ft + u].l[0];
         const uint32_t v = treg[2 * (ft + u)];
-        if (!(l0 & DF_NONE)) { x = v; c = 1; un = (l0 & DF_OVF) ? 1u : 0u; }
+        if (!(l0 & DF_NONE)) { x = v; c = 1; }
         else x = mat_mul(tilet, x) ^ v;
     }
-    px[tid] = x; pc[tid] = c; pu[tid] = un;
+    px[tid] = x; pc[tid] = c;
     __syncthreads();
     for (int l = 0; (1 << l) < FIN_NT; l++) {
         const int d = 1 << l;
-        uint32_t ox = 0, oc = 0, ou = 0;
-        if (tid >= d) { ox = px[tid - d]; oc = pc[tid - d]; ou = pu[tid - d]; }
+        uint32_t ox = 0, oc = 0;
+        if (tid >= d) { ox = px[tid - d]; oc = pc[tid - d]; }
         __syncthreads();
-        if (tid >= d && !c) { x = cly_multmodp(mlev[l], ox) ^ x; c = oc; un = ou; }
-        px[tid] = x; pc[tid] = c; pu[tid] = un;
+        if (tid >= d && !c) { x = cly_multmodp(mlev[l], ox) ^ x; c = oc; }
+        px[tid] = x; pc[tid] = c;
         __syncthreads();
     }
-    uint32_t y = tid ? px[tid - 1] : 0u, yu = tid ? pu[tid - 1] : 0u;
+    uint32_t y = tid ? px[tid - 1] : 0u;
     for (uint32_t u = lo; u < hi; u++) {
         const uint32_t t = ft + u;
         const u64 l0 = loc[t].l[0];
         const uint32_t v = treg[2 * t];
         if (l0 & DF_NONE) { y = mat_mul(tilet, y) ^ v; continue; }
-        if (u > 0 && !yu) {
+        if (u > 0) {
             const LBState S = ti_load(&tin[t]);
             const uint32_t n = (uint32_t)(l0 >> 32), G = (uint32_t)loc[t].l[1];
             const uint32_t tb = (uint32_t)((uint64_t)u * CLY_TILE), TE = tb + (uint32_t)CLY_TILE;
@@ -1982,38 +2027,6 @@ k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __rest
                 atomicMin(&fo->fail_key, ((u64)S.P_last << 32) | (uint64_t)(S.count - 1));
         }
         y = v;
-        yu = (l0 & DF_OVF) ? 1u : 0u;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_ovf (only for tiles whose compact list overflowed; k_emit lists them): one
-// wave per listed tile walks it again from its final entry (tile_body,
-// BM_EMIT), writes every record's tuple to its slot and computes the record's
-// CRC-32 alone (one lane per record, table steps from LDS), compared with the
-// stored one (data/logRecord.go:136-146, data/dataFile.go:105-109); the first
-// failing record of a file wins.
-#define OVF_LDS (SCAN_LDS + SCAN_WAVES * STG_BYTES)
-__global__ void __launch_bounds__(64 * SCAN_WAVES)
-k_ovf(const DevFile* __restrict__ files, FileInfo* finfo, const TileIn* __restrict__ tin, cly_tuple* out_,
-      uint64_t out_cap, const u32x4* __restrict__ ovf, Globals* g, int slot) {
-    if (!g->n_ovf || g->nfix[slot] || g->fail) return;     // (uniform: before the LDS setup's barrier)
-    __shared__ __attribute__((aligned(16))) unsigned char smem_raw[OVF_LDS];
-    CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
-    init_tables(smem);
-    CLY_LDS uint32_t* stg = (CLY_LDS uint32_t*)(smem + SCAN_LDS + wave_id() * STG_BYTES);
-    const CrcLane cl = crc_lane(threadIdx.x & 63);
-    const uint32_t nl = g->n_ovf;
-    for (uint32_t k = blockIdx.x * SCAN_WAVES + wave_id(); k < nl; k += gridDim.x * SCAN_WAVES) {
-        const u32x4 e = ovf[k];
-        const DevFile F = files[e.x];
-        const uint32_t t = e.y;
-        const uint64_t gb = ((uint64_t)e.w << 32) | e.z;
-        const LBState S = ti_load(&tin[t]);
-        u32x4 blk[4], hl;
-        tile_issue(F, t - F.first_tile, threadIdx.x & 63, blk, hl);
-        tile_body<BM_EMIT>(F, t, t - F.first_tile, S.X, false, smem, stg, nullptr, cl, 0u, nullptr, nullptr,
-                           nullptr, nullptr, nullptr, (gtuples)out_, out_cap, gb, g, &finfo[e.x], blk, hl, nullptr, 0u, 0u);
     }
 }
 
@@ -2030,13 +2043,15 @@ struct cly_ctx {
     DevFile* d_files; uint32_t* d_tprefix; FileInfo* d_finfo; uint64_t* d_ftotal; int cap_files;
     DevFile* h_files; uint32_t* h_tprefix; FileInfo* h_finfo;
     TileLocal* d_loc; TileIn* d_tin; uint32_t* d_treg; uint32_t* d_fix; uint32_t* d_rec;
-    uint32_t* d_seg; uint32_t* d_snap; u32x4* d_ovf;   // segment registers, snapshots, k_ovf's list
+    uint32_t* d_seg; uint32_t* d_snap;   // segment registers, snapshots
+    uint32_t* d_chunks;          // per tile CH_WORDS words: spill chunk ids and their count
     int64_t cap_tiles;
+    u32x4* d_sp_rec; uint32_t* d_sp_snap; uint32_t cap_spill;   // the spill pool (chunks of CAP_T entries)
     Globals* d_g; Globals* h_g;
     uint32_t* d_tabs;            // nibble tables (TAB_SH, TAB_TILE, TAB_EM)
     uint32_t* d_pw;              // x^(8 CLY_TILE 2^k) mod P, k < 40
     int scan_grid, emit_grid, loc_grid;
-    float kms[6];                // last call: k_scan, link rounds (k_link/k_refix), k_emit, k_fin, k_ovf, all
+    float kms[6];                // last call: k_scan, link rounds (k_link/k_refix), k_emit, k_fin, discarded attempts, all
     uint8_t* d_bytes; uint64_t cap_bytes;          // host-path staging
     cly_tuple* d_tuples; uint64_t cap_tuples;
     void* merge_scratch;         // clymerge.hip's buffers (grow-only)
@@ -2105,7 +2120,7 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     hipStreamSynchronize(c->stream);
     hipFree(c->d_call); hipFree(c->d_ftotal);
     hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_rec);
-    hipFree(c->d_seg); hipFree(c->d_snap); hipFree(c->d_ovf);
+    hipFree(c->d_seg); hipFree(c->d_snap); hipFree(c->d_chunks); hipFree(c->d_sp_rec); hipFree(c->d_sp_snap);
     hipFree(c->d_tabs); hipFree(c->d_pw); hipFree(c->d_bytes); hipFree(c->d_tuples); hipFree(c->d_dbg);
     hipHostFree(c->h_call);
     cly_merge_scratch_free(c->merge_scratch);
@@ -2148,9 +2163,9 @@ static int ensure_files(cly_ctx* c, int nfiles) {
 static int ensure_tiles(cly_ctx* c, int64_t ntiles) {
     if (ntiles <= c->cap_tiles) return CLY_OK;
     hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_rec);
-    hipFree(c->d_seg); hipFree(c->d_snap); hipFree(c->d_ovf);
+    hipFree(c->d_seg); hipFree(c->d_snap); hipFree(c->d_chunks);
     c->d_loc = nullptr; c->d_tin = nullptr; c->d_treg = nullptr; c->d_fix = nullptr; c->d_rec = nullptr;
-    c->d_seg = nullptr; c->d_snap = nullptr; c->d_ovf = nullptr;
+    c->d_seg = nullptr; c->d_snap = nullptr; c->d_chunks = nullptr;
     c->cap_tiles = 0;
     const int64_t cap = ntiles < 1024 ? 1024 : ntiles;
     HIPCK(hipMalloc(&c->d_loc, sizeof(TileLocal) * cap));
@@ -2158,10 +2173,23 @@ static int ensure_tiles(cly_ctx* c, int64_t ntiles) {
     HIPCK(hipMalloc(&c->d_treg, sizeof(uint32_t) * 2 * cap));
     HIPCK(hipMalloc(&c->d_seg, sizeof(uint32_t) * NSEG * (uint64_t)cap));
     HIPCK(hipMalloc(&c->d_snap, sizeof(uint32_t) * SNAP_T * (uint64_t)cap));
-    HIPCK(hipMalloc(&c->d_ovf, sizeof(u32x4) * cap));
+    HIPCK(hipMalloc(&c->d_chunks, sizeof(uint32_t) * CH_WORDS * (uint64_t)cap));
     HIPCK(hipMalloc(&c->d_fix, sizeof(uint32_t) * cap));
     HIPCK(hipMalloc(&c->d_rec, sizeof(uint32_t) * 4 * (uint64_t)CAP_T * cap));
     c->cap_tiles = cap;
+    return CLY_OK;
+}
+
+// The spill pool: at least `chunks` chunks (grow-only; the first call of a
+// context sizes it for one chunk per 8 tiles)
+static int ensure_spill(cly_ctx* c, uint64_t chunks) {
+    if (chunks <= c->cap_spill) return CLY_OK;
+    if (chunks > 0xFFFFFFF0ull) return CLY_ERR_ARG;
+    hipFree(c->d_sp_rec); hipFree(c->d_sp_snap);
+    c->d_sp_rec = nullptr; c->d_sp_snap = nullptr; c->cap_spill = 0;
+    HIPCK(hipMalloc(&c->d_sp_rec, sizeof(u32x4) * CAP_T * chunks));
+    HIPCK(hipMalloc(&c->d_sp_snap, sizeof(uint32_t) * CAP_T * chunks));
+    c->cap_spill = (uint32_t)chunks;
     return CLY_OK;
 }
 
@@ -2171,9 +2199,9 @@ static int ensure_tiles(cly_ctx* c, int64_t ntiles) {
 // alloc != nullptr: the output is allocated here (hipMalloc, the caller frees
 // it) once the link knows the exact record count, so that it holds exactly
 // needed + 16 tuples (d_out and out_cap are ignored).
-static int scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple* d_out, uint64_t out_cap,
-                       uint64_t* file_first, cly_file_result* res, uint64_t* needed, cly_stats* stats, void* stream_v,
-                       cly_tuple** alloc, uint64_t* alloc_cap) {
+static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple* d_out, uint64_t out_cap,
+                        uint64_t* file_first, cly_file_result* res, uint64_t* needed, cly_stats* stats, void* stream_v,
+                        cly_tuple** alloc, uint64_t* alloc_cap) {
     if (!c || (!files && nfiles) || nfiles < 0 || !res || !file_first) return CLY_ERR_ARG;
     if (alloc) { *alloc = nullptr; d_out = nullptr; out_cap = 0; }
     if (nfiles == 0) { if (needed) *needed = 0; return CLY_OK; }
@@ -2201,7 +2229,10 @@ static int scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple*
     c->h_tprefix[nfiles] = (uint32_t)ntiles;
     rc = ensure_tiles(c, ntiles);
     if (rc) return rc;
+    rc = ensure_spill(c, (uint64_t)ntiles / 8 + 64);
+    if (rc) return rc;
     memset(c->h_g, 0, sizeof(Globals));
+    c->h_g->spill_cap = c->cap_spill;
     memset(c->h_finfo, 0, sizeof(FileInfo) * nfiles);
     for (int i = 0; i < nfiles; i++) c->h_finfo[i].fail_key = ~0ull;
     HIPCK(hipMemcpyAsync(c->d_call, c->h_call, c->call_bytes, hipMemcpyHostToDevice, st));
@@ -2210,7 +2241,8 @@ static int scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple*
     if ((int64_t)grid * SCAN_WAVES > ntiles) grid = (int)((ntiles + SCAN_WAVES - 1) / SCAN_WAVES);
     HIPCK(hipEventRecord(c->ev[0], st));
     hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * SCAN_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
-                       c->d_loc, c->d_rec, c->d_seg, c->d_snap, c->d_treg, c->d_g);
+                       c->d_loc, c->d_rec, c->d_seg, c->d_snap, c->d_treg, c->d_chunks, c->d_sp_rec, c->d_sp_snap,
+                       c->d_g);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[1], st));
     if (c->dbg & 1) {
@@ -2229,7 +2261,8 @@ static int scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple*
     // one repair round on the device, without a host wait: k_refix and
     // k_link return at once when the first link listed no tile
     hipLaunchKernelGGL(k_refix, dim3(REFIX_GRID), dim3(64 * SCAN_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix,
-                       c->d_loc, c->d_tin, c->d_rec, c->d_seg, c->d_snap, c->d_treg, c->d_fix, c->d_g, 0);
+                       c->d_loc, c->d_tin, c->d_rec, c->d_seg, c->d_snap, c->d_treg, c->d_chunks, c->d_sp_rec,
+                       c->d_sp_snap, c->d_fix, c->d_g, 0);
     hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_loc, c->d_tin, c->d_ftotal,
                        c->d_finfo, c->d_fix, c->d_g, 1, 0);
     HIPCK(hipGetLastError());
@@ -2240,17 +2273,13 @@ static int scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple*
         if ((int64_t)eg * EMIT_WAVES > ntiles) eg = (int)((ntiles + EMIT_WAVES - 1) / EMIT_WAVES);
         hipLaunchKernelGGL(k_emit, dim3(eg), dim3(64 * EMIT_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
                            c->d_tin, c->d_loc, c->d_rec, c->d_seg, c->d_snap, c->d_treg, c->d_finfo, c->d_tabs, d_out,
-                           out_cap, c->d_ovf, c->d_g, slot);
+                           out_cap, c->d_chunks, c->d_sp_rec, c->d_sp_snap, c->d_g, slot);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[3], st));
         hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_finfo, c->d_treg, c->d_loc,
                            c->d_tin, c->d_tabs, c->d_pw, c->d_g, slot);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[4], st));
-        hipLaunchKernelGGL(k_ovf, dim3(c->loc_grid), dim3(64 * SCAN_WAVES), 0, st, c->d_files, c->d_finfo, c->d_tin, d_out, out_cap,
-                           c->d_ovf, c->d_g, slot);
-        HIPCK(hipGetLastError());
-        HIPCK(hipEventRecord(c->ev[7], st));
         // one read-back and one wait for the whole call when no repair round is needed
         HIPCK(hipMemcpyAsync(c->h_call, c->d_call, (uint8_t*)(c->h_finfo + nfiles) - c->h_call, hipMemcpyDeviceToHost, st));
         HIPCK(hipStreamSynchronize(st));
@@ -2269,7 +2298,7 @@ static int scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple*
     else {
         HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
         HIPCK(hipStreamSynchronize(st));
-        if (!c->h_g->nfix[slot] && !c->h_g->fail) rc2 = emit_alloc();
+        if (!c->h_g->nfix[slot] && !c->h_g->fail && !c->h_g->spill_over) rc2 = emit_alloc();
     }
     if (rc2) return rc2;
     float ms_fix = 0;
@@ -2286,7 +2315,7 @@ static int scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple*
             HIPCK(hipMemsetAsync(&c->d_g->nfix[ns], 0, sizeof(uint32_t), st));
             hipLaunchKernelGGL(k_refix, dim3((nfix + SCAN_WAVES - 1) / SCAN_WAVES), dim3(64 * SCAN_WAVES), 0, st,
                                c->d_files, nfiles, c->d_tprefix, c->d_loc, c->d_tin, c->d_rec, c->d_seg, c->d_snap,
-                               c->d_treg, c->d_fix, c->d_g, slot);
+                               c->d_treg, c->d_chunks, c->d_sp_rec, c->d_sp_snap, c->d_fix, c->d_g, slot);
             hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_loc, c->d_tin,
                                c->d_ftotal, c->d_finfo, c->d_fix, c->d_g, ns, -1);
             HIPCK(hipGetLastError());
@@ -2298,22 +2327,27 @@ static int scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple*
         HIPCK(hipEventRecord(c->ev[6], st));
         HIPCK(hipEventSynchronize(c->ev[6]));
         HIPCK(hipEventElapsedTime(&ms_fix, c->ev[5], c->ev[6]));
-        if (!c->h_g->fail) {
+        if (!c->h_g->fail && !c->h_g->spill_over) {
             HIPCK(hipEventRecord(c->ev[2], st));
             rc2 = alloc ? emit_alloc() : launch_emit();
             if (rc2) return rc2;
         }
     }
-    float ms_scan = 0, ms_link = 0, ms_emit = 0, ms_fin = 0, ms_loc = 0;
+    float ms_scan = 0, ms_link = 0, ms_emit = 0, ms_fin = 0;
+    if (c->h_g->spill_over) {                    // (k_emit / k_fin did not run: the caller runs the call again)
+        HIPCK(hipStreamSynchronize(st));
+        HIPCK(hipEventElapsedTime(&ms_scan, c->ev[0], c->ev[1]));
+        c->kms[5] = ms_scan + ms_fix;
+        return CLY_OK;
+    }
     HIPCK(hipEventElapsedTime(&ms_scan, c->ev[0], c->ev[1]));
     HIPCK(hipEventElapsedTime(&ms_link, c->ev[1], c->ev[2]));
     HIPCK(hipEventElapsedTime(&ms_emit, c->ev[2], c->ev[3]));
     HIPCK(hipEventElapsedTime(&ms_fin, c->ev[3], c->ev[4]));
-    HIPCK(hipEventElapsedTime(&ms_loc, c->ev[4], c->ev[7]));
     if (ms_fix > 0) ms_link = 0;   // ev[2] was re-recorded after the host repair loop
     c->h_g->refix = refixed;
-    c->kms[0] = ms_scan; c->kms[1] = ms_link + ms_fix; c->kms[2] = ms_emit; c->kms[3] = ms_fin; c->kms[4] = ms_loc;
-    c->kms[5] = ms_scan + ms_link + ms_fix + ms_emit + ms_fin + ms_loc;
+    c->kms[0] = ms_scan; c->kms[1] = ms_link + ms_fix; c->kms[2] = ms_emit; c->kms[3] = ms_fin; c->kms[4] = 0;
+    c->kms[5] = ms_scan + ms_link + ms_fix + ms_emit + ms_fin;
     if (c->h_g->fail) {
         fprintf(stderr, "clyscan: internal error (code %#x)\n", c->h_g->fail);
         return CLY_ERR_DEVICE;
@@ -2336,13 +2370,36 @@ static int scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple*
     }
     if (needed) *needed = c->h_g->total;
     if (stats) {
-        stats->scan_ms = ms_scan + ms_emit; stats->resolve_ms = ms_link + ms_fix + ms_fin + ms_loc;
+        stats->scan_ms = ms_scan + ms_emit; stats->resolve_ms = ms_link + ms_fix + ms_fin;
         stats->total_ms = c->kms[5];
         stats->passes = rounds;
         stats->n_chunks = (uint32_t)(ntiles * CLY_NBLK * CLY_NL); stats->bytes = bytes; stats->records = total;
     }
     if (c->h_g->overflow || c->h_g->total > out_cap) return CLY_ERR_CAPACITY;
     return CLY_OK;
+}
+// One call: an attempt whose tiles needed more spill chunks than the pool
+// held (small records, CAP_T+ per tile) is run again with a pool of the size
+// it asked for; the context keeps the pool for later calls.
+static int scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple* d_out, uint64_t out_cap,
+                       uint64_t* file_first, cly_file_result* res, uint64_t* needed, cly_stats* stats, void* stream_v,
+                       cly_tuple** alloc, uint64_t* alloc_cap) {
+    float discarded = 0;
+    for (int attempt = 0;; attempt++) {
+        const int rc = scan_attempt(c, files, nfiles, d_out, out_cap, file_first, res, needed, stats, stream_v, alloc,
+                                    alloc_cap);
+        if (nfiles == 0 || !c->h_g->spill_over || (rc != CLY_OK && rc != CLY_ERR_CAPACITY)) {
+            c->kms[4] = discarded;
+            c->kms[5] += discarded;
+            return rc;
+        }
+        discarded += c->kms[5];
+        if (alloc && *alloc) { hipFree(*alloc); *alloc = nullptr; }
+        if (attempt >= 3) return CLY_ERR_DEVICE;
+        const uint64_t want = (uint64_t)c->h_g->spill_next;
+        const int r2 = ensure_spill(c, std::max<uint64_t>(2ull * c->cap_spill, want + want / 4 + 64));
+        if (r2) return r2;
+    }
 }
 extern "C" int cly_scan_device(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple* d_out, uint64_t out_cap,
                                uint64_t* file_first, cly_file_result* res, uint64_t* needed, cly_stats* stats,

@@ -128,6 +128,77 @@ def test_tiny_records_irregular(scanner, seed):
     compare(r.file_tuples(0), r.status[0], r.end_offset[0], t, st, end, "tiny %d" % seed)
 
 
+def tiny_records(seed, nbytes):
+    """Commit / rollback markers, tombstones, empty values and short keys:
+    records of 12-30 bytes (hint-index records average 23.6 B)."""
+    import random
+
+    import make_golden as mg
+    rng = random.Random(seed)
+    b = bytearray()
+    while len(b) < nbytes:
+        r = rng.random()
+        if r < 0.25:
+            b += mg.encode_record(mg.key_tx(mg.TX_COMMIT_KEY, rng.randrange(1, 1 << 20)), b"", mg.TXN_COMMIT)
+        elif r < 0.35:
+            b += mg.encode_record(mg.key_tx(mg.TX_ROLLBACK_KEY, rng.randrange(1, 1 << 20)), b"", mg.TXN_ROLLBACK)
+        elif r < 0.6:
+            b += mg.encode_record(mg.key_tx(b"%d" % rng.randrange(10 ** 6), 0), b"", mg.DELETED)
+        else:
+            b += mg.encode_record(mg.key_tx(rng.randbytes(rng.randrange(1, 9)), rng.choice([0, 0, 7])),
+                                  rng.randbytes(rng.randrange(0, 12)), 0, rng.choice([0, 0, 1, 3]))
+    return bytes(b)
+
+
+def test_spill_tiles_then_long_record(scanner):
+    """A tile with more than CAP_T records (its compact list spills into
+    chunks) followed by a 5-MiB record and more tiny records: every tuple
+    and the CRC verdicts bit-exact against the oracle; a flipped byte deep in
+    the long record stops the file at that record (ErrInvalidCRC)."""
+    import make_golden as mg
+    small = tiny_records(1, 40_000)                           # ~2000 records: several tiles' worth
+    big = mg.encode_record(mg.key_tx(b"big", 0), bytes(range(256)) * (5 << 12))
+    data = np.frombuffer(small + big + tiny_records(2, 70_000), np.uint8).copy()
+    for flip in (None, len(small) + len(big) // 2):
+        d = data.copy()
+        if flip is not None:
+            d[flip] ^= 0x08
+        r = scanner.scan([DataFile(d, 3)])
+        t, st, end = co.scan_file(d, 3)
+        compare(r.file_tuples(0), r.status[0], r.end_offset[0], t, st, end, "spill + long %s" % flip)
+        if flip is not None:
+            assert st == _abi.ERR_CRC and end == len(small)
+
+
+def test_tiny_record_file_1gib(scanner):
+    """One 1-GiB data file of 12-30-B records (about 45 M: every tile spills;
+    the context's first call grows the spill pool and runs again, the second
+    does not), bit-exact against the oracle; then a flipped byte in the last
+    tile's records gives ErrInvalidCRC at its record."""
+    torch = pytest.importorskip("torch")
+    base = np.frombuffer(tiny_records(7, 4 << 20), np.uint8)
+    arr = np.tile(base, (1 << 30) // len(base))
+    n_base = len(co.scan_file(base.copy(), 1)[0])
+    d = torch.from_numpy(arr).cuda()
+    t, st, end = co.scan_file(arr, 1)
+    assert st == 0 and len(t) == n_base * ((1 << 30) // len(base))
+    out = torch.empty((len(t) + 64) * 48, dtype=torch.uint8, device="cuda")
+    with Scanner(0, lib=scanner.lib_name) as sc:
+        for call in range(2):
+            first, res, stt, need = sc.scan_device([(d.data_ptr(), len(arr), 1)], out.data_ptr(), len(t) + 64)
+            retry = sc.kernel_ms()["retry"]
+            assert (retry > 0) if call == 0 else (retry == 0), (call, retry)
+        got = out[: need * 48].cpu().numpy().view(TUPLE_DTYPE)
+        compare(got[: res[0].n_records], res[0].status, res[0].end_offset, t, st, end, "1 GiB tiny")
+        del got
+        k = len(t) - 1000
+        arr2 = arr.copy()
+        arr2[int(t["offset"][k]) + 5] ^= 0x01                 # the record's data type byte
+        d.copy_(torch.from_numpy(arr2))
+        first, res, stt, need = sc.scan_device([(d.data_ptr(), len(arr2), 1)], out.data_ptr(), len(t) + 64)
+        assert res[0].status == _abi.ERR_CRC and res[0].n_records == k and res[0].end_offset == int(t["offset"][k])
+
+
 @pytest.mark.parametrize("cut", [0, 1, 4, 5, 6, 13, 27, 31])
 def test_tails_at_chunk_boundaries(scanner, cut):
     # lengths around chunk multiples for both builds (32 KiB and 2 KiB chunks)

@@ -20,6 +20,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define F_SEGT 256
 #define F_NT 512
 #define F_SEGAFT 1024
+#define F_SEG4 2048     // segment registers stored as one b128 per lane every 4 blocks
+#define F_R8 4096       // 8 CRC table replicas (32 KB) instead of 16
+#define F_SNK 8192      // compact entries through a 1-KiB LDS sink per wave, flushed as whole 1-KiB stores
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mk(const void* p, uint32_t n) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)n, 0x00020000);
 }
@@ -51,7 +54,7 @@ __device__ __forceinline__ uint32_t crc_word(const LDSP uint8_t* sm, uint32_t x,
 template <int F>
 __global__ void __launch_bounds__(64 * WAVES) kskel(const uint8_t* buf, uint32_t ntiles, uint32_t* rec, uint32_t* seg,
                                                     uint32_t* snap, uint32_t* out) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[65536 + 256 + WAVES * (STG_BYTES + 256) + ((F & F_SEGT) ? WAVES * 4096 : 0)];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[65536 + 256 + WAVES * (STG_BYTES + 256) + ((F & F_SNK) ? WAVES * 2048 : 0)];
   for (int i = threadIdx.x; i < 16384; i += blockDim.x) ((LDSP uint32_t*)smem)[i] = i * 2654435761u;
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -60,8 +63,9 @@ __global__ void __launch_bounds__(64 * WAVES) kskel(const uint8_t* buf, uint32_t
   LDSP uint32_t* stg = (LDSP uint32_t*)(sm + 65536 + 256 + wv * STG_BYTES);
   LDSP uint32_t* mkk = (LDSP uint32_t*)(sm + 65536 + 256 + WAVES * STG_BYTES + wv * 256);
   LDSP u32x4* sv = (LDSP u32x4*)stg;
-  LDSP uint32_t* segl = (LDSP uint32_t*)(sm + 65536 + 256 + WAVES * (STG_BYTES + 256)) + wv * 1024;
-  const uint32_t r4 = (lane & 15) * 4, h = (lane >> 4) & 1;
+  LDSP u32x4* snk = (LDSP u32x4*)(sm + 65536 + 256 + WAVES * (STG_BYTES + 256)) + wv * 128;
+  LDSP uint32_t* segl = nullptr;
+  const uint32_t r4 = (F & F_R8) ? (lane & 7) * 4 : (lane & 15) * 4, h = (lane >> 4) & 1;
   const uint32_t oe = r4 + 64 * h, oo = r4 + 64 * (1 - h);
   const uint32_t s0 = 0x0c0c0000u | ((4u + (3u - (0u ^ h))) << 8), s1 = 0x0c0c0000u | ((4u + (3u - (1u ^ h))) << 8);
   const uint32_t s2 = 0x0c0c0000u | ((4u + (3u - (2u ^ h))) << 8), s3 = 0x0c0c0000u | ((4u + (3u - (3u ^ h))) << 8);
@@ -77,7 +81,7 @@ __global__ void __launch_bounds__(64 * WAVES) kskel(const uint8_t* buf, uint32_t
 #pragma unroll
     for (int k = 0; k < 4; k++) e[k] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(off0 + 1024u * k), 0, 0);
     if ((F & F_STG) && lane < 2) hl = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(4096 + 16 * lane), 0, 0);
-    uint32_t X = (t * 37u) % 276u, tcnt = 0, nb = 0, Rp = 0;
+    uint32_t X = (t * 37u) % 276u, tcnt = 0, nb = 0, Rp = 0, sq[4] = {0, 0, 0, 0}, sk = 0;
 #pragma unroll 1
     for (int m = 0; m < NBLK; m++) {
       const uint32_t bs = m * 4096;
@@ -93,7 +97,7 @@ __global__ void __launch_bounds__(64 * WAVES) kskel(const uint8_t* buf, uint32_t
 #pragma unroll
       for (int k = 0; k < 4; k++) { w[4*k] = e[k].x; w[4*k+1] = e[k].y; w[4*k+2] = e[k].z; w[4*k+3] = e[k].w; }
       const u32x4 hc = hl;
-      if ((F & F_SEG) && !(F & (F_SEGT | F_SEGAFT)) && m > 0) __builtin_amdgcn_raw_buffer_store_b32(Rp, srs, (int)(((m - 1) * 64 + lane) * 4), 0, (F & F_NT) ? 2 : 0);
+      if ((F & F_SEG) && !(F & (F_SEGT | F_SEGAFT | F_SEG4)) && m > 0) __builtin_amdgcn_raw_buffer_store_b32(Rp, srs, (int)(((m - 1) * 64 + lane) * 4), 0, (F & F_NT) ? 2 : 0);
       if ((F & F_SEGT) && m > 0) segl[(m - 1) * 64 + lane] = Rp;
       if (m + 1 < NBLK) {
 #pragma unroll
@@ -125,7 +129,8 @@ __global__ void __launch_bounds__(64 * WAVES) kskel(const uint8_t* buf, uint32_t
         const uint64_t bm = __ballot(!match);
         const uint32_t kb = bm ? (uint32_t)__ffsll((long long)bm) - 1 : 64u;
         if (k < kb && (F & F_NOST)) acc ^= crc + P;
-        if (k < kb && !(F & F_NOST)) {
+        if ((F & F_SNK) && k < kb) snk[(sk + k) & 127] = (u32x4){crc, 0x11, 0x100, P | 0x4000000};
+        if (k < kb && !(F & (F_NOST | F_SNK))) {
           __builtin_amdgcn_raw_buffer_store_b128((u32x4){crc, 0x11, 0x100, (P - 0) | 0x4000000}, trs, (int)(((tcnt + k) & 511) * 16u), 0, (F & F_NT) ? 2 : 0);
         }
         if (k < kb) {
@@ -138,6 +143,16 @@ __global__ void __launch_bounds__(64 * WAVES) kskel(const uint8_t* buf, uint32_t
         acc ^= lastc;
         tcnt += kb;
         X = X + kb * 276u - 4096u;
+        if (F & F_SNK) {
+          sk += kb;
+          if (sk >= 64) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t b0 = (tcnt - sk) & ~63u;
+            __builtin_amdgcn_raw_buffer_store_b128(snk[((tcnt - sk) + lane) & 127], trs, (int)(((b0 + lane) * 16u) & 8191u), 0, 0);
+            sk -= 64;
+          }
+        }
       }
       if (F & F_CRC) {
         uint32_t R = 0;
@@ -152,6 +167,10 @@ __global__ void __launch_bounds__(64 * WAVES) kskel(const uint8_t* buf, uint32_t
         R = x;
         Rp = R;
         if ((F & F_SEGAFT)) __builtin_amdgcn_raw_buffer_store_b32(R, srs, (int)((m * 64 + lane) * 4), 0, 0);
+        if (F & F_SEG4) {
+          sq[m & 3] = R;
+          if ((m & 3) == 3) __builtin_amdgcn_raw_buffer_store_b128((u32x4){sq[0], sq[1], sq[2], sq[3]}, srs, (int)(((m >> 2) * 64 + lane) * 16), 0, 0);
+        }
         acc ^= R;
       } else {
 #pragma unroll
@@ -180,7 +199,8 @@ __global__ void __launch_bounds__(64 * WAVES) kskel(const uint8_t* buf, uint32_t
         }
       }
     }
-    if ((F & F_SEG) && !(F & (F_SEGT | F_SEGAFT))) __builtin_amdgcn_raw_buffer_store_b32(Rp, srs, (int)((15 * 64 + lane) * 4), 0, 0);
+    if ((F & F_SEG) && !(F & (F_SEGT | F_SEGAFT | F_SEG4))) __builtin_amdgcn_raw_buffer_store_b32(Rp, srs, (int)((15 * 64 + lane) * 4), 0, 0);
+    if ((F & F_SNK) && sk) __builtin_amdgcn_raw_buffer_store_b128(snk[lane], trs, (int)((((tcnt - sk) & ~63u) + lane) * 16u & 8191u), 0, 0);
     if (F & F_SEGT) {
       segl[15 * 64 + lane] = Rp;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -213,6 +233,6 @@ int main() {
   hipMalloc(&seg, (size_t)ntiles * 1024 * 4);
   hipMalloc(&snap, (size_t)ntiles * 516 * 4);
 #define R(F) run<F>(buf, ntiles, rec, seg, snap, out)
-  R(7); R(15); R(15 + 512); R(7 + 1024); R(35); R(35 + 128); R(35 + 512); R(63); R(63 + 128); R(63 + 512);
+  R(7); R(15); R(15 + 512); R(7 + 1024); R(7 + 2048); R(35); R(35 + 128); R(35 + 512); R(63); R(63 + 128); R(55 + 2048); R(55 + 128); R(39 + 128 + 2048);
   return 0;
 }
