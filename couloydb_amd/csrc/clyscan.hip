@@ -75,6 +75,9 @@ __device__ __forceinline__ rsrc_t mk_rsrc(const void* p, uint32_t bytes) {
 #define LM_OFF 3                 // segment beyond the end of the file
 #define CAP_T ((uint32_t)(CLY_TILE / 128))   // compact entries in a tile's own area (more: spill chunks)
 #define CAP_SHIFT (__builtin_ctz(CAP_T))
+// k_scan walks runs of RUN_TILES consecutive tiles of a file: a run's first
+// tile guesses its entry, the others take the exit of the tile before them
+#define RUN_TILES 4
 // Spill: records CAP_T.. of a tile go to chunks of CAP_T entries (and their
 // snapshots) taken from a per-call pool; a tile's chunk table holds up to
 // NCH_MAX chunk ids and, in word CH_NWORD, how many it took.  Records are at
@@ -130,8 +133,9 @@ struct Globals {                 // zeroed per call
     uint32_t spill_next;         // spill chunks taken
     uint32_t spill_cap;          // spill chunks in the pool (set by the host)
     uint32_t spill_over;         // a chunk was refused (the host grows the pool and runs the call again)
-    uint32_t _g0;
+    uint32_t walk_max;           // the longest k_refix walk (tiles), over all rounds
     uint64_t total;              // records over all files
+    uint64_t walk_dbg;           // (length << 32 | first tile) of the longest k_refix walk
 };
 
 // ---------------------------------------------------------------------------
@@ -191,8 +195,9 @@ __device__ __forceinline__ CrcLane crc_lane(int lane) {
 __device__ __forceinline__ uint32_t crc_word(const CLY_LDS uint8_t* smem, uint32_t x, const CrcLane& c) {
     const uint32_t a0 = __builtin_amdgcn_perm(x, c.oe, c.s0), a1 = __builtin_amdgcn_perm(x, c.oo, c.s1);
     const uint32_t a2 = __builtin_amdgcn_perm(x, c.oe, c.s2), a3 = __builtin_amdgcn_perm(x, c.oo, c.s3);
-    return *(const CLY_LDS uint32_t*)(smem + a0) ^ *(const CLY_LDS uint32_t*)(smem + a1) ^
-           *(const CLY_LDS uint32_t*)(smem + a2 + 128) ^ *(const CLY_LDS uint32_t*)(smem + a3 + 128);
+    const uint32_t t0 = *(const CLY_LDS uint32_t*)(smem + a0), t1 = *(const CLY_LDS uint32_t*)(smem + a1);
+    const uint32_t t2 = *(const CLY_LDS uint32_t*)(smem + a2 + 128), t3 = *(const CLY_LDS uint32_t*)(smem + a3 + 128);
+    return __builtin_amdgcn_bitop3_b32(t0, t1, t2, 0x96) ^ t3;        // (0x96: a ^ b ^ c)
 }
 // one byte through the register: T0[(s ^ b) & 0xff] ^ (s >> 8)
 __device__ __forceinline__ uint32_t crc_byte(const CLY_LDS uint8_t* smem, uint32_t s, uint32_t b, uint32_t r4) {
@@ -212,10 +217,12 @@ __device__ __forceinline__ uint32_t crc_unbytes(const CLY_LDS uint8_t* smem, uin
 }
 // M v by a nibble table of M
 __device__ __forceinline__ uint32_t mat_mul(const CLY_LDS uint32_t* t, uint32_t v) {
-    uint32_t p = 0;
+    uint32_t q[8];
     #pragma unroll
-    for (int n = 0; n < 8; n++) p ^= t[n * 16 + ((v >> (4 * n)) & 15u)];
-    return p;
+    for (int n = 0; n < 8; n++) q[n] = t[n * 16 + ((v >> (4 * n)) & 15u)];
+    // (v_bitop3 0x96: a three-input XOR, four of them instead of seven XORs)
+    return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(q[0], q[1], q[2], 0x96),
+                                       __builtin_amdgcn_bitop3_b32(q[3], q[4], q[5], 0x96), q[6] ^ q[7], 0x96);
 }
 // A^m v (m bytes), 1 <= m <= 65536: one nibble-table product per hex digit of m
 // (sh: the TAB_SH tables)
@@ -982,7 +989,8 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     const uint32_t tb = (uint32_t)((uint64_t)tt * CLY_TILE);
     const uint64_t flen = F.len;
     const gbytes base = (gbytes)F.base;
-    const bool known0 = BM != BM_SPEC || tt == 0;
+    // (BM_SPEC: X_in is NONE32 for a guessed entry, else the exit of the run's previous tile)
+    const bool known0 = BM != BM_SPEC || tt == 0 || X_in != NONE32;
     TState S;
     S.X = tt == 0 ? 0u : (known0 ? X_in : NONE32);
     S.dead = tt != 0 && known0 && dead_in;
@@ -1242,7 +1250,8 @@ __device__ __forceinline__ uint32_t k4_const(const CLY_LDS uint8_t* smem, uint32
     return K4;
 }
 
-// k_scan: one wave per tile (grid-stride), every byte of every file read once.
+// k_scan: one wave per run of RUN_TILES tiles (grid-stride), every byte of
+// every file read once.
 #define SCAN_WAVES 16
 #define MK_BYTES (CLY_NL * 4)                                 // a wave's patch-word mask
 #define CHK_BYTES (CH_WORDS * 4)                              // a wave's copy of its tile's spill chunk ids
@@ -1258,7 +1267,7 @@ __device__ __forceinline__ CLY_LDS uint32_t* wave_chk(CLY_LDS uint8_t* smem) {
     return (CLY_LDS uint32_t*)(smem + SCAN_LDS + SCAN_WAVES * (STG_BYTES + MK_BYTES) + wave_id() * CHK_BYTES);
 }
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
-k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
+k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ rprefix, uint32_t nruns,
        TileLocal* loc, uint32_t* rec, uint32_t* seg, uint32_t* snap, uint32_t* treg, uint32_t* chunks, u32x4* sp_rec,
        uint32_t* sp_snap, Globals* g) {
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS_ALL];
@@ -1271,27 +1280,46 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     const CrcLane cl = crc_lane(lane);
     const uint32_t K4 = k4_const(smem, cl.r4);
     const uint32_t stride = gridDim.x * SCAN_WAVES;
-    uint32_t t = blockIdx.x * SCAN_WAVES + wave_id();
-    if (t >= ntiles) return;
-    int f = find_file(tprefix, nfiles, t);
+    // runs of RUN_TILES consecutive tiles of a file, grid-strided; a run's
+    // first tile (not its file's first) guesses its entry, the others take
+    // the exit of the tile before them
+    uint32_t r = blockIdx.x * SCAN_WAVES + wave_id();
+    if (r >= nruns) return;
+    int f = find_file(rprefix, nfiles, r);
+    uint32_t t = files[f].first_tile + (r - rprefix[f]) * RUN_TILES;
     u32x4 e[4], hl;
     {
         const DevFile F = files[f];
         tile_issue(F, t - F.first_tile, lane, e, hl);
     }
+    uint32_t Xc = NONE32;        // the entry carried from the run's previous tile (NONE32: guess)
     for (;;) {
-        const uint32_t tn = t + stride;
-        const int fn = tn < ntiles ? find_file(tprefix, nfiles, tn) : -1;
+        const DevFile F = files[f];
+        const uint32_t rend = min(F.first_tile + (r - rprefix[f] + 1u) * RUN_TILES, F.first_tile + F.ntile);
+        // the wave's next tile: the next of this run, else the first of its next run
+        uint32_t tn = t + 1u, rn = r;
+        int fn = f;
+        if (tn >= rend) {
+            rn = r + stride;
+            fn = rn < nruns ? find_file(rprefix, nfiles, rn) : -1;
+            if (fn >= 0) tn = files[fn].first_tile + (rn - rprefix[fn]) * RUN_TILES;
+        }
         const uint8_t* nbase = nullptr;
         uint32_t nlen = 0, ntb = 0;
         if (fn >= 0) {
             nbase = files[fn].base; nlen = (uint32_t)files[fn].len;
             ntb = (tn - files[fn].first_tile) * (uint32_t)CLY_TILE;
         }
-        const DevFile F = files[f];
-        tile_body<BM_SPEC>(F, t, t - F.first_tile, 0u, false, smem, stg, mk, cl, K4, loc, rec, seg, snap, treg, chk,
-                           chunks, sp_rec, sp_snap, g, e, hl, nbase, nlen, ntb);
+        const TileRes res = tile_body<BM_SPEC>(F, t, t - F.first_tile, Xc, false, smem, stg, mk, cl, K4, loc, rec, seg,
+                                               snap, treg, chk, chunks, sp_rec, sp_snap, g, e, hl, nbase, nlen, ntb);
         if (fn < 0) break;
+        // a chain that ended in this tile is not carried: past the file's true
+        // end nothing reads the tiles, and a false chain's terminal must not
+        // zero the next tile's bytes for the CRC (k_link need not contradict a
+        // tile the true chain only passes through), so the next tile guesses
+        if (rn == r && !res.dead) Xc = res.X;
+        else Xc = NONE32;
+        if (rn != r) r = rn;
         t = tn; f = fn;
     }
 }
@@ -1351,6 +1379,7 @@ k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restric
     if (guard >= 0 && g->nfix[guard] == 0) return;  // (device round: nothing was re-resolved)
     __shared__ RunF rf[2][LINK_NT];
     __shared__ uint32_t badm[LINK_MAXT / 32];
+    __shared__ uint32_t ancm[LINK_MAXT / 32];  // anchors: a run's first tile with a boundary, not contradicted
     __shared__ uint32_t bad_far;             // a contradicted tile beyond the bitmask (listed alone)
     __shared__ uint64_t part[LINK_NT];
     __shared__ uint64_t carry;
@@ -1375,7 +1404,7 @@ k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restric
     // inclusive Kogge-Stone scan of the run functions
     int cur = 0;
     rf[0][tid] = my;
-    for (int i = tid; i < LINK_MAXT / 32; i += LINK_NT) badm[i] = 0;
+    for (int i = tid; i < LINK_MAXT / 32; i += LINK_NT) { badm[i] = 0; ancm[i] = 0; }
     if (tid == 0) bad_far = NONE32;
     __syncthreads();
     for (int d = 1; d < LINK_NT; d <<= 1) {
@@ -1404,7 +1433,8 @@ k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restric
         if (bad) {
             if (u < LINK_MAXT) atomicOr(&badm[u >> 5], 1u << (u & 31));
             else atomicMin(&bad_far, u);
-        }
+        } else if (u < LINK_MAXT && (u == 0 || (u % RUN_TILES == 0 && !(l0 & DF_NONE))))
+            atomicOr(&ancm[u >> 5], 1u << (u & 31));
         s = rf_apply(rf_tile(l0, l1, l2), s);
     };
     #pragma unroll
@@ -1412,10 +1442,20 @@ k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restric
         if (lo + k < hi) visit(lo + k, c0[k], c1[k], c2[k], c3[k]);
     for (uint32_t u = lo + LINK_PER; u < hi; u++) visit(u, L0[u].l[0], L0[u].l[1], L0[u].l[2], L0[u].l[3]);
     __syncthreads();
-    // list the contradicted tiles whose predecessor is not contradicted
+    // list a contradicted tile only when no contradicted tile lies between it
+    // and the anchor before it (the state entering it then comes from tiles
+    // whose chains are right; a tile that carried a wrong exit, or passed one
+    // through without a boundary, would enter it with a false state and send
+    // its walk down a false chain)
     for (uint32_t u = lo; u < hi && u < LINK_MAXT; u++) {
         const bool bu = (badm[u >> 5] >> (u & 31)) & 1u;
-        const bool bp = u > 0 && ((badm[(u - 1) >> 5] >> ((u - 1) & 31)) & 1u);
+        bool bp = false;
+        if (bu && u > 0) {
+            for (uint32_t v = u - 1;; v--) {
+                if ((badm[v >> 5] >> (v & 31)) & 1u) { bp = true; break; }
+                if (v == 0 || ((ancm[v >> 5] >> (v & 31)) & 1u)) break;
+            }
+        }
         if (bu && !bp) {
             const uint32_t k = atomicAdd(&g->nfix[slot], 1u);
             fixlist[k] = F.first_tile + u;
@@ -1497,6 +1537,7 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
     const LBState S0 = ti_load(&tin[t]);
     uint32_t X = S0.X;
     bool dead = S0.dead != 0;
+    const uint32_t t_start = t;
     for (;;) {
         // Suffix: the true entry is the start of the guessed chain's record j
         // (a false start that runs into the true chain).  The chain from there
@@ -1539,6 +1580,10 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
         const bool ok = (n0 & DF_NONE) ? X >= (uint32_t)n3 : X == (uint32_t)n1;
         if (ok) break;
         t++;
+    }
+    if (lane == 0) {
+        atomicMax(&g->walk_max, t - t_start + 1u);
+        atomicMax((unsigned long long*)&g->walk_dbg, ((u64)(t - t_start + 1u) << 32) | t_start);
     }
 }
 
@@ -1599,7 +1644,8 @@ __device__ __forceinline__ uint32_t em_a64(const CLY_LDS uint32_t* emt, uint32_t
 #define EMIT_A64B (NEM * 128 + 4)                       // words: after the nibble tables and kj
 __device__ __forceinline__ uint32_t em_a64b(const CLY_LDS uint32_t* emt, uint32_t v) {
     const CLY_LDS uint32_t* bt = emt + EMIT_A64B;
-    return bt[v & 255u] ^ bt[256 + ((v >> 8) & 255u)] ^ bt[512 + ((v >> 16) & 255u)] ^ bt[768 + (v >> 24)];
+    return __builtin_amdgcn_bitop3_b32(bt[v & 255u], bt[256 + ((v >> 8) & 255u)], bt[512 + ((v >> 16) & 255u)], 0x96) ^
+           bt[768 + (v >> 24)];
 }
 // A^(4-j) v, 1 <= j <= 3
 __device__ __forceinline__ uint32_t em_fj(const CLY_LDS uint32_t* emt, uint32_t j, uint32_t v) {
@@ -2042,6 +2088,7 @@ struct cly_ctx {
     uint8_t* d_call; uint8_t* h_call; size_t call_bytes;     // the per-call block (ensure_files)
     DevFile* d_files; uint32_t* d_tprefix; FileInfo* d_finfo; uint64_t* d_ftotal; int cap_files;
     DevFile* h_files; uint32_t* h_tprefix; FileInfo* h_finfo;
+    uint32_t* d_rprefix; uint32_t* h_rprefix;        // per file its first run of RUN_TILES tiles (k_scan)
     TileLocal* d_loc; TileIn* d_tin; uint32_t* d_treg; uint32_t* d_fix; uint32_t* d_rec;
     uint32_t* d_seg; uint32_t* d_snap;   // segment registers, snapshots
     uint32_t* d_chunks;          // per tile CH_WORDS words: spill chunk ids and their count
@@ -2136,7 +2183,7 @@ extern "C" uint64_t cly_scan_capacity(const cly_file* files, int nfiles) {
 }
 
 // The per-call block, one device allocation and its page-locked mirror:
-// [Globals | FileInfo x cap | DevFile x cap | tprefix x (cap + 1)], so that a
+// [Globals | FileInfo x cap | DevFile x cap | tprefix x (cap + 1) | rprefix x (cap + 1)], so that a
 // call moves its inputs (and zeroes the outputs) with one copy in and reads
 // the results back with one copy out.
 static inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -2147,7 +2194,8 @@ static int ensure_files(cly_ctx* c, int nfiles) {
     c->cap_files = 0;
     const int cap = nfiles < 64 ? 64 : nfiles;
     const size_t o_fi = al16(sizeof(Globals)), o_f = o_fi + al16(sizeof(FileInfo) * cap);
-    const size_t o_tp = o_f + al16(sizeof(DevFile) * cap), tot = o_tp + al16(sizeof(uint32_t) * (cap + 1));
+    const size_t o_tp = o_f + al16(sizeof(DevFile) * cap), o_rp = o_tp + al16(sizeof(uint32_t) * (cap + 1));
+    const size_t tot = o_rp + al16(sizeof(uint32_t) * (cap + 1));
     HIPCK(hipMalloc(&c->d_call, tot));
     HIPCK(hipMalloc(&c->d_ftotal, sizeof(uint64_t) * cap));
     HIPCK(hipHostMalloc(&c->h_call, tot, hipHostMallocDefault));
@@ -2155,6 +2203,7 @@ static int ensure_files(cly_ctx* c, int nfiles) {
     c->d_finfo = (FileInfo*)(c->d_call + o_fi); c->h_finfo = (FileInfo*)(c->h_call + o_fi);
     c->d_files = (DevFile*)(c->d_call + o_f); c->h_files = (DevFile*)(c->h_call + o_f);
     c->d_tprefix = (uint32_t*)(c->d_call + o_tp); c->h_tprefix = (uint32_t*)(c->h_call + o_tp);
+    c->d_rprefix = (uint32_t*)(c->d_call + o_rp); c->h_rprefix = (uint32_t*)(c->h_call + o_rp);
     c->call_bytes = tot;
     c->cap_files = cap;
     return CLY_OK;
@@ -2209,7 +2258,7 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
     hipStream_t st = stream_v ? (hipStream_t)stream_v : c->stream;
     int rc = ensure_files(c, nfiles);
     if (rc) return rc;
-    int64_t ntiles = 0;
+    int64_t ntiles = 0, nruns = 0;
     uint64_t bytes = 0;
     for (int i = 0; i < nfiles; i++) {
         if (files[i].len > MAX_FILE_LEN) return CLY_ERR_ARG;
@@ -2222,11 +2271,14 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
         c->h_files[i].ntile = (uint32_t)nt;
         c->h_files[i]._pad = 0;
         c->h_tprefix[i] = (uint32_t)ntiles;
+        c->h_rprefix[i] = (uint32_t)nruns;
         ntiles += (int64_t)nt;
+        nruns += (int64_t)((nt + RUN_TILES - 1) / RUN_TILES);
         bytes += files[i].len;
     }
     if (ntiles >= (1LL << 31)) return CLY_ERR_ARG;
     c->h_tprefix[nfiles] = (uint32_t)ntiles;
+    c->h_rprefix[nfiles] = (uint32_t)nruns;
     rc = ensure_tiles(c, ntiles);
     if (rc) return rc;
     rc = ensure_spill(c, (uint64_t)ntiles / 8 + 64);
@@ -2238,9 +2290,9 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
     HIPCK(hipMemcpyAsync(c->d_call, c->h_call, c->call_bytes, hipMemcpyHostToDevice, st));
     const uint32_t nt32 = (uint32_t)ntiles;
     int grid = c->scan_grid;
-    if ((int64_t)grid * SCAN_WAVES > ntiles) grid = (int)((ntiles + SCAN_WAVES - 1) / SCAN_WAVES);
+    if ((int64_t)grid * SCAN_WAVES > nruns) grid = (int)((nruns + SCAN_WAVES - 1) / SCAN_WAVES);
     HIPCK(hipEventRecord(c->ev[0], st));
-    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * SCAN_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
+    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * SCAN_WAVES), 0, st, c->d_files, nfiles, c->d_rprefix, (uint32_t)nruns,
                        c->d_loc, c->d_rec, c->d_seg, c->d_snap, c->d_treg, c->d_chunks, c->d_sp_rec, c->d_sp_snap,
                        c->d_g);
     HIPCK(hipGetLastError());
@@ -2311,6 +2363,8 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
             if (rounds > 4096) { fprintf(stderr, "clyscan: chain repair did not converge\n"); return CLY_ERR_NOREPAIR; }
             const uint32_t nfix = c->h_g->nfix[slot];
             refixed += nfix;
+            if (c->dbg & 2) fprintf(stderr, "clyscan: repair round %u: %u tiles listed, longest walk so far %u from tile %u\n",
+                                    rounds, nfix, c->h_g->walk_max, (uint32_t)c->h_g->walk_dbg);
             const int ns = slot ^ 1;
             HIPCK(hipMemsetAsync(&c->d_g->nfix[ns], 0, sizeof(uint32_t), st));
             hipLaunchKernelGGL(k_refix, dim3((nfix + SCAN_WAVES - 1) / SCAN_WAVES), dim3(64 * SCAN_WAVES), 0, st,

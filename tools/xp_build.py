@@ -1,0 +1,65 @@
+"""Timing-only experiment builds (not products): copy the product sources to a
+scratch directory, apply text patches to clyscan.hip, and build
+couloydb_amd/libexp_<name>.so.  Usage: python tools/xp_build.py NAME [NAME...]
+with NAME one of the PATCHES below."""
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PATCHES = {
+    # no compact-entry stores (tuples come out wrong: timing only)
+    "nocomp": [("    if (idx < CAP_T) __builtin_amdgcn_raw_buffer_store_b128(v, rs.trs, (int)(idx * 16u), 0, 0);",
+                "    if (idx < CAP_T && rs.g->walk_max == 12345678u) __builtin_amdgcn_raw_buffer_store_b128(v, rs.trs, (int)(idx * 16u), 0, 0);")],
+    # no segment-register stores
+    "noseg": [("        if (m > 0)\n            __builtin_amdgcn_raw_buffer_store_b32(Rp, srs,",
+               "        if (m > 0 && g->walk_max == 12345678u)\n            __builtin_amdgcn_raw_buffer_store_b32(Rp, srs,")],
+    # no snapshot stores
+    "nosnap": [("    if (r < CAP_T) __builtin_amdgcn_raw_buffer_store_b32(v, rs.nrs, (int)(r * 4u), 0, 0);",
+                "    if (r < CAP_T && rs.g->walk_max == 12345678u) __builtin_amdgcn_raw_buffer_store_b32(v, rs.nrs, (int)(r * 4u), 0, 0);")],
+}
+PATCHES["nostore"] = PATCHES["nocomp"] + PATCHES["noseg"] + PATCHES["nosnap"]
+# every kernel after k_scan returns at once: k_scan alone is timed, and no
+# kernel reads what a patched k_scan left out (a garbled compact entry sent
+# k_emit's header loads out of bounds once)
+SCAN_ONLY = [("    if (guard >= 0 && g->nfix[guard] == 0) return;  // (device round: nothing was re-resolved)",
+              "    if (g->walk_max != 12345678u) return;"),
+             ("    if (g->nfix[slot] == 0) return;                        // (uniform: before the LDS setup's barrier)",
+              "    if (g->walk_max != 12345678u) return;"),
+             ("    if (g->nfix[slot] || g->spill_over) return;     // the chain is not final yet (k_refix first) / run again",
+              "    if (g->walk_max != 12345678u) return;"),
+             ("    if (g->nfix[slot] || g->spill_over) return;     // k_emit did not run",
+              "    if (g->walk_max != 12345678u) return;")]
+for k in ("nocomp", "noseg", "nosnap", "nostore"):
+    PATCHES[k] = PATCHES[k] + SCAN_ONLY
+PATCHES["base"] = list(SCAN_ONLY)
+PATCHES["run1"] = [("#define RUN_TILES 4", "#define RUN_TILES 1")]
+
+
+def build(name):
+    tmp = tempfile.mkdtemp(prefix="clyxp_")
+    try:
+        shutil.copytree(os.path.join(ROOT, "couloydb_amd", "csrc"), os.path.join(tmp, "couloydb_amd", "csrc"))
+        shutil.copytree(os.path.join(ROOT, "include"), os.path.join(tmp, "include"))
+        p = os.path.join(tmp, "couloydb_amd", "csrc", "clyscan.hip")
+        s = open(p).read()
+        for old, new in PATCHES[name]:
+            assert s.count(old) == 1, (name, old[:60])
+            s = s.replace(old, new)
+        open(p, "w").write(s)
+        out = os.path.join(ROOT, "couloydb_amd", "libexp_%s.so" % name)
+        srcs = ["clyscan.hip", "clymerge.hip", "clyindex.hip", "clyload.hip", "clyorder.hip"]
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                               "-w", "-DCLY_SRC_HASH=\"xp-%s\"" % name, "-o", out] + srcs,
+                              cwd=os.path.dirname(p))
+        print("built", out)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(4) as ex:
+        list(ex.map(build, sys.argv[1:]))
