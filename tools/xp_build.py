@@ -36,21 +36,34 @@ for k in ("nocomp", "noseg", "nosnap", "nostore"):
     PATCHES[k] = PATCHES[k] + SCAN_ONLY
 PATCHES["base"] = list(SCAN_ONLY)
 PATCHES["run1"] = [("#define RUN_TILES 4", "#define RUN_TILES 1")]
+PATCHES["run8"] = [("#define RUN_TILES 4", "#define RUN_TILES 8")]
+PATCHES["run16"] = [("#define RUN_TILES 4", "#define RUN_TILES 16")]
 
 
 def build(name):
+    """NAME: a PATCHES key applied to the working tree, or git:<commit> (that
+    commit's sources as they are; the library is libexp_<commit>.so)."""
     tmp = tempfile.mkdtemp(prefix="clyxp_")
     try:
-        shutil.copytree(os.path.join(ROOT, "couloydb_amd", "csrc"), os.path.join(tmp, "couloydb_amd", "csrc"))
-        shutil.copytree(os.path.join(ROOT, "include"), os.path.join(tmp, "include"))
+        if name.startswith("git:"):
+            commit = name[4:]
+            ar = subprocess.run(["git", "-C", ROOT, "archive", commit, "couloydb_amd/csrc", "include"],
+                                check=True, capture_output=True).stdout
+            subprocess.run(["tar", "-x", "-C", tmp], input=ar, check=True)
+            name, patches = commit, []
+        else:
+            shutil.copytree(os.path.join(ROOT, "couloydb_amd", "csrc"), os.path.join(tmp, "couloydb_amd", "csrc"))
+            shutil.copytree(os.path.join(ROOT, "include"), os.path.join(tmp, "include"))
+            patches = PATCHES[name]
         p = os.path.join(tmp, "couloydb_amd", "csrc", "clyscan.hip")
         s = open(p).read()
-        for old, new in PATCHES[name]:
+        for old, new in patches:
             assert s.count(old) == 1, (name, old[:60])
             s = s.replace(old, new)
         open(p, "w").write(s)
         out = os.path.join(ROOT, "couloydb_amd", "libexp_%s.so" % name)
-        srcs = ["clyscan.hip", "clymerge.hip", "clyindex.hip", "clyload.hip", "clyorder.hip"]
+        srcs = [f for f in ["clyscan.hip", "clymerge.hip", "clyindex.hip", "clyload.hip", "clyorder.hip"]
+                if os.path.exists(os.path.join(os.path.dirname(p), f))]
         subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                                "-w", "-DCLY_SRC_HASH=\"xp-%s\"" % name, "-o", out] + srcs,
                               cwd=os.path.dirname(p))
