@@ -73,7 +73,6 @@ struct Mapped {
     uint32_t fid;
     const uint8_t* p;
     uint64_t len;
-    std::string path;            // the open's copy to the device reads the file with pread
 };
 // Go's strconv.Atoi (64-bit int): an optional sign, decimal digits, no overflow
 static bool go_atoi(const char* s, size_t n, int64_t& v) {
@@ -152,7 +151,7 @@ static inline uint64_t flat_ti(uint64_t v) { return v ? (v & FLAT_TI_MASK) - 1 :
 struct cly_db {
     std::vector<Mapped> files;       // in loadIndex's order (fids as sort.Ints orders the stems)
     std::unordered_map<uint32_t, uint32_t> fid_ix;   // uint32(fid) -> its file
-    Mapped hint = {0, nullptr, 0, std::string()};   // hint-index (tuples 0 .. n_hint-1 are its records)
+    Mapped hint = {0, nullptr, 0};   // hint-index (tuples 0 .. n_hint-1 are its records)
     uint64_t n_hint = 0;
     std::vector<cly_pos> hint_pos;   // DecodeLogRecordPos of each hint record's value
     std::vector<uint64_t> expired;   // tuple indices of the String winners the TTL sweep removed
@@ -267,7 +266,6 @@ static int map_file(const char* path, Mapped& m, bool& exists) {
         void* p = mmap(nullptr, m.len, PROT_READ, MAP_PRIVATE, fd, 0);     // for the host's key reads
         if (p == MAP_FAILED) { close(fd); m.len = 0; return CLY_ERR_ARG; }
         m.p = (const uint8_t*)p;
-        m.path = path;
         close(fd);
         return CLY_OK;
     }
@@ -408,22 +406,19 @@ static int stage_ready() {
     return CLY_OK;
 }
 // The files' bytes to device dev: nt threads (staging buffers of threads t0 ..
-// t0+nt-1) read 64-MiB pieces into the page-locked staging buffers with pread
-// (the kernel copies from the page cache; the mapping, which the host's key
-// reads use later, is not faulted in here), the DMA of one buffer running
-// while the other is filled.  A file without a descriptor, or a short read,
-// is copied from its mapping.  The caller holds g_stage_mu.
-static int copy_to_device(int dev, const std::vector<cly_file>& hf, const std::string* paths, std::vector<cly_file>& df,
-                          uint8_t* d_bytes, int t0, int nt) {
-    struct Piece { const uint8_t* src; uint8_t* dst; uint64_t len; const char* path; uint64_t foff; };
+// t0+nt-1) fault the mapped pages in and copy 64-MiB pieces through the
+// page-locked staging buffers (CPU copy of one while the DMA of the other
+// runs).  The caller holds g_stage_mu.
+static int copy_to_device(int dev, const std::vector<cly_file>& hf, std::vector<cly_file>& df, uint8_t* d_bytes,
+                          int t0, int nt) {
+    struct Piece { const uint8_t* src; uint8_t* dst; uint64_t len; };
     std::vector<Piece> pieces;
     uint64_t off = 0;
     for (size_t i = 0; i < hf.size(); i++) {
         df[i] = hf[i];
         df[i].base = d_bytes + off;
         for (uint64_t a = 0; a < hf[i].len; a += LOAD_PIECE)
-            pieces.push_back({hf[i].base + a, d_bytes + off + a, std::min<uint64_t>(LOAD_PIECE, hf[i].len - a),
-                              paths && !paths[i].empty() ? paths[i].c_str() : nullptr, a});
+            pieces.push_back({hf[i].base + a, d_bytes + off + a, std::min<uint64_t>(LOAD_PIECE, hf[i].len - a)});
         off += (hf[i].len + 4095) & ~4095ull;
     }
     std::atomic<size_t> next(0);
@@ -439,18 +434,16 @@ static int copy_to_device(int dev, const std::vector<cly_file>& hf, const std::s
         bool used[2] = {false, false};
         for (size_t k; (k = next.fetch_add(1)) < pieces.size();) {
             const Piece& pc = pieces[k];
-            const int fd = pc.path ? open(pc.path, O_RDONLY) : -1;
             for (uint64_t a = 0; a < pc.len; a += LOAD_STAGE) {
                 const uint64_t n = std::min<uint64_t>(LOAD_STAGE, pc.len - a);
                 uint8_t* stg = (uint8_t*)g_stage[2 * (t0 + t) + b];
                 if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) err = 1;
-                if (fd < 0 || pread(fd, stg, n, (off_t)(pc.foff + a)) != (ssize_t)n) memcpy(stg, pc.src + a, n);
+                memcpy(stg, pc.src + a, n);
                 if (hipMemcpyAsync(pc.dst + a, stg, n, hipMemcpyHostToDevice, ts) != hipSuccess ||
                     hipEventRecord(ev[b], ts) != hipSuccess) err = 1;
                 used[b] = true;
                 b ^= 1;
             }
-            if (fd >= 0) close(fd);
         }
         if (hipStreamSynchronize(ts) != hipSuccess) err = 1;
         hipEventDestroy(ev[0]); hipEventDestroy(ev[1]);
@@ -656,8 +649,7 @@ struct LoadShard {
     int rc = CLY_OK;
     double t_copy = 0, t_scan = 0;
 };
-static void shard_load(LoadShard& S, const std::vector<cly_file>& hf, const std::vector<std::string>& hfd, int t0,
-                       int nt) {
+static void shard_load(LoadShard& S, const std::vector<cly_file>& hf, int t0, int nt) {
     const int n = S.f1 - S.f0;
     const std::vector<cly_file> h(hf.begin() + S.f0, hf.begin() + S.f1);
     S.df.resize(n); S.res.resize(n); S.first.resize(n);
@@ -665,7 +657,7 @@ static void shard_load(LoadShard& S, const std::vector<cly_file>& hf, const std:
     uint64_t total = 0;
     for (const cly_file& f : h) total += (f.len + 4095) & ~4095ull;
     if (hipMalloc((void**)&S.d_bytes, total + 4096) != hipSuccess) { S.d_bytes = nullptr; S.rc = CLY_ERR_DEVICE; return; }
-    S.rc = copy_to_device(S.dev, h, hfd.data() + S.f0, S.df, S.d_bytes, t0, nt);
+    S.rc = copy_to_device(S.dev, h, S.df, S.d_bytes, t0, nt);
     S.t_copy = now_ms();
     if (S.rc != CLY_OK) return;
     // the tuple buffer sized by the exact record count, once the link knows it
@@ -704,7 +696,6 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
     uint8_t* d_state = nullptr;
     cly_pos* d_hpos = nullptr;
     std::vector<cly_file> hf, df;
-    std::vector<std::string> hfd;    // the files' paths (the copy reads them with pread)
     std::vector<cly_file_result> res;
     std::vector<uint64_t> first;
     std::vector<LoadShard> sh(nctx);
@@ -723,12 +714,10 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
     s.n_files = (uint64_t)nf;
     nall = nf + (has_hint ? 1 : 0);
     hf.resize(nall);
-    hfd.resize(nall);
-    if (has_hint) { hf[0].base = db->hint.p; hf[0].len = db->hint.len; hf[0].fid = 0; hf[0]._pad = 0; hfd[0] = db->hint.path; }
+    if (has_hint) { hf[0].base = db->hint.p; hf[0].len = db->hint.len; hf[0].fid = 0; hf[0]._pad = 0; }
     for (int i = 0; i < nf; i++) {
         cly_file& f = hf[i + (has_hint ? 1 : 0)];
         f.base = db->files[i].p; f.len = db->files[i].len; f.fid = db->files[i].fid; f._pad = 0;
-        hfd[i + (has_hint ? 1 : 0)] = db->files[i].path;
         s.bytes += f.len;
     }
     {
@@ -759,7 +748,7 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
         int slot = 0;
         for (LoadShard& S : sh) {
             if (S.f1 == S.f0) continue;
-            th.emplace_back(shard_load, std::ref(S), std::cref(hf), std::cref(hfd), slot, ntk);
+            th.emplace_back(shard_load, std::ref(S), std::cref(hf), slot, ntk);
             slot += ntk;
         }
         for (auto& x : th) x.join();
