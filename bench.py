@@ -336,6 +336,56 @@ def index_load_leg(wl, sc):
         shutil.rmtree(d, ignore_errors=True)
 
 
+def timed_scans(sc, files, d_out, cap, reps=5):
+    """reps device-resident scans of files (after one untimed): best wall time
+    per scan, the k_scan time, the record count and the statuses."""
+    import torch
+    sc.scan_device(files, d_out, cap)
+    best, kscan, need, res = None, None, 0, None
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        first, res, st, need = sc.scan_device(files, d_out, cap)
+        dt = time.perf_counter() - t0
+        if best is None or dt < best:
+            best, kscan = dt, sc.kernel_ms()["k_scan"]
+    return best, kscan, need, res
+
+
+def small_records_leg(sc, torch, nbytes=1 << 30, seed=0x434C59 + 7):
+    """One device-resident data file of 19-30-B records (0x00||%09d keys,
+    values of 0-11 B, a quarter of them tombstones): every 64-KiB tile holds
+    more than CAP_T records, the spill-chunk path (ReadLogRecord's loop over
+    commit markers / short KVs, data/dataFile.go:64-111)."""
+    from couloydb_amd import _abi
+    gen = _abi.load_gen_lib()
+    rng = np.random.default_rng(seed)
+    n = int(nbytes / 24.5)
+    recs = np.zeros(n, dtype=_abi.GEN_DTYPE)
+    recs["value_len"] = rng.integers(0, 12, n)
+    recs["key_index"] = np.arange(n, dtype=np.int64) % 1_000_000_000
+    recs["type"] = (rng.random(n) < 0.25).astype(np.uint8)
+    recs["value_len"][recs["type"] == 1] = 0
+    fo = (ctypes.c_uint64 * 4)()
+    fl = (ctypes.c_uint64 * 4)()
+    nf = ctypes.c_uint32()
+    total = gen.cly_gen_layout(recs.ctypes.data, n, 1 << 62, 4096, fo, fl, 4, ctypes.byref(nf))
+    d_buf = torch.empty(int(total) + 4096, dtype=torch.uint8, device="cuda")
+    d_recs = torch.from_numpy(recs.view(np.uint8)).to("cuda")
+    if gen.cly_gen_encode(ctypes.c_void_p(d_buf.data_ptr()), ctypes.c_void_p(d_recs.data_ptr()), n, seed) != 0:
+        return {"error": "gen"}
+    del d_recs
+    files = [(d_buf.data_ptr() + int(fo[0]), int(fl[0]), 1)]
+    d_out = torch.empty((n + 1024) * 48, dtype=torch.uint8, device="cuda")
+    t, kscan, need, res = timed_scans(sc, files, d_out.data_ptr(), n + 1024)
+    out = {"value": round(int(fl[0]) / t / 2**30, 2), "unit": "GiB/s", "ms": round(t * 1e3, 3),
+           "k_scan_ms": round(kscan, 3), "bytes": int(fl[0]), "records": int(need),
+           "mean_record_bytes": round(int(fl[0]) / max(1, need), 2),
+           "ok": bool(need == n and res[0].status == 0)}
+    del d_out, d_buf
+    return out
+
+
 def append_leg(wl, sc, first, torch, reps=3):
     """The write path over the whole configuration: every scanned record
     re-appended by cly_append_device (appendLogRecord over a batch, db.go:368-413)
@@ -576,6 +626,7 @@ def main():
     out["index"] = index_info
     if args.config == "c2" and rank == 0 and world == 1 and not args.no_host_path:
         out["append"] = append_leg(wl, sc, first, torch)
+        out["small_records"] = small_records_leg(sc, torch)
     if args.config == "c4":
         mi = dict(merge_info)
         lens = mi.pop("out_lens")
@@ -590,6 +641,12 @@ def main():
         f2, r2, _, n2 = sc.scan_device(mfiles, d2.data_ptr(), cap)
         hf = [(wl.d_hint.data_ptr(), mi["hint_bytes"], 0)]
         f3, r3, _, n3 = sc.scan_device(hf, d2.data_ptr(), cap)
+        # loadIndexFromHintFile's scan (merge.go:257-287) of the merge's hint
+        # file: ~24-B records, every tile past CAP_T (spill chunks)
+        ht, hk, hn, hres = timed_scans(sc, hf, d2.data_ptr(), cap)
+        mi["hint_scan"] = {"value": round(mi["hint_bytes"] / ht / 2**30, 2), "unit": "GiB/s",
+                           "ms": round(ht * 1e3, 3), "k_scan_ms": round(hk, 3), "records": int(hn),
+                           "tb_per_s": round(mi["hint_bytes"] / ht / 1e12, 3)}
         mi["rescan_ok"] = bool(n2 == mi["n_live"] and all(r.status == 0 for r in r2) and n3 == mi["n_live"]
                                and r3[0].status == 0)
         out["merge"] = mi

@@ -35,6 +35,31 @@ SCAN_ONLY = [("    if (guard >= 0 && g->nfix[guard] == 0) return;  // (device ro
 for k in ("nocomp", "noseg", "nosnap", "nostore"):
     PATCHES[k] = PATCHES[k] + SCAN_ONLY
 PATCHES["base"] = list(SCAN_ONLY)
+# counters: blocks that reach the general pass, in-wave agreement rounds (stderr)
+PATCHES["cnt"] = [
+    ("""            if (!done) {
+                // ---- general pass""", """            if (!done) {
+                if (lane == 0) atomicAdd(&g->rounds, 1u);
+                // ---- general pass"""),
+    ("""        const u64 bm = __ballot(bad);
+        if (!bm) return L;""", """        const u64 bm = __ballot(bad);
+        if (!bm) return L;
+        if (lane == 0) atomicAdd((unsigned long long*)&g->walk_dbg, 1ull);"""),
+    ("""    float ms_scan = 0, ms_link = 0, ms_emit = 0, ms_fin = 0;""",
+     """    fprintf(stderr, "xp: general-pass blocks %u, agreement rounds %llu\\n", c->h_g->rounds,
+            (unsigned long long)c->h_g->walk_dbg);
+    float ms_scan = 0, ms_link = 0, ms_emit = 0, ms_fin = 0;"""),
+]
+# the stride round repeated while it takes a full 64 records and the chain stays in the block
+PATCHES["sloop"] = [
+    ("""                if (S.ref_ok) stride_round<BM>(F, S, tb, bs, stg, smem, cl, K4, rs, lane, mk);""",
+     """                for (int sr = 0; sr < 8 && S.ref_ok; sr++) {
+                    const uint32_t c1 = S.tcnt;
+                    stride_round<BM>(F, S, tb, bs, stg, smem, cl, K4, rs, lane, mk);
+                    if (S.tcnt - c1 < 64u || S.dead || S.X >= bs + CLY_BLK) break;
+                }"""),
+]
+PATCHES["sloopcnt"] = PATCHES["sloop"] + PATCHES["cnt"]
 PATCHES["run1"] = [("#define RUN_TILES 4", "#define RUN_TILES 1")]
 PATCHES["run8"] = [("#define RUN_TILES 4", "#define RUN_TILES 8")]
 PATCHES["run16"] = [("#define RUN_TILES 4", "#define RUN_TILES 16")]
