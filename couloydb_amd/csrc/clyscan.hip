@@ -1340,7 +1340,7 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
 // computes every file's first tuple index (exclusive prefix over the files'
 // record totals) and the call's total.
 #define LINK_NT 1024
-#define LINK_MAXT 8192           // tiles per file tracked in the contradiction bitmask (512 MiB files)
+#define LINK_MAXT 65536          // tiles per file tracked in the contradiction bitmask (4-GiB files)
 #define RF_ID 0
 #define RF_CONST 1
 #define RF_FOF 2

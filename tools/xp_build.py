@@ -59,6 +59,55 @@ PATCHES["sloop"] = [
                     if (S.tcnt - c1 < 64u || S.dead || S.X >= bs + CLY_BLK) break;
                 }"""),
 ]
+# section clocks of tile_body (s_memtime, summed over waves) and general-pass counts (stderr)
+PATCHES["prof"] = [
+    ("""    uint64_t walk_dbg;           // (length << 32 | first tile) of the longest k_refix walk
+};""", """    uint64_t walk_dbg;           // (length << 32 | first tile) of the longest k_refix walk
+    unsigned long long xp_t[8];
+};"""),
+    ("""    uint32_t Rp = 0;             // the previous block's segment register (stored at the next block's top)""",
+     """    uint32_t Rp = 0;             // the previous block's segment register (stored at the next block's top)
+    unsigned long long xt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tq = __builtin_amdgcn_s_memtime();
+#define XPT(k) { const unsigned long long tn_ = __builtin_amdgcn_s_memtime(); xt[k] += tn_ - tq; tq = tn_; }"""),
+    ("""            if (S.X == NONE32) S.X = guess_entry(F, bs, stg, hc, lane);    // the tile's guessed entry
+            bool done = true;""", """            XPT(6)
+            if (S.X == NONE32) S.X = guess_entry(F, bs, stg, hc, lane);    // the tile's guessed entry
+            XPT(0)
+            bool done = true;"""),
+    ("""            if (!done) {
+                // ---- general pass""", """            XPT(1)
+            if (!done) {
+                xt[7]++;
+                // ---- general pass"""),
+    ("""                {
+                    L = seg_resolve(K, L, lane, X, g);""", """                XPT(2)
+                {
+                    L = seg_resolve(K, L, lane, X, g);
+                    XPT(3)"""),
+    ("""        {
+            // bytes from the terminal on read as zero""", """        XPT(4)
+        {
+            // bytes from the terminal on read as zero"""),
+    ("""            carry = S.carry_next; cmark = S.cmark_next;
+            S.carry_next = 0; S.cmark_next = false;
+        }""", """            carry = S.carry_next; cmark = S.cmark_next;
+            S.carry_next = 0; S.cmark_next = false;
+        }
+        XPT(5)"""),
+    ("""    if (lane == 0) {
+        ctab[CH_NWORD] = S.nch_have;""", """    if (lane == 0) for (int k = 0; k < 8; k++) atomicAdd(&g->xp_t[k], xt[k]);
+    if (lane == 0) {
+        ctab[CH_NWORD] = S.nch_have;"""),
+    ("""        const u64 bm = __ballot(bad);
+        if (!bm) return L;""", """        const u64 bm = __ballot(bad);
+        if (!bm) { if (lane == 0 && iter) atomicAdd((unsigned long long*)&g->walk_dbg, (unsigned long long)iter << 40); return L; }"""),
+    ("""    float ms_scan = 0, ms_link = 0, ms_emit = 0, ms_fin = 0;""",
+     """    fprintf(stderr, "xp: guess %llu pred %llu gen-walk %llu resolve %llu gen-out %llu crc %llu stage %llu | general blocks %llu resolve iters %llu\\\\n",
+            c->h_g->xp_t[0], c->h_g->xp_t[1], c->h_g->xp_t[2], c->h_g->xp_t[3], c->h_g->xp_t[4], c->h_g->xp_t[5],
+            c->h_g->xp_t[6], c->h_g->xp_t[7], (unsigned long long)(c->h_g->walk_dbg >> 40));
+    float ms_scan = 0, ms_link = 0, ms_emit = 0, ms_fin = 0;"""),
+]
 PATCHES["sloopcnt"] = PATCHES["sloop"] + PATCHES["cnt"]
 PATCHES["run1"] = [("#define RUN_TILES 4", "#define RUN_TILES 1")]
 PATCHES["run8"] = [("#define RUN_TILES 4", "#define RUN_TILES 8")]
