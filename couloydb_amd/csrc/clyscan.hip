@@ -97,17 +97,48 @@ struct DevFile {                 // 32 B
     uint32_t ntile;              // tiles of the file (>= 1)
     uint32_t _pad;
 };
+// Files of any length (Options.DataFileSize is an int64, options.go:10,70-71)
+// are walked in parts of PART_TILES tiles: inside a part every position is a
+// u32 offset from the part's first byte x0 (the tile body, TileLocal, the
+// compact entries), and the part's view of the file is its bytes and up to
+// VIEW_MAX past x0 (a record that crosses the part's end is read whole: records
+// are below VIEW_MAX - PART_BYTES, 2 GiB - 128 KiB).  The chain state between tiles (k_link, TileIn), the
+// terminal and failure positions and every tuple offset are u64 file offsets.
+// A file below PART_BYTES is one part (x0 = 0).
+#define PART_TILES 32768u
+#define PART_BYTES ((uint64_t)PART_TILES * CLY_TILE)
+#define VIEW_MAX (0xFFFFFFFFull - 2 * (uint64_t)CLY_TILE)
+#define P_NONE 0xFFFFFFFFFFFFull  // no record start (u64 positions; files are below 2^48 B)
+static_assert(PART_TILES % RUN_TILES == 0, "a run of tiles stays in one part");
+static_assert(PART_BYTES < VIEW_MAX, "a part's view: its bytes and a record that crosses its end");
+__device__ __forceinline__ uint64_t part_x0(uint32_t tt) { return (uint64_t)(tt / PART_TILES) * PART_BYTES; }
+// file F as tile tt's part sees it (base at x0, u32 length), and tt's index in the part
+__device__ __forceinline__ DevFile part_view(const DevFile& F, uint32_t tt, uint32_t& ptt) {
+    const uint64_t x0 = part_x0(tt);
+    ptt = tt % PART_TILES;
+    DevFile V = F;
+    V.base = F.base + x0;
+    V.len = F.len - x0 < VIEW_MAX ? F.len - x0 : VIEW_MAX;
+    return V;
+}
 
-struct FileInfo {                // per file, zeroed per call (fail_key: all ones)
+struct FileInfo {                // per file, zeroed per call (fail_off, fail_idx: all ones)
     uint64_t first_index;        // global tuple index of the file's first record
     uint64_t end_index;          // global index after the file's last record
-    uint32_t term_pos;           // terminal position T of the file's chain
+    uint64_t term_pos;           // terminal position T of the file's chain
+    // the first record whose CRC fails: its offset and its index in the file,
+    // two atomicMins (records are in offset order: both minima are the same record's)
+    u64      fail_off, fail_idx;
     int32_t  term_status;
     uint32_t term_tile;          // global tile index holding T
     uint32_t has_term;
-    u64      fail_key;           // (offset << 32) | index in file of the first record whose CRC fails (atomicMin)
-    uint32_t _r0, _r1;
+    uint32_t _r0;
+    uint64_t _r1;
 };
+__device__ __forceinline__ void fail_at(FileInfo* fo, uint64_t off, uint64_t idx) {
+    atomicMin(&fo->fail_off, (u64)off);
+    atomicMin(&fo->fail_idx, (u64)idx);
+}
 
 // Tile LOCAL (the tile's chain under its own entry), written by k_scan / k_refix:
 // l[0]: bit1 the chain ends in the tile | bit2 no boundary in the tile | bit3
@@ -492,32 +523,35 @@ __device__ __forceinline__ SegChain seg_resolve(const Seg& K, SegChain L, int la
 // Chain state between tiles (k_link).
 struct LBState {
     uint64_t count;              // records before (file-relative in TileIn)
-    uint32_t X;                  // chain position
-    uint32_t crc_last;           // stored CRC of the last record started before (its successor's Q)
-    uint32_t P_last;             // that record's start (NONE32: none in this file)
+    uint64_t X;                  // chain position (file offset)
+    uint64_t P_last;             // the last record started before: its start (P_NONE: none in this file)
+    uint32_t crc_last;           // ... and its stored CRC (its successor's Q)
     int      dead;               // the file's chain has ended
 };
 // TileIn (k_link): the true state entering a tile, 32 B:
-//   w[0..1] count (file-relative), w[2] X, w[3] dead, w[4] crc_last, w[5] P_last
+//   w[0..1] count (file-relative), w[2] X (low word), w[3] dead | fix, w[4] crc_last,
+//   w[5] P_last (low word), w[6] the tile's file (k_emit), w[7] X >> 32 | (P_last >> 32) << 16
 struct TileIn { uint32_t w[8]; };
 #define TI_DEAD 1u
 __device__ __forceinline__ LBState ti_load(const TileIn* p) {
     const u32x4 a = ((const u32x4*)p)[0], b = ((const u32x4*)p)[1];
     LBState s;
-    s.count = ((uint64_t)a.y << 32) | a.x; s.X = a.z; s.dead = (a.w & TI_DEAD) != 0; s.crc_last = b.x; s.P_last = b.y;
+    s.count = ((uint64_t)a.y << 32) | a.x; s.dead = (a.w & TI_DEAD) != 0; s.crc_last = b.x;
+    s.X = a.z | ((uint64_t)(b.w & 0xFFFFu) << 32);
+    s.P_last = b.y | ((uint64_t)(b.w >> 16) << 32);
     return s;
 }
 #define TI_FIX 2u                // listed for k_refix this round
-// (word 6: the tile's file, for k_emit)
 __device__ __forceinline__ void ti_store(TileIn* p, const LBState& s, uint32_t f) {
-    ((u32x4*)p)[0] = (u32x4){(uint32_t)s.count, (uint32_t)(s.count >> 32), s.X, s.dead ? TI_DEAD : 0u};
-    ((u32x4*)p)[1] = (u32x4){s.crc_last, s.P_last, f, 0u};
+    ((u32x4*)p)[0] = (u32x4){(uint32_t)s.count, (uint32_t)(s.count >> 32), (uint32_t)s.X, s.dead ? TI_DEAD : 0u};
+    ((u32x4*)p)[1] = (u32x4){s.crc_last, (uint32_t)s.P_last, f,
+                             ((uint32_t)(s.X >> 32) & 0xFFFFu) | ((uint32_t)(s.P_last >> 32) << 16)};
 }
 
 // ---------------------------------------------------------------------------
 // Outputs of one record.  Tuple (48 B, cly_tuple layout):
-__device__ __forceinline__ void tuple_words(gbytes base, uint32_t p, const Hdr& h, uint32_t fid, u32x4& a, u32x4& b,
-                                            u32x4& c) {
+__device__ __forceinline__ void tuple_words(gbytes base, uint32_t p, uint64_t x0, const Hdr& h, uint32_t fid, u32x4& a,
+                                            u32x4& b, u32x4& c) {
     int tn;
     int64_t tx;
     if (h.key0 < 0x80 && h.ks >= 1) { tn = 1; tx = (int64_t)(h.key0 >> 1) ^ -(int64_t)(h.key0 & 1); }
@@ -525,7 +559,7 @@ __device__ __forceinline__ void tuple_words(gbytes base, uint32_t p, const Hdr& 
         const int64_t klim = h.ks < 11u ? (int64_t)h.ks : 11;
         tx = go_varint(base + p + h.hsz, klim, tn);                     // parseLogRecordKey, db.go:706-710
     }
-    const uint64_t off = p, ex = (uint64_t)h.exp, txv = tn < 0 ? 0ull : (uint64_t)tx;
+    const uint64_t off = x0 + p, ex = (uint64_t)h.exp, txv = tn < 0 ? 0ull : (uint64_t)tx;
     a = (u32x4){(uint32_t)off, (uint32_t)(off >> 32), (uint32_t)ex, (uint32_t)(ex >> 32)};
     b = (u32x4){(uint32_t)txv, (uint32_t)(txv >> 32), fid, (uint32_t)h.size};
     c = (u32x4){h.ks, h.vs,
@@ -667,6 +701,9 @@ __device__ __forceinline__ void patch_word(uint32_t (&w)[16], uint32_t k, uint32
 #define BM_SPEC 0
 #define BM_EXACT 1
 #define PW_ROUNDS 1              // pred_walk rounds per block before the general pass (C3: 1 round 12.7 ms, 2 13.6, 4 15.4)
+#ifndef GP_TRIES
+#define GP_TRIES 2               // candidates a general-pass lane walks for its first chain (small records: 1 try 4.90 ms, 2: 4.59, 5: 4.39 per GiB; C3: 5 tries +0.2 ms)
+#endif
 // Per-tile CRC outputs of the tile body: the segment registers (one per 64-B
 // segment of the tile, stream order) and the records' snapshots (indexed like
 // the compact entries; boundary CAP_T is the last one kept)
@@ -978,7 +1015,8 @@ __device__ __forceinline__ uint32_t guess_entry(const DevFile& F, uint32_t bs, C
 }
 
 template <int BM>
-__device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint32_t tt, uint32_t X_in, bool dead_in,
+__device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint32_t tt, bool first, uint32_t X_in,
+                                             bool dead_in,
                                              const CLY_LDS uint8_t* smem, CLY_LDS uint32_t* stg, CLY_LDS uint32_t* mk,
                                              const CrcLane& cl, uint32_t K4, TileLocal* loc,
                                              uint32_t* rec, uint32_t* seg, uint32_t* snap, uint32_t* treg,
@@ -990,11 +1028,11 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     const uint64_t flen = F.len;
     const gbytes base = (gbytes)F.base;
     // (BM_SPEC: X_in is NONE32 for a guessed entry, else the exit of the run's previous tile)
-    const bool known0 = BM != BM_SPEC || tt == 0 || X_in != NONE32;
+    const bool known0 = BM != BM_SPEC || first || X_in != NONE32;
     TState S;
-    S.X = tt == 0 ? 0u : (known0 ? X_in : NONE32);
-    S.dead = tt != 0 && known0 && dead_in;
-    S.cq_known = tt == 0;        // tile 0: no record before offset 0
+    S.X = first ? 0u : (known0 ? X_in : NONE32);
+    S.dead = !first && known0 && dead_in;
+    S.cq_known = first;          // the file's first tile: no record before offset 0
     S.cq = 0; S.G = NONE32; S.tcnt = 0; S.last_crc = 0; S.P_last = NONE32; S.term = TERM_NONE;
     S.s_last = 0; S.s_prev = 0; S.Tb = NONE32; S.tpatch = 0; S.carry_next = 0; S.cmark_next = false;
     S.ref_ok = false; S.ref_s = 0; S.ref1 = S.ref2 = S.ref3 = S.msk1 = S.msk2 = S.msk3 = S.rw1 = S.rw2 = S.rw3 = 0;
@@ -1092,10 +1130,40 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                 const uint32_t X = S.X;
                 if (!K.on) sc_set(L, LM_OFF);
                 else if (in_seg(K, X)) seg_walk(K, X, true, L);
-                else if (X > K.cb) sc_set(L, LM_NONE);
-                else {
-                    sc_set(L, LM_NONE);
-                    if (cm) { SegChain T; if (seg_walk(K, K.cb + (uint32_t)__builtin_ctzll(cm), false, T)) L = T; }
+                else sc_set(L, LM_NONE);
+                {
+                    // a segment after X: the chain of its first candidate whose
+                    // speculative walk holds and leaves at a candidate of the
+                    // block (or beyond it), else of the first whose walk holds.
+                    // A false start's walk (dense records: the bytes of a
+                    // record's expiration and key read as a header) rarely
+                    // leaves at a candidate; each lane it picks would cost
+                    // seg_resolve a serial exact re-walk.
+                    u64 mm = (K.on && X < K.cb) ? cm : 0ull;
+                    bool fb = false;                               // L holds a fallback chain
+                    for (int tr = 0; tr < GP_TRIES; tr++) {
+                        const bool act = mm != 0ull;
+                        if (!__ballot(act)) break;
+                        SegChain T;
+                        sc_set(T, LM_NONE);
+                        bool ok = false;
+                        if (act) {
+                            const uint32_t q = K.cb + (uint32_t)__builtin_ctzll(mm);
+                            mm &= mm - 1;
+                            ok = seg_walk(K, q, false, T);
+                        }
+                        const bool chk = ok && T.term == TERM_NONE && T.x < bs + CLY_BLK;
+                        const uint32_t off = chk ? T.x - bs : 0u;
+                        const int tl = (int)(off >> 6);
+                        const uint32_t clo = shfl_u32((uint32_t)cm, tl), chi = shfl_u32((uint32_t)(cm >> 32), tl);
+                        bool conf = ok;
+                        if (chk) {
+                            const uint32_t bb = off & 63u;
+                            conf = ((bb < 32 ? clo >> bb : chi >> (bb - 32)) & 1u) != 0;
+                        }
+                        if (conf) { L = T; mm = 0; }
+                        else if (ok && !fb) { L = T; fb = true; }
+                    }
                 }
                 {
                     L = seg_resolve(K, L, lane, X, g);
@@ -1219,7 +1287,7 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
         u64 f0 = (u64)S.tcnt << 32;
         if (S.term != TERM_NONE) f0 |= DF_TERM;
         if (S.G == NONE32) f0 |= DF_NONE;
-        if (tt == 0) f0 |= DF_FOF;
+        if (first) f0 |= DF_FOF;
         if (S.P_last != NONE32) f0 |= DF_REC;
         TileLocal* d = &loc[t];
         d->l[0] = f0;
@@ -1289,8 +1357,9 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     uint32_t t = files[f].first_tile + (r - rprefix[f]) * RUN_TILES;
     u32x4 e[4], hl;
     {
-        const DevFile F = files[f];
-        tile_issue(F, t - F.first_tile, lane, e, hl);
+        uint32_t ptt;
+        const DevFile V = part_view(files[f], t - files[f].first_tile, ptt);
+        tile_issue(V, ptt, lane, e, hl);
     }
     uint32_t Xc = NONE32;        // the entry carried from the run's previous tile (NONE32: guess)
     for (;;) {
@@ -1307,11 +1376,15 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         const uint8_t* nbase = nullptr;
         uint32_t nlen = 0, ntb = 0;
         if (fn >= 0) {
-            nbase = files[fn].base; nlen = (uint32_t)files[fn].len;
-            ntb = (tn - files[fn].first_tile) * (uint32_t)CLY_TILE;
+            uint32_t pn;
+            const DevFile Vn = part_view(files[fn], tn - files[fn].first_tile, pn);
+            nbase = Vn.base; nlen = (uint32_t)Vn.len;
+            ntb = pn * (uint32_t)CLY_TILE;
         }
-        const TileRes res = tile_body<BM_SPEC>(F, t, t - F.first_tile, Xc, false, smem, stg, mk, cl, K4, loc, rec, seg,
-                                               snap, treg, chk, chunks, sp_rec, sp_snap, g, e, hl, nbase, nlen, ntb);
+        uint32_t ptt;
+        const DevFile V = part_view(F, t - F.first_tile, ptt);
+        const TileRes res = tile_body<BM_SPEC>(V, t, ptt, t == F.first_tile, Xc, false, smem, stg, mk, cl, K4, loc, rec,
+                                               seg, snap, treg, chk, chunks, sp_rec, sp_snap, g, e, hl, nbase, nlen, ntb);
         if (fn < 0) break;
         // a chain that ended in this tile is not carried: past the file's true
         // end nothing reads the tiles, and a false chain's terminal must not
@@ -1340,36 +1413,42 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
 // computes every file's first tuple index (exclusive prefix over the files'
 // record totals) and the call's total.
 #define LINK_NT 1024
-#define LINK_MAXT 65536          // tiles per file tracked in the contradiction bitmask (4-GiB files)
+#define LINK_MAXT 131072         // tiles per file tracked in the contradiction bitmask (8-GiB files)
 #define RF_ID 0
 #define RF_CONST 1
 #define RF_FOF 2
-struct RunF { uint32_t kind, X, crc, P, dead, rec; uint64_t cnt; };
-__device__ __forceinline__ RunF rf_tile(u64 l0, u64 l1, u64 l2) {
+#define RF_DEAD 4u
+#define RF_REC 8u
+// a run of tiles as a function of the state entering it; positions are file
+// offsets (a tile's LOCAL positions are its part's: x0 added)
+struct RunF { uint64_t X, P, cnt; uint32_t crc, fl; };   // fl: kind | RF_DEAD | RF_REC
+__device__ __forceinline__ RunF rf_tile(u64 l0, u64 l1, u64 l2, uint64_t x0) {
     RunF f;
-    f.kind = (l0 & DF_FOF) ? RF_FOF : (l0 & DF_NONE) ? RF_ID : RF_CONST;
-    f.X = (uint32_t)(l1 >> 32);
-    f.dead = (l0 & DF_TERM) != 0;
+    const uint32_t kind = (l0 & DF_FOF) ? RF_FOF : (l0 & DF_NONE) ? RF_ID : RF_CONST;
+    f.X = x0 + (l1 >> 32);
     f.cnt = l0 >> 32;
-    f.rec = (l0 & DF_REC) || (l0 & DF_FOF);
+    f.fl = kind | ((l0 & DF_TERM) ? RF_DEAD : 0u) | (((l0 & DF_REC) || (l0 & DF_FOF)) ? RF_REC : 0u);
     f.crc = (l0 & DF_REC) ? (uint32_t)l2 : 0u;
-    f.P = (l0 & DF_REC) ? (uint32_t)(l2 >> 32) : NONE32;
+    f.P = (l0 & DF_REC) ? x0 + (l2 >> 32) : P_NONE;
     return f;
 }
 // g after f
 __device__ __forceinline__ RunF rf_then(const RunF& f, const RunF& g) {
-    if (g.kind == RF_FOF || f.kind == RF_ID) return g;
-    if (g.kind == RF_ID || f.dead) return f;
+    const uint32_t fk = f.fl & 3u, gk = g.fl & 3u;
+    if (gk == RF_FOF || fk == RF_ID) return g;
+    if (gk == RF_ID || (f.fl & RF_DEAD)) return f;
     RunF h = f;
-    h.X = g.X; h.dead = g.dead; h.cnt = f.cnt + g.cnt;
-    if (g.rec) { h.crc = g.crc; h.P = g.P; h.rec = 1; }
+    h.X = g.X; h.cnt = f.cnt + g.cnt;
+    h.fl = (f.fl & ~RF_DEAD) | (g.fl & RF_DEAD);
+    if (g.fl & RF_REC) { h.crc = g.crc; h.P = g.P; h.fl |= RF_REC; }
     return h;
 }
 __device__ __forceinline__ LBState rf_apply(const RunF& f, LBState s) {
-    if (f.kind == RF_ID || (f.kind == RF_CONST && s.dead)) return s;
-    s.count = (f.kind == RF_FOF ? 0 : s.count) + f.cnt;
-    s.X = f.X; s.dead = f.dead;
-    if (f.rec) { s.crc_last = f.crc; s.P_last = f.P; }
+    const uint32_t fk = f.fl & 3u;
+    if (fk == RF_ID || (fk == RF_CONST && s.dead)) return s;
+    s.count = (fk == RF_FOF ? 0 : s.count) + f.cnt;
+    s.X = f.X; s.dead = (f.fl & RF_DEAD) != 0;
+    if (f.fl & RF_REC) { s.crc_last = f.crc; s.P_last = f.P; }
     return s;
 }
 #define LINK_PER 4               // tiles per thread held in registers (more: re-read)
@@ -1396,11 +1475,11 @@ k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restric
         if (lo + k < hi) { c0[k] = L0[lo + k].l[0]; c1[k] = L0[lo + k].l[1]; c2[k] = L0[lo + k].l[2]; c3[k] = L0[lo + k].l[3]; }
     }
     RunF my;
-    my.kind = RF_ID; my.X = 0; my.crc = 0; my.P = NONE32; my.dead = 0; my.rec = 0; my.cnt = 0;
+    my.fl = RF_ID; my.X = 0; my.crc = 0; my.P = P_NONE; my.cnt = 0;
     #pragma unroll
     for (int k = 0; k < LINK_PER; k++)
-        if (lo + k < hi) my = rf_then(my, rf_tile(c0[k], c1[k], c2[k]));
-    for (uint32_t u = lo + LINK_PER; u < hi; u++) my = rf_then(my, rf_tile(L0[u].l[0], L0[u].l[1], L0[u].l[2]));
+        if (lo + k < hi) my = rf_then(my, rf_tile(c0[k], c1[k], c2[k], part_x0(lo + k)));
+    for (uint32_t u = lo + LINK_PER; u < hi; u++) my = rf_then(my, rf_tile(L0[u].l[0], L0[u].l[1], L0[u].l[2], part_x0(u)));
     // inclusive Kogge-Stone scan of the run functions
     int cur = 0;
     rf[0][tid] = my;
@@ -1415,19 +1494,20 @@ k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restric
         __syncthreads();
     }
     LBState s;
-    s.count = 0; s.X = 0; s.crc_last = 0; s.P_last = NONE32; s.dead = 0;
+    s.count = 0; s.X = 0; s.crc_last = 0; s.P_last = P_NONE; s.dead = 0;
     if (tid > 0) s = rf_apply(rf[cur][tid - 1], s);
     if (tid == LINK_NT - 1) {
         LBState s0;
-        s0.count = 0; s0.X = 0; s0.crc_last = 0; s0.P_last = NONE32; s0.dead = 0;
+        s0.count = 0; s0.X = 0; s0.crc_last = 0; s0.P_last = P_NONE; s0.dead = 0;
         ftotal[f] = rf_apply(rf[cur][tid], s0).count;
     }
     auto visit = [&](uint32_t u, u64 l0, u64 l1, u64 l2, u64 l3) {
         bool bad = false;
-        if (l0 & DF_FOF) { s.count = 0; s.X = 0; s.dead = 0; s.crc_last = 0; s.P_last = NONE32; }
+        const uint64_t x0 = part_x0(u);
+        if (l0 & DF_FOF) { s.count = 0; s.X = 0; s.dead = 0; s.crc_last = 0; s.P_last = P_NONE; }
         else if (!s.dead) {
-            if (l0 & DF_NONE) bad = s.X < (uint32_t)l3;
-            else bad = s.X != (uint32_t)l1;
+            if (l0 & DF_NONE) bad = s.X < x0 + (uint32_t)l3;
+            else bad = s.X != x0 + (uint32_t)l1;
         }
         ti_store(&tin[F.first_tile + u], s, (uint32_t)f);
         if (bad) {
@@ -1435,7 +1515,7 @@ k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restric
             else atomicMin(&bad_far, u);
         } else if (u < LINK_MAXT && (u == 0 || (u % RUN_TILES == 0 && !(l0 & DF_NONE))))
             atomicOr(&ancm[u >> 5], 1u << (u & 31));
-        s = rf_apply(rf_tile(l0, l1, l2), s);
+        s = rf_apply(rf_tile(l0, l1, l2, x0), s);
     };
     #pragma unroll
     for (int k = 0; k < LINK_PER; k++)
@@ -1535,8 +1615,9 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
     // entry of a later one is the walk's exit, not its stale TileIn
     if (t > F.first_tile && (tin[t - 1].w[3] & TI_FIX)) return;
     const LBState S0 = ti_load(&tin[t]);
-    uint32_t X = S0.X;
     bool dead = S0.dead != 0;
+    // X: the chain position in the current tile's part
+    uint32_t X = dead ? 0u : (uint32_t)(S0.X - part_x0(t - F.first_tile));
     const uint32_t t_start = t;
     for (;;) {
         // Suffix: the true entry is the start of the guessed chain's record j
@@ -1545,7 +1626,9 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
         // skips their compact entries and snapshots) instead of walking the
         // tile again; its exit stays.
         const u64 l0 = loc[t].l[0], l1 = loc[t].l[1];
-        const uint32_t n = (uint32_t)(l0 >> 32), tb = (t - F.first_tile) * (uint32_t)CLY_TILE;
+        uint32_t ptt;
+        const DevFile V = part_view(F, t - F.first_tile, ptt);
+        const uint32_t n = (uint32_t)(l0 >> 32), tb = ptt * (uint32_t)CLY_TILE;
         bool shortcut = false;
         if (!dead && !(l0 & (DF_NONE | DF_FOF)) && n > 1 && ((loc[t].l[3] >> 40) & 0xFFFFu) == 0) {
             const uint32_t nn = n < 64u ? n : 64u;
@@ -1565,10 +1648,10 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
         }
         if (!shortcut) {
             u32x4 e[4], hl;
-            tile_issue(F, t - F.first_tile, lane, e, hl);
-            const TileRes r = tile_body<BM_EXACT>(F, t, t - F.first_tile, X, dead, smem, stg, mk, cl, K4, loc, rec,
-                                                  seg, snap, treg, chk, chunks, sp_rec, sp_snap, g, e, hl, nullptr,
-                                                  0u, 0u);
+            tile_issue(V, ptt, lane, e, hl);
+            const TileRes r = tile_body<BM_EXACT>(V, t, ptt, t == F.first_tile, X, dead, smem, stg, mk, cl, K4, loc,
+                                                  rec, seg, snap, treg, chk, chunks, sp_rec, sp_snap, g, e, hl,
+                                                  nullptr, 0u, 0u);
             X = r.X; dead = r.dead;
         }
         if (dead || t + 1 >= F.first_tile + F.ntile) break;
@@ -1576,6 +1659,7 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
         // own (it starts a run); any other next tile: consistent with the new
         // exit?  else it is re-resolved here too
         if ((tin[t + 1].w[3] & TI_FIX) && !(tin[t].w[3] & TI_FIX)) break;
+        if (ptt + 1 == PART_TILES) X -= (uint32_t)PART_BYTES;           // into the next part
         const u64 n0 = loc[t + 1].l[0], n1 = loc[t + 1].l[1], n3 = loc[t + 1].l[3];
         const bool ok = (n0 & DF_NONE) ? X >= (uint32_t)n3 : X == (uint32_t)n1;
         if (ok) break;
@@ -1731,11 +1815,14 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         const LBState S = ti_load(&tin[t]);
         if (S.dead) continue;
         const int f = (int)__builtin_amdgcn_readfirstlane(((const uint32_t*)&tin[t])[6]);
-        const DevFile F = files[f];
+        const uint32_t tt = t - files[f].first_tile;
+        uint32_t ptt;
+        const DevFile F = part_view(files[f], tt, ptt);                    // positions below: the part's
+        const uint64_t x0 = part_x0(tt);
         FileInfo* fo = &finfo[f];
         const uint64_t gb = S.count + fo->first_index;
         const u64 l0 = loc[t].l[0], l1 = loc[t].l[1], l3 = loc[t].l[3];
-        const uint32_t tt = t - F.first_tile, tb = (uint32_t)((uint64_t)tt * CLY_TILE), TE = tb + (uint32_t)CLY_TILE;
+        const uint32_t tb = ptt * (uint32_t)CLY_TILE, TE = tb + (uint32_t)CLY_TILE;
         const uint32_t n = (uint32_t)(l0 >> 32);
         const uint32_t skip = (uint32_t)(l3 >> 40) & 0xFFFFu;              // k_refix's suffix (records dropped)
         const gbytes base = (gbytes)F.base;
@@ -1834,12 +1921,12 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                         const uint32_t ks = v.y & 0xFFFFFFu, hsz = 6u + ((v.y >> 24) & 31u), type = v.y >> 29;
                         const uint32_t dt = (v.w >> 16) & 7u, key0 = (v.w >> 19) & 0x7Fu;
                         const uint64_t tx = (uint64_t)((int64_t)(key0 >> 1) ^ -(int64_t)(key0 & 1u));
-                        a = (u32x4){p, 0u, 0u, 0u};
+                        a = (u32x4){(uint32_t)(x0 + p), (uint32_t)((x0 + p) >> 32), 0u, 0u};
                         b = (u32x4){(uint32_t)tx, (uint32_t)(tx >> 32), F.fid, hsz + ks + v.z};
                         c = (u32x4){ks, v.z, type | (dt << 8) | (hsz << 16) | (1u << 24), v.x};
                     } else {
                         const Hdr h = hdr_load(base, p, F.len);
-                        tuple_words(base, p, h, F.fid, a, b, c);
+                        tuple_words(base, p, x0, h, F.fid, a, b, c);
                     }
                     sv[3 * lane] = a; sv[3 * lane + 1] = b; sv[3 * lane + 2] = c;
                     if (!full) {
@@ -1872,7 +1959,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                         const uint32_t val = q.kind ? chk_eval(emt, gin, q, tb) : 0u;
                         if ((q.kind == 1 && val != q.expn) || (q.kind == 2 && val != 0u) ||
                             (q.kind == 3 && term && (val ^ cout) != 0u))
-                            atomicMin(&fo->fail_key, ((u64)p << 32) | (S.count + i));
+                            fail_at(fo, x0 + p, S.count + i);
                         const u64 bl = __ballot(q.kind == 3);
                         if (bl) ex = rdl(val, __ffsll((long long)bl) - 1) ^ cout;
                     }
@@ -1969,7 +2056,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                     // when its patch word is there, else the scan's register
                     ex = wlast == TE ? exp_post(plast & 3u, clast, kj) : gte ^ cout;
                     if (term && ex != 0u && lane == 0)                      // the record ending at the terminal
-                        atomicMin(&fo->fail_key, ((u64)(uint32_t)(loc[t].l[2] >> 32) << 32) | (S.count + n - 1));
+                        fail_at(fo, x0 + (uint32_t)(loc[t].l[2] >> 32), S.count + n - 1);
                     // every record that ends at a record start inside the tile
                     for (uint32_t i = lane; i + 1 < n; i += 64) {
                         const u32x4 v = E.ent(i), v2 = E.ent(i + 1);
@@ -1980,7 +2067,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                         const uint32_t pre = sg2 == sg ? s2 ^ em_f4(emt, (W2 - W) >> 2, s1 ^ exp_post(p & 3u, c1, kj))
                                                        : em_f4(emt, (W2 - tb - 64u * sg2) >> 2, gin[gin_at(sg2, false)]) ^ s2;
                         if (pre != exp_pre(emt, P2 & 3u, c1, c2))
-                            atomicMin(&fo->fail_key, ((u64)p << 32) | (S.count + i));
+                            fail_at(fo, x0 + p, S.count + i);
                     }
                 }
             }
@@ -1989,7 +2076,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             treg[2 * t] = ex;
             treg[2 * t + 1] = dev;
             if (term) {
-                fo->term_pos = T;
+                fo->term_pos = x0 + T;
                 fo->term_status = (int32_t)(int8_t)(uint8_t)(l3 >> 32);
                 fo->term_tile = t;
                 fo->end_index = gb + n;
@@ -2065,12 +2152,12 @@ k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __rest
         if (u > 0) {
             const LBState S = ti_load(&tin[t]);
             const uint32_t n = (uint32_t)(l0 >> 32), G = (uint32_t)loc[t].l[1];
-            const uint32_t tb = (uint32_t)((uint64_t)u * CLY_TILE), TE = tb + (uint32_t)CLY_TILE;
+            const uint32_t tb = (u % PART_TILES) * (uint32_t)CLY_TILE, TE = tb + (uint32_t)CLY_TILE;   // (the part's)
             uint32_t dev = treg[2 * t + 1];
             if ((l0 & DF_TERM) && n == 0) dev ^= shift_b(sht, TE - G, S.crc_last);     // G is the terminal
             else dev = shift_b(sht, TE - patch_word_of(G), dev);
             if (mat_mul(tilet, y) != dev)
-                atomicMin(&fo->fail_key, ((u64)S.P_last << 32) | (uint64_t)(S.count - 1));
+                fail_at(fo, S.P_last, S.count - 1);
         }
         y = v;
     }
@@ -2242,8 +2329,8 @@ static int ensure_spill(cly_ctx* c, uint64_t chunks) {
     return CLY_OK;
 }
 
-// the largest file length the tile arithmetic (u32 offsets) takes
-#define MAX_FILE_LEN (0xFFFFFFFFull - 2 * (uint64_t)CLY_TILE)
+// the largest file length: u64 chain positions in TileIn keep 48 bits (P_NONE above them)
+#define MAX_FILE_LEN ((1ull << 47) - 1)
 
 // alloc != nullptr: the output is allocated here (hipMalloc, the caller frees
 // it) once the link knows the exact record count, so that it holds exactly
@@ -2286,7 +2373,7 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
     memset(c->h_g, 0, sizeof(Globals));
     c->h_g->spill_cap = c->cap_spill;
     memset(c->h_finfo, 0, sizeof(FileInfo) * nfiles);
-    for (int i = 0; i < nfiles; i++) c->h_finfo[i].fail_key = ~0ull;
+    for (int i = 0; i < nfiles; i++) c->h_finfo[i].fail_off = c->h_finfo[i].fail_idx = ~0ull;
     HIPCK(hipMemcpyAsync(c->d_call, c->h_call, c->call_bytes, hipMemcpyHostToDevice, st));
     const uint32_t nt32 = (uint32_t)ntiles;
     int grid = c->scan_grid;
@@ -2410,13 +2497,13 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
     for (int i = 0; i < nfiles; i++) {
         const FileInfo& fi = c->h_finfo[i];
         file_first[i] = fi.first_index;
-        if (fi.fail_key == ~0ull) {              // every record matches its CRC
+        if (fi.fail_idx == ~0ull) {              // every record matches its CRC
             res[i].n_records = fi.end_index - fi.first_index;
-            res[i].end_offset = fi.term_pos;
+            res[i].end_offset = (int64_t)fi.term_pos;
             res[i].status = fi.term_status;
         } else {                                 // the first record whose CRC fails
-            res[i].n_records = fi.fail_key & 0xffffffffull;
-            res[i].end_offset = (int64_t)(fi.fail_key >> 32);
+            res[i].n_records = fi.fail_idx;
+            res[i].end_offset = (int64_t)fi.fail_off;
             res[i].status = CLY_ERR_CRC;
         }
         res[i]._pad = 0;

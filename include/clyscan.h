@@ -46,7 +46,7 @@ extern "C" {
 #define CLY_OK              0
 #define CLY_ERR_CAPACITY  -10  /* out_cap too small for the records found            */
 #define CLY_ERR_DEVICE    -11  /* HIP runtime error                                  */
-#define CLY_ERR_ARG       -12  /* bad argument (null pointer, file >= 4 GiB, ...)    */
+#define CLY_ERR_ARG       -12  /* bad argument (null pointer, file >= 2^47 B, ...)   */
 #define CLY_ERR_NOREPAIR  -13  /* speculation repair did not converge (never seen)   */
 
 /* A data file (`%09d.cly`, hint-index or merge-finished file).  For cly_scan the

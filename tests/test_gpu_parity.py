@@ -554,3 +554,80 @@ def test_gpu_largest_file_offsets_past_2gib(corrupt):
     else:
         assert res[0].status == 0 and res[0].n_records == n and res[0].end_offset == len(arr)
         assert int(got["offset"][-1]) == (n - 1) * 276 > 2**32 - 2**25
+
+
+def part_file(total, cuts, seed):
+    """One data file of `total` bytes: copies of an 8-MB mixed corpus (no tail),
+    and at each cut c (a part end of the scan: 2^31 B for libclyscan, 2^28 B for
+    the small build) a long record that ends exactly at c (first cut: the next
+    record starts a part) or crosses it (the others); records to the end, then
+    a zero tail."""
+    import random
+
+    import make_golden as mg
+    rng = random.Random(seed)
+    base = np.frombuffer(mixed_corpus(seed, 8 << 20, tail=False), np.uint8)
+    pieces, off, i = [], 0, 10**8
+    for j, c in enumerate(list(cuts) + [total]):
+        while off + len(base) <= c - 60_000:
+            pieces.append(base)
+            off += len(base)
+        if j == len(cuts):
+            break
+        key = mg.key_tx(mg.test_key(i), 0)
+        i += 1
+        want = c - off + (0 if j == 0 else 20_000)                     # the record's size
+        vlen = want - 30
+        for _ in range(3):                                             # (the value size's varint length)
+            vlen = want - (len(mg.encode_record(key, b"\0" * vlen)) - vlen)
+        rec = mg.encode_record(key, rng.randbytes(vlen))
+        assert len(rec) == want
+        pieces.append(np.frombuffer(rec, np.uint8))
+        off += len(rec)
+    pieces.append(np.zeros(total - off, np.uint8))
+    arr = np.concatenate(pieces)
+    assert len(arr) == total
+    return arr
+
+
+def _scan_part_file(lib, arr, corrupt_after):
+    torch = pytest.importorskip("torch")
+    t, st, end = co.scan_file(arr, 3)
+    assert st != _abi.ERR_CRC and len(t) > 1000            # (the zero tail ends the file)
+    cap = len(t) + 1024                                    # (tuples past a failing record are written too)
+    if corrupt_after is not None:
+        k = int(np.searchsorted(t["offset"], corrupt_after)) + 17
+        arr = arr.copy()
+        arr[int(t["offset"][k]) + int(t["size"][k]) - 1] ^= 0x10     # the record's last byte
+        t, st, end = co.scan_file(arr, 3)
+        assert st == _abi.ERR_CRC and len(t) == k and end > corrupt_after
+    d = torch.from_numpy(arr).cuda()
+    out = torch.empty(cap * 48, dtype=torch.uint8, device="cuda")
+    with Scanner(0, lib=lib) as sc:
+        first, res, stt, need = sc.scan_device([(d.data_ptr(), len(arr), 3)], out.data_ptr(), cap)
+    got = out[: need * 48].cpu().numpy().view(TUPLE_DTYPE)
+    compare(got[: res[0].n_records], res[0].status, res[0].end_offset, t, st, end, "%s %d B" % (lib, len(arr)))
+    return res
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_records_across_part_ends(scanner, corrupt):
+    """A 700-MB file over three parts of the small build (2^28-B parts: a
+    record ends exactly at the first part end, another crosses the second),
+    one part of libclyscan; bit-exact against the oracle, and a CRC failure in
+    the third part stops the file at its record."""
+    arr = part_file(700_000_000, [1 << 28, 1 << 29], seed=21)
+    _scan_part_file(scanner.lib_name, arr, (1 << 29) + 1_000_000 if corrupt else None)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_gpu_file_past_4gib(corrupt):
+    """One 4.6-GB data file (Options.SetDataFileSizeGB(5), options.go:70-71)
+    over three 2-GiB parts: a record ends exactly at 2^31, another crosses
+    2^32; bit-exact against the oracle (offsets past 2^32 as int64), and a
+    flipped byte at ~4.5 GB gives ErrInvalidCRC at its record."""
+    arr = part_file(4_600_000_000, [1 << 31, 1 << 32], seed=22)
+    res = _scan_part_file("libclyscan.so", arr, 4_500_000_000 if corrupt else None)
+    if not corrupt:
+        assert res[0].status != _abi.ERR_CRC and res[0].end_offset > 1 << 32

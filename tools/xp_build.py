@@ -108,6 +108,8 @@ PATCHES["prof"] = [
             c->h_g->xp_t[6], c->h_g->xp_t[7], (unsigned long long)(c->h_g->walk_dbg >> 40));
     float ms_scan = 0, ms_link = 0, ms_emit = 0, ms_fin = 0;"""),
 ]
+PATCHES["gp1"] = [("#define GP_TRIES 2 ", "#define GP_TRIES 1 ")]
+PATCHES["gp3"] = [("#define GP_TRIES 2 ", "#define GP_TRIES 3 ")]
 PATCHES["sloopcnt"] = PATCHES["sloop"] + PATCHES["cnt"]
 PATCHES["run1"] = [("#define RUN_TILES 4", "#define RUN_TILES 1")]
 PATCHES["run8"] = [("#define RUN_TILES 4", "#define RUN_TILES 8")]
