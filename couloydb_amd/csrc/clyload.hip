@@ -395,15 +395,16 @@ __global__ void k_hint_as_put(cly_tuple* t, uint64_t n) {
     t[i].tx_id = 0; t[i].txid_len = 0; t[i].type = 0; t[i].data_type = 0; t[i].expiration = 0;
 }
 
-// Page-locked staging buffers (two per copy thread), allocated once; the
-// caller holds g_stage_mu.
-static int stage_ready() {
-    for (int k = 0; k < 2 * LOAD_THREADS_MAX; k++)          // (again after a failed allocation)
+// Page-locked staging buffers (two per copy thread), allocated once, each by
+// the copy thread that first uses its slot (the threads' allocations run side
+// by side); the caller holds g_stage_mu.
+static bool stage_pair(int t) {
+    for (int k = 2 * t; k < 2 * t + 2; k++)                // (again after a failed allocation)
         if (!g_stage[k] && hipHostMalloc(&g_stage[k], LOAD_STAGE, hipHostMallocPortable) != hipSuccess) {
             g_stage[k] = nullptr;
-            return CLY_ERR_DEVICE;
+            return false;
         }
-    return CLY_OK;
+    return true;
 }
 // The files' bytes to device dev: nt threads (staging buffers of threads t0 ..
 // t0+nt-1) fault the mapped pages in and copy 64-MiB pieces through the
@@ -424,7 +425,7 @@ static int copy_to_device(int dev, const std::vector<cly_file>& hf, std::vector<
     std::atomic<size_t> next(0);
     std::atomic<int> err(0);
     par_run(nt, [&](int t) {
-        if (hipSetDevice(dev) != hipSuccess) { err = 1; return; }
+        if (hipSetDevice(dev) != hipSuccess || !stage_pair(t0 + t)) { err = 1; return; }
         hipStream_t ts = nullptr;
         hipEvent_t ev[2] = {nullptr, nullptr};
         if (hipStreamCreateWithFlags(&ts, hipStreamNonBlocking) != hipSuccess ||
@@ -466,11 +467,10 @@ static int copy_to_host(cly_ctx* ctx, const std::vector<D2H>& parts, int t0, int
     const int dev = cly_ctx_device_internal(ctx);
     std::unique_lock<std::mutex> lk(g_stage_mu, std::defer_lock);     // (lock = false: the caller holds it)
     if (lock) lk.lock();
-    if (stage_ready() != CLY_OK) return CLY_ERR_DEVICE;
     // (threads t0 .. t0+nt-1, each with its own two staging buffers)
     par_run(nt, [&, t0](int tl) {
         const int t = t0 + tl;
-        if (hipSetDevice(dev) != hipSuccess) { err = 1; return; }
+        if (hipSetDevice(dev) != hipSuccess || !stage_pair(t)) { err = 1; return; }
         hipStream_t ts = nullptr;
         if (hipStreamCreateWithFlags(&ts, hipStreamNonBlocking) != hipSuccess) { err = 1; return; }
         struct Pend { uint8_t* dst; uint64_t n; int b; };
@@ -742,7 +742,6 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
         // the shards in parallel, one host thread each (load_threads() copy
         // threads shared out), each on its own context's device and stream
         std::lock_guard<std::mutex> lk(g_stage_mu);
-        if (stage_ready() != CLY_OK) { rc = CLY_ERR_DEVICE; goto done; }
         const int nt = load_threads(), ntk = std::max(1, nt / (int)s.n_shards);
         std::vector<std::thread> th;
         int slot = 0;
@@ -836,7 +835,6 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
         // on, beside the index rebuild and the tables' build on the device and
         // their read-back on threads 0 .. nb-1
         std::unique_lock<std::mutex> lk(g_stage_mu);
-        if (stage_ready() != CLY_OK) { rc = CLY_ERR_DEVICE; goto done; }
         const int nt = load_threads(), nb = std::max(1, nt / 2);
         int trc = CLY_OK;
         std::thread tcopy([&]() {
