@@ -21,7 +21,7 @@ for cfg in sys.argv[2:]:
         for (k, c), v in agg.items():
             vals[k][c] = v / len(disp[(k, c)])
     for k in sorted(vals):
-        if not any(c.startswith("SQ_INSTS_VALU") or c == "SQ_WAVES" for c in vals[k]):
+        if not any(c.startswith("SQ_") for c in vals[k]):
             continue
         if vals[k].get("SQ_WAVES", 1e9) < 64 and vals[k].get("SQ_INSTS_VALU", 1e9) < 1e6:
             continue
