@@ -13,7 +13,8 @@
 // the device, and their tuples rewritten as String puts of their stored key
 // (no txId) so that the device index rebuild (cly_index_device) applies them
 // first and the data files' String records override them, last writer wins.
-// The tuples and states come back, and the host builds what updateIndex puts
+// The host records (offset, fid, header and key sizes, expiration: 24 B of
+// each 48-B tuple) and the class bytes come back, and the host builds what updateIndex puts
 // in the MemTables (meta/memTable.go:15-30) from the records the device
 // marked as index entries: the String and ListMeta indexes as open-addressing
 // tables over the mapped key bytes, and the per-key Hash (field), List (seq
@@ -148,6 +149,18 @@ __host__ __device__ static inline int flat_shard(uint64_t h, int hshift) { retur
 __host__ __device__ static inline uint64_t flat_tag(uint64_t h) { return (h * 0x9E3779B97F4A7C15ull) >> 40; }
 // the slot's tuple index, or ~0 for an empty slot
 static inline uint64_t flat_ti(uint64_t v) { return v ? (v & FLAT_TI_MASK) - 1 : ~0ull; }
+// What the host keeps of a record for its lookups and enumerations (24 B; the
+// 48-B tuple stays on the device): the file offset (below 2^48) with the
+// header size in bits 48..54, "txId != 0" in bit 55 and the txId varint's
+// length in bits 56..63; the expiration; the fid; the stored key's size.
+// The data type is the class byte's high nibble (k_state_dt).
+struct HostRec { uint64_t a; int64_t exp; uint32_t fid, ks; };
+static_assert(sizeof(HostRec) == 24, "24-B host records");
+#define HR_OFF_MASK ((1ull << 48) - 1)
+static inline uint64_t hr_off(const HostRec& r) { return r.a & HR_OFF_MASK; }
+static inline uint32_t hr_hsz(const HostRec& r) { return (uint32_t)(r.a >> 48) & 0x7Fu; }
+static inline bool hr_tx(const HostRec& r) { return ((r.a >> 55) & 1u) != 0; }
+static inline uint32_t hr_txl(const HostRec& r) { return (uint32_t)(r.a >> 56); }
 struct cly_db {
     std::vector<Mapped> files;       // in loadIndex's order (fids as sort.Ints orders the stems)
     std::unordered_map<uint32_t, uint32_t> fid_ix;   // uint32(fid) -> its file
@@ -157,7 +170,7 @@ struct cly_db {
     std::vector<uint64_t> expired;   // tuple indices of the String winners the TTL sweep removed
     std::vector<cly_db_entry> it[6]; // cly_db_entries, built on first use
     bool it_built[6] = {false, false, false, false, false, false};
-    HostArr<cly_tuple> tuples;
+    HostArr<HostRec> recs;           // per tuple (scan order)
     HostArr<uint8_t> state;
     uint64_t hmask = ~0ull;
     int hshift = 60;
@@ -214,17 +227,17 @@ static const uint8_t* file_of(const cly_db* db, uint32_t fid) {
 // realKey of tuple ti (parseLogRecordKey, db.go:706-710); a hint record's
 // stored key as it is (strIndex.Put(logRecord.Key), merge.go:283)
 static const uint8_t* real_key_ptr(const cly_db* db, uint64_t ti, uint64_t& len) {
-    const cly_tuple& t = db->tuples[ti];
+    const HostRec& t = db->recs[ti];
     const uint8_t* f = ti < db->n_hint ? db->hint.p : file_of(db, t.fid);
-    const uint32_t tl = t.txid_len == 0xFF ? 0 : t.txid_len;
-    len = t.key_size - tl;
-    return f + t.offset + t.header_size + tl;
+    const uint32_t tl = hr_txl(t) == 0xFF ? 0 : hr_txl(t);
+    len = t.ks - tl;
+    return f + hr_off(t) + hr_hsz(t) + tl;
 }
 // the LogPos an index entry at tuple ti holds
 static cly_pos pos_of(const cly_db* db, uint64_t ti) {
     if (ti < db->n_hint) return db->hint_pos[ti];
     cly_pos p;
-    p.offset = db->tuples[ti].offset; p.fid = db->tuples[ti].fid; p._pad = 0;
+    p.offset = (int64_t)hr_off(db->recs[ti]); p.fid = db->recs[ti].fid; p._pad = 0;
     return p;
 }
 // slots of a shard of n keys: a power of two >= 1.5 n (at least 16; none for no key)
@@ -387,6 +400,20 @@ __global__ void k_state_dt(uint8_t* state, const cly_tuple* t, uint64_t n) {
     state[i] = (uint8_t)(state[i] | ((dt < 7 ? dt : 7) << 4));
 }
 
+// The host records of the tuples (what lookups read; half the tuples' bytes
+// over PCIe)
+__global__ void k_host_rec(const cly_tuple* t, HostRec* r, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const cly_tuple x = t[i];
+    HostRec o;
+    o.a = ((uint64_t)x.offset & HR_OFF_MASK) | ((uint64_t)(x.header_size & 0x7Fu) << 48) |
+          ((uint64_t)(x.tx_id != 0) << 55) | ((uint64_t)x.txid_len << 56);
+    o.exp = x.expiration;
+    o.fid = x.fid;
+    o.ks = x.key_size;
+    r[i] = o;
+}
 // A hint record's tuple as the index rebuild takes it: strIndex.Put of its
 // stored key (no txId prefix, merge.go:283), whatever its types, no TTL
 __global__ void k_hint_as_put(cly_tuple* t, uint64_t n) {
@@ -695,6 +722,7 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
     bool own_tup = false;
     uint8_t* d_state = nullptr;
     cly_pos* d_hpos = nullptr;
+    HostRec* d_hrec = nullptr;
     std::vector<cly_file> hf, df;
     std::vector<cly_file_result> res;
     std::vector<uint64_t> first;
@@ -825,20 +853,26 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
     t3 = now_ms();
     s.scan_ms = t3 - t2;
     DCK(hipMalloc((void**)&d_state, need ? need : 1));
-    db->tuples.alloc(need);
+    DCK(hipMalloc((void**)&d_hrec, sizeof(HostRec) * (need ? need : 1)));
+    if (need) {
+        hipLaunchKernelGGL(k_host_rec, dim3((unsigned)((need + 255) / 256)), dim3(256), 0, strm, d_tup, d_hrec, need);
+        DCK(hipGetLastError());
+        DCK(hipStreamSynchronize(strm));
+    }
+    db->recs.alloc(need);
     db->state.alloc(need);
     db->hint_pos.resize(db->n_hint);
     db->hmask = cly_ix_hash_mask_internal(need);
     db->hshift = 64 - __builtin_clzll(db->hmask | 15) - FLAT_SHARD_BITS;
     {
-        // the tuples (what lookups read) come back on copy threads nb.. from now
-        // on, beside the index rebuild and the tables' build on the device and
-        // their read-back on threads 0 .. nb-1
+        // the host records (what lookups read) come back on copy threads nb..
+        // from now on, beside the index rebuild and the tables' build on the
+        // device and their read-back on threads 0 .. nb-1
         std::unique_lock<std::mutex> lk(g_stage_mu);
         const int nt = load_threads(), nb = std::max(1, nt / 2);
         int trc = CLY_OK;
         std::thread tcopy([&]() {
-            if (need) trc = copy_to_host(ctx, {{db->tuples.data(), d_tup, sizeof(cly_tuple) * need}}, nb,
+            if (need) trc = copy_to_host(ctx, {{db->recs.data(), d_hrec, sizeof(HostRec) * need}}, nb,
                                          std::max(1, nt - nb), false);
         });
         rc = flat_device(ctx, db, nall ? df.data() : nullptr, nall, d_tup, first, res, d_state, d_hpos, need, ir, nb, s);
@@ -857,19 +891,21 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
         std::vector<uint64_t> composite;
         composite_list(db, load_threads(), composite);
         for (uint64_t i : composite) {
-            const cly_tuple& t = db->tuples[i];
-            uint32_t off, len;
-            ixk_input(t, off, len, false);
-            const uint8_t* d = file_of(db, t.fid) + t.offset + t.header_size + off;
+            const HostRec& t = db->recs[i];
+            const uint32_t dt = ST_DT(db->state[i]);
+            // ixk_input: the stored key when applied at once (txId 0), else the realKey
+            const uint32_t tl = hr_txl(t) == 0xFF ? 0u : hr_txl(t);
+            const uint32_t off = hr_tx(t) ? tl : 0u, len = hr_tx(t) ? t.ks - tl : t.ks;
+            const uint8_t* d = file_of(db, t.fid) + hr_off(t) + hr_hsz(t) + off;
             IxKey k;
-            if (!ixk_key(t.data_type, d, len, k)) continue;      // (the device rejected a panicking decode)
+            if (!ixk_key(dt, d, len, k)) continue;               // (the device rejected a panicking decode)
             cly_pos p;
-            p.offset = t.offset; p.fid = t.fid; p._pad = 0;
+            p.offset = (int64_t)hr_off(t); p.fid = t.fid; p._pad = 0;
             const uint8_t* r = d + k.r_off;
-            if (t.data_type == 1) {              // realKey = R[0:la], field = R[la:]
+            if (dt == 1) {                       // realKey = R[0:la], field = R[la:]
                 const uint32_t la = k.p[0] | ((uint32_t)k.p[1] << 8) | ((uint32_t)k.p[2] << 16) | ((uint32_t)k.p[3] << 24);
                 db->hash[std::string((const char*)r, la)][std::string((const char*)r + la, k.r_len - la)] = p;
-            } else if (t.data_type == 2) {       // realKey = R, seqBuf = P[1:]
+            } else if (dt == 2) {                // realKey = R, seqBuf = P[1:]
                 db->list[std::string((const char*)r, k.r_len)][std::string((const char*)k.p + 1, k.plen - 1)] = p;
             } else {                             // realKey = R, hashKey = P
                 db->set[std::string((const char*)r, k.r_len)][std::string((const char*)k.p, 4)] = p;
@@ -952,7 +988,7 @@ extern "C" int cly_db_open_multi(cly_ctx* const* ctxs, int nctx, const char* dir
 done:
     (void)hipSetDevice(dev0);
     if (own_tup) hipFree(d_tup);
-    hipFree(d_state); hipFree(d_hpos);
+    hipFree(d_state); hipFree(d_hpos); hipFree(d_hrec);
     for (LoadShard& S : sh) shard_free(S);
     if (st) *st = s;
     if (rc != CLY_OK) { cly_db_close(db); return rc; }
@@ -1061,7 +1097,7 @@ static void build_entries(cly_db* db, int kind) {
             memset(&e, 0, sizeof(e));
             e.key = real_key_ptr(db, ti, e.key_len);
             e.pos = pos_of(db, ti);
-            e.expiration = str && ti >= db->n_hint ? db->tuples[ti].expiration : 0;
+            e.expiration = str && ti >= db->n_hint ? db->recs[ti].exp : 0;
             v.push_back(e);
         }
     };
@@ -1077,7 +1113,7 @@ static void build_entries(cly_db* db, int kind) {
                 memset(&e, 0, sizeof(e));
                 e.key = real_key_ptr(db, i, e.key_len);
                 e.pos = pos_of(db, i);
-                e.expiration = db->tuples[i].expiration;
+                e.expiration = db->recs[i].exp;
                 v.push_back(e);
             }
             break;

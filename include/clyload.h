@@ -62,7 +62,7 @@ typedef struct cly_load_stats {
     double   list_map_ms;     /* readdir + open + mmap of the data files         */
     double   h2d_ms;          /* files to the device                             */
     double   scan_ms;         /* cly_scan_device                                 */
-    double   index_ms;        /* cly_index_device + tuples/states back           */
+    double   index_ms;        /* cly_index_device + tables, host records, states back */
     double   insert_ms;       /* host index inserts (the MemTable Put/Del)       */
     double   total_ms;
     uint64_t n_files, bytes, records;
