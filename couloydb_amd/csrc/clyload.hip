@@ -115,15 +115,34 @@ static Hdr host_read_record(const uint8_t* p, uint64_t len, int64_t off) {
     return h;
 }
 
-// host array without value-initialisation (the device fills it)
+// host array without value-initialisation (the device fills it): an
+// anonymous mapping advised for transparent huge pages, so that the copy
+// threads that first write it (the open's read-back, hundreds of MB) take a
+// page fault per 2 MiB rather than per 4 KiB
 template <class T> struct HostArr {
-    std::unique_ptr<T[]> p;
-    uint64_t n = 0;
-    void alloc(uint64_t k) { p.reset(k ? new T[k] : nullptr); n = k; }
+    T* p = nullptr;
+    uint64_t n = 0, bytes = 0;
+    HostArr() = default;
+    HostArr(const HostArr&) = delete;
+    HostArr& operator=(const HostArr&) = delete;
+    ~HostArr() { release(); }
+    void release() {
+        if (p) munmap(p, bytes);
+        p = nullptr; n = 0; bytes = 0;
+    }
+    void alloc(uint64_t k) {
+        release();
+        if (!k) return;
+        const uint64_t b = (k * sizeof(T) + 4095) & ~4095ull;
+        void* m = mmap(nullptr, b, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (m == MAP_FAILED) throw std::bad_alloc();
+        if (b >= (2ull << 20)) madvise(m, b, MADV_HUGEPAGE);
+        p = (T*)m; n = k; bytes = b;
+    }
     T& operator[](uint64_t i) { return p[i]; }
     const T& operator[](uint64_t i) const { return p[i]; }
     uint64_t size() const { return n; }
-    T* data() { return p.get(); }
+    T* data() { return p; }
 };
 // The String / ListMeta index: open-addressing tables sharded by the key
 // hash's top valid bits, built on the device (k_flat_count, k_flat_insert)
@@ -432,6 +451,22 @@ static bool stage_pair(int t) {
             return false;
         }
     return true;
+}
+// The pool's staging buffers, all of them, allocated by load_threads()
+// threads side by side: cly_ctx_create calls this, so that the first open of a
+// process finds them (allocating the 32 page-locked 8-MiB buffers inside the
+// first open's copy cost it 15-25 ms, profiles/r5_*); once per process.
+extern "C" void cly_load_stage_init_internal() {
+    static bool all = false;
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    int dev = 0;
+    if (all || hipGetDevice(&dev) != hipSuccess) return;
+    std::atomic<int> ok(0);
+    const int nt = load_threads();
+    par_run(nt, [&](int t) {
+        if (hipSetDevice(dev) == hipSuccess && stage_pair(t)) ok++;   // (a failure is retried at first use)
+    });
+    all = ok == nt;
 }
 // The files' bytes to device dev: nt threads (staging buffers of threads t0 ..
 // t0+nt-1) fault the mapped pages in and copy 64-MiB pieces through the

@@ -2195,6 +2195,7 @@ struct cly_ctx {
 };
 extern "C" void cly_merge_scratch_free(void* p);
 
+extern "C" void cly_load_stage_init_internal();     // clyload.hip
 extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     if (!out) return CLY_ERR_ARG;
     *out = nullptr;
@@ -2244,6 +2245,7 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
         c->emit_grid = per_cu * ncu;
         c->loc_grid = ncu;
     }
+    cly_load_stage_init_internal();       // the load driver's page-locked staging (once per process)
     *out = c;
     return CLY_OK;
 }
