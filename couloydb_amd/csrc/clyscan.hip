@@ -75,9 +75,17 @@ __device__ __forceinline__ rsrc_t mk_rsrc(const void* p, uint32_t bytes) {
 #define LM_OFF 3                 // segment beyond the end of the file
 #define CAP_T ((uint32_t)(CLY_TILE / 128))   // compact entries in a tile's own area (more: spill chunks)
 #define CAP_SHIFT (__builtin_ctz(CAP_T))
-// k_scan walks runs of RUN_TILES consecutive tiles of a file: a run's first
-// tile guesses its entry, the others take the exit of the tile before them
+// k_scan walks runs of consecutive tiles of a file: a run's first tile
+// guesses its entry, the others take the exit of the tile before them.  The
+// run length (Globals::run_tiles) is chosen per call: RUN_TILES when the runs
+// still fill the scan's wave slots, else 2 or 1 (small inputs: C1's 1024
+// tiles as 256 runs left 15 of 16 wave slots idle, each run walking 64 blocks
+// in a row).  The 8-KiB-tile test build keeps RUN_TILES, so that its small
+// fixtures walk runs of several tiles.
 #define RUN_TILES 4
+#ifndef CLY_RUN_ADAPT
+#define CLY_RUN_ADAPT (CLY_NBLK == 16)
+#endif
 // Spill: records CAP_T.. of a tile go to chunks of CAP_T entries (and their
 // snapshots) taken from a per-call pool; a tile's chunk table holds up to
 // NCH_MAX chunk ids and, in word CH_NWORD, how many it took.  Records are at
@@ -109,7 +117,7 @@ struct DevFile {                 // 32 B
 #define PART_BYTES ((uint64_t)PART_TILES * CLY_TILE)
 #define VIEW_MAX (0xFFFFFFFFull - 2 * (uint64_t)CLY_TILE)
 #define P_NONE 0xFFFFFFFFFFFFull  // no record start (u64 positions; files are below 2^48 B)
-static_assert(PART_TILES % RUN_TILES == 0, "a run of tiles stays in one part");
+static_assert(PART_TILES % RUN_TILES == 0, "a run of tiles stays in one part (run lengths 1, 2, RUN_TILES)");
 static_assert(PART_BYTES < VIEW_MAX, "a part's view: its bytes and a record that crosses its end");
 __device__ __forceinline__ uint64_t part_x0(uint32_t tt) { return (uint64_t)(tt / PART_TILES) * PART_BYTES; }
 // file F as tile tt's part sees it (base at x0, u32 length), and tt's index in the part
@@ -167,6 +175,8 @@ struct Globals {                 // zeroed per call
     uint32_t walk_max;           // the longest k_refix walk (tiles), over all rounds
     uint64_t total;              // records over all files
     uint64_t walk_dbg;           // (length << 32 | first tile) of the longest k_refix walk
+    uint32_t run_tiles;          // k_scan's run length this call (1, 2 or RUN_TILES; set by the host)
+    uint32_t _pad;
 };
 
 // ---------------------------------------------------------------------------
@@ -1318,7 +1328,7 @@ __device__ __forceinline__ uint32_t k4_const(const CLY_LDS uint8_t* smem, uint32
     return K4;
 }
 
-// k_scan: one wave per run of RUN_TILES tiles (grid-stride), every byte of
+// k_scan: one wave per run of run_tiles tiles (grid-stride), every byte of
 // every file read once.
 #define SCAN_WAVES 16
 #define MK_BYTES (CLY_NL * 4)                                 // a wave's patch-word mask
@@ -1348,13 +1358,14 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     const CrcLane cl = crc_lane(lane);
     const uint32_t K4 = k4_const(smem, cl.r4);
     const uint32_t stride = gridDim.x * SCAN_WAVES;
-    // runs of RUN_TILES consecutive tiles of a file, grid-strided; a run's
+    // runs of run_tiles consecutive tiles of a file, grid-strided; a run's
     // first tile (not its file's first) guesses its entry, the others take
     // the exit of the tile before them
     uint32_t r = blockIdx.x * SCAN_WAVES + wave_id();
     if (r >= nruns) return;
+    const uint32_t rt = __builtin_amdgcn_readfirstlane(g->run_tiles);
     int f = find_file(rprefix, nfiles, r);
-    uint32_t t = files[f].first_tile + (r - rprefix[f]) * RUN_TILES;
+    uint32_t t = files[f].first_tile + (r - rprefix[f]) * rt;
     u32x4 e[4], hl;
     {
         uint32_t ptt;
@@ -1364,14 +1375,14 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     uint32_t Xc = NONE32;        // the entry carried from the run's previous tile (NONE32: guess)
     for (;;) {
         const DevFile F = files[f];
-        const uint32_t rend = min(F.first_tile + (r - rprefix[f] + 1u) * RUN_TILES, F.first_tile + F.ntile);
+        const uint32_t rend = min(F.first_tile + (r - rprefix[f] + 1u) * rt, F.first_tile + F.ntile);
         // the wave's next tile: the next of this run, else the first of its next run
         uint32_t tn = t + 1u, rn = r;
         int fn = f;
         if (tn >= rend) {
             rn = r + stride;
             fn = rn < nruns ? find_file(rprefix, nfiles, rn) : -1;
-            if (fn >= 0) tn = files[fn].first_tile + (rn - rprefix[fn]) * RUN_TILES;
+            if (fn >= 0) tn = files[fn].first_tile + (rn - rprefix[fn]) * rt;
         }
         const uint8_t* nbase = nullptr;
         uint32_t nlen = 0, ntb = 0;
@@ -1465,6 +1476,7 @@ k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restric
     __shared__ int last;
     const int f = blockIdx.x, tid = threadIdx.x;
     const DevFile F = files[f];
+    const uint32_t rt = g->run_tiles;        // k_scan's run length (a run's first tile guessed its entry)
     const uint32_t nt = F.ntile, per = (nt + LINK_NT - 1) / LINK_NT;
     const uint32_t lo = tid * per < nt ? tid * per : nt, hi = lo + per < nt ? lo + per : nt;
     const TileLocal* L0 = loc + F.first_tile;
@@ -1513,7 +1525,7 @@ k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restric
         if (bad) {
             if (u < LINK_MAXT) atomicOr(&badm[u >> 5], 1u << (u & 31));
             else atomicMin(&bad_far, u);
-        } else if (u < LINK_MAXT && (u == 0 || (u % RUN_TILES == 0 && !(l0 & DF_NONE))))
+        } else if (u < LINK_MAXT && (u == 0 || (u % rt == 0 && !(l0 & DF_NONE))))
             atomicOr(&ancm[u >> 5], 1u << (u & 31));
         s = rf_apply(rf_tile(l0, l1, l2, x0), s);
     };
@@ -2175,7 +2187,7 @@ struct cly_ctx {
     uint8_t* d_call; uint8_t* h_call; size_t call_bytes;     // the per-call block (ensure_files)
     DevFile* d_files; uint32_t* d_tprefix; FileInfo* d_finfo; uint64_t* d_ftotal; int cap_files;
     DevFile* h_files; uint32_t* h_tprefix; FileInfo* h_finfo;
-    uint32_t* d_rprefix; uint32_t* h_rprefix;        // per file its first run of RUN_TILES tiles (k_scan)
+    uint32_t* d_rprefix; uint32_t* h_rprefix;        // per file its first run of tiles (k_scan)
     TileLocal* d_loc; TileIn* d_tin; uint32_t* d_treg; uint32_t* d_fix; uint32_t* d_rec;
     uint32_t* d_seg; uint32_t* d_snap;   // segment registers, snapshots
     uint32_t* d_chunks;          // per tile CH_WORDS words: spill chunk ids and their count
@@ -2349,6 +2361,19 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
     if (rc) return rc;
     int64_t ntiles = 0, nruns = 0;
     uint64_t bytes = 0;
+    // the run length: the longest (up to RUN_TILES) whose runs fill the wave slots
+    uint32_t rt = RUN_TILES;
+    if (CLY_RUN_ADAPT) {
+        const int64_t slots = (int64_t)c->scan_grid * SCAN_WAVES;
+        for (; rt > 1; rt >>= 1) {
+            int64_t nr = 0;
+            for (int i = 0; i < nfiles; i++) {
+                const uint64_t nt = files[i].len ? (files[i].len + CLY_TILE - 1) / CLY_TILE : 1;
+                nr += (int64_t)((nt + rt - 1) / rt);
+            }
+            if (nr >= slots) break;
+        }
+    }
     for (int i = 0; i < nfiles; i++) {
         if (files[i].len > MAX_FILE_LEN) return CLY_ERR_ARG;
         if (files[i].len && (((uintptr_t)files[i].base) & 15)) return CLY_ERR_ARG;
@@ -2362,7 +2387,7 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
         c->h_tprefix[i] = (uint32_t)ntiles;
         c->h_rprefix[i] = (uint32_t)nruns;
         ntiles += (int64_t)nt;
-        nruns += (int64_t)((nt + RUN_TILES - 1) / RUN_TILES);
+        nruns += (int64_t)((nt + rt - 1) / rt);
         bytes += files[i].len;
     }
     if (ntiles >= (1LL << 31)) return CLY_ERR_ARG;
@@ -2374,6 +2399,7 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
     if (rc) return rc;
     memset(c->h_g, 0, sizeof(Globals));
     c->h_g->spill_cap = c->cap_spill;
+    c->h_g->run_tiles = rt;
     memset(c->h_finfo, 0, sizeof(FileInfo) * nfiles);
     for (int i = 0; i < nfiles; i++) c->h_finfo[i].fail_off = c->h_finfo[i].fail_idx = ~0ull;
     HIPCK(hipMemcpyAsync(c->d_call, c->h_call, c->call_bytes, hipMemcpyHostToDevice, st));
