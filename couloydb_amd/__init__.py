@@ -322,6 +322,12 @@ class Scanner:
         (UnixNano; 0 = the wall clock at each call)."""
         self.lib.cly_ctx_set_clock(self.ctx, int(now_ns))
 
+    def prepare_load(self):
+        """cly_load_prepare: allocate the load driver's page-locked staging now
+        (an application's start-up step; the first open then does not pay for
+        it).  Returns the status (CLY_OK, or CLY_ERR_DEVICE: opens allocate lazily)."""
+        return int(self.lib.cly_load_prepare())
+
     def open_db(self, path, data_file_size=0, apply_sweep=False):
         """NewCouloyDB's index load (db.go:442-655, merge.go:240-287) from the
         `*.cly`, hint-index and merge-finished files of directory `path`, on

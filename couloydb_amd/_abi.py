@@ -92,7 +92,8 @@ SCAN_SYMBOLS = ["cly_ctx_create", "cly_ctx_destroy", "cly_ctx_set_clock", "cly_s
                 "cly_strerror", "cly_build_info"]
 GEN_SYMBOLS = ["cly_gen_record_size", "cly_gen_layout", "cly_gen_encode"]
 LOAD_SYMBOLS = ["cly_db_open", "cly_db_open_opts", "cly_db_open_multi", "cly_db_close", "cly_db_get", "cly_db_listmeta", "cly_db_hget",
-                "cly_db_lget", "cly_db_sget", "cly_db_value", "cly_index_key", "cly_db_count", "cly_db_entries"]
+                "cly_db_lget", "cly_db_sget", "cly_db_value", "cly_index_key", "cly_db_count", "cly_db_entries",
+                "cly_load_prepare"]
 DB_NOT_FOUND, DB_EOF = 1, 2
 ERR_DIR, ERR_MERGE_FIN, ERR_KEY_EMPTY = -14, -15, -16
 IT_STRING, IT_LISTMETA, IT_HASH, IT_LIST, IT_SET, IT_EXPIRED = range(6)
@@ -163,6 +164,8 @@ def load_scan_lib(name="libclyscan.so"):
     lib.cly_db_entries.restype = ctypes.c_uint64
     lib.cly_db_close.argtypes = [ctypes.c_void_p]
     lib.cly_db_close.restype = None
+    lib.cly_load_prepare.argtypes = []
+    lib.cly_load_prepare.restype = ctypes.c_int
     for fn in ("cly_db_get", "cly_db_listmeta"):
         getattr(lib, fn).argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p]
         getattr(lib, fn).restype = ctypes.c_int

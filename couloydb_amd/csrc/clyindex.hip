@@ -24,7 +24,11 @@
 //   each key; adjacent records of a group with different keys (a hash
 //   collision) send the group to an exact one-thread resolution
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_segmented_radix_sort.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -497,7 +501,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     size_t tmp_bytes = 0, need = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const unsigned grid = ix_grid(n);
-    hipcub::CountingInputIterator<uint32_t> cnt(0);
+    rocprim::counting_iterator<uint32_t> cnt(0);
     uint64_t m = 0, m2 = 0;
     int hbits = 64;
     const uint64_t* d_first = nullptr;
@@ -527,13 +531,13 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     ICK(cly_ix_scratch_internal(ctx, 18, sizeof(GMax) * n, (void**)&d_g));
     ICK(cly_ix_scratch_internal(ctx, 19, sizeof(GMax) * n, (void**)&d_g2));
     // temp storage: the largest of the select / sort / scan needs
-    ICK(hipcub::DeviceSelect::Flagged(nullptr, need, cnt, d_flag, d_sel, d_nsel, (int)n, st));
+    ICK(rocprim::select(nullptr, need, cnt, d_flag, d_sel, d_nsel, (size_t)n, st));
     tmp_bytes = need;
-    ICK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, d_k2, d_txkey, d_sel, d_sidx, (int)n, 0, 64, st));
+    ICK(rocprim::radix_sort_pairs(nullptr, need, d_k2, d_txkey, d_sel, d_sidx, (size_t)n, 0u, 64u, st));
     if (need > tmp_bytes) tmp_bytes = need;
-    ICK(hipcub::DeviceScan::InclusiveScan(nullptr, need, d_rev, d_nxt, TxNextOp(), (int)n, st));
+    ICK(rocprim::inclusive_scan(nullptr, need, d_rev, d_nxt, (size_t)n, TxNextOp(), st));
     if (need > tmp_bytes) tmp_bytes = need;
-    ICK(hipcub::DeviceScan::InclusiveScan(nullptr, need, d_g, d_g2, GMaxOp(), (int)n, st));
+    ICK(rocprim::inclusive_scan(nullptr, need, d_g, d_g2, (size_t)n, GMaxOp(), st));
     if (need > tmp_bytes) tmp_bytes = need;
     ICK(cly_ix_scratch_internal(ctx, 20, tmp_bytes, &d_tmp));
     ICK(hipMemcpyAsync(d_fb, h_fb, sizeof(uint64_t) * (2 * (size_t)nfiles + 1), hipMemcpyHostToDevice, st));
@@ -549,7 +553,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     // ---- transactions: tx records sorted by txId (stable: scan order within a txId)
     if (h_tot.n_tx) {
         size_t tb = tmp_bytes;
-        ICK(hipcub::DeviceSelect::Flagged(d_tmp, tb, cnt, d_flag, d_sel, d_nsel, (int)n, st));
+        ICK(rocprim::select(d_tmp, tb, cnt, d_flag, d_sel, d_nsel, (size_t)n, st));
         ICK(hipMemcpyAsync(&h_nsel, d_nsel, sizeof(h_nsel), hipMemcpyDeviceToHost, st));
         ICK(hipStreamSynchronize(st));
         m = h_nsel;
@@ -559,12 +563,12 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
         {
             size_t tb = tmp_bytes;
             // sorted txIds into d_txkey (free after the gather; d_hash holds k_ixclass's hashes)
-            ICK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_k2, d_txkey, d_sel, d_sidx, (int)m, 0, 64, st));
+            ICK(rocprim::radix_sort_pairs(d_tmp, tb, d_k2, d_txkey, d_sel, d_sidx, (size_t)m, 0u, 64u, st));
         }
         k_ixtxin<<<ix_grid(m), 256, 0, st>>>(d_txkey, d_sidx, d_cls, m, d_rev);
         {
             size_t tb = tmp_bytes;
-            ICK(hipcub::DeviceScan::InclusiveScan(d_tmp, tb, d_rev, d_nxt, TxNextOp(), (int)m, st));
+            ICK(rocprim::inclusive_scan(d_tmp, tb, d_rev, d_nxt, (size_t)m, TxNextOp(), st));
         }
         k_ixtx<<<ix_grid(m), 256, 0, st>>>(d_sidx, d_cls, m, d_nxt, d_order, d_state);
     }
@@ -576,7 +580,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
         m2 = n;                                                 // every record applied: no select
     } else {
         size_t tb = tmp_bytes;
-        ICK(hipcub::DeviceSelect::Flagged(d_tmp, tb, cnt, d_apflag, d_sel, d_nsel, (int)n, st));
+        ICK(rocprim::select(d_tmp, tb, cnt, d_apflag, d_sel, d_nsel, (size_t)n, st));
         ICK(hipMemcpyAsync(&h_nsel, d_nsel, sizeof(h_nsel), hipMemcpyDeviceToHost, st));
         ICK(hipStreamSynchronize(st));
         m2 = h_nsel;
@@ -589,13 +593,13 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
         if (!ident) k_ixgatherd<<<ix_grid(m2), 256, 0, st>>>(d_hash, d_sel, d_del, m2, d_k2, d_vin);
         {
             size_t tb = tmp_bytes;
-            ICK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, ident ? d_hash : d_k2, d_txkey, d_vin, d_sidx, (int)m2,
-                                                   0, hbits, st));
+            ICK(rocprim::radix_sort_pairs(d_tmp, tb, ident ? d_hash : d_k2, d_txkey, d_vin, d_sidx, (size_t)m2,
+                                                   0u, (unsigned)hbits, st));
         }
         if (m) {                    // tx records: application order != scan order, arg-max per group
             k_ixgin<<<ix_grid(m2), 256, 0, st>>>(d_txkey, d_sidx, d_order, m2, d_g);
             size_t tb = tmp_bytes;
-            ICK(hipcub::DeviceScan::InclusiveScan(d_tmp, tb, d_g, d_g2, GMaxOp(), (int)m2, st));
+            ICK(rocprim::inclusive_scan(d_tmp, tb, d_g, d_g2, (size_t)m2, GMaxOp(), st));
         }
         k_ixwin<<<ix_grid(m2), 256, 0, st>>>(d_txkey, d_sidx, m ? d_g2 : nullptr, m2, d_tuples, d_first, d_bases,
                                              nfiles, d_ksig, d_state, d_coll, d_tot, now_ns);

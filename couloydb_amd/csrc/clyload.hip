@@ -453,20 +453,26 @@ static bool stage_pair(int t) {
     return true;
 }
 // The pool's staging buffers, all of them, allocated by load_threads()
-// threads side by side: cly_ctx_create calls this, so that the first open of a
-// process finds them (allocating the 32 page-locked 8-MiB buffers inside the
-// first open's copy cost it 15-25 ms, profiles/r5_*); once per process.
-extern "C" void cly_load_stage_init_internal() {
-    static bool all = false;
+// threads side by side (include/clyload.h cly_load_prepare): an application
+// that opens a database calls it at start-up, so that the first open finds
+// them (allocating the 32 page-locked 8-MiB buffers inside the first open's
+// copy cost it 15-25 ms, profiles/r5_*).  Scan-only users never pay for them;
+// without it the open's copy threads allocate their own pair at first use.
+// Tried once per process: a failure is remembered (the lazy path still tries
+// per copy thread).
+extern "C" int cly_load_prepare(void) {
+    static int state = 0;                  // 0 not tried, 1 all allocated, 2 failed
     std::lock_guard<std::mutex> lk(g_stage_mu);
+    if (state) return state == 1 ? CLY_OK : CLY_ERR_DEVICE;
     int dev = 0;
-    if (all || hipGetDevice(&dev) != hipSuccess) return;
+    if (hipGetDevice(&dev) != hipSuccess) { state = 2; return CLY_ERR_DEVICE; }
     std::atomic<int> ok(0);
     const int nt = load_threads();
     par_run(nt, [&](int t) {
-        if (hipSetDevice(dev) == hipSuccess && stage_pair(t)) ok++;   // (a failure is retried at first use)
+        if (hipSetDevice(dev) == hipSuccess && stage_pair(t)) ok++;
     });
-    all = ok == nt;
+    state = ok == nt ? 1 : 2;
+    return state == 1 ? CLY_OK : CLY_ERR_DEVICE;
 }
 // The files' bytes to device dev: nt threads (staging buffers of threads t0 ..
 // t0+nt-1) fault the mapped pages in and copy 64-MiB pieces through the

@@ -34,7 +34,11 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_segmented_radix_sort.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include "scan_core.h"
 
@@ -1468,11 +1472,11 @@ extern "C" int cly_append_device(cly_ctx* ctx, const cly_rec_in* d_recs, uint64_
     MCK(scratch(ctx, MS_A0 + 3, 2 * sizeof(unsigned long long), &d_mx));
     MCK(hipMemsetAsync(d_mx, 0, sizeof(unsigned long long), st));
     MCK(hipMemsetAsync(d_mx + 1, 0xff, sizeof(unsigned long long), st));
-    MCK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, d_sz, d_g, (int)nt, st));
+    MCK(rocprim::exclusive_scan(nullptr, tb, d_sz, d_g, (uint64_t)0, (size_t)nt, rocprim::plus<uint64_t>(), st));
     MCK(scratch(ctx, MS_A0 + 4, tb + 16, (char**)&d_tmp));
     MCK(hipEventRecord(e0, st));
     k_asize<<<grid, 256, 0, st>>>((const ARec*)d_recs, n, nt, tx_id, d_sz, d_mx);
-    MCK(hipcub::DeviceScan::ExclusiveSum(d_tmp, tb, d_sz, d_g, (int)nt, st));
+    MCK(rocprim::exclusive_scan(d_tmp, tb, d_sz, d_g, (uint64_t)0, (size_t)nt, rocprim::plus<uint64_t>(), st));
     MCK(hipMemcpyAsync(&last, d_sz + nt - 1, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     MCK(hipMemcpyAsync(&total, d_g + nt - 1, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     MCK(hipMemcpyAsync(&h_mx, d_mx, sizeof(h_mx), hipMemcpyDeviceToHost, st));

@@ -20,7 +20,11 @@
 // 8 = more follow) inside the runs only, by a segmented radix sort, until no
 // run is left.  Winners hold distinct keys, so the order is total.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_segmented_radix_sort.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 #include <stdint.h>
 #include <stdio.h>
 
@@ -147,16 +151,16 @@ extern "C" int cly_order_keys_internal(hipStream_t st, const cly_tuple* d_tup, u
     OCK(hipMemsetAsync(d_cnt, 0, sizeof(h_cnt), st));
     OCK(hipMalloc((void**)&d_flag, n ? n : 1));
     OCK(hipMalloc((void**)&d_sel, sizeof(uint32_t) * (n ? n : 1)));
-    OCK(hipcub::DeviceSelect::Flagged(nullptr, need, hipcub::CountingInputIterator<uint32_t>(0), d_flag, d_sel,
-                                      d_cnt, (int)n, st));
+    OCK(rocprim::select(nullptr, need, rocprim::counting_iterator<uint32_t>(0), d_flag, d_sel,
+                                      d_cnt, (size_t)n, st));
     tmp_bytes = need;
-    OCK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, d_k1, d_ka, d_pa, d_pb, (int)n, 0, 64, st));
+    OCK(rocprim::radix_sort_pairs(nullptr, need, d_k1, d_ka, d_pa, d_pb, (size_t)n, 0u, 64u, st));
     if (need > tmp_bytes) tmp_bytes = need;
     OCK(hipMalloc(&d_tmp, tmp_bytes ? tmp_bytes : 1));
     if (n) {
         hipLaunchKernelGGL(k_ord_flag, dim3(ogrid(n)), dim3(256), 0, st, d_state, n, dt, d_flag);
-        OCK(hipcub::DeviceSelect::Flagged(d_tmp, need = tmp_bytes, hipcub::CountingInputIterator<uint32_t>(0), d_flag,
-                                          d_sel, d_cnt, (int)n, st));
+        OCK(rocprim::select(d_tmp, need = tmp_bytes, rocprim::counting_iterator<uint32_t>(0), d_flag,
+                                          d_sel, d_cnt, (size_t)n, st));
         OCK(hipMemcpyAsync(h_cnt, d_cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
         OCK(hipStreamSynchronize(st));
     }
@@ -171,9 +175,9 @@ extern "C" int cly_order_keys_internal(hipStream_t st, const cly_tuple* d_tup, u
         OCK(hipMalloc((void**)&d_tie, m));
         hipLaunchKernelGGL(k_ord_key0, dim3(ogrid(m)), dim3(256), 0, st, d_sel, m, d_tup, d_fb, nf, d_k0, d_k1, d_pa);
         // LSD: by k1 (stable), then by k0 (stable): the 128-bit order
-        OCK(hipcub::DeviceRadixSort::SortPairs(d_tmp, need = tmp_bytes, d_k1, d_ka, d_pa, d_pb, (int)m, 0, 64, st));
+        OCK(rocprim::radix_sort_pairs(d_tmp, need = tmp_bytes, d_k1, d_ka, d_pa, d_pb, (size_t)m, 0u, 64u, st));
         hipLaunchKernelGGL(k_ord_gather, dim3(ogrid(m)), dim3(256), 0, st, d_k0, d_pb, m, d_ka);
-        OCK(hipcub::DeviceRadixSort::SortPairs(d_tmp, need = tmp_bytes, d_ka, d_k0, d_pb, d_pa, (int)m, 0, 64, st));
+        OCK(rocprim::radix_sort_pairs(d_tmp, need = tmp_bytes, d_ka, d_k0, d_pb, d_pa, (size_t)m, 0u, 64u, st));
         hipLaunchKernelGGL(k_ord_fin0, dim3(ogrid(m)), dim3(256), 0, st, d_sel, d_pa, m, d_k0, d_k1, d_ord, d_tie,
                            d_cnt + 1);
         OCK(hipGetLastError());
@@ -187,8 +191,8 @@ extern "C" int cly_order_keys_internal(hipStream_t st, const cly_tuple* d_tup, u
             uint32_t* d_P = d_sel;
             hipLaunchKernelGGL(k_ord_inrun, dim3(ogrid(m)), dim3(256), 0, st, d_tie, m, d_inrun);
             OCK(hipMemsetAsync(d_cnt, 0, sizeof(h_cnt), st));
-            OCK(hipcub::DeviceSelect::Flagged(d_tmp, need = tmp_bytes, hipcub::CountingInputIterator<uint32_t>(0),
-                                              d_inrun, d_P, d_cnt, (int)m, st));
+            OCK(rocprim::select(d_tmp, need = tmp_bytes, rocprim::counting_iterator<uint32_t>(0),
+                                              d_inrun, d_P, d_cnt, (size_t)m, st));
             OCK(hipMemcpyAsync(h_cnt, d_cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
             OCK(hipStreamSynchronize(st));
             const uint64_t np = h_cnt[0];
@@ -201,16 +205,16 @@ extern "C" int cly_order_keys_internal(hipStream_t st, const cly_tuple* d_tup, u
             hipLaunchKernelGGL(k_ord_keyr, dim3(ogrid(np)), dim3(256), 0, st, d_P, np, d_ord, d_tie, d_tup, d_fb, nf,
                                off, d_key, d_val, d_aux);
             // segment begins: the run starts among the members (+ np at the end)
-            OCK(hipcub::DeviceSelect::Flagged(d_tmp, need = tmp_bytes, hipcub::CountingInputIterator<uint32_t>(0),
-                                              d_aux, d_vb, d_cnt + 2, (int)np, st));
+            OCK(rocprim::select(d_tmp, need = tmp_bytes, rocprim::counting_iterator<uint32_t>(0),
+                                              d_aux, d_vb, d_cnt + 2, (size_t)np, st));
             OCK(hipMemcpyAsync(h_cnt, d_cnt, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
             OCK(hipStreamSynchronize(st));
             const uint64_t nseg = h_cnt[2];
             const uint32_t np32 = (uint32_t)np;
             OCK(hipMemcpyAsync(d_vb + nseg, &np32, sizeof(uint32_t), hipMemcpyHostToDevice, st));
             size_t sneed = 0;
-            OCK(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, sneed, d_key, d_keys, d_val, d_vals, (int)np,
-                                                            (int)nseg, d_vb, d_vb + 1, 0, 64, st));
+            OCK(rocprim::segmented_radix_sort_pairs(nullptr, sneed, d_key, d_keys, d_val, d_vals, (unsigned)np,
+                                                        (unsigned)nseg, d_vb, d_vb + 1, 0u, 64u, st));
             if (sneed > tmp_bytes) {
                 OCK(hipStreamSynchronize(st));
                 hipFree(d_tmp);
@@ -218,8 +222,8 @@ extern "C" int cly_order_keys_internal(hipStream_t st, const cly_tuple* d_tup, u
                 tmp_bytes = sneed;
                 OCK(hipMalloc(&d_tmp, tmp_bytes));
             }
-            OCK(hipcub::DeviceSegmentedRadixSort::SortPairs(d_tmp, sneed, d_key, d_keys, d_val, d_vals, (int)np,
-                                                            (int)nseg, d_vb, d_vb + 1, 0, 64, st));
+            OCK(rocprim::segmented_radix_sort_pairs(d_tmp, sneed, d_key, d_keys, d_val, d_vals, (unsigned)np,
+                                                        (unsigned)nseg, d_vb, d_vb + 1, 0u, 64u, st));
             OCK(hipMemsetAsync(d_cnt + 1, 0, sizeof(unsigned long long), st));
             hipLaunchKernelGGL(k_ord_scatter, dim3(ogrid(np)), dim3(256), 0, st, d_P, np, d_keys, d_vals, d_aux,
                                d_ord, d_tie, d_cnt + 1);

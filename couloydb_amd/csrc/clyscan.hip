@@ -88,13 +88,24 @@ __device__ __forceinline__ rsrc_t mk_rsrc(const void* p, uint32_t bytes) {
 #endif
 // Spill: records CAP_T.. of a tile go to chunks of CAP_T entries (and their
 // snapshots) taken from a per-call pool; a tile's chunk table holds up to
-// NCH_MAX chunk ids and, in word CH_NWORD, how many it took.  Records are at
-// least 9 bytes (header of 4 + 1 + 1 + three 1-byte varints) except at a
-// file's end, so a tile holds at most CLY_TILE / 9 + 1 <= (NCH_MAX + 1) CAP_T.
+// NCH_MAX chunk ids and, in word CH_NWORD, how many it took.  Chain density:
+// a record whose three varints end normally has headerSize >= 9.  The only
+// shorter records (4 <= headerSize <= 6, step_hdr) have an expiration varint
+// that overflows at its 10th byte: 9 continuation bytes, then a byte in 2..127.
+// The next record's key-size varint starts inside those 9 bytes unless the
+// record is >= 9 bytes long, so its first byte below 0x80 is that 10th byte,
+// reached at index 9 or 10 by the key-size or value-size varint (an overflow:
+// a negative index, ERR_VARINT) or only by its expiration varint, which needs
+// the key and value varints to fit in front of it: impossible after <= 8 bytes.
+// So a chain holds at most one record under 9 bytes before it ends, plus the
+// short-buffer records of a file's last 26 bytes (at most 5): a tile holds at
+// most CLY_TILE / 9 + 7 <= (NCH_MAX + 1) CAP_T records.  The bound is checked
+// anyway: a chunk index past NCH_MAX stores nothing and fails the call
+// (CLY_ERR_DEVICE, "internal error 0x80") instead of indexing past the table.
 #define NCH_MAX 14
 #define CH_WORDS 16
 #define CH_NWORD 15
-static_assert((NCH_MAX + 1) * (CLY_TILE / 128) >= CLY_TILE / 9 + 1, "spill chunks per tile");
+static_assert((NCH_MAX + 1) * (CLY_TILE / 128) >= CLY_TILE / 9 + 7, "spill chunks per tile");
 static_assert((CAP_T & (CAP_T - 1)) == 0 && CAP_T >= 64, "CAP_T: a power of two, >= a round of 64 records");
 
 struct DevFile {                 // 32 B
@@ -595,17 +606,20 @@ struct RecSink {
     uint32_t* ctab;              // the tile's chunk table (CH_WORDS words)
     Globals* g;
 };
+// (a chunk index past the table: nothing stored, spill_ensure failed the call)
 __device__ __forceinline__ void rec_put(const RecSink& rs, uint32_t idx, const u32x4& v) {
     if (idx < CAP_T) __builtin_amdgcn_raw_buffer_store_b128(v, rs.trs, (int)(idx * 16u), 0, 0);
     else {
-        const uint32_t c = rs.chk[(idx >> CAP_SHIFT) - 1u];
+        const uint32_t ci = (idx >> CAP_SHIFT) - 1u;
+        const uint32_t c = ci < NCH_MAX ? rs.chk[ci] : NONE32;
         if (c != NONE32) rs.sp_rec[(uint64_t)c * CAP_T + (idx & (CAP_T - 1u))] = v;
     }
 }
 __device__ __forceinline__ void snap_put(const RecSink& rs, uint32_t r, uint32_t v) {
     if (r < CAP_T) __builtin_amdgcn_raw_buffer_store_b32(v, rs.nrs, (int)(r * 4u), 0, 0);
     else {
-        const uint32_t c = rs.chk[(r >> CAP_SHIFT) - 1u];
+        const uint32_t ci = (r >> CAP_SHIFT) - 1u;
+        const uint32_t c = ci < NCH_MAX ? rs.chk[ci] : NONE32;
         if (c != NONE32) rs.sp_snap[(uint64_t)c * CAP_T + (r & (CAP_T - 1u))] = v;
     }
 }
@@ -782,10 +796,10 @@ __device__ __forceinline__ void spill_ensure(TState& S, uint32_t hi, const RecSi
                 if (S.nch < NCH_MAX) {
                     id = atomicAdd(&rs.g->spill_next, 1u);
                     if (id >= rs.g->spill_cap) { atomicOr(&rs.g->spill_over, 1u); id = NONE32; }
-                } else atomicOr(&rs.g->fail, 128u);                  // (records >= 9 B: never)
+                } else atomicOr(&rs.g->fail, 128u);                  // (chain density: never)
                 if (S.nch < NCH_MAX) { rs.chk[S.nch] = id; rs.ctab[S.nch] = id; }
             }
-            S.nch_have = S.nch + 1u;
+            S.nch_have = S.nch < NCH_MAX ? S.nch + 1u : NCH_MAX;
         }
         S.nch++;
     }
@@ -1051,7 +1065,7 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     // k_scan starts the tile's chunk list; k_refix reuses the chunks k_scan took
     S.nch_have = BM == BM_SPEC ? 0u : __builtin_amdgcn_readfirstlane(ctab[CH_NWORD]);
     if (BM != BM_SPEC) {
-        if ((uint32_t)lane < S.nch_have) chk[lane] = ctab[lane];
+        if ((uint32_t)lane < S.nch_have && lane < NCH_MAX) chk[lane] = ctab[lane];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
@@ -1804,7 +1818,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
        const uint32_t* __restrict__ seg, const uint32_t* __restrict__ snap, uint32_t* treg, FileInfo* finfo,
        const uint32_t* __restrict__ tabs, cly_tuple* out_, uint64_t out_cap, const uint32_t* __restrict__ chunks,
        const u32x4* __restrict__ sp_rec, const uint32_t* __restrict__ sp_snap, Globals* g, int slot) {
-    if (g->nfix[slot] || g->spill_over) return;     // the chain is not final yet (k_refix first) / run again
+    if (g->nfix[slot] || g->spill_over || g->fail) return;   // the chain is not final yet (k_refix first) / run again / failed
     gtuples out = (gtuples)out_;
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[EMIT_LDS];
     CLY_LDS uint32_t* emt = (CLY_LDS uint32_t*)smem_raw;
@@ -2117,7 +2131,7 @@ k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __rest
     __shared__ uint32_t tabl[NIB_SH * 128 + 128];           // TAB_SH, TAB_TILE
     __shared__ uint32_t px[FIN_NT], pc[FIN_NT];
     __shared__ uint32_t mlev[16];
-    if (g->nfix[slot] || g->spill_over) return;     // k_emit did not run
+    if (g->nfix[slot] || g->spill_over || g->fail) return;   // k_emit did not run
     for (int i = threadIdx.x; i < NIB_SH * 128 + 128; i += FIN_NT) tabl[i] = tabs[TAB_SH + i];
     const CLY_LDS uint32_t* sht = (const CLY_LDS uint32_t*)tabl;
     const CLY_LDS uint32_t* tilet = sht + NIB_SH * 128;
@@ -2207,7 +2221,6 @@ struct cly_ctx {
 };
 extern "C" void cly_merge_scratch_free(void* p);
 
-extern "C" void cly_load_stage_init_internal();     // clyload.hip
 extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     if (!out) return CLY_ERR_ARG;
     *out = nullptr;
@@ -2257,7 +2270,6 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
         c->emit_grid = per_cu * ncu;
         c->loc_grid = ncu;
     }
-    cly_load_stage_init_internal();       // the load driver's page-locked staging (once per process)
     *out = c;
     return CLY_OK;
 }
@@ -2536,6 +2548,25 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
         }
         res[i]._pad = 0;
         total += res[i].n_records;
+        // A part's view ends VIEW_MAX past its first byte: a record of 2+ GiB that
+        // starts there and passes the view's end reads as torn although the file
+        // holds it whole.  Such a terminal is decoded again against the whole
+        // file: a record there is beyond this library's limit (CLY_ERR_ARG), not
+        // the io.EOF ReadLogRecord would not return.
+        if (res[i].status == CLY_END_TORN) {
+            const uint64_t T = (uint64_t)res[i].end_offset, x0 = (T / PART_BYTES) * PART_BYTES;
+            if (files[i].len - x0 > VIEW_MAX) {
+                uint8_t hb[26] = {0};
+                const uint64_t nh = files[i].len - T < 26 ? files[i].len - T : 26;
+                HIPCK(hipMemcpy(hb, files[i].base + T, nh, hipMemcpyDeviceToHost));
+                const Hdr h = step_hdr((const uint8_t*)hb, 0, (int64_t)(files[i].len - T), (int64_t)T);
+                if (h.status == REC_OK) {
+                    fprintf(stderr, "clyscan: file %d: a record of %lld B at %llu crosses a part's 4-GiB view\n", i,
+                            (long long)h.size, (unsigned long long)T);
+                    return CLY_ERR_ARG;
+                }
+            }
+        }
     }
     if (needed) *needed = c->h_g->total;
     if (stats) {

@@ -91,6 +91,13 @@ typedef struct cly_db_options {
 } cly_db_options;
 #define CLY_DB_APPLY_SWEEP 1u
 
+/* Optional start-up call of a process that will open databases: allocates
+ * the load driver's page-locked staging (16 copy threads x 2 x 8 MiB) now, so
+ * that the first open does not (without it each copy thread allocates its
+ * pair at first use: 15-25 ms more on a first open).  The current device's
+ * context must exist.  Tried once per process; CLY_OK, or CLY_ERR_DEVICE
+ * (remembered; the opens still work, allocating lazily).                     */
+int  cly_load_prepare(void);
 /* cly_db_open = cly_db_open_opts with default options (nothing written).    */
 int  cly_db_open(cly_ctx* ctx, const char* dir, cly_db** out, cly_load_stats* st);
 int  cly_db_open_opts(cly_ctx* ctx, const char* dir, const cly_db_options* opt, cly_db** out, cly_load_stats* st);

@@ -51,7 +51,10 @@ extern "C" {
 
 /* A data file (`%09d.cly`, hint-index or merge-finished file).  For cly_scan the
  * base is host memory (typically an mmap of the file); for cly_scan_device it is
- * device memory (HBM) that holds the file's bytes.  len must be < 2^32.        */
+ * device memory (HBM) that holds the file's bytes.  len < 2^47 (files are
+ * walked in parts of 2 GiB, each seeing up to 4 GiB - 128 KiB from its start:
+ * a record of over 2 GiB that crosses a part's end beyond that view fails the
+ * call with CLY_ERR_ARG).                                                      */
 typedef struct cly_file {
     const uint8_t* base;
     uint64_t       len;

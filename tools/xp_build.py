@@ -28,9 +28,9 @@ SCAN_ONLY = [("    if (guard >= 0 && g->nfix[guard] == 0) return;  // (device ro
               "    if (g->walk_max != 12345678u) return;"),
              ("    if (g->nfix[slot] == 0) return;                        // (uniform: before the LDS setup's barrier)",
               "    if (g->walk_max != 12345678u) return;"),
-             ("    if (g->nfix[slot] || g->spill_over) return;     // the chain is not final yet (k_refix first) / run again",
+             ("    if (g->nfix[slot] || g->spill_over || g->fail) return;   // the chain is not final yet (k_refix first) / run again / failed",
               "    if (g->walk_max != 12345678u) return;"),
-             ("    if (g->nfix[slot] || g->spill_over) return;     // k_emit did not run",
+             ("    if (g->nfix[slot] || g->spill_over || g->fail) return;   // k_emit did not run",
               "    if (g->walk_max != 12345678u) return;")]
 for k in ("nocomp", "noseg", "nosnap", "nostore"):
     PATCHES[k] = PATCHES[k] + SCAN_ONLY
@@ -108,6 +108,14 @@ PATCHES["prof"] = [
             c->h_g->xp_t[6], c->h_g->xp_t[7], (unsigned long long)(c->h_g->walk_dbg >> 40));
     float ms_scan = 0, ms_link = 0, ms_emit = 0, ms_fin = 0;"""),
 ]
+# every tile's loads read its part's first tile (L2-resident): k_scan's time with
+# the HBM latency taken out, same record work (timing only)
+PATCHES["l2"] = [
+    ("""    const uint32_t off = bs + 64u * (uint32_t)(lane & 15) + 16u * (uint32_t)(lane >> 4);""",
+     """    const uint32_t off = (bs & (CLY_TILE - 1u)) + 64u * (uint32_t)(lane & 15) + 16u * (uint32_t)(lane >> 4);"""),
+    ("""    if (lane < 2) hl = load16z(base, (uint64_t)bs + CLY_BLK + 16 * lane, flen);""",
+     """    if (lane < 2) hl = load16z(base, (uint64_t)((bs + CLY_BLK) & (CLY_TILE - 1u)) + 16 * lane, flen);"""),
+] + SCAN_ONLY
 PATCHES["gp1"] = [("#define GP_TRIES 2 ", "#define GP_TRIES 1 ")]
 PATCHES["gp3"] = [("#define GP_TRIES 2 ", "#define GP_TRIES 3 ")]
 PATCHES["sloopcnt"] = PATCHES["sloop"] + PATCHES["cnt"]
