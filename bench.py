@@ -342,6 +342,22 @@ def index_load_leg(wl, sc):
         shutil.rmtree(d, ignore_errors=True)
 
 
+def c5_leg(sc, torch, device, steps=5):
+    """BASELINE config 5 on one GPU: one rank's 32-GiB fid range of the C2/C3
+    mix, the same step as the --gpus N > 1 lines time (their per-GPU share), so
+    that the driver's 1/2/4/8-GPU lines have a c5 reference at N = 1."""
+    wl = make_workload("c5", torch, rank=0, device=device)
+    best, kscan, need, res = timed_scans(sc, wl.dev_files, wl.d_out.data_ptr(), wl.out_cap, reps=steps)
+    out = {"workload": "c5", "bytes": wl.bytes, "files": len(wl.dev_files), "records": int(need),
+           "value": round(wl.bytes / best / 2**30, 2), "unit": "GiB/s", "ms": round(best * 1e3, 3),
+           "k_scan_ms": round(kscan, 3), "k_scan_frac": round(wl.bytes / (kscan / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+           "ok": bool(need == wl.expect_records and all(r.status == 0 for r in res)),
+           "note": "best of %d device-resident scans (the N>1 lines' per-rank step)" % steps}
+    del wl
+    torch.cuda.empty_cache()
+    return out
+
+
 def timed_scans(sc, files, d_out, cap, reps=5):
     """reps device-resident scans of files (after one untimed): best wall time
     per scan, the k_scan time, the record count and the statuses."""
@@ -496,7 +512,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default=None, choices=["c1", "c2", "c3", "c4", "c5"],
+                    help="default: c2 at --gpus 1 (BASELINE config 2), c5 at --gpus N > 1 (config 5: a 32-GiB "
+                         "fid range per GPU, 256 GiB at 8)")
+    ap.add_argument("--no-c5-leg", action="store_true", help="skip the N=1 line's C5 reference leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
     ap.add_argument("--verify", action="store_true", help="check one file against the oracle after timing")
@@ -519,6 +538,8 @@ def main():
     if args.dry_protocol:
         dry_protocol(args, rank, world)
         return
+    if args.config is None:
+        args.config = "c5" if world > 1 else "c2"
 
     import torch
     import torch.distributed as dist
@@ -675,6 +696,9 @@ def main():
             # the record source of db.loadIndex (db.go:582-637) from mmap'd files to
             # index tuples in host memory (the cgo path's rate)
             out["host_scan_wall_ms"] = hp["ms"]
+    if args.config == "c2" and world == 1 and not args.no_c5_leg:
+        # the N = 1 point of config 5's scaling curve (the --gpus N > 1 lines run c5)
+        out["c5_n1"] = c5_leg(sc, torch, local)
     if args.config == "c2" and rank == 0 and world == 1 and not args.no_host_path:
         out["index_load"] = index_load_leg(wl, sc)
         out["index_load_wall_ms"] = out["index_load"]["wall_ms"]

@@ -164,8 +164,9 @@ def load_scan_lib(name="libclyscan.so"):
     lib.cly_db_entries.restype = ctypes.c_uint64
     lib.cly_db_close.argtypes = [ctypes.c_void_p]
     lib.cly_db_close.restype = None
-    lib.cly_load_prepare.argtypes = []
-    lib.cly_load_prepare.restype = ctypes.c_int
+    if hasattr(lib, "cly_load_prepare"):          # (libraries of earlier builds, tools/build_r3_lib.sh)
+        lib.cly_load_prepare.argtypes = []
+        lib.cly_load_prepare.restype = ctypes.c_int
     for fn in ("cly_db_get", "cly_db_listmeta"):
         getattr(lib, fn).argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p]
         getattr(lib, fn).restype = ctypes.c_int

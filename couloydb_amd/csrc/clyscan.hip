@@ -1438,7 +1438,8 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
 // computes every file's first tuple index (exclusive prefix over the files'
 // record totals) and the call's total.
 #define LINK_NT 1024
-#define LINK_MAXT 131072         // tiles per file tracked in the contradiction bitmask (8-GiB files)
+#define LINK_MAXT 131072         // tiles per file whose contradiction / anchor bitmasks fit LDS (8-GiB files);
+                                 // a longer file's are in global memory (lmask, words first_tile / 32 + f on)
 #define RF_ID 0
 #define RF_CONST 1
 #define RF_FOF 2
@@ -1479,12 +1480,12 @@ __device__ __forceinline__ LBState rf_apply(const RunF& f, LBState s) {
 #define LINK_PER 4               // tiles per thread held in registers (more: re-read)
 __global__ void __launch_bounds__(LINK_NT)
 k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restrict__ loc, TileIn* tin,
-       uint64_t* ftotal, FileInfo* finfo, uint32_t* fixlist, Globals* g, int slot, int guard) {
+       uint64_t* ftotal, FileInfo* finfo, uint32_t* fixlist, uint32_t* lmask, uint64_t lmask_words, Globals* g,
+       int slot, int guard) {
     if (guard >= 0 && g->nfix[guard] == 0) return;  // (device round: nothing was re-resolved)
     __shared__ RunF rf[2][LINK_NT];
-    __shared__ uint32_t badm[LINK_MAXT / 32];
-    __shared__ uint32_t ancm[LINK_MAXT / 32];  // anchors: a run's first tile with a boundary, not contradicted
-    __shared__ uint32_t bad_far;             // a contradicted tile beyond the bitmask (listed alone)
+    __shared__ uint32_t badm_l[LINK_MAXT / 32];
+    __shared__ uint32_t ancm_l[LINK_MAXT / 32];  // anchors: a run's first tile with a boundary, not contradicted
     __shared__ uint64_t part[LINK_NT];
     __shared__ uint64_t carry;
     __shared__ int last;
@@ -1494,6 +1495,15 @@ k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restric
     const uint32_t nt = F.ntile, per = (nt + LINK_NT - 1) / LINK_NT;
     const uint32_t lo = tid * per < nt ? tid * per : nt, hi = lo + per < nt ? lo + per : nt;
     const TileLocal* L0 = loc + F.first_tile;
+    // the bitmasks: LDS, or for a file of more than LINK_MAXT tiles its words of
+    // lmask (generic pointers either way; reads of lmask bypass the L1)
+    const uint32_t nw = (nt + 31) / 32;
+    const bool far = nt > LINK_MAXT;
+    uint32_t* badm = far ? lmask + F.first_tile / 32 + (uint32_t)f : (uint32_t*)badm_l;
+    uint32_t* ancm = far ? lmask + lmask_words + F.first_tile / 32 + (uint32_t)f : (uint32_t*)ancm_l;
+    auto bit = [](const uint32_t* m, uint32_t u) {
+        return (__hip_atomic_load(m + (u >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (u & 31)) & 1u;
+    };
     u64 c0[LINK_PER], c1[LINK_PER], c2[LINK_PER], c3[LINK_PER];
     #pragma unroll
     for (int k = 0; k < LINK_PER; k++) {
@@ -1509,8 +1519,11 @@ k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restric
     // inclusive Kogge-Stone scan of the run functions
     int cur = 0;
     rf[0][tid] = my;
-    for (int i = tid; i < LINK_MAXT / 32; i += LINK_NT) { badm[i] = 0; ancm[i] = 0; }
-    if (tid == 0) bad_far = NONE32;
+    for (uint32_t i = tid; i < (far ? nw : (uint32_t)(LINK_MAXT / 32)); i += LINK_NT) {
+        __hip_atomic_store(badm + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ancm + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (far) __threadfence();
     __syncthreads();
     for (int d = 1; d < LINK_NT; d <<= 1) {
         RunF v = rf[cur][tid];
@@ -1536,45 +1549,34 @@ k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restric
             else bad = s.X != x0 + (uint32_t)l1;
         }
         ti_store(&tin[F.first_tile + u], s, (uint32_t)f);
-        if (bad) {
-            if (u < LINK_MAXT) atomicOr(&badm[u >> 5], 1u << (u & 31));
-            else atomicMin(&bad_far, u);
-        } else if (u < LINK_MAXT && (u == 0 || (u % rt == 0 && !(l0 & DF_NONE))))
-            atomicOr(&ancm[u >> 5], 1u << (u & 31));
+        if (bad) atomicOr(&badm[u >> 5], 1u << (u & 31));
+        else if (u == 0 || (u % rt == 0 && !(l0 & DF_NONE))) atomicOr(&ancm[u >> 5], 1u << (u & 31));
         s = rf_apply(rf_tile(l0, l1, l2, x0), s);
     };
     #pragma unroll
     for (int k = 0; k < LINK_PER; k++)
         if (lo + k < hi) visit(lo + k, c0[k], c1[k], c2[k], c3[k]);
     for (uint32_t u = lo + LINK_PER; u < hi; u++) visit(u, L0[u].l[0], L0[u].l[1], L0[u].l[2], L0[u].l[3]);
+    if (far) __threadfence();
     __syncthreads();
     // list a contradicted tile only when no contradicted tile lies between it
     // and the anchor before it (the state entering it then comes from tiles
     // whose chains are right; a tile that carried a wrong exit, or passed one
     // through without a boundary, would enter it with a false state and send
     // its walk down a false chain)
-    for (uint32_t u = lo; u < hi && u < LINK_MAXT; u++) {
-        const bool bu = (badm[u >> 5] >> (u & 31)) & 1u;
+    for (uint32_t u = lo; u < hi; u++) {
+        const bool bu = bit(badm, u);
         bool bp = false;
         if (bu && u > 0) {
             for (uint32_t v = u - 1;; v--) {
-                if ((badm[v >> 5] >> (v & 31)) & 1u) { bp = true; break; }
-                if (v == 0 || ((ancm[v >> 5] >> (v & 31)) & 1u)) break;
+                if (bit(badm, v)) { bp = true; break; }
+                if (v == 0 || bit(ancm, v)) break;
             }
         }
         if (bu && !bp) {
             const uint32_t k = atomicAdd(&g->nfix[slot], 1u);
             fixlist[k] = F.first_tile + u;
             tin[F.first_tile + u].w[3] |= TI_FIX;
-        }
-    }
-    if (tid == 0 && bad_far != NONE32) {
-        bool any_near = false;
-        for (int i = 0; i < LINK_MAXT / 32; i++) any_near |= badm[i] != 0;
-        if (!any_near) {
-            const uint32_t k = atomicAdd(&g->nfix[slot], 1u);
-            fixlist[k] = F.first_tile + bad_far;
-            tin[F.first_tile + bad_far].w[3] |= TI_FIX;
         }
     }
     // the workgroup that finishes last: the file bases (its acquire sees every
@@ -2205,6 +2207,8 @@ struct cly_ctx {
     TileLocal* d_loc; TileIn* d_tin; uint32_t* d_treg; uint32_t* d_fix; uint32_t* d_rec;
     uint32_t* d_seg; uint32_t* d_snap;   // segment registers, snapshots
     uint32_t* d_chunks;          // per tile CH_WORDS words: spill chunk ids and their count
+    uint32_t* d_lmask;           // k_link's bitmasks of files past LINK_MAXT tiles (2 x lmask_words)
+    uint64_t lmask_words;
     int64_t cap_tiles;
     u32x4* d_sp_rec; uint32_t* d_sp_snap; uint32_t cap_spill;   // the spill pool (chunks of CAP_T entries)
     Globals* d_g; Globals* h_g;
@@ -2280,7 +2284,7 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     hipStreamSynchronize(c->stream);
     hipFree(c->d_call); hipFree(c->d_ftotal);
     hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_rec);
-    hipFree(c->d_seg); hipFree(c->d_snap); hipFree(c->d_chunks); hipFree(c->d_sp_rec); hipFree(c->d_sp_snap);
+    hipFree(c->d_seg); hipFree(c->d_snap); hipFree(c->d_chunks); hipFree(c->d_lmask); hipFree(c->d_sp_rec); hipFree(c->d_sp_snap);
     hipFree(c->d_tabs); hipFree(c->d_pw); hipFree(c->d_bytes); hipFree(c->d_tuples); hipFree(c->d_dbg);
     hipHostFree(c->h_call);
     cly_merge_scratch_free(c->merge_scratch);
@@ -2325,7 +2329,8 @@ static int ensure_files(cly_ctx* c, int nfiles) {
 static int ensure_tiles(cly_ctx* c, int64_t ntiles) {
     if (ntiles <= c->cap_tiles) return CLY_OK;
     hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_rec);
-    hipFree(c->d_seg); hipFree(c->d_snap); hipFree(c->d_chunks);
+    hipFree(c->d_seg); hipFree(c->d_snap); hipFree(c->d_chunks); hipFree(c->d_lmask);
+    c->d_lmask = nullptr; c->lmask_words = 0;
     c->d_loc = nullptr; c->d_tin = nullptr; c->d_treg = nullptr; c->d_fix = nullptr; c->d_rec = nullptr;
     c->d_seg = nullptr; c->d_snap = nullptr; c->d_chunks = nullptr;
     c->cap_tiles = 0;
@@ -2339,6 +2344,17 @@ static int ensure_tiles(cly_ctx* c, int64_t ntiles) {
     HIPCK(hipMalloc(&c->d_fix, sizeof(uint32_t) * cap));
     HIPCK(hipMalloc(&c->d_rec, sizeof(uint32_t) * 4 * (uint64_t)CAP_T * cap));
     c->cap_tiles = cap;
+    return CLY_OK;
+}
+// k_link's global bitmasks (files of more than LINK_MAXT tiles): file f's words
+// start at first_tile / 32 + f, so no two files share one
+static int ensure_lmask(cly_ctx* c, int64_t ntiles, int nfiles) {
+    const uint64_t words = (uint64_t)ntiles / 32 + (uint64_t)nfiles + 2;
+    if (words <= c->lmask_words) return CLY_OK;
+    hipFree(c->d_lmask);
+    c->d_lmask = nullptr; c->lmask_words = 0;
+    HIPCK(hipMalloc(&c->d_lmask, sizeof(uint32_t) * 2 * words));
+    c->lmask_words = words;
     return CLY_OK;
 }
 
@@ -2407,6 +2423,11 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
     c->h_rprefix[nfiles] = (uint32_t)nruns;
     rc = ensure_tiles(c, ntiles);
     if (rc) return rc;
+    {
+        bool far = false;
+        for (int i = 0; i < nfiles; i++) far |= c->h_files[i].ntile > LINK_MAXT;
+        if (far && (rc = ensure_lmask(c, ntiles, nfiles))) return rc;
+    }
     rc = ensure_spill(c, (uint64_t)ntiles / 8 + 64);
     if (rc) return rc;
     memset(c->h_g, 0, sizeof(Globals));
@@ -2436,14 +2457,14 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
     // k_emit/k_fin, which return at once if the link listed tiles; only then
     // the host waits.  Repair rounds (k_refix + k_link) follow on the host loop.
     hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_loc, c->d_tin, c->d_ftotal,
-                       c->d_finfo, c->d_fix, c->d_g, 0, -1);
+                       c->d_finfo, c->d_fix, c->d_lmask, c->lmask_words, c->d_g, 0, -1);
     // one repair round on the device, without a host wait: k_refix and
     // k_link return at once when the first link listed no tile
     hipLaunchKernelGGL(k_refix, dim3(REFIX_GRID), dim3(64 * SCAN_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix,
                        c->d_loc, c->d_tin, c->d_rec, c->d_seg, c->d_snap, c->d_treg, c->d_chunks, c->d_sp_rec,
                        c->d_sp_snap, c->d_fix, c->d_g, 0);
     hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_loc, c->d_tin, c->d_ftotal,
-                       c->d_finfo, c->d_fix, c->d_g, 1, 0);
+                       c->d_finfo, c->d_fix, c->d_lmask, c->lmask_words, c->d_g, 1, 0);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[2], st));
     int slot = 1;
@@ -2498,7 +2519,7 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
                                c->d_files, nfiles, c->d_tprefix, c->d_loc, c->d_tin, c->d_rec, c->d_seg, c->d_snap,
                                c->d_treg, c->d_chunks, c->d_sp_rec, c->d_sp_snap, c->d_fix, c->d_g, slot);
             hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_loc, c->d_tin,
-                               c->d_ftotal, c->d_finfo, c->d_fix, c->d_g, ns, -1);
+                               c->d_ftotal, c->d_finfo, c->d_fix, c->d_lmask, c->lmask_words, c->d_g, ns, -1);
             HIPCK(hipGetLastError());
             HIPCK(hipMemcpyAsync(c->h_g, c->d_g, sizeof(Globals), hipMemcpyDeviceToHost, st));
             HIPCK(hipStreamSynchronize(st));

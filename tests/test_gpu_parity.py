@@ -631,3 +631,51 @@ def test_gpu_file_past_4gib(corrupt):
     res = _scan_part_file("libclyscan.so", arr, 4_500_000_000 if corrupt else None)
     if not corrupt:
         assert res[0].status != _abi.ERR_CRC and res[0].end_offset > 1 << 32
+
+
+def _tile_bytes(lib):
+    info = _abi.load_scan_lib(lib).cly_build_info().decode()
+    return int(info.split("TILE=")[1].split()[0])
+
+
+def test_tiny_record_file_past_link_mask(scanner):
+    """A data file of 12-30-B records longer than k_link's LDS bitmasks cover
+    (131072 tiles: 8 GiB in the product build, 1 GiB in the 8-KiB-tile build;
+    Options.DataFileSize is an int64, options.go:10,70-71): its contradiction
+    and anchor bitmasks live in global memory, every contradicted tile is
+    listed in the same repair round (no one-tile-per-round fallback), the
+    scan finishes in <= 4 link passes, and every tuple is bit-exact against the
+    oracle's tuples of the repeated 4-MiB unit (records tile exactly: tuple j
+    is the unit's tuple j % n with its offset moved by (j // n) units).""" 
+    torch = pytest.importorskip("torch")
+    base = np.frombuffer(tiny_records(11, 4 << 20), np.uint8)
+    tb, st0, end0 = co.scan_file(base.copy(), 9)
+    assert st0 == 0 and end0 == len(base)
+    n = len(tb)
+    limit = 131072 * _tile_bytes(scanner.lib_name)
+    reps = limit // len(base) + 1 + (limit // 8) // len(base)      # 1/8 past the mask
+    d = torch.from_numpy(base.copy()).cuda().repeat(reps)
+    total = n * reps
+    out = torch.empty((total + 64) * 48, dtype=torch.uint8, device="cuda")
+    with Scanner(0, lib=scanner.lib_name) as sc:
+        first, res, stt, need = sc.scan_device([(d.data_ptr(), d.numel(), 9)], out.data_ptr(), total + 64)
+        assert (res[0].status, res[0].n_records, res[0].end_offset, need) == (0, total, d.numel(), total)
+        # link rounds: the first, the device repair round, then host-driven
+        # rounds that re-resolve every listed tile at once (4 measured on the
+        # product build's 9-GiB file; one round per contradicted tile past the
+        # mask before round 6 would be thousands)
+        assert stt.passes <= 4, stt.passes
+        chunk = 1 << 26
+        for j0 in range(0, total, chunk):
+            j1 = min(total, j0 + chunk)
+            got = out[j0 * 48: j1 * 48].cpu().numpy().view(TUPLE_DTYPE)
+            j = np.arange(j0, j1, dtype=np.int64)
+            exp = tb[j % n].copy()
+            exp["offset"] += (j // n) * len(base)
+            assert (got.view(np.uint8) == exp.view(np.uint8)).all(), "tuples %d..%d" % (j0, j1)
+        # a flipped data-type byte past the LDS bitmasks' reach: ErrInvalidCRC there
+        k = total - 1000
+        off = int(tb["offset"][k % n]) + (k // n) * len(base)
+        d[off + 5] ^= 1
+        first, res, stt, need = sc.scan_device([(d.data_ptr(), d.numel(), 9)], out.data_ptr(), total + 64)
+        assert (res[0].status, res[0].n_records, res[0].end_offset) == (_abi.ERR_CRC, k, off)

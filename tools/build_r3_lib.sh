@@ -1,6 +1,6 @@
 #!/bin/bash
 # Rebuild couloydb_amd/libclyscan_r3.so (the round-3 library the same-box
-# comparisons in tools/gpu_cmp.sh time beside the current build) from commit
+# comparisons in tools/gpu/gpu_cmp.sh time beside the current build) from commit
 # d15e466, whose product sources hash to e028212b75f3 (cly_build_info).
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)

@@ -1,4 +1,4 @@
-"""Copy a tools/gpu_r5prof.sh run (gpurun_out/fin) into profiles/ under a tag:
+"""Copy a tools/gpu/gpu_r5prof.sh run (gpurun_out/fin) into profiles/ under a tag:
 the bench lines (C2 with the host path and index load, C3, C4), the rocprofv3
 kernel stats of the C2 / C3 / C4 scans (tools/scan_once.py: one launch per call
 over the configuration's own input) and of the C4 bench (scan + merge + hint

@@ -1,5 +1,5 @@
 #!/bin/bash
-# SQ instruction counts of the scan kernels: tools/gpu_pmc.sh OUT CFG...
+# SQ instruction counts of the scan kernels: tools/gpu/gpu_pmc.sh OUT CFG...
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 D=gpurun_out/$1; shift

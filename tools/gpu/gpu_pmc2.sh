@@ -1,5 +1,5 @@
 #!/bin/bash
-# stall/activity counters of the scan kernels: tools/gpu_pmc2.sh OUT CFG...
+# stall/activity counters of the scan kernels: tools/gpu/gpu_pmc2.sh OUT CFG...
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 D=gpurun_out/$1; shift

@@ -9,10 +9,10 @@ timeout -k 10 900 python -u -m pytest tests -q -x --timeout 300 --timeout-method
 rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/r4e/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python -u bench.py > gpurun_out/r4e/bench_c2.json 2> gpurun_out/r4e/bench_c2.err || exit $?
-CFG=c2 bash tools/gpu_xp.sh libclyscan.so "$@" || exit $?
+CFG=c2 bash tools/gpu/gpu_xp.sh libclyscan.so "$@" || exit $?
 timeout -k 10 400 python -u bench.py --config c4 --no-host-path --no-cpu-baseline > gpurun_out/r4e/bench_c4.json 2> gpurun_out/r4e/bench_c4.err || exit $?
 timeout -s KILL 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4e/c4_stats -o run -- python3 bench.py --config c4 --steps 3 --warmup 1 --no-host-path --no-cpu-baseline > gpurun_out/r4e/c4_stats.log 2>&1 || exit $?
 timeout -k 10 400 python -u bench.py --config c3 --no-host-path --no-cpu-baseline > gpurun_out/r4e/bench_c3.json 2> gpurun_out/r4e/bench_c3.err || exit $?
 echo done
-CFG=c3 bash tools/gpu_xp.sh libclyscan.so libclyscan_head.so || exit $?
+CFG=c3 bash tools/gpu/gpu_xp.sh libclyscan.so libclyscan_head.so || exit $?
 echo done2

@@ -8,7 +8,7 @@ cd "$GRAFT_REPO_ROOT"
 D=gpurun_out/fin
 mkdir -p $D
 export TMPDIR=/tmp
-bash tools/gpu_cmp.sh > $D/cmp.log 2>&1 || exit $?
+bash tools/gpu/gpu_cmp.sh > $D/cmp.log 2>&1 || exit $?
 cp gpurun_out/cmp/bench_c2.json $D/bench_c2.json
 timeout -k 10 400 python -u bench.py --config c4 --no-host-path --no-cpu-baseline > $D/bench_c4.json 2> $D/bench_c4.err || exit $?
 timeout -k 10 400 python -u bench.py --config c3 --no-host-path --no-cpu-baseline > $D/bench_c3.json 2> $D/bench_c3.err || exit $?

@@ -3,6 +3,6 @@
 # against the baseline (C2, C3, small records), then the open probe
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-bash tools/gpu_xpns.sh || exit $?
-bash tools/gpu_ab.sh libclyscan_xbase.so libclyscan_xsnap.so || exit $?
-bash tools/gpu_open2.sh
+bash tools/gpu/gpu_xpns.sh || exit $?
+bash tools/gpu/gpu_ab.sh libclyscan_xbase.so libclyscan_xsnap.so || exit $?
+bash tools/gpu/gpu_open2.sh

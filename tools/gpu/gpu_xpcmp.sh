@@ -1,5 +1,5 @@
 #!/bin/bash
-# same-box k_scan comparison of experiment builds: tools/gpu_xpcmp.sh CFG LIB...
+# same-box k_scan comparison of experiment builds: tools/gpu/gpu_xpcmp.sh CFG LIB...
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 D=gpurun_out/xpcmp

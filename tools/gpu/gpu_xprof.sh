@@ -10,4 +10,4 @@ for lib in libexp_profbase.so libexp_prof.so; do
   timeout -k 10 300 python3 tools/scan_once.py c3 2 $lib > $D/c3_$lib.log 2>&1 || exit $?
   grep "xp:" $D/c3_$lib.log | tail -1; tail -1 $D/c3_$lib.log
 done
-bash tools/gpu_ab.sh "$@"
+bash tools/gpu/gpu_ab.sh "$@"

@@ -233,6 +233,6 @@ int main() {
   hipMalloc(&seg, (size_t)ntiles * 1024 * 4);
   hipMalloc(&snap, (size_t)ntiles * 516 * 4);
 #define R(F) run<F>(buf, ntiles, rec, seg, snap, out)
-  R(0); R(1); R(3); R(7); R(7 + 64); R(15 + 64); R(31 + 64); R(63 + 64); R(63 + 64 + 4096); R(35 + 64); R(3 + 32);
+  R(7 + 64); R(15 + 64); R(7 + 64 + 8 + 1024); R(7 + 64 + 8 + 2048); R(7 + 64 + 8 + 512); R(35); R(35 + 128); R(35 + 512); R(127); R(127 - 8 + 2048); R(127 + 128); R(127 - 8 + 128);
   return 0;
 }
