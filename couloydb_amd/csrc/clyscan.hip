@@ -435,9 +435,11 @@ struct SegChain {
     int      term;               // terminal status, TERM_NONE if the chain leaves the segment
     uint32_t cnt;                // records starting in the segment
     uint32_t last, last_crc;     // last record start and its stored CRC
+    uint32_t sm0, sm1;           // the record starts: bit i = position cb + i
 };
 __device__ __forceinline__ void sc_set(SegChain& L, int mode) {
     L.mode = mode; L.E = NONE32; L.x = 0; L.term = TERM_NONE; L.cnt = 0; L.last = NONE32; L.last_crc = 0;
+    L.sm0 = L.sm1 = 0;
 }
 // Walk from p: exact (ReadLogRecord semantics, every terminal) or speculative
 // (every record one the writer produces; a terminal only at io.EOF at len).
@@ -455,6 +457,10 @@ __device__ __forceinline__ bool seg_walk(const Seg& K, uint32_t p, bool exact, S
         if (!exact && !h.good) return false;
         L.cnt++;
         L.last = p; L.last_crc = h.crc;
+        {
+            const uint32_t b = p - K.cb;             // (< 64: p is in the segment)
+            if (b < 32) L.sm0 |= 1u << b; else L.sm1 |= 1u << (b - 32);
+        }
         p += (uint32_t)h.size;
     }
     L.x = p;
@@ -512,6 +518,22 @@ __device__ __forceinline__ void wave_last_incl(uint32_t& v, uint32_t& f) {
     WL_STEP(DPP_ROW_SHR(8), 0xf) WL_STEP(DPP_ROW_BCAST15, 0xa) WL_STEP(DPP_ROW_BCAST31, 0xc)
 }
 __device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, 64); }
+
+// The position of the k-th set bit of the 64-bit mask (m0 | m1 << 32), k < its popcount.
+__device__ __forceinline__ uint32_t kth_bit(uint32_t m0, uint32_t m1, uint32_t k) {
+    const uint32_t c0 = (uint32_t)__builtin_popcount(m0);
+    uint32_t m = k < c0 ? m0 : m1, base = k < c0 ? 0u : 32u;
+    k = k < c0 ? k : k - c0;
+    #pragma unroll
+    for (int w = 16; w >= 1; w >>= 1) {
+        const uint32_t lc = (uint32_t)__builtin_popcount(m & ((1u << w) - 1u));
+        const bool up = k >= lc;
+        k = up ? k - lc : k;
+        m = up ? m >> w : m;
+        base += up ? (uint32_t)w : 0u;
+    }
+    return base;
+}
 
 // In-wave agreement: lane l's chain must start where the chain of the nearest
 // segment before it leaves (the block's entry X0 for the first lanes); lanes
@@ -588,25 +610,31 @@ __device__ __forceinline__ void tuple_words(gbytes base, uint32_t p, uint64_t x0
                     ((uint32_t)(tn < 0 ? 0xFF : tn) << 24),
                 h.crc};
 }
-// Compact entry (16 B), k_scan -> k_emit.  Short form (bit 26 of w3; every
-// record the writer produces without a TTL or a txId >= 64): w0 crc,
-// w1 ks (24 bits) | hsz-6 << 24 | type << 29, w2 vs, w3 rel | dt << 16 |
-// key0 << 19 (the txId varint's single byte).  Long form: w3 = rel only
-// (k_emit decodes the header again).
-#define REC_SHORT (1u << 26)
+// Compact entry (16 B), k_scan -> k_emit.  w0 crc; w1 the record's snapshot
+// (stored into the entry once the block's CRC pass has it: no snapshot stream
+// of its own); short form (bit 23 of w3; every record the writer produces
+// without a TTL or a txId >= 64, keys under 256 B, values under 2 MiB):
+// w2 vs (21 bits) | hsz-6 << 21 | type << 26 | dt << 29, w3 rel | key0 << 16
+// (the txId varint's single byte) | ks << 24.  Long form: w2 = 0, w3 = rel
+// only (k_emit decodes the header again).
+#define REC_SHORT (1u << 23)
+#define SH_KS_LIM 256u
+#define SH_VS_LIM (1u << 21)
 // Where a block's compact entries and snapshots go (k_scan, k_refix): stored
 // as they are made (an LDS sink flushed at the next block's top, after its
 // loads, measured 1.6 % slower on C2 and 3.3 % on C4), and the file record
 // checks of k_ovf's re-walk
 struct RecSink {
-    rsrc_t trs, nrs;             // the tile's own entries and snapshots
-    CLY_GL u32x4* sp_rec;        // the spill pool: entries, snapshots (chunk c at c CAP_T)
-    CLY_GL uint32_t* sp_snap;
+    rsrc_t trs;                  // the tile's own entries
+    CLY_GL u32x4* sp_rec;        // the spill pool's entries (chunk c at c CAP_T)
     CLY_LDS uint32_t* chk;       // the wave's copy of the tile's chunk ids
     uint32_t* ctab;              // the tile's chunk table (CH_WORDS words)
     Globals* g;
 };
-// (a chunk index past the table: nothing stored, spill_ensure failed the call)
+// The entry now (word 1 zero) and its snapshot into word 1 when the block's
+// CRC pass has it: two stores of one wave to the same bytes, applied in issue
+// order (one request queue per CU and L2 channel), merged in L2 into one line
+// write (a chunk index past the table: nothing stored, spill_ensure failed the call)
 __device__ __forceinline__ void rec_put(const RecSink& rs, uint32_t idx, const u32x4& v) {
     if (idx < CAP_T) __builtin_amdgcn_raw_buffer_store_b128(v, rs.trs, (int)(idx * 16u), 0, 0);
     else {
@@ -616,19 +644,19 @@ __device__ __forceinline__ void rec_put(const RecSink& rs, uint32_t idx, const u
     }
 }
 __device__ __forceinline__ void snap_put(const RecSink& rs, uint32_t r, uint32_t v) {
-    if (r < CAP_T) __builtin_amdgcn_raw_buffer_store_b32(v, rs.nrs, (int)(r * 4u), 0, 0);
+    if (r < CAP_T) __builtin_amdgcn_raw_buffer_store_b32(v, rs.trs, (int)(r * 16u + 4u), 0, 0);
     else {
         const uint32_t ci = (r >> CAP_SHIFT) - 1u;
         const uint32_t c = ci < NCH_MAX ? rs.chk[ci] : NONE32;
-        if (c != NONE32) rs.sp_snap[(uint64_t)c * CAP_T + (r & (CAP_T - 1u))] = v;
+        if (c != NONE32) ((CLY_GL uint32_t*)(rs.sp_rec + (uint64_t)c * CAP_T + (r & (CAP_T - 1u))))[1] = v;
     }
 }
 __device__ __forceinline__ void rec_store(const RecSink& rs, uint32_t idx, const Hdr& h, uint32_t rel) {
-    const bool sh = h.exp == 0 && h.key0 < 0x80u && h.ks >= 1u && h.ks < (1u << 24) && h.type < 8u && h.dt < 8u &&
-                    h.hsz >= 6 && h.hsz < 38;
+    const bool sh = h.exp == 0 && h.key0 < 0x80u && h.ks >= 1u && h.ks < SH_KS_LIM && h.vs < SH_VS_LIM &&
+                    h.type < 8u && h.dt < 8u && h.hsz >= 6 && h.hsz < 38;
     u32x4 v = (u32x4){0u, 0u, 0u, rel};
-    if (sh) v = (u32x4){h.crc, h.ks | ((uint32_t)(h.hsz - 6) << 24) | (h.type << 29), h.vs,
-                        rel | (h.dt << 16) | (h.key0 << 19) | REC_SHORT};
+    if (sh) v = (u32x4){h.crc, 0u, h.vs | ((uint32_t)(h.hsz - 6) << 21) | (h.type << 26) | (h.dt << 29),
+                        rel | (h.key0 << 16) | REC_SHORT | (h.ks << 24)};
     rec_put(rs, idx, v);
 }
 
@@ -732,7 +760,6 @@ __device__ __forceinline__ void patch_word(uint32_t (&w)[16], uint32_t k, uint32
 // segment of the tile, stream order) and the records' snapshots (indexed like
 // the compact entries; boundary CAP_T is the last one kept)
 #define NSEG (CLY_NBLK * CLY_NL)         // segments per tile
-#define SNAP_T (CAP_T + 4)               // snapshot words per tile (CAP_T + 1 used)
 struct TileRes { uint32_t X; bool dead; };
 // The chain state a wave carries through its tile (wave-uniform).
 struct TState {
@@ -754,7 +781,7 @@ struct TState {
     uint32_t nch_have;           // chunks the tile holds (k_refix reuses k_scan's)
     bool ref_ok;
     uint32_t ref_s;              // the reference record's size (the stride)
-    uint32_t ref1, ref2, ref3, msk1, msk2, msk3, rw1, rw2, rw3;
+    uint32_t ref1, ref2, ref3, msk1, msk2, msk3, rw2, rw3;
 };
 // The block's outputs for record k of a round (lane k): its compact entry.
 // Returns the record's patch word as an index in the block: the word whose
@@ -907,7 +934,7 @@ __device__ __forceinline__ void stride_round(const DevFile& F, TState& S, uint32
     uint32_t pw = 0;
     spill_ensure(S, S.tcnt + kb, rs, lane);
     if (k < kb) {
-        rec_put(rs, S.tcnt + k, (u32x4){crc, S.rw1, S.rw2, (P - tb) | S.rw3});
+        rec_put(rs, S.tcnt + k, (u32x4){crc, 0u, S.rw2, (P - tb) | S.rw3});
         pw = ((P - bs) >> 2) + ((P & 3u) ? 1u : 0u);
         if (pw < PW_CARRY) mark_pw(mk, pw);
     }
@@ -929,8 +956,9 @@ __device__ __forceinline__ void stride_ref(const DevFile& F, TState& S, uint32_t
     if (S.dead || !S.s_last || S.s_last != S.s_prev || S.P_last == NONE32 || S.P_last < bs) return;
     const uint32_t P = S.P_last;
     const Hdr h = hdr_get(P, F.len, stg, bs);
-    const bool sh = h.status == REC_OK && h.exp == 0 && h.key0 < 0x80u && h.ks >= 1u && h.ks < (1u << 24) &&
-                    h.type < 8u && h.dt < 8u && h.hsz >= 6 && h.hsz <= 15 && (uint32_t)h.size == S.s_last;
+    const bool sh = h.status == REC_OK && h.exp == 0 && h.key0 < 0x80u && h.ks >= 1u && h.ks < SH_KS_LIM &&
+                    h.vs < SH_VS_LIM && h.type < 8u && h.dt < 8u && h.hsz >= 6 && h.hsz <= 15 &&
+                    (uint32_t)h.size == S.s_last;
     if (!sh) return;
     const CLY_LDS uint32_t* q = stg + stg_dw((P - bs) >> 2);
     const uint32_t w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4], a = P & 3u;
@@ -944,9 +972,8 @@ __device__ __forceinline__ void stride_ref(const DevFile& F, TState& S, uint32_t
         return m;
     };
     S.msk1 = msk(4); S.msk2 = msk(8); S.msk3 = msk(12);
-    S.rw1 = h.ks | ((uint32_t)(h.hsz - 6) << 24) | (h.type << 29);
-    S.rw2 = h.vs;
-    S.rw3 = (h.dt << 16) | (h.key0 << 19) | REC_SHORT;
+    S.rw2 = h.vs | ((uint32_t)(h.hsz - 6) << 21) | (h.type << 26) | (h.dt << 29);
+    S.rw3 = (h.key0 << 16) | REC_SHORT | (h.ks << 24);
     S.ref_s = (uint32_t)h.size;
     S.ref_ok = true;
 }
@@ -1043,8 +1070,8 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                                              bool dead_in,
                                              const CLY_LDS uint8_t* smem, CLY_LDS uint32_t* stg, CLY_LDS uint32_t* mk,
                                              const CrcLane& cl, uint32_t K4, TileLocal* loc,
-                                             uint32_t* rec, uint32_t* seg, uint32_t* snap, uint32_t* treg,
-                                             CLY_LDS uint32_t* chk, uint32_t* chunks, u32x4* sp_rec, uint32_t* sp_snap,
+                                             uint32_t* rec, uint32_t* seg, uint32_t* treg,
+                                             CLY_LDS uint32_t* chk, uint32_t* chunks, u32x4* sp_rec,
                                              Globals* g, u32x4 (&e)[4], u32x4& hl, const uint8_t* nbase, uint32_t nlen,
                                              uint32_t ntb) {
     const int lane = threadIdx.x & 63;
@@ -1059,7 +1086,7 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     S.cq_known = first;          // the file's first tile: no record before offset 0
     S.cq = 0; S.G = NONE32; S.tcnt = 0; S.last_crc = 0; S.P_last = NONE32; S.term = TERM_NONE;
     S.s_last = 0; S.s_prev = 0; S.Tb = NONE32; S.tpatch = 0; S.carry_next = 0; S.cmark_next = false;
-    S.ref_ok = false; S.ref_s = 0; S.ref1 = S.ref2 = S.ref3 = S.msk1 = S.msk2 = S.msk3 = S.rw1 = S.rw2 = S.rw3 = 0;
+    S.ref_ok = false; S.ref_s = 0; S.ref1 = S.ref2 = S.ref3 = S.msk1 = S.msk2 = S.msk3 = S.rw2 = S.rw3 = 0;
     uint32_t* ctab = chunks + (uint64_t)t * CH_WORDS;
     S.nch = 0;
     // k_scan starts the tile's chunk list; k_refix reuses the chunks k_scan took
@@ -1075,9 +1102,8 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
     const rsrc_t trs = mk_rsrc(rec + (uint64_t)t * CAP_T * 4, CAP_T * 16u);      // the tile's compact entries
     const rsrc_t frs = mk_rsrc(F.base, (uint32_t)flen);
     const rsrc_t srs = mk_rsrc(seg + (uint64_t)t * NSEG, NSEG * 4u);           // segment registers
-    const rsrc_t nrs = mk_rsrc(snap + (uint64_t)t * SNAP_T, CAP_T * 4u);       // snapshots
     RecSink rs;
-    rs.trs = trs; rs.nrs = nrs; rs.sp_rec = (CLY_GL u32x4*)sp_rec; rs.sp_snap = (CLY_GL uint32_t*)sp_snap;
+    rs.trs = trs; rs.sp_rec = (CLY_GL u32x4*)sp_rec;
     rs.chk = chk; rs.ctab = ctab; rs.g = g;
     uint32_t Rp = 0;             // the previous block's segment register (stored at the next block's top)
     CLY_LDS u32x4* sv = (CLY_LDS u32x4*)stg;
@@ -1203,21 +1229,36 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                     uint32_t lv = L.last_crc, lf = c > 0 ? 1u : 0u;
                     wave_last_incl(lv, lf);
                     const uint32_t lvp = dppu<DPP_WF_SR1>(0u, lv), lfp = dppu<DPP_WF_SR1>(0u, lf);
-                    uint32_t pcq = lfp ? lvp : S.cq;
-                    bool pk = lfp ? true : S.cq_known;
-                    // the lane's records: outputs and patch-word marks (headers from the stage)
-                    uint32_t p = L.E, psz = 0, ppsz = 0;
+                    // (the stored CRC before the terminal: the lane's last record's, or inherited)
+                    const uint32_t pcq = c > 0 ? L.last_crc : (lfp ? lvp : S.cq);
+                    const bool pk = c > 0 || lfp || S.cq_known;
+                    // the block's records, record-parallel: record r (in chain order) by
+                    // lane r % 64 of round r / 64: its segment is the first lane whose
+                    // inclusive count exceeds r, its start that lane's (r - lex)-th
+                    // start bit; outputs, patch-word marks (headers from the stage),
+                    // entries stored as consecutive 16-B slots
                     bool cf = false;
+                    uint32_t sz_last = 0, sz_prev = 0;
                     spill_ensure(S, S.tcnt + bcnt, rs, lane);
-                    for (uint32_t i = 0; __ballot(i < c); i++) {
-                        if (i < c) {
+                    for (uint32_t r0 = 0; r0 < bcnt; r0 += 64) {
+                        const uint32_t r = r0 + (uint32_t)lane;
+                        uint32_t own = 0;
+                        #pragma unroll
+                        for (int w = 32; w >= 1; w >>= 1)
+                            if (shfl_u32(incl, (int)own + w - 1) <= r) own += (uint32_t)w;
+                        own = own > 63u ? 63u : own;
+                        const uint32_t k = r - shfl_u32(lex, (int)own);
+                        const uint32_t m0 = shfl_u32(L.sm0, (int)own), m1 = shfl_u32(L.sm1, (int)own);
+                        uint32_t sz = 0;
+                        if (r < bcnt) {
+                            const uint32_t p = bs + 64u * own + kth_bit(m0, m1, k);
                             const Hdr h = hdr_get(p, flen, stg, bs);
-                            const uint32_t pw = rec_out(p, h, S.tcnt + lex + i, tb, bs, rs);
+                            const uint32_t pw = rec_out(p, h, S.tcnt + r, tb, bs, rs);
                             if (pw == PW_CARRY) cf = true; else mark_pw(mk, pw);
-                            pcq = h.crc; pk = true;
-                            ppsz = psz; psz = (uint32_t)h.size;
-                            p += (uint32_t)h.size;
+                            sz = (uint32_t)h.size;
                         }
+                        if (bcnt - 1u - r0 < 64u) sz_last = rdl(sz, (int)(bcnt - 1u - r0));
+                        if (bcnt >= 2u && bcnt - 2u - r0 < 64u) sz_prev = rdl(sz, (int)(bcnt - 2u - r0));
                     }
                     if (__ballot(cf)) S.cmark_next = true;
                     if (kT < 64) {
@@ -1232,10 +1273,10 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                         S.last_crc = rdl(L.last_crc, lr);
                         S.P_last = rdl(L.last, lr);
                         S.cq = S.last_crc; S.cq_known = true;
-                        // sizes of the last two records (the one before may be in an earlier lane)
+                        // sizes of the last two records (0 for the one before when it is in an earlier lane)
                         const uint32_t cl_ = rdl(c, lr);
-                        S.s_last = rdl(psz, lr);
-                        S.s_prev = cl_ >= 2 ? rdl(ppsz, lr) : (bcnt >= 2 ? 0u : S.s_last);
+                        S.s_last = sz_last;
+                        S.s_prev = cl_ >= 2 ? sz_prev : (bcnt >= 2 ? 0u : S.s_last);
                     }
                     S.tcnt += bcnt;
                     const u64 bcc = __ballot(isC);
@@ -1360,8 +1401,7 @@ __device__ __forceinline__ CLY_LDS uint32_t* wave_chk(CLY_LDS uint8_t* smem) {
 }
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
 k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ rprefix, uint32_t nruns,
-       TileLocal* loc, uint32_t* rec, uint32_t* seg, uint32_t* snap, uint32_t* treg, uint32_t* chunks, u32x4* sp_rec,
-       uint32_t* sp_snap, Globals* g) {
+       TileLocal* loc, uint32_t* rec, uint32_t* seg, uint32_t* treg, uint32_t* chunks, u32x4* sp_rec, Globals* g) {
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS_ALL];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
     init_tables(smem);
@@ -1409,7 +1449,7 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         uint32_t ptt;
         const DevFile V = part_view(F, t - F.first_tile, ptt);
         const TileRes res = tile_body<BM_SPEC>(V, t, ptt, t == F.first_tile, Xc, false, smem, stg, mk, cl, K4, loc, rec,
-                                               seg, snap, treg, chk, chunks, sp_rec, sp_snap, g, e, hl, nbase, nlen, ntb);
+                                               seg, treg, chk, chunks, sp_rec, g, e, hl, nbase, nlen, ntb);
         if (fn < 0) break;
         // a chain that ended in this tile is not carried: past the file's true
         // end nothing reads the tiles, and a false chain's terminal must not
@@ -1622,8 +1662,8 @@ k_link(const DevFile* __restrict__ files, int nfiles, const TileLocal* __restric
 // (and is not listed itself).
 __global__ void __launch_bounds__(64 * SCAN_WAVES)
 k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, TileLocal* loc,
-        const TileIn* __restrict__ tin, uint32_t* rec, uint32_t* seg, uint32_t* snap, uint32_t* treg,
-        uint32_t* chunks, u32x4* sp_rec, uint32_t* sp_snap, const uint32_t* __restrict__ fixlist, Globals* g, int slot) {
+        const TileIn* __restrict__ tin, uint32_t* rec, uint32_t* seg, uint32_t* treg,
+        uint32_t* chunks, u32x4* sp_rec, const uint32_t* __restrict__ fixlist, Globals* g, int slot) {
     if (g->nfix[slot] == 0) return;                        // (uniform: before the LDS setup's barrier)
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[SCAN_LDS_ALL];
     CLY_LDS uint8_t* smem = (CLY_LDS uint8_t*)smem_raw;
@@ -1678,7 +1718,7 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
             u32x4 e[4], hl;
             tile_issue(V, ptt, lane, e, hl);
             const TileRes r = tile_body<BM_EXACT>(V, t, ptt, t == F.first_tile, X, dead, smem, stg, mk, cl, K4, loc,
-                                                  rec, seg, snap, treg, chk, chunks, sp_rec, sp_snap, g, e, hl,
+                                                  rec, seg, treg, chk, chunks, sp_rec, g, e, hl,
                                                   nullptr, 0u, 0u);
             X = r.X; dead = r.dead;
         }
@@ -1784,18 +1824,18 @@ __device__ __forceinline__ uint32_t patch_word_of(uint32_t P) { return (P & 3u) 
 // k_refix's suffix skip) in the tile's own area below CAP_T, else in its spill
 // chunks
 struct EntSrc {
-    const u32x4* tile; const uint32_t* tsnap;
-    const u32x4* sp_rec; const uint32_t* sp_snap; const uint32_t* ctab;
+    const u32x4* tile;
+    const u32x4* sp_rec; const uint32_t* ctab;
     uint32_t skip;
     __device__ __forceinline__ u32x4 ent(uint32_t i) const {
         const uint32_t a = i + skip;
         if (a < CAP_T) return tile[a];
         return sp_rec[(uint64_t)ctab[(a >> CAP_SHIFT) - 1u] * CAP_T + (a & (CAP_T - 1u))];
     }
-    __device__ __forceinline__ uint32_t snap(uint32_t i) const {
+    __device__ __forceinline__ uint32_t snap(uint32_t i) const {        // (word 1 of the entry)
         const uint32_t a = i + skip;
-        if (a < CAP_T) return tsnap[a];
-        return sp_snap[(uint64_t)ctab[(a >> CAP_SHIFT) - 1u] * CAP_T + (a & (CAP_T - 1u))];
+        if (a < CAP_T) return ((const uint32_t*)(tile + a))[1];
+        return ((const uint32_t*)(sp_rec + (uint64_t)ctab[(a >> CAP_SHIFT) - 1u] * CAP_T + (a & (CAP_T - 1u))))[1];
     }
 };
 // the fields of record i's check (per-record path): its start's patch word
@@ -1817,9 +1857,9 @@ __device__ __forceinline__ uint32_t chk_eval(const CLY_LDS uint32_t* emt, const 
 __global__ void __launch_bounds__(64 * EMIT_WAVES)
 k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict__ tprefix, uint32_t ntiles,
        const TileIn* __restrict__ tin, const TileLocal* __restrict__ loc, const uint32_t* __restrict__ rec,
-       const uint32_t* __restrict__ seg, const uint32_t* __restrict__ snap, uint32_t* treg, FileInfo* finfo,
+       const uint32_t* __restrict__ seg, uint32_t* treg, FileInfo* finfo,
        const uint32_t* __restrict__ tabs, cly_tuple* out_, uint64_t out_cap, const uint32_t* __restrict__ chunks,
-       const u32x4* __restrict__ sp_rec, const uint32_t* __restrict__ sp_snap, Globals* g, int slot) {
+       const u32x4* __restrict__ sp_rec, Globals* g, int slot) {
     if (g->nfix[slot] || g->spill_over || g->fail) return;   // the chain is not final yet (k_refix first) / run again / failed
     gtuples out = (gtuples)out_;
     __shared__ __attribute__((aligned(16))) unsigned char smem_raw[EMIT_LDS];
@@ -1859,8 +1899,8 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         const bool grec = !none && !gterm;                                  // ... a record start
         const uint32_t T = (uint32_t)(l1 >> 32);                            // the terminal (term)
         EntSrc E;
-        E.tile = (const u32x4*)(rec + (uint64_t)t * CAP_T * 4); E.tsnap = snap + (uint64_t)t * SNAP_T;
-        E.sp_rec = sp_rec; E.sp_snap = sp_snap; E.ctab = chunks + (uint64_t)t * CH_WORDS; E.skip = skip;
+        E.tile = (const u32x4*)(rec + (uint64_t)t * CAP_T * 4);
+        E.sp_rec = sp_rec; E.ctab = chunks + (uint64_t)t * CH_WORDS; E.skip = skip;
         const uint32_t cout = treg[2 * t];                                  // the register XOR due at the tile's end
         // the tile's segment registers into LDS (lane-transposed: lane L's run)
         uint32_t sr[RUN];
@@ -1923,9 +1963,9 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             auto ld = [&](uint32_t j0, u32x4& v, uint32_t& sv, u32x4& vx, uint32_t& sx) {
                 const uint32_t j = j0 + (uint32_t)lane;
                 v = j < n ? E.ent(j) : z4;
-                sv = j < n ? E.snap(j) : 0u;
+                sv = v.y;
                 vx = z4; sx = 0u;
-                if (lane == 63 && j + 1 < n) { vx = E.ent(j + 1); sx = E.snap(j + 1); }
+                if (lane == 63 && j + 1 < n) { vx = E.ent(j + 1); sx = vx.y; }
             };
             u32x4 vc, vx;
             uint32_t sc, sx;
@@ -1946,12 +1986,13 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                     p = tb + rel;
                     u32x4 a, b, c;
                     if (v.w & REC_SHORT) {
-                        const uint32_t ks = v.y & 0xFFFFFFu, hsz = 6u + ((v.y >> 24) & 31u), type = v.y >> 29;
-                        const uint32_t dt = (v.w >> 16) & 7u, key0 = (v.w >> 19) & 0x7Fu;
+                        const uint32_t vs = v.z & (SH_VS_LIM - 1u), hsz = 6u + ((v.z >> 21) & 31u);
+                        const uint32_t type = (v.z >> 26) & 7u, dt = v.z >> 29;
+                        const uint32_t ks = v.w >> 24, key0 = (v.w >> 16) & 0x7Fu;
                         const uint64_t tx = (uint64_t)((int64_t)(key0 >> 1) ^ -(int64_t)(key0 & 1u));
                         a = (u32x4){(uint32_t)(x0 + p), (uint32_t)((x0 + p) >> 32), 0u, 0u};
-                        b = (u32x4){(uint32_t)tx, (uint32_t)(tx >> 32), F.fid, hsz + ks + v.z};
-                        c = (u32x4){ks, v.z, type | (dt << 8) | (hsz << 16) | (1u << 24), v.x};
+                        b = (u32x4){(uint32_t)tx, (uint32_t)(tx >> 32), F.fid, hsz + ks + vs};
+                        c = (u32x4){ks, vs, type | (dt << 8) | (hsz << 16) | (1u << 24), v.x};
                     } else {
                         const Hdr h = hdr_load(base, p, F.len);
                         tuple_words(base, p, x0, h, F.fid, a, b, c);
@@ -2205,12 +2246,12 @@ struct cly_ctx {
     DevFile* h_files; uint32_t* h_tprefix; FileInfo* h_finfo;
     uint32_t* d_rprefix; uint32_t* h_rprefix;        // per file its first run of tiles (k_scan)
     TileLocal* d_loc; TileIn* d_tin; uint32_t* d_treg; uint32_t* d_fix; uint32_t* d_rec;
-    uint32_t* d_seg; uint32_t* d_snap;   // segment registers, snapshots
+    uint32_t* d_seg;             // segment registers
     uint32_t* d_chunks;          // per tile CH_WORDS words: spill chunk ids and their count
     uint32_t* d_lmask;           // k_link's bitmasks of files past LINK_MAXT tiles (2 x lmask_words)
     uint64_t lmask_words;
     int64_t cap_tiles;
-    u32x4* d_sp_rec; uint32_t* d_sp_snap; uint32_t cap_spill;   // the spill pool (chunks of CAP_T entries)
+    u32x4* d_sp_rec; uint32_t cap_spill;   // the spill pool (chunks of CAP_T entries)
     Globals* d_g; Globals* h_g;
     uint32_t* d_tabs;            // nibble tables (TAB_SH, TAB_TILE, TAB_EM)
     uint32_t* d_pw;              // x^(8 CLY_TILE 2^k) mod P, k < 40
@@ -2284,7 +2325,7 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     hipStreamSynchronize(c->stream);
     hipFree(c->d_call); hipFree(c->d_ftotal);
     hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_rec);
-    hipFree(c->d_seg); hipFree(c->d_snap); hipFree(c->d_chunks); hipFree(c->d_lmask); hipFree(c->d_sp_rec); hipFree(c->d_sp_snap);
+    hipFree(c->d_seg); hipFree(c->d_chunks); hipFree(c->d_lmask); hipFree(c->d_sp_rec);
     hipFree(c->d_tabs); hipFree(c->d_pw); hipFree(c->d_bytes); hipFree(c->d_tuples); hipFree(c->d_dbg);
     hipHostFree(c->h_call);
     cly_merge_scratch_free(c->merge_scratch);
@@ -2329,17 +2370,16 @@ static int ensure_files(cly_ctx* c, int nfiles) {
 static int ensure_tiles(cly_ctx* c, int64_t ntiles) {
     if (ntiles <= c->cap_tiles) return CLY_OK;
     hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_rec);
-    hipFree(c->d_seg); hipFree(c->d_snap); hipFree(c->d_chunks); hipFree(c->d_lmask);
+    hipFree(c->d_seg); hipFree(c->d_chunks); hipFree(c->d_lmask);
     c->d_lmask = nullptr; c->lmask_words = 0;
     c->d_loc = nullptr; c->d_tin = nullptr; c->d_treg = nullptr; c->d_fix = nullptr; c->d_rec = nullptr;
-    c->d_seg = nullptr; c->d_snap = nullptr; c->d_chunks = nullptr;
+    c->d_seg = nullptr; c->d_chunks = nullptr;
     c->cap_tiles = 0;
     const int64_t cap = ntiles < 1024 ? 1024 : ntiles;
     HIPCK(hipMalloc(&c->d_loc, sizeof(TileLocal) * cap));
     HIPCK(hipMalloc(&c->d_tin, sizeof(TileIn) * cap));
     HIPCK(hipMalloc(&c->d_treg, sizeof(uint32_t) * 2 * cap));
     HIPCK(hipMalloc(&c->d_seg, sizeof(uint32_t) * NSEG * (uint64_t)cap));
-    HIPCK(hipMalloc(&c->d_snap, sizeof(uint32_t) * SNAP_T * (uint64_t)cap));
     HIPCK(hipMalloc(&c->d_chunks, sizeof(uint32_t) * CH_WORDS * (uint64_t)cap));
     HIPCK(hipMalloc(&c->d_fix, sizeof(uint32_t) * cap));
     HIPCK(hipMalloc(&c->d_rec, sizeof(uint32_t) * 4 * (uint64_t)CAP_T * cap));
@@ -2363,10 +2403,9 @@ static int ensure_lmask(cly_ctx* c, int64_t ntiles, int nfiles) {
 static int ensure_spill(cly_ctx* c, uint64_t chunks) {
     if (chunks <= c->cap_spill) return CLY_OK;
     if (chunks > 0xFFFFFFF0ull) return CLY_ERR_ARG;
-    hipFree(c->d_sp_rec); hipFree(c->d_sp_snap);
-    c->d_sp_rec = nullptr; c->d_sp_snap = nullptr; c->cap_spill = 0;
+    hipFree(c->d_sp_rec);
+    c->d_sp_rec = nullptr; c->cap_spill = 0;
     HIPCK(hipMalloc(&c->d_sp_rec, sizeof(u32x4) * CAP_T * chunks));
-    HIPCK(hipMalloc(&c->d_sp_snap, sizeof(uint32_t) * CAP_T * chunks));
     c->cap_spill = (uint32_t)chunks;
     return CLY_OK;
 }
@@ -2441,8 +2480,7 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
     if ((int64_t)grid * SCAN_WAVES > nruns) grid = (int)((nruns + SCAN_WAVES - 1) / SCAN_WAVES);
     HIPCK(hipEventRecord(c->ev[0], st));
     hipLaunchKernelGGL(k_scan, dim3(grid), dim3(64 * SCAN_WAVES), 0, st, c->d_files, nfiles, c->d_rprefix, (uint32_t)nruns,
-                       c->d_loc, c->d_rec, c->d_seg, c->d_snap, c->d_treg, c->d_chunks, c->d_sp_rec, c->d_sp_snap,
-                       c->d_g);
+                       c->d_loc, c->d_rec, c->d_seg, c->d_treg, c->d_chunks, c->d_sp_rec, c->d_g);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(c->ev[1], st));
     if (c->dbg & 1) {
@@ -2461,8 +2499,8 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
     // one repair round on the device, without a host wait: k_refix and
     // k_link return at once when the first link listed no tile
     hipLaunchKernelGGL(k_refix, dim3(REFIX_GRID), dim3(64 * SCAN_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix,
-                       c->d_loc, c->d_tin, c->d_rec, c->d_seg, c->d_snap, c->d_treg, c->d_chunks, c->d_sp_rec,
-                       c->d_sp_snap, c->d_fix, c->d_g, 0);
+                       c->d_loc, c->d_tin, c->d_rec, c->d_seg, c->d_treg, c->d_chunks, c->d_sp_rec,
+                       c->d_fix, c->d_g, 0);
     hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_loc, c->d_tin, c->d_ftotal,
                        c->d_finfo, c->d_fix, c->d_lmask, c->lmask_words, c->d_g, 1, 0);
     HIPCK(hipGetLastError());
@@ -2472,8 +2510,8 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
         int eg = c->emit_grid;
         if ((int64_t)eg * EMIT_WAVES > ntiles) eg = (int)((ntiles + EMIT_WAVES - 1) / EMIT_WAVES);
         hipLaunchKernelGGL(k_emit, dim3(eg), dim3(64 * EMIT_WAVES), 0, st, c->d_files, nfiles, c->d_tprefix, nt32,
-                           c->d_tin, c->d_loc, c->d_rec, c->d_seg, c->d_snap, c->d_treg, c->d_finfo, c->d_tabs, d_out,
-                           out_cap, c->d_chunks, c->d_sp_rec, c->d_sp_snap, c->d_g, slot);
+                           c->d_tin, c->d_loc, c->d_rec, c->d_seg, c->d_treg, c->d_finfo, c->d_tabs, d_out,
+                           out_cap, c->d_chunks, c->d_sp_rec, c->d_g, slot);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[3], st));
         hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_finfo, c->d_treg, c->d_loc,
@@ -2516,8 +2554,8 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
             const int ns = slot ^ 1;
             HIPCK(hipMemsetAsync(&c->d_g->nfix[ns], 0, sizeof(uint32_t), st));
             hipLaunchKernelGGL(k_refix, dim3((nfix + SCAN_WAVES - 1) / SCAN_WAVES), dim3(64 * SCAN_WAVES), 0, st,
-                               c->d_files, nfiles, c->d_tprefix, c->d_loc, c->d_tin, c->d_rec, c->d_seg, c->d_snap,
-                               c->d_treg, c->d_chunks, c->d_sp_rec, c->d_sp_snap, c->d_fix, c->d_g, slot);
+                               c->d_files, nfiles, c->d_tprefix, c->d_loc, c->d_tin, c->d_rec, c->d_seg,
+                               c->d_treg, c->d_chunks, c->d_sp_rec, c->d_fix, c->d_g, slot);
             hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_loc, c->d_tin,
                                c->d_ftotal, c->d_finfo, c->d_fix, c->d_lmask, c->lmask_words, c->d_g, ns, -1);
             HIPCK(hipGetLastError());

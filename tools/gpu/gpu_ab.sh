@@ -2,7 +2,7 @@
 # same-box A/B: C2, C3 and small-record kernel lines of each build, two passes (A B A B)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-D=gpurun_out/ab
+D=gpurun_out/${ABDIR:-ab}
 mkdir -p $D
 for pass in 1 2; do
   for lib in "$@"; do

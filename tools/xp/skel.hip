@@ -5,6 +5,7 @@
 #include <stdio.h>
 #include <stdint.h>
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 #define LDSP __attribute__((address_space(3)))
 #define NBLK 16
 #define WAVES 16
@@ -23,6 +24,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define F_SEG4 2048     // segment registers stored as one b128 per lane every 4 blocks
 #define F_R8 4096       // 8 CRC table replicas (32 KB) instead of 16
 #define F_SNK 8192      // compact entries through a 1-KiB LDS sink per wave, flushed as whole 1-KiB stores
+#define F_E8 16384      // compact entries of 8 B
+#define F_SEGH 32768    // segment registers at 128-B granularity (even lanes store)
+#define F_SEGQ 65536    // ... at 256-B granularity (lanes % 4 == 0 store)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mk(const void* p, uint32_t n) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)n, 0x00020000);
 }
@@ -97,7 +101,9 @@ __global__ void __launch_bounds__(64 * WAVES) kskel(const uint8_t* buf, uint32_t
 #pragma unroll
       for (int k = 0; k < 4; k++) { w[4*k] = e[k].x; w[4*k+1] = e[k].y; w[4*k+2] = e[k].z; w[4*k+3] = e[k].w; }
       const u32x4 hc = hl;
-      if ((F & F_SEG) && !(F & (F_SEGT | F_SEGAFT | F_SEG4)) && m > 0) __builtin_amdgcn_raw_buffer_store_b32(Rp, srs, (int)(((m - 1) * 64 + lane) * 4), 0, (F & F_NT) ? 2 : 0);
+      const bool segl_on = (F & F_SEGQ) ? (lane & 3) == 0 : (F & F_SEGH) ? (lane & 1) == 0 : true;
+      const int segdiv = (F & F_SEGQ) ? 4 : (F & F_SEGH) ? 2 : 1;
+      if ((F & F_SEG) && !(F & (F_SEGT | F_SEGAFT | F_SEG4)) && m > 0 && segl_on) __builtin_amdgcn_raw_buffer_store_b32(Rp, srs, (int)(((m - 1) * (64 / segdiv) + lane / segdiv) * 4), 0, (F & F_NT) ? 2 : 0);
       if ((F & F_SEGT) && m > 0) segl[(m - 1) * 64 + lane] = Rp;
       if (m + 1 < NBLK) {
 #pragma unroll
@@ -130,8 +136,11 @@ __global__ void __launch_bounds__(64 * WAVES) kskel(const uint8_t* buf, uint32_t
         const uint32_t kb = bm ? (uint32_t)__ffsll((long long)bm) - 1 : 64u;
         if (k < kb && (F & F_NOST)) acc ^= crc + P;
         if ((F & F_SNK) && k < kb) snk[(sk + k) & 127] = (u32x4){crc, 0x11, 0x100, P | 0x4000000};
-        if (k < kb && !(F & (F_NOST | F_SNK))) {
+        if (k < kb && !(F & (F_NOST | F_SNK)) && !(F & F_E8)) {
           __builtin_amdgcn_raw_buffer_store_b128((u32x4){crc, 0x11, 0x100, (P - 0) | 0x4000000}, trs, (int)(((tcnt + k) & 511) * 16u), 0, (F & F_NT) ? 2 : 0);
+        }
+        if (k < kb && !(F & (F_NOST | F_SNK)) && (F & F_E8)) {
+          __builtin_amdgcn_raw_buffer_store_b64((u32x2){crc, (P - 0) | 0x4000000}, trs, (int)(((tcnt + k) & 511) * 8u), 0, 0);
         }
         if (k < kb) {
           if (F & F_SNAP) {
@@ -233,6 +242,6 @@ int main() {
   hipMalloc(&seg, (size_t)ntiles * 1024 * 4);
   hipMalloc(&snap, (size_t)ntiles * 516 * 4);
 #define R(F) run<F>(buf, ntiles, rec, seg, snap, out)
-  R(7 + 64); R(15 + 64); R(7 + 64 + 8 + 1024); R(7 + 64 + 8 + 2048); R(7 + 64 + 8 + 512); R(35); R(35 + 128); R(35 + 512); R(127); R(127 - 8 + 2048); R(127 + 128); R(127 - 8 + 128);
+  R(7 + 64); R(15 + 64); R(15 + 64 + 32768); R(15 + 64 + 65536); R(35); R(35 + 16384); R(35 + 128); R(127); R(127 - 16); R(127 + 16384); R(127 + 32768); R(127 + 65536); R(127 + 16384 + 32768); R(127 - 16 + 16384 + 32768); R(127 - 16 + 16384 + 65536); R(127 - 8 - 16 + 128);
   return 0;
 }

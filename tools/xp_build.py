@@ -17,8 +17,8 @@ PATCHES = {
     "noseg": [("        if (m > 0)\n            __builtin_amdgcn_raw_buffer_store_b32(Rp, srs,",
                "        if (m > 0 && g->walk_max == 12345678u)\n            __builtin_amdgcn_raw_buffer_store_b32(Rp, srs,")],
     # no snapshot stores
-    "nosnap": [("    if (r < CAP_T) __builtin_amdgcn_raw_buffer_store_b32(v, rs.nrs, (int)(r * 4u), 0, 0);",
-                "    if (r < CAP_T) { if (rs.g->walk_max == 12345678u) __builtin_amdgcn_raw_buffer_store_b32(v, rs.nrs, (int)(r * 4u), 0, 0); }")],
+    "nosnap": [("    if (r < CAP_T) __builtin_amdgcn_raw_buffer_store_b32(v, rs.trs, (int)(r * 16u + 4u), 0, 0);",
+                "    if (r < CAP_T) { if (rs.g->walk_max == 12345678u) __builtin_amdgcn_raw_buffer_store_b32(v, rs.trs, (int)(r * 16u + 4u), 0, 0); }")],
 }
 PATCHES["nostore"] = PATCHES["nocomp"] + PATCHES["noseg"] + PATCHES["nosnap"]
 # every kernel after k_scan returns at once: k_scan alone is timed, and no
