@@ -187,7 +187,7 @@ struct Globals {                 // zeroed per call
     uint64_t total;              // records over all files
     uint64_t walk_dbg;           // (length << 32 | first tile) of the longest k_refix walk
     uint32_t run_tiles;          // k_scan's run length this call (1, 2 or RUN_TILES; set by the host)
-    uint32_t _pad;
+    uint32_t run_next;           // k_scan's run counter (runs past the grid's first one each)
 };
 
 // ---------------------------------------------------------------------------
@@ -317,6 +317,35 @@ __device__ __forceinline__ bool hdr_fast(const Gath& g, uint32_t p, uint64_t len
     const uint32_t s = p & 3;
     const uint32_t h0 = alignb(g.w[1], g.w[0], s), h1 = alignb(g.w[2], g.w[1], s), h2 = alignb(g.w[3], g.w[2], s),
                    h3 = alignb(g.w[4], g.w[3], s);
+    h.crc = h0;
+    h.type = h1 & 0xff;
+    h.dt = (h1 >> 8) & 0xff;
+    // Short forms first (the same results as the general form below): the three
+    // varints in one byte each (keys and values under 64 B, no TTL: commit
+    // markers, hint records, small records), or key size and expiration in one
+    // byte and the value size in two (values of 64 B .. 8 KiB)
+    const uint32_t b678 = (h1 >> 16) | ((h2 & 0xffu) << 16);                 // header bytes 6, 7, 8
+    if ((b678 & 0x808080u) == 0u || ((b678 & 0x808080u) == 0x8000u && !(h2 & 0x8000u))) {
+        const bool one = (b678 & 0x8000u) == 0u;
+        const uint32_t b6 = b678 & 0xffu, b7 = (b678 >> 8) & 0xffu, b8 = b678 >> 16, b9 = (h2 >> 8) & 0xffu;
+        const uint32_t uv = one ? b7 : (b7 & 0x7fu) | (b8 << 7), ue = one ? b8 : b9;
+        const int32_t v1 = (int32_t)(b6 >> 1) ^ -(int32_t)(b6 & 1);
+        const int32_t v2 = (int32_t)(uv >> 1) ^ -(int32_t)(uv & 1);
+        h.ks = (uint32_t)v1;
+        h.vs = (uint32_t)v2;
+        h.exp = (int32_t)(ue >> 1) ^ -(int32_t)(ue & 1);
+        h.hsz = one ? 9 : 10;
+        h.key0 = one ? b9 : (h2 >> 16) & 0xffu;
+        h.size = 0;
+        h.good = false;
+        if (h.crc == 0 && h.ks == 0 && h.vs == 0) { h.status = CLY_END_ZERO; return true; }
+        const int64_t kv = (int64_t)h.ks + (int64_t)h.vs;
+        if (kv > 0 && (int64_t)(len - (p + (uint32_t)h.hsz)) < kv) { h.status = CLY_END_TORN; return true; }
+        h.status = REC_OK;
+        h.size = h.hsz + kv;
+        h.good = h.type <= 4 && h.dt <= 4 && v1 >= 1 && v2 >= 0;
+        return true;
+    }
     const uint32_t lo = alignb(h2, h1, 2), hi = alignb(h3, h2, 2);       // bytes 6..9, 10..13
     const uint64_t W = ((uint64_t)hi << 32) | lo;
     const uint64_t T = ~W & 0x8080808080808080ull;
@@ -332,10 +361,7 @@ __device__ __forceinline__ bool hdr_fast(const Gath& g, uint32_t p, uint64_t len
     const int32_t v1 = (int32_t)(u1 >> 1) ^ -(int32_t)(u1 & 1);
     const int32_t v2 = (int32_t)(u2 >> 1) ^ -(int32_t)(u2 & 1);
     const int32_t v3 = (int32_t)(u3 >> 1) ^ -(int32_t)(u3 & 1);
-    h.crc = h0;
     h.key0 = (((7 + e3) >= 12 ? h3 : h2) >> (8 * ((7 + e3) & 3))) & 0xffu;
-    h.type = h1 & 0xff;
-    h.dt = (h1 >> 8) & 0xff;
     h.ks = (uint32_t)v1;
     h.vs = (uint32_t)v2;
     h.exp = v3;
@@ -1383,8 +1409,11 @@ __device__ __forceinline__ uint32_t k4_const(const CLY_LDS uint8_t* smem, uint32
     return K4;
 }
 
-// k_scan: one wave per run of run_tiles tiles (grid-stride), every byte of
-// every file read once.
+// k_scan: one wave per run of run_tiles tiles, every byte of every file read
+// once.  Three quarters of the runs are grid-strided, the last quarter claimed
+// one at a time from a call-wide counter (runs of dense small records cost
+// several times the others: with a fixed stride throughout, C3's slowest waves
+// ended 15-20 % after the mean; claiming every run cost C2 1-3 %).
 #define SCAN_WAVES 16
 #define MK_BYTES (CLY_NL * 4)                                 // a wave's patch-word mask
 #define CHK_BYTES (CH_WORDS * 4)                              // a wave's copy of its tile's spill chunk ids
@@ -1411,12 +1440,18 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
     const int lane = threadIdx.x & 63;
     const CrcLane cl = crc_lane(lane);
     const uint32_t K4 = k4_const(smem, cl.r4);
-    const uint32_t stride = gridDim.x * SCAN_WAVES;
-    // runs of run_tiles consecutive tiles of a file, grid-strided; a run's
-    // first tile (not its file's first) guesses its entry, the others take
-    // the exit of the tile before them
+    const uint32_t slots = gridDim.x * SCAN_WAVES;
+    // runs of run_tiles consecutive tiles of a file; a run's first tile (not
+    // its file's first) guesses its entry, the others take the exit of the
+    // tile before them.  Runs [0, nstat) are grid-strided (three quarters of
+    // them, whole rounds of the grid); the rest are claimed one at a time: a
+    // wave whose next run is a claimed one issues the claim (rq) as its
+    // current run starts and reads it when that run's last tile starts
     uint32_t r = blockIdx.x * SCAN_WAVES + wave_id();
     if (r >= nruns) return;
+    const uint32_t nstat = max(slots, (nruns - nruns / 4) / slots * slots);   // (the first round is always static)
+    uint32_t rq = 0;
+    if (r + slots >= nstat && lane == 0) rq = atomicAdd(&g->run_next, 1u);
     const uint32_t rt = __builtin_amdgcn_readfirstlane(g->run_tiles);
     int f = find_file(rprefix, nfiles, r);
     uint32_t t = files[f].first_tile + (r - rprefix[f]) * rt;
@@ -1434,7 +1469,8 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         uint32_t tn = t + 1u, rn = r;
         int fn = f;
         if (tn >= rend) {
-            rn = r + stride;
+            rn = r + slots < nstat ? r + slots : nstat + (uint32_t)__builtin_amdgcn_readfirstlane((int)rq);
+            if (rn <= r) rn = nruns;   // (runs only increase: never)
             fn = rn < nruns ? find_file(rprefix, nfiles, rn) : -1;
             if (fn >= 0) tn = files[fn].first_tile + (rn - rprefix[fn]) * rt;
         }
@@ -1457,7 +1493,10 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         // tile the true chain only passes through), so the next tile guesses
         if (rn == r && !res.dead) Xc = res.X;
         else Xc = NONE32;
-        if (rn != r) r = rn;
+        if (rn != r) {
+            r = (uint32_t)__builtin_amdgcn_readfirstlane((int)rn);
+            if (r + slots >= nstat && lane == 0) rq = atomicAdd(&g->run_next, 1u);
+        }
         t = tn; f = fn;
     }
 }

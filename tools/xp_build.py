@@ -61,10 +61,8 @@ PATCHES["sloop"] = [
 ]
 # section clocks of tile_body (s_memtime, summed over waves) and general-pass counts (stderr)
 PATCHES["prof"] = [
-    ("""    uint32_t run_tiles;          // k_scan's run length this call (1, 2 or RUN_TILES; set by the host)
-    uint32_t _pad;
-};""", """    uint32_t run_tiles;          // k_scan's run length this call (1, 2 or RUN_TILES; set by the host)
-    uint32_t _pad;
+    ("""    uint32_t run_next;           // k_scan's run counter (runs past the grid's first one each)
+};""", """    uint32_t run_next;           // k_scan's run counter (runs past the grid's first one each)
     unsigned long long xp_t[8];
 };"""),
     ("""    uint32_t Rp = 0;             // the previous block's segment register (stored at the next block's top)""",
