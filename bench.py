@@ -342,6 +342,62 @@ def index_load_leg(wl, sc):
         shutil.rmtree(d, ignore_errors=True)
 
 
+def _record_bytes(key, value):
+    """One NORMAL String LogRecord without expiration (EncodeLogRecord,
+    data/logRecord.go:55-84): crc32 IEEE over the header's type/dataType and the
+    three zig-zag varints, the key and the value."""
+    import zlib
+
+    def varint(x):
+        ux, out = x << 1, bytearray()
+        while ux >= 0x80:
+            out.append((ux & 0x7F) | 0x80)
+            ux >>= 7
+        out.append(ux)
+        return bytes(out)
+    body = bytes([0, 0]) + varint(len(key)) + varint(len(value)) + varint(0) + key + value
+    return (zlib.crc32(body) & 0xFFFFFFFF).to_bytes(4, "little") + body
+
+
+def post_merge_open_leg(wl, sc, torch, lens, hint_bytes, n_live):
+    """NewCouloyDB after a merge (db.go:442-485, merge.go:182-287): the C4
+    merge's output files `%09d.cly` (fids 0..k-1), its hint-index and a
+    merge-finished record naming the first fid the merge did not cover (the
+    old files' count: every later write would go there) in a /dev/shm
+    directory, as loadMergeFiles leaves it; then cly_db_open: the hint preload
+    (every live key's String Put from the hint file) and the scan of the data
+    files, index rebuild, host inserts.  Timed first and second open."""
+    import shutil
+    d = tempfile.mkdtemp(prefix="clymerged_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    try:
+        for k, ln in enumerate(lens):
+            base = k * DATA_FILE_SIZE
+            wl.d_merge[base:base + ln].cpu().numpy().tofile(os.path.join(d, "%09d.cly" % k))
+        wl.d_hint[:hint_bytes].cpu().numpy().tofile(os.path.join(d, "hint-index"))
+        with open(os.path.join(d, "merge-finished"), "wb") as f:
+            f.write(_record_bytes(b"\x07", str(len(wl.dev_files)).encode()))   # MergeFinishedKey, merge.go:154-168
+        walls, stats = [], []
+        for _ in range(2):
+            t0 = time.perf_counter()
+            db = sc.open_db(d)
+            walls.append((time.perf_counter() - t0) * 1e3)
+            stats.append(db.stats)
+            db.close()
+        s = stats[0]
+        nbytes = int(sum(lens)) + hint_bytes
+        return {"wall_ms": round(walls[0], 2), "second_open_wall_ms": round(walls[1], 2),
+                "h2d_ms": round(s.h2d_ms, 2), "scan_ms": round(s.scan_ms, 2), "index_ms": round(s.index_ms, 2),
+                "host_insert_ms": round(s.insert_ms, 2), "list_map_ms": round(s.list_map_ms, 2),
+                "files": int(s.n_files), "bytes": nbytes, "records": int(s.records),
+                "hint_records": int(s.hint_records), "string_keys": int(s.str_keys),
+                "gib_per_s_second_open": round(nbytes / (walls[1] / 1e3) / 2**30, 2),
+                "ok": bool(int(s.hint_records) == n_live and int(s.str_keys) == n_live),
+                "sample": "%d merged files + hint-index (%.2f GiB) + merge-finished in %s" % (
+                    len(lens), nbytes / 2**30, os.path.dirname(d))}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 def c5_leg(sc, torch, device, steps=5):
     """BASELINE config 5 on one GPU: one rank's 32-GiB fid range of the C2/C3
     mix, the same step as the --gpus N > 1 lines time (their per-GPU share), so
@@ -515,6 +571,8 @@ def main():
     ap.add_argument("--config", default=None, choices=["c1", "c2", "c3", "c4", "c5"],
                     help="default: c2 at --gpus 1 (BASELINE config 2), c5 at --gpus N > 1 (config 5: a 32-GiB "
                          "fid range per GPU, 256 GiB at 8)")
+    ap.add_argument("--no-post-merge-open", action="store_true",
+                    help="c4: skip the open of the merge's output (hint preload + merged files)")
     ap.add_argument("--no-c5-leg", action="store_true", help="skip the N=1 line's C5 reference leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true", help="skip the host-buffer (PCIe-inclusive) leg")
@@ -677,6 +735,13 @@ def main():
         mi["rescan_ok"] = bool(n2 == mi["n_live"] and all(r.status == 0 for r in r2) and n3 == mi["n_live"]
                                and r3[0].status == 0)
         out["merge"] = mi
+        if rank == 0 and world == 1 and not args.no_post_merge_open:
+            del d2
+            torch.cuda.empty_cache()
+            try:
+                out["post_merge_open"] = post_merge_open_leg(wl, sc, torch, lens, mi["hint_bytes"], mi["n_live"])
+            except Exception as e:     # reported in the line, not fatal to it
+                out["post_merge_open"] = {"error": repr(e)}
         out["parity_ok"] = bool(ok and mi["n_live"] == wl.n_live and mi["rescan_ok"]
                                 and index_info["matches_workload_live"])
         del d2
