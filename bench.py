@@ -735,8 +735,8 @@ def main():
         mi["rescan_ok"] = bool(n2 == mi["n_live"] and all(r.status == 0 for r in r2) and n3 == mi["n_live"]
                                and r3[0].status == 0)
         out["merge"] = mi
+        del d2
         if rank == 0 and world == 1 and not args.no_post_merge_open:
-            del d2
             torch.cuda.empty_cache()
             try:
                 out["post_merge_open"] = post_merge_open_leg(wl, sc, torch, lens, mi["hint_bytes"], mi["n_live"])
@@ -744,7 +744,6 @@ def main():
                 out["post_merge_open"] = {"error": repr(e)}
         out["parity_ok"] = bool(ok and mi["n_live"] == wl.n_live and mi["rescan_ok"]
                                 and index_info["matches_workload_live"])
-        del d2
     if args.verify and rank == 0:
         from oracle import cly_oracle as co
         from couloydb_amd import TUPLE_DTYPE

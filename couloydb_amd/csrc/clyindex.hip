@@ -19,10 +19,12 @@
 //   select + radix sort of the tx records by txId (stable: scan order kept)
 //   k_ixtx      per tx record: its next marker in the same txId (segmented
 //               suffix scan), a committed data record is applied at its marker
-//   select + radix sort of the applied records by a 64-bit key hash
+//   select + keys-only radix sort of the applied records' packed keys (ix_pk:
+//   hb hash bits | tombstone | record index; 8 B per record and pass)
 //   segmented arg-max of the application order per hash group: the winner of
-//   each key; adjacent records of a group with different keys (a hash
-//   collision) send the group to an exact one-thread resolution
+//   each key (k_ixwin); adjacent records of a group with different keys (a
+//   hash collision) list the group for an exact one-thread resolution (k_ixcoll)
+//   k_ixwinfix  the winners' final states from the flags k_ixclass kept
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -45,8 +47,8 @@ extern "C" hipError_t cly_ix_scratch_internal(cly_ctx* ctx, int k, size_t bytes,
 // record index of a hash-sorted entry: bit 31 carries "LogRecordDeleted" so that
 // the winner's type needs no second (random) read of its tuple
 #define IX_DEL 0x80000000u
-#define IXI(x) ((x) & 0x7fffffffu)
 #define IX_WIN 7                     // a key's winner, its final state not yet decided (k_ixwinfix)
+#define IXI(x) ((x) & 0x7fffffffu)
 enum { K_NONE = 0, K_APPLY = 1, K_TXDATA = 2, K_COMMIT = 3, K_ROLLBACK = 4 };
 
 __device__ __forceinline__ int ix_file(const uint64_t* first, int nfiles, uint64_t i) {
@@ -157,10 +159,18 @@ __device__ __forceinline__ uint64_t ix_hash_ckey(const IxKey& k, const uint8_t* 
     return h;
 }
 
-// hash, signature and tombstone bit of applied record i; returns the bit
+__device__ __forceinline__ bool ix_expired(const cly_tuple& t, int64_t now_ns) {
+    return t.data_type == 0 && t.expiration != 0 && t.expiration <= now_ns;
+}
+// flags of an applied record (its del byte): what a winner's final state needs
+// of its tuple, so that k_ixwinfix reads bytes in scan order instead of tuples
+#define IXF_DEL 1u          // LogRecordDeleted
+#define IXF_EXP 2u          // a String put expired at the context's clock (TTL sweep)
+#define IXF_CHK 4u          // Hash/List/Set without a txId: ix_win_state compares the two decodes
+// hash, signature and flags of applied record i; returns the tombstone bit
 __device__ __forceinline__ bool ix_apply_one(const cly_tuple& t, uint64_t i, const uint64_t* first,
                                              const uint64_t* bases, int nfiles, uint64_t* hash, uint8_t* del,
-                                             uint4* ksig, uint64_t hash_mask, uint32_t* bad) {
+                                             uint4* ksig, uint64_t hash_mask, uint32_t* bad, int64_t now_ns) {
     const int f = ix_file(first, nfiles, i);
     uint4 sg;
     if (ix_composite(t.data_type)) {
@@ -174,12 +184,33 @@ __device__ __forceinline__ bool ix_apply_one(const cly_tuple& t, uint64_t i, con
         hash[i] = ix_hash_sig(t.data_type, k, len, sg) & hash_mask;
     }
     const bool dl = t.type == 1;
-    del[i] = dl;
+    del[i] = (dl ? IXF_DEL : 0u) | (ix_expired(t, now_ns) ? IXF_EXP : 0u) |
+             (ix_composite(t.data_type) && t.tx_id == 0 && t.txid_len != 0 ? IXF_CHK : 0u);
     ksig[i] = sg;
     return dl;
 }
 
-struct IxTot { unsigned long long n_live, n_applied, n_loadonly, n_coll, n_tx, n_now, n_mpanic; uint32_t bad, _pad; };
+// Sort key of an applied record (one u64, sorted keys-only): hb bits of its
+// key hash above the tombstone bit and ib bits of its record index, so that
+// the radix sort moves 8 B per record and pass and sorts only the hb hash bits
+// (stable: scan order inside a hash group).  hb is narrower than the table
+// hash (ix_hash_mask): equal sort hashes of different keys are collisions,
+// which k_ixwin detects from the key signatures and k_ixcoll resolves exactly.
+__device__ __forceinline__ uint64_t ix_pk(uint64_t hash, uint32_t i, bool del, uint32_t ib, uint32_t hb) {
+    return ((hash & ((1ull << hb) - 1)) << (ib + 1)) | ((uint64_t)del << ib) | i;
+}
+__device__ __forceinline__ uint64_t ix_pk_h(uint64_t pk, uint32_t ib) { return pk >> (ib + 1); }
+// the record index with IX_DEL, as the selection values before
+__device__ __forceinline__ uint32_t ix_pk_s(uint64_t pk, uint32_t ib) {
+    return (uint32_t)(pk & ((1ull << ib) - 1)) | (((pk >> ib) & 1) ? IX_DEL : 0u);
+}
+// application order of record i: scan order for a record without a txId
+// (k_ixclass writes none), its commit marker's position for a tx data record
+__device__ __forceinline__ uint64_t ix_order(const uint8_t* cls, const uint64_t* order, uint32_t i) {
+    return cls[i] == 1 /* K_APPLY */ ? ((uint64_t)i << 32) | i : order[i];
+}
+
+struct IxTot { unsigned long long n_live, n_applied, n_loadonly, n_coll, n_tx, n_now, n_mpanic, n_chead; uint32_t bad, _pad; };
 
 // sum of a and b over the workgroup (256 threads), one atomic per counter
 __device__ __forceinline__ void ix_wg_add2(unsigned long long a, unsigned long long b, unsigned long long* da,
@@ -197,10 +228,10 @@ __device__ __forceinline__ void ix_wg_add2(unsigned long long a, unsigned long l
 
 // class of each record (every data type 0..4 is indexed; others: no-op)
 __global__ void __launch_bounds__(256)
-k_ixclass(const cly_tuple* __restrict__ tup, uint64_t n, uint8_t* cls, uint8_t* state, uint64_t* txkey,
-          uint8_t* txflag, IxTot* tot, const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases,
-          int nfiles, uint64_t* order, uint64_t* hash, uint8_t* apflag, uint8_t* del, uint4* ksig, uint32_t* selv,
-          uint64_t hash_mask) {
+k_ixclass(const cly_tuple* __restrict__ tup, uint64_t n, uint8_t* cls, uint8_t* state, uint8_t* txflag, IxTot* tot,
+          const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases, int nfiles, uint64_t* hash,
+          uint8_t* apflag, uint8_t* del, uint4* ksig, uint64_t* pk, uint64_t hash_mask, uint32_t ib, uint32_t hb,
+          int64_t now_ns) {
     unsigned long long ntx = 0, nnow = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         const cly_tuple t = tup[i];
@@ -220,17 +251,16 @@ k_ixclass(const cly_tuple* __restrict__ tup, uint64_t n, uint8_t* cls, uint8_t* 
         }
         cls[i] = c;
         state[i] = CLY_IX_DEAD;
-        txkey[i] = (uint64_t)t.tx_id;
         const bool tx = c == K_TXDATA || c == K_COMMIT || c == K_ROLLBACK;
         txflag[i] = tx;
         ntx += tx;
         nnow += c == K_APPLY;
-        // a record without a txId is applied now: order = scan order, its hash,
-        // signature and tombstone bit come from this same pass over the tuples
+        // a record without a txId is applied now: order = scan order (implicit,
+        // ix_order), its hash, signature and tombstone bit come from this same
+        // pass over the tuples
         if (c == K_APPLY) {
-            order[i] = (i << 32) | i;
-            const bool dl = ix_apply_one(t, i, first, bases, nfiles, hash, del, ksig, hash_mask, &tot->bad);
-            selv[i] = (uint32_t)i | (dl ? IX_DEL : 0u);
+            const bool dl = ix_apply_one(t, i, first, bases, nfiles, hash, del, ksig, hash_mask, &tot->bad, now_ns);
+            pk[i] = ix_pk(hash[i], (uint32_t)i, dl, ib, hb);
         }
         apflag[i] = c == K_APPLY;
     }
@@ -274,10 +304,10 @@ __global__ void __launch_bounds__(256)
 k_ixapply(const cly_tuple* __restrict__ tup, uint64_t n, const uint8_t* __restrict__ cls,
           const uint64_t* __restrict__ order, const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases,
           int nfiles, uint64_t* hash, uint8_t* apflag, uint8_t* del, uint4* ksig, uint64_t hash_mask,
-          uint32_t* bad) {
+          uint32_t* bad, int64_t now_ns) {
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         if (cls[i] != K_TXDATA || order[i] == IX_NONE) continue;   // K_APPLY: done by k_ixclass
-        ix_apply_one(tup[i], i, first, bases, nfiles, hash, del, ksig, hash_mask, bad);
+        ix_apply_one(tup[i], i, first, bases, nfiles, hash, del, ksig, hash_mask, bad, now_ns);
         apflag[i] = 1;
     }
 }
@@ -290,11 +320,12 @@ struct GMaxOp {
     }
 };
 __global__ void __launch_bounds__(256)
-k_ixgin(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, const uint64_t* __restrict__ order,
-        uint64_t m, GMax* g) {
+k_ixgin(const uint64_t* __restrict__ spk, uint32_t ib, const uint8_t* __restrict__ cls,
+        const uint64_t* __restrict__ order, uint64_t m, GMax* g) {
     for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < m; q += (uint64_t)gridDim.x * 256) {
-        const uint32_t i = IXI(sidx[q]);
-        g[q] = GMax{sh[q], order[i], i, (uint32_t)q};
+        const uint64_t v = spk[q];
+        const uint32_t i = IXI(ix_pk_s(v, ib));
+        g[q] = GMax{ix_pk_h(v, ib), ix_order(cls, order, i), i, (uint32_t)q};
     }
 }
 __device__ __forceinline__ bool ix_same_key(const cly_tuple* tup, const uint64_t* first, const uint64_t* bases,
@@ -315,9 +346,6 @@ __device__ __forceinline__ bool ix_same_key(const cly_tuple* tup, const uint64_t
     for (uint32_t q = 0; q < la; q++) if (ka[q] != kb[q]) return false;
     return true;
 }
-__device__ __forceinline__ bool ix_expired(const cly_tuple& t, int64_t now_ns) {
-    return t.data_type == 0 && t.expiration != 0 && t.expiration <= now_ns;
-}
 // state of a key's winner w: LIVE, or LOADONLY when merge.go's lookup (the
 // realKey decoded, merge.go:101-126) names another key than loadIndex's (the
 // stored key decoded, for a Hash/List/Set record without a txId)
@@ -335,64 +363,122 @@ __device__ __forceinline__ uint8_t ix_win_state(const cly_tuple* tup, const uint
 // group ends: the winner (max order) decides the key; adjacent different keys
 // inside a group mark a hash collision (resolved exactly by k_ixcoll)
 __global__ void __launch_bounds__(256)
-k_ixwin(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, const GMax* __restrict__ g, uint64_t m,
+k_ixwin(const uint64_t* __restrict__ spk, uint32_t ib, const GMax* __restrict__ g, uint64_t m,
         const cly_tuple* __restrict__ tup, const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases,
-        int nfiles, const uint4* __restrict__ ksig, uint8_t* state, uint8_t* coll, IxTot* tot, int64_t now_ns) {
-    for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < m; q += (uint64_t)gridDim.x * 256) {
-        bool differ = false;
-        if (q > 0 && sh[q] == sh[q - 1]) {
-            const uint32_t a = IXI(sidx[q]), b = IXI(sidx[q - 1]);
-            const uint4 sa = ksig[a], sb = ksig[b];
-            differ = sa.x != sb.x || sa.y != sb.y || sa.z != sb.z || sa.w != sb.w;
-            if (!differ && ix_sig_long(sa)) differ = !ix_same_key(tup, first, bases, nfiles, a, b);
+        int nfiles, const uint4* __restrict__ ksig, uint8_t* state, uint8_t* coll, uint32_t* heads, IxTot* tot) {
+    unsigned long long ncoll = 0;
+    const int lane = threadIdx.x & 63;
+    // whole waves over consecutive entries: an entry loads its signature once
+    // (when a neighbour shares its hash) and the next lane takes it by shuffle
+    for (uint64_t qw = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); qw < m; qw += (uint64_t)gridDim.x * 256) {
+        const uint64_t q = qw + lane;
+        const bool in = q < m;
+        uint64_t vq = 0, hq = 0;
+        bool eqL = false, eqR = false;
+        if (in) {
+            vq = spk[q];
+            hq = ix_pk_h(vq, ib);
+            eqL = q > 0 && ix_pk_h(spk[q - 1], ib) == hq;
+            eqR = q + 1 < m && ix_pk_h(spk[q + 1], ib) == hq;
         }
-        if (differ) {
-            uint64_t h0 = q;
-            while (h0 > 0 && sh[h0 - 1] == sh[q]) h0--;
-            coll[h0] = 1;
-            atomicAdd(&tot->n_coll, 1ull);
+        uint4 sa = make_uint4(0, 0, 0, 0);
+        if (eqL || eqR) sa = ksig[IXI(ix_pk_s(vq, ib))];
+        uint4 sb;
+        sb.x = __shfl_up(sa.x, 1, 64);
+        sb.y = __shfl_up(sa.y, 1, 64);
+        sb.z = __shfl_up(sa.z, 1, 64);
+        sb.w = __shfl_up(sa.w, 1, 64);
+        // a collided group's head is listed once (the first differing entry to
+        // set its coll byte) for k_ixcoll
+        bool push = false;
+        uint64_t h0 = 0;
+        if (in) {
+            if (lane == 0 && eqL) sb = ksig[IXI(ix_pk_s(spk[q - 1], ib))];
+            bool differ = false;
+            if (eqL) {
+                differ = sa.x != sb.x || sa.y != sb.y || sa.z != sb.z || sa.w != sb.w;
+                if (!differ && ix_sig_long(sa))
+                    differ = !ix_same_key(tup, first, bases, nfiles, IXI(ix_pk_s(vq, ib)), IXI(ix_pk_s(spk[q - 1], ib)));
+            }
+            if (differ) {
+                h0 = q;
+                while (h0 > 0 && ix_pk_h(spk[h0 - 1], ib) == hq) h0--;
+                const uint32_t bit = 1u << (8 * (h0 & 3));
+                push = !(atomicOr((uint32_t*)(coll + (h0 & ~3ull)), bit) & bit);
+                ncoll++;
+            }
+            // the group's last entry decides (g == nullptr: no tx record was
+            // applied, so the application order is the scan order, which the
+            // stable sort keeps inside a group: the last wins)
+            if (!eqR) {
+                const uint32_t sq = ix_pk_s(vq, ib);
+                const uint32_t w = g ? g[q].idx : IXI(sq);
+                const bool deleted = g ? tup[w].type == 1 : (sq & IX_DEL) != 0;
+                // LogRecordDeleted -> key absent; a String key whose winning put expired is
+                // db.Del'd by loadIndex's TTL sweep (db.go:639-651: not exp.After(now))
+                // (the winner's final state from its flags: k_ixwinfix, in scan order;
+                // random byte stores: a bitmap of atomicOr measured 2x slower)
+                if (!deleted) state[w] = IX_WIN;
+            }
         }
-        if (q + 1 < m && sh[q + 1] == sh[q]) continue;         // not the group's last
-        // g == nullptr: no tx record was applied, so the application order is the
-        // scan order, which the stable sort keeps inside a group: the last wins
-        const uint32_t w = g ? g[q].idx : IXI(sidx[q]);
-        const bool deleted = g ? tup[w].type == 1 : (sidx[q] & IX_DEL) != 0;
-        // LogRecordDeleted -> key absent; a String key whose winning put expired is
-        // db.Del'd by loadIndex's TTL sweep (db.go:639-651: not exp.After(now))
-        // (the winner's final state from its tuple: k_ixwinfix, in scan order)
-        if (!deleted) state[w] = IX_WIN;
+        const uint64_t bm = __ballot(push);
+        if (bm) {
+            const int l0 = __builtin_ctzll(bm);
+            uint32_t base = 0;
+            if (lane == l0) base = (uint32_t)atomicAdd(&tot->n_chead, (unsigned long long)__popcll(bm));
+            base = __shfl(base, l0, 64);
+            if (push) heads[base + __popcll(bm & ((1ull << lane) - 1))] = (uint32_t)h0;
+        }
     }
+    // one atomic per wave (a collision per record of a narrow hash is common)
+    for (int d = 32; d >= 1; d >>= 1) ncoll += __shfl_xor(ncoll, d, 64);
+    if ((threadIdx.x & 63) == 0 && ncoll) atomicAdd(&tot->n_coll, ncoll);
 }
 // the winners' states (LIVE, LOADONLY or EXPIRED) in scan order: the tuples
 // read as consecutive runs instead of one line per sorted winner
 __global__ void __launch_bounds__(256)
 k_ixwinfix(const cly_tuple* __restrict__ tup, uint64_t n, const uint64_t* __restrict__ first,
-           const uint64_t* __restrict__ bases, int nfiles, uint8_t* state, int64_t now_ns) {
+           const uint64_t* __restrict__ bases, int nfiles, const uint8_t* __restrict__ flg, uint8_t* state) {
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         if (state[i] != IX_WIN) continue;
-        state[i] = ix_expired(tup[i], now_ns) ? (uint8_t)CLY_IX_EXPIRED
-                                              : ix_win_state(tup, first, bases, nfiles, (uint32_t)i);
+        const uint32_t f = flg[i];
+        state[i] = (f & IXF_EXP) ? (uint8_t)CLY_IX_EXPIRED
+                 : (f & IXF_CHK) ? ix_win_state(tup, first, bases, nfiles, (uint32_t)i) : (uint8_t)CLY_IX_LIVE;
     }
 }
 // exact resolution of a collided hash group (one thread): per distinct key the max order
-__global__ void __launch_bounds__(64)
-k_ixcoll(const uint64_t* __restrict__ sh, const uint32_t* __restrict__ sidx, const uint64_t* __restrict__ order,
-         uint64_t m, const uint8_t* __restrict__ coll, const cly_tuple* __restrict__ tup,
-         const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases, int nfiles, uint8_t* state,
-         int64_t now_ns) {
-    const uint64_t q0 = (uint64_t)blockIdx.x * 64 + threadIdx.x;
-    if (q0 >= m || !coll[q0]) return;
+__global__ void __launch_bounds__(256)
+k_ixcoll(const uint64_t* __restrict__ spk, uint32_t ib, const uint8_t* __restrict__ cls,
+         const uint64_t* __restrict__ order, uint64_t m,
+         const cly_tuple* __restrict__ tup, const uint64_t* __restrict__ first, const uint64_t* __restrict__ bases,
+         int nfiles, const uint4* __restrict__ ksig, const uint64_t* __restrict__ hash, const uint8_t* __restrict__ flg,
+         uint8_t* state, const uint32_t* __restrict__ heads, uint64_t nheads) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= nheads) return;
+    const uint64_t q0 = heads[t];
+    const uint64_t h0 = ix_pk_h(spk[q0], ib);
     uint64_t q1 = q0 + 1;
-    while (q1 < m && sh[q1] == sh[q0]) q1++;
-    for (uint64_t a = q0; a < q1; a++) state[IXI(sidx[a])] = CLY_IX_DEAD;
+    while (q1 < m && ix_pk_h(spk[q1], ib) == h0) q1++;
+    for (uint64_t a = q0; a < q1; a++) state[IXI(ix_pk_s(spk[a], ib))] = CLY_IX_DEAD;
     for (uint64_t a = q0; a < q1; a++) {
-        const uint32_t ia = IXI(sidx[a]);
+        const uint32_t ia = IXI(ix_pk_s(spk[a], ib));
+        const uint64_t oa = ix_order(cls, order, ia);
+        const uint4 sa = ksig[ia];
         bool best = true;
-        for (uint64_t b = q0; b < q1 && best; b++)
-            if (b != a && order[IXI(sidx[b])] > order[ia] &&
-                ix_same_key(tup, first, bases, nfiles, ia, IXI(sidx[b]))) best = false;
-        if (best && tup[ia].type != 1)
-            state[ia] = ix_expired(tup[ia], now_ns) ? (uint8_t)CLY_IX_EXPIRED : ix_win_state(tup, first, bases, nfiles, ia);
+        for (uint64_t b = q0; b < q1 && best; b++) {
+            const uint32_t ibb = IXI(ix_pk_s(spk[b], ib));
+            if (b == a || ix_order(cls, order, ibb) <= oa) continue;
+            // same key: equal signatures (exact for keys of <= 15 bytes), else
+            // equal table hashes and the bytes
+            const uint4 sb = ksig[ibb];
+            if (sa.x != sb.x || sa.y != sb.y || sa.z != sb.z || sa.w != sb.w) continue;
+            if (!ix_sig_long(sa) || (hash[ia] == hash[ibb] && ix_same_key(tup, first, bases, nfiles, ia, ibb)))
+                best = false;
+        }
+        const uint32_t f = flg[ia];
+        if (best && !(f & IXF_DEL))
+            state[ia] = (f & IXF_EXP) ? (uint8_t)CLY_IX_EXPIRED
+                      : (f & IXF_CHK) ? ix_win_state(tup, first, bases, nfiles, ia) : (uint8_t)CLY_IX_LIVE;
     }
 }
 // counts: one atomic per workgroup and counter (a wave-level atomic on one
@@ -421,19 +507,19 @@ k_ixcount(const uint8_t* __restrict__ state, const uint8_t* __restrict__ flag, u
     }
 }
 
+// the txIds of the selected tx records
 __global__ void __launch_bounds__(256)
-k_ixgather(const uint64_t* __restrict__ src, const uint32_t* __restrict__ sel, uint64_t m, uint64_t* dst) {
+k_ixgathertx(const cly_tuple* __restrict__ tup, const uint32_t* __restrict__ sel, uint64_t m, uint64_t* dst) {
     for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < m; p += (uint64_t)gridDim.x * 256)
-        dst[p] = src[sel[p]];
+        dst[p] = (uint64_t)tup[sel[p]].tx_id;
 }
-// hash keys of the applied records and their indices with the IX_DEL bit
+// sort keys of the selected applied records
 __global__ void __launch_bounds__(256)
-k_ixgatherd(const uint64_t* __restrict__ src, const uint32_t* __restrict__ sel, const uint8_t* __restrict__ del,
-            uint64_t m, uint64_t* dst, uint32_t* selv) {
+k_ixgatherd(const uint64_t* __restrict__ hash, const uint32_t* __restrict__ sel, const uint8_t* __restrict__ del,
+            uint64_t m, uint64_t* dst, uint32_t ib, uint32_t hb) {
     for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < m; p += (uint64_t)gridDim.x * 256) {
         const uint32_t i = sel[p];
-        dst[p] = src[i];
-        selv[p] = i | (del[i] ? IX_DEL : 0u);
+        dst[p] = ix_pk(hash[i], i, (del[i] & IXF_DEL) != 0, ib, hb);
     }
 }
 
@@ -457,6 +543,20 @@ static uint64_t ix_hash_mask(uint64_t n, int& hbits) {
     return hm;
 }
 extern "C" uint64_t cly_ix_hash_mask_internal(uint64_t n) { int hb; return ix_hash_mask(n, hb); }
+// Sort-key geometry (ix_pk): ib = ceil(log2 n) index bits, hb = log2(n) + 8
+// hash bits (at most 63 - ib, at most the table hash's width): expected
+// colliding pairs n^2 / 2^(hb+1) <= n / 512, each resolved exactly; the radix
+// sort makes ceil(hb / 8) passes of 8 B per record (C4: 5 passes, before 7
+// passes of a 12-B key-value pair).
+static void ix_pk_bits(uint64_t n, int hbits, uint32_t& ib, uint32_t& hb) {
+    int lg = 0;
+    while (lg < 63 && (1ull << lg) < n) lg++;
+    ib = lg ? (uint32_t)lg : 1u;
+    int h = lg + 8;
+    if (h > 63 - (int)ib) h = 63 - (int)ib;
+    if (h > hbits) h = hbits;
+    hb = (uint32_t)h;
+}
 // The device buffer of the key hashes of the last cly_index_device call of
 // this context (n values: the records applied to an index; others undefined).
 extern "C" hipError_t cly_ix_hash_ptr_internal(cly_ctx* ctx, uint64_t n, void** out) {
@@ -489,7 +589,6 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     uint32_t *d_sel = nullptr, *d_sidx = nullptr;
     uint8_t *d_cls = nullptr, *d_flag = nullptr, *d_coll = nullptr, *d_del = nullptr, *d_apflag = nullptr;
     uint4* d_ksig = nullptr;
-    uint32_t* d_selv = nullptr;
     uint64_t hm = ~0ull;
     TxNext *d_rev = nullptr, *d_nxt = nullptr;
     GMax *d_g = nullptr, *d_g2 = nullptr;
@@ -504,6 +603,8 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     rocprim::counting_iterator<uint32_t> cnt(0);
     uint64_t m = 0, m2 = 0;
     int hbits = 64;
+    uint32_t ib = 1, hb = 1;
+    uint64_t* d_pk = nullptr;
     const uint64_t* d_first = nullptr;
     const uint64_t* d_bases = nullptr;
     ICK(hipEventCreate(&e0));
@@ -515,10 +616,9 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     ICK(cly_ix_scratch_internal(ctx, 2, sizeof(unsigned long long), (void**)&d_nsel));
     ICK(cly_ix_scratch_internal(ctx, 3, n, (void**)&d_cls));
     ICK(cly_ix_scratch_internal(ctx, 4, n, (void**)&d_flag));
-    ICK(cly_ix_scratch_internal(ctx, 5, n, (void**)&d_coll));
+    ICK(cly_ix_scratch_internal(ctx, 5, n + 4, (void**)&d_coll));     // (k_ixwin sets bytes by word atomics)
     ICK(cly_ix_scratch_internal(ctx, 6, n, (void**)&d_del));
     ICK(cly_ix_scratch_internal(ctx, 7, n, (void**)&d_apflag));
-    ICK(cly_ix_scratch_internal(ctx, 8, sizeof(uint32_t) * n, (void**)&d_selv));
     ICK(cly_ix_scratch_internal(ctx, 9, sizeof(uint4) * n, (void**)&d_ksig));
     ICK(cly_ix_scratch_internal(ctx, 10, sizeof(uint64_t) * n, (void**)&d_txkey));
     ICK(cly_ix_scratch_internal(ctx, 11, sizeof(uint64_t) * n, (void**)&d_k2));
@@ -530,10 +630,13 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     ICK(cly_ix_scratch_internal(ctx, 17, sizeof(TxNext) * n, (void**)&d_nxt));
     ICK(cly_ix_scratch_internal(ctx, 18, sizeof(GMax) * n, (void**)&d_g));
     ICK(cly_ix_scratch_internal(ctx, 19, sizeof(GMax) * n, (void**)&d_g2));
+    ICK(cly_ix_scratch_internal(ctx, 21, sizeof(uint64_t) * n, (void**)&d_pk));
     // temp storage: the largest of the select / sort / scan needs
     ICK(rocprim::select(nullptr, need, cnt, d_flag, d_sel, d_nsel, (size_t)n, st));
     tmp_bytes = need;
     ICK(rocprim::radix_sort_pairs(nullptr, need, d_k2, d_txkey, d_sel, d_sidx, (size_t)n, 0u, 64u, st));
+    if (need > tmp_bytes) tmp_bytes = need;
+    ICK(rocprim::radix_sort_keys(nullptr, need, d_k2, d_txkey, (size_t)n, 0u, 64u, st));
     if (need > tmp_bytes) tmp_bytes = need;
     ICK(rocprim::inclusive_scan(nullptr, need, d_rev, d_nxt, (size_t)n, TxNextOp(), st));
     if (need > tmp_bytes) tmp_bytes = need;
@@ -542,12 +645,12 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     ICK(cly_ix_scratch_internal(ctx, 20, tmp_bytes, &d_tmp));
     ICK(hipMemcpyAsync(d_fb, h_fb, sizeof(uint64_t) * (2 * (size_t)nfiles + 1), hipMemcpyHostToDevice, st));
     ICK(hipMemsetAsync(d_tot, 0, sizeof(IxTot), st));
-    ICK(hipMemsetAsync(d_order, 0xff, sizeof(uint64_t) * n, st));
-    ICK(hipMemsetAsync(d_coll, 0, n, st));
+    ICK(hipMemsetAsync(d_coll, 0, n + 4, st));
     ICK(hipEventRecord(e0, st));
     hm = ix_hash_mask(n, hbits);
-    k_ixclass<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_state, d_txkey, d_flag, d_tot, d_first, d_bases, nfiles,
-                                    d_order, d_hash, d_apflag, d_del, d_ksig, d_selv, hm);
+    ix_pk_bits(n, hbits, ib, hb);
+    k_ixclass<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_state, d_flag, d_tot, d_first, d_bases, nfiles, d_hash,
+                                    d_apflag, d_del, d_ksig, d_pk, hm, ib, hb, now_ns);
     ICK(hipMemcpyAsync(&h_tot, d_tot, sizeof(IxTot), hipMemcpyDeviceToHost, st));
     ICK(hipStreamSynchronize(st));
     // ---- transactions: tx records sorted by txId (stable: scan order within a txId)
@@ -559,7 +662,9 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
         m = h_nsel;
     }
     if (m) {
-        k_ixgather<<<ix_grid(m), 256, 0, st>>>(d_txkey, d_sel, m, d_k2);
+        // (tx data records' application orders: k_ixtx; the others stay IX_NONE)
+        ICK(hipMemsetAsync(d_order, 0xff, sizeof(uint64_t) * n, st));
+        k_ixgathertx<<<ix_grid(m), 256, 0, st>>>(d_tuples, d_sel, m, d_k2);
         {
             size_t tb = tmp_bytes;
             // sorted txIds into d_txkey (free after the gather; d_hash holds k_ixclass's hashes)
@@ -575,7 +680,7 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     // ---- applied records: hash, sort, winner per key
     // (records without a txId were hashed by k_ixclass; committed tx data here)
     if (m) k_ixapply<<<grid, 256, 0, st>>>(d_tuples, n, d_cls, d_order, d_first, d_bases, nfiles, d_hash, d_apflag,
-                                           d_del, d_ksig, hm, &d_tot->bad);
+                                           d_del, d_ksig, hm, &d_tot->bad, now_ns);
     if (m == 0 && h_tot.n_now == n) {
         m2 = n;                                                 // every record applied: no select
     } else {
@@ -586,29 +691,31 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
         m2 = h_nsel;
     }
     if (m2) {
-        // every record applied now: k_ixclass wrote the sort input in place;
-        // otherwise gather the selected records' hashes and indices
+        // every record applied now: k_ixclass wrote the sort keys in place;
+        // otherwise build the selected records' keys
         const bool ident = m == 0 && m2 == n;
-        uint32_t* d_vin = ident ? d_selv : (uint32_t*)d_rev;    // d_rev is free after the tx phase
-        if (!ident) k_ixgatherd<<<ix_grid(m2), 256, 0, st>>>(d_hash, d_sel, d_del, m2, d_k2, d_vin);
+        if (!ident) k_ixgatherd<<<ix_grid(m2), 256, 0, st>>>(d_hash, d_sel, d_del, m2, d_k2, ib, hb);
         {
+            // sorted keys into d_txkey (free after the tx phase)
             size_t tb = tmp_bytes;
-            ICK(rocprim::radix_sort_pairs(d_tmp, tb, ident ? d_hash : d_k2, d_txkey, d_vin, d_sidx, (size_t)m2,
-                                                   0u, (unsigned)hbits, st));
+            ICK(rocprim::radix_sort_keys(d_tmp, tb, ident ? d_pk : d_k2, d_txkey, (size_t)m2, ib + 1u, ib + 1u + hb,
+                                         st));
         }
         if (m) {                    // tx records: application order != scan order, arg-max per group
-            k_ixgin<<<ix_grid(m2), 256, 0, st>>>(d_txkey, d_sidx, d_order, m2, d_g);
+            k_ixgin<<<ix_grid(m2), 256, 0, st>>>(d_txkey, ib, d_cls, d_order, m2, d_g);
             size_t tb = tmp_bytes;
             ICK(rocprim::inclusive_scan(d_tmp, tb, d_g, d_g2, (size_t)m2, GMaxOp(), st));
         }
-        k_ixwin<<<ix_grid(m2), 256, 0, st>>>(d_txkey, d_sidx, m ? d_g2 : nullptr, m2, d_tuples, d_first, d_bases,
-                                             nfiles, d_ksig, d_state, d_coll, d_tot, now_ns);
+        // (d_sel is free after the sort: the collided groups' heads)
+        k_ixwin<<<ix_grid(m2), 256, 0, st>>>(d_txkey, ib, m ? d_g2 : nullptr, m2, d_tuples, d_first, d_bases,
+                                             nfiles, d_ksig, d_state, d_coll, d_sel, d_tot);
         ICK(hipMemcpyAsync(&h_tot, d_tot, sizeof(IxTot), hipMemcpyDeviceToHost, st));
         ICK(hipStreamSynchronize(st));
-        if (h_tot.n_coll)
-            k_ixcoll<<<(unsigned)((m2 + 63) / 64), 64, 0, st>>>(d_txkey, d_sidx, d_order, m2, d_coll, d_tuples, d_first,
-                                                                d_bases, nfiles, d_state, now_ns);
-        k_ixwinfix<<<ix_grid(n), 256, 0, st>>>(d_tuples, n, d_first, d_bases, nfiles, d_state, now_ns);
+        if (h_tot.n_chead)
+            k_ixcoll<<<(unsigned)((h_tot.n_chead + 255) / 256), 256, 0, st>>>(
+                d_txkey, ib, d_cls, d_order, m2, d_tuples, d_first, d_bases, nfiles, d_ksig, d_hash, d_del, d_state,
+                d_sel, h_tot.n_chead);
+        k_ixwinfix<<<ix_grid(n), 256, 0, st>>>(d_tuples, n, d_first, d_bases, nfiles, d_del, d_state);
     }
     k_ixcount<<<ix_grid(n) < 1024 ? ix_grid(n) : 1024, 256, 0, st>>>(d_state, d_apflag, n, d_tot);
     ICK(hipGetLastError());

@@ -224,7 +224,9 @@ typedef struct cly_index_result {
     uint64_t n_live;          /* index entries (= records LIVE or LOADONLY)     */
     uint64_t n_applied;       /* records updateIndex sees                       */
     uint64_t n_host;          /* 0 (kept for layout)                            */
-    uint64_t n_collisions;    /* 64-bit key-hash collisions (resolved exactly)  */
+    uint64_t n_collisions;    /* sort-hash collisions: records whose key differs
+                                 from the one before them in hash order
+                                 (resolved exactly; informational)           */
     double   index_ms;        /* device time                                    */
     uint64_t n_loadonly;      /* records in state LOADONLY                      */
     uint64_t n_merge_panic;   /* Hash/List/Set records whose realKey decode
