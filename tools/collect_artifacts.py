@@ -64,7 +64,8 @@ shutil.copy(os.path.join(fin, "c4m_stats", "run_kernel_stats.csv"),
 t4 = traffic("c4", "c4m_p1", "c4m_p2", build, only=lambda k: k.startswith("k_m") or k.startswith("k_hint"),
              source="bench.py --config c4 (merge kernels only)")
 json.dump(t4, open(os.path.join(prof, "%s_c4_merge_traffic.json" % tag), "w"), indent=1)
-sq = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_agg.py"), fin, "c2", "c3", "c4"],
+sq = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_agg.py"), fin, "c2", "c3", "c4"] +
+                    (["c4m"] if os.path.isdir(os.path.join(fin, "c4m_p3")) else []),
                     capture_output=True, text=True).stdout
 open(os.path.join(prof, "%s_pmc_sq.txt" % tag), "w").write(
     "# SQ counters per kernel launch (averages), build %s; per-4-KiB-block figures use the config's input bytes\n%s"

@@ -8,7 +8,7 @@ import os
 import sys
 
 root = sys.argv[1]
-BLOCKS = {"small": 1013434099 / 4096, "c2": 4294966272 / 4096, "c3": 34359738368 / 4096, "c4": 34359738368 / 4096, "c5": 34359738368 / 4096}
+BLOCKS = {"small": 1013434099 / 4096, "c2": 4294966272 / 4096, "c3": 34359738368 / 4096, "c4": 34359738368 / 4096, "c5": 34359738368 / 4096, "c4m": 34359738368 / 4096}
 for cfg in sys.argv[2:]:
     vals = collections.defaultdict(dict)
     for f in sorted(glob.glob(os.path.join(root, cfg + "_p*", "run_counter_collection.csv"))):
