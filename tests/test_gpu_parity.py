@@ -7,7 +7,7 @@ import os
 import numpy as np
 import pytest
 
-from couloydb_amd import DataFile, Scanner, TUPLE_DTYPE, _abi
+from couloydb_amd import DataFile, ScanError, Scanner, TUPLE_DTYPE, _abi
 from oracle import cly_oracle as co
 
 from .gpu_util import FIELDS, compare, fixed_records_file, mixed_corpus
@@ -679,3 +679,34 @@ def test_tiny_record_file_past_link_mask(scanner):
         d[off + 5] ^= 1
         first, res, stt, need = sc.scan_device([(d.data_ptr(), d.numel(), 9)], out.data_ptr(), total + 64)
         assert (res[0].status, res[0].n_records, res[0].end_offset) == (_abi.ERR_CRC, k, off)
+
+
+def test_record_past_part_view(scanner):
+    """A record of nearly 4 GiB (ValueSize is a uint32, data/logRecord.go:101-106)
+    that starts in a part and ends past that part's 4-GiB view, in a file longer
+    than the view: the scan cannot read it whole, and says so (CLY_ERR_ARG)
+    instead of reporting the torn-record io.EOF ReadLogRecord would not return.
+    The same record in a file that ends inside it is a torn tail (CLY_END_TORN),
+    as in the reference (the short ReadAt, data/dataFile.go:94-98)."""
+    torch = pytest.importorskip("torch")
+    import make_golden as mg
+    a = mg.encode_record(mg.key_tx(mg.test_key(1), 0), b"v" * 17)
+    vs = 0xFFFFFFFF                      # past both builds' views (4 GiB less two tiles)
+    key = mg.key_tx(mg.test_key(2), 0)
+    hdr = bytes([0x11, 0x22, 0x33, 0x44, 0, 0]) + mg.put_varint(len(key)) + mg.put_varint(vs) + mg.put_varint(0)
+    end = len(a) + len(hdr) + len(key) + vs
+    for total, want in ((end + 4096, "arg"), (end - 4096, "torn")):
+        d = torch.zeros(total, dtype=torch.uint8, device="cuda")
+        head = np.frombuffer(a + hdr + key, np.uint8)
+        d[: len(head)] = torch.from_numpy(head.copy()).cuda()
+        out = torch.empty(64 * 48, dtype=torch.uint8, device="cuda")
+        with Scanner(0, lib=scanner.lib_name) as sc:
+            if want == "arg":
+                with pytest.raises(ScanError) as ei:
+                    sc.scan_device([(d.data_ptr(), total, 5)], out.data_ptr(), 64)
+                assert ei.value.code == _abi.ERR_ARG
+            else:
+                first, res, st, need = sc.scan_device([(d.data_ptr(), total, 5)], out.data_ptr(), 64)
+                assert (res[0].status, res[0].n_records, res[0].end_offset) == (2, 1, len(a))
+        del d
+        torch.cuda.empty_cache()
