@@ -27,6 +27,10 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 #define F_E8 16384      // compact entries of 8 B
 #define F_SEGH 32768    // segment registers at 128-B granularity (even lanes store)
 #define F_SEGQ 65536    // ... at 256-B granularity (lanes % 4 == 0 store)
+#define F_KS 131072     // no segment registers stored: a segmented Kogge-Stone scan of the
+                        // segments' registers over the lanes (A^(64 2^l) by nibble tables)
+                        // and the register entering a record start's word (A^(4k) by four
+                        // nibble matrices) -- k_scan checking every record itself
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mk(const void* p, uint32_t n) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)n, 0x00020000);
 }
@@ -55,11 +59,19 @@ __device__ __forceinline__ uint32_t crc_word(const LDSP uint8_t* sm, uint32_t x,
   if (F & F_X3) return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(t0, t1, nxt, 0x96), t2, t3, 0x96);
   return t0 ^ t1 ^ t2 ^ t3 ^ nxt;
 }
+__device__ __forceinline__ uint32_t nib_mul(const LDSP uint32_t* T, uint32_t x) {
+  uint32_t y = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) y ^= T[j * 16 + ((x >> (4 * j)) & 15u)];
+  return y;
+}
 template <int F>
 __global__ void __launch_bounds__(64 * WAVES) kskel(const uint8_t* buf, uint32_t ntiles, uint32_t* rec, uint32_t* seg,
                                                     uint32_t* snap, uint32_t* out) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[65536 + 256 + WAVES * (STG_BYTES + 256) + ((F & F_SNK) ? WAVES * 2048 : 0)];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[65536 + 256 + WAVES * (STG_BYTES + 256) + ((F & F_SNK) ? WAVES * 2048 : 0) + ((F & F_KS) ? 10 * 512 : 0)];
   for (int i = threadIdx.x; i < 16384; i += blockDim.x) ((LDSP uint32_t*)smem)[i] = i * 2654435761u;
+  LDSP uint32_t* kst = (LDSP uint32_t*)(smem + 65536 + 256 + WAVES * (STG_BYTES + 256) + ((F & F_SNK) ? WAVES * 2048 : 0));
+  if (F & F_KS) for (int i = threadIdx.x; i < 10 * 128; i += blockDim.x) kst[i] = i * 0x9E3779B9u;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -85,7 +97,7 @@ __global__ void __launch_bounds__(64 * WAVES) kskel(const uint8_t* buf, uint32_t
 #pragma unroll
     for (int k = 0; k < 4; k++) e[k] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(off0 + 1024u * k), 0, 0);
     if ((F & F_STG) && lane < 2) hl = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(4096 + 16 * lane), 0, 0);
-    uint32_t X = (t * 37u) % 276u, tcnt = 0, nb = 0, Rp = 0, sq[4] = {0, 0, 0, 0}, sk = 0;
+    uint32_t X = (t * 37u) % 276u, tcnt = 0, nb = 0, Rp = 0, sq[4] = {0, 0, 0, 0}, sk = 0, gcar = 0;
 #pragma unroll 1
     for (int m = 0; m < NBLK; m++) {
       const uint32_t bs = m * 4096;
@@ -180,6 +192,30 @@ __global__ void __launch_bounds__(64 * WAVES) kskel(const uint8_t* buf, uint32_t
           sq[m & 3] = R;
           if ((m & 3) == 3) __builtin_amdgcn_raw_buffer_store_b128((u32x4){sq[0], sq[1], sq[2], sq[3]}, srs, (int)(((m >> 2) * 64 + lane) * 16), 0, 0);
         }
+        if (F & F_KS) {
+          // segmented inclusive scan of (reset, register) over the lanes
+          uint32_t v = R, rf = ((lane * 7 + m) % 5 == 0) ? 1u : 0u;
+#pragma unroll
+          for (int l = 0; l < 6; l++) {
+            const int d = 1 << l;
+            const uint32_t vp = (uint32_t)__shfl_up((int)v, d, 64), rp = (uint32_t)__shfl_up((int)rf, d, 64);
+            if (lane >= d && !rf) { v = nib_mul(kst + l * 128, vp) ^ v; rf = rp; }
+          }
+          uint32_t gin = (uint32_t)__shfl_up((int)v, 1, 64);
+          if (lane == 0) gin = gcar;
+          gcar = rdl(v, 63);
+          // the register entering the segment's first record start (word k): A^(4k) gin ^ w[k]
+          if (rf) {
+            const uint32_t k = (uint32_t)(lane & 15);
+            uint32_t x = gin;
+            if (k & 1) x = nib_mul(kst + 6 * 128, x);
+            if (k & 2) x = nib_mul(kst + 7 * 128, x);
+            if (k & 4) x = nib_mul(kst + 8 * 128, x);
+            if (k & 8) x = nib_mul(kst + 9 * 128, x);
+            acc ^= x ^ w[k & 15];
+          }
+          acc ^= v;
+        }
         acc ^= R;
       } else {
 #pragma unroll
@@ -242,6 +278,8 @@ int main() {
   hipMalloc(&seg, (size_t)ntiles * 1024 * 4);
   hipMalloc(&snap, (size_t)ntiles * 516 * 4);
 #define R(F) run<F>(buf, ntiles, rec, seg, snap, out)
-  R(7 + 64); R(15 + 64); R(15 + 64 + 32768); R(15 + 64 + 65536); R(35); R(35 + 16384); R(35 + 128); R(127); R(127 - 16); R(127 + 16384); R(127 + 32768); R(127 + 65536); R(127 + 16384 + 32768); R(127 - 16 + 16384 + 32768); R(127 - 16 + 16384 + 65536); R(127 - 8 - 16 + 128);
+  for (int rep = 0; rep < 2; rep++) {
+    R(7 + 64); R(127); R(127 - 8); R(127 - 8 + F_KS); R(127 - 8 - 16); R(127 - 8 - 16 + F_KS); R(127 + F_KS);
+  }
   return 0;
 }
