@@ -1462,6 +1462,7 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         tile_issue(V, ptt, lane, e, hl);
     }
     uint32_t Xc = NONE32;        // the entry carried from the run's previous tile (NONE32: guess)
+    bool bad_run = false;
     for (;;) {
         const DevFile F = files[f];
         const uint32_t rend = min(F.first_tile + (r - rprefix[f] + 1u) * rt, F.first_tile + F.ntile);
@@ -1470,7 +1471,7 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         int fn = f;
         if (tn >= rend) {
             rn = r + slots < nstat ? r + slots : nstat + (uint32_t)__builtin_amdgcn_readfirstlane((int)rq);
-            if (rn <= r) rn = nruns;   // (runs only increase: never)
+            if (rn <= r) { bad_run = true; rn = nruns; }   // (runs only increase: never; fails the call)
             fn = rn < nruns ? find_file(rprefix, nfiles, rn) : -1;
             if (fn >= 0) tn = files[fn].first_tile + (rn - rprefix[fn]) * rt;
         }
@@ -1499,6 +1500,7 @@ k_scan(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
         }
         t = tn; f = fn;
     }
+    if (bad_run && lane == 0) atomicOr(&g->fail, 256u);
 }
 
 // k_link: one workgroup per file: the chain state entering every tile.  A
