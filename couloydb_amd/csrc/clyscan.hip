@@ -205,7 +205,8 @@ struct Globals {                 // zeroed per call
 #define EM_F4 0                   // A^(4k): table k - 1
 #define EM_F1 16                  // A^1, A^2, A^3: tables 16, 17, 18
 #define EM_RUN 19                 // A^(RUN_BYTES 2^l): table 19 + l
-#define NEM 25
+#define EM_SEGP 25                // A^(64 2^l), l = 1..3: table 24 + l (k_emit's A^(64 j), j < 16)
+#define NEM 28
 #define NTAB_ALL (TAB_EM + NEM * 128)
 // LDS of k_scan / k_refix (static: compile-time offsets)
 //   [0, 65536)  CRC slicing-by-4 tables T0..T3, 16 replicas: dword (i*64 + t*16 + r)
@@ -1820,6 +1821,7 @@ k_refix(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restric
 #define EMIT_KJ (NEM * 128)                    // kj[4] after the tables (words)
 #define EMIT_LDS (NEM * 128 * 4 + 16 + 4096 + EMIT_WAVES * EW_BYTES)
 static_assert(CLY_NL * RUN == NSEG, "one run of segments per lane");
+static_assert(RUN <= 16, "gin_true's A^(64 j) from A^64 .. A^512");
 // LDS word of segment sg: plain (the per-record path: neighbouring records'
 // segments in different banks) or lane-transposed (the tile-wide scan: lane
 // L's run of RUN segments in one bank column)
@@ -2129,14 +2131,20 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
+            // one Horner pass over the lane's run of segments from zero (resets
+            // applied): gin keeps the register entering each of them relative to
+            // the run's start (h); the register entering segment j of lane L's
+            // run is h, or, with no reset before it in the run, A^(64 j) y_L ^ h
+            // (y_L: the scan's register entering the run; gin_true)
             uint32_t x = 0, rc = 0, fl = 0;
             #pragma unroll
             for (int k = 0; k < RUN; k++) {
                 const uint32_t sg = (uint32_t)lane * RUN + k;
-                sr[k] = gin[k * 64 + lane];
+                const uint32_t sk = gin[k * 64 + lane];
                 const uint32_t fk = (flg[sg >> 5] >> (sg & 31u)) & 1u;
                 fl |= fk << k;
-                x = fk ? sr[k] : em_a64b(emt, x) ^ sr[k];
+                gin[k * 64 + lane] = x;
+                x = fk ? sk : em_a64b(emt, x) ^ sk;
                 rc |= fk;
             }
             #pragma unroll
@@ -2147,20 +2155,34 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
             }
             uint32_t y = (uint32_t)__shfl_up((int)x, 1, 64);
             if (lane == 0) y = 0;
-            #pragma unroll
-            for (int k = 0; k < RUN; k++) {
-                gin[k * 64 + lane] = y;
-                y = ((fl >> k) & 1u) ? sr[k] : em_a64b(emt, y) ^ sr[k];
-            }
-            const uint32_t gte = rdl(y, 63);                                // the register at the tile's end
+            const uint32_t gte = rdl(x, 63);                                // the register at the tile's end
+            // the lanes' entering registers and reset masks, for gin_true (in the
+            // round's tuple stage: the tuples are out)
+            CLY_LDS uint32_t* yarr = (CLY_LDS uint32_t*)sv;
+            yarr[lane] = y;
+            yarr[64 + lane] = fl;
             if (lane == 0) gin[NSEG] = gte;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            auto gin_true = [&](uint32_t sg) -> uint32_t {
+                if (sg >= NSEG) return gte;
+                const uint32_t L = sg / RUN, j = sg % RUN;
+                uint32_t h = gin[j * 64u + L];
+                if ((yarr[64 + L] & ((1u << j) - 1u)) == 0u) {
+                    uint32_t v = yarr[L];
+                    if (j & 1u) v = em_a64b(emt, v);
+                    if (j & 2u) v = mat_mul(emt + (EM_SEGP + 0) * 128, v);
+                    if (j & 4u) v = mat_mul(emt + (EM_SEGP + 1) * 128, v);
+                    if (j & 8u) v = mat_mul(emt + (EM_SEGP + 2) * 128, v);
+                    h ^= v;
+                }
+                return h;
+            };
             ex = gte;
             if (gterm) { ex = 0; dev = gte ^ cout; }
             else if (grec) {
                 // the tile's own register entering WG (no reset before G)
-                dev = (sigG < NSEG ? em_f4(emt, (WG - tb - 64u * sigG) >> 2, gin[gin_at(sigG, false)]) : gte) ^ sG ^ expG;
+                dev = (sigG < NSEG ? em_f4(emt, (WG - tb - 64u * sigG) >> 2, gin_true(sigG)) : gte) ^ sG ^ expG;
                 {
                     // past the last record start: its reset at the tile's end
                     // when its patch word is there, else the scan's register
@@ -2175,7 +2197,7 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
                         const uint32_t c1 = entry_crc(base, F.len, tb, v), c2 = entry_crc(base, F.len, tb, v2);
                         const uint32_t s1 = E.snap(i), s2 = E.snap(i + 1);
                         const uint32_t pre = sg2 == sg ? s2 ^ em_f4(emt, (W2 - W) >> 2, s1 ^ exp_post(p & 3u, c1, kj))
-                                                       : em_f4(emt, (W2 - tb - 64u * sg2) >> 2, gin[gin_at(sg2, false)]) ^ s2;
+                                                       : em_f4(emt, (W2 - tb - 64u * sg2) >> 2, gin_true(sg2)) ^ s2;
                         if (pre != exp_pre(emt, P2 & 3u, c1, c2))
                             fail_at(fo, x0 + p, S.count + i);
                     }
@@ -2329,7 +2351,8 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
                 const int e = k - 66;                                                // TAB_EM
                 if (e < EM_F1) nbytes = 4ull * (uint64_t)(e + 1);                    // A^(4k), k = 1..16
                 else if (e < EM_RUN) nbytes = (uint64_t)(e - EM_F1 + 1);             // A^1..A^3
-                else nbytes = (uint64_t)RUN_BYTES << (e - EM_RUN);                   // A^(RUN_BYTES 2^l)
+                else if (e < EM_SEGP) nbytes = (uint64_t)RUN_BYTES << (e - EM_RUN);  // A^(RUN_BYTES 2^l)
+                else nbytes = 64ull << (e - EM_SEGP + 1);                            // A^128, A^256, A^512
             }
             const uint32_t xm = cly_x8n(nbytes);
             for (int nb = 0; nb < 8; nb++)
