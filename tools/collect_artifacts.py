@@ -53,7 +53,9 @@ build = b2["kernel"]["build"]
 for cfg in ("c2", "c3", "c4"):
     b = last_json(os.path.join(fin, "bench_%s.json" % cfg))
     json.dump(b, open(os.path.join(prof, "%s_bench%s.json" % (tag, "" if cfg == "c2" else "_" + cfg)), "w"), indent=1)
-for cfg in ("c2", "c3", "c4"):
+for cfg in ("c2", "c3", "c4", "c5"):
+    if not os.path.isdir(os.path.join(fin, cfg + "_stats")):
+        continue
     shutil.copy(os.path.join(fin, cfg + "_stats", "run_kernel_stats.csv"),
                 os.path.join(prof, "%s_%s_rocprof_kernel_stats.csv" % (tag, cfg)))
     t = traffic(cfg, cfg + "_p3", cfg + "_p4", build, source="tools/scan_once.py %s (one scan per launch)" % cfg)
@@ -64,7 +66,7 @@ shutil.copy(os.path.join(fin, "c4m_stats", "run_kernel_stats.csv"),
 t4 = traffic("c4", "c4m_p1", "c4m_p2", build, only=lambda k: k.startswith("k_m") or k.startswith("k_hint"),
              source="bench.py --config c4 (merge kernels only)")
 json.dump(t4, open(os.path.join(prof, "%s_c4_merge_traffic.json" % tag), "w"), indent=1)
-sq = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_agg.py"), fin, "c2", "c3", "c4"] +
+sq = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_agg.py"), fin, "c2", "c3", "c4", "c5"] +
                     (["c4m"] if os.path.isdir(os.path.join(fin, "c4m_p3")) else []),
                     capture_output=True, text=True).stdout
 open(os.path.join(prof, "%s_pmc_sq.txt" % tag), "w").write(

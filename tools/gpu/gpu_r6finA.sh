@@ -15,7 +15,7 @@ timeout -k 10 400 python -u bench.py --config c4 --no-host-path --no-cpu-baselin
 timeout -k 10 400 python -u bench.py --config c3 --no-host-path --no-cpu-baseline > $D/bench_c3.json 2> $D/bench_c3.err || exit $?
 S1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS"
 S2="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT"
-for cfg in c2 c3 c4; do
+for cfg in c2 c3 c4 c5; do
   timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/${cfg}_stats -o run -- python3 tools/scan_once.py $cfg 5 > $D/${cfg}_stats.log 2>&1 || exit $?
   i=0
   for s in "$S1" "$S2" "FETCH_SIZE" "WRITE_SIZE"; do
