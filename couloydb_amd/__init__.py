@@ -127,6 +127,7 @@ class Scanner:
     def __init__(self, device=0, lib="libclyscan.so"):
         self.lib_name = lib
         self.lib = _abi.load_scan_lib(lib)
+        self._dev_key, self._dev_arr = None, None      # scan_device's last file array (reused when equal)
         self.ctx = ctypes.c_void_p()
         rc = self.lib.cly_ctx_create(device, ctypes.byref(self.ctx))
         if rc != 0:
@@ -350,9 +351,13 @@ class Scanner:
         """Device-resident path: dev_files = [(device_ptr, len, fid)], d_out =
         device pointer of out_cap tuples.  Returns (file_first, results, stats, needed)."""
         n = len(dev_files)
-        arr = (_abi.ClyFile * max(1, n))()
-        for i, (ptr, ln, fid) in enumerate(dev_files):
-            arr[i].base, arr[i].len, arr[i].fid = ptr, ln, fid
+        key = tuple(dev_files)
+        if key != self._dev_key:           # (a repeated call over the same files builds no array)
+            arr = (_abi.ClyFile * max(1, n))()
+            for i, (ptr, ln, fid) in enumerate(dev_files):
+                arr[i].base, arr[i].len, arr[i].fid = ptr, ln, fid
+            self._dev_key, self._dev_arr = key, arr
+        arr = self._dev_arr
         first = (ctypes.c_uint64 * max(1, n))()
         res = (_abi.ClyFileResult * max(1, n))()
         need = ctypes.c_uint64()
@@ -361,7 +366,7 @@ class Scanner:
                                       ctypes.byref(st), stream)
         if rc != 0:
             raise ScanError(rc, self.lib.cly_strerror(rc).decode())
-        return [int(first[i]) for i in range(n)], [res[i] for i in range(n)], st, int(need.value)
+        return list(first)[:n], list(res)[:n], st, int(need.value)
 
 
 def build_info(lib="libclyscan.so"):
