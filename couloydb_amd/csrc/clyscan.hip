@@ -1034,7 +1034,7 @@ __device__ __forceinline__ uint32_t guess_entry(const DevFile& F, uint32_t bs, C
         const uint32_t nv = K.ce - K.cb;                    // valid positions
         if (nv < 64) cm &= (1ull << nv) - 1ull;
     }
-    uint32_t E = NONE32;
+    uint32_t E = NONE32, ex_x = 0, ex_sz = 0;       // (an unconfirmed start: its exit and the record there)
     bool conf_in = false;
     u64 mm = cm;
     bool settled = !K.on || !mm;
@@ -1082,12 +1082,34 @@ __device__ __forceinline__ uint32_t guess_entry(const DevFile& F, uint32_t bs, C
                     __builtin_amdgcn_s_waitcnt(0);          // every load of this path done here, not at a join
                 }
                 ok = hdr_plausible(eh, T.x, flen);
+                if (ok && eh.status == REC_OK) { ex_x = T.x; ex_sz = (uint32_t)eh.size; }
             }
         }
         if (act && ok) { E = T.E; conf_in = in; settled = true; }
         if (act && !ok && !mm) settled = true;
     }
-    const u64 bin = __ballot(E != NONE32 && conf_in), ball = __ballot(E != NONE32);
+    const u64 bin = __ballot(E != NONE32 && conf_in);
+    if (!bin) {
+        // no start confirmed inside the block (a long record's value bytes: C3):
+        // the header after the exit's record must be plausible too -- a false
+        // start passes one plausible header now and then, two almost never
+        // (C3: the first link round's contradicted runs)
+        bool drop = false;
+        if (E != NONE32 && ex_sz) {
+            const uint64_t x2 = (uint64_t)ex_x + ex_sz;
+            if (x2 < 0xFFFFFFFFull) {
+                Hdr e2;
+                if (in_stage((uint32_t)x2, bs)) e2 = hdr_get((uint32_t)x2, flen, stg, bs);
+                else {
+                    e2 = hdr_load((gbytes)F.base, (uint32_t)x2, flen);
+                    __builtin_amdgcn_s_waitcnt(0);
+                }
+                drop = !hdr_plausible(e2, (uint32_t)x2, flen);
+            }
+        }
+        if (drop) E = NONE32;
+    }
+    const u64 ball = __ballot(E != NONE32);
     if (!ball) return NONE32;
     return rdl(E, __ffsll((long long)(bin ? bin : ball)) - 1);
 }
@@ -2606,6 +2628,9 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
     float ms_fix = 0;
     uint32_t rounds = 1, refixed = 0;
     if (c->h_g->nfix[0]) { rounds++; refixed += c->h_g->nfix[0]; }          // the device round
+    if ((c->dbg & 2) && c->h_g->nfix[0])
+        fprintf(stderr, "clyscan: device repair round: %u tiles listed, longest walk %u from tile %u\n", c->h_g->nfix[0],
+                c->h_g->walk_max, (uint32_t)c->h_g->walk_dbg);
     if (c->h_g->nfix[slot]) {
         HIPCK(hipEventRecord(c->ev[5], st));
         while (c->h_g->nfix[slot]) {
