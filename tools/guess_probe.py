@@ -1,0 +1,59 @@
+"""Guess probe: one scan of a bench workload (argv[1], default c3) keeping the
+LOCALs before any repair (cly_dbg_set bit 0); lists the run-start tiles whose
+guessed entry differs from the true one (the final TileIn), with the bytes at
+the guess and at the true entry."""
+import ctypes
+import sys
+
+import numpy as np
+
+sys.path.insert(0, ".")
+import torch  # noqa: E402
+from bench import make_workload  # noqa: E402
+from couloydb_amd import Scanner  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+TILE, PART = 65536, 32768 * 65536
+wl = make_workload(cfg, torch)
+sc = Scanner(0)
+sc.lib.cly_dbg_set(sc.ctx, 3)
+first, res, st, need = sc.scan_device(wl.dev_files, wl.d_out.data_ptr(), wl.out_cap)
+nt = [max(1, (ln + TILE - 1) // TILE) for _, ln, _ in wl.dev_files]
+ntiles = sum(nt)
+loc = np.zeros((ntiles, 4), np.uint64)
+tin = np.zeros((ntiles, 8), np.uint32)
+sc.lib.cly_dbg_tiles(sc.ctx, ctypes.c_void_p(loc.ctypes.data), ctypes.c_void_p(tin.ctypes.data), ctypes.c_int64(ntiles))
+rt = 4
+wrong, shown, t0 = 0, 0, 0
+kinds = {}
+for f, (ptr, ln, fid) in enumerate(wl.dev_files):
+    fo = wl.file_off[f]
+    for u in range(0, nt[f], rt):
+        if u == 0:
+            continue
+        t = t0 + u
+        l0, l1 = int(loc[t, 0]), int(loc[t, 1])
+        dead = tin[t, 3] & 1
+        X = int(tin[t, 2]) | ((int(tin[t, 7]) & 0xFFFF) << 32)
+        x0 = (u // 32768) * PART
+        ts = u * TILE
+        none = (l0 & 4) != 0
+        G = x0 + (l1 & 0xFFFFFFFF)
+        if dead:
+            continue
+        true_in = X < ts + TILE
+        if none and not true_in:
+            continue
+        if not none and G == X:
+            continue
+        wrong += 1
+        k = "none-but-start" if none else ("guess-after-true" if G > X else "guess-before-true")
+        kinds[k] = kinds.get(k, 0) + 1
+        if shown < 12:
+            shown += 1
+            gb = wl.d_buf[fo + G: fo + G + 16].cpu().numpy().tobytes().hex() if not none else "-"
+            xb = wl.d_buf[fo + X: fo + X + 16].cpu().numpy().tobytes().hex() if true_in else "-"
+            print("file %d tile %d: %s guess %s (+%d) true %d (+%d) | guess bytes %s | true bytes %s" % (
+                f, u, k, "NONE" if none else str(G), (G - ts) if not none else -1, X, X - ts, gb, xb), flush=True)
+    t0 += nt[f]
+print(cfg, "passes", st.passes, "wrong run-start guesses", wrong, kinds, flush=True)
