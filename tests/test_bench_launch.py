@@ -54,3 +54,22 @@ def test_world_size_mismatch_fails():
     assert "WORLD_SIZE" in r.stderr
     assert not _lines(r.stdout)
 
+
+
+def test_post_merge_open_merge_finished_record():
+    """The post-merge open leg's merge-finished record (bench._record_bytes) is
+    EncodeLogRecord of {MergeFinishedKey, strconv.Itoa(nonMergeFileId)}
+    (merge.go:154-168), byte for byte the golden generator's encoding, and
+    the oracle decodes it back."""
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    sys.path.insert(0, ROOT)
+    import numpy as np
+
+    import bench
+    import make_golden as mg
+    from oracle import cly_oracle as co
+    for v in (b"0", b"128", b"4096", b"1000000"):
+        rec = bench._record_bytes(mg.MERGE_FIN_KEY, v)
+        assert rec == mg.encode_record(mg.MERGE_FIN_KEY, v)
+        t, st, end = co.scan_file(np.frombuffer(rec, np.uint8).copy(), 0)
+        assert len(t) == 1 and end == len(rec) and int(t["value_size"][0]) == len(v)

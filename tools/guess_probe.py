@@ -14,6 +14,7 @@ from couloydb_amd import Scanner  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
 TILE, PART = 65536, 32768 * 65536
+FOCUS = int(sys.argv[2]) if len(sys.argv) > 2 else -100    # a global tile index to show (e.g. the longest walk's)
 wl = make_workload(cfg, torch)
 sc = Scanner(0)
 sc.lib.cly_dbg_set(sc.ctx, 3)
@@ -49,11 +50,14 @@ for f, (ptr, ln, fid) in enumerate(wl.dev_files):
         wrong += 1
         k = "none-but-start" if none else ("guess-after-true" if G > X else "guess-before-true")
         kinds[k] = kinds.get(k, 0) + 1
-        if shown < 12:
+        if shown < 12 or abs(t - FOCUS) <= 4:
             shown += 1
             gb = wl.d_buf[fo + G: fo + G + 16].cpu().numpy().tobytes().hex() if not none else "-"
             xb = wl.d_buf[fo + X: fo + X + 16].cpu().numpy().tobytes().hex() if true_in else "-"
             print("file %d tile %d: %s guess %s (+%d) true %d (+%d) | guess bytes %s | true bytes %s" % (
                 f, u, k, "NONE" if none else str(G), (G - ts) if not none else -1, X, X - ts, gb, xb), flush=True)
     t0 += nt[f]
+if FOCUS >= 0:
+    for t in range(FOCUS - 1, FOCUS + 5):
+        print("tile %d LOCAL %s TileIn %s" % (t, [hex(int(v)) for v in loc[t]], [hex(int(v)) for v in tin[t]]), flush=True)
 print(cfg, "passes", st.passes, "wrong run-start guesses", wrong, kinds, flush=True)
