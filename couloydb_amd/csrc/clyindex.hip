@@ -607,8 +607,8 @@ extern "C" int cly_index_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     uint64_t* d_pk = nullptr;
     const uint64_t* d_first = nullptr;
     const uint64_t* d_bases = nullptr;
-    ICK(hipEventCreate(&e0));
-    ICK(hipEventCreate(&e1));
+    ICK(hipEventCreateWithFlags(&e0, hipEventDisableSystemFence));     // (timing only)
+    ICK(hipEventCreateWithFlags(&e1, hipEventDisableSystemFence));
     ICK(cly_ix_scratch_internal(ctx, 0, sizeof(uint64_t) * (2 * (size_t)nfiles + 2), (void**)&d_fb));
     d_first = d_fb;
     d_bases = d_fb + nfiles + 1;

@@ -1036,8 +1036,8 @@ extern "C" int cly_merge_device(cly_ctx* ctx, const cly_file* files, int nfiles,
     MTot h_tot;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const uint64_t nblk = T / M_BLK + 1;
-    MCK(hipEventCreate(&e0));
-    MCK(hipEventCreate(&e1));
+    MCK(hipEventCreateWithFlags(&e0, hipEventDisableSystemFence));     // (timing only)
+    MCK(hipEventCreateWithFlags(&e1, hipEventDisableSystemFence));
     for (int i = 0; i < nfiles; i++) h_fb[i] = file_first[i];
     h_fb[nfiles] = T;
     for (int i = 0; i < nfiles; i++) h_fb[nfiles + 1 + i] = (uint64_t)files[i].base;
@@ -1464,8 +1464,8 @@ extern "C" int cly_append_device(cly_ctx* ctx, const cly_rec_in* d_recs, uint64_
     unsigned long long h_mx = 0, h_mn = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const unsigned grid = (unsigned)((nt + 255) / 256 < 16384 ? (nt + 255) / 256 : 16384);
-    MCK(hipEventCreate(&e0));
-    MCK(hipEventCreate(&e1));
+    MCK(hipEventCreateWithFlags(&e0, hipEventDisableSystemFence));     // (timing only)
+    MCK(hipEventCreateWithFlags(&e1, hipEventDisableSystemFence));
     MCK(scratch(ctx, MS_A0 + 0, sizeof(uint64_t) * nt, &d_sz));
     MCK(scratch(ctx, MS_A0 + 1, sizeof(uint64_t) * nt, &d_g));
     MCK(scratch(ctx, MS_A0 + 2, sizeof(uint32_t), &d_nout));

@@ -2361,7 +2361,10 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
     if (!c) return CLY_ERR_DEVICE;
     c->device = device;
     HIPCK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    for (int i = 0; i < 8; i++) HIPCK(hipEventCreate(&c->ev[i]));
+    // timing-only markers: no system-scope fence (its L2 writeback and
+    // invalidate left a 6-us gap after every marked kernel); the results come
+    // back by copies and stream waits
+    for (int i = 0; i < 8; i++) HIPCK(hipEventCreateWithFlags(&c->ev[i], hipEventDisableSystemFence));
     {
         static uint32_t hn[NTAB_ALL];
         for (int k = 0; k < NTAB_ALL / 128; k++) {
