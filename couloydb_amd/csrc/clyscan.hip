@@ -2346,7 +2346,8 @@ struct cly_ctx {
     cly_tuple* d_tuples; uint64_t cap_tuples;
     void* merge_scratch;         // clymerge.hip's buffers (grow-only)
     int64_t now_ns;              // loadIndex's time.Now() for the TTL sweep (0: the wall clock per call)
-    int dbg;                     // cly_dbg_set: bit 0 = keep k_scan's LOCALs (before any repair) in d_dbg
+    int dbg;                     // cly_dbg_set: bit 0 = keep k_scan's LOCALs (before any repair) in d_dbg,
+                                 // bit 1 = print the repair rounds, bit 2 = per-kernel timing markers
     TileLocal* d_dbg; int64_t cap_dbg;
 };
 extern "C" void cly_merge_scratch_free(void* p);
@@ -2593,7 +2594,11 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
     hipLaunchKernelGGL(k_link, dim3(nfiles), dim3(LINK_NT), 0, st, c->d_files, nfiles, c->d_loc, c->d_tin, c->d_ftotal,
                        c->d_finfo, c->d_fix, c->d_lmask, c->lmask_words, c->d_g, 1, 0);
     HIPCK(hipGetLastError());
-    HIPCK(hipEventRecord(c->ev[2], st));
+    // per-kernel markers between the link and k_emit and between k_emit and
+    // k_fin only on request (cly_dbg_set bit 2: each marker costs a gap of
+    // ~5 us); otherwise link + k_emit + k_fin are timed as one span
+    const bool detail = (c->dbg & 4) != 0;
+    if (detail) HIPCK(hipEventRecord(c->ev[2], st));
     int slot = 1;
     auto launch_emit = [&]() -> int {
         int eg = c->emit_grid;
@@ -2602,7 +2607,7 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
                            c->d_tin, c->d_loc, c->d_rec, c->d_seg, c->d_treg, c->d_finfo, c->d_tabs, d_out,
                            out_cap, c->d_chunks, c->d_sp_rec, c->d_g, slot);
         HIPCK(hipGetLastError());
-        HIPCK(hipEventRecord(c->ev[3], st));
+        if (detail) HIPCK(hipEventRecord(c->ev[3], st));
         hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_finfo, c->d_treg, c->d_loc,
                            c->d_tin, c->d_tabs, c->d_pw, c->d_g, slot);
         HIPCK(hipGetLastError());
@@ -2673,10 +2678,16 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
         return CLY_OK;
     }
     HIPCK(hipEventElapsedTime(&ms_scan, c->ev[0], c->ev[1]));
-    HIPCK(hipEventElapsedTime(&ms_link, c->ev[1], c->ev[2]));
-    HIPCK(hipEventElapsedTime(&ms_emit, c->ev[2], c->ev[3]));
-    HIPCK(hipEventElapsedTime(&ms_fin, c->ev[3], c->ev[4]));
-    if (ms_fix > 0) ms_link = 0;   // ev[2] was re-recorded after the host repair loop
+    if (detail) {
+        HIPCK(hipEventElapsedTime(&ms_link, c->ev[1], c->ev[2]));
+        HIPCK(hipEventElapsedTime(&ms_emit, c->ev[2], c->ev[3]));
+        HIPCK(hipEventElapsedTime(&ms_fin, c->ev[3], c->ev[4]));
+        if (ms_fix > 0) ms_link = 0;   // ev[2] was re-recorded after the host repair loop
+    } else {
+        // one span: the link and k_emit + k_fin (after a host repair loop, ev[2]
+        // marks the relaunched k_emit)
+        HIPCK(hipEventElapsedTime(&ms_emit, ms_fix > 0 ? c->ev[2] : c->ev[1], c->ev[4]));
+    }
     c->h_g->refix = refixed;
     c->kms[0] = ms_scan; c->kms[1] = ms_link + ms_fix; c->kms[2] = ms_emit; c->kms[3] = ms_fin; c->kms[4] = 0;
     c->kms[5] = ms_scan + ms_link + ms_fix + ms_emit + ms_fin;

@@ -12,6 +12,8 @@ n = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 lib = sys.argv[3] if len(sys.argv) > 3 else "libclyscan.so"
 wl = make_workload(cfg, torch)
 sc = Scanner(0, lib=lib)
+if hasattr(sc.lib, "cly_dbg_set"):
+    sc.lib.cly_dbg_set(sc.ctx, 4)       # per-kernel markers (link / k_emit / k_fin split)
 st = need = None
 for _ in range(n):
     try:

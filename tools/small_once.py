@@ -11,6 +11,5 @@ from couloydb_amd import Scanner  # noqa: E402
 
 lib = sys.argv[1] if len(sys.argv) > 1 else "libclyscan.so"
 sc = Scanner(0, lib=lib)
-if len(sys.argv) > 2:
-    sc.lib.cly_dbg_set(sc.ctx, int(sys.argv[2]))
+sc.lib.cly_dbg_set(sc.ctx, 4 | (int(sys.argv[2]) if len(sys.argv) > 2 else 0))   # per-kernel markers
 print(lib, small_records_leg(sc, torch), sc.kernel_ms(), flush=True)
