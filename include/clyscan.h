@@ -91,8 +91,13 @@ typedef struct cly_file_result {
 
 /* Timing of the last call (device work only; filled when requested).          */
 typedef struct cly_stats {
-    double   scan_ms;         /* decode+CRC kernel(s), HIP events              */
-    double   resolve_ms;      /* chain resolution + per-file result kernel     */
+    double   scan_ms;         /* decode+CRC kernel(s), HIP events; without the
+                                 per-kernel markers (a debug option: each costs a
+                                 ~5-us gap) this includes the link and the
+                                 per-file result kernel                          */
+    double   resolve_ms;      /* chain resolution (host-driven repair rounds;
+                                 with the markers also the link and the per-file
+                                 result kernel)                                  */
     double   total_ms;        /* whole device pipeline incl. repair passes     */
     uint32_t passes;          /* 1 = speculation verified first time           */
     uint32_t n_chunks;
