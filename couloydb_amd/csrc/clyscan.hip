@@ -1033,6 +1033,23 @@ __device__ __forceinline__ uint32_t guess_entry(const DevFile& F, uint32_t bs, C
         cm = cand_mask(wv, n0, n1);
         const uint32_t nv = K.ce - K.cb;                    // valid positions
         if (nv < 64) cm &= (1ull << nv) - 1ull;
+        // a record that starts in the last 4 bytes before the block leaves a
+        // false candidate 4 bytes after its start, in the block's first 4
+        // bytes: its "CRC" is that record's type, data type and size varints,
+        // so its first two bytes are <= 4 (a stored CRC's, 1 in 2600); its walk
+        // over keys of '0'..'9' digits often holds (small records: most of the
+        // wrong run-start guesses).  Not a guess, then.
+        if (lane == 0) {
+            const uint32_t le = swar_le4(wv[0]), le4 = swar_le4(wv[1]) & 0x80u;
+            uint32_t pm = 0;
+            #pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t a = (le >> (8 * k + 7)) & 1u;
+                const uint32_t b = k < 3 ? (le >> (8 * (k + 1) + 7)) & 1u : le4 >> 7;
+                pm |= (a & b) << k;
+            }
+            cm &= ~(u64)pm;
+        }
     }
     uint32_t E = NONE32, ex_x = 0, ex_sz = 0;       // (an unconfirmed start: its exit and the record there)
     bool conf_in = false;

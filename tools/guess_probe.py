@@ -15,7 +15,38 @@ from couloydb_amd import Scanner  # noqa: E402
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
 TILE, PART = 65536, 32768 * 65536
 FOCUS = int(sys.argv[2]) if len(sys.argv) > 2 else -100    # a global tile index to show (e.g. the longest walk's)
-wl = make_workload(cfg, torch)
+class _Small:
+    pass
+
+
+def small_workload():
+    """bench.small_records_leg's file (1 GiB of 19-30-B records), kept in HBM"""
+    from couloydb_amd import _abi
+    gen = _abi.load_gen_lib()
+    seed = 0x434C59 + 7
+    rng = np.random.default_rng(seed)
+    n = int((1 << 30) / 24.5)
+    recs = np.zeros(n, dtype=_abi.GEN_DTYPE)
+    recs["value_len"] = rng.integers(0, 12, n)
+    recs["key_index"] = np.arange(n, dtype=np.int64) % 1_000_000_000
+    recs["type"] = (rng.random(n) < 0.25).astype(np.uint8)
+    recs["value_len"][recs["type"] == 1] = 0
+    fo = (ctypes.c_uint64 * 4)()
+    fl = (ctypes.c_uint64 * 4)()
+    nf = ctypes.c_uint32()
+    total = gen.cly_gen_layout(recs.ctypes.data, n, 1 << 62, 4096, fo, fl, 4, ctypes.byref(nf))
+    w = _Small()
+    w.d_buf = torch.empty(int(total) + 4096, dtype=torch.uint8, device="cuda")
+    d_recs = torch.from_numpy(recs.view(np.uint8)).to("cuda")
+    gen.cly_gen_encode(ctypes.c_void_p(w.d_buf.data_ptr()), ctypes.c_void_p(d_recs.data_ptr()), n, seed)
+    w.dev_files = [(w.d_buf.data_ptr() + int(fo[0]), int(fl[0]), 1)]
+    w.file_off = [int(fo[0])]
+    w.out_cap = n + 1024
+    w.d_out = torch.empty(w.out_cap * 48, dtype=torch.uint8, device="cuda")
+    return w
+
+
+wl = small_workload() if cfg == "small" else make_workload(cfg, torch)
 sc = Scanner(0)
 sc.lib.cly_dbg_set(sc.ctx, 3)
 first, res, st, need = sc.scan_device(wl.dev_files, wl.d_out.data_ptr(), wl.out_cap)
