@@ -1299,21 +1299,32 @@ __device__ __forceinline__ TileRes tile_body(const DevFile& F, uint32_t t, uint3
                     const uint32_t pcq = c > 0 ? L.last_crc : (lfp ? lvp : S.cq);
                     const bool pk = c > 0 || lfp || S.cq_known;
                     // the block's records, record-parallel: record r (in chain order) by
-                    // lane r % 64 of round r / 64: its segment is the first lane whose
-                    // inclusive count exceeds r, its start that lane's (r - lex)-th
-                    // start bit; outputs, patch-word marks (headers from the stage),
-                    // entries stored as consecutive 16-B slots
+                    // lane r % 64 of round r / 64: its segment is the lane whose records
+                    // [lex, incl) hold r, its start that lane's (r - lex)-th start bit;
+                    // outputs, patch-word marks (headers from the stage), entries
+                    // stored as consecutive 16-B slots.  The owners of a round without
+                    // a search over the lanes: each lane with records in the round
+                    // sets the bit of its first one (distinct bits, so a wave sum
+                    // is their OR); record r's owner is the lane of the last set bit
+                    // at or before r, the j-th lane with records in the round.
                     bool cf = false;
                     uint32_t sz_last = 0, sz_prev = 0;
                     spill_ensure(S, S.tcnt + bcnt, rs, lane);
                     for (uint32_t r0 = 0; r0 < bcnt; r0 += 64) {
                         const uint32_t r = r0 + (uint32_t)lane;
-                        uint32_t own = 0;
-                        #pragma unroll
-                        for (int w = 32; w >= 1; w >>= 1)
-                            if (shfl_u32(incl, (int)own + w - 1) <= r) own += (uint32_t)w;
+                        const bool isec = c > 0 && incl > r0 && lex < r0 + 64u;
+                        const uint32_t sb = lex > r0 ? lex - r0 : 0u;
+                        const uint32_t blo = wave_add_incl(isec && sb < 32u ? 1u << sb : 0u);
+                        const uint32_t bhi = wave_add_incl(isec && sb >= 32u ? 1u << (sb - 32u) : 0u);
+                        const u64 B = ((u64)rdl(bhi, 63) << 32) | rdl(blo, 63);
+                        const u64 mi = __ballot(isec);
+                        const u64 Bm = B & ((2ull << lane) - 1ull);              // (lane 63: every bit)
+                        const uint32_t j = (uint32_t)__popcll(Bm), hb = 63u - (uint32_t)__clzll((long long)Bm);
+                        uint32_t own = kth_bit((uint32_t)mi, (uint32_t)(mi >> 32), j - 1u);
                         own = own > 63u ? 63u : own;
-                        const uint32_t k = r - shfl_u32(lex, (int)own);
+                        // the round's first record may continue a lane's records of the round before
+                        const uint32_t d0 = rdl(r0 > lex ? r0 - lex : 0u, __ffsll((long long)mi) - 1);
+                        const uint32_t k = (uint32_t)lane - hb + (hb == 0u ? d0 : 0u);
                         const uint32_t m0 = shfl_u32(L.sm0, (int)own), m1 = shfl_u32(L.sm1, (int)own);
                         uint32_t sz = 0;
                         if (r < bcnt) {
