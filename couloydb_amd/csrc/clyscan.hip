@@ -198,6 +198,7 @@ struct Globals {                 // zeroed per call
 //   TAB_EM:   k_emit's: A^(4k), k = 1..16 (a shift inside a segment; k = 16 is
 //             the segment step A^64), A^1..A^3, and A^(RUN_BYTES 2^l), l < 6
 //             (the lanes' runs of segments)
+//   TAB_PW:   A^(CLY_TILE 2^k), k < NPW (k_fin's scan levels)
 #define NIB_SH 65
 #define TAB_SH 0
 #define TAB_TILE (NIB_SH * 128)
@@ -207,7 +208,9 @@ struct Globals {                 // zeroed per call
 #define EM_RUN 19                 // A^(RUN_BYTES 2^l): table 19 + l
 #define EM_SEGP 25                // A^(64 2^l), l = 1..3: table 24 + l (k_emit's A^(64 j), j < 16)
 #define NEM 28
-#define NTAB_ALL (TAB_EM + NEM * 128)
+#define TAB_PW (TAB_EM + NEM * 128)
+#define NPW 32
+#define NTAB_ALL (TAB_PW + NPW * 128)
 // LDS of k_scan / k_refix (static: compile-time offsets)
 //   [0, 65536)  CRC slicing-by-4 tables T0..T3, 16 replicas: dword (i*64 + t*16 + r)
 //   LDS_INV     inverse of a zero-byte step (top byte of T0 -> index), 256 B
@@ -2277,20 +2280,19 @@ k_emit(const DevFile* __restrict__ files, int nfiles, const uint32_t* __restrict
 // TileIn): A^CLY_TILE (the register entering the tile) must equal the tile's
 // dev shifted to its end.
 #define FIN_NT 1024
+#define FIN_LEV 10                      // log2(FIN_NT): the scan's levels
+#define FIN_B 4                         // tiles a thread loads at once
 __device__ __forceinline__ uint32_t shift_b(const CLY_LDS uint32_t* sh, uint32_t m, uint32_t v) {
     return m ? shift_bytes(sh, m, v) : v;
 }
 __global__ void __launch_bounds__(FIN_NT)
 k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __restrict__ treg,
       const TileLocal* __restrict__ loc, const TileIn* __restrict__ tin, const uint32_t* __restrict__ tabs,
-      const uint32_t* __restrict__ pw, Globals* g, int slot) {
+      Globals* g, int slot) {
     __shared__ uint32_t tabl[NIB_SH * 128 + 128];           // TAB_SH, TAB_TILE
+    __shared__ uint32_t levt[FIN_LEV * 128];                // A^(CLY_TILE per 2^l): level l of the scan
     __shared__ uint32_t px[FIN_NT], pc[FIN_NT];
-    __shared__ uint32_t mlev[16];
     if (g->nfix[slot] || g->spill_over || g->fail) return;   // k_emit did not run
-    for (int i = threadIdx.x; i < NIB_SH * 128 + 128; i += FIN_NT) tabl[i] = tabs[TAB_SH + i];
-    const CLY_LDS uint32_t* sht = (const CLY_LDS uint32_t*)tabl;
-    const CLY_LDS uint32_t* tilet = sht + NIB_SH * 128;
     const int f = blockIdx.x, tid = threadIdx.x;
     const DevFile F = files[f];
     FileInfo* fo = &finfo[f];
@@ -2298,50 +2300,69 @@ k_fin(const DevFile* __restrict__ files, FileInfo* finfo, const uint32_t* __rest
         if (tid == 0) atomicOr(&g->fail, 32u);
         return;
     }
+    // a thread's tiles: a power of two (per = 2^e), so that level l's shift is
+    // the host-built table A^(CLY_TILE 2^(e + l))
     const uint32_t ft = F.first_tile, nt = fo->term_tile - ft + 1;
-    const uint32_t per = (nt + FIN_NT - 1) / FIN_NT;
+    const uint32_t per0 = (nt + FIN_NT - 1) / FIN_NT;
+    const uint32_t e = per0 <= 1u ? 0u : 32u - (uint32_t)__clz((int)(per0 - 1u)), per = 1u << e;
     const uint32_t lo = tid * per < nt ? tid * per : nt, hi = lo + per < nt ? lo + per : nt;
-    if (tid == 0) {                         // A^(CLY_TILE per 2^l): the shift of a level of the scan
-        uint32_t m = 1u << 31;
-        for (uint32_t b = per, k = 0; b; b >>= 1, k++) if (b & 1) m = cly_multmodp(pw[k], m);
-        for (int l = 0; (1 << l) < FIN_NT; l++) { mlev[l] = m; m = cly_multmodp(m, m); }
-    }
-    __syncthreads();
+    for (int i = tid; i < NIB_SH * 128 + 128; i += FIN_NT) tabl[i] = tabs[TAB_SH + i];
+    for (int i = tid; i < FIN_LEV * 128; i += FIN_NT) levt[i] = tabs[TAB_PW + e * 128 + i];
+    const CLY_LDS uint32_t* sht = (const CLY_LDS uint32_t*)tabl;
+    const CLY_LDS uint32_t* tilet = sht + NIB_SH * 128;
+    uint64_t a0[FIN_B];
+    uint32_t av[FIN_B];
+    auto fetch = [&](uint32_t u0) {
+        #pragma unroll
+        for (int q = 0; q < FIN_B; q++)
+            if (u0 + q < hi) { a0[q] = loc[ft + u0 + q].l[0]; av[q] = treg[2 * (ft + u0 + q)]; }
+    };
     uint32_t x = 0, c = 0;
-    for (uint32_t u = lo; u < hi; u++) {
-        const u64 l0 = loc[ft + u].l[0];
-        const uint32_t v = treg[2 * (ft + u)];
-        if (!(l0 & DF_NONE)) { x = v; c = 1; }
-        else x = mat_mul(tilet, x) ^ v;
+    fetch(lo);
+    __syncthreads();                                        // (the tables)
+    for (uint32_t u0 = lo; u0 < hi; u0 += FIN_B) {
+        if (u0 != lo) fetch(u0);
+        #pragma unroll
+        for (int q = 0; q < FIN_B; q++) {
+            if (u0 + q >= hi) break;
+            if (!(a0[q] & DF_NONE)) { x = av[q]; c = 1; }
+            else x = mat_mul(tilet, x) ^ av[q];
+        }
     }
     px[tid] = x; pc[tid] = c;
     __syncthreads();
-    for (int l = 0; (1 << l) < FIN_NT; l++) {
+    for (int l = 0; l < FIN_LEV; l++) {
         const int d = 1 << l;
         uint32_t ox = 0, oc = 0;
         if (tid >= d) { ox = px[tid - d]; oc = pc[tid - d]; }
         __syncthreads();
-        if (tid >= d && !c) { x = cly_multmodp(mlev[l], ox) ^ x; c = oc; }
+        if (tid >= d && !c) { x = mat_mul((const CLY_LDS uint32_t*)levt + l * 128, ox) ^ x; c = oc; }
         px[tid] = x; pc[tid] = c;
         __syncthreads();
     }
     uint32_t y = tid ? px[tid - 1] : 0u;
-    for (uint32_t u = lo; u < hi; u++) {
-        const uint32_t t = ft + u;
-        const u64 l0 = loc[t].l[0];
-        const uint32_t v = treg[2 * t];
-        if (l0 & DF_NONE) { y = mat_mul(tilet, y) ^ v; continue; }
-        if (u > 0) {
-            const LBState S = ti_load(&tin[t]);
-            const uint32_t n = (uint32_t)(l0 >> 32), G = (uint32_t)loc[t].l[1];
-            const uint32_t tb = (u % PART_TILES) * (uint32_t)CLY_TILE, TE = tb + (uint32_t)CLY_TILE;   // (the part's)
-            uint32_t dev = treg[2 * t + 1];
-            if ((l0 & DF_TERM) && n == 0) dev ^= shift_b(sht, TE - G, S.crc_last);     // G is the terminal
-            else dev = shift_b(sht, TE - patch_word_of(G), dev);
-            if (mat_mul(tilet, y) != dev)
-                fail_at(fo, S.P_last, S.count - 1);
+    for (uint32_t u0 = lo; u0 < hi; u0 += FIN_B) {
+        fetch(u0);
+        #pragma unroll
+        for (int q = 0; q < FIN_B; q++) {
+            const uint32_t u = u0 + q;
+            if (u >= hi) break;
+            const uint32_t t = ft + u;
+            const u64 l0 = a0[q];
+            const uint32_t v = av[q];
+            if (l0 & DF_NONE) { y = mat_mul(tilet, y) ^ v; continue; }
+            if (u > 0) {
+                const LBState S = ti_load(&tin[t]);
+                const uint32_t n = (uint32_t)(l0 >> 32), G = (uint32_t)loc[t].l[1];
+                const uint32_t tb = (u % PART_TILES) * (uint32_t)CLY_TILE, TE = tb + (uint32_t)CLY_TILE;   // (the part's)
+                uint32_t dev = treg[2 * t + 1];
+                if ((l0 & DF_TERM) && n == 0) dev ^= shift_b(sht, TE - G, S.crc_last);     // G is the terminal
+                else dev = shift_b(sht, TE - patch_word_of(G), dev);
+                if (mat_mul(tilet, y) != dev)
+                    fail_at(fo, S.P_last, S.count - 1);
+            }
+            y = v;
         }
-        y = v;
     }
 }
 
@@ -2367,7 +2388,6 @@ struct cly_ctx {
     u32x4* d_sp_rec; uint32_t cap_spill;   // the spill pool (chunks of CAP_T entries)
     Globals* d_g; Globals* h_g;
     uint32_t* d_tabs;            // nibble tables (TAB_SH, TAB_TILE, TAB_EM)
-    uint32_t* d_pw;              // x^(8 CLY_TILE 2^k) mod P, k < 40
     int scan_grid, emit_grid, loc_grid;
     float kms[6];                // last call: k_scan, link rounds (k_link/k_refix), k_emit, k_fin, discarded attempts, all
     uint8_t* d_bytes; uint64_t cap_bytes;          // host-path staging
@@ -2401,6 +2421,7 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
             if (k < 64) nbytes = (uint64_t)(k & 15) << (4 * (k >> 4));               // A^(v 16^d)
             else if (k == 64) nbytes = 65536;                                        // A^65536
             else if (k == 65) nbytes = (uint64_t)CLY_TILE;                           // k_fin's tile step
+            else if (k >= TAB_PW / 128) nbytes = (uint64_t)CLY_TILE << (k - TAB_PW / 128);   // k_fin's levels
             else {
                 const int e = k - 66;                                                // TAB_EM
                 if (e < EM_F1) nbytes = 4ull * (uint64_t)(e + 1);                    // A^(4k), k = 1..16
@@ -2414,11 +2435,6 @@ extern "C" int cly_ctx_create(int device, cly_ctx** out) {
         }
         HIPCK(hipMalloc(&c->d_tabs, sizeof(hn)));
         HIPCK(hipMemcpy(c->d_tabs, hn, sizeof(hn), hipMemcpyHostToDevice));
-        uint32_t hp[40];
-        hp[0] = cly_x8n((uint64_t)CLY_TILE);
-        for (int k = 1; k < 40; k++) hp[k] = cly_multmodp(hp[k - 1], hp[k - 1]);
-        HIPCK(hipMalloc(&c->d_pw, sizeof(hp)));
-        HIPCK(hipMemcpy(c->d_pw, hp, sizeof(hp), hipMemcpyHostToDevice));
     }
     {
         int ncu = 0;
@@ -2444,7 +2460,7 @@ extern "C" void cly_ctx_destroy(cly_ctx* c) {
     hipFree(c->d_call); hipFree(c->d_ftotal);
     hipFree(c->d_loc); hipFree(c->d_tin); hipFree(c->d_treg); hipFree(c->d_fix); hipFree(c->d_rec);
     hipFree(c->d_seg); hipFree(c->d_chunks); hipFree(c->d_lmask); hipFree(c->d_sp_rec);
-    hipFree(c->d_tabs); hipFree(c->d_pw); hipFree(c->d_bytes); hipFree(c->d_tuples); hipFree(c->d_dbg);
+    hipFree(c->d_tabs); hipFree(c->d_bytes); hipFree(c->d_tuples); hipFree(c->d_dbg);
     hipHostFree(c->h_call);
     cly_merge_scratch_free(c->merge_scratch);
     for (int i = 0; i < 8; i++) hipEventDestroy(c->ev[i]);
@@ -2637,7 +2653,7 @@ static int scan_attempt(cly_ctx* c, const cly_file* files, int nfiles, cly_tuple
         HIPCK(hipGetLastError());
         if (detail) HIPCK(hipEventRecord(c->ev[3], st));
         hipLaunchKernelGGL(k_fin, dim3(nfiles), dim3(FIN_NT), 0, st, c->d_files, c->d_finfo, c->d_treg, c->d_loc,
-                           c->d_tin, c->d_tabs, c->d_pw, c->d_g, slot);
+                           c->d_tin, c->d_tabs, c->d_g, slot);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(c->ev[4], st));
         // one read-back and one wait for the whole call when no repair round is needed

@@ -116,6 +116,24 @@ PATCHES["l2"] = [
     ("""    if (lane < 2) hl = load16z(base, (uint64_t)bs + CLY_BLK + 16 * lane, flen);""",
      """    if (lane < 2) hl = load16z(base, (uint64_t)((bs + CLY_BLK) & (CLY_TILE - 1u)) + 16 * lane, flen);"""),
 ] + SCAN_ONLY
+# blocks after two general-pass blocks in a row skip the predictive walk (every
+# 8th tries it again)
+PATCHES["pskip"] = [
+    ("""    bool ref_ok;
+""", """    bool ref_ok;
+    uint32_t gp_run;
+"""),
+    ("""    S.ref_ok = false; S.ref_s = 0;""", """    S.gp_run = 0; S.ref_ok = false; S.ref_s = 0;"""),
+    ("""                done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, rs, lane, mk);
+                if (S.tcnt != c0) stride_ref(F, S, bs, stg);
+            }""", """                if (S.gp_run >= 2 && (S.gp_run & 7u) != 0) {
+                    const uint64_t Xs = S.X, be = (uint64_t)bs + CLY_BLK;
+                    done = S.dead || !(Xs < be || (Xs == F.len && F.len == be));
+                } else done = pred_walk<BM>(F, S, tb, bs, stg, smem, cl, K4, rs, lane, mk);
+                if (S.tcnt != c0) stride_ref(F, S, bs, stg);
+            }
+            S.gp_run = done ? 0u : S.gp_run + 1u;"""),
+]
 PATCHES["gp1"] = [("#define GP_TRIES 2 ", "#define GP_TRIES 1 ")]
 PATCHES["gp3"] = [("#define GP_TRIES 2 ", "#define GP_TRIES 3 ")]
 PATCHES["sloopcnt"] = PATCHES["sloop"] + PATCHES["cnt"]
